@@ -1,0 +1,209 @@
+#!/usr/bin/env python3
+"""bench.py — OCC-validated txns/s on MI355X (BASELINE.json metric).
+
+A step is one OCC epoch decision (dcc_occ_validate_epoch) over a resident
+synthetic YCSB batch: 1,048,576 txns x 16 keys, zipf theta 0.9, 16,777,216-key
+table, TXN_WRITE_PERC = TUP_WRITE_PERC = 0.5 (SURVEY.md §8(d) "Headline").
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--txns N] [--theta T]
+
+N > 1 is launched by torch.distributed.run (one rank per GPU, RCCL): keys are
+hash-sharded across the ranks and every round joins a per-txn state allreduce.
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--txns", type=int, default=1 << 20)
+    ap.add_argument("--theta", type=float, default=0.9)
+    ap.add_argument("--keys", type=int, default=16)
+    ap.add_argument("--seed", type=lambda s: int(s, 0), default=0xD3E7A001)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=65536,
+                    help="txns of the batch timed with the CPU reference restatement")
+    return ap.parse_args()
+
+
+def cpu_baseline(batch, sample: int):
+    """Reference CPU path on a bounded sample: the literal OptCC epoch replay
+    (active-list scan, occ.cpp:116-327) restated in oracle/occ_ref.c."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle as orc  # checker / CPU baseline only
+    from deneva_amd import EpochBatch
+
+    n = min(sample, batch.n_txn)
+    off = batch.offsets[: n + 1].copy()
+    sub = EpochBatch(off, batch.keys[: off[-1]], batch.acctype[: off[-1]])
+    t0 = time.perf_counter()
+    rc, _, _ = orc.occ(sub, literal=True)
+    dt = time.perf_counter() - t0
+    # cross-check the sample's decisions with the hash restatement
+    rc2, _, _ = orc.occ(sub)
+    assert np.array_equal(rc, rc2)
+    return {"value": n / dt, "unit": "txns/s", "cores": 1, "kind": "port",
+            "sample": f"first {n} txns of the bench batch, literal OptCC epoch replay "
+                      f"(oracle/occ_ref.c), {dt:.2f} s, 1 thread"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import deneva_amd as d
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    # same batch on every rank (deterministic generator); weak scaling: the
+    # epoch grows with the GPU count, each GPU holds 1/N of the accesses
+    n_total = args.txns * world
+    batch = d.gen_ycsb(n_txn=n_total, zipf_theta=args.theta, req_per_query=args.keys,
+                       seed=args.seed)
+    eng = d.Engine(local)
+    if world > 1:
+        uid = d.comm_unique_id() if rank == 0 else bytes(d._abi.UNIQUE_ID_BYTES)
+        obj = [uid]
+        dist.broadcast_object_list(obj, src=0)
+        eng.comm_init(rank, world, obj[0])
+        mine = d.shard_filter(batch, rank, world)
+    else:
+        mine = batch
+    dbatch = mine.to_torch(f"cuda:{local}")
+    out_rc = torch.empty(n_total, dtype=torch.uint8, device=f"cuda:{local}")
+    torch.cuda.synchronize()
+
+    def step(profile=False):
+        return eng.occ_validate_epoch(dbatch, out_rc=out_rc)[2]
+
+    for _ in range(args.warmup):
+        step()
+    # timed region: barrier + sync on both sides, max over ranks
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    stats = [step() for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=f"cuda:{local}", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    # per-phase kernel times (HIP events on the engine stream), separate pass
+    eng.set_profiling(True)
+    prof = [step() for _ in range(max(3, min(args.steps, 10)))]
+    eng.set_profiling(False)
+    ph_ms = np.mean([p["phase_ms"] for p in prof], axis=0)
+    ph_bytes = prof[-1]["phase_bytes"]
+    dom = int(np.argmax(ph_ms[:2]))  # dominant single kernel: build or round-1 probe
+    dom_name = ["k_build (key-hash build)", "k_round<true> (round-1 probe)"][dom]
+    achieved = ph_bytes[dom] / (ph_ms[dom] * 1e-3) / 1e9
+
+    s0 = stats[-1]
+    ms_per_step = dt / args.steps * 1e3
+    value = n_total * args.steps / dt
+    dev_ms = float(np.mean([s["device_ms"] for s in stats]))
+    epoch_gbs = s0["alg_bytes"] / (dev_ms * 1e-3) / 1e9
+
+    # parity check of the measured decisions against the oracle (rank 0, N=1)
+    parity = None
+    cpu = None
+    if rank == 0 and world == 1:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import _oracle as orc
+        erc, _, _ = orc.occ(batch)
+        parity = bool(np.array_equal(out_rc.cpu().numpy(), erc))
+        if not args.no_cpu_baseline:
+            cpu = cpu_baseline(batch, args.cpu_sample)
+
+    if rank == 0:
+        traffic = None
+        tf = os.path.join(ROOT, "profiles", "traffic.json")
+        if os.path.exists(tf):
+            try:
+                tj = json.load(open(tf))
+                key = f"{n_total}:{args.theta}:{args.keys}:{dom}"
+                traffic = tj.get(key)
+            except Exception:
+                traffic = None
+        line = {
+            "metric": "OCC-validated txns/sec, YCSB theta=0.9",
+            "value": value,
+            "unit": "txns/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic (deterministic YCSB generator, restated gen_requests_zipf)",
+            "config": {
+                "workload": f"YCSB OCC epoch validation, {n_total} txns x {args.keys} keys, "
+                            f"zipf theta={args.theta}, 16,777,216-key table, 50% RO txns, "
+                            f"50% WR tuples",
+                "global_batch": n_total,
+                "keys_per_txn": args.keys,
+                "parallelism": f"key-shard x{world}" if world > 1 else "single GPU",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": dom_name,
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "alg_bytes_per_launch": int(ph_bytes[dom]),
+                "avg_launch_ms": float(ph_ms[dom]),
+            },
+            "epoch": {
+                "device_ms": dev_ms,
+                "alg_bytes": int(s0["alg_bytes"]),
+                "alg_GBps": epoch_gbs,
+                "hbm_frac": epoch_gbs / HBM_PEAK_GBS,
+                "rounds": int(s0["rounds"]),
+                "commits": int(s0["n_commit"]),
+                "aborts": int(s0["n_abort"]),
+                "phase_ms": [float(x) for x in ph_ms],
+                "parity_vs_oracle": parity,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,79 @@
+// dcc_ctx: the per-process, per-device engine context behind the C ABI.
+// Replaces the reference's global OptCC singleton (`occ_man`,
+// system/global.cpp:42) and owns every device workspace so that a validation
+// call performs no allocation once warmed up.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "dcc.h"
+
+struct dcc_ctx;
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  int ensure(dcc_ctx* c, size_t bytes, const char* what);
+  void release();
+};
+
+// A batch as device pointers (aliases the caller's or the ctx's staging).
+struct DevBatch {
+  uint64_t n = 0, nnz = 0;
+  const uint32_t* off = nullptr;
+  const uint64_t* keys = nullptr;
+  const uint8_t* acctype = nullptr;
+  const uint64_t* start_tn = nullptr;
+  const uint64_t* finish_tn = nullptr;
+  const uint64_t* order = nullptr;
+};
+
+struct dcc_comm_state;  // RCCL communicator (dcc_comm.hip)
+
+struct dcc_ctx {
+  int device = 0;
+  int n_cu = 256;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool profiling = false;
+  hipEvent_t pev[8] = {};  // phase boundary events (profiling only)
+  std::string last_error;
+  void* hmisc = nullptr;  // pinned host mirror of `misc`
+
+  // device workspaces (grow-only)
+  DevBuf misc;                                   // counters / error words
+  DevBuf off, keys, acctype, start_tn, finish_tn, order;  // staged host batch
+  DevBuf table;                                  // Slot[cap]
+  DevBuf state, hasw, rc, stat;                  // per-txn bytes
+  DevBuf cflag, bsum, tn;                        // commit-tn scan
+  DevBuf l_tid[2], l_coff[2], l_cent[2];         // ping-pong undecided lists
+  DevBuf hkeys, hoff, htn;                       // history CSR
+  DevBuf perm, calvin_a, calvin_b, calvin_c, calvin_d;  // Calvin workspaces
+
+  // OCC history (occ.h:62-64) and commit counter tnc (occ.h:67)
+  std::vector<std::pair<uint64_t, uint64_t>> hist;
+  bool hist_dirty = false;
+  uint64_t h_nkeys = 0;
+  uint64_t tnc = 0;
+
+  dcc_comm_state* comm = nullptr;
+  int comm_ranks() const;
+
+  int fail(int code, const char* fmt, ...);
+  int hip_fail(hipError_t e, const char* what);
+  std::vector<DevBuf*> all_bufs();
+  int reserve_occ(uint64_t n, uint64_t nnz, uint64_t nnz_w);
+  static uint64_t table_capacity(uint64_t nnz_w);
+  int upload_history();
+  int check_batch(const dcc_batch* b);
+  int stage_batch(const dcc_batch* b, DevBatch& d);
+  int device_prep(const DevBatch& d, uint32_t& maxlen, uint64_t& nnz_w);
+  int occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dcc_stats* st);
+  int occ_epoch_sharded(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dcc_stats* st);
+  int calvin_epoch(const dcc_batch* b, uint32_t* out_group, uint8_t* out_rc, uint32_t* out_wave,
+                   dcc_stats* st);
+};

@@ -1,0 +1,106 @@
+// Kernel argument blocks shared by occ_kernels.hip and the host driver.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dcc {
+
+struct Slot;
+
+constexpr int TILE_CAP = 1024;  // accesses staged per wave (LDS)
+constexpr int TILE_WAVES = 4;   // waves per workgroup
+constexpr uint32_t MAX_TXN_LEN = 64;  // MAX_ROW_PER_TXN (config.h:155)
+constexpr uint32_t MAX_ROUND_TAG = 61;  // largest round tag a k_round may run with
+
+// list-reservation counter: txns in the high bits, entries in the low bits
+constexpr uint32_t CTR_E_BITS = 38;
+constexpr unsigned long long CTR_E_MASK = (1ull << CTR_E_BITS) - 1ull;
+
+// error bits reported by kernels
+constexpr uint32_t ERR_OFFSETS = 1;
+constexpr uint32_t ERR_TILE = 2;
+constexpr uint32_t ERR_KEY = 4;
+constexpr uint32_t ERR_FULL = 8;
+constexpr uint32_t ERR_UNDECIDED = 16;
+
+struct HistArgs {
+  uint64_t n;
+  const uint32_t* off;
+  const uint64_t* keys;
+  const uint8_t* acctype;
+  const uint64_t* start_tn;
+  const uint64_t* finish_tn;
+  const uint64_t* hkeys;
+  uint64_t nkeys;
+  const uint64_t* hoff;
+  const uint64_t* htn;
+  uint8_t* state;
+};
+
+struct BuildArgs {
+  uint64_t n;
+  uint32_t tw;
+  const uint32_t* off;
+  const uint64_t* keys;
+  const uint8_t* acctype;
+  Slot* tab;
+  uint32_t mask;
+  const uint8_t* state;
+  uint8_t* hasw;
+  uint64_t* nnz_w;
+  uint32_t* err;
+};
+
+struct RoundArgs {
+  uint64_t m;             // txns in the input list
+  uint32_t tw;            // txns per wave
+  uint32_t r;             // round tag (1..MAX_ROUND_TAG)
+  uint32_t end_total;     // coff[m] (entries in the input list)
+  const uint32_t* tid;    // list txn ids (nullptr: identity, round 1)
+  const uint32_t* coff;   // list offsets
+  const uint64_t* keys;   // round 1 input
+  const uint8_t* acctype; // round 1 input
+  const uint32_t* cent;   // rounds >= 2 input: ENT_WRITE | sid
+  Slot* tab;
+  uint32_t mask;
+  uint8_t* state;
+  uint32_t* tid_out;
+  uint32_t* coff_out;
+  uint32_t* cent_out;
+  unsigned long long* ctr;
+  uint32_t* err;
+};
+
+struct OwnerArgs {
+  uint64_t m;
+  uint32_t r;
+  uint32_t end_total;
+  const uint32_t* tid;
+  const uint32_t* coff;
+  const uint32_t* cent;
+  Slot* tab;
+};
+
+struct FinalArgs {
+  uint64_t n;
+  const uint8_t* state;
+  const uint8_t* hasw;
+  uint8_t* rc;
+  uint32_t* cflag;
+  uint64_t* counts;  // [0] commit [1] abort [2] readonly [3] committed writers
+  uint32_t* err;
+};
+
+// launchers (occ_kernels.hip)
+void launch_prep(const uint32_t* off, uint64_t n, uint64_t nnz, uint32_t* info, hipStream_t st);
+void launch_hist(const HistArgs& a, hipStream_t st);
+void launch_build(const BuildArgs& a, hipStream_t st);
+void launch_round(const RoundArgs& a, bool from_keys, hipStream_t st);
+void launch_retag(Slot* tab, uint64_t cap, hipStream_t st);
+void launch_owner_list(const OwnerArgs& a, hipStream_t st);
+void launch_final(const FinalArgs& a, hipStream_t st);
+void launch_commit_tn(const uint32_t* cflag, uint64_t n, uint64_t* bsum, uint64_t tnc,
+                      uint64_t* tn, hipStream_t st);
+void launch_count_writes(const uint8_t* at, uint64_t nnz, unsigned long long* cnt, hipStream_t st);
+
+}  // namespace dcc

@@ -1,0 +1,289 @@
+"""Python mirror of the engine's C ABI for tests, bench and tooling.
+
+The product is libdcc.so (HIP kernels + C ABI) and its C++ host shim
+(deneva_amd/csrc/host/); this module is plumbing over ``include/dcc.h``:
+numpy (host) or torch (device) arrays in, per-transaction RC codes out.
+
+Names follow the reference's plugin surface:
+``Engine.occ_validate_epoch`` is ``TxnManager::validate`` / ``OptCC::validate``
+(concurrency_control/occ.cpp:42) for a whole epoch; ``Engine.calvin_order_epoch``
+is the ``Sequencer::send_next_batch`` -> ``acquire_locks`` hand-off
+(system/sequencer.cpp:283, benchmarks/ycsb_txn.cpp:49).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import Optional
+
+import numpy as np
+
+from . import _abi
+from ._abi import DccError, lib
+
+
+def _ptr(a) -> Optional[int]:
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        assert a.flags["C_CONTIGUOUS"], "arrays must be contiguous"
+        return a.ctypes.data
+    return int(a.data_ptr())  # torch tensor
+
+
+def _is_device(a) -> bool:
+    return a is not None and not isinstance(a, np.ndarray) and bool(getattr(a, "is_cuda", False))
+
+
+@dataclass
+class EpochBatch:
+    """One epoch as a CSR of per-transaction access lists (dcc_batch)."""
+
+    offsets: object            # u32 [n_txn+1]
+    keys: object               # u64 [nnz]
+    acctype: object            # u8  [nnz] access_t
+    start_tn: object = None    # u64 [n_txn] or None
+    finish_tn: object = None   # u64 [n_txn] or None
+    order: object = None       # u64 [n_txn] (Calvin sequence key) or None
+    meta: dict = field(default_factory=dict)
+
+    @property
+    def n_txn(self) -> int:
+        return int(self.offsets.shape[0]) - 1
+
+    @property
+    def nnz(self) -> int:
+        return int(self.keys.shape[0])
+
+    @property
+    def on_device(self) -> bool:
+        return _is_device(self.offsets)
+
+    def to_c(self, flags: int = 0) -> _abi.Batch:
+        b = _abi.Batch()
+        b.n_txn = self.n_txn
+        b.nnz = self.nnz
+        b.offsets = _ptr(self.offsets)
+        b.keys = _ptr(self.keys)
+        b.acctype = _ptr(self.acctype)
+        b.start_tn = _ptr(self.start_tn)
+        b.finish_tn = _ptr(self.finish_tn)
+        b.order = _ptr(self.order)
+        b.flags = flags | (_abi.DEVICE_PTRS if self.on_device else 0)
+        return b
+
+    def to_torch(self, device="cuda"):
+        import torch
+
+        def cv(a):
+            if a is None:
+                return None
+            return torch.from_numpy(np.ascontiguousarray(a)).to(device)
+
+        return EpochBatch(cv(self.offsets), cv(self.keys), cv(self.acctype), cv(self.start_tn),
+                          cv(self.finish_tn), cv(self.order), dict(self.meta))
+
+
+def _check(code: int, ctx=None) -> None:
+    if code != _abi.DCC_OK:
+        detail = lib.dcc_last_error(ctx).decode() if ctx else ""
+        raise DccError(code, f"{_abi.strerror(code)}{': ' + detail if detail else ''}")
+
+
+class Engine:
+    """One engine context per process and device (OptCC::init / occ_man)."""
+
+    def __init__(self, device: int = 0):
+        h = C.c_void_p()
+        code = lib.dcc_init(C.byref(h), device)
+        if code != _abi.DCC_OK:
+            raise DccError(code, f"dcc_init(device={device}): {_abi.strerror(code)}")
+        self._h = h
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib.dcc_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    def set_stream(self, stream_ptr: Optional[int]) -> None:
+        _check(lib.dcc_set_stream(self._h, stream_ptr), self._h)
+
+    def set_profiling(self, enable: bool) -> None:
+        _check(lib.dcc_set_profiling(self._h, 1 if enable else 0), self._h)
+
+    def reserve(self, max_txn: int, max_nnz: int) -> None:
+        _check(lib.dcc_reserve(self._h, max_txn, max_nnz), self._h)
+
+    # ------------------------------------------------------------ OCC
+    def occ_validate_epoch(self, batch: EpochBatch, want_tn: bool = False,
+                           append_history: bool = False, out_rc=None, out_tn=None):
+        """Decide every txn of the epoch; returns (rc u8[n], tn u64[n] | None, stats)."""
+        n = batch.n_txn
+        dev = batch.on_device
+        if out_rc is None:
+            if dev:
+                import torch
+                out_rc = torch.empty(max(n, 1), dtype=torch.uint8, device=batch.offsets.device)
+            else:
+                out_rc = np.empty(max(n, 1), np.uint8)
+        if want_tn and out_tn is None:
+            if dev:
+                import torch
+                out_tn = torch.empty(max(n, 1), dtype=torch.int64, device=batch.offsets.device)
+            else:
+                out_tn = np.empty(max(n, 1), np.uint64)
+        st = _abi.Stats()
+        flags = _abi.OCC_APPEND_HISTORY if append_history else 0
+        b = batch.to_c(flags)
+        _check(lib.dcc_occ_validate_epoch(self._h, C.byref(b), _ptr(out_rc), _ptr(out_tn),
+                                          C.byref(st)), self._h)
+        return out_rc[:n], (out_tn[:n] if want_tn else None), st.as_dict()
+
+    def history_append(self, keys: np.ndarray, tn: np.ndarray) -> None:
+        keys = np.ascontiguousarray(keys, np.uint64)
+        tn = np.ascontiguousarray(tn, np.uint64)
+        _check(lib.dcc_occ_history_append(self._h, _ptr(keys), _ptr(tn), keys.shape[0]), self._h)
+
+    def history_clear(self) -> None:
+        _check(lib.dcc_occ_history_clear(self._h), self._h)
+
+    @property
+    def history_size(self) -> int:
+        return int(lib.dcc_occ_history_size(self._h))
+
+    @property
+    def tnc(self) -> int:
+        return int(lib.dcc_occ_get_tnc(self._h))
+
+    @tnc.setter
+    def tnc(self, v: int) -> None:
+        _check(lib.dcc_occ_set_tnc(self._h, v), self._h)
+
+    # ------------------------------------------------------------ Calvin
+    def calvin_order_epoch(self, batch: EpochBatch, want_group: bool = True,
+                           want_wave: bool = False):
+        """Returns (group u32[nnz] | None, rc u8[n], wave u32[n] | None, stats)."""
+        n, nnz = batch.n_txn, batch.nnz
+        dev = batch.on_device
+        if dev:
+            import torch
+            d = batch.offsets.device
+            rc = torch.empty(max(n, 1), dtype=torch.uint8, device=d)
+            grp = torch.empty(max(nnz, 1), dtype=torch.int32, device=d) if want_group else None
+            wav = torch.empty(max(n, 1), dtype=torch.int32, device=d) if want_wave else None
+        else:
+            rc = np.empty(max(n, 1), np.uint8)
+            grp = np.empty(max(nnz, 1), np.uint32) if want_group else None
+            wav = np.empty(max(n, 1), np.uint32) if want_wave else None
+        st = _abi.Stats()
+        b = batch.to_c()
+        _check(lib.dcc_calvin_order_epoch(self._h, C.byref(b), _ptr(grp), _ptr(rc), _ptr(wav),
+                                          C.byref(st)), self._h)
+        return (grp[:nnz] if want_group else None, rc[:n],
+                (wav[:n] if want_wave else None), st.as_dict())
+
+    # ------------------------------------------------------------ multi-GPU
+    def comm_init(self, rank: int, nranks: int, unique_id: bytes) -> None:
+        buf = C.create_string_buffer(bytes(unique_id), _abi.UNIQUE_ID_BYTES)
+        _check(lib.dcc_comm_init(self._h, rank, nranks, buf), self._h)
+
+    def comm_destroy(self) -> None:
+        _check(lib.dcc_comm_destroy(self._h), self._h)
+
+
+def comm_unique_id() -> bytes:
+    buf = C.create_string_buffer(_abi.UNIQUE_ID_BYTES)
+    _check(lib.dcc_comm_unique_id(buf))
+    return buf.raw
+
+
+def key_shard(key: int, nranks: int) -> int:
+    return int(lib.dcc_key_shard(key, nranks))
+
+
+def shard_filter(batch: EpochBatch, rank: int, nranks: int) -> EpochBatch:
+    n, nnz = batch.n_txn, batch.nnz
+    off = np.empty(n + 1, np.uint32)
+    keys = np.empty(max(nnz, 1), np.uint64)
+    at = np.empty(max(nnz, 1), np.uint8)
+    out = C.c_uint64()
+    b = batch.to_c()
+    _check(lib.dcc_shard_filter(C.byref(b), rank, nranks, _ptr(off), _ptr(keys), _ptr(at),
+                                C.byref(out)))
+    w = out.value
+    return EpochBatch(off, keys[:w].copy(), at[:w].copy(), batch.start_tn, batch.finish_tn,
+                      batch.order, dict(batch.meta, shard=(rank, nranks)))
+
+
+def alg_bytes(n_txn: int, nnz: int, nnz_w: int) -> int:
+    return int(lib.dcc_alg_bytes(n_txn, nnz, nnz_w))
+
+
+# ---------------------------------------------------------------- producers
+def ycsb_params(**kw) -> _abi.YcsbParams:
+    p = _abi.YcsbParams()
+    lib.dcc_ycsb_params_default(C.byref(p))
+    for k, v in kw.items():
+        if not hasattr(p, k):
+            raise TypeError(f"unknown YCSB parameter {k!r}")
+        setattr(p, k, v)
+    return p
+
+
+def gen_ycsb(want_home: bool = False, **kw) -> EpochBatch:
+    """Deterministic YCSB batch (gen_requests_zipf, ycsb_query.cpp:303-376)."""
+    p = ycsb_params(**kw)
+    n, k = p.n_txn, p.req_per_query
+    off = np.empty(n + 1, np.uint32)
+    keys = np.empty(max(n * k, 1), np.uint64)
+    at = np.empty(max(n * k, 1), np.uint8)
+    home = np.empty(max(n, 1), np.uint32) if want_home else None
+    _check(lib.dcc_gen_ycsb(C.byref(p), _ptr(off), _ptr(keys), _ptr(at), _ptr(home)))
+    meta = {"workload": "ycsb", **{f: getattr(p, f) for f, _ in p._fields_ if f != "reserved"}}
+    b = EpochBatch(off, keys[: n * k], at[: n * k], meta=meta)
+    if want_home:
+        b.meta["home"] = home[:n]
+    return b
+
+
+def tpcc_params(**kw) -> _abi.TpccParams:
+    p = _abi.TpccParams()
+    lib.dcc_tpcc_params_default(C.byref(p))
+    for k, v in kw.items():
+        if not hasattr(p, k):
+            raise TypeError(f"unknown TPC-C parameter {k!r}")
+        setattr(p, k, v)
+    return p
+
+
+def gen_tpcc(**kw) -> EpochBatch:
+    """Deterministic TPC-C NewOrder/Payment batch (tpcc_query.cpp:149-263)."""
+    p = tpcc_params(**kw)
+    n = p.n_txn
+    cap = n * lib.dcc_tpcc_max_access(C.byref(p))
+    off = np.empty(n + 1, np.uint32)
+    keys = np.empty(max(cap, 1), np.uint64)
+    at = np.empty(max(cap, 1), np.uint8)
+    tt = np.empty(max(n, 1), np.uint8)
+    out = C.c_uint64()
+    _check(lib.dcc_gen_tpcc(C.byref(p), _ptr(off), _ptr(keys), _ptr(at), _ptr(tt), C.byref(out)))
+    w = out.value
+    meta = {"workload": "tpcc", "txn_type": tt[:n].copy(),
+            **{f: getattr(p, f) for f, _ in p._fields_ if f != "reserved"}}
+    return EpochBatch(off, keys[:w].copy(), at[:w].copy(), meta=meta)

@@ -1,0 +1,246 @@
+/*
+ * dcc.h — C ABI of the MI355X-native batched concurrency-control engine
+ * (libdcc.so).  Everything a Deneva-style host binds to for the one hot path
+ * SURVEY.md §8 scopes: deciding commit/abort (OCC) and lock-grant order
+ * (Calvin) for a whole epoch of transactions at once.
+ *
+ * Conventions:
+ *   - extern "C", plain pointers and sizes, no torch / HIP types in signatures
+ *     (streams are passed as opaque `void*`).
+ *   - every entry point returns int: 0 = success, < 0 = -errno-style code
+ *     (DCC_E*).  Nothing aborts the process; batch validation (offset
+ *     monotonicity, nnz bound, reserved key) runs on the host before launch.
+ *   - all pointers are caller-owned; nothing is retained after return.
+ *   - a dcc_ctx is thread-compatible, not thread-safe: the host shim
+ *     serialises calls per context (reference OptCC serialises its list
+ *     mutations with `_semaphore`, concurrency_control/occ.cpp:137-158).
+ *
+ * Reference interfaces each entry point replaces are cited per declaration
+ * (paths relative to the reference tree).
+ */
+#ifndef DCC_H_
+#define DCC_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------- errors */
+#define DCC_OK 0
+#define DCC_EIO (-5)       /* HIP runtime failure (message via dcc_last_error) */
+#define DCC_ENOMEM (-12)   /* device or host allocation failed                  */
+#define DCC_ENODEV (-19)   /* no usable gfx950 device / bad device id           */
+#define DCC_EINVAL (-22)   /* malformed batch or argument                       */
+#define DCC_ERANGE (-34)   /* size exceeds an engine limit                      */
+#define DCC_ECOMM (-70)    /* RCCL failure                                       */
+#define DCC_ENOTSUP (-95)  /* feature not available in this build / mode        */
+
+/* ------------------------------------------------------ reference enums */
+/* access_t, system/global.h:287  {RD, WR, XP, SCAN}.  OCC puts only WR into
+ * the write set (concurrency_control/occ.cpp:379-383, get_rw_set); Calvin
+ * maps RD/SCAN to LOCK_SH and everything else to LOCK_EX (storage/row.cpp:191). */
+#define DCC_RD 0
+#define DCC_WR 1
+#define DCC_XP 2
+#define DCC_SCAN 3
+
+/* RC, system/global.h:236  {RCOK=0, Commit, Abort, WAIT, ...}.  The engine
+ * reports per-transaction RCs with the reference's numeric values. */
+#define DCC_RC_RCOK 0
+#define DCC_RC_ABORT 2
+#define DCC_RC_WAIT 3
+
+/* Keys are canonical 64-bit row identities.  This
+ * one value is reserved as the empty-slot marker of the device hash table. */
+#define DCC_KEY_RESERVED 0xFFFFFFFFFFFFFFFFull
+
+/* group value for a Calvin request removed by per-txn row de-duplication
+ * (TxnManager::get_lock, system/txn.cpp:778-782). */
+#define DCC_GROUP_NONE 0xFFFFFFFFu
+
+/* --------------------------------------------------------------- batch  */
+/* dcc_batch.flags */
+#define DCC_DEVICE_PTRS 0x1u      /* every batch AND output pointer is device memory */
+#define DCC_OCC_APPEND_HISTORY 0x2u /* central_finish semantics: committed write sets
+                                     of this epoch are appended to the history with
+                                     tn = tnc+1, tnc+2, ... in index order
+                                     (occ.cpp:248-294) */
+
+/* One epoch as a CSR of per-transaction access lists in capture order
+ * (Access list of TxnManager, system/txn.h:39-70; txn.cpp:818-847). */
+typedef struct dcc_batch {
+  uint64_t n_txn;
+  uint64_t nnz;
+  const uint32_t* offsets;   /* [n_txn+1]; offsets[0]=0, non-decreasing, offsets[n_txn]=nnz */
+  const uint64_t* keys;      /* [nnz] canonical keys, != DCC_KEY_RESERVED                */
+  const uint8_t* acctype;    /* [nnz] access_t                                           */
+  const uint64_t* start_tn;  /* [n_txn] txn start ts (worker_thread.cpp:500-502) or NULL */
+  const uint64_t* finish_tn; /* [n_txn] validation ts (occ.cpp:142) or NULL.  Both NULL
+                                disables the history window check, which is exactly
+                                the reference behaviour under TS_CLOCK */
+  const uint64_t* order;     /* Calvin: [n_txn] sequence key (epoch<<48|origin<<32|seq,
+                                any monotone encoding) or NULL = index order             */
+  uint32_t flags;
+  uint32_t reserved;
+} dcc_batch;
+
+typedef struct dcc_stats {
+  uint32_t rounds;       /* fixed-point rounds executed                                */
+  uint32_t n_shards;     /* GPUs that took part                                        */
+  uint64_t n_commit;     /* RCOK decisions (Calvin: ready at acquire)                  */
+  uint64_t n_abort;      /* Abort decisions (Calvin: WAIT)                             */
+  uint64_t n_readonly;   /* txns with an empty write set                               */
+  uint64_t nnz_w;        /* write accesses                                             */
+  uint64_t alg_bytes;    /* algorithmic bytes of one pass, SURVEY.md §8(d)             */
+  double device_ms;      /* device time of the decision, batch resident                */
+  double total_ms;       /* wall time of the call incl. H2D/D2H when host pointers      */
+  /* Per-phase device time (HIP events on the engine stream; filled only when
+   * profiling is enabled with dcc_set_profiling) and the algorithmic bytes
+   * of each phase.  OCC phases: 0 = key-hash build, 1 = round-1 probe,
+   * 2 = rounds >= 2 (sum), 3 = prep + finalize.  Calvin: 0 = build,
+   * 1 = grant groups, 2 = waves, 3 = prep + finalize. */
+  double phase_ms[4];
+  uint64_t phase_bytes[4];
+} dcc_stats;
+
+/* ------------------------------------------------------------- context  */
+typedef struct dcc_ctx dcc_ctx;
+
+/* Replaces OptCC::init (occ.cpp:33-40) and the global occ_man singleton
+ * (system/global.cpp:42): one context per process and device.
+ * device_id < 0 selects the current HIP device. */
+int dcc_init(dcc_ctx** out, int device_id);
+void dcc_destroy(dcc_ctx* ctx);
+const char* dcc_strerror(int code);
+const char* dcc_last_error(const dcc_ctx* ctx); /* detail of the last failure */
+int dcc_version(void);                            /* 100*major + minor */
+
+/* Run on an external HIP stream (opaque hipStream_t, e.g. torch's current
+ * stream).  NULL restores the context's own stream. */
+int dcc_set_stream(dcc_ctx* ctx, void* hip_stream);
+/* Record per-phase HIP events inside every call (dcc_stats.phase_ms). */
+int dcc_set_profiling(dcc_ctx* ctx, int enable);
+/* Pre-size device workspaces so a later call performs no allocation. */
+int dcc_reserve(dcc_ctx* ctx, uint64_t max_txn, uint64_t max_nnz);
+
+/* ------------------------------------------------------- multi-GPU     */
+/* Key sharding across the GPUs of one node, one process per GPU
+ * (SURVEY.md §8(e)).  Each rank owns keys with dcc_key_shard(key, n) == rank,
+ * receives the full per-txn offsets plus only its own accesses, and joins a
+ * per-round RCCL ncclMax allreduce of per-txn state bytes — the MI355X form
+ * of 2PC's AND of per-node OK bits (worker_thread.cpp:328-334). */
+#define DCC_UNIQUE_ID_BYTES 128
+int dcc_comm_unique_id(void* out_id /* DCC_UNIQUE_ID_BYTES */);
+int dcc_comm_init(dcc_ctx* ctx, int rank, int nranks, const void* unique_id);
+int dcc_comm_destroy(dcc_ctx* ctx);
+uint32_t dcc_key_shard(uint64_t key, uint32_t nranks);
+/* Host helper: keep only the accesses of `rank` (same n_txn, same order).
+ * out_offsets [n_txn+1]; out_keys/out_acctype sized >= in nnz; *out_nnz set. */
+int dcc_shard_filter(const dcc_batch* in, uint32_t rank, uint32_t nranks,
+                     uint32_t* out_offsets, uint64_t* out_keys,
+                     uint8_t* out_acctype, uint64_t* out_nnz);
+
+/* ------------------------------------------------------------------ OCC */
+/* Epoch validation: the result equals validating every txn of the batch in
+ * index order with OptCC::central_validate (occ.cpp:116-239) and only then
+ * finishing all of them with central_finish (occ.cpp:248-294).
+ *   out_rc[i]        = DCC_RC_RCOK or DCC_RC_ABORT (TxnManager::validate, txn.cpp:935)
+ *   out_commit_tn[i] = history tn given to committed non-read-only txns, else 0
+ *                      (tnc++ / wset->tn = tnc, occ.cpp:283-284); may be NULL. */
+int dcc_occ_validate_epoch(dcc_ctx* ctx, const dcc_batch* batch, uint8_t* out_rc,
+                           uint64_t* out_commit_tn, dcc_stats* out_stats);
+/* Committed write sets of earlier epochs (the `history` list, occ.h:62-64).
+ * keys/tn are host arrays of n (key, tn) pairs; each pair is one write of the
+ * committed txn numbered tn. */
+int dcc_occ_history_append(dcc_ctx* ctx, const uint64_t* keys, const uint64_t* tn, uint64_t n);
+int dcc_occ_history_clear(dcc_ctx* ctx);
+uint64_t dcc_occ_history_size(const dcc_ctx* ctx);
+/* The commit counter `tnc` (occ.h:67). */
+int dcc_occ_set_tnc(dcc_ctx* ctx, uint64_t tnc);
+uint64_t dcc_occ_get_tnc(const dcc_ctx* ctx);
+
+/* --------------------------------------------------------------- Calvin */
+/* Epoch lock ordering: the result equals the epoch's txns calling
+ * acquire_locks (ycsb_txn.cpp:49-88) in sequence order against an empty
+ * Row_lock table in CALVIN mode (row_lock.cpp:52-216), with per-txn row
+ * de-duplication (txn.cpp:778-782) and RD/SCAN->SH, else EX (row.cpp:191).
+ *   out_group[a] = grant group of request a on its row: 0 = granted at
+ *                  acquire, g = granted when group g-1 has fully released
+ *                  (lock_release promotion, row_lock.cpp:317-357);
+ *                  DCC_GROUP_NONE for a de-duplicated request.  May be NULL.
+ *   out_rc[i]    = DCC_RC_RCOK if every request is in group 0, else DCC_RC_WAIT
+ *                  (acquire_locks' return).
+ *   out_wave[i]  = wave in which txn i runs when every txn releases all its
+ *                  locks one wave after it became ready (may be NULL). */
+int dcc_calvin_order_epoch(dcc_ctx* ctx, const dcc_batch* batch, uint32_t* out_group,
+                           uint8_t* out_rc, uint32_t* out_wave, dcc_stats* out_stats);
+
+/* ----------------------------------------------------- batch producers */
+/* Deterministic restatements of the reference workload generators
+ * (SURVEY.md §8(a) a17/a18).  The reference seeds from the clock
+ * (ycsb_query.cpp:31); here every chunk of `chunk_txns` transactions draws
+ * from its own myrand stream (helper.cpp:144-147) seeded from `seed` and the
+ * chunk index, so batches are reproducible and can be generated in parallel. */
+typedef struct dcc_ycsb_params {
+  uint64_t n_txn;
+  uint32_t req_per_query;   /* REQ_PER_QUERY (config.h:177)                    */
+  uint32_t part_cnt;        /* PART_CNT                                        */
+  uint64_t table_size;      /* SYNTH_TABLE_SIZE (config.h:169)                 */
+  double zipf_theta;        /* ZIPF_THETA                                      */
+  double txn_write_perc;    /* TXN_WRITE_PERC                                  */
+  double tup_write_perc;    /* TUP_WRITE_PERC                                  */
+  uint32_t part_per_txn;    /* PART_PER_TXN (used with strict_ppt)             */
+  uint32_t strict_ppt;      /* STRICT_PPT                                      */
+  uint32_t first_part_local;/* FIRST_PART_LOCAL                                */
+  uint32_t chunk_txns;      /* txns per generator stream; also the txns per
+                               origin node for Calvin (home partition =
+                               chunk index % part_cnt)                         */
+  uint64_t seed;
+  uint32_t n_threads;       /* host threads used to generate (0 = auto)        */
+  uint32_t reserved;
+} dcc_ycsb_params;
+void dcc_ycsb_params_default(dcc_ycsb_params* p);
+/* offsets [n_txn+1], keys/acctype [n_txn*req_per_query]; home may be NULL. */
+int dcc_gen_ycsb(const dcc_ycsb_params* p, uint32_t* offsets, uint64_t* keys,
+                 uint8_t* acctype, uint32_t* home);
+
+typedef struct dcc_tpcc_params {
+  uint64_t n_txn;
+  uint32_t num_wh;          /* NUM_WH                                          */
+  uint32_t part_cnt;        /* PART_CNT (wh_to_part, tpcc_helper.cpp:161-164)  */
+  double perc_payment;      /* PERC_PAYMENT                                    */
+  uint32_t wh_update;       /* WH_UPDATE (config.h:194)                        */
+  uint32_t max_items;       /* MAX_ITEMS_NORM (config.h:187)                   */
+  uint32_t cust_per_dist;   /* CUST_PER_DIST_NORM (config.h:188)               */
+  uint32_t dist_per_wh;     /* DIST_PER_WH (config.h:223)                      */
+  uint32_t max_items_per_txn; /* MAX_ITEMS_PER_TXN (config.h:189)              */
+  uint32_t part_per_txn;
+  double mpr;               /* MPR                                             */
+  uint32_t first_part_local;
+  uint32_t chunk_txns;
+  uint64_t seed;
+  uint32_t n_threads;
+  uint32_t reserved;
+} dcc_tpcc_params;
+void dcc_tpcc_params_default(dcc_tpcc_params* p);
+/* Upper bound of accesses per TPC-C txn (NewOrder: 3 + 2*MAX_ITEMS_PER_TXN). */
+uint32_t dcc_tpcc_max_access(const dcc_tpcc_params* p);
+/* offsets [n_txn+1]; keys/acctype sized n_txn*dcc_tpcc_max_access(p);
+ * txn_type [n_txn] (TPCCTxnType: 1 = PAYMENT, 2 = NEW_ORDER) may be NULL. */
+int dcc_gen_tpcc(const dcc_tpcc_params* p, uint32_t* offsets, uint64_t* keys,
+                 uint8_t* acctype, uint8_t* txn_type, uint64_t* out_nnz);
+
+/* Canonical TPC-C key: (table_id << 56) | index key. */
+#define DCC_TPCC_KEY(table_id, ikey) ((((uint64_t)(table_id)) << 56) | ((uint64_t)(ikey)))
+
+/* Algorithmic bytes of one epoch pass:
+ * 4(N+1) + 9 nnz + 16 nnz_w + 16 nnz + N. */
+uint64_t dcc_alg_bytes(uint64_t n_txn, uint64_t nnz, uint64_t nnz_w);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DCC_H_ */

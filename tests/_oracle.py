@@ -1,0 +1,98 @@
+"""ctypes view of oracle/liboracle.so — the CPU restatements used as the checker.
+
+TEST INFRASTRUCTURE ONLY (see oracle/oracle.h): imported by tests/,
+__graft_entry__.smoke() and bench.py's cpu_baseline leg, never by deneva_amd.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+LIB = os.path.join(ORACLE_DIR, "liboracle.so")
+
+
+def _load():
+    srcs = [os.path.join(ORACLE_DIR, f) for f in ("occ_ref.c", "calvin_ref.c", "oracle.h", "kmap.h")]
+    if not os.path.exists(LIB) or any(os.path.getmtime(s) > os.path.getmtime(LIB) for s in srcs
+                                      if os.path.exists(s)):
+        subprocess.run(["make", "-C", ORACLE_DIR], check=True, capture_output=True)
+    lib = C.CDLL(LIB)
+    P = C.c_void_p
+    lib.oracle_occ_replay.argtypes = [C.c_uint64, P, P, P, P, P, C.c_uint64, P, P,
+                                      C.POINTER(C.c_uint64), P, P]
+    lib.oracle_occ_hash.argtypes = lib.oracle_occ_replay.argtypes
+    lib.oracle_occ_round_status.argtypes = [C.c_uint64, P, P, P, P, P]
+    lib.oracle_calvin_replay.argtypes = [C.c_uint64, P, P, P, P, P, P, P]
+    lib.oracle_calvin_formula.argtypes = lib.oracle_calvin_replay.argtypes
+    for f in (lib.oracle_occ_replay, lib.oracle_occ_hash, lib.oracle_occ_round_status,
+              lib.oracle_calvin_replay, lib.oracle_calvin_formula):
+        f.restype = C.c_int
+    return lib
+
+
+lib = _load()
+
+
+def _p(a):
+    return None if a is None else np.ascontiguousarray(a).ctypes.data
+
+
+def _arr(a, dt):
+    return None if a is None else np.ascontiguousarray(a, dt)
+
+
+def occ(batch, hist_keys=None, hist_tn=None, tnc=0, literal=False):
+    """Returns (rc u8[n], tn u64[n], tnc_after)."""
+    n = batch.n_txn
+    off = _arr(batch.offsets, np.uint32)
+    keys = _arr(batch.keys, np.uint64)
+    at = _arr(batch.acctype, np.uint8)
+    st = _arr(batch.start_tn, np.uint64)
+    ft = _arr(batch.finish_tn, np.uint64)
+    hk = _arr(hist_keys, np.uint64)
+    ht = _arr(hist_tn, np.uint64)
+    nh = 0 if hk is None else hk.shape[0]
+    rc = np.empty(max(n, 1), np.uint8)
+    tn = np.empty(max(n, 1), np.uint64)
+    t = C.c_uint64(tnc)
+    fn = lib.oracle_occ_replay if literal else lib.oracle_occ_hash
+    r = fn(n, _p(off), _p(keys), _p(at), _p(st), _p(ft), nh, _p(hk), _p(ht), C.byref(t),
+           rc.ctypes.data, tn.ctypes.data)
+    if r != 0:
+        raise RuntimeError(f"oracle occ failed: {r}")
+    return rc[:n], tn[:n], t.value
+
+
+def occ_round_status(batch, state):
+    n = batch.n_txn
+    off = _arr(batch.offsets, np.uint32)
+    keys = _arr(batch.keys, np.uint64)
+    at = _arr(batch.acctype, np.uint8)
+    state = _arr(state, np.uint8)
+    out = np.empty(max(n, 1), np.uint8)
+    r = lib.oracle_occ_round_status(n, _p(off), _p(keys), _p(at), _p(state), out.ctypes.data)
+    if r != 0:
+        raise RuntimeError("oracle round status failed")
+    return out[:n]
+
+
+def calvin(batch, literal=False):
+    """Returns (group u32[nnz], rc u8[n], wave u32[n])."""
+    n, nnz = batch.n_txn, batch.nnz
+    off = _arr(batch.offsets, np.uint32)
+    keys = _arr(batch.keys, np.uint64)
+    at = _arr(batch.acctype, np.uint8)
+    order = _arr(batch.order, np.uint64)
+    g = np.empty(max(nnz, 1), np.uint32)
+    rc = np.empty(max(n, 1), np.uint8)
+    w = np.empty(max(n, 1), np.uint32)
+    fn = lib.oracle_calvin_replay if literal else lib.oracle_calvin_formula
+    r = fn(n, _p(off), _p(keys), _p(at), _p(order), g.ctypes.data, rc.ctypes.data, w.ctypes.data)
+    if r != 0:
+        raise RuntimeError(f"oracle calvin failed: {r}")
+    return g[:nnz], rc[:n], w[:n]
