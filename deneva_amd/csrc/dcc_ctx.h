@@ -43,9 +43,11 @@ struct dcc_ctx {
   hipEvent_t pev[8] = {};  // phase boundary events (profiling only)
   std::string last_error;
   void* hmisc = nullptr;  // pinned host mirror of `misc`
+  void* hpart = nullptr;  // pinned host mirror of `part`
 
   // device workspaces (grow-only)
   DevBuf misc;                                   // counters / error words
+  DevBuf part;                                   // per-block partial reductions
   DevBuf off, keys, acctype, start_tn, finish_tn, order;  // staged host batch
   DevBuf table;                                  // Slot[cap]
   DevBuf state, hasw, rc, stat;                  // per-txn bytes
@@ -66,12 +68,14 @@ struct dcc_ctx {
   int fail(int code, const char* fmt, ...);
   int hip_fail(hipError_t e, const char* what);
   std::vector<DevBuf*> all_bufs();
-  int reserve_occ(uint64_t n, uint64_t nnz, uint64_t nnz_w);
+  int reserve_occ(uint64_t n, uint64_t nnz, uint64_t nnz_w, uint32_t tw);
+  void list_geometry(uint64_t n, uint32_t tw, uint64_t& seg_ts, uint64_t& seg_es) const;
   static uint64_t table_capacity(uint64_t nnz_w);
   int upload_history();
   int check_batch(const dcc_batch* b);
   int stage_batch(const dcc_batch* b, DevBatch& d);
   int device_prep(const DevBatch& d, uint32_t& maxlen, uint64_t& nnz_w);
+  int read_partials(size_t bytes);
   int occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dcc_stats* st);
   int occ_epoch_sharded(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dcc_stats* st);
   int calvin_epoch(const dcc_batch* b, uint32_t* out_group, uint8_t* out_rc, uint32_t* out_wave,

@@ -117,7 +117,9 @@ extern "C" int dcc_init(dcc_ctx** out, int device_id) {
   CK(hipEventCreate(&ctx->ev1));
   for (auto& e : ctx->pev) CK(hipEventCreate(&e));
   CK(hipHostMalloc((void**)&ctx->hmisc, 4096, hipHostMallocDefault));
+  CK(hipHostMalloc((void**)&ctx->hpart, 1 << 16, hipHostMallocDefault));
   int rc = ctx->misc.ensure(ctx, 4096, "misc");
+  if (!rc) rc = ctx->part.ensure(ctx, 1 << 16, "partials");
   if (rc) {
     dcc_destroy(ctx);
     return rc;
@@ -133,6 +135,7 @@ extern "C" void dcc_destroy(dcc_ctx* ctx) {
   dcc_comm_destroy(ctx);
   for (DevBuf* b : ctx->all_bufs()) b->release();
   if (ctx->hmisc) (void)hipHostFree(ctx->hmisc);
+  if (ctx->hpart) (void)hipHostFree(ctx->hpart);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   for (auto& e : ctx->pev)
@@ -154,7 +157,7 @@ extern "C" int dcc_set_stream(dcc_ctx* ctx, void* s) {
 }
 
 std::vector<DevBuf*> dcc_ctx::all_bufs() {
-  std::vector<DevBuf*> v = {&misc, &off, &keys, &acctype, &start_tn, &finish_tn, &table, &state,
+  std::vector<DevBuf*> v = {&misc, &part, &off, &keys, &acctype, &start_tn, &finish_tn, &table, &state,
                             &hasw, &cflag, &bsum, &tn, &rc, &hkeys, &hoff, &htn, &stat,
                             &order, &perm, &calvin_a, &calvin_b, &calvin_c, &calvin_d};
   for (int i = 0; i < 2; i++) {
@@ -165,32 +168,11 @@ std::vector<DevBuf*> dcc_ctx::all_bufs() {
   return v;
 }
 
-int dcc_ctx::reserve_occ(uint64_t n, uint64_t nnz, uint64_t nnz_w) {
-  dcc_ctx* ctx = this;
-  CR(state.ensure(this, n, "state"));
-  CR(hasw.ensure(this, n, "hasw"));
-  CR(rc.ensure(this, n, "rc"));
-  CR(stat.ensure(this, n, "stat"));
-  for (int i = 0; i < 2; i++) {
-    CR(l_tid[i].ensure(this, n * 4 + 64, "list tid"));
-    CR(l_coff[i].ensure(this, n * 4 + 64, "list off"));
-    CR(l_cent[i].ensure(this, nnz * 4 + 64, "list entries"));
-  }
-  const uint64_t cap = table_capacity(nnz_w);
-  CR(table.ensure(this, cap * sizeof(Slot), "table"));
-  (void)ctx;
-  return DCC_OK;
-}
-
-uint64_t dcc_ctx::table_capacity(uint64_t nnz_w) {
-  // load factor <= 0.8 even if every write key is distinct
-  return std::max<uint64_t>(1024, next_pow2(nnz_w + nnz_w / 4 + 1));
-}
-
 extern "C" int dcc_reserve(dcc_ctx* ctx, uint64_t max_txn, uint64_t max_nnz) {
   if (!ctx) return DCC_EINVAL;
   (void)hipSetDevice(ctx->device);
-  return ctx->reserve_occ(max_txn, max_nnz, max_nnz);
+  const uint32_t tw = 16;  // worst case: MAX_ROW_PER_TXN-long txns
+  return ctx->reserve_occ(max_txn, max_nnz, max_nnz, tw);
 }
 
 // ---------------------------------------------------------------- history
@@ -311,229 +293,6 @@ int dcc_ctx::stage_batch(const dcc_batch* b, DevBatch& d) {
     CK(hipMemcpyAsync(order.p, b->order, d.n * 8, hipMemcpyHostToDevice, stream));
     d.order = (const uint64_t*)order.p;
   }
-  return DCC_OK;
-}
-
-// Offsets check + max length + write count on the device (one sync).
-int dcc_ctx::device_prep(const DevBatch& d, uint32_t& maxlen, uint64_t& nnz_w) {
-  dcc_ctx* ctx = this;
-  uint32_t* info = (uint32_t*)misc.p;  // [0] err [1] maxlen; [2..3] nnz_w (u64)
-  CK(hipMemsetAsync(misc.p, 0, 64, stream));
-  launch_prep(d.off, d.n, d.nnz, info, stream);
-  if (d.nnz) launch_count_writes(d.acctype, d.nnz, (unsigned long long*)(info + 2), stream);
-  CK(hipGetLastError());
-  CK(hipMemcpyAsync(hmisc, misc.p, 64, hipMemcpyDeviceToHost, stream));
-  CK(hipStreamSynchronize(stream));
-  const uint32_t* h = (const uint32_t*)hmisc;
-  if (h[0] & ERR_OFFSETS) return fail(DCC_EINVAL, "batch: malformed offsets");
-  maxlen = h[1];
-  nnz_w = *(const uint64_t*)(h + 2);
-  if (maxlen > MAX_TXN_LEN)
-    return fail(DCC_ERANGE, "batch: a txn has %u accesses (> MAX_ROW_PER_TXN=%u)", maxlen,
-                MAX_TXN_LEN);
-  return DCC_OK;
-}
-
-// ---------------------------------------------------------------- OCC epoch
-int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dcc_stats* st) {
-  dcc_ctx* ctx = this;
-  const auto t_wall0 = std::chrono::steady_clock::now();
-  CR(check_batch(b));
-  const bool dev_out = (b->flags & DCC_DEVICE_PTRS) != 0;
-  dcc_stats S;
-  memset(&S, 0, sizeof S);
-  S.n_shards = comm_ranks();
-  if (b->n_txn == 0) {
-    if (st) *st = S;
-    return DCC_OK;
-  }
-  DevBatch d;
-  CR(stage_batch(b, d));
-  CK(hipEventRecord(ev0, stream));  // device clock starts with the batch resident
-  uint32_t maxlen = 0;
-  uint64_t nnz_w = 0;
-  CR(device_prep(d, maxlen, nnz_w));
-  CR(reserve_occ(d.n, d.nnz, nnz_w));
-  const uint64_t cap = table_capacity(nnz_w);
-  const uint32_t mask = (uint32_t)(cap - 1);
-  if (cap > (1ull << 30)) return fail(DCC_ERANGE, "table capacity exceeds 2^30 slots");
-  const uint32_t tw = std::min<uint32_t>(64, TILE_CAP / std::max<uint32_t>(1, maxlen));
-  Slot* tab = (Slot*)table.p;
-  uint32_t* err = (uint32_t*)misc.p + 16;
-  unsigned long long* ctr = (unsigned long long*)((uint32_t*)misc.p + 32);
-  uint64_t* counts = (uint64_t*)((uint32_t*)misc.p + 64);
-  uint64_t* d_nnzw = (uint64_t*)((uint32_t*)misc.p + 96);
-
-  CK(hipMemsetAsync(misc.p, 0, 1024, stream));
-  CK(hipMemsetAsync(table.p, 0xFF, cap * sizeof(Slot), stream));
-  CK(hipMemsetAsync(state.p, 0, d.n, stream));
-
-  // history window pre-pass (occ.cpp:160-180)
-  const bool use_hist = d.start_tn && !hist.empty();
-  if (use_hist) {
-    CR(upload_history());
-    HistArgs ha{d.n, d.off, d.keys, d.acctype, d.start_tn, d.finish_tn,
-                (const uint64_t*)hkeys.p, h_nkeys, (const uint64_t*)hoff.p,
-                (const uint64_t*)htn.p, (uint8_t*)state.p};
-    launch_hist(ha, stream);
-  }
-
-  BuildArgs ba{d.n, tw, d.off, d.keys, d.acctype, tab, mask, (const uint8_t*)state.p,
-               (uint8_t*)hasw.p, d_nnzw, err};
-  if (profiling) CK(hipEventRecord(pev[0], stream));
-  launch_build(ba, stream);
-  CK(hipGetLastError());
-  if (profiling) CK(hipEventRecord(pev[1], stream));
-  double ph_rest = 0;
-
-  // ---- fixed-point rounds
-  uint64_t m = d.n;
-  uint32_t end_total = (uint32_t)d.nnz;
-  int cur = 0;
-  uint32_t rt = 1;  // round tag
-  uint32_t rounds = 0;
-  for (;;) {
-    const bool first = rounds == 0;
-    if (rt > MAX_ROUND_TAG) {
-      // tag space exhausted: drop stale owner words, republish from the list
-      launch_retag(tab, cap, stream);
-      OwnerArgs oa{m, 1, end_total, (const uint32_t*)l_tid[cur].p,
-                   (const uint32_t*)l_coff[cur].p, (const uint32_t*)l_cent[cur].p, tab};
-      launch_owner_list(oa, stream);
-      rt = 1;
-    }
-    CK(hipMemsetAsync(ctr, 0, 8, stream));
-    RoundArgs ra;
-    ra.m = m;
-    ra.tw = tw;
-    ra.r = rt;
-    ra.end_total = end_total;
-    ra.tid = first ? nullptr : (const uint32_t*)l_tid[cur].p;
-    ra.coff = first ? d.off : (const uint32_t*)l_coff[cur].p;
-    ra.keys = d.keys;
-    ra.acctype = d.acctype;
-    ra.cent = first ? nullptr : (const uint32_t*)l_cent[cur].p;
-    ra.tab = tab;
-    ra.mask = mask;
-    ra.state = (uint8_t*)state.p;
-    ra.tid_out = (uint32_t*)l_tid[cur ^ 1].p;
-    ra.coff_out = (uint32_t*)l_coff[cur ^ 1].p;
-    ra.cent_out = (uint32_t*)l_cent[cur ^ 1].p;
-    ra.ctr = ctr;
-    ra.err = err;
-    if (profiling && !first) CK(hipEventRecord(pev[3], stream));
-    launch_round(ra, first, stream);
-    CK(hipGetLastError());
-    if (profiling) CK(hipEventRecord(first ? pev[2] : pev[4], stream));
-    rounds++;
-    CK(hipMemcpyAsync(hmisc, ctr, 8, hipMemcpyDeviceToHost, stream));
-    CK(hipStreamSynchronize(stream));
-    if (profiling && !first) {
-      float t = 0;
-      CK(hipEventElapsedTime(&t, pev[3], pev[4]));
-      ph_rest += t;
-    }
-    const unsigned long long c = *(const unsigned long long*)hmisc;
-    m = c >> CTR_E_BITS;
-    end_total = (uint32_t)(c & CTR_E_MASK);
-    cur ^= 1;
-    rt++;
-    if (m == 0) break;
-    if (rounds > d.n + 2) return fail(DCC_EIO, "fixed point did not converge");
-  }
-
-  // ---- finalize
-  uint8_t* rc_dev = (dev_out && out_rc) ? out_rc : (uint8_t*)rc.p;
-  uint32_t* cf = nullptr;
-  const bool want_tn = out_tn != nullptr || (b->flags & DCC_OCC_APPEND_HISTORY);
-  if (want_tn) {
-    CR(cflag.ensure(this, d.n * 4, "cflag"));
-    CR(bsum.ensure(this, ((d.n + 1023) / 1024 + 1) * 8, "bsum"));
-    CR(tn.ensure(this, d.n * 8, "tn"));
-    cf = (uint32_t*)cflag.p;
-  }
-  FinalArgs fa{d.n, (const uint8_t*)state.p, (const uint8_t*)hasw.p, rc_dev, cf, counts, err};
-  launch_final(fa, stream);
-  uint64_t* tn_dev = nullptr;
-  if (want_tn) {
-    tn_dev = (dev_out && out_tn) ? out_tn : (uint64_t*)tn.p;
-    launch_commit_tn(cf, d.n, (uint64_t*)bsum.p, tnc, tn_dev, stream);
-  }
-  CK(hipGetLastError());
-  CK(hipEventRecord(ev1, stream));
-  if (!dev_out) {
-    if (out_rc) CK(hipMemcpyAsync(out_rc, rc.p, d.n, hipMemcpyDeviceToHost, stream));
-    if (out_tn) CK(hipMemcpyAsync(out_tn, tn.p, d.n * 8, hipMemcpyDeviceToHost, stream));
-  }
-  CK(hipMemcpyAsync(hmisc, misc.p, 1024, hipMemcpyDeviceToHost, stream));
-  CK(hipStreamSynchronize(stream));
-  const uint32_t* hm = (const uint32_t*)hmisc;
-  const uint32_t e = hm[16];
-  if (e & ERR_KEY) return fail(DCC_EINVAL, "batch: key equal to DCC_KEY_RESERVED");
-  if (e & ERR_FULL) return fail(DCC_EIO, "hash table overflow");
-  if (e & ERR_TILE) return fail(DCC_EIO, "tile capacity exceeded");
-  if (e & ERR_UNDECIDED) return fail(DCC_EIO, "undecided transaction after convergence");
-  const uint64_t* hc = (const uint64_t*)(hm + 64);
-  float ms = 0;
-  CK(hipEventElapsedTime(&ms, ev0, ev1));
-  S.rounds = rounds;
-  S.n_commit = hc[0];
-  S.n_abort = hc[1];
-  S.n_readonly = hc[2];
-  S.nnz_w = *(const uint64_t*)(hm + 96);
-  S.alg_bytes = dcc_alg_bytes(d.n, d.nnz, S.nnz_w);
-  S.device_ms = ms;
-  if (profiling) {
-    float t0 = 0, t1 = 0;
-    CK(hipEventElapsedTime(&t0, pev[0], pev[1]));
-    CK(hipEventElapsedTime(&t1, pev[1], pev[2]));
-    S.phase_ms[0] = t0;
-    S.phase_ms[1] = t1;
-    S.phase_ms[2] = ph_rest;
-    S.phase_ms[3] = ms - t0 - t1 - ph_rest;
-  }
-  // algorithmic bytes per phase: build reads acctype for all
-  // accesses and keys of writes, one 16-B slot update per write; round 1
-  // reads offsets, keys+acctype, one 16-B slot per access, state byte.
-  S.phase_bytes[0] = d.nnz + 8 * S.nnz_w + 16 * S.nnz_w + 4 * (d.n + 1) + d.n;
-  S.phase_bytes[1] = 4 * (d.n + 1) + 9 * d.nnz + 16 * d.nnz + d.n;
-
-  // central_finish (occ.cpp:283-286): committed non-read-only txns take
-  // tn = tnc+1, tnc+2, ... in index order; their write sets join the history.
-  const uint64_t n_cw = hc[3];
-  if (b->flags & DCC_OCC_APPEND_HISTORY) {
-    std::vector<uint64_t> htn_host(d.n);
-    CK(hipMemcpy(htn_host.data(), tn_dev, d.n * 8, hipMemcpyDeviceToHost));
-    std::vector<uint32_t> ho;
-    std::vector<uint64_t> hk;
-    std::vector<uint8_t> ha;
-    const uint32_t* o = b->offsets;
-    const uint64_t* k = b->keys;
-    const uint8_t* at = b->acctype;
-    if (dev_out) {
-      ho.resize(d.n + 1);
-      hk.resize(d.nnz);
-      ha.resize(d.nnz);
-      CK(hipMemcpy(ho.data(), d.off, (d.n + 1) * 4, hipMemcpyDeviceToHost));
-      if (d.nnz) {
-        CK(hipMemcpy(hk.data(), d.keys, d.nnz * 8, hipMemcpyDeviceToHost));
-        CK(hipMemcpy(ha.data(), d.acctype, d.nnz, hipMemcpyDeviceToHost));
-      }
-      o = ho.data();
-      k = hk.data();
-      at = ha.data();
-    }
-    for (uint64_t t = 0; t < d.n; t++) {
-      if (!htn_host[t]) continue;
-      for (uint32_t x = o[t]; x < o[t + 1]; x++)
-        if (at[x] == DCC_WR) hist.emplace_back(k[x], htn_host[t]);
-    }
-    if (n_cw) hist_dirty = true;
-  }
-  tnc += n_cw;
-  const auto t_wall1 = std::chrono::steady_clock::now();
-  S.total_ms = std::chrono::duration<double, std::milli>(t_wall1 - t_wall0).count();
-  if (st) *st = S;
   return DCC_OK;
 }
 

@@ -15,6 +15,8 @@ constexpr uint32_t MAX_ROUND_TAG = 61;  // largest round tag a k_round may run w
 // list-reservation counter: txns in the high bits, entries in the low bits
 constexpr uint32_t CTR_E_BITS = 38;
 constexpr unsigned long long CTR_E_MASK = (1ull << CTR_E_BITS) - 1ull;
+constexpr uint32_t CTR_RING = 64;  // per-round counter sets kept on the device
+constexpr uint32_t NSEG = 8;       // list segments (one reservation counter each)
 
 // error bits reported by kernels
 constexpr uint32_t ERR_OFFSETS = 1;
@@ -22,6 +24,15 @@ constexpr uint32_t ERR_TILE = 2;
 constexpr uint32_t ERR_KEY = 4;
 constexpr uint32_t ERR_FULL = 8;
 constexpr uint32_t ERR_UNDECIDED = 16;
+
+constexpr unsigned PREP_BLOCKS = 512;
+constexpr unsigned FINAL_BLOCKS = 512;
+struct PrepPart {
+  uint32_t err, maxlen, nw, pad;
+};
+struct FinalPart {
+  uint32_t commit, abort, readonly, cwriters, undecided, pad0, pad1, pad2;
+};
 
 struct HistArgs {
   uint64_t n;
@@ -47,12 +58,12 @@ struct BuildArgs {
   uint32_t mask;
   const uint8_t* state;
   uint8_t* hasw;
-  uint64_t* nnz_w;
   uint32_t* err;
 };
 
 struct RoundArgs {
-  uint64_t m;             // txns in the input list
+  const unsigned long long* m_in;  // previous round's NSEG counters (list size) or null
+  uint64_t m;             // txns in the input list (when m_in is null)
   uint32_t tw;            // txns per wave
   uint32_t r;             // round tag (1..MAX_ROUND_TAG)
   uint32_t end_total;     // coff[m] (entries in the input list)
@@ -61,23 +72,26 @@ struct RoundArgs {
   const uint64_t* keys;   // round 1 input
   const uint8_t* acctype; // round 1 input
   const uint32_t* cent;   // rounds >= 2 input: ENT_WRITE | sid
+  uint64_t seg_ts;        // segment stride of tid/coff arrays
+  uint64_t seg_es;        // segment stride of entry arrays
   Slot* tab;
   uint32_t mask;
   uint8_t* state;
   uint32_t* tid_out;
   uint32_t* coff_out;
   uint32_t* cent_out;
-  unsigned long long* ctr;
+  unsigned long long* ctr;       // this round's NSEG reservation counters
+  unsigned long long* ctr_zero;  // next round's NSEG counters, zeroed here
   uint32_t* err;
 };
 
 struct OwnerArgs {
-  uint64_t m;
+  const unsigned long long* m_in;  // NSEG counters of the list
   uint32_t r;
-  uint32_t end_total;
   const uint32_t* tid;
   const uint32_t* coff;
   const uint32_t* cent;
+  uint64_t seg_ts, seg_es;
   Slot* tab;
 };
 
@@ -87,20 +101,20 @@ struct FinalArgs {
   const uint8_t* hasw;
   uint8_t* rc;
   uint32_t* cflag;
-  uint64_t* counts;  // [0] commit [1] abort [2] readonly [3] committed writers
-  uint32_t* err;
+  FinalPart* part;  // [FINAL_BLOCKS]
 };
 
 // launchers (occ_kernels.hip)
-void launch_prep(const uint32_t* off, uint64_t n, uint64_t nnz, uint32_t* info, hipStream_t st);
+void launch_prep(const uint32_t* off, uint64_t n, const uint8_t* at, uint64_t nnz,
+                 PrepPart* part, hipStream_t st);
 void launch_hist(const HistArgs& a, hipStream_t st);
-void launch_build(const BuildArgs& a, hipStream_t st);
-void launch_round(const RoundArgs& a, bool from_keys, hipStream_t st);
+void launch_build(const BuildArgs& a, unsigned max_grid, hipStream_t st);
+void launch_round(const RoundArgs& a, bool from_keys, uint64_t m_bound, unsigned max_grid,
+                  hipStream_t st);
 void launch_retag(Slot* tab, uint64_t cap, hipStream_t st);
-void launch_owner_list(const OwnerArgs& a, hipStream_t st);
+void launch_owner_list(const OwnerArgs& a, uint64_t m_bound, hipStream_t st);
 void launch_final(const FinalArgs& a, hipStream_t st);
 void launch_commit_tn(const uint32_t* cflag, uint64_t n, uint64_t* bsum, uint64_t tnc,
                       uint64_t* tn, hipStream_t st);
-void launch_count_writes(const uint8_t* at, uint64_t nnz, unsigned long long* cnt, hipStream_t st);
 
 }  // namespace dcc

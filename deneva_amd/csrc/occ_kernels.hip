@@ -32,28 +32,58 @@
 namespace dcc {
 
 // --------------------------------------------------------------------------
-// k_prep: offset validation + max txn length (one pass over offsets).
+// k_prep: offset validation, max txn length and write count in one pass over
+// offsets + acctype.  Per-block partials (no same-address atomics: one word
+// serialises device atomics at ~100/us, MI355X_MICROARCH.md "dequeue");
+// the host reduces them after its one synchronisation.
+__device__ inline uint32_t block_sum_u32(uint32_t v, uint32_t* sh) {
+  for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint32_t t = 0;
+  for (uint32_t w = 0; w < (blockDim.x >> 6); w++) t += sh[w];
+  return t;
+}
+__device__ inline uint32_t block_max_u32(uint32_t v, uint32_t* sh) {
+  for (int d = 32; d > 0; d >>= 1) v = max(v, (uint32_t)__shfl_xor(v, d));
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint32_t t = 0;
+  for (uint32_t w = 0; w < (blockDim.x >> 6); w++) t = max(t, sh[w]);
+  return t;
+}
+
 __global__ __launch_bounds__(256) void k_prep(const uint32_t* __restrict__ off, uint64_t n,
-                                              uint64_t nnz, uint32_t* __restrict__ info) {
-  // info[0] = error bits, info[1] = max length
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t len = 0, bad = 0;
-  if (t < n) {
-    const uint32_t a = off[t], b = off[t + 1];
-    if (b < a) bad = ERR_OFFSETS;
-    else len = b - a;
-    if (t == 0 && a != 0) bad = ERR_OFFSETS;
-    if (t == n - 1 && b != nnz) bad = ERR_OFFSETS;
+                                              const uint8_t* __restrict__ at, uint64_t nnz,
+                                              PrepPart* __restrict__ part) {
+  __shared__ uint32_t sh[4];
+  uint32_t len = 0, bad = 0, nw = 0;
+  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t t = tid; t < n; t += stride) {
+    const uint32_t a0 = off[t], b0 = off[t + 1];
+    if (b0 < a0) bad |= ERR_OFFSETS;
+    else len = max(len, b0 - a0);
+    if (t == 0 && a0 != 0) bad |= ERR_OFFSETS;
+    if (t == n - 1 && b0 != nnz) bad |= ERR_OFFSETS;
   }
-  // wave reduce
-  for (int d = 32; d > 0; d >>= 1) {
-    len = max(len, (uint32_t)__shfl_xor(len, d));
-    bad |= (uint32_t)__shfl_xor(bad, d);
+  // acctype: 16 bytes per thread per step when aligned
+  for (uint64_t x = tid * 16; x < nnz; x += stride * 16) {
+    if (x + 16 <= nnz && ((uintptr_t)(at + x) & 15) == 0) {
+      const uint4 v = *reinterpret_cast<const uint4*>(at + x);
+      const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+      for (int q = 0; q < 4; q++)
+        for (int bb = 0; bb < 4; bb++) nw += ((w4[q] >> (8 * bb)) & 0xFFu) == 1u;
+    } else {
+      for (uint64_t y = x; y < nnz && y < x + 16; y++) nw += at[y] == 1;
+    }
   }
-  if ((threadIdx.x & 63) == 0) {
-    if (len) atomicMax(&info[1], len);
-    if (bad) atomicOr(&info[0], bad);
-  }
+  const uint32_t tl = block_max_u32(len, sh);
+  const uint32_t tb = block_max_u32(bad, sh);  // error bits are 0/1 flags: max == or here
+  const uint32_t tw = block_sum_u32(nw, sh);
+  if (threadIdx.x == 0) part[blockIdx.x] = PrepPart{tb, tl, tw, 0};
 }
 
 // --------------------------------------------------------------------------
@@ -135,6 +165,56 @@ __device__ inline bool tile_open(uint64_t j0, uint32_t tw, uint64_t m, const uin
   return true;
 }
 
+// 16-byte slot read: key and both owner words in one load.
+struct SlotV {
+  uint64_t key;
+  uint32_t own0, own1;
+};
+__device__ inline SlotV ld_slot(const Slot* p) {
+  const uint4 v = *reinterpret_cast<const uint4*>(p);
+  return SlotV{((uint64_t)v.y << 32) | v.x, v.z, v.w};
+}
+
+// List geometry of a round.  Round 1 reads the batch CSR (one segment,
+// identity txn ids); later rounds read the NSEG segments written by the
+// previous round, whose sizes sit in its device counters (so the host can
+// enqueue rounds without synchronising).  A workgroup-tile never straddles
+// two segments.
+struct ListGeo {
+  uint64_t pre[NSEG + 1];  // prefix of workgroup-tiles per segment
+  uint64_t m[NSEG];
+  uint32_t end[NSEG];
+  uint32_t nseg;
+};
+
+__device__ inline void list_geo(const unsigned long long* m_in, uint64_t m_host, uint32_t end_host,
+                                uint64_t per_wg, ListGeo& G) {
+  G.pre[0] = 0;
+  if (!m_in) {
+    G.nseg = 1;
+    G.m[0] = m_host;
+    G.end[0] = end_host;
+    G.pre[1] = (m_host + per_wg - 1) / per_wg;
+    return;
+  }
+  G.nseg = NSEG;
+#pragma unroll
+  for (uint32_t q = 0; q < NSEG; q++) {
+    const unsigned long long c = m_in[q];
+    G.m[q] = c >> CTR_E_BITS;
+    G.end[q] = (uint32_t)(c & CTR_E_MASK);
+    G.pre[q + 1] = G.pre[q] + (G.m[q] + per_wg - 1) / per_wg;
+  }
+}
+
+__device__ inline uint32_t geo_seg(const ListGeo& G, uint64_t g) {
+  uint32_t q = 0;
+  while (q + 1 < G.nseg && g >= G.pre[q + 1]) q++;
+  return q;
+}
+
+constexpr int ILP = 4;  // 64-access steps in flight per wave
+
 // --------------------------------------------------------------------------
 // k_build: insert write keys, round-1 owners, per-txn has-write flag.
 template <int CAP, int WAVES>
@@ -142,53 +222,51 @@ __global__ __launch_bounds__(WAVES * 64) void k_build(BuildArgs a) {
   __shared__ uint8_t s_map[WAVES][CAP];
   __shared__ uint32_t s_txn[WAVES][64];
   __shared__ uint32_t s_stat[WAVES][64];
-  __shared__ uint32_t s_nw[WAVES];
   const uint32_t wv = threadIdx.x >> 6, lane = lane_id();
-  const uint64_t j0 = ((uint64_t)blockIdx.x * WAVES + wv) * a.tw;
   uint8_t* map = s_map[wv];
-  Tile T;
-  uint32_t txn, s, e;
-  bool part = true;
-  if (lane < a.tw && j0 + lane < a.n) part = a.state[j0 + lane] == ST_UNDECIDED;
-  const bool live = tile_open<CAP>(j0, a.tw, a.n, nullptr, a.off, 0, part, map, s_txn[wv], T,
-                                   txn, s, e, a.err);
-  s_stat[wv][lane] = 0;
-  __syncthreads();
-  uint32_t nw = 0;
-  if (live) {
-    const uint32_t tag1 = own_word(round_tag(1), 0);
-    for (uint32_t base = T.A0; base < T.A1; base += 64) {
-      const uint32_t x = base + lane;
-      const bool act = x < T.A1;
-      const uint32_t lt = act ? map[x - T.A0] : 0xFFu;
-      bool w = false;
-      if (lt != 0xFFu) {
-        w = a.acctype[x] == 1 /* WR */;
-        if (w) {
-          const uint64_t key = a.keys[x];
-          if (key == KEY_EMPTY) {
-            atomicOr(a.err, ERR_KEY);
-          } else {
-            const uint32_t sid = table_insert(a.tab, a.mask, key);
-            if (sid == SID_NONE) atomicOr(a.err, ERR_FULL);
-            else own_min(&a.tab[sid].own[1], tag1 | s_txn[wv][lt]);
+  const uint32_t tag1 = own_word(round_tag(1), 0);
+  for (uint64_t tile = blockIdx.x; tile * WAVES * a.tw < a.n; tile += gridDim.x) {
+    const uint64_t j0 = (tile * WAVES + wv) * a.tw;
+    Tile T;
+    uint32_t txn, s, e;
+    bool part = true;
+    if (lane < a.tw && j0 + lane < a.n) part = a.state[j0 + lane] == ST_UNDECIDED;
+    const bool live = tile_open<CAP>(j0, a.tw, a.n, nullptr, a.off, 0, part, map, s_txn[wv], T,
+                                     txn, s, e, a.err);
+    s_stat[wv][lane] = 0;
+    __syncthreads();
+    if (live) {
+      for (uint32_t base = T.A0; base < T.A1; base += 64 * ILP) {
+        uint32_t lt[ILP];
+        bool w[ILP];
+        uint64_t key[ILP];
+#pragma unroll
+        for (int u = 0; u < ILP; u++) {
+          const uint32_t x = base + 64 * u + lane;
+          lt[u] = x < T.A1 ? map[x - T.A0] : 0xFFu;
+          w[u] = lt[u] != 0xFFu && a.acctype[x] == 1 /* WR */;
+        }
+#pragma unroll
+        for (int u = 0; u < ILP; u++) key[u] = w[u] ? a.keys[base + 64 * u + lane] : 0;
+#pragma unroll
+        for (int u = 0; u < ILP; u++) {
+          if (w[u]) {
+            if (key[u] == KEY_EMPTY) {
+              atomicOr(a.err, ERR_KEY);
+            } else {
+              const uint32_t sid = table_insert(a.tab, a.mask, key[u]);
+              if (sid == SID_NONE) atomicOr(a.err, ERR_FULL);
+              else own_min(&a.tab[sid].own[1], tag1 | s_txn[wv][lt[u]]);
+            }
           }
+          bool head;
+          const uint32_t v = segment_or2(lt[u], w[u] ? 1u : 0u, head);
+          if (head && lt[u] != 0xFFu && v) atomicOr(&s_stat[wv][lt[u]], v);
         }
       }
-      nw += w ? 1u : 0u;
-      bool head;
-      const uint32_t v = segment_or2(lt, w ? 1u : 0u, head);
-      if (head && lt != 0xFFu && v) atomicOr(&s_stat[wv][lt], v);
     }
-  }
-  for (int d = 32; d > 0; d >>= 1) nw += __shfl_xor(nw, d);
-  if (lane == 0) s_nw[wv] = nw;
-  __syncthreads();
-  if (live && lane < T.nt) a.hasw[j0 + lane] = s_stat[wv][lane] ? 1 : 0;
-  if (threadIdx.x == 0) {
-    uint32_t tot = 0;
-    for (int w = 0; w < WAVES; w++) tot += s_nw[w];
-    if (tot) atomicAdd((unsigned long long*)a.nnz_w, (unsigned long long)tot);
+    __syncthreads();
+    if (live && lane < T.nt) a.hasw[j0 + lane] = s_stat[wv][lane] ? 1 : 0;
   }
 }
 
@@ -205,140 +283,210 @@ __global__ __launch_bounds__(WAVES * 64) void k_round(RoundArgs a) {
   __shared__ unsigned long long s_base;
 
   const uint32_t wv = threadIdx.x >> 6, lane = lane_id();
-  const uint64_t j0 = ((uint64_t)blockIdx.x * WAVES + wv) * a.tw;
   uint8_t* map = s_map[wv];
   uint32_t* ent = s_ent[wv];
   const uint32_t rb = a.r & 1u, nb = (a.r + 1) & 1u;
   const uint32_t tag_r = round_tag(a.r);
   const uint32_t tag_n = own_word(round_tag(a.r + 1), 0);
-
-  Tile T;
-  uint32_t txn, s, e;
-  bool part = true;
-  if (FROM_KEYS && lane < a.tw && j0 + lane < a.m) part = a.state[j0 + lane] == ST_UNDECIDED;
-  const bool live = tile_open<CAP>(j0, a.tw, a.m, a.tid, a.coff, a.end_total, part, map,
-                                   s_txn[wv], T, txn, s, e, a.err);
-  s_stat[wv][lane] = 0;
+  const uint64_t per_wg = (uint64_t)WAVES * a.tw;
+  __shared__ ListGeo G;  // in LDS: runtime-indexed register arrays go to scratch
+  if (threadIdx.x == 0) list_geo(a.m_in, a.m, a.end_total, per_wg, G);
+  if (blockIdx.x == 0 && threadIdx.x < NSEG) a.ctr_zero[threadIdx.x] = 0ull;
   __syncthreads();
 
-  // ---- phase 1: probe every access of the tile (coalesced)
-  if (live) {
-    for (uint32_t base = T.A0; base < T.A1; base += 64) {
-      const uint32_t x = base + lane;
-      const bool act = x < T.A1;
-      const uint32_t lt = act ? map[x - T.A0] : 0xFFu;
-      uint32_t en = SID_NONE, ps = 0;
-      if (lt != 0xFFu) {
-        const uint32_t i = s_txn[wv][lt];
+  for (uint64_t tile = blockIdx.x; tile < G.pre[G.nseg]; tile += gridDim.x) {
+    const uint32_t sg = geo_seg(G, tile);
+    const uint64_t m = G.m[sg];
+    const uint32_t* tid_s = a.tid ? a.tid + sg * a.seg_ts : nullptr;
+    const uint32_t* coff_s = a.m_in ? a.coff + sg * a.seg_ts : a.coff;
+    const uint32_t* cent_s = a.cent ? a.cent + sg * a.seg_es : nullptr;
+    const uint64_t j0 = (tile - G.pre[sg]) * per_wg + (uint64_t)wv * a.tw;
+    // output segment of this workgroup-tile
+    const uint32_t og = (uint32_t)(tile % NSEG);
+    uint32_t* tid_o = a.tid_out + og * a.seg_ts;
+    uint32_t* coff_o = a.coff_out + og * a.seg_ts;
+    uint32_t* cent_o = a.cent_out + og * a.seg_es;
+    Tile T;
+    uint32_t txn, s, e;
+    bool part = true;
+    if (FROM_KEYS && lane < a.tw && j0 + lane < m) part = a.state[j0 + lane] == ST_UNDECIDED;
+    const bool live = tile_open<CAP>(j0, a.tw, m, tid_s, coff_s, G.end[sg], part, map,
+                                     s_txn[wv], T, txn, s, e, a.err);
+    s_stat[wv][lane] = 0;
+    __syncthreads();
+
+    // ---- phase 1: probe every access of the tile (coalesced, ILP steps)
+    if (live) {
+      for (uint32_t base = T.A0; base < T.A1; base += 64 * ILP) {
+        uint32_t lt[ILP], en[ILP], ow[ILP];
+#pragma unroll
+        for (int u = 0; u < ILP; u++) {
+          const uint32_t x = base + 64 * u + lane;
+          lt[u] = x < T.A1 ? map[x - T.A0] : 0xFFu;
+        }
         if (FROM_KEYS) {
-          const uint64_t key = a.keys[x];
-          const bool w = a.acctype[x] == 1 /* WR */;
-          if (key == KEY_EMPTY) atomicOr(a.err, ERR_KEY);
-          en = table_find(a.tab, a.mask, key) | (w ? ENT_WRITE : 0u);
+          uint64_t key[ILP];
+          bool w[ILP];
+          uint32_t h[ILP];
+          SlotV sv[ILP];
+#pragma unroll
+          for (int u = 0; u < ILP; u++) {
+            const uint32_t x = base + 64 * u + lane;
+            key[u] = lt[u] != 0xFFu ? a.keys[x] : KEY_EMPTY;
+            w[u] = lt[u] != 0xFFu && a.acctype[x] == 1 /* WR */;
+          }
+#pragma unroll
+          for (int u = 0; u < ILP; u++) {
+            h[u] = slot_hash(key[u], a.mask);
+            if (lt[u] != 0xFFu) sv[u] = ld_slot(&a.tab[h[u]]);
+          }
+#pragma unroll
+          for (int u = 0; u < ILP; u++) {
+            en[u] = SID_NONE;
+            ow[u] = OWN_EMPTY;
+            if (lt[u] != 0xFFu) {
+              if (key[u] == KEY_EMPTY) atomicOr(a.err, ERR_KEY);
+              // linear probing; the first probe was issued above
+              for (uint32_t q = 0; q <= a.mask; q++) {
+                if (sv[u].key == key[u]) {
+                  en[u] = h[u];
+                  ow[u] = rb ? sv[u].own1 : sv[u].own0;
+                  break;
+                }
+                if (sv[u].key == KEY_EMPTY) break;
+                h[u] = (h[u] + 1) & a.mask;
+                sv[u] = ld_slot(&a.tab[h[u]]);
+              }
+              en[u] |= w[u] ? ENT_WRITE : 0u;
+            }
+          }
         } else {
-          en = a.cent[x];
+#pragma unroll
+          for (int u = 0; u < ILP; u++)
+            en[u] = lt[u] != 0xFFu ? cent_s[base + 64 * u + lane] : SID_NONE;
+#pragma unroll
+          for (int u = 0; u < ILP; u++) {
+            const uint32_t sid = en[u] & ENT_SID;
+            ow[u] = sid != SID_NONE ? a.tab[sid].own[rb] : OWN_EMPTY;
+          }
         }
-        const uint32_t sid = en & ENT_SID;
-        if (sid != SID_NONE) ps = own_status(a.tab[sid].own[rb], tag_r, i);
-        if (ps & PS_BLOCKED) en |= ENT_BLOCK;
+#pragma unroll
+        for (int u = 0; u < ILP; u++) {
+          const uint32_t x = base + 64 * u + lane;
+          uint32_t ps = 0;
+          if (lt[u] != 0xFFu && (en[u] & ENT_SID) != SID_NONE)
+            ps = own_status(ow[u], tag_r, s_txn[wv][lt[u]]);
+          if (ps & PS_BLOCKED) en[u] |= ENT_BLOCK;
+          if (x < T.A1) ent[x - T.A0] = en[u];
+          bool head;
+          const uint32_t v = segment_or2(lt[u], ps, head);
+          if (head && lt[u] != 0xFFu && v) atomicOr(&s_stat[wv][lt[u]], v);
+        }
       }
-      if (act) ent[x - T.A0] = en;
-      bool head;
-      const uint32_t v = segment_or2(lt, ps, head);
-      if (head && lt != 0xFFu && v) atomicOr(&s_stat[wv][lt], v);
     }
-  }
-  __syncthreads();
+    __syncthreads();
 
-  // ---- phase 2: per-txn decision (lane = txn)
-  uint32_t dec = 0;  // 0 none, 1 commit, 2 abort, 3 blocked
-  if (live && lane < T.nt && part) {
-    const uint32_t st = s_stat[wv][lane];
-    dec = (st & PS_KILLED) ? 2u : (st & PS_BLOCKED) ? 3u : 1u;
-    if (dec != 3u) a.state[txn] = (uint8_t)dec;
-  }
-  if (live) s_stat[wv][lane] = dec;
-  __syncthreads();
+    // ---- phase 2: per-txn decision (lane = txn)
+    uint32_t dec = 0;  // 0 none, 1 commit, 2 abort, 3 blocked
+    if (live && lane < T.nt && part) {
+      const uint32_t st = s_stat[wv][lane];
+      dec = (st & PS_KILLED) ? 2u : (st & PS_BLOCKED) ? 3u : 1u;
+      if (dec != 3u) a.state[txn] = (uint8_t)dec;
+    }
+    if (live) s_stat[wv][lane] = dec;
+    __syncthreads();
 
-  // ---- phase 3: count kept entries in access order; record each blocked
-  // txn's output start.  A kept entry: txn blocked, slot known, and the access
-  // is a write (feeds next-round owners) or was blocking.  A read that was
-  // clear stays clear forever (writers are only ever decided, never added).
-  uint32_t wave_e = 0;
-  if (live) {
-    for (uint32_t base = T.A0; base < T.A1; base += 64) {
-      const uint32_t x = base + lane;
-      const bool act = x < T.A1;
-      const uint32_t lt = act ? map[x - T.A0] : 0xFFu;
-      const uint32_t en = act ? ent[x - T.A0] : SID_NONE;
-      const bool keep = lt != 0xFFu && s_stat[wv][lt] == 3u && (en & ENT_SID) != SID_NONE &&
-                        (en & (ENT_WRITE | ENT_BLOCK));
-      const uint64_t km = ballot64(keep);
-      const uint32_t below = (uint32_t)__builtin_popcountll(km & ((1ull << lane) - 1ull));
-      // first access of a txn (txn start inside this tile)
-      const bool first = act && lt != 0xFFu && (x == T.A0 || map[x - 1 - T.A0] != lt);
-      if (first) s_opos[wv][lt] = wave_e + below;
-      wave_e += (uint32_t)__builtin_popcountll(km);
-    }
-  }
-  const uint64_t bm = ballot64(live && lane < T.nt && dec == 3u);
-  const uint32_t wave_t = (uint32_t)__builtin_popcountll(bm);
-  if (lane == 0) {
-    s_wt[wv] = wave_t;
-    s_we[wv] = wave_e;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned long long tt = 0, te = 0;
-    for (int w = 0; w < WAVES; w++) {
-      tt += s_wt[w];
-      te += s_we[w];
-    }
-    unsigned long long base = 0;
-    if (tt) base = atomicAdd(a.ctr, (tt << CTR_E_BITS) | te);
-    s_base = base;
-  }
-  __syncthreads();
-  uint64_t bt = s_base >> CTR_E_BITS, be = s_base & CTR_E_MASK;
-  for (uint32_t w = 0; w < wv; w++) {
-    bt += s_wt[w];
-    be += s_we[w];
-  }
-
-  // ---- phase 4: emit list entries + publish owner words
-  if (live) {
-    if (lane < T.nt && dec == 3u) {
-      const uint32_t p = (uint32_t)__builtin_popcountll(bm & ((1ull << lane) - 1ull));
-      a.tid_out[bt + p] = txn;
-      a.coff_out[bt + p] = (uint32_t)(be + s_opos[wv][lane]);
-    }
-    uint32_t run = 0;
-    for (uint32_t base = T.A0; base < T.A1; base += 64) {
-      const uint32_t x = base + lane;
-      const bool act = x < T.A1;
-      const uint32_t lt = act ? map[x - T.A0] : 0xFFu;
-      const uint32_t en = act ? ent[x - T.A0] : SID_NONE;
-      const uint32_t d = lt != 0xFFu ? s_stat[wv][lt] : 0u;
-      const uint32_t sid = en & ENT_SID;
-      const bool has = sid != SID_NONE;
-      const bool keep = d == 3u && has && (en & (ENT_WRITE | ENT_BLOCK));
-      const uint64_t km = ballot64(keep);
-      if (keep) {
+    // ---- phase 3: count kept entries in access order; record each blocked
+    // txn's output start.  A kept entry: txn blocked, slot known, and the
+    // access is a write (feeds next-round owners) or was blocking.  A read
+    // that was clear stays clear forever (writers are only ever decided).
+    uint32_t wave_e = 0;
+    if (live) {
+      for (uint32_t base = T.A0; base < T.A1; base += 64) {
+        const uint32_t x = base + lane;
+        const bool act = x < T.A1;
+        const uint32_t lt = act ? map[x - T.A0] : 0xFFu;
+        const uint32_t en = act ? ent[x - T.A0] : SID_NONE;
+        const bool keep = lt != 0xFFu && s_stat[wv][lt] == 3u && (en & ENT_SID) != SID_NONE &&
+                          (en & (ENT_WRITE | ENT_BLOCK));
+        const uint64_t km = ballot64(keep);
         const uint32_t below = (uint32_t)__builtin_popcountll(km & ((1ull << lane) - 1ull));
-        a.cent_out[be + run + below] = en & (ENT_WRITE | ENT_SID);
+        const bool first = act && lt != 0xFFu && (x == T.A0 || map[x - 1 - T.A0] != lt);
+        if (first) s_opos[wv][lt] = wave_e + below;
+        wave_e += (uint32_t)__builtin_popcountll(km);
       }
-      run += (uint32_t)__builtin_popcountll(km);
-      if (has && (en & ENT_WRITE)) {
-        const uint32_t i = s_txn[wv][lt];
-        if (d == 1u) {
-          // committed writer: tag-0 word in both buffers (never displaced)
-          atomicMin(&a.tab[sid].own[0], own_word(0, i));
-          atomicMin(&a.tab[sid].own[1], own_word(0, i));
-        } else if (d == 3u) {
-          own_min(&a.tab[sid].own[nb], tag_n | i);
+    }
+    const uint64_t bm = ballot64(live && lane < T.nt && dec == 3u);
+    const uint32_t wave_t = (uint32_t)__builtin_popcountll(bm);
+    if (lane == 0) {
+      s_wt[wv] = wave_t;
+      s_we[wv] = wave_e;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned long long tt = 0, te = 0;
+      for (int w = 0; w < WAVES; w++) {
+        tt += s_wt[w];
+        te += s_we[w];
+      }
+      unsigned long long base = 0;
+      if (tt) base = atomicAdd(&a.ctr[og], (tt << CTR_E_BITS) | te);
+      s_base = base;
+    }
+    __syncthreads();
+    uint64_t bt = s_base >> CTR_E_BITS, be = s_base & CTR_E_MASK;
+    for (uint32_t w = 0; w < wv; w++) {
+      bt += s_wt[w];
+      be += s_we[w];
+    }
+
+    // ---- phase 4: emit list entries + publish owner words
+    if (live) {
+      if (lane < T.nt && dec == 3u) {
+        const uint32_t p = (uint32_t)__builtin_popcountll(bm & ((1ull << lane) - 1ull));
+        tid_o[bt + p] = txn;
+        coff_o[bt + p] = (uint32_t)(be + s_opos[wv][lane]);
+      }
+      uint32_t run = 0;
+      for (uint32_t base = T.A0; base < T.A1; base += 64 * ILP) {
+        uint32_t sid[ILP], act_code[ILP], i_of[ILP], cur[ILP];
+#pragma unroll
+        for (int u = 0; u < ILP; u++) {
+          const uint32_t x = base + 64 * u + lane;
+          const bool act = x < T.A1;
+          const uint32_t lt = act ? map[x - T.A0] : 0xFFu;
+          const uint32_t en = act ? ent[x - T.A0] : SID_NONE;
+          const uint32_t d = lt != 0xFFu ? s_stat[wv][lt] : 0u;
+          sid[u] = en & ENT_SID;
+          const bool has = sid[u] != SID_NONE;
+          const bool keep = d == 3u && has && (en & (ENT_WRITE | ENT_BLOCK));
+          const uint64_t km = ballot64(keep);
+          if (keep) {
+            const uint32_t below = (uint32_t)__builtin_popcountll(km & ((1ull << lane) - 1ull));
+            cent_o[be + run + below] = en & (ENT_WRITE | ENT_SID);
+          }
+          run += (uint32_t)__builtin_popcountll(km);
+          // 1 = committed writer, 2 = blocked writer, 0 = nothing to publish
+          act_code[u] = (has && (en & ENT_WRITE)) ? (d == 1u ? 1u : d == 3u ? 2u : 0u) : 0u;
+          i_of[u] = act_code[u] ? s_txn[wv][lt] : 0u;
+        }
+        // read filters first, then the atomics (keeps the loads pipelined)
+#pragma unroll
+        for (int u = 0; u < ILP; u++)
+          cur[u] = act_code[u] == 2u ? a.tab[sid[u]].own[nb] : 0u;
+#pragma unroll
+        for (int u = 0; u < ILP; u++) {
+          if (act_code[u] == 1u) {
+            // committed writer: tag-0 word in both buffers (never displaced)
+            atomicMin(&a.tab[sid[u]].own[0], own_word(0, i_of[u]));
+            atomicMin(&a.tab[sid[u]].own[1], own_word(0, i_of[u]));
+          } else if (act_code[u] == 2u && (tag_n | i_of[u]) < cur[u]) {
+            atomicMin(&a.tab[sid[u]].own[nb], tag_n | i_of[u]);
+          }
         }
       }
     }
+    __syncthreads();  // LDS reuse by the next tile
   }
 }
 
@@ -355,47 +503,47 @@ __global__ __launch_bounds__(256) void k_retag(Slot* __restrict__ tab, uint64_t 
 
 // k_owner_list: publish round-`r` owners from a list (after a retag).
 __global__ __launch_bounds__(256) void k_owner_list(OwnerArgs a) {
-  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= a.m) return;
-  const uint32_t i = a.tid[j];
-  const uint32_t s = a.coff[j], e = (j + 1 < a.m) ? a.coff[j + 1] : a.end_total;
-  const uint32_t w = own_word(round_tag(a.r), i);
-  for (uint32_t x = s; x < e; x++) {
-    const uint32_t en = a.cent[x];
-    if (en & ENT_WRITE) own_min(&a.tab[en & ENT_SID].own[a.r & 1u], w);
+  const uint32_t w = own_word(round_tag(a.r), 0);
+  for (uint32_t sg = 0; sg < NSEG; sg++) {
+    const unsigned long long c = a.m_in[sg];
+    const uint64_t m = c >> CTR_E_BITS;
+    const uint32_t end_total = (uint32_t)(c & CTR_E_MASK);
+    const uint32_t* tid = a.tid + sg * a.seg_ts;
+    const uint32_t* coff = a.coff + sg * a.seg_ts;
+    const uint32_t* cent = a.cent + sg * a.seg_es;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m;
+         j += (uint64_t)gridDim.x * blockDim.x) {
+      const uint32_t i = tid[j];
+      const uint32_t s = coff[j], e = (j + 1 < m) ? coff[j + 1] : end_total;
+      for (uint32_t x = s; x < e; x++) {
+        const uint32_t en = cent[x];
+        if (en & ENT_WRITE) own_min(&a.tab[en & ENT_SID].own[a.r & 1u], w | i);
+      }
+    }
   }
 }
 
 // --------------------------------------------------------------------------
-// k_final: RC bytes + counts; commit flags for the tn scan.
+// k_final: RC bytes, commit flags for the tn scan, per-block count partials.
 __global__ __launch_bounds__(256) void k_final(FinalArgs a) {
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ uint32_t sh[4];
   uint32_t c = 0, ab = 0, ro = 0, und = 0, cw = 0;
-  if (t < a.n) {
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < a.n;
+       t += (uint64_t)gridDim.x * blockDim.x) {
     const uint8_t st = a.state[t];
     const bool w = a.hasw[t] != 0;
-    if (st == ST_COMMIT) c = 1;
-    else if (st == ST_ABORT) ab = 1;
-    else und = 1;
-    ro = w ? 0 : 1;
-    cw = (st == ST_COMMIT && w) ? 1 : 0;
+    c += st == ST_COMMIT;
+    ab += st == ST_ABORT;
+    und += st == ST_UNDECIDED;
+    ro += w ? 0u : 1u;
+    cw += (st == ST_COMMIT && w) ? 1u : 0u;
     a.rc[t] = st == ST_COMMIT ? 0 /* RCOK */ : 2 /* Abort */;
     if (a.cflag) a.cflag[t] = (st == ST_COMMIT && w) ? 1u : 0u;
   }
-  for (int d = 32; d > 0; d >>= 1) {
-    c += __shfl_xor(c, d);
-    ab += __shfl_xor(ab, d);
-    ro += __shfl_xor(ro, d);
-    und += __shfl_xor(und, d);
-    cw += __shfl_xor(cw, d);
-  }
-  if ((threadIdx.x & 63) == 0) {
-    if (c) atomicAdd((unsigned long long*)&a.counts[0], (unsigned long long)c);
-    if (ab) atomicAdd((unsigned long long*)&a.counts[1], (unsigned long long)ab);
-    if (ro) atomicAdd((unsigned long long*)&a.counts[2], (unsigned long long)ro);
-    if (cw) atomicAdd((unsigned long long*)&a.counts[3], (unsigned long long)cw);
-    if (und) atomicOr(a.err, ERR_UNDECIDED);
-  }
+  const uint32_t s0 = block_sum_u32(c, sh), s1 = block_sum_u32(ab, sh),
+                 s2 = block_sum_u32(ro, sh), s3 = block_sum_u32(cw, sh),
+                 s4 = block_sum_u32(und, sh);
+  if (threadIdx.x == 0) a.part[blockIdx.x] = FinalPart{s0, s1, s2, s3, s4, 0, 0, 0};
 }
 
 // --------------------------------------------------------------------------
@@ -449,30 +597,38 @@ __global__ __launch_bounds__(1024) void k_scan_apply(const uint32_t* __restrict_
 // host launchers (the templates stay private to this translation unit)
 static inline unsigned grid_for(uint64_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
 
-void launch_prep(const uint32_t* off, uint64_t n, uint64_t nnz, uint32_t* info, hipStream_t st) {
-  k_prep<<<grid_for(n, 256), 256, 0, st>>>(off, n, nnz, info);
+void launch_prep(const uint32_t* off, uint64_t n, const uint8_t* at, uint64_t nnz,
+                 PrepPart* part, hipStream_t st) {
+  k_prep<<<PREP_BLOCKS, 256, 0, st>>>(off, n, at, nnz, part);
 }
 void launch_hist(const HistArgs& a, hipStream_t st) {
   k_hist<<<grid_for(a.n, 256), 256, 0, st>>>(a);
 }
-void launch_build(const BuildArgs& a, hipStream_t st) {
-  const uint64_t waves = (a.n + a.tw - 1) / a.tw;
-  k_build<TILE_CAP, TILE_WAVES><<<grid_for(waves, TILE_WAVES), TILE_WAVES * 64, 0, st>>>(a);
+static unsigned tile_grid(uint64_t m, uint32_t tw, unsigned max_grid) {
+  const uint64_t waves = (m + tw - 1) / tw;
+  unsigned g = grid_for(waves, TILE_WAVES);
+  if (g > max_grid) g = max_grid;
+  return g ? g : 1;
 }
-void launch_round(const RoundArgs& a, bool from_keys, hipStream_t st) {
-  const uint64_t waves = (a.m + a.tw - 1) / a.tw;
-  const unsigned g = grid_for(waves, TILE_WAVES);
+void launch_build(const BuildArgs& a, unsigned max_grid, hipStream_t st) {
+  k_build<TILE_CAP, TILE_WAVES><<<tile_grid(a.n, a.tw, max_grid), TILE_WAVES * 64, 0, st>>>(a);
+}
+void launch_round(const RoundArgs& a, bool from_keys, uint64_t m_bound, unsigned max_grid,
+                  hipStream_t st) {
+  const unsigned g = tile_grid(m_bound, a.tw, max_grid);
   if (from_keys) k_round<true, TILE_CAP, TILE_WAVES><<<g, TILE_WAVES * 64, 0, st>>>(a);
   else k_round<false, TILE_CAP, TILE_WAVES><<<g, TILE_WAVES * 64, 0, st>>>(a);
 }
 void launch_retag(Slot* tab, uint64_t cap, hipStream_t st) {
   k_retag<<<grid_for(cap, 256), 256, 0, st>>>(tab, cap);
 }
-void launch_owner_list(const OwnerArgs& a, hipStream_t st) {
-  k_owner_list<<<grid_for(a.m, 256), 256, 0, st>>>(a);
+void launch_owner_list(const OwnerArgs& a, uint64_t m_bound, hipStream_t st) {
+  unsigned g = grid_for(m_bound, 256);
+  if (g > 4096) g = 4096;
+  k_owner_list<<<g ? g : 1, 256, 0, st>>>(a);
 }
 void launch_final(const FinalArgs& a, hipStream_t st) {
-  k_final<<<grid_for(a.n, 256), 256, 0, st>>>(a);
+  k_final<<<FINAL_BLOCKS, 256, 0, st>>>(a);
 }
 void launch_commit_tn(const uint32_t* cflag, uint64_t n, uint64_t* bsum, uint64_t tnc,
                       uint64_t* tn, hipStream_t st) {
@@ -480,30 +636,6 @@ void launch_commit_tn(const uint32_t* cflag, uint64_t n, uint64_t* bsum, uint64_
   k_scan_blocks<<<nb, 1024, 0, st>>>(cflag, n, bsum);
   k_scan_sums<<<1, 64, 0, st>>>(bsum, nb);
   k_scan_apply<<<nb, 1024, 0, st>>>(cflag, n, bsum, tnc, tn);
-}
-
-__global__ __launch_bounds__(256) void k_count_writes(const uint8_t* __restrict__ at, uint64_t nnz,
-                                                      unsigned long long* __restrict__ cnt) {
-  uint32_t c = 0;
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * 16;
-  for (uint64_t x = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16; x < nnz; x += stride) {
-    if (x + 16 <= nnz && ((uintptr_t)(at + x) & 15) == 0) {
-      const uint4 v = *reinterpret_cast<const uint4*>(at + x);
-      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-      for (int q = 0; q < 4; q++)
-        for (int b = 0; b < 4; b++) c += ((w[q] >> (8 * b)) & 0xFF) == 1u;
-    } else {
-      for (uint64_t y = x; y < nnz && y < x + 16; y++) c += at[y] == 1;
-    }
-  }
-  for (int d = 32; d > 0; d >>= 1) c += __shfl_xor(c, d);
-  if ((threadIdx.x & 63) == 0 && c) atomicAdd(cnt, (unsigned long long)c);
-}
-void launch_count_writes(const uint8_t* at, uint64_t nnz, unsigned long long* cnt, hipStream_t st) {
-  uint64_t g = (nnz / 16 + 255) / 256;
-  if (g > 2048) g = 2048;
-  if (g == 0) g = 1;
-  k_count_writes<<<(unsigned)g, 256, 0, st>>>(at, nnz, cnt);
 }
 
 }  // namespace dcc

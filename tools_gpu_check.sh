@@ -1,0 +1,18 @@
+#!/bin/bash
+# One GPU session: parity tests, smoke, bench, rocprofv3 kernel stats.
+# Every GPU step has its own time limit; steps are chained with && so the
+# first failure ends the session.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R"
+mkdir -p gpurun_out
+timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 \
+ && timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 \
+ && timeout -k 10 400 python bench.py --steps 20 --warmup 3 > gpurun_out/bench.log 2>&1 \
+ && (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats \
+      --output-format csv -d "$R/gpurun_out/prof" -o run -- python "$R/bench.py" --steps 5 \
+      --warmup 1 --no-cpu-baseline > "$R/gpurun_out/prof.log" 2>&1)
+rc=$?
+echo "session exit $rc"
+tail -3 gpurun_out/pytest_gpu.log; tail -2 gpurun_out/smoke.log; tail -1 gpurun_out/bench.log
+exit $rc
