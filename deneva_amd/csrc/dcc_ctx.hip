@@ -116,9 +116,9 @@ extern "C" int dcc_init(dcc_ctx** out, int device_id) {
   CK(hipEventCreate(&ctx->ev0));
   CK(hipEventCreate(&ctx->ev1));
   for (auto& e : ctx->pev) CK(hipEventCreate(&e));
-  CK(hipHostMalloc((void**)&ctx->hmisc, 4096, hipHostMallocDefault));
+  CK(hipHostMalloc((void**)&ctx->hmisc, 16384, hipHostMallocDefault));
   CK(hipHostMalloc((void**)&ctx->hpart, 1 << 16, hipHostMallocDefault));
-  int rc = ctx->misc.ensure(ctx, 4096, "misc");
+  int rc = ctx->misc.ensure(ctx, 16384, "misc");
   if (!rc) rc = ctx->part.ensure(ctx, 1 << 16, "partials");
   if (rc) {
     dcc_destroy(ctx);

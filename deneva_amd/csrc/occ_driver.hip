@@ -60,7 +60,7 @@ int dcc_ctx::reserve_occ(uint64_t n, uint64_t nnz, uint64_t nnz_w, uint32_t tw) 
   for (int i = 0; i < 2; i++) {
     CR(l_tid[i].ensure(this, NSEG * ts * 4, "list tid"));
     CR(l_coff[i].ensure(this, NSEG * ts * 4, "list off"));
-    CR(l_cent[i].ensure(this, NSEG * es * 4, "list entries"));
+    CR(l_cent[i].ensure(this, NSEG * es * 8, "list entries"));
   }
   CR(table.ensure(this, table_capacity(nnz_w) * sizeof(Slot), "table"));
   return DCC_OK;
@@ -123,10 +123,13 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   uint64_t seg_ts, seg_es;
   list_geometry(d.n, tw, seg_ts, seg_es);
   Slot* tab = (Slot*)table.p;
-  uint32_t* err = (uint32_t*)misc.p;                                    // [0]
-  unsigned long long* ring = (unsigned long long*)((char*)misc.p + 64);  // CTR_RING x NSEG
+  uint32_t* err = (uint32_t*)misc.p;                                     // [0]
+  uint32_t* one = (uint32_t*)misc.p + 1;                                 // constant 1
+  uint32_t* kflag = (uint32_t*)((char*)misc.p + 64);                     // CTR_RING flags
+  unsigned long long* ring = (unsigned long long*)((char*)misc.p + 512);  // CTR_RING x NSEG
 
-  CK(hipMemsetAsync(misc.p, 0, 64 + CTR_RING * NSEG * 8, stream));
+  CK(hipMemsetAsync(misc.p, 0, 512 + CTR_RING * NSEG * 8, stream));
+  CK(hipMemsetAsync(one, 0x01, 1, stream));
   CK(hipMemsetAsync(table.p, 0xFF, cap * sizeof(Slot), stream));
   CK(hipMemsetAsync(state.p, 0, d.n, stream));
 
@@ -149,10 +152,11 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
 
   // ---- fixed-point rounds.  Round k (0-based) reads its list size from the
   // NSEG counters ring[k-1] (device), reserves its output in ring[k] and
-  // zeroes ring[k+1]; the host enqueues rounds in batches and synchronises
-  // once per batch.
+  // zeroes ring[k+1]; k_pub republishes owner words before round k+1 only if
+  // round k aborted something.  The host enqueues rounds in batches and
+  // synchronises once per batch.
   int cur = 0;
-  uint32_t rt = 1;  // round tag
+  uint32_t rt = 1;  // round tag of the next round
   uint32_t k = 0;   // rounds enqueued
   uint64_t m_bound = d.n;
   uint32_t rounds = 0;
@@ -164,25 +168,42 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
     for (uint32_t q = 0; q < batch; q++, k++) {
       const bool first = k == 0;
       const unsigned long long* prev = first ? nullptr : &ring[((k - 1) % CTR_RING) * NSEG];
-      if (rt > MAX_ROUND_TAG) {
-        // tag space exhausted: drop stale owner words, republish from the list
-        launch_retag(tab, cap, stream);
-        OwnerArgs oa{prev, 1, (const uint32_t*)l_tid[cur].p, (const uint32_t*)l_coff[cur].p,
-                     (const uint32_t*)l_cent[cur].p, seg_ts, seg_es, tab};
-        launch_owner_list(oa, m_bound, stream);
-        rt = 1;
+      if (!first) {
+        PubArgs pa;
+        pa.m_in = prev;
+        pa.tw = tw;
+        pa.kill_flag = &kflag[(k - 1) % CTR_RING];
+        pa.force = 0;
+        pa.state = (const uint8_t*)state.p;
+        if (rt > MAX_ROUND_TAG) {
+          // tag space exhausted: drop stale owner words, every writer republishes
+          launch_retag(tab, cap, stream);
+          rt = 1;
+          pa.kill_flag = one;
+          pa.force = 1;
+        }
+        pa.r = rt;
+        pa.tid = (const uint32_t*)l_tid[cur].p;
+        pa.coff = (const uint32_t*)l_coff[cur].p;
+        pa.cent = (const uint64_t*)l_cent[cur].p;
+        pa.seg_ts = seg_ts;
+        pa.seg_es = seg_es;
+        pa.tab = tab;
+        pa.err = err;
+        launch_pub(pa, m_bound, (unsigned)n_cu * 2, stream);
       }
       RoundArgs ra;
       ra.m_in = prev;
       ra.m = d.n;
       ra.tw = tw;
       ra.r = rt;
+      ra.k = k + 1;  // 1-based: abort round 0 is the history pre-pass
       ra.end_total = (uint32_t)d.nnz;
       ra.tid = first ? nullptr : (const uint32_t*)l_tid[cur].p;
       ra.coff = first ? d.off : (const uint32_t*)l_coff[cur].p;
       ra.keys = d.keys;
       ra.acctype = d.acctype;
-      ra.cent = first ? nullptr : (const uint32_t*)l_cent[cur].p;
+      ra.cent = first ? nullptr : (const uint64_t*)l_cent[cur].p;
       ra.seg_ts = seg_ts;
       ra.seg_es = seg_es;
       ra.tab = tab;
@@ -190,9 +211,11 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
       ra.state = (uint8_t*)state.p;
       ra.tid_out = (uint32_t*)l_tid[cur ^ 1].p;
       ra.coff_out = (uint32_t*)l_coff[cur ^ 1].p;
-      ra.cent_out = (uint32_t*)l_cent[cur ^ 1].p;
+      ra.cent_out = (uint64_t*)l_cent[cur ^ 1].p;
       ra.ctr = &ring[(k % CTR_RING) * NSEG];
       ra.ctr_zero = &ring[((k + 1) % CTR_RING) * NSEG];
+      ra.kill_flag = &kflag[k % CTR_RING];
+      ra.kill_zero = &kflag[(k + 1) % CTR_RING];
       ra.err = err;
       launch_round(ra, first, m_bound, max_grid, stream);
       if (profiling && first) CK(hipEventRecord(pev[2], stream));

@@ -9,6 +9,8 @@ struct Slot;
 
 constexpr int TILE_CAP = 1024;  // accesses staged per wave (LDS)
 constexpr int TILE_WAVES = 4;   // waves per workgroup
+constexpr int PUB_LDS = 2048;   // LDS owner-combiner slots per workgroup
+constexpr int PUB_WAVES = 16;   // waves per workgroup of the build / publish kernels
 constexpr uint32_t MAX_TXN_LEN = 64;  // MAX_ROW_PER_TXN (config.h:155)
 constexpr uint32_t MAX_ROUND_TAG = 61;  // largest round tag a k_round may run with
 
@@ -66,12 +68,13 @@ struct RoundArgs {
   uint64_t m;             // txns in the input list (when m_in is null)
   uint32_t tw;            // txns per wave
   uint32_t r;             // round tag (1..MAX_ROUND_TAG)
+  uint32_t k;             // round index (0-based, never reset)
   uint32_t end_total;     // coff[m] (entries in the input list)
   const uint32_t* tid;    // list txn ids (nullptr: identity, round 1)
   const uint32_t* coff;   // list offsets
   const uint64_t* keys;   // round 1 input
   const uint8_t* acctype; // round 1 input
-  const uint32_t* cent;   // rounds >= 2 input: ENT_WRITE | sid
+  const uint64_t* cent;   // rounds >= 2 input entries (see dcc_device.h)
   uint64_t seg_ts;        // segment stride of tid/coff arrays
   uint64_t seg_es;        // segment stride of entry arrays
   Slot* tab;
@@ -79,20 +82,27 @@ struct RoundArgs {
   uint8_t* state;
   uint32_t* tid_out;
   uint32_t* coff_out;
-  uint32_t* cent_out;
+  uint64_t* cent_out;
   unsigned long long* ctr;       // this round's NSEG reservation counters
   unsigned long long* ctr_zero;  // next round's NSEG counters, zeroed here
+  uint32_t* kill_flag;           // set when this round aborted a txn
+  uint32_t* kill_zero;           // next round's flag, zeroed here
   uint32_t* err;
 };
 
-struct OwnerArgs {
+struct PubArgs {
   const unsigned long long* m_in;  // NSEG counters of the list
-  uint32_t r;
+  uint32_t r;                      // round whose owner words are published
+  uint32_t tw;
+  const uint32_t* kill_flag;       // previous round's abort flag (always-one word to force)
+  uint32_t force;                  // publish every write entry (after a retag)
+  const uint8_t* state;
   const uint32_t* tid;
   const uint32_t* coff;
-  const uint32_t* cent;
+  const uint64_t* cent;
   uint64_t seg_ts, seg_es;
   Slot* tab;
+  uint32_t* err;
 };
 
 struct FinalArgs {
@@ -112,7 +122,7 @@ void launch_build(const BuildArgs& a, unsigned max_grid, hipStream_t st);
 void launch_round(const RoundArgs& a, bool from_keys, uint64_t m_bound, unsigned max_grid,
                   hipStream_t st);
 void launch_retag(Slot* tab, uint64_t cap, hipStream_t st);
-void launch_owner_list(const OwnerArgs& a, uint64_t m_bound, hipStream_t st);
+void launch_pub(const PubArgs& a, uint64_t m_bound, unsigned max_grid, hipStream_t st);
 void launch_final(const FinalArgs& a, hipStream_t st);
 void launch_commit_tn(const uint32_t* cflag, uint64_t n, uint64_t* bsum, uint64_t tnc,
                       uint64_t* tn, hipStream_t st);

@@ -165,14 +165,14 @@ __device__ inline bool tile_open(uint64_t j0, uint32_t tw, uint64_t m, const uin
   return true;
 }
 
-// 16-byte slot read: key and both owner words in one load.
+// 16-byte slot read: key and owner word in one load.
 struct SlotV {
   uint64_t key;
-  uint32_t own0, own1;
+  uint32_t own;
 };
 __device__ inline SlotV ld_slot(const Slot* p) {
   const uint4 v = *reinterpret_cast<const uint4*>(p);
-  return SlotV{((uint64_t)v.y << 32) | v.x, v.z, v.w};
+  return SlotV{((uint64_t)v.y << 32) | v.x, v.z};
 }
 
 // List geometry of a round.  Round 1 reads the batch CSR (one segment,
@@ -216,7 +216,7 @@ __device__ inline uint32_t geo_seg(const ListGeo& G, uint64_t g) {
 constexpr int ILP = 4;  // 64-access steps in flight per wave
 
 // --------------------------------------------------------------------------
-// k_build: insert write keys, round-1 owners, per-txn has-write flag.
+// k_build: insert write keys, round-1 owners (min writer), has-write flag.
 template <int CAP, int WAVES>
 __global__ __launch_bounds__(WAVES * 64) void k_build(BuildArgs a) {
   __shared__ uint8_t s_map[WAVES][CAP];
@@ -256,7 +256,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_build(BuildArgs a) {
             } else {
               const uint32_t sid = table_insert(a.tab, a.mask, key[u]);
               if (sid == SID_NONE) atomicOr(a.err, ERR_FULL);
-              else own_min(&a.tab[sid].own[1], tag1 | s_txn[wv][lt[u]]);
+              else own_min(&a.tab[sid].own, tag1 | s_txn[wv][lt[u]]);
             }
           }
           bool head;
@@ -272,26 +272,35 @@ __global__ __launch_bounds__(WAVES * 64) void k_build(BuildArgs a) {
 
 // --------------------------------------------------------------------------
 // k_round: one fixed-point round over a CSR list of undecided txns.
+//
+// Per access (list entry):
+//   round 1       find the key's slot; owner word -> blocked/killed/clear
+//   entry with B  state[blocker]: COMMIT -> killed, UNDECIDED -> still blocked,
+//                 ABORT -> re-read the owner word (published for this round)
+//   write entry   clear (a clear access stays clear: writers are only ever
+//                 decided, never added) — kept only to publish owners
+// Per txn: killed -> Abort, clear -> Commit (+ tag-0 owner words), blocked ->
+// next list (entries that were blocked or are writes).
 template <bool FROM_KEYS, int CAP, int WAVES>
 __global__ __launch_bounds__(WAVES * 64) void k_round(RoundArgs a) {
   __shared__ uint8_t s_map[WAVES][CAP];
-  __shared__ uint32_t s_ent[WAVES][CAP];
+  __shared__ uint64_t s_ent[WAVES][CAP];
   __shared__ uint32_t s_txn[WAVES][64];
   __shared__ uint32_t s_stat[WAVES][64];
   __shared__ uint32_t s_opos[WAVES][64];
-  __shared__ uint32_t s_wt[WAVES], s_we[WAVES];
+  __shared__ uint32_t s_wt[WAVES], s_we[WAVES], s_wk[WAVES];
   __shared__ unsigned long long s_base;
+  __shared__ ListGeo G;  // in LDS: runtime-indexed register arrays go to scratch
 
   const uint32_t wv = threadIdx.x >> 6, lane = lane_id();
   uint8_t* map = s_map[wv];
-  uint32_t* ent = s_ent[wv];
-  const uint32_t rb = a.r & 1u, nb = (a.r + 1) & 1u;
+  uint64_t* ent = s_ent[wv];
   const uint32_t tag_r = round_tag(a.r);
-  const uint32_t tag_n = own_word(round_tag(a.r + 1), 0);
+  const uint8_t cur_abort = st_abort(a.k);
   const uint64_t per_wg = (uint64_t)WAVES * a.tw;
-  __shared__ ListGeo G;  // in LDS: runtime-indexed register arrays go to scratch
   if (threadIdx.x == 0) list_geo(a.m_in, a.m, a.end_total, per_wg, G);
   if (blockIdx.x == 0 && threadIdx.x < NSEG) a.ctr_zero[threadIdx.x] = 0ull;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *a.kill_zero = 0u;
   __syncthreads();
 
   for (uint64_t tile = blockIdx.x; tile < G.pre[G.nseg]; tile += gridDim.x) {
@@ -299,13 +308,13 @@ __global__ __launch_bounds__(WAVES * 64) void k_round(RoundArgs a) {
     const uint64_t m = G.m[sg];
     const uint32_t* tid_s = a.tid ? a.tid + sg * a.seg_ts : nullptr;
     const uint32_t* coff_s = a.m_in ? a.coff + sg * a.seg_ts : a.coff;
-    const uint32_t* cent_s = a.cent ? a.cent + sg * a.seg_es : nullptr;
+    const uint64_t* cent_s = a.cent ? a.cent + sg * a.seg_es : nullptr;
     const uint64_t j0 = (tile - G.pre[sg]) * per_wg + (uint64_t)wv * a.tw;
     // output segment of this workgroup-tile
     const uint32_t og = (uint32_t)(tile % NSEG);
     uint32_t* tid_o = a.tid_out + og * a.seg_ts;
     uint32_t* coff_o = a.coff_out + og * a.seg_ts;
-    uint32_t* cent_o = a.cent_out + og * a.seg_es;
+    uint64_t* cent_o = a.cent_out + og * a.seg_es;
     Tile T;
     uint32_t txn, s, e;
     bool part = true;
@@ -315,10 +324,10 @@ __global__ __launch_bounds__(WAVES * 64) void k_round(RoundArgs a) {
     s_stat[wv][lane] = 0;
     __syncthreads();
 
-    // ---- phase 1: probe every access of the tile (coalesced, ILP steps)
+    // ---- phase 1: resolve every access of the tile (coalesced, ILP steps)
     if (live) {
       for (uint32_t base = T.A0; base < T.A1; base += 64 * ILP) {
-        uint32_t lt[ILP], en[ILP], ow[ILP];
+        uint32_t lt[ILP], lo[ILP], blk[ILP], ps[ILP];
 #pragma unroll
         for (int u = 0; u < ILP; u++) {
           const uint32_t x = base + 64 * u + lane;
@@ -327,7 +336,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_round(RoundArgs a) {
         if (FROM_KEYS) {
           uint64_t key[ILP];
           bool w[ILP];
-          uint32_t h[ILP];
+          uint32_t h[ILP], stp[ILP];
           SlotV sv[ILP];
 #pragma unroll
           for (int u = 0; u < ILP; u++) {
@@ -337,49 +346,77 @@ __global__ __launch_bounds__(WAVES * 64) void k_round(RoundArgs a) {
           }
 #pragma unroll
           for (int u = 0; u < ILP; u++) {
-            h[u] = slot_hash(key[u], a.mask);
+            h[u] = slot_home(key[u], a.mask);
             if (lt[u] != 0xFFu) sv[u] = ld_slot(&a.tab[h[u]]);
           }
 #pragma unroll
           for (int u = 0; u < ILP; u++) {
-            en[u] = SID_NONE;
-            ow[u] = OWN_EMPTY;
+            lo[u] = SID_NONE;
+            blk[u] = 0;
+            ps[u] = 0;
             if (lt[u] != 0xFFu) {
               if (key[u] == KEY_EMPTY) atomicOr(a.err, ERR_KEY);
-              // linear probing; the first probe was issued above
+              stp[u] = slot_step(key[u], a.mask);
+              // double hashing; the home probe was issued above
               for (uint32_t q = 0; q <= a.mask; q++) {
                 if (sv[u].key == key[u]) {
-                  en[u] = h[u];
-                  ow[u] = rb ? sv[u].own1 : sv[u].own0;
+                  lo[u] = h[u];
+                  ps[u] = own_status(sv[u].own, tag_r, s_txn[wv][lt[u]]);
+                  blk[u] = own_idx(sv[u].own);
                   break;
                 }
                 if (sv[u].key == KEY_EMPTY) break;
-                h[u] = (h[u] + 1) & a.mask;
+                h[u] = (h[u] + stp[u]) & a.mask;
                 sv[u] = ld_slot(&a.tab[h[u]]);
               }
-              en[u] |= w[u] ? ENT_WRITE : 0u;
+              lo[u] |= w[u] ? ENT_WRITE : 0u;
             }
           }
         } else {
+          uint64_t en[ILP];
+          uint8_t bs[ILP];
 #pragma unroll
           for (int u = 0; u < ILP; u++)
-            en[u] = lt[u] != 0xFFu ? cent_s[base + 64 * u + lane] : SID_NONE;
+            en[u] = lt[u] != 0xFFu ? cent_s[base + 64 * u + lane] : (uint64_t)SID_NONE;
 #pragma unroll
           for (int u = 0; u < ILP; u++) {
-            const uint32_t sid = en[u] & ENT_SID;
-            ow[u] = sid != SID_NONE ? a.tab[sid].own[rb] : OWN_EMPTY;
+            lo[u] = (uint32_t)en[u];
+            blk[u] = (uint32_t)(en[u] >> 32);
+            bs[u] = (lo[u] & ENT_BLOCK) ? a.state[blk[u]] : ST_COMMIT;
+          }
+          uint32_t ow[ILP];
+          bool need[ILP];
+#pragma unroll
+          for (int u = 0; u < ILP; u++) {
+            // only an access whose blocker aborted in an EARLIER round needs
+            // the owner word (republished by k_pub since); an abort of this
+            // round keeps blocking until the next one
+            need[u] = (lo[u] & ENT_BLOCK) && bs[u] >= ST_ABORT && bs[u] != cur_abort;
+            ow[u] = need[u] ? a.tab[lo[u] & ENT_SID].own : OWN_EMPTY;
+          }
+#pragma unroll
+          for (int u = 0; u < ILP; u++) {
+            ps[u] = 0;
+            if (lo[u] & ENT_BLOCK) {
+              if (bs[u] == ST_COMMIT) {
+                ps[u] = PS_KILLED;
+              } else if (need[u]) {
+                ps[u] = own_status(ow[u], tag_r, s_txn[wv][lt[u]]);
+                blk[u] = own_idx(ow[u]);
+              } else {
+                ps[u] = PS_BLOCKED;  // undecided, or aborted this very round
+              }
+            }
+            lo[u] &= ~ENT_BLOCK;
           }
         }
 #pragma unroll
         for (int u = 0; u < ILP; u++) {
           const uint32_t x = base + 64 * u + lane;
-          uint32_t ps = 0;
-          if (lt[u] != 0xFFu && (en[u] & ENT_SID) != SID_NONE)
-            ps = own_status(ow[u], tag_r, s_txn[wv][lt[u]]);
-          if (ps & PS_BLOCKED) en[u] |= ENT_BLOCK;
-          if (x < T.A1) ent[x - T.A0] = en[u];
+          if (ps[u] & PS_BLOCKED) lo[u] |= ENT_BLOCK;
+          if (x < T.A1) ent[x - T.A0] = ((uint64_t)blk[u] << 32) | lo[u];
           bool head;
-          const uint32_t v = segment_or2(lt[u], ps, head);
+          const uint32_t v = segment_or2(lt[u], ps[u], head);
           if (head && lt[u] != 0xFFu && v) atomicOr(&s_stat[wv][lt[u]], v);
         }
       }
@@ -391,24 +428,23 @@ __global__ __launch_bounds__(WAVES * 64) void k_round(RoundArgs a) {
     if (live && lane < T.nt && part) {
       const uint32_t st = s_stat[wv][lane];
       dec = (st & PS_KILLED) ? 2u : (st & PS_BLOCKED) ? 3u : 1u;
-      if (dec != 3u) a.state[txn] = (uint8_t)dec;
+      if (dec != 3u) a.state[txn] = dec == 1u ? ST_COMMIT : cur_abort;
     }
     if (live) s_stat[wv][lane] = dec;
     __syncthreads();
 
     // ---- phase 3: count kept entries in access order; record each blocked
-    // txn's output start.  A kept entry: txn blocked, slot known, and the
-    // access is a write (feeds next-round owners) or was blocking.  A read
-    // that was clear stays clear forever (writers are only ever decided).
+    // txn's output start.  Kept: txn blocked, slot known, and the access is a
+    // write (feeds owner words) or is blocked.
     uint32_t wave_e = 0;
     if (live) {
       for (uint32_t base = T.A0; base < T.A1; base += 64) {
         const uint32_t x = base + lane;
         const bool act = x < T.A1;
         const uint32_t lt = act ? map[x - T.A0] : 0xFFu;
-        const uint32_t en = act ? ent[x - T.A0] : SID_NONE;
-        const bool keep = lt != 0xFFu && s_stat[wv][lt] == 3u && (en & ENT_SID) != SID_NONE &&
-                          (en & (ENT_WRITE | ENT_BLOCK));
+        const uint32_t lo = act ? (uint32_t)ent[x - T.A0] : SID_NONE;
+        const bool keep = lt != 0xFFu && s_stat[wv][lt] == 3u && (lo & ENT_SID) != SID_NONE &&
+                          (lo & (ENT_WRITE | ENT_BLOCK));
         const uint64_t km = ballot64(keep);
         const uint32_t below = (uint32_t)__builtin_popcountll(km & ((1ull << lane) - 1ull));
         const bool first = act && lt != 0xFFu && (x == T.A0 || map[x - 1 - T.A0] != lt);
@@ -418,19 +454,23 @@ __global__ __launch_bounds__(WAVES * 64) void k_round(RoundArgs a) {
     }
     const uint64_t bm = ballot64(live && lane < T.nt && dec == 3u);
     const uint32_t wave_t = (uint32_t)__builtin_popcountll(bm);
+    const uint32_t wave_k = (uint32_t)__builtin_popcountll(ballot64(live && lane < T.nt && dec == 2u));
     if (lane == 0) {
       s_wt[wv] = wave_t;
       s_we[wv] = wave_e;
+      s_wk[wv] = wave_k;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-      unsigned long long tt = 0, te = 0;
+      unsigned long long tt = 0, te = 0, tk = 0;
       for (int w = 0; w < WAVES; w++) {
         tt += s_wt[w];
         te += s_we[w];
+        tk += s_wk[w];
       }
       unsigned long long base = 0;
       if (tt) base = atomicAdd(&a.ctr[og], (tt << CTR_E_BITS) | te);
+      if (tk) *a.kill_flag = 1u;  // benign racing plain stores of the same value
       s_base = base;
     }
     __syncthreads();
@@ -440,7 +480,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_round(RoundArgs a) {
       be += s_we[w];
     }
 
-    // ---- phase 4: emit list entries + publish owner words
+    // ---- phase 4: emit list entries, publish committed writers
     if (live) {
       if (lane < T.nt && dec == 3u) {
         const uint32_t p = (uint32_t)__builtin_popcountll(bm & ((1ull << lane) - 1ull));
@@ -448,42 +488,24 @@ __global__ __launch_bounds__(WAVES * 64) void k_round(RoundArgs a) {
         coff_o[bt + p] = (uint32_t)(be + s_opos[wv][lane]);
       }
       uint32_t run = 0;
-      for (uint32_t base = T.A0; base < T.A1; base += 64 * ILP) {
-        uint32_t sid[ILP], act_code[ILP], i_of[ILP], cur[ILP];
-#pragma unroll
-        for (int u = 0; u < ILP; u++) {
-          const uint32_t x = base + 64 * u + lane;
-          const bool act = x < T.A1;
-          const uint32_t lt = act ? map[x - T.A0] : 0xFFu;
-          const uint32_t en = act ? ent[x - T.A0] : SID_NONE;
-          const uint32_t d = lt != 0xFFu ? s_stat[wv][lt] : 0u;
-          sid[u] = en & ENT_SID;
-          const bool has = sid[u] != SID_NONE;
-          const bool keep = d == 3u && has && (en & (ENT_WRITE | ENT_BLOCK));
-          const uint64_t km = ballot64(keep);
-          if (keep) {
-            const uint32_t below = (uint32_t)__builtin_popcountll(km & ((1ull << lane) - 1ull));
-            cent_o[be + run + below] = en & (ENT_WRITE | ENT_SID);
-          }
-          run += (uint32_t)__builtin_popcountll(km);
-          // 1 = committed writer, 2 = blocked writer, 0 = nothing to publish
-          act_code[u] = (has && (en & ENT_WRITE)) ? (d == 1u ? 1u : d == 3u ? 2u : 0u) : 0u;
-          i_of[u] = act_code[u] ? s_txn[wv][lt] : 0u;
+      for (uint32_t base = T.A0; base < T.A1; base += 64) {
+        const uint32_t x = base + lane;
+        const bool act = x < T.A1;
+        const uint32_t lt = act ? map[x - T.A0] : 0xFFu;
+        const uint64_t en = act ? ent[x - T.A0] : (uint64_t)SID_NONE;
+        const uint32_t lo = (uint32_t)en;
+        const uint32_t d = lt != 0xFFu ? s_stat[wv][lt] : 0u;
+        const uint32_t sid = lo & ENT_SID;
+        const bool has = sid != SID_NONE;
+        const bool keep = d == 3u && has && (lo & (ENT_WRITE | ENT_BLOCK));
+        const uint64_t km = ballot64(keep);
+        if (keep) {
+          const uint32_t below = (uint32_t)__builtin_popcountll(km & ((1ull << lane) - 1ull));
+          cent_o[be + run + below] = en;
         }
-        // read filters first, then the atomics (keeps the loads pipelined)
-#pragma unroll
-        for (int u = 0; u < ILP; u++)
-          cur[u] = act_code[u] == 2u ? a.tab[sid[u]].own[nb] : 0u;
-#pragma unroll
-        for (int u = 0; u < ILP; u++) {
-          if (act_code[u] == 1u) {
-            // committed writer: tag-0 word in both buffers (never displaced)
-            atomicMin(&a.tab[sid[u]].own[0], own_word(0, i_of[u]));
-            atomicMin(&a.tab[sid[u]].own[1], own_word(0, i_of[u]));
-          } else if (act_code[u] == 2u && (tag_n | i_of[u]) < cur[u]) {
-            atomicMin(&a.tab[sid[u]].own[nb], tag_n | i_of[u]);
-          }
-        }
+        run += (uint32_t)__builtin_popcountll(km);
+        // committed writer: tag-0 word (never displaced)
+        if (d == 1u && has && (lo & ENT_WRITE)) atomicMin(&a.tab[sid].own, own_word(0, s_txn[wv][lt]));
       }
     }
     __syncthreads();  // LDS reuse by the next tile
@@ -491,36 +513,78 @@ __global__ __launch_bounds__(WAVES * 64) void k_round(RoundArgs a) {
 }
 
 // --------------------------------------------------------------------------
-// k_retag: after MAX_TAG_ROUND rounds, drop every non-committed owner word.
+// k_pub: after a round that aborted something, the writers of keys whose
+// owner aborted publish the next round's owner words (tag r+1).  Those are
+// exactly the write entries whose recorded blocker aborted: every undecided
+// writer of a key carries the key's current owner as its blocker, so when the
+// owner aborts all of them become candidates and atomicMin elects the new
+// minimum.  A key whose owner is still undecided keeps its (older-tag) word,
+// which is never consulted — only accesses whose blocker aborted re-read
+// owner words.  A round without aborts publishes nothing.
+template <int CAP, int WAVES>
+__global__ __launch_bounds__(WAVES * 64) void k_pub(PubArgs a) {
+  __shared__ uint8_t s_map[WAVES][CAP];
+  __shared__ uint32_t s_txn[WAVES][64];
+  __shared__ ListGeo G;
+  __shared__ LdsMin<PUB_LDS> comb;
+  if (*a.kill_flag == 0u) return;  // uniform: no aborts last round
+  const uint32_t wv = threadIdx.x >> 6, lane = lane_id();
+  uint8_t* map = s_map[wv];
+  const uint64_t per_wg = (uint64_t)WAVES * a.tw;
+  const uint32_t tagw = own_word(round_tag(a.r), 0);
+  if (threadIdx.x == 0) list_geo(a.m_in, 0, 0, per_wg, G);
+  comb.init();
+  __syncthreads();
+  for (uint64_t tile = blockIdx.x; tile < G.pre[G.nseg]; tile += gridDim.x) {
+    const uint32_t sg = geo_seg(G, tile);
+    const uint64_t m = G.m[sg];
+    const uint64_t j0 = (tile - G.pre[sg]) * per_wg + (uint64_t)wv * a.tw;
+    const uint64_t* cent_s = a.cent + sg * a.seg_es;
+    Tile T;
+    uint32_t txn, s, e;
+    const bool live = tile_open<CAP>(j0, a.tw, m, a.tid + sg * a.seg_ts, a.coff + sg * a.seg_ts,
+                                     G.end[sg], true, map, s_txn[wv], T, txn, s, e, a.err);
+    __syncthreads();
+    if (live) {
+      for (uint32_t base = T.A0; base < T.A1; base += 64 * ILP) {
+        uint64_t en[ILP];
+        uint32_t lt[ILP];
+        uint8_t bs[ILP];
+#pragma unroll
+        for (int u = 0; u < ILP; u++) {
+          const uint32_t x = base + 64 * u + lane;
+          lt[u] = x < T.A1 ? map[x - T.A0] : 0xFFu;
+          en[u] = lt[u] != 0xFFu ? cent_s[x] : 0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < ILP; u++) {
+          const uint32_t lo = (uint32_t)en[u];
+          const bool wb = (lo & ENT_WRITE) && (lo & ENT_BLOCK) && !a.force;
+          bs[u] = wb ? a.state[(uint32_t)(en[u] >> 32)] : ST_UNDECIDED;
+        }
+#pragma unroll
+        for (int u = 0; u < ILP; u++) {
+          const uint32_t lo = (uint32_t)en[u];
+          const bool cand = (lo & ENT_WRITE) && (a.force || ((lo & ENT_BLOCK) && bs[u] >= ST_ABORT));
+          if (cand) {
+            const uint32_t sid = lo & ENT_SID, wd = tagw | s_txn[wv][lt[u]];
+            if (!comb.add(sid, wd)) own_min(&a.tab[sid].own, wd);
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  comb.flush(a.tab);
+}
+
+// --------------------------------------------------------------------------
+// k_retag: after MAX_ROUND_TAG rounds, drop every non-committed owner word.
 __global__ __launch_bounds__(256) void k_retag(Slot* __restrict__ tab, uint64_t cap) {
   const uint64_t sidx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (sidx >= cap) return;
-  for (int b = 0; b < 2; b++) {
-    const uint32_t w = tab[sidx].own[b];
-    if ((w >> IDX_BITS) != 0) tab[sidx].own[b] = OWN_EMPTY;
-  }
-}
-
-// k_owner_list: publish round-`r` owners from a list (after a retag).
-__global__ __launch_bounds__(256) void k_owner_list(OwnerArgs a) {
-  const uint32_t w = own_word(round_tag(a.r), 0);
-  for (uint32_t sg = 0; sg < NSEG; sg++) {
-    const unsigned long long c = a.m_in[sg];
-    const uint64_t m = c >> CTR_E_BITS;
-    const uint32_t end_total = (uint32_t)(c & CTR_E_MASK);
-    const uint32_t* tid = a.tid + sg * a.seg_ts;
-    const uint32_t* coff = a.coff + sg * a.seg_ts;
-    const uint32_t* cent = a.cent + sg * a.seg_es;
-    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m;
-         j += (uint64_t)gridDim.x * blockDim.x) {
-      const uint32_t i = tid[j];
-      const uint32_t s = coff[j], e = (j + 1 < m) ? coff[j + 1] : end_total;
-      for (uint32_t x = s; x < e; x++) {
-        const uint32_t en = cent[x];
-        if (en & ENT_WRITE) own_min(&a.tab[en & ENT_SID].own[a.r & 1u], w | i);
-      }
-    }
-  }
+  const uint32_t w = tab[sidx].own;
+  if ((w >> IDX_BITS) != 0) tab[sidx].own = OWN_EMPTY;
 }
 
 // --------------------------------------------------------------------------
@@ -533,7 +597,7 @@ __global__ __launch_bounds__(256) void k_final(FinalArgs a) {
     const uint8_t st = a.state[t];
     const bool w = a.hasw[t] != 0;
     c += st == ST_COMMIT;
-    ab += st == ST_ABORT;
+    ab += st >= ST_ABORT;
     und += st == ST_UNDECIDED;
     ro += w ? 0u : 1u;
     cw += (st == ST_COMMIT && w) ? 1u : 0u;
@@ -622,10 +686,12 @@ void launch_round(const RoundArgs& a, bool from_keys, uint64_t m_bound, unsigned
 void launch_retag(Slot* tab, uint64_t cap, hipStream_t st) {
   k_retag<<<grid_for(cap, 256), 256, 0, st>>>(tab, cap);
 }
-void launch_owner_list(const OwnerArgs& a, uint64_t m_bound, hipStream_t st) {
-  unsigned g = grid_for(m_bound, 256);
-  if (g > 4096) g = 4096;
-  k_owner_list<<<g ? g : 1, 256, 0, st>>>(a);
+void launch_pub(const PubArgs& a, uint64_t m_bound, unsigned max_grid, hipStream_t st) {
+  // tiles here are PUB_WAVES waves; the list geometry is recomputed in-kernel
+  const uint64_t waves = (m_bound + a.tw - 1) / a.tw + NSEG * TILE_WAVES;
+  unsigned g = grid_for(waves, PUB_WAVES);
+  if (g > max_grid) g = max_grid;
+  k_pub<TILE_CAP, PUB_WAVES><<<g ? g : 1, PUB_WAVES * 64, 0, st>>>(a);
 }
 void launch_final(const FinalArgs& a, hipStream_t st) {
   k_final<<<FINAL_BLOCKS, 256, 0, st>>>(a);
