@@ -29,6 +29,8 @@ GROUP_NONE = 0xFFFFFFFF
 DEVICE_PTRS = 0x1
 OCC_APPEND_HISTORY = 0x2
 UNIQUE_ID_BYTES = 128
+OPT_RECHECK = 1
+OPT_BATCH_MAX = 2
 
 
 class Batch(C.Structure):
@@ -119,6 +121,7 @@ _SIGS = [
     ("dcc_version", C.c_int, []),
     ("dcc_set_stream", C.c_int, [_P, _P]),
     ("dcc_set_profiling", C.c_int, [_P, C.c_int]),
+    ("dcc_set_option", C.c_int, [_P, C.c_int, C.c_int64]),
     ("dcc_reserve", C.c_int, [_P, C.c_uint64, C.c_uint64]),
     ("dcc_comm_unique_id", C.c_int, [_P]),
     ("dcc_comm_init", C.c_int, [_P, C.c_int, C.c_int, _P]),

@@ -40,6 +40,8 @@ struct dcc_ctx {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool profiling = false;
+  uint64_t recheck_max = 16384;   // fold the kill wave into rounds with lists <= this
+  uint32_t batch_max = 8;       // rounds enqueued between host synchronisations
   hipEvent_t pev[8] = {};  // phase boundary events (profiling only)
   std::string last_error;
   void* hmisc = nullptr;  // pinned host mirror of `misc`

@@ -150,6 +150,21 @@ extern "C" int dcc_set_profiling(dcc_ctx* ctx, int enable) {
   return DCC_OK;
 }
 
+extern "C" int dcc_set_option(dcc_ctx* ctx, int option, int64_t value) {
+  if (!ctx) return DCC_EINVAL;
+  switch (option) {
+    case DCC_OPT_RECHECK:
+      if (value < 0) return DCC_EINVAL;
+      ctx->recheck_max = (uint64_t)value;
+      return DCC_OK;
+    case DCC_OPT_BATCH_MAX:
+      if (value < 1 || value > 32) return DCC_EINVAL;
+      ctx->batch_max = (uint32_t)value;
+      return DCC_OK;
+    default: return DCC_EINVAL;
+  }
+}
+
 extern "C" int dcc_set_stream(dcc_ctx* ctx, void* s) {
   if (!ctx) return DCC_EINVAL;
   ctx->stream = s ? (hipStream_t)s : ctx->own_stream;
@@ -171,7 +186,7 @@ std::vector<DevBuf*> dcc_ctx::all_bufs() {
 extern "C" int dcc_reserve(dcc_ctx* ctx, uint64_t max_txn, uint64_t max_nnz) {
   if (!ctx) return DCC_EINVAL;
   (void)hipSetDevice(ctx->device);
-  const uint32_t tw = 16;  // worst case: MAX_ROW_PER_TXN-long txns
+  const uint32_t tw = ROUND_CAP / MAX_TXN_LEN;  // worst case: MAX_ROW_PER_TXN-long txns
   return ctx->reserve_occ(max_txn, max_nnz, max_nnz, tw);
 }
 

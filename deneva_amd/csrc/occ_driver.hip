@@ -47,7 +47,7 @@ void dcc_ctx::list_geometry(uint64_t n, uint32_t tw, uint64_t& seg_ts, uint64_t&
   const uint64_t tiles = (n + per_tile - 1) / per_tile;
   const uint64_t seg_tiles = (tiles + NSEG - 1) / NSEG + 1;
   seg_ts = seg_tiles * per_tile;
-  seg_es = seg_tiles * (uint64_t)TILE_WAVES * TILE_CAP;
+  seg_es = seg_tiles * (uint64_t)TILE_WAVES * ROUND_CAP;
 }
 
 int dcc_ctx::reserve_occ(uint64_t n, uint64_t nnz, uint64_t nnz_w, uint32_t tw) {
@@ -115,7 +115,9 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   uint32_t maxlen = 0;
   uint64_t nnz_w = 0;
   CR(device_prep(d, maxlen, nnz_w));
-  const uint32_t tw = std::min<uint32_t>(64, TILE_CAP / std::max<uint32_t>(1, maxlen));
+  // txns per wave: build tiles stage TILE_CAP accesses, round tiles ROUND_CAP
+  const uint32_t tw_b = std::min<uint32_t>(64, TILE_CAP / std::max<uint32_t>(1, maxlen));
+  const uint32_t tw = std::min<uint32_t>(64, ROUND_CAP / std::max<uint32_t>(1, maxlen));
   CR(reserve_occ(d.n, d.nnz, nnz_w, tw));
   const uint64_t cap = table_capacity(nnz_w);
   if (cap > (1ull << 30)) return fail(DCC_ERANGE, "table capacity exceeds 2^30 slots");
@@ -127,8 +129,9 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   uint32_t* one = (uint32_t*)misc.p + 1;                                 // constant 1
   uint32_t* kflag = (uint32_t*)((char*)misc.p + 64);                     // CTR_RING flags
   unsigned long long* ring = (unsigned long long*)((char*)misc.p + 512);  // CTR_RING x NSEG
+  char* bars = (char*)misc.p + 512 + CTR_RING * NSEG * 8;                 // CTR_RING x 16 B
 
-  CK(hipMemsetAsync(misc.p, 0, 512 + CTR_RING * NSEG * 8, stream));
+  CK(hipMemsetAsync(misc.p, 0, 512 + CTR_RING * NSEG * 8 + CTR_RING * 16, stream));
   CK(hipMemsetAsync(one, 0x01, 1, stream));
   CK(hipMemsetAsync(table.p, 0xFF, cap * sizeof(Slot), stream));
   CK(hipMemsetAsync(state.p, 0, d.n, stream));
@@ -143,7 +146,7 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   }
 
   // ---- key-hash build: round-1 owners
-  BuildArgs ba{d.n, tw, d.off, d.keys, d.acctype, tab, mask, (const uint8_t*)state.p,
+  BuildArgs ba{d.n, tw_b, d.off, d.keys, d.acctype, tab, mask, (const uint8_t*)state.p,
                (uint8_t*)hasw.p, err};
   if (profiling) CK(hipEventRecord(pev[0], stream));
   launch_build(ba, (unsigned)n_cu * 16, stream);
@@ -161,7 +164,13 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   uint64_t m_bound = d.n;
   uint32_t rounds = 0;
   const unsigned max_grid = (unsigned)n_cu * 8;
-  uint32_t batch = 2;
+  // recheck (kill wave folded into the round) pays off on short lists where
+  // per-round fixed costs dominate.  Such rounds keep every workgroup
+  // resident for the grid barrier:
+  // k_round fits 5 workgroups of 4 waves per CU (LDS ~21 KB, <= 96 VGPRs);
+  // launch 4 per CU.
+  const unsigned resident_grid = (unsigned)n_cu * 4;
+  uint32_t batch = std::min<uint32_t>(2, batch_max);
   bool done = false;
   while (!done) {
     const uint32_t k0 = k;
@@ -216,8 +225,12 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
       ra.ctr_zero = &ring[((k + 1) % CTR_RING) * NSEG];
       ra.kill_flag = &kflag[k % CTR_RING];
       ra.kill_zero = &kflag[(k + 1) % CTR_RING];
+      // m_bound bounds this round's list (lists only shrink)
+      const bool recheck = !first && m_bound <= recheck_max;
+      ra.bar = recheck ? (GridBar*)(bars + (k % CTR_RING) * 16) : nullptr;
+      ra.bar_zero = (uint32_t*)(bars + ((k + 1) % CTR_RING) * 16);
       ra.err = err;
-      launch_round(ra, first, m_bound, max_grid, stream);
+      launch_round(ra, first, m_bound, recheck ? resident_grid : max_grid, stream);
       if (profiling && first) CK(hipEventRecord(pev[2], stream));
       cur ^= 1;
       rt++;
@@ -237,7 +250,7 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
       m_bound = mq;
     }
     if (!done && k > d.n + 2) return fail(DCC_EIO, "fixed point did not converge");
-    batch = std::min<uint32_t>(batch * 2, 8);
+    batch = std::min<uint32_t>(batch * 2, batch_max);
   }
   if (profiling) CK(hipEventRecord(pev[4], stream));
 
@@ -269,6 +282,13 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   CR(read_partials(FINAL_BLOCKS * sizeof(FinalPart)));
   CK(hipStreamSynchronize(stream));
   const uint32_t e = *(const uint32_t*)hmisc;
+  {
+    // barrier timeout words (third word of each GridBar in the ring)
+    std::vector<uint32_t> bw(CTR_RING * 4);
+    CK(hipMemcpy(bw.data(), bars, CTR_RING * 16, hipMemcpyDeviceToHost));
+    for (uint32_t q = 0; q < CTR_RING; q++)
+      if (bw[q * 4 + 2]) return fail(DCC_EIO, "grid barrier timed out (grid not co-resident)");
+  }
   if (e & ERR_KEY) return fail(DCC_EINVAL, "batch: key equal to DCC_KEY_RESERVED");
   if (e & ERR_FULL) return fail(DCC_EIO, "hash table overflow");
   if (e & ERR_TILE) return fail(DCC_EIO, "tile capacity exceeded");

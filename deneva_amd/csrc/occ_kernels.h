@@ -7,7 +7,8 @@ namespace dcc {
 
 struct Slot;
 
-constexpr int TILE_CAP = 1024;  // accesses staged per wave (LDS)
+constexpr int TILE_CAP = 1024;  // accesses staged per wave (LDS), build kernel
+constexpr int ROUND_CAP = 512;  // accesses staged per wave, round / publish kernels
 constexpr int TILE_WAVES = 4;   // waves per workgroup
 constexpr int PUB_LDS = 2048;   // LDS owner-combiner slots per workgroup
 constexpr int PUB_WAVES = 16;   // waves per workgroup of the build / publish kernels
@@ -34,6 +35,12 @@ struct PrepPart {
 };
 struct FinalPart {
   uint32_t commit, abort, readonly, cwriters, undecided, pad0, pad1, pad2;
+};
+
+struct GridBar;
+constexpr uint32_t RECHECK_TILES = 32;  // tiles a workgroup can recheck per round
+struct TileOut {
+  uint32_t og, bt, nt, be, ne;
 };
 
 struct HistArgs {
@@ -87,6 +94,8 @@ struct RoundArgs {
   unsigned long long* ctr_zero;  // next round's NSEG counters, zeroed here
   uint32_t* kill_flag;           // set when this round aborted a txn
   uint32_t* kill_zero;           // next round's flag, zeroed here
+  GridBar* bar;                  // grid barrier words (recheck enabled) or null
+  uint32_t* bar_zero;            // next round's barrier words, zeroed here
   uint32_t* err;
 };
 

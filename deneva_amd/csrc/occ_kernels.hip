@@ -216,6 +216,46 @@ __device__ inline uint32_t geo_seg(const ListGeo& G, uint64_t g) {
 constexpr int ILP = 4;  // 64-access steps in flight per wave
 
 // --------------------------------------------------------------------------
+// Software grid barrier for a fully resident grid (host sizes the grid well
+// under the co-residency limit).  Release/acquire recipe of the CDNA guide
+// (§6 Guideline 16): every storing wave drains, one lane releases and
+// arrives on a device-scope counter, the last arriver flips the generation
+// word; waiters poll it relaxed with s_sleep and acquire once.  Spins are
+// bounded: on timeout the flag is raised and the host fails the call.
+struct GridBar {
+  unsigned count;
+  unsigned gen;
+  unsigned timeout;
+  unsigned pad;
+};
+
+__device__ inline void grid_barrier(GridBar* b) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned a = __hip_atomic_fetch_add(&b->count, 1u, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+    if (a == gridDim.x - 1) {
+      __hip_atomic_store(&b->gen, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      unsigned spins = 0;
+      while (__hip_atomic_load(&b->gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > (1u << 23)) {
+          __hip_atomic_store(&b->timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+
+// --------------------------------------------------------------------------
 // k_build: insert write keys, round-1 owners (min writer), has-write flag.
 template <int CAP, int WAVES>
 __global__ __launch_bounds__(WAVES * 64) void k_build(BuildArgs a) {
@@ -291,16 +331,20 @@ __global__ __launch_bounds__(WAVES * 64) void k_round(RoundArgs a) {
   __shared__ uint32_t s_wt[WAVES], s_we[WAVES], s_wk[WAVES];
   __shared__ unsigned long long s_base;
   __shared__ ListGeo G;  // in LDS: runtime-indexed register arrays go to scratch
+  __shared__ TileOut s_rec[RECHECK_TILES];
+  __shared__ uint32_t s_nrec;
 
   const uint32_t wv = threadIdx.x >> 6, lane = lane_id();
   uint8_t* map = s_map[wv];
   uint64_t* ent = s_ent[wv];
+  if (threadIdx.x == 0) s_nrec = 0;
   const uint32_t tag_r = round_tag(a.r);
   const uint8_t cur_abort = st_abort(a.k);
   const uint64_t per_wg = (uint64_t)WAVES * a.tw;
   if (threadIdx.x == 0) list_geo(a.m_in, a.m, a.end_total, per_wg, G);
   if (blockIdx.x == 0 && threadIdx.x < NSEG) a.ctr_zero[threadIdx.x] = 0ull;
   if (blockIdx.x == 0 && threadIdx.x == 0) *a.kill_zero = 0u;
+  if (blockIdx.x == 0 && threadIdx.x < 4 && a.bar_zero) a.bar_zero[threadIdx.x] = 0u;
   __syncthreads();
 
   for (uint64_t tile = blockIdx.x; tile < G.pre[G.nseg]; tile += gridDim.x) {
@@ -318,7 +362,8 @@ __global__ __launch_bounds__(WAVES * 64) void k_round(RoundArgs a) {
     Tile T;
     uint32_t txn, s, e;
     bool part = true;
-    if (FROM_KEYS && lane < a.tw && j0 + lane < m) part = a.state[j0 + lane] == ST_UNDECIDED;
+    if (lane < a.tw && j0 + lane < m)  // txns killed by the previous round's recheck are skipped
+      part = a.state[tid_s ? tid_s[j0 + lane] : (uint32_t)(j0 + lane)] == ST_UNDECIDED;
     const bool live = tile_open<CAP>(j0, a.tw, m, tid_s, coff_s, G.end[sg], part, map,
                                      s_txn[wv], T, txn, s, e, a.err);
     s_stat[wv][lane] = 0;
@@ -472,6 +517,9 @@ __global__ __launch_bounds__(WAVES * 64) void k_round(RoundArgs a) {
       if (tt) base = atomicAdd(&a.ctr[og], (tt << CTR_E_BITS) | te);
       if (tk) *a.kill_flag = 1u;  // benign racing plain stores of the same value
       s_base = base;
+      if (tt && s_nrec < RECHECK_TILES)
+        s_rec[s_nrec++] = TileOut{og, (uint32_t)(base >> CTR_E_BITS), (uint32_t)tt,
+                                  (uint32_t)(base & CTR_E_MASK), (uint32_t)te};
     }
     __syncthreads();
     uint64_t bt = s_base >> CTR_E_BITS, be = s_base & CTR_E_MASK;
@@ -510,6 +558,42 @@ __global__ __launch_bounds__(WAVES * 64) void k_round(RoundArgs a) {
     }
     __syncthreads();  // LDS reuse by the next tile
   }
+
+  // ---- recheck: after every workgroup's decisions are visible, abort the
+  // emitted txns whose recorded blocker committed in this round (the work of
+  // the next round's kill wave, done without re-reading the table).
+  // Entry-parallel and coalesced: the tile's output offsets go to LDS and a
+  // hit finds its txn by binary search.
+  if (a.bar) {
+    grid_barrier(a.bar);
+    uint32_t* s_off = reinterpret_cast<uint32_t*>(&s_map[0][0]);  // >= WAVES*64+1 words
+    const uint32_t nrec = s_nrec;
+    bool any = false;
+    for (uint32_t q = 0; q < nrec; q++) {
+      const TileOut r = s_rec[q];
+      const uint32_t* tid_o = a.tid_out + r.og * a.seg_ts;
+      const uint32_t* coff_o = a.coff_out + r.og * a.seg_ts;
+      const uint64_t* cent_o = a.cent_out + r.og * a.seg_es;
+      for (uint32_t p = threadIdx.x; p < r.nt; p += blockDim.x) s_off[p] = coff_o[r.bt + p];
+      if (threadIdx.x == 0) s_off[r.nt] = r.be + r.ne;
+      __syncthreads();
+      for (uint32_t x = r.be + threadIdx.x; x < r.be + r.ne; x += blockDim.x) {
+        const uint64_t en = cent_o[x];
+        if (((uint32_t)en & ENT_BLOCK) && a.state[(uint32_t)(en >> 32)] == ST_COMMIT) {
+          uint32_t lo = 0, hi = r.nt;  // last p with s_off[p] <= x
+          while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (s_off[mid] <= x) lo = mid;
+            else hi = mid;
+          }
+          a.state[tid_o[r.bt + lo]] = cur_abort;  // racing stores of the same byte
+          any = true;
+        }
+      }
+      __syncthreads();
+    }
+    if (any) *a.kill_flag = 1u;
+  }
 }
 
 // --------------------------------------------------------------------------
@@ -540,10 +624,13 @@ __global__ __launch_bounds__(WAVES * 64) void k_pub(PubArgs a) {
     const uint64_t m = G.m[sg];
     const uint64_t j0 = (tile - G.pre[sg]) * per_wg + (uint64_t)wv * a.tw;
     const uint64_t* cent_s = a.cent + sg * a.seg_es;
+    const uint32_t* tid_s = a.tid + sg * a.seg_ts;
     Tile T;
     uint32_t txn, s, e;
-    const bool live = tile_open<CAP>(j0, a.tw, m, a.tid + sg * a.seg_ts, a.coff + sg * a.seg_ts,
-                                     G.end[sg], true, map, s_txn[wv], T, txn, s, e, a.err);
+    bool part = true;  // a txn aborted by the recheck publishes nothing
+    if (lane < a.tw && j0 + lane < m) part = a.state[tid_s[j0 + lane]] == ST_UNDECIDED;
+    const bool live = tile_open<CAP>(j0, a.tw, m, tid_s, a.coff + sg * a.seg_ts, G.end[sg], part,
+                                     map, s_txn[wv], T, txn, s, e, a.err);
     __syncthreads();
     if (live) {
       for (uint32_t base = T.A0; base < T.A1; base += 64 * ILP) {
@@ -680,8 +767,8 @@ void launch_build(const BuildArgs& a, unsigned max_grid, hipStream_t st) {
 void launch_round(const RoundArgs& a, bool from_keys, uint64_t m_bound, unsigned max_grid,
                   hipStream_t st) {
   const unsigned g = tile_grid(m_bound, a.tw, max_grid);
-  if (from_keys) k_round<true, TILE_CAP, TILE_WAVES><<<g, TILE_WAVES * 64, 0, st>>>(a);
-  else k_round<false, TILE_CAP, TILE_WAVES><<<g, TILE_WAVES * 64, 0, st>>>(a);
+  if (from_keys) k_round<true, ROUND_CAP, TILE_WAVES><<<g, TILE_WAVES * 64, 0, st>>>(a);
+  else k_round<false, ROUND_CAP, TILE_WAVES><<<g, TILE_WAVES * 64, 0, st>>>(a);
 }
 void launch_retag(Slot* tab, uint64_t cap, hipStream_t st) {
   k_retag<<<grid_for(cap, 256), 256, 0, st>>>(tab, cap);
@@ -691,7 +778,7 @@ void launch_pub(const PubArgs& a, uint64_t m_bound, unsigned max_grid, hipStream
   const uint64_t waves = (m_bound + a.tw - 1) / a.tw + NSEG * TILE_WAVES;
   unsigned g = grid_for(waves, PUB_WAVES);
   if (g > max_grid) g = max_grid;
-  k_pub<TILE_CAP, PUB_WAVES><<<g ? g : 1, PUB_WAVES * 64, 0, st>>>(a);
+  k_pub<ROUND_CAP, PUB_WAVES><<<g ? g : 1, PUB_WAVES * 64, 0, st>>>(a);
 }
 void launch_final(const FinalArgs& a, hipStream_t st) {
   k_final<<<FINAL_BLOCKS, 256, 0, st>>>(a);

@@ -127,6 +127,9 @@ class Engine:
     def set_profiling(self, enable: bool) -> None:
         _check(lib.dcc_set_profiling(self._h, 1 if enable else 0), self._h)
 
+    def set_option(self, option: int, value: int) -> None:
+        _check(lib.dcc_set_option(self._h, option, value), self._h)
+
     def reserve(self, max_txn: int, max_nnz: int) -> None:
         _check(lib.dcc_reserve(self._h, max_txn, max_nnz), self._h)
 

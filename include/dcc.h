@@ -123,6 +123,10 @@ int dcc_version(void);                            /* 100*major + minor */
 int dcc_set_stream(dcc_ctx* ctx, void* hip_stream);
 /* Record per-phase HIP events inside every call (dcc_stats.phase_ms). */
 int dcc_set_profiling(dcc_ctx* ctx, int enable);
+/* Tuning knobs (defaults are the tuned values; for A/B measurement). */
+#define DCC_OPT_RECHECK 1     /* fold kill waves into rounds whose list has <= value txns */
+#define DCC_OPT_BATCH_MAX 2   /* max rounds enqueued between host synchronisations        */
+int dcc_set_option(dcc_ctx* ctx, int option, int64_t value);
 /* Pre-size device workspaces so a later call performs no allocation. */
 int dcc_reserve(dcc_ctx* ctx, uint64_t max_txn, uint64_t max_nnz);
 
