@@ -142,6 +142,7 @@ _SIGS = [
     ("dcc_tpcc_max_access", C.c_uint32, [C.POINTER(TpccParams)]),
     ("dcc_gen_tpcc", C.c_int, [C.POINTER(TpccParams), _P, _P, _P, _P, C.POINTER(C.c_uint64)]),
     ("dcc_alg_bytes", C.c_uint64, [C.c_uint64, C.c_uint64, C.c_uint64]),
+    ("dcc_calvin_alg_bytes", C.c_uint64, [C.c_uint64, C.c_uint64, C.c_int, C.c_int]),
 ]
 EXPORTED = [s[0] for s in _SIGS]
 

@@ -1,11 +1,733 @@
-// Calvin epoch lock ordering — placeholder until the grant-group kernels land.
+// Calvin epoch lock ordering on gfx950.
+//
+// Reference semantics (parity target): the sequencer fixes a global order of
+// the epoch (Sequencer::process_txn / send_next_batch, sequencer.cpp:184-326;
+// QWorkQueue::sched_dequeue, work_queue.cpp:105-151); one lock thread walks
+// the epoch in that order calling acquire_locks (calvin_thread.cpp:40-100,
+// ycsb_txn.cpp:49-88), which requests every row once (txn.cpp:778-782) in SH
+// for RD/SCAN, else EX (row.cpp:191) from Row_lock in CALVIN mode: FIFO, no
+// barging past waiters (row_lock.cpp:78-81, 152-170); lock_release promotes
+// the compatible head of the waiter queue (row_lock.cpp:317-357).
+//
+// Against an empty lock table that is a pure per-row function of the
+// requests in sequence order:
+//   grant group of a request = number of group boundaries before it on its
+//     row, where consecutive requests start a new group iff either is EX
+//     (an SH run shares one group, every EX is alone);
+//   acquire_locks returns RCOK iff every request of the txn is in group 0;
+//   wave(txn) = 1 + max over its requests of the max wave of the row's
+//     previous group (0 when all requests are in group 0): the txn's place in
+//     a schedule where every ready txn runs and then releases all its locks.
+//
+// Device pipeline (one stream, one host sync after the prep reduction):
+//   k_cv_prep      OR/AND of keys and of order -> which bits vary
+//   rank           stable radix sort of packed order -> seq (sched order)
+//   k_cv_layout    requests in sequence order: packed key, (txn, j, EX) value
+//   key sort       stable radix sort by packed key -> per-row FIFO runs
+//   k_cv_up/top/down  one segmented scan (monoid below) -> group, dedup,
+//                  readiness, and the group links the wave kernel needs
+//   k_cv_wave      (optional) wave levels, dependency-driven, one txn per
+//                  wave64 in sequence order
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
 
 #include "dcc.h"
 #include "dcc_ctx.h"
+#include "dcc_device.h"
+#include "occ_kernels.h"
+#include "radix_sort.h"
 
-int dcc_ctx::calvin_epoch(const dcc_batch*, uint32_t*, uint8_t*, uint32_t*, dcc_stats*) {
-  return fail(DCC_ENOTSUP, "Calvin engine not built yet");
+using namespace dcc;
+
+#define CK(expr)                                           \
+  do {                                                     \
+    hipError_t e_ = (expr);                                \
+    if (e_ != hipSuccess) return ctx->hip_fail(e_, #expr); \
+  } while (0)
+#define CR(expr)                 \
+  do {                           \
+    int r_ = (expr);             \
+    if (r_ != DCC_OK) return r_; \
+  } while (0)
+
+namespace {
+
+constexpr uint32_t CV_SH = 0, CV_EX = 1, CV_NONE = 2;
+constexpr uint32_t NOPOS = 0xFFFFFFFFu;
+constexpr uint32_t CV_MAX_TXN = 1u << 25;  // value = txn:25 | j:6 | EX:1
+constexpr unsigned CV_PREP_BLOCKS = 512;
+constexpr uint32_t CV_ITEMS = 16;                  // scan elements per thread
+constexpr uint32_t CV_TILE = 256 * CV_ITEMS;       // scan elements per workgroup
+constexpr uint32_t ERR_WAVE_TIMEOUT = 1u << 8;
+
+struct CvPart {
+  uint64_t kor, kand, oor, oand;
+  uint32_t nex, pad[3];
+};
+
+// ---------------------------------------------------------------- prep
+__global__ __launch_bounds__(256) void k_cv_prep(const uint64_t* __restrict__ keys, uint64_t nnz,
+                                                 const uint8_t* __restrict__ at,
+                                                 const uint64_t* __restrict__ order, uint64_t n,
+                                                 CvPart* __restrict__ part) {
+  __shared__ uint64_t s[4][4];
+  __shared__ uint32_t s_ex[4];
+  uint64_t kor = 0, kand = ~0ull, oor = 0, oand = ~0ull;
+  uint32_t nex = 0;
+  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t x = tid; x < nnz; x += stride) {
+    const uint64_t k = keys[x];
+    kor |= k;
+    kand &= k;
+    const uint8_t a = at[x];
+    nex += (a != DCC_RD && a != DCC_SCAN) ? 1u : 0u;
+  }
+  if (order)
+    for (uint64_t t = tid; t < n; t += stride) {
+      const uint64_t o = order[t];
+      oor |= o;
+      oand &= o;
+    }
+  for (int d = 32; d > 0; d >>= 1) {
+    kor |= __shfl_xor(kor, d);
+    kand &= __shfl_xor(kand, d);
+    oor |= __shfl_xor(oor, d);
+    oand &= __shfl_xor(oand, d);
+    nex += __shfl_xor(nex, d);
+  }
+  const uint32_t wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    s[wv][0] = kor;
+    s[wv][1] = kand;
+    s[wv][2] = oor;
+    s[wv][3] = oand;
+    s_ex[wv] = nex;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    CvPart p{0, ~0ull, 0, ~0ull, 0, {0, 0, 0}};
+    for (int w = 0; w < 4; w++) {
+      p.kor |= s[w][0];
+      p.kand &= s[w][1];
+      p.oor |= s[w][2];
+      p.oand &= s[w][3];
+      p.nex += s_ex[w];
+    }
+    part[blockIdx.x] = p;
+  }
+}
+
+// ---------------------------------------------------------------- rank
+template <typename K>
+__global__ __launch_bounds__(256) void k_cv_order_init(const uint64_t* __restrict__ order,
+                                                       uint64_t n, KeyPack kp, K* __restrict__ ok,
+                                                       uint32_t* __restrict__ ov) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  ok[t] = (K)keypack_apply(kp, order[t]);
+  ov[t] = (uint32_t)t;
+}
+
+// lengths in sequence order, then per-tile sums (u32 exclusive scan, pass 1)
+__global__ __launch_bounds__(256) void k_cv_len_tiles(const uint32_t* __restrict__ off,
+                                                      const uint32_t* __restrict__ seq, uint64_t n,
+                                                      uint32_t* __restrict__ len,
+                                                      uint32_t* __restrict__ tsum) {
+  __shared__ uint32_t sh[4];
+  const uint64_t base = (uint64_t)blockIdx.x * CV_TILE;
+  uint32_t s = 0;
+  for (uint32_t it = 0; it < CV_ITEMS; it++) {
+    const uint64_t q = base + it * 256 + threadIdx.x;
+    if (q < n) {
+      const uint32_t t = seq[q];
+      const uint32_t l = off[t + 1] - off[t];
+      len[q] = l;
+      s += l;
+    }
+  }
+  for (int d = 32; d > 0; d >>= 1) s += __shfl_xor(s, d);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) tsum[blockIdx.x] = sh[0] + sh[1] + sh[2] + sh[3];
+}
+
+// exclusive scan of len (tile prefix from the scanned tsum) -> off2 [n+1]
+__global__ __launch_bounds__(256) void k_cv_len_apply(const uint32_t* __restrict__ len, uint64_t n,
+                                                      const uint32_t* __restrict__ tpre,
+                                                      uint32_t nnz, uint32_t* __restrict__ off2) {
+  __shared__ uint32_t sh[4];
+  const uint64_t base = (uint64_t)blockIdx.x * CV_TILE + (uint64_t)threadIdx.x * CV_ITEMS;
+  uint32_t v[CV_ITEMS], s = 0;
+  for (uint32_t i = 0; i < CV_ITEMS; i++) {
+    v[i] = base + i < n ? len[base + i] : 0u;
+    s += v[i];
+  }
+  const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+  uint32_t x = s;
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d);
+    if (lane >= (uint32_t)d) x += y;
+  }
+  if (lane == 63) sh[wv] = x;
+  __syncthreads();
+  uint32_t run = tpre[blockIdx.x] + x - s;
+  for (uint32_t w = 0; w < wv; w++) run += sh[w];
+  for (uint32_t i = 0; i < CV_ITEMS; i++) {
+    if (base + i < n) off2[base + i] = run;
+    run += v[i];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) off2[n] = nnz;
+}
+
+// ---------------------------------------------------------------- layout
+// One thread per sequence position q: txn t = seq[q] writes its requests to
+// [off2[q], off2[q+1]) as (packed key, t:25 | j:6 | EX:1).
+template <typename K>
+__global__ __launch_bounds__(256) void k_cv_layout(const uint32_t* __restrict__ off,
+                                                   const uint32_t* __restrict__ seq,
+                                                   const uint32_t* __restrict__ off2, uint64_t n,
+                                                   const uint64_t* __restrict__ keys,
+                                                   const uint8_t* __restrict__ at, KeyPack kp,
+                                                   K* __restrict__ ak, uint32_t* __restrict__ av) {
+  const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= n) return;
+  const uint32_t t = seq ? seq[q] : (uint32_t)q;
+  const uint32_t s = off[t], e = off[t + 1];
+  const uint32_t d = off2 ? off2[q] : s;
+  for (uint32_t j = 0; j < e - s; j++) {
+    const uint8_t a = at[s + j];
+    ak[d + j] = (K)keypack_apply(kp, keys[s + j]);
+    av[d + j] = (t << 7) | (j << 1) | ((a != DCC_RD && a != DCC_SCAN) ? 1u : 0u);
+  }
+}
+
+// ---------------------------------------------------------------- group scan
+// Segmented scan over the key-sorted requests.  State of an interval "since
+// the last row start" (flag = the interval holds a row start):
+//   ft/fpos  first non-dup lock type and its position, lt last one
+//   cnt      group boundaries between consecutive non-dup requests
+//   ns       group starts inside the interval; gs / pgs the last two
+//   gnd      non-dup requests since the last group start (all if ns == 0)
+//   nd       non-dup requests
+// A de-duplicated request (same row, same txn as its predecessor — a txn's
+// requests on one row are adjacent after the stable sort) is neutral.
+struct Gs {
+  uint32_t flag, ft, lt, fpos, cnt, ns, gs, pgs, gnd, nd;
+};
+
+__device__ inline Gs gs_identity() { return Gs{0, CV_NONE, CV_NONE, 0, 0, 0, NOPOS, NOPOS, 0, 0}; }
+
+__device__ inline Gs gs_combine(const Gs& A, const Gs& B) {
+  if (B.flag) return B;
+  Gs R;
+  R.flag = A.flag;
+  const bool bnd = A.lt != CV_NONE && B.ft != CV_NONE && (A.lt == CV_EX || B.ft == CV_EX);
+  const bool af = A.ft != CV_NONE;
+  R.ft = af ? A.ft : B.ft;
+  R.fpos = af ? A.fpos : B.fpos;
+  R.lt = B.lt != CV_NONE ? B.lt : A.lt;
+  R.cnt = A.cnt + B.cnt + (bnd ? 1u : 0u);
+  R.ns = A.ns + B.ns + (bnd ? 1u : 0u);
+  if (B.ns >= 1) {
+    R.gs = B.gs;
+    R.gnd = B.gnd;
+    R.pgs = B.ns >= 2 ? B.pgs : (bnd ? B.fpos : A.gs);
+  } else if (bnd) {
+    R.gs = B.fpos;
+    R.gnd = B.nd;
+    R.pgs = A.gs;
+  } else {
+    R.gs = A.gs;
+    R.gnd = A.gnd + B.nd;
+    R.pgs = A.pgs;
+  }
+  R.nd = A.nd + B.nd;
+  return R;
+}
+
+template <typename K>
+__device__ inline Gs gs_element(uint64_t p, K key, uint32_t val, K pkey, uint32_t pval) {
+  const bool start = p == 0 || key != pkey;
+  const uint32_t typ = (val & 1u) ? CV_EX : CV_SH;
+  if (start) return Gs{1, typ, typ, (uint32_t)p, 0, 1, (uint32_t)p, NOPOS, 1, 1};
+  if ((val >> 7) == (pval >> 7)) return gs_identity();  // duplicate row of the same txn
+  return Gs{0, typ, typ, (uint32_t)p, 0, 0, NOPOS, NOPOS, 1, 1};
+}
+
+struct ScanOut {
+  const uint32_t* off;
+  uint32_t* group;  // [nnz] or null
+  uint8_t* rc;      // [n]
+  uint32_t* pgx;    // [nnz] previous group start per request (waves) or null
+  uint32_t* gsx;    // [nnz] own group start per request (waves) or null
+  uint32_t* gsize;  // [nnz] group size by start position (waves) or null
+};
+
+// Ordered tree reduction of 256 per-thread states (LDS).
+__device__ inline Gs block_reduce_gs(Gs v, Gs* s) {
+  s[threadIdx.x] = v;
+  __syncthreads();
+  for (uint32_t w = 1; w < 256; w <<= 1) {
+    if ((threadIdx.x & (2 * w - 1)) == 0) s[threadIdx.x] = gs_combine(s[threadIdx.x], s[threadIdx.x + w]);
+    __syncthreads();
+  }
+  return s[0];
+}
+
+// Exclusive scan of 256 per-thread states (Hillis-Steele in LDS).
+__device__ inline Gs block_excl_gs(Gs v, Gs* s) {
+  s[threadIdx.x] = v;
+  __syncthreads();
+  for (uint32_t d = 1; d < 256; d <<= 1) {
+    Gs r = s[threadIdx.x];
+    if (threadIdx.x >= d) r = gs_combine(s[threadIdx.x - d], r);
+    __syncthreads();
+    s[threadIdx.x] = r;
+    __syncthreads();
+  }
+  const Gs ex = threadIdx.x ? s[threadIdx.x - 1] : gs_identity();
+  __syncthreads();
+  return ex;
+}
+
+template <typename K>
+__device__ inline void load_run(const K* sk, const uint32_t* sv, uint64_t m, uint64_t p0, K* k,
+                                uint32_t* v, K& pk, uint32_t& pv) {
+#pragma unroll
+  for (uint32_t i = 0; i < CV_ITEMS; i++) {
+    k[i] = p0 + i < m ? sk[p0 + i] : (K)0;
+    v[i] = p0 + i < m ? sv[p0 + i] : 0u;
+  }
+  pk = p0 ? sk[p0 - 1] : (K)0;
+  pv = p0 ? sv[p0 - 1] : 0u;
+}
+
+template <typename K>
+__global__ __launch_bounds__(256) void k_cv_up(const K* __restrict__ sk,
+                                               const uint32_t* __restrict__ sv, uint64_t m,
+                                               Gs* __restrict__ agg) {
+  __shared__ Gs s[256];
+  const uint64_t p0 = (uint64_t)blockIdx.x * CV_TILE + (uint64_t)threadIdx.x * CV_ITEMS;
+  K k[CV_ITEMS];
+  uint32_t v[CV_ITEMS];
+  K pk;
+  uint32_t pv;
+  Gs acc = gs_identity();
+  if (p0 < m) {
+    load_run(sk, sv, m, p0, k, v, pk, pv);
+#pragma unroll
+    for (uint32_t i = 0; i < CV_ITEMS; i++) {
+      if (p0 + i < m) acc = gs_combine(acc, gs_element(p0 + i, k[i], v[i], pk, pv));
+      pk = k[i];
+      pv = v[i];
+    }
+  }
+  const Gs r = block_reduce_gs(acc, s);
+  if (threadIdx.x == 0) agg[blockIdx.x] = r;
+}
+
+// one workgroup: exclusive scan of the tile aggregates in place
+__global__ __launch_bounds__(256) void k_cv_top(Gs* __restrict__ agg, uint32_t tiles) {
+  __shared__ Gs s[256];
+  __shared__ Gs s_last;
+  Gs carry = gs_identity();
+  for (uint32_t c0 = 0; c0 < tiles; c0 += 256) {
+    const uint32_t i = c0 + threadIdx.x;
+    const Gs v = i < tiles ? agg[i] : gs_identity();
+    const Gs ex = block_excl_gs(v, s);
+    if (i < tiles) agg[i] = gs_combine(carry, ex);
+    // total of this chunk = ex(last) (+) v(last)
+    if (threadIdx.x == 255) s_last = gs_combine(ex, v);
+    __syncthreads();
+    carry = gs_combine(carry, s_last);
+    __syncthreads();
+  }
+}
+
+template <typename K>
+__global__ __launch_bounds__(256) void k_cv_down(const K* __restrict__ sk,
+                                                 const uint32_t* __restrict__ sv, uint64_t m,
+                                                 const Gs* __restrict__ pre, ScanOut o) {
+  __shared__ Gs s[256];
+  const uint64_t p0 = (uint64_t)blockIdx.x * CV_TILE + (uint64_t)threadIdx.x * CV_ITEMS;
+  K k[CV_ITEMS];
+  uint32_t v[CV_ITEMS];
+  K pk0 = 0;
+  uint32_t pv0 = 0;
+  Gs acc = gs_identity();
+  if (p0 < m) {
+    load_run(sk, sv, m, p0, k, v, pk0, pv0);
+    K pk = pk0;
+    uint32_t pv = pv0;
+#pragma unroll
+    for (uint32_t i = 0; i < CV_ITEMS; i++) {
+      if (p0 + i < m) acc = gs_combine(acc, gs_element(p0 + i, k[i], v[i], pk, pv));
+      pk = k[i];
+      pv = v[i];
+    }
+  }
+  Gs run = gs_combine(pre[blockIdx.x], block_excl_gs(acc, s));
+  if (p0 >= m) return;
+  K pk = pk0;
+  uint32_t pv = pv0;
+  uint32_t last_gs = NOPOS, last_gnd = 0;
+  for (uint32_t i = 0; i < CV_ITEMS && p0 + i < m; i++) {
+    const uint64_t p = p0 + i;
+    const Gs e = gs_element(p, k[i], v[i], pk, pv);
+    const bool dup = !e.flag && e.ft == CV_NONE;
+    run = gs_combine(run, e);
+    pk = k[i];
+    pv = v[i];
+    const uint32_t t = v[i] >> 7, j = (v[i] >> 1) & 63u;
+    const uint32_t x = o.off[t] + j;
+    if (dup) {
+      if (o.group) o.group[x] = DCC_GROUP_NONE;
+      if (o.pgx) {
+        o.pgx[x] = NOPOS;
+        o.gsx[x] = NOPOS;
+      }
+      continue;
+    }
+    if (o.group) o.group[x] = run.cnt;
+    if (run.cnt) o.rc[t] = DCC_RC_WAIT;  // racing stores of the same byte
+    if (o.pgx) {
+      o.pgx[x] = run.cnt ? run.pgs : NOPOS;
+      o.gsx[x] = run.gs;
+      if (last_gs != NOPOS && last_gs != run.gs) atomicMax(&o.gsize[last_gs], last_gnd);
+      last_gs = run.gs;
+      last_gnd = run.gnd;
+    }
+  }
+  if (o.gsize && last_gs != NOPOS) atomicMax(&o.gsize[last_gs], last_gnd);
+}
+
+// ---------------------------------------------------------------- waves
+// Dependency-driven wave levels.  Wave w of the persistent grid takes the
+// sequence positions w, w+W, ... in order; lanes are the txn's requests.  A
+// request in group g > 0 waits until every member of the row's previous
+// group has published (done == size), then the txn's level is 1 + the max
+// published level over those groups; it publishes max(level) into its own
+// groups and counts itself done.  Every dependency is an earlier sequence
+// position, every wave owns at most one unfinished position and the grid is
+// co-resident, so the earliest unfinished position always progresses.  Spins
+// are bounded by a wall-clock budget; on expiry the error word is raised.
+struct WaveArgs {
+  uint64_t n;
+  const uint32_t* seq;  // or null (index order)
+  const uint32_t* off;
+  const uint32_t* pgx;
+  const uint32_t* gsx;
+  const uint32_t* gsize;
+  uint32_t* done;
+  uint32_t* maxl;
+  uint32_t* wave;
+  uint32_t* err;
+  uint64_t budget;  // s_memrealtime ticks (100 MHz)
+};
+
+__global__ __launch_bounds__(256) void k_cv_wave(WaveArgs a) {
+  const uint32_t lane = lane_id();
+  const uint64_t W = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  const uint64_t w = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  bool expired = false;
+  for (uint64_t q = w; q < a.n; q += W) {
+    const uint32_t t = a.seq ? a.seq[q] : (uint32_t)q;
+    const uint32_t s = a.off[t], len = a.off[t + 1] - s;
+    const bool act = lane < len;
+    const uint32_t pg = act ? a.pgx[s + lane] : NOPOS;
+    const uint32_t g = act ? a.gsx[s + lane] : NOPOS;
+    const uint32_t need = pg != NOPOS ? a.gsize[pg] : 0u;
+    uint32_t lvl = 0;
+    if (ballot64(pg != NOPOS)) {
+      bool ok = pg == NOPOS;
+      while (!expired) {
+        if (!ok) ok = __hip_atomic_load(&a.done[pg], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need;
+        if (ballot64(!ok) == 0) break;
+        __builtin_amdgcn_s_sleep(1);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > a.budget) expired = true;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      if (pg != NOPOS)
+        lvl = __hip_atomic_load(&a.maxl[pg], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+      for (int d = 32; d > 0; d >>= 1) lvl = max(lvl, (uint32_t)__shfl_xor(lvl, d));
+    }
+    if (g != NOPOS) __hip_atomic_fetch_max(&a.maxl[g], lvl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    if (g != NOPOS) __hip_atomic_fetch_add(&a.done[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) a.wave[t] = lvl;
+  }
+  if (expired && lane == 0) atomicOr(a.err, ERR_WAVE_TIMEOUT);
+}
+
+// ---------------------------------------------------------------- counts
+struct CvCount {
+  uint32_t ready, maxwave, pad0, pad1;
+};
+__global__ __launch_bounds__(256) void k_cv_count(const uint8_t* __restrict__ rc,
+                                                  const uint32_t* __restrict__ wave, uint64_t n,
+                                                  CvCount* __restrict__ part) {
+  __shared__ uint32_t s[2][4];
+  uint32_t r = 0, mw = 0;
+  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (uint64_t t = tid; t < n; t += (uint64_t)gridDim.x * blockDim.x) {
+    r += rc[t] == DCC_RC_RCOK;
+    if (wave) mw = max(mw, wave[t]);
+  }
+  for (int d = 32; d > 0; d >>= 1) {
+    r += __shfl_xor(r, d);
+    mw = max(mw, (uint32_t)__shfl_xor(mw, d));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    s[0][threadIdx.x >> 6] = r;
+    s[1][threadIdx.x >> 6] = mw;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0)
+    part[blockIdx.x] = CvCount{s[0][0] + s[0][1] + s[0][2] + s[0][3],
+                               max(max(s[1][0], s[1][1]), max(s[1][2], s[1][3])), 0, 0};
+}
+
+inline unsigned grid1(uint64_t n, unsigned b) {
+  const uint64_t g = (n + b - 1) / b;
+  return (unsigned)(g ? g : 1);
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- driver
+template <typename K>
+static int calvin_sort_and_scan(dcc_ctx* ctx, const DevBatch& d, const uint32_t* seq,
+                                const uint32_t* off2, const KeyPack& kp, const ScanOut& so,
+                                bool prof) {
+  const uint64_t m = d.nnz;
+  hipStream_t st = ctx->stream;
+  CR(ctx->calvin_a.ensure(ctx, std::max<uint64_t>(16, m * sizeof(K)), "calvin keys a"));
+  CR(ctx->calvin_b.ensure(ctx, std::max<uint64_t>(16, m * sizeof(K)), "calvin keys b"));
+  CR(ctx->calvin_c.ensure(ctx, std::max<uint64_t>(16, m * 4), "calvin vals a"));
+  CR(ctx->calvin_d.ensure(ctx, std::max<uint64_t>(16, m * 4), "calvin vals b"));
+  CR(ctx->cv_scratch.ensure(ctx, rs_scratch_words(m) * 4 + 64, "radix scratch"));
+  const uint64_t tiles = (m + CV_TILE - 1) / CV_TILE;
+  CR(ctx->cv_agg.ensure(ctx, std::max<uint64_t>(1, tiles) * sizeof(Gs), "calvin scan"));
+  K* kb[2] = {(K*)ctx->calvin_a.p, (K*)ctx->calvin_b.p};
+  uint32_t* vb[2] = {(uint32_t*)ctx->calvin_c.p, (uint32_t*)ctx->calvin_d.p};
+  k_cv_layout<K><<<grid1(d.n, 256), 256, 0, st>>>(d.off, seq, off2, d.n, d.keys, d.acctype, kp,
+                                                  kb[0], vb[0]);
+  if (prof) CK(hipEventRecord(ctx->pev[1], st));
+  int cur;
+  if (sizeof(K) == 4)
+    cur = radix_sort_u32((uint32_t**)kb, vb, m, kp.bits, (uint32_t*)ctx->cv_scratch.p, st);
+  else
+    cur = radix_sort_u64((uint64_t**)kb, vb, m, kp.bits, (uint32_t*)ctx->cv_scratch.p, st);
+  if (prof) CK(hipEventRecord(ctx->pev[2], st));
+  Gs* agg = (Gs*)ctx->cv_agg.p;
+  k_cv_up<K><<<(unsigned)tiles, 256, 0, st>>>(kb[cur], vb[cur], m, agg);
+  k_cv_top<<<1, 256, 0, st>>>(agg, (uint32_t)tiles);
+  k_cv_down<K><<<(unsigned)tiles, 256, 0, st>>>(kb[cur], vb[cur], m, agg, so);
+  CK(hipGetLastError());
+  return DCC_OK;
+}
+
+int dcc_ctx::calvin_epoch(const dcc_batch* b, uint32_t* out_group, uint8_t* out_rc,
+                          uint32_t* out_wave, dcc_stats* st) {
+  dcc_ctx* ctx = this;
+  const auto t_wall0 = std::chrono::steady_clock::now();
+  CR(check_batch(b));
+  const bool dev_out = (b->flags & DCC_DEVICE_PTRS) != 0;
+  dcc_stats S;
+  memset(&S, 0, sizeof S);
+  S.n_shards = 1;
+  if (b->n_txn == 0) {
+    if (st) *st = S;
+    return DCC_OK;
+  }
+  if (b->n_txn >= CV_MAX_TXN)
+    return fail(DCC_ERANGE, "calvin: n_txn %llu exceeds %u per epoch",
+                (unsigned long long)b->n_txn, CV_MAX_TXN - 1);
+  DevBatch d;
+  CR(stage_batch(b, d));
+  CK(hipEventRecord(ev0, stream));
+  if (profiling) CK(hipEventRecord(pev[0], stream));
+
+  // ---- prep: offsets/length validation + which key / order bits vary
+  launch_prep(d.off, d.n, d.acctype, d.nnz, (PrepPart*)part.p, stream);
+  CvPart* cvp = (CvPart*)((char*)part.p + 16384);
+  k_cv_prep<<<CV_PREP_BLOCKS, 256, 0, stream>>>(d.keys, d.nnz, d.acctype, d.order, d.n, cvp);
+  CK(hipGetLastError());
+  CK(hipMemcpyAsync(hpart, part.p, 16384 + CV_PREP_BLOCKS * sizeof(CvPart), hipMemcpyDeviceToHost,
+                    stream));
+  CK(hipStreamSynchronize(stream));
+  uint32_t maxlen = 0, perr = 0;
+  uint64_t kor = 0, kand = ~0ull, oor = 0, oand = ~0ull, nex = 0;
+  {
+    const PrepPart* pp = (const PrepPart*)hpart;
+    for (unsigned q = 0; q < PREP_BLOCKS; q++) {
+      perr |= pp[q].err;
+      maxlen = std::max(maxlen, pp[q].maxlen);
+    }
+    const CvPart* cp = (const CvPart*)((const char*)hpart + 16384);
+    for (unsigned q = 0; q < CV_PREP_BLOCKS; q++) {
+      kor |= cp[q].kor;
+      kand &= cp[q].kand;
+      oor |= cp[q].oor;
+      oand &= cp[q].oand;
+      nex += cp[q].nex;
+    }
+  }
+  if (perr & ERR_OFFSETS) return fail(DCC_EINVAL, "batch: malformed offsets");
+  if (maxlen > MAX_TXN_LEN)
+    return fail(DCC_ERANGE, "batch: a txn has %u accesses (> MAX_ROW_PER_TXN=%u)", maxlen,
+                MAX_TXN_LEN);
+  const KeyPack kp = make_keypack(d.nnz ? (kor ^ kand) : 0);
+
+  // ---- outputs / workspaces
+  CR(rc.ensure(this, d.n + 16, "rc"));
+  uint8_t* rc_dev = (dev_out && out_rc) ? out_rc : (uint8_t*)rc.p;
+  CK(hipMemsetAsync(rc_dev, DCC_RC_RCOK, d.n, stream));
+  uint32_t* grp_dev = nullptr;
+  if (out_group) {
+    if (dev_out) {
+      grp_dev = out_group;
+    } else {
+      CR(cv_group.ensure(this, std::max<uint64_t>(16, d.nnz * 4), "calvin group"));
+      grp_dev = (uint32_t*)cv_group.p;
+    }
+  }
+  const bool waves = out_wave != nullptr;
+  uint32_t* wave_dev = nullptr;
+  ScanOut so{d.off, grp_dev, rc_dev, nullptr, nullptr, nullptr};
+  if (waves) {
+    if (dev_out) {
+      wave_dev = out_wave;
+    } else {
+      CR(cv_wave.ensure(this, d.n * 4 + 16, "calvin wave"));
+      wave_dev = (uint32_t*)cv_wave.p;
+    }
+    const uint64_t m = std::max<uint64_t>(16, d.nnz * 4);
+    CR(cv_pgx.ensure(this, m, "calvin pgx"));
+    CR(cv_gsx.ensure(this, m, "calvin gsx"));
+    CR(cv_gsize.ensure(this, m, "calvin gsize"));
+    CR(cv_done.ensure(this, m, "calvin done"));
+    CR(cv_maxl.ensure(this, m, "calvin maxl"));
+    CK(hipMemsetAsync(cv_gsize.p, 0, m, stream));
+    CK(hipMemsetAsync(cv_done.p, 0, m, stream));
+    CK(hipMemsetAsync(cv_maxl.p, 0, m, stream));
+    so.pgx = (uint32_t*)cv_pgx.p;
+    so.gsx = (uint32_t*)cv_gsx.p;
+    so.gsize = (uint32_t*)cv_gsize.p;
+  }
+  uint32_t* err = (uint32_t*)misc.p;
+  CK(hipMemsetAsync(err, 0, 4, stream));
+
+  // ---- rank: seq[q] = txn at sequence position q (stable in index order)
+  const uint32_t* seq = nullptr;
+  const uint32_t* off2 = nullptr;
+  if (d.order && (oor ^ oand)) {
+    const KeyPack op = make_keypack(oor ^ oand);
+    CR(perm.ensure(this, d.n * 4 + 16, "calvin seq a"));
+    CR(cv_seq_b.ensure(this, d.n * 4 + 16, "calvin seq b"));
+    CR(cv_ok.ensure(this, d.n * 8 * 2 + 32, "calvin order keys"));
+    CR(cv_scratch.ensure(this, rs_scratch_words(std::max<uint64_t>(d.n, d.nnz)) * 4 + 64,
+                         "radix scratch"));
+    uint32_t* vb[2] = {(uint32_t*)perm.p, (uint32_t*)cv_seq_b.p};
+    int cur;
+    if (op.bits <= 32) {
+      uint32_t* kb[2] = {(uint32_t*)cv_ok.p, (uint32_t*)cv_ok.p + d.n + 4};
+      k_cv_order_init<uint32_t><<<grid1(d.n, 256), 256, 0, stream>>>(d.order, d.n, op, kb[0], vb[0]);
+      cur = radix_sort_u32(kb, vb, d.n, op.bits, (uint32_t*)cv_scratch.p, stream);
+    } else {
+      uint64_t* kb[2] = {(uint64_t*)cv_ok.p, (uint64_t*)cv_ok.p + d.n + 2};
+      k_cv_order_init<uint64_t><<<grid1(d.n, 256), 256, 0, stream>>>(d.order, d.n, op, kb[0], vb[0]);
+      cur = radix_sort_u64(kb, vb, d.n, op.bits, (uint32_t*)cv_scratch.p, stream);
+    }
+    seq = vb[cur];
+    // request offsets in sequence order
+    const uint64_t lt = (d.n + CV_TILE - 1) / CV_TILE;
+    CR(cv_len.ensure(this, d.n * 4 + 16, "calvin len"));
+    CR(cv_off2.ensure(this, (d.n + 1) * 4 + 16, "calvin off2"));
+    CR(cv_tsum.ensure(this, (lt + 1) * 4 + 16, "calvin tile sums"));
+    uint32_t* tsum = (uint32_t*)cv_tsum.p;
+    k_cv_len_tiles<<<(unsigned)lt, 256, 0, stream>>>(d.off, seq, d.n, (uint32_t*)cv_len.p, tsum);
+    rs_scan_one(tsum, (uint32_t)lt, tsum + lt, stream);
+    k_cv_len_apply<<<(unsigned)lt, 256, 0, stream>>>((const uint32_t*)cv_len.p, d.n, tsum,
+                                                     (uint32_t)d.nnz, (uint32_t*)cv_off2.p);
+    off2 = (const uint32_t*)cv_off2.p;
+  }
+  CK(hipGetLastError());
+
+  // ---- requests in sequence order -> sorted by row -> group scan
+  if (d.nnz) {
+    if (kp.bits <= 32) CR(calvin_sort_and_scan<uint32_t>(this, d, seq, off2, kp, so, profiling));
+    else CR(calvin_sort_and_scan<uint64_t>(this, d, seq, off2, kp, so, profiling));
+  } else if (profiling) {
+    CK(hipEventRecord(pev[1], stream));
+    CK(hipEventRecord(pev[2], stream));
+  }
+  if (profiling) CK(hipEventRecord(pev[3], stream));
+
+  // ---- wave levels
+  if (waves) {
+    WaveArgs wa{d.n, seq, d.off, so.pgx, so.gsx, so.gsize, (uint32_t*)cv_done.p,
+                (uint32_t*)cv_maxl.p, wave_dev, err, 100000000ull * 20};
+    // co-resident persistent grid: 4 workgroups of 4 waves per CU
+    const unsigned g = (unsigned)std::min<uint64_t>((uint64_t)n_cu * 4, (d.n + 3) / 4);
+    k_cv_wave<<<g ? g : 1, 256, 0, stream>>>(wa);
+    CK(hipGetLastError());
+  }
+  if (profiling) CK(hipEventRecord(pev[4], stream));
+  CvCount* cc = (CvCount*)part.p;
+  k_cv_count<<<CV_PREP_BLOCKS, 256, 0, stream>>>(rc_dev, wave_dev, d.n, cc);
+  CK(hipGetLastError());
+  CK(hipEventRecord(ev1, stream));
+  if (!dev_out) {
+    if (out_rc) CK(hipMemcpyAsync(out_rc, rc_dev, d.n, hipMemcpyDeviceToHost, stream));
+    if (out_group && d.nnz)
+      CK(hipMemcpyAsync(out_group, grp_dev, d.nnz * 4, hipMemcpyDeviceToHost, stream));
+    if (waves) CK(hipMemcpyAsync(out_wave, wave_dev, d.n * 4, hipMemcpyDeviceToHost, stream));
+  }
+  CK(hipMemcpyAsync(hmisc, misc.p, 64, hipMemcpyDeviceToHost, stream));
+  CK(hipMemcpyAsync(hpart, part.p, CV_PREP_BLOCKS * sizeof(CvCount), hipMemcpyDeviceToHost, stream));
+  CK(hipStreamSynchronize(stream));
+  if (*(const uint32_t*)hmisc & ERR_WAVE_TIMEOUT)
+    return fail(DCC_EIO, "calvin: wave kernel exceeded its time budget");
+  uint64_t ready = 0;
+  uint32_t maxwave = 0;
+  for (unsigned q = 0; q < CV_PREP_BLOCKS; q++) {
+    ready += ((const CvCount*)hpart)[q].ready;
+    maxwave = std::max(maxwave, ((const CvCount*)hpart)[q].maxwave);
+  }
+  float ms = 0;
+  CK(hipEventElapsedTime(&ms, ev0, ev1));
+  S.rounds = waves ? maxwave + 1 : 0;
+  S.n_commit = ready;
+  S.n_abort = d.n - ready;
+  S.nnz_w = nex;
+  S.alg_bytes = dcc_calvin_alg_bytes(d.n, d.nnz, d.order != nullptr, waves);
+  S.device_ms = ms;
+  if (profiling) {
+    float t[4] = {0, 0, 0, 0};
+    CK(hipEventElapsedTime(&t[0], pev[0], pev[1]));  // prep + rank + layout
+    CK(hipEventElapsedTime(&t[1], pev[1], pev[2]));  // key sort
+    CK(hipEventElapsedTime(&t[2], pev[2], pev[3]));  // group scan
+    CK(hipEventElapsedTime(&t[3], pev[3], pev[4]));  // waves
+    for (int q = 0; q < 4; q++) S.phase_ms[q] = t[q];
+  }
+  const auto t_wall1 = std::chrono::steady_clock::now();
+  S.total_ms = std::chrono::duration<double, std::milli>(t_wall1 - t_wall0).count();
+  if (st) *st = S;
+  return DCC_OK;
+}
+
+extern "C" uint64_t dcc_calvin_alg_bytes(uint64_t n_txn, uint64_t nnz, int with_order,
+                                         int with_wave) {
+  // offsets, key + acctype per request, group per request, RC byte per txn,
+  // order per txn (if given), wave per txn (if requested)
+  return 4 * (n_txn + 1) + 9 * nnz + 4 * nnz + n_txn + (with_order ? 8 * n_txn : 0) +
+         (with_wave ? 4 * n_txn : 0);
 }
 
 extern "C" int dcc_calvin_order_epoch(dcc_ctx* ctx, const dcc_batch* batch, uint32_t* out_group,

@@ -57,6 +57,8 @@ struct dcc_ctx {
   DevBuf l_tid[2], l_coff[2], l_cent[2];         // ping-pong undecided lists
   DevBuf hkeys, hoff, htn;                       // history CSR
   DevBuf perm, calvin_a, calvin_b, calvin_c, calvin_d;  // Calvin workspaces
+  DevBuf cv_scratch, cv_agg, cv_group, cv_wave, cv_pgx, cv_gsx, cv_gsize, cv_done, cv_maxl;
+  DevBuf cv_seq_b, cv_ok, cv_len, cv_off2, cv_tsum;
 
   // OCC history (occ.h:62-64) and commit counter tnc (occ.h:67)
   std::vector<std::pair<uint64_t, uint64_t>> hist;

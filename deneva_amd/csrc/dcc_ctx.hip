@@ -174,7 +174,10 @@ extern "C" int dcc_set_stream(dcc_ctx* ctx, void* s) {
 std::vector<DevBuf*> dcc_ctx::all_bufs() {
   std::vector<DevBuf*> v = {&misc, &part, &off, &keys, &acctype, &start_tn, &finish_tn, &table, &state,
                             &hasw, &cflag, &bsum, &tn, &rc, &hkeys, &hoff, &htn, &stat,
-                            &order, &perm, &calvin_a, &calvin_b, &calvin_c, &calvin_d};
+                            &order, &perm, &calvin_a, &calvin_b, &calvin_c, &calvin_d,
+                            &cv_scratch, &cv_agg, &cv_group, &cv_wave, &cv_pgx, &cv_gsx,
+                            &cv_gsize, &cv_done, &cv_maxl, &cv_seq_b, &cv_ok, &cv_len,
+                            &cv_off2, &cv_tsum};
   for (int i = 0; i < 2; i++) {
     v.push_back(&l_tid[i]);
     v.push_back(&l_coff[i]);

@@ -1,0 +1,236 @@
+// gfx950 stable LSD radix sort of (key, u32 value) pairs — see radix_sort.h.
+#include <hip/hip_runtime.h>
+
+#include "dcc_device.h"
+#include "radix_sort.h"
+
+namespace dcc {
+
+// Lanes of the wave whose 8-bit digit equals this lane's (8 ballots).
+__device__ inline uint64_t digit_peers(uint32_t d, bool act) {
+  uint64_t m = ballot64(act);
+#pragma unroll
+  for (int b = 0; b < 8; b++) {
+    const uint64_t bb = ballot64((d >> b) & 1u);
+    m &= ((d >> b) & 1u) ? bb : ~bb;
+  }
+  return act ? m : 0ull;
+}
+
+__device__ inline uint64_t lanemask_lt() {
+  const uint32_t l = lane_id();
+  return l == 0 ? 0ull : (~0ull >> (64 - l));
+}
+
+// Exclusive scan of one u32 per thread over a 256-thread workgroup.
+__device__ inline uint32_t block_excl_scan256(uint32_t v, uint32_t* sh /*[4]*/, uint32_t& total) {
+  const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d);
+    if (lane >= (uint32_t)d) x += y;
+  }
+  __syncthreads();
+  if (lane == 63) sh[wv] = x;
+  __syncthreads();
+  uint32_t off = 0;
+  total = 0;
+  for (uint32_t w = 0; w < 4; w++) {
+    if (w < wv) off += sh[w];
+    total += sh[w];
+  }
+  return off + x - v;
+}
+
+template <typename K>
+__global__ __launch_bounds__(RS_THREADS) void k_rs_hist(const K* __restrict__ keys, uint64_t m,
+                                                        uint32_t shift, uint32_t* __restrict__ cnt,
+                                                        uint32_t tiles) {
+  __shared__ uint32_t s_h[256];
+  s_h[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
+  K k[RS_ITEMS];
+#pragma unroll
+  for (uint32_t it = 0; it < RS_ITEMS; it++) {
+    const uint64_t p = base + it * RS_THREADS + threadIdx.x;
+    k[it] = p < m ? keys[p] : (K)0;
+  }
+  const uint64_t lt = lanemask_lt();
+#pragma unroll
+  for (uint32_t it = 0; it < RS_ITEMS; it++) {
+    const uint64_t p = base + it * RS_THREADS + threadIdx.x;
+    const uint32_t d = (uint32_t)(k[it] >> shift) & 255u;
+    const uint64_t peers = digit_peers(d, p < m);
+    if (peers && (peers & lt) == 0) atomicAdd(&s_h[d], (uint32_t)__builtin_popcountll(peers));
+  }
+  __syncthreads();
+  cnt[(uint64_t)threadIdx.x * tiles + blockIdx.x] = s_h[threadIdx.x];
+}
+
+// One workgroup per digit: exclusive scan of cnt[d][0..tiles) in place,
+// digit total to tot[d].
+__global__ __launch_bounds__(RS_THREADS) void k_rs_scan(uint32_t* __restrict__ cnt, uint32_t tiles,
+                                                        uint32_t* __restrict__ tot) {
+  __shared__ uint32_t sh[4];
+  uint32_t* row = cnt + (uint64_t)blockIdx.x * tiles;
+  uint32_t run = 0;
+  for (uint32_t c0 = 0; c0 < tiles; c0 += RS_THREADS * 4) {
+    uint32_t v[4], s = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const uint32_t i = c0 + threadIdx.x * 4 + q;
+      v[q] = i < tiles ? row[i] : 0u;
+      s += v[q];
+    }
+    uint32_t total;
+    uint32_t pre = run + block_excl_scan256(s, sh, total);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const uint32_t i = c0 + threadIdx.x * 4 + q;
+      if (i < tiles) row[i] = pre;
+      pre += v[q];
+    }
+    run += total;
+  }
+  if (threadIdx.x == 0) tot[blockIdx.x] = run;
+}
+
+template <typename K>
+__global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(const K* __restrict__ kin,
+                                                           const uint32_t* __restrict__ vin,
+                                                           K* __restrict__ kout,
+                                                           uint32_t* __restrict__ vout, uint64_t m,
+                                                           uint32_t shift,
+                                                           const uint32_t* __restrict__ cnt,
+                                                           const uint32_t* __restrict__ tot,
+                                                           uint32_t tiles) {
+  __shared__ K s_key[RS_TILE];
+  __shared__ uint32_t s_val[RS_TILE];
+  __shared__ uint32_t s_wc[4][256];
+  __shared__ uint32_t s_run[256];  // running per-digit count inside the tile
+  __shared__ uint32_t s_gb[256];   // global destination base per digit
+  __shared__ uint32_t s_tb[256];   // tile-local base per digit
+  __shared__ uint32_t sh[4];
+  const uint32_t tid = threadIdx.x, wv = tid >> 6;
+  const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
+
+  K k[RS_ITEMS];
+  uint32_t v[RS_ITEMS];
+#pragma unroll
+  for (uint32_t it = 0; it < RS_ITEMS; it++) {
+    const uint64_t p = base + it * RS_THREADS + tid;
+    k[it] = p < m ? kin[p] : (K)0;
+    v[it] = p < m ? vin[p] : 0u;
+  }
+  {
+    uint32_t total;
+    const uint32_t g = block_excl_scan256(tot[tid], sh, total);
+    s_gb[tid] = g + cnt[(uint64_t)tid * tiles + blockIdx.x];
+  }
+  s_run[tid] = 0;
+#pragma unroll
+  for (int w = 0; w < 4; w++) s_wc[w][tid] = 0;
+  __syncthreads();
+
+  // stable in-tile ranking: item order = (iteration, thread)
+  const uint64_t lt = lanemask_lt();
+  uint32_t loc[RS_ITEMS];
+#pragma unroll
+  for (uint32_t it = 0; it < RS_ITEMS; it++) {
+    const uint64_t p = base + it * RS_THREADS + tid;
+    const bool act = p < m;
+    const uint32_t d = (uint32_t)(k[it] >> shift) & 255u;
+    const uint64_t peers = digit_peers(d, act);
+    const uint32_t lr = (uint32_t)__builtin_popcountll(peers & lt);
+    if (act && lr == 0) s_wc[wv][d] = (uint32_t)__builtin_popcountll(peers);
+    __syncthreads();
+    uint32_t o = s_run[d] + lr;
+    for (uint32_t w = 0; w < wv; w++) o += s_wc[w][d];
+    loc[it] = o;
+    __syncthreads();
+    s_run[tid] += s_wc[0][tid] + s_wc[1][tid] + s_wc[2][tid] + s_wc[3][tid];
+#pragma unroll
+    for (int w = 0; w < 4; w++) s_wc[w][tid] = 0;
+    __syncthreads();
+  }
+  {
+    uint32_t total;
+    s_tb[tid] = block_excl_scan256(s_run[tid], sh, total);
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t it = 0; it < RS_ITEMS; it++) {
+    const uint64_t p = base + it * RS_THREADS + tid;
+    if (p < m) {
+      const uint32_t d = (uint32_t)(k[it] >> shift) & 255u;
+      const uint32_t pos = s_tb[d] + loc[it];
+      s_key[pos] = k[it];
+      s_val[pos] = v[it];
+    }
+  }
+  __syncthreads();
+  const uint32_t n_here = (uint32_t)min<uint64_t>(RS_TILE, m - base);
+  for (uint32_t j = tid; j < n_here; j += RS_THREADS) {
+    const K kk = s_key[j];
+    const uint32_t d = (uint32_t)(kk >> shift) & 255u;
+    const uint64_t dst = (uint64_t)s_gb[d] + (j - s_tb[d]);
+    kout[dst] = kk;
+    vout[dst] = s_val[j];
+  }
+}
+
+template <typename K>
+static int radix_sort_impl(K* k[2], uint32_t* v[2], uint64_t m, uint32_t bits, uint32_t* scratch,
+                           hipStream_t st) {
+  int cur = 0;
+  if (m <= 1 || bits == 0) return cur;
+  const uint32_t tiles = (uint32_t)rs_tiles(m);
+  uint32_t* cnt = scratch;
+  uint32_t* tot = scratch + 256ull * tiles;
+  for (uint32_t shift = 0; shift < bits; shift += 8) {
+    k_rs_hist<K><<<tiles, RS_THREADS, 0, st>>>(k[cur], m, shift, cnt, tiles);
+    k_rs_scan<<<256, RS_THREADS, 0, st>>>(cnt, tiles, tot);
+    k_rs_scatter<K><<<tiles, RS_THREADS, 0, st>>>(k[cur], v[cur], k[cur ^ 1], v[cur ^ 1], m, shift,
+                                                  cnt, tot, tiles);
+    cur ^= 1;
+  }
+  return cur;
+}
+
+int radix_sort_u32(uint32_t* k[2], uint32_t* v[2], uint64_t m, uint32_t bits, uint32_t* scratch,
+                   hipStream_t st) {
+  return radix_sort_impl<uint32_t>(k, v, m, bits > 32 ? 32 : bits, scratch, st);
+}
+int radix_sort_u64(uint64_t* k[2], uint32_t* v[2], uint64_t m, uint32_t bits, uint32_t* scratch,
+                   hipStream_t st) {
+  return radix_sort_impl<uint64_t>(k, v, m, bits > 64 ? 64 : bits, scratch, st);
+}
+
+void rs_scan_one(uint32_t* row, uint32_t len, uint32_t* total, hipStream_t st) {
+  k_rs_scan<<<1, RS_THREADS, 0, st>>>(row, len, total);
+}
+
+KeyPack make_keypack(uint64_t varying) {
+  KeyPack p{};
+  uint32_t dst = 0;
+  for (uint32_t b = 0; b < 64;) {
+    if (!((varying >> b) & 1ull)) {
+      b++;
+      continue;
+    }
+    uint32_t w = 0;
+    while (b + w < 64 && ((varying >> (b + w)) & 1ull)) w++;
+    p.src[p.nruns] = (uint8_t)b;
+    p.width[p.nruns] = (uint8_t)w;
+    p.dst[p.nruns] = (uint8_t)dst;
+    p.nruns++;
+    dst += w;
+    b += w;
+  }
+  p.bits = dst;
+  return p;
+}
+
+}  // namespace dcc

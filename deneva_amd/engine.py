@@ -238,6 +238,10 @@ def alg_bytes(n_txn: int, nnz: int, nnz_w: int) -> int:
     return int(lib.dcc_alg_bytes(n_txn, nnz, nnz_w))
 
 
+def calvin_alg_bytes(n_txn: int, nnz: int, with_order: bool, with_wave: bool) -> int:
+    return int(lib.dcc_calvin_alg_bytes(n_txn, nnz, int(with_order), int(with_wave)))
+
+
 # ---------------------------------------------------------------- producers
 def ycsb_params(**kw) -> _abi.YcsbParams:
     p = _abi.YcsbParams()

@@ -178,7 +178,12 @@ uint64_t dcc_occ_get_tnc(const dcc_ctx* ctx);
  *   out_rc[i]    = DCC_RC_RCOK if every request is in group 0, else DCC_RC_WAIT
  *                  (acquire_locks' return).
  *   out_wave[i]  = wave in which txn i runs when every txn releases all its
- *                  locks one wave after it became ready (may be NULL). */
+ *                  locks one wave after it became ready (may be NULL).
+ * batch->order (may be NULL = index order) is the sequencer's order key
+ * (origin << 32 | seq); ties keep index order.
+ * n_txn < 2^25.  Stats: n_commit = txns ready at acquire (RCOK), n_abort =
+ * txns that WAIT, nnz_w = EX requests, rounds = number of waves (0 when
+ * out_wave is NULL). */
 int dcc_calvin_order_epoch(dcc_ctx* ctx, const dcc_batch* batch, uint32_t* out_group,
                            uint8_t* out_rc, uint32_t* out_wave, dcc_stats* out_stats);
 
@@ -243,6 +248,9 @@ int dcc_gen_tpcc(const dcc_tpcc_params* p, uint32_t* offsets, uint64_t* keys,
 /* Algorithmic bytes of one epoch pass:
  * 4(N+1) + 9 nnz + 16 nnz_w + 16 nnz + N. */
 uint64_t dcc_alg_bytes(uint64_t n_txn, uint64_t nnz, uint64_t nnz_w);
+/* Algorithmic bytes of one Calvin epoch: 4(N+1) offsets + 9 nnz (key, type)
+ * + 4 nnz (grant group) + N (RC) [+ 8N order] [+ 4N wave]. */
+uint64_t dcc_calvin_alg_bytes(uint64_t n_txn, uint64_t nnz, int with_order, int with_wave);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,152 @@
+"""GPU parity of the Calvin epoch lock-ordering engine against the oracle:
+bit-exact grant group per request, acquire_locks RC per txn and wave level
+per txn, on identical batches."""
+import numpy as np
+import pytest
+
+import _oracle as orc
+import deneva_amd as d
+from deneva_amd import RD, WR, XP, SCAN
+from helpers import make_batch, random_batch
+
+pytestmark = pytest.mark.gpu
+
+
+def run(engine, b, waves=True, literal=False):
+    g, rc, w, st = engine.calvin_order_epoch(b, want_group=True, want_wave=waves)
+    eg, erc, ew = orc.calvin(b, literal=literal)
+    g = np.asarray(g).astype(np.uint32)
+    rc = np.asarray(rc)
+    bad = np.nonzero(g != eg)[0]
+    assert bad.size == 0, f"group mismatch at requests {bad[:10]} (gpu {g[bad[:10]]} oracle {eg[bad[:10]]})"
+    bad = np.nonzero(rc != erc)[0]
+    assert bad.size == 0, f"rc mismatch at txns {bad[:10]}"
+    if waves:
+        w = np.asarray(w).astype(np.uint32)
+        bad = np.nonzero(w != ew)[0]
+        assert bad.size == 0, f"wave mismatch at txns {bad[:10]} (gpu {w[bad[:10]]} oracle {ew[bad[:10]]})"
+        if b.n_txn:
+            assert st["rounds"] == int(ew.max()) + 1
+    assert st["n_commit"] == int((erc == 0).sum())
+    assert st["n_abort"] == int((erc == 3).sum())
+    return g, rc, st
+
+
+def c4_order(b):
+    """Sequencer order of a partitioned YCSB batch: (origin = home partition,
+    FIFO seq within the origin) — sched_dequeue's (epoch, origin, FIFO)."""
+    home = b.meta["home"].astype(np.uint64)
+    seq = np.zeros(b.n_txn, np.uint64)
+    for h in np.unique(home):
+        idx = np.nonzero(home == h)[0]
+        seq[idx] = np.arange(idx.size, dtype=np.uint64)
+    return (home << np.uint64(32)) | seq
+
+
+def test_kat_fifo_no_barging(engine):
+    g, rc, _ = run(engine, make_batch([[(1, RD)], [(1, WR)], [(1, RD)], [(1, RD)], [(1, WR)]]),
+                   literal=True)
+    assert list(g) == [0, 1, 2, 2, 3]
+    assert list(rc) == [0, 3, 3, 3, 3]
+
+
+def test_kat_dedup_and_types(engine):
+    g, rc, _ = run(engine, make_batch([[(5, RD), (5, WR)], [(5, SCAN)], [(6, XP)], [(6, SCAN)]]),
+                   literal=True)
+    assert g[1] == d.GROUP_NONE
+
+
+def test_kat_order(engine):
+    b = make_batch([[(1, WR)], [(1, WR)], [(1, RD)]], order=[(1 << 32) | 5, 0, (1 << 32) | 1])
+    g, rc, _ = run(engine, b, literal=True)
+    assert list(g) == [2, 0, 1]
+
+
+def test_empty_and_zero_length(engine):
+    run(engine, make_batch([]))
+    run(engine, make_batch([[], [], []]))
+    run(engine, make_batch([[], [(3, WR)], [], [(3, RD)]]))
+    run(engine, make_batch([[(7, RD)]]))
+
+
+@pytest.mark.parametrize("n_keys", [1, 8, 200, 100000])
+def test_random_dups_all_types(engine, n_keys):
+    rng = np.random.default_rng(n_keys)
+    b = random_batch(rng, 3000, 20, n_keys, types=(RD, WR, XP, SCAN), unique=False)
+    run(engine, b, literal=True)
+
+
+def test_random_max_len(engine):
+    rng = np.random.default_rng(3)
+    run(engine, random_batch(rng, 2000, 64, 5000, types=(RD, WR, XP, SCAN), unique=False))
+
+
+@pytest.mark.parametrize("theta", [0.0, 0.9, 0.99])
+@pytest.mark.parametrize("n", [1, 1000, 65536])
+def test_ycsb_index_order(engine, theta, n):
+    run(engine, d.gen_ycsb(n_txn=n, zipf_theta=theta, req_per_query=16))
+
+
+@pytest.mark.parametrize("theta", [0.6, 0.9])
+def test_ycsb_c4_order(engine, theta):
+    b = d.gen_ycsb(n_txn=65536, zipf_theta=theta, part_cnt=16, chunk_txns=4096, want_home=True)
+    b.order = c4_order(b)
+    run(engine, b)
+
+
+def test_random_order_with_ties(engine):
+    rng = np.random.default_rng(11)
+    b = d.gen_ycsb(n_txn=20000, zipf_theta=0.9, req_per_query=8, table_size=5000)
+    b.order = rng.integers(0, 50, size=b.n_txn).astype(np.uint64)  # many equal keys: index order
+    run(engine, b)
+
+
+def test_order_wide_bits(engine):
+    # > 32 varying order bits: 64-bit order sort path
+    rng = np.random.default_rng(12)
+    b = d.gen_ycsb(n_txn=30000, zipf_theta=0.9, req_per_query=8, table_size=20000)
+    b.order = rng.integers(0, 2**63, size=b.n_txn, dtype=np.uint64)
+    run(engine, b)
+
+
+def test_wide_keys(engine):
+    # canonical TPC-C style keys (table << 56 | key) and random 64-bit keys:
+    # more than 32 varying bits -> 64-bit key sort path
+    rng = np.random.default_rng(13)
+    b = random_batch(rng, 5000, 16, 3000, types=(RD, WR), unique=False)
+    tbl = rng.integers(1, 9, size=b.nnz).astype(np.uint64)
+    b.keys = (tbl << np.uint64(56)) | (b.keys * np.uint64(0x9E3779B1) & np.uint64((1 << 40) - 1))
+    run(engine, b)
+    b.keys = rng.integers(0, 2**64 - 1, size=b.nnz, dtype=np.uint64)
+    run(engine, b)
+
+
+def test_single_key_all_txns(engine):
+    # one hot row, alternating SH runs and EX: deep group chain
+    rng = np.random.default_rng(14)
+    txns = [[(42, WR if rng.random() < 0.3 else RD)] for _ in range(20000)]
+    run(engine, make_batch(txns))
+
+
+def test_c4_full_size(engine):
+    # C4: 1,048,576 txns x 16 keys, 16 partitions, sequencer order
+    b = d.gen_ycsb(n_txn=1 << 20, zipf_theta=0.9, part_cnt=16, chunk_txns=65536, want_home=True)
+    b.order = c4_order(b)
+    run(engine, b, waves=False)
+
+
+def test_device_pointers(engine):
+    import torch
+    b = d.gen_ycsb(n_txn=50000, zipf_theta=0.9)
+    g, rc, _ = run(engine, b)
+    db = b.to_torch("cuda:0")
+    g2, rc2, w2, st = engine.calvin_order_epoch(db, want_group=True, want_wave=True)
+    assert np.array_equal(g2.cpu().numpy().astype(np.uint32)[:b.nnz], g)
+    assert np.array_equal(rc2.cpu().numpy()[:b.n_txn], rc)
+
+
+def test_repeat_deterministic(engine):
+    b = d.gen_ycsb(n_txn=100000, zipf_theta=0.99)
+    g1, rc1, _ = run(engine, b, waves=False)
+    g2, rc2, _, _ = engine.calvin_order_epoch(b, want_group=True, want_wave=False)
+    assert np.array_equal(np.asarray(g2), g1) and np.array_equal(np.asarray(rc2), rc1)
