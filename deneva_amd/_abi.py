@@ -29,6 +29,8 @@ GROUP_NONE = 0xFFFFFFFF
 DEVICE_PTRS = 0x1
 OCC_APPEND_HISTORY = 0x2
 UNIQUE_ID_BYTES = 128
+# int (*)(void* user, uint8_t* host_buf, uint64_t n): in-place MAX all-reduce
+EXCHANGE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint8), C.c_uint64)
 OPT_RECHECK = 1
 OPT_BATCH_MAX = 2
 
@@ -125,6 +127,9 @@ _SIGS = [
     ("dcc_reserve", C.c_int, [_P, C.c_uint64, C.c_uint64]),
     ("dcc_comm_unique_id", C.c_int, [_P]),
     ("dcc_comm_init", C.c_int, [_P, C.c_int, C.c_int, _P]),
+    ("dcc_comm_init_host", C.c_int, [_P, C.c_int, C.c_int, C.c_void_p, _P]),
+    ("dcc_comm_rank", C.c_int, [_P]),
+    ("dcc_comm_size", C.c_int, [_P]),
     ("dcc_comm_destroy", C.c_int, [_P]),
     ("dcc_key_shard", C.c_uint32, [C.c_uint64, C.c_uint32]),
     ("dcc_shard_filter", C.c_int, [C.POINTER(Batch), C.c_uint32, C.c_uint32, _P, _P, _P,

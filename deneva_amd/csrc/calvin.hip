@@ -540,11 +540,13 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, uint32_t* out_group, uint8_t* out_
   const bool dev_out = (b->flags & DCC_DEVICE_PTRS) != 0;
   dcc_stats S;
   memset(&S, 0, sizeof S);
-  S.n_shards = 1;
+  S.n_shards = (uint32_t)comm_ranks();
   if (b->n_txn == 0) {
     if (st) *st = S;
     return DCC_OK;
   }
+  if (out_wave && comm_ranks() > 1)
+    return fail(DCC_ENOTSUP, "calvin: wave levels need the whole epoch on one GPU");
   if (b->n_txn >= CV_MAX_TXN)
     return fail(DCC_ERANGE, "calvin: n_txn %llu exceeds %u per epoch",
                 (unsigned long long)b->n_txn, CV_MAX_TXN - 1);
@@ -668,6 +670,10 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, uint32_t* out_group, uint8_t* out_
     CK(hipEventRecord(pev[2], stream));
   }
   if (profiling) CK(hipEventRecord(pev[3], stream));
+
+  // ---- sharded: grant groups are per row, hence shard-local; a txn is
+  // ready only if it is ready on every shard (WAIT = 3 > RCOK = 0)
+  if (comm_ranks() > 1) CR(comm_allreduce_max_u8(rc_dev, d.n));
 
   // ---- wave levels
   if (waves) {

@@ -1,24 +1,120 @@
-// Multi-GPU key sharding over RCCL — placeholder until the
-// sharded round driver lands.
+// Multi-GPU key sharding: one process per GPU, each owning
+// the keys with dcc_key_shard(key, nranks) == rank.  The only exchange is an
+// in-place all-reduce MAX of per-txn bytes once per fixed-point round (OCC
+// status: 0 clear, 1 blocked, 2 killed — killed on any shard dominates, the
+// 2PC AND of votes of worker_thread.cpp:328-334) and once per epoch for
+// Calvin readiness.
+//
+// Two backends behind one call:
+//   RCCL  (dcc_comm_init): ncclAllReduce(ncclUint8, ncclMax) enqueued on the
+//         engine stream — no host synchronisation, rounds stay batched.
+//   host  (dcc_comm_init_host): the caller's exchange function runs on a
+//         pinned host copy (used by tests that put several ranks on one GPU
+//         and exchange over torch.distributed/gloo).
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
 
 #include "dcc.h"
 #include "dcc_ctx.h"
 
+static_assert(sizeof(ncclUniqueId) == DCC_UNIQUE_ID_BYTES, "unique id size");
+
 struct dcc_comm_state {
   int rank = 0, nranks = 1;
+  ncclComm_t nccl = nullptr;
+  dcc_exchange_fn fn = nullptr;
+  void* user = nullptr;
+  uint8_t* hbuf = nullptr;  // pinned staging for the host backend
+  uint64_t hcap = 0;
 };
 
 int dcc_ctx::comm_ranks() const { return comm ? comm->nranks : 1; }
 
-extern "C" int dcc_comm_unique_id(void*) { return DCC_ENOTSUP; }
-extern "C" int dcc_comm_init(dcc_ctx*, int, int, const void*) { return DCC_ENOTSUP; }
+int dcc_ctx::comm_allreduce_max_u8(uint8_t* dev, uint64_t n) {
+  dcc_ctx* ctx = this;
+  if (!comm || comm->nranks <= 1 || n == 0) return DCC_OK;
+  if (comm->nccl) {
+    const ncclResult_t r = ncclAllReduce(dev, dev, n, ncclUint8, ncclMax, comm->nccl, stream);
+    if (r != ncclSuccess) return fail(DCC_ECOMM, "ncclAllReduce: %s", ncclGetErrorString(r));
+    return DCC_OK;
+  }
+  if (comm->hcap < n) {
+    if (comm->hbuf) (void)hipHostFree(comm->hbuf);
+    comm->hbuf = nullptr;
+    comm->hcap = 0;
+    hipError_t e = hipHostMalloc((void**)&comm->hbuf, n, hipHostMallocDefault);
+    if (e != hipSuccess) return hip_fail(e, "hipHostMalloc(exchange)");
+    comm->hcap = n;
+  }
+  hipError_t e = hipMemcpyAsync(comm->hbuf, dev, n, hipMemcpyDeviceToHost, stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(stream);
+  if (e != hipSuccess) return ctx->hip_fail(e, "exchange D2H");
+  if (comm->fn(comm->user, comm->hbuf, n) != 0) return fail(DCC_ECOMM, "exchange callback failed");
+  e = hipMemcpyAsync(dev, comm->hbuf, n, hipMemcpyHostToDevice, stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(stream);  // hbuf is reused by the next call
+  if (e != hipSuccess) return ctx->hip_fail(e, "exchange H2D");
+  return DCC_OK;
+}
+
+extern "C" int dcc_comm_unique_id(void* out_id) {
+  if (!out_id) return DCC_EINVAL;
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return DCC_ECOMM;
+  memcpy(out_id, &id, sizeof id);
+  return DCC_OK;
+}
+
+static int comm_check(dcc_ctx* ctx, int rank, int nranks) {
+  if (!ctx || nranks < 1 || rank < 0 || rank >= nranks) return DCC_EINVAL;
+  if (ctx->comm) return ctx->fail(DCC_EINVAL, "communicator already initialised");
+  return DCC_OK;
+}
+
+extern "C" int dcc_comm_init(dcc_ctx* ctx, int rank, int nranks, const void* unique_id) {
+  int r = comm_check(ctx, rank, nranks);
+  if (r) return r;
+  if (!unique_id) return DCC_EINVAL;
+  if (hipSetDevice(ctx->device) != hipSuccess) return DCC_ENODEV;
+  auto* c = new dcc_comm_state;
+  c->rank = rank;
+  c->nranks = nranks;
+  if (nranks > 1) {
+    ncclUniqueId id;
+    memcpy(&id, unique_id, sizeof id);
+    const ncclResult_t e = ncclCommInitRank(&c->nccl, nranks, id, rank);
+    if (e != ncclSuccess) {
+      delete c;
+      return ctx->fail(DCC_ECOMM, "ncclCommInitRank: %s", ncclGetErrorString(e));
+    }
+  }
+  ctx->comm = c;
+  return DCC_OK;
+}
+
+extern "C" int dcc_comm_init_host(dcc_ctx* ctx, int rank, int nranks, dcc_exchange_fn fn,
+                                  void* user) {
+  int r = comm_check(ctx, rank, nranks);
+  if (r) return r;
+  if (!fn) return DCC_EINVAL;
+  auto* c = new dcc_comm_state;
+  c->rank = rank;
+  c->nranks = nranks;
+  c->fn = fn;
+  c->user = user;
+  ctx->comm = c;
+  return DCC_OK;
+}
+
 extern "C" int dcc_comm_destroy(dcc_ctx* ctx) {
   if (!ctx || !ctx->comm) return DCC_OK;
+  if (ctx->comm->nccl) (void)ncclCommDestroy(ctx->comm->nccl);
+  if (ctx->comm->hbuf) (void)hipHostFree(ctx->comm->hbuf);
   delete ctx->comm;
   ctx->comm = nullptr;
   return DCC_OK;
 }
-int dcc_ctx::occ_epoch_sharded(const dcc_batch*, uint8_t*, uint64_t*, dcc_stats*) {
-  return fail(DCC_ENOTSUP, "sharded OCC not built yet");
-}
+
+extern "C" int dcc_comm_rank(const dcc_ctx* ctx) { return ctx && ctx->comm ? ctx->comm->rank : 0; }
+extern "C" int dcc_comm_size(const dcc_ctx* ctx) { return ctx && ctx->comm ? ctx->comm->nranks : 1; }

@@ -54,6 +54,7 @@ struct dcc_ctx {
   DevBuf table;                                  // Slot[cap]
   DevBuf state, hasw, rc, stat;                  // per-txn bytes
   DevBuf cflag, bsum, tn;                        // commit-tn scan
+  DevBuf gst;                                    // sharded per-txn status
   DevBuf l_tid[2], l_coff[2], l_cent[2];         // ping-pong undecided lists
   DevBuf hkeys, hoff, htn;                       // history CSR
   DevBuf perm, calvin_a, calvin_b, calvin_c, calvin_d;  // Calvin workspaces
@@ -68,6 +69,7 @@ struct dcc_ctx {
 
   dcc_comm_state* comm = nullptr;
   int comm_ranks() const;
+  int comm_allreduce_max_u8(uint8_t* dev, uint64_t n);  // in place, on `stream`
 
   int fail(int code, const char* fmt, ...);
   int hip_fail(hipError_t e, const char* what);
@@ -81,7 +83,6 @@ struct dcc_ctx {
   int device_prep(const DevBatch& d, uint32_t& maxlen, uint64_t& nnz_w);
   int read_partials(size_t bytes);
   int occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dcc_stats* st);
-  int occ_epoch_sharded(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dcc_stats* st);
   int calvin_epoch(const dcc_batch* b, uint32_t* out_group, uint8_t* out_rc, uint32_t* out_wave,
                    dcc_stats* st);
 };

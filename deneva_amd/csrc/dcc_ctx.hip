@@ -177,7 +177,7 @@ std::vector<DevBuf*> dcc_ctx::all_bufs() {
                             &order, &perm, &calvin_a, &calvin_b, &calvin_c, &calvin_d,
                             &cv_scratch, &cv_agg, &cv_group, &cv_wave, &cv_pgx, &cv_gsx,
                             &cv_gsize, &cv_done, &cv_maxl, &cv_seq_b, &cv_ok, &cv_len,
-                            &cv_off2, &cv_tsum};
+                            &cv_off2, &cv_tsum, &gst};
   for (int i = 0; i < 2; i++) {
     v.push_back(&l_tid[i]);
     v.push_back(&l_coff[i]);
@@ -318,6 +318,5 @@ extern "C" int dcc_occ_validate_epoch(dcc_ctx* ctx, const dcc_batch* batch, uint
                                       uint64_t* out_commit_tn, dcc_stats* out_stats) {
   if (!ctx) return DCC_EINVAL;
   if (hipSetDevice(ctx->device) != hipSuccess) return DCC_ENODEV;
-  if (ctx->comm_ranks() > 1) return ctx->occ_epoch_sharded(batch, out_rc, out_commit_tn, out_stats);
   return ctx->occ_epoch(batch, out_rc, out_commit_tn, out_stats);
 }

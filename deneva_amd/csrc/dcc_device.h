@@ -44,6 +44,7 @@ __host__ __device__ inline uint8_t st_abort(uint32_t round) { return (uint8_t)(2
 // per-access / per-txn probe status bits
 constexpr uint32_t PS_BLOCKED = 1;
 constexpr uint32_t PS_KILLED = 2;
+constexpr uint32_t PS_WRITE = 4;  // sharded rounds: the txn keeps a write entry here
 
 struct __attribute__((aligned(16))) Slot {
   uint64_t key;
@@ -162,21 +163,29 @@ __device__ inline uint64_t ballot64(bool p) { return __ballot(p); }
 __device__ inline uint32_t lane_id() { return __lane_id(); }
 
 // OR-reduce per contiguous segment of lanes.  `seg` is the segment id of the
-// lane (equal ids are contiguous); returns for HEAD lanes the OR of `bits`
-// over the segment (2 bits), 0 elsewhere, and sets is_head.
-__device__ inline uint32_t segment_or2(uint32_t seg, uint32_t bits, bool& is_head) {
+// lane (equal ids are contiguous); returns for HEAD lanes the OR of the low
+// NB bits of `bits` over the segment, 0 elsewhere, and sets is_head.
+template <int NB>
+__device__ inline uint32_t segment_or(uint32_t seg, uint32_t bits, bool& is_head) {
   const uint32_t lane = lane_id();
   const uint32_t prev = __shfl_up(seg, 1);
   is_head = (lane == 0) || (prev != seg);
   const uint64_t hm = ballot64(is_head);
-  const uint64_t b0 = ballot64(bits & 1u);
-  const uint64_t b1 = ballot64(bits & 2u);
+  uint64_t b[NB];
+#pragma unroll
+  for (int q = 0; q < NB; q++) b[q] = ballot64(bits & (1u << q));
   if (!is_head) return 0;
   const uint64_t above = lane == 63 ? 0ull : (hm & ~((2ull << lane) - 1ull));
   const uint32_t end = above ? (uint32_t)__builtin_ctzll(above) : 64u;
   const uint64_t hi = end == 64 ? ~0ull : ((1ull << end) - 1ull);
   const uint64_t m = hi & ~((1ull << lane) - 1ull);
-  return ((b0 & m) ? 1u : 0u) | ((b1 & m) ? 2u : 0u);
+  uint32_t v = 0;
+#pragma unroll
+  for (int q = 0; q < NB; q++) v |= (b[q] & m) ? (1u << q) : 0u;
+  return v;
+}
+__device__ inline uint32_t segment_or2(uint32_t seg, uint32_t bits, bool& is_head) {
+  return segment_or<2>(seg, bits, is_head);
 }
 
 }  // namespace dcc

@@ -97,12 +97,14 @@ int dcc_ctx::device_prep(const DevBatch& d, uint32_t& maxlen, uint64_t& nnz_w) {
 
 int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dcc_stats* st) {
   dcc_ctx* ctx = this;
+  // key-sharded across ranks: this rank holds only its keys
+  const bool sh = comm_ranks() > 1;
   const auto t_wall0 = std::chrono::steady_clock::now();
   CR(check_batch(b));
   const bool dev_out = (b->flags & DCC_DEVICE_PTRS) != 0;
   dcc_stats S;
   memset(&S, 0, sizeof S);
-  S.n_shards = 1;
+  S.n_shards = (uint32_t)comm_ranks();
   if (b->n_txn == 0) {
     if (st) *st = S;
     return DCC_OK;
@@ -130,11 +132,18 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   uint32_t* kflag = (uint32_t*)((char*)misc.p + 64);                     // CTR_RING flags
   unsigned long long* ring = (unsigned long long*)((char*)misc.p + 512);  // CTR_RING x NSEG
   char* bars = (char*)misc.p + 512 + CTR_RING * NSEG * 8;                 // CTR_RING x 16 B
+  uint32_t* und = (uint32_t*)((char*)misc.p + 8192);                      // CTR_RING (sharded)
 
-  CK(hipMemsetAsync(misc.p, 0, 512 + CTR_RING * NSEG * 8 + CTR_RING * 16, stream));
+  CK(hipMemsetAsync(misc.p, 0, 8192 + CTR_RING * 4, stream));
   CK(hipMemsetAsync(one, 0x01, 1, stream));
   CK(hipMemsetAsync(table.p, 0xFF, cap * sizeof(Slot), stream));
   CK(hipMemsetAsync(state.p, 0, d.n, stream));
+  uint8_t* gstat = nullptr;
+  if (sh) {
+    CR(gst.ensure(this, d.n + 16, "shard status"));
+    gstat = (uint8_t*)gst.p;
+    CK(hipMemsetAsync(gstat, 0, d.n, stream));
+  }
 
   // ---- history window pre-pass (occ.cpp:160-180)
   if (d.start_tn && !hist.empty()) {
@@ -144,6 +153,8 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
                 (const uint64_t*)htn.p, (uint8_t*)state.p};
     launch_hist(ha, stream);
   }
+  // the history window is checked on each shard's keys: any shard's abort wins
+  if (sh && d.start_tn) CR(comm_allreduce_max_u8((uint8_t*)state.p, d.n));
 
   // ---- key-hash build: round-1 owners
   BuildArgs ba{d.n, tw_b, d.off, d.keys, d.acctype, tab, mask, (const uint8_t*)state.p,
@@ -151,6 +162,7 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   if (profiling) CK(hipEventRecord(pev[0], stream));
   launch_build(ba, (unsigned)n_cu * 16, stream);
   CK(hipGetLastError());
+  if (sh) CR(comm_allreduce_max_u8((uint8_t*)hasw.p, d.n));  // read-only is a global property
   if (profiling) CK(hipEventRecord(pev[1], stream));
 
   // ---- fixed-point rounds.  Round k (0-based) reads its list size from the
@@ -181,7 +193,8 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
         PubArgs pa;
         pa.m_in = prev;
         pa.tw = tw;
-        pa.kill_flag = &kflag[(k - 1) % CTR_RING];
+        // sharded: always run (committed writers publish their tag-0 words here)
+        pa.kill_flag = sh ? one : &kflag[(k - 1) % CTR_RING];
         pa.force = 0;
         pa.state = (const uint8_t*)state.p;
         if (rt > MAX_ROUND_TAG) {
@@ -226,23 +239,33 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
       ra.kill_flag = &kflag[k % CTR_RING];
       ra.kill_zero = &kflag[(k + 1) % CTR_RING];
       // m_bound bounds this round's list (lists only shrink)
-      const bool recheck = !first && m_bound <= recheck_max;
+      const bool recheck = !sh && !first && m_bound <= recheck_max;
       ra.bar = recheck ? (GridBar*)(bars + (k % CTR_RING) * 16) : nullptr;
       ra.bar_zero = (uint32_t*)(bars + ((k + 1) % CTR_RING) * 16);
+      ra.gst = gstat;
       ra.err = err;
       launch_round(ra, first, m_bound, recheck ? resident_grid : max_grid, stream);
+      if (sh) {
+        CR(comm_allreduce_max_u8(gstat, d.n));
+        launch_decide((uint8_t*)state.p, gstat, d.n, st_abort(k + 1), &und[k % CTR_RING],
+                      &und[(k + 1) % CTR_RING], stream);
+      }
       if (profiling && first) CK(hipEventRecord(pev[2], stream));
       cur ^= 1;
       rt++;
     }
     CK(hipGetLastError());
     CK(hipMemcpyAsync(hmisc, ring, CTR_RING * NSEG * 8, hipMemcpyDeviceToHost, stream));
+    if (sh) CK(hipMemcpyAsync((char*)hmisc + 8192, und, CTR_RING * 4, hipMemcpyDeviceToHost, stream));
     CK(hipStreamSynchronize(stream));
     const unsigned long long* hr = (const unsigned long long*)hmisc;
+    const uint32_t* hu = (const uint32_t*)((const char*)hmisc + 8192);
     for (uint32_t q = k0; q < k; q++) {
       uint64_t mq = 0;
       for (uint32_t g = 0; g < NSEG; g++) mq += hr[(q % CTR_RING) * NSEG + g] >> CTR_E_BITS;
-      if (mq == 0) {
+      // sharded: the local list can empty while other shards still decide;
+      // the all-reduced undecided count (equal on every rank) ends the loop
+      if (sh ? hu[q % CTR_RING] == 0 : mq == 0) {
         rounds = q + 1;
         done = true;
         break;

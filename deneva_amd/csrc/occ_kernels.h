@@ -96,6 +96,7 @@ struct RoundArgs {
   uint32_t* kill_zero;           // next round's flag, zeroed here
   GridBar* bar;                  // grid barrier words (recheck enabled) or null
   uint32_t* bar_zero;            // next round's barrier words, zeroed here
+  uint8_t* gst;                  // sharded: per-txn local status out (1 blocked, 2 killed)
   uint32_t* err;
 };
 
@@ -133,6 +134,10 @@ void launch_round(const RoundArgs& a, bool from_keys, uint64_t m_bound, unsigned
 void launch_retag(Slot* tab, uint64_t cap, hipStream_t st);
 void launch_pub(const PubArgs& a, uint64_t m_bound, unsigned max_grid, hipStream_t st);
 void launch_final(const FinalArgs& a, hipStream_t st);
+// sharded rounds: apply the all-reduced status (0 commit, 1 stay, >=2 abort),
+// clear it for the next round, add the undecided count to *und.
+void launch_decide(uint8_t* state, uint8_t* gst, uint64_t n, uint8_t abort_byte, uint32_t* und,
+                   uint32_t* und_next, hipStream_t st);
 void launch_commit_tn(const uint32_t* cflag, uint64_t n, uint64_t* bsum, uint64_t tnc,
                       uint64_t* tn, hipStream_t st);
 

@@ -321,7 +321,13 @@ __global__ __launch_bounds__(WAVES * 64) void k_build(BuildArgs a) {
 //                 decided, never added) — kept only to publish owners
 // Per txn: killed -> Abort, clear -> Commit (+ tag-0 owner words), blocked ->
 // next list (entries that were blocked or are writes).
-template <bool FROM_KEYS, int CAP, int WAVES>
+//
+// SHARD (key-sharded across GPUs): the shard sees only its
+// keys, so it cannot decide.  It reports the txn's local status into gst
+// (killed dominates blocked), keeps every txn it did not kill in the next
+// list, and publishes nothing; the host all-reduces gst (MAX) and k_decide
+// applies the verdict, identical on every shard.
+template <bool FROM_KEYS, bool SHARD, int CAP, int WAVES>
 __global__ __launch_bounds__(WAVES * 64) void k_round(RoundArgs a) {
   __shared__ uint8_t s_map[WAVES][CAP];
   __shared__ uint64_t s_ent[WAVES][CAP];
@@ -461,7 +467,13 @@ __global__ __launch_bounds__(WAVES * 64) void k_round(RoundArgs a) {
           if (ps[u] & PS_BLOCKED) lo[u] |= ENT_BLOCK;
           if (x < T.A1) ent[x - T.A0] = ((uint64_t)blk[u] << 32) | lo[u];
           bool head;
-          const uint32_t v = segment_or2(lt[u], ps[u], head);
+          uint32_t v;
+          if (SHARD) {
+            const bool wk = (lo[u] & ENT_WRITE) && (lo[u] & ENT_SID) != SID_NONE;
+            v = segment_or<3>(lt[u], ps[u] | (wk ? PS_WRITE : 0u), head);
+          } else {
+            v = segment_or2(lt[u], ps[u], head);
+          }
           if (head && lt[u] != 0xFFu && v) atomicOr(&s_stat[wv][lt[u]], v);
         }
       }
@@ -472,8 +484,17 @@ __global__ __launch_bounds__(WAVES * 64) void k_round(RoundArgs a) {
     uint32_t dec = 0;  // 0 none, 1 commit, 2 abort, 3 blocked
     if (live && lane < T.nt && part) {
       const uint32_t st = s_stat[wv][lane];
-      dec = (st & PS_KILLED) ? 2u : (st & PS_BLOCKED) ? 3u : 1u;
-      if (dec != 3u) a.state[txn] = dec == 1u ? ST_COMMIT : cur_abort;
+      if (SHARD) {
+        // keep what can still matter here: a blocked txn (its blocked
+        // entries) or a clear one with a local write (its owner words); a
+        // clear read-only txn reports 0 on this shard from now on
+        dec = (st & PS_KILLED) ? 2u : (st & (PS_BLOCKED | PS_WRITE)) ? 3u : 0u;
+        const uint8_t v = (st & PS_KILLED) ? 2 : (st & PS_BLOCKED) ? 1 : 0;
+        if (v) a.gst[txn] = v;
+      } else {
+        dec = (st & PS_KILLED) ? 2u : (st & PS_BLOCKED) ? 3u : 1u;
+        if (dec != 3u) a.state[txn] = dec == 1u ? ST_COMMIT : cur_abort;
+      }
     }
     if (live) s_stat[wv][lane] = dec;
     __syncthreads();
@@ -611,6 +632,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_pub(PubArgs a) {
   __shared__ uint32_t s_txn[WAVES][64];
   __shared__ ListGeo G;
   __shared__ LdsMin<PUB_LDS> comb;
+  __shared__ uint8_t s_com[WAVES][64];
   if (*a.kill_flag == 0u) return;  // uniform: no aborts last round
   const uint32_t wv = threadIdx.x >> 6, lane = lane_id();
   uint8_t* map = s_map[wv];
@@ -627,8 +649,16 @@ __global__ __launch_bounds__(WAVES * 64) void k_pub(PubArgs a) {
     const uint32_t* tid_s = a.tid + sg * a.seg_ts;
     Tile T;
     uint32_t txn, s, e;
-    bool part = true;  // a txn aborted by the recheck publishes nothing
-    if (lane < a.tw && j0 + lane < m) part = a.state[tid_s[j0 + lane]] == ST_UNDECIDED;
+    // a txn aborted by the recheck publishes nothing; a txn committed by the
+    // last sharded decision (only sharded lists hold one) publishes its tag-0
+    // words, which an unsharded round does at commit time
+    bool part = true, com = false;
+    if (lane < a.tw && j0 + lane < m) {
+      const uint8_t st = a.state[tid_s[j0 + lane]];
+      part = st == ST_UNDECIDED || st == ST_COMMIT;
+      com = st == ST_COMMIT;
+    }
+    s_com[wv][lane] = com ? 1 : 0;
     const bool live = tile_open<CAP>(j0, a.tw, m, tid_s, a.coff + sg * a.seg_ts, G.end[sg], part,
                                      map, s_txn[wv], T, txn, s, e, a.err);
     __syncthreads();
@@ -652,9 +682,12 @@ __global__ __launch_bounds__(WAVES * 64) void k_pub(PubArgs a) {
 #pragma unroll
         for (int u = 0; u < ILP; u++) {
           const uint32_t lo = (uint32_t)en[u];
-          const bool cand = (lo & ENT_WRITE) && (a.force || ((lo & ENT_BLOCK) && bs[u] >= ST_ABORT));
+          const bool com = lt[u] != 0xFFu && s_com[wv][lt[u]];
+          const bool cand = (lo & ENT_WRITE) &&
+                            (com || a.force || ((lo & ENT_BLOCK) && bs[u] >= ST_ABORT));
           if (cand) {
-            const uint32_t sid = lo & ENT_SID, wd = tagw | s_txn[wv][lt[u]];
+            const uint32_t sid = lo & ENT_SID;
+            const uint32_t wd = (com ? 0u : tagw) | s_txn[wv][lt[u]];
             if (!comb.add(sid, wd)) own_min(&a.tab[sid].own, wd);
           }
         }
@@ -672,6 +705,34 @@ __global__ __launch_bounds__(256) void k_retag(Slot* __restrict__ tab, uint64_t 
   if (sidx >= cap) return;
   const uint32_t w = tab[sidx].own;
   if ((w >> IDX_BITS) != 0) tab[sidx].own = OWN_EMPTY;
+}
+
+// --------------------------------------------------------------------------
+// k_decide (sharded): 16 txns per thread step; one atomic per workgroup.
+constexpr unsigned DECIDE_BLOCKS = 128;
+__global__ __launch_bounds__(256) void k_decide(uint8_t* __restrict__ state,
+                                                uint8_t* __restrict__ gst, uint64_t n,
+                                                uint8_t abort_byte, uint32_t* __restrict__ und,
+                                                uint32_t* __restrict__ und_next) {
+  __shared__ uint32_t sh[4];
+  if (blockIdx.x == 0 && threadIdx.x == 0) *und_next = 0;
+  uint32_t cnt = 0;
+  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t t0 = tid * 16; t0 < n; t0 += stride * 16) {
+    const uint64_t t1 = t0 + 16 < n ? t0 + 16 : n;
+    for (uint64_t t = t0; t < t1; t++) {
+      const uint8_t s = state[t];
+      if (s != ST_UNDECIDED) continue;
+      const uint8_t g = gst[t];
+      if (g >= 2) state[t] = abort_byte;
+      else if (g == 0) state[t] = ST_COMMIT;
+      else cnt++;
+      gst[t] = 0;
+    }
+  }
+  const uint32_t tot = block_sum_u32(cnt, sh);
+  if (threadIdx.x == 0 && tot) atomicAdd(und, tot);
 }
 
 // --------------------------------------------------------------------------
@@ -767,8 +828,18 @@ void launch_build(const BuildArgs& a, unsigned max_grid, hipStream_t st) {
 void launch_round(const RoundArgs& a, bool from_keys, uint64_t m_bound, unsigned max_grid,
                   hipStream_t st) {
   const unsigned g = tile_grid(m_bound, a.tw, max_grid);
-  if (from_keys) k_round<true, ROUND_CAP, TILE_WAVES><<<g, TILE_WAVES * 64, 0, st>>>(a);
-  else k_round<false, ROUND_CAP, TILE_WAVES><<<g, TILE_WAVES * 64, 0, st>>>(a);
+  constexpr unsigned B = TILE_WAVES * 64;
+  if (a.gst) {
+    if (from_keys) k_round<true, true, ROUND_CAP, TILE_WAVES><<<g, B, 0, st>>>(a);
+    else k_round<false, true, ROUND_CAP, TILE_WAVES><<<g, B, 0, st>>>(a);
+  } else {
+    if (from_keys) k_round<true, false, ROUND_CAP, TILE_WAVES><<<g, B, 0, st>>>(a);
+    else k_round<false, false, ROUND_CAP, TILE_WAVES><<<g, B, 0, st>>>(a);
+  }
+}
+void launch_decide(uint8_t* state, uint8_t* gst, uint64_t n, uint8_t abort_byte, uint32_t* und,
+                   uint32_t* und_next, hipStream_t st) {
+  k_decide<<<DECIDE_BLOCKS, 256, 0, st>>>(state, gst, n, abort_byte, und, und_next);
 }
 void launch_retag(Slot* tab, uint64_t cap, hipStream_t st) {
   k_retag<<<grid_for(cap, 256), 256, 0, st>>>(tab, cap);

@@ -206,6 +206,31 @@ class Engine:
         buf = C.create_string_buffer(bytes(unique_id), _abi.UNIQUE_ID_BYTES)
         _check(lib.dcc_comm_init(self._h, rank, nranks, buf), self._h)
 
+    def comm_init_host(self, rank: int, nranks: int, allreduce_max) -> None:
+        """Shard this engine with a host-side exchange: ``allreduce_max(buf)``
+        must MAX-all-reduce the uint8 numpy array ``buf`` in place across the
+        ranks (e.g. torch.distributed over gloo)."""
+        def _cb(user, ptr, n):
+            try:
+                if n:
+                    allreduce_max(np.ctypeslib.as_array(ptr, shape=(int(n),)))
+                return 0
+            except Exception:  # noqa: BLE001 - reported as DCC_ECOMM by the engine
+                import traceback
+                traceback.print_exc()
+                return 1
+        self._exchange = _abi.EXCHANGE_FN(_cb)  # keep alive as long as the engine
+        _check(lib.dcc_comm_init_host(self._h, rank, nranks,
+                                      C.cast(self._exchange, C.c_void_p), None), self._h)
+
+    @property
+    def comm_rank(self) -> int:
+        return int(lib.dcc_comm_rank(self._h))
+
+    @property
+    def comm_size(self) -> int:
+        return int(lib.dcc_comm_size(self._h))
+
     def comm_destroy(self) -> None:
         _check(lib.dcc_comm_destroy(self._h), self._h)
 

@@ -138,8 +138,16 @@ int dcc_reserve(dcc_ctx* ctx, uint64_t max_txn, uint64_t max_nnz);
  * of 2PC's AND of per-node OK bits (worker_thread.cpp:328-334). */
 #define DCC_UNIQUE_ID_BYTES 128
 int dcc_comm_unique_id(void* out_id /* DCC_UNIQUE_ID_BYTES */);
+/* RCCL communicator: every rank passes rank 0's unique id. */
 int dcc_comm_init(dcc_ctx* ctx, int rank, int nranks, const void* unique_id);
+/* Host-exchange communicator: `fn` all-reduces n bytes in place with MAX
+ * across the ranks (returns 0 on success).  For harnesses whose ranks cannot
+ * form an RCCL clique, e.g. several ranks sharing one GPU in tests. */
+typedef int (*dcc_exchange_fn)(void* user, uint8_t* host_buf, uint64_t n);
+int dcc_comm_init_host(dcc_ctx* ctx, int rank, int nranks, dcc_exchange_fn fn, void* user);
 int dcc_comm_destroy(dcc_ctx* ctx);
+int dcc_comm_rank(const dcc_ctx* ctx);
+int dcc_comm_size(const dcc_ctx* ctx);
 uint32_t dcc_key_shard(uint64_t key, uint32_t nranks);
 /* Host helper: keep only the accesses of `rank` (same n_txn, same order).
  * out_offsets [n_txn+1]; out_keys/out_acctype sized >= in nnz; *out_nnz set. */
