@@ -39,6 +39,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=65536,
                     help="txns of the batch timed with the CPU reference restatement")
+    ap.add_argument("--exchange", choices=["rccl", "host"], default="rccl",
+                    help="N>1 status all-reduce: RCCL over xGMI (one GPU per rank), or "
+                         "host/gloo (rehearsal: ranks may share one GPU)")
     return ap.parse_args()
 
 
@@ -75,9 +78,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.exchange == "host":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.exchange == "rccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
 
     # same batch on every rank (deterministic generator); weak scaling: the
     # epoch grows with the GPU count, each GPU holds 1/N of the accesses
@@ -86,10 +94,16 @@ def main():
                        seed=args.seed)
     eng = d.Engine(local)
     if world > 1:
-        uid = d.comm_unique_id() if rank == 0 else bytes(d._abi.UNIQUE_ID_BYTES)
-        obj = [uid]
-        dist.broadcast_object_list(obj, src=0)
-        eng.comm_init(rank, world, obj[0])
+        if args.exchange == "rccl":
+            uid = d.comm_unique_id() if rank == 0 else bytes(d._abi.UNIQUE_ID_BYTES)
+            obj = [uid]
+            dist.broadcast_object_list(obj, src=0)
+            eng.comm_init(rank, world, obj[0])
+        else:
+            def allreduce_max(buf):
+                t = torch.from_numpy(buf)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            eng.comm_init_host(rank, world, allreduce_max)
         mine = d.shard_filter(batch, rank, world)
     else:
         mine = batch
@@ -113,7 +127,8 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([dt], device=f"cuda:{local}", dtype=torch.float64)
+        dev = f"cuda:{local}" if args.exchange == "rccl" else "cpu"
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
@@ -136,12 +151,12 @@ def main():
     # parity check of the measured decisions against the oracle (rank 0, N=1)
     parity = None
     cpu = None
-    if rank == 0 and world == 1:
+    if rank == 0:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
-        import _oracle as orc
+        import _oracle as orc  # checker only, outside the timed region
         erc, _, _ = orc.occ(batch)
         parity = bool(np.array_equal(out_rc.cpu().numpy(), erc))
-        if not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(batch, args.cpu_sample)
 
     if rank == 0:
@@ -173,7 +188,8 @@ def main():
                             f"50% WR tuples",
                 "global_batch": n_total,
                 "keys_per_txn": args.keys,
-                "parallelism": f"key-shard x{world}" if world > 1 else "single GPU",
+                "parallelism": (f"key-shard x{world} ({args.exchange} all-reduce)" if world > 1
+                                else "single GPU"),
             },
             "roofline": {
                 "bound": "hbm",
