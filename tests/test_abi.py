@@ -125,3 +125,48 @@ def test_shard_filter_partitions_accesses():
     cnt = sum(np.diff(p.offsets.astype(np.int64)) for p in parts)
     assert np.array_equal(cnt, np.diff(b.offsets.astype(np.int64)))
     assert d.key_shard(12345, 1) == 0
+
+
+def test_tpcc_generator_access_sets():
+    # Payment: WH (WR, WH_UPDATE) / DIST WR / CUST WR; NewOrder: WH RD, CUST RD,
+    # DIST WR, then ITEM RD + STOCK WR per order line (tpcc_txn.cpp:140-230)
+    b = d.gen_tpcc(n_txn=20000, num_wh=16)
+    tt = b.meta["txn_type"]
+    off = b.offsets.astype(np.int64)
+    L = np.diff(off)
+    assert set(np.unique(tt)) == {1, 2}
+    assert 0.45 < (tt == 1).mean() < 0.55                       # PERC_PAYMENT 0.5
+    assert (L[tt == 1] == 3).all()
+    assert L[tt == 2].min() >= 3 + 2 * 5 and L[tt == 2].max() <= 3 + 2 * 15  # ol_cnt in [5,15]
+    tbl = (b.keys >> np.uint64(56)).astype(np.int64)
+    low = b.keys & np.uint64((1 << 56) - 1)
+    for t in np.nonzero(tt == 1)[0][:300]:
+        s = off[t]
+        assert list(tbl[s:s + 3]) == [0, 1, 2] and list(b.acctype[s:s + 3]) == [d.WR] * 3
+        assert 1 <= low[s] <= 16
+    for t in np.nonzero(tt == 2)[0][:300]:
+        s, e = off[t], off[t + 1]
+        assert list(tbl[s:s + 3]) == [0, 2, 1]
+        assert list(b.acctype[s:s + 3]) == [d.RD, d.RD, d.WR]
+        assert (tbl[s + 3:e:2] == 7).all() and (tbl[s + 4:e:2] == 8).all()
+        assert (b.acctype[s + 3:e:2] == d.RD).all() and (b.acctype[s + 4:e:2] == d.WR).all()
+        items = low[s + 3:e:2]
+        assert len(np.unique(items)) == len(items)               # distinct ol_i_id
+        assert items.min() >= 1 and items.max() <= 100000
+        w = int(low[s])
+        # district key = w * DIST_PER_WH + d (tpcc_helper.cpp:19-21)
+        assert w * 10 + 1 <= int(low[s + 2]) <= w * 10 + 10
+    b2 = d.gen_tpcc(n_txn=4096, num_wh=4, wh_update=0)
+    pay = b2.meta["txn_type"] == 1
+    assert (b2.acctype[b2.offsets[:-1][pay]] == d.RD).all()      # WH_UPDATE false -> RD
+
+
+def test_tpcc_generator_golden_digest_and_threads():
+    import hashlib
+    b = d.gen_tpcc(n_txn=4096, seed=0xD3E7A003)
+    h = hashlib.sha256(b.offsets.tobytes() + b.keys.tobytes() + b.acctype.tobytes()).hexdigest()
+    golden = open(os.path.join(ROOT, "tests", "golden", "tpcc_4096_seed_D3E7A003.sha256")).read()
+    assert h == golden.strip()
+    b1 = d.gen_tpcc(n_txn=150000, chunk_txns=4096, n_threads=1)
+    b8 = d.gen_tpcc(n_txn=150000, chunk_txns=4096, n_threads=8)
+    assert np.array_equal(b1.keys, b8.keys) and np.array_equal(b1.offsets, b8.offsets)

@@ -150,3 +150,10 @@ def test_repeat_deterministic(engine):
     g1, rc1, _ = run(engine, b, waves=False)
     g2, rc2, _, _ = engine.calvin_order_epoch(b, want_group=True, want_wave=False)
     assert np.array_equal(np.asarray(g2), g1) and np.array_equal(np.asarray(rc2), rc1)
+
+
+@pytest.mark.parametrize("num_wh", [128, 4])
+def test_tpcc_calvin(engine, num_wh):
+    # canonical TPC-C keys: table id in the top byte, packed to the bits that vary
+    b = d.gen_tpcc(n_txn=50000 if num_wh == 4 else 262144, num_wh=num_wh)
+    run(engine, b, waves=num_wh == 4)

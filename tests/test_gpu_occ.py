@@ -201,3 +201,10 @@ def test_errors(engine):
     assert e.value.code == -22
     # the engine stays usable after errors
     run(engine, make_batch([[(1, WR)], [(1, RD)]]))
+
+
+@pytest.mark.parametrize("num_wh,wh_update", [(128, 1), (4, 1), (16, 0)])
+def test_tpcc_parity(engine, num_wh, wh_update):
+    # C3: TPC-C NewOrder + Payment, 262,144-txn batch at 128 warehouses
+    n = 262144 if num_wh == 128 else 50000
+    run(engine, d.gen_tpcc(n_txn=n, num_wh=num_wh, wh_update=wh_update))
