@@ -39,6 +39,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=65536,
                     help="txns of the batch timed with the CPU reference restatement")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the other BASELINE configs (C2, C3, C4, C5) at N=1")
     ap.add_argument("--exchange", choices=["rccl", "host"], default="rccl",
                     help="N>1 status all-reduce: RCCL over xGMI (one GPU per rank), or "
                          "host/gloo (rehearsal: ranks may share one GPU)")
@@ -64,6 +66,77 @@ def cpu_baseline(batch, sample: int):
     return {"value": n / dt, "unit": "txns/s", "cores": 1, "kind": "port",
             "sample": f"first {n} txns of the bench batch, literal OptCC epoch replay "
                       f"(oracle/occ_ref.c), {dt:.2f} s, 1 thread"}
+
+
+def c4_order(b):
+    """Sequencer order (origin = home partition, FIFO within the origin):
+    sched_dequeue's (epoch, origin, FIFO) order (work_queue.cpp:105-151)."""
+    home = b.meta["home"].astype(np.uint64)
+    seq = np.zeros(b.n_txn, np.uint64)
+    for h in np.unique(home):
+        idx = np.nonzero(home == h)[0]
+        seq[idx] = np.arange(idx.size, dtype=np.uint64)
+    return (home << np.uint64(32)) | seq
+
+
+def secondary_configs(eng, local, steps=10, warmup=3):
+    """The other BASELINE.json configs on one GPU (each its own workload;
+    inputs resident, decisions checked against the oracle outside the timing)."""
+    import torch
+    import deneva_amd as d
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle as orc  # checker only
+    dev = f"cuda:{local}"
+    out = {}
+
+    def timed(fn):
+        for _ in range(warmup):
+            fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        st = [fn() for _ in range(steps)]
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / steps, st[-1]
+
+    occ_cfgs = [
+        ("C2", "YCSB OCC, 65,536 txns x 16 keys, theta=0.9",
+         lambda: d.gen_ycsb(n_txn=65536, zipf_theta=0.9)),
+        ("C3", "TPC-C NewOrder+Payment OCC, 128 warehouses, 262,144 txns",
+         lambda: d.gen_tpcc(n_txn=262144, num_wh=128)),
+        ("C5", "YCSB OCC, 1,048,576 txns x 16 keys, theta=0.99",
+         lambda: d.gen_ycsb(n_txn=1 << 20, zipf_theta=0.99, seed=0xD3E7A002)),
+    ]
+    for tag, desc, gen in occ_cfgs:
+        b = gen()
+        db = b.to_torch(dev)
+        rc = torch.empty(b.n_txn, dtype=torch.uint8, device=dev)
+        dt, st = timed(lambda: eng.occ_validate_epoch(db, out_rc=rc)[2])
+        erc, _, _ = orc.occ(b)
+        out[tag] = {"workload": desc, "txns_per_s": b.n_txn / dt, "ms_per_epoch": dt * 1e3,
+                    "device_ms": st["device_ms"], "rounds": int(st["rounds"]),
+                    "commits": int(st["n_commit"]),
+                    "parity_vs_oracle": bool(np.array_equal(rc.cpu().numpy(), erc))}
+    # C4: Calvin lock ordering, 16 partitions, 1M txns, sequencer order
+    b = d.gen_ycsb(n_txn=1 << 20, zipf_theta=0.9, part_cnt=16, chunk_txns=65536, want_home=True)
+    b.order = c4_order(b)
+    db = b.to_torch(dev)
+    res = {}
+
+    def cv():
+        g, rc, _, st = eng.calvin_order_epoch(db, want_group=True)
+        res["g"], res["rc"] = g, rc
+        return st
+    dt, st = timed(cv)
+    eg, erc, _ = orc.calvin(b)
+    par = bool(np.array_equal(res["g"].cpu().numpy().astype(np.uint32)[:b.nnz], eg) and
+               np.array_equal(res["rc"].cpu().numpy()[:b.n_txn], erc))
+    out["C4"] = {"workload": "Calvin lock ordering, YCSB theta=0.9, 16 partitions, "
+                             "1,048,576 txns x 16 keys, sequencer (origin, FIFO) order",
+                 "txns_per_s": b.n_txn / dt, "ms_per_epoch": dt * 1e3,
+                 "device_ms": st["device_ms"], "ready_at_acquire": int(st["n_commit"]),
+                 "alg_GBps": st["alg_bytes"] / (st["device_ms"] * 1e-3) / 1e9,
+                 "parity_vs_oracle": par}
+    return out
 
 
 def main():
@@ -158,6 +231,9 @@ def main():
         parity = bool(np.array_equal(out_rc.cpu().numpy(), erc))
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(batch, args.cpu_sample)
+    secondary = None
+    if world == 1 and not args.no_secondary:
+        secondary = secondary_configs(eng, local)
 
     if rank == 0:
         traffic = None
@@ -214,6 +290,7 @@ def main():
                 "parity_vs_oracle": parity,
             },
             "cpu_baseline": cpu,
+            "other_configs": secondary,
         }
         print(json.dumps(line), flush=True)
     eng.close()

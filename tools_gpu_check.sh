@@ -11,7 +11,7 @@ timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.lo
  && timeout -k 10 400 python bench.py --steps 20 --warmup 3 > gpurun_out/bench.log 2>&1 \
  && (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats \
       --output-format csv -d "$R/gpurun_out/prof" -o run -- python "$R/bench.py" --steps 5 \
-      --warmup 1 --no-cpu-baseline > "$R/gpurun_out/prof.log" 2>&1)
+      --warmup 1 --no-cpu-baseline --no-secondary > "$R/gpurun_out/prof.log" 2>&1)
 rc=$?
 echo "session exit $rc"
 tail -3 gpurun_out/pytest_gpu.log; tail -2 gpurun_out/smoke.log; tail -1 gpurun_out/bench.log
