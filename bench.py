@@ -41,6 +41,10 @@ def parse():
                     help="txns of the batch timed with the CPU reference restatement")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the other BASELINE configs (C2, C3, C4, C5) at N=1")
+    ap.add_argument("--peel", type=int, default=-1,
+                    help="OCC prefix peel: -1 auto (default), 0 off, >0 prefix length")
+    ap.add_argument("--solver", type=int, default=0,
+                    help="OCC (sub-)batch solver: 0 auto, 1 rounds, 2 asynchronous")
     ap.add_argument("--exchange", choices=["rccl", "host"], default="rccl",
                     help="N>1 status all-reduce: RCCL over xGMI (one GPU per rank), or "
                          "host/gloo (rehearsal: ranks may share one GPU)")
@@ -114,7 +118,8 @@ def secondary_configs(eng, local, steps=10, warmup=3):
         erc, _, _ = orc.occ(b)
         out[tag] = {"workload": desc, "txns_per_s": b.n_txn / dt, "ms_per_epoch": dt * 1e3,
                     "device_ms": st["device_ms"], "rounds": int(st["rounds"]),
-                    "commits": int(st["n_commit"]),
+                    "commits": int(st["n_commit"]), "peel_prefix": int(st["peel_prefix"]),
+                    "survivors": int(st["n_survivors"]),
                     "parity_vs_oracle": bool(np.array_equal(rc.cpu().numpy(), erc))}
     # C4: Calvin lock ordering, 16 partitions, 1M txns, sequencer order
     b = d.gen_ycsb(n_txn=1 << 20, zipf_theta=0.9, part_cnt=16, chunk_txns=65536, want_home=True)
@@ -166,6 +171,8 @@ def main():
     batch = d.gen_ycsb(n_txn=n_total, zipf_theta=args.theta, req_per_query=args.keys,
                        seed=args.seed)
     eng = d.Engine(local)
+    eng.set_option(d._abi.OPT_PEEL, args.peel)
+    eng.set_option(d._abi.OPT_SOLVER, args.solver)
     if world > 1:
         if args.exchange == "rccl":
             uid = d.comm_unique_id() if rank == 0 else bytes(d._abi.UNIQUE_ID_BYTES)
@@ -211,8 +218,16 @@ def main():
     eng.set_profiling(False)
     ph_ms = np.mean([p["phase_ms"] for p in prof], axis=0)
     ph_bytes = prof[-1]["phase_bytes"]
-    dom = int(np.argmax(ph_ms[:2]))  # dominant single kernel: build or round-1 probe
-    dom_name = ["k_build (key-hash build)", "k_round<true> (round-1 probe)"][dom]
+    peeled = prof[-1]["peel_prefix"] > 0
+    if peeled:
+        # prefix peel: k_filter is the one kernel that streams the whole epoch
+        # (every offset, key and access type); the rest runs on the prefix and
+        # the few survivors
+        dom = 1
+        dom_name = "k_filter (committed-prefix filter pass)"
+    else:
+        dom = int(np.argmax(ph_ms[:2]))  # dominant single kernel: build or round-1 probe
+        dom_name = ["k_build (key-hash build)", "k_round<true> (round-1 probe)"][dom]
     achieved = ph_bytes[dom] / (ph_ms[dom] * 1e-3) / 1e9
 
     s0 = stats[-1]
@@ -241,7 +256,7 @@ def main():
         if os.path.exists(tf):
             try:
                 tj = json.load(open(tf))
-                key = f"{n_total}:{args.theta}:{args.keys}:{dom}"
+                key = f"{n_total}:{args.theta}:{args.keys}:{dom_name.split()[0]}"
                 traffic = tj.get(key)
             except Exception:
                 traffic = None
@@ -287,6 +302,11 @@ def main():
                 "commits": int(s0["n_commit"]),
                 "aborts": int(s0["n_abort"]),
                 "phase_ms": [float(x) for x in ph_ms],
+                "phases": (["prefix solve", "k_filter", "survivor compaction+solve",
+                            "prep+final"] if peeled else
+                           ["k_build", "round 1", "rounds>=2", "prep+final"]),
+                "peel_prefix": int(s0["peel_prefix"]),
+                "survivors": int(s0["n_survivors"]),
                 "parity_vs_oracle": parity,
             },
             "cpu_baseline": cpu,

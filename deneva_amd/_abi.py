@@ -33,6 +33,9 @@ UNIQUE_ID_BYTES = 128
 EXCHANGE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint8), C.c_uint64)
 OPT_RECHECK = 1
 OPT_BATCH_MAX = 2
+OPT_PEEL = 3
+OPT_PEEL_MIN = 4
+OPT_SOLVER = 5
 
 
 class Batch(C.Structure):
@@ -63,6 +66,8 @@ class Stats(C.Structure):
         ("total_ms", C.c_double),
         ("phase_ms", C.c_double * 4),
         ("phase_bytes", C.c_uint64 * 4),
+        ("peel_prefix", C.c_uint64),
+        ("n_survivors", C.c_uint64),
     ]
 
     def as_dict(self) -> dict:
@@ -113,6 +118,30 @@ class TpccParams(C.Structure):
     ]
 
 
+class FileInfo(C.Structure):
+    _fields_ = [
+        ("version", C.c_uint32),
+        ("kind", C.c_uint32),
+        ("sections", C.c_uint32),
+        ("reserved", C.c_uint32),
+        ("n_txn", C.c_uint64),
+        ("nnz", C.c_uint64),
+        ("seed", C.c_uint64),
+        ("epoch", C.c_uint64),
+        ("tnc_before", C.c_uint64),
+    ]
+
+
+FILE_OCC = 1
+FILE_CALVIN = 2
+FILE_HAS_TN = 0x1
+FILE_HAS_ORDER = 0x2
+FILE_HAS_RC = 0x4
+FILE_HAS_COMMIT_TN = 0x8
+FILE_HAS_GROUP = 0x10
+FILE_HAS_WAVE = 0x20
+
+
 # (name, restype, argtypes) for every entry point in include/dcc.h
 _P = C.c_void_p
 _SIGS = [
@@ -148,6 +177,10 @@ _SIGS = [
     ("dcc_gen_tpcc", C.c_int, [C.POINTER(TpccParams), _P, _P, _P, _P, C.POINTER(C.c_uint64)]),
     ("dcc_alg_bytes", C.c_uint64, [C.c_uint64, C.c_uint64, C.c_uint64]),
     ("dcc_calvin_alg_bytes", C.c_uint64, [C.c_uint64, C.c_uint64, C.c_int, C.c_int]),
+    ("dcc_file_write", C.c_int, [C.c_char_p, C.POINTER(FileInfo), C.POINTER(Batch), _P, _P, _P,
+                                 _P]),
+    ("dcc_file_read_info", C.c_int, [C.c_char_p, C.POINTER(FileInfo)]),
+    ("dcc_file_read", C.c_int, [C.c_char_p, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
 ]
 EXPORTED = [s[0] for s in _SIGS]
 

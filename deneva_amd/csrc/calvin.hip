@@ -556,7 +556,7 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, uint32_t* out_group, uint8_t* out_
   if (profiling) CK(hipEventRecord(pev[0], stream));
 
   // ---- prep: offsets/length validation + which key / order bits vary
-  launch_prep(d.off, d.n, d.acctype, d.nnz, (PrepPart*)part.p, stream);
+  launch_prep(d.off, d.n, d.acctype, d.nnz, 0, (PrepPart*)part.p, stream);
   CvPart* cvp = (CvPart*)((char*)part.p + 16384);
   k_cv_prep<<<CV_PREP_BLOCKS, 256, 0, stream>>>(d.keys, d.nnz, d.acctype, d.order, d.n, cvp);
   CK(hipGetLastError());

@@ -33,6 +33,26 @@ struct DevBatch {
 
 struct dcc_comm_state;  // RCCL communicator (dcc_comm.hip)
 
+// One OCC (sub-)batch: txn i has accesses [off[i], off[i+1]) of keys/acctype
+// and the state byte state[i]; nnz bounds off[n], w_bound its write count.
+struct SubProb {
+  uint64_t n = 0, nnz = 0, w_bound = 0;
+  const uint32_t* off = nullptr;
+  const uint64_t* keys = nullptr;
+  const uint8_t* acctype = nullptr;
+  uint8_t* state = nullptr;
+  uint8_t* hasw = nullptr;   // has-write bytes out
+  bool hasw_global = false;  // hasw is the epoch's (all-reduced when sharded)
+};
+struct PeelInfo {
+  uint64_t prefix = 0, survivors = 0;
+};
+// Dense survivor sub-batch of one peel level.
+struct SubBufs {
+  DevBuf tid, off, keys, acctype, state;
+};
+constexpr int PEEL_MAX_LEVEL = 3;
+
 struct dcc_ctx {
   int device = 0;
   int n_cu = 256;
@@ -42,6 +62,13 @@ struct dcc_ctx {
   bool profiling = false;
   uint64_t recheck_max = 16384;   // fold the kill wave into rounds with lists <= this
   uint32_t batch_max = 8;       // rounds enqueued between host synchronisations
+  int64_t peel_mode = -1;       // -1 auto prefix, 0 off, > 0 fixed prefix length
+  uint64_t peel_min = 32768;    // auto: peel (sub-)batches of at least this many txns
+  int solver = 0;               // 0 auto (async when unsharded), 1 rounds, 2 async
+  bool force_rounds = false;    // retry after an async-solver limit
+  uint32_t* async_passes_dev = nullptr;
+  uint64_t prefix_w_top = 0;    // write accesses in the top-level peel prefix
+  bool use_async() const { return !force_rounds && solver != 1 && comm_ranks() <= 1; }
   hipEvent_t pev[8] = {};  // phase boundary events (profiling only)
   std::string last_error;
   void* hmisc = nullptr;  // pinned host mirror of `misc`
@@ -55,6 +82,9 @@ struct dcc_ctx {
   DevBuf state, hasw, rc, stat;                  // per-txn bytes
   DevBuf cflag, bsum, tn;                        // commit-tn scan
   DevBuf gst;                                    // sharded per-txn status
+  DevBuf hasw_scr, cset_tab, cset_keys;          // prefix peel
+  DevBuf a_cnt, a_writers, a_big, a_st32;        // async solver
+  SubBufs subs[PEEL_MAX_LEVEL];
   DevBuf l_tid[2], l_coff[2], l_cent[2];         // ping-pong undecided lists
   DevBuf hkeys, hoff, htn;                       // history CSR
   DevBuf perm, calvin_a, calvin_b, calvin_c, calvin_d;  // Calvin workspaces
@@ -80,9 +110,14 @@ struct dcc_ctx {
   int upload_history();
   int check_batch(const dcc_batch* b);
   int stage_batch(const dcc_batch* b, DevBatch& d);
-  int device_prep(const DevBatch& d, uint32_t& maxlen, uint64_t& nnz_w);
+  int device_prep(const DevBatch& d, uint32_t& maxlen, uint64_t& nnz_w, uint64_t p = 0,
+                  uint64_t* nnz_w_prefix = nullptr);
   int read_partials(size_t bytes);
   int occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dcc_stats* st);
+  int occ_rounds(const SubProb& sp, uint32_t maxlen, bool prof, uint32_t& rounds);
+  int occ_async(const SubProb& sp, uint32_t maxlen, uint32_t& passes);
+  int occ_peel(const SubProb& sp, uint32_t maxlen, int level, uint32_t& rounds, PeelInfo& info);
+  uint64_t peel_prefix(uint64_t m, int level) const;
   int calvin_epoch(const dcc_batch* b, uint32_t* out_group, uint8_t* out_rc, uint32_t* out_wave,
                    dcc_stats* st);
 };

@@ -157,6 +157,18 @@ extern "C" int dcc_set_option(dcc_ctx* ctx, int option, int64_t value) {
       if (value < 0) return DCC_EINVAL;
       ctx->recheck_max = (uint64_t)value;
       return DCC_OK;
+    case DCC_OPT_PEEL:
+      if (value < -1) return DCC_EINVAL;
+      ctx->peel_mode = value;
+      return DCC_OK;
+    case DCC_OPT_PEEL_MIN:
+      if (value < 2) return DCC_EINVAL;
+      ctx->peel_min = (uint64_t)value;
+      return DCC_OK;
+    case DCC_OPT_SOLVER:
+      if (value < 0 || value > 2) return DCC_EINVAL;
+      ctx->solver = (int)value;
+      return DCC_OK;
     case DCC_OPT_BATCH_MAX:
       if (value < 1 || value > 32) return DCC_EINVAL;
       ctx->batch_max = (uint32_t)value;
@@ -177,7 +189,10 @@ std::vector<DevBuf*> dcc_ctx::all_bufs() {
                             &order, &perm, &calvin_a, &calvin_b, &calvin_c, &calvin_d,
                             &cv_scratch, &cv_agg, &cv_group, &cv_wave, &cv_pgx, &cv_gsx,
                             &cv_gsize, &cv_done, &cv_maxl, &cv_seq_b, &cv_ok, &cv_len,
-                            &cv_off2, &cv_tsum, &gst};
+                            &cv_off2, &cv_tsum, &gst, &hasw_scr, &cset_tab, &cset_keys,
+                            &a_cnt, &a_writers, &a_big, &a_st32};
+  for (auto& sb : subs)
+    for (DevBuf* b : {&sb.tid, &sb.off, &sb.keys, &sb.acctype, &sb.state}) v.push_back(b);
   for (int i = 0; i < 2; i++) {
     v.push_back(&l_tid[i]);
     v.push_back(&l_coff[i]);
@@ -190,6 +205,10 @@ extern "C" int dcc_reserve(dcc_ctx* ctx, uint64_t max_txn, uint64_t max_nnz) {
   if (!ctx) return DCC_EINVAL;
   (void)hipSetDevice(ctx->device);
   const uint32_t tw = ROUND_CAP / MAX_TXN_LEN;  // worst case: MAX_ROW_PER_TXN-long txns
+  int rc = ctx->state.ensure(ctx, max_txn + 16, "state");
+  if (!rc) rc = ctx->hasw.ensure(ctx, max_txn + 16, "hasw");
+  if (!rc) rc = ctx->rc.ensure(ctx, max_txn + 16, "rc");
+  if (rc) return rc;
   return ctx->reserve_occ(max_txn, max_nnz, max_nnz, tw);
 }
 

@@ -107,6 +107,19 @@ __device__ inline uint32_t table_insert(Slot* tab, uint32_t mask, uint64_t key) 
   return SID_NONE;  // table full: host sizing guarantees this never happens
 }
 
+// Find a key inserted by an earlier kernel (read-only probe).
+__device__ inline uint32_t table_find(const Slot* tab, uint32_t mask, uint64_t key) {
+  uint32_t h = slot_home(key, mask);
+  const uint32_t st = slot_step(key, mask);
+  for (uint32_t n = 0; n <= mask; n++) {
+    const uint64_t cur = tab[h].key;
+    if (cur == key) return h;
+    if (cur == KEY_EMPTY) return SID_NONE;
+    h = (h + st) & mask;
+  }
+  return SID_NONE;
+}
+
 // atomicMin with a read filter: hot keys see one real atomic per round instead
 // of one per writer.  A stale read can only be HIGHER than the true value
 // (owner words only decrease between resets), so skipping is always safe.

@@ -52,9 +52,6 @@ void dcc_ctx::list_geometry(uint64_t n, uint32_t tw, uint64_t& seg_ts, uint64_t&
 
 int dcc_ctx::reserve_occ(uint64_t n, uint64_t nnz, uint64_t nnz_w, uint32_t tw) {
   (void)nnz;
-  CR(state.ensure(this, n + 16, "state"));
-  CR(hasw.ensure(this, n + 16, "hasw"));
-  CR(rc.ensure(this, n + 16, "rc"));
   uint64_t ts, es;
   list_geometry(n, tw, ts, es);
   for (int i = 0; i < 2; i++) {
@@ -73,9 +70,10 @@ int dcc_ctx::read_partials(size_t bytes) {
 }
 
 // Offsets check + max length + write count on the device (one sync).
-int dcc_ctx::device_prep(const DevBatch& d, uint32_t& maxlen, uint64_t& nnz_w) {
+int dcc_ctx::device_prep(const DevBatch& d, uint32_t& maxlen, uint64_t& nnz_w, uint64_t p,
+                         uint64_t* nnz_w_prefix) {
   dcc_ctx* ctx = this;
-  launch_prep(d.off, d.n, d.acctype, d.nnz, (PrepPart*)part.p, stream);
+  launch_prep(d.off, d.n, d.acctype, d.nnz, p, (PrepPart*)part.p, stream);
   CK(hipGetLastError());
   CR(read_partials(PREP_BLOCKS * sizeof(PrepPart)));
   CK(hipStreamSynchronize(stream));
@@ -83,15 +81,357 @@ int dcc_ctx::device_prep(const DevBatch& d, uint32_t& maxlen, uint64_t& nnz_w) {
   uint32_t err = 0;
   maxlen = 0;
   nnz_w = 0;
+  uint64_t wp = 0;
   for (unsigned b = 0; b < PREP_BLOCKS; b++) {
     err |= pp[b].err;
     maxlen = std::max(maxlen, pp[b].maxlen);
     nnz_w += pp[b].nw;
+    wp += pp[b].nw_prefix;
   }
+  if (nnz_w_prefix) *nnz_w_prefix = wp;
   if (err & ERR_OFFSETS) return fail(DCC_EINVAL, "batch: malformed offsets");
   if (maxlen > MAX_TXN_LEN)
     return fail(DCC_ERANGE, "batch: a txn has %u accesses (> MAX_ROW_PER_TXN=%u)", maxlen,
                 MAX_TXN_LEN);
+  return DCC_OK;
+}
+
+// misc layout (bytes): [0] error word, [4] constant 1, [64..) kill flags
+// (CTR_RING), [512..) round counter ring (CTR_RING x NSEG), then grid barrier
+// words (CTR_RING x 16 B), [8192..) sharded undecided counts (CTR_RING),
+// [12288 + 16*level..) peel totals per level, [12800..) peel counters.
+static constexpr size_t MISC_KFLAG = 64, MISC_RING = 512,
+                        MISC_BARS = 512 + CTR_RING * NSEG * 8, MISC_UND = 8192,
+                        MISC_TOT = 12288, MISC_CCOUNT = 12800, MISC_ASYNC = 12928;
+
+// Prefix length of a peel over m txns (0 = solve directly with rounds).
+uint64_t dcc_ctx::peel_prefix(uint64_t m, int level) const {
+  if (peel_mode == 0 || level >= PEEL_MAX_LEVEL) return 0;
+  if (peel_mode > 0) return (uint64_t)peel_mode < m ? (uint64_t)peel_mode : 0;
+  if (m < peel_min) return 0;
+  uint64_t p = next_pow2(m / 64);
+  p = std::min<uint64_t>(std::max<uint64_t>(p, 1024), 65536);
+  return p < m ? p : 0;
+}
+
+// Build + fixed-point rounds for one (sub-)batch: txn i of the sub-batch has
+// accesses [off[i], off[i+1]) and state byte state[i]; only UNDECIDED txns
+// take part.  Rounds are enqueued in batches with one host synchronisation
+// per batch.
+int dcc_ctx::occ_rounds(const SubProb& sp, uint32_t maxlen, bool prof, uint32_t& rounds_out) {
+  dcc_ctx* ctx = this;
+  const bool sh = comm_ranks() > 1;
+  rounds_out = 0;
+  if (sp.n == 0) return DCC_OK;
+  // txns per wave: build tiles stage TILE_CAP accesses, round tiles ROUND_CAP
+  const uint32_t tw_b = std::min<uint32_t>(64, TILE_CAP / std::max<uint32_t>(1, maxlen));
+  const uint32_t tw = std::min<uint32_t>(64, ROUND_CAP / std::max<uint32_t>(1, maxlen));
+  CR(reserve_occ(sp.n, 0, sp.w_bound, tw));
+  const uint64_t cap = table_capacity(sp.w_bound);
+  if (cap > (1ull << 30)) return fail(DCC_ERANGE, "table capacity exceeds 2^30 slots");
+  const uint32_t mask = (uint32_t)(cap - 1);
+  uint64_t seg_ts, seg_es;
+  list_geometry(sp.n, tw, seg_ts, seg_es);
+  Slot* tab = (Slot*)table.p;
+  char* mb = (char*)misc.p;
+  uint32_t* err = (uint32_t*)mb;
+  uint32_t* one = (uint32_t*)mb + 1;
+  uint32_t* kflag = (uint32_t*)(mb + MISC_KFLAG);
+  unsigned long long* ring = (unsigned long long*)(mb + MISC_RING);
+  char* bars = mb + MISC_BARS;
+  uint32_t* und = (uint32_t*)(mb + MISC_UND);
+  CK(hipMemsetAsync(mb + MISC_KFLAG, 0, MISC_UND + CTR_RING * 4 - MISC_KFLAG, stream));
+  CK(hipMemsetAsync(table.p, 0xFF, cap * sizeof(Slot), stream));
+  uint8_t* gstat = nullptr;
+  if (sh) {
+    CR(gst.ensure(this, sp.n + 16, "shard status"));
+    gstat = (uint8_t*)gst.p;
+    CK(hipMemsetAsync(gstat, 0, sp.n, stream));
+  }
+
+  // ---- key-hash build: round-1 owners
+  BuildArgs ba{sp.n, tw_b, sp.off, sp.keys, sp.acctype, tab, mask, sp.state, sp.hasw, err};
+  if (prof) CK(hipEventRecord(pev[0], stream));
+  launch_build(ba, (unsigned)n_cu * 16, stream);
+  CK(hipGetLastError());
+  if (sh && sp.hasw_global) CR(comm_allreduce_max_u8(sp.hasw, sp.n));  // global property
+  if (prof) CK(hipEventRecord(pev[1], stream));
+
+  // ---- fixed-point rounds.  Round k (0-based) reads its list size from the
+  // NSEG counters ring[k-1] (device), reserves its output in ring[k] and
+  // zeroes ring[k+1]; k_pub republishes owner words before round k+1 only if
+  // round k aborted something.  The host enqueues rounds in batches and
+  // synchronises once per batch.
+  int cur = 0;
+  uint32_t rt = 1;  // round tag of the next round
+  uint32_t k = 0;   // rounds enqueued
+  uint64_t m_bound = sp.n;
+  uint32_t rounds = 0;
+  const unsigned max_grid = (unsigned)n_cu * 8;
+  // recheck (kill wave folded into the round) pays off on short lists where
+  // per-round fixed costs dominate.  Such rounds keep every workgroup
+  // resident for the grid barrier:
+  // k_round fits 5 workgroups of 4 waves per CU (LDS ~21 KB, <= 96 VGPRs);
+  // launch 4 per CU.
+  const unsigned resident_grid = (unsigned)n_cu * 4;
+  uint32_t batch = std::min<uint32_t>(sp.n > 65536 ? 2 : 4, batch_max);
+  bool done = false;
+  while (!done) {
+    const uint32_t k0 = k;
+    for (uint32_t q = 0; q < batch; q++, k++) {
+      const bool first = k == 0;
+      const unsigned long long* prev = first ? nullptr : &ring[((k - 1) % CTR_RING) * NSEG];
+      if (!first) {
+        PubArgs pa;
+        pa.m_in = prev;
+        pa.tw = tw;
+        // sharded: always run (committed writers publish their tag-0 words here)
+        pa.kill_flag = sh ? one : &kflag[(k - 1) % CTR_RING];
+        pa.force = 0;
+        pa.state = sp.state;
+        if (rt > MAX_ROUND_TAG) {
+          // tag space exhausted: drop stale owner words, every writer republishes
+          launch_retag(tab, cap, stream);
+          rt = 1;
+          pa.kill_flag = one;
+          pa.force = 1;
+        }
+        pa.r = rt;
+        pa.tid = (const uint32_t*)l_tid[cur].p;
+        pa.coff = (const uint32_t*)l_coff[cur].p;
+        pa.cent = (const uint64_t*)l_cent[cur].p;
+        pa.seg_ts = seg_ts;
+        pa.seg_es = seg_es;
+        pa.tab = tab;
+        pa.err = err;
+        launch_pub(pa, m_bound, (unsigned)n_cu * 2, stream);
+      }
+      RoundArgs ra;
+      ra.m_in = prev;
+      ra.m = sp.n;
+      ra.tw = tw;
+      ra.r = rt;
+      ra.k = k + 1;  // 1-based: abort round 0 is the history pre-pass
+      ra.end_total = 0;  // identity lists read off[m]; later lists carry counters
+      ra.tid = first ? nullptr : (const uint32_t*)l_tid[cur].p;
+      ra.coff = first ? sp.off : (const uint32_t*)l_coff[cur].p;
+      ra.keys = sp.keys;
+      ra.acctype = sp.acctype;
+      ra.cent = first ? nullptr : (const uint64_t*)l_cent[cur].p;
+      ra.seg_ts = seg_ts;
+      ra.seg_es = seg_es;
+      ra.tab = tab;
+      ra.mask = mask;
+      ra.state = sp.state;
+      ra.tid_out = (uint32_t*)l_tid[cur ^ 1].p;
+      ra.coff_out = (uint32_t*)l_coff[cur ^ 1].p;
+      ra.cent_out = (uint64_t*)l_cent[cur ^ 1].p;
+      ra.ctr = &ring[(k % CTR_RING) * NSEG];
+      ra.ctr_zero = &ring[((k + 1) % CTR_RING) * NSEG];
+      ra.kill_flag = &kflag[k % CTR_RING];
+      ra.kill_zero = &kflag[(k + 1) % CTR_RING];
+      // m_bound bounds this round's list (lists only shrink)
+      const bool recheck = !sh && !first && m_bound <= recheck_max;
+      ra.bar = recheck ? (GridBar*)(bars + (k % CTR_RING) * 16) : nullptr;
+      ra.bar_zero = (uint32_t*)(bars + ((k + 1) % CTR_RING) * 16);
+      ra.gst = gstat;
+      ra.err = err;
+      launch_round(ra, first, m_bound, recheck ? resident_grid : max_grid, stream);
+      if (sh) {
+        CR(comm_allreduce_max_u8(gstat, sp.n));
+        launch_decide(sp.state, gstat, sp.n, st_abort(k + 1), &und[k % CTR_RING],
+                      &und[(k + 1) % CTR_RING], stream);
+      }
+      if (prof && first) CK(hipEventRecord(pev[2], stream));
+      cur ^= 1;
+      rt++;
+    }
+    CK(hipGetLastError());
+    CK(hipMemcpyAsync(hmisc, ring, CTR_RING * NSEG * 8, hipMemcpyDeviceToHost, stream));
+    if (sh) CK(hipMemcpyAsync((char*)hmisc + MISC_UND, und, CTR_RING * 4, hipMemcpyDeviceToHost, stream));
+    CK(hipStreamSynchronize(stream));
+    const unsigned long long* hr = (const unsigned long long*)hmisc;
+    const uint32_t* hu = (const uint32_t*)((const char*)hmisc + MISC_UND);
+    for (uint32_t q = k0; q < k; q++) {
+      uint64_t mq = 0;
+      for (uint32_t g = 0; g < NSEG; g++) mq += hr[(q % CTR_RING) * NSEG + g] >> CTR_E_BITS;
+      // sharded: the local list can empty while other shards still decide;
+      // the all-reduced undecided count (equal on every rank) ends the loop
+      if (sh ? hu[q % CTR_RING] == 0 : mq == 0) {
+        rounds = q + 1;
+        done = true;
+        break;
+      }
+      m_bound = mq;
+    }
+    if (!done && k > sp.n + 2) return fail(DCC_EIO, "fixed point did not converge");
+    batch = std::min<uint32_t>(batch * 2, batch_max);
+  }
+  if (prof) CK(hipEventRecord(pev[4], stream));
+  rounds_out = rounds;
+  return DCC_OK;
+}
+
+// Asynchronous solver (occ_async.hip): per-key writer segments sorted by
+// txn, then chunked waves decide without rounds or host synchronisation.
+int dcc_ctx::occ_async(const SubProb& sp, uint32_t maxlen, uint32_t& passes_out) {
+  dcc_ctx* ctx = this;
+  passes_out = 0;
+  if (sp.n == 0) return DCC_OK;
+  const uint64_t cap = table_capacity(sp.w_bound);
+  if (cap > (1ull << 30)) return fail(DCC_ERANGE, "table capacity exceeds 2^30 slots");
+  CR(table.ensure(this, cap * sizeof(Slot), "table"));
+  CR(a_cnt.ensure(this, cap * 4 * 4, "async key arrays"));
+  CR(a_writers.ensure(this, std::max<uint64_t>(16, sp.w_bound * 4), "async writers"));
+  CR(a_big.ensure(this, std::max<uint64_t>(16, (sp.w_bound / ASORT_SMALL + 1) * 4), "async big"));
+  CR(a_st32.ensure(this, sp.n * 4 + 16, "async state"));
+  char* mb = (char*)misc.p;
+  uint32_t* cnt = (uint32_t*)a_cnt.p;
+  AsyncArgs a;
+  a.m = sp.n;
+  // small (sub-)batches: narrow tiles, so that every CU gets waves
+  const uint32_t len = std::max<uint32_t>(1, maxlen);
+  const uint64_t want = (sp.n + (uint64_t)n_cu * 16 - 1) / ((uint64_t)n_cu * 16);
+  a.tw_pre = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, ASYNC_CAP / len));
+  a.tw_pre = std::min<uint32_t>(a.tw_pre, 64);
+  a.tw = std::min<uint32_t>(std::max<uint32_t>(a.tw_pre, 4), ASYNC_KCAP / len);
+  a.tw = std::max<uint32_t>(1, std::min<uint32_t>(a.tw, 64));
+  a.off = sp.off;
+  a.keys = sp.keys;
+  a.acctype = sp.acctype;
+  a.state = sp.state;
+  a.st32 = (uint32_t*)a_st32.p;
+  a.tab = (Slot*)table.p;
+  a.mask = (uint32_t)(cap - 1);
+  a.wcnt = cnt;
+  a.wstart = cnt + cap;
+  a.wfill = cnt + 2 * cap;
+  a.cursor = cnt + 3 * cap;
+  a.writers = (uint32_t*)a_writers.p;
+  a.bump = (uint32_t*)(mb + MISC_ASYNC);
+  a.nbig = (uint32_t*)(mb + MISC_ASYNC + 4);
+  a.passes = (uint32_t*)(mb + MISC_ASYNC + 8);
+  a.ticket = (unsigned long long*)(mb + MISC_ASYNC + 16);
+  a.big = (uint32_t*)a_big.p;
+  a.err = (uint32_t*)mb;
+  a.hasw = sp.hasw;
+  launch_async(a, cap, (unsigned)n_cu, stream);
+  CK(hipGetLastError());
+  async_passes_dev = a.passes;
+  passes_out = 0;  // read back with the epoch's final synchronisation
+  return DCC_OK;
+}
+
+// Prefix peel (occ_peel.hip): solve [0, p) with rounds, kill every later txn
+// touching a committed prefix write key, compact the survivors into a dense
+// sub-batch (index order kept) and decide it, peeling again if it is large.
+int dcc_ctx::occ_peel(const SubProb& sp, uint32_t maxlen, int level, uint32_t& rounds_out,
+                      PeelInfo& info) {
+  dcc_ctx* ctx = this;
+  const bool sh = comm_ranks() > 1;
+  const uint64_t p = peel_prefix(sp.n, level);
+  if (p == 0) return use_async() ? occ_async(sp, maxlen, rounds_out)
+                                 : occ_rounds(sp, maxlen, false, rounds_out);
+  const bool top = level == 0;
+  char* mb = (char*)misc.p;
+  uint32_t* err = (uint32_t*)mb;
+
+  // ---- 1. the prefix, exactly
+  CR(hasw_scr.ensure(this, sp.n + 16, "hasw scratch"));
+  SubProb pre = sp;
+  pre.n = p;
+  pre.nnz = std::min<uint64_t>(sp.nnz, p * (uint64_t)maxlen);
+  pre.w_bound = top ? std::max<uint64_t>(1, prefix_w_top) : pre.nnz;
+  pre.hasw = (uint8_t*)hasw_scr.p;
+  pre.hasw_global = false;
+  if (top && profiling) CK(hipEventRecord(pev[0], stream));
+  uint32_t r_pre = 0;
+  if (use_async()) CR(occ_async(pre, maxlen, r_pre));
+  else CR(occ_rounds(pre, maxlen, false, r_pre));
+
+  // ---- 2. committed write keys of the prefix
+  const uint64_t gcap = std::max<uint64_t>(1024, next_pow2(2 * pre.w_bound + 1));
+  CR(cset_tab.ensure(this, gcap * 8, "cset table"));
+  CR(cset_keys.ensure(this, std::max<uint64_t>(8, pre.w_bound * 8), "cset keys"));
+  uint32_t* ccount = (uint32_t*)(mb + MISC_CCOUNT);
+  CK(hipMemsetAsync(cset_tab.p, 0xFF, gcap * 8, stream));
+  CK(hipMemsetAsync(ccount, 0, 4, stream));
+  const uint32_t twf = std::min<uint32_t>(64, FILTER_CAP / std::max<uint32_t>(1, maxlen));
+  CsetArgs ca{p, twf, sp.off, sp.keys, sp.acctype, sp.state, (uint64_t*)cset_tab.p,
+              (uint32_t)(gcap - 1), (uint64_t*)cset_keys.p, ccount};
+  launch_cset(ca, stream);
+
+  // ---- 3. filter [p, n): two workgroups per CU, each builds the LDS set once
+  const uint64_t step = (uint64_t)FILTER_WAVES * twf;
+  uint64_t grid = (sp.n + step - 1) / step;
+  grid = std::max<uint64_t>(1, std::min<uint64_t>(grid, std::min<uint64_t>(FILTER_MAX_GRID,
+                                                                          2 * (uint64_t)n_cu)));
+  const uint64_t per_blk = (sp.n + grid - 1) / grid;
+  uint8_t* kill = nullptr;
+  if (sh) {
+    CR(gst.ensure(this, sp.n + 16, "shard status"));
+    kill = (uint8_t*)gst.p;
+    CK(hipMemsetAsync(kill, 0, sp.n, stream));
+  }
+  SurvPart* sparts = (SurvPart*)part.p;
+  FilterArgs fa{p, sp.n, per_blk, twf, sp.off, sp.keys, sp.acctype,
+                (const uint64_t*)cset_keys.p, ccount, (const uint64_t*)cset_tab.p,
+                (uint32_t)(gcap - 1), sp.state, kill, top ? sp.hasw : (uint8_t*)hasw_scr.p,
+                sparts, err};
+  if (top && profiling) CK(hipEventRecord(pev[1], stream));
+  launch_filter(fa, (unsigned)grid, stream);
+  if (top && profiling) CK(hipEventRecord(pev[2], stream));
+  if (sh) {
+    CR(comm_allreduce_max_u8(kill, sp.n));  // a kill on any shard wins
+    launch_survivors(fa, (unsigned)grid, stream);
+    if (top) CR(comm_allreduce_max_u8(sp.hasw, sp.n));
+  }
+
+  // ---- 4. survivors -> dense sub-batch (index order)
+  SubBufs& sb = subs[level];
+  CR(sb.tid.ensure(this, sp.n * 4 + 16, "sub tid"));
+  CR(sb.off.ensure(this, (sp.n + 1) * 4 + 16, "sub offsets"));
+  CR(sb.keys.ensure(this, std::max<uint64_t>(8, sp.nnz * 8), "sub keys"));
+  CR(sb.acctype.ensure(this, std::max<uint64_t>(16, sp.nnz), "sub acctype"));
+  CR(sb.state.ensure(this, sp.n + 16, "sub state"));
+  uint32_t* tot = (uint32_t*)(mb + MISC_TOT + 16 * level);
+  launch_surv_scan(sparts, (uint32_t)grid, tot, (uint32_t*)sb.off.p, stream);
+  CompactArgs cp{p, sp.n, per_blk, sp.off, sp.keys, sp.acctype, sp.state, sparts,
+                 (uint32_t*)sb.tid.p, (uint32_t*)sb.off.p, (uint64_t*)sb.keys.p,
+                 (uint8_t*)sb.acctype.p};
+  launch_compact(cp, (unsigned)grid, stream);
+  CK(hipGetLastError());
+  CK(hipMemcpyAsync((char*)hmisc + MISC_TOT, tot, 12, hipMemcpyDeviceToHost, stream));
+  CK(hipStreamSynchronize(stream));
+  const uint32_t* ht = (const uint32_t*)((const char*)hmisc + MISC_TOT);
+  const uint64_t n_s = ht[0], nnz_s = ht[1], w_s = ht[2];
+  if (top) {
+    info.prefix = p;
+    info.survivors = n_s;
+  }
+
+  // ---- 5. decide the survivors, write their decisions back
+  uint32_t r_sub = 0;
+  if (n_s) {
+    CK(hipMemsetAsync(sb.state.p, 0, n_s, stream));
+    SubProb sub;
+    sub.n = n_s;
+    sub.nnz = nnz_s;
+    sub.off = (const uint32_t*)sb.off.p;
+    sub.keys = (const uint64_t*)sb.keys.p;
+    sub.acctype = (const uint8_t*)sb.acctype.p;
+    sub.state = (uint8_t*)sb.state.p;
+    sub.hasw = (uint8_t*)hasw_scr.p;
+    sub.hasw_global = false;
+    sub.w_bound = std::max<uint64_t>(1, w_s);
+    if (sh) sub.w_bound = std::max<uint64_t>(1, nnz_s);  // local write counts differ per shard
+    CR(occ_peel(sub, maxlen, level + 1, r_sub, info));
+    launch_scatter((const uint8_t*)sb.state.p, (const uint32_t*)sb.tid.p, tot, n_s, sp.state,
+                   stream);
+    CK(hipGetLastError());
+  }
+  if (top && profiling) CK(hipEventRecord(pev[3], stream));
+  rounds_out = r_pre + r_sub;
   return DCC_OK;
 }
 
@@ -116,34 +456,16 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   // ---- prep: validation, max length (tile width), write count (table size)
   uint32_t maxlen = 0;
   uint64_t nnz_w = 0;
-  CR(device_prep(d, maxlen, nnz_w));
-  // txns per wave: build tiles stage TILE_CAP accesses, round tiles ROUND_CAP
-  const uint32_t tw_b = std::min<uint32_t>(64, TILE_CAP / std::max<uint32_t>(1, maxlen));
-  const uint32_t tw = std::min<uint32_t>(64, ROUND_CAP / std::max<uint32_t>(1, maxlen));
-  CR(reserve_occ(d.n, d.nnz, nnz_w, tw));
-  const uint64_t cap = table_capacity(nnz_w);
-  if (cap > (1ull << 30)) return fail(DCC_ERANGE, "table capacity exceeds 2^30 slots");
-  const uint32_t mask = (uint32_t)(cap - 1);
-  uint64_t seg_ts, seg_es;
-  list_geometry(d.n, tw, seg_ts, seg_es);
-  Slot* tab = (Slot*)table.p;
-  uint32_t* err = (uint32_t*)misc.p;                                     // [0]
-  uint32_t* one = (uint32_t*)misc.p + 1;                                 // constant 1
-  uint32_t* kflag = (uint32_t*)((char*)misc.p + 64);                     // CTR_RING flags
-  unsigned long long* ring = (unsigned long long*)((char*)misc.p + 512);  // CTR_RING x NSEG
-  char* bars = (char*)misc.p + 512 + CTR_RING * NSEG * 8;                 // CTR_RING x 16 B
-  uint32_t* und = (uint32_t*)((char*)misc.p + 8192);                      // CTR_RING (sharded)
-
-  CK(hipMemsetAsync(misc.p, 0, 8192 + CTR_RING * 4, stream));
+  const uint64_t p0 = peel_prefix(d.n, 0);
+  CR(device_prep(d, maxlen, nnz_w, p0, &prefix_w_top));
+  CR(state.ensure(this, d.n + 16, "state"));
+  CR(hasw.ensure(this, d.n + 16, "hasw"));
+  CR(rc.ensure(this, d.n + 16, "rc"));
+  uint32_t* one = (uint32_t*)misc.p + 1;
+  CK(hipMemsetAsync(misc.p, 0, 64, stream));
+  CK(hipMemsetAsync((char*)misc.p + MISC_ASYNC + 8, 0, 4, stream));  // async pass count
   CK(hipMemsetAsync(one, 0x01, 1, stream));
-  CK(hipMemsetAsync(table.p, 0xFF, cap * sizeof(Slot), stream));
   CK(hipMemsetAsync(state.p, 0, d.n, stream));
-  uint8_t* gstat = nullptr;
-  if (sh) {
-    CR(gst.ensure(this, d.n + 16, "shard status"));
-    gstat = (uint8_t*)gst.p;
-    CK(hipMemsetAsync(gstat, 0, d.n, stream));
-  }
 
   // ---- history window pre-pass (occ.cpp:160-180)
   if (d.start_tn && !hist.empty()) {
@@ -156,126 +478,24 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   // the history window is checked on each shard's keys: any shard's abort wins
   if (sh && d.start_tn) CR(comm_allreduce_max_u8((uint8_t*)state.p, d.n));
 
-  // ---- key-hash build: round-1 owners
-  BuildArgs ba{d.n, tw_b, d.off, d.keys, d.acctype, tab, mask, (const uint8_t*)state.p,
-               (uint8_t*)hasw.p, err};
-  if (profiling) CK(hipEventRecord(pev[0], stream));
-  launch_build(ba, (unsigned)n_cu * 16, stream);
-  CK(hipGetLastError());
-  if (sh) CR(comm_allreduce_max_u8((uint8_t*)hasw.p, d.n));  // read-only is a global property
-  if (profiling) CK(hipEventRecord(pev[1], stream));
-
-  // ---- fixed-point rounds.  Round k (0-based) reads its list size from the
-  // NSEG counters ring[k-1] (device), reserves its output in ring[k] and
-  // zeroes ring[k+1]; k_pub republishes owner words before round k+1 only if
-  // round k aborted something.  The host enqueues rounds in batches and
-  // synchronises once per batch.
-  int cur = 0;
-  uint32_t rt = 1;  // round tag of the next round
-  uint32_t k = 0;   // rounds enqueued
-  uint64_t m_bound = d.n;
+  SubProb top;
+  top.n = d.n;
+  top.nnz = d.nnz;
+  top.off = d.off;
+  top.keys = d.keys;
+  top.acctype = d.acctype;
+  top.state = (uint8_t*)state.p;
+  top.hasw = (uint8_t*)hasw.p;
+  top.hasw_global = true;
+  top.w_bound = nnz_w;
   uint32_t rounds = 0;
-  const unsigned max_grid = (unsigned)n_cu * 8;
-  // recheck (kill wave folded into the round) pays off on short lists where
-  // per-round fixed costs dominate.  Such rounds keep every workgroup
-  // resident for the grid barrier:
-  // k_round fits 5 workgroups of 4 waves per CU (LDS ~21 KB, <= 96 VGPRs);
-  // launch 4 per CU.
-  const unsigned resident_grid = (unsigned)n_cu * 4;
-  uint32_t batch = std::min<uint32_t>(2, batch_max);
-  bool done = false;
-  while (!done) {
-    const uint32_t k0 = k;
-    for (uint32_t q = 0; q < batch; q++, k++) {
-      const bool first = k == 0;
-      const unsigned long long* prev = first ? nullptr : &ring[((k - 1) % CTR_RING) * NSEG];
-      if (!first) {
-        PubArgs pa;
-        pa.m_in = prev;
-        pa.tw = tw;
-        // sharded: always run (committed writers publish their tag-0 words here)
-        pa.kill_flag = sh ? one : &kflag[(k - 1) % CTR_RING];
-        pa.force = 0;
-        pa.state = (const uint8_t*)state.p;
-        if (rt > MAX_ROUND_TAG) {
-          // tag space exhausted: drop stale owner words, every writer republishes
-          launch_retag(tab, cap, stream);
-          rt = 1;
-          pa.kill_flag = one;
-          pa.force = 1;
-        }
-        pa.r = rt;
-        pa.tid = (const uint32_t*)l_tid[cur].p;
-        pa.coff = (const uint32_t*)l_coff[cur].p;
-        pa.cent = (const uint64_t*)l_cent[cur].p;
-        pa.seg_ts = seg_ts;
-        pa.seg_es = seg_es;
-        pa.tab = tab;
-        pa.err = err;
-        launch_pub(pa, m_bound, (unsigned)n_cu * 2, stream);
-      }
-      RoundArgs ra;
-      ra.m_in = prev;
-      ra.m = d.n;
-      ra.tw = tw;
-      ra.r = rt;
-      ra.k = k + 1;  // 1-based: abort round 0 is the history pre-pass
-      ra.end_total = (uint32_t)d.nnz;
-      ra.tid = first ? nullptr : (const uint32_t*)l_tid[cur].p;
-      ra.coff = first ? d.off : (const uint32_t*)l_coff[cur].p;
-      ra.keys = d.keys;
-      ra.acctype = d.acctype;
-      ra.cent = first ? nullptr : (const uint64_t*)l_cent[cur].p;
-      ra.seg_ts = seg_ts;
-      ra.seg_es = seg_es;
-      ra.tab = tab;
-      ra.mask = mask;
-      ra.state = (uint8_t*)state.p;
-      ra.tid_out = (uint32_t*)l_tid[cur ^ 1].p;
-      ra.coff_out = (uint32_t*)l_coff[cur ^ 1].p;
-      ra.cent_out = (uint64_t*)l_cent[cur ^ 1].p;
-      ra.ctr = &ring[(k % CTR_RING) * NSEG];
-      ra.ctr_zero = &ring[((k + 1) % CTR_RING) * NSEG];
-      ra.kill_flag = &kflag[k % CTR_RING];
-      ra.kill_zero = &kflag[(k + 1) % CTR_RING];
-      // m_bound bounds this round's list (lists only shrink)
-      const bool recheck = !sh && !first && m_bound <= recheck_max;
-      ra.bar = recheck ? (GridBar*)(bars + (k % CTR_RING) * 16) : nullptr;
-      ra.bar_zero = (uint32_t*)(bars + ((k + 1) % CTR_RING) * 16);
-      ra.gst = gstat;
-      ra.err = err;
-      launch_round(ra, first, m_bound, recheck ? resident_grid : max_grid, stream);
-      if (sh) {
-        CR(comm_allreduce_max_u8(gstat, d.n));
-        launch_decide((uint8_t*)state.p, gstat, d.n, st_abort(k + 1), &und[k % CTR_RING],
-                      &und[(k + 1) % CTR_RING], stream);
-      }
-      if (profiling && first) CK(hipEventRecord(pev[2], stream));
-      cur ^= 1;
-      rt++;
-    }
-    CK(hipGetLastError());
-    CK(hipMemcpyAsync(hmisc, ring, CTR_RING * NSEG * 8, hipMemcpyDeviceToHost, stream));
-    if (sh) CK(hipMemcpyAsync((char*)hmisc + 8192, und, CTR_RING * 4, hipMemcpyDeviceToHost, stream));
-    CK(hipStreamSynchronize(stream));
-    const unsigned long long* hr = (const unsigned long long*)hmisc;
-    const uint32_t* hu = (const uint32_t*)((const char*)hmisc + 8192);
-    for (uint32_t q = k0; q < k; q++) {
-      uint64_t mq = 0;
-      for (uint32_t g = 0; g < NSEG; g++) mq += hr[(q % CTR_RING) * NSEG + g] >> CTR_E_BITS;
-      // sharded: the local list can empty while other shards still decide;
-      // the all-reduced undecided count (equal on every rank) ends the loop
-      if (sh ? hu[q % CTR_RING] == 0 : mq == 0) {
-        rounds = q + 1;
-        done = true;
-        break;
-      }
-      m_bound = mq;
-    }
-    if (!done && k > d.n + 2) return fail(DCC_EIO, "fixed point did not converge");
-    batch = std::min<uint32_t>(batch * 2, batch_max);
-  }
-  if (profiling) CK(hipEventRecord(pev[4], stream));
+  PeelInfo info;
+  const bool peel = peel_prefix(d.n, 0) != 0;
+  async_passes_dev = nullptr;
+  if (peel) CR(occ_peel(top, maxlen, 0, rounds, info));
+  else if (use_async()) CR(occ_async(top, maxlen, rounds));
+  else CR(occ_rounds(top, maxlen, profiling, rounds));
+  if (profiling && !peel) CK(hipEventRecord(pev[3], stream));
 
   // ---- finalize: RC bytes, counts, central_finish tn numbering
   uint8_t* rc_dev = (dev_out && out_rc) ? out_rc : (uint8_t*)rc.p;
@@ -302,13 +522,25 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
     if (out_tn) CK(hipMemcpyAsync(out_tn, tn.p, d.n * 8, hipMemcpyDeviceToHost, stream));
   }
   CK(hipMemcpyAsync(hmisc, misc.p, 64, hipMemcpyDeviceToHost, stream));
+  if (async_passes_dev)
+    CK(hipMemcpyAsync((char*)hmisc + MISC_ASYNC, (char*)misc.p + MISC_ASYNC, 16,
+                      hipMemcpyDeviceToHost, stream));
   CR(read_partials(FINAL_BLOCKS * sizeof(FinalPart)));
   CK(hipStreamSynchronize(stream));
   const uint32_t e = *(const uint32_t*)hmisc;
+  if ((e & (ERR_SEG | ERR_ASYNC)) && !force_rounds) {
+    // a writer segment too long for the LDS sort, or the pass guard tripped:
+    // decide the epoch again with the round solver
+    force_rounds = true;
+    const int r2 = occ_epoch(b, out_rc, out_tn, st);
+    force_rounds = false;
+    return r2;
+  }
+  if (async_passes_dev) rounds += *(const uint32_t*)((const char*)hmisc + MISC_ASYNC + 8);
   {
     // barrier timeout words (third word of each GridBar in the ring)
     std::vector<uint32_t> bw(CTR_RING * 4);
-    CK(hipMemcpy(bw.data(), bars, CTR_RING * 16, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(bw.data(), (char*)misc.p + MISC_BARS, CTR_RING * 16, hipMemcpyDeviceToHost));
     for (uint32_t q = 0; q < CTR_RING; q++)
       if (bw[q * 4 + 2]) return fail(DCC_EIO, "grid barrier timed out (grid not co-resident)");
   }
@@ -335,21 +567,38 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   S.nnz_w = nnz_w;
   S.alg_bytes = dcc_alg_bytes(d.n, d.nnz, nnz_w);
   S.device_ms = ms;
+  S.peel_prefix = info.prefix;
+  S.n_survivors = info.survivors;
   if (profiling) {
     float t0 = 0, t1 = 0, t2 = 0;
-    CK(hipEventElapsedTime(&t0, pev[0], pev[1]));
-    CK(hipEventElapsedTime(&t1, pev[1], pev[2]));
-    CK(hipEventElapsedTime(&t2, pev[2], pev[4]));
+    if (peel) {
+      // phases: 0 = prefix solve + committed-key set, 1 = filter pass,
+      // 2 = compaction + survivor solve + scatter, 3 = prep + finalize
+      CK(hipEventElapsedTime(&t0, pev[0], pev[1]));
+      CK(hipEventElapsedTime(&t1, pev[1], pev[2]));
+      CK(hipEventElapsedTime(&t2, pev[2], pev[3]));
+    } else {
+      // phases: 0 = key-hash build, 1 = round 1, 2 = rounds >= 2, 3 = prep + finalize
+      CK(hipEventElapsedTime(&t0, pev[0], pev[1]));
+      CK(hipEventElapsedTime(&t1, pev[1], pev[2]));
+      CK(hipEventElapsedTime(&t2, pev[2], pev[4]));
+    }
     S.phase_ms[0] = t0;
     S.phase_ms[1] = t1;
     S.phase_ms[2] = t2;
     S.phase_ms[3] = ms - t0 - t1 - t2;
   }
-  // algorithmic bytes per phase: the build reads acctype of
-  // every access and the keys of writes, one 16-B slot update per write;
-  // round 1 reads offsets, keys + acctype, one 16-B slot per access, state.
-  S.phase_bytes[0] = d.nnz + 8 * nnz_w + 16 * nnz_w + 4 * (d.n + 1) + d.n;
-  S.phase_bytes[1] = 4 * (d.n + 1) + 9 * d.nnz + 16 * d.nnz + d.n;
+  if (peel) {
+    // the filter pass reads offsets, keys + acctype of every access and the
+    // state byte of every txn, and writes the has-write (and kill) bytes
+    S.phase_bytes[1] = 4 * (d.n + 1) + 9 * d.nnz + 2 * d.n;
+  } else {
+    // algorithmic bytes per phase: the build reads acctype of
+    // every access and the keys of writes, one 16-B slot update per write;
+    // round 1 reads offsets, keys + acctype, one 16-B slot per access, state.
+    S.phase_bytes[0] = d.nnz + 8 * nnz_w + 16 * nnz_w + 4 * (d.n + 1) + d.n;
+    S.phase_bytes[1] = 4 * (d.n + 1) + 9 * d.nnz + 16 * d.nnz + d.n;
+  }
 
   // central_finish (occ.cpp:283-286): committed non-read-only txns take
   // tn = tnc+1, tnc+2, ... in index order; their write sets join the history.

@@ -57,11 +57,13 @@ __device__ inline uint32_t block_max_u32(uint32_t v, uint32_t* sh) {
 
 __global__ __launch_bounds__(256) void k_prep(const uint32_t* __restrict__ off, uint64_t n,
                                               const uint8_t* __restrict__ at, uint64_t nnz,
-                                              PrepPart* __restrict__ part) {
+                                              uint64_t p, PrepPart* __restrict__ part) {
   __shared__ uint32_t sh[4];
-  uint32_t len = 0, bad = 0, nw = 0;
+  uint32_t len = 0, bad = 0, nw = 0, nwp = 0;
   const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  // writes inside the peel prefix [0, off[p]) size its key table
+  const uint64_t lim = (p && p <= n) ? off[p] : 0;
   for (uint64_t t = tid; t < n; t += stride) {
     const uint32_t a0 = off[t], b0 = off[t + 1];
     if (b0 < a0) bad |= ERR_OFFSETS;
@@ -74,16 +76,27 @@ __global__ __launch_bounds__(256) void k_prep(const uint32_t* __restrict__ off, 
     if (x + 16 <= nnz && ((uintptr_t)(at + x) & 15) == 0) {
       const uint4 v = *reinterpret_cast<const uint4*>(at + x);
       const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+      uint32_t c = 0, cp = 0;
       for (int q = 0; q < 4; q++)
-        for (int bb = 0; bb < 4; bb++) nw += ((w4[q] >> (8 * bb)) & 0xFFu) == 1u;
+        for (int bb = 0; bb < 4; bb++) {
+          const uint32_t is = ((w4[q] >> (8 * bb)) & 0xFFu) == 1u;
+          c += is;
+          cp += (x + 4 * q + bb < lim) ? is : 0u;
+        }
+      nw += c;
+      nwp += cp;
     } else {
-      for (uint64_t y = x; y < nnz && y < x + 16; y++) nw += at[y] == 1;
+      for (uint64_t y = x; y < nnz && y < x + 16; y++) {
+        nw += at[y] == 1;
+        nwp += (y < lim && at[y] == 1) ? 1u : 0u;
+      }
     }
   }
   const uint32_t tl = block_max_u32(len, sh);
   const uint32_t tb = block_max_u32(bad, sh);  // error bits are 0/1 flags: max == or here
   const uint32_t tw = block_sum_u32(nw, sh);
-  if (threadIdx.x == 0) part[blockIdx.x] = PrepPart{tb, tl, tw, 0};
+  const uint32_t tp = block_sum_u32(nwp, sh);
+  if (threadIdx.x == 0) part[blockIdx.x] = PrepPart{tb, tl, tw, tp};
 }
 
 // --------------------------------------------------------------------------
@@ -280,14 +293,17 @@ __global__ __launch_bounds__(WAVES * 64) void k_build(BuildArgs a) {
         uint32_t lt[ILP];
         bool w[ILP];
         uint64_t key[ILP];
+        // unconditional, clamped loads: branch-free code keeps every load of
+        // the step in flight (a conditional load gets its own vmcnt(0) wait)
 #pragma unroll
         for (int u = 0; u < ILP; u++) {
           const uint32_t x = base + 64 * u + lane;
+          const uint32_t xs = x < T.A1 ? x : T.A0;
           lt[u] = x < T.A1 ? map[x - T.A0] : 0xFFu;
-          w[u] = lt[u] != 0xFFu && a.acctype[x] == 1 /* WR */;
+          const uint8_t at = a.acctype[xs];
+          key[u] = a.keys[xs];
+          w[u] = lt[u] != 0xFFu && at == 1 /* WR */;
         }
-#pragma unroll
-        for (int u = 0; u < ILP; u++) key[u] = w[u] ? a.keys[base + 64 * u + lane] : 0;
 #pragma unroll
         for (int u = 0; u < ILP; u++) {
           if (w[u]) {
@@ -392,13 +408,16 @@ __global__ __launch_bounds__(WAVES * 64) void k_round(RoundArgs a) {
 #pragma unroll
           for (int u = 0; u < ILP; u++) {
             const uint32_t x = base + 64 * u + lane;
-            key[u] = lt[u] != 0xFFu ? a.keys[x] : KEY_EMPTY;
-            w[u] = lt[u] != 0xFFu && a.acctype[x] == 1 /* WR */;
+            const uint32_t xs = x < T.A1 ? x : T.A0;  // clamped: branch-free loads
+            const uint64_t k = a.keys[xs];
+            const uint8_t at = a.acctype[xs];
+            key[u] = lt[u] != 0xFFu ? k : KEY_EMPTY;
+            w[u] = lt[u] != 0xFFu && at == 1 /* WR */;
           }
 #pragma unroll
           for (int u = 0; u < ILP; u++) {
             h[u] = slot_home(key[u], a.mask);
-            if (lt[u] != 0xFFu) sv[u] = ld_slot(&a.tab[h[u]]);
+            sv[u] = ld_slot(&a.tab[h[u]]);  // unconditional: all probes in flight
           }
 #pragma unroll
           for (int u = 0; u < ILP; u++) {
@@ -426,14 +445,19 @@ __global__ __launch_bounds__(WAVES * 64) void k_round(RoundArgs a) {
         } else {
           uint64_t en[ILP];
           uint8_t bs[ILP];
+          // clamped, unconditional loads (branch-free: all in flight together)
 #pragma unroll
-          for (int u = 0; u < ILP; u++)
-            en[u] = lt[u] != 0xFFu ? cent_s[base + 64 * u + lane] : (uint64_t)SID_NONE;
+          for (int u = 0; u < ILP; u++) {
+            const uint32_t x = base + 64 * u + lane;
+            const uint64_t e = cent_s[x < T.A1 ? x : T.A0];
+            en[u] = lt[u] != 0xFFu ? e : (uint64_t)SID_NONE;
+          }
 #pragma unroll
           for (int u = 0; u < ILP; u++) {
             lo[u] = (uint32_t)en[u];
             blk[u] = (uint32_t)(en[u] >> 32);
-            bs[u] = (lo[u] & ENT_BLOCK) ? a.state[blk[u]] : ST_COMMIT;
+            const uint8_t b = a.state[(lo[u] & ENT_BLOCK) ? blk[u] : 0u];
+            bs[u] = (lo[u] & ENT_BLOCK) ? b : ST_COMMIT;
           }
           uint32_t ow[ILP];
           bool need[ILP];
@@ -443,7 +467,8 @@ __global__ __launch_bounds__(WAVES * 64) void k_round(RoundArgs a) {
             // the owner word (republished by k_pub since); an abort of this
             // round keeps blocking until the next one
             need[u] = (lo[u] & ENT_BLOCK) && bs[u] >= ST_ABORT && bs[u] != cur_abort;
-            ow[u] = need[u] ? a.tab[lo[u] & ENT_SID].own : OWN_EMPTY;
+            const uint32_t o = a.tab[need[u] ? (lo[u] & ENT_SID) : 0u].own;
+            ow[u] = need[u] ? o : OWN_EMPTY;
           }
 #pragma unroll
           for (int u = 0; u < ILP; u++) {
@@ -671,13 +696,15 @@ __global__ __launch_bounds__(WAVES * 64) void k_pub(PubArgs a) {
         for (int u = 0; u < ILP; u++) {
           const uint32_t x = base + 64 * u + lane;
           lt[u] = x < T.A1 ? map[x - T.A0] : 0xFFu;
-          en[u] = lt[u] != 0xFFu ? cent_s[x] : 0ull;
+          const uint64_t e = cent_s[x < T.A1 ? x : T.A0];  // clamped: branch-free
+          en[u] = lt[u] != 0xFFu ? e : 0ull;
         }
 #pragma unroll
         for (int u = 0; u < ILP; u++) {
           const uint32_t lo = (uint32_t)en[u];
           const bool wb = (lo & ENT_WRITE) && (lo & ENT_BLOCK) && !a.force;
-          bs[u] = wb ? a.state[(uint32_t)(en[u] >> 32)] : ST_UNDECIDED;
+          const uint8_t b = a.state[wb ? (uint32_t)(en[u] >> 32) : 0u];
+          bs[u] = wb ? b : ST_UNDECIDED;
         }
 #pragma unroll
         for (int u = 0; u < ILP; u++) {
@@ -809,9 +836,9 @@ __global__ __launch_bounds__(1024) void k_scan_apply(const uint32_t* __restrict_
 // host launchers (the templates stay private to this translation unit)
 static inline unsigned grid_for(uint64_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
 
-void launch_prep(const uint32_t* off, uint64_t n, const uint8_t* at, uint64_t nnz,
+void launch_prep(const uint32_t* off, uint64_t n, const uint8_t* at, uint64_t nnz, uint64_t p,
                  PrepPart* part, hipStream_t st) {
-  k_prep<<<PREP_BLOCKS, 256, 0, st>>>(off, n, at, nnz, part);
+  k_prep<<<PREP_BLOCKS, 256, 0, st>>>(off, n, at, nnz, p, part);
 }
 void launch_hist(const HistArgs& a, hipStream_t st) {
   k_hist<<<grid_for(a.n, 256), 256, 0, st>>>(a);

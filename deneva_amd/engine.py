@@ -319,3 +319,46 @@ def gen_tpcc(**kw) -> EpochBatch:
     meta = {"workload": "tpcc", "txn_type": tt[:n].copy(),
             **{f: getattr(p, f) for f, _ in p._fields_ if f != "reserved"}}
     return EpochBatch(off, keys[:w].copy(), at[:w].copy(), meta=meta)
+
+
+# ---------------------------------------------------------------- batch files
+def write_batch_file(path: str, batch: EpochBatch, kind: int = _abi.FILE_OCC, rc=None,
+                     commit_tn=None, group=None, wave=None, seed: int = 0, epoch: int = 0,
+                     tnc_before: int = 0) -> None:
+    """One epoch (and optionally its decisions) as a .dccb file (dcc_file_write)."""
+    info = _abi.FileInfo(kind=kind, seed=seed, epoch=epoch, tnc_before=tnc_before)
+
+    def c(a, dt):
+        return None if a is None else np.ascontiguousarray(a, dt)
+    host = EpochBatch(c(batch.offsets, np.uint32), c(batch.keys, np.uint64),
+                      c(batch.acctype, np.uint8), c(batch.start_tn, np.uint64),
+                      c(batch.finish_tn, np.uint64), c(batch.order, np.uint64))
+    arrs = [c(rc, np.uint8), c(commit_tn, np.uint64), c(group, np.uint32), c(wave, np.uint32)]
+    b = host.to_c()
+    _check(lib.dcc_file_write(path.encode(), C.byref(info), C.byref(b),
+                              *[_ptr(a) for a in arrs]))
+
+
+def read_batch_file(path: str):
+    """Returns (EpochBatch, info dict, decisions dict) of a .dccb file."""
+    info = _abi.FileInfo()
+    _check(lib.dcc_file_read_info(path.encode(), C.byref(info)))
+    n, nnz, sec = info.n_txn, info.nnz, info.sections
+    off = np.empty(n + 1, np.uint32)
+    keys = np.empty(max(nnz, 1), np.uint64)
+    at = np.empty(max(nnz, 1), np.uint8)
+    has = lambda bit: bool(sec & bit)  # noqa: E731
+    st = np.empty(max(n, 1), np.uint64) if has(_abi.FILE_HAS_TN) else None
+    ft = np.empty(max(n, 1), np.uint64) if has(_abi.FILE_HAS_TN) else None
+    od = np.empty(max(n, 1), np.uint64) if has(_abi.FILE_HAS_ORDER) else None
+    rc = np.empty(max(n, 1), np.uint8) if has(_abi.FILE_HAS_RC) else None
+    tn = np.empty(max(n, 1), np.uint64) if has(_abi.FILE_HAS_COMMIT_TN) else None
+    gr = np.empty(max(nnz, 1), np.uint32) if has(_abi.FILE_HAS_GROUP) else None
+    wv = np.empty(max(n, 1), np.uint32) if has(_abi.FILE_HAS_WAVE) else None
+    _check(lib.dcc_file_read(path.encode(), *[_ptr(a) for a in (off, keys, at, st, ft, od, rc,
+                                                                   tn, gr, wv)]))
+    cut = lambda a, k: None if a is None else a[:k]  # noqa: E731
+    b = EpochBatch(off, keys[:nnz], at[:nnz], cut(st, n), cut(ft, n), cut(od, n))
+    meta = {f: getattr(info, f) for f, _ in info._fields_ if f != "reserved"}
+    dec = {"rc": cut(rc, n), "commit_tn": cut(tn, n), "group": cut(gr, nnz), "wave": cut(wv, n)}
+    return b, meta, dec

@@ -100,10 +100,16 @@ typedef struct dcc_stats {
   /* Per-phase device time (HIP events on the engine stream; filled only when
    * profiling is enabled with dcc_set_profiling) and the algorithmic bytes
    * of each phase.  OCC phases: 0 = key-hash build, 1 = round-1 probe,
-   * 2 = rounds >= 2 (sum), 3 = prep + finalize.  Calvin: 0 = build,
+   * 2 = rounds >= 2 (sum), 3 = prep + finalize; with the prefix peel:
+   * 0 = prefix solve, 1 = filter pass, 2 = survivor compaction + solve,
+   * 3 = prep + finalize.  Calvin: 0 = build,
    * 1 = grant groups, 2 = waves, 3 = prep + finalize. */
   double phase_ms[4];
   uint64_t phase_bytes[4];
+  /* OCC prefix peel: prefix length solved first (0 = the
+   * epoch was decided by rounds alone) and txns that survived the filter. */
+  uint64_t peel_prefix;
+  uint64_t n_survivors;
 } dcc_stats;
 
 /* ------------------------------------------------------------- context  */
@@ -126,6 +132,10 @@ int dcc_set_profiling(dcc_ctx* ctx, int enable);
 /* Tuning knobs (defaults are the tuned values; for A/B measurement). */
 #define DCC_OPT_RECHECK 1     /* fold kill waves into rounds whose list has <= value txns */
 #define DCC_OPT_BATCH_MAX 2   /* max rounds enqueued between host synchronisations        */
+#define DCC_OPT_PEEL 3        /* OCC prefix peel: -1 auto (default), 0 off, > 0 prefix length */
+#define DCC_OPT_PEEL_MIN 4    /* auto peel applies to (sub-)batches of >= value txns        */
+#define DCC_OPT_SOLVER 5      /* OCC (sub-)batch solver: 0 auto (async unless key-sharded),
+                                 1 fixed-point rounds, 2 asynchronous (unsharded only)    */
 int dcc_set_option(dcc_ctx* ctx, int option, int64_t value);
 /* Pre-size device workspaces so a later call performs no allocation. */
 int dcc_reserve(dcc_ctx* ctx, uint64_t max_txn, uint64_t max_nnz);
@@ -252,6 +262,43 @@ int dcc_gen_tpcc(const dcc_tpcc_params* p, uint32_t* offsets, uint64_t* keys,
 
 /* Canonical TPC-C key: (table_id << 56) | index key. */
 #define DCC_TPCC_KEY(table_id, ikey) ((((uint64_t)(table_id)) << 56) | ((uint64_t)(ikey)))
+
+/* ------------------------------------------------- batch files (.dccb) */
+/* One captured epoch on disk: the CSR access lists,
+ * optional timestamps / sequencer order, optional decisions.  Versioned,
+ * checksummed (FNV-1a 64), little-endian; layout in batch_file.cpp.  Host
+ * pointers only. */
+#define DCC_FILE_VERSION 1
+#define DCC_FILE_OCC 1
+#define DCC_FILE_CALVIN 2
+#define DCC_FILE_HAS_TN 0x1u         /* start_tn + finish_tn                     */
+#define DCC_FILE_HAS_ORDER 0x2u      /* Calvin sequencer order                   */
+#define DCC_FILE_HAS_RC 0x4u         /* per-txn RC                               */
+#define DCC_FILE_HAS_COMMIT_TN 0x8u  /* OCC history tn of committed writers      */
+#define DCC_FILE_HAS_GROUP 0x10u     /* Calvin grant group per request           */
+#define DCC_FILE_HAS_WAVE 0x20u      /* Calvin wave per txn                      */
+typedef struct dcc_file_info {
+  uint32_t version;     /* DCC_FILE_VERSION                                      */
+  uint32_t kind;        /* DCC_FILE_OCC / DCC_FILE_CALVIN                        */
+  uint32_t sections;    /* DCC_FILE_HAS_* bits present (read); ignored on write  */
+  uint32_t reserved;
+  uint64_t n_txn, nnz;  /* read only (taken from the batch on write)             */
+  uint64_t seed;        /* generator seed or capture id                          */
+  uint64_t epoch;       /* epoch number within a capture                         */
+  uint64_t tnc_before;  /* OCC commit counter before the epoch (occ.h:67)        */
+} dcc_file_info;
+/* Sections are written for every non-NULL array (start_tn/finish_tn/order from
+ * the batch).  Returns DCC_EIO on a file error. */
+int dcc_file_write(const char* path, const dcc_file_info* info, const dcc_batch* batch,
+                   const uint8_t* rc, const uint64_t* commit_tn, const uint32_t* group,
+                   const uint32_t* wave);
+int dcc_file_read_info(const char* path, dcc_file_info* info);
+/* Fills every non-NULL destination whose section is present (size them from
+ * dcc_file_read_info).  DCC_EINVAL: bad magic, truncated, checksum or offsets
+ * mismatch; DCC_ENOTSUP: another format version. */
+int dcc_file_read(const char* path, uint32_t* offsets, uint64_t* keys, uint8_t* acctype,
+                  uint64_t* start_tn, uint64_t* finish_tn, uint64_t* order, uint8_t* rc,
+                  uint64_t* commit_tn, uint32_t* group, uint32_t* wave);
 
 /* Algorithmic bytes of one epoch pass:
  * 4(N+1) + 9 nnz + 16 nnz_w + 16 nnz + N. */

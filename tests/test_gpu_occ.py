@@ -104,10 +104,33 @@ def test_keys_near_reserved(engine):
 
 def test_chain_many_rounds(engine):
     # ~n rounds: crosses the 61-round tag space several times (retag path)
+    from deneva_amd._abi import OPT_SOLVER
     b = chain_batch(300)
-    rc, st = run(engine, b)
+    engine.set_option(OPT_SOLVER, 1)
+    try:
+        rc, st = run(engine, b)
+    finally:
+        engine.set_option(OPT_SOLVER, 0)
     assert st["rounds"] > 130
     assert list(rc[:6]) == [0, 2, 0, 2, 0, 2]
+
+
+@pytest.mark.parametrize("solver", [1, 2])
+def test_solvers_agree(engine, solver):
+    # every batch shape through both (sub-)batch solvers explicitly
+    from deneva_amd._abi import OPT_PEEL, OPT_SOLVER
+    rng = np.random.default_rng(33)
+    engine.set_option(OPT_SOLVER, solver)
+    engine.set_option(OPT_PEEL, 0)
+    try:
+        run(engine, chain_batch(2000))
+        run(engine, random_batch(rng, 5000, 64, 300, p_write=0.5))
+        run(engine, random_batch(rng, 5000, 16, 40, types=(RD, WR, XP, SCAN), unique=False))
+        run(engine, d.gen_ycsb(n_txn=30000, zipf_theta=0.99, table_size=1 << 16))
+        run(engine, make_batch([[(7, WR)] for _ in range(40000)]))  # one segment > 32K writers
+    finally:
+        engine.set_option(OPT_SOLVER, 0)
+        engine.set_option(OPT_PEEL, -1)
 
 
 def test_history_window(engine):

@@ -1,8 +1,8 @@
 """A/B timing of engine variants in ONE process (interleaved rounds), on the
-bench batch.  Usage: python tools_ab.py [--txns N] [--theta T] [--reps R]"""
+bench batch.  Usage: python tools/ab.py [--txns N] [--theta T] [--reps R]"""
 import argparse, json, os, sys, time
 import numpy as np
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 import deneva_amd as d
 from deneva_amd import _abi

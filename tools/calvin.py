@@ -2,7 +2,7 @@
 sequencer order), device-resident, with per-phase profiling."""
 import argparse, json, os, sys, time
 import numpy as np
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 import deneva_amd as d
 

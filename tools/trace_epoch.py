@@ -1,0 +1,29 @@
+#!/usr/bin/env python3
+"""Print the kernel timeline of one OCC epoch from a rocprofv3 kernel trace
+(csv): every dispatch between two k_prep launches, with its duration and the
+idle gap before it.  Usage: trace_epoch.py <kernel_trace.csv> [epoch_index]"""
+import csv
+import sys
+
+
+def main():
+    rows = list(csv.DictReader(open(sys.argv[1])))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    starts = [i for i, r in enumerate(rows) if "k_prep" in r["Kernel_Name"]]
+    e = int(sys.argv[2]) if len(sys.argv) > 2 else len(starts) - 2
+    a, b = starts[e], (starts[e + 1] if e + 1 < len(starts) else len(rows))
+    t0 = int(rows[a]["Start_Timestamp"])
+    prev_end = t0
+    busy = 0
+    for r in rows[a:b]:
+        s, en = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        name = r["Kernel_Name"].split("(")[0][:60]
+        print(f"{(s - t0) / 1e3:9.1f} us  gap {(s - prev_end) / 1e3:7.1f}  dur {(en - s) / 1e3:8.1f}  "
+              f"grid {r.get('Grid_Size_X', r.get('Grid_Size', '?')):>8}  {name}")
+        busy += en - s
+        prev_end = en
+    print(f"epoch span {(prev_end - t0) / 1e3:.1f} us, kernels busy {busy / 1e3:.1f} us")
+
+
+if __name__ == "__main__":
+    main()
