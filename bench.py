@@ -44,7 +44,8 @@ def parse():
     ap.add_argument("--peel", type=int, default=-1,
                     help="OCC prefix peel: -1 auto (default), 0 off, >0 prefix length")
     ap.add_argument("--solver", type=int, default=0,
-                    help="OCC (sub-)batch solver: 0 auto, 1 rounds, 2 asynchronous")
+                    help="OCC solver: 0 auto (sweep on one GPU), 1 rounds, 2 asynchronous, "
+                         "3 sweep")
     ap.add_argument("--exchange", choices=["rccl", "host"], default="rccl",
                     help="N>1 status all-reduce: RCCL over xGMI (one GPU per rank), or "
                          "host/gloo (rehearsal: ranks may share one GPU)")
@@ -219,7 +220,14 @@ def main():
     ph_ms = np.mean([p["phase_ms"] for p in prof], axis=0)
     ph_bytes = prof[-1]["phase_bytes"]
     peeled = prof[-1]["peel_prefix"] > 0
-    if peeled:
+    swept = args.solver in (0, 3) and args.peel == -1 and world == 1
+    if swept:
+        # sweep solver: the level-0 filter is the one kernel that streams the
+        # whole epoch (every offset, key and access type); the serial passes
+        # and later levels run on short lists
+        dom = 1
+        dom_name = "k_sw_filter (level-0 committed-key filter)"
+    elif peeled:
         # prefix peel: k_filter is the one kernel that streams the whole epoch
         # (every offset, key and access type); the rest runs on the prefix and
         # the few survivors
@@ -302,7 +310,9 @@ def main():
                 "commits": int(s0["n_commit"]),
                 "aborts": int(s0["n_abort"]),
                 "phase_ms": [float(x) for x in ph_ms],
-                "phases": (["prefix solve", "k_filter", "survivor compaction+solve",
+                "phases": (["level-0 records+serial pass", "level-0 filter", "later levels",
+                            "prep+final"] if swept else
+                           ["prefix solve", "k_filter", "survivor compaction+solve",
                             "prep+final"] if peeled else
                            ["k_build", "round 1", "rounds>=2", "prep+final"]),
                 "peel_prefix": int(s0["peel_prefix"]),

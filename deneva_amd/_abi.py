@@ -36,6 +36,7 @@ OPT_BATCH_MAX = 2
 OPT_PEEL = 3
 OPT_PEEL_MIN = 4
 OPT_SOLVER = 5
+OPT_SWEEP_LEVELS = 6
 
 
 class Batch(C.Structure):

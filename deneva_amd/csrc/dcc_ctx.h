@@ -64,11 +64,16 @@ struct dcc_ctx {
   uint32_t batch_max = 8;       // rounds enqueued between host synchronisations
   int64_t peel_mode = -1;       // -1 auto prefix, 0 off, > 0 fixed prefix length
   uint64_t peel_min = 32768;    // auto: peel (sub-)batches of at least this many txns
-  int solver = 0;               // 0 auto (async when unsharded), 1 rounds, 2 async
+  int solver = 0;               // 0 auto (sweep when unsharded), 1 rounds, 2 async, 3 sweep
   bool force_rounds = false;    // retry after an async-solver limit
   uint32_t* async_passes_dev = nullptr;
   uint64_t prefix_w_top = 0;    // write accesses in the top-level peel prefix
   bool use_async() const { return !force_rounds && solver != 1 && comm_ranks() <= 1; }
+  bool use_sweep() const {
+    return !force_rounds && comm_ranks() <= 1 && (solver == 3 || (solver == 0 && peel_mode == -1));
+  }
+  uint32_t sw_levels = 6;
+  bool sw_debug = false;        // DCC_SW_DEBUG: per-tile clock stamps of the serial pass       // sweep levels enqueued between host synchronisations
   hipEvent_t pev[8] = {};  // phase boundary events (profiling only)
   std::string last_error;
   void* hmisc = nullptr;  // pinned host mirror of `misc`
@@ -84,6 +89,9 @@ struct dcc_ctx {
   DevBuf gst;                                    // sharded per-txn status
   DevBuf hasw_scr, cset_tab, cset_keys;          // prefix peel
   DevBuf a_cnt, a_writers, a_big, a_st32;        // async solver
+  DevBuf sw_ctl, sw_status, sw_ckeys, sw_dbg;            // sweep solver: level control, look-back, C
+  DevBuf sw_rec, sw_rk, sw_rp, sw_rtid, sw_tinfo, sw_gtab;  // sweep tile records
+  SubBufs sw_list[2];                            // sweep level lists (ping-pong)
   SubBufs subs[PEEL_MAX_LEVEL];
   DevBuf l_tid[2], l_coff[2], l_cent[2];         // ping-pong undecided lists
   DevBuf hkeys, hoff, htn;                       // history CSR
@@ -117,6 +125,9 @@ struct dcc_ctx {
   int occ_rounds(const SubProb& sp, uint32_t maxlen, bool prof, uint32_t& rounds);
   int occ_async(const SubProb& sp, uint32_t maxlen, uint32_t& passes);
   int occ_peel(const SubProb& sp, uint32_t maxlen, int level, uint32_t& rounds, PeelInfo& info);
+  int sweep_reserve(const DevBatch& d);
+  int sweep_enqueue(const DevBatch& d, int l0, int l1);
+  int occ_sweep_finish(const DevBatch& d, int& next_level, bool& done, uint32_t maxlen);
   uint64_t peel_prefix(uint64_t m, int level) const;
   int calvin_epoch(const dcc_batch* b, uint32_t* out_group, uint8_t* out_rc, uint32_t* out_wave,
                    dcc_stats* st);

@@ -166,8 +166,12 @@ extern "C" int dcc_set_option(dcc_ctx* ctx, int option, int64_t value) {
       ctx->peel_min = (uint64_t)value;
       return DCC_OK;
     case DCC_OPT_SOLVER:
-      if (value < 0 || value > 2) return DCC_EINVAL;
+      if (value < 0 || value > 3) return DCC_EINVAL;
       ctx->solver = (int)value;
+      return DCC_OK;
+    case DCC_OPT_SWEEP_LEVELS:
+      if (value < 1 || value > SW_MAX_LEVEL) return DCC_EINVAL;
+      ctx->sw_levels = (uint32_t)value;
       return DCC_OK;
     case DCC_OPT_BATCH_MAX:
       if (value < 1 || value > 32) return DCC_EINVAL;
@@ -190,7 +194,11 @@ std::vector<DevBuf*> dcc_ctx::all_bufs() {
                             &cv_scratch, &cv_agg, &cv_group, &cv_wave, &cv_pgx, &cv_gsx,
                             &cv_gsize, &cv_done, &cv_maxl, &cv_seq_b, &cv_ok, &cv_len,
                             &cv_off2, &cv_tsum, &gst, &hasw_scr, &cset_tab, &cset_keys,
-                            &a_cnt, &a_writers, &a_big, &a_st32};
+                            &a_cnt, &a_writers, &a_big, &a_st32, &sw_ctl, &sw_status, &sw_dbg,
+                            &sw_ckeys, &sw_gtab, &sw_rec, &sw_rk, &sw_rp, &sw_rtid,
+                            &sw_tinfo};
+  for (auto& sb : sw_list)
+    for (DevBuf* b : {&sb.tid, &sb.off, &sb.keys, &sb.acctype, &sb.state}) v.push_back(b);
   for (auto& sb : subs)
     for (DevBuf* b : {&sb.tid, &sb.off, &sb.keys, &sb.acctype, &sb.state}) v.push_back(b);
   for (int i = 0; i < 2; i++) {

@@ -8,6 +8,8 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -435,6 +437,136 @@ int dcc_ctx::occ_peel(const SubProb& sp, uint32_t maxlen, int level, uint32_t& r
   return DCC_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Sweep solver (occ_sweep.hip): per level, tile records + one serial pass in
+// one CU + a filter/compaction pass; levels are enqueued without host
+// synchronisation (list lengths live on the device), sw_levels at a time.
+static constexpr size_t SW_PREP_OFF = 32768;  // prep partials inside `part` / `hpart`
+static constexpr size_t SW_HCTL = 13312;      // control-block copy inside `hmisc`
+static constexpr uint32_t SW_PMAX_TOP = 65536;
+static constexpr uint32_t SW_CAP0 = 0x7FFFFFFFu, SW_CAP = 0x7FFFFFFFu;  // C is unbounded (bitmap)
+                                                          // the serial pass's LDS set)
+static uint32_t sw_pmax(int level) {
+  return level >= 6 ? SW_PMAX_TOP : (1024u << level);
+}
+static size_t sw_ctl_bytes() { return (SW_MAX_LEVEL + 2) * sizeof(SwLevel) + 64; }
+// key-table slots of a level: twice the accesses of p_max 16-access txns
+static uint32_t sw_gbits(int level) {
+  uint32_t b = 12;
+  while (b < SW_GBITS_MAX && (1ull << b) < 2ull * sw_pmax(level) * 16) b++;
+  return b;
+}
+
+int dcc_ctx::sweep_reserve(const DevBatch& d) {
+  const uint64_t tiles = SW_PMAX_TOP / SW_T;
+  sw_debug = getenv("DCC_SW_DEBUG") != nullptr;
+  if (sw_debug) {
+    CR(sw_dbg.ensure(this, (4096 + 4 * 256 * 8) * 8, "sweep debug"));
+    dcc_ctx* ctx = this;
+    CK(hipMemsetAsync(sw_dbg.p, 0, (4096 + 4 * 256 * 8) * 8, stream));
+  }
+  CR(sw_ctl.ensure(this, sw_ctl_bytes(), "sweep control"));
+  CR(sw_status.ensure(this, ((d.n + SW_CHUNK - 1) / SW_CHUNK + 64) * 8, "sweep look-back"));
+  CR(sw_ckeys.ensure(this, ((1ull << SW_GBITS_MAX) / 32 + (1ull << SW_BLOOM_LOG) / 32) * 4,
+                     "sweep committed set"));
+  CR(sw_rec.ensure(this, (tiles + SW_SEQ_B) * sizeof(SwRec), "sweep tile records"));
+  CR(sw_rk.ensure(this, tiles * (SW_TA - SW_REC_ACC) * 4, "sweep tile key ids"));
+  CR(sw_gtab.ensure(this, 2 * (1ull << SW_GBITS_MAX) * 8, "sweep key tables"));
+  CR(sw_rp.ensure(this, tiles * (SW_TA - SW_REC_ACC), "sweep tile bytes"));
+  CR(sw_rtid.ensure(this, tiles * SW_T * 4, "sweep tile txns"));
+  CR(sw_tinfo.ensure(this, tiles * sizeof(SwTile), "sweep tile info"));
+  for (SubBufs& b : sw_list) {
+    CR(b.tid.ensure(this, d.n * 4 + 16, "sweep list tid"));
+    CR(b.off.ensure(this, (d.n + 1) * 4 + 16, "sweep list offsets"));
+    CR(b.keys.ensure(this, std::max<uint64_t>(8, d.nnz * 8), "sweep list keys"));
+    CR(b.acctype.ensure(this, std::max<uint64_t>(16, d.nnz), "sweep list acctype"));
+    CR(b.state.ensure(this, d.n + 16, "sweep list state"));
+  }
+  return DCC_OK;
+}
+
+// Enqueue levels [l0, l1) (list l0 must exist: the epoch, or written by the
+// filter of level l0 - 1).
+int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1) {
+  dcc_ctx* ctx = this;
+  SwLevel* ctl = (SwLevel*)sw_ctl.p;
+  uint32_t* abandon = (uint32_t*)(ctl + SW_MAX_LEVEL + 1);
+  uint32_t* err = (uint32_t*)misc.p;
+  const uint32_t n = (uint32_t)d.n;
+  const uint32_t status_n = (uint32_t)((d.n + SW_CHUNK - 1) / SW_CHUNK + 1);
+  const unsigned fgrid = (unsigned)std::max<uint64_t>(
+      1, std::min<uint64_t>((d.n + SW_CHUNK - 1) / SW_CHUNK, 4ull * n_cu));
+  uint64_t* gtab0 = (uint64_t*)sw_gtab.p;
+  uint32_t* cbits_d = (uint32_t*)sw_ckeys.p;
+  uint32_t* bloom_d = cbits_d + (1u << SW_GBITS_MAX) / 32;
+  for (int l = l0; l < l1; l++) {
+    const bool top = l == 0;
+    SwList in;
+    if (top) {
+      in = SwList{nullptr, d.off, d.keys, d.acctype, d.nnz};
+    } else {
+      const SubBufs& b = sw_list[(l - 1) & 1];
+      in = SwList{(const uint32_t*)b.tid.p, (const uint32_t*)b.off.p, (const uint64_t*)b.keys.p,
+                  (const uint8_t*)b.acctype.p, d.nnz};
+    }
+    SubBufs& out = sw_list[l & 1];
+    SwLevel* lv = ctl + l;
+    const uint32_t* mdev = top ? nullptr : &lv->m;
+    const uint32_t pmax = sw_pmax(l);
+    const uint64_t tiles = (std::min<uint64_t>(pmax, d.n) + SW_T - 1) / SW_T;
+    SwPreArgs pa{in, mdev, n, pmax, top ? (const uint8_t*)state.p : nullptr,
+                 (SwRec*)sw_rec.p, (uint32_t*)sw_rk.p, (uint8_t*)sw_rp.p,
+                 gtab0 + (size_t)(l & 1) * (1ull << SW_GBITS_MAX), sw_gbits(l),
+                 1u << (sw_gbits(l) - 1),
+                 (uint32_t*)sw_rtid.p, (SwTile*)sw_tinfo.p, abandon, err};
+    launch_sw_pre(pa, (unsigned)std::min<uint64_t>(tiles, n_cu), stream);
+    SwSeqArgs sa{mdev, n, pmax, top ? SW_CAP0 : SW_CAP, top ? 1 : 0,
+                 (const SwRec*)sw_rec.p, (const uint32_t*)sw_rk.p, (const uint8_t*)sw_rp.p,
+                 gtab0 + (size_t)(l & 1) * (1ull << SW_GBITS_MAX), sw_gbits(l),
+                 (const uint32_t*)sw_rtid.p, (const SwTile*)sw_tinfo.p, (uint8_t*)state.p, (uint8_t*)hasw.p,
+                 cbits_d, bloom_d, lv, lv + 1, (uint32_t*)out.off.p,
+                 (unsigned long long*)sw_status.p, status_n, abandon, err, nullptr};
+    if (sw_debug && l < 4) sa.dbg = (uint64_t*)sw_dbg.p + (size_t)l * 1024;
+    launch_sw_seq(sa, stream);
+    if (top && profiling) CK(hipEventRecord(pev[1], stream));
+    SwFilterArgs fa;
+    fa.in = in;
+    fa.m_dev = mdev;
+    fa.m_host = n;
+    fa.cand_state = top ? 1 : 0;
+    fa.write_hasw = top ? 1 : 0;
+    fa.level = (uint32_t)l;
+    fa.gtab = gtab0 + (size_t)(l & 1) * (1ull << SW_GBITS_MAX);
+    fa.gbits = sw_gbits(l);
+    fa.cbits = cbits_d;
+    fa.bloom = bloom_d;
+    fa.lv = lv;
+    fa.lv_next = lv + 1;
+    fa.state = (uint8_t*)state.p;
+    fa.hasw = (uint8_t*)hasw.p;
+    fa.tid_out = (uint32_t*)out.tid.p;
+    fa.off_out = (uint32_t*)out.off.p;
+    fa.keys_out = (uint64_t*)out.keys.p;
+    fa.acc_out = (uint8_t*)out.acctype.p;
+    fa.status = (unsigned long long*)sw_status.p;
+    fa.abandon = abandon;
+    fa.abandon_out = abandon;
+    // hand the survivors to the round solver when the committed keys stop
+    // killing: > 1/4 of the epoch survive level 0, > 3/4 of a later list
+    fa.abandon_min = 65536;
+    fa.abandon_num = top ? 1 : 3;
+    fa.abandon_den = 4;
+    fa.gclear = gtab0 + (size_t)((l + 1) & 1) * (1ull << SW_GBITS_MAX);
+    fa.gclear_n = 1ull << sw_gbits(l + 1);
+    fa.err = err;
+    fa.dbg = (sw_debug && l < 4) ? (uint64_t*)sw_dbg.p + 4096 + (size_t)l * 256 * 8 : nullptr;
+    launch_sw_filter(fa, fgrid, stream);
+    if (top && profiling) CK(hipEventRecord(pev[2], stream));
+  }
+  CK(hipGetLastError());
+  return DCC_OK;
+}
+
 int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dcc_stats* st) {
   dcc_ctx* ctx = this;
   // key-sharded across ranks: this rank holds only its keys
@@ -451,13 +583,19 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   }
   DevBatch d;
   CR(stage_batch(b, d));
+  const bool sweep = use_sweep();
+  if (sweep) CR(sweep_reserve(d));
   CK(hipEventRecord(ev0, stream));  // device clock starts with the batch resident
 
-  // ---- prep: validation, max length (tile width), write count (table size)
+  // ---- prep: validation, max length (tile width), write count (table size).
+  // The sweep needs none of it up front (its kernels clamp every index): its
+  // partials are read back with the epoch's one synchronisation.
   uint32_t maxlen = 0;
   uint64_t nnz_w = 0;
-  const uint64_t p0 = peel_prefix(d.n, 0);
-  CR(device_prep(d, maxlen, nnz_w, p0, &prefix_w_top));
+  const uint64_t p0 = sweep ? 0 : peel_prefix(d.n, 0);
+  if (sweep) launch_prep(d.off, d.n, d.acctype, d.nnz, 0,
+                         (PrepPart*)((char*)part.p + SW_PREP_OFF), stream);
+  else CR(device_prep(d, maxlen, nnz_w, p0, &prefix_w_top));
   CR(state.ensure(this, d.n + 16, "state"));
   CR(hasw.ensure(this, d.n + 16, "hasw"));
   CR(rc.ensure(this, d.n + 16, "rc"));
@@ -466,6 +604,10 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   CK(hipMemsetAsync((char*)misc.p + MISC_ASYNC + 8, 0, 4, stream));  // async pass count
   CK(hipMemsetAsync(one, 0x01, 1, stream));
   CK(hipMemsetAsync(state.p, 0, d.n, stream));
+  if (sweep) {
+    CK(hipMemsetAsync(sw_ctl.p, 0, sw_ctl_bytes(), stream));
+    CK(hipMemsetAsync(sw_gtab.p, 0xFF, (1ull << sw_gbits(0)) * 8, stream));
+  }
 
   // ---- history window pre-pass (occ.cpp:160-180)
   if (d.start_tn && !hist.empty()) {
@@ -490,11 +632,20 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   top.w_bound = nnz_w;
   uint32_t rounds = 0;
   PeelInfo info;
-  const bool peel = peel_prefix(d.n, 0) != 0;
+  const bool peel = !sweep && p0 != 0;
   async_passes_dev = nullptr;
-  if (peel) CR(occ_peel(top, maxlen, 0, rounds, info));
-  else if (use_async()) CR(occ_async(top, maxlen, rounds));
-  else CR(occ_rounds(top, maxlen, profiling, rounds));
+  int next_level = 0;
+  if (sweep) {
+    if (profiling) CK(hipEventRecord(pev[0], stream));
+    next_level = (int)std::min<uint32_t>(sw_levels, SW_MAX_LEVEL - 1);
+    CR(sweep_enqueue(d, 0, next_level));
+  } else if (peel) {
+    CR(occ_peel(top, maxlen, 0, rounds, info));
+  } else if (use_async()) {
+    CR(occ_async(top, maxlen, rounds));
+  } else {
+    CR(occ_rounds(top, maxlen, profiling, rounds));
+  }
   if (profiling && !peel) CK(hipEventRecord(pev[3], stream));
 
   // ---- finalize: RC bytes, counts, central_finish tn numbering
@@ -507,26 +658,141 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
     CR(tn.ensure(this, d.n * 8, "tn"));
     cf = (uint32_t*)cflag.p;
   }
-  FinalArgs fa{d.n, (const uint8_t*)state.p, (const uint8_t*)hasw.p, rc_dev, cf,
-               (FinalPart*)part.p};
-  launch_final(fa, stream);
-  uint64_t* tn_dev = nullptr;
-  if (want_tn) {
-    tn_dev = (dev_out && out_tn) ? out_tn : (uint64_t*)tn.p;
-    launch_commit_tn(cf, d.n, (uint64_t*)bsum.p, tnc, tn_dev, stream);
+  uint64_t* tn_dev = want_tn ? ((dev_out && out_tn) ? out_tn : (uint64_t*)tn.p) : nullptr;
+  auto enqueue_final = [&]() -> int {
+    FinalArgs fa{d.n, (const uint8_t*)state.p, (const uint8_t*)hasw.p, rc_dev, cf,
+                 (FinalPart*)part.p};
+    launch_final(fa, stream);
+    if (want_tn) launch_commit_tn(cf, d.n, (uint64_t*)bsum.p, tnc, tn_dev, stream);
+    CK(hipGetLastError());
+    CK(hipEventRecord(ev1, stream));
+    if (!dev_out) {
+      if (out_rc) CK(hipMemcpyAsync(out_rc, rc.p, d.n, hipMemcpyDeviceToHost, stream));
+      if (out_tn) CK(hipMemcpyAsync(out_tn, tn.p, d.n * 8, hipMemcpyDeviceToHost, stream));
+    }
+    CK(hipMemcpyAsync(hmisc, misc.p, 64, hipMemcpyDeviceToHost, stream));
+    if (async_passes_dev)
+      CK(hipMemcpyAsync((char*)hmisc + MISC_ASYNC, (char*)misc.p + MISC_ASYNC, 16,
+                        hipMemcpyDeviceToHost, stream));
+    if (sweep) {
+      CK(hipMemcpyAsync((char*)hmisc + SW_HCTL, sw_ctl.p, sw_ctl_bytes(), hipMemcpyDeviceToHost,
+                        stream));
+      CK(hipMemcpyAsync((char*)hpart + SW_PREP_OFF, (char*)part.p + SW_PREP_OFF,
+                        PREP_BLOCKS * sizeof(PrepPart), hipMemcpyDeviceToHost, stream));
+    }
+    CR(read_partials(FINAL_BLOCKS * sizeof(FinalPart)));
+    CK(hipStreamSynchronize(stream));
+    return DCC_OK;
+  };
+  CR(enqueue_final());
+
+  if (sweep) {
+    // prep results: the batch is rejected exactly as device_prep would
+    const PrepPart* pp = (const PrepPart*)((const char*)hpart + SW_PREP_OFF);
+    uint32_t perr = 0;
+    for (unsigned q = 0; q < PREP_BLOCKS; q++) {
+      perr |= pp[q].err;
+      maxlen = std::max(maxlen, pp[q].maxlen);
+      nnz_w += pp[q].nw;
+    }
+    if (perr & ERR_OFFSETS) return fail(DCC_EINVAL, "batch: malformed offsets");
+    if (maxlen > MAX_TXN_LEN)
+      return fail(DCC_ERANGE, "batch: a txn has %u accesses (> MAX_ROW_PER_TXN=%u)", maxlen,
+                  MAX_TXN_LEN);
+    // more levels, or hand the remaining list to the round solver
+    bool again = false;
+    for (;;) {
+      const SwLevel* hc = (const SwLevel*)((const char*)hmisc + SW_HCTL);
+      const uint32_t ab = *(const uint32_t*)(hc + SW_MAX_LEVEL + 1);
+      const uint32_t e = *(const uint32_t*)hmisc;
+      if (e & (ERR_SPIN | ERR_TILE | ERR_FULL)) break;  // reported below
+      int L = -1;
+      if (ab) L = (int)ab;
+      else if (hc[next_level].m == 0) break;  // every list decided
+      else if (next_level + (int)sw_levels >= SW_MAX_LEVEL) L = next_level;
+      if (L < 0) {
+        const int l1 = next_level + (int)sw_levels;
+        CR(sweep_enqueue(d, next_level, l1));
+        next_level = l1;
+        CK(hipMemcpyAsync((char*)hmisc + SW_HCTL, sw_ctl.p, sw_ctl_bytes(),
+                          hipMemcpyDeviceToHost, stream));
+        CK(hipMemcpyAsync(hmisc, misc.p, 64, hipMemcpyDeviceToHost, stream));
+        CK(hipStreamSynchronize(stream));
+        again = true;
+        continue;
+      }
+      // list L (written by the filter of level L-1): decide it with rounds
+      const SubBufs& lb = sw_list[(L - 1) & 1];
+      SubProb sub;
+      sub.n = hc[L].m;
+      sub.nnz = hc[L].acc;
+      sub.off = (const uint32_t*)lb.off.p;
+      sub.keys = (const uint64_t*)lb.keys.p;
+      sub.acctype = (const uint8_t*)lb.acctype.p;
+      sub.state = (uint8_t*)lb.state.p;
+      CR(hasw_scr.ensure(this, d.n + 16, "hasw scratch"));
+      sub.hasw = (uint8_t*)hasw_scr.p;
+      sub.hasw_global = false;
+      sub.w_bound = std::max<uint64_t>(1, sub.nnz);
+      CK(hipMemsetAsync(sub.state, 0, sub.n, stream));
+      uint32_t r_sub = 0;
+      if (use_async()) CR(occ_async(sub, maxlen, r_sub));
+      else CR(occ_rounds(sub, maxlen, false, r_sub));
+      rounds += r_sub;
+      launch_scatter(sub.state, (const uint32_t*)lb.tid.p,
+                     &((SwLevel*)sw_ctl.p)[L].m, sub.n, (uint8_t*)state.p, stream);
+      CK(hipGetLastError());
+      again = true;
+      break;
+    }
+    if (again) {
+      if (profiling) CK(hipEventRecord(pev[3], stream));
+      CR(enqueue_final());
+    }
+    const SwLevel* hc = (const SwLevel*)((const char*)hmisc + SW_HCTL);
+    if (sw_debug) {
+      std::vector<uint64_t> dv(4096 + 4 * 256 * 8);
+      CK(hipMemcpy(dv.data(), sw_dbg.p, dv.size() * 8, hipMemcpyDeviceToHost));
+      for (int l = 0; l < 4; l++) {
+        const uint64_t* t = dv.data() + l * 1024;
+        double ph[4] = {0, 0, 0, 0};
+        int nt = 0;
+        for (int k = 0; k < 128 && t[k * 4 + 3]; k++, nt++) {
+          ph[0] += t[k * 4 + 1] - t[k * 4];
+          ph[1] += t[k * 4 + 2] - t[k * 4 + 1];
+          ph[2] += t[k * 4 + 3] - t[k * 4 + 2];
+          if (k + 1 < 128 && t[k * 4 + 4]) ph[3] += t[k * 4 + 4] - t[k * 4 + 3];
+        }
+        if (nt)
+          fprintf(stderr, "sweep L%d: %d tiles, cycles/tile probe %.0f resolve %.0f insert %.0f "
+                          "between %.0f\n", l, nt, ph[0] / nt, ph[1] / nt, ph[2] / nt, ph[3] / nt);
+        // filter: per workgroup init / first chunk local / look-back / writes / total
+        const uint64_t* f = dv.data() + 4096 + l * 256 * 8;
+        double fi = 0, fl = 0, fb = 0, fw = 0, ft = 0, nc = 0;
+        int nw = 0, nwc = 0;
+        for (int w = 0; w < 256 && f[w * 8]; w++, nw++) {
+          const uint64_t* x = f + w * 8;
+          fi += x[1] - x[0];
+          ft += x[5] - x[0];
+          nc += x[6];
+          if (x[6]) {
+            fl += x[2] - x[1];
+            fb += x[3] - x[2];
+            fw += x[4] - x[3];
+            nwc++;
+          }
+        }
+        if (nw)
+          fprintf(stderr, "  filter L%d: %d WGs, chunks/WG %.2f, init %.0f, chunk local %.0f "
+                          "lookback %.0f writes %.0f, WG total %.0f cycles\n", l, nw, nc / nw,
+                  fi / nw, nwc ? fl / nwc : 0, nwc ? fb / nwc : 0, nwc ? fw / nwc : 0, ft / nw);
+      }
+    }
+    info.prefix = hc[0].pos;
+    info.survivors = hc[1].m;
+    for (int l = 0; l < next_level && (l == 0 || hc[l].m); l++) rounds++;
   }
-  CK(hipGetLastError());
-  CK(hipEventRecord(ev1, stream));
-  if (!dev_out) {
-    if (out_rc) CK(hipMemcpyAsync(out_rc, rc.p, d.n, hipMemcpyDeviceToHost, stream));
-    if (out_tn) CK(hipMemcpyAsync(out_tn, tn.p, d.n * 8, hipMemcpyDeviceToHost, stream));
-  }
-  CK(hipMemcpyAsync(hmisc, misc.p, 64, hipMemcpyDeviceToHost, stream));
-  if (async_passes_dev)
-    CK(hipMemcpyAsync((char*)hmisc + MISC_ASYNC, (char*)misc.p + MISC_ASYNC, 16,
-                      hipMemcpyDeviceToHost, stream));
-  CR(read_partials(FINAL_BLOCKS * sizeof(FinalPart)));
-  CK(hipStreamSynchronize(stream));
+
   const uint32_t e = *(const uint32_t*)hmisc;
   if ((e & (ERR_SEG | ERR_ASYNC)) && !force_rounds) {
     // a writer segment too long for the LDS sort, or the pass guard tripped:
@@ -547,6 +813,7 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   if (e & ERR_KEY) return fail(DCC_EINVAL, "batch: key equal to DCC_KEY_RESERVED");
   if (e & ERR_FULL) return fail(DCC_EIO, "hash table overflow");
   if (e & ERR_TILE) return fail(DCC_EIO, "tile capacity exceeded");
+  if (e & ERR_SPIN) return fail(DCC_EIO, "sweep look-back did not complete");
   const FinalPart* fp = (const FinalPart*)hpart;
   uint64_t n_commit = 0, n_abort = 0, n_ro = 0, n_cw = 0, n_und = 0;
   for (unsigned q = 0; q < FINAL_BLOCKS; q++) {
@@ -571,7 +838,13 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   S.n_survivors = info.survivors;
   if (profiling) {
     float t0 = 0, t1 = 0, t2 = 0;
-    if (peel) {
+    if (sweep) {
+      // phases: 0 = level-0 records + serial pass, 1 = level-0 filter,
+      // 2 = later levels (+ fallback), 3 = prep + finalize
+      CK(hipEventElapsedTime(&t0, pev[0], pev[1]));
+      CK(hipEventElapsedTime(&t1, pev[1], pev[2]));
+      CK(hipEventElapsedTime(&t2, pev[2], pev[3]));
+    } else if (peel) {
       // phases: 0 = prefix solve + committed-key set, 1 = filter pass,
       // 2 = compaction + survivor solve + scatter, 3 = prep + finalize
       CK(hipEventElapsedTime(&t0, pev[0], pev[1]));
@@ -588,7 +861,7 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
     S.phase_ms[2] = t2;
     S.phase_ms[3] = ms - t0 - t1 - t2;
   }
-  if (peel) {
+  if (sweep || peel) {
     // the filter pass reads offsets, keys + acctype of every access and the
     // state byte of every txn, and writes the has-write (and kill) bytes
     S.phase_bytes[1] = 4 * (d.n + 1) + 9 * d.nnz + 2 * d.n;

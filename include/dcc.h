@@ -102,12 +102,15 @@ typedef struct dcc_stats {
    * of each phase.  OCC phases: 0 = key-hash build, 1 = round-1 probe,
    * 2 = rounds >= 2 (sum), 3 = prep + finalize; with the prefix peel:
    * 0 = prefix solve, 1 = filter pass, 2 = survivor compaction + solve,
+   * 3 = prep + finalize; with the sweep solver: 0 = level-0 tile records +
+   * serial pass, 1 = level-0 filter, 2 = later levels (and any fallback),
    * 3 = prep + finalize.  Calvin: 0 = build,
    * 1 = grant groups, 2 = waves, 3 = prep + finalize. */
   double phase_ms[4];
   uint64_t phase_bytes[4];
-  /* OCC prefix peel: prefix length solved first (0 = the
-   * epoch was decided by rounds alone) and txns that survived the filter. */
+  /* OCC prefix peel / sweep: prefix length solved first (0 =
+   * the epoch was decided by rounds alone) and txns that survived the first
+   * filter.  The sweep reports its levels in `rounds`. */
   uint64_t peel_prefix;
   uint64_t n_survivors;
 } dcc_stats;
@@ -134,8 +137,9 @@ int dcc_set_profiling(dcc_ctx* ctx, int enable);
 #define DCC_OPT_BATCH_MAX 2   /* max rounds enqueued between host synchronisations        */
 #define DCC_OPT_PEEL 3        /* OCC prefix peel: -1 auto (default), 0 off, > 0 prefix length */
 #define DCC_OPT_PEEL_MIN 4    /* auto peel applies to (sub-)batches of >= value txns        */
-#define DCC_OPT_SOLVER 5      /* OCC (sub-)batch solver: 0 auto (async unless key-sharded),
-                                 1 fixed-point rounds, 2 asynchronous (unsharded only)    */
+#define DCC_OPT_SOLVER 5      /* OCC solver: 0 auto (sweep unless key-sharded), 1 fixed-point
+                                 rounds, 2 asynchronous, 3 sweep (unsharded only)          */
+#define DCC_OPT_SWEEP_LEVELS 6 /* sweep levels enqueued between host synchronisations       */
 int dcc_set_option(dcc_ctx* ctx, int option, int64_t value);
 /* Pre-size device workspaces so a later call performs no allocation. */
 int dcc_reserve(dcc_ctx* ctx, uint64_t max_txn, uint64_t max_nnz);

@@ -10,7 +10,7 @@ import pytest
 import _oracle as orc
 import deneva_amd as d
 from deneva_amd import RD, WR, XP, SCAN
-from deneva_amd._abi import OPT_PEEL, OPT_PEEL_MIN
+from deneva_amd._abi import OPT_PEEL, OPT_PEEL_MIN, OPT_SOLVER
 from helpers import chain_batch, make_batch, random_batch
 
 pytestmark = pytest.mark.gpu
@@ -18,7 +18,10 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture
 def peel_engine(engine):
+    # the default solver is the sweep (test_gpu_sweep.py); pin the peel path
+    engine.set_option(OPT_SOLVER, 2)
     yield engine
+    engine.set_option(OPT_SOLVER, 0)
     engine.set_option(OPT_PEEL, -1)
     engine.set_option(OPT_PEEL_MIN, 32768)
 
