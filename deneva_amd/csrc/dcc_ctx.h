@@ -72,7 +72,7 @@ struct dcc_ctx {
   bool use_sweep() const {
     return !force_rounds && comm_ranks() <= 1 && (solver == 3 || (solver == 0 && peel_mode == -1));
   }
-  uint32_t sw_levels = 6;
+  uint32_t sw_levels = 4;
   bool sw_debug = false;        // DCC_SW_DEBUG: per-tile clock stamps of the serial pass       // sweep levels enqueued between host synchronisations
   hipEvent_t pev[8] = {};  // phase boundary events (profiling only)
   std::string last_error;
@@ -90,7 +90,7 @@ struct dcc_ctx {
   DevBuf hasw_scr, cset_tab, cset_keys;          // prefix peel
   DevBuf a_cnt, a_writers, a_big, a_st32;        // async solver
   DevBuf sw_ctl, sw_status, sw_ckeys, sw_dbg;            // sweep solver: level control, look-back, C
-  DevBuf sw_rec, sw_rk, sw_rp, sw_rtid, sw_tinfo, sw_gtab;  // sweep tile records
+  DevBuf sw_rec, sw_rk, sw_rp, sw_rtid, sw_tinfo, sw_gtab, sw_ids;  // sweep tile records
   SubBufs sw_list[2];                            // sweep level lists (ping-pong)
   SubBufs subs[PEEL_MAX_LEVEL];
   DevBuf l_tid[2], l_coff[2], l_cent[2];         // ping-pong undecided lists

@@ -461,19 +461,22 @@ int dcc_ctx::sweep_reserve(const DevBatch& d) {
   const uint64_t tiles = SW_PMAX_TOP / SW_T;
   sw_debug = getenv("DCC_SW_DEBUG") != nullptr;
   if (sw_debug) {
-    CR(sw_dbg.ensure(this, (4096 + 4 * 256 * 8) * 8, "sweep debug"));
+    CR(sw_dbg.ensure(this, (4096 + 4 * 256 * 8 + 4 * 64 * 8) * 8, "sweep debug"));
     dcc_ctx* ctx = this;
-    CK(hipMemsetAsync(sw_dbg.p, 0, (4096 + 4 * 256 * 8) * 8, stream));
+    CK(hipMemsetAsync(sw_dbg.p, 0, (4096 + 4 * 256 * 8 + 4 * 64 * 8) * 8, stream));
   }
   CR(sw_ctl.ensure(this, sw_ctl_bytes(), "sweep control"));
-  CR(sw_status.ensure(this, ((d.n + SW_CHUNK - 1) / SW_CHUNK + 64) * 8, "sweep look-back"));
-  CR(sw_ckeys.ensure(this, ((1ull << SW_GBITS_MAX) / 32 + (1ull << SW_BLOOM_LOG) / 32) * 4,
+  CR(sw_status.ensure(this, ((d.n + 63) / 64 + 64) * 16 + (4ull * n_cu + 64) * 8,
+                        "sweep survivor bits + tile counts"));
+  CR(sw_ckeys.ensure(this, ((1ull << SW_GBITS_MAX) / 32 + (1ull << SW_BLOOM_LOG) / 32) * 4 +
+                                (1ull << SW_GBITS_MAX) * 8,
                      "sweep committed set"));
   CR(sw_rec.ensure(this, (tiles + SW_SEQ_B) * sizeof(SwRec), "sweep tile records"));
   CR(sw_rk.ensure(this, tiles * (SW_TA - SW_REC_ACC) * 4, "sweep tile key ids"));
   CR(sw_gtab.ensure(this, 2 * (1ull << SW_GBITS_MAX) * 8, "sweep key tables"));
   CR(sw_rp.ensure(this, tiles * (SW_TA - SW_REC_ACC), "sweep tile bytes"));
   CR(sw_rtid.ensure(this, tiles * SW_T * 4, "sweep tile txns"));
+  CR(sw_ids.ensure(this, (1ull << (SW_GBITS_MAX - 1)) * 4, "sweep key ids"));
   CR(sw_tinfo.ensure(this, tiles * sizeof(SwTile), "sweep tile info"));
   for (SubBufs& b : sw_list) {
     CR(b.tid.ensure(this, d.n * 4 + 16, "sweep list tid"));
@@ -493,12 +496,16 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1) {
   uint32_t* abandon = (uint32_t*)(ctl + SW_MAX_LEVEL + 1);
   uint32_t* err = (uint32_t*)misc.p;
   const uint32_t n = (uint32_t)d.n;
-  const uint32_t status_n = (uint32_t)((d.n + SW_CHUNK - 1) / SW_CHUNK + 1);
   const unsigned fgrid = (unsigned)std::max<uint64_t>(
       1, std::min<uint64_t>((d.n + SW_CHUNK - 1) / SW_CHUNK, 4ull * n_cu));
   uint64_t* gtab0 = (uint64_t*)sw_gtab.p;
   uint32_t* cbits_d = (uint32_t*)sw_ckeys.p;
   uint32_t* bloom_d = cbits_d + (1u << SW_GBITS_MAX) / 32;
+  uint64_t* ckeys_d = (uint64_t*)(bloom_d + (1u << SW_BLOOM_LOG) / 32);
+  const uint64_t n64 = (d.n + 63) / 64;
+  uint64_t* sflag_d = (uint64_t*)sw_status.p;
+  unsigned long long* tcount_d = (unsigned long long*)(sflag_d + n64 + 32);
+  unsigned long long* bsum_d = tcount_d + n64 + 32;
   for (int l = l0; l < l1; l++) {
     const bool top = l == 0;
     SwList in;
@@ -517,15 +524,17 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1) {
     SwPreArgs pa{in, mdev, n, pmax, top ? (const uint8_t*)state.p : nullptr,
                  (SwRec*)sw_rec.p, (uint32_t*)sw_rk.p, (uint8_t*)sw_rp.p,
                  gtab0 + (size_t)(l & 1) * (1ull << SW_GBITS_MAX), sw_gbits(l),
-                 1u << (sw_gbits(l) - 1),
-                 (uint32_t*)sw_rtid.p, (SwTile*)sw_tinfo.p, abandon, err};
+                 1u << (sw_gbits(l) - 1), (uint32_t*)sw_ids.p,
+                 (uint32_t*)sw_rtid.p, (SwTile*)sw_tinfo.p, abandon, err, nullptr};
+    if (sw_debug && l < 4) pa.dbg = (uint64_t*)sw_dbg.p + 4096 + 4 * 256 * 8 + (size_t)l * 64 * 8;
+    launch_sw_ids(pa, (unsigned)std::min<uint64_t>(pa.budget / 256, 4ull * n_cu), stream);
     launch_sw_pre(pa, (unsigned)std::min<uint64_t>(tiles, n_cu), stream);
     SwSeqArgs sa{mdev, n, pmax, top ? SW_CAP0 : SW_CAP, top ? 1 : 0,
                  (const SwRec*)sw_rec.p, (const uint32_t*)sw_rk.p, (const uint8_t*)sw_rp.p,
                  gtab0 + (size_t)(l & 1) * (1ull << SW_GBITS_MAX), sw_gbits(l),
                  (const uint32_t*)sw_rtid.p, (const SwTile*)sw_tinfo.p, (uint8_t*)state.p, (uint8_t*)hasw.p,
-                 cbits_d, bloom_d, lv, lv + 1, (uint32_t*)out.off.p,
-                 (unsigned long long*)sw_status.p, status_n, abandon, err, nullptr};
+                 cbits_d, ckeys_d, bloom_d, lv, lv + 1, (uint32_t*)out.off.p, abandon, err,
+                 nullptr};
     if (sw_debug && l < 4) sa.dbg = (uint64_t*)sw_dbg.p + (size_t)l * 1024;
     launch_sw_seq(sa, stream);
     if (top && profiling) CK(hipEventRecord(pev[1], stream));
@@ -540,6 +549,11 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1) {
     fa.gbits = sw_gbits(l);
     fa.cbits = cbits_d;
     fa.bloom = bloom_d;
+    fa.ckeys = ckeys_d;
+    fa.sflag = sflag_d;
+    fa.tcount = tcount_d;
+    fa.bsum = bsum_d;
+    fa.nblocks = fgrid;
     fa.lv = lv;
     fa.lv_next = lv + 1;
     fa.state = (uint8_t*)state.p;
@@ -548,7 +562,6 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1) {
     fa.off_out = (uint32_t*)out.off.p;
     fa.keys_out = (uint64_t*)out.keys.p;
     fa.acc_out = (uint8_t*)out.acctype.p;
-    fa.status = (unsigned long long*)sw_status.p;
     fa.abandon = abandon;
     fa.abandon_out = abandon;
     // hand the survivors to the round solver when the committed keys stop
@@ -561,6 +574,8 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1) {
     fa.err = err;
     fa.dbg = (sw_debug && l < 4) ? (uint64_t*)sw_dbg.p + 4096 + (size_t)l * 256 * 8 : nullptr;
     launch_sw_filter(fa, fgrid, stream);
+    launch_sw_scan(fa, stream);
+    launch_sw_compact(fa, fgrid, stream);
     if (top && profiling) CK(hipEventRecord(pev[2], stream));
   }
   CK(hipGetLastError());
@@ -751,7 +766,7 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
     }
     const SwLevel* hc = (const SwLevel*)((const char*)hmisc + SW_HCTL);
     if (sw_debug) {
-      std::vector<uint64_t> dv(4096 + 4 * 256 * 8);
+      std::vector<uint64_t> dv(4096 + 4 * 256 * 8 + 4 * 64 * 8);
       CK(hipMemcpy(dv.data(), sw_dbg.p, dv.size() * 8, hipMemcpyDeviceToHost));
       for (int l = 0; l < 4; l++) {
         const uint64_t* t = dv.data() + l * 1024;
@@ -781,6 +796,27 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
             fw += x[4] - x[3];
             nwc++;
           }
+        }
+        {
+          const uint64_t* pp = dv.data() + 4096 + 4 * 256 * 8 + l * 64 * 8;
+          double q1 = 0, q2 = 0, q3 = 0, q4 = 0, q5 = 0, q6 = 0, q7 = 0;
+          int np = 0;
+          for (int w = 0; w < 64 && pp[w * 8 + 5]; w++) {
+            const uint64_t* x = pp + w * 8;
+            if (!x[4]) continue;
+            q1 += x[1] - x[0];
+            q2 += x[2] - x[1];
+            q3 += x[3] - x[2];
+            q4 += x[4] - x[3];
+            q5 += x[5] - x[0];
+            q6 += x[6] - x[1];
+            q7 += x[7] - x[6];
+            np++;
+          }
+          if (np)
+            fprintf(stderr, "  pre L%d: %d WGs, offsets %.0f keys+ids %.0f (keys+search %.0f, "
+                            "bucket+cas(thread0) %.0f) masks+out %.0f tail %.0f WG total %.0f\n",
+                    l, np, q1 / np, q2 / np, q6 / np, q7 / np, q3 / np, q4 / np, q5 / np);
         }
         if (nw)
           fprintf(stderr, "  filter L%d: %d WGs, chunks/WG %.2f, init %.0f, chunk local %.0f "

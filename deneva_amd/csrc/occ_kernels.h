@@ -225,32 +225,33 @@ struct AsyncArgs {
 void launch_async(const AsyncArgs& a, uint64_t cap, unsigned n_cu, hipStream_t st);
 
 // ---- sweep solver (occ_sweep.hip)
-constexpr uint32_t SW_T = 64;        // txns per sequential tile (one dependency mask bit each)
-constexpr uint32_t SW_TA = 4096;     // accesses per tile (SW_T x MAX_ROW_PER_TXN)
+constexpr uint32_t SW_T = 128;       // txns per sequential tile (two 64-bit mask words)
+constexpr uint32_t SW_TA = 8192;     // accesses per tile (SW_T x MAX_ROW_PER_TXN)
+constexpr uint32_t SW_WA = 4096;     // accesses of one filter wave (64 txns x MAX_ROW_PER_TXN)
 constexpr uint32_t SW_CHUNK = 256;   // txns per filter chunk (4 waves x 64)
 constexpr uint32_t SW_BLOOM_LOG = 17; // Bloom filter of a level's committed keys (16 KiB)
 constexpr int SW_MAX_LEVEL = 24;
-constexpr uint32_t SW_PMAX_TILES = 1024;  // tiles one serial pass may decide (65,536 txns)
+constexpr uint32_t SW_PMAX_TILES = 512;  // tiles one serial pass may decide (65,536 txns)
 
-struct SwTile {      // per 64-txn tile of a level's solve range
-  uint32_t nt, cnt;  // txns, accesses
-  uint64_t prekill;  // txns decided before the solver (history window)
-  uint64_t hasw;     // txns with a write
+struct SwTile {         // per 128-txn tile of a level's solve range
+  uint32_t nt, cnt;     // txns, accesses
+  uint64_t prekill[2];  // txns decided before the solver (history window)
+  uint64_t hasw[2];     // txns with a write
 };
-// One 64-txn tile as k_sw_seq copies it into LDS (6 KiB, 16-B multiple).
+// One 128-txn tile as k_sw_seq copies it into LDS (12,864 B, 16-B multiple).
 // Keys are replaced by their slot in the level's global key table (`gtab`),
 // so the serial pass keeps its committed set as an LDS bitmap over slots.
 struct SwRec {
-  uint32_t id[1024];   // slot ids of the tile's first 1024 accesses (more: id_ovf)
-  uint64_t dep[64];    // intra-tile dependency mask per txn
-  uint32_t span[64];   // (start - A0) | len << 16 per txn
-  uint8_t pk[1024];    // local txn | W << 7 per access
-  uint32_t nt, cnt;    // cnt == SW_STOP: the level's access budget ends before this tile
-  uint64_t prekill, hasw;
-  uint8_t pad[232];
+  uint32_t id[2048];     // slot ids of the tile's first 2048 accesses (more: id_ovf)
+  uint64_t dep[2][128];  // intra-tile dependency masks: dep[h][t] = writers 64h.. of t
+  uint32_t span[128];    // (start - A0) | len << 16 per txn
+  uint8_t pk[2048];      // local txn | W << 7 per access
+  uint32_t nt, cnt;      // cnt == SW_STOP: the level's access budget ends before this tile
+  uint64_t prekill[2], hasw[2];
+  uint8_t pad[24];
 };
-constexpr uint32_t SW_REC_ACC = 1024;
-constexpr uint32_t SW_SEQ_B = 8;  // tiles per LDS super-step of k_sw_seq
+constexpr uint32_t SW_REC_ACC = 2048;
+constexpr uint32_t SW_SEQ_B = 4;  // tiles per LDS super-step of k_sw_seq
 constexpr uint32_t SW_STOP = 0xFFFFFFFFu;
 constexpr uint32_t SW_GBITS_MAX = 19;  // key-table slots of one level (LDS bitmap: 64 KiB)
 struct SwLevel {     // device control words of one level
@@ -280,10 +281,12 @@ struct SwPreArgs {
   uint64_t* gtab;         // [1 << gbits] key table (KEY_EMPTY-filled), slot = key id
   uint32_t gbits;
   uint32_t budget;        // accesses the level's tiles may hold (gtab at <= 50% load)
+  uint32_t* ids;          // [budget] key id per access of the serial range (k_sw_ids)
   uint32_t* rtid;         // [tiles * SW_T]
   SwTile* tinfo;          // [tiles]
   const uint32_t* abandon;
   uint32_t* err;
+  uint64_t* dbg;          // per-workgroup clock stamps (DCC_SW_DEBUG) or null
 };
 struct SwSeqArgs {
   const uint32_t* m_dev;
@@ -301,16 +304,16 @@ struct SwSeqArgs {
   uint8_t* state;
   uint8_t* hasw;
   uint32_t* cbits_out;    // out: committed ids (bitmap over the key table's slots)
+  uint64_t* ckeys_out;    // out: the committed keys (lv->ccount of them)
   uint32_t* bloom_out;    // out: Bloom filter of the committed keys
   SwLevel* lv;
   SwLevel* lv_next;
   uint32_t* next_off;     // the next list's offsets (off[0] = 0 written here)
-  unsigned long long* status;  // the level filter's look-back words, zeroed here
-  uint32_t status_n;
   const uint32_t* abandon;
   uint32_t* err;
   uint64_t* dbg;          // per-tile clock stamps (DCC_SW_DEBUG) or null
 };
+// k_sw_filter / k_sw_scan / k_sw_compact (one argument block for the three)
 struct SwFilterArgs {
   SwList in;
   const uint32_t* m_dev;
@@ -318,19 +321,23 @@ struct SwFilterArgs {
   int cand_state;         // identity list: only UNDECIDED txns are candidates
   int write_hasw;
   uint32_t level;
-  const uint64_t* gtab;   // the level's key table / committed ids / Bloom filter
-  uint32_t gbits;         // (k_sw_seq's outputs): the committed set C
+  const uint64_t* gtab;   // the level's key table / committed ids / Bloom filter /
+  uint32_t gbits;         // committed keys (k_sw_seq's outputs): the committed set C
   const uint32_t* cbits;
   const uint32_t* bloom;
+  const uint64_t* ckeys;
   SwLevel* lv;
   SwLevel* lv_next;
   uint8_t* state;
   uint8_t* hasw;
+  uint64_t* sflag;        // survivor bit per list position past pos (64 per word)
+  unsigned long long* tcount;  // per 64-txn tile: survivors << 34 | their accesses
+  unsigned long long* bsum;    // per filter workgroup: its tiles' total (scanned in place)
+  uint32_t nblocks;            // filter / compaction grid
   uint32_t* tid_out;
   uint32_t* off_out;
   uint64_t* keys_out;
   uint8_t* acc_out;
-  unsigned long long* status;
   const uint32_t* abandon;
   uint32_t* abandon_out;  // = level + 1 when the survivors stay too many
   uint32_t abandon_min, abandon_num, abandon_den;
@@ -339,9 +346,12 @@ struct SwFilterArgs {
   uint32_t* err;
   uint64_t* dbg;          // per-workgroup clock stamps (DCC_SW_DEBUG) or null
 };
+void launch_sw_ids(const SwPreArgs& a, unsigned grid, hipStream_t st);
 void launch_sw_pre(const SwPreArgs& a, unsigned grid, hipStream_t st);
 void launch_sw_seq(const SwSeqArgs& a, hipStream_t st);
 void launch_sw_filter(const SwFilterArgs& a, unsigned grid, hipStream_t st);
+void launch_sw_scan(const SwFilterArgs& a, hipStream_t st);
+void launch_sw_compact(const SwFilterArgs& a, unsigned grid, hipStream_t st);
 
 // launchers (occ_kernels.hip)
 void launch_prep(const uint32_t* off, uint64_t n, const uint8_t* at, uint64_t nnz, uint64_t p,

@@ -23,10 +23,10 @@ def sw(engine):
     engine.set_option(OPT_SOLVER, 3)
     yield engine
     engine.set_option(OPT_SOLVER, 0)
-    engine.set_option(OPT_SWEEP_LEVELS, 6)
+    engine.set_option(OPT_SWEEP_LEVELS, 4)
 
 
-def run(engine, b, levels=6, hist=None, tnc=0):
+def run(engine, b, levels=4, hist=None, tnc=0):
     engine.set_option(OPT_SWEEP_LEVELS, levels)
     engine.tnc = tnc
     rc, tn, st = engine.occ_validate_epoch(b, want_tn=True)
