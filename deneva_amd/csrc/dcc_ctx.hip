@@ -118,6 +118,8 @@ extern "C" int dcc_init(dcc_ctx** out, int device_id) {
   for (auto& e : ctx->pev) CK(hipEventCreate(&e));
   CK(hipHostMalloc((void**)&ctx->hmisc, 16384, hipHostMallocDefault));
   CK(hipHostMalloc((void**)&ctx->hpart, 1 << 16, hipHostMallocDefault));
+  CK(hipHostGetDevicePointer(&ctx->hmisc_dev, ctx->hmisc, 0));
+  CK(hipHostGetDevicePointer(&ctx->hpart_dev, ctx->hpart, 0));
   int rc = ctx->misc.ensure(ctx, 16384, "misc");
   if (!rc) rc = ctx->part.ensure(ctx, 1 << 16, "partials");
   if (rc) {
@@ -195,8 +197,7 @@ std::vector<DevBuf*> dcc_ctx::all_bufs() {
                             &cv_gsize, &cv_done, &cv_maxl, &cv_seq_b, &cv_ok, &cv_len,
                             &cv_off2, &cv_tsum, &gst, &hasw_scr, &cset_tab, &cset_keys,
                             &a_cnt, &a_writers, &a_big, &a_st32, &sw_ctl, &sw_status, &sw_dbg,
-                            &sw_ckeys, &sw_gtab, &sw_ids, &sw_rec, &sw_rk, &sw_rp, &sw_rtid,
-                            &sw_tinfo};
+                            &sw_ckeys, &sw_gtab, &sw_rec, &sw_rk};
   for (auto& sb : sw_list)
     for (DevBuf* b : {&sb.tid, &sb.off, &sb.keys, &sb.acctype, &sb.state}) v.push_back(b);
   for (auto& sb : subs)

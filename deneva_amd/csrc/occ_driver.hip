@@ -444,7 +444,6 @@ int dcc_ctx::occ_peel(const SubProb& sp, uint32_t maxlen, int level, uint32_t& r
 static constexpr size_t SW_PREP_OFF = 32768;  // prep partials inside `part` / `hpart`
 static constexpr size_t SW_HCTL = 13312;      // control-block copy inside `hmisc`
 static constexpr uint32_t SW_PMAX_TOP = 65536;
-static constexpr uint32_t SW_CAP0 = 0x7FFFFFFFu, SW_CAP = 0x7FFFFFFFu;  // C is unbounded (bitmap)
                                                           // the serial pass's LDS set)
 static uint32_t sw_pmax(int level) {
   return level >= 6 ? SW_PMAX_TOP : (1024u << level);
@@ -471,13 +470,9 @@ int dcc_ctx::sweep_reserve(const DevBatch& d) {
   CR(sw_ckeys.ensure(this, ((1ull << SW_GBITS_MAX) / 32 + (1ull << SW_BLOOM_LOG) / 32) * 4 +
                                 (1ull << SW_GBITS_MAX) * 8,
                      "sweep committed set"));
-  CR(sw_rec.ensure(this, (tiles + SW_SEQ_B) * sizeof(SwRec), "sweep tile records"));
-  CR(sw_rk.ensure(this, tiles * (SW_TA - SW_REC_ACC) * 4, "sweep tile key ids"));
+  CR(sw_rec.ensure(this, tiles * sizeof(SwRec), "sweep tile records"));
+  CR(sw_rk.ensure(this, tiles * SW_T * SW_OVN * 4, "sweep overflow key ids"));
   CR(sw_gtab.ensure(this, 2 * (1ull << SW_GBITS_MAX) * 8, "sweep key tables"));
-  CR(sw_rp.ensure(this, tiles * (SW_TA - SW_REC_ACC), "sweep tile bytes"));
-  CR(sw_rtid.ensure(this, tiles * SW_T * 4, "sweep tile txns"));
-  CR(sw_ids.ensure(this, (1ull << (SW_GBITS_MAX - 1)) * 4, "sweep key ids"));
-  CR(sw_tinfo.ensure(this, tiles * sizeof(SwTile), "sweep tile info"));
   for (SubBufs& b : sw_list) {
     CR(b.tid.ensure(this, d.n * 4 + 16, "sweep list tid"));
     CR(b.off.ensure(this, (d.n + 1) * 4 + 16, "sweep list offsets"));
@@ -522,17 +517,13 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1) {
     const uint32_t pmax = sw_pmax(l);
     const uint64_t tiles = (std::min<uint64_t>(pmax, d.n) + SW_T - 1) / SW_T;
     SwPreArgs pa{in, mdev, n, pmax, top ? (const uint8_t*)state.p : nullptr,
-                 (SwRec*)sw_rec.p, (uint32_t*)sw_rk.p, (uint8_t*)sw_rp.p,
+                 (SwRec*)sw_rec.p, (uint32_t*)sw_rk.p,
                  gtab0 + (size_t)(l & 1) * (1ull << SW_GBITS_MAX), sw_gbits(l),
-                 1u << (sw_gbits(l) - 1), (uint32_t*)sw_ids.p,
-                 (uint32_t*)sw_rtid.p, (SwTile*)sw_tinfo.p, abandon, err, nullptr};
-    if (sw_debug && l < 4) pa.dbg = (uint64_t*)sw_dbg.p + 4096 + 4 * 256 * 8 + (size_t)l * 64 * 8;
-    launch_sw_ids(pa, (unsigned)std::min<uint64_t>(pa.budget / 256, 4ull * n_cu), stream);
-    launch_sw_pre(pa, (unsigned)std::min<uint64_t>(tiles, n_cu), stream);
-    SwSeqArgs sa{mdev, n, pmax, top ? SW_CAP0 : SW_CAP, top ? 1 : 0,
-                 (const SwRec*)sw_rec.p, (const uint32_t*)sw_rk.p, (const uint8_t*)sw_rp.p,
+                 1u << (sw_gbits(l) - 1), abandon, err};
+    launch_sw_pre(pa, (unsigned)tiles, stream);
+    SwSeqArgs sa{mdev, n, pmax, top ? 1 : 0, (const SwRec*)sw_rec.p, (const uint32_t*)sw_rk.p,
                  gtab0 + (size_t)(l & 1) * (1ull << SW_GBITS_MAX), sw_gbits(l),
-                 (const uint32_t*)sw_rtid.p, (const SwTile*)sw_tinfo.p, (uint8_t*)state.p, (uint8_t*)hasw.p,
+                 (uint8_t*)state.p, (uint8_t*)hasw.p,
                  cbits_d, ckeys_d, bloom_d, lv, lv + 1, (uint32_t*)out.off.p, abandon, err,
                  nullptr};
     if (sw_debug && l < 4) sa.dbg = (uint64_t*)sw_dbg.p + (size_t)l * 1024;
@@ -614,14 +605,22 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   CR(state.ensure(this, d.n + 16, "state"));
   CR(hasw.ensure(this, d.n + 16, "hasw"));
   CR(rc.ensure(this, d.n + 16, "rc"));
-  uint32_t* one = (uint32_t*)misc.p + 1;
-  CK(hipMemsetAsync(misc.p, 0, 64, stream));
-  CK(hipMemsetAsync((char*)misc.p + MISC_ASYNC + 8, 0, 4, stream));  // async pass count
-  CK(hipMemsetAsync(one, 0x01, 1, stream));
-  CK(hipMemsetAsync(state.p, 0, d.n, stream));
-  if (sweep) {
-    CK(hipMemsetAsync(sw_ctl.p, 0, sw_ctl_bytes(), stream));
-    CK(hipMemsetAsync(sw_gtab.p, 0xFF, (1ull << sw_gbits(0)) * 8, stream));
+  {
+    // one launch: error word 0, the constant-one word 1, words 2..15, the
+    // async pass count, the state bytes, and for the sweep its control block
+    // and level-0 key table
+    uint32_t* mw = (uint32_t*)misc.p;
+    FillArgs fa{};
+    fa.job[fa.n++] = FillJob{mw, 1, 0u};
+    fa.job[fa.n++] = FillJob{mw + 1, 1, 1u};
+    fa.job[fa.n++] = FillJob{mw + 2, 14, 0u};
+    fa.job[fa.n++] = FillJob{(uint32_t*)((char*)misc.p + MISC_ASYNC + 8), 1, 0u};
+    fa.job[fa.n++] = FillJob{(uint32_t*)state.p, (d.n + 3) / 4, 0u};  // state holds n + 16
+    if (sweep) {
+      fa.job[fa.n++] = FillJob{(uint32_t*)sw_ctl.p, sw_ctl_bytes() / 4, 0u};
+      fa.job[fa.n++] = FillJob{(uint32_t*)sw_gtab.p, (1ull << sw_gbits(0)) * 2, 0xFFFFFFFFu};
+    }
+    launch_fill(fa, stream);
   }
 
   // ---- history window pre-pass (occ.cpp:160-180)
@@ -685,17 +684,22 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
       if (out_rc) CK(hipMemcpyAsync(out_rc, rc.p, d.n, hipMemcpyDeviceToHost, stream));
       if (out_tn) CK(hipMemcpyAsync(out_tn, tn.p, d.n * 8, hipMemcpyDeviceToHost, stream));
     }
-    CK(hipMemcpyAsync(hmisc, misc.p, 64, hipMemcpyDeviceToHost, stream));
-    if (async_passes_dev)
-      CK(hipMemcpyAsync((char*)hmisc + MISC_ASYNC, (char*)misc.p + MISC_ASYNC, 16,
-                        hipMemcpyDeviceToHost, stream));
+    // everything the host reads back, in one launch into pinned memory
+    GatherArgs ga{};
+    auto job = [&](void* hdst_dev, const void* src, size_t bytes) {
+      ga.job[ga.n++] = CopyJob{(const uint32_t*)src, (uint32_t*)hdst_dev, (uint32_t)(bytes / 4)};
+    };
+    job(hmisc_dev, misc.p, 64);
+    job((char*)hmisc_dev + MISC_BARS, (char*)misc.p + MISC_BARS, CTR_RING * 16);
+    if (async_passes_dev) job((char*)hmisc_dev + MISC_ASYNC, (char*)misc.p + MISC_ASYNC, 16);
     if (sweep) {
-      CK(hipMemcpyAsync((char*)hmisc + SW_HCTL, sw_ctl.p, sw_ctl_bytes(), hipMemcpyDeviceToHost,
-                        stream));
-      CK(hipMemcpyAsync((char*)hpart + SW_PREP_OFF, (char*)part.p + SW_PREP_OFF,
-                        PREP_BLOCKS * sizeof(PrepPart), hipMemcpyDeviceToHost, stream));
+      job((char*)hmisc_dev + SW_HCTL, sw_ctl.p, sw_ctl_bytes());
+      job((char*)hpart_dev + SW_PREP_OFF, (char*)part.p + SW_PREP_OFF,
+          PREP_BLOCKS * sizeof(PrepPart));
     }
-    CR(read_partials(FINAL_BLOCKS * sizeof(FinalPart)));
+    job(hpart_dev, part.p, FINAL_BLOCKS * sizeof(FinalPart));
+    launch_gather(ga, stream);
+    CK(hipGetLastError());
     CK(hipStreamSynchronize(stream));
     return DCC_OK;
   };
@@ -729,9 +733,13 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
         const int l1 = next_level + (int)sw_levels;
         CR(sweep_enqueue(d, next_level, l1));
         next_level = l1;
-        CK(hipMemcpyAsync((char*)hmisc + SW_HCTL, sw_ctl.p, sw_ctl_bytes(),
-                          hipMemcpyDeviceToHost, stream));
-        CK(hipMemcpyAsync(hmisc, misc.p, 64, hipMemcpyDeviceToHost, stream));
+        GatherArgs ga{};
+        ga.job[ga.n++] = CopyJob{(const uint32_t*)sw_ctl.p,
+                                 (uint32_t*)((char*)hmisc_dev + SW_HCTL),
+                                 (uint32_t)(sw_ctl_bytes() / 4)};
+        ga.job[ga.n++] = CopyJob{(const uint32_t*)misc.p, (uint32_t*)hmisc_dev, 16};
+        launch_gather(ga, stream);
+        CK(hipGetLastError());
         CK(hipStreamSynchronize(stream));
         again = true;
         continue;
@@ -769,18 +777,15 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
       std::vector<uint64_t> dv(4096 + 4 * 256 * 8 + 4 * 64 * 8);
       CK(hipMemcpy(dv.data(), sw_dbg.p, dv.size() * 8, hipMemcpyDeviceToHost));
       for (int l = 0; l < 4; l++) {
+        // k_sw_seq stamps (s_memrealtime, 100 MHz): start, init done, loop
+        // done, decisions written, end; consumer wait polls; tiles
         const uint64_t* t = dv.data() + l * 1024;
-        double ph[4] = {0, 0, 0, 0};
-        int nt = 0;
-        for (int k = 0; k < 128 && t[k * 4 + 3]; k++, nt++) {
-          ph[0] += t[k * 4 + 1] - t[k * 4];
-          ph[1] += t[k * 4 + 2] - t[k * 4 + 1];
-          ph[2] += t[k * 4 + 3] - t[k * 4 + 2];
-          if (k + 1 < 128 && t[k * 4 + 4]) ph[3] += t[k * 4 + 4] - t[k * 4 + 3];
-        }
-        if (nt)
-          fprintf(stderr, "sweep L%d: %d tiles, cycles/tile probe %.0f resolve %.0f insert %.0f "
-                          "between %.0f\n", l, nt, ph[0] / nt, ph[1] / nt, ph[2] / nt, ph[3] / nt);
+        if (t[4])
+          fprintf(stderr, "sweep L%d seq: %llu tiles, init %.2f us, loop %.2f us, decisions "
+                          "%.2f us, C out %.2f us, consumer waits %llu, producer waits %llu\n",
+                  l, (unsigned long long)t[6], (t[1] - t[0]) * 0.01, (t[2] - t[1]) * 0.01,
+                  (t[3] - t[2]) * 0.01, (t[4] - t[3]) * 0.01, (unsigned long long)t[5],
+                  (unsigned long long)t[7]);
         // filter: per workgroup init / first chunk local / look-back / writes / total
         const uint64_t* f = dv.data() + 4096 + l * 256 * 8;
         double fi = 0, fl = 0, fb = 0, fw = 0, ft = 0, nc = 0;
@@ -841,8 +846,8 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   if (async_passes_dev) rounds += *(const uint32_t*)((const char*)hmisc + MISC_ASYNC + 8);
   {
     // barrier timeout words (third word of each GridBar in the ring)
-    std::vector<uint32_t> bw(CTR_RING * 4);
-    CK(hipMemcpy(bw.data(), (char*)misc.p + MISC_BARS, CTR_RING * 16, hipMemcpyDeviceToHost));
+    // (read back with the epoch's gather)
+    const uint32_t* bw = (const uint32_t*)((const char*)hmisc + MISC_BARS);
     for (uint32_t q = 0; q < CTR_RING; q++)
       if (bw[q * 4 + 2]) return fail(DCC_EIO, "grid barrier timed out (grid not co-resident)");
   }

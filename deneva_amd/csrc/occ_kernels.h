@@ -225,35 +225,40 @@ struct AsyncArgs {
 void launch_async(const AsyncArgs& a, uint64_t cap, unsigned n_cu, hipStream_t st);
 
 // ---- sweep solver (occ_sweep.hip)
-constexpr uint32_t SW_T = 128;       // txns per sequential tile (two 64-bit mask words)
-constexpr uint32_t SW_TA = 8192;     // accesses per tile (SW_T x MAX_ROW_PER_TXN)
+constexpr uint32_t SW_T = 64;        // txns per serial tile (one 64-bit mask word)
+constexpr uint32_t SW_TA = 4096;     // accesses per tile (SW_T x MAX_ROW_PER_TXN)
+constexpr uint32_t SW_IDN = 16;      // key ids per txn held in the tile record (more: id_ovf)
+constexpr uint32_t SW_OVN = 48;      // key ids per txn in the overflow area (MAX_ROW_PER_TXN - SW_IDN)
 constexpr uint32_t SW_WA = 4096;     // accesses of one filter wave (64 txns x MAX_ROW_PER_TXN)
 constexpr uint32_t SW_CHUNK = 256;   // txns per filter chunk (4 waves x 64)
 constexpr uint32_t SW_BLOOM_LOG = 17; // Bloom filter of a level's committed keys (16 KiB)
 constexpr int SW_MAX_LEVEL = 24;
-constexpr uint32_t SW_PMAX_TILES = 512;  // tiles one serial pass may decide (65,536 txns)
-
-struct SwTile {         // per 128-txn tile of a level's solve range
-  uint32_t nt, cnt;     // txns, accesses
-  uint64_t prekill[2];  // txns decided before the solver (history window)
-  uint64_t hasw[2];     // txns with a write
-};
-// One 128-txn tile as k_sw_seq copies it into LDS (12,864 B, 16-B multiple).
-// Keys are replaced by their slot in the level's global key table (`gtab`),
-// so the serial pass keeps its committed set as an LDS bitmap over slots.
-struct SwRec {
-  uint32_t id[2048];     // slot ids of the tile's first 2048 accesses (more: id_ovf)
-  uint64_t dep[2][128];  // intra-tile dependency masks: dep[h][t] = writers 64h.. of t
-  uint32_t span[128];    // (start - A0) | len << 16 per txn
-  uint8_t pk[2048];      // local txn | W << 7 per access
-  uint32_t nt, cnt;      // cnt == SW_STOP: the level's access budget ends before this tile
-  uint64_t prekill[2], hasw[2];
-  uint8_t pad[24];
-};
-constexpr uint32_t SW_REC_ACC = 2048;
-constexpr uint32_t SW_SEQ_B = 4;  // tiles per LDS super-step of k_sw_seq
-constexpr uint32_t SW_STOP = 0xFFFFFFFFu;
+constexpr uint32_t SW_PMAX_TILES = 1024;  // tiles one serial pass may decide (65,536 txns)
 constexpr uint32_t SW_GBITS_MAX = 19;  // key-table slots of one level (LDS bitmap: 64 KiB)
+// A record entry is a key id (slot of the level's key table) packed for the
+// serial pass's LDS bitmap: byte address of the bitmap word << 8 | WR << 5 |
+// bit.  The shift instructions use only the low 5 bits of their shift operand,
+// so a probe is: word at (e >> 8), shifted right by e.
+__host__ __device__ constexpr uint32_t sw_pack(uint32_t id, bool w) {
+  return ((id >> 5) << 10) | (w ? 32u : 0u) | (id & 31u);
+}
+__host__ __device__ constexpr uint32_t sw_unpack(uint32_t e) { return ((e >> 10) << 5) | (e & 31u); }
+// an unused record entry: one past the largest table slot, i.e. the
+// always-zero word that ends the serial pass's committed bitmap
+constexpr uint32_t SW_ID_NONE = 1u << SW_GBITS_MAX;
+constexpr uint32_t SW_E_NONE = sw_pack(SW_ID_NONE, false);
+// per-txn meta word of a tile record: flags, and the txn's length in bits 8-15
+constexpr uint32_t SWM_VALID = 1, SWM_PRE = 2, SWM_HASW = 4, SWM_LONG = 8, SWM_STOP = 16;
+// One 64-txn tile of a level's serial range as k_sw_seq reads it (5,120 B).
+// Txn-major: lane t of the serial wave loads its txn's 16 key ids with four
+// 16-B loads.  Keys are replaced by their slot in the level's global key table
+// (`gtab`), so the serial pass keeps the committed set as an LDS bitmap.
+struct SwRec {
+  uint32_t id[SW_T][SW_IDN];  // sw_pack(key id, WR); SW_E_NONE past the txn's length
+  uint64_t dep[SW_T];         // dep[t]: earlier txns of the tile writing a key t touches
+  uint32_t meta[SW_T];        // SWM_* (SWM_STOP on every txn: the access budget ends here)
+  uint32_t rtid[SW_T];        // original txn index
+};
 struct SwLevel {     // device control words of one level
   uint32_t m;        // list length (written by the previous level's filter)
   uint32_t acc;      // accesses of the list
@@ -275,32 +280,23 @@ struct SwPreArgs {
   uint32_t m_host;
   uint32_t p_max;
   const uint8_t* state;   // identity list: decisions made before the solver, else null
-  SwRec* rec;             // [tiles + SW_SEQ_B]
-  uint32_t* id_ovf;       // [tiles * (SW_TA - SW_REC_ACC)] accesses beyond the record
-  uint8_t* rp_ovf;
+  SwRec* rec;             // [tiles]
+  uint32_t* id_ovf;       // [tiles][SW_T][SW_OVN] key ids past SW_IDN
   uint64_t* gtab;         // [1 << gbits] key table (KEY_EMPTY-filled), slot = key id
   uint32_t gbits;
   uint32_t budget;        // accesses the level's tiles may hold (gtab at <= 50% load)
-  uint32_t* ids;          // [budget] key id per access of the serial range (k_sw_ids)
-  uint32_t* rtid;         // [tiles * SW_T]
-  SwTile* tinfo;          // [tiles]
   const uint32_t* abandon;
   uint32_t* err;
-  uint64_t* dbg;          // per-workgroup clock stamps (DCC_SW_DEBUG) or null
 };
 struct SwSeqArgs {
   const uint32_t* m_dev;
   uint32_t m_host;
   uint32_t p_max;
-  uint32_t cap;           // committed keys the level may collect
   int write_hasw;
   const SwRec* rec;
   const uint32_t* id_ovf;
-  const uint8_t* rp_ovf;
   const uint64_t* gtab;
   uint32_t gbits;
-  const uint32_t* rtid;
-  const SwTile* tinfo;
   uint8_t* state;
   uint8_t* hasw;
   uint32_t* cbits_out;    // out: committed ids (bitmap over the key table's slots)
@@ -346,12 +342,36 @@ struct SwFilterArgs {
   uint32_t* err;
   uint64_t* dbg;          // per-workgroup clock stamps (DCC_SW_DEBUG) or null
 };
-void launch_sw_ids(const SwPreArgs& a, unsigned grid, hipStream_t st);
 void launch_sw_pre(const SwPreArgs& a, unsigned grid, hipStream_t st);
 void launch_sw_seq(const SwSeqArgs& a, hipStream_t st);
 void launch_sw_filter(const SwFilterArgs& a, unsigned grid, hipStream_t st);
 void launch_sw_scan(const SwFilterArgs& a, hipStream_t st);
 void launch_sw_compact(const SwFilterArgs& a, unsigned grid, hipStream_t st);
+
+// Several word fills in one launch (replaces a run of hipMemsetAsync calls,
+// each of which costs a dispatch and an idle gap on the stream).
+struct FillJob {
+  uint32_t* p;
+  uint64_t words;
+  uint32_t value;
+};
+struct FillArgs {
+  FillJob job[8];
+  uint32_t n;
+};
+void launch_fill(const FillArgs& a, hipStream_t st);
+// Several small device -> pinned-host copies in one launch (word granular):
+// the control words, counters and partials the host reads after an epoch.
+struct CopyJob {
+  const uint32_t* src;
+  uint32_t* dst;  // device-visible pointer of pinned host memory
+  uint32_t words;
+};
+struct GatherArgs {
+  CopyJob job[8];
+  uint32_t n;
+};
+void launch_gather(const GatherArgs& a, hipStream_t st);
 
 // launchers (occ_kernels.hip)
 void launch_prep(const uint32_t* off, uint64_t n, const uint8_t* at, uint64_t nnz, uint64_t p,

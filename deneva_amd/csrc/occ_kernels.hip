@@ -26,6 +26,8 @@
 // and the per-txn reduction is a ballot segmented OR (no per-lane LDS atomics).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "dcc_device.h"
 #include "occ_kernels.h"
 
@@ -878,6 +880,29 @@ void launch_pub(const PubArgs& a, uint64_t m_bound, unsigned max_grid, hipStream
   if (g > max_grid) g = max_grid;
   k_pub<ROUND_CAP, PUB_WAVES><<<g ? g : 1, PUB_WAVES * 64, 0, st>>>(a);
 }
+__global__ __launch_bounds__(256) void k_fill(FillArgs a) {
+  const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x, stride = (uint64_t)gridDim.x * 256;
+  for (uint32_t q = 0; q < a.n; q++) {
+    const FillJob& f = a.job[q];
+    for (uint64_t i = t; i < f.words; i += stride) f.p[i] = f.value;
+  }
+}
+void launch_fill(const FillArgs& a, hipStream_t st) {
+  uint64_t mx = 1;
+  for (uint32_t q = 0; q < a.n; q++) mx = a.job[q].words > mx ? a.job[q].words : mx;
+  const unsigned grid = (unsigned)std::min<uint64_t>((mx + 255) / 256, 2048);
+  k_fill<<<grid, 256, 0, st>>>(a);
+}
+
+__global__ __launch_bounds__(256) void k_gather(GatherArgs a) {
+  for (uint32_t q = 0; q < a.n; q++) {
+    const CopyJob& c = a.job[q];
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < c.words; i += gridDim.x * 256)
+      c.dst[i] = c.src[i];
+  }
+}
+void launch_gather(const GatherArgs& a, hipStream_t st) { k_gather<<<16, 256, 0, st>>>(a); }
+
 void launch_final(const FinalArgs& a, hipStream_t st) {
   k_final<<<FINAL_BLOCKS, 256, 0, st>>>(a);
 }

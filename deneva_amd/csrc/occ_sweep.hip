@@ -12,16 +12,20 @@
 // (level 0 = the epoch in index order, level l+1 = the survivors of level l,
 // still in index order):
 //
-//   k_sw_pre     (grid)   per 64-txn tile of the list's first p_max txns:
-//                         stage the tile's keys, the local txn of every
-//                         access and the intra-tile dependency masks
-//                         dep[t] = {u < t : W_u and keys(t) intersect}
-//   k_sw_seq     (1 CU)   the exact serial decision, tile by tile, with C in
-//                         LDS: a txn dies if a key is in C or an earlier
-//                         committed txn of its tile writes one of its keys
-//                         (a bit-parallel fixed point over the 64 dep masks);
-//                         committed write keys join C.  Stops at p_max txns
-//                         or when C would outgrow its LDS table.
+//   k_sw_pre     (grid)   one 64-txn tile of the list's first p_max txns per
+//                         workgroup: key ids (slots of the level's global key
+//                         table, each distinct key entered once per tile via
+//                         an LDS map), txn-major id rows and the intra-tile
+//                         dependency masks dep[t] = {u < t : W_u and keys(t)
+//                         intersect}
+//   k_sw_seq     (1 wave) the exact serial decision, tile by tile, with C as
+//                         an LDS bitmap over key ids: a txn dies if a key is
+//                         in C or an earlier committed txn of its tile writes
+//                         one of its keys (a bit-parallel fixed point over the
+//                         64 dep masks); committed write keys join C.  No
+//                         barrier inside the loop; records are prefetched
+//                         into registers.  Stops at p_max txns or when the
+//                         level's key table budget ends.
 //   k_sw_filter  (grid)   one streaming pass over the rest of the list: a txn
 //                         touching a key of C dies (its committed writer is
 //                         earlier); the survivors are compacted in index
@@ -39,8 +43,6 @@
 
 namespace dcc {
 
-constexpr uint32_t SW_U = SW_TA / 1024;  // accesses per thread of a tile (1024 threads)
-constexpr uint32_t SW_MAP = 8192;        // LDS key -> writer-mask map of k_sw_pre
 constexpr uint32_t LB_ACC_BITS = 34;
 
 __device__ inline uint32_t sw_hash(uint64_t key, uint32_t log2s) {
@@ -217,87 +219,76 @@ __device__ inline uint32_t list_len(const uint32_t* m_dev, uint32_t m_host) {
 }
 
 // ---------------------------------------------------------------------------
-// k_sw_pre: tile records (SwRec) of list txns [0, min(m, p_max)), 128 txns
-// per tile: key ids, (local txn | W << 7) bytes, spans and the intra-tile
-// dependency masks, built in two passes over an LDS key -> writer-mask map
-// (writers 0..63, then 64..127).
-__device__ inline uint32_t map_slot(uint64_t* mkey, uint64_t key, bool insert) {
-  uint32_t h = sw_hash(key, 13);
-  for (uint32_t q = 0; q < SW_MAP; q++) {
-    if (insert) {
+// k_sw_pre: tile records (SwRec) of list txns [0, min(m, p_max)), one 64-txn
+// tile per workgroup: key ids, dependency masks, per-txn meta.  Each distinct
+// key of a tile is entered once in an LDS map (key -> writer mask, key id);
+// only its first access touches the level's global key table, so a hot key
+// costs one global CAS per tile rather than one per access.
+constexpr uint32_t PRE_MAP = 4096;       // LDS map slots (<= 2048 distinct keys per pass)
+constexpr uint32_t PRE_U = SW_TA / 1024;  // accesses per thread (1024 threads)
+
+__device__ inline uint32_t pre_map_insert(uint64_t* mkey, uint64_t key, bool& first) {
+  uint32_t h = sw_hash(key, 12);
+  for (uint32_t q = 0; q < PRE_MAP; q++) {
+    const uint64_t v = mkey[h];
+    if (v == key) {
+      first = false;
+      return h;
+    }
+    if (v == KEY_EMPTY) {
       const unsigned long long prev = atomicCAS((unsigned long long*)&mkey[h],
                                                 (unsigned long long)KEY_EMPTY,
                                                 (unsigned long long)key);
-      if (prev == KEY_EMPTY || prev == key) return h;
-    } else {
-      const uint64_t kv = mkey[h];
-      if (kv == key) return h;
-      if (kv == KEY_EMPTY) return ~0u;
+      if (prev == KEY_EMPTY) {
+        first = true;
+        return h;
+      }
+      if (prev == key) {
+        first = false;
+        return h;
+      }
     }
-    h = (h + 1) & (SW_MAP - 1);
+    h = (h + 1) & (PRE_MAP - 1);
   }
-  return ~0u;
-}
-
-// k_sw_ids: key ids of the level's serial range (list accesses [off[0],
-// min(off[lim], off[0] + budget))), spread over the whole grid: one home
-// bucket read + one CAS per access (the rare lost race or full bucket: the
-// slow path).  Random table traffic costs a CU ~4 cycles per lane, so it must
-// not sit on the one CU of a tile.
-__global__ __launch_bounds__(256) void k_sw_ids(SwPreArgs a) {
-  if (*a.abandon) return;
-  const uint32_t m = list_len(a.m_dev, a.m_host);
-  const uint32_t lim = min(m, a.p_max);
-  const uint64_t nnz = a.in.nnz;
-  const uint64_t off0 = min((uint64_t)a.in.off[0], nnz);
-  const uint64_t end = min(min((uint64_t)a.in.off[lim], nnz), off0 + a.budget);
-  for (uint64_t x = off0 + (uint64_t)blockIdx.x * 256 + threadIdx.x; x < end;
-       x += (uint64_t)gridDim.x * 256) {
-    const uint64_t key = a.in.keys[x];
-    const uint32_t hb = sw_hash(key, a.gbits - 2);
-    const uint4* p = (const uint4*)(a.gtab + 4 * (uint64_t)hb);
-    const uint4 bx = p[0], by = p[1];
-    const uint64_t sv[4] = {((uint64_t)bx.y << 32) | bx.x, ((uint64_t)bx.w << 32) | bx.z,
-                            ((uint64_t)by.y << 32) | by.x, ((uint64_t)by.w << 32) | by.z};
-    uint32_t id = ~0u, fre = 4;
-#pragma unroll
-    for (uint32_t i = 0; i < 4; i++) {
-      if (sv[i] == key && id == ~0u) id = 4 * hb + i;
-      if (sv[i] == KEY_EMPTY && fre == 4) fre = i;
-    }
-    if (id == ~0u && fre < 4) {
-      const unsigned long long prev =
-          atomicCAS((unsigned long long*)(a.gtab + 4 * (uint64_t)hb + fre),
-                    (unsigned long long)KEY_EMPTY, (unsigned long long)key);
-      if (prev == KEY_EMPTY || prev == key) id = 4 * hb + fre;
-    }
-    if (id == ~0u) id = gtab_insert(a.gtab, a.gbits, key);
-    a.ids[x - off0] = id;
-  }
+  first = false;
+  return 0;  // unreachable: a pass holds <= PRE_MAP distinct keys
 }
 
 __global__ __launch_bounds__(1024) void k_sw_pre(SwPreArgs a) {
-  __shared__ uint64_t mkey[SW_MAP];
-  __shared__ uint64_t mmask[SW_MAP];
-  __shared__ uint64_t s_dep[2][SW_T];
+  __shared__ uint64_t mkey[PRE_MAP];
+  __shared__ uint64_t mmask[PRE_MAP];
+  __shared__ uint32_t mgid[PRE_MAP];
+  __shared__ uint64_t s_dep[SW_T];
   __shared__ uint32_t s_off[SW_T + 1];
-  __shared__ uint64_t s_hw[2];
+  __shared__ uint32_t s_meta[SW_T];
   __shared__ uint32_t s_bad;
   if (*a.abandon) return;
   const uint32_t m = list_len(a.m_dev, a.m_host);
   const uint32_t lim = min(m, a.p_max);
   const uint32_t ntiles = (lim + SW_T - 1) / SW_T;
-  const uint32_t j = threadIdx.x, lane = lane_id();
+  const uint32_t j = threadIdx.x;
   const uint64_t nnz = a.in.nnz;
   const uint64_t off0 = min((uint64_t)a.in.off[0], nnz);
-  uint64_t* pd = (a.dbg && blockIdx.x < 64) ? a.dbg + blockIdx.x * 8 : nullptr;
-  if (pd && j == 0) pd[0] = clock64();
-  for (uint32_t k = blockIdx.x; k < ntiles; k += gridDim.x) {
+  // one tile per workgroup (the host launches one workgroup per tile of p_max)
+  const uint32_t k = blockIdx.x;
+  if (k >= ntiles) return;
+  {
+    SwRec& R = a.rec[k];
     const uint32_t i0 = k * SW_T;
     const uint32_t nt = min(SW_T, lim - i0);
     if (j <= nt) s_off[j] = (uint32_t)min((uint64_t)a.in.off[i0 + j], nnz);
-    if (j < 2 * SW_T) s_dep[j / SW_T][j % SW_T] = 0;
-    if (j < 2) s_hw[j] = 0;
+    // per-txn inputs of the record, read now (used at the end)
+    uint32_t my_tid = 0;
+    bool my_pre = false;
+    if (j < nt) {
+      my_tid = a.in.tid ? a.in.tid[i0 + j] : i0 + j;
+      // identity lists carry decisions made before the solver (history window)
+      my_pre = a.state && a.state[i0 + j] != ST_UNDECIDED;
+    }
+    if (j < SW_T) {
+      s_dep[j] = 0;
+      s_meta[j] = 0;
+    }
     if (j == 0) s_bad = 0;
     __syncthreads();
     if (j < nt && s_off[j + 1] < s_off[j]) atomicOr(&s_bad, ERR_OFFSETS);
@@ -306,43 +297,31 @@ __global__ __launch_bounds__(1024) void k_sw_pre(SwPreArgs a) {
     __syncthreads();
     uint32_t bad = s_bad;
     if (cnt > SW_TA) bad |= ERR_TILE;
-    if (bad) {
-      if (j == 0) {
-        atomicOr(a.err, bad);
-        a.tinfo[k] = SwTile{0, 0, {0, 0}, {0, 0}};
-        a.rec[k].nt = 0;
-        a.rec[k].cnt = 0;
-      }
-      __syncthreads();
-      continue;
-    }
     // the level's key table holds `budget` accesses: the serial pass stops here
-    if ((uint64_t)A1 - off0 > a.budget) {
-      if (j == 0) {
-        a.tinfo[k] = SwTile{0, SW_STOP, {0, 0}, {0, 0}};
-        a.rec[k].nt = 0;
-        a.rec[k].cnt = SW_STOP;
-      }
-      __syncthreads();
-      continue;
+    const bool stop = !bad && (uint64_t)A1 - off0 > a.budget;
+    if (bad || stop) {
+      if (bad && j == 0) atomicOr(a.err, bad);
+      // a malformed tile is reported by the host; both end the serial pass
+      if (j < SW_T) R.meta[j] = SWM_STOP;
+      return;
     }
-    if (pd && j == 0 && k == blockIdx.x) pd[1] = clock64();
-    uint64_t key[SW_U];
-    uint32_t lt[SW_U];
-    bool w[SW_U], v[SW_U];
-    uint64_t hw0 = 0, hw1 = 0;
+    // per-thread accesses j + 1024u; flags packed into bit masks over u
+    uint64_t key[PRE_U];
+    uint32_t lt[PRE_U], slot[PRE_U];
+    uint32_t vm = 0, wmk = 0;
 #pragma unroll
-    for (uint32_t u = 0; u < SW_U; u++) {
-      const uint32_t xr = j + 1024 * u;
-      v[u] = xr < cnt;
+    for (uint32_t u = 0; u < PRE_U; u++) {
       key[u] = KEY_EMPTY;
       lt[u] = 0;
-      w[u] = false;
-      if (v[u]) {
+      slot[u] = 0;
+      if (u && cnt <= 1024u * u) continue;  // uniform
+      const uint32_t xr = j + 1024 * u;
+      if (xr < cnt) {
+        vm |= 1u << u;
         const uint32_t x = A0 + xr;
         key[u] = a.in.keys[x];
         if (key[u] == KEY_EMPTY) atomicOr(a.err, ERR_KEY);  // reserved: reported by the host
-        w[u] = a.in.acctype[x] == 1;  // WR (occ.cpp:379-383)
+        const bool w = a.in.acctype[x] == 1;  // WR (occ.cpp:379-383)
         // largest t < nt with s_off[t] <= x (empty txns never own an access)
         uint32_t lo = 0, hi = nt;  // invariant: s_off[lo] <= x < s_off[hi]
         while (hi - lo > 1) {
@@ -351,119 +330,172 @@ __global__ __launch_bounds__(1024) void k_sw_pre(SwPreArgs a) {
           else hi = mid;
         }
         lt[u] = lo;
-        if (w[u]) {
-          if (lo < 64) hw0 |= 1ull << lo;
-          else hw1 |= 1ull << (lo - 64);
+        if (w) {
+          wmk |= 1u << u;
+          atomicOr(&s_meta[lo], SWM_HASW);
         }
       }
     }
-    // key ids (assigned by k_sw_ids) into the record
-#pragma unroll
-    for (uint32_t u = 0; u < SW_U; u++) {
-      if (u && cnt <= 1024 * u) break;  // uniform
-      if (!v[u]) continue;
-      const uint32_t xr = j + 1024 * u;
-      const uint32_t id = a.ids[(A0 - off0) + xr];
-      const uint8_t pkv = (uint8_t)(lt[u] | (w[u] ? 0x80u : 0u));
-      if (xr < SW_REC_ACC) {
-        a.rec[k].id[xr] = id;
-        a.rec[k].pk[xr] = pkv;
-      } else {
-        const uint64_t o = (uint64_t)k * (SW_TA - SW_REC_ACC) + (xr - SW_REC_ACC);
-        a.id_ovf[o] = id;
-        a.rp_ovf[o] = pkv;
-      }
-    }
-    hw0 = wave_or64(hw0);
-    hw1 = wave_or64(hw1);
-    if (lane == 0 && hw0) atomicOr((unsigned long long*)&s_hw[0], (unsigned long long)hw0);
-    if (lane == 0 && hw1) atomicOr((unsigned long long*)&s_hw[1], (unsigned long long)hw1);
-    __syncthreads();
-    if (pd && j == 0 && k == blockIdx.x) pd[2] = clock64();
-    // dependency masks: half h = writers 64h .. 64h+63
-    for (uint32_t h = 0; h < 2; h++) {
-      for (uint32_t q = j; q < SW_MAP; q += 1024) {
+    // passes over key-hash classes keep each map pass <= 2048 distinct keys
+    const uint32_t P = cnt <= PRE_MAP / 2 ? 1u : 2u;
+    for (uint32_t p = 0; p < P; p++) {
+      for (uint32_t q = j; q < PRE_MAP; q += 1024) {
         mkey[q] = KEY_EMPTY;
         mmask[q] = 0;
       }
       __syncthreads();
+      uint32_t pm = vm;  // this pass's accesses
+      if (P > 1)
 #pragma unroll
-      for (uint32_t u = 0; u < SW_U; u++) {
-        if (!v[u] || !w[u] || (lt[u] >> 6) != h) continue;
-        const uint32_t sl = map_slot(mkey, key[u], true);
-        if (sl != ~0u) atomicOr((unsigned long long*)&mmask[sl], 1ull << (lt[u] & 63));
+        for (uint32_t u = 0; u < PRE_U; u++)
+          if ((sw_hash(key[u], 13) & 1u) != p) pm &= ~(1u << u);
+      uint32_t fm = 0;
+#pragma unroll
+      for (uint32_t u = 0; u < PRE_U; u++) {
+        if (!((pm >> u) & 1u)) continue;
+        bool first;
+        slot[u] = pre_map_insert(mkey, key[u], first);
+        if (first) fm |= 1u << u;
+        if ((wmk >> u) & 1u) atomicOr((unsigned long long*)&mmask[slot[u]], 1ull << lt[u]);
+      }
+      // the first access of each key enters it in the global table: every
+      // home-bucket read in flight at once, then every CAS, then the rare
+      // full-bucket / lost-race slow path
+      {
+        const uint32_t lb = a.gbits - 2;
+        uint4 bx[PRE_U], by[PRE_U];
+#pragma unroll
+        for (uint32_t u = 0; u < PRE_U; u++) {
+          bx[u] = make_uint4(0, 0, 0, 0);
+          by[u] = bx[u];
+          if (!((fm >> u) & 1u)) continue;
+          const uint4* hp = (const uint4*)(a.gtab + 4 * (uint64_t)sw_hash(key[u], lb));
+          bx[u] = hp[0];
+          by[u] = hp[1];
+        }
+        uint32_t gid[PRE_U], tried = 0;
+#pragma unroll
+        for (uint32_t u = 0; u < PRE_U; u++) {
+          gid[u] = ~0u;
+          if (!((fm >> u) & 1u)) continue;
+          const uint32_t hb = sw_hash(key[u], lb);
+          const uint64_t sv[4] = {((uint64_t)bx[u].y << 32) | bx[u].x,
+                                  ((uint64_t)bx[u].w << 32) | bx[u].z,
+                                  ((uint64_t)by[u].y << 32) | by[u].x,
+                                  ((uint64_t)by[u].w << 32) | by[u].z};
+          uint32_t fre = 4;
+#pragma unroll
+          for (uint32_t i = 0; i < 4; i++) {
+            if (sv[i] == key[u] && gid[u] == ~0u) gid[u] = 4 * hb + i;
+            if (sv[i] == KEY_EMPTY && fre == 4) fre = i;
+          }
+          if (gid[u] == ~0u && fre < 4) {
+            gid[u] = 4 * hb + fre;
+            tried |= 1u << u;
+          }
+        }
+        unsigned long long prev[PRE_U];
+#pragma unroll
+        for (uint32_t u = 0; u < PRE_U; u++)
+          prev[u] = KEY_EMPTY;
+#pragma unroll
+        for (uint32_t u = 0; u < PRE_U; u++)
+          if ((tried >> u) & 1u)
+            prev[u] = atomicCAS((unsigned long long*)(a.gtab + gid[u]),
+                                (unsigned long long)KEY_EMPTY, (unsigned long long)key[u]);
+#pragma unroll
+        for (uint32_t u = 0; u < PRE_U; u++) {
+          if (!((fm >> u) & 1u)) continue;
+          if (((tried >> u) & 1u) && prev[u] != KEY_EMPTY && prev[u] != key[u]) gid[u] = ~0u;
+          if (gid[u] == ~0u) gid[u] = gtab_insert(a.gtab, a.gbits, key[u]);
+          mgid[slot[u]] = gid[u];
+        }
       }
       __syncthreads();
 #pragma unroll
-      for (uint32_t u = 0; u < SW_U; u++) {
-        if (!v[u] || lt[u] <= 64 * h) continue;  // no writer of this half precedes it
-        const uint32_t sl = map_slot(mkey, key[u], false);
-        if (sl == ~0u) continue;
-        const uint32_t rel = lt[u] - 64 * h;  // earlier writers of the half only
-        const uint64_t wm = mmask[sl] & (rel >= 64 ? ~0ull : ((1ull << rel) - 1ull));
-        if (wm) atomicOr((unsigned long long*)&s_dep[h][lt[u]], (unsigned long long)wm);
+      for (uint32_t u = 0; u < PRE_U; u++) {
+        if (!((pm >> u) & 1u)) continue;
+        const uint32_t t = lt[u];
+        const uint64_t wm = mmask[slot[u]] & ((1ull << t) - 1ull);  // earlier writers only
+        if (wm) atomicOr((unsigned long long*)&s_dep[t], (unsigned long long)wm);
+        const uint32_t id = sw_pack(mgid[slot[u]], (wmk >> u) & 1u);
+        const uint32_t pos = A0 + j + 1024 * u - s_off[t];
+        if (pos < SW_IDN) R.id[t][pos] = id;
+        else if (pos < SW_IDN + SW_OVN)  // longer txns are rejected by the host (prep)
+          a.id_ovf[((uint64_t)k * SW_T + t) * SW_OVN + (pos - SW_IDN)] = id;
       }
-      __syncthreads();
+      __syncthreads();  // map reuse by the next pass
+    }
+    // unused entries of the inline id rows, then the per-txn words
+    for (uint32_t q = j; q < SW_T * SW_IDN; q += 1024) {
+      const uint32_t t = q / SW_IDN, pos = q % SW_IDN;
+      const uint32_t len = t < nt ? s_off[t + 1] - s_off[t] : 0u;
+      if (pos >= len) R.id[t][pos] = SW_E_NONE;
     }
     if (j < SW_T) {
-      const uint64_t r = (uint64_t)k * SW_T + j;
-      a.rec[k].dep[0][j] = s_dep[0][j];
-      a.rec[k].dep[1][j] = s_dep[1][j];
-      a.rec[k].span[j] = j < nt ? (s_off[j] - A0) | ((s_off[j + 1] - s_off[j]) << 16) : 0u;
-      a.rtid[r] = j < nt ? (a.in.tid ? a.in.tid[i0 + j] : i0 + j) : 0u;
-      // identity lists carry decisions made before the solver (history window)
-      const bool pre = j < nt && a.state && a.state[i0 + j] != ST_UNDECIDED;
-      const uint64_t pk = ballot64(pre);
-      if (lane == 0) {
-        a.tinfo[k].prekill[j >> 6] = pk;
-        a.rec[k].prekill[j >> 6] = pk;
+      const uint32_t len = j < nt ? s_off[j + 1] - s_off[j] : 0u;
+      uint32_t mt = s_meta[j];
+      if (j < nt) {
+        mt |= SWM_VALID | (min(len, MAX_TXN_LEN) << 8);
+        if (len > SW_IDN) mt |= SWM_LONG;
+        if (my_pre) mt |= SWM_PRE;
       }
-      if (j == 0) {
-        a.tinfo[k].nt = nt;
-        a.tinfo[k].cnt = cnt;
-        a.tinfo[k].hasw[0] = s_hw[0];
-        a.tinfo[k].hasw[1] = s_hw[1];
-        a.rec[k].nt = nt;
-        a.rec[k].cnt = cnt;
-        a.rec[k].hasw[0] = s_hw[0];
-        a.rec[k].hasw[1] = s_hw[1];
-      }
+      R.meta[j] = mt;
+      R.dep[j] = s_dep[j];
+      R.rtid[j] = my_tid;
     }
-    if (pd && j == 0 && k == blockIdx.x) pd[3] = clock64();
-    __syncthreads();  // LDS reuse by the next tile
-    if (pd && j == 0 && k == blockIdx.x) pd[4] = clock64();
   }
-  if (pd && j == 0) pd[5] = clock64();
 }
 
 // ---------------------------------------------------------------------------
-// k_sw_seq: one workgroup decides the tiles in order (see header).  Tile
-// records reach LDS SW_SEQ_B at a time as one contiguous copy whose loads
-// are issued a super-step ahead (registers), so the loop itself touches
-// global memory only on the rare long-tile path; decisions and C go out
-// after the last tile.
-constexpr uint32_t SEQ_N16 = SW_SEQ_B * sizeof(SwRec) / 16;  // uint4 per super-step
-constexpr uint32_t SEQ_R = (SEQ_N16 + 1023) / 1024;           // uint4 per thread
-static_assert(sizeof(SwRec) == 12864, "SwRec layout");
-static_assert(SEQ_R == 4, "super-step copy width");
-constexpr uint32_t SEQ_UR = SW_REC_ACC / 1024;  // accesses per thread held in the record
+// k_sw_seq: the exact serial decision of the level's tiles, in order, by ONE
+// wave (lane t = txn t of the tile): no barriers inside the loop.  The
+// committed set C lives in LDS as a bitmap over key ids; a wave's LDS
+// operations complete in order, so a tile's inserts are visible to the next
+// tile's probes.  The other 15 waves stream the tile records from global
+// memory into an LDS ring ahead of it (one tile per wave in flight; ready and
+// consumed counters in LDS), then all 16 join for the write-out.
+constexpr uint32_t SEQ_RING = 12;  // LDS record slots (61,440 B)
+constexpr uint32_t SEQ_PROD = 15;  // producer waves
+constexpr uint32_t SEQ_V4 = sizeof(SwRec) / 16;  // uint4 per record
+static_assert(sizeof(SwRec) % (16 * 64) == 0, "record copy: whole uint4 per lane");
+
+// A load the compiler's wait-count tracking does not see: it completes inside
+// the asm (vmcnt(0)); used on the rare overflow path of long txns.
+__device__ inline uint32_t ld_sync(const uint32_t* p) {
+  uint32_t v;
+  asm volatile("global_load_dword %0, %1, off\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p));
+  return v;
+}
+// workgroup-scope acquire / release on the LDS hand-off counters
+__device__ inline uint32_t lds_ld(uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ inline void lds_st(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// committed-set bitmap probe / insert of a packed record entry (sw_pack)
+__device__ inline uint32_t cb_probe(const uint32_t* cb, uint32_t e) {
+  return *(const uint32_t*)((const char*)cb + (e >> 8)) >> (e & 31u);
+}
+__device__ inline void cb_insert_w(uint32_t* cb, uint32_t e) {
+  atomicOr((uint32_t*)((char*)cb + (e >> 8)), ((e >> 5) & 1u) << (e & 31u));
+}
 
 __global__ __launch_bounds__(1024) void k_sw_seq(SwSeqArgs a) {
-  __shared__ __attribute__((aligned(16))) SwRec ring[SW_SEQ_B];
-  __shared__ uint32_t cbits[(1u << SW_GBITS_MAX) / 32];  // committed set over key ids
-  __shared__ uint64_t s_hit[SW_TA / 64];
-  __shared__ uint64_t s_M[SW_PMAX_TILES][2];  // commit masks per decided tile
-  __shared__ uint64_t s_stamp[128 * 4];       // DCC_SW_DEBUG clock stamps
+  __shared__ uint32_t cbits[(1u << SW_GBITS_MAX) / 32 + 1];  // + the SW_ID_NONE word
+  __shared__ uint64_t s_M[SW_PMAX_TILES];  // commit mask per decided tile
   __shared__ uint32_t sbloom[(1u << SW_BLOOM_LOG) / 32];
-  __shared__ uint32_t s_cnt, s_kc;
+  __shared__ __attribute__((aligned(16))) SwRec ring[SEQ_RING];
+  __shared__ uint32_t s_ready[SEQ_RING];
+  __shared__ uint32_t s_done, s_stop, s_k;
   const uint32_t j = threadIdx.x, lane = lane_id(), wv = j >> 6;
   if (*a.abandon) return;
   const uint32_t m = list_len(a.m_dev, a.m_host);
   const uint32_t lim = min(m, a.p_max);
   const uint32_t ntiles = min((lim + SW_T - 1) / SW_T, SW_PMAX_TILES);
   for (uint32_t q = j; q < (1u << SW_BLOOM_LOG) / 32; q += 1024) sbloom[q] = 0;
-  if (j == 0) s_kc = 0;
-  const uint32_t nsup = (ntiles + SW_SEQ_B - 1) / SW_SEQ_B;
   // the filter of this level starts from a clean look-back and ticket; the
   // next level's list is empty unless the filter writes it
   if (j == 0) {
@@ -471,212 +503,188 @@ __global__ __launch_bounds__(1024) void k_sw_seq(SwSeqArgs a) {
     a.lv_next->m = 0;
     a.lv_next->acc = 0;
     a.next_off[0] = 0;
-    s_cnt = 0;
+    s_k = 0;
+    s_done = 0;
+    s_stop = 0;
   }
+  if (j < SEQ_RING) s_ready[j] = 0;
+  uint64_t* dbg = a.dbg;
+  if (dbg && j == 0) dbg[0] = __builtin_amdgcn_s_memrealtime();
   const uint32_t nwords = (1u << a.gbits) / 32;
   for (uint32_t q = j; q < nwords; q += 1024) cbits[q] = 0;
+  if (j == 0) cbits[SW_ID_NONE / 32] = 0;  // the SW_E_NONE word
+  __syncthreads();
 
-  const uint4* src = (const uint4*)a.rec;
-  uint4* dst = (uint4*)ring;
-  // named registers per thread: an array captured by a lambda would live in
-  // scratch
-  uint4 R0, R1, R2, R3;
-  const uint32_t c0 = j, c1 = j + 1024, c2 = j + 2048, c3 = min(j + 3072, SEQ_N16 - 1);
-#define SEQ_LOAD(sidx)                                     \
-  do {                                                     \
-    const uint4* p_ = src + (uint64_t)(sidx) * SEQ_N16;    \
-    R0 = p_[c0];                                           \
-    R1 = p_[c1];                                           \
-    R2 = p_[c2];                                           \
-    R3 = p_[c3];                                           \
-  } while (0)
-#define SEQ_STORE()  \
-  do {               \
-    dst[c0] = R0;    \
-    dst[c1] = R1;    \
-    dst[c2] = R2;    \
-    dst[c3] = R3;    \
-  } while (0)
-  uint64_t* dbg = a.dbg;
-  auto stamp = [&](uint32_t k, uint32_t i) {
-    if (dbg && j == 0 && k < 128) s_stamp[k * 4 + i] = clock64();
-  };
-
-  // one tile; false = stopped before it (the level's access budget ends)
-  const uint32_t idmask = (1u << a.gbits) - 1u;
-  auto step = [&](const SwRec& T, uint32_t k) -> bool {
-    const uint32_t nt = T.nt, cnt = T.cnt;
-    if (cnt == SW_STOP) return false;  // uniform
-    stamp(k, 0);
-    // the common path: a thread's two accesses of the record, branch-free
-    // (ids past cnt are masked: records are not cleared between tiles)
-    const uint32_t i0 = T.id[j] & idmask, i1 = T.id[j + 1024] & idmask;
-    const uint32_t p0 = T.pk[j], p1 = T.pk[j + 1024];
-    const bool v0 = j < cnt, v1 = j + 1024 < cnt;
-    // (1) probe C: one bitmap word per access; hit ballots into the tile bitmap
-    {
-      const uint32_t w0 = cbits[i0 >> 5], w1 = cbits[i1 >> 5];  // unconditional reads
-      const bool h0 = ((w0 >> (i0 & 31u)) & (uint32_t)v0) != 0;
-      const bool h1 = ((w1 >> (i1 & 31u)) & (uint32_t)v1) != 0;
-      const uint64_t b0 = ballot64(h0), b1 = ballot64(h1);
-      if (lane == 0) {
-        s_hit[wv] = b0;
-        s_hit[wv + 16] = b1;
-      }
-    }
-    if (cnt > SW_REC_ACC) {  // long tiles (scalar branch): accesses beyond the record
-      for (uint32_t u = SEQ_UR; u < SW_U; u++) {
-        const uint32_t xr = j + 1024 * u;
-        bool h = false;
-        if (xr < cnt) {
-          const uint32_t id =
-              a.id_ovf[(uint64_t)k * (SW_TA - SW_REC_ACC) + xr - SW_REC_ACC] & idmask;
-          h = (cbits[id >> 5] >> (id & 31u)) & 1u;
+  if (dbg && j == 0) dbg[1] = __builtin_amdgcn_s_memrealtime();
+  if (wv > 0) {
+    uint32_t pw = 0;
+    // producers: wave p copies tiles p-1, p-1+15, ... into slot k % SEQ_RING
+    for (uint32_t k = wv - 1; k < ntiles; k += SEQ_PROD) {
+      const uint32_t slot = k % SEQ_RING;
+      bool stopped = false;
+      while (true) {
+        if (lds_ld(&s_stop)) {
+          stopped = true;
+          break;
         }
-        const uint64_t b = ballot64(h);
-        if (lane == 0) s_hit[wv + 16 * u] = b;
+        if (lds_ld(&s_done) + SEQ_RING > k) break;
+        pw++;
+        __builtin_amdgcn_s_sleep(1);
       }
+      if (stopped) break;
+      const uint4* src = (const uint4*)(a.rec + k);
+      uint4* dst = (uint4*)&ring[slot];
+      uint4 v[SEQ_V4 / 64];
+#pragma unroll
+      for (uint32_t q = 0; q < SEQ_V4 / 64; q++) v[q] = src[q * 64 + lane];
+#pragma unroll
+      for (uint32_t q = 0; q < SEQ_V4 / 64; q++) dst[q * 64 + lane] = v[q];
+      if (lane == 0) lds_st(&s_ready[slot], k + 1);  // release: the record is in LDS
     }
-    __syncthreads();
-    stamp(k, 1);
-    // (2) wave 0: kills, then the tile's serial order as a fixed point over
-    // the dependency masks (lane l holds txns l and l + 64)
-    if (wv == 0) {
-      const bool va = lane < nt, vb = lane + 64 < nt;
-      bool ka = ((T.prekill[0] >> lane) & 1ull) != 0;
-      bool kb = ((T.prekill[1] >> lane) & 1ull) != 0;
-      const uint32_t spa = T.span[lane], spb = T.span[lane + 64];
-      if (va && !ka) ka = range_any(s_hit, spa & 0xFFFFu, spa >> 16);
-      if (vb && !kb) kb = range_any(s_hit, spb & 0xFFFFu, spb >> 16);
-      const uint64_t d0 = T.dep[0][lane];                                   // txn l < 64
-      const uint64_t d1l = T.dep[0][lane + 64], d1h = T.dep[1][lane + 64];  // txn l + 64
-      uint64_t Ul = ballot64(va && !ka), Uh = ballot64(vb && !kb), Ml = 0, Mh = 0;
-#pragma unroll 1
-      while (Ul | Uh) {
-        const bool m0 = ((Ul >> lane) & 1ull) != 0, m1 = ((Uh >> lane) & 1ull) != 0;
-        const bool c0 = m0 && (d0 & (Ml | Ul)) == 0;
-        const bool a0 = m0 && (d0 & Ml) != 0;
-        const bool c1 = m1 && ((d1l & (Ml | Ul)) | (d1h & (Mh | Uh))) == 0;
-        const bool a1 = m1 && ((d1l & Ml) | (d1h & Mh)) != 0;
-        const uint64_t cl = ballot64(c0), al = ballot64(a0), ch = ballot64(c1), ah = ballot64(a1);
-        Ml |= cl;
-        Mh |= ch;
-        Ul &= ~(cl | al);
-        Uh &= ~(ch | ah);
+    if (dbg && lane == 0 && pw) atomicAdd((unsigned long long*)&dbg[7], (unsigned long long)pw);
+  } else if (ntiles) {
+    uint32_t k = 0, cw = 0;
+    for (; k < ntiles; k++) {
+      const uint32_t slot = k % SEQ_RING;
+      while (lds_ld(&s_ready[slot]) != k + 1) {
+        cw++;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      const SwRec& T = ring[slot];
+      const uint4* ip = (const uint4*)T.id[lane];
+      const uint4 i0 = ip[0], i1 = ip[1], i2 = ip[2], i3 = ip[3];
+      const uint64_t dep = T.dep[lane];
+      const uint32_t meta = T.meta[lane];
+      if (__builtin_amdgcn_readfirstlane(meta) & SWM_STOP) break;
+      const uint32_t ids[SW_IDN] = {i0.x, i0.y, i0.z, i0.w, i1.x, i1.y, i1.z, i1.w,
+                                    i2.x, i2.y, i2.z, i2.w, i3.x, i3.y, i3.z, i3.w};
+      // (1) probe C: a txn touching a committed key is dead
+      uint32_t hit = 0;
+#pragma unroll
+      for (uint32_t q = 0; q < SW_IDN; q++) hit |= cb_probe(cbits, ids[q]);
+      hit &= 1u;
+      // txns with more than SW_IDN accesses (rare): the tail from the
+      // overflow area, synchronously
+      const bool lng = (meta & SWM_LONG) != 0;
+      const uint64_t lmask = ballot64(lng);
+      const uint32_t* ovf = a.id_ovf + ((uint64_t)k * SW_T + lane) * SW_OVN;
+      const uint32_t extra = lng ? min((meta >> 8) - SW_IDN, SW_OVN) : 0u;
+      if (lmask)
+        for (uint32_t q = 0; q < extra; q++) hit |= cb_probe(cbits, ld_sync(ovf + q)) & 1u;
+      // (2) the tile's serial order: fixed point over the dependency masks
+      const bool cand = (meta & SWM_VALID) && !(meta & SWM_PRE) && !hit;
+      uint64_t U = ballot64(cand), M = 0;
+      while (U) {
+        const bool mu = (U >> lane) & 1ull;
+        const bool c = mu && (dep & (M | U)) == 0;
+        const bool ab = mu && (dep & M) != 0;
+        const uint64_t cm = ballot64(c), am = ballot64(ab);
+        M |= cm;
+        U &= ~(cm | am);
+      }
+      // (3) committed write keys join C
+      if (((M >> lane) & 1ull) && (meta & SWM_HASW)) {
+#pragma unroll
+        for (uint32_t q = 0; q < SW_IDN; q++) cb_insert_w(cbits, ids[q]);
+        for (uint32_t q = 0; q < extra; q++) cb_insert_w(cbits, ld_sync(ovf + q));
       }
       if (lane == 0) {
-        s_M[k][0] = Ml;
-        s_M[k][1] = Mh;
+        s_M[k] = M;
+        lds_st(&s_done, k + 1);  // the slot's reads are complete (values used above)
       }
     }
-    __syncthreads();
-    stamp(k, 2);
-    // (3) committed write keys join C (no-return atomics: nothing waits)
-    const uint64_t Ml = s_M[k][0], Mh = s_M[k][1];
-    {
-      const bool c0 = v0 && (p0 & 0x80u) && ((((p0 & 64u) ? Mh : Ml) >> (p0 & 63u)) & 1ull);
-      const bool c1 = v1 && (p1 & 0x80u) && ((((p1 & 64u) ? Mh : Ml) >> (p1 & 63u)) & 1ull);
-      if (c0) atomicOr(&cbits[i0 >> 5], 1u << (i0 & 31u));
-      if (c1) atomicOr(&cbits[i1 >> 5], 1u << (i1 & 31u));
-    }
-    if (cnt > SW_REC_ACC) {
-      for (uint32_t u = SEQ_UR; u < SW_U; u++) {
-        const uint32_t xr = j + 1024 * u;
-        if (xr >= cnt) continue;
-        const uint64_t o = (uint64_t)k * (SW_TA - SW_REC_ACC) + xr - SW_REC_ACC;
-        const uint32_t pk = a.rp_ovf[o];
-        if ((pk & 0x80u) && ((((pk & 64u) ? Mh : Ml) >> (pk & 63u)) & 1ull)) {
-          const uint32_t id = a.id_ovf[o] & idmask;
-          atomicOr(&cbits[id >> 5], 1u << (id & 31u));
-        }
+    if (lane == 0) {
+      s_k = k;
+      lds_st(&s_stop, 1u);
+      if (dbg) {
+        dbg[2] = __builtin_amdgcn_s_memrealtime();
+        dbg[5] = cw;
+        dbg[6] = k;
       }
     }
-    __syncthreads();
-    stamp(k, 3);
-    return true;
-  };
-
-  __syncthreads();
-  if (nsup) {
-    SEQ_LOAD(0);
-    SEQ_STORE();
   }
   __syncthreads();
-  uint32_t k = 0;
-  bool stop = false;
-  for (uint32_t sidx = 0; sidx < nsup && !stop; sidx++) {
-    SEQ_LOAD(min(sidx + 1, nsup - 1));  // unconditional: exact wait counts
-#pragma unroll 1
-    for (uint32_t b = 0; b < SW_SEQ_B; b++) {
-      if (k >= ntiles || !step(ring[b], k)) {
-        stop = true;
-        break;
-      }
-      k++;
-    }
-    if (stop || sidx + 1 == nsup) break;
-    SEQ_STORE();  // every wave passed the last step's barrier: the ring is free
-    __syncthreads();
-  }
-#undef SEQ_LOAD
-#undef SEQ_STORE
+  const uint32_t k = s_k;
   // ---- write-out: decisions of tiles [0, k), the level's committed keys
   for (uint32_t q = j; q < k * SW_T; q += 1024) {
     const uint32_t kk = q / SW_T, t = q % SW_T;
-    const SwTile& ti = a.tinfo[kk];
-    if (t >= ti.nt) continue;
-    const uint32_t tid = a.rtid[q];
-    const uint32_t h = t >> 6, b = t & 63;
-    if (!((ti.prekill[h] >> b) & 1ull))
-      a.state[tid] = ((s_M[kk][h] >> b) & 1ull) ? ST_COMMIT : ST_ABORT;
-    if (a.write_hasw) a.hasw[tid] = (uint8_t)((ti.hasw[h] >> b) & 1ull);
+    const uint32_t mt = a.rec[kk].meta[t];
+    if (!(mt & SWM_VALID)) continue;
+    const uint32_t tid = a.rec[kk].rtid[t];
+    if (!(mt & SWM_PRE)) a.state[tid] = ((s_M[kk] >> t) & 1ull) ? ST_COMMIT : ST_ABORT;
+    if (a.write_hasw) a.hasw[tid] = (mt & SWM_HASW) ? 1 : 0;
   }
-  // C for the filter: the committed-id bitmap and a Bloom filter of the keys
-  {
-    // keys of the committed ids, 8 table reads in flight per thread
-    uint32_t ids[8];
-    uint32_t nid = 0;
-    auto flush = [&]() {
-      uint64_t kk[8];
-#pragma unroll
-      for (uint32_t i = 0; i < 8; i++) kk[i] = i < nid ? a.gtab[ids[i]] : 0ull;
-#pragma unroll
-      for (uint32_t i = 0; i < 8; i++) {
-        if (i >= nid) break;
-        uint32_t b1, b2;
-        bloom_bits(kk[i], b1, b2);
-        atomicOr(&sbloom[b1 >> 5], 1u << (b1 & 31));
-        atomicOr(&sbloom[b2 >> 5], 1u << (b2 & 31));
-        a.ckeys_out[atomicAdd(&s_kc, 1u)] = kk[i];
-      }
-      nid = 0;
-    };
-    for (uint32_t q = j; q < nwords; q += 1024) {
-      uint32_t w = cbits[q];
+  if (dbg) {
+    __syncthreads();
+    if (j == 0) dbg[3] = __builtin_amdgcn_s_memrealtime();
+  }
+  // C for the filter: the committed-id bitmap, the committed keys (ids
+  // listed in LDS in bitmap order, chunk by chunk) and their Bloom filter
+  constexpr uint32_t WPT = (1u << SW_GBITS_MAX) / 32 / 1024;  // bitmap words per thread
+  uint32_t* list = (uint32_t*)ring;  // the record ring is free now
+  constexpr uint32_t LCAP = sizeof(ring) / 4;
+  uint32_t myc = 0;  // committed ids in this thread's words j*WPT .. +WPT
+  for (uint32_t i = 0; i < WPT; i++) {
+    const uint32_t q = j * WPT + i;
+    if (q < nwords) {
+      const uint32_t w = cbits[q];
       a.cbits_out[q] = w;
-      while (w) {
-        ids[nid & 7] = q * 32 + (uint32_t)__builtin_ctz(w);
-        w &= w - 1;
-        if (++nid == 8) flush();
+      myc += (uint32_t)__popc(w);
+    }
+  }
+  // block exclusive scan of the per-thread counts
+  __shared__ uint32_t s_wsum[16];
+  uint32_t tot;
+  const uint32_t wex = wave_excl_u32(myc, tot);
+  if (lane == 0) s_wsum[wv] = tot;
+  __syncthreads();
+  uint32_t base = wex, ccount = 0;
+  for (uint32_t w = 0; w < 16; w++) {
+    const uint32_t x = s_wsum[w];
+    if (w < wv) base += x;
+    ccount += x;
+  }
+  for (uint32_t c0 = 0; c0 < ccount; c0 += LCAP) {
+    // list entries [c0, c0 + LCAP): this thread's ids in bitmap order
+    if (base + myc > c0 && base < c0 + LCAP) {
+      uint32_t r = base;
+      for (uint32_t i = 0; i < WPT; i++) {
+        const uint32_t q = j * WPT + i;
+        uint32_t w = q < nwords ? cbits[q] : 0u;
+        while (w) {
+          if (r >= c0 && r < c0 + LCAP) list[r - c0] = q * 32 + (uint32_t)__builtin_ctz(w);
+          r++;
+          w &= w - 1;
+        }
       }
     }
-    flush();
+    __syncthreads();
+    const uint32_t n = min(LCAP, ccount - c0);
+    for (uint32_t i0 = 0; i0 < n; i0 += 1024 * 8) {
+      uint64_t kk[8];
+#pragma unroll
+      for (uint32_t u = 0; u < 8; u++) {
+        const uint32_t i = i0 + u * 1024 + j;
+        kk[u] = i < n ? a.gtab[list[i]] : 0ull;
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < 8; u++) {
+        const uint32_t i = i0 + u * 1024 + j;
+        if (i >= n) continue;
+        uint32_t b1, b2;
+        bloom_bits(kk[u], b1, b2);
+        atomicOr(&sbloom[b1 >> 5], 1u << (b1 & 31));
+        atomicOr(&sbloom[b2 >> 5], 1u << (b2 & 31));
+        a.ckeys_out[c0 + i] = kk[u];
+      }
+    }
+    __syncthreads();
   }
-  __syncthreads();
   for (uint32_t q = j; q < (1u << SW_BLOOM_LOG) / 32; q += 1024) a.bloom_out[q] = sbloom[q];
-  {
-    uint32_t c = 0;
-    for (uint32_t q = j; q < nwords; q += 1024) c += (uint32_t)__popc(cbits[q]);
-    for (int dd = 32; dd > 0; dd >>= 1) c += __shfl_xor(c, dd);
-    if (lane == 0) atomicAdd(&s_cnt, c);
-  }
-  __syncthreads();
-  const uint32_t ncid = s_cnt;
-  if (dbg)
-    for (uint32_t q = j; q < min(k, 128u) * 4; q += 1024) dbg[q] = s_stamp[q];
   if (j == 0) {
     a.lv->pos = min(k * SW_T, lim);
-    a.lv->ccount = ncid;
+    a.lv->ccount = ccount;
+    if (dbg) dbg[4] = __builtin_amdgcn_s_memrealtime();
   }
 }
 
@@ -1014,9 +1022,6 @@ __global__ __launch_bounds__(SW_CHUNK) void k_sw_compact(SwFilterArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-void launch_sw_ids(const SwPreArgs& a, unsigned grid, hipStream_t st) {
-  k_sw_ids<<<grid ? grid : 1u, 256, 0, st>>>(a);
-}
 void launch_sw_pre(const SwPreArgs& a, unsigned grid, hipStream_t st) {
   k_sw_pre<<<grid ? grid : 1u, 1024, 0, st>>>(a);
 }
