@@ -92,7 +92,7 @@ struct dcc_ctx {
   DevBuf hasw_scr, cset_tab, cset_keys;          // prefix peel
   DevBuf a_cnt, a_writers, a_big, a_st32;        // async solver
   DevBuf sw_ctl, sw_status, sw_ckeys, sw_dbg;            // sweep solver: level control, look-back, C
-  DevBuf sw_rec, sw_rk, sw_gtab;  // sweep tile records
+  DevBuf sw_rec, sw_rk, sw_gtab, sw_fw, sw_aent, sw_mg;  // sweep tile records
   SubBufs sw_list[2];                            // sweep level lists (ping-pong)
   SubBufs subs[PEEL_MAX_LEVEL];
   DevBuf l_tid[2], l_coff[2], l_cent[2];         // ping-pong undecided lists

@@ -471,8 +471,11 @@ int dcc_ctx::sweep_reserve(const DevBatch& d) {
                                 (1ull << SW_GBITS_MAX) * 8,
                      "sweep committed set"));
   CR(sw_rec.ensure(this, tiles * sizeof(SwRec), "sweep tile records"));
-  CR(sw_rk.ensure(this, tiles * SW_T * SW_OVN * 4, "sweep overflow key ids"));
+  CR(sw_rk.ensure(this, tiles * SW_OVF * 4, "sweep tile-list overflow"));
   CR(sw_gtab.ensure(this, 2 * (1ull << SW_GBITS_MAX) * 8, "sweep key tables"));
+  CR(sw_fw.ensure(this, 2 * (1ull << SW_GBITS_MAX) * 4, "sweep first writer / last accessor"));
+  CR(sw_aent.ensure(this, 2 * (1ull << (SW_GBITS_MAX - 1)) * 4, "sweep access entries"));
+  CR(sw_mg.ensure(this, SW_PMAX_TILES * 8, "sweep tile commit masks"));
   for (SubBufs& b : sw_list) {
     CR(b.tid.ensure(this, d.n * 4 + 16, "sweep list tid"));
     CR(b.off.ensure(this, (d.n + 1) * 4 + 16, "sweep list offsets"));
@@ -516,18 +519,26 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1) {
     const uint32_t* mdev = top ? nullptr : &lv->m;
     const uint32_t pmax = sw_pmax(l);
     const uint64_t tiles = (std::min<uint64_t>(pmax, d.n) + SW_T - 1) / SW_T;
+    uint32_t* fw = (uint32_t*)sw_fw.p;
+    uint32_t* la = fw + (1u << SW_GBITS_MAX);
+    uint32_t* aent = (uint32_t*)sw_aent.p;
+    uint32_t* apos = aent + (1u << (SW_GBITS_MAX - 1));
     SwPreArgs pa{in, mdev, n, pmax, top ? (const uint8_t*)state.p : nullptr,
                  (SwRec*)sw_rec.p, (uint32_t*)sw_rk.p,
                  gtab0 + (size_t)(l & 1) * (1ull << SW_GBITS_MAX), sw_gbits(l),
-                 1u << (sw_gbits(l) - 1), abandon, err};
+                 1u << (sw_gbits(l) - 1), fw, la, aent, apos, abandon, err, nullptr};
+    if (sw_debug && l < 4) pa.dbg = (uint64_t*)sw_dbg.p + 4096 + 4 * 256 * 8 + (size_t)l * 64 * 8;
     launch_sw_pre(pa, (unsigned)tiles, stream);
+    launch_sw_rows(pa, (unsigned)((tiles + 3) / 4), stream);
     SwSeqArgs sa{mdev, n, pmax, top ? 1 : 0, (const SwRec*)sw_rec.p, (const uint32_t*)sw_rk.p,
                  gtab0 + (size_t)(l & 1) * (1ull << SW_GBITS_MAX), sw_gbits(l),
                  (uint8_t*)state.p, (uint8_t*)hasw.p,
-                 cbits_d, ckeys_d, bloom_d, lv, lv + 1, (uint32_t*)out.off.p, abandon, err,
-                 nullptr};
+                 cbits_d, ckeys_d, bloom_d, lv, lv + 1, (uint32_t*)out.off.p, (uint64_t*)sw_mg.p,
+                 abandon, err, nullptr};
     if (sw_debug && l < 4) sa.dbg = (uint64_t*)sw_dbg.p + (size_t)l * 1024;
     launch_sw_seq(sa, stream);
+    SwCoutArgs ca{in, aent, apos, (const uint64_t*)sw_mg.p, lv, cbits_d, ckeys_d, bloom_d, abandon};
+    launch_sw_cout(ca, (unsigned)std::min<uint64_t>((pa.budget + 255) / 256, 4ull * n_cu), stream);
     if (top && profiling) CK(hipEventRecord(pev[1], stream));
     SwFilterArgs fa;
     fa.in = in;
@@ -562,6 +573,8 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1) {
     fa.abandon_den = 4;
     fa.gclear = gtab0 + (size_t)((l + 1) & 1) * (1ull << SW_GBITS_MAX);
     fa.gclear_n = 1ull << sw_gbits(l + 1);
+    fa.fw_clear = fw;
+    fa.la_clear = la;
     fa.err = err;
     fa.dbg = (sw_debug && l < 4) ? (uint64_t*)sw_dbg.p + 4096 + (size_t)l * 256 * 8 : nullptr;
     launch_sw_filter(fa, fgrid, stream);
@@ -619,6 +632,8 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
     if (sweep) {
       fa.job[fa.n++] = FillJob{(uint32_t*)sw_ctl.p, sw_ctl_bytes() / 4, 0u};
       fa.job[fa.n++] = FillJob{(uint32_t*)sw_gtab.p, (1ull << sw_gbits(0)) * 2, 0xFFFFFFFFu};
+      fa.job[fa.n++] = FillJob{(uint32_t*)sw_fw.p, 1ull << sw_gbits(0), 0xFFFFFFFFu};
+      fa.job[fa.n++] = FillJob{(uint32_t*)sw_fw.p + (1u << SW_GBITS_MAX), 1ull << sw_gbits(0), 0u};
     }
     launch_fill(fa, stream);
   }
@@ -782,10 +797,11 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
         const uint64_t* t = dv.data() + l * 1024;
         if (t[4])
           fprintf(stderr, "sweep L%d seq: %llu tiles, init %.2f us, loop %.2f us, decisions "
-                          "%.2f us, C out %.2f us, consumer waits %llu, producer waits %llu\n",
+                          "%.2f us, C out %.2f us, consumer waits %llu, producer waits %llu, "
+                          "loop cycles/tile %.0f\n",
                   l, (unsigned long long)t[6], (t[1] - t[0]) * 0.01, (t[2] - t[1]) * 0.01,
                   (t[3] - t[2]) * 0.01, (t[4] - t[3]) * 0.01, (unsigned long long)t[5],
-                  (unsigned long long)t[7]);
+                  (unsigned long long)t[7], t[6] ? (double)t[8] / t[6] : 0.0);
         // filter: per workgroup init / first chunk local / look-back / writes / total
         const uint64_t* f = dv.data() + 4096 + l * 256 * 8;
         double fi = 0, fl = 0, fb = 0, fw = 0, ft = 0, nc = 0;
@@ -803,25 +819,16 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
           }
         }
         {
+          // k_sw_pre / k_sw_rows stamps of workgroup 0 (s_memrealtime, 100 MHz)
           const uint64_t* pp = dv.data() + 4096 + 4 * 256 * 8 + l * 64 * 8;
-          double q1 = 0, q2 = 0, q3 = 0, q4 = 0, q5 = 0, q6 = 0, q7 = 0;
-          int np = 0;
-          for (int w = 0; w < 64 && pp[w * 8 + 5]; w++) {
-            const uint64_t* x = pp + w * 8;
-            if (!x[4]) continue;
-            q1 += x[1] - x[0];
-            q2 += x[2] - x[1];
-            q3 += x[3] - x[2];
-            q4 += x[4] - x[3];
-            q5 += x[5] - x[0];
-            q6 += x[6] - x[1];
-            q7 += x[7] - x[6];
-            np++;
-          }
-          if (np)
-            fprintf(stderr, "  pre L%d: %d WGs, offsets %.0f keys+ids %.0f (keys+search %.0f, "
-                            "bucket+cas(thread0) %.0f) masks+out %.0f tail %.0f WG total %.0f\n",
-                    l, np, q1 / np, q2 / np, q6 / np, q7 / np, q3 / np, q4 / np, q5 / np);
+          if (pp[6])
+            fprintf(stderr, "  pre L%d (us): offsets %.2f check %.2f keys+map clear %.2f "
+                            "map+gid %.2f deps+out %.2f tail %.2f\n", l,
+                    (pp[1] - pp[0]) * 0.01, (pp[2] - pp[1]) * 0.01, (pp[3] - pp[2]) * 0.01,
+                    (pp[4] - pp[3]) * 0.01, (pp[5] - pp[4]) * 0.01, (pp[6] - pp[5]) * 0.01);
+          if (pp[11])
+            fprintf(stderr, "  rows L%d (us): offsets %.2f pass1 %.2f pass2 %.2f\n", l,
+                    (pp[9] - pp[8]) * 0.01, (pp[10] - pp[9]) * 0.01, (pp[11] - pp[10]) * 0.01);
         }
         if (nw)
           fprintf(stderr, "  filter L%d: %d WGs, chunks/WG %.2f, init %.0f, chunk local %.0f "

@@ -227,43 +227,53 @@ void launch_async(const AsyncArgs& a, uint64_t cap, unsigned n_cu, hipStream_t s
 // ---- sweep solver (occ_sweep.hip)
 constexpr uint32_t SW_T = 64;        // txns per serial tile (one 64-bit mask word)
 constexpr uint32_t SW_TA = 4096;     // accesses per tile (SW_T x MAX_ROW_PER_TXN)
-constexpr uint32_t SW_IDN = 16;      // key ids per txn held in the tile record (more: id_ovf)
-constexpr uint32_t SW_OVN = 48;      // key ids per txn in the overflow area (MAX_ROW_PER_TXN - SW_IDN)
+constexpr uint32_t SW_PL = 640;      // probe entries held in a tile record (more: lst_ovf)
+constexpr uint32_t SW_IL = 312;      // insert entries held in a tile record (more: lst_ovf)
+constexpr uint32_t SW_OVF = 2 * SW_TA;  // overflow entries per tile: probes, then inserts
 constexpr uint32_t SW_WA = 4096;     // accesses of one filter wave (64 txns x MAX_ROW_PER_TXN)
 constexpr uint32_t SW_CHUNK = 256;   // txns per filter chunk (4 waves x 64)
 constexpr uint32_t SW_BLOOM_LOG = 17; // Bloom filter of a level's committed keys (16 KiB)
 constexpr int SW_MAX_LEVEL = 24;
 constexpr uint32_t SW_PMAX_TILES = 1024;  // tiles one serial pass may decide (65,536 txns)
 constexpr uint32_t SW_GBITS_MAX = 19;  // key-table slots of one level (LDS bitmap: 64 KiB)
-// A record entry is a key id (slot of the level's key table) packed for the
-// serial pass's LDS bitmap: byte address of the bitmap word << 8 | WR << 5 |
-// bit.  The shift instructions use only the low 5 bits of their shift operand,
-// so a probe is: word at (e >> 8), shifted right by e.
-__host__ __device__ constexpr uint32_t sw_pack(uint32_t id, bool w) {
-  return ((id >> 5) << 10) | (w ? 32u : 0u) | (id & 31u);
+// Per-access key ids (slots of the level's key table) as k_sw_pre records
+// them: id << 6 | WR << 5.
+__host__ __device__ constexpr uint32_t sw_apack(uint32_t id, bool w) {
+  return (id << 6) | (w ? 32u : 0u);
 }
-__host__ __device__ constexpr uint32_t sw_unpack(uint32_t e) { return ((e >> 10) << 5) | (e & 31u); }
-// an unused record entry: one past the largest table slot, i.e. the
-// always-zero word that ends the serial pass's committed bitmap
+__host__ __device__ constexpr uint32_t sw_aid(uint32_t e) { return e >> 6; }
+// A tile-list entry as the serial pass reads it: bitmap word << 12 | txn of
+// the tile << 6 | WR << 5 | bit.  The probe is the LDS word at byte address
+// (e >> 10) & ~3 shifted right by e (shifts use only the low 5 bits).
+__host__ __device__ constexpr uint32_t sw_tpack(uint32_t id, uint32_t t, bool w) {
+  return ((id >> 5) << 12) | (t << 6) | (w ? 32u : 0u) | (id & 31u);
+}
+// an id one past the largest table slot: the always-zero word that ends the
+// serial pass's committed bitmap
 constexpr uint32_t SW_ID_NONE = 1u << SW_GBITS_MAX;
-constexpr uint32_t SW_E_NONE = sw_pack(SW_ID_NONE, false);
-// per-txn meta word of a tile record: flags, and the txn's length in bits 8-15
-constexpr uint32_t SWM_VALID = 1, SWM_PRE = 2, SWM_HASW = 4, SWM_LONG = 8, SWM_STOP = 16;
+constexpr uint32_t SW_A_NONE = sw_apack(SW_ID_NONE, false);
+constexpr uint32_t SW_E_NONE = sw_tpack(SW_ID_NONE, 0, false);
+// per-txn meta word of a tile record
+constexpr uint32_t SWM_VALID = 1, SWM_PRE = 2, SWM_HASW = 4, SWM_STOP = 16;
 // One 64-txn tile of a level's serial range as k_sw_seq reads it (5,120 B).
-// Txn-major: lane t of the serial wave loads its txn's 16 key ids with four
-// 16-B loads.  Keys are replaced by their slot in the level's global key table
-// (`gtab`), so the serial pass keeps the committed set as an LDS bitmap.
+// Only the accesses the serial pass must look at, as two tile-wide lists:
+// probes (accesses whose key an earlier txn of the range writes), grouped by
+// txn (txn t's are [pspan & 0xFFFF, pspan >> 16)), and inserts (writes whose
+// key a later txn of the range accesses).
 struct SwRec {
-  uint32_t id[SW_T][SW_IDN];  // sw_pack(key id, WR); SW_E_NONE past the txn's length
-  uint64_t dep[SW_T];         // dep[t]: earlier txns of the tile writing a key t touches
-  uint32_t meta[SW_T];        // SWM_* (SWM_STOP on every txn: the access budget ends here)
-  uint32_t rtid[SW_T];        // original txn index
+  uint32_t probe[SW_PL];
+  uint32_t ins[SW_IL];
+  uint64_t dep[SW_T];     // dep[t]: earlier txns of the tile writing a key t touches
+  uint32_t meta[SW_T];    // SWM_* (SWM_STOP on every txn: the access budget ends here)
+  uint32_t rtid[SW_T];    // original txn index
+  uint32_t pspan[SW_T];
+  uint32_t np, ni, pad[6];
 };
 struct SwLevel {     // device control words of one level
   uint32_t m;        // list length (written by the previous level's filter)
   uint32_t acc;      // accesses of the list
   uint32_t pos;      // list txns decided by the level's sequential pass
-  uint32_t ccount;   // committed write keys the pass collected
+  uint32_t ccount;   // committed write keys of the pass (k_sw_cout's fill counter)
   uint32_t ticket;   // filter chunk ticket
   uint32_t pad[3];
 };
@@ -281,12 +291,17 @@ struct SwPreArgs {
   uint32_t p_max;
   const uint8_t* state;   // identity list: decisions made before the solver, else null
   SwRec* rec;             // [tiles]
-  uint32_t* id_ovf;       // [tiles][SW_T][SW_OVN] key ids past SW_IDN
+  uint32_t* lst_ovf;      // [tiles][SW_OVF] list entries past the record's
   uint64_t* gtab;         // [1 << gbits] key table (KEY_EMPTY-filled), slot = key id
   uint32_t gbits;
   uint32_t budget;        // accesses the level's tiles may hold (gtab at <= 50% load)
+  uint32_t* first_w;      // [1 << gbits] first writer (list position) per key id, ~0u-filled
+  uint32_t* last_a;       // [1 << gbits] last accessor per key id, 0-filled
+  uint32_t* aent;         // [budget] sw_apack(key id, WR) per access of the serial range
+  uint32_t* apos;         // [budget] list position of the access's txn
   const uint32_t* abandon;
   uint32_t* err;
+  uint64_t* dbg;          // workgroup-0 stamps (DCC_SW_DEBUG) or null
 };
 struct SwSeqArgs {
   const uint32_t* m_dev;
@@ -294,7 +309,7 @@ struct SwSeqArgs {
   uint32_t p_max;
   int write_hasw;
   const SwRec* rec;
-  const uint32_t* id_ovf;
+  const uint32_t* lst_ovf;
   const uint64_t* gtab;
   uint32_t gbits;
   uint8_t* state;
@@ -305,9 +320,21 @@ struct SwSeqArgs {
   SwLevel* lv;
   SwLevel* lv_next;
   uint32_t* next_off;     // the next list's offsets (off[0] = 0 written here)
+  uint64_t* mg;           // out: commit mask per decided tile
   const uint32_t* abandon;
   uint32_t* err;
   uint64_t* dbg;          // per-tile clock stamps (DCC_SW_DEBUG) or null
+};
+struct SwCoutArgs {
+  SwList in;
+  const uint32_t* aent;
+  const uint32_t* apos;
+  const uint64_t* mg;
+  SwLevel* lv;            // pos in, ccount out
+  uint32_t* cbits_out;
+  uint64_t* ckeys_out;
+  uint32_t* bloom_out;
+  const uint32_t* abandon;
 };
 // k_sw_filter / k_sw_scan / k_sw_compact (one argument block for the three)
 struct SwFilterArgs {
@@ -339,11 +366,15 @@ struct SwFilterArgs {
   uint32_t abandon_min, abandon_num, abandon_den;
   uint64_t* gclear;       // the next level's key table, KEY_EMPTY-filled here
   uint64_t gclear_n;
+  uint32_t* fw_clear;     // the next level's first-writer / last-accessor words
+  uint32_t* la_clear;
   uint32_t* err;
   uint64_t* dbg;          // per-workgroup clock stamps (DCC_SW_DEBUG) or null
 };
 void launch_sw_pre(const SwPreArgs& a, unsigned grid, hipStream_t st);
 void launch_sw_seq(const SwSeqArgs& a, hipStream_t st);
+void launch_sw_rows(const SwPreArgs& a, unsigned grid, hipStream_t st);
+void launch_sw_cout(const SwCoutArgs& a, unsigned grid, hipStream_t st);
 void launch_sw_filter(const SwFilterArgs& a, unsigned grid, hipStream_t st);
 void launch_sw_scan(const SwFilterArgs& a, hipStream_t st);
 void launch_sw_compact(const SwFilterArgs& a, unsigned grid, hipStream_t st);
@@ -356,7 +387,7 @@ struct FillJob {
   uint32_t value;
 };
 struct FillArgs {
-  FillJob job[8];
+  FillJob job[12];
   uint32_t n;
 };
 void launch_fill(const FillArgs& a, hipStream_t st);
@@ -368,7 +399,7 @@ struct CopyJob {
   uint32_t words;
 };
 struct GatherArgs {
-  CopyJob job[8];
+  CopyJob job[12];
   uint32_t n;
 };
 void launch_gather(const GatherArgs& a, hipStream_t st);

@@ -225,7 +225,8 @@ __device__ inline uint32_t list_len(const uint32_t* m_dev, uint32_t m_host) {
 // only its first access touches the level's global key table, so a hot key
 // costs one global CAS per tile rather than one per access.
 constexpr uint32_t PRE_MAP = 4096;       // LDS map slots (<= 2048 distinct keys per pass)
-constexpr uint32_t PRE_U = SW_TA / 1024;  // accesses per thread (1024 threads)
+constexpr uint32_t PRE_B = 512;           // threads per workgroup
+constexpr uint32_t PRE_U = SW_TA / PRE_B;  // accesses per thread
 
 __device__ inline uint32_t pre_map_insert(uint64_t* mkey, uint64_t key, bool& first) {
   uint32_t h = sw_hash(key, 12);
@@ -254,15 +255,17 @@ __device__ inline uint32_t pre_map_insert(uint64_t* mkey, uint64_t key, bool& fi
   return 0;  // unreachable: a pass holds <= PRE_MAP distinct keys
 }
 
-__global__ __launch_bounds__(1024) void k_sw_pre(SwPreArgs a) {
+__global__ __launch_bounds__(PRE_B) void k_sw_pre(SwPreArgs a) {
   __shared__ uint64_t mkey[PRE_MAP];
-  __shared__ uint64_t mmask[PRE_MAP];
+  __shared__ uint64_t mmask[PRE_MAP];   // writers of the key in the tile
+  __shared__ uint64_t mamask[PRE_MAP];  // accessors of the key in the tile
   __shared__ uint32_t mgid[PRE_MAP];
   __shared__ uint64_t s_dep[SW_T];
   __shared__ uint32_t s_off[SW_T + 1];
   __shared__ uint32_t s_meta[SW_T];
   __shared__ uint32_t s_bad;
   if (*a.abandon) return;
+    if (a.dbg && blockIdx.x == 0 && threadIdx.x == 0) a.dbg[0] = __builtin_amdgcn_s_memrealtime();
   const uint32_t m = list_len(a.m_dev, a.m_host);
   const uint32_t lim = min(m, a.p_max);
   const uint32_t ntiles = (lim + SW_T - 1) / SW_T;
@@ -291,10 +294,12 @@ __global__ __launch_bounds__(1024) void k_sw_pre(SwPreArgs a) {
     }
     if (j == 0) s_bad = 0;
     __syncthreads();
+    if (a.dbg && blockIdx.x == 0 && threadIdx.x == 0) a.dbg[1] = __builtin_amdgcn_s_memrealtime();
     if (j < nt && s_off[j + 1] < s_off[j]) atomicOr(&s_bad, ERR_OFFSETS);
     const uint32_t A0 = s_off[0], A1 = s_off[nt];
     const uint32_t cnt = A1 >= A0 ? A1 - A0 : 0u;
     __syncthreads();
+    if (a.dbg && blockIdx.x == 0 && threadIdx.x == 0) a.dbg[2] = __builtin_amdgcn_s_memrealtime();
     uint32_t bad = s_bad;
     if (cnt > SW_TA) bad |= ERR_TILE;
     // the level's key table holds `budget` accesses: the serial pass stops here
@@ -305,23 +310,29 @@ __global__ __launch_bounds__(1024) void k_sw_pre(SwPreArgs a) {
       if (j < SW_T) R.meta[j] = SWM_STOP;
       return;
     }
-    // per-thread accesses j + 1024u; flags packed into bit masks over u
+    // per-thread accesses j + PRE_B u; flags packed into bit masks over u.
+    // Every load is issued first (clamped addresses), then the accesses are
+    // classified, so the loads of a thread are in flight together.
     uint64_t key[PRE_U];
     uint32_t lt[PRE_U], slot[PRE_U];
     uint32_t vm = 0, wmk = 0;
+    {
+      uint8_t atv[PRE_U];
+      const uint32_t xmax = cnt ? A0 + cnt - 1 : A0;
 #pragma unroll
-    for (uint32_t u = 0; u < PRE_U; u++) {
-      key[u] = KEY_EMPTY;
-      lt[u] = 0;
-      slot[u] = 0;
-      if (u && cnt <= 1024u * u) continue;  // uniform
-      const uint32_t xr = j + 1024 * u;
-      if (xr < cnt) {
-        vm |= 1u << u;
-        const uint32_t x = A0 + xr;
+      for (uint32_t u = 0; u < PRE_U; u++) {
+        const uint32_t x = min(A0 + j + PRE_B * u, xmax);
         key[u] = a.in.keys[x];
-        if (key[u] == KEY_EMPTY) atomicOr(a.err, ERR_KEY);  // reserved: reported by the host
-        const bool w = a.in.acctype[x] == 1;  // WR (occ.cpp:379-383)
+        atv[u] = a.in.acctype[x];
+      }
+      uint32_t bad_key = 0;
+#pragma unroll
+      for (uint32_t u = 0; u < PRE_U; u++) {
+        lt[u] = 0;
+        slot[u] = 0;
+        const uint32_t xr = j + PRE_B * u;
+        if (xr >= cnt) continue;
+        const uint32_t x = A0 + xr;
         // largest t < nt with s_off[t] <= x (empty txns never own an access)
         uint32_t lo = 0, hi = nt;  // invariant: s_off[lo] <= x < s_off[hi]
         while (hi - lo > 1) {
@@ -330,20 +341,32 @@ __global__ __launch_bounds__(1024) void k_sw_pre(SwPreArgs a) {
           else hi = mid;
         }
         lt[u] = lo;
-        if (w) {
+        if (atv[u] == 1) {  // WR (occ.cpp:379-383)
           wmk |= 1u << u;
           atomicOr(&s_meta[lo], SWM_HASW);
         }
+        if (key[u] == KEY_EMPTY) {
+          // the reserved key is reported by the host; it gets no key id (its
+          // access is recorded as an unused entry)
+          bad_key = 1;
+          a.aent[A0 - (uint32_t)off0 + xr] = SW_A_NONE;
+          a.apos[A0 - (uint32_t)off0 + xr] = k * SW_T;
+        } else {
+          vm |= 1u << u;
+        }
       }
+      if (bad_key) atomicOr(a.err, ERR_KEY);
     }
     // passes over key-hash classes keep each map pass <= 2048 distinct keys
     const uint32_t P = cnt <= PRE_MAP / 2 ? 1u : 2u;
     for (uint32_t p = 0; p < P; p++) {
-      for (uint32_t q = j; q < PRE_MAP; q += 1024) {
+      for (uint32_t q = j; q < PRE_MAP; q += PRE_B) {
         mkey[q] = KEY_EMPTY;
         mmask[q] = 0;
+        mamask[q] = 0;
       }
       __syncthreads();
+    if (a.dbg && blockIdx.x == 0 && threadIdx.x == 0) a.dbg[3] = __builtin_amdgcn_s_memrealtime();
       uint32_t pm = vm;  // this pass's accesses
       if (P > 1)
 #pragma unroll
@@ -357,6 +380,7 @@ __global__ __launch_bounds__(1024) void k_sw_pre(SwPreArgs a) {
         slot[u] = pre_map_insert(mkey, key[u], first);
         if (first) fm |= 1u << u;
         if ((wmk >> u) & 1u) atomicOr((unsigned long long*)&mmask[slot[u]], 1ull << lt[u]);
+        atomicOr((unsigned long long*)&mamask[slot[u]], 1ull << lt[u]);
       }
       // the first access of each key enters it in the global table: every
       // home-bucket read in flight at once, then every CAS, then the rare
@@ -365,10 +389,7 @@ __global__ __launch_bounds__(1024) void k_sw_pre(SwPreArgs a) {
         const uint32_t lb = a.gbits - 2;
         uint4 bx[PRE_U], by[PRE_U];
 #pragma unroll
-        for (uint32_t u = 0; u < PRE_U; u++) {
-          bx[u] = make_uint4(0, 0, 0, 0);
-          by[u] = bx[u];
-          if (!((fm >> u) & 1u)) continue;
+        for (uint32_t u = 0; u < PRE_U; u++) {  // unconditional: all in flight together
           const uint4* hp = (const uint4*)(a.gtab + 4 * (uint64_t)sw_hash(key[u], lb));
           bx[u] = hp[0];
           by[u] = hp[1];
@@ -412,39 +433,145 @@ __global__ __launch_bounds__(1024) void k_sw_pre(SwPreArgs a) {
         }
       }
       __syncthreads();
+    if (a.dbg && blockIdx.x == 0 && threadIdx.x == 0) a.dbg[4] = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
       for (uint32_t u = 0; u < PRE_U; u++) {
         if (!((pm >> u) & 1u)) continue;
         const uint32_t t = lt[u];
-        const uint64_t wm = mmask[slot[u]] & ((1ull << t) - 1ull);  // earlier writers only
+        const uint64_t wmask = mmask[slot[u]];
+        const uint64_t wm = wmask & ((1ull << t) - 1ull);  // earlier writers only
         if (wm) atomicOr((unsigned long long*)&s_dep[t], (unsigned long long)wm);
-        const uint32_t id = sw_pack(mgid[slot[u]], (wmk >> u) & 1u);
-        const uint32_t pos = A0 + j + 1024 * u - s_off[t];
-        if (pos < SW_IDN) R.id[t][pos] = id;
-        else if (pos < SW_IDN + SW_OVN)  // longer txns are rejected by the host (prep)
-          a.id_ovf[((uint64_t)k * SW_T + t) * SW_OVN + (pos - SW_IDN)] = id;
+        const uint32_t gid = mgid[slot[u]];
+        // the key's first writer and last accessor in the level's serial
+        // range (list positions), once per distinct key of the tile
+        if ((fm >> u) & 1u) {
+          if (wmask) atomicMin(&a.first_w[gid], k * SW_T + (uint32_t)__builtin_ctzll(wmask));
+          atomicMax(&a.last_a[gid], k * SW_T + 63u - (uint32_t)__builtin_clzll(mamask[slot[u]]));
+        }
+        const uint32_t xo = A0 - (uint32_t)off0 + j + PRE_B * u;
+        a.aent[xo] = sw_apack(gid, (wmk >> u) & 1u);
+        a.apos[xo] = k * SW_T + t;
       }
       __syncthreads();  // map reuse by the next pass
+    if (a.dbg && blockIdx.x == 0 && threadIdx.x == 0) a.dbg[5] = __builtin_amdgcn_s_memrealtime();
     }
-    // unused entries of the inline id rows, then the per-txn words
-    for (uint32_t q = j; q < SW_T * SW_IDN; q += 1024) {
-      const uint32_t t = q / SW_IDN, pos = q % SW_IDN;
-      const uint32_t len = t < nt ? s_off[t + 1] - s_off[t] : 0u;
-      if (pos >= len) R.id[t][pos] = SW_E_NONE;
-    }
+    // the per-txn words (k_sw_rows adds the row length)
     if (j < SW_T) {
-      const uint32_t len = j < nt ? s_off[j + 1] - s_off[j] : 0u;
       uint32_t mt = s_meta[j];
       if (j < nt) {
-        mt |= SWM_VALID | (min(len, MAX_TXN_LEN) << 8);
-        if (len > SW_IDN) mt |= SWM_LONG;
+        mt |= SWM_VALID;
         if (my_pre) mt |= SWM_PRE;
       }
       R.meta[j] = mt;
       R.dep[j] = s_dep[j];
       R.rtid[j] = my_tid;
     }
+    if (a.dbg && blockIdx.x == 0 && j == 0) {
+      __builtin_amdgcn_s_waitcnt(0);
+      a.dbg[6] = __builtin_amdgcn_s_memrealtime();
+    }
   }
+}
+
+// ---------------------------------------------------------------------------
+// k_sw_rows: the tile's two lists, one wave per tile (lane = txn): only the
+// accesses the serial pass must look at.  An access is probed when an earlier
+// txn of the serial range writes its key ("live": otherwise the key cannot be
+// in C when the txn is decided); a write is inserted into the pass's C when a
+// later txn of the range accesses the key ("needed").  Probes are grouped by
+// txn (prefix sum over the lanes).  The full C of the level (every committed
+// write) is listed afterwards by k_sw_cout.
+__global__ __launch_bounds__(256) void k_sw_rows(SwPreArgs a) {
+  if (*a.abandon) return;
+  const uint32_t m = list_len(a.m_dev, a.m_host);
+  const uint32_t lim = min(m, a.p_max);
+  const uint32_t ntiles = (lim + SW_T - 1) / SW_T;
+  const uint32_t k = blockIdx.x * 4 + (threadIdx.x >> 6), t = lane_id();
+  if (k >= ntiles) return;  // per wave: no barriers below
+  uint64_t* dbg = (a.dbg && k == 0) ? a.dbg : nullptr;
+  auto stamp = [&](int i) {
+    if (dbg) {
+      __builtin_amdgcn_s_waitcnt(0);
+      if (t == 0) dbg[i] = __builtin_amdgcn_s_memrealtime();
+    }
+  };
+  stamp(8);
+  SwRec& R = a.rec[k];
+  const uint32_t meta0 = R.meta[t];
+  if (__builtin_amdgcn_readfirstlane(meta0) & SWM_STOP) return;
+  const uint64_t nnz = a.in.nnz;
+  const uint32_t off0 = (uint32_t)min((uint64_t)a.in.off[0], nnz);
+  const uint32_t nt = min(SW_T, lim - k * SW_T);
+  const uint32_t p = k * SW_T + t;
+  uint32_t s = 0, len = 0;
+  if (t < nt) {
+    s = (uint32_t)min((uint64_t)a.in.off[p], nnz);
+    const uint32_t e = (uint32_t)min((uint64_t)a.in.off[p + 1], nnz);
+    len = e > s ? min(e - s, MAX_TXN_LEN) : 0u;  // longer txns are rejected by the host
+    s -= off0;
+  }
+  stamp(9);
+  const uint32_t idlim = 1u << a.gbits;
+  // pass 1: live / needed bits of the txn's accesses (len <= 64)
+  uint64_t lm = 0, nm = 0;
+  for (uint32_t q0 = 0; ballot64(q0 < len); q0 += 16) {
+    // branch-free: every load is issued (clamped addresses), then masked, so
+    // the 16 + 32 loads of a chunk are in flight together
+    uint32_t ent[16], fw[16], la[16];
+    const uint32_t xl = len ? len - 1 : 0u;
+#pragma unroll
+    for (uint32_t u = 0; u < 16; u++) ent[u] = a.aent[s + min(q0 + u, xl)];
+#pragma unroll
+    for (uint32_t u = 0; u < 16; u++) {
+      const uint32_t id = sw_aid(ent[u]);
+      const uint32_t ic = id < idlim ? id : 0u;
+      fw[u] = a.first_w[ic];
+      la[u] = a.last_a[ic];
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < 16; u++) {
+      const bool in = q0 + u < len && sw_aid(ent[u]) < idlim;
+      lm |= (uint64_t)(in && fw[u] < p) << (q0 + u);
+      nm |= (uint64_t)(in && (ent[u] & 32u) && la[u] > p) << (q0 + u);
+    }
+  }
+  uint32_t np, ni;
+  uint32_t ps = wave_excl_u32((uint32_t)__popcll(lm), np);
+  uint32_t is = wave_excl_u32((uint32_t)__popcll(nm), ni);
+  R.pspan[t] = ps | ((ps + (uint32_t)__popcll(lm)) << 16);
+  if (t == 0) {
+    R.np = np;
+    R.ni = ni;
+  }
+  stamp(10);
+  // pass 2: the entries (the txn's accesses again, from L2)
+  uint32_t* ovf = a.lst_ovf + (uint64_t)k * SW_OVF;
+  for (uint32_t q0 = 0; ballot64(q0 < 64 && ((lm | nm) >> q0) != 0); q0 += 16) {
+    uint32_t ent[16];
+    const uint32_t sel = (uint32_t)(((lm | nm) >> q0) & 0xFFFFu);
+    const uint32_t xl = len ? len - 1 : 0u;
+#pragma unroll
+    for (uint32_t u = 0; u < 16; u++) ent[u] = a.aent[s + min(q0 + u, xl)];
+#pragma unroll
+    for (uint32_t u = 0; u < 16; u++) {
+      if (!((sel >> u) & 1u)) continue;
+      const uint32_t id = sw_aid(ent[u]);
+      const bool w = (ent[u] & 32u) != 0;
+      if ((lm >> (q0 + u)) & 1ull) {
+        const uint32_t e = sw_tpack(id, t, false);
+        if (ps < SW_PL) R.probe[ps] = e;
+        else ovf[ps - SW_PL] = e;
+        ps++;
+      }
+      if ((nm >> (q0 + u)) & 1ull) {
+        const uint32_t e = sw_tpack(id, t, w);
+        if (is < SW_IL) R.ins[is] = e;
+        else ovf[SW_TA + is - SW_IL] = e;
+        is++;
+      }
+    }
+  }
+  stamp(11);
 }
 
 // ---------------------------------------------------------------------------
@@ -475,18 +602,25 @@ __device__ inline void lds_st(uint32_t* p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// committed-set bitmap probe / insert of a packed record entry (sw_pack)
+// committed-set bitmap probe / insert of a tile-list entry (sw_tpack)
 __device__ inline uint32_t cb_probe(const uint32_t* cb, uint32_t e) {
-  return *(const uint32_t*)((const char*)cb + (e >> 8)) >> (e & 31u);
+  return *(const uint32_t*)((const char*)cb + ((e >> 10) & ~3u)) >> (e & 31u);
 }
 __device__ inline void cb_insert_w(uint32_t* cb, uint32_t e) {
-  atomicOr((uint32_t*)((char*)cb + (e >> 8)), ((e >> 5) & 1u) << (e & 31u));
+  atomicOr((uint32_t*)((char*)cb + ((e >> 10) & ~3u)), ((e >> 5) & 1u) << (e & 31u));
+}
+// any bit of hm (entries q0 .. q0+63) inside the entry range [ps, pe)
+__device__ inline bool seg_any(uint64_t hm, uint32_t ps, uint32_t pe, uint32_t q0) {
+  const uint32_t lo = max(ps, q0), hi = min(pe, q0 + 64);
+  if (hi <= lo) return false;
+  const uint32_t n = hi - lo;
+  const uint64_t msk = n >= 64 ? ~0ull : ((1ull << n) - 1ull);
+  return ((hm >> (lo - q0)) & msk) != 0;
 }
 
 __global__ __launch_bounds__(1024) void k_sw_seq(SwSeqArgs a) {
   __shared__ uint32_t cbits[(1u << SW_GBITS_MAX) / 32 + 1];  // + the SW_ID_NONE word
   __shared__ uint64_t s_M[SW_PMAX_TILES];  // commit mask per decided tile
-  __shared__ uint32_t sbloom[(1u << SW_BLOOM_LOG) / 32];
   __shared__ __attribute__((aligned(16))) SwRec ring[SEQ_RING];
   __shared__ uint32_t s_ready[SEQ_RING];
   __shared__ uint32_t s_done, s_stop, s_k;
@@ -495,7 +629,6 @@ __global__ __launch_bounds__(1024) void k_sw_seq(SwSeqArgs a) {
   const uint32_t m = list_len(a.m_dev, a.m_host);
   const uint32_t lim = min(m, a.p_max);
   const uint32_t ntiles = min((lim + SW_T - 1) / SW_T, SW_PMAX_TILES);
-  for (uint32_t q = j; q < (1u << SW_BLOOM_LOG) / 32; q += 1024) sbloom[q] = 0;
   // the filter of this level starts from a clean look-back and ticket; the
   // next level's list is empty unless the filter writes it
   if (j == 0) {
@@ -529,7 +662,7 @@ __global__ __launch_bounds__(1024) void k_sw_seq(SwSeqArgs a) {
         }
         if (lds_ld(&s_done) + SEQ_RING > k) break;
         pw++;
-        __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(8);
       }
       if (stopped) break;
       const uint4* src = (const uint4*)(a.rec + k);
@@ -543,36 +676,58 @@ __global__ __launch_bounds__(1024) void k_sw_seq(SwSeqArgs a) {
     }
     if (dbg && lane == 0 && pw) atomicAdd((unsigned long long*)&dbg[7], (unsigned long long)pw);
   } else if (ntiles) {
+    // software pipelined: tile k+1's record (per-txn words and the first
+    // chunk of each list) is read while tile k resolves
     uint32_t k = 0, cw = 0;
+    __builtin_amdgcn_s_setprio(3);  // the serial wave issues ahead of the producers
+    const uint64_t cyc0 = __builtin_amdgcn_s_memtime();
+    while (lds_ld(&s_ready[0]) != 1u) {
+      cw++;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    uint64_t cdep;
+    uint32_t cmeta, cspan, cnp, cni, cpe, cie;
+    auto read_rec = [&](const SwRec& T) {
+      cdep = T.dep[lane];
+      cmeta = T.meta[lane];
+      cspan = T.pspan[lane];
+      cnp = T.np;
+      cni = T.ni;
+      cpe = T.probe[lane];
+      cie = T.ins[lane];
+    };
+    read_rec(ring[0]);
     for (; k < ntiles; k++) {
-      const uint32_t slot = k % SEQ_RING;
-      while (lds_ld(&s_ready[slot]) != k + 1) {
-        cw++;
-        __builtin_amdgcn_s_sleep(1);
-      }
-      const SwRec& T = ring[slot];
-      const uint4* ip = (const uint4*)T.id[lane];
-      const uint4 i0 = ip[0], i1 = ip[1], i2 = ip[2], i3 = ip[3];
-      const uint64_t dep = T.dep[lane];
-      const uint32_t meta = T.meta[lane];
+      const uint32_t meta = cmeta;
       if (__builtin_amdgcn_readfirstlane(meta) & SWM_STOP) break;
-      const uint32_t ids[SW_IDN] = {i0.x, i0.y, i0.z, i0.w, i1.x, i1.y, i1.z, i1.w,
-                                    i2.x, i2.y, i2.z, i2.w, i3.x, i3.y, i3.z, i3.w};
-      // (1) probe C: a txn touching a committed key is dead
-      uint32_t hit = 0;
-#pragma unroll
-      for (uint32_t q = 0; q < SW_IDN; q++) hit |= cb_probe(cbits, ids[q]);
-      hit &= 1u;
-      // txns with more than SW_IDN accesses (rare): the tail from the
-      // overflow area, synchronously
-      const bool lng = (meta & SWM_LONG) != 0;
-      const uint64_t lmask = ballot64(lng);
-      const uint32_t* ovf = a.id_ovf + ((uint64_t)k * SW_T + lane) * SW_OVN;
-      const uint32_t extra = lng ? min((meta >> 8) - SW_IDN, SW_OVN) : 0u;
-      if (lmask)
-        for (uint32_t q = 0; q < extra; q++) hit |= cb_probe(cbits, ld_sync(ovf + q)) & 1u;
+      const uint64_t dep = cdep;
+      const uint32_t ps = cspan & 0xFFFFu, pe = cspan >> 16;
+      const uint32_t np = __builtin_amdgcn_readfirstlane(cnp);
+      const uint32_t ni = __builtin_amdgcn_readfirstlane(cni);
+      const uint32_t e0 = lane < np ? cpe : SW_E_NONE, i0 = lane < ni ? cie : SW_E_NONE;
+      const uint32_t slot = k % SEQ_RING;
+      const uint32_t* ovf = a.lst_ovf + (uint64_t)k * SW_OVF;
+      // (1) probe C, 64 list entries per round: a txn touching a committed
+      // key is dead
+      const uint32_t h0 = cb_probe(cbits, e0) & 1u;
+      // the next record (its flag read shares this round trip)
+      const uint32_t kn = k + 1, sn = kn % SEQ_RING;
+      if (kn < ntiles) {
+        while (lds_ld(&s_ready[sn]) != kn + 1) {
+          cw++;
+          __builtin_amdgcn_s_sleep(1);
+        }
+        read_rec(ring[sn]);
+      }
+      bool kill = seg_any(ballot64(h0), ps, pe, 0);
+      for (uint32_t q0 = 64; q0 < np; q0 += 64) {  // long lists (uniform)
+        const uint32_t q = q0 + lane;
+        uint32_t e = SW_E_NONE;
+        if (q < np) e = q < SW_PL ? ring[slot].probe[q] : ld_sync(ovf + (q - SW_PL));
+        kill |= seg_any(ballot64(cb_probe(cbits, e) & 1u), ps, pe, q0);
+      }
       // (2) the tile's serial order: fixed point over the dependency masks
-      const bool cand = (meta & SWM_VALID) && !(meta & SWM_PRE) && !hit;
+      const bool cand = (meta & SWM_VALID) && !(meta & SWM_PRE) && !kill;
       uint64_t U = ballot64(cand), M = 0;
       while (U) {
         const bool mu = (U >> lane) & 1ull;
@@ -582,16 +737,22 @@ __global__ __launch_bounds__(1024) void k_sw_seq(SwSeqArgs a) {
         M |= cm;
         U &= ~(cm | am);
       }
-      // (3) committed write keys join C
-      if (((M >> lane) & 1ull) && (meta & SWM_HASW)) {
-#pragma unroll
-        for (uint32_t q = 0; q < SW_IDN; q++) cb_insert_w(cbits, ids[q]);
-        for (uint32_t q = 0; q < extra; q++) cb_insert_w(cbits, ld_sync(ovf + q));
+      // (3) needed writes of committed txns join C
+      if (M) {
+        if ((M >> ((i0 >> 6) & 63u)) & 1ull) cb_insert_w(cbits, i0);
+        for (uint32_t q0 = 64; q0 < ni; q0 += 64) {  // long lists (uniform)
+          const uint32_t q = q0 + lane;
+          uint32_t e = SW_E_NONE;
+          if (q < ni) e = q < SW_IL ? ring[slot].ins[q] : ld_sync(ovf + SW_TA + (q - SW_IL));
+          if ((M >> ((e >> 6) & 63u)) & 1ull) cb_insert_w(cbits, e);
+        }
       }
-      if (lane == 0) {
-        s_M[k] = M;
-        lds_st(&s_done, k + 1);  // the slot's reads are complete (values used above)
-      }
+      if (lane == 0) s_M[k] = M;
+      // free consumed slots four at a time (the release waits for this
+      // wave's LDS operations); tile k's slot stays held until kn is
+      // published, tile kn's until later
+      if ((kn & 3u) == 0 || kn == ntiles)
+        if (lane == 0) lds_st(&s_done, kn);
     }
     if (lane == 0) {
       s_k = k;
@@ -600,6 +761,7 @@ __global__ __launch_bounds__(1024) void k_sw_seq(SwSeqArgs a) {
         dbg[2] = __builtin_amdgcn_s_memrealtime();
         dbg[5] = cw;
         dbg[6] = k;
+        dbg[8] = __builtin_amdgcn_s_memtime() - cyc0;
       }
     }
   }
@@ -618,73 +780,56 @@ __global__ __launch_bounds__(1024) void k_sw_seq(SwSeqArgs a) {
     __syncthreads();
     if (j == 0) dbg[3] = __builtin_amdgcn_s_memrealtime();
   }
-  // C for the filter: the committed-id bitmap, the committed keys (ids
-  // listed in LDS in bitmap order, chunk by chunk) and their Bloom filter
-  constexpr uint32_t WPT = (1u << SW_GBITS_MAX) / 32 / 1024;  // bitmap words per thread
-  uint32_t* list = (uint32_t*)ring;  // the record ring is free now
-  constexpr uint32_t LCAP = sizeof(ring) / 4;
-  uint32_t myc = 0;  // committed ids in this thread's words j*WPT .. +WPT
-  for (uint32_t i = 0; i < WPT; i++) {
-    const uint32_t q = j * WPT + i;
-    if (q < nwords) {
-      const uint32_t w = cbits[q];
-      a.cbits_out[q] = w;
-      myc += (uint32_t)__popc(w);
-    }
-  }
-  // block exclusive scan of the per-thread counts
-  __shared__ uint32_t s_wsum[16];
-  uint32_t tot;
-  const uint32_t wex = wave_excl_u32(myc, tot);
-  if (lane == 0) s_wsum[wv] = tot;
-  __syncthreads();
-  uint32_t base = wex, ccount = 0;
-  for (uint32_t w = 0; w < 16; w++) {
-    const uint32_t x = s_wsum[w];
-    if (w < wv) base += x;
-    ccount += x;
-  }
-  for (uint32_t c0 = 0; c0 < ccount; c0 += LCAP) {
-    // list entries [c0, c0 + LCAP): this thread's ids in bitmap order
-    if (base + myc > c0 && base < c0 + LCAP) {
-      uint32_t r = base;
-      for (uint32_t i = 0; i < WPT; i++) {
-        const uint32_t q = j * WPT + i;
-        uint32_t w = q < nwords ? cbits[q] : 0u;
-        while (w) {
-          if (r >= c0 && r < c0 + LCAP) list[r - c0] = q * 32 + (uint32_t)__builtin_ctz(w);
-          r++;
-          w &= w - 1;
-        }
-      }
-    }
-    __syncthreads();
-    const uint32_t n = min(LCAP, ccount - c0);
-    for (uint32_t i0 = 0; i0 < n; i0 += 1024 * 8) {
-      uint64_t kk[8];
-#pragma unroll
-      for (uint32_t u = 0; u < 8; u++) {
-        const uint32_t i = i0 + u * 1024 + j;
-        kk[u] = i < n ? a.gtab[list[i]] : 0ull;
-      }
-#pragma unroll
-      for (uint32_t u = 0; u < 8; u++) {
-        const uint32_t i = i0 + u * 1024 + j;
-        if (i >= n) continue;
-        uint32_t b1, b2;
-        bloom_bits(kk[u], b1, b2);
-        atomicOr(&sbloom[b1 >> 5], 1u << (b1 & 31));
-        atomicOr(&sbloom[b2 >> 5], 1u << (b2 & 31));
-        a.ckeys_out[c0 + i] = kk[u];
-      }
-    }
-    __syncthreads();
-  }
-  for (uint32_t q = j; q < (1u << SW_BLOOM_LOG) / 32; q += 1024) a.bloom_out[q] = sbloom[q];
+  // C for the filter is listed by k_sw_cout from the committed masks: clear
+  // its bitmap, Bloom filter and count here
+  for (uint32_t q = j; q < k; q += 1024) a.mg[q] = s_M[q];
+  for (uint32_t q = j; q < nwords; q += 1024) a.cbits_out[q] = 0;
+  for (uint32_t q = j; q < (1u << SW_BLOOM_LOG) / 32; q += 1024) a.bloom_out[q] = 0;
   if (j == 0) {
     a.lv->pos = min(k * SW_T, lim);
-    a.lv->ccount = ccount;
+    a.lv->ccount = 0;  // k_sw_cout's fill counter
     if (dbg) dbg[4] = __builtin_amdgcn_s_memrealtime();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_sw_cout: the level's committed set C for the filter, across the grid:
+// every WR access of a committed txn of the serial range [0, pos) gives its
+// key (Bloom filter, key list with wave-aggregated positions: the filter
+// uses them as a set) and its key id (bitmap for the exact check).
+__global__ __launch_bounds__(256) void k_sw_cout(SwCoutArgs a) {
+  if (*a.abandon) return;
+  const uint32_t lane = lane_id();
+  const uint64_t nnz = a.in.nnz;
+  const uint32_t off0 = (uint32_t)min((uint64_t)a.in.off[0], nnz);
+  const uint32_t pos = a.lv->pos;
+  const uint32_t range = (uint32_t)min((uint64_t)a.in.off[pos], nnz) - off0;
+  const uint32_t stride = gridDim.x * 256;
+  for (uint32_t x0 = blockIdx.x * 256 + (threadIdx.x & ~63u); x0 < range; x0 += stride) {
+    const uint32_t x = x0 + lane;
+    bool c = false;
+    uint32_t ent = 0;
+    if (x < range) {
+      ent = a.aent[x];
+      if (ent & 32u) {
+        const uint32_t p = a.apos[x];
+        c = (a.mg[p >> 6] >> (p & 63u)) & 1ull;
+      }
+    }
+    const uint64_t cm = ballot64(c);
+    if (!cm) continue;  // uniform
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(&a.lv->ccount, (uint32_t)__popcll(cm));
+    base = __shfl(base, 0);
+    if (!c) continue;
+    const uint64_t key = a.in.keys[off0 + x];
+    a.ckeys_out[base + (uint32_t)__popcll(cm & lanemask_lt())] = key;
+    const uint32_t id = sw_aid(ent);
+    if (id < SW_ID_NONE) atomicOr(&a.cbits_out[id >> 5], 1u << (id & 31u));
+    uint32_t b1, b2;
+    bloom_bits(key, b1, b2);
+    atomicOr(&a.bloom_out[b1 >> 5], 1u << (b1 & 31));
+    atomicOr(&a.bloom_out[b2 >> 5], 1u << (b2 & 31));
   }
 }
 
@@ -721,41 +866,55 @@ __device__ inline bool c_exact(const SwFilterArgs& a, uint64_t key) {
   return false;
 }
 constexpr uint32_t F_STASH = 256;  // Bloom-positive keys kept in LDS per wave
+constexpr uint32_t F_XS = 4096;    // exact-only filter: LDS set slots
+constexpr uint32_t F_XCAP = 2048;  // ... for C of up to this many keys (<= 50% load)
 
 // ---------------------------------------------------------------------------
 // k_sw_filter: list txns [pos, m) against C, 64 per wave, grid-stride (no
 // cross-workgroup waits).  A txn touching a key of C is killed; the others
 // get a survivor bit and per-tile counts for the compaction.
+// Two instances: X (exact) when C has <= F_XCAP keys -- C as an LDS hash set
+// and nothing else, so a workgroup holds 36 KB of LDS and four fit a CU --
+// and the Bloom-filtered one otherwise.  Both are launched; the one whose
+// case it is not returns at once.
+template <bool X>
 __global__ __launch_bounds__(SW_CHUNK) void k_sw_filter(SwFilterArgs a) {
-  __shared__ uint32_t bl[(1u << SW_BLOOM_LOG) / 32];
-  __shared__ __attribute__((aligned(16))) uint64_t cex[F_EXACT];
+  constexpr uint32_t CS = X ? F_XS : F_EXACT;  // exact-set slots
+  __shared__ uint32_t bl[X ? 1 : (1u << SW_BLOOM_LOG) / 32];
+  __shared__ __attribute__((aligned(16))) uint64_t cex[CS];
   __shared__ uint64_t s_hit[FW][SW_WA / 64];
   __shared__ uint64_t s_wr[FW][SW_WA / 64];
-  __shared__ uint64_t s_stash[FW][F_STASH];
-  __shared__ uint32_t s_wpre[FW][SW_WA / 64];
+  __shared__ uint64_t s_stash[FW][X ? 1 : F_STASH];
+  __shared__ uint32_t s_wpre[FW][X ? 1 : SW_WA / 64];
   const uint32_t j = threadIdx.x, lane = lane_id(), wv = j >> 6;
   if (*a.abandon) return;
   const uint32_t m = list_len(a.m_dev, a.m_host);
   const uint32_t pos = a.lv->pos;
   const uint32_t ccount = a.lv->ccount;
+  if (X != (ccount <= F_XCAP)) return;
   // the next level's key table (its pre-pass runs after this kernel)
   for (uint64_t q = (uint64_t)blockIdx.x * SW_CHUNK + j; q < a.gclear_n;
-       q += (uint64_t)gridDim.x * SW_CHUNK)
+       q += (uint64_t)gridDim.x * SW_CHUNK) {
     a.gclear[q] = KEY_EMPTY;
+    a.fw_clear[q] = ~0u;
+    a.la_clear[q] = 0u;
+  }
   if (pos >= m) return;
   const uint32_t n64 = (m - pos + 63) / 64;
   const uint64_t nnz = a.in.nnz;
-  const bool small = ccount <= F_EXACT / 2;  // exact checks in LDS
+  const bool small = X || ccount <= F_EXACT / 2;  // exact checks in LDS
   {
-    const uint4* src = (const uint4*)a.bloom;
-    uint4* dst = (uint4*)bl;
-    for (uint32_t q = j; q < (1u << SW_BLOOM_LOG) / 128; q += SW_CHUNK) dst[q] = src[q];
+    if (!X) {
+      const uint4* src = (const uint4*)a.bloom;
+      uint4* dst = (uint4*)bl;
+      for (uint32_t q = j; q < (1u << SW_BLOOM_LOG) / 128; q += SW_CHUNK) dst[q] = src[q];
+    }
     if (small)
-      for (uint32_t q = j; q < F_EXACT; q += SW_CHUNK) cex[q] = KEY_EMPTY;
+      for (uint32_t q = j; q < CS; q += SW_CHUNK) cex[q] = KEY_EMPTY;
   }
   __syncthreads();
   if (small) {
-    for (uint32_t q = j; q < ccount; q += SW_CHUNK) lset_insert<F_EXACT>(cex, a.ckeys[q]);
+    for (uint32_t q = j; q < ccount; q += SW_CHUNK) lset_insert<CS>(cex, a.ckeys[q]);
     __syncthreads();
   }
   uint64_t* hit = s_hit[wv];
@@ -806,16 +965,23 @@ __global__ __launch_bounds__(SW_CHUNK) void k_sw_filter(SwFilterArgs a) {
         if (b0 + 64 * u >= span) continue;  // uniform; no break: the loop must unroll
         const bool in = xr < span;
         bad_key |= in && key[u] == KEY_EMPTY;
-        uint32_t b1, b2;
-        bloom_bits(key[u], b1, b2);
-        const uint32_t wa = bl[b1 >> 5], wb = bl[b2 >> 5];
-        const bool h = in && (((wa >> (b1 & 31u)) & (wb >> (b2 & 31u)) & 1u) != 0);
-        const uint64_t hb = ballot64(h), wbm = ballot64(in && at[u] == 1);
-        if (h) {
-          const uint32_t ci = npos + (uint32_t)__popcll(hb & lanemask_lt());
-          if (ci < F_STASH) stash[ci] = key[u];
+        bool h;
+        if (X) {
+          h = in && lset_find<CS>(cex, key[u]);
+        } else {
+          uint32_t b1, b2;
+          bloom_bits(key[u], b1, b2);
+          const uint32_t wa = bl[b1 >> 5], wb = bl[b2 >> 5];
+          h = in && (((wa >> (b1 & 31u)) & (wb >> (b2 & 31u)) & 1u) != 0);
         }
-        npos += (uint32_t)__popcll(hb);
+        const uint64_t hb = ballot64(h), wbm = ballot64(in && at[u] == 1);
+        if (!X) {
+          if (h) {
+            const uint32_t ci = npos + (uint32_t)__popcll(hb & lanemask_lt());
+            if (ci < F_STASH) stash[ci] = key[u];
+          }
+          npos += (uint32_t)__popcll(hb);
+        }
         if (lane == 0) {
           hit[(b0 >> 6) + u] = hb;
           wr[(b0 >> 6) + u] = wbm;
@@ -826,27 +992,32 @@ __global__ __launch_bounds__(SW_CHUNK) void k_sw_filter(SwFilterArgs a) {
     // per txn (the wave's own LDS rows: no barrier needed)
     const uint32_t rlo = s - A0, rlen = e - s;
     const bool ok = valid && (rlen == 0 || (uint64_t)rlo + rlen <= span);
-    {
-      const uint32_t pw = lane < nw ? (uint32_t)__popcll(hit[lane]) : 0u;
-      uint32_t ptot;
-      const uint32_t pre = wave_excl_u32(pw, ptot);
-      if (lane < nw) s_wpre[wv][lane] = pre;
-    }
-    // Bloom-positive accesses of the txn, verified one by one (almost always
-    // the first is a true hit): the key from the LDS stash, then the exact set
     bool killed = false;
-    if (cand && ok && rlen) {
-      for (uint32_t x = rlo; x < rlo + rlen; x++) {
-        const uint32_t nx = range_next(hit, x, rlo + rlen);
-        if (nx >= rlo + rlen) break;
-        const uint32_t ci = s_wpre[wv][nx >> 6] +
-                            (uint32_t)__popcll(hit[nx >> 6] & ((1ull << (nx & 63)) - 1ull));
-        const uint64_t kx = ci < F_STASH ? stash[ci] : a.in.keys[A0 + nx];
-        if (small ? lset_find<F_EXACT>(cex, kx) : c_exact(a, kx)) {
-          killed = true;
-          break;
+    if (X) {
+      // every LDS hit is exact
+      killed = cand && ok && rlen && range_any(hit, rlo, rlen);
+    } else {
+      {
+        const uint32_t pw = lane < nw ? (uint32_t)__popcll(hit[lane]) : 0u;
+        uint32_t ptot;
+        const uint32_t pre = wave_excl_u32(pw, ptot);
+        if (lane < nw) s_wpre[wv][lane] = pre;
+      }
+      // Bloom-positive accesses of the txn, verified one by one (almost always
+      // the first is a true hit): the key from the LDS stash, then the exact set
+      if (cand && ok && rlen) {
+        for (uint32_t x = rlo; x < rlo + rlen; x++) {
+          const uint32_t nx = range_next(hit, x, rlo + rlen);
+          if (nx >= rlo + rlen) break;
+          const uint32_t ci = s_wpre[wv][nx >> 6] +
+                              (uint32_t)__popcll(hit[nx >> 6] & ((1ull << (nx & 63)) - 1ull));
+          const uint64_t kx = ci < F_STASH ? stash[ci] : a.in.keys[A0 + nx];
+          if (small ? lset_find<CS>(cex, kx) : c_exact(a, kx)) {
+            killed = true;
+            break;
+          }
+          x = nx;
         }
-        x = nx;
       }
     }
     if (valid && a.write_hasw) a.hasw[tid] = ok && rlen && range_any(wr, rlo, rlen) ? 1 : 0;
@@ -1023,11 +1194,18 @@ __global__ __launch_bounds__(SW_CHUNK) void k_sw_compact(SwFilterArgs a) {
 
 // ---------------------------------------------------------------------------
 void launch_sw_pre(const SwPreArgs& a, unsigned grid, hipStream_t st) {
-  k_sw_pre<<<grid ? grid : 1u, 1024, 0, st>>>(a);
+  k_sw_pre<<<grid ? grid : 1u, PRE_B, 0, st>>>(a);
 }
 void launch_sw_seq(const SwSeqArgs& a, hipStream_t st) { k_sw_seq<<<1, 1024, 0, st>>>(a); }
+void launch_sw_rows(const SwPreArgs& a, unsigned grid, hipStream_t st) {
+  k_sw_rows<<<grid ? grid : 1u, 256, 0, st>>>(a);
+}
+void launch_sw_cout(const SwCoutArgs& a, unsigned grid, hipStream_t st) {
+  k_sw_cout<<<grid ? grid : 1u, 256, 0, st>>>(a);
+}
 void launch_sw_filter(const SwFilterArgs& a, unsigned grid, hipStream_t st) {
-  k_sw_filter<<<grid ? grid : 1u, SW_CHUNK, 0, st>>>(a);
+  k_sw_filter<true><<<grid ? grid : 1u, SW_CHUNK, 0, st>>>(a);
+  k_sw_filter<false><<<grid ? grid : 1u, SW_CHUNK, 0, st>>>(a);
 }
 void launch_sw_scan(const SwFilterArgs& a, hipStream_t st) { k_sw_scan<<<1, 1024, 0, st>>>(a); }
 void launch_sw_compact(const SwFilterArgs& a, unsigned grid, hipStream_t st) {
