@@ -451,10 +451,14 @@ static uint32_t sw_pmax(int level) {
 static size_t sw_ctl_bytes() { return (SW_MAX_LEVEL + 2) * sizeof(SwLevel) + 64; }
 // key-table slots of a level: twice the accesses of p_max 16-access txns
 static uint32_t sw_gbits(int level) {
+  // key-table slots of a level: four times the accesses of p_max 16-access
+  // txns, so the table stays <= 25% full and a home bucket pair almost never
+  // overflows (the pre-pass resolves an insert in one read + one CAS)
   uint32_t b = 12;
-  while (b < SW_GBITS_MAX && (1ull << b) < 2ull * sw_pmax(level) * 16) b++;
+  while (b < SW_GBITS_MAX && (1ull << b) < 4ull * sw_pmax(level) * 16) b++;
   return b;
 }
+static uint32_t sw_budget(int level) { return 1u << (sw_gbits(level) - 2); }
 
 int dcc_ctx::sweep_reserve(const DevBatch& d) {
   const uint64_t tiles = SW_PMAX_TOP / SW_T;
@@ -526,10 +530,10 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1) {
     SwPreArgs pa{in, mdev, n, pmax, top ? (const uint8_t*)state.p : nullptr,
                  (SwRec*)sw_rec.p, (uint32_t*)sw_rk.p,
                  gtab0 + (size_t)(l & 1) * (1ull << SW_GBITS_MAX), sw_gbits(l),
-                 1u << (sw_gbits(l) - 1), fw, la, aent, apos, abandon, err, nullptr};
+                 sw_budget(l), fw, la, aent, apos, abandon, err, nullptr};
     if (sw_debug && l < 4) pa.dbg = (uint64_t*)sw_dbg.p + 4096 + 4 * 256 * 8 + (size_t)l * 64 * 8;
     launch_sw_pre(pa, (unsigned)tiles, stream);
-    launch_sw_rows(pa, (unsigned)((tiles + 3) / 4), stream);
+    launch_sw_rows(pa, (unsigned)tiles, stream);
     SwSeqArgs sa{mdev, n, pmax, top ? 1 : 0, (const SwRec*)sw_rec.p, (const uint32_t*)sw_rk.p,
                  gtab0 + (size_t)(l & 1) * (1ull << SW_GBITS_MAX), sw_gbits(l),
                  (uint8_t*)state.p, (uint8_t*)hasw.p,
@@ -577,8 +581,7 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1) {
     fa.la_clear = la;
     fa.err = err;
     fa.dbg = (sw_debug && l < 4) ? (uint64_t*)sw_dbg.p + 4096 + (size_t)l * 256 * 8 : nullptr;
-    launch_sw_filter(fa, fgrid, stream);
-    launch_sw_scan(fa, stream);
+    launch_sw_filter(fa, fgrid, top, stream);
     launch_sw_compact(fa, fgrid, stream);
     if (top && profiling) CK(hipEventRecord(pev[2], stream));
   }
@@ -827,7 +830,7 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
                     (pp[1] - pp[0]) * 0.01, (pp[2] - pp[1]) * 0.01, (pp[3] - pp[2]) * 0.01,
                     (pp[4] - pp[3]) * 0.01, (pp[5] - pp[4]) * 0.01, (pp[6] - pp[5]) * 0.01);
           if (pp[11])
-            fprintf(stderr, "  rows L%d (us): offsets %.2f pass1 %.2f pass2 %.2f\n", l,
+            fprintf(stderr, "  rows L%d (us): offsets %.2f flags %.2f lists %.2f\n", l,
                     (pp[9] - pp[8]) * 0.01, (pp[10] - pp[9]) * 0.01, (pp[11] - pp[10]) * 0.01);
         }
         if (nw)

@@ -342,6 +342,7 @@ struct SwFilterArgs {
   const uint32_t* m_dev;
   uint32_t m_host;
   int cand_state;         // identity list: only UNDECIDED txns are candidates
+  int exact_launched;     // the exact-set filter instance runs too (small C is its case)
   int write_hasw;
   uint32_t level;
   const uint64_t* gtab;   // the level's key table / committed ids / Bloom filter /
@@ -375,7 +376,7 @@ void launch_sw_pre(const SwPreArgs& a, unsigned grid, hipStream_t st);
 void launch_sw_seq(const SwSeqArgs& a, hipStream_t st);
 void launch_sw_rows(const SwPreArgs& a, unsigned grid, hipStream_t st);
 void launch_sw_cout(const SwCoutArgs& a, unsigned grid, hipStream_t st);
-void launch_sw_filter(const SwFilterArgs& a, unsigned grid, hipStream_t st);
+void launch_sw_filter(const SwFilterArgs& a, unsigned grid, bool exact_too, hipStream_t st);
 void launch_sw_scan(const SwFilterArgs& a, hipStream_t st);
 void launch_sw_compact(const SwFilterArgs& a, unsigned grid, hipStream_t st);
 

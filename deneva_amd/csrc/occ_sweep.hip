@@ -57,22 +57,28 @@ __device__ inline uint32_t sw_hash(uint64_t key, uint32_t log2s) {
 __device__ inline uint32_t gtab_insert(uint64_t* gt, uint32_t gbits, uint64_t key) {
   const uint32_t nbm = (1u << (gbits - 2)) - 1u;
   uint32_t b = sw_hash(key, gbits - 2);
-  for (uint32_t q = 0; q <= nbm; q++) {
+  for (uint32_t q = 0; q <= nbm;) {
+    const uint4* p = (const uint4*)(gt + 4 * b);
+    const uint4 x = p[0], y = p[1];
+    const uint64_t sv[4] = {((uint64_t)x.y << 32) | x.x, ((uint64_t)x.w << 32) | x.z,
+                            ((uint64_t)y.y << 32) | y.x, ((uint64_t)y.w << 32) | y.z};
+    uint32_t fre = 4;
 #pragma unroll
     for (uint32_t i = 0; i < 4; i++) {
-      uint64_t* slot = gt + 4 * b + i;
-      const uint64_t v = *slot;
-      if (v == key) return 4 * b + i;
-      if (v == KEY_EMPTY) {
-        const unsigned long long prev = atomicCAS((unsigned long long*)slot,
-                                                  (unsigned long long)KEY_EMPTY,
-                                                  (unsigned long long)key);
-        if (prev == KEY_EMPTY || prev == key) return 4 * b + i;
-      }
+      if (sv[i] == key) return 4 * b + i;
+      if (sv[i] == KEY_EMPTY && fre == 4) fre = i;
     }
-    b = (b + 1) & nbm;
+    if (fre < 4) {
+      const unsigned long long prev = atomicCAS((unsigned long long*)(gt + 4 * b + fre),
+                                                (unsigned long long)KEY_EMPTY,
+                                                (unsigned long long)key);
+      if (prev == KEY_EMPTY || prev == key) return 4 * b + fre;
+      continue;  // lost the slot: read the bucket again
+    }
+    b = (b + 1) & nbm;  // full bucket: the next one
+    q++;
   }
-  return 0;  // unreachable: the access budget keeps the table <= 50% full
+  return 0;  // unreachable: the access budget keeps the table <= 25% full
 }
 // slot of `key`, or ~0u when absent
 __device__ inline uint32_t gtab_find(const uint64_t* gt, uint32_t gbits, uint64_t key) {
@@ -482,96 +488,104 @@ __global__ __launch_bounds__(PRE_B) void k_sw_pre(SwPreArgs a) {
 // txn (prefix sum over the lanes).  The full C of the level (every committed
 // write) is listed afterwards by k_sw_cout.
 __global__ __launch_bounds__(256) void k_sw_rows(SwPreArgs a) {
+  __shared__ uint32_t s_off[SW_T + 1];
+  __shared__ uint32_t s_ent[SW_TA];  // the tile's access entries (sw_apack)
+  __shared__ uint8_t s_flag[SW_TA];  // live | needed << 1 per access
   if (*a.abandon) return;
   const uint32_t m = list_len(a.m_dev, a.m_host);
   const uint32_t lim = min(m, a.p_max);
   const uint32_t ntiles = (lim + SW_T - 1) / SW_T;
-  const uint32_t k = blockIdx.x * 4 + (threadIdx.x >> 6), t = lane_id();
-  if (k >= ntiles) return;  // per wave: no barriers below
-  uint64_t* dbg = (a.dbg && k == 0) ? a.dbg : nullptr;
-  auto stamp = [&](int i) {
-    if (dbg) {
-      __builtin_amdgcn_s_waitcnt(0);
-      if (t == 0) dbg[i] = __builtin_amdgcn_s_memrealtime();
-    }
-  };
-  stamp(8);
+  const uint32_t k = blockIdx.x, j = threadIdx.x, lane = lane_id();
+  if (k >= ntiles) return;
   SwRec& R = a.rec[k];
-  const uint32_t meta0 = R.meta[t];
-  if (__builtin_amdgcn_readfirstlane(meta0) & SWM_STOP) return;
+  if (R.meta[0] & SWM_STOP) return;  // uniform: written on every txn of a stopped tile
+  uint64_t* dbg = (a.dbg && k == 0) ? a.dbg : nullptr;
+  if (dbg && j == 0) dbg[8] = __builtin_amdgcn_s_memrealtime();
   const uint64_t nnz = a.in.nnz;
   const uint32_t off0 = (uint32_t)min((uint64_t)a.in.off[0], nnz);
   const uint32_t nt = min(SW_T, lim - k * SW_T);
-  const uint32_t p = k * SW_T + t;
-  uint32_t s = 0, len = 0;
-  if (t < nt) {
-    s = (uint32_t)min((uint64_t)a.in.off[p], nnz);
-    const uint32_t e = (uint32_t)min((uint64_t)a.in.off[p + 1], nnz);
-    len = e > s ? min(e - s, MAX_TXN_LEN) : 0u;  // longer txns are rejected by the host
-    s -= off0;
-  }
-  stamp(9);
+  if (j <= nt) s_off[j] = (uint32_t)min((uint64_t)a.in.off[k * SW_T + j], nnz);
+  __syncthreads();
+  if (dbg && j == 0) dbg[9] = __builtin_amdgcn_s_memrealtime();
+  const uint32_t A0 = s_off[0];
+  const uint32_t cnt = min(s_off[nt] >= A0 ? s_off[nt] - A0 : 0u, SW_TA);  // pre checked it
   const uint32_t idlim = 1u << a.gbits;
-  // pass 1: live / needed bits of the txn's accesses (len <= 64)
-  uint64_t lm = 0, nm = 0;
-  for (uint32_t q0 = 0; ballot64(q0 < len); q0 += 16) {
-    // branch-free: every load is issued (clamped addresses), then masked, so
-    // the 16 + 32 loads of a chunk are in flight together
-    uint32_t ent[16], fw[16], la[16];
-    const uint32_t xl = len ? len - 1 : 0u;
+  // (1) access-parallel: coalesced entry / position loads, then the random
+  // first-writer / last-accessor lookups, four accesses per thread in flight
+  for (uint32_t x0 = 0; x0 < cnt; x0 += 1024) {
+    uint32_t e[4], pp[4], fw[4], la[4];
 #pragma unroll
-    for (uint32_t u = 0; u < 16; u++) ent[u] = a.aent[s + min(q0 + u, xl)];
+    for (uint32_t u = 0; u < 4; u++) {
+      const uint32_t x = min(x0 + j + 256 * u, cnt - 1);
+      e[u] = a.aent[A0 - off0 + x];
+      pp[u] = a.apos[A0 - off0 + x];
+    }
 #pragma unroll
-    for (uint32_t u = 0; u < 16; u++) {
-      const uint32_t id = sw_aid(ent[u]);
+    for (uint32_t u = 0; u < 4; u++) {
+      const uint32_t id = sw_aid(e[u]);
       const uint32_t ic = id < idlim ? id : 0u;
       fw[u] = a.first_w[ic];
       la[u] = a.last_a[ic];
     }
 #pragma unroll
-    for (uint32_t u = 0; u < 16; u++) {
-      const bool in = q0 + u < len && sw_aid(ent[u]) < idlim;
-      lm |= (uint64_t)(in && fw[u] < p) << (q0 + u);
-      nm |= (uint64_t)(in && (ent[u] & 32u) && la[u] > p) << (q0 + u);
+    for (uint32_t u = 0; u < 4; u++) {
+      const uint32_t x = x0 + j + 256 * u;
+      if (x >= cnt) continue;
+      const bool in = sw_aid(e[u]) < idlim;
+      const uint32_t f = (in && fw[u] < pp[u] ? 1u : 0u) |
+                         (in && (e[u] & 32u) && la[u] > pp[u] ? 2u : 0u);
+      s_ent[x] = e[u];
+      s_flag[x] = (uint8_t)f;
     }
   }
+  __syncthreads();
+  if (dbg && j == 0) dbg[10] = __builtin_amdgcn_s_memrealtime();
+  if (j >= 64) return;
+  // (2) wave 0, lane = txn: counts, prefix sums, the two lists from LDS
+  const uint32_t t = lane;
+  uint32_t s = 0, len = 0;
+  if (t < nt) {
+    s = s_off[t] - A0;
+    len = s_off[t + 1] > s_off[t] ? min(s_off[t + 1] - s_off[t], MAX_TXN_LEN) : 0u;
+    if (s + len > cnt) len = s < cnt ? cnt - s : 0u;
+  }
+  uint32_t cp = 0, ci = 0;
+  for (uint32_t q = 0; q < len; q++) {
+    const uint32_t f = s_flag[s + q];
+    cp += f & 1u;
+    ci += f >> 1;
+  }
   uint32_t np, ni;
-  uint32_t ps = wave_excl_u32((uint32_t)__popcll(lm), np);
-  uint32_t is = wave_excl_u32((uint32_t)__popcll(nm), ni);
-  R.pspan[t] = ps | ((ps + (uint32_t)__popcll(lm)) << 16);
+  uint32_t ps = wave_excl_u32(cp, np);
+  uint32_t is = wave_excl_u32(ci, ni);
+  R.pspan[t] = ps | ((ps + cp) << 16);
   if (t == 0) {
     R.np = np;
     R.ni = ni;
   }
-  stamp(10);
-  // pass 2: the entries (the txn's accesses again, from L2)
   uint32_t* ovf = a.lst_ovf + (uint64_t)k * SW_OVF;
-  for (uint32_t q0 = 0; ballot64(q0 < 64 && ((lm | nm) >> q0) != 0); q0 += 16) {
-    uint32_t ent[16];
-    const uint32_t sel = (uint32_t)(((lm | nm) >> q0) & 0xFFFFu);
-    const uint32_t xl = len ? len - 1 : 0u;
-#pragma unroll
-    for (uint32_t u = 0; u < 16; u++) ent[u] = a.aent[s + min(q0 + u, xl)];
-#pragma unroll
-    for (uint32_t u = 0; u < 16; u++) {
-      if (!((sel >> u) & 1u)) continue;
-      const uint32_t id = sw_aid(ent[u]);
-      const bool w = (ent[u] & 32u) != 0;
-      if ((lm >> (q0 + u)) & 1ull) {
-        const uint32_t e = sw_tpack(id, t, false);
-        if (ps < SW_PL) R.probe[ps] = e;
-        else ovf[ps - SW_PL] = e;
-        ps++;
-      }
-      if ((nm >> (q0 + u)) & 1ull) {
-        const uint32_t e = sw_tpack(id, t, w);
-        if (is < SW_IL) R.ins[is] = e;
-        else ovf[SW_TA + is - SW_IL] = e;
-        is++;
-      }
+  for (uint32_t q = 0; q < len; q++) {
+    const uint32_t f = s_flag[s + q];
+    if (!f) continue;
+    const uint32_t ent = s_ent[s + q];
+    const uint32_t id = sw_aid(ent);
+    if (f & 1u) {
+      const uint32_t e = sw_tpack(id, t, false);
+      if (ps < SW_PL) R.probe[ps] = e;
+      else ovf[ps - SW_PL] = e;
+      ps++;
+    }
+    if (f & 2u) {
+      const uint32_t e = sw_tpack(id, t, true);
+      if (is < SW_IL) R.ins[is] = e;
+      else ovf[SW_TA + is - SW_IL] = e;
+      is++;
     }
   }
-  stamp(11);
+  if (dbg && t == 0) {
+    __builtin_amdgcn_s_waitcnt(0);
+    dbg[11] = __builtin_amdgcn_s_memrealtime();
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -891,7 +905,7 @@ __global__ __launch_bounds__(SW_CHUNK) void k_sw_filter(SwFilterArgs a) {
   const uint32_t m = list_len(a.m_dev, a.m_host);
   const uint32_t pos = a.lv->pos;
   const uint32_t ccount = a.lv->ccount;
-  if (X != (ccount <= F_XCAP)) return;
+  if (X ? ccount > F_XCAP : (a.exact_launched && ccount <= F_XCAP)) return;
   // the next level's key table (its pre-pass runs after this kernel)
   for (uint64_t q = (uint64_t)blockIdx.x * SW_CHUNK + j; q < a.gclear_n;
        q += (uint64_t)gridDim.x * SW_CHUNK) {
@@ -1103,7 +1117,8 @@ __global__ __launch_bounds__(1024) void k_sw_scan(SwFilterArgs a) {
 // k_sw_compact: the survivors, in index order, into the next level's list.
 __global__ __launch_bounds__(SW_CHUNK) void k_sw_compact(SwFilterArgs a) {
   const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
-  // a hand-off decided by this level's scan still needs its list
+  // an earlier level's hand-off: nothing to compact (this level's own
+  // decision is made below and still needs its list)
   const uint32_t ab = *a.abandon;
   if (ab && ab != a.level + 1) return;
   const uint32_t m = list_len(a.m_dev, a.m_host);
@@ -1115,12 +1130,49 @@ __global__ __launch_bounds__(SW_CHUNK) void k_sw_compact(SwFilterArgs a) {
   const uint32_t R = (n64 + a.nblocks - 1) / a.nblocks;
   const uint32_t t_lo = min(blockIdx.x * R, n64), t_hi = min(t_lo + R, n64);
   __shared__ unsigned long long s_tb[SW_CMP_MAXR];
+  __shared__ unsigned long long s_part[SW_CHUNK / 64][2];
   if (R > SW_CMP_MAXR) {
     if (threadIdx.x == 0) atomicOr(a.err, ERR_TILE);
     return;
   }
+  // this workgroup's base: the filter workgroups' totals before it (no
+  // separate scan pass); workgroup 0 also closes the level with the total
+  {
+    uint64_t pre = 0, all = 0;
+    for (uint32_t q = threadIdx.x; q < a.nblocks; q += SW_CHUNK) {
+      const uint64_t v = a.bsum[q];
+      all += v;
+      if (q < blockIdx.x) pre += v;
+    }
+    pre = wave_sum64(pre);
+    all = wave_sum64(all);
+    if (lane == 0) {
+      s_part[wv][0] = pre;
+      s_part[wv][1] = all;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint64_t p0 = 0, a0 = 0;
+      for (uint32_t w = 0; w < SW_CHUNK / 64; w++) {
+        p0 += s_part[w][0];
+        a0 += s_part[w][1];
+      }
+      s_part[0][0] = p0;
+      if (blockIdx.x == 0) {
+        const uint32_t tot = (uint32_t)(a0 >> LB_ACC_BITS);
+        const uint64_t acc = a0 & ((1ull << LB_ACC_BITS) - 1);
+        a.lv_next->m = tot;
+        a.lv_next->acc = (uint32_t)acc;
+        a.off_out[tot] = (uint32_t)acc;
+        const uint32_t in_n = m - pos;
+        if (tot > a.abandon_min && (uint64_t)tot * a.abandon_den > (uint64_t)in_n * a.abandon_num)
+          atomicMax(a.abandon_out, a.level + 1);
+      }
+    }
+    __syncthreads();
+  }
   if (wv == 0) {
-    uint64_t run = a.bsum[blockIdx.x];
+    uint64_t run = s_part[0][0];
     for (uint32_t c0 = t_lo; c0 < t_hi; c0 += 64) {
       const uint32_t q = c0 + lane;
       const uint64_t v = q < t_hi ? a.tcount[q] : 0ull;
@@ -1198,14 +1250,18 @@ void launch_sw_pre(const SwPreArgs& a, unsigned grid, hipStream_t st) {
 }
 void launch_sw_seq(const SwSeqArgs& a, hipStream_t st) { k_sw_seq<<<1, 1024, 0, st>>>(a); }
 void launch_sw_rows(const SwPreArgs& a, unsigned grid, hipStream_t st) {
-  k_sw_rows<<<grid ? grid : 1u, 256, 0, st>>>(a);
+  k_sw_rows<<<grid ? grid : 1u, 256, 0, st>>>(a);  // one workgroup per tile
 }
 void launch_sw_cout(const SwCoutArgs& a, unsigned grid, hipStream_t st) {
   k_sw_cout<<<grid ? grid : 1u, 256, 0, st>>>(a);
 }
-void launch_sw_filter(const SwFilterArgs& a, unsigned grid, hipStream_t st) {
-  k_sw_filter<true><<<grid ? grid : 1u, SW_CHUNK, 0, st>>>(a);
-  k_sw_filter<false><<<grid ? grid : 1u, SW_CHUNK, 0, st>>>(a);
+void launch_sw_filter(const SwFilterArgs& a, unsigned grid, bool exact_too, hipStream_t st) {
+  // the exact-set instance only where C can be small: level 0 (later levels
+  // collect thousands of keys; the Bloom instance serves any size)
+  SwFilterArgs b = a;
+  b.exact_launched = exact_too ? 1 : 0;
+  if (exact_too) k_sw_filter<true><<<grid ? grid : 1u, SW_CHUNK, 0, st>>>(b);
+  k_sw_filter<false><<<grid ? grid : 1u, SW_CHUNK, 0, st>>>(b);
 }
 void launch_sw_scan(const SwFilterArgs& a, hipStream_t st) { k_sw_scan<<<1, 1024, 0, st>>>(a); }
 void launch_sw_compact(const SwFilterArgs& a, unsigned grid, hipStream_t st) {
