@@ -78,6 +78,23 @@ struct dcc_ctx {
   std::string last_error;
   void* hmisc = nullptr;  // pinned host mirror of `misc`
   void* hpart = nullptr;  // pinned host mirror of `part`
+  // the sweep epoch's captured launch sequence (occ_epoch) and what it was
+  // captured with; buf_gen counts workspace reallocations
+  struct GraphKey {
+    const void *off, *keys, *acc;
+    uint64_t n, nnz;
+    const void* out_rc;
+    bool dev_out;
+    uint32_t levels;
+    uint64_t gen;
+    bool operator==(const GraphKey& o) const {
+      return off == o.off && keys == o.keys && acc == o.acc && n == o.n && nnz == o.nnz &&
+             out_rc == o.out_rc && dev_out == o.dev_out && levels == o.levels && gen == o.gen;
+    }
+  };
+  hipGraphExec_t graph_exec = nullptr;
+  GraphKey graph_key{};
+  uint64_t buf_gen = 0;
   void* hmisc_dev = nullptr;  // device-visible addresses of the two (k_gather targets)
   void* hpart_dev = nullptr;
 

@@ -34,6 +34,7 @@ int dcc_ctx::hip_fail(hipError_t e, const char* what) {
 
 int DevBuf::ensure(dcc_ctx* c, size_t bytes, const char* what) {
   if (bytes <= cap) return DCC_OK;
+  c->buf_gen++;  // a captured graph holding the old address is stale
   if (p) (void)hipFree(p);
   p = nullptr;
   cap = 0;
@@ -134,6 +135,7 @@ extern "C" void dcc_destroy(dcc_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->graph_exec) (void)hipGraphExecDestroy(ctx->graph_exec);
   dcc_comm_destroy(ctx);
   for (DevBuf* b : ctx->all_bufs()) b->release();
   if (ctx->hmisc) (void)hipHostFree(ctx->hmisc);

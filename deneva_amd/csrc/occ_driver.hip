@@ -607,7 +607,49 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   CR(stage_batch(b, d));
   const bool sweep = use_sweep();
   if (sweep) CR(sweep_reserve(d));
-  CK(hipEventRecord(ev0, stream));  // device clock starts with the batch resident
+  CR(state.ensure(this, d.n + 16, "state"));
+  CR(hasw.ensure(this, d.n + 16, "hasw"));
+  CR(rc.ensure(this, d.n + 16, "rc"));
+  const bool want_tn = out_tn != nullptr || (b->flags & DCC_OCC_APPEND_HISTORY);
+  if (want_tn) {
+    CR(cflag.ensure(this, d.n * 4, "cflag"));
+    CR(bsum.ensure(this, ((d.n + 1023) / 1024 + 1) * 8, "bsum"));
+    CR(tn.ensure(this, d.n * 8, "tn"));
+  }
+  // The sweep's whole launch sequence (prep ... gather) is replayed from a
+  // captured HIP graph when the batch, the outputs and every workspace are
+  // the ones it was captured with: one graph launch instead of ~30 kernel
+  // launches, so the device never waits for the host between kernels.
+  const bool hist_on = d.start_tn && !hist.empty();
+  const bool graph_ok = sweep && !profiling && !sw_debug && !want_tn && !hist_on && !sh &&
+                        !getenv("DCC_NO_GRAPH");
+  const GraphKey gkey{d.off, d.keys, d.acctype, d.n, d.nnz, out_rc, dev_out, sw_levels, buf_gen};
+  bool replay = graph_ok && graph_exec && gkey == graph_key;
+  bool capturing = false;
+  // a failure while capturing must still end the capture
+  struct CaptureGuard {
+    hipStream_t s;
+    bool* on;
+    ~CaptureGuard() {
+      if (*on) {
+        hipGraph_t g = nullptr;
+        (void)hipStreamEndCapture(s, &g);
+        if (g) (void)hipGraphDestroy(g);
+        (void)hipGetLastError();
+      }
+    }
+  } capture_guard{stream, &capturing};
+  if (graph_ok && !replay) {
+    if (graph_exec) {
+      (void)hipGraphExecDestroy(graph_exec);
+      graph_exec = nullptr;
+    }
+    CK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+    capturing = true;
+  }
+  // device clock starts with the batch resident (around the graph launch
+  // when one is used: event timing of graph-internal records is unsupported)
+  if (!replay && !capturing) CK(hipEventRecord(ev0, stream));
 
   // ---- prep: validation, max length (tile width), write count (table size).
   // The sweep needs none of it up front (its kernels clamp every index): its
@@ -615,13 +657,14 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   uint32_t maxlen = 0;
   uint64_t nnz_w = 0;
   const uint64_t p0 = sweep ? 0 : peel_prefix(d.n, 0);
-  if (sweep) launch_prep(d.off, d.n, d.acctype, d.nnz, 0,
-                         (PrepPart*)((char*)part.p + SW_PREP_OFF), stream);
-  else CR(device_prep(d, maxlen, nnz_w, p0, &prefix_w_top));
-  CR(state.ensure(this, d.n + 16, "state"));
-  CR(hasw.ensure(this, d.n + 16, "hasw"));
-  CR(rc.ensure(this, d.n + 16, "rc"));
-  {
+  if (sweep) {
+    if (!replay)
+      launch_prep(d.off, d.n, d.acctype, d.nnz, 0, (PrepPart*)((char*)part.p + SW_PREP_OFF),
+                  stream);
+  } else {
+    CR(device_prep(d, maxlen, nnz_w, p0, &prefix_w_top));
+  }
+  if (!replay) {
     // one launch: error word 0, the constant-one word 1, words 2..15, the
     // async pass count, the state bytes, and for the sweep its control block
     // and level-0 key table
@@ -642,7 +685,7 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   }
 
   // ---- history window pre-pass (occ.cpp:160-180)
-  if (d.start_tn && !hist.empty()) {
+  if (hist_on) {
     CR(upload_history());
     HistArgs ha{d.n, d.off, d.keys, d.acctype, d.start_tn, d.finish_tn,
                 (const uint64_t*)hkeys.p, h_nkeys, (const uint64_t*)hoff.p,
@@ -670,7 +713,7 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   if (sweep) {
     if (profiling) CK(hipEventRecord(pev[0], stream));
     next_level = (int)std::min<uint32_t>(sw_levels, SW_MAX_LEVEL - 1);
-    CR(sweep_enqueue(d, 0, next_level));
+    if (!replay) CR(sweep_enqueue(d, 0, next_level));
   } else if (peel) {
     CR(occ_peel(top, maxlen, 0, rounds, info));
   } else if (use_async()) {
@@ -682,22 +725,23 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
 
   // ---- finalize: RC bytes, counts, central_finish tn numbering
   uint8_t* rc_dev = (dev_out && out_rc) ? out_rc : (uint8_t*)rc.p;
-  uint32_t* cf = nullptr;
-  const bool want_tn = out_tn != nullptr || (b->flags & DCC_OCC_APPEND_HISTORY);
-  if (want_tn) {
-    CR(cflag.ensure(this, d.n * 4, "cflag"));
-    CR(bsum.ensure(this, ((d.n + 1023) / 1024 + 1) * 8, "bsum"));
-    CR(tn.ensure(this, d.n * 8, "tn"));
-    cf = (uint32_t*)cflag.p;
-  }
+  uint32_t* cf = want_tn ? (uint32_t*)cflag.p : nullptr;
   uint64_t* tn_dev = want_tn ? ((dev_out && out_tn) ? out_tn : (uint64_t*)tn.p) : nullptr;
   auto enqueue_final = [&]() -> int {
+    if (replay) {  // once: a second finalize (after more levels) runs directly
+      replay = false;
+      CK(hipEventRecord(ev0, stream));
+      CK(hipGraphLaunch(graph_exec, stream));
+      CK(hipEventRecord(ev1, stream));
+      CK(hipStreamSynchronize(stream));
+      return DCC_OK;
+    }
     FinalArgs fa{d.n, (const uint8_t*)state.p, (const uint8_t*)hasw.p, rc_dev, cf,
                  (FinalPart*)part.p};
     launch_final(fa, stream);
     if (want_tn) launch_commit_tn(cf, d.n, (uint64_t*)bsum.p, tnc, tn_dev, stream);
     CK(hipGetLastError());
-    CK(hipEventRecord(ev1, stream));
+    if (!capturing) CK(hipEventRecord(ev1, stream));
     if (!dev_out) {
       if (out_rc) CK(hipMemcpyAsync(out_rc, rc.p, d.n, hipMemcpyDeviceToHost, stream));
       if (out_tn) CK(hipMemcpyAsync(out_tn, tn.p, d.n * 8, hipMemcpyDeviceToHost, stream));
@@ -718,6 +762,21 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
     job(hpart_dev, part.p, FINAL_BLOCKS * sizeof(FinalPart));
     launch_gather(ga, stream);
     CK(hipGetLastError());
+    if (capturing) {
+      capturing = false;
+      hipGraph_t g = nullptr;
+      CK(hipStreamEndCapture(stream, &g));
+      const hipError_t ie = hipGraphInstantiate(&graph_exec, g, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(g);
+      if (ie != hipSuccess) {
+        graph_exec = nullptr;
+        return fail(DCC_EIO, "hipGraphInstantiate: %s", hipGetErrorString(ie));
+      }
+      graph_key = gkey;
+      CK(hipEventRecord(ev0, stream));
+      CK(hipGraphLaunch(graph_exec, stream));
+      CK(hipEventRecord(ev1, stream));
+    }
     CK(hipStreamSynchronize(stream));
     return DCC_OK;
   };
