@@ -226,16 +226,19 @@ def main():
         # whole epoch (every offset, key and access type); the serial passes
         # and later levels run on short lists
         dom = 1
-        dom_name = "k_sw_filter (level-0 committed-key filter)"
+        dom_name = "k_sw_filter<true> (level-0 committed-key filter, exact-set instance)"
+        dom_key = "k_sw_filter"
     elif peeled:
         # prefix peel: k_filter is the one kernel that streams the whole epoch
         # (every offset, key and access type); the rest runs on the prefix and
         # the few survivors
         dom = 1
         dom_name = "k_filter (committed-prefix filter pass)"
+        dom_key = "k_filter"
     else:
         dom = int(np.argmax(ph_ms[:2]))  # dominant single kernel: build or round-1 probe
         dom_name = ["k_build (key-hash build)", "k_round<true> (round-1 probe)"][dom]
+        dom_key = dom_name.split()[0]
     achieved = ph_bytes[dom] / (ph_ms[dom] * 1e-3) / 1e9
 
     s0 = stats[-1]
@@ -264,7 +267,7 @@ def main():
         if os.path.exists(tf):
             try:
                 tj = json.load(open(tf))
-                key = f"{n_total}:{args.theta}:{args.keys}:{dom_name.split()[0]}"
+                key = f"{n_total}:{args.theta}:{args.keys}:{dom_key}"
                 traffic = tj.get(key)
             except Exception:
                 traffic = None
@@ -310,7 +313,8 @@ def main():
                 "commits": int(s0["n_commit"]),
                 "aborts": int(s0["n_abort"]),
                 "phase_ms": [float(x) for x in ph_ms],
-                "phases": (["level-0 records+serial pass", "level-0 filter", "later levels",
+                "phases": (["level-0 tile lists+serial pass+committed set",
+                            "level-0 filter kernel", "level-0 compaction+later levels",
                             "prep+final"] if swept else
                            ["prefix solve", "k_filter", "survivor compaction+solve",
                             "prep+final"] if peeled else

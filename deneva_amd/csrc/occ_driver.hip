@@ -543,7 +543,6 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1) {
     launch_sw_seq(sa, stream);
     SwCoutArgs ca{in, aent, apos, (const uint64_t*)sw_mg.p, lv, cbits_d, ckeys_d, bloom_d, abandon};
     launch_sw_cout(ca, (unsigned)std::min<uint64_t>((pa.budget + 255) / 256, 4ull * n_cu), stream);
-    if (top && profiling) CK(hipEventRecord(pev[1], stream));
     SwFilterArgs fa;
     fa.in = in;
     fa.m_dev = mdev;
@@ -581,9 +580,15 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1) {
     fa.la_clear = la;
     fa.err = err;
     fa.dbg = (sw_debug && l < 4) ? (uint64_t*)sw_dbg.p + 4096 + (size_t)l * 256 * 8 : nullptr;
-    launch_sw_filter(fa, fgrid, top, stream);
+    fa.exact_launched = top ? 1 : 0;
+    if (top) {
+      // phase 1 of the profile is exactly the level-0 streaming filter
+      if (profiling) CK(hipEventRecord(pev[1], stream));
+      launch_sw_filter_x(fa, fgrid, stream);
+      if (profiling) CK(hipEventRecord(pev[2], stream));
+    }
+    launch_sw_filter_b(fa, fgrid, stream);
     launch_sw_compact(fa, fgrid, stream);
-    if (top && profiling) CK(hipEventRecord(pev[2], stream));
   }
   CK(hipGetLastError());
   return DCC_OK;
@@ -949,8 +954,9 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   if (profiling) {
     float t0 = 0, t1 = 0, t2 = 0;
     if (sweep) {
-      // phases: 0 = level-0 records + serial pass, 1 = level-0 filter,
-      // 2 = later levels (+ fallback), 3 = prep + finalize
+      // phases: 0 = level-0 records + serial pass + committed set, 1 = the
+      // level-0 filter kernel, 2 = level-0 compaction + later levels (+
+      // fallback), 3 = prep + finalize
       CK(hipEventElapsedTime(&t0, pev[0], pev[1]));
       CK(hipEventElapsedTime(&t1, pev[1], pev[2]));
       CK(hipEventElapsedTime(&t2, pev[2], pev[3]));

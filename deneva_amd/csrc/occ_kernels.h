@@ -376,7 +376,8 @@ void launch_sw_pre(const SwPreArgs& a, unsigned grid, hipStream_t st);
 void launch_sw_seq(const SwSeqArgs& a, hipStream_t st);
 void launch_sw_rows(const SwPreArgs& a, unsigned grid, hipStream_t st);
 void launch_sw_cout(const SwCoutArgs& a, unsigned grid, hipStream_t st);
-void launch_sw_filter(const SwFilterArgs& a, unsigned grid, bool exact_too, hipStream_t st);
+void launch_sw_filter_x(const SwFilterArgs& a, unsigned grid, hipStream_t st);
+void launch_sw_filter_b(const SwFilterArgs& a, unsigned grid, hipStream_t st);
 void launch_sw_scan(const SwFilterArgs& a, hipStream_t st);
 void launch_sw_compact(const SwFilterArgs& a, unsigned grid, hipStream_t st);
 

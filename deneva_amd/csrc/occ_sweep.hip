@@ -1255,13 +1255,15 @@ void launch_sw_rows(const SwPreArgs& a, unsigned grid, hipStream_t st) {
 void launch_sw_cout(const SwCoutArgs& a, unsigned grid, hipStream_t st) {
   k_sw_cout<<<grid ? grid : 1u, 256, 0, st>>>(a);
 }
-void launch_sw_filter(const SwFilterArgs& a, unsigned grid, bool exact_too, hipStream_t st) {
-  // the exact-set instance only where C can be small: level 0 (later levels
-  // collect thousands of keys; the Bloom instance serves any size)
-  SwFilterArgs b = a;
-  b.exact_launched = exact_too ? 1 : 0;
-  if (exact_too) k_sw_filter<true><<<grid ? grid : 1u, SW_CHUNK, 0, st>>>(b);
-  k_sw_filter<false><<<grid ? grid : 1u, SW_CHUNK, 0, st>>>(b);
+// The exact-set instance runs only where C can be small, level 0 (later
+// levels collect thousands of keys; the Bloom instance serves any size):
+// launch_sw_filter_x then launch_sw_filter_b with exact_launched = 1, or
+// launch_sw_filter_b alone with exact_launched = 0.
+void launch_sw_filter_x(const SwFilterArgs& a, unsigned grid, hipStream_t st) {
+  k_sw_filter<true><<<grid ? grid : 1u, SW_CHUNK, 0, st>>>(a);
+}
+void launch_sw_filter_b(const SwFilterArgs& a, unsigned grid, hipStream_t st) {
+  k_sw_filter<false><<<grid ? grid : 1u, SW_CHUNK, 0, st>>>(a);
 }
 void launch_sw_scan(const SwFilterArgs& a, hipStream_t st) { k_sw_scan<<<1, 1024, 0, st>>>(a); }
 void launch_sw_compact(const SwFilterArgs& a, unsigned grid, hipStream_t st) {
