@@ -1,0 +1,169 @@
+// occ_epoch.h — host-side OCC plugin shim over libdcc.
+//
+// Mirrors the reference's validation surface for the OCC branch: every worker
+// thread calls validate() the way it calls TxnManager::validate()
+// (system/txn.cpp:935) -> OptCC::validate (concurrency_control/occ.cpp:42),
+// with the access set its execution captured (Access list, system/txn.h:39-70)
+// and gets RCOK or Abort (system/global.h:236).  Instead of validating one
+// txn at a time against the active/history lists, the shim appends the txn to
+// the open epoch and blocks until the epoch is decided on the GPU by
+// dcc_occ_validate_epoch, whose decisions equal central_validate in epoch
+// (index) order followed by central_finish (occ.cpp:116-294).
+//
+// An epoch closes when it holds max_txns txns, when every registered worker is
+// waiting in validate() (nobody else can add to it), or when the oldest waiter
+// has waited timer_ms.  Decided epochs can be captured as .dccb files
+// (dcc_file_write) with their decisions, for offline parity checks.
+//
+// Timestamps: with the reference's default TS_CLOCK (config.h:124) the history
+// window of central_validate never fires, so the shim
+// passes no start/finish timestamps.  The class is thread-safe; the dcc_ctx it
+// drives must not be used by anyone else meanwhile (a context is
+// thread-compatible, dcc.h).
+#pragma once
+
+#include <chrono>
+#include <condition_variable>
+#include <cstdint>
+#include <cstdio>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "dcc.h"
+
+namespace dcc_host {
+
+struct Access {   // one entry of a txn's access list
+  uint64_t key;   // canonical row key
+  uint8_t type;   // access_t: DCC_RD / DCC_WR / DCC_XP / DCC_SCAN
+};
+
+class OccEpoch {
+ public:
+  struct Options {
+    uint64_t max_txns = 65536;   // epoch size cap
+    int n_workers = 1;           // threads that call validate()
+    double timer_ms = 5.0;       // SEQ_BATCH_TIMER-like close timer (config.h:348)
+    std::string capture_dir;     // "" = no capture
+  };
+  struct Stats {
+    uint64_t epochs = 0, txns = 0, commits = 0, aborts = 0;
+    double device_ms = 0, wall_ms = 0;
+  };
+
+  OccEpoch(dcc_ctx* ctx, const Options& o) : ctx_(ctx), opt_(o) { off_.push_back(0); }
+
+  // TxnManager::validate for CC_ALG == OCC: DCC_RC_RCOK or DCC_RC_ABORT in *rc.
+  // Returns a dcc error code (0 = ok).
+  int validate(const Access* acc, size_t n, uint8_t* rc) {
+    std::unique_lock<std::mutex> lk(mu_);
+    const uint64_t ep = epoch_;
+    const uint64_t slot = off_.size() - 1;
+    for (size_t i = 0; i < n; i++) {
+      keys_.push_back(acc[i].key);
+      at_.push_back(acc[i].type);
+    }
+    off_.push_back((uint32_t)keys_.size());
+    if (slot == 0) opened_ = std::chrono::steady_clock::now();
+    waiting_++;
+    int err = 0;
+    while (decided_.find(ep) == decided_.end()) {
+      const bool full = off_.size() - 1 >= opt_.max_txns;
+      const bool all_in = waiting_ >= opt_.n_workers;
+      const auto age = std::chrono::duration<double, std::milli>(
+                           std::chrono::steady_clock::now() - opened_).count();
+      if (ep == epoch_ && (full || all_in || age >= opt_.timer_ms)) {
+        err = close_locked();
+        break;
+      }
+      cv_.wait_for(lk, std::chrono::microseconds(200));
+    }
+    waiting_--;
+    auto it = decided_.find(ep);
+    if (it == decided_.end()) return err ? err : DCC_EIO;
+    if (it->second.err) err = it->second.err;
+    *rc = err ? (uint8_t)DCC_RC_ABORT : it->second.rc[slot];
+    if (--it->second.readers == 0) decided_.erase(it);
+    return err;
+  }
+
+  // a worker that stops calling validate() (end of its run): the epoch no
+  // longer waits for it
+  void leave() {
+    std::lock_guard<std::mutex> lk(mu_);
+    opt_.n_workers--;
+    cv_.notify_all();
+  }
+
+  Stats stats() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return stats_;
+  }
+
+ private:
+  struct Decided {
+    std::vector<uint8_t> rc;
+    uint64_t readers = 0;
+    int err = 0;
+  };
+
+  // decide the open epoch (mutex held): one engine call, then wake everyone
+  int close_locked() {
+    const uint64_t n = off_.size() - 1;
+    Decided d;
+    d.rc.assign(n, DCC_RC_ABORT);
+    d.readers = n;
+    dcc_batch b{};
+    b.n_txn = n;
+    b.nnz = keys_.size();
+    b.offsets = off_.data();
+    b.keys = keys_.data();
+    b.acctype = at_.data();
+    b.flags = DCC_OCC_APPEND_HISTORY;  // central_finish: commit tn + history
+    dcc_stats st{};
+    const uint64_t tnc0 = dcc_occ_get_tnc(ctx_);
+    const auto t0 = std::chrono::steady_clock::now();
+    d.err = n ? dcc_occ_validate_epoch(ctx_, &b, d.rc.data(), nullptr, &st) : 0;
+    const auto t1 = std::chrono::steady_clock::now();
+    if (!d.err && !opt_.capture_dir.empty()) {
+      dcc_file_info fi{};
+      fi.kind = DCC_FILE_OCC;
+      fi.epoch = epoch_;
+      fi.tnc_before = tnc0;
+      char path[4096];
+      snprintf(path, sizeof path, "%s/epoch_%06llu.dccb", opt_.capture_dir.c_str(),
+               (unsigned long long)epoch_);
+      d.err = dcc_file_write(path, &fi, &b, d.rc.data(), nullptr, nullptr, nullptr);
+    }
+    stats_.epochs++;
+    stats_.txns += n;
+    for (uint8_t r : d.rc) (r == DCC_RC_RCOK ? stats_.commits : stats_.aborts)++;
+    stats_.device_ms += st.device_ms;
+    stats_.wall_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
+    const int err = d.err;
+    decided_.emplace(epoch_, std::move(d));
+    epoch_++;
+    off_.assign(1, 0);
+    keys_.clear();
+    at_.clear();
+    cv_.notify_all();
+    return err;
+  }
+
+  dcc_ctx* ctx_;
+  Options opt_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::vector<uint32_t> off_;
+  std::vector<uint64_t> keys_;
+  std::vector<uint8_t> at_;
+  std::chrono::steady_clock::time_point opened_{};
+  uint64_t epoch_ = 0;
+  int waiting_ = 0;
+  std::map<uint64_t, Decided> decided_;
+  Stats stats_;
+};
+
+}  // namespace dcc_host

@@ -1,0 +1,61 @@
+"""The host plugin shims (deneva_amd/csrc/host: OccEpoch behind
+TxnManager::validate, CalvinEpoch behind the sequencer hand-off) driven by
+the C1 driver: THREAD_CNT=4 workers, YCSB 10 req/txn, theta 0.6 (BASELINE.json
+configs[0]).  Every epoch the concurrent workers formed is captured as a .dccb
+file with the engine's decisions and checked against the oracle replaying the
+same epoch in capture order."""
+import glob
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import deneva_amd as d
+import _oracle as orc
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DRIVER = os.path.join(ROOT, "deneva_amd", "c1_driver")
+
+
+def run_driver(*args, timeout=120):
+    p = subprocess.run([DRIVER, *args], capture_output=True, text=True, timeout=timeout)
+    assert p.returncode == 0, p.stderr[-2000:]
+    return json.loads(p.stdout.strip().splitlines()[-1])
+
+
+def test_driver_built_and_usage():
+    assert os.path.exists(DRIVER), "build() compiles deneva_amd/csrc/host"
+    p = subprocess.run([DRIVER, "--help"], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 0 and "--threads" in p.stderr
+    p = subprocess.run([DRIVER, "--bogus", "1"], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 2
+
+
+@pytest.mark.gpu
+def test_c1_occ_epochs_match_oracle(tmp_path):
+    cap = tmp_path / "cap"
+    cap.mkdir()
+    out = run_driver("--threads", "4", "--txns", "1500", "--theta", "0.6", "--req", "10",
+                     "--table", "65536", "--epoch-max", "256", "--timer-ms", "2",
+                     "--capture", str(cap))
+    total = 4 * 1500
+    assert out["failed"] == 0 and out["commits"] == total  # every txn commits eventually
+    files = sorted(glob.glob(str(cap / "epoch_*.dccb")))
+    assert len(files) == out["epochs"] >= 2
+    seen = 0
+    for f in files:
+        b, meta, dec = d.read_batch_file(f)
+        erc, _, _ = orc.occ(b)
+        assert np.array_equal(dec["rc"], erc), f
+        seen += b.n_txn
+    assert seen == total + out["restarts"]  # restarted txns are validated again
+
+
+@pytest.mark.gpu
+def test_c1_calvin_handoff():
+    out = run_driver("--calvin", "--threads", "4", "--txns", "1000", "--theta", "0.6",
+                     "--epoch-max", "512")
+    assert out["failed"] == 0 and out["ready"] + out["waits"] == 4 * 1000
+    assert out["epochs"] == (1000 + 127) // 128 and out["ready"] > 0
