@@ -880,8 +880,9 @@ __device__ inline bool c_exact(const SwFilterArgs& a, uint64_t key) {
   return false;
 }
 constexpr uint32_t F_STASH = 256;  // Bloom-positive keys kept in LDS per wave
-constexpr uint32_t F_XS = 4096;    // exact-only filter: LDS set slots
-constexpr uint32_t F_XCAP = 2048;  // ... for C of up to this many keys (<= 50% load)
+constexpr uint32_t F_XS = 2048;    // small-C filter instance: LDS exact-set slots
+constexpr uint32_t F_XCAP = 1024;  // ... for C of up to this many keys (<= 50% load)
+constexpr uint32_t F_XB = 256;     // ... threads per workgroup
 
 // ---------------------------------------------------------------------------
 // k_sw_filter: list txns [pos, m) against C, 64 per wave, grid-stride (no
@@ -892,14 +893,18 @@ constexpr uint32_t F_XCAP = 2048;  // ... for C of up to this many keys (<= 50% 
 // and the Bloom-filtered one otherwise.  Both are launched; the one whose
 // case it is not returns at once.
 template <bool X>
-__global__ __launch_bounds__(SW_CHUNK) void k_sw_filter(SwFilterArgs a) {
+__global__ __launch_bounds__(X ? F_XB : SW_CHUNK) void k_sw_filter(SwFilterArgs a) {
+  // (both instances map the same tiles to each workgroup)
+  constexpr uint32_t B = X ? F_XB : SW_CHUNK, FW = B / 64;
   constexpr uint32_t CS = X ? F_XS : F_EXACT;  // exact-set slots
-  __shared__ uint32_t bl[X ? 1 : (1u << SW_BLOOM_LOG) / 32];
+  // X: a one-hash bitmap of C built here (one conflict-light ds_read_b32 per
+  // access) in front of the exact set; otherwise the level's Bloom filter
+  __shared__ uint32_t bl[(1u << SW_BLOOM_LOG) / 32];
   __shared__ __attribute__((aligned(16))) uint64_t cex[CS];
   __shared__ uint64_t s_hit[FW][SW_WA / 64];
   __shared__ uint64_t s_wr[FW][SW_WA / 64];
   __shared__ uint64_t s_stash[FW][X ? 1 : F_STASH];
-  __shared__ uint32_t s_wpre[FW][X ? 1 : SW_WA / 64];
+  __shared__ uint32_t s_wpre[FW][SW_WA / 64];
   const uint32_t j = threadIdx.x, lane = lane_id(), wv = j >> 6;
   if (*a.abandon) return;
   const uint32_t m = list_len(a.m_dev, a.m_host);
@@ -907,8 +912,8 @@ __global__ __launch_bounds__(SW_CHUNK) void k_sw_filter(SwFilterArgs a) {
   const uint32_t ccount = a.lv->ccount;
   if (X ? ccount > F_XCAP : (a.exact_launched && ccount <= F_XCAP)) return;
   // the next level's key table (its pre-pass runs after this kernel)
-  for (uint64_t q = (uint64_t)blockIdx.x * SW_CHUNK + j; q < a.gclear_n;
-       q += (uint64_t)gridDim.x * SW_CHUNK) {
+  for (uint64_t q = (uint64_t)blockIdx.x * B + j; q < a.gclear_n;
+       q += (uint64_t)gridDim.x * B) {
     a.gclear[q] = KEY_EMPTY;
     a.fw_clear[q] = ~0u;
     a.la_clear[q] = 0u;
@@ -921,14 +926,24 @@ __global__ __launch_bounds__(SW_CHUNK) void k_sw_filter(SwFilterArgs a) {
     if (!X) {
       const uint4* src = (const uint4*)a.bloom;
       uint4* dst = (uint4*)bl;
-      for (uint32_t q = j; q < (1u << SW_BLOOM_LOG) / 128; q += SW_CHUNK) dst[q] = src[q];
+      for (uint32_t q = j; q < (1u << SW_BLOOM_LOG) / 128; q += B) dst[q] = src[q];
+    } else {
+      for (uint32_t q = j; q < (1u << SW_BLOOM_LOG) / 32; q += B) bl[q] = 0;
     }
     if (small)
-      for (uint32_t q = j; q < CS; q += SW_CHUNK) cex[q] = KEY_EMPTY;
+      for (uint32_t q = j; q < CS; q += B) cex[q] = KEY_EMPTY;
   }
   __syncthreads();
   if (small) {
-    for (uint32_t q = j; q < ccount; q += SW_CHUNK) lset_insert<CS>(cex, a.ckeys[q]);
+    for (uint32_t q = j; q < ccount; q += B) {
+      const uint64_t kq = a.ckeys[q];
+      lset_insert<CS>(cex, kq);
+      if (X) {
+        uint32_t b1, b2;
+        bloom_bits(kq, b1, b2);
+        atomicOr(&bl[b1 >> 5], 1u << (b1 & 31u));
+      }
+    }
     __syncthreads();
   }
   uint64_t* hit = s_hit[wv];
@@ -938,18 +953,30 @@ __global__ __launch_bounds__(SW_CHUNK) void k_sw_filter(SwFilterArgs a) {
   const uint32_t R = (n64 + gridDim.x - 1) / gridDim.x;
   const uint32_t t_lo = min(blockIdx.x * R, n64), t_hi = min(t_lo + R, n64);
   uint64_t wsum = 0;
+  // the per-txn words of a wave's next tile are loaded while the current
+  // tile's keys are in flight (branch-free, clamped: they issue together)
+  uint32_t ns = 0, ne = 0, ntid = 0, nst = 0;
+  auto prefetch = [&](uint32_t wt) {
+    const uint32_t pc = min(pos + wt * 64 + lane, m - 1);
+    ns = a.in.off[pc];
+    ne = a.in.off[pc + 1];
+    ntid = a.in.tid ? a.in.tid[pc] : pc;
+    nst = a.cand_state ? a.state[pc] : 0u;
+  };
+  if (t_lo + wv < t_hi) prefetch(t_lo + wv);
   for (uint32_t wt = t_lo + wv; wt < t_hi; wt += FW) {
     const uint32_t p = pos + wt * 64 + lane;
     const bool valid = p < m;
     uint32_t s = 0, e = 0, tid = 0;
     bool cand = false;
     if (valid) {
-      s = (uint32_t)min((uint64_t)a.in.off[p], nnz);
-      e = (uint32_t)min((uint64_t)a.in.off[p + 1], nnz);
+      s = (uint32_t)min((uint64_t)ns, nnz);
+      e = (uint32_t)min((uint64_t)ne, nnz);
       if (e < s) e = s;
-      tid = a.in.tid ? a.in.tid[p] : p;
-      cand = a.cand_state ? a.state[p] == ST_UNDECIDED : true;
+      tid = ntid;
+      cand = nst == ST_UNDECIDED;
     }
+    bool pref = false;
     const uint64_t vm = ballot64(valid);
     const uint32_t A0 = vm ? __shfl(s, 0) : 0u;
     const uint32_t A1 = wave_max32(valid ? e : 0u);
@@ -973,6 +1000,10 @@ __global__ __launch_bounds__(SW_CHUNK) void k_sw_filter(SwFilterArgs a) {
         key[u] = a.in.keys[x];
         at[u] = a.in.acctype[x];
       }
+      if (!pref) {
+        pref = true;
+        if (wt + FW < t_hi) prefetch(wt + FW);
+      }
 #pragma unroll
       for (uint32_t u = 0; u < FK; u++) {
         const uint32_t xr = b0 + 64 * u + lane;
@@ -980,11 +1011,11 @@ __global__ __launch_bounds__(SW_CHUNK) void k_sw_filter(SwFilterArgs a) {
         const bool in = xr < span;
         bad_key |= in && key[u] == KEY_EMPTY;
         bool h;
+        uint32_t b1, b2;
+        bloom_bits(key[u], b1, b2);
         if (X) {
-          h = in && lset_find<CS>(cex, key[u]);
+          h = in && ((bl[b1 >> 5] >> (b1 & 31u)) & 1u) != 0;
         } else {
-          uint32_t b1, b2;
-          bloom_bits(key[u], b1, b2);
           const uint32_t wa = bl[b1 >> 5], wb = bl[b2 >> 5];
           h = in && (((wa >> (b1 & 31u)) & (wb >> (b2 & 31u)) & 1u) != 0);
         }
@@ -1002,15 +1033,13 @@ __global__ __launch_bounds__(SW_CHUNK) void k_sw_filter(SwFilterArgs a) {
         }
       }
     }
+    if (!pref && wt + FW < t_hi) prefetch(wt + FW);  // a tile without accesses
     if (ballot64(bad_key) && lane == 0) atomicOr(a.err, ERR_KEY);
     // per txn (the wave's own LDS rows: no barrier needed)
     const uint32_t rlo = s - A0, rlen = e - s;
     const bool ok = valid && (rlen == 0 || (uint64_t)rlo + rlen <= span);
     bool killed = false;
-    if (X) {
-      // every LDS hit is exact
-      killed = cand && ok && rlen && range_any(hit, rlo, rlen);
-    } else {
+    {
       {
         const uint32_t pw = lane < nw ? (uint32_t)__popcll(hit[lane]) : 0u;
         uint32_t ptot;
@@ -1025,7 +1054,8 @@ __global__ __launch_bounds__(SW_CHUNK) void k_sw_filter(SwFilterArgs a) {
           if (nx >= rlo + rlen) break;
           const uint32_t ci = s_wpre[wv][nx >> 6] +
                               (uint32_t)__popcll(hit[nx >> 6] & ((1ull << (nx & 63)) - 1ull));
-          const uint64_t kx = ci < F_STASH ? stash[ci] : a.in.keys[A0 + nx];
+          // (X keeps no stash: the key again, from L1/L2)
+          const uint64_t kx = (!X && ci < F_STASH) ? stash[ci] : a.in.keys[A0 + nx];
           if (small ? lset_find<CS>(cex, kx) : c_exact(a, kx)) {
             killed = true;
             break;
@@ -1260,7 +1290,7 @@ void launch_sw_cout(const SwCoutArgs& a, unsigned grid, hipStream_t st) {
 // launch_sw_filter_x then launch_sw_filter_b with exact_launched = 1, or
 // launch_sw_filter_b alone with exact_launched = 0.
 void launch_sw_filter_x(const SwFilterArgs& a, unsigned grid, hipStream_t st) {
-  k_sw_filter<true><<<grid ? grid : 1u, SW_CHUNK, 0, st>>>(a);
+  k_sw_filter<true><<<grid ? grid : 1u, F_XB, 0, st>>>(a);
 }
 void launch_sw_filter_b(const SwFilterArgs& a, unsigned grid, hipStream_t st) {
   k_sw_filter<false><<<grid ? grid : 1u, SW_CHUNK, 0, st>>>(a);

@@ -1,0 +1,18 @@
+#!/bin/bash
+# SQ counters of the sweep kernels (per dispatch): where the level-0 filter's
+# cycles go.  One counter group per pass, kernel trace only.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT="$R/gpurun_out/pmcf"
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp
+ARGS="$R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-secondary"
+i=0
+for grp in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM" \
+           "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_WAVES SQ_INSTS_SMEM GRBM_GUI_ACTIVE"; do
+  i=$((i+1))
+  timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d "$OUT/p$i" -o run \
+      -- python3 $ARGS > "$OUT/p$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/p$i.log"; exit 1; }
+done
+python3 "$R/tools/pmc_dispatch.py" "$OUT" "k_sw_filter<true>" 3
+python3 "$R/tools/pmc_dispatch.py" "$OUT" "k_sw_seq" 4
