@@ -220,7 +220,7 @@ def main():
     ph_ms = np.mean([p["phase_ms"] for p in prof], axis=0)
     ph_bytes = prof[-1]["phase_bytes"]
     peeled = prof[-1]["peel_prefix"] > 0
-    swept = args.solver in (0, 3) and args.peel == -1 and world == 1
+    swept = args.solver in (0, 3) and args.peel == -1
     if swept:
         # sweep solver: the level-0 filter is the one kernel that streams the
         # whole epoch (every offset, key and access type); the serial passes

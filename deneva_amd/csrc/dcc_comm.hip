@@ -31,6 +31,7 @@ struct dcc_comm_state {
 };
 
 int dcc_ctx::comm_ranks() const { return comm ? comm->nranks : 1; }
+int dcc_ctx::comm_rank() const { return comm ? comm->rank : 0; }
 
 int dcc_ctx::comm_allreduce_max_u8(uint8_t* dev, uint64_t n) {
   dcc_ctx* ctx = this;

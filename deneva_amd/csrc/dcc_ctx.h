@@ -11,6 +11,10 @@
 
 #include "dcc.h"
 
+namespace dcc {
+struct SwShard;  // occ_kernels.h: one key-sharded sweep level's serial range
+}
+
 struct dcc_ctx;
 
 struct DevBuf {
@@ -70,7 +74,7 @@ struct dcc_ctx {
   uint64_t prefix_w_top = 0;    // write accesses in the top-level peel prefix
   bool use_async() const { return !force_rounds && solver != 1 && comm_ranks() <= 1; }
   bool use_sweep() const {
-    return !force_rounds && comm_ranks() <= 1 && (solver == 3 || (solver == 0 && peel_mode == -1));
+    return !force_rounds && (solver == 3 || (solver == 0 && peel_mode == -1));
   }
   uint32_t sw_levels = 4;
   bool sw_debug = false;        // DCC_SW_DEBUG: per-tile clock stamps of the serial pass       // sweep levels enqueued between host synchronisations
@@ -109,7 +113,8 @@ struct dcc_ctx {
   DevBuf hasw_scr, cset_tab, cset_keys;          // prefix peel
   DevBuf a_cnt, a_writers, a_big, a_st32;        // async solver
   DevBuf sw_ctl, sw_status, sw_ckeys, sw_dbg;            // sweep solver: level control, look-back, C
-  DevBuf sw_rec, sw_rk, sw_gtab, sw_fw, sw_aent, sw_mg;  // sweep tile records
+  DevBuf sw_rec, sw_rk, sw_gtab, sw_fw, sw_aent, sw_mg;
+  DevBuf sw_xcnt, sw_xrec, sw_mcnt, sw_moff, sw_mkeys, sw_mat, sw_kill;  // key-sharded sweep  // sweep tile records
   SubBufs sw_list[2];                            // sweep level lists (ping-pong)
   SubBufs subs[PEEL_MAX_LEVEL];
   DevBuf l_tid[2], l_coff[2], l_cent[2];         // ping-pong undecided lists
@@ -127,6 +132,7 @@ struct dcc_ctx {
   dcc_comm_state* comm = nullptr;
   int comm_ranks() const;
   int comm_allreduce_max_u8(uint8_t* dev, uint64_t n);  // in place, on `stream`
+  int comm_rank() const;
 
   int fail(int code, const char* fmt, ...);
   int hip_fail(hipError_t e, const char* what);
@@ -145,7 +151,8 @@ struct dcc_ctx {
   int occ_async(const SubProb& sp, uint32_t maxlen, uint32_t& passes);
   int occ_peel(const SubProb& sp, uint32_t maxlen, int level, uint32_t& rounds, PeelInfo& info);
   int sweep_reserve(const DevBatch& d);
-  int sweep_enqueue(const DevBatch& d, int l0, int l1);
+  int sweep_enqueue(const DevBatch& d, int l0, int l1, const dcc::SwShard* shard = nullptr);
+  int sweep_sharded(const DevBatch& d, int& next_level);
   int occ_sweep_finish(const DevBatch& d, int& next_level, bool& done, uint32_t maxlen);
   uint64_t peel_prefix(uint64_t m, int level) const;
   int calvin_epoch(const dcc_batch* b, uint32_t* out_group, uint8_t* out_rc, uint32_t* out_wave,

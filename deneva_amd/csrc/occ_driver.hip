@@ -443,6 +443,7 @@ int dcc_ctx::occ_peel(const SubProb& sp, uint32_t maxlen, int level, uint32_t& r
 // synchronisation (list lengths live on the device), sw_levels at a time.
 static constexpr size_t SW_PREP_OFF = 32768;  // prep partials inside `part` / `hpart`
 static constexpr size_t SW_HCTL = 13312;      // control-block copy inside `hmisc`
+static constexpr size_t SW_HX = 14336;        // key-sharded sweep: list length + abandon word
 static constexpr uint32_t SW_PMAX_TOP = 65536;
                                                           // the serial pass's LDS set)
 static uint32_t sw_pmax(int level) {
@@ -492,7 +493,7 @@ int dcc_ctx::sweep_reserve(const DevBatch& d) {
 
 // Enqueue levels [l0, l1) (list l0 must exist: the epoch, or written by the
 // filter of level l0 - 1).
-int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1) {
+int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1, const SwShard* shl) {
   dcc_ctx* ctx = this;
   SwLevel* ctl = (SwLevel*)sw_ctl.p;
   uint32_t* abandon = (uint32_t*)(ctl + SW_MAX_LEVEL + 1);
@@ -527,21 +528,26 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1) {
     uint32_t* la = fw + (1u << SW_GBITS_MAX);
     uint32_t* aent = (uint32_t*)sw_aent.p;
     uint32_t* apos = aent + (1u << (SW_GBITS_MAX - 1));
-    SwPreArgs pa{in, mdev, n, pmax, top ? (const uint8_t*)state.p : nullptr,
+    // key-sharded: the serial part runs on the merged serial range (every
+    // shard's accesses of list txns [0, P)), identically on every rank
+    const SwList sin = shl ? shl->serial : in;
+    const uint32_t* smdev = shl ? nullptr : mdev;
+    const uint32_t sm_host = shl ? shl->P : n;
+    SwPreArgs pa{sin, smdev, sm_host, pmax, top ? (const uint8_t*)state.p : nullptr,
                  (SwRec*)sw_rec.p, (uint32_t*)sw_rk.p,
                  gtab0 + (size_t)(l & 1) * (1ull << SW_GBITS_MAX), sw_gbits(l),
                  sw_budget(l), fw, la, aent, apos, abandon, err, nullptr};
     if (sw_debug && l < 4) pa.dbg = (uint64_t*)sw_dbg.p + 4096 + 4 * 256 * 8 + (size_t)l * 64 * 8;
     launch_sw_pre(pa, (unsigned)tiles, stream);
     launch_sw_rows(pa, (unsigned)tiles, stream);
-    SwSeqArgs sa{mdev, n, pmax, top ? 1 : 0, (const SwRec*)sw_rec.p, (const uint32_t*)sw_rk.p,
+    SwSeqArgs sa{smdev, sm_host, pmax, top ? 1 : 0, (const SwRec*)sw_rec.p, (const uint32_t*)sw_rk.p,
                  gtab0 + (size_t)(l & 1) * (1ull << SW_GBITS_MAX), sw_gbits(l),
                  (uint8_t*)state.p, (uint8_t*)hasw.p,
                  cbits_d, ckeys_d, bloom_d, lv, lv + 1, (uint32_t*)out.off.p, (uint64_t*)sw_mg.p,
                  abandon, err, nullptr};
     if (sw_debug && l < 4) sa.dbg = (uint64_t*)sw_dbg.p + (size_t)l * 1024;
     launch_sw_seq(sa, stream);
-    SwCoutArgs ca{in, aent, apos, (const uint64_t*)sw_mg.p, lv, cbits_d, ckeys_d, bloom_d, abandon};
+    SwCoutArgs ca{sin, aent, apos, (const uint64_t*)sw_mg.p, lv, cbits_d, ckeys_d, bloom_d, abandon};
     launch_sw_cout(ca, (unsigned)std::min<uint64_t>((pa.budget + 255) / 256, 4ull * n_cu), stream);
     SwFilterArgs fa;
     fa.in = in;
@@ -581,6 +587,8 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1) {
     fa.err = err;
     fa.dbg = (sw_debug && l < 4) ? (uint64_t*)sw_dbg.p + 4096 + (size_t)l * 256 * 8 : nullptr;
     fa.exact_launched = top ? 1 : 0;
+    fa.kill_out = shl ? shl->kill : nullptr;
+    fa.kill_in = shl ? shl->kill : nullptr;
     if (top) {
       // phase 1 of the profile is exactly the level-0 streaming filter
       if (profiling) CK(hipEventRecord(pev[1], stream));
@@ -588,9 +596,101 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1) {
       if (profiling) CK(hipEventRecord(pev[2], stream));
     }
     launch_sw_filter_b(fa, fgrid, stream);
+    if (shl) {
+      // a kill on any shard wins; then every rank applies the same decision
+      CR(comm_allreduce_max_u8(shl->kill, shl->m));
+      if (top) CR(comm_allreduce_max_u8((uint8_t*)hasw.p, d.n));
+      launch_sw_apply(fa, fgrid, stream);
+    }
     launch_sw_compact(fa, fgrid, stream);
   }
   CK(hipGetLastError());
+  return DCC_OK;
+}
+
+// Key-sharded sweep: levels one at a time.  Per level: the
+// list length and this rank's share of the serial range, an all-gather of the
+// shares' sizes and then of the records themselves (a byte-wise MAX
+// all-reduce over a zeroed buffer in which each rank fills its slot), the
+// merged serial range, then sweep_enqueue with the filter in kill-bit mode.
+// On return next_level is the first level not run; its list is empty, or
+// handed off (abandon), or left to the round solver.
+int dcc_ctx::sweep_sharded(const DevBatch& d, int& next_level) {
+  dcc_ctx* ctx = this;
+  const int R = comm_ranks(), me = comm_rank();
+  SwLevel* ctl = (SwLevel*)sw_ctl.p;
+  const uint32_t* abandon = (const uint32_t*)(ctl + SW_MAX_LEVEL + 1);
+  CR(sw_xcnt.ensure(this, 64ull * R + 64, "sweep exchange counts"));
+  for (int l = 0; l < SW_MAX_LEVEL - 1; l++) {
+    next_level = l;
+    const bool top = l == 0;
+    SwList in;
+    if (top) {
+      in = SwList{nullptr, d.off, d.keys, d.acctype, d.nnz};
+    } else {
+      const SubBufs& b = sw_list[(l - 1) & 1];
+      in = SwList{(const uint32_t*)b.tid.p, (const uint32_t*)b.off.p, (const uint64_t*)b.keys.p,
+                  (const uint8_t*)b.acctype.p, d.nnz};
+    }
+    // (1) list length, abandon word, this rank's accesses of [0, P)
+    uint32_t m = (uint32_t)d.n;
+    uint32_t* hx = (uint32_t*)((char*)hmisc + SW_HX);
+    {
+      GatherArgs ga{};
+      ga.job[ga.n++] = CopyJob{&ctl[l].m, (uint32_t*)((char*)hmisc_dev + SW_HX), 1};
+      ga.job[ga.n++] = CopyJob{abandon, (uint32_t*)((char*)hmisc_dev + SW_HX) + 1, 1};
+      launch_gather(ga, stream);
+      CK(hipStreamSynchronize(stream));
+      if (!top) m = hx[0];
+      if (hx[1]) return DCC_OK;  // an earlier level handed off
+    }
+    if (m == 0) return DCC_OK;
+    const uint32_t P = std::min<uint32_t>(sw_pmax(l), m);
+    uint32_t offs[2];
+    CK(hipMemcpyAsync(offs, top ? d.off : in.off, 4, hipMemcpyDeviceToHost, stream));
+    CK(hipMemcpyAsync(offs + 1, (top ? d.off : in.off) + P, 4, hipMemcpyDeviceToHost, stream));
+    CK(hipStreamSynchronize(stream));
+    const uint32_t mine = offs[1] - offs[0];
+    // (2) every rank's share: all-gather of one u32 per rank
+    uint32_t* cnt = (uint32_t*)sw_xcnt.p;
+    CK(hipMemsetAsync(cnt, 0, 4ull * R, stream));
+    CK(hipMemcpyAsync(cnt + me, &mine, 4, hipMemcpyHostToDevice, stream));
+    CR(comm_allreduce_max_u8((uint8_t*)cnt, 4ull * R));
+    std::vector<uint32_t> share(R);
+    CK(hipMemcpyAsync(share.data(), cnt, 4ull * R, hipMemcpyDeviceToHost, stream));
+    CK(hipStreamSynchronize(stream));
+    uint64_t total = 0, before = 0;
+    for (int r = 0; r < R; r++) {
+      if (r < me) before += share[r];
+      total += share[r];
+    }
+    // (3) the records, all-gathered; merged by txn into one CSR
+    CR(sw_xrec.ensure(this, std::max<uint64_t>(64, total * 12), "sweep exchange records"));
+    CR(sw_mcnt.ensure(this, 8ull * (P + 1) + 64, "sweep merge counts"));
+    CR(sw_moff.ensure(this, 4ull * (P + 1) + 64, "sweep merged offsets"));
+    CR(sw_mkeys.ensure(this, std::max<uint64_t>(64, total * 8), "sweep merged keys"));
+    CR(sw_mat.ensure(this, std::max<uint64_t>(64, total), "sweep merged types"));
+    CR(sw_kill.ensure(this, (uint64_t)d.n + 64, "sweep kill bits"));
+    uint32_t* xrec = (uint32_t*)sw_xrec.p;
+    uint32_t* mcnt = (uint32_t*)sw_mcnt.p;
+    CK(hipMemsetAsync(xrec, 0, total * 12, stream));
+    CK(hipMemsetAsync(mcnt, 0, 4ull * (P + 1), stream));
+    CK(hipMemsetAsync(sw_kill.p, 0, m, stream));
+    launch_sw_merge(in, P, xrec, (uint32_t)(3 * before), 0, nullptr, nullptr, nullptr, nullptr,
+                    nullptr, true, stream);
+    CR(comm_allreduce_max_u8((uint8_t*)xrec, total * 12));
+    launch_sw_merge(in, P, xrec, 0, (uint32_t)total, mcnt, mcnt + (P + 1), (uint32_t*)sw_moff.p,
+                    (uint64_t*)sw_mkeys.p, (uint8_t*)sw_mat.p, false, stream);
+    CK(hipGetLastError());
+    SwShard shl;
+    shl.serial = SwList{top ? nullptr : in.tid, (const uint32_t*)sw_moff.p,
+                        (const uint64_t*)sw_mkeys.p, (const uint8_t*)sw_mat.p, total};
+    shl.P = P;
+    shl.m = m;
+    shl.kill = (uint8_t*)sw_kill.p;
+    CR(sweep_enqueue(d, l, l + 1, &shl));
+  }
+  next_level = SW_MAX_LEVEL - 1;
   return DCC_OK;
 }
 
@@ -718,7 +818,8 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   if (sweep) {
     if (profiling) CK(hipEventRecord(pev[0], stream));
     next_level = (int)std::min<uint32_t>(sw_levels, SW_MAX_LEVEL - 1);
-    if (!replay) CR(sweep_enqueue(d, 0, next_level));
+    if (sh) CR(sweep_sharded(d, next_level));
+    else if (!replay) CR(sweep_enqueue(d, 0, next_level));
   } else if (peel) {
     CR(occ_peel(top, maxlen, 0, rounds, info));
   } else if (use_async()) {
@@ -810,7 +911,7 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
       int L = -1;
       if (ab) L = (int)ab;
       else if (hc[next_level].m == 0) break;  // every list decided
-      else if (next_level + (int)sw_levels >= SW_MAX_LEVEL) L = next_level;
+      else if (sh || next_level + (int)sw_levels >= SW_MAX_LEVEL) L = next_level;
       if (L < 0) {
         const int l1 = next_level + (int)sw_levels;
         CR(sweep_enqueue(d, next_level, l1));

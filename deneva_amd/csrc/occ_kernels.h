@@ -365,12 +365,22 @@ struct SwFilterArgs {
   const uint32_t* abandon;
   uint32_t* abandon_out;  // = level + 1 when the survivors stay too many
   uint32_t abandon_min, abandon_num, abandon_den;
+  uint8_t* kill_out;      // key-sharded: per list position, this shard's kill bit (else null)
+  const uint8_t* kill_in; // key-sharded: the all-reduced kill bits (k_sw_apply)
   uint64_t* gclear;       // the next level's key table, KEY_EMPTY-filled here
   uint64_t gclear_n;
   uint32_t* fw_clear;     // the next level's first-writer / last-accessor words
   uint32_t* la_clear;
   uint32_t* err;
   uint64_t* dbg;          // per-workgroup clock stamps (DCC_SW_DEBUG) or null
+};
+// One key-sharded sweep level (the host side of SURVEY.md §8(e)): the merged
+// serial range, its txn count, the list length and the kill-bit buffer.
+struct SwShard {
+  SwList serial;
+  uint32_t P;
+  uint32_t m;
+  uint8_t* kill;
 };
 void launch_sw_pre(const SwPreArgs& a, unsigned grid, hipStream_t st);
 void launch_sw_seq(const SwSeqArgs& a, hipStream_t st);
@@ -380,6 +390,12 @@ void launch_sw_filter_x(const SwFilterArgs& a, unsigned grid, hipStream_t st);
 void launch_sw_filter_b(const SwFilterArgs& a, unsigned grid, hipStream_t st);
 void launch_sw_scan(const SwFilterArgs& a, hipStream_t st);
 void launch_sw_compact(const SwFilterArgs& a, unsigned grid, hipStream_t st);
+void launch_sw_apply(const SwFilterArgs& a, unsigned grid, hipStream_t st);
+// key-sharded serial range: export this rank's records at xbuf + xoff_words
+// (export_only), or merge the all-gathered n_all records into one CSR
+void launch_sw_merge(const SwList& in, uint32_t P, uint32_t* xbuf, uint32_t xoff_words,
+                     uint32_t n_all, uint32_t* cnt, uint32_t* cur, uint32_t* moff,
+                     uint64_t* mkeys, uint8_t* mat, bool export_only, hipStream_t st);
 
 // Several word fills in one launch (replaces a run of hipMemsetAsync calls,
 // each of which costs a dispatch and an idle gap on the stream).

@@ -38,6 +38,8 @@
 // peel, occ_peel.hip).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "dcc_device.h"
 #include "occ_kernels.h"
 
@@ -1065,6 +1067,10 @@ __global__ __launch_bounds__(X ? F_XB : SW_CHUNK) void k_sw_filter(SwFilterArgs 
       }
     }
     if (valid && a.write_hasw) a.hasw[tid] = ok && rlen && range_any(wr, rlo, rlen) ? 1 : 0;
+    if (a.kill_out) {  // key-sharded: this shard's kill bit only (k_sw_apply decides)
+      if (valid) a.kill_out[p] = killed ? 1 : 0;
+      continue;
+    }
     if (killed) a.state[tid] = ST_ABORT;
     if (cand && ok && rlen == 0) a.state[tid] = ST_COMMIT;  // no keys: nothing can kill it
     const bool surv = cand && ok && rlen && !killed;
@@ -1077,6 +1083,7 @@ __global__ __launch_bounds__(X ? F_XB : SW_CHUNK) void k_sw_filter(SwFilterArgs 
       a.tcount[wt] = cnt;
     }
   }
+  if (a.kill_out) return;
   __shared__ unsigned long long s_bs[FW];
   if (lane == 0) s_bs[wv] = wsum;
   __syncthreads();
@@ -1084,6 +1091,127 @@ __global__ __launch_bounds__(X ? F_XB : SW_CHUNK) void k_sw_filter(SwFilterArgs 
     uint64_t t = 0;
     for (uint32_t w = 0; w < FW; w++) t += s_bs[w];
     a.bsum[blockIdx.x] = t;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Key-sharded sweep: every rank holds all txns but only the
+// accesses of its key shard.
+//
+// k_sw_apply: after the MAX all-reduce of the filters' kill bits, the level's
+// decision on every rank alike: a candidate killed on any shard aborts, every
+// other candidate survives (also one without accesses on this shard: another
+// shard may hold them; a txn with none at all commits in a later serial pass).
+// Same tile -> workgroup mapping as the filter (survivor words, counts, totals
+// for k_sw_compact).
+__global__ __launch_bounds__(SW_CHUNK) void k_sw_apply(SwFilterArgs a) {
+  const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+  if (*a.abandon) return;
+  const uint32_t m = list_len(a.m_dev, a.m_host);
+  const uint32_t pos = a.lv->pos;
+  if (pos >= m) return;
+  const uint32_t n64 = (m - pos + 63) / 64;
+  const uint64_t nnz = a.in.nnz;
+  const uint32_t R = (n64 + gridDim.x - 1) / gridDim.x;
+  const uint32_t t_lo = min(blockIdx.x * R, n64), t_hi = min(t_lo + R, n64);
+  uint64_t wsum = 0;
+  for (uint32_t wt = t_lo + wv; wt < t_hi; wt += SW_CHUNK / 64) {
+    const uint32_t p = pos + wt * 64 + lane;
+    bool surv = false;
+    uint32_t len = 0;
+    if (p < m) {
+      const uint32_t tid = a.in.tid ? a.in.tid[p] : p;
+      const bool cand = a.cand_state ? a.state[p] == ST_UNDECIDED : true;
+      const uint32_t s = (uint32_t)min((uint64_t)a.in.off[p], nnz);
+      const uint32_t e = (uint32_t)min((uint64_t)a.in.off[p + 1], nnz);
+      len = e > s ? e - s : 0u;
+      if (cand && a.kill_in[p]) a.state[tid] = ST_ABORT;
+      surv = cand && !a.kill_in[p];
+    }
+    const uint64_t sm = ballot64(surv);
+    const uint64_t acc = wave_sum64(surv ? len : 0u);
+    const uint64_t cnt = ((uint64_t)__popcll(sm) << LB_ACC_BITS) | acc;
+    wsum += cnt;
+    if (lane == 0) {
+      a.sflag[wt] = sm;
+      a.tcount[wt] = cnt;
+    }
+  }
+  __shared__ unsigned long long s_bs[SW_CHUNK / 64];
+  if (lane == 0) s_bs[wv] = wsum;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t t = 0;
+    for (uint32_t w = 0; w < SW_CHUNK / 64; w++) t += s_bs[w];
+    a.bsum[blockIdx.x] = t;
+  }
+}
+
+// k_sw_export: this rank's accesses of the level's serial range (list txns
+// [0, P)) as 12-byte records {key, txn | type << 30} at its slot of the
+// exchange buffer (zero elsewhere: a byte-wise MAX all-reduce then is an
+// all-gather).
+__global__ __launch_bounds__(256) void k_sw_export(SwList in, uint32_t P, uint32_t* rec) {
+  const uint64_t nnz = in.nnz;
+  const uint32_t off0 = (uint32_t)min((uint64_t)in.off[0], nnz);
+  for (uint32_t t = blockIdx.x * 4 + (threadIdx.x >> 6); t < P; t += gridDim.x * 4) {
+    const uint32_t s = (uint32_t)min((uint64_t)in.off[t], nnz);
+    const uint32_t e = (uint32_t)min((uint64_t)in.off[t + 1], nnz);
+    for (uint32_t x = s + lane_id(); x < e; x += 64) {
+      const uint64_t k = in.keys[x];
+      uint32_t* r = rec + 3ull * (x - off0);
+      r[0] = (uint32_t)k;
+      r[1] = (uint32_t)(k >> 32);
+      r[2] = t | ((uint32_t)(in.acctype[x] & 3u) << 30);
+    }
+  }
+}
+
+// k_sw_mcount / k_sw_mscan / k_sw_mscatter: every rank's records merged into
+// one CSR of the serial range, grouped by txn (a counting sort; the order of a
+// txn's accesses is irrelevant to OCC, which compares sets).
+__global__ __launch_bounds__(256) void k_sw_mcount(const uint32_t* rec, uint32_t n, uint32_t* cnt) {
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)
+    atomicAdd(&cnt[rec[3ull * i + 2] & 0x3FFFFFFFu], 1u);
+}
+__global__ __launch_bounds__(1024) void k_sw_mscan(uint32_t* cnt, uint32_t P, uint32_t* off,
+                                                   uint32_t* cur) {
+  __shared__ uint32_t s_w[16];
+  __shared__ uint32_t s_carry;
+  const uint32_t j = threadIdx.x, lane = lane_id(), wv = j >> 6;
+  if (j == 0) s_carry = 0;
+  __syncthreads();
+  for (uint32_t c0 = 0; c0 < P; c0 += 1024) {
+    const uint32_t t = c0 + j;
+    const uint32_t v = t < P ? cnt[t] : 0u;
+    uint32_t tot;
+    const uint32_t ex = wave_excl_u32(v, tot);
+    if (lane == 0) s_w[wv] = tot;
+    __syncthreads();
+    uint32_t base = s_carry;
+    for (uint32_t w = 0; w < wv; w++) base += s_w[w];
+    if (t < P) {
+      off[t] = base + ex;
+      cur[t] = base + ex;
+    }
+    __syncthreads();
+    if (j == 0) {
+      uint32_t all = 0;
+      for (uint32_t w = 0; w < 16; w++) all += s_w[w];
+      s_carry += all;
+    }
+    __syncthreads();
+  }
+  if (j == 0) off[P] = s_carry;
+}
+__global__ __launch_bounds__(256) void k_sw_mscatter(const uint32_t* rec, uint32_t n,
+                                                     uint32_t* cur, uint64_t* keys,
+                                                     uint8_t* at) {
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const uint32_t w2 = rec[3ull * i + 2];
+    const uint32_t q = atomicAdd(&cur[w2 & 0x3FFFFFFFu], 1u);
+    keys[q] = ((uint64_t)rec[3ull * i + 1] << 32) | rec[3ull * i];
+    at[q] = (uint8_t)(w2 >> 30);
   }
 }
 
@@ -1296,6 +1424,21 @@ void launch_sw_filter_b(const SwFilterArgs& a, unsigned grid, hipStream_t st) {
   k_sw_filter<false><<<grid ? grid : 1u, SW_CHUNK, 0, st>>>(a);
 }
 void launch_sw_scan(const SwFilterArgs& a, hipStream_t st) { k_sw_scan<<<1, 1024, 0, st>>>(a); }
+void launch_sw_apply(const SwFilterArgs& a, unsigned grid, hipStream_t st) {
+  k_sw_apply<<<grid ? grid : 1u, SW_CHUNK, 0, st>>>(a);
+}
+void launch_sw_merge(const SwList& in, uint32_t P, uint32_t* xbuf, uint32_t xoff_words,
+                     uint32_t n_all, uint32_t* cnt, uint32_t* cur, uint32_t* moff,
+                     uint64_t* mkeys, uint8_t* mat, bool export_only, hipStream_t st) {
+  if (export_only) {
+    k_sw_export<<<256, 256, 0, st>>>(in, P, xbuf + xoff_words);
+    return;
+  }
+  const unsigned g = (unsigned)std::min<uint32_t>((n_all + 255) / 256 + 1, 2048);
+  k_sw_mcount<<<g, 256, 0, st>>>(xbuf, n_all, cnt);
+  k_sw_mscan<<<1, 1024, 0, st>>>(cnt, P, moff, cur);
+  k_sw_mscatter<<<g, 256, 0, st>>>(xbuf, n_all, cur, mkeys, mat);
+}
 void launch_sw_compact(const SwFilterArgs& a, unsigned grid, hipStream_t st) {
   k_sw_compact<<<grid ? grid : 1u, SW_CHUNK, 0, st>>>(a);
 }

@@ -137,8 +137,8 @@ int dcc_set_profiling(dcc_ctx* ctx, int enable);
 #define DCC_OPT_BATCH_MAX 2   /* max rounds enqueued between host synchronisations        */
 #define DCC_OPT_PEEL 3        /* OCC prefix peel: -1 auto (default), 0 off, > 0 prefix length */
 #define DCC_OPT_PEEL_MIN 4    /* auto peel applies to (sub-)batches of >= value txns        */
-#define DCC_OPT_SOLVER 5      /* OCC solver: 0 auto (sweep unless key-sharded), 1 fixed-point
-                                 rounds, 2 asynchronous, 3 sweep (unsharded only)          */
+#define DCC_OPT_SOLVER 5      /* OCC solver: 0 auto (sweep; key-sharded too), 1 fixed-point
+                                 rounds, 2 asynchronous, 3 sweep                           */
 #define DCC_OPT_SWEEP_LEVELS 6 /* sweep levels enqueued between host synchronisations       */
 int dcc_set_option(dcc_ctx* ctx, int option, int64_t value);
 /* Pre-size device workspaces so a later call performs no allocation. */

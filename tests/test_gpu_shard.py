@@ -4,7 +4,8 @@ Ranks are separate processes sharing the box's one GPU; each owns the keys
 with dcc_key_shard(key, world) == rank and exchanges the per-round status
 through dcc_comm_init_host (gloo all-reduce MAX on the host).  The engine
 code path is the one RCCL drives on an 8-GPU node — only the all-reduce
-transport differs.  Decisions, commit tn, history across epochs, and Calvin
+transport differs.  OCC runs the key-sharded sweep (the serial range
+all-gathered and merged on every rank, the filters' kill bits all-reduced).  Decisions, commit tn, history across epochs, and Calvin
 grant groups / readiness must equal the unsharded oracle bit for bit."""
 import os
 import socket
@@ -52,7 +53,7 @@ def _worker(rank, world, port, out):
         eng.tnc = 0  # each batch is checked as a fresh epoch
         rc, tn, st = eng.occ_validate_epoch(d.shard_filter(b, rank, world), want_tn=True)
         res["occ"].append((np.asarray(rc).copy(), np.asarray(tn).copy(), st["rounds"],
-                           st["n_shards"]))
+                           st["n_shards"], st["peel_prefix"], b.n_txn))
     # three epochs with history (start/finish windows) appended across epochs
     eng.tnc = 0
     eng.history_clear()
@@ -81,8 +82,10 @@ def test_sharded_engine_matches_unsharded(world):
     for bi, b in enumerate(_occ_batches()):
         erc, etn, _ = orc.occ(b)
         for r in range(world):
-            rc, tn, rounds, nsh = out[r]["occ"][bi]
+            rc, tn, rounds, nsh, prefix, n = out[r]["occ"][bi]
             assert nsh == world
+            if n > 1024:
+                assert prefix > 0, "the key-sharded sweep decided the serial prefix"
             assert np.array_equal(rc, erc), f"rank {r} batch {bi}: rc differs from unsharded"
             assert np.array_equal(tn.astype(np.uint64), etn), f"rank {r} batch {bi}: tn differs"
     # history epochs: replay the oracle epoch by epoch with the same windows
