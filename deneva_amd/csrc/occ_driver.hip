@@ -443,7 +443,6 @@ int dcc_ctx::occ_peel(const SubProb& sp, uint32_t maxlen, int level, uint32_t& r
 // synchronisation (list lengths live on the device), sw_levels at a time.
 static constexpr size_t SW_PREP_OFF = 32768;  // prep partials inside `part` / `hpart`
 static constexpr size_t SW_HCTL = 13312;      // control-block copy inside `hmisc`
-static constexpr size_t SW_HX = 14336;        // key-sharded sweep: list length + abandon word
 static constexpr uint32_t SW_PMAX_TOP = 65536;
                                                           // the serial pass's LDS set)
 static uint32_t sw_pmax(int level) {
@@ -632,33 +631,21 @@ int dcc_ctx::sweep_sharded(const DevBatch& d, int& next_level) {
       in = SwList{(const uint32_t*)b.tid.p, (const uint32_t*)b.off.p, (const uint64_t*)b.keys.p,
                   (const uint8_t*)b.acctype.p, d.nnz};
     }
-    // (1) list length, abandon word, this rank's accesses of [0, P)
-    uint32_t m = (uint32_t)d.n;
-    uint32_t* hx = (uint32_t*)((char*)hmisc + SW_HX);
-    {
-      GatherArgs ga{};
-      ga.job[ga.n++] = CopyJob{&ctl[l].m, (uint32_t*)((char*)hmisc_dev + SW_HX), 1};
-      ga.job[ga.n++] = CopyJob{abandon, (uint32_t*)((char*)hmisc_dev + SW_HX) + 1, 1};
-      launch_gather(ga, stream);
-      CK(hipStreamSynchronize(stream));
-      if (!top) m = hx[0];
-      if (hx[1]) return DCC_OK;  // an earlier level handed off
-    }
+    // (1) one size exchange per level: the list length and abandon word
+    // (alike on every rank) and each rank's accesses of the serial range
+    uint32_t* cnt = (uint32_t*)sw_xcnt.p;
+    CK(hipMemsetAsync(cnt, 0, 4ull * (R + 2), stream));
+    launch_sw_share(top ? nullptr : &ctl[l].m, (uint32_t)d.n, abandon, top ? d.off : in.off,
+                    sw_pmax(l), (uint32_t)me, cnt, stream);
+    CR(comm_allreduce_max_u8((uint8_t*)cnt, 4ull * (R + 2)));
+    std::vector<uint32_t> hc(R + 2);
+    CK(hipMemcpyAsync(hc.data(), cnt, 4ull * (R + 2), hipMemcpyDeviceToHost, stream));
+    CK(hipStreamSynchronize(stream));
+    const uint32_t m = hc[0];
+    if (hc[1]) return DCC_OK;  // an earlier level handed off
     if (m == 0) return DCC_OK;
     const uint32_t P = std::min<uint32_t>(sw_pmax(l), m);
-    uint32_t offs[2];
-    CK(hipMemcpyAsync(offs, top ? d.off : in.off, 4, hipMemcpyDeviceToHost, stream));
-    CK(hipMemcpyAsync(offs + 1, (top ? d.off : in.off) + P, 4, hipMemcpyDeviceToHost, stream));
-    CK(hipStreamSynchronize(stream));
-    const uint32_t mine = offs[1] - offs[0];
-    // (2) every rank's share: all-gather of one u32 per rank
-    uint32_t* cnt = (uint32_t*)sw_xcnt.p;
-    CK(hipMemsetAsync(cnt, 0, 4ull * R, stream));
-    CK(hipMemcpyAsync(cnt + me, &mine, 4, hipMemcpyHostToDevice, stream));
-    CR(comm_allreduce_max_u8((uint8_t*)cnt, 4ull * R));
-    std::vector<uint32_t> share(R);
-    CK(hipMemcpyAsync(share.data(), cnt, 4ull * R, hipMemcpyDeviceToHost, stream));
-    CK(hipStreamSynchronize(stream));
+    const uint32_t* share = hc.data() + 2;
     uint64_t total = 0, before = 0;
     for (int r = 0; r < R; r++) {
       if (r < me) before += share[r];

@@ -391,6 +391,9 @@ void launch_sw_filter_b(const SwFilterArgs& a, unsigned grid, hipStream_t st);
 void launch_sw_scan(const SwFilterArgs& a, hipStream_t st);
 void launch_sw_compact(const SwFilterArgs& a, unsigned grid, hipStream_t st);
 void launch_sw_apply(const SwFilterArgs& a, unsigned grid, hipStream_t st);
+void launch_sw_share(const uint32_t* m_dev, uint32_t m_host, const uint32_t* abandon,
+                     const uint32_t* off, uint32_t p_max, uint32_t rank, uint32_t* cnt,
+                     hipStream_t st);
 // key-sharded serial range: export this rank's records at xbuf + xoff_words
 // (export_only), or merge the all-gathered n_all records into one CSR
 void launch_sw_merge(const SwList& in, uint32_t P, uint32_t* xbuf, uint32_t xoff_words,

@@ -1147,6 +1147,18 @@ __global__ __launch_bounds__(SW_CHUNK) void k_sw_apply(SwFilterArgs a) {
   }
 }
 
+// k_sw_share (one thread): a key-sharded level's sizes in this rank's slots
+// of the size exchange: list length (every rank alike), the abandon word, the
+// serial range's txn count and this rank's accesses of it.
+__global__ void k_sw_share(const uint32_t* m_dev, uint32_t m_host, const uint32_t* abandon,
+                           const uint32_t* off, uint32_t p_max, uint32_t rank, uint32_t* cnt) {
+  const uint32_t m = m_dev ? *m_dev : m_host;
+  const uint32_t P = min(p_max, m);
+  cnt[0] = m;
+  cnt[1] = *abandon;
+  cnt[2 + rank] = m ? off[P] - off[0] : 0u;
+}
+
 // k_sw_export: this rank's accesses of the level's serial range (list txns
 // [0, P)) as 12-byte records {key, txn | type << 30} at its slot of the
 // exchange buffer (zero elsewhere: a byte-wise MAX all-reduce then is an
@@ -1424,6 +1436,11 @@ void launch_sw_filter_b(const SwFilterArgs& a, unsigned grid, hipStream_t st) {
   k_sw_filter<false><<<grid ? grid : 1u, SW_CHUNK, 0, st>>>(a);
 }
 void launch_sw_scan(const SwFilterArgs& a, hipStream_t st) { k_sw_scan<<<1, 1024, 0, st>>>(a); }
+void launch_sw_share(const uint32_t* m_dev, uint32_t m_host, const uint32_t* abandon,
+                     const uint32_t* off, uint32_t p_max, uint32_t rank, uint32_t* cnt,
+                     hipStream_t st) {
+  k_sw_share<<<1, 1, 0, st>>>(m_dev, m_host, abandon, off, p_max, rank, cnt);
+}
 void launch_sw_apply(const SwFilterArgs& a, unsigned grid, hipStream_t st) {
   k_sw_apply<<<grid ? grid : 1u, SW_CHUNK, 0, st>>>(a);
 }
