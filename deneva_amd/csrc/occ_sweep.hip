@@ -885,6 +885,7 @@ constexpr uint32_t F_STASH = 256;  // Bloom-positive keys kept in LDS per wave
 constexpr uint32_t F_XS = 2048;    // small-C filter instance: LDS exact-set slots
 constexpr uint32_t F_XCAP = 1024;  // ... for C of up to this many keys (<= 50% load)
 constexpr uint32_t F_XB = 256;     // ... threads per workgroup
+constexpr uint32_t F_XBITS_LOG = 16;  // ... its one-hash bitmap of C (8 KiB)
 
 // ---------------------------------------------------------------------------
 // k_sw_filter: list txns [pos, m) against C, 64 per wave, grid-stride (no
@@ -901,11 +902,12 @@ __global__ __launch_bounds__(X ? F_XB : SW_CHUNK) void k_sw_filter(SwFilterArgs 
   constexpr uint32_t CS = X ? F_XS : F_EXACT;  // exact-set slots
   // X: a one-hash bitmap of C built here (one conflict-light ds_read_b32 per
   // access) in front of the exact set; otherwise the level's Bloom filter
-  __shared__ uint32_t bl[(1u << SW_BLOOM_LOG) / 32];
+  constexpr uint32_t BLOG = X ? F_XBITS_LOG : SW_BLOOM_LOG;  // filter bits (log2)
+  __shared__ uint32_t bl[(1u << BLOG) / 32];
   __shared__ __attribute__((aligned(16))) uint64_t cex[CS];
   __shared__ uint64_t s_hit[FW][SW_WA / 64];
   __shared__ uint64_t s_wr[FW][SW_WA / 64];
-  __shared__ uint64_t s_stash[FW][X ? 1 : F_STASH];
+  __shared__ uint64_t s_stash[FW][F_STASH];
   __shared__ uint32_t s_wpre[FW][SW_WA / 64];
   const uint32_t j = threadIdx.x, lane = lane_id(), wv = j >> 6;
   if (*a.abandon) return;
@@ -930,7 +932,7 @@ __global__ __launch_bounds__(X ? F_XB : SW_CHUNK) void k_sw_filter(SwFilterArgs 
       uint4* dst = (uint4*)bl;
       for (uint32_t q = j; q < (1u << SW_BLOOM_LOG) / 128; q += B) dst[q] = src[q];
     } else {
-      for (uint32_t q = j; q < (1u << SW_BLOOM_LOG) / 32; q += B) bl[q] = 0;
+      for (uint32_t q = j; q < (1u << BLOG) / 32; q += B) bl[q] = 0;
     }
     if (small)
       for (uint32_t q = j; q < CS; q += B) cex[q] = KEY_EMPTY;
@@ -943,6 +945,7 @@ __global__ __launch_bounds__(X ? F_XB : SW_CHUNK) void k_sw_filter(SwFilterArgs 
       if (X) {
         uint32_t b1, b2;
         bloom_bits(kq, b1, b2);
+        b1 >>= SW_BLOOM_LOG - BLOG;
         atomicOr(&bl[b1 >> 5], 1u << (b1 & 31u));
       }
     }
@@ -1016,19 +1019,18 @@ __global__ __launch_bounds__(X ? F_XB : SW_CHUNK) void k_sw_filter(SwFilterArgs 
         uint32_t b1, b2;
         bloom_bits(key[u], b1, b2);
         if (X) {
+          b1 >>= SW_BLOOM_LOG - BLOG;
           h = in && ((bl[b1 >> 5] >> (b1 & 31u)) & 1u) != 0;
         } else {
           const uint32_t wa = bl[b1 >> 5], wb = bl[b2 >> 5];
           h = in && (((wa >> (b1 & 31u)) & (wb >> (b2 & 31u)) & 1u) != 0);
         }
         const uint64_t hb = ballot64(h), wbm = ballot64(in && at[u] == 1);
-        if (!X) {
-          if (h) {
-            const uint32_t ci = npos + (uint32_t)__popcll(hb & lanemask_lt());
-            if (ci < F_STASH) stash[ci] = key[u];
-          }
-          npos += (uint32_t)__popcll(hb);
+        if (h) {
+          const uint32_t ci = npos + (uint32_t)__popcll(hb & lanemask_lt());
+          if (ci < F_STASH) stash[ci] = key[u];
         }
+        npos += (uint32_t)__popcll(hb);
         if (lane == 0) {
           hit[(b0 >> 6) + u] = hb;
           wr[(b0 >> 6) + u] = wbm;
@@ -1056,8 +1058,7 @@ __global__ __launch_bounds__(X ? F_XB : SW_CHUNK) void k_sw_filter(SwFilterArgs 
           if (nx >= rlo + rlen) break;
           const uint32_t ci = s_wpre[wv][nx >> 6] +
                               (uint32_t)__popcll(hit[nx >> 6] & ((1ull << (nx & 63)) - 1ull));
-          // (X keeps no stash: the key again, from L1/L2)
-          const uint64_t kx = (!X && ci < F_STASH) ? stash[ci] : a.in.keys[A0 + nx];
+          const uint64_t kx = ci < F_STASH ? stash[ci] : a.in.keys[A0 + nx];
           if (small ? lset_find<CS>(cex, kx) : c_exact(a, kx)) {
             killed = true;
             break;
