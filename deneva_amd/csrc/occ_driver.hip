@@ -446,6 +446,20 @@ static constexpr size_t SW_HCTL = 13312;      // control-block copy inside `hmis
 static constexpr uint32_t SW_PMAX_TOP = 65536;
                                                           // the serial pass's LDS set)
 static uint32_t sw_pmax(int level) {
+  // DCC_SW_PMAX="p0,p1,...": per-level serial prefixes (tuning experiments)
+  static const std::vector<uint32_t> ov = [] {
+    std::vector<uint32_t> v;
+    if (const char* e = getenv("DCC_SW_PMAX"))
+      for (const char* c = e; *c;) {
+        char* x;
+        const unsigned long p = strtoul(c, &x, 10);
+        if (x == c) break;
+        v.push_back((uint32_t)std::min<unsigned long>(std::max<unsigned long>(p, SW_T), SW_PMAX_TOP));
+        c = *x ? x + 1 : x;
+      }
+    return v;
+  }();
+  if (level < (int)ov.size()) return ov[level];
   return level >= 6 ? SW_PMAX_TOP : (1024u << level);
 }
 static size_t sw_ctl_bytes() { return (SW_MAX_LEVEL + 2) * sizeof(SwLevel) + 64; }
@@ -951,12 +965,15 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
         // done, decisions written, end; consumer wait polls; tiles
         const uint64_t* t = dv.data() + l * 1024;
         if (t[4])
-          fprintf(stderr, "sweep L%d seq: %llu tiles, init %.2f us, loop %.2f us, decisions "
+          fprintf(stderr, "sweep L%d (m %u, pos %u) seq: %llu tiles, init %.2f us, loop %.2f us, decisions "
                           "%.2f us, C out %.2f us, consumer waits %llu, producer waits %llu, "
                           "loop cycles/tile %.0f\n",
-                  l, (unsigned long long)t[6], (t[1] - t[0]) * 0.01, (t[2] - t[1]) * 0.01,
+                  l, hc[l].m, hc[l].pos, (unsigned long long)t[6], (t[1] - t[0]) * 0.01, (t[2] - t[1]) * 0.01,
                   (t[3] - t[2]) * 0.01, (t[4] - t[3]) * 0.01, (unsigned long long)t[5],
                   (unsigned long long)t[7], t[6] ? (double)t[8] / t[6] : 0.0);
+        if (t[6])
+          fprintf(stderr, "  seq L%d: candidates/tile %.2f, fixed-point rounds after the first/tile %.2f\n",
+                  l, (double)t[9] / t[6], (double)t[10] / t[6]);
         // filter: per workgroup init / first chunk local / look-back / writes / total
         const uint64_t* f = dv.data() + 4096 + l * 256 * 8;
         double fi = 0, fl = 0, fb = 0, fw = 0, ft = 0, nc = 0;

@@ -242,20 +242,34 @@ __host__ __device__ constexpr uint32_t sw_apack(uint32_t id, bool w) {
   return (id << 6) | (w ? 32u : 0u);
 }
 __host__ __device__ constexpr uint32_t sw_aid(uint32_t e) { return e >> 6; }
-// A tile-list entry as the serial pass reads it: bitmap word << 12 | txn of
-// the tile << 6 | WR << 5 | bit.  The probe is the LDS word at byte address
-// (e >> 10) & ~3 shifted right by e (shifts use only the low 5 bits).
-__host__ __device__ constexpr uint32_t sw_tpack(uint32_t id, uint32_t t, bool w) {
-  return ((id >> 5) << 12) | (t << 6) | (w ? 32u : 0u) | (id & 31u);
+// Tile-list entries as the serial pass reads them, laid out so that one
+// shift gives the LDS byte address of the committed bitmap's word and the
+// bit / txn fields sit where the shift instructions read them (their low 5
+// or 6 bits):
+//   probe:  word << 7  | bit            address e >> 5,  bit e & 31
+//   insert: word << 13 | bit << 6 | t   address e >> 11, bit (e >> 6) & 31,
+//                                       txn of the tile e & 63
+__host__ __device__ constexpr uint32_t sw_ppack(uint32_t id) {
+  return ((id >> 5) << 7) | (id & 31u);
+}
+__host__ __device__ constexpr uint32_t sw_ipack(uint32_t id, uint32_t t) {
+  return ((id >> 5) << 13) | ((id & 31u) << 6) | t;
 }
 // an id one past the largest table slot: the always-zero word that ends the
-// serial pass's committed bitmap
+// serial pass's committed bitmap (64 spare words follow it: lane q of an
+// unused insert slot ORs 0 into spare word q)
 constexpr uint32_t SW_ID_NONE = 1u << SW_GBITS_MAX;
 constexpr uint32_t SW_A_NONE = sw_apack(SW_ID_NONE, false);
-constexpr uint32_t SW_E_NONE = sw_tpack(SW_ID_NONE, 0, false);
+constexpr uint32_t SW_P_NONE = sw_ppack(SW_ID_NONE);
+__host__ __device__ constexpr uint32_t sw_idummy(uint32_t q) {
+  return sw_ipack(SW_ID_NONE + 32u * (1u + (q & 63u)), 0);
+}
 // per-txn meta word of a tile record
 constexpr uint32_t SWM_VALID = 1, SWM_PRE = 2, SWM_HASW = 4, SWM_STOP = 16;
-// One 64-txn tile of a level's serial range as k_sw_seq reads it (5,120 B).
+// list chunks the serial pass holds in registers: the first SW_RC * 64
+// entries of each list (padded with no-op entries by k_sw_rows)
+constexpr uint32_t SW_RC = 2;
+// One 64-txn tile of a level's serial range as k_sw_seq reads it (6,144 B).
 // Only the accesses the serial pass must look at, as two tile-wide lists:
 // probes (accesses whose key an earlier txn of the range writes), grouped by
 // txn (txn t's are [pspan & 0xFFFF, pspan >> 16)), and inserts (writes whose
@@ -267,8 +281,13 @@ struct SwRec {
   uint32_t meta[SW_T];    // SWM_* (SWM_STOP on every txn: the access budget ends here)
   uint32_t rtid[SW_T];    // original txn index
   uint32_t pspan[SW_T];
-  uint32_t np, ni, pad[6];
+  // seg[c][t]: txn t's probe entries among list positions [64c, 64c + 64)
+  uint64_t seg[SW_RC][SW_T];
+  uint32_t np, ni;
+  uint32_t hdr;  // SWH_*: the serial pass's per-tile branches
+  uint32_t pad[5];
 };
+constexpr uint32_t SWH_PLONG = 1, SWH_ILONG = 2, SWH_STOP = 4;
 struct SwLevel {     // device control words of one level
   uint32_t m;        // list length (written by the previous level's filter)
   uint32_t acc;      // accesses of the list

@@ -500,7 +500,10 @@ __global__ __launch_bounds__(256) void k_sw_rows(SwPreArgs a) {
   const uint32_t k = blockIdx.x, j = threadIdx.x, lane = lane_id();
   if (k >= ntiles) return;
   SwRec& R = a.rec[k];
-  if (R.meta[0] & SWM_STOP) return;  // uniform: written on every txn of a stopped tile
+  if (R.meta[0] & SWM_STOP) {  // uniform: written on every txn of a stopped tile
+    if (j == 0) R.hdr = SWH_STOP;
+    return;
+  }
   uint64_t* dbg = (a.dbg && k == 0) ? a.dbg : nullptr;
   if (dbg && j == 0) dbg[8] = __builtin_amdgcn_s_memrealtime();
   const uint64_t nnz = a.in.nnz;
@@ -564,6 +567,16 @@ __global__ __launch_bounds__(256) void k_sw_rows(SwPreArgs a) {
   if (t == 0) {
     R.np = np;
     R.ni = ni;
+    R.hdr = (np > SW_RC * 64 ? SWH_PLONG : 0u) | (ni > SW_RC * 64 ? SWH_ILONG : 0u);
+  }
+  // the register chunks: per txn its entries in each, no-op padding
+#pragma unroll
+  for (uint32_t c = 0; c < SW_RC; c++) {
+    const uint32_t lo = max(ps, c * 64), hi = min(ps + cp, c * 64 + 64);
+    const uint32_t nb = hi > lo ? hi - lo : 0u;
+    R.seg[c][t] = nb ? (nb >= 64 ? ~0ull : ((1ull << nb) - 1ull)) << (lo - c * 64) : 0ull;
+    if (c * 64 + t >= np) R.probe[c * 64 + t] = SW_P_NONE;
+    if (c * 64 + t >= ni) R.ins[c * 64 + t] = sw_idummy(t);
   }
   uint32_t* ovf = a.lst_ovf + (uint64_t)k * SW_OVF;
   for (uint32_t q = 0; q < len; q++) {
@@ -572,13 +585,13 @@ __global__ __launch_bounds__(256) void k_sw_rows(SwPreArgs a) {
     const uint32_t ent = s_ent[s + q];
     const uint32_t id = sw_aid(ent);
     if (f & 1u) {
-      const uint32_t e = sw_tpack(id, t, false);
+      const uint32_t e = sw_ppack(id);
       if (ps < SW_PL) R.probe[ps] = e;
       else ovf[ps - SW_PL] = e;
       ps++;
     }
     if (f & 2u) {
-      const uint32_t e = sw_tpack(id, t, true);
+      const uint32_t e = sw_ipack(id, t);
       if (is < SW_IL) R.ins[is] = e;
       else ovf[SW_TA + is - SW_IL] = e;
       is++;
@@ -598,9 +611,10 @@ __global__ __launch_bounds__(256) void k_sw_rows(SwPreArgs a) {
 // tile's probes.  The other 15 waves stream the tile records from global
 // memory into an LDS ring ahead of it (one tile per wave in flight; ready and
 // consumed counters in LDS), then all 16 join for the write-out.
-constexpr uint32_t SEQ_RING = 12;  // LDS record slots (61,440 B)
+constexpr uint32_t SEQ_RING = 12;  // LDS record slots (73,728 B)
 constexpr uint32_t SEQ_PROD = 15;  // producer waves
 constexpr uint32_t SEQ_V4 = sizeof(SwRec) / 16;  // uint4 per record
+static_assert(SW_RC * 64 <= SW_IL, "register chunks inside the record");
 static_assert(sizeof(SwRec) % (16 * 64) == 0, "record copy: whole uint4 per lane");
 
 // A load the compiler's wait-count tracking does not see: it completes inside
@@ -614,16 +628,22 @@ __device__ inline uint32_t ld_sync(const uint32_t* p) {
 __device__ inline uint32_t lds_ld(uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+__device__ inline uint32_t lds_ld_rlx(uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 __device__ inline void lds_st(uint32_t* p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// committed-set bitmap probe / insert of a tile-list entry (sw_tpack)
+// committed-set bitmap probe of a probe entry (sw_ppack): its bit
 __device__ inline uint32_t cb_probe(const uint32_t* cb, uint32_t e) {
-  return *(const uint32_t*)((const char*)cb + ((e >> 10) & ~3u)) >> (e & 31u);
+  return (*(const uint32_t*)((const char*)cb + (e >> 5)) >> (e & 31u)) & 1u;
 }
-__device__ inline void cb_insert_w(uint32_t* cb, uint32_t e) {
-  atomicOr((uint32_t*)((char*)cb + ((e >> 10) & ~3u)), ((e >> 5) & 1u) << (e & 31u));
+// insert entry (sw_ipack): the key joins C if its txn committed (bit of M);
+// ORs 0 otherwise
+__device__ inline void cb_insert_m(uint32_t* cb, uint32_t e, uint64_t M) {
+  const uint32_t b = (uint32_t)(M >> (e & 63u)) & 1u;
+  atomicOr((uint32_t*)((char*)cb + (e >> 11)), b << ((e >> 6) & 31u));
 }
 // any bit of hm (entries q0 .. q0+63) inside the entry range [ps, pe)
 __device__ inline bool seg_any(uint64_t hm, uint32_t ps, uint32_t pe, uint32_t q0) {
@@ -635,11 +655,21 @@ __device__ inline bool seg_any(uint64_t hm, uint32_t ps, uint32_t pe, uint32_t q
 }
 
 __global__ __launch_bounds__(1024) void k_sw_seq(SwSeqArgs a) {
-  __shared__ uint32_t cbits[(1u << SW_GBITS_MAX) / 32 + 1];  // + the SW_ID_NONE word
-  __shared__ uint64_t s_M[SW_PMAX_TILES];  // commit mask per decided tile
-  __shared__ __attribute__((aligned(16))) SwRec ring[SEQ_RING];
-  __shared__ uint32_t s_ready[SEQ_RING];
-  __shared__ uint32_t s_done, s_stop, s_k;
+  // one block, the committed bitmap first: its word addresses are the list
+  // entries' shifted fields with no base to add
+  struct Lds {
+    uint32_t cbits[(1u << SW_GBITS_MAX) / 32 + 1 + 64];  // + the SW_ID_NONE word, spare words
+    uint32_t s_ready[SEQ_RING];
+    uint32_t s_done, s_stop, s_k;
+    uint64_t s_M[SW_PMAX_TILES];  // commit mask per decided tile
+    SwRec ring[SEQ_RING];
+  };
+  __shared__ __attribute__((aligned(16))) Lds L;
+  uint32_t* const cbits = L.cbits;
+  uint32_t* const s_ready = L.s_ready;
+  uint32_t &s_done = L.s_done, &s_stop = L.s_stop, &s_k = L.s_k;
+  uint64_t* const s_M = L.s_M;
+  SwRec* const ring = L.ring;
   const uint32_t j = threadIdx.x, lane = lane_id(), wv = j >> 6;
   if (*a.abandon) return;
   const uint32_t m = list_len(a.m_dev, a.m_host);
@@ -661,7 +691,7 @@ __global__ __launch_bounds__(1024) void k_sw_seq(SwSeqArgs a) {
   if (dbg && j == 0) dbg[0] = __builtin_amdgcn_s_memrealtime();
   const uint32_t nwords = (1u << a.gbits) / 32;
   for (uint32_t q = j; q < nwords; q += 1024) cbits[q] = 0;
-  if (j == 0) cbits[SW_ID_NONE / 32] = 0;  // the SW_E_NONE word
+  if (j == 0) cbits[SW_ID_NONE / 32] = 0;  // the word padding probes read
   __syncthreads();
 
   if (dbg && j == 0) dbg[1] = __builtin_amdgcn_s_memrealtime();
@@ -692,83 +722,123 @@ __global__ __launch_bounds__(1024) void k_sw_seq(SwSeqArgs a) {
     }
     if (dbg && lane == 0 && pw) atomicAdd((unsigned long long*)&dbg[7], (unsigned long long)pw);
   } else if (ntiles) {
-    // software pipelined: tile k+1's record (per-txn words and the first
-    // chunk of each list) is read while tile k resolves
-    uint32_t k = 0, cw = 0;
+    // software pipelined: while tile k resolves, tile k+1's record (per-txn
+    // words and the first SW_RC chunks of its lists) is read into registers
+    // behind tile k's probes, and tile k+2's ready flag with it
+    uint32_t k = 0, cw = 0, st_it = 0;
+    uint64_t st_u = 0;
     __builtin_amdgcn_s_setprio(3);  // the serial wave issues ahead of the producers
     const uint64_t cyc0 = __builtin_amdgcn_s_memtime();
     while (lds_ld(&s_ready[0]) != 1u) {
       cw++;
       __builtin_amdgcn_s_sleep(1);
     }
-    uint64_t cdep;
-    uint32_t cmeta, cspan, cnp, cni, cpe, cie;
+    uint64_t cdep, cseg[SW_RC];
+    uint32_t cmeta, chdr, cpe[SW_RC], cie[SW_RC];
     auto read_rec = [&](const SwRec& T) {
       cdep = T.dep[lane];
       cmeta = T.meta[lane];
-      cspan = T.pspan[lane];
-      cnp = T.np;
-      cni = T.ni;
-      cpe = T.probe[lane];
-      cie = T.ins[lane];
+      chdr = T.hdr;
+#pragma unroll
+      for (uint32_t c = 0; c < SW_RC; c++) {
+        cpe[c] = T.probe[c * 64 + lane];
+        cie[c] = T.ins[c * 64 + lane];
+        cseg[c] = T.seg[c][lane];
+      }
     };
     read_rec(ring[0]);
-    for (; k < ntiles; k++) {
-      const uint32_t meta = cmeta;
-      if (__builtin_amdgcn_readfirstlane(meta) & SWM_STOP) break;
-      const uint64_t dep = cdep;
-      const uint32_t ps = cspan & 0xFFFFu, pe = cspan >> 16;
-      const uint32_t np = __builtin_amdgcn_readfirstlane(cnp);
-      const uint32_t ni = __builtin_amdgcn_readfirstlane(cni);
-      const uint32_t e0 = lane < np ? cpe : SW_E_NONE, i0 = lane < ni ? cie : SW_E_NONE;
-      const uint32_t slot = k % SEQ_RING;
-      const uint32_t* ovf = a.lst_ovf + (uint64_t)k * SW_OVF;
-      // (1) probe C, 64 list entries per round: a txn touching a committed
-      // key is dead
-      const uint32_t h0 = cb_probe(cbits, e0) & 1u;
-      // the next record (its flag read shares this round trip)
-      const uint32_t kn = k + 1, sn = kn % SEQ_RING;
-      if (kn < ntiles) {
-        while (lds_ld(&s_ready[sn]) != kn + 1) {
-          cw++;
-          __builtin_amdgcn_s_sleep(1);
-        }
-        read_rec(ring[sn]);
+    if (ntiles > 1)
+      while (lds_ld(&s_ready[1 % SEQ_RING]) != 2u) {
+        cw++;
+        __builtin_amdgcn_s_sleep(1);
       }
-      bool kill = seg_any(ballot64(h0), ps, pe, 0);
-      for (uint32_t q0 = 64; q0 < np; q0 += 64) {  // long lists (uniform)
-        const uint32_t q = q0 + lane;
-        uint32_t e = SW_E_NONE;
-        if (q < np) e = q < SW_PL ? ring[slot].probe[q] : ld_sync(ovf + (q - SW_PL));
-        kill |= seg_any(ballot64(cb_probe(cbits, e) & 1u), ps, pe, q0);
+    uint32_t fl = 0, slot = 0;
+    for (; k < ntiles; k++) {
+      const uint32_t hdr = __builtin_amdgcn_readfirstlane(chdr);
+      if (hdr & SWH_STOP) break;
+      const uint64_t dep = cdep;
+      const uint32_t meta = cmeta;
+      uint64_t seg[SW_RC];
+      uint32_t pe[SW_RC], ie[SW_RC];
+#pragma unroll
+      for (uint32_t c = 0; c < SW_RC; c++) {
+        seg[c] = cseg[c];
+        pe[c] = cpe[c];
+        ie[c] = cie[c];
+      }
+      const uint32_t kn = k + 1, sn = slot + 1 == SEQ_RING ? 0u : slot + 1;
+      // (1) probe C with the register chunks: a txn touching a committed key
+      // is dead (padding entries read the always-zero word)
+      uint32_t h[SW_RC];
+#pragma unroll
+      for (uint32_t c = 0; c < SW_RC; c++) h[c] = cb_probe(cbits, pe[c]);
+      // tile k+1's record (its ready flag was checked during tile k-1; a
+      // wave's LDS operations complete in order, so these reads see the
+      // producer's writes; a slot past the last tile is read but never used)
+      // and tile k+2's flag share the probes' round trip
+      read_rec(ring[sn]);
+      fl = lds_ld_rlx(&s_ready[sn + 1 == SEQ_RING ? 0u : sn + 1]);
+      uint64_t kv = 0;
+#pragma unroll
+      for (uint32_t c = 0; c < SW_RC; c++) kv |= ballot64(h[c] != 0) & seg[c];
+      uint64_t K = ballot64(kv != 0);
+      if (hdr & SWH_PLONG) {  // long probe lists (rare)
+        const uint32_t np = __builtin_amdgcn_readfirstlane(ring[slot].np);
+        const uint32_t sp = ring[slot].pspan[lane];
+        const uint32_t ps = sp & 0xFFFFu, pe2 = sp >> 16;
+        const uint32_t* ovf = a.lst_ovf + (uint64_t)k * SW_OVF;
+        bool kill = false;
+        for (uint32_t q0 = SW_RC * 64; q0 < np; q0 += 64) {
+          const uint32_t q = q0 + lane;
+          uint32_t e = SW_P_NONE;
+          if (q < np) e = q < SW_PL ? ring[slot].probe[q] : ld_sync(ovf + (q - SW_PL));
+          kill |= seg_any(ballot64(cb_probe(cbits, e) != 0), ps, pe2, q0);
+        }
+        K |= ballot64(kill);
       }
       // (2) the tile's serial order: fixed point over the dependency masks
-      const bool cand = (meta & SWM_VALID) && !(meta & SWM_PRE) && !kill;
-      uint64_t U = ballot64(cand), M = 0;
-      while (U) {
-        const bool mu = (U >> lane) & 1ull;
-        const bool c = mu && (dep & (M | U)) == 0;
-        const bool ab = mu && (dep & M) != 0;
-        const uint64_t cm = ballot64(c), am = ballot64(ab);
-        M |= cm;
-        U &= ~(cm | am);
-      }
-      // (3) needed writes of committed txns join C
-      if (M) {
-        if ((M >> ((i0 >> 6) & 63u)) & 1ull) cb_insert_w(cbits, i0);
-        for (uint32_t q0 = 64; q0 < ni; q0 += 64) {  // long lists (uniform)
-          const uint32_t q = q0 + lane;
-          uint32_t e = SW_E_NONE;
-          if (q < ni) e = q < SW_IL ? ring[slot].ins[q] : ld_sync(ovf + SW_TA + (q - SW_IL));
-          if ((M >> ((e >> 6) & 63u)) & 1ull) cb_insert_w(cbits, e);
+      // (round 1: candidates with no earlier candidate conflict commit)
+      uint64_t U = ballot64((meta & (SWM_VALID | SWM_PRE)) == SWM_VALID) & ~K, M = 0;
+      st_u += __builtin_popcountll(U);
+      if (U) {
+        const uint64_t d = ballot64((dep & U) == 0);
+        M = U & d;
+        U &= ~d;
+        while (U) {
+          const uint64_t cm = U & ballot64((dep & (M | U)) == 0);
+          const uint64_t am = U & ballot64((dep & M) != 0);
+          M |= cm;
+          U &= ~(cm | am);
+          st_it++;
         }
       }
-      if (lane == 0) s_M[k] = M;
-      // free consumed slots four at a time (the release waits for this
-      // wave's LDS operations); tile k's slot stays held until kn is
-      // published, tile kn's until later
-      if ((kn & 3u) == 0 || kn == ntiles)
-        if (lane == 0) lds_st(&s_done, kn);
+      // tile k+2's record must be in its slot before tile k+1 reads it
+      if (kn + 1 < ntiles)
+        while (fl != kn + 2) {
+          cw++;
+          __builtin_amdgcn_s_sleep(1);
+          fl = lds_ld_rlx(&s_ready[sn + 1 == SEQ_RING ? 0u : sn + 1]);
+        }
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      // (3) needed writes of committed txns join C: a fixed number of LDS
+      // operations per tile, so the next tile's wait counts stay exact
+#pragma unroll
+      for (uint32_t c = 0; c < SW_RC; c++) cb_insert_m(cbits, ie[c], M);
+      if (hdr & SWH_ILONG) {  // long insert lists (rare)
+        const uint32_t ni = __builtin_amdgcn_readfirstlane(ring[slot].ni);
+        const uint32_t* ovf = a.lst_ovf + (uint64_t)k * SW_OVF;
+        for (uint32_t q0 = SW_RC * 64; q0 < ni; q0 += 64) {
+          const uint32_t q = q0 + lane;
+          uint32_t e = sw_idummy(lane);
+          if (q < ni) e = q < SW_IL ? ring[slot].ins[q] : ld_sync(ovf + SW_TA + (q - SW_IL));
+          cb_insert_m(cbits, e, M);
+        }
+      }
+      s_M[k] = M;  // every lane stores the same word (no exec branch)
+      // free tile k's slot: LDS executes this wave's operations in order, so
+      // a producer that sees kn has the slot's reads behind it
+      __hip_atomic_store(&s_done, kn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      slot = sn;
     }
     if (lane == 0) {
       s_k = k;
@@ -778,6 +848,8 @@ __global__ __launch_bounds__(1024) void k_sw_seq(SwSeqArgs a) {
         dbg[5] = cw;
         dbg[6] = k;
         dbg[8] = __builtin_amdgcn_s_memtime() - cyc0;
+        dbg[9] = st_u;
+        dbg[10] = st_it;
       }
     }
   }
