@@ -560,8 +560,9 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1, const SwShard* shl
                  abandon, err, nullptr};
     if (sw_debug && l < 4) sa.dbg = (uint64_t*)sw_dbg.p + (size_t)l * 1024;
     launch_sw_seq(sa, stream);
-    SwCoutArgs ca{sin, aent, apos, (const uint64_t*)sw_mg.p, lv, cbits_d, ckeys_d, bloom_d, abandon};
-    launch_sw_cout(ca, (unsigned)std::min<uint64_t>((pa.budget + 255) / 256, 4ull * n_cu), stream);
+    SwCoutArgs ca{sin,     aent,    apos,    (const uint64_t*)sw_mg.p, lv, cbits_d, ckeys_d,
+                  bloom_d, abandon, smdev, sm_host, shl ? 0 : 1};
+    launch_sw_cout(ca, (unsigned)std::min<uint64_t>((pa.budget + 1023) / 1024, 4ull * n_cu), stream);
     SwFilterArgs fa;
     fa.in = in;
     fa.m_dev = mdev;

@@ -354,6 +354,9 @@ struct SwCoutArgs {
   uint64_t* ckeys_out;
   uint32_t* bloom_out;
   const uint32_t* abandon;
+  const uint32_t* m_dev;  // list length: with skip_done, a level whose serial
+  uint32_t m_host;        // pass decided the whole list lists nothing (no
+  int skip_done;          // filter follows)
 };
 // k_sw_filter / k_sw_scan / k_sw_compact (one argument block for the three)
 struct SwFilterArgs {

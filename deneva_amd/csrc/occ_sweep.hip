@@ -886,38 +886,66 @@ __global__ __launch_bounds__(1024) void k_sw_seq(SwSeqArgs a) {
 // key (Bloom filter, key list with wave-aggregated positions: the filter
 // uses them as a set) and its key id (bitmap for the exact check).
 __global__ __launch_bounds__(256) void k_sw_cout(SwCoutArgs a) {
+  __shared__ uint32_t s_cnt[4];
+  __shared__ uint32_t s_base;
   if (*a.abandon) return;
-  const uint32_t lane = lane_id();
+  const uint32_t pos = a.lv->pos;
+  if (a.skip_done && pos >= list_len(a.m_dev, a.m_host)) return;
+  const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
   const uint64_t nnz = a.in.nnz;
   const uint32_t off0 = (uint32_t)min((uint64_t)a.in.off[0], nnz);
-  const uint32_t pos = a.lv->pos;
   const uint32_t range = (uint32_t)min((uint64_t)a.in.off[pos], nnz) - off0;
-  const uint32_t stride = gridDim.x * 256;
-  for (uint32_t x0 = blockIdx.x * 256 + (threadIdx.x & ~63u); x0 < range; x0 += stride) {
-    const uint32_t x = x0 + lane;
-    bool c = false;
-    uint32_t ent = 0;
-    if (x < range) {
-      ent = a.aent[x];
-      if (ent & 32u) {
+  // 1024 accesses per workgroup round (wave w: [256w, 256w + 256)), one
+  // fill-counter atomic per round
+  for (uint32_t x0 = blockIdx.x * 1024; x0 < range; x0 += gridDim.x * 1024) {
+    uint32_t ent[4];
+    bool c[4];
+#pragma unroll
+    for (uint32_t u = 0; u < 4; u++) {
+      const uint32_t x = x0 + wv * 256 + u * 64 + lane;
+      ent[u] = x < range ? a.aent[x] : 0u;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < 4; u++) {
+      const uint32_t x = x0 + wv * 256 + u * 64 + lane;
+      c[u] = false;
+      if (ent[u] & 32u) {
         const uint32_t p = a.apos[x];
-        c = (a.mg[p >> 6] >> (p & 63u)) & 1ull;
+        c[u] = (a.mg[p >> 6] >> (p & 63u)) & 1ull;
       }
     }
-    const uint64_t cm = ballot64(c);
-    if (!cm) continue;  // uniform
-    uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(&a.lv->ccount, (uint32_t)__popcll(cm));
-    base = __shfl(base, 0);
-    if (!c) continue;
-    const uint64_t key = a.in.keys[off0 + x];
-    a.ckeys_out[base + (uint32_t)__popcll(cm & lanemask_lt())] = key;
-    const uint32_t id = sw_aid(ent);
-    if (id < SW_ID_NONE) atomicOr(&a.cbits_out[id >> 5], 1u << (id & 31u));
-    uint32_t b1, b2;
-    bloom_bits(key, b1, b2);
-    atomicOr(&a.bloom_out[b1 >> 5], 1u << (b1 & 31));
-    atomicOr(&a.bloom_out[b2 >> 5], 1u << (b2 & 31));
+    uint64_t cm[4];
+    uint32_t wc = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < 4; u++) {
+      cm[u] = ballot64(c[u]);
+      wc += (uint32_t)__popcll(cm[u]);
+    }
+    if (lane == 0) s_cnt[wv] = wc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint32_t tot = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+      s_base = tot ? atomicAdd(&a.lv->ccount, tot) : 0u;
+    }
+    __syncthreads();
+    uint32_t base = s_base;
+    for (uint32_t w = 0; w < wv; w++) base += s_cnt[w];
+#pragma unroll
+    for (uint32_t u = 0; u < 4; u++) {
+      if (c[u]) {
+        const uint32_t x = x0 + wv * 256 + u * 64 + lane;
+        const uint64_t key = a.in.keys[off0 + x];
+        a.ckeys_out[base + (uint32_t)__popcll(cm[u] & lanemask_lt())] = key;
+        const uint32_t id = sw_aid(ent[u]);
+        if (id < SW_ID_NONE) atomicOr(&a.cbits_out[id >> 5], 1u << (id & 31u));
+        uint32_t b1, b2;
+        bloom_bits(key, b1, b2);
+        atomicOr(&a.bloom_out[b1 >> 5], 1u << (b1 & 31));
+        atomicOr(&a.bloom_out[b2 >> 5], 1u << (b2 & 31));
+      }
+      base += (uint32_t)__popcll(cm[u]);
+    }
+    __syncthreads();  // s_cnt / s_base of the next round
   }
 }
 
@@ -987,6 +1015,10 @@ __global__ __launch_bounds__(X ? F_XB : SW_CHUNK) void k_sw_filter(SwFilterArgs 
   const uint32_t pos = a.lv->pos;
   const uint32_t ccount = a.lv->ccount;
   if (X ? ccount > F_XCAP : (a.exact_launched && ccount <= F_XCAP)) return;
+  // the serial pass decided the whole list: no next level (the epoch's first
+  // level table is filled by the epoch's setup); sharded ranks still serve
+  // the merged serial range of the next level
+  if (pos >= m && !a.kill_out) return;
   // the next level's key table (its pre-pass runs after this kernel)
   for (uint64_t q = (uint64_t)blockIdx.x * B + j; q < a.gclear_n;
        q += (uint64_t)gridDim.x * B) {
