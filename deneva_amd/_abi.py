@@ -54,6 +54,15 @@ class Batch(C.Structure):
     ]
 
 
+class Snapshot(C.Structure):
+    """dcc_occ_snapshot: one captured critical-section view per txn."""
+    _fields_ = [
+        ("hist_top", C.c_void_p),
+        ("active_off", C.c_void_p),
+        ("active_idx", C.c_void_p),
+    ]
+
+
 class Stats(C.Structure):
     _fields_ = [
         ("rounds", C.c_uint32),
@@ -165,6 +174,8 @@ _SIGS = [
     ("dcc_shard_filter", C.c_int, [C.POINTER(Batch), C.c_uint32, C.c_uint32, _P, _P, _P,
                                    C.POINTER(C.c_uint64)]),
     ("dcc_occ_validate_epoch", C.c_int, [_P, C.POINTER(Batch), _P, _P, C.POINTER(Stats)]),
+    ("dcc_occ_validate_snapshot", C.c_int,
+     [_P, C.POINTER(Batch), C.POINTER(Snapshot), _P, C.POINTER(Stats)]),
     ("dcc_occ_history_append", C.c_int, [_P, _P, _P, C.c_uint64]),
     ("dcc_occ_history_clear", C.c_int, [_P]),
     ("dcc_occ_history_size", C.c_uint64, [_P]),

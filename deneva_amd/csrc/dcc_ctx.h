@@ -122,6 +122,7 @@ struct dcc_ctx {
   DevBuf perm, calvin_a, calvin_b, calvin_c, calvin_d;  // Calvin workspaces
   DevBuf cv_scratch, cv_agg, cv_group, cv_wave, cv_pgx, cv_gsx, cv_gsize, cv_done, cv_maxl;
   DevBuf cv_seq_b, cv_ok, cv_len, cv_off2, cv_tsum;
+  DevBuf snap_top, snap_aoff, snap_aidx, snap_cnt;  // captured-snapshot validation
 
   // OCC history (occ.h:62-64) and commit counter tnc (occ.h:67)
   std::vector<std::pair<uint64_t, uint64_t>> hist;
@@ -155,6 +156,7 @@ struct dcc_ctx {
   int sweep_sharded(const DevBatch& d, int& next_level);
   int occ_sweep_finish(const DevBatch& d, int& next_level, bool& done, uint32_t maxlen);
   uint64_t peel_prefix(uint64_t m, int level) const;
+  int occ_snapshot(const dcc_batch* b, const dcc_occ_snapshot* s, uint8_t* out_rc, dcc_stats* st);
   int calvin_epoch(const dcc_batch* b, uint32_t* out_group, uint8_t* out_rc, uint32_t* out_wave,
                    dcc_stats* st);
 };

@@ -200,7 +200,8 @@ std::vector<DevBuf*> dcc_ctx::all_bufs() {
                             &cv_off2, &cv_tsum, &gst, &hasw_scr, &cset_tab, &cset_keys,
                             &a_cnt, &a_writers, &a_big, &a_st32, &sw_ctl, &sw_status, &sw_dbg,
                             &sw_ckeys, &sw_gtab, &sw_rec, &sw_rk, &sw_fw, &sw_aent, &sw_mg, &sw_xcnt,
-                            &sw_xrec, &sw_mcnt, &sw_moff, &sw_mkeys, &sw_mat, &sw_kill};
+                            &sw_xrec, &sw_mcnt, &sw_moff, &sw_mkeys, &sw_mat, &sw_kill,
+                            &snap_top, &snap_aoff, &snap_aidx, &snap_cnt};
   for (auto& sb : sw_list)
     for (DevBuf* b : {&sb.tid, &sb.off, &sb.keys, &sb.acctype, &sb.state}) v.push_back(b);
   for (auto& sb : subs)

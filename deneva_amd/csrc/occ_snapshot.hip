@@ -1,0 +1,264 @@
+// Captured-snapshot OCC validation (C ABI
+// dcc_occ_validate_snapshot in include/dcc.h).
+//
+// A live concurrent run decides each txn inside central_validate
+// (concurrency_control/occ.cpp:116-239) against what its critical section saw
+// (occ.cpp:137-158): the history head and the active list.  With those two
+// captured, every txn's decision is independent of every other's, so the
+// whole capture is validated in one data-parallel pass — no fixed point:
+//
+//   abort(i) <=> [finish_tn > start_tn and some visible history entry with
+//                 start_tn < tn <= finish_tn wrote a key i READ]   (occ.cpp:167-180)
+//             or [some captured active write set meets i's keys]   (occ.cpp:185-199)
+//
+// One wave per txn (grid-stride over txns, so the per-wave statistics need
+// one atomic per wave): lane l holds access l of txn i (MAX_ROW_PER_TXN = 64
+// = one wavefront).  The history window is a binary search in the context's
+// key-sorted history CSR; for each captured active txn j the lanes load j's
+// accesses and compare j's writes against i's keys, broadcast one at a time
+// with v_readlane (i's keys stay in VGPRs; no LDS needed).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <vector>
+
+#include "dcc.h"
+#include "dcc_ctx.h"
+#include "dcc_device.h"
+#include "occ_kernels.h"
+
+using namespace dcc;
+
+namespace {
+
+constexpr int SNAP_WAVES = 4;           // waves per 256-thread workgroup
+constexpr uint32_t SNAP_ERR_LEN = 1;    // a txn longer than MAX_ROW_PER_TXN
+constexpr uint32_t SNAP_ERR_IDX = 2;    // an active index >= n_txn
+constexpr uint32_t SNAP_ERR_AOFF = 4;   // active_off decreasing
+
+struct SnapArgs {
+  uint64_t n;
+  const uint32_t* off;
+  const uint64_t* keys;
+  const uint8_t* acctype;
+  const uint64_t* start_tn;  // NULL: history window closed (TS_CLOCK)
+  const uint64_t* finish_tn;
+  const uint64_t* hist_top;  // NULL: whole history visible
+  const uint32_t* aoff;
+  const uint32_t* aidx;
+  const uint64_t* hkeys;
+  uint64_t nkeys;
+  const uint64_t* hoff;
+  const uint64_t* htn;
+  uint8_t* out_rc;
+  unsigned long long* cnt;  // [0] error bits, [1] commits, [2] read-only, [3] writes, [4] bytes
+};
+
+__device__ inline uint64_t readlane64(uint64_t v, uint32_t lane) {
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, lane);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), lane);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// first history tn of `key` that is > lo, tested against hi (history CSR:
+// hkeys unique ascending, htn[hoff[u] .. hoff[u+1]) ascending)
+__device__ inline bool hist_window_hit(const SnapArgs& a, uint64_t key, uint64_t lo, uint64_t hi) {
+  uint64_t l = 0, h = a.nkeys;
+  while (l < h) {
+    const uint64_t m = (l + h) >> 1;
+    if (a.hkeys[m] < key) l = m + 1;
+    else h = m;
+  }
+  if (l >= a.nkeys || a.hkeys[l] != key) return false;
+  uint64_t b = a.hoff[l], e = a.hoff[l + 1];
+  while (b < e) {
+    const uint64_t m = (b + e) >> 1;
+    if (a.htn[m] <= lo) b = m + 1;
+    else e = m;
+  }
+  return b < a.hoff[l + 1] && a.htn[b] <= hi;
+}
+
+__global__ __launch_bounds__(256) void k_snap(SnapArgs a) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t wave0 = (uint64_t)blockIdx.x * SNAP_WAVES + (threadIdx.x >> 6);
+  const uint64_t stride = (uint64_t)gridDim.x * SNAP_WAVES;
+  uint32_t err = 0, n_commit = 0, n_ro = 0, n_w = 0;
+  uint64_t bytes = 0;
+  for (uint64_t t = wave0; t < a.n; t += stride) {
+    const uint32_t o0 = a.off[t], o1 = a.off[t + 1];
+    uint32_t len = o1 - o0;
+    if (o1 < o0 || len > MAX_TXN_LEN) {
+      err |= SNAP_ERR_LEN;
+      len = 0;
+    }
+    const bool have = lane < len;
+    const uint64_t k = have ? a.keys[o0 + lane] : 0;
+    const bool wr = have && a.acctype[o0 + lane] == DCC_WR;
+    const uint64_t wmask = ballot64(wr);
+    bytes += 4 + 9ull * len;
+    bool hit = false;
+    // history window, read set only (occ.cpp:167-180)
+    if (a.start_tn) {
+      const uint64_t s = a.start_tn[t], f = a.finish_tn[t];
+      uint64_t hi = f;
+      if (a.hist_top) hi = min(hi, a.hist_top[t]);
+      bytes += a.hist_top ? 24 : 16;
+      if (f > s && hi > s && have && !wr) hit = hist_window_hit(a, k, s, hi);
+    }
+    bool conflict = ballot64(hit) != 0;
+    // captured active list: W_j vs R_i, then W_j vs W_i (occ.cpp:185-199)
+    const uint32_t q0 = a.aoff[t], q1 = a.aoff[t + 1];
+    if (q1 < q0) err |= SNAP_ERR_AOFF;
+    bytes += 8;
+    for (uint32_t q = q0; q < q1 && !conflict; q++) {
+      const uint32_t j = a.aidx[q];
+      bytes += 4;
+      if (j >= a.n) {
+        err |= SNAP_ERR_IDX;
+        continue;
+      }
+      const uint32_t j0 = a.off[j];
+      uint32_t jl = a.off[j + 1] - j0;
+      if (jl > MAX_TXN_LEN) jl = 0;  // reported when txn j itself is visited
+      bytes += 8 + 9ull * jl;
+      const bool jw = lane < jl && a.acctype[j0 + lane] == DCC_WR;
+      const uint64_t kj = jw ? a.keys[j0 + lane] : 0;
+      bool h = false;
+      for (uint32_t x = 0; x < len; x++) h |= jw && readlane64(k, x) == kj;
+      conflict = ballot64(h) != 0;
+    }
+    if (lane == 0) a.out_rc[t] = conflict ? DCC_RC_ABORT : DCC_RC_RCOK;
+    n_commit += conflict ? 0 : 1;
+    n_ro += wmask ? 0 : 1;
+    n_w += __popcll(wmask);
+  }
+  if (lane == 0 && wave0 < a.n) {
+    if (err) atomicOr(&a.cnt[0], (unsigned long long)err);
+    atomicAdd(&a.cnt[1], (unsigned long long)n_commit);
+    atomicAdd(&a.cnt[2], (unsigned long long)n_ro);
+    atomicAdd(&a.cnt[3], (unsigned long long)n_w);
+    atomicAdd(&a.cnt[4], (unsigned long long)bytes);
+  }
+}
+
+#define CK(expr)                                           \
+  do {                                                     \
+    hipError_t e_ = (expr);                                \
+    if (e_ != hipSuccess) return ctx->hip_fail(e_, #expr); \
+  } while (0)
+#define CR(expr)                 \
+  do {                           \
+    int r_ = (expr);             \
+    if (r_ != DCC_OK) return r_; \
+  } while (0)
+
+}  // namespace
+
+int dcc_ctx::occ_snapshot(const dcc_batch* b, const dcc_occ_snapshot* s, uint8_t* out_rc,
+                          dcc_stats* st) {
+  dcc_ctx* ctx = this;
+  const auto t_wall0 = std::chrono::steady_clock::now();
+  if (!s || !s->active_off) return fail(DCC_EINVAL, "snapshot: null snapshot or active_off");
+  if (comm_ranks() > 1) return fail(DCC_ENOTSUP, "snapshot validation is single-GPU");
+  CR(check_batch(b));
+  dcc_stats S;
+  memset(&S, 0, sizeof S);
+  S.n_shards = 1;
+  if (b->n_txn == 0) {
+    if (st) *st = S;
+    return DCC_OK;
+  }
+  if (!out_rc) return fail(DCC_EINVAL, "snapshot: null out_rc");
+  const uint64_t n = b->n_txn;
+  const bool dev = (b->flags & DCC_DEVICE_PTRS) != 0;
+  uint64_t n_active = 0;
+  if (!dev) {
+    // host capture: full structural validation before any launch
+    const uint32_t* ao = s->active_off;
+    if (ao[0] != 0) return fail(DCC_EINVAL, "snapshot: active_off[0] must be 0");
+    for (uint64_t t = 0; t < n; t++)
+      if (ao[t + 1] < ao[t])
+        return fail(DCC_EINVAL, "snapshot: active_off decreases at txn %llu", (unsigned long long)t);
+    n_active = ao[n];
+    if (n_active && !s->active_idx) return fail(DCC_EINVAL, "snapshot: null active_idx");
+    for (uint64_t q = 0; q < n_active; q++)
+      if (s->active_idx[q] >= n)
+        return fail(DCC_EINVAL, "snapshot: active_idx[%llu] = %u >= n_txn", (unsigned long long)q,
+                    s->active_idx[q]);
+  }
+  DevBatch d;
+  CR(stage_batch(b, d));
+  const uint64_t* top = s->hist_top;
+  const uint32_t* aoff = s->active_off;
+  const uint32_t* aidx = s->active_idx;
+  if (!dev) {
+    CR(snap_aoff.ensure(this, (n + 1) * 4, "snapshot active_off"));
+    CR(snap_aidx.ensure(this, std::max<uint64_t>(16, n_active * 4), "snapshot active_idx"));
+    CK(hipMemcpyAsync(snap_aoff.p, aoff, (n + 1) * 4, hipMemcpyHostToDevice, stream));
+    if (n_active)
+      CK(hipMemcpyAsync(snap_aidx.p, aidx, n_active * 4, hipMemcpyHostToDevice, stream));
+    aoff = (const uint32_t*)snap_aoff.p;
+    aidx = (const uint32_t*)snap_aidx.p;
+    if (top) {
+      CR(snap_top.ensure(this, n * 8, "snapshot hist_top"));
+      CK(hipMemcpyAsync(snap_top.p, top, n * 8, hipMemcpyHostToDevice, stream));
+      top = (const uint64_t*)snap_top.p;
+    }
+    CR(rc.ensure(this, n + 16, "rc"));
+  }
+  const bool hist_on = d.start_tn && !hist.empty();
+  if (hist_on) CR(upload_history());
+  CR(snap_cnt.ensure(this, 64, "snapshot counters"));
+  CK(hipMemsetAsync(snap_cnt.p, 0, 40, stream));
+  SnapArgs a{n,
+             d.off,
+             d.keys,
+             d.acctype,
+             hist_on ? d.start_tn : nullptr,
+             hist_on ? d.finish_tn : nullptr,
+             top,
+             aoff,
+             aidx,
+             (const uint64_t*)hkeys.p,
+             hist_on ? h_nkeys : 0,
+             (const uint64_t*)hoff.p,
+             (const uint64_t*)htn.p,
+             dev ? out_rc : (uint8_t*)rc.p,
+             (unsigned long long*)snap_cnt.p};
+  const uint64_t waves_needed = n;
+  uint64_t grid = (waves_needed + SNAP_WAVES - 1) / SNAP_WAVES;
+  grid = std::min<uint64_t>(grid, (uint64_t)n_cu * 16);
+  CK(hipEventRecord(ev0, stream));
+  k_snap<<<(unsigned)grid, 256, 0, stream>>>(a);
+  CK(hipGetLastError());
+  CK(hipEventRecord(ev1, stream));
+  unsigned long long cnt[5];
+  CK(hipMemcpyAsync(cnt, snap_cnt.p, sizeof cnt, hipMemcpyDeviceToHost, stream));
+  if (!dev) CK(hipMemcpyAsync(out_rc, rc.p, n, hipMemcpyDeviceToHost, stream));
+  CK(hipStreamSynchronize(stream));
+  if (cnt[0])
+    return fail(DCC_EINVAL, "snapshot: malformed device capture (error bits 0x%llx)", cnt[0]);
+  float ms = 0.f;
+  CK(hipEventElapsedTime(&ms, ev0, ev1));
+  S.n_commit = cnt[1];
+  S.n_abort = n - cnt[1];
+  S.n_readonly = cnt[2];
+  S.nnz_w = cnt[3];
+  S.alg_bytes = cnt[4];
+  S.device_ms = ms;
+  S.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_wall0)
+                   .count();
+  if (st) *st = S;
+  return DCC_OK;
+}
+
+extern "C" int dcc_occ_validate_snapshot(dcc_ctx* ctx, const dcc_batch* batch,
+                                         const dcc_occ_snapshot* snap, uint8_t* out_rc,
+                                         dcc_stats* out_stats) {
+  if (!ctx) return DCC_EINVAL;
+  if (hipSetDevice(ctx->device) != hipSuccess) return DCC_ENODEV;
+  return ctx->occ_snapshot(batch, snap, out_rc, out_stats);
+}

@@ -158,6 +158,35 @@ class Engine:
                                           C.byref(st)), self._h)
         return out_rc[:n], (out_tn[:n] if want_tn else None), st.as_dict()
 
+    def occ_validate_snapshot(self, batch: EpochBatch, active_off, active_idx,
+                              hist_top=None, out_rc=None):
+        """Captured-snapshot validation (dcc_occ_validate_snapshot): every txn
+        against its own captured history head and active list
+        (occ.cpp:137-158); returns (rc u8[n], stats).  Arrays live where the
+        batch lives (numpy on the host, torch on the device)."""
+        n = batch.n_txn
+        dev = batch.on_device
+        if not dev:
+            active_off = np.ascontiguousarray(active_off, np.uint32)
+            active_idx = np.ascontiguousarray(active_idx, np.uint32)
+            if hist_top is not None:
+                hist_top = np.ascontiguousarray(hist_top, np.uint64)
+        if out_rc is None:
+            if dev:
+                import torch
+                out_rc = torch.empty(max(n, 1), dtype=torch.uint8, device=batch.offsets.device)
+            else:
+                out_rc = np.empty(max(n, 1), np.uint8)
+        sn = _abi.Snapshot()
+        sn.hist_top = _ptr(hist_top)
+        sn.active_off = _ptr(active_off)
+        sn.active_idx = _ptr(active_idx) if len(active_idx) else None
+        st = _abi.Stats()
+        b = batch.to_c(0)
+        _check(lib.dcc_occ_validate_snapshot(self._h, C.byref(b), C.byref(sn), _ptr(out_rc),
+                                             C.byref(st)), self._h)
+        return out_rc[:n], st.as_dict()
+
     def history_append(self, keys: np.ndarray, tn: np.ndarray) -> None:
         keys = np.ascontiguousarray(keys, np.uint64)
         tn = np.ascontiguousarray(tn, np.uint64)

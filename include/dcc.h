@@ -188,6 +188,32 @@ uint64_t dcc_occ_history_size(const dcc_ctx* ctx);
 int dcc_occ_set_tnc(dcc_ctx* ctx, uint64_t tnc);
 uint64_t dcc_occ_get_tnc(const dcc_ctx* ctx);
 
+/* Captured-snapshot validation.  A live, genuinely
+ * concurrent run records, for every validating txn, what its critical section
+ * saw (occ.cpp:137-158): the history head and the active list.  Every txn is
+ * then validated independently and in parallel against exactly that snapshot,
+ * reproducing central_validate's decision (occ.cpp:116-239) bit for bit.
+ *   hist_top[i]   tn of the history head at i's critical section: entries with
+ *                 tn > hist_top[i] were pushed later and are invisible to i.
+ *                 NULL = the whole context history is visible.
+ *   active_off    [n_txn+1] CSR; active_idx[active_off[i] .. active_off[i+1])
+ *                 are the batch indices of the txns whose write sets were on the
+ *                 active list (finish_active, occ.cpp:146-150) when i entered.
+ * The history itself is the context's (dcc_occ_history_append).  start_tn /
+ * finish_tn of the batch open the window exactly as in central_validate
+ * (checked against the read set only, occ.cpp:167-180); the active check is
+ * against the read set, then the write set (occ.cpp:185-199).  Pointers are
+ * device memory when batch->flags has DCC_DEVICE_PTRS (then out_rc too).
+ * Nothing is committed: central_finish of a live run is the caller's.
+ * Stats: n_commit, n_abort, n_readonly, nnz_w, device_ms, total_ms, alg_bytes. */
+typedef struct dcc_occ_snapshot {
+  const uint64_t* hist_top;   /* [n_txn] or NULL */
+  const uint32_t* active_off; /* [n_txn+1] */
+  const uint32_t* active_idx; /* [active_off[n_txn]] indices < n_txn */
+} dcc_occ_snapshot;
+int dcc_occ_validate_snapshot(dcc_ctx* ctx, const dcc_batch* batch, const dcc_occ_snapshot* snap,
+                              uint8_t* out_rc, dcc_stats* out_stats);
+
 /* --------------------------------------------------------------- Calvin */
 /* Epoch lock ordering: the result equals the epoch's txns calling
  * acquire_locks (ycsb_txn.cpp:49-88) in sequence order against an empty

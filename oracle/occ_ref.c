@@ -298,3 +298,81 @@ int oracle_occ_round_status(uint64_t n, const uint32_t* off, const uint64_t* key
   kmap_free(&com);
   return 0;
 }
+
+/* Captured-snapshot validation, literal: for each txn t, central_validate
+ * (occ.cpp:116-239) against what its critical section captured
+ * (occ.cpp:137-158) — the history stack from the entry with the largest
+ * tn <= hist_top[t] downwards (his = history; NULL hist_top = whole history),
+ * and the write sets of active_idx[active_off[t] .. active_off[t+1]) as
+ * finish_active.  History pairs form one set_ent per distinct tn. */
+int oracle_occ_snapshot(uint64_t n, const uint32_t* off, const uint64_t* keys,
+                        const uint8_t* acctype, const uint64_t* start_tn,
+                        const uint64_t* finish_tn, const uint64_t* hist_top,
+                        const uint32_t* active_off, const uint32_t* active_idx, uint64_t n_hist,
+                        const uint64_t* hist_keys, const uint64_t* hist_tn, uint8_t* out_rc) {
+  /* history as an array of entries in descending tn (the stack, head first) */
+  set_ent* hv = NULL;
+  uint64_t nh = 0;
+  if (n_hist) {
+    uint64_t* idx = (uint64_t*)malloc(n_hist * sizeof(uint64_t));
+    hv = (set_ent*)calloc(n_hist, sizeof(set_ent));
+    if (!idx || !hv) return -1;
+    for (uint64_t i = 0; i < n_hist; i++) idx[i] = i;
+    for (uint64_t gap = n_hist / 2; gap; gap /= 2) /* shell sort, descending tn */
+      for (uint64_t i = gap; i < n_hist; i++) {
+        uint64_t t = idx[i], j = i;
+        while (j >= gap && hist_tn[idx[j - gap]] < hist_tn[t]) {
+          idx[j] = idx[j - gap];
+          j -= gap;
+        }
+        idx[j] = t;
+      }
+    for (uint64_t i = 0; i < n_hist;) {
+      uint64_t j = i;
+      while (j < n_hist && hist_tn[idx[j]] == hist_tn[idx[i]]) j++;
+      set_ent* e = &hv[nh++];
+      e->tn = hist_tn[idx[i]];
+      e->rows = (uint64_t*)malloc(sizeof(uint64_t) * (j - i));
+      if (!e->rows) return -1;
+      for (uint64_t q = i; q < j; q++) e->rows[e->set_size++] = hist_keys[idx[q]];
+      i = j;
+    }
+    free(idx);
+  }
+  set_ent** wsets = (set_ent**)calloc(n ? n : 1, sizeof(set_ent*));
+  set_ent** rsets = (set_ent**)calloc(n ? n : 1, sizeof(set_ent*));
+  if (!wsets || !rsets) return -1;
+  for (uint64_t t = 0; t < n; t++)
+    if (get_rw_set((int64_t)t, off, keys, acctype, &rsets[t], &wsets[t])) return -1;
+  for (uint64_t t = 0; t < n; t++) {
+    int valid = 1;
+    uint64_t h = 0; /* his = history, as seen at t's critical section */
+    if (hist_top)
+      while (h < nh && hv[h].tn > hist_top[t]) h++;
+    if (start_tn && finish_tn && finish_tn[t] > start_tn[t]) { /* occ.cpp:167-180 */
+      while (h < nh && hv[h].tn > finish_tn[t]) h++;
+      while (h < nh && hv[h].tn > start_tn[t]) {
+        valid = test_valid(&hv[h], rsets[t]);
+        if (!valid) break;
+        h++;
+      }
+    }
+    if (valid) /* occ.cpp:185-199 */
+      for (uint32_t q = active_off[t]; q < active_off[t + 1]; q++) {
+        const set_ent* wact = wsets[active_idx[q]];
+        valid = test_valid(wact, rsets[t]);
+        if (valid) valid = test_valid(wact, wsets[t]);
+        if (!valid) break;
+      }
+    out_rc[t] = valid ? RC_RCOK : RC_ABORT;
+  }
+  for (uint64_t t = 0; t < n; t++) {
+    free_ent(rsets[t]);
+    free_ent(wsets[t]);
+  }
+  free(rsets);
+  free(wsets);
+  for (uint64_t i = 0; i < nh; i++) free(hv[i].rows);
+  free(hv);
+  return 0;
+}

@@ -44,6 +44,17 @@ int oracle_occ_hash(uint64_t n, const uint32_t* off, const uint64_t* keys, const
                     const uint64_t* hist_keys, const uint64_t* hist_tn, uint64_t* tnc,
                     uint8_t* out_rc, uint64_t* out_tn);
 
+/* Captured-snapshot validation, literal (central_validate, occ.cpp:116-239,
+ * against each txn's captured critical-section view, occ.cpp:137-158):
+ * hist_top[t] = tn of the history head t saw (NULL = all visible);
+ * active_idx[active_off[t] .. active_off[t+1]) = finish_active of t.
+ * out_rc[t] = 0 (RCOK) or 2 (Abort).  Returns 0, or -1 on allocation failure. */
+int oracle_occ_snapshot(uint64_t n, const uint32_t* off, const uint64_t* keys,
+                        const uint8_t* acctype, const uint64_t* start_tn,
+                        const uint64_t* finish_tn, const uint64_t* hist_top,
+                        const uint32_t* active_off, const uint32_t* active_idx, uint64_t n_hist,
+                        const uint64_t* hist_keys, const uint64_t* hist_tn, uint8_t* out_rc);
+
 /* Round-based fixed point (the algorithm the GPU runs), one shard's view:
  * given the global per-txn state (0 undecided, 1 commit, 2 abort) at the start
  * of a round and this shard's accesses, return per-txn status bits

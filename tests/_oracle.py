@@ -26,6 +26,8 @@ def _load():
     lib.oracle_occ_replay.argtypes = [C.c_uint64, P, P, P, P, P, C.c_uint64, P, P,
                                       C.POINTER(C.c_uint64), P, P]
     lib.oracle_occ_hash.argtypes = lib.oracle_occ_replay.argtypes
+    lib.oracle_occ_snapshot.argtypes = [C.c_uint64, P, P, P, P, P, P, P, P, C.c_uint64, P, P, P]
+    lib.oracle_occ_snapshot.restype = C.c_int
     lib.oracle_occ_round_status.argtypes = [C.c_uint64, P, P, P, P, P]
     lib.oracle_calvin_replay.argtypes = [C.c_uint64, P, P, P, P, P, P, P]
     lib.oracle_calvin_formula.argtypes = lib.oracle_calvin_replay.argtypes
@@ -66,6 +68,30 @@ def occ(batch, hist_keys=None, hist_tn=None, tnc=0, literal=False):
     if r != 0:
         raise RuntimeError(f"oracle occ failed: {r}")
     return rc[:n], tn[:n], t.value
+
+
+def occ_snapshot(batch, active_off, active_idx, hist_top=None, hist_keys=None, hist_tn=None):
+    """Literal captured-snapshot validation; returns rc u8[n]."""
+    n = batch.n_txn
+    off = _arr(batch.offsets, np.uint32)
+    keys = _arr(batch.keys, np.uint64)
+    at = _arr(batch.acctype, np.uint8)
+    st = _arr(batch.start_tn, np.uint64)
+    ft = _arr(batch.finish_tn, np.uint64)
+    top = _arr(hist_top, np.uint64)
+    ao = _arr(active_off, np.uint32)
+    ai = _arr(active_idx, np.uint32)
+    if ai is not None and ai.shape[0] == 0:
+        ai = np.zeros(1, np.uint32)
+    hk = _arr(hist_keys, np.uint64)
+    ht = _arr(hist_tn, np.uint64)
+    nh = 0 if hk is None else hk.shape[0]
+    rc = np.empty(max(n, 1), np.uint8)
+    r = lib.oracle_occ_snapshot(n, _p(off), _p(keys), _p(at), _p(st), _p(ft), _p(top), _p(ao),
+                                _p(ai), nh, _p(hk), _p(ht), rc.ctypes.data)
+    if r != 0:
+        raise RuntimeError(f"oracle occ snapshot failed: {r}")
+    return rc[:n]
 
 
 def occ_round_status(batch, state):
