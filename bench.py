@@ -142,7 +142,57 @@ def secondary_configs(eng, local, steps=10, warmup=3):
                  "device_ms": st["device_ms"], "ready_at_acquire": int(st["n_commit"]),
                  "alg_GBps": st["alg_bytes"] / (st["device_ms"] * 1e-3) / 1e9,
                  "parity_vs_oracle": par}
+    out["C6"] = snapshot_config(eng, dev, timed, orc)
     return out
+
+
+def snapshot_capture(n, seed=0xD3E7A006, max_active=8, n_hist=20000):
+    """Synthetic live capture over the headline batch shape: txn i's critical
+    section saw up to `max_active` of the 64 txns before it on the active list,
+    a history head hist_top, and a TS_CAS window (start_tn, finish_tn]."""
+    import deneva_amd as d
+    rng = np.random.default_rng(seed)
+    b = d.gen_ycsb(n_txn=n, zipf_theta=0.9)
+    cnt = np.minimum(rng.integers(0, max_active + 1, size=n), np.arange(n))
+    aoff = np.zeros(n + 1, np.uint32)
+    aoff[1:] = np.cumsum(cnt)
+    t = np.repeat(np.arange(n, dtype=np.int64), cnt)
+    aidx = (t - 1 - rng.integers(0, 64, size=t.size) % np.maximum(t, 1)).astype(np.uint32)
+    st = rng.integers(0, 1200, size=n).astype(np.uint64)
+    ft = st + rng.integers(0, 8, size=n).astype(np.uint64)
+    top = rng.integers(0, 1200, size=n).astype(np.uint64)
+    hk = b.keys[rng.integers(0, b.nnz, size=n_hist)].astype(np.uint64)
+    ht = rng.integers(1, 1200, size=n_hist).astype(np.uint64)
+    return d.EpochBatch(b.offsets, b.keys, b.acctype, st, ft), aoff, aidx, top, hk, ht
+
+
+def snapshot_config(eng, dev, timed, orc, n=1 << 20, check=131072):
+    """C6: captured-snapshot validation (dcc_occ_validate_snapshot) of 1M
+    captured YCSB txns; parity on the first `check` txns (a capture prefix only
+    refers to earlier txns, so it is self-contained)."""
+    import torch
+    from deneva_amd import EpochBatch
+    b, aoff, aidx, top, hk, ht = snapshot_capture(n)
+    eng.history_clear()
+    eng.history_append(hk, ht)
+    db = b.to_torch(dev)
+    t32 = lambda a: torch.from_numpy(a.view(np.int32)).to(dev)
+    daoff, daidx = t32(aoff), t32(aidx)
+    dtop = torch.from_numpy(top.view(np.int64)).to(dev)
+    rc = torch.empty(n, dtype=torch.uint8, device=dev)
+    dt, st = timed(lambda: eng.occ_validate_snapshot(db, daoff, daidx, dtop, out_rc=rc)[1])
+    off = b.offsets[: check + 1]
+    sub = EpochBatch(off, b.keys[: off[-1]], b.acctype[: off[-1]], b.start_tn[:check],
+                     b.finish_tn[:check])
+    erc = orc.occ_snapshot(sub, aoff[: check + 1], aidx[: aoff[check]], top[:check], hk, ht)
+    eng.history_clear()
+    return {"workload": "captured-snapshot OCC, 1,048,576 YCSB txns x 16 keys (theta=0.9), "
+                        "<=8 captured active txns each, 20,000-pair history, TS_CAS windows",
+            "txns_per_s": n / dt, "ms_per_epoch": dt * 1e3, "device_ms": st["device_ms"],
+            "commits": int(st["n_commit"]), "alg_bytes": int(st["alg_bytes"]),
+            "alg_GBps": st["alg_bytes"] / (st["device_ms"] * 1e-3) / 1e9,
+            "parity_vs_oracle": bool(np.array_equal(rc[:check].cpu().numpy(), erc)),
+            "parity_sample": f"first {check} txns"}
 
 
 def main():

@@ -22,6 +22,7 @@
 #include "calvin_epoch.h"
 #include "dcc.h"
 #include "occ_epoch.h"
+#include "occ_live.h"
 
 using namespace dcc_host;
 
@@ -37,6 +38,7 @@ struct Cfg {
   int device = 0;
   int max_retries = 1000;
   bool calvin = false;
+  bool live = false;           // live OptCC run on the workers, capture replayed on the GPU
   std::string capture;
 };
 
@@ -44,7 +46,7 @@ static void usage() {
   fprintf(stderr,
           "c1_driver [--threads N] [--txns N] [--theta T] [--req N] [--table N]\n"
           "          [--epoch-max N] [--timer-ms T] [--seed S] [--device D]\n"
-          "          [--capture DIR] [--calvin]\n");
+          "          [--capture DIR] [--calvin | --live]\n");
 }
 
 static int parse(int argc, char** argv, Cfg& c) {
@@ -54,6 +56,7 @@ static int parse(int argc, char** argv, Cfg& c) {
     const char* v = nullptr;
     if (a == "--help" || a == "-h") return 1;
     if (a == "--calvin") { c.calvin = true; continue; }
+    if (a == "--live") { c.live = true; continue; }
     if (!(v = val())) return 2;
     if (a == "--threads") c.threads = atoi(v);
     else if (a == "--txns") c.txns = strtoull(v, nullptr, 0);
@@ -113,8 +116,54 @@ int main(int argc, char** argv) {
   std::atomic<uint64_t> commits{0}, restarts{0}, ready{0}, waits{0};
   uint64_t epochs = 0;
   double device_ms = 0;
+  long long live_mismatch = -1;
 
-  if (!c.calvin) {
+  if (c.live) {
+    // live, concurrent OptCC on the worker threads (occ_live.h), then the
+    // whole capture decided again by dcc_occ_validate_snapshot
+    LiveOcc occ;
+    std::vector<std::thread> ws;
+    for (int w = 0; w < c.threads; w++)
+      ws.emplace_back([&, w] {
+        std::vector<Access> acc;
+        uint64_t spin = c.seed * 2654435761ull + (uint64_t)w;
+        for (uint64_t i = 0; i < c.txns && !failed; i++) {
+          acc.clear();
+          for (uint32_t x = off[w][i]; x < off[w][i + 1]; x++) acc.push_back({keys[w][x], at[w][x]});
+          for (int attempt = 0;; attempt++) {  // WorkerThread: restart on Abort
+            const uint64_t st = occ.get_ts();
+            spin = spin * 6364136223846793005ull + 1442695040888963407ull;
+            for (volatile uint64_t z = 0; z < ((spin >> 33) & 1023); z = z + 1) {}  // execution
+            uint8_t rc = DCC_RC_ABORT;
+            const uint32_t rec = occ.validate(acc.data(), acc.size(), st, &rc);
+            if (rc == DCC_RC_RCOK) {
+              occ.finish_commit(rec);
+              commits++;
+              break;
+            }
+            restarts++;
+            if (attempt >= c.max_retries) {
+              failed = 2;
+              break;
+            }
+          }
+        }
+      });
+    for (auto& t : ws) t.join();
+    const LiveCapture cap = occ.take();
+    uint64_t bad = 0;
+    dcc_stats s{};
+    if (int e = validate_capture(ctx, cap, &bad, &s)) {
+      fprintf(stderr, "dcc_occ_validate_snapshot: %s (%s)\n", dcc_strerror(e), dcc_last_error(ctx));
+      failed = 1;
+    } else {
+      live_mismatch = (long long)bad;
+      if (bad) failed = 3;
+      if (s.n_commit != commits.load()) failed = 4;
+    }
+    epochs = 1;
+    device_ms = s.device_ms;
+  } else if (!c.calvin) {
     OccEpoch::Options o;
     o.max_txns = c.epoch_max;
     o.n_workers = c.threads;
@@ -186,11 +235,12 @@ int main(int argc, char** argv) {
   printf("{\"driver\": \"c1\", \"cc\": \"%s\", \"threads\": %d, \"txns\": %llu, "
          "\"epochs\": %llu, \"commits\": %llu, \"restarts\": %llu, \"ready\": %llu, "
          "\"waits\": %llu, \"device_ms\": %.3f, \"wall_s\": %.3f, \"txns_per_s\": %.1f, "
-         "\"failed\": %d}\n",
-         c.calvin ? "CALVIN" : "OCC", c.threads, (unsigned long long)total,
+         "\"live_mismatch\": %lld, \"failed\": %d}\n",
+         c.calvin ? "CALVIN" : (c.live ? "OCC-live" : "OCC"), c.threads, (unsigned long long)total,
          (unsigned long long)epochs, (unsigned long long)commits.load(),
          (unsigned long long)restarts.load(), (unsigned long long)ready.load(),
-         (unsigned long long)waits.load(), device_ms, wall, total / wall, failed.load());
+         (unsigned long long)waits.load(), device_ms, wall, total / wall, live_mismatch,
+         failed.load());
   dcc_destroy(ctx);
   return failed ? 1 : 0;
 }

@@ -14,9 +14,10 @@
 // One wave per txn (grid-stride over txns, so the per-wave statistics need
 // one atomic per wave): lane l holds access l of txn i (MAX_ROW_PER_TXN = 64
 // = one wavefront).  The history window is a binary search in the context's
-// key-sorted history CSR; for each captured active txn j the lanes load j's
-// accesses and compare j's writes against i's keys, broadcast one at a time
-// with v_readlane (i's keys stay in VGPRs; no LDS needed).
+// key-sorted history CSR; the captured active txns are taken four at a time
+// (one per 16-lane group), the lanes load their accesses and compare the
+// writes against i's keys, broadcast one at a time with v_readlane (i's keys
+// stay in VGPRs; no LDS needed).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -98,42 +99,57 @@ __global__ __launch_bounds__(256) void k_snap(SnapArgs a) {
     const uint64_t k = have ? a.keys[o0 + lane] : 0;
     const bool wr = have && a.acctype[o0 + lane] == DCC_WR;
     const uint64_t wmask = ballot64(wr);
-    bytes += 4 + 9ull * len;
+    if (lane == 0) bytes += 4 + 9ull * len;
     bool hit = false;
     // history window, read set only (occ.cpp:167-180)
     if (a.start_tn) {
       const uint64_t s = a.start_tn[t], f = a.finish_tn[t];
       uint64_t hi = f;
       if (a.hist_top) hi = min(hi, a.hist_top[t]);
-      bytes += a.hist_top ? 24 : 16;
+      if (lane == 0) bytes += a.hist_top ? 24 : 16;
       if (f > s && hi > s && have && !wr) hit = hist_window_hit(a, k, s, hi);
     }
     bool conflict = ballot64(hit) != 0;
-    // captured active list: W_j vs R_i, then W_j vs W_i (occ.cpp:185-199)
+    // captured active list: W_j vs R_i, then W_j vs W_i (occ.cpp:185-199).
+    // Four entries per step: 16-lane group g takes entry q0 + step + g, so
+    // the dependent loads (aidx -> off -> accesses) of four entries overlap.
     const uint32_t q0 = a.aoff[t], q1 = a.aoff[t + 1];
     if (q1 < q0) err |= SNAP_ERR_AOFF;
-    bytes += 8;
-    for (uint32_t q = q0; q < q1 && !conflict; q++) {
-      const uint32_t j = a.aidx[q];
-      bytes += 4;
-      if (j >= a.n) {
-        err |= SNAP_ERR_IDX;
-        continue;
+    if (lane == 0) bytes += 8;
+    const uint32_t g = lane >> 4, sl = lane & 15;
+    for (uint32_t qb = q0; qb < q1 && !conflict; qb += 4) {
+      const uint32_t q = qb + g;
+      uint32_t j0 = 0, jl = 0;
+      if (q < q1) {
+        const uint32_t j = a.aidx[q];
+        if (j >= a.n) {
+          err |= SNAP_ERR_IDX;
+        } else {
+          j0 = a.off[j];
+          jl = a.off[j + 1] - j0;
+          if (jl > MAX_TXN_LEN) jl = 0;  // reported when txn j itself is visited
+        }
+        if (sl == 0) bytes += 4 + 8 + 9ull * jl;
       }
-      const uint32_t j0 = a.off[j];
-      uint32_t jl = a.off[j + 1] - j0;
-      if (jl > MAX_TXN_LEN) jl = 0;  // reported when txn j itself is visited
-      bytes += 8 + 9ull * jl;
-      const bool jw = lane < jl && a.acctype[j0 + lane] == DCC_WR;
-      const uint64_t kj = jw ? a.keys[j0 + lane] : 0;
       bool h = false;
-      for (uint32_t x = 0; x < len; x++) h |= jw && readlane64(k, x) == kj;
+      for (uint32_t base = 0;; base += 16) {
+        const bool act = base + sl < jl;
+        if (ballot64(act) == 0) break;
+        const bool jw = act && a.acctype[j0 + base + sl] == DCC_WR;
+        const uint64_t kj = jw ? a.keys[j0 + base + sl] : 0;
+        for (uint32_t x = 0; x < len; x++) h |= jw && readlane64(k, x) == kj;
+      }
       conflict = ballot64(h) != 0;
     }
     if (lane == 0) a.out_rc[t] = conflict ? DCC_RC_ABORT : DCC_RC_RCOK;
     n_commit += conflict ? 0 : 1;
     n_ro += wmask ? 0 : 1;
     n_w += __popcll(wmask);
+  }
+  // error bits and byte counts are per lane now: reduce over the wave
+  for (int m = 32; m >= 1; m >>= 1) {
+    bytes += __shfl_xor(bytes, m);
+    err |= __shfl_xor(err, m);
   }
   if (lane == 0 && wave0 < a.n) {
     if (err) atomicOr(&a.cnt[0], (unsigned long long)err);

@@ -3,7 +3,9 @@ TxnManager::validate, CalvinEpoch behind the sequencer hand-off) driven by
 the C1 driver: THREAD_CNT=4 workers, YCSB 10 req/txn, theta 0.6 (BASELINE.json
 configs[0]).  Every epoch the concurrent workers formed is captured as a .dccb
 file with the engine's decisions and checked against the oracle replaying the
-same epoch in capture order."""
+same epoch in capture order.  --live runs
+OptCC itself on the workers and replays its critical-section capture on the
+GPU with dcc_occ_validate_snapshot."""
 import glob
 import json
 import os
@@ -59,3 +61,18 @@ def test_c1_calvin_handoff():
                      "--epoch-max", "512")
     assert out["failed"] == 0 and out["ready"] + out["waits"] == 4 * 1000
     assert out["epochs"] == (1000 + 127) // 128 and out["ready"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("threads,theta,table", [(4, 0.6, 65536), (16, 0.9, 65536)])
+def test_c1_live_capture_replayed_on_gpu(threads, theta, table):
+    # real worker threads run OptCC live (occ_live.h), capturing every
+    # critical section; dcc_occ_validate_snapshot must decide every captured
+    # validation exactly as the live run did
+    out = run_driver("--live", "--threads", str(threads), "--txns", "1000", "--theta", str(theta),
+                     "--req", "10", "--table", str(table))
+    assert out["failed"] == 0, out
+    assert out["live_mismatch"] == 0
+    assert out["commits"] == threads * 1000
+    if threads > 4:
+        assert out["restarts"] > 0  # the run was really concurrent
