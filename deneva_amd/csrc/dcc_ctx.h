@@ -17,6 +17,11 @@ struct SwShard;  // occ_kernels.h: one key-sharded sweep level's serial range
 
 struct dcc_ctx;
 
+// history hash slot of a key (host build and device probe must agree)
+__host__ __device__ inline uint64_t hist_hash_slot(uint64_t key, uint32_t bits) {
+  return (key * 0x9E3779B97F4A7C15ull) >> (64 - bits);
+}
+
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
@@ -119,6 +124,7 @@ struct dcc_ctx {
   SubBufs subs[PEEL_MAX_LEVEL];
   DevBuf l_tid[2], l_coff[2], l_cent[2];         // ping-pong undecided lists
   DevBuf hkeys, hoff, htn;                       // history CSR
+  DevBuf hhash;                                  // history key -> CSR row, open addressing
   DevBuf perm, calvin_a, calvin_b, calvin_c, calvin_d;  // Calvin workspaces
   DevBuf cv_scratch, cv_agg, cv_group, cv_wave, cv_pgx, cv_gsx, cv_gsize, cv_done, cv_maxl;
   DevBuf cv_seq_b, cv_ok, cv_len, cv_off2, cv_tsum;
@@ -128,6 +134,7 @@ struct dcc_ctx {
   std::vector<std::pair<uint64_t, uint64_t>> hist;
   bool hist_dirty = false;
   uint64_t h_nkeys = 0;
+  uint32_t h_hbits = 0;  // log2 of hhash slots (16 B each: key, row)
   uint64_t tnc = 0;
 
   dcc_comm_state* comm = nullptr;

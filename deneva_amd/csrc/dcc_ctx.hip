@@ -201,7 +201,7 @@ std::vector<DevBuf*> dcc_ctx::all_bufs() {
                             &a_cnt, &a_writers, &a_big, &a_st32, &sw_ctl, &sw_status, &sw_dbg,
                             &sw_ckeys, &sw_gtab, &sw_rec, &sw_rk, &sw_fw, &sw_aent, &sw_mg, &sw_xcnt,
                             &sw_xrec, &sw_mcnt, &sw_moff, &sw_mkeys, &sw_mat, &sw_kill,
-                            &snap_top, &snap_aoff, &snap_aidx, &snap_cnt};
+                            &snap_top, &snap_aoff, &snap_aidx, &snap_cnt, &hhash};
   for (auto& sb : sw_list)
     for (DevBuf* b : {&sb.tid, &sb.off, &sb.keys, &sb.acctype, &sb.state}) v.push_back(b);
   for (auto& sb : subs)
@@ -271,6 +271,20 @@ int dcc_ctx::upload_history() {
   if (!hk.empty()) CK(hipMemcpy(hkeys.p, hk.data(), hk.size() * 8, hipMemcpyHostToDevice));
   CK(hipMemcpy(hoff.p, ho.data(), ho.size() * 8, hipMemcpyHostToDevice));
   if (!ht.empty()) CK(hipMemcpy(htn.p, ht.data(), ht.size() * 8, hipMemcpyHostToDevice));
+  // key -> CSR row as an open-addressing table at <= 50% load (one probe of
+  // 16 B instead of a log2(keys)-deep binary search; snapshot validation)
+  h_hbits = 4;
+  while ((1ull << h_hbits) < 2 * hk.size()) h_hbits++;
+  std::vector<uint64_t> tab(2ull << h_hbits, DCC_KEY_RESERVED);
+  const uint64_t mask = (1ull << h_hbits) - 1;
+  for (size_t u = 0; u < hk.size(); u++) {
+    uint64_t slot = hist_hash_slot(hk[u], h_hbits);
+    while (tab[2 * slot] != DCC_KEY_RESERVED) slot = (slot + 1) & mask;
+    tab[2 * slot] = hk[u];
+    tab[2 * slot + 1] = u;
+  }
+  CR(hhash.ensure(this, tab.size() * 8, "hist hash"));
+  CK(hipMemcpy(hhash.p, tab.data(), tab.size() * 8, hipMemcpyHostToDevice));
   hist_dirty = false;
   return DCC_OK;
 }

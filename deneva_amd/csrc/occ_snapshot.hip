@@ -11,10 +11,10 @@
 //                 start_tn < tn <= finish_tn wrote a key i READ]   (occ.cpp:167-180)
 //             or [some captured active write set meets i's keys]   (occ.cpp:185-199)
 //
-// One wave per txn (grid-stride over txns, so the per-wave statistics need
-// one atomic per wave): lane l holds access l of txn i (MAX_ROW_PER_TXN = 64
-// = one wavefront).  The history window is a binary search in the context's
-// key-sorted history CSR; the captured active txns are taken four at a time
+// One wave per txn (grid-stride over txns; per-wave statistics are plain
+// stores folded by k_snap_sum, no same-address atomics): lane l holds access l of txn i (MAX_ROW_PER_TXN = 64
+// = one wavefront).  The history window is a lookup in the context's
+// history CSR, its rows found through an open-addressing key table; the captured active txns are taken four at a time
 // (one per 16-lane group), the lanes load their accesses and compare the
 // writes against i's keys, broadcast one at a time with v_readlane (i's keys
 // stay in VGPRs; no LDS needed).
@@ -49,13 +49,36 @@ struct SnapArgs {
   const uint64_t* hist_top;  // NULL: whole history visible
   const uint32_t* aoff;
   const uint32_t* aidx;
-  const uint64_t* hkeys;
+  const uint64_t* hhash;  // [2 << hbits] (key, row) slots, DCC_KEY_RESERVED = empty
+  uint32_t hbits;
   uint64_t nkeys;
   const uint64_t* hoff;
   const uint64_t* htn;
   uint8_t* out_rc;
-  unsigned long long* cnt;  // [0] error bits, [1] commits, [2] read-only, [3] writes, [4] bytes
+  unsigned long long* part;  // [waves][SNAP_NCNT] per-wave partials (plain stores, no atomics)
 };
+constexpr int SNAP_NCNT = 5;  // error bits, commits, read-only, writes, bytes
+
+// one workgroup folds the per-wave partials into cnt[SNAP_NCNT]
+__global__ __launch_bounds__(256) void k_snap_sum(const unsigned long long* part, uint32_t waves,
+                                                  unsigned long long* cnt) {
+  __shared__ unsigned long long sh[SNAP_NCNT][256];
+  unsigned long long v[SNAP_NCNT] = {0, 0, 0, 0, 0};
+  for (uint32_t w = threadIdx.x; w < waves; w += 256) {
+    v[0] |= part[(uint64_t)w * SNAP_NCNT];
+    for (int c = 1; c < SNAP_NCNT; c++) v[c] += part[(uint64_t)w * SNAP_NCNT + c];
+  }
+  for (int c = 0; c < SNAP_NCNT; c++) sh[c][threadIdx.x] = v[c];
+  __syncthreads();
+  for (int s = 128; s >= 1; s >>= 1) {
+    if (threadIdx.x < (unsigned)s) {
+      sh[0][threadIdx.x] |= sh[0][threadIdx.x + s];
+      for (int c = 1; c < SNAP_NCNT; c++) sh[c][threadIdx.x] += sh[c][threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < SNAP_NCNT) cnt[threadIdx.x] = sh[threadIdx.x][0];
+}
 
 __device__ inline uint64_t readlane64(uint64_t v, uint32_t lane) {
   const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, lane);
@@ -63,16 +86,22 @@ __device__ inline uint64_t readlane64(uint64_t v, uint32_t lane) {
   return ((uint64_t)hi << 32) | lo;
 }
 
-// first history tn of `key` that is > lo, tested against hi (history CSR:
-// hkeys unique ascending, htn[hoff[u] .. hoff[u+1]) ascending)
+// first history tn of `key` that is > lo, tested against hi (history CSR row
+// u of the key found through the open-addressing table, htn[hoff[u] ..
+// hoff[u+1]) ascending)
 __device__ inline bool hist_window_hit(const SnapArgs& a, uint64_t key, uint64_t lo, uint64_t hi) {
-  uint64_t l = 0, h = a.nkeys;
-  while (l < h) {
-    const uint64_t m = (l + h) >> 1;
-    if (a.hkeys[m] < key) l = m + 1;
-    else h = m;
+  if (a.nkeys == 0) return false;
+  const uint64_t mask = (1ull << a.hbits) - 1;
+  uint64_t slot = hist_hash_slot(key, a.hbits), l = ~0ull;
+  for (;;) {  // <= 50% load: every probe sequence ends at an empty slot
+    const uint64_t k2 = a.hhash[2 * slot];
+    if (k2 == key) {
+      l = a.hhash[2 * slot + 1];
+      break;
+    }
+    if (k2 == DCC_KEY_RESERVED) return false;
+    slot = (slot + 1) & mask;
   }
-  if (l >= a.nkeys || a.hkeys[l] != key) return false;
   uint64_t b = a.hoff[l], e = a.hoff[l + 1];
   while (b < e) {
     const uint64_t m = (b + e) >> 1;
@@ -151,12 +180,11 @@ __global__ __launch_bounds__(256) void k_snap(SnapArgs a) {
     bytes += __shfl_xor(bytes, m);
     err |= __shfl_xor(err, m);
   }
-  if (lane == 0 && wave0 < a.n) {
-    if (err) atomicOr(&a.cnt[0], (unsigned long long)err);
-    atomicAdd(&a.cnt[1], (unsigned long long)n_commit);
-    atomicAdd(&a.cnt[2], (unsigned long long)n_ro);
-    atomicAdd(&a.cnt[3], (unsigned long long)n_w);
-    atomicAdd(&a.cnt[4], (unsigned long long)bytes);
+  if (lane < SNAP_NCNT) {  // every wave of the grid writes its row
+    const unsigned long long v[SNAP_NCNT] = {err, n_commit, n_ro, n_w, bytes};
+    unsigned long long x = v[0];
+    for (int c = 1; c < SNAP_NCNT; c++) x = lane == (uint32_t)c ? v[c] : x;
+    a.part[wave0 * SNAP_NCNT + lane] = x;
   }
 }
 
@@ -227,8 +255,12 @@ int dcc_ctx::occ_snapshot(const dcc_batch* b, const dcc_occ_snapshot* s, uint8_t
   }
   const bool hist_on = d.start_tn && !hist.empty();
   if (hist_on) CR(upload_history());
-  CR(snap_cnt.ensure(this, 64, "snapshot counters"));
-  CK(hipMemsetAsync(snap_cnt.p, 0, 40, stream));
+  const uint64_t waves_needed = n;
+  uint64_t grid = (waves_needed + SNAP_WAVES - 1) / SNAP_WAVES;
+  grid = std::min<uint64_t>(grid, (uint64_t)n_cu * 16);
+  const uint32_t waves = (uint32_t)grid * SNAP_WAVES;
+  CR(snap_cnt.ensure(this, 64 + (uint64_t)waves * SNAP_NCNT * 8, "snapshot counters"));
+  unsigned long long* cnt_dev = (unsigned long long*)snap_cnt.p;
   SnapArgs a{n,
              d.off,
              d.keys,
@@ -238,21 +270,21 @@ int dcc_ctx::occ_snapshot(const dcc_batch* b, const dcc_occ_snapshot* s, uint8_t
              top,
              aoff,
              aidx,
-             (const uint64_t*)hkeys.p,
+             (const uint64_t*)hhash.p,
+             h_hbits,
              hist_on ? h_nkeys : 0,
              (const uint64_t*)hoff.p,
              (const uint64_t*)htn.p,
              dev ? out_rc : (uint8_t*)rc.p,
-             (unsigned long long*)snap_cnt.p};
-  const uint64_t waves_needed = n;
-  uint64_t grid = (waves_needed + SNAP_WAVES - 1) / SNAP_WAVES;
-  grid = std::min<uint64_t>(grid, (uint64_t)n_cu * 16);
+             cnt_dev + 8};
   CK(hipEventRecord(ev0, stream));
   k_snap<<<(unsigned)grid, 256, 0, stream>>>(a);
   CK(hipGetLastError());
+  k_snap_sum<<<1, 256, 0, stream>>>(cnt_dev + 8, waves, cnt_dev);
+  CK(hipGetLastError());
   CK(hipEventRecord(ev1, stream));
   unsigned long long cnt[5];
-  CK(hipMemcpyAsync(cnt, snap_cnt.p, sizeof cnt, hipMemcpyDeviceToHost, stream));
+  CK(hipMemcpyAsync(cnt, cnt_dev, sizeof cnt, hipMemcpyDeviceToHost, stream));
   if (!dev) CK(hipMemcpyAsync(out_rc, rc.p, n, hipMemcpyDeviceToHost, stream));
   CK(hipStreamSynchronize(stream));
   if (cnt[0])
