@@ -11,13 +11,15 @@
 //                 start_tn < tn <= finish_tn wrote a key i READ]   (occ.cpp:167-180)
 //             or [some captured active write set meets i's keys]   (occ.cpp:185-199)
 //
-// One wave per txn (grid-stride over txns; per-wave statistics are plain
-// stores folded by k_snap_sum, no same-address atomics): lane l holds access l of txn i (MAX_ROW_PER_TXN = 64
-// = one wavefront).  The history window is a lookup in the context's
-// history CSR, its rows found through an open-addressing key table; the captured active txns are taken four at a time
-// (one per 16-lane group), the lanes load their accesses and compare the
-// writes against i's keys, broadcast one at a time with v_readlane (i's keys
-// stay in VGPRs; no LDS needed).
+// Grid-stride over steps of four txns; per-wave statistics are plain stores
+// folded by k_snap_sum (no same-address atomics).  When all four txns have
+// <= 16 accesses a 16-lane group decides each (snap_grouped); otherwise the
+// wave decides them one at a time, lane l holding access l
+// (MAX_ROW_PER_TXN = 64 = one wavefront, snap_full).  The history window is
+// a lookup in the context's history CSR, its rows found through an
+// open-addressing key table.  Captured active txns: the lanes load their
+// accesses and compare the writes against i's keys, broadcast one at a time
+// (v_readlane / ds_bpermute; i's keys stay in VGPRs, no LDS needed).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -111,79 +113,174 @@ __device__ inline bool hist_window_hit(const SnapArgs& a, uint64_t key, uint64_t
   return b < a.hoff[l + 1] && a.htn[b] <= hi;
 }
 
+struct SnapCnt {  // per-lane partials, reduced over the wave at the end
+  uint32_t err = 0, n_commit = 0, n_ro = 0, n_w = 0;
+  uint64_t bytes = 0;
+};
+
+// Whole-wave path: txn t, lane l holds access l (any length <= 64).
+__device__ void snap_full(const SnapArgs& a, uint64_t t, uint32_t lane, SnapCnt& c) {
+  const uint32_t o0 = a.off[t], o1 = a.off[t + 1];
+  uint32_t len = o1 - o0;
+  if (o1 < o0 || len > MAX_TXN_LEN) {
+    c.err |= SNAP_ERR_LEN;
+    len = 0;
+  }
+  const bool have = lane < len;
+  const uint64_t k = have ? a.keys[o0 + lane] : 0;
+  const bool wr = have && a.acctype[o0 + lane] == DCC_WR;
+  const uint64_t wmask = ballot64(wr);
+  if (lane == 0) c.bytes += 4 + 9ull * len;
+  bool hit = false;
+  // history window, read set only (occ.cpp:167-180)
+  if (a.start_tn) {
+    const uint64_t s = a.start_tn[t], f = a.finish_tn[t];
+    uint64_t hi = f;
+    if (a.hist_top) hi = min(hi, a.hist_top[t]);
+    if (lane == 0) c.bytes += a.hist_top ? 24 : 16;
+    if (f > s && hi > s && have && !wr) hit = hist_window_hit(a, k, s, hi);
+  }
+  bool conflict = ballot64(hit) != 0;
+  // captured active list: W_j vs R_i, then W_j vs W_i (occ.cpp:185-199).
+  // Four entries per step: 16-lane group g takes entry q0 + step + g, so
+  // the dependent loads (aidx -> off -> accesses) of four entries overlap.
+  const uint32_t q0 = a.aoff[t], q1 = a.aoff[t + 1];
+  if (q1 < q0) c.err |= SNAP_ERR_AOFF;
+  if (lane == 0) c.bytes += 8;
+  const uint32_t g = lane >> 4, sl = lane & 15;
+  for (uint32_t qb = q0; qb < q1 && !conflict; qb += 4) {
+    const uint32_t q = qb + g;
+    uint32_t j0 = 0, jl = 0;
+    if (q < q1) {
+      const uint32_t j = a.aidx[q];
+      if (j >= a.n) {
+        c.err |= SNAP_ERR_IDX;
+      } else {
+        j0 = a.off[j];
+        jl = a.off[j + 1] - j0;
+        if (jl > MAX_TXN_LEN) jl = 0;  // reported when txn j itself is visited
+      }
+      if (sl == 0) c.bytes += 4 + 8 + 9ull * jl;
+    }
+    bool h = false;
+    for (uint32_t base = 0;; base += 16) {
+      const bool act = base + sl < jl;
+      if (ballot64(act) == 0) break;
+      const bool jw = act && a.acctype[j0 + base + sl] == DCC_WR;
+      const uint64_t kj = jw ? a.keys[j0 + base + sl] : 0;
+      for (uint32_t x = 0; x < len; x++) h |= jw && readlane64(k, x) == kj;
+    }
+    conflict = ballot64(h) != 0;
+  }
+  if (lane == 0) {
+    a.out_rc[t] = conflict ? DCC_RC_ABORT : DCC_RC_RCOK;
+    c.n_commit += conflict ? 0 : 1;
+    c.n_ro += wmask ? 0 : 1;
+    c.n_w += __popcll(wmask);
+  }
+}
+
+// Grouped path: four txns per wave, 16-lane group g owns txn tb + g and lane
+// sl of it holds access sl (every txn of the four has <= 16 accesses, e.g.
+// YCSB's REQ_PER_QUERY = 16).  Each group walks its own captured active list
+// one entry per step; i's keys are broadcast inside the group with ds_bpermute.
+__device__ void snap_grouped(const SnapArgs& a, uint64_t t, bool tv, uint32_t o0, uint32_t len,
+                             uint32_t lane, SnapCnt& c) {
+  const uint32_t g = lane >> 4, sl = lane & 15;
+  const bool have = tv && sl < len;
+  const uint64_t k = have ? a.keys[o0 + sl] : 0;
+  const bool wr = have && a.acctype[o0 + sl] == DCC_WR;
+  const uint64_t wgrp = (ballot64(wr) >> (16 * g)) & 0xFFFFull;
+  if (tv && sl == 0) c.bytes += 4 + 9ull * len;
+  bool hit = false;
+  if (tv && a.start_tn) {
+    const uint64_t s = a.start_tn[t], f = a.finish_tn[t];
+    uint64_t hi = f;
+    if (a.hist_top) hi = min(hi, a.hist_top[t]);
+    if (sl == 0) c.bytes += a.hist_top ? 24 : 16;
+    if (f > s && hi > s && have && !wr) hit = hist_window_hit(a, k, s, hi);
+  }
+  bool conflict = ((ballot64(hit) >> (16 * g)) & 0xFFFFull) != 0;
+  uint32_t q0 = 0, q1 = 0;
+  if (tv) {
+    q0 = a.aoff[t];
+    q1 = a.aoff[t + 1];
+    if (q1 < q0) {
+      c.err |= SNAP_ERR_AOFF;
+      q1 = q0;
+    }
+    if (sl == 0) c.bytes += 8;
+  }
+  for (uint32_t step = 0;; step++) {
+    const bool go = tv && !conflict && q0 + step < q1;
+    if (ballot64(go) == 0) break;
+    uint32_t j0 = 0, jl = 0;
+    if (go) {
+      const uint32_t j = a.aidx[q0 + step];
+      if (j >= a.n) {
+        c.err |= SNAP_ERR_IDX;
+      } else {
+        j0 = a.off[j];
+        jl = a.off[j + 1] - j0;
+        if (jl > MAX_TXN_LEN) jl = 0;
+      }
+      if (sl == 0) c.bytes += 4 + 8 + 9ull * jl;
+    }
+    bool h = false;
+    for (uint32_t base = 0;; base += 16) {
+      const bool act = base + sl < jl;
+      if (ballot64(act) == 0) break;
+      const bool jw = act && a.acctype[j0 + base + sl] == DCC_WR;
+      const uint64_t kj = jw ? a.keys[j0 + base + sl] : 0;
+      for (uint32_t x = 0; x < 16; x++) {
+        const uint64_t kx = __shfl(k, (int)(g * 16 + x));
+        h |= jw && x < len && kx == kj;
+      }
+    }
+    conflict = conflict || ((ballot64(h) >> (16 * g)) & 0xFFFFull) != 0;
+  }
+  if (tv && sl == 0) {
+    a.out_rc[t] = conflict ? DCC_RC_ABORT : DCC_RC_RCOK;
+    c.n_commit += conflict ? 0 : 1;
+    c.n_ro += wgrp ? 0 : 1;
+    c.n_w += __popcll(wgrp);
+  }
+}
+
 __global__ __launch_bounds__(256) void k_snap(SnapArgs a) {
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t wave0 = (uint64_t)blockIdx.x * SNAP_WAVES + (threadIdx.x >> 6);
   const uint64_t stride = (uint64_t)gridDim.x * SNAP_WAVES;
-  uint32_t err = 0, n_commit = 0, n_ro = 0, n_w = 0;
-  uint64_t bytes = 0;
-  for (uint64_t t = wave0; t < a.n; t += stride) {
-    const uint32_t o0 = a.off[t], o1 = a.off[t + 1];
-    uint32_t len = o1 - o0;
-    if (o1 < o0 || len > MAX_TXN_LEN) {
-      err |= SNAP_ERR_LEN;
-      len = 0;
+  SnapCnt c;
+  for (uint64_t tb = wave0 * 4; tb < a.n; tb += stride * 4) {
+    const uint64_t t = tb + (lane >> 4);
+    const bool tv = t < a.n;
+    uint32_t o0 = 0, len = 0;
+    if (tv) {
+      o0 = a.off[t];
+      len = a.off[t + 1] - o0;  // a decreasing offset wraps to a huge length
     }
-    const bool have = lane < len;
-    const uint64_t k = have ? a.keys[o0 + lane] : 0;
-    const bool wr = have && a.acctype[o0 + lane] == DCC_WR;
-    const uint64_t wmask = ballot64(wr);
-    if (lane == 0) bytes += 4 + 9ull * len;
-    bool hit = false;
-    // history window, read set only (occ.cpp:167-180)
-    if (a.start_tn) {
-      const uint64_t s = a.start_tn[t], f = a.finish_tn[t];
-      uint64_t hi = f;
-      if (a.hist_top) hi = min(hi, a.hist_top[t]);
-      if (lane == 0) bytes += a.hist_top ? 24 : 16;
-      if (f > s && hi > s && have && !wr) hit = hist_window_hit(a, k, s, hi);
+    if (ballot64(len > 16) == 0) {
+      snap_grouped(a, t, tv, o0, len, lane, c);
+    } else {
+      for (uint64_t u = tb; u < tb + 4 && u < a.n; u++) snap_full(a, u, lane, c);
     }
-    bool conflict = ballot64(hit) != 0;
-    // captured active list: W_j vs R_i, then W_j vs W_i (occ.cpp:185-199).
-    // Four entries per step: 16-lane group g takes entry q0 + step + g, so
-    // the dependent loads (aidx -> off -> accesses) of four entries overlap.
-    const uint32_t q0 = a.aoff[t], q1 = a.aoff[t + 1];
-    if (q1 < q0) err |= SNAP_ERR_AOFF;
-    if (lane == 0) bytes += 8;
-    const uint32_t g = lane >> 4, sl = lane & 15;
-    for (uint32_t qb = q0; qb < q1 && !conflict; qb += 4) {
-      const uint32_t q = qb + g;
-      uint32_t j0 = 0, jl = 0;
-      if (q < q1) {
-        const uint32_t j = a.aidx[q];
-        if (j >= a.n) {
-          err |= SNAP_ERR_IDX;
-        } else {
-          j0 = a.off[j];
-          jl = a.off[j + 1] - j0;
-          if (jl > MAX_TXN_LEN) jl = 0;  // reported when txn j itself is visited
-        }
-        if (sl == 0) bytes += 4 + 8 + 9ull * jl;
-      }
-      bool h = false;
-      for (uint32_t base = 0;; base += 16) {
-        const bool act = base + sl < jl;
-        if (ballot64(act) == 0) break;
-        const bool jw = act && a.acctype[j0 + base + sl] == DCC_WR;
-        const uint64_t kj = jw ? a.keys[j0 + base + sl] : 0;
-        for (uint32_t x = 0; x < len; x++) h |= jw && readlane64(k, x) == kj;
-      }
-      conflict = ballot64(h) != 0;
-    }
-    if (lane == 0) a.out_rc[t] = conflict ? DCC_RC_ABORT : DCC_RC_RCOK;
-    n_commit += conflict ? 0 : 1;
-    n_ro += wmask ? 0 : 1;
-    n_w += __popcll(wmask);
   }
-  // error bits and byte counts are per lane now: reduce over the wave
+  // per-lane partials: reduce over the wave
+  uint64_t v1 = c.n_commit, v2 = c.n_ro, v3 = c.n_w;
+  uint32_t err = c.err;
+  uint64_t bytes = c.bytes;
   for (int m = 32; m >= 1; m >>= 1) {
     bytes += __shfl_xor(bytes, m);
+    v1 += __shfl_xor(v1, m);
+    v2 += __shfl_xor(v2, m);
+    v3 += __shfl_xor(v3, m);
     err |= __shfl_xor(err, m);
   }
   if (lane < SNAP_NCNT) {  // every wave of the grid writes its row
-    const unsigned long long v[SNAP_NCNT] = {err, n_commit, n_ro, n_w, bytes};
+    const unsigned long long v[SNAP_NCNT] = {err, v1, v2, v3, bytes};
     unsigned long long x = v[0];
-    for (int c = 1; c < SNAP_NCNT; c++) x = lane == (uint32_t)c ? v[c] : x;
+    for (int q = 1; q < SNAP_NCNT; q++) x = lane == (uint32_t)q ? v[q] : x;
     a.part[wave0 * SNAP_NCNT + lane] = x;
   }
 }
@@ -255,7 +352,7 @@ int dcc_ctx::occ_snapshot(const dcc_batch* b, const dcc_occ_snapshot* s, uint8_t
   }
   const bool hist_on = d.start_tn && !hist.empty();
   if (hist_on) CR(upload_history());
-  const uint64_t waves_needed = n;
+  const uint64_t waves_needed = (n + 3) / 4;  // four txns per wave step
   uint64_t grid = (waves_needed + SNAP_WAVES - 1) / SNAP_WAVES;
   grid = std::min<uint64_t>(grid, (uint64_t)n_cu * 16);
   const uint32_t waves = (uint32_t)grid * SNAP_WAVES;
