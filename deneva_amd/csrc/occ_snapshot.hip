@@ -211,11 +211,28 @@ __device__ void snap_grouped(const SnapArgs& a, uint64_t t, bool tv, uint32_t o0
     }
     if (sl == 0) c.bytes += 8;
   }
+  // the first 16 captured entries of every group are resolved up front, one
+  // per lane (aidx -> off in parallel), so a step only loads j's accesses
+  uint32_t pj0 = 0, pjl = 0;
+  if (tv && q0 + sl < q1) {
+    const uint32_t j = a.aidx[q0 + sl];
+    if (j >= a.n) {
+      c.err |= SNAP_ERR_IDX;
+    } else {
+      pj0 = a.off[j];
+      pjl = a.off[j + 1] - pj0;
+      if (pjl > MAX_TXN_LEN) pjl = 0;
+    }
+  }
   for (uint32_t step = 0;; step++) {
     const bool go = tv && !conflict && q0 + step < q1;
     if (ballot64(go) == 0) break;
     uint32_t j0 = 0, jl = 0;
-    if (go) {
+    if (step < 16) {
+      j0 = __shfl(pj0, (int)(g * 16 + step));
+      jl = __shfl(pjl, (int)(g * 16 + step));
+      if (!go) jl = 0;
+    } else if (go) {
       const uint32_t j = a.aidx[q0 + step];
       if (j >= a.n) {
         c.err |= SNAP_ERR_IDX;
@@ -224,8 +241,8 @@ __device__ void snap_grouped(const SnapArgs& a, uint64_t t, bool tv, uint32_t o0
         jl = a.off[j + 1] - j0;
         if (jl > MAX_TXN_LEN) jl = 0;
       }
-      if (sl == 0) c.bytes += 4 + 8 + 9ull * jl;
     }
+    if (go && sl == 0) c.bytes += 4 + 8 + 9ull * jl;
     bool h = false;
     for (uint32_t base = 0;; base += 16) {
       const bool act = base + sl < jl;
