@@ -113,7 +113,7 @@ int main(int argc, char** argv) {
     }
   const auto t0 = std::chrono::steady_clock::now();
   std::atomic<int> failed{0};
-  std::atomic<uint64_t> commits{0}, restarts{0}, ready{0}, waits{0};
+  std::atomic<uint64_t> commits{0}, restarts{0}, ready{0}, waits{0}, gave_up{0};
   uint64_t epochs = 0;
   double device_ms = 0;
   long long live_mismatch = -1;
@@ -142,8 +142,8 @@ int main(int argc, char** argv) {
               break;
             }
             restarts++;
-            if (attempt >= c.max_retries) {
-              failed = 2;
+            if (attempt >= c.max_retries) {  // starved by hot writers: the live
+              gave_up++;                     // run moves on (not an engine error)
               break;
             }
           }
@@ -235,12 +235,12 @@ int main(int argc, char** argv) {
   printf("{\"driver\": \"c1\", \"cc\": \"%s\", \"threads\": %d, \"txns\": %llu, "
          "\"epochs\": %llu, \"commits\": %llu, \"restarts\": %llu, \"ready\": %llu, "
          "\"waits\": %llu, \"device_ms\": %.3f, \"wall_s\": %.3f, \"txns_per_s\": %.1f, "
-         "\"live_mismatch\": %lld, \"failed\": %d}\n",
+         "\"live_mismatch\": %lld, \"gave_up\": %llu, \"failed\": %d}\n",
          c.calvin ? "CALVIN" : (c.live ? "OCC-live" : "OCC"), c.threads, (unsigned long long)total,
          (unsigned long long)epochs, (unsigned long long)commits.load(),
          (unsigned long long)restarts.load(), (unsigned long long)ready.load(),
          (unsigned long long)waits.load(), device_ms, wall, total / wall, live_mismatch,
-         failed.load());
+         (unsigned long long)gave_up.load(), failed.load());
   dcc_destroy(ctx);
   return failed ? 1 : 0;
 }
