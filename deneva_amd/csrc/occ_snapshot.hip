@@ -62,17 +62,18 @@ struct SnapArgs {
 constexpr int SNAP_NCNT = 5;  // error bits, commits, read-only, writes, bytes
 
 // one workgroup folds the per-wave partials into cnt[SNAP_NCNT]
-__global__ __launch_bounds__(256) void k_snap_sum(const unsigned long long* part, uint32_t waves,
-                                                  unsigned long long* cnt) {
-  __shared__ unsigned long long sh[SNAP_NCNT][256];
+constexpr int SUM_THREADS = 1024;
+__global__ __launch_bounds__(SUM_THREADS) void k_snap_sum(const unsigned long long* part,
+                                                          uint32_t waves, unsigned long long* cnt) {
+  __shared__ unsigned long long sh[SNAP_NCNT][SUM_THREADS];
   unsigned long long v[SNAP_NCNT] = {0, 0, 0, 0, 0};
-  for (uint32_t w = threadIdx.x; w < waves; w += 256) {
+  for (uint32_t w = threadIdx.x; w < waves; w += SUM_THREADS) {
     v[0] |= part[(uint64_t)w * SNAP_NCNT];
     for (int c = 1; c < SNAP_NCNT; c++) v[c] += part[(uint64_t)w * SNAP_NCNT + c];
   }
   for (int c = 0; c < SNAP_NCNT; c++) sh[c][threadIdx.x] = v[c];
   __syncthreads();
-  for (int s = 128; s >= 1; s >>= 1) {
+  for (int s = SUM_THREADS / 2; s >= 1; s >>= 1) {
     if (threadIdx.x < (unsigned)s) {
       sh[0][threadIdx.x] |= sh[0][threadIdx.x + s];
       for (int c = 1; c < SNAP_NCNT; c++) sh[c][threadIdx.x] += sh[c][threadIdx.x + s];
@@ -192,15 +193,6 @@ __device__ void snap_grouped(const SnapArgs& a, uint64_t t, bool tv, uint32_t o0
   const bool wr = have && a.acctype[o0 + sl] == DCC_WR;
   const uint64_t wgrp = (ballot64(wr) >> (16 * g)) & 0xFFFFull;
   if (tv && sl == 0) c.bytes += 4 + 9ull * len;
-  bool hit = false;
-  if (tv && a.start_tn) {
-    const uint64_t s = a.start_tn[t], f = a.finish_tn[t];
-    uint64_t hi = f;
-    if (a.hist_top) hi = min(hi, a.hist_top[t]);
-    if (sl == 0) c.bytes += a.hist_top ? 24 : 16;
-    if (f > s && hi > s && have && !wr) hit = hist_window_hit(a, k, s, hi);
-  }
-  bool conflict = ((ballot64(hit) >> (16 * g)) & 0xFFFFull) != 0;
   uint32_t q0 = 0, q1 = 0;
   if (tv) {
     q0 = a.aoff[t];
@@ -211,6 +203,7 @@ __device__ void snap_grouped(const SnapArgs& a, uint64_t t, bool tv, uint32_t o0
     }
     if (sl == 0) c.bytes += 8;
   }
+  // (issued before the history lookup: the two gather chains overlap)
   // the first 16 captured entries of every group are resolved up front, one
   // per lane (aidx -> off in parallel), so a step only loads j's accesses
   uint32_t pj0 = 0, pjl = 0;
@@ -224,6 +217,15 @@ __device__ void snap_grouped(const SnapArgs& a, uint64_t t, bool tv, uint32_t o0
       if (pjl > MAX_TXN_LEN) pjl = 0;
     }
   }
+  bool hit = false;
+  if (tv && a.start_tn) {
+    const uint64_t s = a.start_tn[t], f = a.finish_tn[t];
+    uint64_t hi = f;
+    if (a.hist_top) hi = min(hi, a.hist_top[t]);
+    if (sl == 0) c.bytes += a.hist_top ? 24 : 16;
+    if (f > s && hi > s && have && !wr) hit = hist_window_hit(a, k, s, hi);
+  }
+  bool conflict = ((ballot64(hit) >> (16 * g)) & 0xFFFFull) != 0;
   for (uint32_t step = 0;; step++) {
     const bool go = tv && !conflict && q0 + step < q1;
     if (ballot64(go) == 0) break;
@@ -394,7 +396,7 @@ int dcc_ctx::occ_snapshot(const dcc_batch* b, const dcc_occ_snapshot* s, uint8_t
   CK(hipEventRecord(ev0, stream));
   k_snap<<<(unsigned)grid, 256, 0, stream>>>(a);
   CK(hipGetLastError());
-  k_snap_sum<<<1, 256, 0, stream>>>(cnt_dev + 8, waves, cnt_dev);
+  k_snap_sum<<<1, SUM_THREADS, 0, stream>>>(cnt_dev + 8, waves, cnt_dev);
   CK(hipGetLastError());
   CK(hipEventRecord(ev1, stream));
   unsigned long long cnt[5];
