@@ -19,7 +19,7 @@
 // a lookup in the context's history CSR, its rows found through an
 // open-addressing key table.  Captured active txns: the lanes load their
 // accesses and compare the writes against i's keys, broadcast one at a time
-// (v_readlane / ds_bpermute; i's keys stay in VGPRs, no LDS needed).
+// (v_readlane on the whole-wave path, an LDS row per wave on the grouped one).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -184,12 +184,20 @@ __device__ void snap_full(const SnapArgs& a, uint64_t t, uint32_t lane, SnapCnt&
 // Grouped path: four txns per wave, 16-lane group g owns txn tb + g and lane
 // sl of it holds access sl (every txn of the four has <= 16 accesses, e.g.
 // YCSB's REQ_PER_QUERY = 16).  Each group walks its own captured active list
-// one entry per step; i's keys are broadcast inside the group with ds_bpermute.
+// one entry per step; i's keys are read back from LDS as broadcast pairs.
 __device__ void snap_grouped(const SnapArgs& a, uint64_t t, bool tv, uint32_t o0, uint32_t len,
-                             uint32_t lane, SnapCnt& c) {
+                             uint32_t lane, uint64_t* sk, SnapCnt& c) {
   const uint32_t g = lane >> 4, sl = lane & 15;
   const bool have = tv && sl < len;
   const uint64_t k = have ? a.keys[o0 + sl] : 0;
+  // the group's keys in this wave's LDS row; read back as broadcast 16-B
+  // pairs (one LDS op per two keys instead of two ds_bpermute per key).
+  // LDS ops of one wave complete in order; the wave barrier keeps the
+  // compiler from moving the reads above the write.
+  __builtin_amdgcn_wave_barrier();
+  sk[lane] = k;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
   const bool wr = have && a.acctype[o0 + sl] == DCC_WR;
   const uint64_t wgrp = (ballot64(wr) >> (16 * g)) & 0xFFFFull;
   if (tv && sl == 0) c.bytes += 4 + 9ull * len;
@@ -251,9 +259,9 @@ __device__ void snap_grouped(const SnapArgs& a, uint64_t t, bool tv, uint32_t o0
       if (ballot64(act) == 0) break;
       const bool jw = act && a.acctype[j0 + base + sl] == DCC_WR;
       const uint64_t kj = jw ? a.keys[j0 + base + sl] : 0;
-      for (uint32_t x = 0; x < 16; x++) {
-        const uint64_t kx = __shfl(k, (int)(g * 16 + x));
-        h |= jw && x < len && kx == kj;
+      for (uint32_t x = 0; x < 16; x += 2) {
+        const ulonglong2 kx = *reinterpret_cast<const ulonglong2*>(&sk[g * 16 + x]);
+        h |= jw && ((x < len && kx.x == kj) || (x + 1 < len && kx.y == kj));
       }
     }
     conflict = conflict || ((ballot64(h) >> (16 * g)) & 0xFFFFull) != 0;
@@ -270,6 +278,8 @@ __global__ __launch_bounds__(256) void k_snap(SnapArgs a) {
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t wave0 = (uint64_t)blockIdx.x * SNAP_WAVES + (threadIdx.x >> 6);
   const uint64_t stride = (uint64_t)gridDim.x * SNAP_WAVES;
+  __shared__ __attribute__((aligned(16))) uint64_t skeys[SNAP_WAVES][64];
+  uint64_t* sk = skeys[threadIdx.x >> 6];
   SnapCnt c;
   for (uint64_t tb = wave0 * 4; tb < a.n; tb += stride * 4) {
     const uint64_t t = tb + (lane >> 4);
@@ -280,7 +290,7 @@ __global__ __launch_bounds__(256) void k_snap(SnapArgs a) {
       len = a.off[t + 1] - o0;  // a decreasing offset wraps to a huge length
     }
     if (ballot64(len > 16) == 0) {
-      snap_grouped(a, t, tv, o0, len, lane, c);
+      snap_grouped(a, t, tv, o0, len, lane, sk, c);
     } else {
       for (uint64_t u = tb; u < tb + 4 && u < a.n; u++) snap_full(a, u, lane, c);
     }
