@@ -234,16 +234,16 @@ __device__ void snap_grouped(const SnapArgs& a, uint64_t t, bool tv, uint32_t o0
     if (f > s && hi > s && have && !wr) hit = hist_window_hit(a, k, s, hi);
   }
   bool conflict = ((ballot64(hit) >> (16 * g)) & 0xFFFFull) != 0;
-  for (uint32_t step = 0;; step++) {
-    const bool go = tv && !conflict && q0 + step < q1;
-    if (ballot64(go) == 0) break;
-    uint32_t j0 = 0, jl = 0;
-    if (step < 16) {
-      j0 = __shfl(pj0, (int)(g * 16 + step));
-      jl = __shfl(pjl, (int)(g * 16 + step));
+  // entry e (uniform) of this group's list: from the up-front lanes when e < 16
+  auto entry = [&](uint32_t e, bool go, uint32_t& j0, uint32_t& jl) {
+    j0 = 0;
+    jl = 0;
+    if (e < 16) {
+      j0 = __shfl(pj0, (int)(g * 16 + e));
+      jl = __shfl(pjl, (int)(g * 16 + e));
       if (!go) jl = 0;
     } else if (go) {
-      const uint32_t j = a.aidx[q0 + step];
+      const uint32_t j = a.aidx[q0 + e];
       if (j >= a.n) {
         c.err |= SNAP_ERR_IDX;
       } else {
@@ -253,15 +253,29 @@ __device__ void snap_grouped(const SnapArgs& a, uint64_t t, bool tv, uint32_t o0
       }
     }
     if (go && sl == 0) c.bytes += 4 + 8 + 9ull * jl;
+  };
+  // two entries per step: both entries' accesses are in flight together
+  // (an entry checked after a conflict cannot change the decision)
+  for (uint32_t step = 0;; step += 2) {
+    const bool goa = tv && !conflict && q0 + step < q1;
+    if (ballot64(goa) == 0) break;
+    const bool gob = goa && q0 + step + 1 < q1;
+    uint32_t ja, la, jb, lb;
+    entry(step, goa, ja, la);
+    entry(step + 1, gob, jb, lb);
     bool h = false;
     for (uint32_t base = 0;; base += 16) {
-      const bool act = base + sl < jl;
-      if (ballot64(act) == 0) break;
-      const bool jw = act && a.acctype[j0 + base + sl] == DCC_WR;
-      const uint64_t kj = jw ? a.keys[j0 + base + sl] : 0;
+      const bool acta = base + sl < la, actb = base + sl < lb;
+      if (ballot64(acta || actb) == 0) break;
+      const bool jwa = acta && a.acctype[ja + base + sl] == DCC_WR;
+      const bool jwb = actb && a.acctype[jb + base + sl] == DCC_WR;
+      const uint64_t ka = jwa ? a.keys[ja + base + sl] : 0;
+      const uint64_t kb = jwb ? a.keys[jb + base + sl] : 0;
       for (uint32_t x = 0; x < 16; x += 2) {
         const ulonglong2 kx = *reinterpret_cast<const ulonglong2*>(&sk[g * 16 + x]);
-        h |= jw && ((x < len && kx.x == kj) || (x + 1 < len && kx.y == kj));
+        const bool m0 = x < len, m1 = x + 1 < len;
+        h |= jwa && ((m0 && kx.x == ka) || (m1 && kx.y == ka));
+        h |= jwb && ((m0 && kx.x == kb) || (m1 && kx.y == kb));
       }
     }
     conflict = conflict || ((ballot64(h) >> (16 * g)) & 0xFFFFull) != 0;
