@@ -37,6 +37,7 @@ using namespace dcc;
 namespace {
 
 constexpr int SNAP_WAVES = 4;           // waves per 256-thread workgroup
+constexpr int SNAP_EPS = 2;             // captured entries per step (4 measured no faster)
 constexpr uint32_t SNAP_ERR_LEN = 1;    // a txn longer than MAX_ROW_PER_TXN
 constexpr uint32_t SNAP_ERR_IDX = 2;    // an active index >= n_txn
 constexpr uint32_t SNAP_ERR_AOFF = 4;   // active_off decreasing
@@ -254,28 +255,35 @@ __device__ void snap_grouped(const SnapArgs& a, uint64_t t, bool tv, uint32_t o0
     }
     if (go && sl == 0) c.bytes += 4 + 8 + 9ull * jl;
   };
-  // two entries per step: both entries' accesses are in flight together
-  // (an entry checked after a conflict cannot change the decision)
-  for (uint32_t step = 0;; step += 2) {
-    const bool goa = tv && !conflict && q0 + step < q1;
-    if (ballot64(goa) == 0) break;
-    const bool gob = goa && q0 + step + 1 < q1;
-    uint32_t ja, la, jb, lb;
-    entry(step, goa, ja, la);
-    entry(step + 1, gob, jb, lb);
+  // SNAP_EPS entries per step: their accesses are in flight together (an
+  // entry checked after a conflict cannot change the decision)
+  for (uint32_t step = 0;; step += SNAP_EPS) {
+    const bool go0 = tv && !conflict && q0 + step < q1;
+    if (ballot64(go0) == 0) break;
+    uint32_t je[SNAP_EPS], le[SNAP_EPS];
+#pragma unroll
+    for (int e = 0; e < SNAP_EPS; e++)
+      entry(step + e, go0 && q0 + step + e < q1, je[e], le[e]);
     bool h = false;
     for (uint32_t base = 0;; base += 16) {
-      const bool acta = base + sl < la, actb = base + sl < lb;
-      if (ballot64(acta || actb) == 0) break;
-      const bool jwa = acta && a.acctype[ja + base + sl] == DCC_WR;
-      const bool jwb = actb && a.acctype[jb + base + sl] == DCC_WR;
-      const uint64_t ka = jwa ? a.keys[ja + base + sl] : 0;
-      const uint64_t kb = jwb ? a.keys[jb + base + sl] : 0;
+      bool any = false;
+#pragma unroll
+      for (int e = 0; e < SNAP_EPS; e++) any |= base + sl < le[e];
+      if (ballot64(any) == 0) break;
+      uint64_t ke[SNAP_EPS];
+      bool we[SNAP_EPS];
+#pragma unroll
+      for (int e = 0; e < SNAP_EPS; e++) {
+        const bool act = base + sl < le[e];
+        we[e] = act && a.acctype[je[e] + base + sl] == DCC_WR;
+        ke[e] = we[e] ? a.keys[je[e] + base + sl] : 0;
+      }
       for (uint32_t x = 0; x < 16; x += 2) {
         const ulonglong2 kx = *reinterpret_cast<const ulonglong2*>(&sk[g * 16 + x]);
         const bool m0 = x < len, m1 = x + 1 < len;
-        h |= jwa && ((m0 && kx.x == ka) || (m1 && kx.y == ka));
-        h |= jwb && ((m0 && kx.x == kb) || (m1 && kx.y == kb));
+#pragma unroll
+        for (int e = 0; e < SNAP_EPS; e++)
+          h |= we[e] && ((m0 && kx.x == ke[e]) || (m1 && kx.y == ke[e]));
       }
     }
     conflict = conflict || ((ballot64(h) >> (16 * g)) & 0xFFFFull) != 0;
