@@ -37,7 +37,7 @@ def parse():
     ap.add_argument("--keys", type=int, default=16)
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0xD3E7A001)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=65536,
+    ap.add_argument("--cpu-sample", type=int, default=131072,
                     help="txns of the batch timed with the CPU reference restatement")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the other BASELINE configs (C2, C3, C4, C5) at N=1")
@@ -46,31 +46,74 @@ def parse():
     ap.add_argument("--solver", type=int, default=0,
                     help="OCC solver: 0 auto (sweep on one GPU), 1 rounds, 2 asynchronous, "
                          "3 sweep")
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling: one fixed batch of --txns txns key-sharded over the "
+                         "N ranks (BASELINE config C5 with --theta 0.99 --seed 0xD3E7A002); "
+                         "default is weak scaling (N x --txns txns)")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r02", "traffic.json"),
+                    help="PMC traffic summary (tools/gpu_pmc.sh) the roofline.traffic field "
+                         "is read from; null when it holds no entry for this workload")
     ap.add_argument("--exchange", choices=["rccl", "host"], default="rccl",
                     help="N>1 status all-reduce: RCCL over xGMI (one GPU per rank), or "
                          "host/gloo (rehearsal: ranks may share one GPU)")
     return ap.parse_args()
 
 
+def _cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(batch, sample: int):
-    """Reference CPU path on a bounded sample: the literal OptCC epoch replay
-    (active-list scan, occ.cpp:116-327) restated in oracle/occ_ref.c."""
+    """The reference CPU path and its two faster restatements, timed on this
+    host, on the same batch:
+      (i)   REF-LITERAL: the literal OptCC epoch replay (active-list scan with
+            test_valid pointer compares, occ.cpp:116-327; oracle/occ_ref.c),
+            1 thread, on the first `sample` txns (O(N * commits * k^2), so
+            bounded to ~10 s of CPU work);
+      (ii)  HASH-SERIAL: serial hash-set scan, identical decisions, 1 thread,
+            whole batch;
+      (iii) ROUNDS-MT: the round-based fixed point (oracle/occ_mt.c) on every
+            host thread this process may use, whole batch.
+    `value` is (i), the reference algorithm; (ii) and (iii) are listed in
+    `variants`.  Each variant's decisions are checked against the others."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import _oracle as orc  # checker / CPU baseline only
     from deneva_amd import EpochBatch
 
+    threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or (os.cpu_count() or 1)
     n = min(sample, batch.n_txn)
     off = batch.offsets[: n + 1].copy()
     sub = EpochBatch(off, batch.keys[: off[-1]], batch.acctype[: off[-1]])
     t0 = time.perf_counter()
-    rc, _, _ = orc.occ(sub, literal=True)
-    dt = time.perf_counter() - t0
-    # cross-check the sample's decisions with the hash restatement
-    rc2, _, _ = orc.occ(sub)
-    assert np.array_equal(rc, rc2)
-    return {"value": n / dt, "unit": "txns/s", "cores": 1, "kind": "port",
-            "sample": f"first {n} txns of the bench batch, literal OptCC epoch replay "
-                      f"(oracle/occ_ref.c), {dt:.2f} s, 1 thread"}
+    rc_lit, _, _ = orc.occ(sub, literal=True)
+    t_lit = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    rc_hash, tn_hash, _ = orc.occ(batch)
+    t_hash = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    rc_mt, tn_mt, _, mt_rounds = orc.occ_rounds_mt(batch, threads)
+    t_mt = time.perf_counter() - t0
+    assert np.array_equal(rc_lit, rc_hash[:n])
+    assert np.array_equal(rc_mt, rc_hash) and np.array_equal(tn_mt, tn_hash)
+    host = {"nproc": os.cpu_count(), "cpu_model": _cpu_model(), "threads_used": threads}
+    return {"value": n / t_lit, "unit": "txns/s", "cores": 1, "kind": "port",
+            "sample": f"REF-LITERAL: first {n} txns of the bench batch, literal OptCC epoch "
+                      f"replay (oracle/occ_ref.c), {t_lit:.2f} s, 1 thread",
+            "host": host,
+            "variants": {
+                "REF-LITERAL": {"txns_per_s": n / t_lit, "txns": n, "seconds": t_lit,
+                                "threads": 1},
+                "HASH-SERIAL": {"txns_per_s": batch.n_txn / t_hash, "txns": batch.n_txn,
+                                "seconds": t_hash, "threads": 1},
+                "ROUNDS-MT": {"txns_per_s": batch.n_txn / t_mt, "txns": batch.n_txn,
+                              "seconds": t_mt, "threads": threads, "rounds": int(mt_rounds)},
+            }}
 
 
 def c4_order(b):
@@ -218,7 +261,7 @@ def main():
 
     # same batch on every rank (deterministic generator); weak scaling: the
     # epoch grows with the GPU count, each GPU holds 1/N of the accesses
-    n_total = args.txns * world
+    n_total = args.txns if args.strong else args.txns * world
     batch = d.gen_ycsb(n_txn=n_total, zipf_theta=args.theta, req_per_query=args.keys,
                        seed=args.seed)
     eng = d.Engine(local)
@@ -269,27 +312,14 @@ def main():
     eng.set_profiling(False)
     ph_ms = np.mean([p["phase_ms"] for p in prof], axis=0)
     ph_bytes = prof[-1]["phase_bytes"]
-    peeled = prof[-1]["peel_prefix"] > 0
-    swept = args.solver in (0, 3) and args.peel == -1
-    if swept:
-        # sweep solver: the level-0 filter is the one kernel that streams the
-        # whole epoch (every offset, key and access type); the serial passes
-        # and later levels run on short lists
-        dom = 1
-        dom_name = "k_sw_filter<true> (level-0 committed-key filter, exact-set instance)"
-        dom_key = "k_sw_filter"
-    elif peeled:
-        # prefix peel: k_filter is the one kernel that streams the whole epoch
-        # (every offset, key and access type); the rest runs on the prefix and
-        # the few survivors
-        dom = 1
-        dom_name = "k_filter (committed-prefix filter pass)"
-        dom_key = "k_filter"
-    else:
-        dom = int(np.argmax(ph_ms[:2]))  # dominant single kernel: build or round-1 probe
-        dom_name = ["k_build (key-hash build)", "k_round<true> (round-1 probe)"][dom]
-        dom_key = dom_name.split()[0]
-    achieved = ph_bytes[dom] / (ph_ms[dom] * 1e-3) / 1e9
+    # the one kernel that streams the whole epoch (every offset, key and access
+    # type): the level-0 committed-key filter; reported as a
+    # sub-field, the headline roofline is the whole epoch
+    filt = {"kernel": "k_sw_filter<true> (level-0 committed-key filter)",
+            "alg_bytes_per_launch": int(ph_bytes[1]), "avg_launch_ms": float(ph_ms[1]),
+            "achieved": ph_bytes[1] / (ph_ms[1] * 1e-3) / 1e9 if ph_ms[1] > 0 else None}
+    if filt["achieved"] is not None:
+        filt["frac"] = filt["achieved"] / HBM_PEAK_GBS
 
     s0 = stats[-1]
     ms_per_step = dt / args.steps * 1e3
@@ -312,14 +342,18 @@ def main():
         secondary = secondary_configs(eng, local)
 
     if rank == 0:
-        traffic = None
-        tf = os.path.join(ROOT, "profiles", "traffic.json")
-        if os.path.exists(tf):
+        # HBM traffic of one epoch (PMC FETCH_SIZE x2 + WRITE_SIZE summed over the
+        # epoch's kernels, tools/gpu_pmc.sh), read from the committed summary
+        # named by --traffic; null when it has no entry for this workload
+        traffic, traffic_src = None, None
+        if os.path.exists(args.traffic):
             try:
-                tj = json.load(open(tf))
-                key = f"{n_total}:{args.theta}:{args.keys}:{dom_key}"
-                traffic = tj.get(key)
-            except Exception:
+                tj = json.load(open(args.traffic))
+                ent = tj.get(f"{n_total}:{args.theta}:{args.keys}:{world}")
+                if ent:
+                    traffic = ent["bytes_per_epoch"]
+                    traffic_src = f"{os.path.relpath(args.traffic, ROOT)} ({ent.get('source', '')})"
+            except (OSError, ValueError, KeyError):
                 traffic = None
         line = {
             "metric": "OCC-validated txns/sec, YCSB theta=0.9",
@@ -330,7 +364,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.strong else "weak",
             "vs_baseline": None,
             "dtype": "u64",
             "data": "synthetic (deterministic YCSB generator, restated gen_requests_zipf)",
@@ -345,14 +379,17 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": dom_name,
-                "achieved": achieved,
+                "scope": "whole epoch: every kernel of dcc_occ_validate_epoch, HIP events "
+                         "around the epoch on the engine stream (SURVEY.md 8(d))",
+                "achieved": epoch_gbs,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
+                "frac": epoch_gbs / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "alg_bytes_per_launch": int(ph_bytes[dom]),
-                "avg_launch_ms": float(ph_ms[dom]),
+                "traffic_source": traffic_src,
+                "alg_bytes_per_launch": int(s0["alg_bytes"]),
+                "avg_launch_ms": dev_ms,
+                "streaming_kernel": filt,
             },
             "epoch": {
                 "device_ms": dev_ms,
@@ -363,12 +400,9 @@ def main():
                 "commits": int(s0["n_commit"]),
                 "aborts": int(s0["n_abort"]),
                 "phase_ms": [float(x) for x in ph_ms],
-                "phases": (["level-0 tile lists+serial pass+committed set",
-                            "level-0 filter kernel", "level-0 compaction+later levels",
-                            "prep+final"] if swept else
-                           ["prefix solve", "k_filter", "survivor compaction+solve",
-                            "prep+final"] if peeled else
-                           ["k_build", "round 1", "rounds>=2", "prep+final"]),
+                "phases": ["level-0 tile lists+serial pass+committed set",
+                           "level-0 filter kernel", "level-0 compaction+later levels",
+                           "prep+final"],
                 "peel_prefix": int(s0["peel_prefix"]),
                 "survivors": int(s0["n_survivors"]),
                 "parity_vs_oracle": parity,

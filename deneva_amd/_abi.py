@@ -78,6 +78,8 @@ class Stats(C.Structure):
         ("phase_bytes", C.c_uint64 * 4),
         ("peel_prefix", C.c_uint64),
         ("n_survivors", C.c_uint64),
+        ("fallback", C.c_uint32),
+        ("reserved2", C.c_uint32),
     ]
 
     def as_dict(self) -> dict:

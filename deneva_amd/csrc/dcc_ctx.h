@@ -129,6 +129,19 @@ struct dcc_ctx {
   DevBuf cv_scratch, cv_agg, cv_group, cv_wave, cv_pgx, cv_gsx, cv_gsize, cv_done, cv_maxl;
   DevBuf cv_seq_b, cv_ok, cv_len, cv_off2, cv_tsum;
   DevBuf snap_top, snap_aoff, snap_aidx, snap_cnt;  // captured-snapshot validation
+  // OCC stage solver (occ_stage.hip): per-stage control + epoch state, the
+  // ping-pong stage lists, the deciders' committed-key lists
+  DevBuf st_ctl;
+  DevBuf st_tid[2], st_ast[2], st_alen[2], st_keys[2], st_at[2], st_hdr[2], st_ck[2];
+  DevBuf st_hsh[2], st_dep[2], st_tile[2];
+  void* st_host = nullptr;      // pinned mirror of StEpoch + StCtl[] (k_stage_final)
+  void* st_host_dev = nullptr;
+  uint64_t st_tnc_dev = ~0ull;  // tnc the device StEpoch holds (~0: unknown)
+  hipGraphExec_t st_graph = nullptr;
+  GraphKey st_graph_key{};
+  uint32_t st_fallbacks = 0;    // epochs handed to the round solver (lifetime)
+  bool st_debug = false;        // DCC_ST_DEBUG: decider / filter stamps to stderr
+  DevBuf st_dbg;
 
   // OCC history (occ.h:62-64) and commit counter tnc (occ.h:67)
   std::vector<std::pair<uint64_t, uint64_t>> hist;
@@ -155,6 +168,14 @@ struct dcc_ctx {
                   uint64_t* nnz_w_prefix = nullptr);
   int read_partials(size_t bytes);
   int occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dcc_stats* st);
+  bool use_stage() const { return !force_rounds && solver == 4 && comm_ranks() <= 1; }
+  int stage_reserve(const DevBatch& d);
+  int stage_enqueue(const DevBatch& d, uint32_t l0, uint32_t l1, uint8_t* rc_dev, uint64_t* tn_dev,
+                    const uint8_t* hkill);
+  int occ_stage_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dcc_stats* st);
+  uint64_t st_tnc_upload = 0;   // host source of the tnc upload (must outlive the copy)
+  int history_append_epoch(const dcc_batch* b, const DevBatch& d, const uint64_t* tn_dev, bool dev_out,
+                           uint64_t n_cw);
   int occ_rounds(const SubProb& sp, uint32_t maxlen, bool prof, uint32_t& rounds);
   int occ_async(const SubProb& sp, uint32_t maxlen, uint32_t& passes);
   int occ_peel(const SubProb& sp, uint32_t maxlen, int level, uint32_t& rounds, PeelInfo& info);

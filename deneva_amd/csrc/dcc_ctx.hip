@@ -121,6 +121,8 @@ extern "C" int dcc_init(dcc_ctx** out, int device_id) {
   CK(hipHostMalloc((void**)&ctx->hpart, 1 << 16, hipHostMallocDefault));
   CK(hipHostGetDevicePointer(&ctx->hmisc_dev, ctx->hmisc, 0));
   CK(hipHostGetDevicePointer(&ctx->hpart_dev, ctx->hpart, 0));
+  CK(hipHostMalloc((void**)&ctx->st_host, 8192, hipHostMallocDefault));
+  CK(hipHostGetDevicePointer(&ctx->st_host_dev, ctx->st_host, 0));
   int rc = ctx->misc.ensure(ctx, 16384, "misc");
   if (!rc) rc = ctx->part.ensure(ctx, 1 << 16, "partials");
   if (rc) {
@@ -140,6 +142,8 @@ extern "C" void dcc_destroy(dcc_ctx* ctx) {
   for (DevBuf* b : ctx->all_bufs()) b->release();
   if (ctx->hmisc) (void)hipHostFree(ctx->hmisc);
   if (ctx->hpart) (void)hipHostFree(ctx->hpart);
+  if (ctx->st_host) (void)hipHostFree(ctx->st_host);
+  if (ctx->st_graph) (void)hipGraphExecDestroy(ctx->st_graph);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   for (auto& e : ctx->pev)
@@ -170,7 +174,7 @@ extern "C" int dcc_set_option(dcc_ctx* ctx, int option, int64_t value) {
       ctx->peel_min = (uint64_t)value;
       return DCC_OK;
     case DCC_OPT_SOLVER:
-      if (value < 0 || value > 3) return DCC_EINVAL;
+      if (value < 0 || value > 4) return DCC_EINVAL;
       ctx->solver = (int)value;
       return DCC_OK;
     case DCC_OPT_SWEEP_LEVELS:
@@ -204,6 +208,11 @@ std::vector<DevBuf*> dcc_ctx::all_bufs() {
                             &snap_top, &snap_aoff, &snap_aidx, &snap_cnt, &hhash};
   for (auto& sb : sw_list)
     for (DevBuf* b : {&sb.tid, &sb.off, &sb.keys, &sb.acctype, &sb.state}) v.push_back(b);
+  v.push_back(&st_ctl);
+  for (int i = 0; i < 2; i++)
+    for (DevBuf* b : {&st_tid[i], &st_ast[i], &st_alen[i], &st_keys[i], &st_at[i], &st_hdr[i], &st_ck[i],
+                      &st_hsh[i], &st_dep[i], &st_tile[i]})
+      v.push_back(b);
   for (auto& sb : subs)
     for (DevBuf* b : {&sb.tid, &sb.off, &sb.keys, &sb.acctype, &sb.state}) v.push_back(b);
   for (int i = 0; i < 2; i++) {

@@ -696,8 +696,45 @@ int dcc_ctx::sweep_sharded(const DevBatch& d, int& next_level) {
   return DCC_OK;
 }
 
+
+// central_finish (occ.cpp:283-286): committed non-read-only txns take
+// tn = tnc+1, tnc+2, ... in index order; their write sets join the history.
+int dcc_ctx::history_append_epoch(const dcc_batch* b, const DevBatch& d, const uint64_t* tn_dev,
+                                  bool dev_out, uint64_t n_cw) {
+  dcc_ctx* ctx = this;
+  std::vector<uint64_t> htn_host(d.n);
+  CK(hipMemcpy(htn_host.data(), tn_dev, d.n * 8, hipMemcpyDeviceToHost));
+  std::vector<uint32_t> ho;
+  std::vector<uint64_t> hk;
+  std::vector<uint8_t> ha;
+  const uint32_t* o = b->offsets;
+  const uint64_t* kk = b->keys;
+  const uint8_t* at = b->acctype;
+  if (dev_out) {
+    ho.resize(d.n + 1);
+    hk.resize(d.nnz);
+    ha.resize(d.nnz);
+    CK(hipMemcpy(ho.data(), d.off, (d.n + 1) * 4, hipMemcpyDeviceToHost));
+    if (d.nnz) {
+      CK(hipMemcpy(hk.data(), d.keys, d.nnz * 8, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(ha.data(), d.acctype, d.nnz, hipMemcpyDeviceToHost));
+    }
+    o = ho.data();
+    kk = hk.data();
+    at = ha.data();
+  }
+  for (uint64_t t = 0; t < d.n; t++) {
+    if (!htn_host[t]) continue;
+    for (uint32_t x = o[t]; x < o[t + 1]; x++)
+      if (at[x] == DCC_WR) hist.emplace_back(kk[x], htn_host[t]);
+  }
+  if (n_cw) hist_dirty = true;
+  return DCC_OK;
+}
+
 int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dcc_stats* st) {
   dcc_ctx* ctx = this;
+  if (use_stage()) return occ_stage_epoch(b, out_rc, out_tn, st);
   // key-sharded across ranks: this rank holds only its keys
   const bool sh = comm_ranks() > 1;
   const auto t_wall0 = std::chrono::steady_clock::now();
@@ -1095,37 +1132,7 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
     S.phase_bytes[1] = 4 * (d.n + 1) + 9 * d.nnz + 16 * d.nnz + d.n;
   }
 
-  // central_finish (occ.cpp:283-286): committed non-read-only txns take
-  // tn = tnc+1, tnc+2, ... in index order; their write sets join the history.
-  if (b->flags & DCC_OCC_APPEND_HISTORY) {
-    std::vector<uint64_t> htn_host(d.n);
-    CK(hipMemcpy(htn_host.data(), tn_dev, d.n * 8, hipMemcpyDeviceToHost));
-    std::vector<uint32_t> ho;
-    std::vector<uint64_t> hk;
-    std::vector<uint8_t> ha;
-    const uint32_t* o = b->offsets;
-    const uint64_t* kk = b->keys;
-    const uint8_t* at = b->acctype;
-    if (dev_out) {
-      ho.resize(d.n + 1);
-      hk.resize(d.nnz);
-      ha.resize(d.nnz);
-      CK(hipMemcpy(ho.data(), d.off, (d.n + 1) * 4, hipMemcpyDeviceToHost));
-      if (d.nnz) {
-        CK(hipMemcpy(hk.data(), d.keys, d.nnz * 8, hipMemcpyDeviceToHost));
-        CK(hipMemcpy(ha.data(), d.acctype, d.nnz, hipMemcpyDeviceToHost));
-      }
-      o = ho.data();
-      kk = hk.data();
-      at = ha.data();
-    }
-    for (uint64_t t = 0; t < d.n; t++) {
-      if (!htn_host[t]) continue;
-      for (uint32_t x = o[t]; x < o[t + 1]; x++)
-        if (at[x] == DCC_WR) hist.emplace_back(kk[x], htn_host[t]);
-    }
-    if (n_cw) hist_dirty = true;
-  }
+  if (b->flags & DCC_OCC_APPEND_HISTORY) CR(history_append_epoch(b, d, tn_dev, dev_out, n_cw));
   tnc += n_cw;
   const auto t_wall1 = std::chrono::steady_clock::now();
   S.total_ms = std::chrono::duration<double, std::milli>(t_wall1 - t_wall0).count();

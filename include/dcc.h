@@ -113,6 +113,9 @@ typedef struct dcc_stats {
    * filter.  The sweep reports its levels in `rounds`. */
   uint64_t peel_prefix;
   uint64_t n_survivors;
+  uint32_t fallback;     /* 1: the stage solver handed this epoch to the round solver
+                            (its lists stopped shrinking); the decisions are the same */
+  uint32_t reserved2;
 } dcc_stats;
 
 /* ------------------------------------------------------------- context  */

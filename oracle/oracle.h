@@ -44,6 +44,14 @@ int oracle_occ_hash(uint64_t n, const uint32_t* off, const uint64_t* keys, const
                     const uint64_t* hist_keys, const uint64_t* hist_tn, uint64_t* tnc,
                     uint8_t* out_rc, uint64_t* out_tn);
 
+/* ROUNDS-MT (occ_mt.c): the round-based fixed point on `nthreads` host
+ * threads, the parallel CPU baseline of SURVEY.md §8(d).  Same decisions as
+ * oracle_occ_hash without a history window; out_tn / *tnc as there.
+ * *out_rounds = rounds executed.  Returns 0, -1 on allocation failure. */
+int oracle_occ_rounds_mt(uint64_t n, const uint32_t* off, const uint64_t* keys,
+                         const uint8_t* acctype, int nthreads, uint64_t* tnc, uint8_t* out_rc,
+                         uint64_t* out_tn, uint32_t* out_rounds);
+
 /* Captured-snapshot validation, literal (central_validate, occ.cpp:116-239,
  * against each txn's captured critical-section view, occ.cpp:137-158):
  * hist_top[t] = tn of the history head t saw (NULL = all visible);

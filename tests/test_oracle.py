@@ -111,6 +111,21 @@ def test_round_status_fixed_point_equals_serial():
         assert np.array_equal(np.where(state == 1, 0, 2), rc)
 
 
+@pytest.mark.parametrize("threads", [1, 3, 8])
+def test_rounds_mt_equals_serial(threads):
+    """ROUNDS-MT (the multi-core CPU baseline of SURVEY.md §8(d)) decides
+    exactly like the serial scan, tn numbering included."""
+    rng = np.random.default_rng(8)
+    for b in (d.gen_ycsb(n_txn=20000, zipf_theta=0.9, table_size=1 << 16),
+              d.gen_ycsb(n_txn=5000, zipf_theta=0.99),
+              random_batch(rng, 1500, 16, 300, types=(RD, WR, XP, SCAN)), chain_batch(40),
+              make_batch([])):
+        rc, tn, tnc = orc.occ(b, tnc=5)
+        rc2, tn2, tnc2, rounds = orc.occ_rounds_mt(b, threads, tnc=5)
+        assert np.array_equal(rc, rc2) and np.array_equal(tn, tn2) and tnc == tnc2
+        assert rounds <= b.n_txn + 1
+
+
 # ---------------------------------------------------------------- Calvin
 def calvin_both(b):
     g1, r1, w1 = orc.calvin(b, literal=True)

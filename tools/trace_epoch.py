@@ -1,7 +1,11 @@
 #!/usr/bin/env python3
 """Print the kernel timeline of one OCC epoch from a rocprofv3 kernel trace
-(csv): every dispatch between two k_prep launches, with its duration and the
-idle gap before it.  Usage: trace_epoch.py <kernel_trace.csv> [epoch_index]"""
+(csv): every dispatch of the epoch, with its duration and the idle gap before
+it.  An epoch ends with the k_stage_final dispatch (stage solver) or starts
+with k_prep (older solvers).
+
+    trace_epoch.py <kernel_trace.csv> [epoch_index]   (default: the second to last)
+"""
 import csv
 import sys
 
@@ -9,9 +13,14 @@ import sys
 def main():
     rows = list(csv.DictReader(open(sys.argv[1])))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    starts = [i for i, r in enumerate(rows) if "k_prep" in r["Kernel_Name"]]
-    e = int(sys.argv[2]) if len(sys.argv) > 2 else len(starts) - 2
-    a, b = starts[e], (starts[e + 1] if e + 1 < len(starts) else len(rows))
+    ends = [i for i, r in enumerate(rows) if "k_stage_final" in r["Kernel_Name"]]
+    if ends:
+        bounds = [(ends[i - 1] + 1 if i else 0, ends[i] + 1) for i in range(len(ends))]
+    else:
+        starts = [i for i, r in enumerate(rows) if "k_prep" in r["Kernel_Name"]]
+        bounds = [(s, starts[i + 1] if i + 1 < len(starts) else len(rows)) for i, s in enumerate(starts)]
+    e = int(sys.argv[2]) if len(sys.argv) > 2 else max(0, len(bounds) - 2)
+    a, b = bounds[e]
     t0 = int(rows[a]["Start_Timestamp"])
     prev_end = t0
     busy = 0
