@@ -41,11 +41,8 @@ def parse():
                     help="txns of the batch timed with the CPU reference restatement")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the other BASELINE configs (C2, C3, C4, C5) at N=1")
-    ap.add_argument("--peel", type=int, default=-1,
-                    help="OCC prefix peel: -1 auto (default), 0 off, >0 prefix length")
     ap.add_argument("--solver", type=int, default=0,
-                    help="OCC solver: 0 auto (sweep on one GPU), 1 rounds, 2 asynchronous, "
-                         "3 sweep")
+                    help="OCC solver: 0 auto (sweep), 1 fixed-point rounds only, 3 sweep")
     ap.add_argument("--strong", action="store_true",
                     help="strong scaling: one fixed batch of --txns txns key-sharded over the "
                          "N ranks (BASELINE config C5 with --theta 0.99 --seed 0xD3E7A002); "
@@ -265,7 +262,6 @@ def main():
     batch = d.gen_ycsb(n_txn=n_total, zipf_theta=args.theta, req_per_query=args.keys,
                        seed=args.seed)
     eng = d.Engine(local)
-    eng.set_option(d._abi.OPT_PEEL, args.peel)
     eng.set_option(d._abi.OPT_SOLVER, args.solver)
     if world > 1:
         if args.exchange == "rccl":

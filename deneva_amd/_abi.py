@@ -33,10 +33,9 @@ UNIQUE_ID_BYTES = 128
 EXCHANGE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint8), C.c_uint64)
 OPT_RECHECK = 1
 OPT_BATCH_MAX = 2
-OPT_PEEL = 3
-OPT_PEEL_MIN = 4
 OPT_SOLVER = 5
 OPT_SWEEP_LEVELS = 6
+OPT_HIST_MERGE = 7
 
 
 class Batch(C.Structure):
@@ -61,6 +60,10 @@ class Snapshot(C.Structure):
         ("active_off", C.c_void_p),
         ("active_idx", C.c_void_p),
     ]
+
+
+class CalvinHeld(C.Structure):
+    _fields_ = [("n", C.c_uint64), ("keys", C.c_void_p), ("acctype", C.c_void_p)]
 
 
 class Stats(C.Structure):
@@ -181,9 +184,13 @@ _SIGS = [
     ("dcc_occ_history_append", C.c_int, [_P, _P, _P, C.c_uint64]),
     ("dcc_occ_history_clear", C.c_int, [_P]),
     ("dcc_occ_history_size", C.c_uint64, [_P]),
+    ("dcc_occ_history_trim", C.c_int, [_P, C.c_uint64]),
+    ("dcc_occ_history_export", C.c_int, [_P, _P, _P, C.c_uint64, _P]),
     ("dcc_occ_set_tnc", C.c_int, [_P, C.c_uint64]),
     ("dcc_occ_get_tnc", C.c_uint64, [_P]),
     ("dcc_calvin_order_epoch", C.c_int, [_P, C.POINTER(Batch), _P, _P, _P, C.POINTER(Stats)]),
+    ("dcc_calvin_order_epoch_held", C.c_int,
+     [_P, C.POINTER(Batch), C.POINTER(CalvinHeld), _P, _P, _P, C.POINTER(Stats)]),
     ("dcc_ycsb_params_default", None, [C.POINTER(YcsbParams)]),
     ("dcc_gen_ycsb", C.c_int, [C.POINTER(YcsbParams), _P, _P, _P, _P]),
     ("dcc_tpcc_params_default", None, [C.POINTER(TpccParams)]),

@@ -72,6 +72,7 @@ struct CvPart {
 __global__ __launch_bounds__(256) void k_cv_prep(const uint64_t* __restrict__ keys, uint64_t nnz,
                                                  const uint8_t* __restrict__ at,
                                                  const uint64_t* __restrict__ order, uint64_t n,
+                                                 const uint64_t* __restrict__ hkeys, uint64_t nh,
                                                  CvPart* __restrict__ part) {
   __shared__ uint64_t s[4][4];
   __shared__ uint32_t s_ex[4];
@@ -85,6 +86,11 @@ __global__ __launch_bounds__(256) void k_cv_prep(const uint64_t* __restrict__ ke
     kand &= k;
     const uint8_t a = at[x];
     nex += (a != DCC_RD && a != DCC_SCAN) ? 1u : 0u;
+  }
+  for (uint64_t x = tid; x < nh; x += stride) {  // rows of the held prefix
+    const uint64_t k = hkeys[x];
+    kor |= k;
+    kand &= k;
   }
   if (order)
     for (uint64_t t = tid; t < n; t += stride) {
@@ -192,17 +198,34 @@ __global__ __launch_bounds__(256) void k_cv_layout(const uint32_t* __restrict__ 
                                                    const uint32_t* __restrict__ off2, uint64_t n,
                                                    const uint64_t* __restrict__ keys,
                                                    const uint8_t* __restrict__ at, KeyPack kp,
-                                                   K* __restrict__ ak, uint32_t* __restrict__ av) {
+                                                   uint32_t base, K* __restrict__ ak,
+                                                   uint32_t* __restrict__ av) {
   const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= n) return;
   const uint32_t t = seq ? seq[q] : (uint32_t)q;
   const uint32_t s = off[t], e = off[t + 1];
-  const uint32_t d = off2 ? off2[q] : s;
+  const uint32_t d = base + (off2 ? off2[q] : s);
   for (uint32_t j = 0; j < e - s; j++) {
     const uint8_t a = at[s + j];
     ak[d + j] = (K)keypack_apply(kp, keys[s + j]);
     av[d + j] = (t << 7) | (j << 1) | ((a != DCC_RD && a != DCC_SCAN) ? 1u : 0u);
   }
+}
+
+// The held prefix (rows still locked when the epoch starts, row_lock.cpp:
+// 219-372: owners first, then waiters, per row in FIFO order) ahead of the
+// epoch's requests: request i is pseudo-txn n + i, so it is never a duplicate
+// and has no output slot.
+template <typename K>
+__global__ __launch_bounds__(256) void k_cv_layout_held(const uint64_t* __restrict__ hkeys,
+                                                        const uint8_t* __restrict__ hat, uint64_t nh,
+                                                        uint32_t n, KeyPack kp, K* __restrict__ ak,
+                                                        uint32_t* __restrict__ av) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nh) return;
+  const uint8_t a = hat[i];
+  ak[i] = (K)keypack_apply(kp, hkeys[i]);
+  av[i] = ((n + (uint32_t)i) << 7) | ((a != DCC_RD && a != DCC_SCAN) ? 1u : 0u);
 }
 
 // ---------------------------------------------------------------- group scan
@@ -260,6 +283,7 @@ __device__ inline Gs gs_element(uint64_t p, K key, uint32_t val, K pkey, uint32_
 
 struct ScanOut {
   const uint32_t* off;
+  uint32_t n;       // epoch txns: values with txn >= n are the held prefix (no outputs)
   uint32_t* group;  // [nnz] or null
   uint8_t* rc;      // [n]
   uint32_t* pgx;    // [nnz] previous group start per request (waves) or null
@@ -383,6 +407,7 @@ __global__ __launch_bounds__(256) void k_cv_down(const K* __restrict__ sk,
     pk = k[i];
     pv = v[i];
     const uint32_t t = v[i] >> 7, j = (v[i] >> 1) & 63u;
+    if (t >= o.n) continue;  // held-prefix request: part of the scan only (no waves)
     const uint32_t x = o.off[t] + j;
     if (dup) {
       if (o.group) o.group[x] = DCC_GROUP_NONE;
@@ -503,8 +528,9 @@ inline unsigned grid1(uint64_t n, unsigned b) {
 template <typename K>
 static int calvin_sort_and_scan(dcc_ctx* ctx, const DevBatch& d, const uint32_t* seq,
                                 const uint32_t* off2, const KeyPack& kp, const ScanOut& so,
+                                const uint64_t* hkeys, const uint8_t* hat, uint64_t nh,
                                 bool prof) {
-  const uint64_t m = d.nnz;
+  const uint64_t m = nh + d.nnz;
   hipStream_t st = ctx->stream;
   CR(ctx->calvin_a.ensure(ctx, std::max<uint64_t>(16, m * sizeof(K)), "calvin keys a"));
   CR(ctx->calvin_b.ensure(ctx, std::max<uint64_t>(16, m * sizeof(K)), "calvin keys b"));
@@ -515,8 +541,11 @@ static int calvin_sort_and_scan(dcc_ctx* ctx, const DevBatch& d, const uint32_t*
   CR(ctx->cv_agg.ensure(ctx, std::max<uint64_t>(1, tiles) * sizeof(Gs), "calvin scan"));
   K* kb[2] = {(K*)ctx->calvin_a.p, (K*)ctx->calvin_b.p};
   uint32_t* vb[2] = {(uint32_t*)ctx->calvin_c.p, (uint32_t*)ctx->calvin_d.p};
+  if (nh)
+    k_cv_layout_held<K><<<grid1(nh, 256), 256, 0, st>>>(hkeys, hat, nh, (uint32_t)d.n, kp, kb[0],
+                                                         vb[0]);
   k_cv_layout<K><<<grid1(d.n, 256), 256, 0, st>>>(d.off, seq, off2, d.n, d.keys, d.acctype, kp,
-                                                  kb[0], vb[0]);
+                                                  (uint32_t)nh, kb[0], vb[0]);
   if (prof) CK(hipEventRecord(ctx->pev[1], st));
   int cur;
   if (sizeof(K) == 4)
@@ -532,8 +561,8 @@ static int calvin_sort_and_scan(dcc_ctx* ctx, const DevBatch& d, const uint32_t*
   return DCC_OK;
 }
 
-int dcc_ctx::calvin_epoch(const dcc_batch* b, uint32_t* out_group, uint8_t* out_rc,
-                          uint32_t* out_wave, dcc_stats* st) {
+int dcc_ctx::calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint32_t* out_group,
+                          uint8_t* out_rc, uint32_t* out_wave, dcc_stats* st) {
   dcc_ctx* ctx = this;
   const auto t_wall0 = std::chrono::steady_clock::now();
   CR(check_batch(b));
@@ -547,18 +576,40 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, uint32_t* out_group, uint8_t* out_
   }
   if (out_wave && comm_ranks() > 1)
     return fail(DCC_ENOTSUP, "calvin: wave levels need the whole epoch on one GPU");
-  if (b->n_txn >= CV_MAX_TXN)
-    return fail(DCC_ERANGE, "calvin: n_txn %llu exceeds %u per epoch",
-                (unsigned long long)b->n_txn, CV_MAX_TXN - 1);
+  const uint64_t nh = held ? held->n : 0;
+  if (nh && (!held->keys || !held->acctype)) return fail(DCC_EINVAL, "calvin: null held arrays");
+  if (nh && out_wave)
+    return fail(DCC_ENOTSUP, "calvin: wave levels need an empty lock table (no held prefix)");
+  if (b->n_txn + nh >= CV_MAX_TXN)
+    return fail(DCC_ERANGE, "calvin: n_txn + held %llu exceeds %u per epoch",
+                (unsigned long long)(b->n_txn + nh), CV_MAX_TXN - 1);
+  if (b->nnz + nh >= 0xFFFFFFFFull) return fail(DCC_ERANGE, "calvin: requests exceed 2^32-1");
   DevBatch d;
   CR(stage_batch(b, d));
+  // the held prefix: device arrays alongside a device batch, else uploaded
+  const uint64_t* hkeys = nullptr;
+  const uint8_t* hat = nullptr;
+  if (nh) {
+    if (dev_out) {
+      hkeys = held->keys;
+      hat = held->acctype;
+    } else {
+      CR(cv_hkeys.ensure(this, nh * 8, "calvin held keys"));
+      CR(cv_hat.ensure(this, nh, "calvin held types"));
+      CK(hipMemcpyAsync(cv_hkeys.p, held->keys, nh * 8, hipMemcpyHostToDevice, stream));
+      CK(hipMemcpyAsync(cv_hat.p, held->acctype, nh, hipMemcpyHostToDevice, stream));
+      hkeys = (const uint64_t*)cv_hkeys.p;
+      hat = (const uint8_t*)cv_hat.p;
+    }
+  }
   CK(hipEventRecord(ev0, stream));
   if (profiling) CK(hipEventRecord(pev[0], stream));
 
   // ---- prep: offsets/length validation + which key / order bits vary
   launch_prep(d.off, d.n, d.acctype, d.nnz, 0, (PrepPart*)part.p, stream);
   CvPart* cvp = (CvPart*)((char*)part.p + 16384);
-  k_cv_prep<<<CV_PREP_BLOCKS, 256, 0, stream>>>(d.keys, d.nnz, d.acctype, d.order, d.n, cvp);
+  k_cv_prep<<<CV_PREP_BLOCKS, 256, 0, stream>>>(d.keys, d.nnz, d.acctype, d.order, d.n, hkeys, nh,
+                                                cvp);
   CK(hipGetLastError());
   CK(hipMemcpyAsync(hpart, part.p, 16384 + CV_PREP_BLOCKS * sizeof(CvPart), hipMemcpyDeviceToHost,
                     stream));
@@ -584,7 +635,7 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, uint32_t* out_group, uint8_t* out_
   if (maxlen > MAX_TXN_LEN)
     return fail(DCC_ERANGE, "batch: a txn has %u accesses (> MAX_ROW_PER_TXN=%u)", maxlen,
                 MAX_TXN_LEN);
-  const KeyPack kp = make_keypack(d.nnz ? (kor ^ kand) : 0);
+  const KeyPack kp = make_keypack(d.nnz + nh ? (kor ^ kand) : 0);
 
   // ---- outputs / workspaces
   CR(rc.ensure(this, d.n + 16, "rc"));
@@ -601,7 +652,7 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, uint32_t* out_group, uint8_t* out_
   }
   const bool waves = out_wave != nullptr;
   uint32_t* wave_dev = nullptr;
-  ScanOut so{d.off, grp_dev, rc_dev, nullptr, nullptr, nullptr};
+  ScanOut so{d.off, (uint32_t)d.n, grp_dev, rc_dev, nullptr, nullptr, nullptr};
   if (waves) {
     if (dev_out) {
       wave_dev = out_wave;
@@ -633,7 +684,7 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, uint32_t* out_group, uint8_t* out_
     CR(perm.ensure(this, d.n * 4 + 16, "calvin seq a"));
     CR(cv_seq_b.ensure(this, d.n * 4 + 16, "calvin seq b"));
     CR(cv_ok.ensure(this, d.n * 8 * 2 + 32, "calvin order keys"));
-    CR(cv_scratch.ensure(this, rs_scratch_words(std::max<uint64_t>(d.n, d.nnz)) * 4 + 64,
+    CR(cv_scratch.ensure(this, rs_scratch_words(std::max<uint64_t>(d.n, d.nnz + nh)) * 4 + 64,
                          "radix scratch"));
     uint32_t* vb[2] = {(uint32_t*)perm.p, (uint32_t*)cv_seq_b.p};
     int cur;
@@ -663,8 +714,10 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, uint32_t* out_group, uint8_t* out_
 
   // ---- requests in sequence order -> sorted by row -> group scan
   if (d.nnz) {
-    if (kp.bits <= 32) CR(calvin_sort_and_scan<uint32_t>(this, d, seq, off2, kp, so, profiling));
-    else CR(calvin_sort_and_scan<uint64_t>(this, d, seq, off2, kp, so, profiling));
+    if (kp.bits <= 32)
+      CR(calvin_sort_and_scan<uint32_t>(this, d, seq, off2, kp, so, hkeys, hat, nh, profiling));
+    else
+      CR(calvin_sort_and_scan<uint64_t>(this, d, seq, off2, kp, so, hkeys, hat, nh, profiling));
   } else if (profiling) {
     CK(hipEventRecord(pev[1], stream));
     CK(hipEventRecord(pev[2], stream));
@@ -740,5 +793,13 @@ extern "C" int dcc_calvin_order_epoch(dcc_ctx* ctx, const dcc_batch* batch, uint
                                       uint8_t* out_rc, uint32_t* out_wave, dcc_stats* st) {
   if (!ctx) return DCC_EINVAL;
   if (hipSetDevice(ctx->device) != hipSuccess) return DCC_ENODEV;
-  return ctx->calvin_epoch(batch, out_group, out_rc, out_wave, st);
+  return ctx->calvin_epoch(batch, nullptr, out_group, out_rc, out_wave, st);
+}
+
+extern "C" int dcc_calvin_order_epoch_held(dcc_ctx* ctx, const dcc_batch* batch,
+                                           const dcc_calvin_held* held, uint32_t* out_group,
+                                           uint8_t* out_rc, uint32_t* out_wave, dcc_stats* st) {
+  if (!ctx) return DCC_EINVAL;
+  if (hipSetDevice(ctx->device) != hipSuccess) return DCC_ENODEV;
+  return ctx->calvin_epoch(batch, held, out_group, out_rc, out_wave, st);
 }

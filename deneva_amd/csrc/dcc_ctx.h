@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "dcc.h"
+#include "occ_history.h"
 
 namespace dcc {
 struct SwShard;  // occ_kernels.h: one key-sharded sweep level's serial range
@@ -17,10 +18,6 @@ struct SwShard;  // occ_kernels.h: one key-sharded sweep level's serial range
 
 struct dcc_ctx;
 
-// history hash slot of a key (host build and device probe must agree)
-__host__ __device__ inline uint64_t hist_hash_slot(uint64_t key, uint32_t bits) {
-  return (key * 0x9E3779B97F4A7C15ull) >> (64 - bits);
-}
 
 struct DevBuf {
   void* p = nullptr;
@@ -42,6 +39,20 @@ struct DevBatch {
 
 struct dcc_comm_state;  // RCCL communicator (dcc_comm.hip)
 
+// One level of the device OCC history (occ_history.h): flat (key, tn) pairs in
+// append order and, once built, the pairs sorted by (key, tn) with the key
+// table.
+struct HistStore {
+  DevBuf fk, ft;            // flat pairs
+  DevBuf skey, stn, hash;   // built level
+  uint64_t m = 0;           // pairs
+  uint32_t hbits = 0;
+  bool built = true;        // the built level matches the flat pairs
+  bool mono = true;         // append order is tn order within every key
+  uint64_t max_tn = 0;      // largest tn appended
+  uint64_t min_tn = ~0ull;  // smallest tn appended
+};
+
 // One OCC (sub-)batch: txn i has accesses [off[i], off[i+1]) of keys/acctype
 // and the state byte state[i]; nnz bounds off[n], w_bound its write count.
 struct SubProb {
@@ -60,7 +71,6 @@ struct PeelInfo {
 struct SubBufs {
   DevBuf tid, off, keys, acctype, state;
 };
-constexpr int PEEL_MAX_LEVEL = 3;
 
 struct dcc_ctx {
   int device = 0;
@@ -71,16 +81,8 @@ struct dcc_ctx {
   bool profiling = false;
   uint64_t recheck_max = 16384;   // fold the kill wave into rounds with lists <= this
   uint32_t batch_max = 8;       // rounds enqueued between host synchronisations
-  int64_t peel_mode = -1;       // -1 auto prefix, 0 off, > 0 fixed prefix length
-  uint64_t peel_min = 32768;    // auto: peel (sub-)batches of at least this many txns
-  int solver = 0;               // 0 auto (sweep when unsharded), 1 rounds, 2 async, 3 sweep
-  bool force_rounds = false;    // retry after an async-solver limit
-  uint32_t* async_passes_dev = nullptr;
-  uint64_t prefix_w_top = 0;    // write accesses in the top-level peel prefix
-  bool use_async() const { return !force_rounds && solver != 1 && comm_ranks() <= 1; }
-  bool use_sweep() const {
-    return !force_rounds && (solver == 3 || (solver == 0 && peel_mode == -1));
-  }
+  int solver = 0;               // 0 auto (sweep), 1 fixed-point rounds, 3 sweep
+  bool use_sweep() const { return solver != 1; }
   uint32_t sw_levels = 4;
   bool sw_debug = false;        // DCC_SW_DEBUG: per-tile clock stamps of the serial pass       // sweep levels enqueued between host synchronisations
   hipEvent_t pev[8] = {};  // phase boundary events (profiling only)
@@ -115,39 +117,21 @@ struct dcc_ctx {
   DevBuf state, hasw, rc, stat;                  // per-txn bytes
   DevBuf cflag, bsum, tn;                        // commit-tn scan
   DevBuf gst;                                    // sharded per-txn status
-  DevBuf hasw_scr, cset_tab, cset_keys;          // prefix peel
-  DevBuf a_cnt, a_writers, a_big, a_st32;        // async solver
+  DevBuf hasw_scr;                               // round-solver hand-off
   DevBuf sw_ctl, sw_status, sw_ckeys, sw_dbg;            // sweep solver: level control, look-back, C
   DevBuf sw_rec, sw_rk, sw_gtab, sw_fw, sw_aent, sw_mg;
   DevBuf sw_xcnt, sw_xrec, sw_mcnt, sw_moff, sw_mkeys, sw_mat, sw_kill;  // key-sharded sweep  // sweep tile records
   SubBufs sw_list[2];                            // sweep level lists (ping-pong)
-  SubBufs subs[PEEL_MAX_LEVEL];
   DevBuf l_tid[2], l_coff[2], l_cent[2];         // ping-pong undecided lists
-  DevBuf hkeys, hoff, htn;                       // history CSR
-  DevBuf hhash;                                  // history key -> CSR row, open addressing
+  // OCC history (occ.h:62-64) on the device: base + delta levels
+  HistStore hs[2];
+  uint64_t hist_merge_min = 65536;  // DCC_OPT_HIST_MERGE
+  DevBuf h_K[2], h_V[2], h_scr, h_bsum;          // level-build sort buffers, append scan
   DevBuf perm, calvin_a, calvin_b, calvin_c, calvin_d;  // Calvin workspaces
   DevBuf cv_scratch, cv_agg, cv_group, cv_wave, cv_pgx, cv_gsx, cv_gsize, cv_done, cv_maxl;
-  DevBuf cv_seq_b, cv_ok, cv_len, cv_off2, cv_tsum;
+  DevBuf cv_seq_b, cv_ok, cv_len, cv_off2, cv_tsum, cv_hkeys, cv_hat;
   DevBuf snap_top, snap_aoff, snap_aidx, snap_cnt;  // captured-snapshot validation
-  // OCC stage solver (occ_stage.hip): per-stage control + epoch state, the
-  // ping-pong stage lists, the deciders' committed-key lists
-  DevBuf st_ctl;
-  DevBuf st_tid[2], st_ast[2], st_alen[2], st_keys[2], st_at[2], st_hdr[2], st_ck[2];
-  DevBuf st_hsh[2], st_dep[2], st_tile[2];
-  void* st_host = nullptr;      // pinned mirror of StEpoch + StCtl[] (k_stage_final)
-  void* st_host_dev = nullptr;
-  uint64_t st_tnc_dev = ~0ull;  // tnc the device StEpoch holds (~0: unknown)
-  hipGraphExec_t st_graph = nullptr;
-  GraphKey st_graph_key{};
-  uint32_t st_fallbacks = 0;    // epochs handed to the round solver (lifetime)
-  bool st_debug = false;        // DCC_ST_DEBUG: decider / filter stamps to stderr
-  DevBuf st_dbg;
-
-  // OCC history (occ.h:62-64) and commit counter tnc (occ.h:67)
-  std::vector<std::pair<uint64_t, uint64_t>> hist;
-  bool hist_dirty = false;
-  uint64_t h_nkeys = 0;
-  uint32_t h_hbits = 0;  // log2 of hhash slots (16 B each: key, row)
+  // commit counter tnc (occ.h:67)
   uint64_t tnc = 0;
 
   dcc_comm_state* comm = nullptr;
@@ -161,30 +145,26 @@ struct dcc_ctx {
   int reserve_occ(uint64_t n, uint64_t nnz, uint64_t nnz_w, uint32_t tw);
   void list_geometry(uint64_t n, uint32_t tw, uint64_t& seg_ts, uint64_t& seg_es) const;
   static uint64_t table_capacity(uint64_t nnz_w);
-  int upload_history();
+  // device history (occ_history.h / dcc_ctx.hip)
+  uint64_t hist_size() const { return hs[0].m + hs[1].m; }
+  int hist_grow_flat(HistStore& h, uint64_t need);
+  void hist_note(HistStore& h, uint64_t lo_tn, uint64_t hi_tn);
+  int hist_build(HistStore& h);
+  int hist_prepare();  // merge policy + rebuild: call before a window check
+  dcc::HistView hist_view() const;
+  int hist_append_epoch(const DevBatch& d, const uint64_t* tn_dev, uint64_t nnz_w, uint64_t n_cw);
   int check_batch(const dcc_batch* b);
   int stage_batch(const dcc_batch* b, DevBatch& d);
   int device_prep(const DevBatch& d, uint32_t& maxlen, uint64_t& nnz_w, uint64_t p = 0,
                   uint64_t* nnz_w_prefix = nullptr);
   int read_partials(size_t bytes);
   int occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dcc_stats* st);
-  bool use_stage() const { return !force_rounds && solver == 4 && comm_ranks() <= 1; }
-  int stage_reserve(const DevBatch& d);
-  int stage_enqueue(const DevBatch& d, uint32_t l0, uint32_t l1, uint8_t* rc_dev, uint64_t* tn_dev,
-                    const uint8_t* hkill);
-  int occ_stage_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dcc_stats* st);
-  uint64_t st_tnc_upload = 0;   // host source of the tnc upload (must outlive the copy)
-  int history_append_epoch(const dcc_batch* b, const DevBatch& d, const uint64_t* tn_dev, bool dev_out,
-                           uint64_t n_cw);
   int occ_rounds(const SubProb& sp, uint32_t maxlen, bool prof, uint32_t& rounds);
-  int occ_async(const SubProb& sp, uint32_t maxlen, uint32_t& passes);
-  int occ_peel(const SubProb& sp, uint32_t maxlen, int level, uint32_t& rounds, PeelInfo& info);
   int sweep_reserve(const DevBatch& d);
   int sweep_enqueue(const DevBatch& d, int l0, int l1, const dcc::SwShard* shard = nullptr);
   int sweep_sharded(const DevBatch& d, int& next_level);
   int occ_sweep_finish(const DevBatch& d, int& next_level, bool& done, uint32_t maxlen);
-  uint64_t peel_prefix(uint64_t m, int level) const;
   int occ_snapshot(const dcc_batch* b, const dcc_occ_snapshot* s, uint8_t* out_rc, dcc_stats* st);
-  int calvin_epoch(const dcc_batch* b, uint32_t* out_group, uint8_t* out_rc, uint32_t* out_wave,
-                   dcc_stats* st);
+  int calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint32_t* out_group,
+                   uint8_t* out_rc, uint32_t* out_wave, dcc_stats* st);
 };

@@ -12,6 +12,7 @@
 
 #include "dcc.h"
 #include "dcc_ctx.h"
+#include "radix_sort.h"
 #include "dcc_device.h"
 #include "occ_kernels.h"
 
@@ -121,8 +122,6 @@ extern "C" int dcc_init(dcc_ctx** out, int device_id) {
   CK(hipHostMalloc((void**)&ctx->hpart, 1 << 16, hipHostMallocDefault));
   CK(hipHostGetDevicePointer(&ctx->hmisc_dev, ctx->hmisc, 0));
   CK(hipHostGetDevicePointer(&ctx->hpart_dev, ctx->hpart, 0));
-  CK(hipHostMalloc((void**)&ctx->st_host, 8192, hipHostMallocDefault));
-  CK(hipHostGetDevicePointer(&ctx->st_host_dev, ctx->st_host, 0));
   int rc = ctx->misc.ensure(ctx, 16384, "misc");
   if (!rc) rc = ctx->part.ensure(ctx, 1 << 16, "partials");
   if (rc) {
@@ -142,8 +141,6 @@ extern "C" void dcc_destroy(dcc_ctx* ctx) {
   for (DevBuf* b : ctx->all_bufs()) b->release();
   if (ctx->hmisc) (void)hipHostFree(ctx->hmisc);
   if (ctx->hpart) (void)hipHostFree(ctx->hpart);
-  if (ctx->st_host) (void)hipHostFree(ctx->st_host);
-  if (ctx->st_graph) (void)hipGraphExecDestroy(ctx->st_graph);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   for (auto& e : ctx->pev)
@@ -165,21 +162,17 @@ extern "C" int dcc_set_option(dcc_ctx* ctx, int option, int64_t value) {
       if (value < 0) return DCC_EINVAL;
       ctx->recheck_max = (uint64_t)value;
       return DCC_OK;
-    case DCC_OPT_PEEL:
-      if (value < -1) return DCC_EINVAL;
-      ctx->peel_mode = value;
-      return DCC_OK;
-    case DCC_OPT_PEEL_MIN:
-      if (value < 2) return DCC_EINVAL;
-      ctx->peel_min = (uint64_t)value;
-      return DCC_OK;
     case DCC_OPT_SOLVER:
-      if (value < 0 || value > 4) return DCC_EINVAL;
+      if (value != 0 && value != 1 && value != 3) return DCC_EINVAL;
       ctx->solver = (int)value;
       return DCC_OK;
     case DCC_OPT_SWEEP_LEVELS:
       if (value < 1 || value > SW_MAX_LEVEL) return DCC_EINVAL;
       ctx->sw_levels = (uint32_t)value;
+      return DCC_OK;
+    case DCC_OPT_HIST_MERGE:
+      if (value < 1) return DCC_EINVAL;
+      ctx->hist_merge_min = (uint64_t)value;
       return DCC_OK;
     case DCC_OPT_BATCH_MAX:
       if (value < 1 || value > 32) return DCC_EINVAL;
@@ -197,23 +190,18 @@ extern "C" int dcc_set_stream(dcc_ctx* ctx, void* s) {
 
 std::vector<DevBuf*> dcc_ctx::all_bufs() {
   std::vector<DevBuf*> v = {&misc, &part, &off, &keys, &acctype, &start_tn, &finish_tn, &table, &state,
-                            &hasw, &cflag, &bsum, &tn, &rc, &hkeys, &hoff, &htn, &stat,
+                            &hasw, &cflag, &bsum, &tn, &rc, &stat,
                             &order, &perm, &calvin_a, &calvin_b, &calvin_c, &calvin_d,
                             &cv_scratch, &cv_agg, &cv_group, &cv_wave, &cv_pgx, &cv_gsx,
                             &cv_gsize, &cv_done, &cv_maxl, &cv_seq_b, &cv_ok, &cv_len,
-                            &cv_off2, &cv_tsum, &gst, &hasw_scr, &cset_tab, &cset_keys,
-                            &a_cnt, &a_writers, &a_big, &a_st32, &sw_ctl, &sw_status, &sw_dbg,
+                            &cv_off2, &cv_tsum, &cv_hkeys, &cv_hat, &gst, &hasw_scr, &sw_ctl, &sw_status, &sw_dbg,
                             &sw_ckeys, &sw_gtab, &sw_rec, &sw_rk, &sw_fw, &sw_aent, &sw_mg, &sw_xcnt,
                             &sw_xrec, &sw_mcnt, &sw_moff, &sw_mkeys, &sw_mat, &sw_kill,
-                            &snap_top, &snap_aoff, &snap_aidx, &snap_cnt, &hhash};
+                            &snap_top, &snap_aoff, &snap_aidx, &snap_cnt,
+                            &h_K[0], &h_K[1], &h_V[0], &h_V[1], &h_scr, &h_bsum};
+  for (auto& h : hs)
+    for (DevBuf* b : {&h.fk, &h.ft, &h.skey, &h.stn, &h.hash}) v.push_back(b);
   for (auto& sb : sw_list)
-    for (DevBuf* b : {&sb.tid, &sb.off, &sb.keys, &sb.acctype, &sb.state}) v.push_back(b);
-  v.push_back(&st_ctl);
-  for (int i = 0; i < 2; i++)
-    for (DevBuf* b : {&st_tid[i], &st_ast[i], &st_alen[i], &st_keys[i], &st_at[i], &st_hdr[i], &st_ck[i],
-                      &st_hsh[i], &st_dep[i], &st_tile[i]})
-      v.push_back(b);
-  for (auto& sb : subs)
     for (DevBuf* b : {&sb.tid, &sb.off, &sb.keys, &sb.acctype, &sb.state}) v.push_back(b);
   for (int i = 0; i < 2; i++) {
     v.push_back(&l_tid[i]);
@@ -235,68 +223,226 @@ extern "C" int dcc_reserve(dcc_ctx* ctx, uint64_t max_txn, uint64_t max_nnz) {
 }
 
 // ---------------------------------------------------------------- history
+// The history lives on the device (occ_history.h): host appends are uploaded
+// into the delta level's flat pairs, epochs append there on the device.
+int dcc_ctx::hist_grow_flat(HistStore& h, uint64_t need) {
+  dcc_ctx* ctx = this;
+  if (need * 8 <= h.fk.cap && need * 8 <= h.ft.cap) return DCC_OK;
+  const uint64_t want = std::max<uint64_t>(need + need / 2, 4096);
+  for (DevBuf* b : {&h.fk, &h.ft}) {
+    DevBuf nb;
+    CR(nb.ensure(this, want * 8, "history pairs"));
+    if (h.m) CK(hipMemcpyAsync(nb.p, b->p, h.m * 8, hipMemcpyDeviceToDevice, stream));
+    CK(hipStreamSynchronize(stream));
+    b->release();
+    *b = nb;
+  }
+  return DCC_OK;
+}
+
+// pairs with tns in [lo_tn, hi_tn] were appended after the first h.m
+void dcc_ctx::hist_note(HistStore& h, uint64_t lo_tn, uint64_t hi_tn) {
+  if (lo_tn < h.max_tn) h.mono = false;
+  h.max_tn = std::max(h.max_tn, hi_tn);
+  h.min_tn = std::min(h.min_tn, lo_tn);
+  h.built = false;
+}
+
+int dcc_ctx::hist_build(HistStore& h) {
+  dcc_ctx* ctx = this;
+  if (h.built) return DCC_OK;
+  if (h.m == 0) {
+    h.built = true;
+    h.mono = true;
+    return DCC_OK;
+  }
+  h.hbits = 4;
+  while ((1ull << h.hbits) < 2 * h.m) h.hbits++;
+  CR(h.skey.ensure(this, h.m * 8, "history keys"));
+  CR(h.stn.ensure(this, h.m * 8, "history tns"));
+  CR(h.hash.ensure(this, 16ull << h.hbits, "history table"));
+  for (int q = 0; q < 2; q++) {
+    CR(h_K[q].ensure(this, h.m * 8, "history sort keys"));
+    CR(h_V[q].ensure(this, h.m * 4, "history sort values"));
+  }
+  CR(h_scr.ensure(this, rs_scratch_words(h.m) * 4, "history sort scratch"));
+  HistBuild b{h.m,
+              (const uint64_t*)h.fk.p,
+              (const uint64_t*)h.ft.p,
+              h.mono,
+              {(uint64_t*)h_K[0].p, (uint64_t*)h_K[1].p},
+              {(uint32_t*)h_V[0].p, (uint32_t*)h_V[1].p},
+              (uint32_t*)h_scr.p,
+              (uint64_t*)h.skey.p,
+              (uint64_t*)h.stn.p,
+              (uint64_t*)h.hash.p,
+              h.hbits};
+  if (hist_build_level(b, stream)) CK(hipGetLastError());
+  h.built = true;
+  return DCC_OK;
+}
+
+// Merge the delta into the base once it outgrows a quarter of it (or 64K
+// pairs), then rebuild whatever changed.
+int dcc_ctx::hist_prepare() {
+  dcc_ctx* ctx = this;
+  HistStore& B = hs[0];
+  HistStore& D = hs[1];
+  if (D.m > std::max<uint64_t>(hist_merge_min, B.m / 4)) {
+    CR(hist_grow_flat(B, B.m + D.m));
+    CK(hipMemcpyAsync((uint64_t*)B.fk.p + B.m, D.fk.p, D.m * 8, hipMemcpyDeviceToDevice, stream));
+    CK(hipMemcpyAsync((uint64_t*)B.ft.p + B.m, D.ft.p, D.m * 8, hipMemcpyDeviceToDevice, stream));
+    // still tn-ordered within every key if the delta's tns all follow the base's
+    B.mono = B.mono && D.mono && (B.m == 0 || D.min_tn >= B.max_tn);
+    B.m += D.m;
+    B.max_tn = std::max(B.max_tn, D.max_tn);
+    B.min_tn = std::min(B.min_tn, D.min_tn);
+    B.built = false;
+    D = HistStore{D.fk, D.ft, D.skey, D.stn, D.hash};  // buffers kept, level emptied
+  }
+  CR(hist_build(B));
+  CR(hist_build(D));
+  return DCC_OK;
+}
+
+HistView dcc_ctx::hist_view() const {
+  HistView v{};
+  for (int q = 0; q < 2; q++) {
+    const HistStore& h = hs[q];
+    v.lv[q] = HistLevel{(const uint64_t*)h.hash.p, (const uint64_t*)h.stn.p, h.hbits,
+                        h.m && h.built ? 1u : 0u};
+  }
+  return v;
+}
+
+// central_finish for the epoch (occ.cpp:277-286): every write of a txn with a
+// commit tn joins the delta level, in index (= tn) order, on the device.
+int dcc_ctx::hist_append_epoch(const DevBatch& d, const uint64_t* tn_dev, uint64_t nnz_w,
+                               uint64_t n_cw) {
+  dcc_ctx* ctx = this;
+  if (!n_cw || !nnz_w) return DCC_OK;
+  HistStore& D = hs[1];
+  CR(hist_grow_flat(D, D.m + nnz_w));
+  const uint64_t nb = (d.n + 1023) / 1024;
+  CR(h_bsum.ensure(this, (nb + 1) * 4 + 64, "history append scan"));
+  uint32_t* bsum = (uint32_t*)h_bsum.p;
+  uint32_t* total = bsum + nb + 1;
+  launch_hist_count(d.n, d.off, d.acctype, d.nnz, tn_dev, bsum, stream);
+  rs_scan_one(bsum, (uint32_t)nb, total, stream);
+  launch_hist_emit(d.n, d.off, d.keys, d.acctype, d.nnz, tn_dev, bsum, (uint64_t*)D.fk.p + D.m,
+                   (uint64_t*)D.ft.p + D.m, stream);
+  CK(hipGetLastError());
+  CK(hipMemcpyAsync(hmisc, total, 4, hipMemcpyDeviceToHost, stream));
+  CK(hipStreamSynchronize(stream));
+  const uint32_t added = *(const uint32_t*)hmisc;
+  if (added > nnz_w) return fail(DCC_EIO, "history append: %u writes > %llu", added,
+                                 (unsigned long long)nnz_w);
+  D.m += added;
+  hist_note(D, tnc + 1, tnc + n_cw);
+  return DCC_OK;
+}
+
 extern "C" int dcc_occ_history_append(dcc_ctx* ctx, const uint64_t* keys, const uint64_t* tn,
                                       uint64_t n) {
   if (!ctx || (n && (!keys || !tn))) return DCC_EINVAL;
-  ctx->hist.reserve(ctx->hist.size() + n);
-  for (uint64_t i = 0; i < n; i++) ctx->hist.emplace_back(keys[i], tn[i]);
-  if (n) ctx->hist_dirty = true;
+  if (n == 0) return DCC_OK;
+  if (hipSetDevice(ctx->device) != hipSuccess) return DCC_ENODEV;
+  // stable by tn, so that the batch keeps tn order within every key
+  std::vector<uint64_t> idx(n);
+  for (uint64_t i = 0; i < n; i++) idx[i] = i;
+  std::stable_sort(idx.begin(), idx.end(), [&](uint64_t a, uint64_t b) { return tn[a] < tn[b]; });
+  std::vector<uint64_t> k2(n), t2(n);
+  for (uint64_t i = 0; i < n; i++) {
+    k2[i] = keys[idx[i]];
+    t2[i] = tn[idx[i]];
+  }
+  HistStore& D = ctx->hs[1];
+  CR(ctx->hist_grow_flat(D, D.m + n));
+  CK(hipMemcpy((uint64_t*)D.fk.p + D.m, k2.data(), n * 8, hipMemcpyHostToDevice));
+  CK(hipMemcpy((uint64_t*)D.ft.p + D.m, t2.data(), n * 8, hipMemcpyHostToDevice));
+  D.m += n;
+  ctx->hist_note(D, t2.front(), t2.back());
   return DCC_OK;
 }
 
 extern "C" int dcc_occ_history_clear(dcc_ctx* ctx) {
   if (!ctx) return DCC_EINVAL;
-  ctx->hist.clear();
-  ctx->hist_dirty = true;
+  for (HistStore& h : ctx->hs) {
+    h.m = 0;
+    h.max_tn = 0;
+    h.min_tn = ~0ull;
+    h.mono = true;
+    h.built = true;
+  }
   return DCC_OK;
 }
 
-extern "C" uint64_t dcc_occ_history_size(const dcc_ctx* ctx) { return ctx ? ctx->hist.size() : 0; }
+extern "C" int dcc_occ_history_trim(dcc_ctx* ctx, uint64_t tn_floor) {
+  if (!ctx) return DCC_EINVAL;
+  if (hipSetDevice(ctx->device) != hipSuccess) return DCC_ENODEV;
+  HistStore& B = ctx->hs[0];
+  HistStore& D = ctx->hs[1];
+  const uint64_t tot = B.m + D.m;
+  if (tot == 0) return DCC_OK;
+  // survivors (tn > floor) of both levels into fresh flat arrays, then the base
+  HistStore N;
+  CR(ctx->hist_grow_flat(N, tot));
+  CR(ctx->h_bsum.ensure(ctx, 64, "history trim count"));
+  unsigned long long* cnt = (unsigned long long*)ctx->h_bsum.p;
+  CK(hipMemsetAsync(cnt, 0, 8, ctx->stream));
+  launch_hist_trim((const uint64_t*)B.fk.p, (const uint64_t*)B.ft.p, B.m, (const uint64_t*)D.fk.p,
+                   (const uint64_t*)D.ft.p, D.m, tn_floor, (uint64_t*)N.fk.p, (uint64_t*)N.ft.p, cnt,
+                   ctx->stream);
+  CK(hipGetLastError());
+  CK(hipMemcpyAsync(ctx->hmisc, cnt, 8, hipMemcpyDeviceToHost, ctx->stream));
+  CK(hipStreamSynchronize(ctx->stream));
+  const uint64_t kept = *(const uint64_t*)ctx->hmisc;
+  const uint64_t mx = std::max(B.max_tn, D.max_tn);
+  B.fk.release();
+  B.ft.release();
+  B.fk = N.fk;
+  B.ft = N.ft;
+  N.fk = DevBuf{};
+  N.ft = DevBuf{};
+  B.m = kept;
+  B.max_tn = mx;
+  B.mono = false;  // the compaction does not keep the order
+  B.built = false;
+  D.m = 0;
+  D.max_tn = 0;
+  D.min_tn = ~0ull;
+  D.mono = true;
+  D.built = true;
+  ctx->buf_gen++;
+  return DCC_OK;
+}
+
+extern "C" uint64_t dcc_occ_history_size(const dcc_ctx* ctx) { return ctx ? ctx->hist_size() : 0; }
+
+extern "C" int dcc_occ_history_export(dcc_ctx* ctx, uint64_t* keys, uint64_t* tn, uint64_t cap,
+                                      uint64_t* out_n) {
+  if (!ctx || !out_n) return DCC_EINVAL;
+  if (hipSetDevice(ctx->device) != hipSuccess) return DCC_ENODEV;
+  const uint64_t n = ctx->hist_size();
+  *out_n = n;
+  if (!keys || !tn) return DCC_OK;  // size query
+  if (cap < n) return DCC_ERANGE;
+  uint64_t at = 0;
+  for (HistStore& h : ctx->hs) {
+    if (!h.m) continue;
+    CK(hipMemcpy(keys + at, h.fk.p, h.m * 8, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(tn + at, h.ft.p, h.m * 8, hipMemcpyDeviceToHost));
+    at += h.m;
+  }
+  return DCC_OK;
+}
+
 extern "C" int dcc_occ_set_tnc(dcc_ctx* ctx, uint64_t tnc) {
   if (!ctx) return DCC_EINVAL;
   ctx->tnc = tnc;
   return DCC_OK;
 }
 extern "C" uint64_t dcc_occ_get_tnc(const dcc_ctx* ctx) { return ctx ? ctx->tnc : 0; }
-
-int dcc_ctx::upload_history() {
-  dcc_ctx* ctx = this;
-  if (!hist_dirty) return DCC_OK;
-  std::sort(hist.begin(), hist.end());
-  std::vector<uint64_t> hk, ho, ht;
-  ht.reserve(hist.size());
-  for (size_t i = 0; i < hist.size(); i++) {
-    if (i == 0 || hist[i].first != hist[i - 1].first) {
-      hk.push_back(hist[i].first);
-      ho.push_back(ht.size());
-    }
-    ht.push_back(hist[i].second);
-  }
-  ho.push_back(ht.size());
-  h_nkeys = hk.size();
-  CR(hkeys.ensure(this, std::max<size_t>(8, hk.size() * 8), "hist keys"));
-  CR(hoff.ensure(this, ho.size() * 8, "hist off"));
-  CR(htn.ensure(this, std::max<size_t>(8, ht.size() * 8), "hist tn"));
-  if (!hk.empty()) CK(hipMemcpy(hkeys.p, hk.data(), hk.size() * 8, hipMemcpyHostToDevice));
-  CK(hipMemcpy(hoff.p, ho.data(), ho.size() * 8, hipMemcpyHostToDevice));
-  if (!ht.empty()) CK(hipMemcpy(htn.p, ht.data(), ht.size() * 8, hipMemcpyHostToDevice));
-  // key -> CSR row as an open-addressing table at <= 50% load (one probe of
-  // 16 B instead of a log2(keys)-deep binary search; snapshot validation)
-  h_hbits = 4;
-  while ((1ull << h_hbits) < 2 * hk.size()) h_hbits++;
-  std::vector<uint64_t> tab(2ull << h_hbits, DCC_KEY_RESERVED);
-  const uint64_t mask = (1ull << h_hbits) - 1;
-  for (size_t u = 0; u < hk.size(); u++) {
-    uint64_t slot = hist_hash_slot(hk[u], h_hbits);
-    while (tab[2 * slot] != DCC_KEY_RESERVED) slot = (slot + 1) & mask;
-    tab[2 * slot] = hk[u];
-    tab[2 * slot + 1] = u;
-  }
-  CR(hhash.ensure(this, tab.size() * 8, "hist hash"));
-  CK(hipMemcpy(hhash.p, tab.data(), tab.size() * 8, hipMemcpyHostToDevice));
-  hist_dirty = false;
-  return DCC_OK;
-}
 
 // ---------------------------------------------------------------- batch checks
 int dcc_ctx::check_batch(const dcc_batch* b) {

@@ -16,8 +16,13 @@
 // (dcc_file_write) with their decisions, for offline parity checks.
 //
 // Timestamps: with the reference's default TS_CLOCK (config.h:124) the history
-// window of central_validate never fires, so the shim
-// passes no start/finish timestamps.  The class is thread-safe; the dcc_ctx it
+// window of central_validate never fires, so by
+// default the shim passes no start/finish timestamps and keeps no history (the
+// reference's history would only grow).  With
+// Options::ts_window (TS_CAS-style timestamps) every validate() passes the
+// txn's start_tn / finish_tn (occ.cpp:142) and committed write sets join the
+// context's history (central_finish, occ.cpp:277-286), so later epochs'
+// windows see them.  The class is thread-safe; the dcc_ctx it
 // drives must not be used by anyone else meanwhile (a context is
 // thread-compatible, dcc.h).
 #pragma once
@@ -47,17 +52,21 @@ class OccEpoch {
     int n_workers = 1;           // threads that call validate()
     double timer_ms = 5.0;       // SEQ_BATCH_TIMER-like close timer (config.h:348)
     std::string capture_dir;     // "" = no capture
+    bool ts_window = false;      // pass start/finish tn and keep the history
   };
   struct Stats {
     uint64_t epochs = 0, txns = 0, commits = 0, aborts = 0;
+    uint64_t capture_errors = 0;  // .dccb writes that failed (decisions unaffected)
     double device_ms = 0, wall_ms = 0;
   };
 
   OccEpoch(dcc_ctx* ctx, const Options& o) : ctx_(ctx), opt_(o) { off_.push_back(0); }
 
   // TxnManager::validate for CC_ALG == OCC: DCC_RC_RCOK or DCC_RC_ABORT in *rc.
+  // start_tn / finish_tn are read only with Options::ts_window.
   // Returns a dcc error code (0 = ok).
-  int validate(const Access* acc, size_t n, uint8_t* rc) {
+  int validate(const Access* acc, size_t n, uint8_t* rc, uint64_t start_tn = 0,
+               uint64_t finish_tn = 0) {
     std::unique_lock<std::mutex> lk(mu_);
     const uint64_t ep = epoch_;
     const uint64_t slot = off_.size() - 1;
@@ -66,6 +75,10 @@ class OccEpoch {
       at_.push_back(acc[i].type);
     }
     off_.push_back((uint32_t)keys_.size());
+    if (opt_.ts_window) {
+      start_.push_back(start_tn);
+      finish_.push_back(finish_tn);
+    }
     if (slot == 0) opened_ = std::chrono::steady_clock::now();
     waiting_++;
     int err = 0;
@@ -121,7 +134,11 @@ class OccEpoch {
     b.offsets = off_.data();
     b.keys = keys_.data();
     b.acctype = at_.data();
-    b.flags = DCC_OCC_APPEND_HISTORY;  // central_finish: commit tn + history
+    if (opt_.ts_window) {
+      b.start_tn = start_.data();
+      b.finish_tn = finish_.data();
+      b.flags = DCC_OCC_APPEND_HISTORY;  // central_finish: commit tn + history
+    }
     dcc_stats st{};
     const uint64_t tnc0 = dcc_occ_get_tnc(ctx_);
     const auto t0 = std::chrono::steady_clock::now();
@@ -135,7 +152,10 @@ class OccEpoch {
       char path[4096];
       snprintf(path, sizeof path, "%s/epoch_%06llu.dccb", opt_.capture_dir.c_str(),
                (unsigned long long)epoch_);
-      d.err = dcc_file_write(path, &fi, &b, d.rc.data(), nullptr, nullptr, nullptr);
+      // the epoch is decided (tnc and history advanced): a failed capture is
+      // counted, never turned into aborts
+      if (dcc_file_write(path, &fi, &b, d.rc.data(), nullptr, nullptr, nullptr) != DCC_OK)
+        stats_.capture_errors++;
     }
     stats_.epochs++;
     stats_.txns += n;
@@ -148,6 +168,8 @@ class OccEpoch {
     off_.assign(1, 0);
     keys_.clear();
     at_.clear();
+    start_.clear();
+    finish_.clear();
     cv_.notify_all();
     return err;
   }
@@ -159,6 +181,7 @@ class OccEpoch {
   std::vector<uint32_t> off_;
   std::vector<uint64_t> keys_;
   std::vector<uint8_t> at_;
+  std::vector<uint64_t> start_, finish_;
   std::chrono::steady_clock::time_point opened_{};
   uint64_t epoch_ = 0;
   int waiting_ = 0;

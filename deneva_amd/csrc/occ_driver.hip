@@ -100,21 +100,9 @@ int dcc_ctx::device_prep(const DevBatch& d, uint32_t& maxlen, uint64_t& nnz_w, u
 
 // misc layout (bytes): [0] error word, [4] constant 1, [64..) kill flags
 // (CTR_RING), [512..) round counter ring (CTR_RING x NSEG), then grid barrier
-// words (CTR_RING x 16 B), [8192..) sharded undecided counts (CTR_RING),
-// [12288 + 16*level..) peel totals per level, [12800..) peel counters.
+// words (CTR_RING x 16 B), [8192..) sharded undecided counts (CTR_RING).
 static constexpr size_t MISC_KFLAG = 64, MISC_RING = 512,
-                        MISC_BARS = 512 + CTR_RING * NSEG * 8, MISC_UND = 8192,
-                        MISC_TOT = 12288, MISC_CCOUNT = 12800, MISC_ASYNC = 12928;
-
-// Prefix length of a peel over m txns (0 = solve directly with rounds).
-uint64_t dcc_ctx::peel_prefix(uint64_t m, int level) const {
-  if (peel_mode == 0 || level >= PEEL_MAX_LEVEL) return 0;
-  if (peel_mode > 0) return (uint64_t)peel_mode < m ? (uint64_t)peel_mode : 0;
-  if (m < peel_min) return 0;
-  uint64_t p = next_pow2(m / 64);
-  p = std::min<uint64_t>(std::max<uint64_t>(p, 1024), 65536);
-  return p < m ? p : 0;
-}
+                        MISC_BARS = 512 + CTR_RING * NSEG * 8, MISC_UND = 8192;
 
 // Build + fixed-point rounds for one (sub-)batch: txn i of the sub-batch has
 // accesses [off[i], off[i+1]) and state byte state[i]; only UNDECIDED txns
@@ -271,169 +259,6 @@ int dcc_ctx::occ_rounds(const SubProb& sp, uint32_t maxlen, bool prof, uint32_t&
   }
   if (prof) CK(hipEventRecord(pev[4], stream));
   rounds_out = rounds;
-  return DCC_OK;
-}
-
-// Asynchronous solver (occ_async.hip): per-key writer segments sorted by
-// txn, then chunked waves decide without rounds or host synchronisation.
-int dcc_ctx::occ_async(const SubProb& sp, uint32_t maxlen, uint32_t& passes_out) {
-  dcc_ctx* ctx = this;
-  passes_out = 0;
-  if (sp.n == 0) return DCC_OK;
-  const uint64_t cap = table_capacity(sp.w_bound);
-  if (cap > (1ull << 30)) return fail(DCC_ERANGE, "table capacity exceeds 2^30 slots");
-  CR(table.ensure(this, cap * sizeof(Slot), "table"));
-  CR(a_cnt.ensure(this, cap * 4 * 4, "async key arrays"));
-  CR(a_writers.ensure(this, std::max<uint64_t>(16, sp.w_bound * 4), "async writers"));
-  CR(a_big.ensure(this, std::max<uint64_t>(16, (sp.w_bound / ASORT_SMALL + 1) * 4), "async big"));
-  CR(a_st32.ensure(this, sp.n * 4 + 16, "async state"));
-  char* mb = (char*)misc.p;
-  uint32_t* cnt = (uint32_t*)a_cnt.p;
-  AsyncArgs a;
-  a.m = sp.n;
-  // small (sub-)batches: narrow tiles, so that every CU gets waves
-  const uint32_t len = std::max<uint32_t>(1, maxlen);
-  const uint64_t want = (sp.n + (uint64_t)n_cu * 16 - 1) / ((uint64_t)n_cu * 16);
-  a.tw_pre = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, ASYNC_CAP / len));
-  a.tw_pre = std::min<uint32_t>(a.tw_pre, 64);
-  a.tw = std::min<uint32_t>(std::max<uint32_t>(a.tw_pre, 4), ASYNC_KCAP / len);
-  a.tw = std::max<uint32_t>(1, std::min<uint32_t>(a.tw, 64));
-  a.off = sp.off;
-  a.keys = sp.keys;
-  a.acctype = sp.acctype;
-  a.state = sp.state;
-  a.st32 = (uint32_t*)a_st32.p;
-  a.tab = (Slot*)table.p;
-  a.mask = (uint32_t)(cap - 1);
-  a.wcnt = cnt;
-  a.wstart = cnt + cap;
-  a.wfill = cnt + 2 * cap;
-  a.cursor = cnt + 3 * cap;
-  a.writers = (uint32_t*)a_writers.p;
-  a.bump = (uint32_t*)(mb + MISC_ASYNC);
-  a.nbig = (uint32_t*)(mb + MISC_ASYNC + 4);
-  a.passes = (uint32_t*)(mb + MISC_ASYNC + 8);
-  a.ticket = (unsigned long long*)(mb + MISC_ASYNC + 16);
-  a.big = (uint32_t*)a_big.p;
-  a.err = (uint32_t*)mb;
-  a.hasw = sp.hasw;
-  launch_async(a, cap, (unsigned)n_cu, stream);
-  CK(hipGetLastError());
-  async_passes_dev = a.passes;
-  passes_out = 0;  // read back with the epoch's final synchronisation
-  return DCC_OK;
-}
-
-// Prefix peel (occ_peel.hip): solve [0, p) with rounds, kill every later txn
-// touching a committed prefix write key, compact the survivors into a dense
-// sub-batch (index order kept) and decide it, peeling again if it is large.
-int dcc_ctx::occ_peel(const SubProb& sp, uint32_t maxlen, int level, uint32_t& rounds_out,
-                      PeelInfo& info) {
-  dcc_ctx* ctx = this;
-  const bool sh = comm_ranks() > 1;
-  const uint64_t p = peel_prefix(sp.n, level);
-  if (p == 0) return use_async() ? occ_async(sp, maxlen, rounds_out)
-                                 : occ_rounds(sp, maxlen, false, rounds_out);
-  const bool top = level == 0;
-  char* mb = (char*)misc.p;
-  uint32_t* err = (uint32_t*)mb;
-
-  // ---- 1. the prefix, exactly
-  CR(hasw_scr.ensure(this, sp.n + 16, "hasw scratch"));
-  SubProb pre = sp;
-  pre.n = p;
-  pre.nnz = std::min<uint64_t>(sp.nnz, p * (uint64_t)maxlen);
-  pre.w_bound = top ? std::max<uint64_t>(1, prefix_w_top) : pre.nnz;
-  pre.hasw = (uint8_t*)hasw_scr.p;
-  pre.hasw_global = false;
-  if (top && profiling) CK(hipEventRecord(pev[0], stream));
-  uint32_t r_pre = 0;
-  if (use_async()) CR(occ_async(pre, maxlen, r_pre));
-  else CR(occ_rounds(pre, maxlen, false, r_pre));
-
-  // ---- 2. committed write keys of the prefix
-  const uint64_t gcap = std::max<uint64_t>(1024, next_pow2(2 * pre.w_bound + 1));
-  CR(cset_tab.ensure(this, gcap * 8, "cset table"));
-  CR(cset_keys.ensure(this, std::max<uint64_t>(8, pre.w_bound * 8), "cset keys"));
-  uint32_t* ccount = (uint32_t*)(mb + MISC_CCOUNT);
-  CK(hipMemsetAsync(cset_tab.p, 0xFF, gcap * 8, stream));
-  CK(hipMemsetAsync(ccount, 0, 4, stream));
-  const uint32_t twf = std::min<uint32_t>(64, FILTER_CAP / std::max<uint32_t>(1, maxlen));
-  CsetArgs ca{p, twf, sp.off, sp.keys, sp.acctype, sp.state, (uint64_t*)cset_tab.p,
-              (uint32_t)(gcap - 1), (uint64_t*)cset_keys.p, ccount};
-  launch_cset(ca, stream);
-
-  // ---- 3. filter [p, n): two workgroups per CU, each builds the LDS set once
-  const uint64_t step = (uint64_t)FILTER_WAVES * twf;
-  uint64_t grid = (sp.n + step - 1) / step;
-  grid = std::max<uint64_t>(1, std::min<uint64_t>(grid, std::min<uint64_t>(FILTER_MAX_GRID,
-                                                                          2 * (uint64_t)n_cu)));
-  const uint64_t per_blk = (sp.n + grid - 1) / grid;
-  uint8_t* kill = nullptr;
-  if (sh) {
-    CR(gst.ensure(this, sp.n + 16, "shard status"));
-    kill = (uint8_t*)gst.p;
-    CK(hipMemsetAsync(kill, 0, sp.n, stream));
-  }
-  SurvPart* sparts = (SurvPart*)part.p;
-  FilterArgs fa{p, sp.n, per_blk, twf, sp.off, sp.keys, sp.acctype,
-                (const uint64_t*)cset_keys.p, ccount, (const uint64_t*)cset_tab.p,
-                (uint32_t)(gcap - 1), sp.state, kill, top ? sp.hasw : (uint8_t*)hasw_scr.p,
-                sparts, err};
-  if (top && profiling) CK(hipEventRecord(pev[1], stream));
-  launch_filter(fa, (unsigned)grid, stream);
-  if (top && profiling) CK(hipEventRecord(pev[2], stream));
-  if (sh) {
-    CR(comm_allreduce_max_u8(kill, sp.n));  // a kill on any shard wins
-    launch_survivors(fa, (unsigned)grid, stream);
-    if (top) CR(comm_allreduce_max_u8(sp.hasw, sp.n));
-  }
-
-  // ---- 4. survivors -> dense sub-batch (index order)
-  SubBufs& sb = subs[level];
-  CR(sb.tid.ensure(this, sp.n * 4 + 16, "sub tid"));
-  CR(sb.off.ensure(this, (sp.n + 1) * 4 + 16, "sub offsets"));
-  CR(sb.keys.ensure(this, std::max<uint64_t>(8, sp.nnz * 8), "sub keys"));
-  CR(sb.acctype.ensure(this, std::max<uint64_t>(16, sp.nnz), "sub acctype"));
-  CR(sb.state.ensure(this, sp.n + 16, "sub state"));
-  uint32_t* tot = (uint32_t*)(mb + MISC_TOT + 16 * level);
-  launch_surv_scan(sparts, (uint32_t)grid, tot, (uint32_t*)sb.off.p, stream);
-  CompactArgs cp{p, sp.n, per_blk, sp.off, sp.keys, sp.acctype, sp.state, sparts,
-                 (uint32_t*)sb.tid.p, (uint32_t*)sb.off.p, (uint64_t*)sb.keys.p,
-                 (uint8_t*)sb.acctype.p};
-  launch_compact(cp, (unsigned)grid, stream);
-  CK(hipGetLastError());
-  CK(hipMemcpyAsync((char*)hmisc + MISC_TOT, tot, 12, hipMemcpyDeviceToHost, stream));
-  CK(hipStreamSynchronize(stream));
-  const uint32_t* ht = (const uint32_t*)((const char*)hmisc + MISC_TOT);
-  const uint64_t n_s = ht[0], nnz_s = ht[1], w_s = ht[2];
-  if (top) {
-    info.prefix = p;
-    info.survivors = n_s;
-  }
-
-  // ---- 5. decide the survivors, write their decisions back
-  uint32_t r_sub = 0;
-  if (n_s) {
-    CK(hipMemsetAsync(sb.state.p, 0, n_s, stream));
-    SubProb sub;
-    sub.n = n_s;
-    sub.nnz = nnz_s;
-    sub.off = (const uint32_t*)sb.off.p;
-    sub.keys = (const uint64_t*)sb.keys.p;
-    sub.acctype = (const uint8_t*)sb.acctype.p;
-    sub.state = (uint8_t*)sb.state.p;
-    sub.hasw = (uint8_t*)hasw_scr.p;
-    sub.hasw_global = false;
-    sub.w_bound = std::max<uint64_t>(1, w_s);
-    if (sh) sub.w_bound = std::max<uint64_t>(1, nnz_s);  // local write counts differ per shard
-    CR(occ_peel(sub, maxlen, level + 1, r_sub, info));
-    launch_scatter((const uint8_t*)sb.state.p, (const uint32_t*)sb.tid.p, tot, n_s, sp.state,
-                   stream);
-    CK(hipGetLastError());
-  }
-  if (top && profiling) CK(hipEventRecord(pev[3], stream));
-  rounds_out = r_pre + r_sub;
   return DCC_OK;
 }
 
@@ -697,44 +522,8 @@ int dcc_ctx::sweep_sharded(const DevBatch& d, int& next_level) {
 }
 
 
-// central_finish (occ.cpp:283-286): committed non-read-only txns take
-// tn = tnc+1, tnc+2, ... in index order; their write sets join the history.
-int dcc_ctx::history_append_epoch(const dcc_batch* b, const DevBatch& d, const uint64_t* tn_dev,
-                                  bool dev_out, uint64_t n_cw) {
-  dcc_ctx* ctx = this;
-  std::vector<uint64_t> htn_host(d.n);
-  CK(hipMemcpy(htn_host.data(), tn_dev, d.n * 8, hipMemcpyDeviceToHost));
-  std::vector<uint32_t> ho;
-  std::vector<uint64_t> hk;
-  std::vector<uint8_t> ha;
-  const uint32_t* o = b->offsets;
-  const uint64_t* kk = b->keys;
-  const uint8_t* at = b->acctype;
-  if (dev_out) {
-    ho.resize(d.n + 1);
-    hk.resize(d.nnz);
-    ha.resize(d.nnz);
-    CK(hipMemcpy(ho.data(), d.off, (d.n + 1) * 4, hipMemcpyDeviceToHost));
-    if (d.nnz) {
-      CK(hipMemcpy(hk.data(), d.keys, d.nnz * 8, hipMemcpyDeviceToHost));
-      CK(hipMemcpy(ha.data(), d.acctype, d.nnz, hipMemcpyDeviceToHost));
-    }
-    o = ho.data();
-    kk = hk.data();
-    at = ha.data();
-  }
-  for (uint64_t t = 0; t < d.n; t++) {
-    if (!htn_host[t]) continue;
-    for (uint32_t x = o[t]; x < o[t + 1]; x++)
-      if (at[x] == DCC_WR) hist.emplace_back(kk[x], htn_host[t]);
-  }
-  if (n_cw) hist_dirty = true;
-  return DCC_OK;
-}
-
 int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dcc_stats* st) {
   dcc_ctx* ctx = this;
-  if (use_stage()) return occ_stage_epoch(b, out_rc, out_tn, st);
   // key-sharded across ranks: this rank holds only its keys
   const bool sh = comm_ranks() > 1;
   const auto t_wall0 = std::chrono::steady_clock::now();
@@ -764,7 +553,7 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   // captured HIP graph when the batch, the outputs and every workspace are
   // the ones it was captured with: one graph launch instead of ~30 kernel
   // launches, so the device never waits for the host between kernels.
-  const bool hist_on = d.start_tn && !hist.empty();
+  const bool hist_on = d.start_tn && hist_size() > 0;
   const bool graph_ok = sweep && !profiling && !sw_debug && !want_tn && !hist_on && !sh &&
                         !getenv("DCC_NO_GRAPH");
   const GraphKey gkey{d.off, d.keys, d.acctype, d.n, d.nnz, out_rc, dev_out, sw_levels, buf_gen};
@@ -800,13 +589,12 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   // partials are read back with the epoch's one synchronisation.
   uint32_t maxlen = 0;
   uint64_t nnz_w = 0;
-  const uint64_t p0 = sweep ? 0 : peel_prefix(d.n, 0);
   if (sweep) {
     if (!replay)
       launch_prep(d.off, d.n, d.acctype, d.nnz, 0, (PrepPart*)((char*)part.p + SW_PREP_OFF),
                   stream);
   } else {
-    CR(device_prep(d, maxlen, nnz_w, p0, &prefix_w_top));
+    CR(device_prep(d, maxlen, nnz_w));
   }
   if (!replay) {
     // one launch: error word 0, the constant-one word 1, words 2..15, the
@@ -817,7 +605,6 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
     fa.job[fa.n++] = FillJob{mw, 1, 0u};
     fa.job[fa.n++] = FillJob{mw + 1, 1, 1u};
     fa.job[fa.n++] = FillJob{mw + 2, 14, 0u};
-    fa.job[fa.n++] = FillJob{(uint32_t*)((char*)misc.p + MISC_ASYNC + 8), 1, 0u};
     fa.job[fa.n++] = FillJob{(uint32_t*)state.p, (d.n + 3) / 4, 0u};  // state holds n + 16
     if (sweep) {
       fa.job[fa.n++] = FillJob{(uint32_t*)sw_ctl.p, sw_ctl_bytes() / 4, 0u};
@@ -830,10 +617,9 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
 
   // ---- history window pre-pass (occ.cpp:160-180)
   if (hist_on) {
-    CR(upload_history());
-    HistArgs ha{d.n, d.off, d.keys, d.acctype, d.start_tn, d.finish_tn,
-                (const uint64_t*)hkeys.p, h_nkeys, (const uint64_t*)hoff.p,
-                (const uint64_t*)htn.p, (uint8_t*)state.p};
+    CR(hist_prepare());
+    HistArgs ha{d.n, d.nnz, d.off, d.keys, d.acctype, d.start_tn, d.finish_tn, hist_view(),
+                (uint8_t*)state.p, (uint32_t*)misc.p};
     launch_hist(ha, stream);
   }
   // the history window is checked on each shard's keys: any shard's abort wins
@@ -850,23 +636,18 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   top.hasw_global = true;
   top.w_bound = nnz_w;
   uint32_t rounds = 0;
+  uint32_t handoffs = 0;  // sweep lists handed to the round solver
   PeelInfo info;
-  const bool peel = !sweep && p0 != 0;
-  async_passes_dev = nullptr;
   int next_level = 0;
   if (sweep) {
     if (profiling) CK(hipEventRecord(pev[0], stream));
     next_level = (int)std::min<uint32_t>(sw_levels, SW_MAX_LEVEL - 1);
     if (sh) CR(sweep_sharded(d, next_level));
     else if (!replay) CR(sweep_enqueue(d, 0, next_level));
-  } else if (peel) {
-    CR(occ_peel(top, maxlen, 0, rounds, info));
-  } else if (use_async()) {
-    CR(occ_async(top, maxlen, rounds));
   } else {
     CR(occ_rounds(top, maxlen, profiling, rounds));
   }
-  if (profiling && !peel) CK(hipEventRecord(pev[3], stream));
+  if (profiling) CK(hipEventRecord(pev[3], stream));
 
   // ---- finalize: RC bytes, counts, central_finish tn numbering
   uint8_t* rc_dev = (dev_out && out_rc) ? out_rc : (uint8_t*)rc.p;
@@ -898,7 +679,6 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
     };
     job(hmisc_dev, misc.p, 64);
     job((char*)hmisc_dev + MISC_BARS, (char*)misc.p + MISC_BARS, CTR_RING * 16);
-    if (async_passes_dev) job((char*)hmisc_dev + MISC_ASYNC, (char*)misc.p + MISC_ASYNC, 16);
     if (sweep) {
       job((char*)hmisc_dev + SW_HCTL, sw_ctl.p, sw_ctl_bytes());
       job((char*)hpart_dev + SW_PREP_OFF, (char*)part.p + SW_PREP_OFF,
@@ -981,8 +761,8 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
       sub.w_bound = std::max<uint64_t>(1, sub.nnz);
       CK(hipMemsetAsync(sub.state, 0, sub.n, stream));
       uint32_t r_sub = 0;
-      if (use_async()) CR(occ_async(sub, maxlen, r_sub));
-      else CR(occ_rounds(sub, maxlen, false, r_sub));
+      CR(occ_rounds(sub, maxlen, false, r_sub));
+      handoffs++;
       rounds += r_sub;
       launch_scatter(sub.state, (const uint32_t*)lb.tid.p,
                      &((SwLevel*)sw_ctl.p)[L].m, sub.n, (uint8_t*)state.p, stream);
@@ -1052,15 +832,6 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   }
 
   const uint32_t e = *(const uint32_t*)hmisc;
-  if ((e & (ERR_SEG | ERR_ASYNC)) && !force_rounds) {
-    // a writer segment too long for the LDS sort, or the pass guard tripped:
-    // decide the epoch again with the round solver
-    force_rounds = true;
-    const int r2 = occ_epoch(b, out_rc, out_tn, st);
-    force_rounds = false;
-    return r2;
-  }
-  if (async_passes_dev) rounds += *(const uint32_t*)((const char*)hmisc + MISC_ASYNC + 8);
   {
     // barrier timeout words (third word of each GridBar in the ring)
     // (read back with the epoch's gather)
@@ -1093,6 +864,7 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   S.alg_bytes = dcc_alg_bytes(d.n, d.nnz, nnz_w);
   S.device_ms = ms;
   S.peel_prefix = info.prefix;
+  S.fallback = handoffs;
   S.n_survivors = info.survivors;
   if (profiling) {
     float t0 = 0, t1 = 0, t2 = 0;
@@ -1100,12 +872,6 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
       // phases: 0 = level-0 records + serial pass + committed set, 1 = the
       // level-0 filter kernel, 2 = level-0 compaction + later levels (+
       // fallback), 3 = prep + finalize
-      CK(hipEventElapsedTime(&t0, pev[0], pev[1]));
-      CK(hipEventElapsedTime(&t1, pev[1], pev[2]));
-      CK(hipEventElapsedTime(&t2, pev[2], pev[3]));
-    } else if (peel) {
-      // phases: 0 = prefix solve + committed-key set, 1 = filter pass,
-      // 2 = compaction + survivor solve + scatter, 3 = prep + finalize
       CK(hipEventElapsedTime(&t0, pev[0], pev[1]));
       CK(hipEventElapsedTime(&t1, pev[1], pev[2]));
       CK(hipEventElapsedTime(&t2, pev[2], pev[3]));
@@ -1120,7 +886,7 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
     S.phase_ms[2] = t2;
     S.phase_ms[3] = ms - t0 - t1 - t2;
   }
-  if (sweep || peel) {
+  if (sweep) {
     // the filter pass reads offsets, keys + acctype of every access and the
     // state byte of every txn, and writes the has-write (and kill) bytes
     S.phase_bytes[1] = 4 * (d.n + 1) + 9 * d.nnz + 2 * d.n;
@@ -1132,7 +898,8 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
     S.phase_bytes[1] = 4 * (d.n + 1) + 9 * d.nnz + 16 * d.nnz + d.n;
   }
 
-  if (b->flags & DCC_OCC_APPEND_HISTORY) CR(history_append_epoch(b, d, tn_dev, dev_out, n_cw));
+  // central_finish (occ.cpp:277-286): committed write sets join the history
+  if (b->flags & DCC_OCC_APPEND_HISTORY) CR(hist_append_epoch(d, tn_dev, nnz_w, n_cw));
   tnc += n_cw;
   const auto t_wall1 = std::chrono::steady_clock::now();
   S.total_ms = std::chrono::duration<double, std::milli>(t_wall1 - t_wall0).count();

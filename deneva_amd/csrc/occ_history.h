@@ -1,0 +1,93 @@
+// Device-resident OCC history (the `history` list of committed write sets,
+// concurrency_control/occ.h:62-64, pushed by central_finish, occ.cpp:277-286,
+// scanned by the window check of central_validate, occ.cpp:160-180).
+//
+// The history is a multiset of (key, tn) pairs: one per write of a committed
+// txn numbered tn.  It lives in HBM as two levels, a large `base` and a small
+// `delta` (a two-level log-structured merge): an epoch appends its committed
+// writes to the delta's flat pair array on the device (count, scan, emit: no
+// D2H of the batch), the delta is rebuilt, and it is merged into the base when
+// it outgrows a quarter of it.  A built level is its pairs sorted by (key, tn)
+// plus an open-addressing table key -> (first pair, pair count) at <= 50 %
+// load, so a window query is one probe per level and a binary search of the
+// key's run of tns.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dcc.h"
+
+// history hash slot of a key (device build and probe agree)
+__host__ __device__ inline uint64_t hist_hash_slot(uint64_t key, uint32_t bits) {
+  return (key * 0x9E3779B97F4A7C15ull) >> (64 - bits);
+}
+
+namespace dcc {
+
+struct HistLevel {
+  const uint64_t* hash;  // [2 << hbits]: key, first | count << 32 (DCC_KEY_RESERVED = empty)
+  const uint64_t* tn;    // [m] tns, ascending within a key's run
+  uint32_t hbits;
+  uint32_t on;           // 0: the level is empty
+};
+struct HistView {
+  HistLevel lv[2];  // base, delta
+};
+
+// does the level hold a pair (key, tn) with lo < tn <= hi?
+__device__ inline bool hist_level_hit(const HistLevel& L, uint64_t key, uint64_t lo, uint64_t hi) {
+  if (!L.on) return false;
+  const uint64_t mask = (1ull << L.hbits) - 1;
+  uint64_t slot = hist_hash_slot(key, L.hbits), v = 0;
+  for (;;) {  // <= 50 % load: every probe sequence ends at an empty slot
+    const uint64_t k2 = L.hash[2 * slot];
+    if (k2 == key) {
+      v = L.hash[2 * slot + 1];
+      break;
+    }
+    if (k2 == DCC_KEY_RESERVED) return false;
+    slot = (slot + 1) & mask;
+  }
+  const uint64_t first = (uint32_t)v, end = first + (v >> 32);
+  uint64_t b = first, e = end;
+  while (b < e) {  // first tn > lo
+    const uint64_t m = (b + e) >> 1;
+    if (L.tn[m] <= lo) b = m + 1;
+    else e = m;
+  }
+  return b < end && L.tn[b] <= hi;
+}
+__device__ inline bool hist_hit(const HistView& h, uint64_t key, uint64_t lo, uint64_t hi) {
+  return hist_level_hit(h.lv[1], key, lo, hi) || hist_level_hit(h.lv[0], key, lo, hi);
+}
+
+// ---- build kernels (occ_history.hip)
+// per 1024-txn block: the writes of committed txns (tn[t] != 0)
+void launch_hist_count(uint64_t n, const uint32_t* off, const uint8_t* acctype, uint64_t nnz,
+                       const uint64_t* tn, uint32_t* bsum, hipStream_t st);
+// pairs of block b's committed writes at out + bsum[b] (scanned) + block rank
+void launch_hist_emit(uint64_t n, const uint32_t* off, const uint64_t* keys, const uint8_t* acctype,
+                      uint64_t nnz, const uint64_t* tn, const uint32_t* bsum, uint64_t* out_k,
+                      uint64_t* out_t, hipStream_t st);
+// level build from flat pairs (fk, ft)[m]; K/V are radix-sort ping-pong buffers
+struct HistBuild {
+  uint64_t m;
+  const uint64_t* fk;
+  const uint64_t* ft;
+  bool mono;            // flat tns ascend within every key (append order is tn order)
+  uint64_t* K[2];
+  uint32_t* V[2];
+  uint32_t* scratch;
+  uint64_t* skey;       // out: sorted keys
+  uint64_t* stn;        // out: sorted tns
+  uint64_t* hash;       // out: [2 << hbits]
+  uint32_t hbits;
+};
+int hist_build_level(const HistBuild& b, hipStream_t st);
+// pairs with tn > floor of (ak, at)[na] then (bk, bt)[nb], appended at
+// (ok, ot) + *cnt (atomic position: order not kept)
+void launch_hist_trim(const uint64_t* ak, const uint64_t* at, uint64_t na, const uint64_t* bk,
+                      const uint64_t* bt, uint64_t nb, uint64_t floor, uint64_t* ok, uint64_t* ot,
+                      unsigned long long* cnt, hipStream_t st);
+
+}  // namespace dcc

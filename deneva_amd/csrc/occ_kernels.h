@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include "occ_history.h"
 
 namespace dcc {
 
@@ -27,8 +28,6 @@ constexpr uint32_t ERR_TILE = 2;
 constexpr uint32_t ERR_KEY = 4;
 constexpr uint32_t ERR_FULL = 8;
 constexpr uint32_t ERR_UNDECIDED = 16;
-constexpr uint32_t ERR_SEG = 32;    // async solver: a key segment too long to sort in LDS
-constexpr uint32_t ERR_ASYNC = 64;  // async solver: pass limit reached
 constexpr uint32_t ERR_SPIN = 128;  // sweep filter: look-back spin limit reached
 
 constexpr unsigned PREP_BLOCKS = 512;
@@ -47,17 +46,15 @@ struct TileOut {
 };
 
 struct HistArgs {
-  uint64_t n;
+  uint64_t n, nnz;
   const uint32_t* off;
   const uint64_t* keys;
   const uint8_t* acctype;
   const uint64_t* start_tn;
   const uint64_t* finish_tn;
-  const uint64_t* hkeys;
-  uint64_t nkeys;
-  const uint64_t* hoff;
-  const uint64_t* htn;
+  HistView hist;   // device history levels (occ_history.h)
   uint8_t* state;
+  uint32_t* err;   // ERR_OFFSETS on a malformed device batch
 };
 
 struct BuildArgs {
@@ -127,102 +124,9 @@ struct FinalArgs {
   FinalPart* part;  // [FINAL_BLOCKS]
 };
 
-// ---- prefix peel (occ_peel.hip)
-constexpr int FILTER_CAP = 1024;  // accesses staged per wave
-constexpr int FILTER_WAVES = 8;
-constexpr int FILTER_ILP = 16;  // all of a wave tile's accesses in flight at once
-constexpr unsigned FILTER_MAX_GRID = 2048;  // per-block partials fit `part`
-
-struct SurvPart {
-  uint32_t t, a, w, pad;  // survivors: txns, accesses, writes (scanned: bases)
-};
-
-struct CsetArgs {
-  uint64_t p;  // prefix length
-  uint32_t tw;  // txns per wave tile
-  const uint32_t* off;
-  const uint64_t* keys;
-  const uint8_t* acctype;
-  const uint8_t* state;
-  uint64_t* gset;  // exact set, capacity gmask + 1, pre-filled with KEY_EMPTY
-  uint32_t gmask;
-  uint64_t* ckeys;  // compact list of the set's keys
-  uint32_t* ccount;
-};
-
-struct FilterArgs {
-  uint64_t t0, n;    // kill candidates [t0, n); has-write bytes for [0, n)
-  uint64_t per_blk;  // txns per block (block b: [b*per_blk, (b+1)*per_blk))
-  uint32_t tw;       // txns per wave tile
-  const uint32_t* off;
-  const uint64_t* keys;
-  const uint8_t* acctype;
-  const uint64_t* ckeys;
-  const uint32_t* ccount;
-  const uint64_t* gset;
-  uint32_t gmask;
-  uint8_t* state;
-  uint8_t* kill;  // sharded: local kill byte out (all-reduced MAX), else null
-  uint8_t* hasw;
-  SurvPart* part;  // [grid]
-  uint32_t* err;
-};
-
-struct CompactArgs {
-  uint64_t t0, n, per_blk;
-  const uint32_t* off;
-  const uint64_t* keys;
-  const uint8_t* acctype;
-  const uint8_t* state;
-  const SurvPart* part;  // scanned bases per block
-  uint32_t* sub_tid;
-  uint32_t* sub_off;
-  uint64_t* sub_keys;
-  uint8_t* sub_acctype;
-};
-
-void launch_cset(const CsetArgs& a, hipStream_t st);
-void launch_filter(const FilterArgs& a, unsigned grid, hipStream_t st);
-void launch_survivors(const FilterArgs& a, unsigned grid, hipStream_t st);
-void launch_surv_scan(SurvPart* part, uint32_t nb, uint32_t* tot, uint32_t* sub_off,
-                      hipStream_t st);
-void launch_compact(const CompactArgs& a, unsigned grid, hipStream_t st);
+// sub-list decisions back to the epoch's state bytes (round-solver hand-off)
 void launch_scatter(const uint8_t* sub_state, const uint32_t* sub_tid, const uint32_t* n_sub,
                     uint64_t m_bound, uint8_t* state, hipStream_t st);
-
-// ---- asynchronous solver (occ_async.hip)
-constexpr int ASYNC_CAP = 1024;   // accesses staged per wave (preprocessing)
-constexpr int ASYNC_KCAP = 512;   // accesses staged per wave (k_async)
-constexpr int ASYNC_WAVES = 8;
-constexpr uint32_t ASORT_SMALL = 16;   // segments sorted by one thread
-constexpr uint32_t ASORT_BIG = 32768;  // longest segment the LDS sort takes
-constexpr uint32_t ASYNC_MAX_PASS = 1u << 20;
-
-struct AsyncArgs {
-  uint64_t m;   // txns of the (sub-)batch
-  uint32_t tw;  // txns per wave chunk (k_async)
-  uint32_t tw_pre;  // txns per wave tile (preprocessing)
-  const uint32_t* off;
-  const uint64_t* keys;
-  const uint8_t* acctype;
-  uint8_t* state;   // u8 decisions in (history aborts) / out
-  uint32_t* st32;   // working state words (agent-scope atomics)
-  Slot* tab;
-  uint32_t mask;
-  uint32_t* wcnt;     // [cap] writers per key
-  uint32_t* wstart;   // [cap] segment start
-  uint32_t* wfill;    // [cap] fill counters
-  uint32_t* cursor;   // [cap] first writer not known aborted
-  uint32_t* writers;  // segments of writer txn ids, sorted per key
-  uint32_t* bump;
-  uint32_t* big;      // keys with long segments
-  uint32_t* nbig;
-  unsigned long long* ticket;
-  uint32_t* passes;
-  uint32_t* err;
-  uint8_t* hasw;  // has-write byte per txn out (may be null)
-};
-void launch_async(const AsyncArgs& a, uint64_t cap, unsigned n_cu, hipStream_t st);
 
 // ---- sweep solver (occ_sweep.hip)
 constexpr uint32_t SW_T = 64;        // txns per serial tile (one 64-bit mask word)

@@ -104,36 +104,22 @@ __global__ __launch_bounds__(256) void k_prep(const uint32_t* __restrict__ off, 
 // --------------------------------------------------------------------------
 // k_hist: the history window check (occ.cpp:160-180): if finish_tn > start_tn,
 // txn i aborts when a committed history entry with start_tn < tn <= finish_tn
-// wrote a key i READ (history is checked against the read set only).
-// History is a CSR sorted by key: hkeys[u] unique ascending, htn[hoff[u]..)
-// ascending.  One thread per txn (this path is off under TS_CLOCK).
-__device__ inline int64_t hist_find(const uint64_t* hk, uint64_t nk, uint64_t key) {
-  uint64_t lo = 0, hi = nk;
-  while (lo < hi) {
-    const uint64_t mid = (lo + hi) >> 1;
-    if (hk[mid] < key) lo = mid + 1;
-    else hi = mid;
-  }
-  return (lo < nk && hk[lo] == key) ? (int64_t)lo : -1;
-}
-
+// wrote a key i READ (history is checked against the read set only).  The
+// history is the device's base + delta levels (occ_history.h).  One thread
+// per txn (this path is off under TS_CLOCK); offsets are clamped to nnz.
 __global__ __launch_bounds__(256) void k_hist(HistArgs a) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= a.n) return;
   const uint64_t s_tn = a.start_tn[t], f_tn = a.finish_tn[t];
   if (!(f_tn > s_tn)) return;
-  for (uint32_t x = a.off[t]; x < a.off[t + 1]; x++) {
+  const uint64_t o0 = min((uint64_t)a.off[t], a.nnz), o1 = min((uint64_t)a.off[t + 1], a.nnz);
+  if (o1 < o0 || o1 - o0 > MAX_TXN_LEN) {
+    atomicOr(a.err, ERR_OFFSETS);
+    return;
+  }
+  for (uint64_t x = o0; x < o1; x++) {
     if (a.acctype[x] == 1 /* WR */) continue;
-    const int64_t u = hist_find(a.hkeys, a.nkeys, a.keys[x]);
-    if (u < 0) continue;
-    // any tn in (s_tn, f_tn]: first tn > s_tn, then test <= f_tn
-    uint64_t lo = a.hoff[u], hi = a.hoff[u + 1];
-    while (lo < hi) {
-      const uint64_t mid = (lo + hi) >> 1;
-      if (a.htn[mid] <= s_tn) lo = mid + 1;
-      else hi = mid;
-    }
-    if (lo < a.hoff[u + 1] && a.htn[lo] <= f_tn) {
+    if (hist_hit(a.hist, a.keys[x], s_tn, f_tn)) {
       a.state[t] = ST_ABORT;
       return;
     }
@@ -912,6 +898,26 @@ void launch_commit_tn(const uint32_t* cflag, uint64_t n, uint64_t* bsum, uint64_
   k_scan_blocks<<<nb, 1024, 0, st>>>(cflag, n, bsum);
   k_scan_sums<<<1, 64, 0, st>>>(bsum, nb);
   k_scan_apply<<<nb, 1024, 0, st>>>(cflag, n, bsum, tnc, tn);
+}
+
+// ---------------------------------------------------------------------------
+// k_scatter: sub-batch decisions back to the epoch's state bytes.
+__global__ __launch_bounds__(256) void k_scatter(const uint8_t* __restrict__ sub_state,
+                                                 const uint32_t* __restrict__ sub_tid,
+                                                 const uint32_t* __restrict__ n_sub,
+                                                 uint8_t* __restrict__ state) {
+  const uint32_t m = *n_sub;
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < m; j += gridDim.x * blockDim.x) {
+    const uint8_t s = sub_state[j];
+    state[sub_tid[j]] = s == ST_COMMIT ? ST_COMMIT : s == ST_UNDECIDED ? ST_UNDECIDED : ST_ABORT;
+  }
+}
+
+void launch_scatter(const uint8_t* sub_state, const uint32_t* sub_tid, const uint32_t* n_sub,
+                    uint64_t m_bound, uint8_t* state, hipStream_t st) {
+  unsigned g = (unsigned)((m_bound + 255) / 256);
+  if (g > 1024) g = 1024;
+  k_scatter<<<g ? g : 1, 256, 0, st>>>(sub_state, sub_tid, n_sub, state);
 }
 
 }  // namespace dcc

@@ -52,11 +52,7 @@ struct SnapArgs {
   const uint64_t* hist_top;  // NULL: whole history visible
   const uint32_t* aoff;
   const uint32_t* aidx;
-  const uint64_t* hhash;  // [2 << hbits] (key, row) slots, DCC_KEY_RESERVED = empty
-  uint32_t hbits;
-  uint64_t nkeys;
-  const uint64_t* hoff;
-  const uint64_t* htn;
+  HistView hist;  // device history levels (occ_history.h); both off: no window
   uint8_t* out_rc;
   unsigned long long* part;  // [waves][SNAP_NCNT] per-wave partials (plain stores, no atomics)
 };
@@ -90,31 +86,6 @@ __device__ inline uint64_t readlane64(uint64_t v, uint32_t lane) {
   return ((uint64_t)hi << 32) | lo;
 }
 
-// first history tn of `key` that is > lo, tested against hi (history CSR row
-// u of the key found through the open-addressing table, htn[hoff[u] ..
-// hoff[u+1]) ascending)
-__device__ inline bool hist_window_hit(const SnapArgs& a, uint64_t key, uint64_t lo, uint64_t hi) {
-  if (a.nkeys == 0) return false;
-  const uint64_t mask = (1ull << a.hbits) - 1;
-  uint64_t slot = hist_hash_slot(key, a.hbits), l = ~0ull;
-  for (;;) {  // <= 50% load: every probe sequence ends at an empty slot
-    const uint64_t k2 = a.hhash[2 * slot];
-    if (k2 == key) {
-      l = a.hhash[2 * slot + 1];
-      break;
-    }
-    if (k2 == DCC_KEY_RESERVED) return false;
-    slot = (slot + 1) & mask;
-  }
-  uint64_t b = a.hoff[l], e = a.hoff[l + 1];
-  while (b < e) {
-    const uint64_t m = (b + e) >> 1;
-    if (a.htn[m] <= lo) b = m + 1;
-    else e = m;
-  }
-  return b < a.hoff[l + 1] && a.htn[b] <= hi;
-}
-
 struct SnapCnt {  // per-lane partials, reduced over the wave at the end
   uint32_t err = 0, n_commit = 0, n_ro = 0, n_w = 0;
   uint64_t bytes = 0;
@@ -140,7 +111,7 @@ __device__ void snap_full(const SnapArgs& a, uint64_t t, uint32_t lane, SnapCnt&
     uint64_t hi = f;
     if (a.hist_top) hi = min(hi, a.hist_top[t]);
     if (lane == 0) c.bytes += a.hist_top ? 24 : 16;
-    if (f > s && hi > s && have && !wr) hit = hist_window_hit(a, k, s, hi);
+    if (f > s && hi > s && have && !wr) hit = hist_hit(a.hist, k, s, hi);
   }
   bool conflict = ballot64(hit) != 0;
   // captured active list: W_j vs R_i, then W_j vs W_i (occ.cpp:185-199).
@@ -232,7 +203,7 @@ __device__ void snap_grouped(const SnapArgs& a, uint64_t t, bool tv, uint32_t o0
     uint64_t hi = f;
     if (a.hist_top) hi = min(hi, a.hist_top[t]);
     if (sl == 0) c.bytes += a.hist_top ? 24 : 16;
-    if (f > s && hi > s && have && !wr) hit = hist_window_hit(a, k, s, hi);
+    if (f > s && hi > s && have && !wr) hit = hist_hit(a.hist, k, s, hi);
   }
   bool conflict = ((ballot64(hit) >> (16 * g)) & 0xFFFFull) != 0;
   // entry e (uniform) of this group's list: from the up-front lanes when e < 16
@@ -354,6 +325,10 @@ int dcc_ctx::occ_snapshot(const dcc_batch* b, const dcc_occ_snapshot* s, uint8_t
   dcc_ctx* ctx = this;
   const auto t_wall0 = std::chrono::steady_clock::now();
   if (!s || !s->active_off) return fail(DCC_EINVAL, "snapshot: null snapshot or active_off");
+  // a device capture is not read on the host: its lists must be addressable
+  if ((b && (b->flags & DCC_DEVICE_PTRS)) && !s->active_idx)
+    return fail(DCC_EINVAL, "snapshot: device capture needs active_idx (a 1-element buffer "
+                            "when every list is empty)");
   if (comm_ranks() > 1) return fail(DCC_ENOTSUP, "snapshot validation is single-GPU");
   CR(check_batch(b));
   dcc_stats S;
@@ -401,8 +376,10 @@ int dcc_ctx::occ_snapshot(const dcc_batch* b, const dcc_occ_snapshot* s, uint8_t
     }
     CR(rc.ensure(this, n + 16, "rc"));
   }
-  const bool hist_on = d.start_tn && !hist.empty();
-  if (hist_on) CR(upload_history());
+  const bool hist_on = d.start_tn && hist_size() > 0;
+  if (hist_on) CR(hist_prepare());
+  HistView hv{};
+  if (hist_on) hv = hist_view();
   const uint64_t waves_needed = (n + 3) / 4;  // four txns per wave step
   uint64_t grid = (waves_needed + SNAP_WAVES - 1) / SNAP_WAVES;
   grid = std::min<uint64_t>(grid, (uint64_t)n_cu * 16);
@@ -418,11 +395,7 @@ int dcc_ctx::occ_snapshot(const dcc_batch* b, const dcc_occ_snapshot* s, uint8_t
              top,
              aoff,
              aidx,
-             (const uint64_t*)hhash.p,
-             h_hbits,
-             hist_on ? h_nkeys : 0,
-             (const uint64_t*)hoff.p,
-             (const uint64_t*)htn.p,
+             hv,
              dev ? out_rc : (uint8_t*)rc.p,
              cnt_dev + 8};
   CK(hipEventRecord(ev0, stream));

@@ -192,6 +192,22 @@ class Engine:
         tn = np.ascontiguousarray(tn, np.uint64)
         _check(lib.dcc_occ_history_append(self._h, _ptr(keys), _ptr(tn), keys.shape[0]), self._h)
 
+    def history_trim(self, tn_floor: int) -> None:
+        """Drop history entries with tn <= tn_floor (dcc_occ_history_trim)."""
+        _check(lib.dcc_occ_history_trim(self._h, tn_floor), self._h)
+
+    def history_export(self):
+        """The history's (key, tn) pairs, sorted by (key, tn)."""
+        n = C.c_uint64(0)
+        _check(lib.dcc_occ_history_export(self._h, None, None, 0, C.byref(n)), self._h)
+        k = np.empty(n.value, np.uint64)
+        t = np.empty(n.value, np.uint64)
+        if n.value:
+            _check(lib.dcc_occ_history_export(self._h, _ptr(k), _ptr(t), n.value, C.byref(n)),
+                   self._h)
+        o = np.lexsort((t, k))
+        return k[o], t[o]
+
     def history_clear(self) -> None:
         _check(lib.dcc_occ_history_clear(self._h), self._h)
 
@@ -209,8 +225,10 @@ class Engine:
 
     # ------------------------------------------------------------ Calvin
     def calvin_order_epoch(self, batch: EpochBatch, want_group: bool = True,
-                           want_wave: bool = False):
-        """Returns (group u32[nnz] | None, rc u8[n], wave u32[n] | None, stats)."""
+                           want_wave: bool = False, held=None):
+        """Returns (group u32[nnz] | None, rc u8[n], wave u32[n] | None, stats).
+        held = (keys u64[h], acctype u8[h]): rows still locked at the epoch's
+        start, per row owners first then waiters (dcc_calvin_order_epoch_held)."""
         n, nnz = batch.n_txn, batch.nnz
         dev = batch.on_device
         if dev:
@@ -225,8 +243,17 @@ class Engine:
             wav = np.empty(max(n, 1), np.uint32) if want_wave else None
         st = _abi.Stats()
         b = batch.to_c()
-        _check(lib.dcc_calvin_order_epoch(self._h, C.byref(b), _ptr(grp), _ptr(rc), _ptr(wav),
-                                          C.byref(st)), self._h)
+        if held is None:
+            _check(lib.dcc_calvin_order_epoch(self._h, C.byref(b), _ptr(grp), _ptr(rc), _ptr(wav),
+                                              C.byref(st)), self._h)
+        else:
+            hk, ha = held
+            if not dev:
+                hk = np.ascontiguousarray(hk, np.uint64)
+                ha = np.ascontiguousarray(ha, np.uint8)
+            h = _abi.CalvinHeld(int(hk.shape[0]), _ptr(hk), _ptr(ha))
+            _check(lib.dcc_calvin_order_epoch_held(self._h, C.byref(b), C.byref(h), _ptr(grp),
+                                                   _ptr(rc), _ptr(wav), C.byref(st)), self._h)
         return (grp[:nnz] if want_group else None, rc[:n],
                 (wav[:n] if want_wave else None), st.as_dict())
 

@@ -99,22 +99,20 @@ typedef struct dcc_stats {
   double total_ms;       /* wall time of the call incl. H2D/D2H when host pointers      */
   /* Per-phase device time (HIP events on the engine stream; filled only when
    * profiling is enabled with dcc_set_profiling) and the algorithmic bytes
-   * of each phase.  OCC phases: 0 = key-hash build, 1 = round-1 probe,
-   * 2 = rounds >= 2 (sum), 3 = prep + finalize; with the prefix peel:
-   * 0 = prefix solve, 1 = filter pass, 2 = survivor compaction + solve,
-   * 3 = prep + finalize; with the sweep solver: 0 = level-0 tile records +
-   * serial pass, 1 = level-0 filter, 2 = later levels (and any fallback),
-   * 3 = prep + finalize.  Calvin: 0 = build,
-   * 1 = grant groups, 2 = waves, 3 = prep + finalize. */
+   * of each phase.  OCC sweep: 0 = level-0 tile records + serial pass,
+   * 1 = level-0 filter, 2 = later levels (and any round-solver hand-off),
+   * 3 = prep + finalize; round solver only: 0 = key-hash build, 1 = round 1,
+   * 2 = rounds >= 2, 3 = prep + finalize.  Calvin: 0 = build, 1 = grant
+   * groups, 2 = waves, 3 = prep + finalize. */
   double phase_ms[4];
   uint64_t phase_bytes[4];
-  /* OCC prefix peel / sweep: prefix length solved first (0 =
-   * the epoch was decided by rounds alone) and txns that survived the first
-   * filter.  The sweep reports its levels in `rounds`. */
+  /* OCC sweep: the level-0 serial prefix (0 = the epoch was
+   * decided by rounds alone) and the txns that survived the level-0 filter.
+   * The sweep reports its levels in `rounds`. */
   uint64_t peel_prefix;
   uint64_t n_survivors;
-  uint32_t fallback;     /* 1: the stage solver handed this epoch to the round solver
-                            (its lists stopped shrinking); the decisions are the same */
+  uint32_t fallback;     /* sweep lists handed to the round solver (they stopped
+                            shrinking); the decisions are the same                    */
   uint32_t reserved2;
 } dcc_stats;
 
@@ -138,11 +136,12 @@ int dcc_set_profiling(dcc_ctx* ctx, int enable);
 /* Tuning knobs (defaults are the tuned values; for A/B measurement). */
 #define DCC_OPT_RECHECK 1     /* fold kill waves into rounds whose list has <= value txns */
 #define DCC_OPT_BATCH_MAX 2   /* max rounds enqueued between host synchronisations        */
-#define DCC_OPT_PEEL 3        /* OCC prefix peel: -1 auto (default), 0 off, > 0 prefix length */
-#define DCC_OPT_PEEL_MIN 4    /* auto peel applies to (sub-)batches of >= value txns        */
-#define DCC_OPT_SOLVER 5      /* OCC solver: 0 auto (sweep; key-sharded too), 1 fixed-point
-                                 rounds, 2 asynchronous, 3 sweep                           */
+#define DCC_OPT_SOLVER 5      /* OCC solver: 0 auto (= 3), 1 fixed-point rounds only, 3 sweep
+                                 (key-sharded too; hands lists that stop shrinking to the
+                                 round solver)                                             */
 #define DCC_OPT_SWEEP_LEVELS 6 /* sweep levels enqueued between host synchronisations       */
+#define DCC_OPT_HIST_MERGE 7  /* device history: delta pairs above which the delta merges into
+                                 the base (default 65536; the base/4 rule also applies)      */
 int dcc_set_option(dcc_ctx* ctx, int option, int64_t value);
 /* Pre-size device workspaces so a later call performs no allocation. */
 int dcc_reserve(dcc_ctx* ctx, uint64_t max_txn, uint64_t max_nnz);
@@ -183,10 +182,20 @@ int dcc_occ_validate_epoch(dcc_ctx* ctx, const dcc_batch* batch, uint8_t* out_rc
                            uint64_t* out_commit_tn, dcc_stats* out_stats);
 /* Committed write sets of earlier epochs (the `history` list, occ.h:62-64).
  * keys/tn are host arrays of n (key, tn) pairs; each pair is one write of the
- * committed txn numbered tn. */
+ * committed txn numbered tn.  The history is device-resident: epochs with
+ * DCC_OCC_APPEND_HISTORY append their committed writes on the device. */
 int dcc_occ_history_append(dcc_ctx* ctx, const uint64_t* keys, const uint64_t* tn, uint64_t n);
 int dcc_occ_history_clear(dcc_ctx* ctx);
 uint64_t dcc_occ_history_size(const dcc_ctx* ctx);
+/* Drop every history entry with tn <= tn_floor.  The reference never frees
+ * history (occ.cpp:277-286 only pushes); an entry is visible to
+ * a window (start_tn, finish_tn] only if tn > start_tn, so a caller that knows
+ * no txn will ever validate with start_tn < tn_floor can bound the history. */
+int dcc_occ_history_trim(dcc_ctx* ctx, uint64_t tn_floor);
+/* Copy the history's (key, tn) pairs to host arrays of cap entries (any
+ * order); *out_n = the history size.  DCC_ERANGE when cap is too small. */
+int dcc_occ_history_export(dcc_ctx* ctx, uint64_t* keys, uint64_t* tn, uint64_t cap,
+                           uint64_t* out_n);
 /* The commit counter `tnc` (occ.h:67). */
 int dcc_occ_set_tnc(dcc_ctx* ctx, uint64_t tnc);
 uint64_t dcc_occ_get_tnc(const dcc_ctx* ctx);
@@ -237,6 +246,29 @@ int dcc_occ_validate_snapshot(dcc_ctx* ctx, const dcc_batch* batch, const dcc_oc
  * out_wave is NULL). */
 int dcc_calvin_order_epoch(dcc_ctx* ctx, const dcc_batch* batch, uint32_t* out_group,
                            uint8_t* out_rc, uint32_t* out_wave, dcc_stats* out_stats);
+
+/* Rows still locked when the epoch starts.  Releases are asynchronous
+ * (Row_lock::lock_release, row_lock.cpp:219-372), so the lock thread may
+ * acquire an epoch while rows are still owned, or queued for, by txns of an
+ * earlier epoch.  The held prefix lists those requests per row in FIFO order:
+ * the current owners first, then the waiters (any interleaving of rows; the
+ * order among one row's requests is the queue order).  They enter the same
+ * per-row order ahead of the epoch's requests, so:
+ *   out_group[a] counts group boundaries from the row's owners (group 0 = the
+ *                current owners; an epoch request in group 0 joins them),
+ *   out_rc[i]    = RCOK iff every request of txn i joins its row's owners.
+ * Equal to replaying the prefix requests, then the epoch, through Row_lock in
+ * CALVIN mode.  Host arrays, or device arrays when batch->flags has
+ * DCC_DEVICE_PTRS.  Wave levels need an empty table: out_wave must be NULL
+ * (DCC_ENOTSUP otherwise).  Key-sharded: each rank passes its own rows. */
+typedef struct dcc_calvin_held {
+  uint64_t n;              /* held requests                                 */
+  const uint64_t* keys;    /* [n] rows                                      */
+  const uint8_t* acctype;  /* [n] access_t (RD/SCAN -> SH, else EX)         */
+} dcc_calvin_held;
+int dcc_calvin_order_epoch_held(dcc_ctx* ctx, const dcc_batch* batch, const dcc_calvin_held* held,
+                                uint32_t* out_group, uint8_t* out_rc, uint32_t* out_wave,
+                                dcc_stats* out_stats);
 
 /* ----------------------------------------------------- batch producers */
 /* Deterministic restatements of the reference workload generators

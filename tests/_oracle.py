@@ -142,3 +142,28 @@ def calvin(batch, literal=False):
     if r != 0:
         raise RuntimeError(f"oracle calvin failed: {r}")
     return g[:nnz], rc[:n], w[:n]
+
+
+def calvin_held(batch, held_keys, held_acctype, literal=True):
+    """Calvin against a pre-seeded lock table: the held requests (per row,
+    owners first, then waiters) are replayed through Row_lock first as
+    one-request pseudo-txns, then the epoch in sequence order (the literal
+    oracle_calvin_replay over the combined batch).  Returns the epoch's
+    (group u32[nnz], rc u8[n])."""
+    from deneva_amd import EpochBatch
+    h = int(len(held_keys))
+    n = batch.n_txn
+    off = _arr(batch.offsets, np.uint32).astype(np.uint64)
+    coff = np.concatenate([np.arange(h + 1, dtype=np.uint64), h + off[1:]]).astype(np.uint32)
+    ckeys = np.concatenate([np.asarray(held_keys, np.uint64), _arr(batch.keys, np.uint64)])
+    cat = np.concatenate([np.asarray(held_acctype, np.uint8), _arr(batch.acctype, np.uint8)])
+    if batch.order is None:
+        pos = np.arange(n, dtype=np.uint64)
+    else:
+        seq = np.argsort(_arr(batch.order, np.uint64), kind="stable")
+        pos = np.empty(n, np.uint64)
+        pos[seq] = np.arange(n, dtype=np.uint64)
+    corder = np.concatenate([np.arange(h, dtype=np.uint64), np.uint64(h) + pos])
+    cb = EpochBatch(coff, ckeys, cat, order=corder)
+    g, rc, _ = calvin(cb, literal=literal)
+    return g[h:], rc[h:]

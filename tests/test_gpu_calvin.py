@@ -157,3 +157,69 @@ def test_tpcc_calvin(engine, num_wh):
     # canonical TPC-C keys: table id in the top byte, packed to the bits that vary
     b = d.gen_tpcc(n_txn=50000 if num_wh == 4 else 262144, num_wh=num_wh)
     run(engine, b, waves=num_wh == 4)
+
+
+# ---------------------------------------------------------------- held prefix
+def run_held(engine, b, hk, ha, dev=False):
+    """Grant groups / readiness against a pre-seeded lock table vs the literal
+    Row_lock replay of (held requests, then the epoch)."""
+    bb = b.to_torch("cuda:0") if dev else b
+    if dev:
+        import torch
+        held = (torch.from_numpy(np.ascontiguousarray(hk, np.uint64).view(np.int64)).cuda(),
+                torch.from_numpy(np.ascontiguousarray(ha, np.uint8)).cuda())
+    else:
+        held = (hk, ha)
+    g, rc, _, st = engine.calvin_order_epoch(bb, want_group=True, held=held)
+    if dev:
+        g, rc = g.cpu().numpy(), rc.cpu().numpy()
+    eg, erc = orc.calvin_held(b, hk, ha)
+    assert np.array_equal(np.asarray(g).astype(np.uint32), eg), "group mismatch"
+    assert np.array_equal(np.asarray(rc), erc), "rc mismatch"
+    assert st["n_commit"] == int((erc == 0).sum())
+    return eg, erc
+
+
+def test_held_kat(engine):
+    # A held EX: a reader waits (group 1).  B held SH: a reader joins (group 0).
+    # C held SH with an EX waiter: a reader waits behind it (group 2, no barging).
+    A, B, C = 10, 20, 30
+    b = make_batch([[(A, RD)], [(B, RD)], [(C, RD)], [(B, WR)]])
+    hk = np.array([A, B, C, C], np.uint64)
+    ha = np.array([WR, RD, RD, WR], np.uint8)
+    eg, erc = run_held(engine, b, hk, ha)
+    assert list(eg) == [1, 0, 2, 1]
+    assert list(erc) == [3, 0, 3, 3]
+
+
+@pytest.mark.parametrize("dev", [False, True])
+@pytest.mark.parametrize("ordered", [False, True])
+def test_held_random(engine, dev, ordered):
+    rng = np.random.default_rng(21 + dev + 2 * ordered)
+    b = random_batch(rng, 20000, 12, 3000, types=(RD, WR, XP, SCAN), unique=False)
+    if ordered:
+        b.order = rng.integers(0, 5000, size=b.n_txn).astype(np.uint64)
+    h = 4000
+    hk = rng.integers(0, 3000, size=h).astype(np.uint64)
+    ha = rng.choice(np.array([RD, WR, XP, SCAN], np.uint8), size=h)
+    run_held(engine, b, hk, ha, dev=dev)
+
+
+def test_held_ycsb_full(engine):
+    b = d.gen_ycsb(n_txn=1 << 18, zipf_theta=0.9, part_cnt=16, chunk_txns=16384, want_home=True)
+    b.order = c4_order(b)
+    rng = np.random.default_rng(5)
+    # the previous epoch's hot rows are still held (owners + queued writers)
+    hot = np.unique(b.keys[: 1 << 14])
+    hk = np.repeat(hot[:2000], 2)
+    ha = np.tile(np.array([RD, WR], np.uint8), 2000)
+    eg, erc = run_held(engine, b, hk, ha)
+    _, erc0, _ = orc.calvin(b)
+    assert (erc == 0).sum() < (erc0 == 0).sum()  # held rows delay some txns
+
+
+def test_held_rejects_waves(engine):
+    b = make_batch([[(1, RD)]])
+    with pytest.raises(d.DccError):
+        engine.calvin_order_epoch(b, want_wave=True, held=(np.array([1], np.uint64),
+                                                            np.array([WR], np.uint8)))

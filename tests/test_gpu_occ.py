@@ -115,13 +115,13 @@ def test_chain_many_rounds(engine):
     assert list(rc[:6]) == [0, 2, 0, 2, 0, 2]
 
 
-@pytest.mark.parametrize("solver", [1, 2])
+@pytest.mark.parametrize("solver", [1, 3])
 def test_solvers_agree(engine, solver):
-    # every batch shape through both (sub-)batch solvers explicitly
-    from deneva_amd._abi import OPT_PEEL, OPT_SOLVER
+    # every batch shape through the round solver (the sweep's hand-off) and
+    # the sweep explicitly
+    from deneva_amd._abi import OPT_SOLVER
     rng = np.random.default_rng(33)
     engine.set_option(OPT_SOLVER, solver)
-    engine.set_option(OPT_PEEL, 0)
     try:
         run(engine, chain_batch(2000))
         run(engine, random_batch(rng, 5000, 64, 300, p_write=0.5))
@@ -130,7 +130,6 @@ def test_solvers_agree(engine, solver):
         run(engine, make_batch([[(7, WR)] for _ in range(40000)]))  # one segment > 32K writers
     finally:
         engine.set_option(OPT_SOLVER, 0)
-        engine.set_option(OPT_PEEL, -1)
 
 
 def test_history_window(engine):

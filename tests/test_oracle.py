@@ -175,3 +175,17 @@ def test_calvin_replay_equals_formula_random():
     b = d.gen_ycsb(n_txn=3000, zipf_theta=0.9, req_per_query=8, table_size=2000)
     b.order = np.random.default_rng(9).permutation(b.n_txn).astype(np.uint64)
     calvin_both(b)
+
+
+def test_calvin_held_prefix_kat():
+    """Held rows (row_lock.cpp:219-372: releases are asynchronous): the literal
+    replay of (held requests, then the epoch) and the per-row formula agree,
+    and give the hand-worked groups."""
+    A, B, C = 10, 20, 30
+    b = make_batch([[(A, RD)], [(B, RD)], [(C, RD)], [(B, WR)]])
+    hk = np.array([A, B, C, C], np.uint64)
+    ha = np.array([WR, RD, RD, WR], np.uint8)
+    g, rc = orc.calvin_held(b, hk, ha, literal=True)
+    g2, rc2 = orc.calvin_held(b, hk, ha, literal=False)
+    assert list(g) == [1, 0, 2, 1] and list(rc) == [3, 0, 3, 3]
+    assert np.array_equal(g, g2) and np.array_equal(rc, rc2)
