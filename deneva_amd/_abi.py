@@ -28,6 +28,7 @@ KEY_RESERVED = 0xFFFFFFFFFFFFFFFF
 GROUP_NONE = 0xFFFFFFFF
 DEVICE_PTRS = 0x1
 OCC_APPEND_HISTORY = 0x2
+MAAT_READ_AND_PREWRITE = 0x4
 UNIQUE_ID_BYTES = 128
 # int (*)(void* user, uint8_t* host_buf, uint64_t n): in-place MAX all-reduce
 EXCHANGE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint8), C.c_uint64)
@@ -188,6 +189,12 @@ _SIGS = [
     ("dcc_occ_history_export", C.c_int, [_P, _P, _P, C.c_uint64, _P]),
     ("dcc_occ_set_tnc", C.c_int, [_P, C.c_uint64]),
     ("dcc_occ_get_tnc", C.c_uint64, [_P]),
+    ("dcc_maat_validate_epoch", C.c_int, [_P, C.POINTER(Batch), _P, _P, C.POINTER(Stats)]),
+    ("dcc_maat_rows_set", C.c_int, [_P, _P, _P, _P, C.c_uint64]),
+    ("dcc_maat_rows_get", C.c_int, [_P, _P, _P, _P, C.c_uint64]),
+    ("dcc_maat_rows_clear", C.c_int, [_P]),
+    ("dcc_maat_rows_size", C.c_uint64, [_P]),
+    ("dcc_maat_alg_bytes", C.c_uint64, [C.c_uint64, C.c_uint64]),
     ("dcc_calvin_order_epoch", C.c_int, [_P, C.POINTER(Batch), _P, _P, _P, C.POINTER(Stats)]),
     ("dcc_calvin_order_epoch_held", C.c_int,
      [_P, C.POINTER(Batch), C.POINTER(CalvinHeld), _P, _P, _P, C.POINTER(Stats)]),

@@ -131,6 +131,11 @@ struct dcc_ctx {
   DevBuf cv_scratch, cv_agg, cv_group, cv_wave, cv_pgx, cv_gsx, cv_gsize, cv_done, cv_maxl;
   DevBuf cv_seq_b, cv_ok, cv_len, cv_off2, cv_tsum, cv_hkeys, cv_hat;
   DevBuf snap_top, snap_aoff, snap_aidx, snap_cnt;  // captured-snapshot validation
+  DevBuf mt_rk, mt_rlr, mt_rlw;                  // MaaT row table: key, last read / write ts
+  uint32_t mt_bits = 0;                          // log2 row-table slots (0: none yet)
+  uint64_t mt_rows = 0;                          // rows in the table
+  uint32_t mt_rows32 = 0;                        // upload source of the row counter
+  DevBuf mt_misc, mt_slot, mt_sval, mt_slot2, mt_sval2, mt_owner, mt_sfl, mt_stx, mt_txn, mt_agg;
   // commit counter tnc (occ.h:67)
   uint64_t tnc = 0;
 
@@ -165,6 +170,9 @@ struct dcc_ctx {
   int sweep_sharded(const DevBatch& d, int& next_level);
   int occ_sweep_finish(const DevBatch& d, int& next_level, bool& done, uint32_t maxlen);
   int occ_snapshot(const dcc_batch* b, const dcc_occ_snapshot* s, uint8_t* out_rc, dcc_stats* st);
+  // MaaT (maat.hip): row timestamp table + epoch workspaces
+  int maat_rows_reserve(uint64_t want);
+  int maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, dcc_stats* st);
   int calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint32_t* out_group,
                    uint8_t* out_rc, uint32_t* out_wave, dcc_stats* st);
 };

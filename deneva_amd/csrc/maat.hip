@@ -1,0 +1,738 @@
+// MaaT epoch validation on gfx950.
+//
+// Reference: Maat::validate / find_bound (concurrency_control/maat.cpp:29-191)
+// over the per-row soft locks of Row_maat (row_maat.cpp:38-316).  The epoch
+// model (include/dcc.h, dcc_maat_validate_epoch): every txn accesses its rows
+// (index order), then in index order each txn validates and commits or aborts.
+// A txn's copied uncommitted sets then hold only earlier txns, decided and
+// released by the time it validates, so the set loops of Maat::validate never
+// tighten anything; what reaches txn i is the forward validation of earlier
+// commits (Row_maat::commit) and the row timestamps copied at access time:
+//
+//   L_i = max(gwts_i + 1, grts_i + 1, max{cts_j + 1 : j < i committed, j read a row i wrote})
+//   U_i = min(UINT64_MAX, min{cts_j - 1 : j < i committed, j wrote a row i accessed})
+//   commit iff L_i < U_i, with commit timestamp cts_i = L_i (find_bound)
+//
+// (oracle/maat_ref.c restates both the literal replay and this formula).
+// L only grows and U only shrinks as earlier txns commit, so the GPU decides
+// by rounds: accesses sorted by row (stable, so index order within a row),
+// one segmented scan per round gives each (row, txn) group the max commit
+// timestamp of earlier committed readers, the min of earlier committed
+// writers and whether an earlier reader / writer is still undecided; a txn
+// whose known L >= known U aborts (final), one with no undecided relevant
+// predecessor commits at L, the rest wait for the next round.  The smallest
+// undecided txn always decides, so the rounds terminate.
+//
+// Row timestamps (timestamp_last_read / _write, row_maat.cpp:25-26) persist
+// in an HBM open-addressing table across epochs; committed txns raise them
+// with atomicMax at the end of the epoch (row_maat.cpp:251-262, 280-284).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+
+#include "dcc.h"
+#include "dcc_ctx.h"
+#include "dcc_device.h"
+#include "occ_kernels.h"
+#include "radix_sort.h"
+
+using namespace dcc;
+
+#define CK(expr)                                           \
+  do {                                                     \
+    hipError_t e_ = (expr);                                \
+    if (e_ != hipSuccess) return ctx->hip_fail(e_, #expr); \
+  } while (0)
+#define CR(expr)                 \
+  do {                           \
+    int r_ = (expr);             \
+    if (r_ != DCC_OK) return r_; \
+  } while (0)
+
+namespace {
+
+constexpr uint64_t U64MAX = ~0ull;
+constexpr uint32_t MT_ITEMS = 16;
+constexpr uint32_t MT_TILE = 256 * MT_ITEMS;
+constexpr uint32_t MT_RING = 64;          // per-round undecided counters
+constexpr uint32_t MT_BATCH = 4;          // rounds enqueued per host check
+constexpr uint8_t ST_UND = 0, ST_COM = 1, ST_ABO = 2;
+// sorted-position flags
+constexpr uint8_t F_R = 1, F_W = 2, F_LAST = 4, F_START = 8;
+constexpr uint32_t MT_ERR_OFF = 1, MT_ERR_KEY = 2, MT_ERR_FULL = 4;
+
+__device__ inline uint64_t mt_hash(uint64_t key, uint32_t bits) {
+  return (key * 0x9E3779B97F4A7C15ull) >> (64 - bits);
+}
+
+// ---------------------------------------------------------------- row table
+// insert-or-find the row of `key`; its lr / lw stay 0 until an epoch commits
+__device__ inline uint32_t mt_row(uint64_t* rk, uint32_t bits, uint64_t key, uint32_t* nrows,
+                                  uint32_t* err) {
+  const uint64_t mask = (1ull << bits) - 1;
+  uint64_t s = mt_hash(key, bits);
+  for (uint64_t q = 0; q <= mask; q++) {
+    const uint64_t v = rk[s];
+    if (v == key) return (uint32_t)s;
+    if (v == DCC_KEY_RESERVED) {
+      const unsigned long long prev = atomicCAS((unsigned long long*)&rk[s],
+                                                (unsigned long long)DCC_KEY_RESERVED,
+                                                (unsigned long long)key);
+      if (prev == DCC_KEY_RESERVED) {
+        atomicAdd(nrows, 1u);
+        return (uint32_t)s;
+      }
+      if (prev == key) return (uint32_t)s;
+    }
+    s = (s + 1) & mask;
+  }
+  atomicOr(err, MT_ERR_FULL);
+  return 0;
+}
+
+// rehash: every row of the old table into the new one (values carried)
+__global__ __launch_bounds__(256) void k_mt_rehash(const uint64_t* ok, const uint64_t* olr,
+                                                   const uint64_t* olw, uint64_t ocap, uint64_t* nk,
+                                                   uint64_t* nlr, uint64_t* nlw, uint32_t nbits,
+                                                   uint32_t* nrows, uint32_t* err) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < ocap; i += (uint64_t)gridDim.x * 256) {
+    const uint64_t k = ok[i];
+    if (k == DCC_KEY_RESERVED) continue;
+    const uint32_t s = mt_row(nk, nbits, k, nrows, err);
+    nlr[s] = olr[i];
+    nlw[s] = olw[i];
+  }
+}
+
+// host-seeded rows (dcc_maat_rows_set): insert and overwrite the timestamps
+__global__ __launch_bounds__(256) void k_mt_seed(const uint64_t* keys, const uint64_t* lr,
+                                                 const uint64_t* lw, uint64_t n, uint64_t* rk,
+                                                 uint64_t* rlr, uint64_t* rlw, uint32_t bits,
+                                                 uint32_t* nrows, uint32_t* err) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+    if (keys[i] == DCC_KEY_RESERVED) {
+      atomicOr(err, MT_ERR_KEY);
+      continue;
+    }
+    const uint32_t s = mt_row(rk, bits, keys[i], nrows, err);
+    rlr[s] = lr[i];
+    rlw[s] = lw[i];
+  }
+}
+__global__ __launch_bounds__(256) void k_mt_get(const uint64_t* keys, uint64_t n, const uint64_t* rk,
+                                                const uint64_t* rlr, const uint64_t* rlw,
+                                                uint32_t bits, uint64_t* lr, uint64_t* lw) {
+  const uint64_t mask = (1ull << bits) - 1;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+    const uint64_t key = keys[i];
+    uint64_t s = mt_hash(key, bits), a = 0, b = 0;
+    for (uint64_t q = 0; q <= mask; q++) {
+      const uint64_t v = rk[s];
+      if (v == key) {
+        a = rlr[s];
+        b = rlw[s];
+        break;
+      }
+      if (v == DCC_KEY_RESERVED) break;
+      s = (s + 1) & mask;
+    }
+    lr[i] = a;
+    lw[i] = b;
+  }
+}
+
+// ---------------------------------------------------------------- base
+// One thread per txn: each access enters its row (slot id), owner and sort
+// value; the txn's lower bound from the copied row timestamps: gwts over rows
+// read or written, grts over rows written (Row_maat::read / prewrite copy
+// them at access time, row_maat.cpp:119-121, 159-165; Maat::validate raises
+// lower past them, maat.cpp:47-50, 70-73).
+struct BaseArgs {
+  uint64_t n, nnz;
+  const uint32_t* off;
+  const uint64_t* keys;
+  const uint8_t* at;
+  uint32_t rw_all;
+  uint64_t* rk;
+  const uint64_t* rlr;
+  const uint64_t* rlw;
+  uint32_t bits;
+  uint32_t* nrows;
+  uint32_t* slot;   // [nnz] row slot per access (sort key; pre-zeroed)
+  uint32_t* owner;  // [nnz] txn of each access (pre-zeroed)
+  uint64_t* base;   // [n]
+  uint8_t* state;   // [n] zeroed here
+  uint64_t* lacc;   // [n] 0
+  uint64_t* uacc;   // [n] U64MAX
+  uint32_t* pend;   // [n] 0
+  uint32_t* err;
+};
+__global__ __launch_bounds__(256) void k_mt_base(BaseArgs a) {
+  const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= a.n) return;
+  const uint64_t o0 = min((uint64_t)a.off[t], a.nnz), o1 = min((uint64_t)a.off[t + 1], a.nnz);
+  if (a.off[t + 1] < a.off[t] || o1 - o0 > MAX_TXN_LEN) atomicOr(a.err, MT_ERR_OFF);
+  uint64_t gw = 0, gr = 0;
+  if ((t == 0 && a.off[0] != 0) || (t + 1 == a.n && a.off[a.n] != a.nnz)) atomicOr(a.err, MT_ERR_OFF);
+  for (uint64_t x = o0; x < o1; x++) {
+    const uint64_t key = a.keys[x];
+    uint32_t s = 0;
+    if (key == DCC_KEY_RESERVED) atomicOr(a.err, MT_ERR_KEY);
+    else s = mt_row(a.rk, a.bits, key, a.nrows, a.err);
+    a.slot[x] = s;
+    a.owner[x] = (uint32_t)t;
+    const uint8_t ty = a.at[x];
+    const bool rd = a.rw_all || ty == DCC_RD, wr = a.rw_all || ty == DCC_WR;
+    if (rd || wr) gw = max(gw, a.rlw[s]);
+    if (wr) gr = max(gr, a.rlr[s]);
+  }
+  a.base[t] = max(gw, gr) + 1;
+  a.state[t] = ST_UND;
+  a.lacc[t] = 0;
+  a.uacc[t] = U64MAX;
+  a.pend[t] = 0;
+}
+
+__global__ __launch_bounds__(256) void k_mt_iota(uint32_t* v, uint64_t m) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < m; i += (uint64_t)gridDim.x * 256)
+    v[i] = (uint32_t)i;
+}
+
+// Group flags per sorted position: a (row, txn) group is a run of equal
+// (slot, owner); its last position carries the OR of its R / W bits.
+__global__ __launch_bounds__(256) void k_mt_groups(const uint32_t* ss, const uint32_t* sv,
+                                                   const uint32_t* owner, const uint8_t* at,
+                                                   uint32_t rw_all, uint64_t m, uint8_t* sfl,
+                                                   uint32_t* stx) {
+  for (uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x; p < m; p += (uint64_t)gridDim.x * 256) {
+    const uint32_t s = ss[p], t = owner[sv[p]];
+    uint8_t f = 0;
+    if (p == 0 || ss[p - 1] != s) f |= F_START;
+    const bool last = p + 1 == m || ss[p + 1] != s || owner[sv[p + 1]] != t;
+    if (last) {
+      f |= F_LAST;
+      for (uint64_t q = p;; q--) {  // the group's accesses (<= MAX_ROW_PER_TXN)
+        const uint8_t ty = at[sv[q]];
+        if (rw_all || ty == DCC_RD) f |= F_R;
+        if (rw_all || ty == DCC_WR) f |= F_W;
+        if (q == 0 || ss[q - 1] != s || owner[sv[q - 1]] != t) break;
+      }
+    }
+    sfl[p] = f;
+    stx[p] = t;
+  }
+}
+
+// ---------------------------------------------------------------- round scan
+// State of an interval since the last row start: flag = holds a row start;
+// rmax / wmin over committed readers / writers; und bit 0 / 1 = an undecided
+// reader / writer.  Contributions sit at each group's last position, so the
+// exclusive prefix at a group excludes the group's own txn.
+struct Ms {
+  uint32_t flag, und;
+  uint64_t rmax, wmin;
+};
+__device__ inline Ms ms_id() { return Ms{0, 0, 0, U64MAX}; }
+__device__ inline Ms ms_comb(const Ms& A, const Ms& B) {
+  if (B.flag) return B;
+  return Ms{A.flag, A.und | B.und, max(A.rmax, B.rmax), min(A.wmin, B.wmin)};
+}
+__device__ inline Ms ms_elem(uint8_t f, uint8_t st, uint64_t cts) {
+  Ms e = ms_id();
+  if (f & F_START) e.flag = 1;
+  if (f & F_LAST) {
+    if (st == ST_COM) {
+      if (f & F_R) e.rmax = cts;
+      if (f & F_W) e.wmin = cts;
+    } else if (st == ST_UND) {
+      e.und = ((f & F_R) ? 1u : 0u) | ((f & F_W) ? 2u : 0u);
+    }
+  }
+  return e;
+}
+
+struct MtRoundArgs {
+  uint64_t m, n;
+  const uint8_t* sfl;
+  const uint32_t* stx;
+  const uint8_t* state;
+  const uint64_t* cts;
+  uint64_t* lacc;
+  uint64_t* uacc;
+  uint32_t* pend;
+  Ms* agg;
+};
+
+__device__ inline Ms block_reduce_ms(Ms v, Ms* s) {
+  s[threadIdx.x] = v;
+  __syncthreads();
+  for (uint32_t w = 1; w < 256; w <<= 1) {
+    if ((threadIdx.x & (2 * w - 1)) == 0) s[threadIdx.x] = ms_comb(s[threadIdx.x], s[threadIdx.x + w]);
+    __syncthreads();
+  }
+  return s[0];
+}
+__device__ inline Ms block_excl_ms(Ms v, Ms* s) {
+  s[threadIdx.x] = v;
+  __syncthreads();
+  for (uint32_t d = 1; d < 256; d <<= 1) {
+    Ms r = s[threadIdx.x];
+    if (threadIdx.x >= d) r = ms_comb(s[threadIdx.x - d], r);
+    __syncthreads();
+    s[threadIdx.x] = r;
+    __syncthreads();
+  }
+  const Ms ex = threadIdx.x ? s[threadIdx.x - 1] : ms_id();
+  __syncthreads();
+  return ex;
+}
+
+__global__ __launch_bounds__(256) void k_mt_up(MtRoundArgs a) {
+  __shared__ Ms s[256];
+  const uint64_t p0 = (uint64_t)blockIdx.x * MT_TILE + (uint64_t)threadIdx.x * MT_ITEMS;
+  Ms acc = ms_id();
+#pragma unroll
+  for (uint32_t i = 0; i < MT_ITEMS; i++) {
+    const uint64_t p = p0 + i;
+    if (p < a.m) {
+      const uint8_t f = a.sfl[p];
+      uint8_t st = ST_ABO;
+      uint64_t c = 0;
+      if (f & F_LAST) {
+        const uint32_t t = a.stx[p];
+        st = a.state[t];
+        if (st == ST_COM) c = a.cts[t];
+      }
+      acc = ms_comb(acc, ms_elem(f, st, c));
+    }
+  }
+  const Ms r = block_reduce_ms(acc, s);
+  if (threadIdx.x == 0) a.agg[blockIdx.x] = r;
+}
+
+__global__ __launch_bounds__(256) void k_mt_top(Ms* agg, uint32_t tiles) {
+  __shared__ Ms s[256];
+  __shared__ Ms s_last;
+  Ms carry = ms_id();
+  for (uint32_t c0 = 0; c0 < tiles; c0 += 256) {
+    const uint32_t i = c0 + threadIdx.x;
+    const Ms v = i < tiles ? agg[i] : ms_id();
+    const Ms ex = block_excl_ms(v, s);
+    if (i < tiles) agg[i] = ms_comb(carry, ex);
+    if (threadIdx.x == 255) s_last = ms_comb(ex, v);
+    __syncthreads();
+    carry = ms_comb(carry, s_last);
+    __syncthreads();
+  }
+}
+
+// exclusive prefix per position; every group's last position of an
+// undecided txn folds what the earlier txns of its row imply into the txn:
+// L from committed readers of a row it writes, U from committed writers of a
+// row it touches, pending from undecided ones
+__global__ __launch_bounds__(256) void k_mt_down(MtRoundArgs a) {
+  __shared__ Ms s[256];
+  const uint64_t p0 = (uint64_t)blockIdx.x * MT_TILE + (uint64_t)threadIdx.x * MT_ITEMS;
+  uint8_t f[MT_ITEMS], st[MT_ITEMS];
+  uint32_t tx[MT_ITEMS];
+  uint64_t c[MT_ITEMS];
+  Ms acc = ms_id();
+#pragma unroll
+  for (uint32_t i = 0; i < MT_ITEMS; i++) {
+    const uint64_t p = p0 + i;
+    f[i] = 0;
+    st[i] = ST_ABO;
+    tx[i] = 0;
+    c[i] = 0;
+    if (p < a.m) {
+      f[i] = a.sfl[p];
+      if (f[i] & F_LAST) {
+        tx[i] = a.stx[p];
+        st[i] = a.state[tx[i]];
+        if (st[i] == ST_COM) c[i] = a.cts[tx[i]];
+      }
+      acc = ms_comb(acc, ms_elem(f[i], st[i], c[i]));
+    }
+  }
+  Ms run = ms_comb(a.agg[blockIdx.x], block_excl_ms(acc, s));
+#pragma unroll
+  for (uint32_t i = 0; i < MT_ITEMS; i++) {
+    const uint64_t p = p0 + i;
+    if (p >= a.m) break;
+    if (f[i] & F_START) run = Ms{1, 0, 0, U64MAX};  // own group excluded: contributions at its end
+    // a group that only scans / XPs its row is not on the row's soft locks
+    if ((f[i] & F_LAST) && (f[i] & (F_R | F_W)) && st[i] == ST_UND) {
+      const uint32_t t = tx[i];
+      if ((f[i] & F_W) && run.rmax) atomicMax((unsigned long long*)&a.lacc[t], run.rmax + 1);
+      if (run.wmin != U64MAX) atomicMin((unsigned long long*)&a.uacc[t], run.wmin - 1);
+      if ((run.und & 2u) || ((f[i] & F_W) && (run.und & 1u))) atomicOr(&a.pend[t], 1u);
+    }
+    run = ms_comb(run, ms_elem(f[i] & ~F_START, st[i], c[i]));
+  }
+}
+
+// decide: abort when the known bounds are already empty, commit when no
+// relevant predecessor is undecided; reset the accumulators
+__global__ __launch_bounds__(256) void k_mt_decide(uint64_t n, const uint64_t* base, uint8_t* state,
+                                                   uint64_t* cts, uint64_t* lacc, uint64_t* uacc,
+                                                   uint32_t* pend, uint32_t* und_out,
+                                                   uint32_t* und_zero) {
+  __shared__ uint32_t sh[4];
+  uint32_t und = 0;
+  for (uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x; t < n; t += (uint64_t)gridDim.x * 256) {
+    if (state[t] != ST_UND) continue;
+    const uint64_t L = max(base[t], lacc[t]);
+    const uint64_t U = uacc[t];
+    if (L >= U) {
+      state[t] = ST_ABO;
+    } else if (!pend[t]) {
+      state[t] = ST_COM;
+      cts[t] = L;
+    } else {
+      und++;
+    }
+    lacc[t] = 0;
+    uacc[t] = U64MAX;
+    pend[t] = 0;
+  }
+  for (int d = 32; d > 0; d >>= 1) und += __shfl_xor(und, d);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = und;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t s = sh[0] + sh[1] + sh[2] + sh[3];
+    if (s) atomicAdd(und_out, s);
+    if (blockIdx.x == 0) *und_zero = 0;
+  }
+}
+
+// ---------------------------------------------------------------- finish
+// RC bytes, commit timestamps, counts; committed txns raise their rows'
+// timestamps (Row_maat::commit, row_maat.cpp:251-262, 280-284)
+struct FinArgs {
+  uint64_t n, nnz;
+  const uint32_t* off;
+  const uint8_t* at;
+  uint32_t rw_all;
+  const uint8_t* state;
+  const uint64_t* cts;
+  const uint32_t* slot;
+  uint64_t* rlr;
+  uint64_t* rlw;
+  uint8_t* rc;
+  uint64_t* cts_out;
+  uint32_t* cnt;  // [0] commits, [1] undecided, [2] write accesses
+};
+__global__ __launch_bounds__(256) void k_mt_finish(FinArgs a) {
+  __shared__ uint32_t sh[3][4];
+  uint32_t com = 0, und = 0, nw = 0;
+  for (uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x; t < a.n; t += (uint64_t)gridDim.x * 256) {
+    const uint8_t s = a.state[t];
+    const bool ok = s == ST_COM;
+    a.rc[t] = ok ? DCC_RC_RCOK : DCC_RC_ABORT;
+    if (a.cts_out) a.cts_out[t] = ok ? a.cts[t] : 0;
+    com += ok;
+    und += s == ST_UND;
+    const uint64_t o0 = min((uint64_t)a.off[t], a.nnz), o1 = min((uint64_t)a.off[t + 1], a.nnz);
+    const uint64_t c = ok ? a.cts[t] : 0;
+    for (uint64_t x = o0; x < o1; x++) {
+      const uint8_t ty = a.at[x];
+      nw += ty == DCC_WR;
+      if (!ok) continue;
+      const uint32_t sl = a.slot[x];
+      if (a.rw_all || ty == DCC_RD) atomicMax((unsigned long long*)&a.rlr[sl], c);
+      if (a.rw_all || ty == DCC_WR) atomicMax((unsigned long long*)&a.rlw[sl], c);
+    }
+  }
+  for (int d = 32; d > 0; d >>= 1) {
+    com += __shfl_xor(com, d);
+    und += __shfl_xor(und, d);
+    nw += __shfl_xor(nw, d);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    sh[0][threadIdx.x >> 6] = com;
+    sh[1][threadIdx.x >> 6] = und;
+    sh[2][threadIdx.x >> 6] = nw;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    const uint32_t v = sh[threadIdx.x][0] + sh[threadIdx.x][1] + sh[threadIdx.x][2] + sh[threadIdx.x][3];
+    if (v) atomicAdd(&a.cnt[threadIdx.x], v);
+  }
+}
+
+inline unsigned g1(uint64_t n, uint64_t cap = 8192) {
+  uint64_t g = (n + 255) / 256;
+  return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(g, cap));
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- host
+// Row table capacity for `want` rows at <= 50 % load (rehash on growth).
+int dcc_ctx::maat_rows_reserve(uint64_t want) {
+  dcc_ctx* ctx = this;
+  uint32_t* cnt = (uint32_t*)mt_misc.p;  // [0] rows, [1] errors
+  if (mt_bits && (2 * want) <= (1ull << mt_bits)) return DCC_OK;
+  uint32_t bits = std::max<uint32_t>(mt_bits, 12);
+  while ((1ull << bits) < 2 * want) bits++;
+  if (bits > 31) return fail(DCC_ERANGE, "maat: row table exceeds 2^31 slots");
+  const uint64_t cap = 1ull << bits;
+  DevBuf nk, nlr, nlw;
+  CR(nk.ensure(this, cap * 8, "maat row keys"));
+  CR(nlr.ensure(this, cap * 8, "maat row lr"));
+  CR(nlw.ensure(this, cap * 8, "maat row lw"));
+  CK(hipMemsetAsync(nk.p, 0xFF, cap * 8, stream));
+  CK(hipMemsetAsync(nlr.p, 0, cap * 8, stream));
+  CK(hipMemsetAsync(nlw.p, 0, cap * 8, stream));
+  CK(hipMemsetAsync(cnt, 0, 4, stream));
+  if (mt_bits) {
+    const uint64_t ocap = 1ull << mt_bits;
+    k_mt_rehash<<<g1(ocap), 256, 0, stream>>>((const uint64_t*)mt_rk.p, (const uint64_t*)mt_rlr.p,
+                                              (const uint64_t*)mt_rlw.p, ocap, (uint64_t*)nk.p,
+                                              (uint64_t*)nlr.p, (uint64_t*)nlw.p, bits, cnt, cnt + 1);
+    CK(hipGetLastError());
+  }
+  CK(hipStreamSynchronize(stream));
+  mt_rk.release();
+  mt_rlr.release();
+  mt_rlw.release();
+  mt_rk = nk;
+  mt_rlr = nlr;
+  mt_rlw = nlw;
+  mt_bits = bits;
+  return DCC_OK;
+}
+
+int dcc_ctx::maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, dcc_stats* st) {
+  dcc_ctx* ctx = this;
+  const auto t_wall0 = std::chrono::steady_clock::now();
+  CR(check_batch(b));
+  if (comm_ranks() > 1) return fail(DCC_ENOTSUP, "maat: single-GPU engine");
+  const bool dev = (b->flags & DCC_DEVICE_PTRS) != 0;
+  const uint32_t rw_all = (b->flags & DCC_MAAT_READ_AND_PREWRITE) ? 1u : 0u;
+  dcc_stats S;
+  memset(&S, 0, sizeof S);
+  S.n_shards = 1;
+  if (b->n_txn == 0) {
+    if (st) *st = S;
+    return DCC_OK;
+  }
+  DevBatch d;
+  CR(stage_batch(b, d));
+  const uint64_t n = d.n, m = d.nnz;
+  CR(mt_misc.ensure(this, 64 + MT_RING * 4, "maat counters"));
+  uint32_t* cnt = (uint32_t*)mt_misc.p;  // [0] rows, [1] err, [2..4] finish counts, ring at 8
+  uint32_t* ring = cnt + 8;
+  // the row counter survives between epochs in mt_rows (host copy)
+  CR(maat_rows_reserve(mt_rows + m));
+  mt_rows32 = (uint32_t)mt_rows;
+  CK(hipMemcpyAsync(cnt, &mt_rows32, 4, hipMemcpyHostToDevice, stream));
+  CK(hipMemsetAsync(cnt + 1, 0, 4 * 7 + MT_RING * 4, stream));
+  const uint64_t mm = std::max<uint64_t>(m, 1);
+  CR(mt_slot.ensure(this, mm * 4, "maat slots"));
+  CR(mt_sval.ensure(this, mm * 4, "maat sort values"));
+  CR(mt_slot2.ensure(this, mm * 4, "maat slots b"));
+  CR(mt_sval2.ensure(this, mm * 4, "maat sort values b"));
+  CR(mt_owner.ensure(this, mm * 4, "maat owners"));
+  CR(mt_sfl.ensure(this, mm, "maat flags"));
+  CR(mt_stx.ensure(this, mm * 4, "maat sorted txns"));
+  CR(mt_txn.ensure(this, n * (8 * 4 + 4 + 1) + 64, "maat txn state"));
+  CR(cv_scratch.ensure(this, rs_scratch_words(mm) * 4 + 64, "radix scratch"));
+  const uint64_t tiles = (m + MT_TILE - 1) / MT_TILE;
+  CR(mt_agg.ensure(this, std::max<uint64_t>(1, tiles) * sizeof(Ms), "maat scan"));
+  uint64_t* base = (uint64_t*)mt_txn.p;
+  uint64_t* cts = base + n;
+  uint64_t* lacc = cts + n;
+  uint64_t* uacc = lacc + n;
+  uint32_t* pend = (uint32_t*)(uacc + n);
+  uint8_t* state = (uint8_t*)(pend + n);
+  CR(rc.ensure(this, n + 16, "rc"));
+  uint8_t* rc_dev = (dev && out_rc) ? out_rc : (uint8_t*)rc.p;
+  uint64_t* cts_dev = nullptr;
+  if (out_cts) {
+    if (dev) {
+      cts_dev = out_cts;
+    } else {
+      CR(tn.ensure(this, n * 8, "maat cts"));
+      cts_dev = (uint64_t*)tn.p;
+    }
+  }
+
+  CK(hipEventRecord(ev0, stream));
+  // every access gets a slot / owner / sort value even in a malformed batch
+  CK(hipMemsetAsync(mt_slot.p, 0, mm * 4, stream));
+  CK(hipMemsetAsync(mt_owner.p, 0, mm * 4, stream));
+  k_mt_iota<<<g1(mm), 256, 0, stream>>>((uint32_t*)mt_sval.p, m);
+  BaseArgs ba{n,    m,    d.off,   d.keys,  d.acctype, rw_all, (uint64_t*)mt_rk.p,
+              (const uint64_t*)mt_rlr.p,     (const uint64_t*)mt_rlw.p, mt_bits, cnt,
+              (uint32_t*)mt_slot.p, (uint32_t*)mt_owner.p, base, state, lacc, uacc, pend,
+              cnt + 1};
+  k_mt_base<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(ba);
+  // rows sorted by slot (stable: index order within a row)
+  uint32_t* kb[2] = {(uint32_t*)mt_slot.p, (uint32_t*)mt_slot2.p};
+  uint32_t* vb[2] = {(uint32_t*)mt_sval.p, (uint32_t*)mt_sval2.p};
+  int cur = 0;
+  if (m) {
+    // the base kernel's slots are needed again at the end: sort a copy
+    CK(hipMemcpyAsync(mt_slot2.p, mt_slot.p, m * 4, hipMemcpyDeviceToDevice, stream));
+    uint32_t* kk[2] = {(uint32_t*)mt_slot2.p, (uint32_t*)mt_stx.p};  // stx doubles as ping-pong
+    cur = radix_sort_u32(kk, vb, m, mt_bits, (uint32_t*)cv_scratch.p, stream);
+    kb[0] = kk[cur];
+    // the sorted slots must not live in stx, which k_mt_groups writes
+    if (kb[0] == (uint32_t*)mt_stx.p) {
+      CK(hipMemcpyAsync(mt_slot2.p, mt_stx.p, m * 4, hipMemcpyDeviceToDevice, stream));
+      kb[0] = (uint32_t*)mt_slot2.p;
+    }
+    k_mt_groups<<<g1(m), 256, 0, stream>>>(kb[0], vb[cur], (const uint32_t*)mt_owner.p, d.acctype,
+                                           rw_all, m, (uint8_t*)mt_sfl.p, (uint32_t*)mt_stx.p);
+  }
+  CK(hipGetLastError());
+
+  // ---- rounds, MT_BATCH between host checks
+  MtRoundArgs ra{m, n, (const uint8_t*)mt_sfl.p, (const uint32_t*)mt_stx.p, state, cts, lacc, uacc,
+               pend, (Ms*)mt_agg.p};
+  uint32_t rounds = 0;
+  bool done = false;
+  while (!done) {
+    const uint32_t k0 = rounds;
+    for (uint32_t q = 0; q < MT_BATCH; q++, rounds++) {
+      if (m) {
+        k_mt_up<<<(unsigned)tiles, 256, 0, stream>>>(ra);
+        k_mt_top<<<1, 256, 0, stream>>>((Ms*)mt_agg.p, (uint32_t)tiles);
+        k_mt_down<<<(unsigned)tiles, 256, 0, stream>>>(ra);
+      }
+      k_mt_decide<<<g1(n, 2048), 256, 0, stream>>>(n, base, state, cts, lacc, uacc, pend,
+                                                   &ring[rounds % MT_RING],
+                                                   &ring[(rounds + 1) % MT_RING]);
+    }
+    CK(hipGetLastError());
+    CK(hipMemcpyAsync(hmisc, ring, MT_RING * 4, hipMemcpyDeviceToHost, stream));
+    CK(hipStreamSynchronize(stream));
+    const uint32_t* hr = (const uint32_t*)hmisc;
+    for (uint32_t q = k0; q < rounds; q++)
+      if (hr[q % MT_RING] == 0) {
+        rounds = q + 1;
+        done = true;
+        break;
+      }
+    if (!done && rounds > n + 8) return fail(DCC_EIO, "maat: rounds did not converge");
+  }
+  FinArgs fa{n, m, d.off, d.acctype, rw_all, state, cts, (const uint32_t*)mt_slot.p,
+             (uint64_t*)mt_rlr.p, (uint64_t*)mt_rlw.p, rc_dev, cts_dev, cnt + 2};
+  k_mt_finish<<<g1(n, 2048), 256, 0, stream>>>(fa);
+  CK(hipGetLastError());
+  CK(hipEventRecord(ev1, stream));
+  if (!dev) {
+    if (out_rc) CK(hipMemcpyAsync(out_rc, rc_dev, n, hipMemcpyDeviceToHost, stream));
+    if (out_cts) CK(hipMemcpyAsync(out_cts, cts_dev, n * 8, hipMemcpyDeviceToHost, stream));
+  }
+  CK(hipMemcpyAsync(hmisc, cnt, 32, hipMemcpyDeviceToHost, stream));
+  CK(hipStreamSynchronize(stream));
+  const uint32_t* hc = (const uint32_t*)hmisc;
+  if (hc[1] & MT_ERR_OFF) return fail(DCC_EINVAL, "batch: malformed offsets");
+  if (hc[1] & MT_ERR_KEY) return fail(DCC_EINVAL, "batch: key equal to DCC_KEY_RESERVED");
+  if (hc[1] & MT_ERR_FULL) return fail(DCC_EIO, "maat: row table full");
+  if (hc[3]) return fail(DCC_EIO, "maat: %u undecided transactions", hc[3]);
+  mt_rows = hc[0];
+  float ms = 0;
+  CK(hipEventElapsedTime(&ms, ev0, ev1));
+  S.rounds = rounds;
+  S.n_commit = hc[2];
+  S.n_abort = n - hc[2];
+  S.nnz_w = hc[4];
+  S.alg_bytes = dcc_maat_alg_bytes(n, m);
+  S.device_ms = ms;
+  S.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_wall0)
+                   .count();
+  if (st) *st = S;
+  return DCC_OK;
+}
+
+extern "C" uint64_t dcc_maat_alg_bytes(uint64_t n_txn, uint64_t nnz) {
+  // offsets, key + acctype per access, one 24-B row-table slot read (key,
+  // lr, lw) and one timestamp update per access, RC byte + commit timestamp
+  return 4 * (n_txn + 1) + 9 * nnz + 24 * nnz + 8 * nnz + n_txn + 8 * n_txn;
+}
+
+extern "C" int dcc_maat_validate_epoch(dcc_ctx* ctx, const dcc_batch* batch, uint8_t* out_rc,
+                                       uint64_t* out_commit_ts, dcc_stats* out_stats) {
+  if (!ctx) return DCC_EINVAL;
+  if (hipSetDevice(ctx->device) != hipSuccess) return DCC_ENODEV;
+  return ctx->maat_epoch(batch, out_rc, out_commit_ts, out_stats);
+}
+
+extern "C" int dcc_maat_rows_clear(dcc_ctx* ctx) {
+  if (!ctx) return DCC_EINVAL;
+  if (hipSetDevice(ctx->device) != hipSuccess) return DCC_ENODEV;
+  if (ctx->mt_bits) {
+    const uint64_t cap = 1ull << ctx->mt_bits;
+    if (hipMemsetAsync(ctx->mt_rk.p, 0xFF, cap * 8, ctx->stream) != hipSuccess ||
+        hipMemsetAsync(ctx->mt_rlr.p, 0, cap * 8, ctx->stream) != hipSuccess ||
+        hipMemsetAsync(ctx->mt_rlw.p, 0, cap * 8, ctx->stream) != hipSuccess ||
+        hipStreamSynchronize(ctx->stream) != hipSuccess)
+      return ctx->hip_fail(hipGetLastError(), "maat rows clear");
+  }
+  ctx->mt_rows = 0;
+  return DCC_OK;
+}
+
+extern "C" int dcc_maat_rows_set(dcc_ctx* ctx, const uint64_t* keys, const uint64_t* last_read,
+                                 const uint64_t* last_write, uint64_t n) {
+  if (!ctx || (n && (!keys || !last_read || !last_write))) return DCC_EINVAL;
+  if (n == 0) return DCC_OK;
+  if (hipSetDevice(ctx->device) != hipSuccess) return DCC_ENODEV;
+  CR(ctx->mt_misc.ensure(ctx, 64 + MT_RING * 4, "maat counters"));
+  CR(ctx->maat_rows_reserve(ctx->mt_rows + n));
+  DevBuf tmp;
+  CR(tmp.ensure(ctx, n * 24, "maat seed"));
+  uint64_t* t = (uint64_t*)tmp.p;
+  uint32_t* cnt = (uint32_t*)ctx->mt_misc.p;
+  ctx->mt_rows32 = (uint32_t)ctx->mt_rows;
+  CK(hipMemcpyAsync(cnt, &ctx->mt_rows32, 4, hipMemcpyHostToDevice, ctx->stream));
+  CK(hipMemsetAsync(cnt + 1, 0, 4, ctx->stream));
+  CK(hipMemcpyAsync(t, keys, n * 8, hipMemcpyHostToDevice, ctx->stream));
+  CK(hipMemcpyAsync(t + n, last_read, n * 8, hipMemcpyHostToDevice, ctx->stream));
+  CK(hipMemcpyAsync(t + 2 * n, last_write, n * 8, hipMemcpyHostToDevice, ctx->stream));
+  k_mt_seed<<<g1(n), 256, 0, ctx->stream>>>(t, t + n, t + 2 * n, n, (uint64_t*)ctx->mt_rk.p,
+                                            (uint64_t*)ctx->mt_rlr.p, (uint64_t*)ctx->mt_rlw.p,
+                                            ctx->mt_bits, cnt, cnt + 1);
+  CK(hipGetLastError());
+  uint32_t hc[2];
+  CK(hipMemcpyAsync(hc, cnt, 8, hipMemcpyDeviceToHost, ctx->stream));
+  CK(hipStreamSynchronize(ctx->stream));
+  tmp.release();
+  if (hc[1] & MT_ERR_KEY) return ctx->fail(DCC_EINVAL, "maat rows: key equal to DCC_KEY_RESERVED");
+  if (hc[1] & MT_ERR_FULL) return ctx->fail(DCC_EIO, "maat: row table full");
+  ctx->mt_rows = hc[0];
+  return DCC_OK;
+}
+
+extern "C" int dcc_maat_rows_get(dcc_ctx* ctx, const uint64_t* keys, uint64_t* last_read,
+                                 uint64_t* last_write, uint64_t n) {
+  if (!ctx || (n && (!keys || !last_read || !last_write))) return DCC_EINVAL;
+  if (n == 0) return DCC_OK;
+  if (hipSetDevice(ctx->device) != hipSuccess) return DCC_ENODEV;
+  if (!ctx->mt_bits) {
+    memset(last_read, 0, n * 8);
+    memset(last_write, 0, n * 8);
+    return DCC_OK;
+  }
+  DevBuf tmp;
+  CR(tmp.ensure(ctx, n * 24, "maat get"));
+  uint64_t* t = (uint64_t*)tmp.p;
+  CK(hipMemcpyAsync(t, keys, n * 8, hipMemcpyHostToDevice, ctx->stream));
+  k_mt_get<<<g1(n), 256, 0, ctx->stream>>>(t, n, (const uint64_t*)ctx->mt_rk.p,
+                                           (const uint64_t*)ctx->mt_rlr.p,
+                                           (const uint64_t*)ctx->mt_rlw.p, ctx->mt_bits, t + n,
+                                           t + 2 * n);
+  CK(hipGetLastError());
+  CK(hipMemcpyAsync(last_read, t + n, n * 8, hipMemcpyDeviceToHost, ctx->stream));
+  CK(hipMemcpyAsync(last_write, t + 2 * n, n * 8, hipMemcpyDeviceToHost, ctx->stream));
+  CK(hipStreamSynchronize(ctx->stream));
+  tmp.release();
+  return DCC_OK;
+}
+
+extern "C" uint64_t dcc_maat_rows_size(const dcc_ctx* ctx) { return ctx ? ctx->mt_rows : 0; }

@@ -158,6 +158,53 @@ class Engine:
                                           C.byref(st)), self._h)
         return out_rc[:n], (out_tn[:n] if want_tn else None), st.as_dict()
 
+    # ----------------------------------------------------------------- MaaT
+    def maat_validate_epoch(self, batch: EpochBatch, want_cts: bool = True,
+                            read_and_prewrite: bool = False, out_rc=None, out_cts=None):
+        """MaaT epoch (dcc_maat_validate_epoch): returns (rc u8[n],
+        commit_ts u64[n] | None, stats).  read_and_prewrite: the TPC-C path."""
+        n = batch.n_txn
+        dev = batch.on_device
+        if out_rc is None:
+            if dev:
+                import torch
+                out_rc = torch.empty(max(n, 1), dtype=torch.uint8, device=batch.offsets.device)
+            else:
+                out_rc = np.empty(max(n, 1), np.uint8)
+        if want_cts and out_cts is None:
+            if dev:
+                import torch
+                out_cts = torch.empty(max(n, 1), dtype=torch.int64, device=batch.offsets.device)
+            else:
+                out_cts = np.empty(max(n, 1), np.uint64)
+        st = _abi.Stats()
+        b = batch.to_c(_abi.MAAT_READ_AND_PREWRITE if read_and_prewrite else 0)
+        _check(lib.dcc_maat_validate_epoch(self._h, C.byref(b), _ptr(out_rc), _ptr(out_cts),
+                                           C.byref(st)), self._h)
+        return out_rc[:n], (out_cts[:n] if want_cts else None), st.as_dict()
+
+    def maat_rows_set(self, keys, last_read, last_write) -> None:
+        keys = np.ascontiguousarray(keys, np.uint64)
+        lr = np.ascontiguousarray(last_read, np.uint64)
+        lw = np.ascontiguousarray(last_write, np.uint64)
+        _check(lib.dcc_maat_rows_set(self._h, _ptr(keys), _ptr(lr), _ptr(lw), keys.shape[0]),
+               self._h)
+
+    def maat_rows_get(self, keys):
+        keys = np.ascontiguousarray(keys, np.uint64)
+        lr = np.empty(keys.shape[0], np.uint64)
+        lw = np.empty(keys.shape[0], np.uint64)
+        _check(lib.dcc_maat_rows_get(self._h, _ptr(keys), _ptr(lr), _ptr(lw), keys.shape[0]),
+               self._h)
+        return lr, lw
+
+    def maat_rows_clear(self) -> None:
+        _check(lib.dcc_maat_rows_clear(self._h), self._h)
+
+    @property
+    def maat_rows_size(self) -> int:
+        return int(lib.dcc_maat_rows_size(self._h))
+
     def occ_validate_snapshot(self, batch: EpochBatch, active_off, active_idx,
                               hist_top=None, out_rc=None):
         """Captured-snapshot validation (dcc_occ_validate_snapshot): every txn

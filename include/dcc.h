@@ -64,6 +64,9 @@ extern "C" {
 /* --------------------------------------------------------------- batch  */
 /* dcc_batch.flags */
 #define DCC_DEVICE_PTRS 0x1u      /* every batch AND output pointer is device memory */
+#define DCC_MAAT_READ_AND_PREWRITE 0x4u /* MaaT: every access both reads and prewrites its row
+                                          (the TPC-C path, Row_maat::read_and_prewrite,
+                                          row_maat.cpp:40-41, 54-98)                     */
 #define DCC_OCC_APPEND_HISTORY 0x2u /* central_finish semantics: committed write sets
                                      of this epoch are appended to the history with
                                      tn = tnc+1, tnc+2, ... in index order
@@ -225,6 +228,37 @@ typedef struct dcc_occ_snapshot {
 } dcc_occ_snapshot;
 int dcc_occ_validate_snapshot(dcc_ctx* ctx, const dcc_batch* batch, const dcc_occ_snapshot* snap,
                               uint8_t* out_rc, dcc_stats* out_stats);
+
+/* ----------------------------------------------------------------- MaaT */
+/* MaaT epoch validation.  Epoch model: every txn of
+ * the batch is initialised in the time table ([0, UINT64_MAX], RUNNING;
+ * worker_thread.cpp:503-508) and performs its Row_maat accesses in index
+ * order (RD -> read, WR -> prewrite, XP/SCAN -> none; with
+ * DCC_MAAT_READ_AND_PREWRITE every access does read_and_prewrite,
+ * row_maat.cpp:38-171); then, in index order, each txn runs Maat::validate
+ * and find_bound (maat.cpp:29-191; the node is the home node) and commits
+ * (Row_maat::commit with the forward validation of the later txns still on
+ * its rows, row_maat.cpp:227-316) or aborts (row_maat.cpp:205-225).
+ *   out_rc[i]        = DCC_RC_RCOK or DCC_RC_ABORT
+ *   out_commit_ts[i] = commit_timestamp (the lower bound find_bound picks) or 0
+ * Row timestamps (timestamp_last_read / _write, row_maat.cpp:25-26) persist in
+ * the context across epochs; rows never seen start at 0.
+ * Stats: n_commit, n_abort, nnz_w, rounds (of the GPU fixed point),
+ * device_ms, total_ms, alg_bytes (dcc_maat_alg_bytes). */
+int dcc_maat_validate_epoch(dcc_ctx* ctx, const dcc_batch* batch, uint8_t* out_rc,
+                            uint64_t* out_commit_ts, dcc_stats* out_stats);
+/* Row timestamps: seed (overwrite) / read (0 for unknown rows) / forget.
+ * Host arrays of n entries. */
+int dcc_maat_rows_set(dcc_ctx* ctx, const uint64_t* keys, const uint64_t* last_read,
+                      const uint64_t* last_write, uint64_t n);
+int dcc_maat_rows_get(dcc_ctx* ctx, const uint64_t* keys, uint64_t* last_read,
+                      uint64_t* last_write, uint64_t n);
+int dcc_maat_rows_clear(dcc_ctx* ctx);
+uint64_t dcc_maat_rows_size(const dcc_ctx* ctx);
+/* Algorithmic bytes of one MaaT epoch: 4(N+1) offsets + 9 nnz (key, type)
+ * + 24 nnz (row slot: key, last read, last write) + 8 nnz (timestamp update)
+ * + N (RC) + 8 N (commit timestamp). */
+uint64_t dcc_maat_alg_bytes(uint64_t n_txn, uint64_t nnz);
 
 /* --------------------------------------------------------------- Calvin */
 /* Epoch lock ordering: the result equals the epoch's txns calling

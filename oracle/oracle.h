@@ -90,6 +90,24 @@ int oracle_calvin_formula(uint64_t n, const uint32_t* off, const uint64_t* keys,
                           const uint8_t* acctype, const uint64_t* order, uint32_t* out_group,
                           uint8_t* out_rc, uint32_t* out_wave);
 
+/* MaaT epoch validation (maat_ref.c): every txn of the epoch executes its
+ * Row_maat accesses in index order (row_maat.cpp:38-171), then, in index
+ * order, Maat::validate + find_bound (maat.cpp:29-191) and commit
+ * (Row_maat::commit, row_maat.cpp:227-316, cleanup in reverse access order)
+ * or abort (row_maat.cpp:205-225), with time_table.release after each.
+ * rw_all != 0: the TPC-C path (read_and_prewrite for every access).
+ * row_keys/row_lr/row_lw [n_rows]: timestamp_last_read / _write per row, in
+ * (before the epoch; unlisted rows start at 0) and out (after it).
+ * out_rc[i] = 0 RCOK / 2 Abort; out_cts[i] = commit timestamp or 0. */
+int oracle_maat_replay(uint64_t n, const uint32_t* off, const uint64_t* keys, const uint8_t* acctype,
+                       int rw_all, uint64_t n_rows, const uint64_t* row_keys, uint64_t* row_lr,
+                       uint64_t* row_lw, uint8_t* out_rc, uint64_t* out_cts);
+/* Independent restatement of the same epoch: the per-row running maxima /
+ * minima of committed readers' / writers' commit timestamps (see maat_ref.c). */
+int oracle_maat_formula(uint64_t n, const uint32_t* off, const uint64_t* keys, const uint8_t* acctype,
+                        int rw_all, uint64_t n_rows, const uint64_t* row_keys, uint64_t* row_lr,
+                        uint64_t* row_lw, uint8_t* out_rc, uint64_t* out_cts);
+
 #ifdef __cplusplus
 }
 #endif

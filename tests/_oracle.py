@@ -17,7 +17,7 @@ LIB = os.path.join(ORACLE_DIR, "liboracle.so")
 
 
 def _load():
-    srcs = [os.path.join(ORACLE_DIR, f) for f in ("occ_ref.c", "occ_mt.c", "calvin_ref.c", "oracle.h", "kmap.h")]
+    srcs = [os.path.join(ORACLE_DIR, f) for f in ("occ_ref.c", "occ_mt.c", "calvin_ref.c", "maat_ref.c", "oracle.h", "kmap.h")]
     if not os.path.exists(LIB) or any(os.path.getmtime(s) > os.path.getmtime(LIB) for s in srcs
                                       if os.path.exists(s)):
         subprocess.run(["make", "-C", ORACLE_DIR], check=True, capture_output=True)
@@ -34,8 +34,11 @@ def _load():
     lib.oracle_occ_round_status.argtypes = [C.c_uint64, P, P, P, P, P]
     lib.oracle_calvin_replay.argtypes = [C.c_uint64, P, P, P, P, P, P, P]
     lib.oracle_calvin_formula.argtypes = lib.oracle_calvin_replay.argtypes
+    lib.oracle_maat_replay.argtypes = [C.c_uint64, P, P, P, C.c_int, C.c_uint64, P, P, P, P, P]
+    lib.oracle_maat_formula.argtypes = lib.oracle_maat_replay.argtypes
     for f in (lib.oracle_occ_replay, lib.oracle_occ_hash, lib.oracle_occ_round_status,
-              lib.oracle_calvin_replay, lib.oracle_calvin_formula):
+              lib.oracle_calvin_replay, lib.oracle_calvin_formula, lib.oracle_maat_replay,
+              lib.oracle_maat_formula):
         f.restype = C.c_int
     return lib
 
@@ -167,3 +170,28 @@ def calvin_held(batch, held_keys, held_acctype, literal=True):
     cb = EpochBatch(coff, ckeys, cat, order=corder)
     g, rc, _ = calvin(cb, literal=literal)
     return g[h:], rc[h:]
+
+
+def maat(batch, row_keys=None, row_lr=None, row_lw=None, rw_all=False, literal=False):
+    """MaaT epoch (oracle_maat_replay / _formula).  Returns (rc u8[n],
+    cts u64[n], (keys, lr, lw) of every row touched or pre-seeded, after)."""
+    n = batch.n_txn
+    off = _arr(batch.offsets, np.uint32)
+    keys = _arr(batch.keys, np.uint64)
+    at = _arr(batch.acctype, np.uint8)
+    pre_k = np.zeros(0, np.uint64) if row_keys is None else np.asarray(row_keys, np.uint64)
+    rk = np.unique(np.concatenate([pre_k, keys if keys is not None else np.zeros(0, np.uint64)]))
+    lr = np.zeros(rk.size, np.uint64)
+    lw = np.zeros(rk.size, np.uint64)
+    if pre_k.size:
+        pos = np.searchsorted(rk, pre_k)
+        lr[pos] = np.asarray(row_lr, np.uint64)
+        lw[pos] = np.asarray(row_lw, np.uint64)
+    rc = np.empty(max(n, 1), np.uint8)
+    cts = np.empty(max(n, 1), np.uint64)
+    fn = lib.oracle_maat_replay if literal else lib.oracle_maat_formula
+    r = fn(n, _p(off), _p(keys), _p(at), 1 if rw_all else 0, rk.size, _p(rk), _p(lr), _p(lw),
+           rc.ctypes.data, cts.ctypes.data)
+    if r != 0:
+        raise RuntimeError(f"oracle maat failed: {r}")
+    return rc[:n], cts[:n], (rk, lr, lw)
