@@ -41,6 +41,9 @@ def parse():
                     help="txns of the batch timed with the CPU reference restatement")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the other BASELINE configs (C2, C3, C4, C5) at N=1")
+    ap.add_argument("--only", default="",
+                    help="comma-separated secondary configs to run INSTEAD of the headline "
+                         "(profiling aid): " + ",".join(CONFIGS))
     ap.add_argument("--solver", type=int, default=0,
                     help="OCC solver: 0 auto (sweep), 1 fixed-point rounds only, 3 sweep")
     ap.add_argument("--strong", action="store_true",
@@ -124,15 +127,8 @@ def c4_order(b):
     return (home << np.uint64(32)) | seq
 
 
-def secondary_configs(eng, local, steps=10, warmup=3):
-    """The other BASELINE.json configs on one GPU (each its own workload;
-    inputs resident, decisions checked against the oracle outside the timing)."""
+def _timer(steps, warmup):
     import torch
-    import deneva_amd as d
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import _oracle as orc  # checker only
-    dev = f"cuda:{local}"
-    out = {}
 
     def timed(fn):
         for _ in range(warmup):
@@ -142,27 +138,37 @@ def secondary_configs(eng, local, steps=10, warmup=3):
         st = [fn() for _ in range(steps)]
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) / steps, st[-1]
+    return timed
 
-    occ_cfgs = [
-        ("C2", "YCSB OCC, 65,536 txns x 16 keys, theta=0.9",
-         lambda: d.gen_ycsb(n_txn=65536, zipf_theta=0.9)),
-        ("C3", "TPC-C NewOrder+Payment OCC, 128 warehouses, 262,144 txns",
-         lambda: d.gen_tpcc(n_txn=262144, num_wh=128)),
-        ("C5", "YCSB OCC, 1,048,576 txns x 16 keys, theta=0.99",
-         lambda: d.gen_ycsb(n_txn=1 << 20, zipf_theta=0.99, seed=0xD3E7A002)),
-    ]
-    for tag, desc, gen in occ_cfgs:
-        b = gen()
-        db = b.to_torch(dev)
-        rc = torch.empty(b.n_txn, dtype=torch.uint8, device=dev)
-        dt, st = timed(lambda: eng.occ_validate_epoch(db, out_rc=rc)[2])
-        erc, _, _ = orc.occ(b)
-        out[tag] = {"workload": desc, "txns_per_s": b.n_txn / dt, "ms_per_epoch": dt * 1e3,
-                    "device_ms": st["device_ms"], "rounds": int(st["rounds"]),
-                    "commits": int(st["n_commit"]), "peel_prefix": int(st["peel_prefix"]),
-                    "survivors": int(st["n_survivors"]),
-                    "parity_vs_oracle": bool(np.array_equal(rc.cpu().numpy(), erc))}
-    # C4: Calvin lock ordering, 16 partitions, 1M txns, sequencer order
+
+def occ_config(eng, dev, timed, orc, tag):
+    """C2 / C3 / C5: OCC epoch validation of one resident batch."""
+    import torch
+    import deneva_amd as d
+    desc, gen = {
+        "C2": ("YCSB OCC, 65,536 txns x 16 keys, theta=0.9",
+               lambda: d.gen_ycsb(n_txn=65536, zipf_theta=0.9)),
+        "C3": ("TPC-C NewOrder+Payment OCC, 128 warehouses, 262,144 txns",
+               lambda: d.gen_tpcc(n_txn=262144, num_wh=128)),
+        "C5": ("YCSB OCC, 1,048,576 txns x 16 keys, theta=0.99",
+               lambda: d.gen_ycsb(n_txn=1 << 20, zipf_theta=0.99, seed=0xD3E7A002)),
+    }[tag]
+    b = gen()
+    db = b.to_torch(dev)
+    rc = torch.empty(b.n_txn, dtype=torch.uint8, device=dev)
+    dt, st = timed(lambda: eng.occ_validate_epoch(db, out_rc=rc)[2])
+    erc, _, _ = orc.occ(b)
+    return {"workload": desc, "txns_per_s": b.n_txn / dt, "ms_per_epoch": dt * 1e3,
+            "device_ms": st["device_ms"], "rounds": int(st["rounds"]),
+            "commits": int(st["n_commit"]), "peel_prefix": int(st["peel_prefix"]),
+            "survivors": int(st["n_survivors"]),
+            "alg_GBps": st["alg_bytes"] / (st["device_ms"] * 1e-3) / 1e9,
+            "parity_vs_oracle": bool(np.array_equal(rc.cpu().numpy(), erc))}
+
+
+def calvin_config(eng, dev, timed, orc, tag="C4"):
+    """C4: Calvin lock ordering, 16 partitions, 1M txns, sequencer order."""
+    import deneva_amd as d
     b = d.gen_ycsb(n_txn=1 << 20, zipf_theta=0.9, part_cnt=16, chunk_txns=65536, want_home=True)
     b.order = c4_order(b)
     db = b.to_torch(dev)
@@ -176,13 +182,56 @@ def secondary_configs(eng, local, steps=10, warmup=3):
     eg, erc, _ = orc.calvin(b)
     par = bool(np.array_equal(res["g"].cpu().numpy().astype(np.uint32)[:b.nnz], eg) and
                np.array_equal(res["rc"].cpu().numpy()[:b.n_txn], erc))
-    out["C4"] = {"workload": "Calvin lock ordering, YCSB theta=0.9, 16 partitions, "
-                             "1,048,576 txns x 16 keys, sequencer (origin, FIFO) order",
-                 "txns_per_s": b.n_txn / dt, "ms_per_epoch": dt * 1e3,
-                 "device_ms": st["device_ms"], "ready_at_acquire": int(st["n_commit"]),
-                 "alg_GBps": st["alg_bytes"] / (st["device_ms"] * 1e-3) / 1e9,
-                 "parity_vs_oracle": par}
-    out["C6"] = snapshot_config(eng, dev, timed, orc)
+    return {"workload": "Calvin lock ordering, YCSB theta=0.9, 16 partitions, "
+                        "1,048,576 txns x 16 keys, sequencer (origin, FIFO) order",
+            "txns_per_s": b.n_txn / dt, "ms_per_epoch": dt * 1e3,
+            "device_ms": st["device_ms"], "ready_at_acquire": int(st["n_commit"]),
+            "alg_GBps": st["alg_bytes"] / (st["device_ms"] * 1e-3) / 1e9,
+            "hbm_frac": st["alg_bytes"] / (st["device_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "parity_vs_oracle": par}
+
+
+def maat_config(eng, dev, timed, orc, tag="MAAT_C2"):
+    """MaaT epoch validation on the C2 / headline
+    YCSB shapes; each step starts from the same (empty) row timestamps."""
+    import torch
+    import deneva_amd as d
+    n = 65536 if tag == "MAAT_C2" else 1 << 20
+    b = d.gen_ycsb(n_txn=n, zipf_theta=0.9)
+    db = b.to_torch(dev)
+    rc = torch.empty(n, dtype=torch.uint8, device=dev)
+
+    def step():
+        eng.maat_rows_clear()
+        return eng.maat_validate_epoch(db, want_cts=False, out_rc=rc)[2]
+    dt, st = timed(step)
+    erc, _, _ = orc.maat(b)
+    return {"workload": f"MaaT epoch validation, YCSB {n} txns x 16 keys, theta=0.9, empty row "
+                        f"timestamps",
+            "txns_per_s": n / dt, "ms_per_epoch": dt * 1e3, "device_ms": st["device_ms"],
+            "rounds": int(st["rounds"]), "commits": int(st["n_commit"]),
+            "alg_GBps": st["alg_bytes"] / (st["device_ms"] * 1e-3) / 1e9,
+            "parity_vs_oracle": bool(np.array_equal(rc.cpu().numpy(), erc))}
+
+
+CONFIGS = {"C2": occ_config, "C3": occ_config, "C5": occ_config, "C4": calvin_config,
+           "C6": None, "MAAT_C2": maat_config, "MAAT_1M": maat_config}
+
+
+def secondary_configs(eng, local, steps=10, warmup=3, only=None):
+    """The other BASELINE.json configs (and the §8(f) engines) on one GPU,
+    each its own workload; inputs resident, decisions checked against the
+    oracle outside the timing."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle as orc  # checker only
+    dev = f"cuda:{local}"
+    timed = _timer(steps, warmup)
+    out = {}
+    for tag, fn in CONFIGS.items():
+        if only and tag not in only:
+            continue
+        out[tag] = (snapshot_config(eng, dev, timed, orc) if tag == "C6"
+                    else fn(eng, dev, timed, orc, tag))
     return out
 
 
@@ -241,6 +290,12 @@ def main():
     import torch.distributed as dist
 
     import deneva_amd as d
+    if args.only:
+        torch.cuda.set_device(0)
+        with d.Engine(0) as eng:
+            print(json.dumps(secondary_configs(eng, 0, steps=args.steps, warmup=args.warmup,
+                                               only=args.only.split(","))), flush=True)
+        return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

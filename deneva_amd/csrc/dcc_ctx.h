@@ -136,6 +136,7 @@ struct dcc_ctx {
   uint64_t mt_rows = 0;                          // rows in the table
   uint32_t mt_rows32 = 0;                        // upload source of the row counter
   DevBuf mt_misc, mt_slot, mt_sval, mt_slot2, mt_sval2, mt_owner, mt_sfl, mt_stx, mt_txn, mt_agg;
+  DevBuf mt_sflB, mt_stxB, mt_k1, mt_tcnt;
   // commit counter tnc (occ.h:67)
   uint64_t tnc = 0;
 

@@ -68,11 +68,13 @@ __device__ inline uint64_t mt_hash(uint64_t key, uint32_t bits) {
 }
 
 // ---------------------------------------------------------------- row table
-// insert-or-find the row of `key`; its lr / lw stay 0 until an epoch commits
-__device__ inline uint32_t mt_row(uint64_t* rk, uint32_t bits, uint64_t key, uint32_t* nrows,
+// insert-or-find the row of `key` (ins: this call created it); its lr / lw
+// stay 0 until an epoch commits
+__device__ inline uint32_t mt_row(uint64_t* rk, uint32_t bits, uint64_t key, bool& ins,
                                   uint32_t* err) {
   const uint64_t mask = (1ull << bits) - 1;
   uint64_t s = mt_hash(key, bits);
+  ins = false;
   for (uint64_t q = 0; q <= mask; q++) {
     const uint64_t v = rk[s];
     if (v == key) return (uint32_t)s;
@@ -81,7 +83,7 @@ __device__ inline uint32_t mt_row(uint64_t* rk, uint32_t bits, uint64_t key, uin
                                                 (unsigned long long)DCC_KEY_RESERVED,
                                                 (unsigned long long)key);
       if (prev == DCC_KEY_RESERVED) {
-        atomicAdd(nrows, 1u);
+        ins = true;
         return (uint32_t)s;
       }
       if (prev == key) return (uint32_t)s;
@@ -92,18 +94,34 @@ __device__ inline uint32_t mt_row(uint64_t* rk, uint32_t bits, uint64_t key, uin
   return 0;
 }
 
+// one atomic per workgroup for a per-thread count (256 threads)
+__device__ inline void block_add(uint32_t c, uint32_t* ctr) {
+  __shared__ uint32_t s_c[4];
+  for (int d = 32; d > 0; d >>= 1) c += __shfl_xor(c, d);
+  if ((threadIdx.x & 63) == 0) s_c[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t v = s_c[0] + s_c[1] + s_c[2] + s_c[3];
+    if (v) atomicAdd(ctr, v);
+  }
+}
+
 // rehash: every row of the old table into the new one (values carried)
 __global__ __launch_bounds__(256) void k_mt_rehash(const uint64_t* ok, const uint64_t* olr,
                                                    const uint64_t* olw, uint64_t ocap, uint64_t* nk,
                                                    uint64_t* nlr, uint64_t* nlw, uint32_t nbits,
                                                    uint32_t* nrows, uint32_t* err) {
+  uint32_t c = 0;
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < ocap; i += (uint64_t)gridDim.x * 256) {
     const uint64_t k = ok[i];
     if (k == DCC_KEY_RESERVED) continue;
-    const uint32_t s = mt_row(nk, nbits, k, nrows, err);
+    bool ins;
+    const uint32_t s = mt_row(nk, nbits, k, ins, err);
+    c += ins;
     nlr[s] = olr[i];
     nlw[s] = olw[i];
   }
+  block_add(c, nrows);
 }
 
 // host-seeded rows (dcc_maat_rows_set): insert and overwrite the timestamps
@@ -111,15 +129,19 @@ __global__ __launch_bounds__(256) void k_mt_seed(const uint64_t* keys, const uin
                                                  const uint64_t* lw, uint64_t n, uint64_t* rk,
                                                  uint64_t* rlr, uint64_t* rlw, uint32_t bits,
                                                  uint32_t* nrows, uint32_t* err) {
+  uint32_t c = 0;
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
     if (keys[i] == DCC_KEY_RESERVED) {
       atomicOr(err, MT_ERR_KEY);
       continue;
     }
-    const uint32_t s = mt_row(rk, bits, keys[i], nrows, err);
+    bool ins;
+    const uint32_t s = mt_row(rk, bits, keys[i], ins, err);
+    c += ins;
     rlr[s] = lr[i];
     rlw[s] = lw[i];
   }
+  block_add(c, nrows);
 }
 __global__ __launch_bounds__(256) void k_mt_get(const uint64_t* keys, uint64_t n, const uint64_t* rk,
                                                 const uint64_t* rlr, const uint64_t* rlw,
@@ -144,23 +166,38 @@ __global__ __launch_bounds__(256) void k_mt_get(const uint64_t* keys, uint64_t n
 }
 
 // ---------------------------------------------------------------- base
-// One thread per txn: each access enters its row (slot id), owner and sort
-// value; the txn's lower bound from the copied row timestamps: gwts over rows
-// read or written, grts over rows written (Row_maat::read / prewrite copy
-// them at access time, row_maat.cpp:119-121, 159-165; Maat::validate raises
-// lower past them, maat.cpp:47-50, 70-73).
+// Access-parallel: every access enters its row (slot id) in the table.
+__global__ __launch_bounds__(256) void k_mt_slots(const uint64_t* keys, uint64_t nnz, uint64_t* rk,
+                                                  uint32_t bits, uint32_t* slot, uint32_t* nrows,
+                                                  uint32_t* err) {
+  uint32_t c = 0;
+  for (uint64_t x = (uint64_t)blockIdx.x * 256 + threadIdx.x; x < nnz; x += (uint64_t)gridDim.x * 256) {
+    const uint64_t key = keys[x];
+    uint32_t sl = 0;
+    if (key == DCC_KEY_RESERVED) {
+      atomicOr(err, MT_ERR_KEY);
+    } else {
+      bool ins;
+      sl = mt_row(rk, bits, key, ins, err);
+      c += ins;
+    }
+    slot[x] = sl;
+  }
+  block_add(c, nrows);
+}
+
+// One thread per txn: owners, and the txn's lower bound from the row
+// timestamps copied at access time: gwts over rows read or written, grts over
+// rows written (Row_maat::read / prewrite, row_maat.cpp:119-121, 159-165;
+// Maat::validate raises lower past them, maat.cpp:47-50, 70-73).
 struct BaseArgs {
   uint64_t n, nnz;
   const uint32_t* off;
-  const uint64_t* keys;
   const uint8_t* at;
   uint32_t rw_all;
-  uint64_t* rk;
   const uint64_t* rlr;
   const uint64_t* rlw;
-  uint32_t bits;
-  uint32_t* nrows;
-  uint32_t* slot;   // [nnz] row slot per access (sort key; pre-zeroed)
+  const uint32_t* slot;
   uint32_t* owner;  // [nnz] txn of each access (pre-zeroed)
   uint64_t* base;   // [n]
   uint8_t* state;   // [n] zeroed here
@@ -174,14 +211,10 @@ __global__ __launch_bounds__(256) void k_mt_base(BaseArgs a) {
   if (t >= a.n) return;
   const uint64_t o0 = min((uint64_t)a.off[t], a.nnz), o1 = min((uint64_t)a.off[t + 1], a.nnz);
   if (a.off[t + 1] < a.off[t] || o1 - o0 > MAX_TXN_LEN) atomicOr(a.err, MT_ERR_OFF);
-  uint64_t gw = 0, gr = 0;
   if ((t == 0 && a.off[0] != 0) || (t + 1 == a.n && a.off[a.n] != a.nnz)) atomicOr(a.err, MT_ERR_OFF);
+  uint64_t gw = 0, gr = 0;
   for (uint64_t x = o0; x < o1; x++) {
-    const uint64_t key = a.keys[x];
-    uint32_t s = 0;
-    if (key == DCC_KEY_RESERVED) atomicOr(a.err, MT_ERR_KEY);
-    else s = mt_row(a.rk, a.bits, key, a.nrows, a.err);
-    a.slot[x] = s;
+    const uint32_t s = a.slot[x];
     a.owner[x] = (uint32_t)t;
     const uint8_t ty = a.at[x];
     const bool rd = a.rw_all || ty == DCC_RD, wr = a.rw_all || ty == DCC_WR;
@@ -407,6 +440,78 @@ __global__ __launch_bounds__(256) void k_mt_decide(uint64_t n, const uint64_t* b
   }
 }
 
+// ---------------------------------------------------------------- compaction
+// Between rounds the scan input shrinks to what can still matter: the last
+// position of every group of an undecided or committed txn (aborted txns
+// never constrain anyone; a group's other positions carry nothing).  Rows
+// keep their order, so per-row index order is kept; row starts are
+// recomputed from the slots.
+__device__ inline bool mt_keep(uint8_t f, uint8_t st) {
+  return (f & F_LAST) && (f & (F_R | F_W)) && st != ST_ABO;
+}
+__global__ __launch_bounds__(256) void k_mt_keep_count(uint64_t m, const uint8_t* sfl,
+                                                       const uint32_t* stx, const uint8_t* state,
+                                                       uint32_t* tcnt) {
+  __shared__ uint32_t s_c[4];
+  const uint64_t p0 = (uint64_t)blockIdx.x * MT_TILE + (uint64_t)threadIdx.x * MT_ITEMS;
+  uint32_t c = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < MT_ITEMS; i++) {
+    const uint64_t p = p0 + i;
+    if (p < m) {
+      const uint8_t f = sfl[p];
+      if ((f & F_LAST) && mt_keep(f, state[stx[p]])) c++;
+    }
+  }
+  for (int d = 32; d > 0; d >>= 1) c += __shfl_xor(c, d);
+  if ((threadIdx.x & 63) == 0) s_c[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) tcnt[blockIdx.x] = s_c[0] + s_c[1] + s_c[2] + s_c[3];
+}
+__global__ __launch_bounds__(256) void k_mt_keep_scatter(uint64_t m, const uint8_t* sfl,
+                                                         const uint32_t* stx, const uint32_t* ss,
+                                                         const uint8_t* state, const uint32_t* tpre,
+                                                         uint8_t* sfl2, uint32_t* stx2, uint32_t* ss2) {
+  __shared__ uint32_t s_w[4];
+  const uint64_t p0 = (uint64_t)blockIdx.x * MT_TILE + (uint64_t)threadIdx.x * MT_ITEMS;
+  uint32_t keep = 0, c = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < MT_ITEMS; i++) {
+    const uint64_t p = p0 + i;
+    if (p < m) {
+      const uint8_t f = sfl[p];
+      if ((f & F_LAST) && mt_keep(f, state[stx[p]])) {
+        keep |= 1u << i;
+        c++;
+      }
+    }
+  }
+  // exclusive scan of c over the workgroup (thread order = position order)
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t x = c;
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d);
+    if (lane >= (uint32_t)d) x += y;
+  }
+  if (lane == 63) s_w[w] = x;
+  __syncthreads();
+  uint32_t q = tpre[blockIdx.x] + x - c;
+  for (uint32_t v = 0; v < w; v++) q += s_w[v];
+#pragma unroll
+  for (uint32_t i = 0; i < MT_ITEMS; i++) {
+    if (!((keep >> i) & 1u)) continue;
+    const uint64_t p = p0 + i;
+    sfl2[q] = sfl[p] & (F_R | F_W | F_LAST);
+    stx2[q] = stx[p];
+    ss2[q] = ss[p];
+    q++;
+  }
+}
+__global__ __launch_bounds__(256) void k_mt_starts(uint64_t m, const uint32_t* ss, uint8_t* sfl) {
+  for (uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x; q < m; q += (uint64_t)gridDim.x * 256)
+    if (q == 0 || ss[q - 1] != ss[q]) sfl[q] |= F_START;
+}
+
 // ---------------------------------------------------------------- finish
 // RC bytes, commit timestamps, counts; committed txns raise their rows'
 // timestamps (Row_maat::commit, row_maat.cpp:251-262, 280-284)
@@ -537,6 +642,10 @@ int dcc_ctx::maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, 
   CR(mt_sval2.ensure(this, mm * 4, "maat sort values b"));
   CR(mt_owner.ensure(this, mm * 4, "maat owners"));
   CR(mt_sfl.ensure(this, mm, "maat flags"));
+  CR(mt_sflB.ensure(this, mm, "maat flags b"));
+  CR(mt_stxB.ensure(this, mm * 4, "maat sorted txns b"));
+  CR(mt_k1.ensure(this, mm * 4, "maat sort keys b"));
+  CR(mt_tcnt.ensure(this, ((mm + MT_TILE - 1) / MT_TILE + 2) * 4, "maat tile counts"));
   CR(mt_stx.ensure(this, mm * 4, "maat sorted txns"));
   CR(mt_txn.ensure(this, n * (8 * 4 + 4 + 1) + 64, "maat txn state"));
   CR(cv_scratch.ensure(this, rs_scratch_words(mm) * 4 + 64, "radix scratch"));
@@ -565,50 +674,58 @@ int dcc_ctx::maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, 
   CK(hipMemsetAsync(mt_slot.p, 0, mm * 4, stream));
   CK(hipMemsetAsync(mt_owner.p, 0, mm * 4, stream));
   k_mt_iota<<<g1(mm), 256, 0, stream>>>((uint32_t*)mt_sval.p, m);
-  BaseArgs ba{n,    m,    d.off,   d.keys,  d.acctype, rw_all, (uint64_t*)mt_rk.p,
-              (const uint64_t*)mt_rlr.p,     (const uint64_t*)mt_rlw.p, mt_bits, cnt,
-              (uint32_t*)mt_slot.p, (uint32_t*)mt_owner.p, base, state, lacc, uacc, pend,
-              cnt + 1};
+  k_mt_slots<<<g1(mm, 16384), 256, 0, stream>>>(d.keys, m, (uint64_t*)mt_rk.p, mt_bits,
+                                                 (uint32_t*)mt_slot.p, cnt, cnt + 1);
+  BaseArgs ba{n,     m,     d.off, d.acctype, rw_all, (const uint64_t*)mt_rlr.p,
+              (const uint64_t*)mt_rlw.p, (const uint32_t*)mt_slot.p, (uint32_t*)mt_owner.p,
+              base,  state, lacc,  uacc,      pend,   cnt + 1};
   k_mt_base<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(ba);
-  // rows sorted by slot (stable: index order within a row)
-  uint32_t* kb[2] = {(uint32_t*)mt_slot.p, (uint32_t*)mt_slot2.p};
-  uint32_t* vb[2] = {(uint32_t*)mt_sval.p, (uint32_t*)mt_sval2.p};
-  int cur = 0;
+  // rows sorted by slot (stable: index order within a row); the sorted slots
+  // and the other key buffer become the two slot arrays of the compaction
+  uint8_t* sflb[2] = {(uint8_t*)mt_sfl.p, (uint8_t*)mt_sflB.p};
+  uint32_t* stxb[2] = {(uint32_t*)mt_stx.p, (uint32_t*)mt_stxB.p};
+  uint32_t* ssb[2] = {(uint32_t*)mt_slot2.p, (uint32_t*)mt_k1.p};
   if (m) {
-    // the base kernel's slots are needed again at the end: sort a copy
     CK(hipMemcpyAsync(mt_slot2.p, mt_slot.p, m * 4, hipMemcpyDeviceToDevice, stream));
-    uint32_t* kk[2] = {(uint32_t*)mt_slot2.p, (uint32_t*)mt_stx.p};  // stx doubles as ping-pong
-    cur = radix_sort_u32(kk, vb, m, mt_bits, (uint32_t*)cv_scratch.p, stream);
-    kb[0] = kk[cur];
-    // the sorted slots must not live in stx, which k_mt_groups writes
-    if (kb[0] == (uint32_t*)mt_stx.p) {
-      CK(hipMemcpyAsync(mt_slot2.p, mt_stx.p, m * 4, hipMemcpyDeviceToDevice, stream));
-      kb[0] = (uint32_t*)mt_slot2.p;
-    }
-    k_mt_groups<<<g1(m), 256, 0, stream>>>(kb[0], vb[cur], (const uint32_t*)mt_owner.p, d.acctype,
-                                           rw_all, m, (uint8_t*)mt_sfl.p, (uint32_t*)mt_stx.p);
+    uint32_t* kk[2] = {(uint32_t*)mt_slot2.p, (uint32_t*)mt_k1.p};
+    uint32_t* vb[2] = {(uint32_t*)mt_sval.p, (uint32_t*)mt_sval2.p};
+    const int cur = radix_sort_u32(kk, vb, m, mt_bits, (uint32_t*)cv_scratch.p, stream);
+    ssb[0] = kk[cur];
+    ssb[1] = kk[cur ^ 1];
+    k_mt_groups<<<g1(m), 256, 0, stream>>>(ssb[0], vb[cur], (const uint32_t*)mt_owner.p, d.acctype,
+                                           rw_all, m, sflb[0], stxb[0]);
   }
   CK(hipGetLastError());
 
-  // ---- rounds, MT_BATCH between host checks
-  MtRoundArgs ra{m, n, (const uint8_t*)mt_sfl.p, (const uint32_t*)mt_stx.p, state, cts, lacc, uacc,
-               pend, (Ms*)mt_agg.p};
+  // ---- rounds: one, then MT_BATCH between host checks; after each check
+  // the scan input is compacted to the groups that can still matter
   uint32_t rounds = 0;
   bool done = false;
+  uint64_t mc = m;  // current scan length
+  int cb = 0;       // current buffer set
+  uint32_t* tcnt = (uint32_t*)mt_tcnt.p;
   while (!done) {
     const uint32_t k0 = rounds;
-    for (uint32_t q = 0; q < MT_BATCH; q++, rounds++) {
-      if (m) {
-        k_mt_up<<<(unsigned)tiles, 256, 0, stream>>>(ra);
-        k_mt_top<<<1, 256, 0, stream>>>((Ms*)mt_agg.p, (uint32_t)tiles);
-        k_mt_down<<<(unsigned)tiles, 256, 0, stream>>>(ra);
+    const uint64_t tiles_c = (mc + MT_TILE - 1) / MT_TILE;
+    MtRoundArgs ra{mc, n, sflb[cb], stxb[cb], state, cts, lacc, uacc, pend, (Ms*)mt_agg.p};
+    const uint32_t nb = rounds == 0 ? 1u : MT_BATCH;
+    for (uint32_t q = 0; q < nb; q++, rounds++) {
+      if (mc) {
+        k_mt_up<<<(unsigned)tiles_c, 256, 0, stream>>>(ra);
+        k_mt_top<<<1, 256, 0, stream>>>((Ms*)mt_agg.p, (uint32_t)tiles_c);
+        k_mt_down<<<(unsigned)tiles_c, 256, 0, stream>>>(ra);
       }
       k_mt_decide<<<g1(n, 2048), 256, 0, stream>>>(n, base, state, cts, lacc, uacc, pend,
                                                    &ring[rounds % MT_RING],
                                                    &ring[(rounds + 1) % MT_RING]);
     }
+    if (mc) {
+      k_mt_keep_count<<<(unsigned)tiles_c, 256, 0, stream>>>(mc, sflb[cb], stxb[cb], state, tcnt);
+      rs_scan_one(tcnt, (uint32_t)tiles_c, tcnt + tiles_c, stream);
+    }
     CK(hipGetLastError());
     CK(hipMemcpyAsync(hmisc, ring, MT_RING * 4, hipMemcpyDeviceToHost, stream));
+    if (mc) CK(hipMemcpyAsync((char*)hmisc + MT_RING * 4, tcnt + tiles_c, 4, hipMemcpyDeviceToHost, stream));
     CK(hipStreamSynchronize(stream));
     const uint32_t* hr = (const uint32_t*)hmisc;
     for (uint32_t q = k0; q < rounds; q++)
@@ -618,6 +735,16 @@ int dcc_ctx::maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, 
         break;
       }
     if (!done && rounds > n + 8) return fail(DCC_EIO, "maat: rounds did not converge");
+    if (!done && mc) {
+      const uint64_t m2 = hr[MT_RING];
+      k_mt_keep_scatter<<<(unsigned)tiles_c, 256, 0, stream>>>(mc, sflb[cb], stxb[cb], ssb[cb], state,
+                                                             tcnt, sflb[cb ^ 1], stxb[cb ^ 1],
+                                                             ssb[cb ^ 1]);
+      if (m2) k_mt_starts<<<g1(m2), 256, 0, stream>>>(m2, ssb[cb ^ 1], sflb[cb ^ 1]);
+      CK(hipGetLastError());
+      cb ^= 1;
+      mc = m2;
+    }
   }
   FinArgs fa{n, m, d.off, d.acctype, rw_all, state, cts, (const uint32_t*)mt_slot.p,
              (uint64_t*)mt_rlr.p, (uint64_t*)mt_rlw.p, rc_dev, cts_dev, cnt + 2};
