@@ -7,7 +7,9 @@
 //
 // Layout (little-endian, every section 8-byte aligned, in this order):
 //   header   64 B   magic "DCCB", version, kind, section bits, n_txn, nnz,
-//                   seed, epoch, tnc_before, FNV-1a 64 of the payload
+//                   seed, epoch, tnc_before, FNV-1a 64 checksum (version 2:
+//                   of the header's first 56 bytes and the payload; version
+//                   1, still read: of the payload only)
 //   offsets  u32[n_txn+1]
 //   keys     u64[nnz]
 //   acctype  u8[nnz]
@@ -17,6 +19,7 @@
 //   commit_tn u64[n_txn]                         (DCC_FILE_HAS_COMMIT_TN)
 //   group    u32[nnz]                            (DCC_FILE_HAS_GROUP)
 //   wave     u32[n_txn]                          (DCC_FILE_HAS_WAVE)
+#include <cstddef>
 #include <cstdio>
 #include <cstring>
 #include <vector>
@@ -84,12 +87,21 @@ std::vector<Section> sections(uint32_t bits, uint64_t n, uint64_t nnz, const voi
   return v;
 }
 
+constexpr uint32_t kKnownSections = DCC_FILE_HAS_TN | DCC_FILE_HAS_ORDER | DCC_FILE_HAS_RC |
+                                    DCC_FILE_HAS_COMMIT_TN | DCC_FILE_HAS_GROUP | DCC_FILE_HAS_WAVE;
+
 int read_header(FILE* f, Header& h) {
   if (fread(&h, sizeof h, 1, f) != 1) return DCC_EINVAL;
   if (h.magic != kMagic || h.header_bytes != sizeof(Header)) return DCC_EINVAL;
-  if (h.version != DCC_FILE_VERSION) return DCC_ENOTSUP;
-  if (h.nnz >= 0xFFFFFFFFull) return DCC_ERANGE;
+  if (h.version != 1 && h.version != DCC_FILE_VERSION) return DCC_ENOTSUP;
+  if (h.kind > DCC_FILE_CALVIN || (h.sections & ~kKnownSections)) return DCC_EINVAL;
+  if (h.nnz >= 0xFFFFFFFFull || h.n_txn >= 0xFFFFFFFFull) return DCC_ERANGE;
   return DCC_OK;
+}
+
+// the checksum's start: version 2 covers the header (all but its checksum)
+void checksum_header(Fnv& fnv, const Header& h) {
+  if (h.version >= 2) fnv.add(&h, offsetof(Header, checksum));
 }
 
 }  // namespace
@@ -113,13 +125,9 @@ extern "C" int dcc_file_write(const char* path, const dcc_file_info* info, const
                          b->keys, b->acctype, b->start_tn, b->finish_tn, b->order,
                          rc, commit_tn, group, wave};
   const std::vector<Section> secs = sections(bits, n, nnz, src, nullptr);
-  Fnv fnv;
   static const uint8_t zeros[8] = {0};
-  for (const Section& s : secs) {
+  for (const Section& s : secs)
     if (s.bytes && !s.src) return DCC_EINVAL;
-    fnv.add(s.src, s.bytes);
-    fnv.add(zeros, pad8(s.bytes) - s.bytes);
-  }
   Header h{};
   h.magic = kMagic;
   h.version = DCC_FILE_VERSION;
@@ -131,6 +139,12 @@ extern "C" int dcc_file_write(const char* path, const dcc_file_info* info, const
   h.seed = info->seed;
   h.epoch = info->epoch;
   h.tnc_before = info->tnc_before;
+  Fnv fnv;
+  checksum_header(fnv, h);
+  for (const Section& s : secs) {
+    fnv.add(s.src, s.bytes);
+    fnv.add(zeros, pad8(s.bytes) - s.bytes);
+  }
   h.checksum = fnv.h;
   FILE* f = fopen(path, "wb");
   if (!f) return DCC_EIO;
@@ -181,6 +195,7 @@ extern "C" int dcc_file_read(const char* path, uint32_t* offsets, uint64_t* keys
   void* dst[10] = {offsets, keys, acctype, start_tn, finish_tn, order, rc, commit_tn, group, wave};
   const std::vector<Section> secs = sections(h.sections, h.n_txn, h.nnz, nullptr, dst);
   Fnv fnv;
+  checksum_header(fnv, h);
   std::vector<uint8_t> buf;
   r = DCC_OK;
   for (const Section& s : secs) {
@@ -193,6 +208,7 @@ extern "C" int dcc_file_read(const char* path, uint32_t* offsets, uint64_t* keys
     fnv.add(buf.data(), total);
     if (s.dst && s.bytes) memcpy(s.dst, buf.data(), s.bytes);
   }
+  if (r == DCC_OK && fgetc(f) != EOF) r = DCC_EINVAL;  // trailing bytes
   fclose(f);
   if (r != DCC_OK) return r;
   if (fnv.h != h.checksum) return DCC_EINVAL;  // corrupted payload

@@ -58,7 +58,7 @@ namespace {
 constexpr uint32_t CV_SH = 0, CV_EX = 1, CV_NONE = 2;
 constexpr uint32_t NOPOS = 0xFFFFFFFFu;
 constexpr uint32_t CV_MAX_TXN = 1u << 25;  // value = txn:25 | j:6 | EX:1
-constexpr unsigned CV_PREP_BLOCKS = 512;
+constexpr unsigned CV_PREP_BLOCKS = 1024;
 constexpr uint32_t CV_ITEMS = 16;                  // scan elements per thread
 constexpr uint32_t CV_TILE = 256 * CV_ITEMS;       // scan elements per workgroup
 constexpr uint32_t ERR_WAVE_TIMEOUT = 1u << 8;
@@ -80,10 +80,30 @@ __global__ __launch_bounds__(256) void k_cv_prep(const uint64_t* __restrict__ ke
   uint32_t nex = 0;
   const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t x = tid; x < nnz; x += stride) {
-    const uint64_t k = keys[x];
-    kor |= k;
-    kand &= k;
+  // 16-B loads: two keys, sixteen access types per load (when aligned)
+  const uint64_t n2 = ((uintptr_t)keys & 15) ? 0 : nnz / 2;
+  const uint64_t n16 = ((uintptr_t)at & 15) ? 0 : nnz / 16;
+  for (uint64_t x = tid; x < n2; x += stride) {
+    const ulonglong2 k = ((const ulonglong2*)keys)[x];
+    kor |= k.x | k.y;
+    kand &= k.x & k.y;
+  }
+  for (uint64_t x = 2 * n2 + tid; x < nnz; x += stride) {
+    kor |= keys[x];
+    kand &= keys[x];
+  }
+  for (uint64_t x = tid; x < n16; x += stride) {
+    const uint4 q = ((const uint4*)at)[x];
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int b = 0; b < 4; b++)
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        const uint32_t a = (w[b] >> (8 * c)) & 255u;
+        nex += (a != DCC_RD && a != DCC_SCAN) ? 1u : 0u;
+      }
+  }
+  for (uint64_t x = 16 * n16 + tid; x < nnz; x += stride) {
     const uint8_t a = at[x];
     nex += (a != DCC_RD && a != DCC_SCAN) ? 1u : 0u;
   }
@@ -190,8 +210,12 @@ __global__ __launch_bounds__(256) void k_cv_len_apply(const uint32_t* __restrict
 }
 
 // ---------------------------------------------------------------- layout
-// One thread per sequence position q: txn t = seq[q] writes its requests to
-// [off2[q], off2[q+1]) as (packed key, t:25 | j:6 | EX:1).
+// Requests in sequence order: position q's txn t = seq[q] writes its requests
+// to [off2[q], off2[q+1]) as (packed key, t:25 | j:6 | EX:1).  One wave per
+// 64 positions: the lanes walk the wave's whole request range together (the
+// txn of each output found by a search of the wave's length prefix in LDS),
+// so both the key / type reads and the writes are coalesced instead of one
+// lane streaming one txn.
 template <typename K>
 __global__ __launch_bounds__(256) void k_cv_layout(const uint32_t* __restrict__ off,
                                                    const uint32_t* __restrict__ seq,
@@ -200,15 +224,44 @@ __global__ __launch_bounds__(256) void k_cv_layout(const uint32_t* __restrict__ 
                                                    const uint8_t* __restrict__ at, KeyPack kp,
                                                    uint32_t base, K* __restrict__ ak,
                                                    uint32_t* __restrict__ av) {
-  const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= n) return;
-  const uint32_t t = seq ? seq[q] : (uint32_t)q;
-  const uint32_t s = off[t], e = off[t + 1];
-  const uint32_t d = base + (off2 ? off2[q] : s);
-  for (uint32_t j = 0; j < e - s; j++) {
-    const uint8_t a = at[s + j];
-    ak[d + j] = (K)keypack_apply(kp, keys[s + j]);
-    av[d + j] = (t << 7) | (j << 1) | ((a != DCC_RD && a != DCC_SCAN) ? 1u : 0u);
+  __shared__ uint32_t s_src[4][64], s_pre[4][65], s_t[4][64];
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t q0 = ((uint64_t)blockIdx.x * 4 + w) * 64;
+  if (q0 >= n) return;  // whole wave: no barrier below is workgroup-wide
+  const uint64_t q = q0 + lane;
+  uint32_t t = 0, src = 0, len = 0;
+  if (q < n) {
+    t = seq ? seq[q] : (uint32_t)q;
+    src = off[t];
+    len = off[t + 1] - src;
+  }
+  uint32_t x = len;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d);
+    if (lane >= (uint32_t)d) x += y;
+  }
+  const uint32_t total = __shfl(x, 63);
+  s_src[w][lane] = src;
+  s_pre[w][lane] = x - len;
+  s_t[w][lane] = t;
+  if (lane == 0) s_pre[w][64] = total;
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  const uint64_t d0 = (uint64_t)base + (off2 ? off2[q0] : off[q0]);
+  for (uint32_t jj = lane; jj < total; jj += 64) {
+    // largest k with pre[k] <= jj (empty txns share a prefix value: take the last)
+    uint32_t lo = 0, hi = 64;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (s_pre[w][mid] <= jj) lo = mid;
+      else hi = mid;
+    }
+    const uint32_t j = jj - s_pre[w][lo];
+    const uint32_t xs = s_src[w][lo] + j;
+    const uint8_t a = at[xs];
+    ak[d0 + jj] = (K)keypack_apply(kp, keys[xs]);
+    av[d0 + jj] = (s_t[w][lo] << 7) | (j << 1) | ((a != DCC_RD && a != DCC_SCAN) ? 1u : 0u);
   }
 }
 
@@ -318,31 +371,52 @@ __device__ inline Gs block_excl_gs(Gs v, Gs* s) {
   return ex;
 }
 
+// The tile's keys / values staged through LDS with coalesced global loads
+// (one padding word per 16, so a thread's 16 consecutive items are read
+// bank-conflict free), then each thread takes its run of CV_ITEMS and the
+// element before it.
 template <typename K>
-__device__ inline void load_run(const K* sk, const uint32_t* sv, uint64_t m, uint64_t p0, K* k,
-                                uint32_t* v, K& pk, uint32_t& pv) {
+__device__ inline void load_run(const K* sk, const uint32_t* sv, uint64_t m, K* lk, uint32_t* lv,
+                                K* k, uint32_t* v, K& pk, uint32_t& pv) {
+  const uint64_t base = (uint64_t)blockIdx.x * CV_TILE;
+  for (uint32_t i = threadIdx.x; i < CV_TILE; i += 256) {
+    const uint64_t p = base + i;
+    const uint32_t li = i + (i >> 4);
+    lk[li] = p < m ? sk[p] : (K)0;
+    lv[li] = p < m ? sv[p] : 0u;
+  }
+  __syncthreads();
+  const uint32_t b = threadIdx.x * (CV_ITEMS + 1);
 #pragma unroll
   for (uint32_t i = 0; i < CV_ITEMS; i++) {
-    k[i] = p0 + i < m ? sk[p0 + i] : (K)0;
-    v[i] = p0 + i < m ? sv[p0 + i] : 0u;
+    k[i] = lk[b + i];
+    v[i] = lv[b + i];
   }
-  pk = p0 ? sk[p0 - 1] : (K)0;
-  pv = p0 ? sv[p0 - 1] : 0u;
+  if (threadIdx.x) {
+    pk = lk[b - 2];  // item 16 * tid - 1 sits at 17 * tid - 2
+    pv = lv[b - 2];
+  } else {
+    pk = base ? sk[base - 1] : (K)0;
+    pv = base ? sv[base - 1] : 0u;
+  }
 }
+constexpr uint32_t CV_LDS = CV_TILE + CV_TILE / 16;
 
 template <typename K>
 __global__ __launch_bounds__(256) void k_cv_up(const K* __restrict__ sk,
                                                const uint32_t* __restrict__ sv, uint64_t m,
                                                Gs* __restrict__ agg) {
   __shared__ Gs s[256];
+  __shared__ K lk[CV_LDS];
+  __shared__ uint32_t lv[CV_LDS];
   const uint64_t p0 = (uint64_t)blockIdx.x * CV_TILE + (uint64_t)threadIdx.x * CV_ITEMS;
   K k[CV_ITEMS];
   uint32_t v[CV_ITEMS];
   K pk;
   uint32_t pv;
+  load_run(sk, sv, m, lk, lv, k, v, pk, pv);
   Gs acc = gs_identity();
   if (p0 < m) {
-    load_run(sk, sv, m, p0, k, v, pk, pv);
 #pragma unroll
     for (uint32_t i = 0; i < CV_ITEMS; i++) {
       if (p0 + i < m) acc = gs_combine(acc, gs_element(p0 + i, k[i], v[i], pk, pv));
@@ -354,17 +428,23 @@ __global__ __launch_bounds__(256) void k_cv_up(const K* __restrict__ sk,
   if (threadIdx.x == 0) agg[blockIdx.x] = r;
 }
 
-// one workgroup: exclusive scan of the tile aggregates in place
+// one workgroup: exclusive scan of the tile aggregates in place; each thread
+// folds 16 consecutive aggregates, so one block scan covers 4096 tiles
 __global__ __launch_bounds__(256) void k_cv_top(Gs* __restrict__ agg, uint32_t tiles) {
   __shared__ Gs s[256];
   __shared__ Gs s_last;
   Gs carry = gs_identity();
-  for (uint32_t c0 = 0; c0 < tiles; c0 += 256) {
-    const uint32_t i = c0 + threadIdx.x;
-    const Gs v = i < tiles ? agg[i] : gs_identity();
+  for (uint32_t c0 = 0; c0 < tiles; c0 += 256 * 16) {
+    const uint32_t i0 = c0 + threadIdx.x * 16;
+    Gs v = gs_identity();
+    for (uint32_t q = 0; q < 16 && i0 + q < tiles; q++) v = gs_combine(v, agg[i0 + q]);
     const Gs ex = block_excl_gs(v, s);
-    if (i < tiles) agg[i] = gs_combine(carry, ex);
-    // total of this chunk = ex(last) (+) v(last)
+    Gs run = gs_combine(carry, ex);
+    for (uint32_t q = 0; q < 16 && i0 + q < tiles; q++) {
+      const Gs a = agg[i0 + q];
+      agg[i0 + q] = run;
+      run = gs_combine(run, a);
+    }
     if (threadIdx.x == 255) s_last = gs_combine(ex, v);
     __syncthreads();
     carry = gs_combine(carry, s_last);
@@ -377,14 +457,16 @@ __global__ __launch_bounds__(256) void k_cv_down(const K* __restrict__ sk,
                                                  const uint32_t* __restrict__ sv, uint64_t m,
                                                  const Gs* __restrict__ pre, ScanOut o) {
   __shared__ Gs s[256];
+  __shared__ K lk[CV_LDS];
+  __shared__ uint32_t lv[CV_LDS];
   const uint64_t p0 = (uint64_t)blockIdx.x * CV_TILE + (uint64_t)threadIdx.x * CV_ITEMS;
   K k[CV_ITEMS];
   uint32_t v[CV_ITEMS];
   K pk0 = 0;
   uint32_t pv0 = 0;
+  load_run(sk, sv, m, lk, lv, k, v, pk0, pv0);
   Gs acc = gs_identity();
   if (p0 < m) {
-    load_run(sk, sv, m, p0, k, v, pk0, pv0);
     K pk = pk0;
     uint32_t pv = pv0;
 #pragma unroll
@@ -396,6 +478,9 @@ __global__ __launch_bounds__(256) void k_cv_down(const K* __restrict__ sk,
   }
   Gs run = gs_combine(pre[blockIdx.x], block_excl_gs(acc, s));
   if (p0 >= m) return;
+  // group of each request, straight to its place in request order (a random
+  // 4-B scatter: measured no slower than partitioning by destination first
+  // and placing window by window, profiles/r02/calvin_*)
   K pk = pk0;
   uint32_t pv = pv0;
   uint32_t last_gs = NOPOS, last_gnd = 0;
@@ -410,15 +495,14 @@ __global__ __launch_bounds__(256) void k_cv_down(const K* __restrict__ sk,
     if (t >= o.n) continue;  // held-prefix request: part of the scan only (no waves)
     const uint32_t x = o.off[t] + j;
     if (dup) {
-      if (o.group) o.group[x] = DCC_GROUP_NONE;
+      o.group[x] = DCC_GROUP_NONE;
       if (o.pgx) {
         o.pgx[x] = NOPOS;
         o.gsx[x] = NOPOS;
       }
       continue;
     }
-    if (o.group) o.group[x] = run.cnt;
-    if (run.cnt) o.rc[t] = DCC_RC_WAIT;  // racing stores of the same byte
+    o.group[x] = run.cnt;
     if (o.pgx) {
       o.pgx[x] = run.cnt ? run.pgs : NOPOS;
       o.gsx[x] = run.gs;
@@ -428,6 +512,38 @@ __global__ __launch_bounds__(256) void k_cv_down(const K* __restrict__ sk,
     }
   }
   if (o.gsize && last_gs != NOPOS) atomicMax(&o.gsize[last_gs], last_gnd);
+}
+
+// acquire_locks' return (ycsb_txn.cpp:76-79): RCOK iff every request of the
+// txn is in group 0.  One wave per 64 txns walks their contiguous requests.
+__global__ __launch_bounds__(256) void k_cv_ready(const uint32_t* __restrict__ off, uint64_t n,
+                                                  const uint32_t* __restrict__ group,
+                                                  uint8_t* __restrict__ rc) {
+  __shared__ uint32_t s_o[4][65];
+  __shared__ uint32_t s_w[4][64];
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t t0 = ((uint64_t)blockIdx.x * 4 + w) * 64;
+  if (t0 >= n) return;
+  const uint64_t t = t0 + lane;
+  const uint64_t tl = min<uint64_t>(n, t0 + 64);
+  s_o[w][lane] = off[min(t, tl)];
+  if (lane == 0) s_o[w][64] = off[tl];
+  s_w[w][lane] = 0;
+  __builtin_amdgcn_wave_barrier();
+  const uint32_t a0 = s_o[w][0], a1 = s_o[w][64];
+  for (uint32_t x = a0 + lane; x < a1; x += 64) {
+    const uint32_t g = group[x];
+    if (g == 0 || g == DCC_GROUP_NONE) continue;
+    uint32_t lo = 0, hi = 64;  // largest k with s_o[k] <= x
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (s_o[w][mid] <= x) lo = mid;
+      else hi = mid;
+    }
+    s_w[w][lo] = 1;
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (t < n) rc[t] = s_w[w][lane] ? DCC_RC_WAIT : DCC_RC_RCOK;
 }
 
 // ---------------------------------------------------------------- waves
@@ -545,7 +661,7 @@ static int calvin_sort_and_scan(dcc_ctx* ctx, const DevBatch& d, const uint32_t*
     k_cv_layout_held<K><<<grid1(nh, 256), 256, 0, st>>>(hkeys, hat, nh, (uint32_t)d.n, kp, kb[0],
                                                          vb[0]);
   k_cv_layout<K><<<grid1(d.n, 256), 256, 0, st>>>(d.off, seq, off2, d.n, d.keys, d.acctype, kp,
-                                                  (uint32_t)nh, kb[0], vb[0]);
+                                                  (uint32_t)nh, kb[0], vb[0]);  // 4 waves x 64
   if (prof) CK(hipEventRecord(ctx->pev[1], st));
   int cur;
   if (sizeof(K) == 4)
@@ -640,15 +756,13 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint3
   // ---- outputs / workspaces
   CR(rc.ensure(this, d.n + 16, "rc"));
   uint8_t* rc_dev = (dev_out && out_rc) ? out_rc : (uint8_t*)rc.p;
-  CK(hipMemsetAsync(rc_dev, DCC_RC_RCOK, d.n, stream));
+  // groups are always produced (readiness is derived from them)
   uint32_t* grp_dev = nullptr;
-  if (out_group) {
-    if (dev_out) {
-      grp_dev = out_group;
-    } else {
-      CR(cv_group.ensure(this, std::max<uint64_t>(16, d.nnz * 4), "calvin group"));
-      grp_dev = (uint32_t*)cv_group.p;
-    }
+  if (out_group && dev_out) {
+    grp_dev = out_group;
+  } else {
+    CR(cv_group.ensure(this, std::max<uint64_t>(16, d.nnz * 4), "calvin group"));
+    grp_dev = (uint32_t*)cv_group.p;
   }
   const bool waves = out_wave != nullptr;
   uint32_t* wave_dev = nullptr;
@@ -722,6 +836,9 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint3
     CK(hipEventRecord(pev[1], stream));
     CK(hipEventRecord(pev[2], stream));
   }
+  if (d.nnz) k_cv_ready<<<grid1(d.n, 256), 256, 0, stream>>>(d.off, d.n, grp_dev, rc_dev);
+  else CK(hipMemsetAsync(rc_dev, DCC_RC_RCOK, d.n, stream));
+  CK(hipGetLastError());
   if (profiling) CK(hipEventRecord(pev[3], stream));
 
   // ---- sharded: grant groups are per row, hence shard-local; a txn is

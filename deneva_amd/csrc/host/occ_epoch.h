@@ -91,7 +91,9 @@ class OccEpoch {
         err = close_locked();
         break;
       }
-      cv_.wait_for(lk, std::chrono::microseconds(200));
+      // a system_clock deadline (pthread_cond_timedwait: the wait ThreadSanitizer
+      // intercepts; a 200 us poll does not care about clock steps)
+      cv_.wait_until(lk, std::chrono::system_clock::now() + std::chrono::microseconds(200));
     }
     waiting_--;
     auto it = decided_.find(ep);

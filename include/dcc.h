@@ -366,8 +366,8 @@ int dcc_gen_tpcc(const dcc_tpcc_params* p, uint32_t* offsets, uint64_t* keys,
 /* One captured epoch on disk: the CSR access lists,
  * optional timestamps / sequencer order, optional decisions.  Versioned,
  * checksummed (FNV-1a 64), little-endian; layout in batch_file.cpp.  Host
- * pointers only. */
-#define DCC_FILE_VERSION 1
+ * pointers only.  Version 2's checksum also covers the header fields. */
+#define DCC_FILE_VERSION 2   /* written; version 1 files are still read */
 #define DCC_FILE_OCC 1
 #define DCC_FILE_CALVIN 2
 #define DCC_FILE_HAS_TN 0x1u         /* start_tn + finish_tn                     */

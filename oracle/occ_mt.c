@@ -145,7 +145,8 @@ static void* worker(void* p) {
     for (uint64_t q = b; q < e; q++) {
       const uint32_t t = L[q];
       for (uint32_t x = s->off[t]; x < s->off[t + 1]; x++)
-        if (s->at[x] == AT_WR) s->und[s->aslot[x]] = NONE;
+        if (s->at[x] == AT_WR)  /* several threads may reset one key: atomic (TSan) */
+          __atomic_store_n(&s->und[s->aslot[x]], NONE, __ATOMIC_RELAXED);
     }
     pthread_barrier_wait(&s->bar);
     if (id == 0) {

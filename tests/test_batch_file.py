@@ -81,8 +81,19 @@ def test_truncated_and_foreign(tmp_path):
     with pytest.raises(DccError):
         d.read_batch_file(str(tmp_path / "missing.dccb"))
     bad = bytearray(raw)
-    bad[4:6] = (2).to_bytes(2, "little")  # a future version
+    bad[4:6] = (3).to_bytes(2, "little")  # a future version
     open(p, "wb").write(bytes(bad))
+    with pytest.raises(DccError):
+        d.read_batch_file(p)
+    # version 2 checksums the header too: a flipped seed / epoch is caught
+    for pos in (32, 41, 50, 6, 9):
+        bad = bytearray(raw)
+        bad[pos] ^= 0x5A
+        open(p, "wb").write(bytes(bad))
+        with pytest.raises(DccError):
+            d.read_batch_file(p)
+    # trailing bytes are rejected
+    open(p, "wb").write(raw + b"\0" * 8)
     with pytest.raises(DccError):
         d.read_batch_file(p)
 
