@@ -162,6 +162,7 @@ FILE_HAS_WAVE = 0x20
 _P = C.c_void_p
 _SIGS = [
     ("dcc_init", C.c_int, [C.POINTER(C.c_void_p), C.c_int]),
+    ("dcc_init_multi", C.c_int, [C.POINTER(C.c_void_p), C.c_int, _P]),
     ("dcc_destroy", None, [_P]),
     ("dcc_strerror", C.c_char_p, [C.c_int]),
     ("dcc_last_error", C.c_char_p, [_P]),

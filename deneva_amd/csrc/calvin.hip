@@ -909,6 +909,7 @@ extern "C" uint64_t dcc_calvin_alg_bytes(uint64_t n_txn, uint64_t nnz, int with_
 extern "C" int dcc_calvin_order_epoch(dcc_ctx* ctx, const dcc_batch* batch, uint32_t* out_group,
                                       uint8_t* out_rc, uint32_t* out_wave, dcc_stats* st) {
   if (!ctx) return DCC_EINVAL;
+  if (ctx->multi) return dcc_multi_calvin_epoch(ctx, batch, nullptr, out_group, out_rc, out_wave, st);
   if (hipSetDevice(ctx->device) != hipSuccess) return DCC_ENODEV;
   return ctx->calvin_epoch(batch, nullptr, out_group, out_rc, out_wave, st);
 }
@@ -917,6 +918,7 @@ extern "C" int dcc_calvin_order_epoch_held(dcc_ctx* ctx, const dcc_batch* batch,
                                            const dcc_calvin_held* held, uint32_t* out_group,
                                            uint8_t* out_rc, uint32_t* out_wave, dcc_stats* st) {
   if (!ctx) return DCC_EINVAL;
+  if (ctx->multi) return dcc_multi_calvin_epoch(ctx, batch, held, out_group, out_rc, out_wave, st);
   if (hipSetDevice(ctx->device) != hipSuccess) return DCC_ENODEV;
   return ctx->calvin_epoch(batch, held, out_group, out_rc, out_wave, st);
 }

@@ -59,6 +59,25 @@ int dcc_ctx::comm_allreduce_max_u8(uint8_t* dev, uint64_t n) {
   return DCC_OK;
 }
 
+int dcc_ctx::comm_allgather_u8(const uint8_t* send, uint8_t* recv, uint64_t bytes) {
+  const int R = comm_ranks(), me = comm_rank();
+  if (R <= 1) {
+    const hipError_t e = hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, stream);
+    return e == hipSuccess ? DCC_OK : hip_fail(e, "allgather copy");
+  }
+  if (comm->nccl) {
+    const ncclResult_t r = ncclAllGather(send, recv, bytes, ncclUint8, comm->nccl, stream);
+    if (r != ncclSuccess) return fail(DCC_ECOMM, "ncclAllGather: %s", ncclGetErrorString(r));
+    return DCC_OK;
+  }
+  // host exchange: own slot in a zeroed buffer, then the byte-wise MAX
+  hipError_t e = hipMemsetAsync(recv, 0, bytes * R, stream);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(recv + (uint64_t)me * bytes, send, bytes, hipMemcpyDeviceToDevice, stream);
+  if (e != hipSuccess) return hip_fail(e, "allgather staging");
+  return comm_allreduce_max_u8(recv, bytes * R);
+}
+
 extern "C" int dcc_comm_unique_id(void* out_id) {
   if (!out_id) return DCC_EINVAL;
   ncclUniqueId id;
@@ -69,6 +88,7 @@ extern "C" int dcc_comm_unique_id(void* out_id) {
 
 static int comm_check(dcc_ctx* ctx, int rank, int nranks) {
   if (!ctx || nranks < 1 || rank < 0 || rank >= nranks) return DCC_EINVAL;
+  if (ctx->multi) return ctx->fail(DCC_EINVAL, "multi-GPU context: its communicator is internal");
   if (ctx->comm) return ctx->fail(DCC_EINVAL, "communicator already initialised");
   return DCC_OK;
 }
@@ -90,6 +110,16 @@ extern "C" int dcc_comm_init(dcc_ctx* ctx, int rank, int nranks, const void* uni
       return ctx->fail(DCC_ECOMM, "ncclCommInitRank: %s", ncclGetErrorString(e));
     }
   }
+  ctx->comm = c;
+  return DCC_OK;
+}
+
+// dcc_init_multi: a sub-context joins the clique ncclCommInitAll made
+int dcc_comm_attach(dcc_ctx* ctx, int rank, int nranks, void* nccl_comm) {
+  auto* c = new dcc_comm_state;
+  c->rank = rank;
+  c->nranks = nranks;
+  c->nccl = (ncclComm_t)nccl_comm;
   ctx->comm = c;
   return DCC_OK;
 }
@@ -118,4 +148,7 @@ extern "C" int dcc_comm_destroy(dcc_ctx* ctx) {
 }
 
 extern "C" int dcc_comm_rank(const dcc_ctx* ctx) { return ctx && ctx->comm ? ctx->comm->rank : 0; }
-extern "C" int dcc_comm_size(const dcc_ctx* ctx) { return ctx && ctx->comm ? ctx->comm->nranks : 1; }
+extern "C" int dcc_comm_size(const dcc_ctx* ctx) {
+  if (ctx && ctx->multi) return dcc_multi_size(ctx);
+  return ctx && ctx->comm ? ctx->comm->nranks : 1;
+}

@@ -38,6 +38,7 @@ struct DevBatch {
 };
 
 struct dcc_comm_state;  // RCCL communicator (dcc_comm.hip)
+struct dcc_multi;       // single-process multi-GPU context (dcc_multi.cpp)
 
 // One level of the device OCC history (occ_history.h): flat (key, tn) pairs in
 // append order and, once built, the pairs sorted by (key, tn) with the key
@@ -81,6 +82,7 @@ struct dcc_ctx {
   bool profiling = false;
   uint64_t recheck_max = 16384;   // fold the kill wave into rounds with lists <= this
   uint32_t batch_max = 8;       // rounds enqueued between host synchronisations
+  bool bars_used = false;       // this epoch's rounds used grid-barrier words
   int solver = 0;               // 0 auto (sweep), 1 fixed-point rounds, 3 sweep
   bool use_sweep() const { return solver != 1; }
   uint32_t sw_levels = 4;
@@ -120,7 +122,7 @@ struct dcc_ctx {
   DevBuf hasw_scr;                               // round-solver hand-off
   DevBuf sw_ctl, sw_status, sw_ckeys, sw_dbg;            // sweep solver: level control, look-back, C
   DevBuf sw_rec, sw_rk, sw_gtab, sw_fw, sw_aent, sw_mg;
-  DevBuf sw_xcnt, sw_xrec, sw_mcnt, sw_moff, sw_mkeys, sw_mat, sw_kill;  // key-sharded sweep  // sweep tile records
+  DevBuf sw_xcnt, sw_xsend, sw_xrec, sw_mcnt, sw_moff, sw_mkeys, sw_mat, sw_kill;  // key-sharded sweep  // sweep tile records
   SubBufs sw_list[2];                            // sweep level lists (ping-pong)
   DevBuf l_tid[2], l_coff[2], l_cent[2];         // ping-pong undecided lists
   // OCC history (occ.h:62-64) on the device: base + delta levels
@@ -141,8 +143,11 @@ struct dcc_ctx {
   uint64_t tnc = 0;
 
   dcc_comm_state* comm = nullptr;
+  dcc_multi* multi = nullptr;  // non-null: this context drives per-GPU sub-contexts
   int comm_ranks() const;
   int comm_allreduce_max_u8(uint8_t* dev, uint64_t n);  // in place, on `stream`
+  // every rank's `bytes` from send into recv[rank * bytes ...], on `stream`
+  int comm_allgather_u8(const uint8_t* send, uint8_t* recv, uint64_t bytes);
   int comm_rank() const;
 
   int fail(int code, const char* fmt, ...);
@@ -177,3 +182,13 @@ struct dcc_ctx {
   int calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint32_t* out_group,
                    uint8_t* out_rc, uint32_t* out_wave, dcc_stats* st);
 };
+
+// multi-GPU context (dcc_multi.cpp)
+int dcc_multi_size(const dcc_ctx* ctx);
+void dcc_multi_destroy(dcc_ctx* ctx);
+int dcc_multi_occ_epoch(dcc_ctx* ctx, const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn,
+                        dcc_stats* st);
+int dcc_multi_calvin_epoch(dcc_ctx* ctx, const dcc_batch* b, const dcc_calvin_held* held,
+                           uint32_t* out_group, uint8_t* out_rc, uint32_t* out_wave, dcc_stats* st);
+int dcc_multi_each(dcc_ctx* ctx, int (*fn)(dcc_ctx*, void*), void* user);
+dcc_ctx* dcc_multi_sub(dcc_ctx* ctx, int rank);

@@ -124,6 +124,10 @@ extern "C" int dcc_init(dcc_ctx** out, int device_id) {
   CK(hipHostGetDevicePointer(&ctx->hpart_dev, ctx->hpart, 0));
   int rc = ctx->misc.ensure(ctx, 16384, "misc");
   if (!rc) rc = ctx->part.ensure(ctx, 1 << 16, "partials");
+  // counters and barrier words start zeroed (hipMalloc memory is not)
+  if (!rc && (hipMemset(ctx->misc.p, 0, 16384) != hipSuccess ||
+              hipMemset(ctx->part.p, 0, 1 << 16) != hipSuccess))
+    rc = DCC_EIO;
   if (rc) {
     dcc_destroy(ctx);
     return rc;
@@ -134,6 +138,7 @@ extern "C" int dcc_init(dcc_ctx** out, int device_id) {
 
 extern "C" void dcc_destroy(dcc_ctx* ctx) {
   if (!ctx) return;
+  dcc_multi_destroy(ctx);
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->graph_exec) (void)hipGraphExecDestroy(ctx->graph_exec);
@@ -151,12 +156,19 @@ extern "C" void dcc_destroy(dcc_ctx* ctx) {
 
 extern "C" int dcc_set_profiling(dcc_ctx* ctx, int enable) {
   if (!ctx) return DCC_EINVAL;
+  if (ctx->multi)
+    for (int r = 0; r < dcc_multi_size(ctx); r++) dcc_multi_sub(ctx, r)->profiling = enable != 0;
   ctx->profiling = enable != 0;
   return DCC_OK;
 }
 
 extern "C" int dcc_set_option(dcc_ctx* ctx, int option, int64_t value) {
   if (!ctx) return DCC_EINVAL;
+  if (ctx->multi)
+    for (int r = 0; r < dcc_multi_size(ctx); r++) {
+      const int e = dcc_set_option(dcc_multi_sub(ctx, r), option, value);
+      if (e != DCC_OK) return e;
+    }
   switch (option) {
     case DCC_OPT_RECHECK:
       if (value < 0) return DCC_EINVAL;
@@ -184,6 +196,7 @@ extern "C" int dcc_set_option(dcc_ctx* ctx, int option, int64_t value) {
 
 extern "C" int dcc_set_stream(dcc_ctx* ctx, void* s) {
   if (!ctx) return DCC_EINVAL;
+  if (ctx->multi) return ctx->fail(DCC_ENOTSUP, "multi-GPU context: one stream per sub-context");
   ctx->stream = s ? (hipStream_t)s : ctx->own_stream;
   return DCC_OK;
 }
@@ -195,7 +208,7 @@ std::vector<DevBuf*> dcc_ctx::all_bufs() {
                             &cv_scratch, &cv_agg, &cv_group, &cv_wave, &cv_pgx, &cv_gsx,
                             &cv_gsize, &cv_done, &cv_maxl, &cv_seq_b, &cv_ok, &cv_len,
                             &cv_off2, &cv_tsum, &cv_hkeys, &cv_hat, &gst, &hasw_scr, &sw_ctl, &sw_status, &sw_dbg,
-                            &sw_ckeys, &sw_gtab, &sw_rec, &sw_rk, &sw_fw, &sw_aent, &sw_mg, &sw_xcnt,
+                            &sw_ckeys, &sw_gtab, &sw_rec, &sw_rk, &sw_fw, &sw_aent, &sw_mg, &sw_xcnt, &sw_xsend,
                             &sw_xrec, &sw_mcnt, &sw_moff, &sw_mkeys, &sw_mat, &sw_kill,
                             &snap_top, &snap_aoff, &snap_aidx, &snap_cnt, &mt_rk, &mt_rlr, &mt_rlw,
                             &mt_misc, &mt_slot, &mt_sval, &mt_slot2, &mt_sval2, &mt_owner, &mt_sfl,
@@ -215,6 +228,11 @@ std::vector<DevBuf*> dcc_ctx::all_bufs() {
 
 extern "C" int dcc_reserve(dcc_ctx* ctx, uint64_t max_txn, uint64_t max_nnz) {
   if (!ctx) return DCC_EINVAL;
+  if (ctx->multi)
+    for (int r = 0; r < dcc_multi_size(ctx); r++) {
+      const int e = dcc_reserve(dcc_multi_sub(ctx, r), max_txn, max_nnz);
+      if (e != DCC_OK) return e;
+    }
   (void)hipSetDevice(ctx->device);
   const uint32_t tw = ROUND_CAP / MAX_TXN_LEN;  // worst case: MAX_ROW_PER_TXN-long txns
   int rc = ctx->state.ensure(ctx, max_txn + 16, "state");
@@ -348,6 +366,19 @@ extern "C" int dcc_occ_history_append(dcc_ctx* ctx, const uint64_t* keys, const 
                                       uint64_t n) {
   if (!ctx || (n && (!keys || !tn))) return DCC_EINVAL;
   if (n == 0) return DCC_OK;
+  if (ctx->multi) {  // each rank keeps its key shard's history
+    const int R = dcc_multi_size(ctx);
+    std::vector<std::vector<uint64_t>> k(R), t(R);
+    for (uint64_t i = 0; i < n; i++) {
+      const uint32_t r = dcc_key_shard(keys[i], (uint32_t)R);
+      k[r].push_back(keys[i]);
+      t[r].push_back(tn[i]);
+    }
+    for (int r = 0; r < R; r++)
+      if (!k[r].empty()) CR(dcc_occ_history_append(dcc_multi_sub(ctx, r), k[r].data(), t[r].data(),
+                                                   k[r].size()));
+    return DCC_OK;
+  }
   if (hipSetDevice(ctx->device) != hipSuccess) return DCC_ENODEV;
   // stable by tn, so that the batch keeps tn order within every key
   std::vector<uint64_t> idx(n);
@@ -369,6 +400,8 @@ extern "C" int dcc_occ_history_append(dcc_ctx* ctx, const uint64_t* keys, const 
 
 extern "C" int dcc_occ_history_clear(dcc_ctx* ctx) {
   if (!ctx) return DCC_EINVAL;
+  if (ctx->multi)
+    for (int r = 0; r < dcc_multi_size(ctx); r++) dcc_occ_history_clear(dcc_multi_sub(ctx, r));
   for (HistStore& h : ctx->hs) {
     h.m = 0;
     h.max_tn = 0;
@@ -381,6 +414,10 @@ extern "C" int dcc_occ_history_clear(dcc_ctx* ctx) {
 
 extern "C" int dcc_occ_history_trim(dcc_ctx* ctx, uint64_t tn_floor) {
   if (!ctx) return DCC_EINVAL;
+  if (ctx->multi) {
+    for (int r = 0; r < dcc_multi_size(ctx); r++) CR(dcc_occ_history_trim(dcc_multi_sub(ctx, r), tn_floor));
+    return DCC_OK;
+  }
   if (hipSetDevice(ctx->device) != hipSuccess) return DCC_ENODEV;
   HistStore& B = ctx->hs[0];
   HistStore& D = ctx->hs[1];
@@ -419,11 +456,32 @@ extern "C" int dcc_occ_history_trim(dcc_ctx* ctx, uint64_t tn_floor) {
   return DCC_OK;
 }
 
-extern "C" uint64_t dcc_occ_history_size(const dcc_ctx* ctx) { return ctx ? ctx->hist_size() : 0; }
+extern "C" uint64_t dcc_occ_history_size(const dcc_ctx* ctx) {
+  if (!ctx) return 0;
+  if (ctx->multi) {
+    uint64_t s = 0;
+    for (int r = 0; r < dcc_multi_size(ctx); r++) s += dcc_multi_sub((dcc_ctx*)ctx, r)->hist_size();
+    return s;
+  }
+  return ctx->hist_size();
+}
 
 extern "C" int dcc_occ_history_export(dcc_ctx* ctx, uint64_t* keys, uint64_t* tn, uint64_t cap,
                                       uint64_t* out_n) {
   if (!ctx || !out_n) return DCC_EINVAL;
+  if (ctx->multi) {
+    const uint64_t total = dcc_occ_history_size(ctx);
+    *out_n = total;
+    if (!keys || !tn) return DCC_OK;
+    if (cap < total) return DCC_ERANGE;
+    uint64_t at = 0;
+    for (int r = 0; r < dcc_multi_size(ctx); r++) {
+      uint64_t m = 0;
+      CR(dcc_occ_history_export(dcc_multi_sub(ctx, r), keys + at, tn + at, cap - at, &m));
+      at += m;
+    }
+    return DCC_OK;
+  }
   if (hipSetDevice(ctx->device) != hipSuccess) return DCC_ENODEV;
   const uint64_t n = ctx->hist_size();
   *out_n = n;
@@ -441,10 +499,15 @@ extern "C" int dcc_occ_history_export(dcc_ctx* ctx, uint64_t* keys, uint64_t* tn
 
 extern "C" int dcc_occ_set_tnc(dcc_ctx* ctx, uint64_t tnc) {
   if (!ctx) return DCC_EINVAL;
+  if (ctx->multi)
+    for (int r = 0; r < dcc_multi_size(ctx); r++) dcc_multi_sub(ctx, r)->tnc = tnc;
   ctx->tnc = tnc;
   return DCC_OK;
 }
-extern "C" uint64_t dcc_occ_get_tnc(const dcc_ctx* ctx) { return ctx ? ctx->tnc : 0; }
+extern "C" uint64_t dcc_occ_get_tnc(const dcc_ctx* ctx) {
+  if (ctx && ctx->multi) return dcc_multi_sub((dcc_ctx*)ctx, 0)->tnc;
+  return ctx ? ctx->tnc : 0;
+}
 
 // ---------------------------------------------------------------- batch checks
 int dcc_ctx::check_batch(const dcc_batch* b) {
@@ -520,6 +583,7 @@ int dcc_ctx::stage_batch(const dcc_batch* b, DevBatch& d) {
 extern "C" int dcc_occ_validate_epoch(dcc_ctx* ctx, const dcc_batch* batch, uint8_t* out_rc,
                                       uint64_t* out_commit_tn, dcc_stats* out_stats) {
   if (!ctx) return DCC_EINVAL;
+  if (ctx->multi) return dcc_multi_occ_epoch(ctx, batch, out_rc, out_commit_tn, out_stats);
   if (hipSetDevice(ctx->device) != hipSuccess) return DCC_ENODEV;
   return ctx->occ_epoch(batch, out_rc, out_commit_tn, out_stats);
 }

@@ -1,0 +1,294 @@
+// Single-process multi-GPU context (dcc_init(&ctx, n_gpus,
+// device_ids), multi-GPU internal to the context).  A reference node is one
+// rundb process with one occ_man (system/global.cpp:42); with this context
+// that one process drives every GPU of the node.
+//
+// The context owns one per-device sub-context per GPU, key-sharded exactly
+// like the one-process-per-GPU path (dcc_key_shard; each sub-context holds
+// only its shard's accesses).  The sub-contexts talk over one RCCL clique
+// made with ncclCommInitAll when the device ids are distinct; when ids repeat
+// (several shards on one GPU: tests, or a node with fewer GPUs than shards)
+// over an in-process host exchange.  One host thread per sub-context runs its
+// epoch, so every rank's collectives and host synchronisations proceed as in
+// the multi-process path.  Decisions are identical on every rank (the kill /
+// readiness bytes are all-reduced): rank 0's are returned.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <condition_variable>
+#include <cstring>
+#include <mutex>
+#include <set>
+#include <thread>
+#include <vector>
+
+#include "dcc.h"
+#include "dcc_ctx.h"
+
+int dcc_comm_attach(dcc_ctx* ctx, int rank, int nranks, void* nccl_comm);  // dcc_comm.hip
+
+namespace {
+
+// Byte-wise MAX all-reduce among the host threads of one process.
+struct LocalExchange {
+  int n = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+  uint64_t gen = 0;
+  int arrived = 0;
+  bool bad = false;
+  std::vector<uint8_t> acc, result;
+};
+struct LocalPart {
+  LocalExchange* x;
+  int rank;
+};
+
+int local_exchange(void* user, uint8_t* buf, uint64_t nb) {
+  LocalPart* p = (LocalPart*)user;
+  LocalExchange* X = p->x;
+  std::unique_lock<std::mutex> lk(X->mu);
+  const uint64_t g = X->gen;
+  if (X->arrived == 0) {
+    X->acc.assign(buf, buf + nb);
+    X->bad = false;
+  } else if (X->acc.size() != nb) {
+    X->bad = true;  // ranks disagree on the exchange size: every rank fails
+  } else {
+    for (uint64_t i = 0; i < nb; i++) X->acc[i] = std::max(X->acc[i], buf[i]);
+  }
+  if (++X->arrived == X->n) {
+    X->result.swap(X->acc);
+    X->arrived = 0;
+    X->gen++;
+    X->cv.notify_all();
+  } else {
+    X->cv.wait(lk, [&] { return X->gen != g; });
+  }
+  if (X->bad || X->result.size() != nb) return 1;
+  memcpy(buf, X->result.data(), nb);
+  return 0;
+}
+
+// The shard of one rank: its accesses, and where each sat in the batch.
+struct Shard {
+  std::vector<uint32_t> off;
+  std::vector<uint64_t> keys;
+  std::vector<uint8_t> at;
+  std::vector<uint32_t> src;  // batch access index of each shard access
+};
+
+void make_shards(const dcc_batch* b, int R, std::vector<Shard>& sh) {
+  sh.assign(R, Shard{});
+  for (int r = 0; r < R; r++) {
+    sh[r].off.assign(b->n_txn + 1, 0);
+    sh[r].keys.reserve(b->nnz / R + 16);
+    sh[r].at.reserve(b->nnz / R + 16);
+    sh[r].src.reserve(b->nnz / R + 16);
+  }
+  for (uint64_t t = 0; t < b->n_txn; t++) {
+    for (uint32_t x = b->offsets[t]; x < b->offsets[t + 1]; x++) {
+      const int r = (int)dcc_key_shard(b->keys[x], (uint32_t)R);
+      sh[r].keys.push_back(b->keys[x]);
+      sh[r].at.push_back(b->acctype[x]);
+      sh[r].src.push_back(x);
+    }
+    for (int r = 0; r < R; r++) sh[r].off[t + 1] = (uint32_t)sh[r].keys.size();
+  }
+}
+
+dcc_batch shard_batch(const dcc_batch* b, const Shard& s) {
+  dcc_batch o = *b;
+  o.nnz = s.keys.size();
+  o.offsets = s.off.data();
+  o.keys = s.keys.data();
+  o.acctype = s.at.data();
+  return o;
+}
+
+}  // namespace
+
+struct dcc_multi {
+  std::vector<dcc_ctx*> sub;
+  LocalExchange lx;
+  std::vector<LocalPart> parts;
+};
+
+// Runs fn(rank) on one host thread per sub-context; the first failure's code
+// and message become the multi context's.
+template <typename F>
+static int run_ranks(dcc_ctx* ctx, F fn) {
+  dcc_multi* M = ctx->multi;
+  const int R = (int)M->sub.size();
+  std::vector<int> rc(R, DCC_OK);
+  std::vector<std::thread> th;
+  for (int r = 0; r < R; r++)
+    th.emplace_back([&, r] {
+      if (hipSetDevice(M->sub[r]->device) != hipSuccess) {
+        rc[r] = DCC_ENODEV;
+        return;
+      }
+      rc[r] = fn(r, M->sub[r]);
+    });
+  for (auto& t : th) t.join();
+  for (int r = 0; r < R; r++)
+    if (rc[r] != DCC_OK) {
+      ctx->last_error = "rank " + std::to_string(r) + ": " + M->sub[r]->last_error;
+      return rc[r];
+    }
+  return DCC_OK;
+}
+
+extern "C" int dcc_init_multi(dcc_ctx** out, int n_gpus, const int* device_ids) {
+  if (!out || n_gpus < 1 || !device_ids) return DCC_EINVAL;
+  *out = nullptr;
+  dcc_ctx* root = nullptr;
+  int r = dcc_init(&root, device_ids[0]);
+  if (r != DCC_OK) return r;
+  dcc_multi* M = new dcc_multi;
+  root->multi = M;
+  for (int i = 0; i < n_gpus; i++) {
+    dcc_ctx* s = nullptr;
+    r = dcc_init(&s, device_ids[i]);
+    if (r != DCC_OK) {
+      dcc_destroy(root);
+      return r;
+    }
+    M->sub.push_back(s);
+  }
+  if (n_gpus > 1) {
+    const std::set<int> distinct(device_ids, device_ids + n_gpus);
+    if ((int)distinct.size() == n_gpus) {
+      // one RCCL clique over the node's GPUs (xGMI), one communicator per rank
+      std::vector<ncclComm_t> comms(n_gpus);
+      const ncclResult_t e = ncclCommInitAll(comms.data(), n_gpus, device_ids);
+      if (e != ncclSuccess) {
+        root->last_error = std::string("ncclCommInitAll: ") + ncclGetErrorString(e);
+        dcc_destroy(root);
+        return DCC_ECOMM;
+      }
+      for (int i = 0; i < n_gpus; i++) dcc_comm_attach(M->sub[i], i, n_gpus, comms[i]);
+    } else {
+      // shards sharing a GPU: the in-process host exchange
+      M->lx.n = n_gpus;
+      M->parts.resize(n_gpus);
+      for (int i = 0; i < n_gpus; i++) {
+        M->parts[i] = LocalPart{&M->lx, i};
+        r = dcc_comm_init_host(M->sub[i], i, n_gpus, local_exchange, &M->parts[i]);
+        if (r != DCC_OK) {
+          dcc_destroy(root);
+          return r;
+        }
+      }
+    }
+  }
+  *out = root;
+  return DCC_OK;
+}
+
+int dcc_multi_size(const dcc_ctx* ctx) { return ctx && ctx->multi ? (int)ctx->multi->sub.size() : 1; }
+
+void dcc_multi_destroy(dcc_ctx* ctx) {
+  if (!ctx->multi) return;
+  for (dcc_ctx* s : ctx->multi->sub) dcc_destroy(s);
+  delete ctx->multi;
+  ctx->multi = nullptr;
+}
+
+int dcc_multi_occ_epoch(dcc_ctx* ctx, const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn,
+                        dcc_stats* st) {
+  if (!b) return ctx->fail(DCC_EINVAL, "null batch");
+  if (b->flags & DCC_DEVICE_PTRS)
+    return ctx->fail(DCC_ENOTSUP, "multi-GPU context: host batches (it shards them itself)");
+  // the whole batch is validated before it is sharded: every rank then
+  // runs the same collectives (no rank may fail alone mid-exchange)
+  if (int e = ctx->check_batch(b)) return e;
+  const int R = (int)ctx->multi->sub.size();
+  std::vector<Shard> sh;
+  make_shards(b, R, sh);
+  std::vector<std::vector<uint8_t>> rc(R, std::vector<uint8_t>(b->n_txn + 1));
+  std::vector<std::vector<uint64_t>> tn(R, std::vector<uint64_t>(out_tn ? b->n_txn + 1 : 0));
+  std::vector<dcc_stats> S(R);
+  const int e = run_ranks(ctx, [&](int r, dcc_ctx* s) {
+    const dcc_batch sb = shard_batch(b, sh[r]);
+    return dcc_occ_validate_epoch(s, &sb, rc[r].data(), out_tn ? tn[r].data() : nullptr, &S[r]);
+  });
+  if (e != DCC_OK) return e;
+  for (int r = 1; r < R; r++)
+    if (memcmp(rc[r].data(), rc[0].data(), b->n_txn) != 0)
+      return ctx->fail(DCC_EIO, "multi-GPU: ranks 0 and %d decided differently", r);
+  if (out_rc) memcpy(out_rc, rc[0].data(), b->n_txn);
+  if (out_tn) memcpy(out_tn, tn[0].data(), b->n_txn * 8);
+  if (st) {
+    *st = S[0];
+    for (int r = 1; r < R; r++) st->device_ms = std::max(st->device_ms, S[r].device_ms);
+    st->nnz_w = 0;
+    for (int r = 0; r < R; r++) st->nnz_w += S[r].nnz_w;
+    st->alg_bytes = dcc_alg_bytes(b->n_txn, b->nnz, st->nnz_w);
+  }
+  return DCC_OK;
+}
+
+int dcc_multi_calvin_epoch(dcc_ctx* ctx, const dcc_batch* b, const dcc_calvin_held* held,
+                           uint32_t* out_group, uint8_t* out_rc, uint32_t* out_wave,
+                           dcc_stats* st) {
+  if (!b) return ctx->fail(DCC_EINVAL, "null batch");
+  if (b->flags & DCC_DEVICE_PTRS)
+    return ctx->fail(DCC_ENOTSUP, "multi-GPU context: host batches (it shards them itself)");
+  if (out_wave) return ctx->fail(DCC_ENOTSUP, "calvin: wave levels need the whole epoch on one GPU");
+  if (int e = ctx->check_batch(b)) return e;
+  if (held && held->n && (!held->keys || !held->acctype))
+    return ctx->fail(DCC_EINVAL, "calvin: null held arrays");
+  const int R = (int)ctx->multi->sub.size();
+  std::vector<Shard> sh;
+  make_shards(b, R, sh);
+  // the held prefix is sharded by row as well
+  std::vector<std::vector<uint64_t>> hk(R);
+  std::vector<std::vector<uint8_t>> ha(R);
+  if (held)
+    for (uint64_t i = 0; i < held->n; i++) {
+      const int r = (int)dcc_key_shard(held->keys[i], (uint32_t)R);
+      hk[r].push_back(held->keys[i]);
+      ha[r].push_back(held->acctype[i]);
+    }
+  std::vector<std::vector<uint8_t>> rc(R, std::vector<uint8_t>(b->n_txn + 1));
+  std::vector<std::vector<uint32_t>> grp(R);
+  std::vector<dcc_stats> S(R);
+  const int e = run_ranks(ctx, [&](int r, dcc_ctx* s) {
+    const dcc_batch sb = shard_batch(b, sh[r]);
+    grp[r].resize(sh[r].keys.size() + 1);
+    if (held) {
+      const dcc_calvin_held h{hk[r].size(), hk[r].data(), ha[r].data()};
+      return dcc_calvin_order_epoch_held(s, &sb, &h, grp[r].data(), rc[r].data(), nullptr, &S[r]);
+    }
+    return dcc_calvin_order_epoch(s, &sb, grp[r].data(), rc[r].data(), nullptr, &S[r]);
+  });
+  if (e != DCC_OK) return e;
+  if (out_rc) memcpy(out_rc, rc[0].data(), b->n_txn);
+  if (out_group)
+    for (int r = 0; r < R; r++)
+      for (size_t j = 0; j < sh[r].src.size(); j++) out_group[sh[r].src[j]] = grp[r][j];
+  if (st) {
+    *st = S[0];
+    for (int r = 1; r < R; r++) st->device_ms = std::max(st->device_ms, S[r].device_ms);
+    st->nnz_w = 0;
+    for (int r = 0; r < R; r++) st->nnz_w += S[r].nnz_w;
+    st->alg_bytes = dcc_calvin_alg_bytes(b->n_txn, b->nnz, b->order != nullptr, 0);
+  }
+  return DCC_OK;
+}
+
+// per-rank state kept identical on every rank (options, tnc, history)
+int dcc_multi_each(dcc_ctx* ctx, int (*fn)(dcc_ctx*, void*), void* user) {
+  for (dcc_ctx* s : ctx->multi->sub) {
+    const int r = fn(s, user);
+    if (r != DCC_OK) {
+      ctx->last_error = s->last_error;
+      return r;
+    }
+  }
+  return DCC_OK;
+}
+
+dcc_ctx* dcc_multi_sub(dcc_ctx* ctx, int rank) { return ctx->multi->sub[rank]; }

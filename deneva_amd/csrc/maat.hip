@@ -786,12 +786,14 @@ extern "C" uint64_t dcc_maat_alg_bytes(uint64_t n_txn, uint64_t nnz) {
 extern "C" int dcc_maat_validate_epoch(dcc_ctx* ctx, const dcc_batch* batch, uint8_t* out_rc,
                                        uint64_t* out_commit_ts, dcc_stats* out_stats) {
   if (!ctx) return DCC_EINVAL;
+  if (ctx->multi) return ctx->fail(DCC_ENOTSUP, "maat: single-GPU engine");
   if (hipSetDevice(ctx->device) != hipSuccess) return DCC_ENODEV;
   return ctx->maat_epoch(batch, out_rc, out_commit_ts, out_stats);
 }
 
 extern "C" int dcc_maat_rows_clear(dcc_ctx* ctx) {
   if (!ctx) return DCC_EINVAL;
+  if (ctx->multi) return ctx->fail(DCC_ENOTSUP, "maat: single-GPU engine");
   if (hipSetDevice(ctx->device) != hipSuccess) return DCC_ENODEV;
   if (ctx->mt_bits) {
     const uint64_t cap = 1ull << ctx->mt_bits;
@@ -808,6 +810,7 @@ extern "C" int dcc_maat_rows_clear(dcc_ctx* ctx) {
 extern "C" int dcc_maat_rows_set(dcc_ctx* ctx, const uint64_t* keys, const uint64_t* last_read,
                                  const uint64_t* last_write, uint64_t n) {
   if (!ctx || (n && (!keys || !last_read || !last_write))) return DCC_EINVAL;
+  if (ctx->multi) return ctx->fail(DCC_ENOTSUP, "maat: single-GPU engine");
   if (n == 0) return DCC_OK;
   if (hipSetDevice(ctx->device) != hipSuccess) return DCC_ENODEV;
   CR(ctx->mt_misc.ensure(ctx, 64 + MT_RING * 4, "maat counters"));
@@ -839,6 +842,7 @@ extern "C" int dcc_maat_rows_set(dcc_ctx* ctx, const uint64_t* keys, const uint6
 extern "C" int dcc_maat_rows_get(dcc_ctx* ctx, const uint64_t* keys, uint64_t* last_read,
                                  uint64_t* last_write, uint64_t n) {
   if (!ctx || (n && (!keys || !last_read || !last_write))) return DCC_EINVAL;
+  if (ctx->multi) return ctx->fail(DCC_ENOTSUP, "maat: single-GPU engine");
   if (n == 0) return DCC_OK;
   if (hipSetDevice(ctx->device) != hipSuccess) return DCC_ENODEV;
   if (!ctx->mt_bits) {

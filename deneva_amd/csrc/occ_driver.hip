@@ -223,6 +223,7 @@ int dcc_ctx::occ_rounds(const SubProb& sp, uint32_t maxlen, bool prof, uint32_t&
       // m_bound bounds this round's list (lists only shrink)
       const bool recheck = !sh && !first && m_bound <= recheck_max;
       ra.bar = recheck ? (GridBar*)(bars + (k % CTR_RING) * 16) : nullptr;
+      bars_used |= recheck;
       ra.bar_zero = (uint32_t*)(bars + ((k + 1) % CTR_RING) * 16);
       ra.gst = gstat;
       ra.err = err;
@@ -491,8 +492,13 @@ int dcc_ctx::sweep_sharded(const DevBatch& d, int& next_level) {
       if (r < me) before += share[r];
       total += share[r];
     }
-    // (3) the records, all-gathered; merged by txn into one CSR
-    CR(sw_xrec.ensure(this, std::max<uint64_t>(64, total * 12), "sweep exchange records"));
+    // (3) the records, all-gathered (ncclAllGather of every rank's share,
+    // padded to the largest); merged by txn into one CSR
+    uint32_t maxshare = 0;
+    for (int r = 0; r < R; r++) maxshare = std::max(maxshare, share[r]);
+    const uint64_t chunk = std::max<uint64_t>(1, maxshare) * 12;
+    CR(sw_xsend.ensure(this, chunk, "sweep exchange send"));
+    CR(sw_xrec.ensure(this, chunk * R, "sweep exchange records"));
     CR(sw_mcnt.ensure(this, 8ull * (P + 1) + 64, "sweep merge counts"));
     CR(sw_moff.ensure(this, 4ull * (P + 1) + 64, "sweep merged offsets"));
     CR(sw_mkeys.ensure(this, std::max<uint64_t>(64, total * 8), "sweep merged keys"));
@@ -500,14 +506,15 @@ int dcc_ctx::sweep_sharded(const DevBatch& d, int& next_level) {
     CR(sw_kill.ensure(this, (uint64_t)d.n + 64, "sweep kill bits"));
     uint32_t* xrec = (uint32_t*)sw_xrec.p;
     uint32_t* mcnt = (uint32_t*)sw_mcnt.p;
-    CK(hipMemsetAsync(xrec, 0, total * 12, stream));
+    CK(hipMemsetAsync(sw_xsend.p, 0xFF, chunk, stream));
     CK(hipMemsetAsync(mcnt, 0, 4ull * (P + 1), stream));
     CK(hipMemsetAsync(sw_kill.p, 0, m, stream));
-    launch_sw_merge(in, P, xrec, (uint32_t)(3 * before), 0, nullptr, nullptr, nullptr, nullptr,
+    launch_sw_merge(in, P, (uint32_t*)sw_xsend.p, 0, 0, nullptr, nullptr, nullptr, nullptr,
                     nullptr, true, stream);
-    CR(comm_allreduce_max_u8((uint8_t*)xrec, total * 12));
-    launch_sw_merge(in, P, xrec, 0, (uint32_t)total, mcnt, mcnt + (P + 1), (uint32_t*)sw_moff.p,
-                    (uint64_t*)sw_mkeys.p, (uint8_t*)sw_mat.p, false, stream);
+    CR(comm_allgather_u8((const uint8_t*)sw_xsend.p, (uint8_t*)xrec, chunk));
+    (void)before;
+    launch_sw_merge(in, P, xrec, 0, (uint32_t)(R * (chunk / 12)), mcnt, mcnt + (P + 1),
+                    (uint32_t*)sw_moff.p, (uint64_t*)sw_mkeys.p, (uint8_t*)sw_mat.p, false, stream);
     CK(hipGetLastError());
     SwShard shl;
     shl.serial = SwList{top ? nullptr : in.tid, (const uint32_t*)sw_moff.p,
@@ -637,6 +644,7 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   top.w_bound = nnz_w;
   uint32_t rounds = 0;
   uint32_t handoffs = 0;  // sweep lists handed to the round solver
+  bars_used = false;
   PeelInfo info;
   int next_level = 0;
   if (sweep) {
@@ -833,10 +841,10 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
 
   const uint32_t e = *(const uint32_t*)hmisc;
   {
-    // barrier timeout words (third word of each GridBar in the ring)
-    // (read back with the epoch's gather)
+    // barrier timeout words (third word of each GridBar in the ring, read
+    // back with the epoch's gather) of the rounds that used a grid barrier
     const uint32_t* bw = (const uint32_t*)((const char*)hmisc + MISC_BARS);
-    for (uint32_t q = 0; q < CTR_RING; q++)
+    for (uint32_t q = 0; q < CTR_RING && bars_used; q++)
       if (bw[q * 4 + 2]) return fail(DCC_EIO, "grid barrier timed out (grid not co-resident)");
   }
   if (e & ERR_KEY) return fail(DCC_EINVAL, "batch: key equal to DCC_KEY_RESERVED");

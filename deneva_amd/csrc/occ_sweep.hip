@@ -1265,9 +1265,8 @@ __global__ void k_sw_share(const uint32_t* m_dev, uint32_t m_host, const uint32_
 }
 
 // k_sw_export: this rank's accesses of the level's serial range (list txns
-// [0, P)) as 12-byte records {key, txn | type << 30} at its slot of the
-// exchange buffer (zero elsewhere: a byte-wise MAX all-reduce then is an
-// all-gather).
+// [0, P)) as 12-byte records {key, txn | type << 30} into its all-gather
+// contribution (padded with 0xFF records up to the largest share).
 __global__ __launch_bounds__(256) void k_sw_export(SwList in, uint32_t P, uint32_t* rec) {
   const uint64_t nnz = in.nnz;
   const uint32_t off0 = (uint32_t)min((uint64_t)in.off[0], nnz);
@@ -1287,9 +1286,13 @@ __global__ __launch_bounds__(256) void k_sw_export(SwList in, uint32_t P, uint32
 // k_sw_mcount / k_sw_mscan / k_sw_mscatter: every rank's records merged into
 // one CSR of the serial range, grouped by txn (a counting sort; the order of a
 // txn's accesses is irrelevant to OCC, which compares sets).
-__global__ __launch_bounds__(256) void k_sw_mcount(const uint32_t* rec, uint32_t n, uint32_t* cnt) {
-  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)
-    atomicAdd(&cnt[rec[3ull * i + 2] & 0x3FFFFFFFu], 1u);
+// (records whose txn field is >= P are all-gather padding: skipped)
+__global__ __launch_bounds__(256) void k_sw_mcount(const uint32_t* rec, uint32_t n, uint32_t P,
+                                                   uint32_t* cnt) {
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const uint32_t t = rec[3ull * i + 2] & 0x3FFFFFFFu;
+    if (t < P) atomicAdd(&cnt[t], 1u);
+  }
 }
 __global__ __launch_bounds__(1024) void k_sw_mscan(uint32_t* cnt, uint32_t P, uint32_t* off,
                                                    uint32_t* cur) {
@@ -1321,11 +1324,12 @@ __global__ __launch_bounds__(1024) void k_sw_mscan(uint32_t* cnt, uint32_t P, ui
   }
   if (j == 0) off[P] = s_carry;
 }
-__global__ __launch_bounds__(256) void k_sw_mscatter(const uint32_t* rec, uint32_t n,
+__global__ __launch_bounds__(256) void k_sw_mscatter(const uint32_t* rec, uint32_t n, uint32_t P,
                                                      uint32_t* cur, uint64_t* keys,
                                                      uint8_t* at) {
   for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
     const uint32_t w2 = rec[3ull * i + 2];
+    if ((w2 & 0x3FFFFFFFu) >= P) continue;  // padding
     const uint32_t q = atomicAdd(&cur[w2 & 0x3FFFFFFFu], 1u);
     keys[q] = ((uint64_t)rec[3ull * i + 1] << 32) | rec[3ull * i];
     at[q] = (uint8_t)(w2 >> 30);
@@ -1557,9 +1561,9 @@ void launch_sw_merge(const SwList& in, uint32_t P, uint32_t* xbuf, uint32_t xoff
     return;
   }
   const unsigned g = (unsigned)std::min<uint32_t>((n_all + 255) / 256 + 1, 2048);
-  k_sw_mcount<<<g, 256, 0, st>>>(xbuf, n_all, cnt);
+  k_sw_mcount<<<g, 256, 0, st>>>(xbuf, n_all, P, cnt);
   k_sw_mscan<<<1, 1024, 0, st>>>(cnt, P, moff, cur);
-  k_sw_mscatter<<<g, 256, 0, st>>>(xbuf, n_all, cur, mkeys, mat);
+  k_sw_mscatter<<<g, 256, 0, st>>>(xbuf, n_all, P, cur, mkeys, mat);
 }
 void launch_sw_compact(const SwFilterArgs& a, unsigned grid, hipStream_t st) {
   k_sw_compact<<<grid ? grid : 1u, SW_CHUNK, 0, st>>>(a);

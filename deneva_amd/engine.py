@@ -91,13 +91,21 @@ def _check(code: int, ctx=None) -> None:
 
 
 class Engine:
-    """One engine context per process and device (OptCC::init / occ_man)."""
+    """One engine context per process and device (OptCC::init / occ_man).
+    devices=[...]: one process drives several GPUs (dcc_init_multi): every
+    epoch is key-sharded over them inside the context."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, devices=None):
         h = C.c_void_p()
-        code = lib.dcc_init(C.byref(h), device)
+        if devices is not None:
+            ids = (C.c_int * len(devices))(*devices)
+            code = lib.dcc_init_multi(C.byref(h), len(devices), ids)
+        else:
+            code = lib.dcc_init(C.byref(h), device)
         if code != _abi.DCC_OK:
-            raise DccError(code, f"dcc_init(device={device}): {_abi.strerror(code)}")
+            detail = lib.dcc_last_error(h).decode() if h.value else ""
+            raise DccError(code, f"dcc_init(device={device}, devices={devices}): "
+                                 f"{_abi.strerror(code)} {detail}")
         self._h = h
 
     def close(self) -> None:

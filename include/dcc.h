@@ -126,6 +126,14 @@ typedef struct dcc_ctx dcc_ctx;
  * (system/global.cpp:42): one context per process and device.
  * device_id < 0 selects the current HIP device. */
 int dcc_init(dcc_ctx** out, int device_id);
+/* One process, n GPUs (multi-GPU internal to the context):
+ * the context key-shards every epoch over n per-device sub-contexts
+ * (dcc_key_shard) that exchange over one RCCL clique (ncclCommInitAll) when
+ * the ids are distinct, else over an in-process host exchange (shards sharing
+ * a GPU).  OCC and Calvin epochs take host batches and return the same
+ * decisions as one GPU; options, tnc and history apply to every shard.
+ * Snapshot validation, MaaT and dcc_set_stream are DCC_ENOTSUP on it. */
+int dcc_init_multi(dcc_ctx** out, int n_gpus, const int* device_ids);
 void dcc_destroy(dcc_ctx* ctx);
 const char* dcc_strerror(int code);
 const char* dcc_last_error(const dcc_ctx* ctx); /* detail of the last failure */

@@ -1,0 +1,78 @@
+"""GPU: the single-process multi-GPU context (dcc_init_multi, SURVEY.md
+§8(b): one process, the node's GPUs internal to the context).  On a one-GPU
+box the shards share the GPU and exchange in-process (the path is the one
+ncclCommInitAll drives on an 8-GPU node, only the transport differs).
+Decisions, commit tns, history and Calvin groups must equal one GPU / the
+oracle bit for bit, at the full C5 size."""
+import numpy as np
+import pytest
+
+import _oracle as orc
+import deneva_amd as d
+from deneva_amd import RD, WR
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def c5():
+    b = d.gen_ycsb(n_txn=1 << 20, zipf_theta=0.99, seed=0xD3E7A002)
+    erc, etn, etnc = orc.occ(b)
+    return b, erc, etn, etnc
+
+
+@pytest.mark.parametrize("shards", [2, 4, 8])
+def test_multi_occ_c5_full(c5, shards):
+    b, erc, etn, etnc = c5
+    with d.Engine(devices=[0] * shards) as eng:
+        assert eng.comm_size == shards
+        eng.tnc = 0
+        rc, tn, st = eng.occ_validate_epoch(b, want_tn=True)
+        assert np.array_equal(np.asarray(rc), erc)
+        assert np.array_equal(np.asarray(tn, np.uint64), etn)
+        assert eng.tnc == etnc and st["n_shards"] == shards
+
+
+def test_multi_history_and_calvin():
+    rng = np.random.default_rng(3)
+    with d.Engine(devices=[0, 0, 0]) as eng:
+        eng.tnc = 0
+        eng.history_clear()
+        hk, ht = np.zeros(0, np.uint64), np.zeros(0, np.uint64)
+        tnc = 0
+        for e in range(3):
+            b = d.gen_ycsb(n_txn=20000, zipf_theta=0.7, table_size=1 << 14, seed=40 + e)
+            b.start_tn = rng.integers(0, tnc + 1, size=b.n_txn).astype(np.uint64)
+            b.finish_tn = (b.start_tn + rng.integers(0, 200, size=b.n_txn)).astype(np.uint64)
+            erc, etn, etnc = orc.occ(b, hist_keys=hk, hist_tn=ht, tnc=tnc)
+            rc, tn, _ = eng.occ_validate_epoch(b, want_tn=True, append_history=True)
+            assert np.array_equal(np.asarray(rc), erc) and np.array_equal(np.asarray(tn), etn)
+            off = np.asarray(b.offsets, np.int64)
+            owner = np.repeat(np.arange(b.n_txn), np.diff(off))
+            sel = (np.asarray(b.acctype) == WR) & (etn[owner] != 0)
+            hk = np.concatenate([hk, np.asarray(b.keys)[sel]])
+            ht = np.concatenate([ht, etn[owner[sel]]])
+            tnc = etnc
+        assert eng.history_size == hk.size
+        c = d.gen_ycsb(n_txn=50000, zipf_theta=0.9, part_cnt=4, chunk_txns=4096)
+        c.order = rng.integers(0, 1 << 20, size=c.n_txn).astype(np.uint64)
+        g, crc, _, _ = eng.calvin_order_epoch(c, want_group=True)
+        eg, erc2, _ = orc.calvin(c)
+        assert np.array_equal(np.asarray(g).astype(np.uint32), eg)
+        assert np.array_equal(np.asarray(crc), erc2)
+        hk2 = np.asarray(c.keys[:3000], np.uint64)
+        ha2 = np.where(np.arange(3000) % 3 == 0, WR, RD).astype(np.uint8)
+        g, crc, _, _ = eng.calvin_order_epoch(c, want_group=True, held=(hk2, ha2))
+        eg, erc2 = orc.calvin_held(c, hk2, ha2)
+        assert np.array_equal(np.asarray(g).astype(np.uint32), eg)
+        assert np.array_equal(np.asarray(crc), erc2)
+
+
+def test_multi_rejects_device_batches_and_snapshot():
+    import torch
+    b = d.gen_ycsb(n_txn=1000, zipf_theta=0.9)
+    with d.Engine(devices=[0, 0]) as eng:
+        with pytest.raises(d.DccError):
+            eng.occ_validate_epoch(b.to_torch("cuda:0"))
+        with pytest.raises(d.DccError):
+            eng.maat_validate_epoch(b)

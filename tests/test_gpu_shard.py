@@ -120,3 +120,41 @@ def test_sharded_engine_matches_unsharded(world):
             got[owner == r] = g.astype(np.uint32)
             assert np.array_equal(crc, ecrc), f"rank {r}: calvin readiness differs"
         assert np.array_equal(got, eg), "calvin grant groups differ"
+
+
+def _c5_worker(rank, world, port, out):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def allreduce_max(buf):
+        t = torch.from_numpy(buf)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+
+    eng = d.Engine(0)
+    eng.comm_init_host(rank, world, allreduce_max)
+    b = d.gen_ycsb(n_txn=1 << 20, zipf_theta=0.99, seed=0xD3E7A002)
+    eng.tnc = 0
+    rc, tn, st = eng.occ_validate_epoch(d.shard_filter(b, rank, world), want_tn=True)
+    out[rank] = (np.asarray(rc).copy(), np.asarray(tn).copy(), st["n_shards"], eng.tnc)
+    eng.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_sharded_c5_full_size(world):
+    """BASELINE config C5 (1,048,576 YCSB txns, theta=0.99) key-sharded over
+    4 and 8 ranks (processes sharing the GPU, gloo exchange)."""
+    import torch.multiprocessing as mp
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_c5_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    b = d.gen_ycsb(n_txn=1 << 20, zipf_theta=0.99, seed=0xD3E7A002)
+    erc, etn, etnc = orc.occ(b)
+    for r in range(world):
+        rc, tn, nsh, tnc = out[r]
+        assert nsh == world and tnc == etnc
+        assert np.array_equal(rc, erc), f"rank {r}: rc differs from the oracle"
+        assert np.array_equal(tn.astype(np.uint64), etn), f"rank {r}: tn differs"
