@@ -29,6 +29,7 @@ GROUP_NONE = 0xFFFFFFFF
 DEVICE_PTRS = 0x1
 OCC_APPEND_HISTORY = 0x2
 MAAT_READ_AND_PREWRITE = 0x4
+ROW_NONE = 0xFFFFFFFFFFFFFFFF
 UNIQUE_ID_BYTES = 128
 # int (*)(void* user, uint8_t* host_buf, uint64_t n): in-place MAX all-reduce
 EXCHANGE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint8), C.c_uint64)
@@ -163,6 +164,7 @@ _P = C.c_void_p
 _SIGS = [
     ("dcc_init", C.c_int, [C.POINTER(C.c_void_p), C.c_int]),
     ("dcc_init_multi", C.c_int, [C.POINTER(C.c_void_p), C.c_int, _P]),
+    ("dcc_device_count", C.c_int, []),
     ("dcc_destroy", None, [_P]),
     ("dcc_strerror", C.c_char_p, [C.c_int]),
     ("dcc_last_error", C.c_char_p, [_P]),
@@ -197,6 +199,12 @@ _SIGS = [
     ("dcc_maat_rows_size", C.c_uint64, [_P]),
     ("dcc_maat_alg_bytes", C.c_uint64, [C.c_uint64, C.c_uint64]),
     ("dcc_calvin_order_epoch", C.c_int, [_P, C.POINTER(Batch), _P, _P, _P, C.POINTER(Stats)]),
+    ("dcc_calvin_dispatch", C.c_int, [_P, _P, _P, C.c_uint64, C.c_uint32, _P, C.c_uint64, _P, _P]),
+    ("dcc_index_insert", C.c_int, [_P, _P, _P, C.c_uint64]),
+    ("dcc_index_probe", C.c_int, [_P, _P, C.c_uint64, _P, C.c_uint32, _P]),
+    ("dcc_index_clear", C.c_int, [_P]),
+    ("dcc_index_size", C.c_uint64, [_P]),
+    ("dcc_index_last_ms", C.c_double, [_P]),
     ("dcc_calvin_order_epoch_held", C.c_int,
      [_P, C.POINTER(Batch), C.POINTER(CalvinHeld), _P, _P, _P, C.POINTER(Stats)]),
     ("dcc_ycsb_params_default", None, [C.POINTER(YcsbParams)]),

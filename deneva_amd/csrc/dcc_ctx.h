@@ -139,6 +139,11 @@ struct dcc_ctx {
   uint32_t mt_rows32 = 0;                        // upload source of the row counter
   DevBuf mt_misc, mt_slot, mt_sval, mt_slot2, mt_sval2, mt_owner, mt_sfl, mt_stx, mt_txn, mt_agg;
   DevBuf mt_sflB, mt_stxB, mt_k1, mt_tcnt;
+  // GPU index (index.hip): key table, newest insert ordinal per key, rows
+  DevBuf ix_keys, ix_ord, ix_rows, ix_cnt, wv_buf;
+  uint32_t ix_bits = 0;
+  uint64_t ix_nkeys = 0, ix_nrows = 0;
+  double ix_last_ms = 0;
   // commit counter tnc (occ.h:67)
   uint64_t tnc = 0;
 
@@ -178,6 +183,7 @@ struct dcc_ctx {
   int occ_snapshot(const dcc_batch* b, const dcc_occ_snapshot* s, uint8_t* out_rc, dcc_stats* st);
   // MaaT (maat.hip): row timestamp table + epoch workspaces
   int maat_rows_reserve(uint64_t want);
+  int index_reserve(uint64_t want);
   int maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, dcc_stats* st);
   int calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint32_t* out_group,
                    uint8_t* out_rc, uint32_t* out_wave, dcc_stats* st);

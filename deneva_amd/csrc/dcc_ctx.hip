@@ -74,6 +74,20 @@ static uint64_t next_pow2(uint64_t x) {
 }
 
 // ---------------------------------------------------------------- lifecycle
+extern "C" int dcc_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  int g = 0;
+  for (int i = 0; i < n; i++) {
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, i) == hipSuccess && strncmp(p.gcnArchName, "gfx950", 6) == 0) g++;
+  }
+  return g;
+}
+
 extern "C" int dcc_version(void) { return 100; }
 
 extern "C" const char* dcc_strerror(int code) {
@@ -212,7 +226,7 @@ std::vector<DevBuf*> dcc_ctx::all_bufs() {
                             &sw_xrec, &sw_mcnt, &sw_moff, &sw_mkeys, &sw_mat, &sw_kill,
                             &snap_top, &snap_aoff, &snap_aidx, &snap_cnt, &mt_rk, &mt_rlr, &mt_rlw,
                             &mt_misc, &mt_slot, &mt_sval, &mt_slot2, &mt_sval2, &mt_owner, &mt_sfl,
-                            &mt_stx, &mt_txn, &mt_agg, &mt_sflB, &mt_stxB, &mt_k1, &mt_tcnt,
+                            &mt_stx, &mt_txn, &mt_agg, &mt_sflB, &mt_stxB, &mt_k1, &mt_tcnt, &ix_keys, &ix_ord, &ix_rows, &ix_cnt, &wv_buf,
                             &h_K[0], &h_K[1], &h_V[0], &h_V[1], &h_scr, &h_bsum};
   for (auto& h : hs)
     for (DevBuf* b : {&h.fk, &h.ft, &h.skey, &h.stn, &h.hash}) v.push_back(b);

@@ -36,6 +36,7 @@ struct Cfg {
   double timer_ms = 5.0;
   uint64_t seed = 7;
   int device = 0;
+  int gpus = 0;                // > 0: one process drives this many shards (dcc_init_multi)
   int max_retries = 1000;
   bool calvin = false;
   bool live = false;           // live OptCC run on the workers, capture replayed on the GPU
@@ -45,7 +46,7 @@ struct Cfg {
 static void usage() {
   fprintf(stderr,
           "c1_driver [--threads N] [--txns N] [--theta T] [--req N] [--table N]\n"
-          "          [--epoch-max N] [--timer-ms T] [--seed S] [--device D]\n"
+          "          [--epoch-max N] [--timer-ms T] [--seed S] [--device D] [--gpus N]\n"
           "          [--capture DIR] [--calvin | --live]\n");
 }
 
@@ -67,6 +68,7 @@ static int parse(int argc, char** argv, Cfg& c) {
     else if (a == "--timer-ms") c.timer_ms = atof(v);
     else if (a == "--seed") c.seed = strtoull(v, nullptr, 0);
     else if (a == "--device") c.device = atoi(v);
+    else if (a == "--gpus") c.gpus = atoi(v);
     else if (a == "--capture") c.capture = v;
     else return 2;
   }
@@ -99,8 +101,20 @@ int main(int argc, char** argv) {
     return r == 1 ? 0 : 2;
   }
   dcc_ctx* ctx = nullptr;
-  if (int e = dcc_init(&ctx, c.device)) {
-    fprintf(stderr, "dcc_init: %s\n", dcc_strerror(e));
+  int e = 0;
+  if (c.gpus > 0) {
+    // the node's GPUs inside one context: devices 0..N-1 when present, else
+    // the shards share the GPUs there are (in-process exchange)
+    int ndev = dcc_device_count();
+    if (ndev < 1) ndev = 1;
+    std::vector<int> ids(c.gpus);
+    for (int g = 0; g < c.gpus; g++) ids[g] = g % ndev;
+    e = dcc_init_multi(&ctx, c.gpus, ids.data());
+  } else {
+    e = dcc_init(&ctx, c.device);
+  }
+  if (e) {
+    fprintf(stderr, "dcc_init: %s %s\n", dcc_strerror(e), ctx ? dcc_last_error(ctx) : "");
     return 1;
   }
   std::vector<std::vector<uint32_t>> off(c.threads);

@@ -312,6 +312,64 @@ class Engine:
         return (grp[:nnz] if want_group else None, rc[:n],
                 (wav[:n] if want_wave else None), st.as_dict())
 
+    def calvin_dispatch(self, wave, order=None):
+        """Wave dispatch lists (dcc_calvin_dispatch): returns (wave_off u32[W+1],
+        txn u32[n]) — txn[wave_off[w]:wave_off[w+1]] run in wave w."""
+        dev = hasattr(wave, "device") and str(wave.device).startswith("cuda")
+        n = int(wave.shape[0])
+        nw = C.c_uint32(0)
+        if dev:
+            import torch
+            txn = torch.empty(max(n, 1), dtype=torch.int32, device=wave.device)
+            _check(lib.dcc_calvin_dispatch(self._h, _ptr(wave), _ptr(order), n, _abi.DEVICE_PTRS,
+                                           None, 0, _ptr(txn), C.byref(nw)), self._h)
+            off = torch.empty(nw.value + 1, dtype=torch.int32, device=wave.device)
+            _check(lib.dcc_calvin_dispatch(self._h, _ptr(wave), _ptr(order), n, _abi.DEVICE_PTRS,
+                                           _ptr(off), nw.value + 1, _ptr(txn), C.byref(nw)),
+                   self._h)
+            return off, txn[:n]
+        wave = np.ascontiguousarray(wave, np.uint32)
+        order = None if order is None else np.ascontiguousarray(order, np.uint64)
+        txn = np.empty(max(n, 1), np.uint32)
+        _check(lib.dcc_calvin_dispatch(self._h, _ptr(wave), _ptr(order), n, 0, None, 0,
+                                       _ptr(txn), C.byref(nw)), self._h)
+        off = np.empty(nw.value + 1, np.uint32)
+        _check(lib.dcc_calvin_dispatch(self._h, _ptr(wave), _ptr(order), n, 0, _ptr(off),
+                                       off.size, _ptr(txn), C.byref(nw)), self._h)
+        return off, txn[:n]
+
+    # ----------------------------------------------------------- GPU index
+    def index_insert(self, keys, rows) -> None:
+        keys = np.ascontiguousarray(keys, np.uint64)
+        rows = np.ascontiguousarray(rows, np.uint64)
+        _check(lib.dcc_index_insert(self._h, _ptr(keys), _ptr(rows), keys.shape[0]), self._h)
+
+    def index_probe(self, keys):
+        """Rows of keys (DCC_ROW_NONE when absent) and the missing count."""
+        miss = C.c_uint64(0)
+        if hasattr(keys, "device") and str(keys.device).startswith("cuda"):
+            import torch
+            out = torch.empty(keys.shape[0], dtype=torch.int64, device=keys.device)
+            _check(lib.dcc_index_probe(self._h, _ptr(keys), keys.shape[0], _ptr(out),
+                                       _abi.DEVICE_PTRS, C.byref(miss)), self._h)
+            return out, miss.value
+        keys = np.ascontiguousarray(keys, np.uint64)
+        out = np.empty(keys.shape[0], np.uint64)
+        _check(lib.dcc_index_probe(self._h, _ptr(keys), keys.shape[0], _ptr(out), 0, C.byref(miss)),
+               self._h)
+        return out, miss.value
+
+    def index_clear(self) -> None:
+        _check(lib.dcc_index_clear(self._h), self._h)
+
+    @property
+    def index_size(self) -> int:
+        return int(lib.dcc_index_size(self._h))
+
+    @property
+    def index_last_ms(self) -> float:
+        return float(lib.dcc_index_last_ms(self._h))
+
     # ------------------------------------------------------------ multi-GPU
     def comm_init(self, rank: int, nranks: int, unique_id: bytes) -> None:
         buf = C.create_string_buffer(bytes(unique_id), _abi.UNIQUE_ID_BYTES)

@@ -138,6 +138,7 @@ void dcc_destroy(dcc_ctx* ctx);
 const char* dcc_strerror(int code);
 const char* dcc_last_error(const dcc_ctx* ctx); /* detail of the last failure */
 int dcc_version(void);                            /* 100*major + minor */
+int dcc_device_count(void);                       /* gfx950 devices visible (0 if none) */
 
 /* Run on an external HIP stream (opaque hipStream_t, e.g. torch's current
  * stream).  NULL restores the context's own stream. */
@@ -311,6 +312,35 @@ typedef struct dcc_calvin_held {
 int dcc_calvin_order_epoch_held(dcc_ctx* ctx, const dcc_batch* batch, const dcc_calvin_held* held,
                                 uint32_t* out_group, uint8_t* out_rc, uint32_t* out_wave,
                                 dcc_stats* out_stats);
+
+/* Wave dispatch: the wave levels of an epoch
+ * (out_wave of dcc_calvin_order_epoch) as the lists a dispatcher releases:
+ * out_txn[out_wave_off[w] .. out_wave_off[w+1]) = the txns of wave w in
+ * sequence order (order = the batch's sequencer key, NULL = index order;
+ * ties keep index order).  Wave w+1 starts once every txn of wave w has
+ * released its locks (TxnTable::restart_txn, txn_table.cpp:151-176, after the
+ * lock_release promotions of row_lock.cpp:317-357).  *out_n_waves = max
+ * wave + 1; out_wave_off needs *out_n_waves + 1 entries (off_cap; may be NULL
+ * to query the count).  Device pointers with DCC_DEVICE_PTRS in flags. */
+int dcc_calvin_dispatch(dcc_ctx* ctx, const uint32_t* wave, const uint64_t* order, uint64_t n,
+                        uint32_t flags, uint32_t* out_wave_off, uint64_t off_cap,
+                        uint32_t* out_txn, uint32_t* out_n_waves);
+
+/* ------------------------------------------------------------ GPU index */
+/* The key -> row lookups execution does through IndexHash (index_insert /
+ * index_read, storage/index_hash.cpp:58-137, 160-231) as one HBM table probed
+ * for a whole epoch's accesses at once.  A key inserted more than once reads
+ * as its newest insert (insert_item prepends, read_item takes the head); a
+ * missing key (the reference's M_ASSERT_V, index_hash.cpp:221) reads as
+ * DCC_ROW_NONE and is counted in *out_missing. */
+#define DCC_ROW_NONE 0xFFFFFFFFFFFFFFFFull
+int dcc_index_insert(dcc_ctx* ctx, const uint64_t* keys, const uint64_t* rows, uint64_t n);
+/* keys / out_rows: host arrays, or device arrays with DCC_DEVICE_PTRS in flags */
+int dcc_index_probe(dcc_ctx* ctx, const uint64_t* keys, uint64_t n, uint64_t* out_rows,
+                    uint32_t flags, uint64_t* out_missing);
+int dcc_index_clear(dcc_ctx* ctx);
+uint64_t dcc_index_size(const dcc_ctx* ctx);      /* distinct keys            */
+double dcc_index_last_ms(const dcc_ctx* ctx);     /* device ms of the last probe */
 
 /* ----------------------------------------------------- batch producers */
 /* Deterministic restatements of the reference workload generators

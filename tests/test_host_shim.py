@@ -36,12 +36,15 @@ def test_driver_built_and_usage():
 
 
 @pytest.mark.gpu
-def test_c1_occ_epochs_match_oracle(tmp_path):
+@pytest.mark.parametrize("gpus", [0, 3])
+def test_c1_occ_epochs_match_oracle(tmp_path, gpus):
+    # gpus=3: the OccEpoch shim over a single-process multi-GPU context
+    # (dcc_init_multi; on a one-GPU box the three shards share it)
     cap = tmp_path / "cap"
     cap.mkdir()
     out = run_driver("--threads", "4", "--txns", "1500", "--theta", "0.6", "--req", "10",
                      "--table", "65536", "--epoch-max", "256", "--timer-ms", "2",
-                     "--capture", str(cap))
+                     "--capture", str(cap), *(["--gpus", str(gpus)] if gpus else []))
     total = 4 * 1500
     assert out["failed"] == 0 and out["commits"] == total  # every txn commits eventually
     files = sorted(glob.glob(str(cap / "epoch_*.dccb")))
