@@ -59,6 +59,28 @@ def parse():
     return ap.parse_args()
 
 
+def stream_copy_gbps(dev, mib=2048, reps=10):
+    """Achievable HBM bandwidth on this GPU: a device-to-device copy of a
+    `mib` MiB buffer (read + write bytes / time), HIP events (BASELINE.md §4:
+    the measured stream-copy peak is reported next to the 8 TB/s spec)."""
+    import torch
+    n = mib << 20
+    a = torch.empty(n, dtype=torch.uint8, device=dev)
+    b = torch.empty(n, dtype=torch.uint8, device=dev)
+    a.fill_(1)
+    for _ in range(2):
+        b.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    del a, b
+    return 2.0 * n / (ms * 1e-3) / 1e9
+
+
 def _cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -372,6 +394,7 @@ def main():
     if filt["achieved"] is not None:
         filt["frac"] = filt["achieved"] / HBM_PEAK_GBS
 
+    copy_gbps = stream_copy_gbps(f"cuda:{local}") if rank == 0 else None
     s0 = stats[-1]
     ms_per_step = dt / args.steps * 1e3
     value = n_total * args.steps / dt
@@ -436,6 +459,8 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": epoch_gbs / HBM_PEAK_GBS,
+                "stream_copy_GBps": copy_gbps,
+                "frac_of_stream_copy": epoch_gbs / copy_gbps if copy_gbps else None,
                 "traffic": traffic,
                 "traffic_source": traffic_src,
                 "alg_bytes_per_launch": int(s0["alg_bytes"]),
