@@ -1,7 +1,7 @@
 // MaaT epoch validation on gfx950.
 //
 // Reference: Maat::validate / find_bound (concurrency_control/maat.cpp:29-191)
-// over the per-row soft locks of Row_maat (row_maat.cpp:38-316).  The epoch
+// over the per-row soft locks of Row_maat (row_maat.cpp:38-314).  The epoch
 // model (include/dcc.h, dcc_maat_validate_epoch): every txn accesses its rows
 // (index order), then in index order each txn validates and commits or aborts.
 // A txn's copied uncommitted sets then hold only earlier txns, decided and
@@ -23,9 +23,9 @@
 // predecessor commits at L, the rest wait for the next round.  The smallest
 // undecided txn always decides, so the rounds terminate.
 //
-// Row timestamps (timestamp_last_read / _write, row_maat.cpp:25-26) persist
+// Row timestamps (timestamp_last_read / _write, row_maat.h:38-39) persist
 // in an HBM open-addressing table across epochs; committed txns raise them
-// with atomicMax at the end of the epoch (row_maat.cpp:251-262, 280-284).
+// with atomicMax at the end of the epoch (row_maat.cpp:249-251, 276-278).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -188,8 +188,8 @@ __global__ __launch_bounds__(256) void k_mt_slots(const uint64_t* keys, uint64_t
 
 // One thread per txn: owners, and the txn's lower bound from the row
 // timestamps copied at access time: gwts over rows read or written, grts over
-// rows written (Row_maat::read / prewrite, row_maat.cpp:119-121, 159-165;
-// Maat::validate raises lower past them, maat.cpp:47-50, 70-73).
+// rows written (Row_maat::read / prewrite, row_maat.cpp:115-117, 150-156;
+// Maat::validate raises lower past them, maat.cpp:46-49, 69-72).
 struct BaseArgs {
   uint64_t n, nnz;
   const uint32_t* off;
@@ -514,7 +514,7 @@ __global__ __launch_bounds__(256) void k_mt_starts(uint64_t m, const uint32_t* s
 
 // ---------------------------------------------------------------- finish
 // RC bytes, commit timestamps, counts; committed txns raise their rows'
-// timestamps (Row_maat::commit, row_maat.cpp:251-262, 280-284)
+// timestamps (Row_maat::commit, row_maat.cpp:249-251, 276-278)
 struct FinArgs {
   uint64_t n, nnz;
   const uint32_t* off;

@@ -66,7 +66,7 @@ extern "C" {
 #define DCC_DEVICE_PTRS 0x1u      /* every batch AND output pointer is device memory */
 #define DCC_MAAT_READ_AND_PREWRITE 0x4u /* MaaT: every access both reads and prewrites its row
                                           (the TPC-C path, Row_maat::read_and_prewrite,
-                                          row_maat.cpp:40-41, 54-98)                     */
+                                          row_maat.cpp:40-41, 54-96)                     */
 #define DCC_OCC_APPEND_HISTORY 0x2u /* central_finish semantics: committed write sets
                                      of this epoch are appended to the history with
                                      tn = tnc+1, tnc+2, ... in index order
@@ -244,13 +244,13 @@ int dcc_occ_validate_snapshot(dcc_ctx* ctx, const dcc_batch* batch, const dcc_oc
  * worker_thread.cpp:503-508) and performs its Row_maat accesses in index
  * order (RD -> read, WR -> prewrite, XP/SCAN -> none; with
  * DCC_MAAT_READ_AND_PREWRITE every access does read_and_prewrite,
- * row_maat.cpp:38-171); then, in index order, each txn runs Maat::validate
+ * row_maat.cpp:38-164); then, in index order, each txn runs Maat::validate
  * and find_bound (maat.cpp:29-191; the node is the home node) and commits
  * (Row_maat::commit with the forward validation of the later txns still on
- * its rows, row_maat.cpp:227-316) or aborts (row_maat.cpp:205-225).
+ * its rows, row_maat.cpp:189-314) or aborts (row_maat.cpp:167-187).
  *   out_rc[i]        = DCC_RC_RCOK or DCC_RC_ABORT
  *   out_commit_ts[i] = commit_timestamp (the lower bound find_bound picks) or 0
- * Row timestamps (timestamp_last_read / _write, row_maat.cpp:25-26) persist in
+ * Row timestamps (timestamp_last_read / _write, row_maat.h:38-39) persist in
  * the context across epochs; rows never seen start at 0.
  * Stats: n_commit, n_abort, nnz_w, rounds (of the GPU fixed point),
  * device_ms, total_ms, alg_bytes (dcc_maat_alg_bytes). */

@@ -7,13 +7,13 @@
  * epoch is initialised in the time table (lower 0, upper UINT64_MAX, RUNNING;
  * worker_thread.cpp:503-508) and executes its accesses in index order
  * (Row_maat::access, row_maat.cpp:38-52); then, in index order, each txn
- * validates (Maat::validate, maat.cpp:29-175, then find_bound, maat.cpp:
- * 177-191, TxnManager::validate, txn.cpp:946-951) and is committed
+ * validates (Maat::validate, maat.cpp:29-174, then find_bound, maat.cpp:
+ * 176-190, TxnManager::validate, txn.cpp:946-951) and is committed
  * (TxnManager::commit, txn.cpp:427-432: cleanup in reverse access order,
- * txn.cpp:747-760, Row_maat::commit row_maat.cpp:227-316, time_table.release)
- * or aborted (txn.cpp:445-463, Row_maat::abort row_maat.cpp:205-225).
+ * txn.cpp:747-760, Row_maat::commit row_maat.cpp:189-314, time_table.release)
+ * or aborted (txn.cpp:445-463, Row_maat::abort row_maat.cpp:167-187).
  *
- * Row timestamps (timestamp_last_read / _write, row_maat.cpp:25-26) carry over
+ * Row timestamps (timestamp_last_read / _write, row_maat.h:38-39) carry over
  * between epochs: row_keys[n_rows] with row_lr / row_lw in/out (keys the batch
  * touches must all be listed; unlisted rows start at 0).
  *
@@ -129,13 +129,13 @@ static void tt_set_state(ttab* t, uint64_t i, int v) {
   if (t->present[i]) t->state[i] = (uint8_t)v;
 }
 
-/* Maat::validate, maat.cpp:29-175 (the semaphore serialises it) */
+/* Maat::validate, maat.cpp:29-174 (the semaphore serialises it) */
 static int maat_validate(ttab* tt, mtxn* tx, uint64_t id, idset* before, idset* after) {
   int rc = RC_RCOK;
   uint64_t lower = tt_lower(tt, id), upper = tt_upper(tt, id);
   before->n = after->n = 0;
-  if (lower <= tx->gwts) lower = tx->gwts + 1; /* :47-50 */
-  for (uint64_t q = 0; q < tx->uw.n; q++) {    /* :52-68 */
+  if (lower <= tx->gwts) lower = tx->gwts + 1; /* :46-49 */
+  for (uint64_t q = 0; q < tx->uw.n; q++) {    /* :51-67 */
     const uint64_t it = tx->uw.v[q];
     const uint64_t it_lower = tt_lower(tt, it);
     if (upper >= it_lower) {
@@ -144,8 +144,8 @@ static int maat_validate(ttab* tt, mtxn* tx, uint64_t id, idset* before, idset* 
       if (st == MAAT_RUNNING && is_insert(after, it)) return -1;
     }
   }
-  if (lower <= tx->grts) lower = tx->grts + 1; /* :70-73 */
-  for (uint64_t q = 0; q < tx->ur.n; q++) {    /* :75-91 */
+  if (lower <= tx->grts) lower = tx->grts + 1; /* :69-72 */
+  for (uint64_t q = 0; q < tx->ur.n; q++) {    /* :74-90 */
     const uint64_t it = tx->ur.v[q];
     const uint64_t it_upper = tt_upper(tt, it);
     if (lower <= it_upper) {
@@ -154,7 +154,7 @@ static int maat_validate(ttab* tt, mtxn* tx, uint64_t id, idset* before, idset* 
       if (st == MAAT_RUNNING && is_insert(before, it)) return -1;
     }
   }
-  for (uint64_t q = 0; q < tx->uwy.n; q++) { /* :93-111 */
+  for (uint64_t q = 0; q < tx->uwy.n; q++) { /* :92-111 */
     const uint64_t it = tx->uwy.v[q];
     const int st = tt_state(tt, it);
     const uint64_t it_upper = tt_upper(tt, it);
@@ -166,7 +166,7 @@ static int maat_validate(ttab* tt, mtxn* tx, uint64_t id, idset* before, idset* 
   if (lower >= upper) { /* :112-115 */
     tt_set_state(tt, id, MAAT_ABORTED);
     rc = RC_ABORT;
-  } else { /* :116-160 */
+  } else { /* :116-162 */
     tt_set_state(tt, id, MAAT_VALIDATED);
     for (uint64_t q = 0; q < before->n; q++) {
       const uint64_t it_upper = tt_upper(tt, before->v[q]);
@@ -187,12 +187,12 @@ static int maat_validate(ttab* tt, mtxn* tx, uint64_t id, idset* before, idset* 
       if (it_lower <= upper) tt_set_lower(tt, after->v[q], upper < U64MAX ? upper + 1 : upper);
     }
   }
-  tt_set_lower(tt, id, lower); /* :165-166 */
+  tt_set_lower(tt, id, lower); /* :163-164 */
   tt_set_upper(tt, id, upper);
   return rc;
 }
 
-/* Maat::find_bound, maat.cpp:177-191 */
+/* Maat::find_bound, maat.cpp:176-190 */
 static int maat_find_bound(ttab* tt, mtxn* tx, uint64_t id) {
   const uint64_t lower = tt_lower(tt, id), upper = tt_upper(tt, id);
   if (lower >= upper) {
@@ -204,7 +204,7 @@ static int maat_find_bound(ttab* tt, mtxn* tx, uint64_t id) {
   return RC_RCOK;
 }
 
-/* Row_maat::commit, row_maat.cpp:227-316 (both the TPCC and the RD/WR paths) */
+/* Row_maat::commit, row_maat.cpp:189-314 (both the TPCC and the RD/WR paths) */
 static void row_commit(ttab* tt, mrow* r, mtxn* tx, uint64_t id, int type, int rw_all) {
   const uint64_t cts = tx->cts;
   const int rd = rw_all || type == ACC_RD, wr = rw_all || type == ACC_WR;
@@ -241,7 +241,7 @@ static void row_commit(ttab* tt, mrow* r, mtxn* tx, uint64_t id, int type, int r
   }
 }
 
-/* Row_maat::abort, row_maat.cpp:205-225 */
+/* Row_maat::abort, row_maat.cpp:167-187 */
 static void row_abort(mrow* r, uint64_t id, int type, int rw_all) {
   if (rw_all || type == ACC_RD) is_erase(&r->ur, id);
   if (rw_all || type == ACC_WR) is_erase(&r->uw, id);
@@ -286,17 +286,17 @@ int oracle_maat_replay(uint64_t n, const uint32_t* off, const uint64_t* keys, co
       mrow* r = &R[*v];
       rix[x] = *v;
       const int type = acctype[x];
-      if (rw_all) { /* read_and_prewrite, :54-98 */
+      if (rw_all) { /* read_and_prewrite, :54-96 */
         if (is_union(&tx->uw, &r->uw) || is_union(&tx->uwy, &r->uw) || is_union(&tx->ur, &r->ur))
           ret = -1;
         if (tx->grts < r->lr) tx->grts = r->lr;
         if (tx->gwts < r->lw) tx->gwts = r->lw;
         if (is_insert(&r->ur, i) || is_insert(&r->uw, i)) ret = -1;
-      } else if (type == ACC_RD) { /* read, :101-130 */
+      } else if (type == ACC_RD) { /* read, :99-125 */
         if (is_union(&tx->uw, &r->uw)) ret = -1;
         if (tx->gwts < r->lw) tx->gwts = r->lw;
         if (is_insert(&r->ur, i)) ret = -1;
-      } else if (type == ACC_WR) { /* prewrite, :132-171 */
+      } else if (type == ACC_WR) { /* prewrite, :127-164 */
         if (is_union(&tx->ur, &r->ur) || is_union(&tx->uwy, &r->uw)) ret = -1;
         if (tx->grts < r->lr) tx->grts = r->lr;
         if (tx->gwts < r->lw) tx->gwts = r->lw;

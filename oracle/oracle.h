@@ -91,10 +91,10 @@ int oracle_calvin_formula(uint64_t n, const uint32_t* off, const uint64_t* keys,
                           uint8_t* out_rc, uint32_t* out_wave);
 
 /* MaaT epoch validation (maat_ref.c): every txn of the epoch executes its
- * Row_maat accesses in index order (row_maat.cpp:38-171), then, in index
+ * Row_maat accesses in index order (row_maat.cpp:38-164), then, in index
  * order, Maat::validate + find_bound (maat.cpp:29-191) and commit
- * (Row_maat::commit, row_maat.cpp:227-316, cleanup in reverse access order)
- * or abort (row_maat.cpp:205-225), with time_table.release after each.
+ * (Row_maat::commit, row_maat.cpp:189-314, cleanup in reverse access order)
+ * or abort (row_maat.cpp:167-187), with time_table.release after each.
  * rw_all != 0: the TPC-C path (read_and_prewrite for every access).
  * row_keys/row_lr/row_lw [n_rows]: timestamp_last_read / _write per row, in
  * (before the epoch; unlisted rows start at 0) and out (after it).

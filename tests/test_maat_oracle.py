@@ -1,5 +1,5 @@
 """MaaT oracle (oracle/maat_ref.c): the literal replay of Maat::validate /
-find_bound / Row_maat (maat.cpp:29-191, row_maat.cpp:38-316) in the epoch
+find_bound / Row_maat (maat.cpp:29-191, row_maat.cpp:38-314) in the epoch
 model and the running-bounds formula agree, and hand-worked cases traced to
 those lines hold."""
 import numpy as np
@@ -22,10 +22,10 @@ def both(b, rows=None, rw_all=False):
 
 
 def test_kat_reader_then_writer():
-    # T0 reads k (commits at 1: lower 0 <= gwts 0 -> 1, maat.cpp:47-50); its
+    # T0 reads k (commits at 1: lower 0 <= gwts 0 -> 1, maat.cpp:46-49); its
     # commit pushes the later writer T1 after it: lower(T1) = 2
-    # (row_maat.cpp:274-286); T1 commits at 2; the row's last read / write
-    # timestamps become 1 / 2 (row_maat.cpp:253-256, 281-284).
+    # (row_maat.cpp:254-266); T1 commits at 2; the row's last read / write
+    # timestamps become 1 / 2 (row_maat.cpp:249-251, 276-278).
     b = make_batch([[(5, RD)], [(5, WR)]])
     rc, cts, (rk, lr, lw) = both(b)
     assert list(rc) == [0, 0] and list(cts) == [1, 2]
@@ -34,7 +34,7 @@ def test_kat_reader_then_writer():
 
 def test_kat_writer_then_reader():
     # T0 writes k at 1; its commit caps the later reader T1 at lower(T0) - 1 =
-    # 0 (row_maat.cpp:302-312) while T1's lower is >= 1: T1 aborts
+    # 0 (row_maat.cpp:295-305) while T1's lower is >= 1: T1 aborts
     # (maat.cpp:112-115).
     b = make_batch([[(5, WR)], [(5, RD)]])
     rc, cts, _ = both(b)
@@ -43,7 +43,7 @@ def test_kat_writer_then_reader():
 
 def test_kat_row_timestamps():
     # a row last written at 7 (an earlier epoch): the reader's lower becomes 8
-    # (greatest_write_timestamp, row_maat.cpp:119-121; maat.cpp:47-50)
+    # (greatest_write_timestamp, row_maat.cpp:115-117; maat.cpp:46-49)
     b = make_batch([[(5, RD)], [(6, WR)]])
     rc, cts, (rk, lr, lw) = both(b, rows=(np.array([5, 6], np.uint64), np.array([0, 3], np.uint64),
                                           np.array([7, 0], np.uint64)))
@@ -52,7 +52,7 @@ def test_kat_row_timestamps():
 
 
 def test_kat_xp_scan_untracked():
-    # XP / SCAN accesses do nothing in Row_maat::access (row_maat.cpp:46-49)
+    # XP / SCAN accesses do nothing in Row_maat::access (row_maat.cpp:42-46)
     b = make_batch([[(5, WR)], [(5, XP)], [(5, SCAN)]])
     rc, cts, _ = both(b)
     assert list(rc) == [0, 0, 0]
