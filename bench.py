@@ -236,8 +236,64 @@ def maat_config(eng, dev, timed, orc, tag="MAAT_C2"):
             "parity_vs_oracle": bool(np.array_equal(rc.cpu().numpy(), erc))}
 
 
+def history_config(eng, dev, timed, orc, tag="HIST", n=1 << 18, epochs=8):
+    """Multi-epoch OCC with the device history: each step runs
+    `epochs` consecutive epochs from an empty history (tnc 0), every one with
+    TS_CAS windows (start_tn, finish_tn] reaching about one epoch back, its
+    committed writes appended on the device (DCC_OCC_APPEND_HISTORY, device
+    pointers) and the history trimmed below the next windows.  The batches and
+    their windows are built once, epoch by epoch, from the oracle's commit
+    counter; the last step's decisions are checked against the oracle chain."""
+    import torch
+    import deneva_amd as d
+    rng = np.random.default_rng(0xD3E7A00B)
+    spread = n
+    hk, ht = np.zeros(0, np.uint64), np.zeros(0, np.uint64)
+    tnc, batches, floors, expect = 0, [], [], []
+    for e in range(epochs):
+        b = d.gen_ycsb(n_txn=n, zipf_theta=0.9, seed=0xD3E7A100 + e)
+        b.start_tn = (tnc - rng.integers(0, spread, size=n)).clip(0).astype(np.uint64)
+        b.finish_tn = (b.start_tn + rng.integers(0, 2 * spread, size=n)).astype(np.uint64)
+        erc, etn, etnc = orc.occ(b, hist_keys=hk, hist_tn=ht, tnc=tnc)
+        off = np.asarray(b.offsets, np.int64)
+        owner = np.repeat(np.arange(n), np.diff(off))
+        sel = (np.asarray(b.acctype) == d.WR) & (etn[owner] != 0)
+        hk = np.concatenate([hk, np.asarray(b.keys, np.uint64)[sel]])
+        ht = np.concatenate([ht, etn[owner[sel]]])
+        floors.append(max(tnc - spread, 0))
+        batches.append(b.to_torch(dev))
+        expect.append(erc)
+        tnc = etnc
+    rcs = [torch.empty(n, dtype=torch.uint8, device=dev) for _ in range(epochs)]
+    acc = {}
+
+    def step():
+        eng.history_clear()
+        eng.tnc = 0
+        dev_ms, alg = 0.0, 0
+        for e in range(epochs):
+            if floors[e]:
+                eng.history_trim(floors[e])
+            st = eng.occ_validate_epoch(batches[e], append_history=True, out_rc=rcs[e])[2]
+            dev_ms += st["device_ms"]
+            alg += st["alg_bytes"]
+        acc["hist"] = eng.history_size
+        return {"device_ms": dev_ms, "alg_bytes": alg}
+    dt, st = timed(step)
+    par = all(np.array_equal(rcs[e].cpu().numpy(), expect[e]) for e in range(epochs))
+    par = par and eng.tnc == tnc
+    return {"workload": f"{epochs} consecutive OCC epochs of {n} YCSB txns x 16 keys (theta=0.9), "
+                        f"TS_CAS windows ~1 epoch deep, device history append + trim",
+            "txns_per_s": epochs * n / dt, "ms_per_epoch": dt * 1e3 / epochs,
+            "device_ms_per_epoch": st["device_ms"] / epochs,
+            "history_pairs_at_end": int(acc["hist"]), "history_pairs_untrimmed": int(hk.size),
+            "alg_GBps": st["alg_bytes"] / (st["device_ms"] * 1e-3) / 1e9,
+            "parity_vs_oracle": bool(par)}
+
+
 CONFIGS = {"C2": occ_config, "C3": occ_config, "C5": occ_config, "C4": calvin_config,
-           "C6": None, "MAAT_C2": maat_config, "MAAT_1M": maat_config}
+           "C6": None, "HIST": history_config, "MAAT_C2": maat_config,
+           "MAAT_1M": maat_config}
 
 
 def secondary_configs(eng, local, steps=10, warmup=3, only=None):

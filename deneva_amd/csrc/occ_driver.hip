@@ -804,8 +804,10 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
         const uint64_t* f = dv.data() + 4096 + l * 256 * 8;
         double fi = 0, fl = 0, fb = 0, fw = 0, ft = 0, nc = 0;
         int nw = 0, nwc = 0;
-        for (int w = 0; w < 256 && f[w * 8]; w++, nw++) {
+        for (int w = 0; w < 256 && f[w * 8]; w++) {
           const uint64_t* x = f + w * 8;
+          if (!x[5]) continue;  // returned early (nothing to filter)
+          nw++;
           fi += x[1] - x[0];
           ft += x[5] - x[0];
           nc += x[6];
@@ -829,9 +831,10 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
                     (pp[9] - pp[8]) * 0.01, (pp[10] - pp[9]) * 0.01, (pp[11] - pp[10]) * 0.01);
         }
         if (nw)
-          fprintf(stderr, "  filter L%d: %d WGs, chunks/WG %.2f, init %.0f, chunk local %.0f "
-                          "lookback %.0f writes %.0f, WG total %.0f cycles\n", l, nw, nc / nw,
-                  fi / nw, nwc ? fl / nwc : 0, nwc ? fb / nwc : 0, nwc ? fw / nwc : 0, ft / nw);
+          fprintf(stderr, "  filter L%d (us, wave 0 of WGs < 256): %d WGs, tiles/wave %.2f, setup %.2f, "
+                          "first tile loads %.2f exact %.2f writes %.2f, total %.2f\n", l, nw, nc / nw,
+                  0.01 * fi / nw, nwc ? 0.01 * fl / nwc : 0, nwc ? 0.01 * fb / nwc : 0,
+                  nwc ? 0.01 * fw / nwc : 0, 0.01 * ft / nw);
       }
     }
     info.prefix = hc[0].pos;

@@ -1015,6 +1015,10 @@ __global__ __launch_bounds__(X ? F_XB : SW_CHUNK) void k_sw_filter(SwFilterArgs 
   const uint32_t pos = a.lv->pos;
   const uint32_t ccount = a.lv->ccount;
   if (X ? ccount > F_XCAP : (a.exact_launched && ccount <= F_XCAP)) return;
+  // DCC_SW_DEBUG: wave 0 of workgroups < 256 stamps start / setup / loads /
+  // exact checks / writes / end and counts its tiles
+  uint64_t* dbg = (a.dbg && blockIdx.x < 256 && j == 0) ? a.dbg + 8 * blockIdx.x : nullptr;
+  if (dbg) dbg[0] = __builtin_amdgcn_s_memrealtime();
   // the serial pass decided the whole list: no next level (the epoch's first
   // level table is filled by the epoch's setup); sharded ranks still serve
   // the merged serial range of the next level
@@ -1055,6 +1059,7 @@ __global__ __launch_bounds__(X ? F_XB : SW_CHUNK) void k_sw_filter(SwFilterArgs 
     }
     __syncthreads();
   }
+  if (dbg) dbg[1] = __builtin_amdgcn_s_memrealtime();
   uint64_t* hit = s_hit[wv];
   uint64_t* wr = s_wr[wv];
   uint64_t* stash = s_stash[wv];
@@ -1143,6 +1148,7 @@ __global__ __launch_bounds__(X ? F_XB : SW_CHUNK) void k_sw_filter(SwFilterArgs 
     }
     if (!pref && wt + FW < t_hi) prefetch(wt + FW);  // a tile without accesses
     if (ballot64(bad_key) && lane == 0) atomicOr(a.err, ERR_KEY);
+    if (dbg && wt == t_lo) dbg[2] = __builtin_amdgcn_s_memrealtime();
     // per txn (the wave's own LDS rows: no barrier needed)
     const uint32_t rlo = s - A0, rlen = e - s;
     const bool ok = valid && (rlen == 0 || (uint64_t)rlo + rlen <= span);
@@ -1171,6 +1177,8 @@ __global__ __launch_bounds__(X ? F_XB : SW_CHUNK) void k_sw_filter(SwFilterArgs 
         }
       }
     }
+    if (dbg && wt == t_lo) dbg[3] = __builtin_amdgcn_s_memrealtime();
+    if (dbg) dbg[6]++;
     if (valid && a.write_hasw) a.hasw[tid] = ok && rlen && range_any(wr, rlo, rlen) ? 1 : 0;
     if (a.kill_out) {  // key-sharded: this shard's kill bit only (k_sw_apply decides)
       if (valid) a.kill_out[p] = killed ? 1 : 0;
@@ -1187,6 +1195,10 @@ __global__ __launch_bounds__(X ? F_XB : SW_CHUNK) void k_sw_filter(SwFilterArgs 
       a.sflag[wt] = sm;
       a.tcount[wt] = cnt;
     }
+    if (dbg && wt == t_lo) {
+      __builtin_amdgcn_s_waitcnt(0);
+      dbg[4] = __builtin_amdgcn_s_memrealtime();
+    }
   }
   if (a.kill_out) return;
   __shared__ unsigned long long s_bs[FW];
@@ -1196,6 +1208,10 @@ __global__ __launch_bounds__(X ? F_XB : SW_CHUNK) void k_sw_filter(SwFilterArgs 
     uint64_t t = 0;
     for (uint32_t w = 0; w < FW; w++) t += s_bs[w];
     a.bsum[blockIdx.x] = t;
+  }
+  if (dbg) {
+    __builtin_amdgcn_s_waitcnt(0);
+    dbg[5] = __builtin_amdgcn_s_memrealtime();
   }
 }
 
