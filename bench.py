@@ -444,7 +444,7 @@ def main():
     # the one kernel that streams the whole epoch (every offset, key and access
     # type): the level-0 committed-key filter; reported as a
     # sub-field, the headline roofline is the whole epoch
-    filt = {"kernel": "k_sw_filter<true> (level-0 committed-key filter)",
+    filt = {"kernel": "k_sw_filter (level 0: the committed-key filter over the whole epoch)",
             "alg_bytes_per_launch": int(ph_bytes[1]), "avg_launch_ms": float(ph_ms[1]),
             "achieved": ph_bytes[1] / (ph_ms[1] * 1e-3) / 1e9 if ph_ms[1] > 0 else None}
     if filt["achieved"] is not None:

@@ -289,16 +289,27 @@ static uint32_t sw_pmax(int level) {
   return level >= 6 ? SW_PMAX_TOP : (1024u << level);
 }
 static size_t sw_ctl_bytes() { return (SW_MAX_LEVEL + 2) * sizeof(SwLevel) + 64; }
-// key-table slots of a level: twice the accesses of p_max 16-access txns
-static uint32_t sw_gbits(int level) {
-  // key-table slots of a level: four times the accesses of p_max 16-access
-  // txns, so the table stays <= 25% full and a home bucket pair almost never
-  // overflows (the pre-pass resolves an insert in one read + one CAS)
+// the access budget of a level's serial range: a quarter of the smallest
+// table with four slots per access of p_max 16-access txns
+static uint32_t sw_budget_bits(int level) {
   uint32_t b = 12;
   while (b < SW_GBITS_MAX && (1ull << b) < 4ull * sw_pmax(level) * 16) b++;
   return b;
 }
-static uint32_t sw_budget(int level) { return 1u << (sw_gbits(level) - 2); }
+static uint32_t sw_budget(int level) { return 1u << (sw_budget_bits(level) - 2); }
+// key-table slots of a level: sparse (2^18 at level 0, 2^19 after; the
+// DCC_SW_GBITS override for experiments), so a pre-pass workgroup's ~500
+// first inserts almost never meet another key at their first slot -- each
+// lost slot is one more dependent round trip for the whole workgroup
+static uint32_t sw_gbits(int level) {
+  static const int ov = [] {
+    const char* c = getenv("DCC_SW_GBITS");
+    return c ? atoi(c) : 0;
+  }();
+  uint32_t b = ov > 0 ? (uint32_t)ov : (level == 0 ? 18u : 19u);
+  b = std::max(b, sw_budget_bits(level));
+  return std::min<uint32_t>(b, SW_GBITS_MAX);
+}
 
 int dcc_ctx::sweep_reserve(const DevBatch& d) {
   const uint64_t tiles = SW_PMAX_TOP / SW_T;
@@ -426,16 +437,12 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1, const SwShard* shl
     fa.la_clear = la;
     fa.err = err;
     fa.dbg = (sw_debug && l < 4) ? (uint64_t*)sw_dbg.p + 4096 + (size_t)l * 256 * 8 : nullptr;
-    fa.exact_launched = top ? 1 : 0;
     fa.kill_out = shl ? shl->kill : nullptr;
     fa.kill_in = shl ? shl->kill : nullptr;
-    if (top) {
-      // phase 1 of the profile is exactly the level-0 streaming filter
-      if (profiling) CK(hipEventRecord(pev[1], stream));
-      launch_sw_filter_x(fa, fgrid, stream);
-      if (profiling) CK(hipEventRecord(pev[2], stream));
-    }
-    launch_sw_filter_b(fa, fgrid, stream);
+    // phase 1 of the profile is exactly the level-0 streaming filter
+    if (top && profiling) CK(hipEventRecord(pev[1], stream));
+    launch_sw_filter(fa, fgrid, stream);
+    if (top && profiling) CK(hipEventRecord(pev[2], stream));
     if (shl) {
       // a kill on any shard wins; then every rank applies the same decision
       CR(comm_allreduce_max_u8(shl->kill, shl->m));
@@ -596,13 +603,9 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   // partials are read back with the epoch's one synchronisation.
   uint32_t maxlen = 0;
   uint64_t nnz_w = 0;
-  if (sweep) {
-    if (!replay)
-      launch_prep(d.off, d.n, d.acctype, d.nnz, 0, (PrepPart*)((char*)part.p + SW_PREP_OFF),
-                  stream);
-  } else {
-    CR(device_prep(d, maxlen, nnz_w));
-  }
+  // the sweep's prep pass shares the fill launch below (its partials go
+  // straight to pinned memory; only the host reads them)
+  if (!sweep) CR(device_prep(d, maxlen, nnz_w));
   if (!replay) {
     // one launch: error word 0, the constant-one word 1, words 2..15, the
     // async pass count, the state bytes, and for the sweep its control block
@@ -619,7 +622,11 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
       fa.job[fa.n++] = FillJob{(uint32_t*)sw_fw.p, 1ull << sw_gbits(0), 0xFFFFFFFFu};
       fa.job[fa.n++] = FillJob{(uint32_t*)sw_fw.p + (1u << SW_GBITS_MAX), 1ull << sw_gbits(0), 0u};
     }
-    launch_fill(fa, stream);
+    if (sweep)
+      launch_fill_prep(fa, d.off, d.n, d.acctype, d.nnz,
+                       (PrepPart*)((char*)hpart_dev + SW_PREP_OFF), stream);
+    else
+      launch_fill(fa, stream);
   }
 
   // ---- history window pre-pass (occ.cpp:160-180)
@@ -670,9 +677,19 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
       CK(hipStreamSynchronize(stream));
       return DCC_OK;
     }
+    // everything the host reads back goes to pinned memory from k_final
+    // itself: its partials directly, the error words and the sweep's control
+    // block copied by its last workgroup (prep wrote its partials directly)
+    GatherArgs ga{};
+    auto job = [&](void* hdst_dev, const void* src, size_t bytes) {
+      ga.job[ga.n++] = CopyJob{(const uint32_t*)src, (uint32_t*)hdst_dev, (uint32_t)(bytes / 4)};
+    };
+    job(hmisc_dev, misc.p, 64);
+    job((char*)hmisc_dev + MISC_BARS, (char*)misc.p + MISC_BARS, CTR_RING * 16);
+    if (sweep) job((char*)hmisc_dev + SW_HCTL, sw_ctl.p, sw_ctl_bytes());
     FinalArgs fa{d.n, (const uint8_t*)state.p, (const uint8_t*)hasw.p, rc_dev, cf,
-                 (FinalPart*)part.p};
-    launch_final(fa, stream);
+                 (FinalPart*)hpart_dev};
+    launch_final(fa, ga, stream);
     if (want_tn) launch_commit_tn(cf, d.n, (uint64_t*)bsum.p, tnc, tn_dev, stream);
     CK(hipGetLastError());
     if (!capturing) CK(hipEventRecord(ev1, stream));
@@ -680,21 +697,6 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
       if (out_rc) CK(hipMemcpyAsync(out_rc, rc.p, d.n, hipMemcpyDeviceToHost, stream));
       if (out_tn) CK(hipMemcpyAsync(out_tn, tn.p, d.n * 8, hipMemcpyDeviceToHost, stream));
     }
-    // everything the host reads back, in one launch into pinned memory
-    GatherArgs ga{};
-    auto job = [&](void* hdst_dev, const void* src, size_t bytes) {
-      ga.job[ga.n++] = CopyJob{(const uint32_t*)src, (uint32_t*)hdst_dev, (uint32_t)(bytes / 4)};
-    };
-    job(hmisc_dev, misc.p, 64);
-    job((char*)hmisc_dev + MISC_BARS, (char*)misc.p + MISC_BARS, CTR_RING * 16);
-    if (sweep) {
-      job((char*)hmisc_dev + SW_HCTL, sw_ctl.p, sw_ctl_bytes());
-      job((char*)hpart_dev + SW_PREP_OFF, (char*)part.p + SW_PREP_OFF,
-          PREP_BLOCKS * sizeof(PrepPart));
-    }
-    job(hpart_dev, part.p, FINAL_BLOCKS * sizeof(FinalPart));
-    launch_gather(ga, stream);
-    CK(hipGetLastError());
     if (capturing) {
       capturing = false;
       hipGraph_t g = nullptr;
@@ -826,6 +828,11 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
                             "map+gid %.2f deps+out %.2f tail %.2f\n", l,
                     (pp[1] - pp[0]) * 0.01, (pp[2] - pp[1]) * 0.01, (pp[3] - pp[2]) * 0.01,
                     (pp[4] - pp[3]) * 0.01, (pp[5] - pp[4]) * 0.01, (pp[6] - pp[5]) * 0.01);
+          if (pp[12] && pp[14])
+            fprintf(stderr, "  pre L%d map+gid (us): LDS map %.2f first CAS %.2f second CAS %.2f rest "
+                            "%.2f; first inserts %llu, lost first slots %llu\n", l, (pp[12] - pp[3]) * 0.01,
+                    (pp[13] - pp[12]) * 0.01, (pp[14] - pp[13]) * 0.01, (pp[4] - pp[14]) * 0.01,
+                    (unsigned long long)pp[16], (unsigned long long)pp[15]);
           if (pp[11])
             fprintf(stderr, "  rows L%d (us): offsets %.2f flags %.2f lists %.2f\n", l,
                     (pp[9] - pp[8]) * 0.01, (pp[10] - pp[9]) * 0.01, (pp[11] - pp[10]) * 0.01);

@@ -121,7 +121,7 @@ struct FinalArgs {
   const uint8_t* hasw;
   uint8_t* rc;
   uint32_t* cflag;
-  FinalPart* part;  // [FINAL_BLOCKS]
+  FinalPart* part;  // [FINAL_BLOCKS] (pinned host memory: read back directly)
 };
 
 // sub-list decisions back to the epoch's state bytes (round-solver hand-off)
@@ -268,7 +268,6 @@ struct SwFilterArgs {
   const uint32_t* m_dev;
   uint32_t m_host;
   int cand_state;         // identity list: only UNDECIDED txns are candidates
-  int exact_launched;     // the exact-set filter instance runs too (small C is its case)
   int write_hasw;
   uint32_t level;
   const uint64_t* gtab;   // the level's key table / committed ids / Bloom filter /
@@ -312,8 +311,7 @@ void launch_sw_pre(const SwPreArgs& a, unsigned grid, hipStream_t st);
 void launch_sw_seq(const SwSeqArgs& a, hipStream_t st);
 void launch_sw_rows(const SwPreArgs& a, unsigned grid, hipStream_t st);
 void launch_sw_cout(const SwCoutArgs& a, unsigned grid, hipStream_t st);
-void launch_sw_filter_x(const SwFilterArgs& a, unsigned grid, hipStream_t st);
-void launch_sw_filter_b(const SwFilterArgs& a, unsigned grid, hipStream_t st);
+void launch_sw_filter(const SwFilterArgs& a, unsigned grid, hipStream_t st);
 void launch_sw_scan(const SwFilterArgs& a, hipStream_t st);
 void launch_sw_compact(const SwFilterArgs& a, unsigned grid, hipStream_t st);
 void launch_sw_apply(const SwFilterArgs& a, unsigned grid, hipStream_t st);
@@ -338,6 +336,8 @@ struct FillArgs {
   uint32_t n;
 };
 void launch_fill(const FillArgs& a, hipStream_t st);
+void launch_fill_prep(const FillArgs& a, const uint32_t* off, uint64_t n, const uint8_t* at,
+                      uint64_t nnz, PrepPart* part, hipStream_t st);
 // Several small device -> pinned-host copies in one launch (word granular):
 // the control words, counters and partials the host reads after an epoch.
 struct CopyJob {
@@ -360,7 +360,8 @@ void launch_round(const RoundArgs& a, bool from_keys, uint64_t m_bound, unsigned
                   hipStream_t st);
 void launch_retag(Slot* tab, uint64_t cap, hipStream_t st);
 void launch_pub(const PubArgs& a, uint64_t m_bound, unsigned max_grid, hipStream_t st);
-void launch_final(const FinalArgs& a, hipStream_t st);
+// k_final also performs the read-back copies of g (pinned host targets)
+void launch_final(const FinalArgs& a, const GatherArgs& g, hipStream_t st);
 // sharded rounds: apply the all-reduced status (0 commit, 1 stay, >=2 abort),
 // clear it for the next round, add the undecided count to *und.
 void launch_decide(uint8_t* state, uint8_t* gst, uint64_t n, uint8_t abort_byte, uint32_t* und,

@@ -57,13 +57,14 @@ __device__ inline uint32_t block_max_u32(uint32_t v, uint32_t* sh) {
   return t;
 }
 
-__global__ __launch_bounds__(256) void k_prep(const uint32_t* __restrict__ off, uint64_t n,
-                                              const uint8_t* __restrict__ at, uint64_t nnz,
-                                              uint64_t p, PrepPart* __restrict__ part) {
+// workgroup `blk` of `nblk` (every thread of the workgroup calls it)
+__device__ void prep_body(const uint32_t* __restrict__ off, uint64_t n, const uint8_t* __restrict__ at,
+                          uint64_t nnz, uint64_t p, PrepPart* __restrict__ part, uint32_t blk,
+                          uint32_t nblk) {
   __shared__ uint32_t sh[4];
   uint32_t len = 0, bad = 0, nw = 0, nwp = 0;
-  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t tid = (uint64_t)blk * blockDim.x + threadIdx.x;
+  const uint64_t stride = (uint64_t)nblk * blockDim.x;
   // writes inside the peel prefix [0, off[p]) size its key table
   const uint64_t lim = (p && p <= n) ? off[p] : 0;
   for (uint64_t t = tid; t < n; t += stride) {
@@ -98,7 +99,12 @@ __global__ __launch_bounds__(256) void k_prep(const uint32_t* __restrict__ off, 
   const uint32_t tb = block_max_u32(bad, sh);  // error bits are 0/1 flags: max == or here
   const uint32_t tw = block_sum_u32(nw, sh);
   const uint32_t tp = block_sum_u32(nwp, sh);
-  if (threadIdx.x == 0) part[blockIdx.x] = PrepPart{tb, tl, tw, tp};
+  if (threadIdx.x == 0) part[blk] = PrepPart{tb, tl, tw, tp};
+}
+__global__ __launch_bounds__(256) void k_prep(const uint32_t* __restrict__ off, uint64_t n,
+                                              const uint8_t* __restrict__ at, uint64_t nnz,
+                                              uint64_t p, PrepPart* __restrict__ part) {
+  prep_body(off, n, at, nnz, p, part, blockIdx.x, gridDim.x);
 }
 
 // --------------------------------------------------------------------------
@@ -752,9 +758,17 @@ __global__ __launch_bounds__(256) void k_decide(uint8_t* __restrict__ state,
 
 // --------------------------------------------------------------------------
 // k_final: RC bytes, commit flags for the tn scan, per-block count partials.
-__global__ __launch_bounds__(256) void k_final(FinalArgs a) {
+__global__ __launch_bounds__(256) void k_final(FinalArgs a, GatherArgs g) {
   __shared__ uint32_t sh[4];
   uint32_t c = 0, ab = 0, ro = 0, und = 0, cw = 0;
+  // what the host reads back besides the partials (error words, the sweep's
+  // control block), copied by the last workgroup into pinned host memory: no
+  // separate gather launch
+  if (blockIdx.x == gridDim.x - 1)
+    for (uint32_t q = 0; q < g.n; q++) {
+      const CopyJob& cj = g.job[q];
+      for (uint32_t i = threadIdx.x; i < cj.words; i += blockDim.x) cj.dst[i] = cj.src[i];
+    }
   for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < a.n;
        t += (uint64_t)gridDim.x * blockDim.x) {
     const uint8_t st = a.state[t];
@@ -879,6 +893,26 @@ void launch_fill(const FillArgs& a, hipStream_t st) {
   const unsigned grid = (unsigned)std::min<uint64_t>((mx + 255) / 256, 2048);
   k_fill<<<grid, 256, 0, st>>>(a);
 }
+// the epoch's fills and k_prep's pass in one launch: workgroups < PREP_BLOCKS
+// also run prep (partials straight to the host-visible `part`)
+__global__ __launch_bounds__(256) void k_fill_prep(FillArgs a, const uint32_t* __restrict__ off,
+                                                   uint64_t n, const uint8_t* __restrict__ at,
+                                                   uint64_t nnz, PrepPart* __restrict__ part) {
+  const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x, stride = (uint64_t)gridDim.x * 256;
+  for (uint32_t q = 0; q < a.n; q++) {
+    const FillJob& f = a.job[q];
+    for (uint64_t i = t; i < f.words; i += stride) f.p[i] = f.value;
+  }
+  if (blockIdx.x < PREP_BLOCKS) prep_body(off, n, at, nnz, 0, part, blockIdx.x, PREP_BLOCKS);
+}
+void launch_fill_prep(const FillArgs& a, const uint32_t* off, uint64_t n, const uint8_t* at,
+                      uint64_t nnz, PrepPart* part, hipStream_t st) {
+  uint64_t mx = 1;
+  for (uint32_t q = 0; q < a.n; q++) mx = a.job[q].words > mx ? a.job[q].words : mx;
+  const unsigned grid = (unsigned)std::max<uint64_t>(std::min<uint64_t>((mx + 255) / 256, 2048),
+                                                     PREP_BLOCKS);
+  k_fill_prep<<<grid, 256, 0, st>>>(a, off, n, at, nnz, part);
+}
 
 __global__ __launch_bounds__(256) void k_gather(GatherArgs a) {
   for (uint32_t q = 0; q < a.n; q++) {
@@ -889,8 +923,8 @@ __global__ __launch_bounds__(256) void k_gather(GatherArgs a) {
 }
 void launch_gather(const GatherArgs& a, hipStream_t st) { k_gather<<<16, 256, 0, st>>>(a); }
 
-void launch_final(const FinalArgs& a, hipStream_t st) {
-  k_final<<<FINAL_BLOCKS, 256, 0, st>>>(a);
+void launch_final(const FinalArgs& a, const GatherArgs& g, hipStream_t st) {
+  k_final<<<FINAL_BLOCKS, 256, 0, st>>>(a, g);
 }
 void launch_commit_tn(const uint32_t* cflag, uint64_t n, uint64_t* bsum, uint64_t tnc,
                       uint64_t* tn, hipStream_t st) {

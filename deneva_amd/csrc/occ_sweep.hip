@@ -52,53 +52,33 @@ __device__ inline uint32_t sw_hash(uint64_t key, uint32_t log2s) {
   return h >> (32 - log2s);
 }
 
-// Level key table in global memory: 4-slot buckets (32 B) filled in slot
-// order, so one read answers most lookups; a key's id is its slot.  Slots
-// never change once set: a plain read that sees the key is exact and a stale
-// EMPTY only costs a CAS.
-__device__ inline uint32_t gtab_insert(uint64_t* gt, uint32_t gbits, uint64_t key) {
+// Level key table in global memory: 4-slot buckets (32 B); a key's id is its
+// slot.  A key's probe sequence is the slots of its home bucket in its own
+// cyclic order, starting at its preferred slot (the two hash bits below the
+// bucket bits), then the next bucket's the same way; an insert CASes the
+// slots of its sequence in turn (no reads) and stops at the first that was
+// empty or holds the key.  Slots never change once set, so every inserter of
+// a key stops at the same slot (no duplicates), and a key lives beyond its
+// home bucket only if that bucket is full (a lookup stops at a bucket with a
+// free slot).  The table is kept sparse, so most inserts settle with one CAS.
+__device__ inline uint32_t gtab_step(uint64_t key, uint32_t gbits, uint32_t step) {
+  const uint32_t h = sw_hash(key, gbits);  // bucket bits, then the preferred slot
   const uint32_t nbm = (1u << (gbits - 2)) - 1u;
-  uint32_t b = sw_hash(key, gbits - 2);
-  for (uint32_t q = 0; q <= nbm;) {
-    const uint4* p = (const uint4*)(gt + 4 * b);
-    const uint4 x = p[0], y = p[1];
-    const uint64_t sv[4] = {((uint64_t)x.y << 32) | x.x, ((uint64_t)x.w << 32) | x.z,
-                            ((uint64_t)y.y << 32) | y.x, ((uint64_t)y.w << 32) | y.z};
-    uint32_t fre = 4;
-#pragma unroll
-    for (uint32_t i = 0; i < 4; i++) {
-      if (sv[i] == key) return 4 * b + i;
-      if (sv[i] == KEY_EMPTY && fre == 4) fre = i;
-    }
-    if (fre < 4) {
-      const unsigned long long prev = atomicCAS((unsigned long long*)(gt + 4 * b + fre),
-                                                (unsigned long long)KEY_EMPTY,
-                                                (unsigned long long)key);
-      if (prev == KEY_EMPTY || prev == key) return 4 * b + fre;
-      continue;  // lost the slot: read the bucket again
-    }
-    b = (b + 1) & nbm;  // full bucket: the next one
-    q++;
-  }
-  return 0;  // unreachable: the access budget keeps the table <= 25% full
+  const uint32_t b = ((h >> 2) + (step >> 2)) & nbm;
+  return 4 * b + (((h & 3u) + step) & 3u);
 }
-// slot of `key`, or ~0u when absent
-__device__ inline uint32_t gtab_find(const uint64_t* gt, uint32_t gbits, uint64_t key) {
-  const uint32_t nbm = (1u << (gbits - 2)) - 1u;
-  uint32_t b = sw_hash(key, gbits - 2);
-  for (uint32_t q = 0; q <= nbm; q++) {
-    const uint4* p = (const uint4*)(gt + 4 * b);
-    const uint4 x = p[0], y = p[1];
-    const uint64_t v0 = ((uint64_t)x.y << 32) | x.x, v1 = ((uint64_t)x.w << 32) | x.z;
-    const uint64_t v2 = ((uint64_t)y.y << 32) | y.x, v3 = ((uint64_t)y.w << 32) | y.z;
-    if (v0 == key) return 4 * b;
-    if (v1 == key) return 4 * b + 1;
-    if (v2 == key) return 4 * b + 2;
-    if (v3 == key) return 4 * b + 3;
-    if (v3 == KEY_EMPTY) return ~0u;
-    b = (b + 1) & nbm;
+__device__ inline unsigned long long gtab_cas(uint64_t* gt, uint32_t slot, uint64_t key) {
+  return atomicCAS((unsigned long long*)(gt + slot), (unsigned long long)KEY_EMPTY,
+                   (unsigned long long)key);
+}
+// the key's slot, walking its sequence from `step`
+__device__ inline uint32_t gtab_insert(uint64_t* gt, uint32_t gbits, uint64_t key, uint32_t step) {
+  for (uint32_t q = step; q < (4u << (gbits - 2)); q++) {
+    const uint32_t sl = gtab_step(key, gbits, q);
+    const unsigned long long prev = gtab_cas(gt, sl, key);
+    if (prev == KEY_EMPTY || prev == key) return sl;
   }
-  return ~0u;
+  return 0;  // unreachable: the table is far from full
 }
 
 // Two Bloom-filter bits of a key (2^SW_BLOOM_LOG bits).
@@ -224,6 +204,14 @@ __device__ inline uint64_t lanemask_lt() {
 
 __device__ inline uint32_t list_len(const uint32_t* m_dev, uint32_t m_host) {
   return m_dev ? *m_dev : m_host;
+}
+
+// 64-txn tiles per filter workgroup (filter, apply and compaction agree): at
+// least one per wave, so a short list keeps fewer workgroups busy, each with
+// all its waves, and the idle ones leave at once instead of running a second
+// generation of half-empty workgroups through the whole setup
+__device__ inline uint32_t sw_tiles_per_wg(uint32_t n64, uint32_t nblocks) {
+  return max((n64 + nblocks - 1) / nblocks, SW_CHUNK / 64);
 }
 
 // ---------------------------------------------------------------------------
@@ -390,53 +378,51 @@ __global__ __launch_bounds__(PRE_B) void k_sw_pre(SwPreArgs a) {
         if ((wmk >> u) & 1u) atomicOr((unsigned long long*)&mmask[slot[u]], 1ull << lt[u]);
         atomicOr((unsigned long long*)&mamask[slot[u]], 1ull << lt[u]);
       }
+      if (a.dbg && blockIdx.x == 0) {  // debug only: phase boundaries of the block
+        __syncthreads();
+        if (j == 0 && p == 0) a.dbg[12] = __builtin_amdgcn_s_memrealtime();
+      }
       // the first access of each key enters it in the global table: every
-      // home-bucket read in flight at once, then every CAS, then the rare
-      // full-bucket / lost-race slow path
+      // CAS of the first slot of the key's sequence in flight at once; a
+      // lost slot (another key holds it) takes the next slot in a second
+      // round, and only a second loss walks on alone
       {
-        const uint32_t lb = a.gbits - 2;
-        uint4 bx[PRE_U], by[PRE_U];
-#pragma unroll
-        for (uint32_t u = 0; u < PRE_U; u++) {  // unconditional: all in flight together
-          const uint4* hp = (const uint4*)(a.gtab + 4 * (uint64_t)sw_hash(key[u], lb));
-          bx[u] = hp[0];
-          by[u] = hp[1];
-        }
-        uint32_t gid[PRE_U], tried = 0;
-#pragma unroll
-        for (uint32_t u = 0; u < PRE_U; u++) {
-          gid[u] = ~0u;
-          if (!((fm >> u) & 1u)) continue;
-          const uint32_t hb = sw_hash(key[u], lb);
-          const uint64_t sv[4] = {((uint64_t)bx[u].y << 32) | bx[u].x,
-                                  ((uint64_t)bx[u].w << 32) | bx[u].z,
-                                  ((uint64_t)by[u].y << 32) | by[u].x,
-                                  ((uint64_t)by[u].w << 32) | by[u].z};
-          uint32_t fre = 4;
-#pragma unroll
-          for (uint32_t i = 0; i < 4; i++) {
-            if (sv[i] == key[u] && gid[u] == ~0u) gid[u] = 4 * hb + i;
-            if (sv[i] == KEY_EMPTY && fre == 4) fre = i;
-          }
-          if (gid[u] == ~0u && fre < 4) {
-            gid[u] = 4 * hb + fre;
-            tried |= 1u << u;
-          }
-        }
         unsigned long long prev[PRE_U];
+        uint32_t gid[PRE_U];
 #pragma unroll
-        for (uint32_t u = 0; u < PRE_U; u++)
+        for (uint32_t u = 0; u < PRE_U; u++) {
+          gid[u] = gtab_step(key[u], a.gbits, 0);
           prev[u] = KEY_EMPTY;
+          if ((fm >> u) & 1u) prev[u] = gtab_cas(a.gtab, gid[u], key[u]);
+        }
+        uint32_t lost = 0;
 #pragma unroll
         for (uint32_t u = 0; u < PRE_U; u++)
-          if ((tried >> u) & 1u)
-            prev[u] = atomicCAS((unsigned long long*)(a.gtab + gid[u]),
-                                (unsigned long long)KEY_EMPTY, (unsigned long long)key[u]);
+          if (((fm >> u) & 1u) && prev[u] != KEY_EMPTY && prev[u] != key[u]) lost |= 1u << u;
+        if (a.dbg && blockIdx.x == 0) {
+          __syncthreads();
+          if (j == 0 && p == 0) a.dbg[13] = __builtin_amdgcn_s_memrealtime();
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < PRE_U; u++)
+          if ((lost >> u) & 1u) {
+            gid[u] = gtab_step(key[u], a.gbits, 1);
+            prev[u] = gtab_cas(a.gtab, gid[u], key[u]);
+          }
+        uint32_t slow = 0;
+#pragma unroll
+        for (uint32_t u = 0; u < PRE_U; u++)
+          if (((lost >> u) & 1u) && prev[u] != KEY_EMPTY && prev[u] != key[u]) slow |= 1u << u;
+        if (a.dbg && blockIdx.x == 0) {
+          __syncthreads();
+          if (j == 0 && p == 0) a.dbg[14] = __builtin_amdgcn_s_memrealtime();
+          if (lost) atomicAdd((unsigned long long*)&a.dbg[15], (unsigned long long)__popc(lost));
+          if (fm) atomicAdd((unsigned long long*)&a.dbg[16], (unsigned long long)__popc(fm));
+        }
 #pragma unroll
         for (uint32_t u = 0; u < PRE_U; u++) {
           if (!((fm >> u) & 1u)) continue;
-          if (((tried >> u) & 1u) && prev[u] != KEY_EMPTY && prev[u] != key[u]) gid[u] = ~0u;
-          if (gid[u] == ~0u) gid[u] = gtab_insert(a.gtab, a.gbits, key[u]);
+          if ((slow >> u) & 1u) gid[u] = gtab_insert(a.gtab, a.gbits, key[u], 2);
           mgid[slot[u]] = gid[u];
         }
       }
@@ -956,7 +942,6 @@ __global__ __launch_bounds__(256) void k_sw_cout(SwCoutArgs a) {
 
 constexpr uint32_t FW = SW_CHUNK / 64;  // waves per filter workgroup
 constexpr uint32_t FK = 16;             // access rounds kept in registers (1024 accesses)
-constexpr uint32_t F_EXACT = 2048;      // LDS exact set of small C (<= 1024 keys)
 constexpr uint32_t SW_CMP_MAXR = 4096;  // tiles of one filter workgroup
 
 // exact membership of a Bloom-positive key: its slot in the level's key
@@ -976,7 +961,8 @@ __device__ inline bool c_exact(const SwFilterArgs& a, uint64_t key) {
     if (v1 == key) return (nib >> 1) & 1u;
     if (v2 == key) return (nib >> 2) & 1u;
     if (v3 == key) return (nib >> 3) & 1u;
-    if (v3 == KEY_EMPTY) return false;
+    // a bucket with a free slot ends the chain (gtab_insert)
+    if (v0 == KEY_EMPTY || v1 == KEY_EMPTY || v2 == KEY_EMPTY || v3 == KEY_EMPTY) return false;
     b = (b + 1) & nbm;
   }
   return false;
@@ -984,27 +970,30 @@ __device__ inline bool c_exact(const SwFilterArgs& a, uint64_t key) {
 constexpr uint32_t F_STASH = 256;  // Bloom-positive keys kept in LDS per wave
 constexpr uint32_t F_XS = 2048;    // small-C filter instance: LDS exact-set slots
 constexpr uint32_t F_XCAP = 1024;  // ... for C of up to this many keys (<= 50% load)
-constexpr uint32_t F_XB = 256;     // ... threads per workgroup
 constexpr uint32_t F_XBITS_LOG = 16;  // ... its one-hash bitmap of C (8 KiB)
 
 // ---------------------------------------------------------------------------
 // k_sw_filter: list txns [pos, m) against C, 64 per wave, grid-stride (no
 // cross-workgroup waits).  A txn touching a key of C is killed; the others
 // get a survivor bit and per-tile counts for the compaction.
-// Two instances: X (exact) when C has <= F_XCAP keys -- C as an LDS hash set
-// and nothing else, so a workgroup holds 36 KB of LDS and four fit a CU --
-// and the Bloom-filtered one otherwise.  Both are launched; the one whose
-// case it is not returns at once.
-template <bool X>
-__global__ __launch_bounds__(X ? F_XB : SW_CHUNK) void k_sw_filter(SwFilterArgs a) {
-  // (both instances map the same tiles to each workgroup)
-  constexpr uint32_t B = X ? F_XB : SW_CHUNK, FW = B / 64;
-  constexpr uint32_t CS = X ? F_XS : F_EXACT;  // exact-set slots
-  // X: a one-hash bitmap of C built here (one conflict-light ds_read_b32 per
-  // access) in front of the exact set; otherwise the level's Bloom filter
-  constexpr uint32_t BLOG = X ? F_XBITS_LOG : SW_BLOOM_LOG;  // filter bits (log2)
-  __shared__ uint32_t bl[(1u << BLOG) / 32];
-  __shared__ __attribute__((aligned(16))) uint64_t cex[CS];
+// Two modes, chosen per launch from |C|: exact (X) when C has <= F_XCAP keys
+// -- C as an LDS hash set behind a one-hash LDS bitmap, nothing global --
+// and the level's Bloom filter with exact checks in the global key table
+// otherwise.  Their LDS overlaps (36 KB in all: four workgroups fit a CU).
+__global__ __launch_bounds__(SW_CHUNK) void k_sw_filter(SwFilterArgs a) {
+  constexpr uint32_t B = SW_CHUNK, FW = B / 64;
+  constexpr uint32_t CS = F_XS;  // exact-set slots (X)
+  struct XSet {
+    uint32_t bl[(1u << F_XBITS_LOG) / 32];
+    uint64_t cex[F_XS];
+  };
+  union FSet {
+    XSet x;
+    uint32_t bl[(1u << SW_BLOOM_LOG) / 32];
+  };
+  __shared__ __attribute__((aligned(16))) FSet fs;
+  uint32_t* const bl = fs.bl;     // both modes' bitmaps start the union
+  uint64_t* const cex = fs.x.cex;
   __shared__ uint64_t s_hit[FW][SW_WA / 64];
   __shared__ uint64_t s_wr[FW][SW_WA / 64];
   __shared__ uint64_t s_stash[FW][F_STASH];
@@ -1014,7 +1003,7 @@ __global__ __launch_bounds__(X ? F_XB : SW_CHUNK) void k_sw_filter(SwFilterArgs 
   const uint32_t m = list_len(a.m_dev, a.m_host);
   const uint32_t pos = a.lv->pos;
   const uint32_t ccount = a.lv->ccount;
-  if (X ? ccount > F_XCAP : (a.exact_launched && ccount <= F_XCAP)) return;
+  const bool X = ccount <= F_XCAP;  // uniform
   // DCC_SW_DEBUG: wave 0 of workgroups < 256 stamps start / setup / loads /
   // exact checks / writes / end and counts its tiles
   uint64_t* dbg = (a.dbg && blockIdx.x < 256 && j == 0) ? a.dbg + 8 * blockIdx.x : nullptr;
@@ -1033,17 +1022,23 @@ __global__ __launch_bounds__(X ? F_XB : SW_CHUNK) void k_sw_filter(SwFilterArgs 
   if (pos >= m) return;
   const uint32_t n64 = (m - pos + 63) / 64;
   const uint64_t nnz = a.in.nnz;
-  const bool small = X || ccount <= F_EXACT / 2;  // exact checks in LDS
+  // workgroup g: tiles [g R, (g + 1) R), its total into bsum[g] (two-level scan)
+  const uint32_t R = sw_tiles_per_wg(n64, gridDim.x);
+  const uint32_t t_lo = min(blockIdx.x * R, n64), t_hi = min(t_lo + R, n64);
+  if (t_lo >= t_hi) {  // idle: no setup
+    if (!a.kill_out && j == 0) a.bsum[blockIdx.x] = 0;
+    return;
+  }
+  const bool small = X;  // exact checks in LDS
   {
     if (!X) {
       const uint4* src = (const uint4*)a.bloom;
       uint4* dst = (uint4*)bl;
       for (uint32_t q = j; q < (1u << SW_BLOOM_LOG) / 128; q += B) dst[q] = src[q];
     } else {
-      for (uint32_t q = j; q < (1u << BLOG) / 32; q += B) bl[q] = 0;
-    }
-    if (small)
+      for (uint32_t q = j; q < (1u << F_XBITS_LOG) / 32; q += B) bl[q] = 0;
       for (uint32_t q = j; q < CS; q += B) cex[q] = KEY_EMPTY;
+    }
   }
   __syncthreads();
   if (small) {
@@ -1053,7 +1048,7 @@ __global__ __launch_bounds__(X ? F_XB : SW_CHUNK) void k_sw_filter(SwFilterArgs 
       if (X) {
         uint32_t b1, b2;
         bloom_bits(kq, b1, b2);
-        b1 >>= SW_BLOOM_LOG - BLOG;
+        b1 >>= SW_BLOOM_LOG - F_XBITS_LOG;
         atomicOr(&bl[b1 >> 5], 1u << (b1 & 31u));
       }
     }
@@ -1063,9 +1058,6 @@ __global__ __launch_bounds__(X ? F_XB : SW_CHUNK) void k_sw_filter(SwFilterArgs 
   uint64_t* hit = s_hit[wv];
   uint64_t* wr = s_wr[wv];
   uint64_t* stash = s_stash[wv];
-  // workgroup g: tiles [g R, (g + 1) R), its total into bsum[g] (two-level scan)
-  const uint32_t R = (n64 + gridDim.x - 1) / gridDim.x;
-  const uint32_t t_lo = min(blockIdx.x * R, n64), t_hi = min(t_lo + R, n64);
   uint64_t wsum = 0;
   // the per-txn words of a wave's next tile are loaded while the current
   // tile's keys are in flight (branch-free, clamped: they issue together)
@@ -1128,7 +1120,7 @@ __global__ __launch_bounds__(X ? F_XB : SW_CHUNK) void k_sw_filter(SwFilterArgs 
         uint32_t b1, b2;
         bloom_bits(key[u], b1, b2);
         if (X) {
-          b1 >>= SW_BLOOM_LOG - BLOG;
+          b1 >>= SW_BLOOM_LOG - F_XBITS_LOG;
           h = in && ((bl[b1 >> 5] >> (b1 & 31u)) & 1u) != 0;
         } else {
           const uint32_t wa = bl[b1 >> 5], wb = bl[b2 >> 5];
@@ -1233,7 +1225,7 @@ __global__ __launch_bounds__(SW_CHUNK) void k_sw_apply(SwFilterArgs a) {
   if (pos >= m) return;
   const uint32_t n64 = (m - pos + 63) / 64;
   const uint64_t nnz = a.in.nnz;
-  const uint32_t R = (n64 + gridDim.x - 1) / gridDim.x;
+  const uint32_t R = sw_tiles_per_wg(n64, gridDim.x);
   const uint32_t t_lo = min(blockIdx.x * R, n64), t_hi = min(t_lo + R, n64);
   uint64_t wsum = 0;
   for (uint32_t wt = t_lo + wv; wt < t_hi; wt += SW_CHUNK / 64) {
@@ -1422,8 +1414,9 @@ __global__ __launch_bounds__(SW_CHUNK) void k_sw_compact(SwFilterArgs a) {
   const uint32_t n64 = (m - pos + 63) / 64;
   const uint64_t nnz = a.in.nnz;
   // the filter's block ranges: block base from the scan, tile bases in LDS
-  const uint32_t R = (n64 + a.nblocks - 1) / a.nblocks;
+  const uint32_t R = sw_tiles_per_wg(n64, a.nblocks);
   const uint32_t t_lo = min(blockIdx.x * R, n64), t_hi = min(t_lo + R, n64);
+  if (t_lo >= t_hi && blockIdx.x) return;  // idle (workgroup 0 closes the level)
   __shared__ unsigned long long s_tb[SW_CMP_MAXR];
   __shared__ unsigned long long s_part[SW_CHUNK / 64][2];
   if (R > SW_CMP_MAXR) {
@@ -1550,15 +1543,8 @@ void launch_sw_rows(const SwPreArgs& a, unsigned grid, hipStream_t st) {
 void launch_sw_cout(const SwCoutArgs& a, unsigned grid, hipStream_t st) {
   k_sw_cout<<<grid ? grid : 1u, 256, 0, st>>>(a);
 }
-// The exact-set instance runs only where C can be small, level 0 (later
-// levels collect thousands of keys; the Bloom instance serves any size):
-// launch_sw_filter_x then launch_sw_filter_b with exact_launched = 1, or
-// launch_sw_filter_b alone with exact_launched = 0.
-void launch_sw_filter_x(const SwFilterArgs& a, unsigned grid, hipStream_t st) {
-  k_sw_filter<true><<<grid ? grid : 1u, F_XB, 0, st>>>(a);
-}
-void launch_sw_filter_b(const SwFilterArgs& a, unsigned grid, hipStream_t st) {
-  k_sw_filter<false><<<grid ? grid : 1u, SW_CHUNK, 0, st>>>(a);
+void launch_sw_filter(const SwFilterArgs& a, unsigned grid, hipStream_t st) {
+  k_sw_filter<<<grid ? grid : 1u, SW_CHUNK, 0, st>>>(a);
 }
 void launch_sw_scan(const SwFilterArgs& a, hipStream_t st) { k_sw_scan<<<1, 1024, 0, st>>>(a); }
 void launch_sw_share(const uint32_t* m_dev, uint32_t m_host, const uint32_t* abandon,

@@ -52,10 +52,11 @@ def main():
     tot = [2.0 * sum(d["v"] for d in fe[i]) * 1024 + sum(d["v"] for d in wr[i]) * 1024 for i in range(n)]
     filt = []
     for i in range(n):
-        f = [d["v"] for d in fe[i] if "k_sw_filter<true>" in d["name"]]
-        w = [d["v"] for d in wr[i] if "k_sw_filter<true>" in d["name"]]
+        # the epoch's first filter dispatch is level 0's
+        f = [d["v"] for d in fe[i] if "k_sw_filter" in d["name"]]
+        w = [d["v"] for d in wr[i] if "k_sw_filter" in d["name"]]
         if f and w:
-            filt.append(2.0 * max(f) * 1024 + max(w) * 1024)
+            filt.append(2.0 * f[0] * 1024 + w[0] * 1024)
     res = {"bytes_per_epoch": statistics.median(tot), "epochs": n,
            "filter_bytes_per_launch": statistics.median(filt) if filt else None,
            "source": src, "correction": "FETCH_SIZE x2 (gfx950 128-B requests counted at 64 B)"}

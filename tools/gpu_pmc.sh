@@ -16,6 +16,6 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
 done
 python3 "$R/tools/pmc_summary.py" "$OUT" k_sw_ > "$OUT/summary.txt" 2>&1
 cp -f "$R/profiles/traffic.json" "$OUT/traffic.json" 2>/dev/null || true
-python3 "$R/tools/traffic.py" "$OUT" "k_sw_filter<true>" "1048576:0.9:16:k_sw_filter" "$OUT/traffic.json" || exit 1
+python3 "$R/tools/traffic.py" "$OUT" "k_sw_filter" "1048576:0.9:16:k_sw_filter" "$OUT/traffic.json" || exit 1
 cp -f "$OUT/traffic.json" "$R/profiles/traffic.json"
 echo "pmc done"

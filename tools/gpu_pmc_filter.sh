@@ -14,5 +14,5 @@ for grp in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE
   timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d "$OUT/p$i" -o run \
       -- python3 $ARGS > "$OUT/p$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/p$i.log"; exit 1; }
 done
-python3 "$R/tools/pmc_dispatch.py" "$OUT" "k_sw_filter<true>" 3
+python3 "$R/tools/pmc_dispatch.py" "$OUT" "k_sw_filter" 3
 python3 "$R/tools/pmc_dispatch.py" "$OUT" "k_sw_seq" 4
