@@ -437,6 +437,7 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1, const SwShard* shl
     fa.la_clear = la;
     fa.err = err;
     fa.dbg = (sw_debug && l < 4) ? (uint64_t*)sw_dbg.p + 4096 + (size_t)l * 256 * 8 : nullptr;
+    fa.cdbg = pa.dbg ? pa.dbg + 32 : nullptr;
     fa.kill_out = shl ? shl->kill : nullptr;
     fa.kill_in = shl ? shl->kill : nullptr;
     // phase 1 of the profile is exactly the level-0 streaming filter
@@ -833,6 +834,9 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
                             "%.2f; first inserts %llu, lost first slots %llu\n", l, (pp[12] - pp[3]) * 0.01,
                     (pp[13] - pp[12]) * 0.01, (pp[14] - pp[13]) * 0.01, (pp[4] - pp[14]) * 0.01,
                     (unsigned long long)pp[16], (unsigned long long)pp[15]);
+          if (pp[36])
+            fprintf(stderr, "  compact L%d (us, workgroup 0): totals %.2f tile bases %.2f moves %.2f\n", l,
+                    (pp[33] - pp[32]) * 0.01, (pp[34] - pp[33]) * 0.01, (pp[36] - pp[34]) * 0.01);
           if (pp[11])
             fprintf(stderr, "  rows L%d (us): offsets %.2f flags %.2f lists %.2f\n", l,
                     (pp[9] - pp[8]) * 0.01, (pp[10] - pp[9]) * 0.01, (pp[11] - pp[10]) * 0.01);

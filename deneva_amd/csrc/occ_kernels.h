@@ -298,6 +298,7 @@ struct SwFilterArgs {
   uint32_t* la_clear;
   uint32_t* err;
   uint64_t* dbg;          // per-workgroup clock stamps (DCC_SW_DEBUG) or null
+  uint64_t* cdbg;         // k_sw_compact's workgroup-0 stamps (DCC_SW_DEBUG) or null
 };
 // One key-sharded sweep level (the host side of SURVEY.md §8(e)): the merged
 // serial range, its txn count, the list length and the kill-bit buffer.

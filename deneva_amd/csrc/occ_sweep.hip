@@ -222,7 +222,6 @@ __device__ inline uint32_t sw_tiles_per_wg(uint32_t n64, uint32_t nblocks) {
 // costs one global CAS per tile rather than one per access.
 constexpr uint32_t PRE_MAP = 4096;       // LDS map slots (<= 2048 distinct keys per pass)
 constexpr uint32_t PRE_B = 512;           // threads per workgroup
-constexpr uint32_t PRE_U = SW_TA / PRE_B;  // accesses per thread
 
 __device__ inline uint32_t pre_map_insert(uint64_t* mkey, uint64_t key, bool& first) {
   uint32_t h = sw_hash(key, 12);
@@ -251,15 +250,181 @@ __device__ inline uint32_t pre_map_insert(uint64_t* mkey, uint64_t key, bool& fi
   return 0;  // unreachable: a pass holds <= PRE_MAP distinct keys
 }
 
+// the tile's accesses, U per thread (j + PRE_B u): key ids, writer /
+// accessor masks, dependency masks, first-writer / last-accessor positions.
+// Instantiated for U = 2, 4, 8 and chosen per tile, so the common short tile
+// (<= 1024 accesses) runs without the register pressure of the longest.
+struct PreLds {
+  uint64_t mkey[PRE_MAP];
+  uint64_t mmask[PRE_MAP];   // writers of the key in the tile
+  uint64_t mamask[PRE_MAP];  // accessors of the key in the tile
+  uint32_t mgid[PRE_MAP];
+  uint64_t s_dep[SW_T];
+  uint32_t s_off[SW_T + 1];
+  uint32_t s_meta[SW_T];
+  uint32_t s_bad;
+};
+template <uint32_t U>
+__device__ inline void pre_tile(const SwPreArgs& a, PreLds& L, uint32_t k, uint32_t j, uint32_t nt,
+                                uint32_t A0, uint32_t cnt, uint64_t off0) {
+  uint64_t* const mkey = L.mkey;
+  uint64_t* const mmask = L.mmask;
+  uint64_t* const mamask = L.mamask;
+  uint32_t* const mgid = L.mgid;
+  uint64_t* const s_dep = L.s_dep;
+  const uint32_t* const s_off = L.s_off;
+  uint32_t* const s_meta = L.s_meta;
+  // per-thread accesses j + PRE_B u; flags packed into bit masks over u.
+  // Every load is issued first (clamped addresses), then the accesses are
+  // classified, so the loads of a thread are in flight together.
+  uint64_t key[U];
+  uint32_t lt[U], slot[U];
+  uint32_t vm = 0, wmk = 0;
+  {
+    uint8_t atv[U];
+    const uint32_t xmax = cnt ? A0 + cnt - 1 : A0;
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++) {
+      const uint32_t x = min(A0 + j + PRE_B * u, xmax);
+      key[u] = a.in.keys[x];
+      atv[u] = a.in.acctype[x];
+    }
+    uint32_t bad_key = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++) {
+      lt[u] = 0;
+      slot[u] = 0;
+      const uint32_t xr = j + PRE_B * u;
+      if (xr >= cnt) continue;
+      const uint32_t x = A0 + xr;
+      // largest t < nt with s_off[t] <= x (empty txns never own an access)
+      uint32_t lo = 0, hi = nt;  // invariant: s_off[lo] <= x < s_off[hi]
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (s_off[mid] <= x) lo = mid;
+        else hi = mid;
+      }
+      lt[u] = lo;
+      if (atv[u] == 1) {  // WR (occ.cpp:379-383)
+        wmk |= 1u << u;
+        atomicOr(&s_meta[lo], SWM_HASW);
+      }
+      if (key[u] == KEY_EMPTY) {
+        // the reserved key is reported by the host; it gets no key id (its
+        // access is recorded as an unused entry)
+        bad_key = 1;
+        a.aent[A0 - (uint32_t)off0 + xr] = SW_A_NONE;
+        a.apos[A0 - (uint32_t)off0 + xr] = k * SW_T;
+      } else {
+        vm |= 1u << u;
+      }
+    }
+    if (bad_key) atomicOr(a.err, ERR_KEY);
+  }
+  // passes over key-hash classes keep each map pass <= 2048 distinct keys
+  const uint32_t P = cnt <= PRE_MAP / 2 ? 1u : 2u;
+  for (uint32_t p = 0; p < P; p++) {
+    for (uint32_t q = j; q < PRE_MAP; q += PRE_B) {
+      mkey[q] = KEY_EMPTY;
+      mmask[q] = 0;
+      mamask[q] = 0;
+    }
+    __syncthreads();
+  if (a.dbg && blockIdx.x == 0 && threadIdx.x == 0) a.dbg[3] = __builtin_amdgcn_s_memrealtime();
+    uint32_t pm = vm;  // this pass's accesses
+    if (P > 1)
+#pragma unroll
+      for (uint32_t u = 0; u < U; u++)
+        if ((sw_hash(key[u], 13) & 1u) != p) pm &= ~(1u << u);
+    uint32_t fm = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++) {
+      if (!((pm >> u) & 1u)) continue;
+      bool first;
+      slot[u] = pre_map_insert(mkey, key[u], first);
+      if (first) fm |= 1u << u;
+      if ((wmk >> u) & 1u) atomicOr((unsigned long long*)&mmask[slot[u]], 1ull << lt[u]);
+      atomicOr((unsigned long long*)&mamask[slot[u]], 1ull << lt[u]);
+    }
+    if (a.dbg && blockIdx.x == 0) {  // debug only: phase boundaries of the block
+      __syncthreads();
+      if (j == 0 && p == 0) a.dbg[12] = __builtin_amdgcn_s_memrealtime();
+    }
+    // the first access of each key enters it in the global table: every
+    // CAS of the first slot of the key's sequence in flight at once; a
+    // lost slot (another key holds it) takes the next slot in a second
+    // round, and only a second loss walks on alone
+    {
+      unsigned long long prev[U];
+      uint32_t gid[U];
+#pragma unroll
+      for (uint32_t u = 0; u < U; u++) {
+        gid[u] = gtab_step(key[u], a.gbits, 0);
+        prev[u] = KEY_EMPTY;
+        if ((fm >> u) & 1u) prev[u] = gtab_cas(a.gtab, gid[u], key[u]);
+      }
+      uint32_t lost = 0;
+#pragma unroll
+      for (uint32_t u = 0; u < U; u++)
+        if (((fm >> u) & 1u) && prev[u] != KEY_EMPTY && prev[u] != key[u]) lost |= 1u << u;
+      if (a.dbg && blockIdx.x == 0) {
+        __syncthreads();
+        if (j == 0 && p == 0) a.dbg[13] = __builtin_amdgcn_s_memrealtime();
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < U; u++)
+        if ((lost >> u) & 1u) {
+          gid[u] = gtab_step(key[u], a.gbits, 1);
+          prev[u] = gtab_cas(a.gtab, gid[u], key[u]);
+        }
+      uint32_t slow = 0;
+#pragma unroll
+      for (uint32_t u = 0; u < U; u++)
+        if (((lost >> u) & 1u) && prev[u] != KEY_EMPTY && prev[u] != key[u]) slow |= 1u << u;
+      if (a.dbg && blockIdx.x == 0) {
+        __syncthreads();
+        if (j == 0 && p == 0) a.dbg[14] = __builtin_amdgcn_s_memrealtime();
+        if (lost) atomicAdd((unsigned long long*)&a.dbg[15], (unsigned long long)__popc(lost));
+        if (fm) atomicAdd((unsigned long long*)&a.dbg[16], (unsigned long long)__popc(fm));
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < U; u++) {
+        if (!((fm >> u) & 1u)) continue;
+        if ((slow >> u) & 1u) gid[u] = gtab_insert(a.gtab, a.gbits, key[u], 2);
+        mgid[slot[u]] = gid[u];
+      }
+    }
+    __syncthreads();
+  if (a.dbg && blockIdx.x == 0 && threadIdx.x == 0) a.dbg[4] = __builtin_amdgcn_s_memrealtime();
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++) {
+      if (!((pm >> u) & 1u)) continue;
+      const uint32_t t = lt[u];
+      const uint64_t wmask = mmask[slot[u]];
+      const uint64_t wm = wmask & ((1ull << t) - 1ull);  // earlier writers only
+      if (wm) atomicOr((unsigned long long*)&s_dep[t], (unsigned long long)wm);
+      const uint32_t gid = mgid[slot[u]];
+      // the key's first writer and last accessor in the level's serial
+      // range (list positions), once per distinct key of the tile
+      if ((fm >> u) & 1u) {
+        if (wmask) atomicMin(&a.first_w[gid], k * SW_T + (uint32_t)__builtin_ctzll(wmask));
+        atomicMax(&a.last_a[gid], k * SW_T + 63u - (uint32_t)__builtin_clzll(mamask[slot[u]]));
+      }
+      const uint32_t xo = A0 - (uint32_t)off0 + j + PRE_B * u;
+      a.aent[xo] = sw_apack(gid, (wmk >> u) & 1u);
+      a.apos[xo] = k * SW_T + t;
+    }
+    __syncthreads();  // map reuse by the next pass
+  if (a.dbg && blockIdx.x == 0 && threadIdx.x == 0) a.dbg[5] = __builtin_amdgcn_s_memrealtime();
+  }
+}
+
 __global__ __launch_bounds__(PRE_B) void k_sw_pre(SwPreArgs a) {
-  __shared__ uint64_t mkey[PRE_MAP];
-  __shared__ uint64_t mmask[PRE_MAP];   // writers of the key in the tile
-  __shared__ uint64_t mamask[PRE_MAP];  // accessors of the key in the tile
-  __shared__ uint32_t mgid[PRE_MAP];
-  __shared__ uint64_t s_dep[SW_T];
-  __shared__ uint32_t s_off[SW_T + 1];
-  __shared__ uint32_t s_meta[SW_T];
-  __shared__ uint32_t s_bad;
+  __shared__ PreLds L;
+  uint64_t* const s_dep = L.s_dep;
+  uint32_t* const s_off = L.s_off;
+  uint32_t* const s_meta = L.s_meta;
+  uint32_t& s_bad = L.s_bad;
   if (*a.abandon) return;
     if (a.dbg && blockIdx.x == 0 && threadIdx.x == 0) a.dbg[0] = __builtin_amdgcn_s_memrealtime();
   const uint32_t m = list_len(a.m_dev, a.m_host);
@@ -306,149 +471,9 @@ __global__ __launch_bounds__(PRE_B) void k_sw_pre(SwPreArgs a) {
       if (j < SW_T) R.meta[j] = SWM_STOP;
       return;
     }
-    // per-thread accesses j + PRE_B u; flags packed into bit masks over u.
-    // Every load is issued first (clamped addresses), then the accesses are
-    // classified, so the loads of a thread are in flight together.
-    uint64_t key[PRE_U];
-    uint32_t lt[PRE_U], slot[PRE_U];
-    uint32_t vm = 0, wmk = 0;
-    {
-      uint8_t atv[PRE_U];
-      const uint32_t xmax = cnt ? A0 + cnt - 1 : A0;
-#pragma unroll
-      for (uint32_t u = 0; u < PRE_U; u++) {
-        const uint32_t x = min(A0 + j + PRE_B * u, xmax);
-        key[u] = a.in.keys[x];
-        atv[u] = a.in.acctype[x];
-      }
-      uint32_t bad_key = 0;
-#pragma unroll
-      for (uint32_t u = 0; u < PRE_U; u++) {
-        lt[u] = 0;
-        slot[u] = 0;
-        const uint32_t xr = j + PRE_B * u;
-        if (xr >= cnt) continue;
-        const uint32_t x = A0 + xr;
-        // largest t < nt with s_off[t] <= x (empty txns never own an access)
-        uint32_t lo = 0, hi = nt;  // invariant: s_off[lo] <= x < s_off[hi]
-        while (hi - lo > 1) {
-          const uint32_t mid = (lo + hi) >> 1;
-          if (s_off[mid] <= x) lo = mid;
-          else hi = mid;
-        }
-        lt[u] = lo;
-        if (atv[u] == 1) {  // WR (occ.cpp:379-383)
-          wmk |= 1u << u;
-          atomicOr(&s_meta[lo], SWM_HASW);
-        }
-        if (key[u] == KEY_EMPTY) {
-          // the reserved key is reported by the host; it gets no key id (its
-          // access is recorded as an unused entry)
-          bad_key = 1;
-          a.aent[A0 - (uint32_t)off0 + xr] = SW_A_NONE;
-          a.apos[A0 - (uint32_t)off0 + xr] = k * SW_T;
-        } else {
-          vm |= 1u << u;
-        }
-      }
-      if (bad_key) atomicOr(a.err, ERR_KEY);
-    }
-    // passes over key-hash classes keep each map pass <= 2048 distinct keys
-    const uint32_t P = cnt <= PRE_MAP / 2 ? 1u : 2u;
-    for (uint32_t p = 0; p < P; p++) {
-      for (uint32_t q = j; q < PRE_MAP; q += PRE_B) {
-        mkey[q] = KEY_EMPTY;
-        mmask[q] = 0;
-        mamask[q] = 0;
-      }
-      __syncthreads();
-    if (a.dbg && blockIdx.x == 0 && threadIdx.x == 0) a.dbg[3] = __builtin_amdgcn_s_memrealtime();
-      uint32_t pm = vm;  // this pass's accesses
-      if (P > 1)
-#pragma unroll
-        for (uint32_t u = 0; u < PRE_U; u++)
-          if ((sw_hash(key[u], 13) & 1u) != p) pm &= ~(1u << u);
-      uint32_t fm = 0;
-#pragma unroll
-      for (uint32_t u = 0; u < PRE_U; u++) {
-        if (!((pm >> u) & 1u)) continue;
-        bool first;
-        slot[u] = pre_map_insert(mkey, key[u], first);
-        if (first) fm |= 1u << u;
-        if ((wmk >> u) & 1u) atomicOr((unsigned long long*)&mmask[slot[u]], 1ull << lt[u]);
-        atomicOr((unsigned long long*)&mamask[slot[u]], 1ull << lt[u]);
-      }
-      if (a.dbg && blockIdx.x == 0) {  // debug only: phase boundaries of the block
-        __syncthreads();
-        if (j == 0 && p == 0) a.dbg[12] = __builtin_amdgcn_s_memrealtime();
-      }
-      // the first access of each key enters it in the global table: every
-      // CAS of the first slot of the key's sequence in flight at once; a
-      // lost slot (another key holds it) takes the next slot in a second
-      // round, and only a second loss walks on alone
-      {
-        unsigned long long prev[PRE_U];
-        uint32_t gid[PRE_U];
-#pragma unroll
-        for (uint32_t u = 0; u < PRE_U; u++) {
-          gid[u] = gtab_step(key[u], a.gbits, 0);
-          prev[u] = KEY_EMPTY;
-          if ((fm >> u) & 1u) prev[u] = gtab_cas(a.gtab, gid[u], key[u]);
-        }
-        uint32_t lost = 0;
-#pragma unroll
-        for (uint32_t u = 0; u < PRE_U; u++)
-          if (((fm >> u) & 1u) && prev[u] != KEY_EMPTY && prev[u] != key[u]) lost |= 1u << u;
-        if (a.dbg && blockIdx.x == 0) {
-          __syncthreads();
-          if (j == 0 && p == 0) a.dbg[13] = __builtin_amdgcn_s_memrealtime();
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < PRE_U; u++)
-          if ((lost >> u) & 1u) {
-            gid[u] = gtab_step(key[u], a.gbits, 1);
-            prev[u] = gtab_cas(a.gtab, gid[u], key[u]);
-          }
-        uint32_t slow = 0;
-#pragma unroll
-        for (uint32_t u = 0; u < PRE_U; u++)
-          if (((lost >> u) & 1u) && prev[u] != KEY_EMPTY && prev[u] != key[u]) slow |= 1u << u;
-        if (a.dbg && blockIdx.x == 0) {
-          __syncthreads();
-          if (j == 0 && p == 0) a.dbg[14] = __builtin_amdgcn_s_memrealtime();
-          if (lost) atomicAdd((unsigned long long*)&a.dbg[15], (unsigned long long)__popc(lost));
-          if (fm) atomicAdd((unsigned long long*)&a.dbg[16], (unsigned long long)__popc(fm));
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < PRE_U; u++) {
-          if (!((fm >> u) & 1u)) continue;
-          if ((slow >> u) & 1u) gid[u] = gtab_insert(a.gtab, a.gbits, key[u], 2);
-          mgid[slot[u]] = gid[u];
-        }
-      }
-      __syncthreads();
-    if (a.dbg && blockIdx.x == 0 && threadIdx.x == 0) a.dbg[4] = __builtin_amdgcn_s_memrealtime();
-#pragma unroll
-      for (uint32_t u = 0; u < PRE_U; u++) {
-        if (!((pm >> u) & 1u)) continue;
-        const uint32_t t = lt[u];
-        const uint64_t wmask = mmask[slot[u]];
-        const uint64_t wm = wmask & ((1ull << t) - 1ull);  // earlier writers only
-        if (wm) atomicOr((unsigned long long*)&s_dep[t], (unsigned long long)wm);
-        const uint32_t gid = mgid[slot[u]];
-        // the key's first writer and last accessor in the level's serial
-        // range (list positions), once per distinct key of the tile
-        if ((fm >> u) & 1u) {
-          if (wmask) atomicMin(&a.first_w[gid], k * SW_T + (uint32_t)__builtin_ctzll(wmask));
-          atomicMax(&a.last_a[gid], k * SW_T + 63u - (uint32_t)__builtin_clzll(mamask[slot[u]]));
-        }
-        const uint32_t xo = A0 - (uint32_t)off0 + j + PRE_B * u;
-        a.aent[xo] = sw_apack(gid, (wmk >> u) & 1u);
-        a.apos[xo] = k * SW_T + t;
-      }
-      __syncthreads();  // map reuse by the next pass
-    if (a.dbg && blockIdx.x == 0 && threadIdx.x == 0) a.dbg[5] = __builtin_amdgcn_s_memrealtime();
-    }
+    if (cnt <= 2 * PRE_B) pre_tile<2>(a, L, k, j, nt, A0, cnt, off0);
+    else if (cnt <= 4 * PRE_B) pre_tile<4>(a, L, k, j, nt, A0, cnt, off0);
+    else pre_tile<8>(a, L, k, j, nt, A0, cnt, off0);
     // the per-txn words (k_sw_rows adds the row length)
     if (j < SW_T) {
       uint32_t mt = s_meta[j];
@@ -1417,6 +1442,8 @@ __global__ __launch_bounds__(SW_CHUNK) void k_sw_compact(SwFilterArgs a) {
   const uint32_t R = sw_tiles_per_wg(n64, a.nblocks);
   const uint32_t t_lo = min(blockIdx.x * R, n64), t_hi = min(t_lo + R, n64);
   if (t_lo >= t_hi && blockIdx.x) return;  // idle (workgroup 0 closes the level)
+  uint64_t* dbg = (a.cdbg && blockIdx.x == 0 && threadIdx.x == 0) ? a.cdbg : nullptr;
+  if (dbg) dbg[0] = __builtin_amdgcn_s_memrealtime();
   __shared__ unsigned long long s_tb[SW_CMP_MAXR];
   __shared__ unsigned long long s_part[SW_CHUNK / 64][2];
   if (R > SW_CMP_MAXR) {
@@ -1459,6 +1486,7 @@ __global__ __launch_bounds__(SW_CHUNK) void k_sw_compact(SwFilterArgs a) {
     }
     __syncthreads();
   }
+  if (dbg) dbg[1] = __builtin_amdgcn_s_memrealtime();
   if (wv == 0) {
     uint64_t run = s_part[0][0];
     for (uint32_t c0 = t_lo; c0 < t_hi; c0 += 64) {
@@ -1475,60 +1503,81 @@ __global__ __launch_bounds__(SW_CHUNK) void k_sw_compact(SwFilterArgs a) {
     }
   }
   __syncthreads();
-  for (uint32_t wt = t_lo + wv; wt < t_hi; wt += FW) {
-    const uint64_t word = a.sflag[wt];
-    if (!word) continue;  // uniform
-    const uint64_t base = s_tb[wt - t_lo];
-    const uint32_t tb = (uint32_t)(base >> LB_ACC_BITS);
-    const uint32_t abase = (uint32_t)(base & ((1ull << LB_ACC_BITS) - 1));
-    const bool surv = (word >> lane) & 1ull;
-    const uint32_t p = pos + wt * 64 + lane;
-    uint32_t s = 0, len = 0, tid = 0;
-    if (surv) {
-      s = (uint32_t)min((uint64_t)a.in.off[p], nnz);
-      len = (uint32_t)min((uint64_t)a.in.off[p + 1], nnz) - s;
-      tid = a.in.tid ? a.in.tid[p] : p;
-    }
-    uint32_t atot;
-    const uint32_t aex = wave_excl_u32(len, atot);
-    if (surv) {
-      const uint32_t r = tb + (uint32_t)__popcll(word & lanemask_lt());
-      a.tid_out[r] = tid;
-      a.off_out[r] = abase + aex;
-    }
-    // accesses: lanes over the wave's survivor accesses; output position q
-    // belongs to the first lane whose inclusive access prefix exceeds q
-    const uint32_t incl = aex + len;
-    for (uint32_t q0 = 0; q0 < atot; q0 += 64 * 4) {
-      uint32_t src[4];
-      bool in[4];
+  if (dbg) dbg[2] = __builtin_amdgcn_s_memrealtime();
+  // a wave's tiles CB at a time: every survivor word, offset pair and txn id
+  // of the CB tiles in flight together, then each tile's moves
+  constexpr uint32_t CB = 4;
+  for (uint32_t w0 = t_lo + wv; w0 < t_hi; w0 += FW * CB) {
+    uint64_t wordv[CB];
+    uint32_t sv[CB], ev[CB], tv[CB];
 #pragma unroll
-      for (uint32_t r = 0; r < 4; r++) {
-        const uint32_t q = q0 + 64 * r + lane;
-        uint32_t lo = 0;  // first lane l with incl[l] > q (all lanes take part)
+    for (uint32_t i = 0; i < CB; i++) {
+      const uint32_t wt = w0 + FW * i;
+      const uint32_t pc = min(pos + min(wt, n64 - 1) * 64 + lane, m - 1);
+      wordv[i] = wt < t_hi ? a.sflag[wt] : 0ull;
+      sv[i] = a.in.off[pc];
+      ev[i] = a.in.off[pc + 1];
+      tv[i] = a.in.tid ? a.in.tid[pc] : pc;
+    }
 #pragma unroll
-        for (uint32_t st = 32; st > 0; st >>= 1) {
-          const uint32_t v = __shfl(incl, lo + st - 1);
-          if (v <= q) lo += st;
+    for (uint32_t i = 0; i < CB; i++) {
+      const uint32_t wt = w0 + FW * i;
+      const uint64_t word = wordv[i];
+      if (!word) continue;  // uniform
+      const uint64_t base = s_tb[wt - t_lo];
+      const uint32_t tb = (uint32_t)(base >> LB_ACC_BITS);
+      const uint32_t abase = (uint32_t)(base & ((1ull << LB_ACC_BITS) - 1));
+      const bool surv = (word >> lane) & 1ull;
+      uint32_t s = 0, len = 0;
+      if (surv) {
+        s = (uint32_t)min((uint64_t)sv[i], nnz);
+        len = (uint32_t)min((uint64_t)ev[i], nnz) - s;
+      }
+      uint32_t atot;
+      const uint32_t aex = wave_excl_u32(len, atot);
+      if (surv) {
+        const uint32_t r = tb + (uint32_t)__popcll(word & lanemask_lt());
+        a.tid_out[r] = tv[i];
+        a.off_out[r] = abase + aex;
+      }
+      // accesses: lanes over the wave's survivor accesses; output position q
+      // belongs to the first lane whose inclusive access prefix exceeds q
+      const uint32_t incl = aex + len;
+      for (uint32_t q0 = 0; q0 < atot; q0 += 64 * 4) {
+        uint32_t src[4];
+        bool in[4];
+#pragma unroll
+        for (uint32_t r = 0; r < 4; r++) {
+          const uint32_t q = q0 + 64 * r + lane;
+          uint32_t lo = 0;  // first lane l with incl[l] > q (all lanes take part)
+#pragma unroll
+          for (uint32_t st = 32; st > 0; st >>= 1) {
+            const uint32_t v = __shfl(incl, lo + st - 1);
+            if (v <= q) lo += st;
+          }
+          in[r] = q < atot;
+          src[r] = __shfl(s, lo) + (q - __shfl(aex, lo));
         }
-        in[r] = q < atot;
-        src[r] = __shfl(s, lo) + (q - __shfl(aex, lo));
-      }
-      uint64_t kk[4];
-      uint8_t aa[4];
+        uint64_t kk[4];
+        uint8_t aa[4];
 #pragma unroll
-      for (uint32_t r = 0; r < 4; r++) {
-        kk[r] = in[r] ? a.in.keys[src[r]] : 0ull;
-        aa[r] = in[r] ? a.in.acctype[src[r]] : (uint8_t)0;
-      }
+        for (uint32_t r = 0; r < 4; r++) {
+          kk[r] = in[r] ? a.in.keys[src[r]] : 0ull;
+          aa[r] = in[r] ? a.in.acctype[src[r]] : (uint8_t)0;
+        }
 #pragma unroll
-      for (uint32_t r = 0; r < 4; r++) {
-        if (!in[r]) continue;
-        const uint32_t q = q0 + 64 * r + lane;
-        a.keys_out[abase + q] = kk[r];
-        a.acc_out[abase + q] = aa[r];
+        for (uint32_t r = 0; r < 4; r++) {
+          if (!in[r]) continue;
+          const uint32_t q = q0 + 64 * r + lane;
+          a.keys_out[abase + q] = kk[r];
+          a.acc_out[abase + q] = aa[r];
+        }
       }
     }
+  }
+  if (dbg) {
+    __builtin_amdgcn_s_waitcnt(0);
+    dbg[4] = __builtin_amdgcn_s_memrealtime();
   }
 }
 
