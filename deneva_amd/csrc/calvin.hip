@@ -481,10 +481,20 @@ __global__ __launch_bounds__(256) void k_cv_down(const K* __restrict__ sk,
   // group of each request, straight to its place in request order (a random
   // 4-B scatter: measured no slower than partitioning by destination first
   // and placing window by window, profiles/r02/calvin_*)
+  // every request's txn offset first, all in flight together (a dependent
+  // random load per item inside the loop serialised 16 round trips)
+  uint32_t xo[CV_ITEMS];
+#pragma unroll
+  for (uint32_t i = 0; i < CV_ITEMS; i++) {
+    const uint32_t t = v[i] >> 7;
+    xo[i] = (p0 + i < m && t < o.n) ? o.off[t] : 0u;
+  }
   K pk = pk0;
   uint32_t pv = pv0;
   uint32_t last_gs = NOPOS, last_gnd = 0;
-  for (uint32_t i = 0; i < CV_ITEMS && p0 + i < m; i++) {
+#pragma unroll
+  for (uint32_t i = 0; i < CV_ITEMS; i++) {
+    if (p0 + i >= m) break;
     const uint64_t p = p0 + i;
     const Gs e = gs_element(p, k[i], v[i], pk, pv);
     const bool dup = !e.flag && e.ft == CV_NONE;
@@ -493,7 +503,7 @@ __global__ __launch_bounds__(256) void k_cv_down(const K* __restrict__ sk,
     pv = v[i];
     const uint32_t t = v[i] >> 7, j = (v[i] >> 1) & 63u;
     if (t >= o.n) continue;  // held-prefix request: part of the scan only (no waves)
-    const uint32_t x = o.off[t] + j;
+    const uint32_t x = xo[i] + j;
     if (dup) {
       o.group[x] = DCC_GROUP_NONE;
       if (o.pgx) {

@@ -186,10 +186,14 @@ __global__ __launch_bounds__(256) void k_mt_slots(const uint64_t* keys, uint64_t
   block_add(c, nrows);
 }
 
-// One thread per txn: owners, and the txn's lower bound from the row
-// timestamps copied at access time: gwts over rows read or written, grts over
-// rows written (Row_maat::read / prewrite, row_maat.cpp:115-117, 150-156;
-// Maat::validate raises lower past them, maat.cpp:46-49, 69-72).
+// The txn's lower bound from the row timestamps copied at access time: gwts
+// over rows read or written, grts over rows written (Row_maat::read /
+// prewrite, row_maat.cpp:115-117, 150-156; Maat::validate raises lower past
+// them, maat.cpp:46-49, 69-72).  A wave per 64 txns walks their contiguous
+// accesses 64 at a time (coalesced slot / type loads, four rounds in flight),
+// finds each access's txn in the wave's LDS offset prefix and folds the row
+// timestamps per txn with LDS atomicMax.  Each access's sort value packs its
+// txn and R / W bits, so the sorted groups need no gathers.
 struct BaseArgs {
   uint64_t n, nnz;
   const uint32_t* off;
@@ -198,7 +202,7 @@ struct BaseArgs {
   const uint64_t* rlr;
   const uint64_t* rlw;
   const uint32_t* slot;
-  uint32_t* owner;  // [nnz] txn of each access (pre-zeroed)
+  uint32_t* sval;   // [nnz] txn << 2 | R << 1 | W (pre-zeroed)
   uint64_t* base;   // [n]
   uint8_t* state;   // [n] zeroed here
   uint64_t* lacc;   // [n] 0
@@ -206,51 +210,92 @@ struct BaseArgs {
   uint32_t* pend;   // [n] 0
   uint32_t* err;
 };
+constexpr uint32_t SV_R = 2, SV_W = 1;
 __global__ __launch_bounds__(256) void k_mt_base(BaseArgs a) {
-  const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (t >= a.n) return;
-  const uint64_t o0 = min((uint64_t)a.off[t], a.nnz), o1 = min((uint64_t)a.off[t + 1], a.nnz);
-  if (a.off[t + 1] < a.off[t] || o1 - o0 > MAX_TXN_LEN) atomicOr(a.err, MT_ERR_OFF);
-  if ((t == 0 && a.off[0] != 0) || (t + 1 == a.n && a.off[a.n] != a.nnz)) atomicOr(a.err, MT_ERR_OFF);
-  uint64_t gw = 0, gr = 0;
-  for (uint64_t x = o0; x < o1; x++) {
-    const uint32_t s = a.slot[x];
-    a.owner[x] = (uint32_t)t;
-    const uint8_t ty = a.at[x];
-    const bool rd = a.rw_all || ty == DCC_RD, wr = a.rw_all || ty == DCC_WR;
-    if (rd || wr) gw = max(gw, a.rlw[s]);
-    if (wr) gr = max(gr, a.rlr[s]);
+  __shared__ uint32_t s_o[4][65];
+  __shared__ unsigned long long s_gw[4][64], s_gr[4][64];
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t t0 = ((uint64_t)blockIdx.x * 4 + w) * 64;
+  if (t0 >= a.n) return;
+  const uint32_t nt = (uint32_t)min<uint64_t>(64, a.n - t0);
+  const uint64_t t = t0 + lane;
+  if (lane < nt) {
+    const uint32_t o0 = a.off[t], o1 = a.off[t + 1];
+    if (o1 < o0 || o1 - o0 > MAX_TXN_LEN) atomicOr(a.err, MT_ERR_OFF);
+    if ((t == 0 && o0 != 0) || (t + 1 == a.n && o1 != a.nnz)) atomicOr(a.err, MT_ERR_OFF);
   }
-  a.base[t] = max(gw, gr) + 1;
-  a.state[t] = ST_UND;
-  a.lacc[t] = 0;
-  a.uacc[t] = U64MAX;
-  a.pend[t] = 0;
-}
-
-__global__ __launch_bounds__(256) void k_mt_iota(uint32_t* v, uint64_t m) {
-  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < m; i += (uint64_t)gridDim.x * 256)
-    v[i] = (uint32_t)i;
+  // clamped, made monotone: a malformed batch is reported, never overrun
+  uint32_t ov = lane <= nt ? (uint32_t)min<uint64_t>(a.off[t0 + lane], a.nnz) : 0u;
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(ov, d);
+    if (lane >= (uint32_t)d && lane <= nt) ov = max(ov, y);
+  }
+  s_o[w][lane] = ov;
+  if (lane == 0) s_o[w][64] = 0;
+  s_gw[w][lane] = 0;
+  s_gr[w][lane] = 0;
+  __builtin_amdgcn_wave_barrier();
+  if (nt == 64 && lane == 0)
+    s_o[w][64] = max(s_o[w][63], (uint32_t)min<uint64_t>(a.off[t0 + 64], a.nnz));
+  __builtin_amdgcn_wave_barrier();
+  const uint32_t a0 = s_o[w][0], a1 = s_o[w][nt];
+  for (uint32_t x0 = a0; x0 < a1; x0 += 4 * 64) {
+    uint32_t sl[4];
+    uint8_t ty[4];
+#pragma unroll
+    for (uint32_t u = 0; u < 4; u++) {
+      const uint32_t x = min(x0 + 64 * u + lane, a1 - 1);
+      sl[u] = a.slot[x];
+      ty[u] = a.at[x];
+    }
+    uint64_t lw[4], lr[4];
+#pragma unroll
+    for (uint32_t u = 0; u < 4; u++) {
+      lw[u] = a.rlw[sl[u]];
+      lr[u] = a.rlr[sl[u]];
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < 4; u++) {
+      const uint32_t x = x0 + 64 * u + lane;
+      if (x >= a1) continue;
+      uint32_t lo = 0, hi = nt;  // largest k < nt with s_o[k] <= x
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (s_o[w][mid] <= x) lo = mid;
+        else hi = mid;
+      }
+      const bool rd = a.rw_all || ty[u] == DCC_RD, wr = a.rw_all || ty[u] == DCC_WR;
+      if (rd || wr) atomicMax(&s_gw[w][lo], (unsigned long long)lw[u]);
+      if (wr) atomicMax(&s_gr[w][lo], (unsigned long long)lr[u]);
+      a.sval[x] = ((uint32_t)(t0 + lo) << 2) | (rd ? SV_R : 0u) | (wr ? SV_W : 0u);
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (lane < nt) {
+    a.base[t] = max(s_gw[w][lane], s_gr[w][lane]) + 1;
+    a.state[t] = ST_UND;
+    a.lacc[t] = 0;
+    a.uacc[t] = U64MAX;
+    a.pend[t] = 0;
+  }
 }
 
 // Group flags per sorted position: a (row, txn) group is a run of equal
-// (slot, owner); its last position carries the OR of its R / W bits.
+// (slot, txn); its last position carries the OR of its R / W bits.
 __global__ __launch_bounds__(256) void k_mt_groups(const uint32_t* ss, const uint32_t* sv,
-                                                   const uint32_t* owner, const uint8_t* at,
-                                                   uint32_t rw_all, uint64_t m, uint8_t* sfl,
-                                                   uint32_t* stx) {
+                                                   uint64_t m, uint8_t* sfl, uint32_t* stx) {
   for (uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x; p < m; p += (uint64_t)gridDim.x * 256) {
-    const uint32_t s = ss[p], t = owner[sv[p]];
+    const uint32_t s = ss[p], v = sv[p], t = v >> 2;
     uint8_t f = 0;
     if (p == 0 || ss[p - 1] != s) f |= F_START;
-    const bool last = p + 1 == m || ss[p + 1] != s || owner[sv[p + 1]] != t;
+    const bool last = p + 1 == m || ss[p + 1] != s || (sv[p + 1] >> 2) != t;
     if (last) {
       f |= F_LAST;
       for (uint64_t q = p;; q--) {  // the group's accesses (<= MAX_ROW_PER_TXN)
-        const uint8_t ty = at[sv[q]];
-        if (rw_all || ty == DCC_RD) f |= F_R;
-        if (rw_all || ty == DCC_WR) f |= F_W;
-        if (q == 0 || ss[q - 1] != s || owner[sv[q - 1]] != t) break;
+        const uint32_t vq = sv[q];
+        if (vq & SV_R) f |= F_R;
+        if (vq & SV_W) f |= F_W;
+        if (q == 0 || ss[q - 1] != s || (sv[q - 1] >> 2) != t) break;
       }
     }
     sfl[p] = f;
@@ -640,7 +685,6 @@ int dcc_ctx::maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, 
   CR(mt_sval.ensure(this, mm * 4, "maat sort values"));
   CR(mt_slot2.ensure(this, mm * 4, "maat slots b"));
   CR(mt_sval2.ensure(this, mm * 4, "maat sort values b"));
-  CR(mt_owner.ensure(this, mm * 4, "maat owners"));
   CR(mt_sfl.ensure(this, mm, "maat flags"));
   CR(mt_sflB.ensure(this, mm, "maat flags b"));
   CR(mt_stxB.ensure(this, mm * 4, "maat sorted txns b"));
@@ -672,14 +716,13 @@ int dcc_ctx::maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, 
   CK(hipEventRecord(ev0, stream));
   // every access gets a slot / owner / sort value even in a malformed batch
   CK(hipMemsetAsync(mt_slot.p, 0, mm * 4, stream));
-  CK(hipMemsetAsync(mt_owner.p, 0, mm * 4, stream));
-  k_mt_iota<<<g1(mm), 256, 0, stream>>>((uint32_t*)mt_sval.p, m);
+  CK(hipMemsetAsync(mt_sval.p, 0, mm * 4, stream));
   k_mt_slots<<<g1(mm, 16384), 256, 0, stream>>>(d.keys, m, (uint64_t*)mt_rk.p, mt_bits,
                                                  (uint32_t*)mt_slot.p, cnt, cnt + 1);
   BaseArgs ba{n,     m,     d.off, d.acctype, rw_all, (const uint64_t*)mt_rlr.p,
-              (const uint64_t*)mt_rlw.p, (const uint32_t*)mt_slot.p, (uint32_t*)mt_owner.p,
+              (const uint64_t*)mt_rlw.p, (const uint32_t*)mt_slot.p, (uint32_t*)mt_sval.p,
               base,  state, lacc,  uacc,      pend,   cnt + 1};
-  k_mt_base<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(ba);
+  k_mt_base<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(ba);  // a wave per 64 txns
   // rows sorted by slot (stable: index order within a row); the sorted slots
   // and the other key buffer become the two slot arrays of the compaction
   uint8_t* sflb[2] = {(uint8_t*)mt_sfl.p, (uint8_t*)mt_sflB.p};
@@ -692,8 +735,7 @@ int dcc_ctx::maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, 
     const int cur = radix_sort_u32(kk, vb, m, mt_bits, (uint32_t*)cv_scratch.p, stream);
     ssb[0] = kk[cur];
     ssb[1] = kk[cur ^ 1];
-    k_mt_groups<<<g1(m), 256, 0, stream>>>(ssb[0], vb[cur], (const uint32_t*)mt_owner.p, d.acctype,
-                                           rw_all, m, sflb[0], stxb[0]);
+    k_mt_groups<<<g1(m), 256, 0, stream>>>(ssb[0], vb[cur], m, sflb[0], stxb[0]);
   }
   CK(hipGetLastError());
 

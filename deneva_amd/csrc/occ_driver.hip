@@ -721,8 +721,9 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   if (sweep) {
     // prep results: the batch is rejected exactly as device_prep would
     const PrepPart* pp = (const PrepPart*)((const char*)hpart + SW_PREP_OFF);
+    static_assert(SW_PREP_OFF + SW_PREP_BLOCKS * sizeof(PrepPart) <= (1u << 16), "hpart holds them");
     uint32_t perr = 0;
-    for (unsigned q = 0; q < PREP_BLOCKS; q++) {
+    for (unsigned q = 0; q < SW_PREP_BLOCKS; q++) {
       perr |= pp[q].err;
       maxlen = std::max(maxlen, pp[q].maxlen);
       nnz_w += pp[q].nw;

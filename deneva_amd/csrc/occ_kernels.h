@@ -31,6 +31,7 @@ constexpr uint32_t ERR_UNDECIDED = 16;
 constexpr uint32_t ERR_SPIN = 128;  // sweep filter: look-back spin limit reached
 
 constexpr unsigned PREP_BLOCKS = 512;
+constexpr unsigned SW_PREP_BLOCKS = 2048;  // the sweep's prep (inside the fill launch)
 constexpr unsigned FINAL_BLOCKS = 512;
 struct PrepPart {
   uint32_t err, maxlen, nw, nw_prefix;

@@ -769,17 +769,37 @@ __global__ __launch_bounds__(256) void k_final(FinalArgs a, GatherArgs g) {
       const CopyJob& cj = g.job[q];
       for (uint32_t i = threadIdx.x; i < cj.words; i += blockDim.x) cj.dst[i] = cj.src[i];
     }
-  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < a.n;
-       t += (uint64_t)gridDim.x * blockDim.x) {
-    const uint8_t st = a.state[t];
-    const bool w = a.hasw[t] != 0;
+  auto one = [&](uint8_t st, bool w) -> uint32_t {  // counts; returns the commit flag
     c += st == ST_COMMIT;
     ab += st >= ST_ABORT;
     und += st == ST_UNDECIDED;
     ro += w ? 0u : 1u;
-    cw += (st == ST_COMMIT && w) ? 1u : 0u;
+    const uint32_t f = (st == ST_COMMIT && w) ? 1u : 0u;
+    cw += f;
+    return f;
+  };
+  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  // four txns per thread and step (word loads / stores) when the output is
+  // word-aligned (state / has-write / flags are the engine's own buffers)
+  const uint64_t n4 = ((uintptr_t)a.rc & 3u) == 0 ? a.n / 4 : 0;
+  for (uint64_t q = tid; q < n4; q += stride) {
+    const uint32_t s4 = ((const uint32_t*)a.state)[q], h4 = ((const uint32_t*)a.hasw)[q];
+    uint32_t r4 = 0, fl[4];
+#pragma unroll
+    for (uint32_t b = 0; b < 4; b++) {
+      const uint8_t st = (uint8_t)(s4 >> (8 * b));
+      fl[b] = one(st, ((h4 >> (8 * b)) & 0xFFu) != 0);
+      r4 |= (st == ST_COMMIT ? 0u /* RCOK */ : 2u /* Abort */) << (8 * b);
+    }
+    ((uint32_t*)a.rc)[q] = r4;
+    if (a.cflag) ((uint4*)a.cflag)[q] = make_uint4(fl[0], fl[1], fl[2], fl[3]);
+  }
+  for (uint64_t t = 4 * n4 + tid; t < a.n; t += stride) {
+    const uint8_t st = a.state[t];
+    const uint32_t f = one(st, a.hasw[t] != 0);
     a.rc[t] = st == ST_COMMIT ? 0 /* RCOK */ : 2 /* Abort */;
-    if (a.cflag) a.cflag[t] = (st == ST_COMMIT && w) ? 1u : 0u;
+    if (a.cflag) a.cflag[t] = f;
   }
   const uint32_t s0 = block_sum_u32(c, sh), s1 = block_sum_u32(ab, sh),
                  s2 = block_sum_u32(ro, sh), s3 = block_sum_u32(cw, sh),
@@ -893,7 +913,7 @@ void launch_fill(const FillArgs& a, hipStream_t st) {
   const unsigned grid = (unsigned)std::min<uint64_t>((mx + 255) / 256, 2048);
   k_fill<<<grid, 256, 0, st>>>(a);
 }
-// the epoch's fills and k_prep's pass in one launch: workgroups < PREP_BLOCKS
+// the epoch's fills and k_prep's pass in one launch: workgroups < SW_PREP_BLOCKS
 // also run prep (partials straight to the host-visible `part`)
 __global__ __launch_bounds__(256) void k_fill_prep(FillArgs a, const uint32_t* __restrict__ off,
                                                    uint64_t n, const uint8_t* __restrict__ at,
@@ -903,14 +923,14 @@ __global__ __launch_bounds__(256) void k_fill_prep(FillArgs a, const uint32_t* _
     const FillJob& f = a.job[q];
     for (uint64_t i = t; i < f.words; i += stride) f.p[i] = f.value;
   }
-  if (blockIdx.x < PREP_BLOCKS) prep_body(off, n, at, nnz, 0, part, blockIdx.x, PREP_BLOCKS);
+  if (blockIdx.x < SW_PREP_BLOCKS) prep_body(off, n, at, nnz, 0, part, blockIdx.x, SW_PREP_BLOCKS);
 }
 void launch_fill_prep(const FillArgs& a, const uint32_t* off, uint64_t n, const uint8_t* at,
                       uint64_t nnz, PrepPart* part, hipStream_t st) {
   uint64_t mx = 1;
   for (uint32_t q = 0; q < a.n; q++) mx = a.job[q].words > mx ? a.job[q].words : mx;
   const unsigned grid = (unsigned)std::max<uint64_t>(std::min<uint64_t>((mx + 255) / 256, 2048),
-                                                     PREP_BLOCKS);
+                                                     SW_PREP_BLOCKS);
   k_fill_prep<<<grid, 256, 0, st>>>(a, off, n, at, nnz, part);
 }
 
