@@ -623,7 +623,8 @@ __global__ __launch_bounds__(256) void k_sw_rows(SwPreArgs a) {
 // memory into an LDS ring ahead of it (one tile per wave in flight; ready and
 // consumed counters in LDS), then all 16 join for the write-out.
 constexpr uint32_t SEQ_RING = 12;  // LDS record slots (73,728 B)
-constexpr uint32_t SEQ_PROD = 15;  // producer waves
+constexpr uint32_t SEQ_B = 1024;   // threads of the serial pass's workgroup
+constexpr uint32_t SEQ_PROD = SEQ_B / 64 - 1;  // producer waves
 constexpr uint32_t SEQ_V4 = sizeof(SwRec) / 16;  // uint4 per record
 static_assert(SW_RC * 64 <= SW_IL, "register chunks inside the record");
 static_assert(sizeof(SwRec) % (16 * 64) == 0, "record copy: whole uint4 per lane");
@@ -665,7 +666,7 @@ __device__ inline bool seg_any(uint64_t hm, uint32_t ps, uint32_t pe, uint32_t q
   return ((hm >> (lo - q0)) & msk) != 0;
 }
 
-__global__ __launch_bounds__(1024) void k_sw_seq(SwSeqArgs a) {
+__global__ __launch_bounds__(SEQ_B) void k_sw_seq(SwSeqArgs a) {
   // one block, the committed bitmap first: its word addresses are the list
   // entries' shifted fields with no base to add
   struct Lds {
@@ -701,7 +702,7 @@ __global__ __launch_bounds__(1024) void k_sw_seq(SwSeqArgs a) {
   uint64_t* dbg = a.dbg;
   if (dbg && j == 0) dbg[0] = __builtin_amdgcn_s_memrealtime();
   const uint32_t nwords = (1u << a.gbits) / 32;
-  for (uint32_t q = j; q < nwords; q += 1024) cbits[q] = 0;
+  for (uint32_t q = j; q < nwords; q += SEQ_B) cbits[q] = 0;
   if (j == 0) cbits[SW_ID_NONE / 32] = 0;  // the word padding probes read
   __syncthreads();
 
@@ -867,7 +868,7 @@ __global__ __launch_bounds__(1024) void k_sw_seq(SwSeqArgs a) {
   __syncthreads();
   const uint32_t k = s_k;
   // ---- write-out: decisions of tiles [0, k), the level's committed keys
-  for (uint32_t q = j; q < k * SW_T; q += 1024) {
+  for (uint32_t q = j; q < k * SW_T; q += SEQ_B) {
     const uint32_t kk = q / SW_T, t = q % SW_T;
     const uint32_t mt = a.rec[kk].meta[t];
     if (!(mt & SWM_VALID)) continue;
@@ -881,9 +882,9 @@ __global__ __launch_bounds__(1024) void k_sw_seq(SwSeqArgs a) {
   }
   // C for the filter is listed by k_sw_cout from the committed masks: clear
   // its bitmap, Bloom filter and count here
-  for (uint32_t q = j; q < k; q += 1024) a.mg[q] = s_M[q];
-  for (uint32_t q = j; q < nwords; q += 1024) a.cbits_out[q] = 0;
-  for (uint32_t q = j; q < (1u << SW_BLOOM_LOG) / 32; q += 1024) a.bloom_out[q] = 0;
+  for (uint32_t q = j; q < k; q += SEQ_B) a.mg[q] = s_M[q];
+  for (uint32_t q = j; q < nwords; q += SEQ_B) a.cbits_out[q] = 0;
+  for (uint32_t q = j; q < (1u << SW_BLOOM_LOG) / 32; q += SEQ_B) a.bloom_out[q] = 0;
   if (j == 0) {
     a.lv->pos = min(k * SW_T, lim);
     a.lv->ccount = 0;  // k_sw_cout's fill counter
@@ -1585,7 +1586,7 @@ __global__ __launch_bounds__(SW_CHUNK) void k_sw_compact(SwFilterArgs a) {
 void launch_sw_pre(const SwPreArgs& a, unsigned grid, hipStream_t st) {
   k_sw_pre<<<grid ? grid : 1u, PRE_B, 0, st>>>(a);
 }
-void launch_sw_seq(const SwSeqArgs& a, hipStream_t st) { k_sw_seq<<<1, 1024, 0, st>>>(a); }
+void launch_sw_seq(const SwSeqArgs& a, hipStream_t st) { k_sw_seq<<<1, SEQ_B, 0, st>>>(a); }
 void launch_sw_rows(const SwPreArgs& a, unsigned grid, hipStream_t st) {
   k_sw_rows<<<grid ? grid : 1u, 256, 0, st>>>(a);  // one workgroup per tile
 }
