@@ -52,6 +52,7 @@ struct HistStore {
   bool mono = true;         // append order is tn order within every key
   uint64_t max_tn = 0;      // largest tn appended
   uint64_t min_tn = ~0ull;  // smallest tn appended
+  uint64_t max_key = 0;     // largest key appended (radix passes of the build)
 };
 
 // One OCC (sub-)batch: txn i has accesses [off[i], off[i+1]) of keys/acctype

@@ -310,7 +310,9 @@ int dcc_ctx::hist_build(HistStore& h) {
               (uint64_t*)h.skey.p,
               (uint64_t*)h.stn.p,
               (uint64_t*)h.hash.p,
-              h.hbits};
+              h.hbits,
+              h.max_key ? 64u - (uint32_t)__builtin_clzll(h.max_key) : 1u,
+              64u - (uint32_t)__builtin_clzll(h.max_tn | 1ull)};
   if (hist_build_level(b, stream)) CK(hipGetLastError());
   h.built = true;
   return DCC_OK;
@@ -331,6 +333,7 @@ int dcc_ctx::hist_prepare() {
     B.m += D.m;
     B.max_tn = std::max(B.max_tn, D.max_tn);
     B.min_tn = std::min(B.min_tn, D.min_tn);
+    B.max_key = std::max(B.max_key, D.max_key);
     B.built = false;
     D = HistStore{D.fk, D.ft, D.skey, D.stn, D.hash};  // buffers kept, level emptied
   }
@@ -358,17 +361,21 @@ int dcc_ctx::hist_append_epoch(const DevBatch& d, const uint64_t* tn_dev, uint64
   HistStore& D = hs[1];
   CR(hist_grow_flat(D, D.m + nnz_w));
   const uint64_t nb = (d.n + 1023) / 1024;
-  CR(h_bsum.ensure(this, (nb + 1) * 4 + 64, "history append scan"));
+  CR(h_bsum.ensure(this, (nb + 1) * 4 + 96, "history append scan"));
   uint32_t* bsum = (uint32_t*)h_bsum.p;
-  uint32_t* total = bsum + nb + 1;
+  // the total and the largest key appended share one read-back (16 B)
+  uint32_t* total = bsum + ((nb + 1 + 3) & ~3ull);
+  unsigned long long* kmax = (unsigned long long*)(total + 2);
+  CK(hipMemsetAsync(total, 0, 16, stream));
   launch_hist_count(d.n, d.off, d.acctype, d.nnz, tn_dev, bsum, stream);
   rs_scan_one(bsum, (uint32_t)nb, total, stream);
   launch_hist_emit(d.n, d.off, d.keys, d.acctype, d.nnz, tn_dev, bsum, (uint64_t*)D.fk.p + D.m,
-                   (uint64_t*)D.ft.p + D.m, stream);
+                   (uint64_t*)D.ft.p + D.m, kmax, stream);
   CK(hipGetLastError());
-  CK(hipMemcpyAsync(hmisc, total, 4, hipMemcpyDeviceToHost, stream));
+  CK(hipMemcpyAsync(hmisc, total, 16, hipMemcpyDeviceToHost, stream));
   CK(hipStreamSynchronize(stream));
   const uint32_t added = *(const uint32_t*)hmisc;
+  D.max_key = std::max<uint64_t>(D.max_key, *(const uint64_t*)((const char*)hmisc + 8));
   if (added > nnz_w) return fail(DCC_EIO, "history append: %u writes > %llu", added,
                                  (unsigned long long)nnz_w);
   D.m += added;
@@ -409,6 +416,7 @@ extern "C" int dcc_occ_history_append(dcc_ctx* ctx, const uint64_t* keys, const 
   CK(hipMemcpy((uint64_t*)D.ft.p + D.m, t2.data(), n * 8, hipMemcpyHostToDevice));
   D.m += n;
   ctx->hist_note(D, t2.front(), t2.back());
+  D.max_key = std::max(D.max_key, *std::max_element(k2.begin(), k2.end()));
   return DCC_OK;
 }
 
@@ -420,6 +428,7 @@ extern "C" int dcc_occ_history_clear(dcc_ctx* ctx) {
     h.m = 0;
     h.max_tn = 0;
     h.min_tn = ~0ull;
+    h.max_key = 0;
     h.mono = true;
     h.built = true;
   }
@@ -459,6 +468,8 @@ extern "C" int dcc_occ_history_trim(dcc_ctx* ctx, uint64_t tn_floor) {
   N.ft = DevBuf{};
   B.m = kept;
   B.max_tn = mx;
+  B.max_key = std::max(B.max_key, D.max_key);
+  D.max_key = 0;
   B.mono = false;  // the compaction does not keep the order
   B.built = false;
   D.m = 0;

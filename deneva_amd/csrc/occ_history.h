@@ -66,9 +66,10 @@ __device__ inline bool hist_hit(const HistView& h, uint64_t key, uint64_t lo, ui
 void launch_hist_count(uint64_t n, const uint32_t* off, const uint8_t* acctype, uint64_t nnz,
                        const uint64_t* tn, uint32_t* bsum, hipStream_t st);
 // pairs of block b's committed writes at out + bsum[b] (scanned) + block rank
+// (*kmax raised to the largest key emitted)
 void launch_hist_emit(uint64_t n, const uint32_t* off, const uint64_t* keys, const uint8_t* acctype,
                       uint64_t nnz, const uint64_t* tn, const uint32_t* bsum, uint64_t* out_k,
-                      uint64_t* out_t, hipStream_t st);
+                      uint64_t* out_t, unsigned long long* kmax, hipStream_t st);
 // level build from flat pairs (fk, ft)[m]; K/V are radix-sort ping-pong buffers
 struct HistBuild {
   uint64_t m;
@@ -82,6 +83,7 @@ struct HistBuild {
   uint64_t* stn;        // out: sorted tns
   uint64_t* hash;       // out: [2 << hbits]
   uint32_t hbits;
+  uint32_t kbits, tbits;  // significant bits of the keys / tns (radix passes)
 };
 int hist_build_level(const HistBuild& b, hipStream_t st);
 // pairs with tn > floor of (ak, at)[na] then (bk, bt)[nb], appended at

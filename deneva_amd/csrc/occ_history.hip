@@ -68,21 +68,32 @@ __global__ __launch_bounds__(HB) void k_hist_emit(uint64_t n, const uint32_t* of
                                                   const uint64_t* keys, const uint8_t* acctype,
                                                   uint64_t nnz, const uint64_t* tn,
                                                   const uint32_t* bsum, uint64_t* out_k,
-                                                  uint64_t* out_t) {
+                                                  uint64_t* out_t, unsigned long long* kmax) {
+  __shared__ unsigned long long s_mx;
   const uint64_t t = (uint64_t)blockIdx.x * HB + threadIdx.x;
   uint32_t a0 = 0;
   const uint32_t c = t < n ? hist_writes_of(t, off, acctype, nnz, tn, a0) : 0u;
   uint32_t ex;
   (void)block_excl_scan1024(c, ex);
-  if (!c) return;
-  uint64_t p = (uint64_t)bsum[blockIdx.x] + ex;
-  const uint64_t my_tn = tn[t];
-  for (uint64_t x = a0; p < (uint64_t)bsum[blockIdx.x] + ex + c; x++) {
-    if (acctype[x] != DCC_WR) continue;
-    out_k[p] = keys[x];
-    out_t[p] = my_tn;
-    p++;
+  if (threadIdx.x == 0) s_mx = 0;
+  __syncthreads();
+  uint64_t mx = 0;
+  if (c) {
+    uint64_t p = (uint64_t)bsum[blockIdx.x] + ex;
+    const uint64_t my_tn = tn[t];
+    for (uint64_t x = a0; p < (uint64_t)bsum[blockIdx.x] + ex + c; x++) {
+      if (acctype[x] != DCC_WR) continue;
+      const uint64_t k = keys[x];
+      out_k[p] = k;
+      out_t[p] = my_tn;
+      mx = max(mx, k);
+      p++;
+    }
   }
+  for (int d = 32; d > 0; d >>= 1) mx = max(mx, (uint64_t)__shfl_xor(mx, d));
+  if ((threadIdx.x & 63) == 0 && mx) atomicMax(&s_mx, (unsigned long long)mx);
+  __syncthreads();
+  if (threadIdx.x == 0 && s_mx) atomicMax(kmax, s_mx);  // one per workgroup
 }
 
 void launch_hist_count(uint64_t n, const uint32_t* off, const uint8_t* acctype, uint64_t nnz,
@@ -92,9 +103,9 @@ void launch_hist_count(uint64_t n, const uint32_t* off, const uint8_t* acctype, 
 }
 void launch_hist_emit(uint64_t n, const uint32_t* off, const uint64_t* keys, const uint8_t* acctype,
                       uint64_t nnz, const uint64_t* tn, const uint32_t* bsum, uint64_t* out_k,
-                      uint64_t* out_t, hipStream_t st) {
+                      uint64_t* out_t, unsigned long long* kmax, hipStream_t st) {
   const unsigned g = (unsigned)((n + HB - 1) / HB);
-  k_hist_emit<<<g ? g : 1, HB, 0, st>>>(n, off, keys, acctype, nnz, tn, bsum, out_k, out_t);
+  k_hist_emit<<<g ? g : 1, HB, 0, st>>>(n, off, keys, acctype, nnz, tn, bsum, out_k, out_t, kmax);
 }
 
 // ---------------------------------------------------------------- level build
@@ -167,15 +178,15 @@ int hist_build_level(const HistBuild& b, hipStream_t st) {
   if (b.mono) {
     // append order is tn order within every key: one stable sort by key
     k_hist_init<<<hgrid(b.m), 256, 0, st>>>(b.fk, b.m, K[0], V[0]);
-    r = radix_sort_u64(K, V, b.m, 64, b.scratch, st);
+    r = radix_sort_u64(K, V, b.m, b.kbits, b.scratch, st);
   } else {
     // LSD over (key, tn): by tn, then stably by key
     k_hist_init<<<hgrid(b.m), 256, 0, st>>>(b.ft, b.m, K[0], V[0]);
-    const int r1 = radix_sort_u64(K, V, b.m, 64, b.scratch, st);
+    const int r1 = radix_sort_u64(K, V, b.m, b.tbits, b.scratch, st);
     k_hist_regather<<<hgrid(b.m), 256, 0, st>>>(b.fk, V[r1], b.m, K[r1 ^ 1], V[r1 ^ 1]);
     uint64_t* K2[2] = {K[r1 ^ 1], K[r1]};
     uint32_t* V2[2] = {V[r1 ^ 1], V[r1]};
-    const int r2 = radix_sort_u64(K2, V2, b.m, 64, b.scratch, st);
+    const int r2 = radix_sort_u64(K2, V2, b.m, b.kbits, b.scratch, st);
     K[0] = K2[r2];
     V[0] = V2[r2];
     r = 0;

@@ -824,13 +824,30 @@ __global__ __launch_bounds__(1024) void k_scan_blocks(const uint32_t* __restrict
   }
 }
 
-__global__ __launch_bounds__(64) void k_scan_sums(uint64_t* __restrict__ bsum, uint64_t nb) {
-  if (threadIdx.x != 0) return;
-  uint64_t run = 0;
-  for (uint64_t b = 0; b < nb; b++) {
-    const uint64_t v = bsum[b];
-    bsum[b] = run;
-    run += v;
+// exclusive scan of the block sums in place: one workgroup, 1024 sums per
+// step (a serial loop over 256+ sums took 30 us)
+__global__ __launch_bounds__(1024) void k_scan_sums(uint64_t* __restrict__ bsum, uint64_t nb) {
+  __shared__ uint64_t s_w[16];
+  __shared__ uint64_t s_carry;
+  const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+  if (threadIdx.x == 0) s_carry = 0;
+  __syncthreads();
+  for (uint64_t c0 = 0; c0 < nb; c0 += 1024) {
+    const uint64_t q = c0 + threadIdx.x;
+    const uint64_t v = q < nb ? bsum[q] : 0ull;
+    uint64_t x = v;
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint64_t y = __shfl_up(x, d);
+      if (lane >= (uint32_t)d) x += y;
+    }
+    if (lane == 63) s_w[wv] = x;
+    __syncthreads();
+    uint64_t base = s_carry;
+    for (uint32_t w = 0; w < wv; w++) base += s_w[w];
+    if (q < nb) bsum[q] = base + x - v;
+    __syncthreads();
+    if (threadIdx.x == 1023) s_carry = base + x;
+    __syncthreads();
   }
 }
 
@@ -950,7 +967,7 @@ void launch_commit_tn(const uint32_t* cflag, uint64_t n, uint64_t* bsum, uint64_
                       uint64_t* tn, hipStream_t st) {
   const unsigned nb = grid_for(n, 1024);
   k_scan_blocks<<<nb, 1024, 0, st>>>(cflag, n, bsum);
-  k_scan_sums<<<1, 64, 0, st>>>(bsum, nb);
+  k_scan_sums<<<1, 1024, 0, st>>>(bsum, nb);
   k_scan_apply<<<nb, 1024, 0, st>>>(cflag, n, bsum, tnc, tn);
 }
 
