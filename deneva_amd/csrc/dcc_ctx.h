@@ -178,7 +178,10 @@ struct dcc_ctx {
   int occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dcc_stats* st);
   int occ_rounds(const SubProb& sp, uint32_t maxlen, bool prof, uint32_t& rounds);
   int sweep_reserve(const DevBatch& d);
-  int sweep_enqueue(const DevBatch& d, int l0, int l1, const dcc::SwShard* shard = nullptr);
+  // levels [l0, l1); resume: level l0's serial part already ran (start at its
+  // committed-set listing); tail_serial: level l1 - 1 runs its serial part only
+  int sweep_enqueue(const DevBatch& d, int l0, int l1, const dcc::SwShard* shard = nullptr,
+                    bool resume = false, bool tail_serial = false);
   int sweep_sharded(const DevBatch& d, int& next_level);
   int occ_sweep_finish(const DevBatch& d, int& next_level, bool& done, uint32_t maxlen);
   int occ_snapshot(const dcc_batch* b, const dcc_occ_snapshot* s, uint8_t* out_rc, dcc_stats* st);

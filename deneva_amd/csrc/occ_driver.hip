@@ -343,7 +343,8 @@ int dcc_ctx::sweep_reserve(const DevBatch& d) {
 
 // Enqueue levels [l0, l1) (list l0 must exist: the epoch, or written by the
 // filter of level l0 - 1).
-int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1, const SwShard* shl) {
+int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1, const SwShard* shl, bool resume,
+                           bool tail_serial) {
   dcc_ctx* ctx = this;
   SwLevel* ctl = (SwLevel*)sw_ctl.p;
   uint32_t* abandon = (uint32_t*)(ctl + SW_MAX_LEVEL + 1);
@@ -388,15 +389,22 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1, const SwShard* shl
                  gtab0 + (size_t)(l & 1) * (1ull << SW_GBITS_MAX), sw_gbits(l),
                  sw_budget(l), fw, la, aent, apos, abandon, err, nullptr};
     if (sw_debug && l < 4) pa.dbg = (uint64_t*)sw_dbg.p + 4096 + 4 * 256 * 8 + (size_t)l * 64 * 8;
-    launch_sw_pre(pa, (unsigned)tiles, stream);
-    launch_sw_rows(pa, (unsigned)tiles, stream);
+    const bool serial_part = !(resume && l == l0);
+    if (serial_part) {
+      launch_sw_pre(pa, (unsigned)tiles, stream);
+      launch_sw_rows(pa, (unsigned)tiles, stream);
+    }
     SwSeqArgs sa{smdev, sm_host, pmax, top ? 1 : 0, (const SwRec*)sw_rec.p, (const uint32_t*)sw_rk.p,
                  gtab0 + (size_t)(l & 1) * (1ull << SW_GBITS_MAX), sw_gbits(l),
                  (uint8_t*)state.p, (uint8_t*)hasw.p,
                  cbits_d, ckeys_d, bloom_d, lv, lv + 1, (uint32_t*)out.off.p, (uint64_t*)sw_mg.p,
                  abandon, err, nullptr};
     if (sw_debug && l < 4) sa.dbg = (uint64_t*)sw_dbg.p + (size_t)l * 1024;
-    launch_sw_seq(sa, stream);
+    if (serial_part) launch_sw_seq(sa, stream);
+    // the last level of a graph-captured epoch usually decides its whole list
+    // serially: its listing, filter and compaction are enqueued only when the
+    // host finds list txns past the serial range (occ_epoch)
+    if (tail_serial && l == l1 - 1) break;
     SwCoutArgs ca{sin,     aent,    apos,    (const uint64_t*)sw_mg.p, lv, cbits_d, ckeys_d,
                   bloom_d, abandon, smdev, sm_host, shl ? 0 : 1};
     launch_sw_cout(ca, (unsigned)std::min<uint64_t>((pa.budget + 1023) / 1024, 4ull * n_cu), stream);
@@ -655,11 +663,13 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   bars_used = false;
   PeelInfo info;
   int next_level = 0;
+  int serial_tail = -1;  // level enqueued without its filter (sweep_enqueue tail_serial)
   if (sweep) {
     if (profiling) CK(hipEventRecord(pev[0], stream));
     next_level = (int)std::min<uint32_t>(sw_levels, SW_MAX_LEVEL - 1);
+    if (!sh && next_level >= 2) serial_tail = next_level - 1;
     if (sh) CR(sweep_sharded(d, next_level));
-    else if (!replay) CR(sweep_enqueue(d, 0, next_level));
+    else if (!replay) CR(sweep_enqueue(d, 0, next_level, nullptr, false, serial_tail >= 0));
   } else {
     CR(occ_rounds(top, maxlen, profiling, rounds));
   }
@@ -739,6 +749,28 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
       const uint32_t ab = *(const uint32_t*)(hc + SW_MAX_LEVEL + 1);
       const uint32_t e = *(const uint32_t*)hmisc;
       if (e & (ERR_SPIN | ERR_TILE | ERR_FULL)) break;  // reported below
+      if (serial_tail >= 0) {
+        // the serial-only last level left list txns past its serial range:
+        // its committed-set listing, filter and compaction, then more levels
+        const SwLevel& t = hc[serial_tail];
+        const int lt = serial_tail;
+        serial_tail = -1;
+        if (!ab && t.m > 0 && t.pos < t.m) {
+          const int l1 = std::min(lt + 1 + (int)sw_levels, SW_MAX_LEVEL - 1);
+          CR(sweep_enqueue(d, lt, l1, nullptr, true, false));
+          next_level = l1;
+          GatherArgs ga{};
+          ga.job[ga.n++] = CopyJob{(const uint32_t*)sw_ctl.p,
+                                   (uint32_t*)((char*)hmisc_dev + SW_HCTL),
+                                   (uint32_t)(sw_ctl_bytes() / 4)};
+          ga.job[ga.n++] = CopyJob{(const uint32_t*)misc.p, (uint32_t*)hmisc_dev, 16};
+          launch_gather(ga, stream);
+          CK(hipGetLastError());
+          CK(hipStreamSynchronize(stream));
+          again = true;
+          continue;
+        }
+      }
       int L = -1;
       if (ab) L = (int)ab;
       else if (hc[next_level].m == 0) break;  // every list decided

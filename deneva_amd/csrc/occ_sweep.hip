@@ -425,30 +425,34 @@ __global__ __launch_bounds__(PRE_B) void k_sw_pre(SwPreArgs a) {
   uint32_t* const s_off = L.s_off;
   uint32_t* const s_meta = L.s_meta;
   uint32_t& s_bad = L.s_bad;
-  if (*a.abandon) return;
-    if (a.dbg && blockIdx.x == 0 && threadIdx.x == 0) a.dbg[0] = __builtin_amdgcn_s_memrealtime();
+  // every control word and the tile's offsets, txn ids and states are read
+  // at once (indices clamped to the host's list bound m_host, which every
+  // list buffer covers), before the first branch on any of them: one
+  // dependent round trip instead of four
+  const uint32_t j = threadIdx.x;
+  const uint32_t k = blockIdx.x;  // one tile per workgroup (one workgroup per tile of p_max)
+  const uint32_t i0 = k * SW_T;
+  const uint32_t ab = *a.abandon;
   const uint32_t m = list_len(a.m_dev, a.m_host);
+  const uint32_t xj = min(i0 + j, a.m_host);
+  const uint32_t o_raw = a.in.off[xj], o0_raw = a.in.off[0];
+  const uint32_t tid_raw = a.in.tid ? a.in.tid[xj] : i0 + j;
+  const uint8_t st_raw = a.state ? a.state[xj] : (uint8_t)ST_UNDECIDED;
+  if (ab) return;
+    if (a.dbg && blockIdx.x == 0 && threadIdx.x == 0) a.dbg[0] = __builtin_amdgcn_s_memrealtime();
   const uint32_t lim = min(m, a.p_max);
   const uint32_t ntiles = (lim + SW_T - 1) / SW_T;
-  const uint32_t j = threadIdx.x;
   const uint64_t nnz = a.in.nnz;
-  const uint64_t off0 = min((uint64_t)a.in.off[0], nnz);
-  // one tile per workgroup (the host launches one workgroup per tile of p_max)
-  const uint32_t k = blockIdx.x;
+  const uint64_t off0 = min((uint64_t)o0_raw, nnz);
   if (k >= ntiles) return;
   {
     SwRec& R = a.rec[k];
-    const uint32_t i0 = k * SW_T;
     const uint32_t nt = min(SW_T, lim - i0);
-    if (j <= nt) s_off[j] = (uint32_t)min((uint64_t)a.in.off[i0 + j], nnz);
-    // per-txn inputs of the record, read now (used at the end)
-    uint32_t my_tid = 0;
-    bool my_pre = false;
-    if (j < nt) {
-      my_tid = a.in.tid ? a.in.tid[i0 + j] : i0 + j;
-      // identity lists carry decisions made before the solver (history window)
-      my_pre = a.state && a.state[i0 + j] != ST_UNDECIDED;
-    }
+    if (j <= nt) s_off[j] = (uint32_t)min((uint64_t)o_raw, nnz);
+    // per-txn inputs of the record (used at the end); identity lists carry
+    // decisions made before the solver (history window)
+    const uint32_t my_tid = j < nt ? tid_raw : 0u;
+    const bool my_pre = j < nt && st_raw != ST_UNDECIDED;
     if (j < SW_T) {
       s_dep[j] = 0;
       s_meta[j] = 0;
@@ -504,23 +508,29 @@ __global__ __launch_bounds__(256) void k_sw_rows(SwPreArgs a) {
   __shared__ uint32_t s_off[SW_T + 1];
   __shared__ uint32_t s_ent[SW_TA];  // the tile's access entries (sw_apack)
   __shared__ uint8_t s_flag[SW_TA];  // live | needed << 1 per access
-  if (*a.abandon) return;
+  const uint32_t k = blockIdx.x, j = threadIdx.x, lane = lane_id();
+  // control words, the tile's stop mark and offsets in one round trip
+  // (indices clamped to the host's list bound; records of tiles past the
+  // list are never read by the serial pass)
+  const uint32_t ab = *a.abandon;
   const uint32_t m = list_len(a.m_dev, a.m_host);
+  SwRec& R = a.rec[k];
+  const uint32_t meta0 = R.meta[0];
+  const uint32_t o_raw = a.in.off[min(k * SW_T + j, a.m_host)], o0_raw = a.in.off[0];
+  if (ab) return;
   const uint32_t lim = min(m, a.p_max);
   const uint32_t ntiles = (lim + SW_T - 1) / SW_T;
-  const uint32_t k = blockIdx.x, j = threadIdx.x, lane = lane_id();
   if (k >= ntiles) return;
-  SwRec& R = a.rec[k];
-  if (R.meta[0] & SWM_STOP) {  // uniform: written on every txn of a stopped tile
+  if (meta0 & SWM_STOP) {  // uniform: written on every txn of a stopped tile
     if (j == 0) R.hdr = SWH_STOP;
     return;
   }
   uint64_t* dbg = (a.dbg && k == 0) ? a.dbg : nullptr;
   if (dbg && j == 0) dbg[8] = __builtin_amdgcn_s_memrealtime();
   const uint64_t nnz = a.in.nnz;
-  const uint32_t off0 = (uint32_t)min((uint64_t)a.in.off[0], nnz);
+  const uint32_t off0 = (uint32_t)min((uint64_t)o0_raw, nnz);
   const uint32_t nt = min(SW_T, lim - k * SW_T);
-  if (j <= nt) s_off[j] = (uint32_t)min((uint64_t)a.in.off[k * SW_T + j], nnz);
+  if (j <= nt) s_off[j] = (uint32_t)min((uint64_t)o_raw, nnz);
   __syncthreads();
   if (dbg && j == 0) dbg[9] = __builtin_amdgcn_s_memrealtime();
   const uint32_t A0 = s_off[0];
@@ -683,8 +693,9 @@ __global__ __launch_bounds__(SEQ_B) void k_sw_seq(SwSeqArgs a) {
   uint64_t* const s_M = L.s_M;
   SwRec* const ring = L.ring;
   const uint32_t j = threadIdx.x, lane = lane_id(), wv = j >> 6;
-  if (*a.abandon) return;
+  const uint32_t ab = *a.abandon;
   const uint32_t m = list_len(a.m_dev, a.m_host);
+  if (ab) return;
   const uint32_t lim = min(m, a.p_max);
   const uint32_t ntiles = min((lim + SW_T - 1) / SW_T, SW_PMAX_TILES);
   // the filter of this level starts from a clean look-back and ticket; the
@@ -900,12 +911,15 @@ __global__ __launch_bounds__(SEQ_B) void k_sw_seq(SwSeqArgs a) {
 __global__ __launch_bounds__(256) void k_sw_cout(SwCoutArgs a) {
   __shared__ uint32_t s_cnt[4];
   __shared__ uint32_t s_base;
-  if (*a.abandon) return;
+  const uint32_t ab = *a.abandon;
   const uint32_t pos = a.lv->pos;
-  if (a.skip_done && pos >= list_len(a.m_dev, a.m_host)) return;
+  const uint32_t m = list_len(a.m_dev, a.m_host);
+  const uint32_t o0_raw = a.in.off[0];
+  if (ab) return;
+  if (a.skip_done && pos >= m) return;
   const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
   const uint64_t nnz = a.in.nnz;
-  const uint32_t off0 = (uint32_t)min((uint64_t)a.in.off[0], nnz);
+  const uint32_t off0 = (uint32_t)min((uint64_t)o0_raw, nnz);
   const uint32_t range = (uint32_t)min((uint64_t)a.in.off[pos], nnz) - off0;
   // 1024 accesses per workgroup round (wave w: [256w, 256w + 256)), one
   // fill-counter atomic per round
@@ -1025,10 +1039,11 @@ __global__ __launch_bounds__(SW_CHUNK) void k_sw_filter(SwFilterArgs a) {
   __shared__ uint64_t s_stash[FW][F_STASH];
   __shared__ uint32_t s_wpre[FW][SW_WA / 64];
   const uint32_t j = threadIdx.x, lane = lane_id(), wv = j >> 6;
-  if (*a.abandon) return;
+  const uint32_t ab = *a.abandon;
   const uint32_t m = list_len(a.m_dev, a.m_host);
   const uint32_t pos = a.lv->pos;
   const uint32_t ccount = a.lv->ccount;
+  if (ab) return;
   const bool X = ccount <= F_XCAP;  // uniform
   // DCC_SW_DEBUG: wave 0 of workgroups < 256 stamps start / setup / loads /
   // exact checks / writes / end and counts its tiles
@@ -1433,9 +1448,9 @@ __global__ __launch_bounds__(SW_CHUNK) void k_sw_compact(SwFilterArgs a) {
   // an earlier level's hand-off: nothing to compact (this level's own
   // decision is made below and still needs its list)
   const uint32_t ab = *a.abandon;
-  if (ab && ab != a.level + 1) return;
   const uint32_t m = list_len(a.m_dev, a.m_host);
   const uint32_t pos = a.lv->pos;
+  if (ab && ab != a.level + 1) return;
   if (pos >= m) return;
   const uint32_t n64 = (m - pos + 63) / 64;
   const uint64_t nnz = a.in.nnz;

@@ -127,8 +127,13 @@ def test_tpcc(sw):
     run(sw, d.gen_tpcc(n_txn=65536, num_wh=16))
 
 
-def test_device_batch_and_repeat(sw):
+@pytest.mark.parametrize("levels", [2, 4])
+def test_device_batch_and_repeat(sw, levels):
+    # graph-captured epochs; at 2 levels per synchronisation the serial-only
+    # last level leaves list txns past its serial range, so every replay
+    # resumes with that level's filter and more levels
     import torch
+    sw.set_option(OPT_SWEEP_LEVELS, levels)
     b = d.gen_ycsb(n_txn=100000, zipf_theta=0.9)
     db = b.to_torch("cuda:0")
     erc, _, _ = orc.occ(b)
