@@ -336,6 +336,7 @@ __device__ inline Gs gs_element(uint64_t p, K key, uint32_t val, K pkey, uint32_
 
 struct ScanOut {
   const uint32_t* off;
+  uint32_t ulen;    // every txn has this many requests (off[t] = t * ulen), or 0: ragged
   uint32_t n;       // epoch txns: values with txn >= n are the held prefix (no outputs)
   uint32_t* group;  // [nnz] or null
   uint8_t* rc;      // [n]
@@ -487,7 +488,7 @@ __global__ __launch_bounds__(256) void k_cv_down(const K* __restrict__ sk,
 #pragma unroll
   for (uint32_t i = 0; i < CV_ITEMS; i++) {
     const uint32_t t = v[i] >> 7;
-    xo[i] = (p0 + i < m && t < o.n) ? o.off[t] : 0u;
+    xo[i] = (p0 + i < m && t < o.n) ? (o.ulen ? t * o.ulen : o.off[t]) : 0u;
   }
   K pk = pk0;
   uint32_t pv = pv0;
@@ -522,6 +523,151 @@ __global__ __launch_bounds__(256) void k_cv_down(const K* __restrict__ sk,
     }
   }
   if (o.gsize && last_gs != NOPOS) atomicMax(&o.gsize[last_gs], last_gnd);
+}
+
+// ---- the same scan when no wave levels are asked for: only the grant group
+// count is needed, so the state packs into one word -- segment start (bit 0),
+// first and last lock type of the run (2 bits each: SH, EX, NONE) and the
+// groups started since the segment's first request (27 bits) -- and the block
+// scans are wave shuffles instead of 10-word LDS trees.  Same monoid as Gs
+// restricted to (flag, ft, lt, cnt).
+__host__ __device__ constexpr uint32_t gl_pack(uint32_t flag, uint32_t ft, uint32_t lt, uint32_t cnt) {
+  return flag | (ft << 1) | (lt << 3) | (cnt << 5);
+}
+constexpr uint32_t GL_ID = gl_pack(0, CV_NONE, CV_NONE, 0);
+__device__ inline uint32_t gl_combine(uint32_t A, uint32_t B) {
+  if (B & 1u) return B;
+  const uint32_t aft = (A >> 1) & 3u, alt = (A >> 3) & 3u, bft = (B >> 1) & 3u, blt = (B >> 3) & 3u;
+  const bool bnd = alt != CV_NONE && bft != CV_NONE && (alt == CV_EX || bft == CV_EX);
+  const uint32_t ft = aft != CV_NONE ? aft : bft;
+  const uint32_t lt = blt != CV_NONE ? blt : alt;
+  return (A & 1u) | (ft << 1) | (lt << 3) | (((A >> 5) + (B >> 5) + (bnd ? 1u : 0u)) << 5);
+}
+template <typename K>
+__device__ inline uint32_t gl_element(uint64_t p, K key, uint32_t val, K pkey, uint32_t pval) {
+  const bool start = p == 0 || key != pkey;
+  const uint32_t typ = (val & 1u) ? CV_EX : CV_SH;
+  if (start) return gl_pack(1, typ, typ, 0);
+  if ((val >> 7) == (pval >> 7)) return GL_ID;  // duplicate row of the same txn
+  return gl_pack(0, typ, typ, 0);
+}
+// inclusive scan of a wave, then the block's exclusive prefix of each thread
+// (4 waves; the wave totals through LDS); returns the exclusive prefix and
+// the block total
+__device__ inline uint32_t gl_block_excl(uint32_t v, uint32_t* s_w, uint32_t& total) {
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d);
+    if (lane >= d) x = gl_combine(y, x);
+  }
+  if (lane == 63) s_w[w] = x;
+  __syncthreads();
+  uint32_t wp = GL_ID;
+  for (uint32_t q = 0; q < w; q++) wp = gl_combine(wp, s_w[q]);
+  total = gl_combine(gl_combine(gl_combine(s_w[0], s_w[1]), s_w[2]), s_w[3]);
+  const uint32_t ex_in = __shfl_up(x, 1);
+  __syncthreads();
+  return gl_combine(wp, lane ? ex_in : GL_ID);
+}
+
+template <typename K>
+__global__ __launch_bounds__(256) void k_cv_up_l(const K* __restrict__ sk,
+                                                 const uint32_t* __restrict__ sv, uint64_t m,
+                                                 uint32_t* __restrict__ agg) {
+  __shared__ uint32_t s_w[4];
+  __shared__ K lk[CV_LDS];
+  __shared__ uint32_t lv[CV_LDS];
+  const uint64_t p0 = (uint64_t)blockIdx.x * CV_TILE + (uint64_t)threadIdx.x * CV_ITEMS;
+  K k[CV_ITEMS];
+  uint32_t v[CV_ITEMS];
+  K pk;
+  uint32_t pv;
+  load_run(sk, sv, m, lk, lv, k, v, pk, pv);
+  uint32_t acc = GL_ID;
+  if (p0 < m) {
+#pragma unroll
+    for (uint32_t i = 0; i < CV_ITEMS; i++) {
+      if (p0 + i < m) acc = gl_combine(acc, gl_element(p0 + i, k[i], v[i], pk, pv));
+      pk = k[i];
+      pv = v[i];
+    }
+  }
+  uint32_t total;
+  (void)gl_block_excl(acc, s_w, total);
+  if (threadIdx.x == 0) agg[blockIdx.x] = total;
+}
+
+// one workgroup: exclusive scan of the tile aggregates in place (16 per thread)
+__global__ __launch_bounds__(256) void k_cv_top_l(uint32_t* __restrict__ agg, uint32_t tiles) {
+  __shared__ uint32_t s_w[4];
+  uint32_t carry = GL_ID;
+  for (uint32_t c0 = 0; c0 < tiles; c0 += 256 * 16) {
+    const uint32_t i0 = c0 + threadIdx.x * 16;
+    uint32_t a[16], v = GL_ID;
+#pragma unroll
+    for (uint32_t q = 0; q < 16; q++) {
+      a[q] = i0 + q < tiles ? agg[i0 + q] : GL_ID;
+      v = gl_combine(v, a[q]);
+    }
+    uint32_t total;
+    uint32_t run = gl_combine(carry, gl_block_excl(v, s_w, total));
+#pragma unroll
+    for (uint32_t q = 0; q < 16; q++) {
+      if (i0 + q < tiles) agg[i0 + q] = run;
+      run = gl_combine(run, a[q]);
+    }
+    carry = gl_combine(carry, total);
+  }
+}
+
+template <typename K>
+__global__ __launch_bounds__(256) void k_cv_down_l(const K* __restrict__ sk,
+                                                   const uint32_t* __restrict__ sv, uint64_t m,
+                                                   const uint32_t* __restrict__ pre, ScanOut o) {
+  __shared__ uint32_t s_w[4];
+  __shared__ K lk[CV_LDS];
+  __shared__ uint32_t lv[CV_LDS];
+  const uint64_t p0 = (uint64_t)blockIdx.x * CV_TILE + (uint64_t)threadIdx.x * CV_ITEMS;
+  K k[CV_ITEMS];
+  uint32_t v[CV_ITEMS];
+  K pk0 = 0;
+  uint32_t pv0 = 0;
+  load_run(sk, sv, m, lk, lv, k, v, pk0, pv0);
+  uint32_t acc = GL_ID;
+  if (p0 < m) {
+    K pk = pk0;
+    uint32_t pv = pv0;
+#pragma unroll
+    for (uint32_t i = 0; i < CV_ITEMS; i++) {
+      if (p0 + i < m) acc = gl_combine(acc, gl_element(p0 + i, k[i], v[i], pk, pv));
+      pk = k[i];
+      pv = v[i];
+    }
+  }
+  uint32_t total;
+  uint32_t run = gl_combine(pre[blockIdx.x], gl_block_excl(acc, s_w, total));
+  if (p0 >= m) return;
+  uint32_t xo[CV_ITEMS];
+#pragma unroll
+  for (uint32_t i = 0; i < CV_ITEMS; i++) {
+    const uint32_t t = v[i] >> 7;
+    xo[i] = (p0 + i < m && t < o.n) ? (o.ulen ? t * o.ulen : o.off[t]) : 0u;
+  }
+  K pk = pk0;
+  uint32_t pv = pv0;
+#pragma unroll
+  for (uint32_t i = 0; i < CV_ITEMS; i++) {
+    if (p0 + i >= m) break;
+    const uint32_t e = gl_element(p0 + i, k[i], v[i], pk, pv);
+    run = gl_combine(run, e);
+    pk = k[i];
+    pv = v[i];
+    const uint32_t t = v[i] >> 7, j = (v[i] >> 1) & 63u;
+    if (t >= o.n) continue;  // held-prefix request: part of the scan only
+    o.group[xo[i] + j] = e == GL_ID ? DCC_GROUP_NONE : run >> 5;
+  }
 }
 
 // acquire_locks' return (ycsb_txn.cpp:76-79): RCOK iff every request of the
@@ -679,10 +825,17 @@ static int calvin_sort_and_scan(dcc_ctx* ctx, const DevBatch& d, const uint32_t*
   else
     cur = radix_sort_u64((uint64_t**)kb, vb, m, kp.bits, (uint32_t*)ctx->cv_scratch.p, st);
   if (prof) CK(hipEventRecord(ctx->pev[2], st));
-  Gs* agg = (Gs*)ctx->cv_agg.p;
-  k_cv_up<K><<<(unsigned)tiles, 256, 0, st>>>(kb[cur], vb[cur], m, agg);
-  k_cv_top<<<1, 256, 0, st>>>(agg, (uint32_t)tiles);
-  k_cv_down<K><<<(unsigned)tiles, 256, 0, st>>>(kb[cur], vb[cur], m, agg, so);
+  if (so.pgx) {  // wave levels: the full scan state
+    Gs* agg = (Gs*)ctx->cv_agg.p;
+    k_cv_up<K><<<(unsigned)tiles, 256, 0, st>>>(kb[cur], vb[cur], m, agg);
+    k_cv_top<<<1, 256, 0, st>>>(agg, (uint32_t)tiles);
+    k_cv_down<K><<<(unsigned)tiles, 256, 0, st>>>(kb[cur], vb[cur], m, agg, so);
+  } else {  // grant groups only: the one-word state
+    uint32_t* agg = (uint32_t*)ctx->cv_agg.p;
+    k_cv_up_l<K><<<(unsigned)tiles, 256, 0, st>>>(kb[cur], vb[cur], m, agg);
+    k_cv_top_l<<<1, 256, 0, st>>>(agg, (uint32_t)tiles);
+    k_cv_down_l<K><<<(unsigned)tiles, 256, 0, st>>>(kb[cur], vb[cur], m, agg, so);
+  }
   CK(hipGetLastError());
   return DCC_OK;
 }
@@ -776,7 +929,10 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint3
   }
   const bool waves = out_wave != nullptr;
   uint32_t* wave_dev = nullptr;
-  ScanOut so{d.off, (uint32_t)d.n, grp_dev, rc_dev, nullptr, nullptr, nullptr};
+  // uniform txn length (YCSB's fixed request count): a request's place in
+  // request order is t * len + j, no offset lookup per request
+  const uint32_t ulen = (maxlen && d.nnz == (uint64_t)d.n * maxlen) ? maxlen : 0u;
+  ScanOut so{d.off, ulen, (uint32_t)d.n, grp_dev, rc_dev, nullptr, nullptr, nullptr};
   if (waves) {
     if (dev_out) {
       wave_dev = out_wave;
