@@ -97,6 +97,13 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scan(uint32_t* __restrict__ c
   if (threadIdx.x == 0) tot[blockIdx.x] = run;
 }
 
+// Stable scatter of one tile.  Wave w owns the tile's items
+// [w * 1024, w * 1024 + 1024) (item it of lane l at w * 1024 + 64 it + l), so
+// position order is (wave, round, lane): each wave ranks its own items with a
+// running per-digit count in its own LDS row -- no workgroup barrier per
+// round (a wave's LDS operations execute in order) -- and the waves' counts
+// are combined once.  Then the tile is staged in LDS in digit order and
+// written out with coalesced runs per digit.
 template <typename K>
 __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(const K* __restrict__ kin,
                                                            const uint32_t* __restrict__ vin,
@@ -106,21 +113,22 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(const K* __restrict__
                                                            const uint32_t* __restrict__ cnt,
                                                            const uint32_t* __restrict__ tot,
                                                            uint32_t tiles) {
+  constexpr uint32_t W = RS_THREADS / 64, WI = RS_TILE / W;  // waves, items per wave
   __shared__ K s_key[RS_TILE];
   __shared__ uint32_t s_val[RS_TILE];
-  __shared__ uint32_t s_wc[4][256];
-  __shared__ uint32_t s_run[256];  // running per-digit count inside the tile
-  __shared__ uint32_t s_gb[256];   // global destination base per digit
-  __shared__ uint32_t s_tb[256];   // tile-local base per digit
+  __shared__ uint32_t s_wc[W][256];  // per wave: running digit count, then its base in the tile
+  __shared__ uint32_t s_gb[256];     // global destination base per digit
+  __shared__ uint32_t s_tb[256];     // tile-local base per digit
   __shared__ uint32_t sh[4];
-  const uint32_t tid = threadIdx.x, wv = tid >> 6;
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
   const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
+  const uint64_t wbase = base + (uint64_t)wv * WI;
 
   K k[RS_ITEMS];
   uint32_t v[RS_ITEMS];
 #pragma unroll
   for (uint32_t it = 0; it < RS_ITEMS; it++) {
-    const uint64_t p = base + it * RS_THREADS + tid;
+    const uint64_t p = wbase + it * 64 + lane;
     k[it] = p < m ? kin[p] : (K)0;
     v[it] = p < m ? vin[p] : 0u;
   }
@@ -129,43 +137,50 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(const K* __restrict__
     const uint32_t g = block_excl_scan256(tot[tid], sh, total);
     s_gb[tid] = g + cnt[(uint64_t)tid * tiles + blockIdx.x];
   }
-  s_run[tid] = 0;
 #pragma unroll
-  for (int w = 0; w < 4; w++) s_wc[w][tid] = 0;
+  for (uint32_t w = 0; w < W; w++) s_wc[w][tid] = 0;
   __syncthreads();
 
-  // stable in-tile ranking: item order = (iteration, thread)
   const uint64_t lt = lanemask_lt();
   uint32_t loc[RS_ITEMS];
+  uint32_t* wc = s_wc[wv];
 #pragma unroll
   for (uint32_t it = 0; it < RS_ITEMS; it++) {
-    const uint64_t p = base + it * RS_THREADS + tid;
+    const uint64_t p = wbase + it * 64 + lane;
     const bool act = p < m;
     const uint32_t d = (uint32_t)(k[it] >> shift) & 255u;
     const uint64_t peers = digit_peers(d, act);
     const uint32_t lr = (uint32_t)__builtin_popcountll(peers & lt);
-    if (act && lr == 0) s_wc[wv][d] = (uint32_t)__builtin_popcountll(peers);
-    __syncthreads();
-    uint32_t o = s_run[d] + lr;
-    for (uint32_t w = 0; w < wv; w++) o += s_wc[w][d];
-    loc[it] = o;
-    __syncthreads();
-    s_run[tid] += s_wc[0][tid] + s_wc[1][tid] + s_wc[2][tid] + s_wc[3][tid];
-#pragma unroll
-    for (int w = 0; w < 4; w++) s_wc[w][tid] = 0;
-    __syncthreads();
+    const uint32_t before = wc[d];
+    loc[it] = before + lr;
+    // the digit's first lane advances the count; the read above and this
+    // write are the same wave's, in order
+    if (act && lr == 0) wc[d] = before + (uint32_t)__builtin_popcountll(peers);
   }
+  __syncthreads();
   {
+    uint32_t c[W], t = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < W; w++) {
+      c[w] = s_wc[w][tid];
+      t += c[w];
+    }
     uint32_t total;
-    s_tb[tid] = block_excl_scan256(s_run[tid], sh, total);
+    uint32_t b = block_excl_scan256(t, sh, total);
+    s_tb[tid] = b;
+#pragma unroll
+    for (uint32_t w = 0; w < W; w++) {
+      s_wc[w][tid] = b;
+      b += c[w];
+    }
   }
   __syncthreads();
 #pragma unroll
   for (uint32_t it = 0; it < RS_ITEMS; it++) {
-    const uint64_t p = base + it * RS_THREADS + tid;
+    const uint64_t p = wbase + it * 64 + lane;
     if (p < m) {
       const uint32_t d = (uint32_t)(k[it] >> shift) & 255u;
-      const uint32_t pos = s_tb[d] + loc[it];
+      const uint32_t pos = wc[d] + loc[it];
       s_key[pos] = k[it];
       s_val[pos] = v[it];
     }
