@@ -43,12 +43,17 @@ __device__ inline uint32_t block_excl_scan256(uint32_t v, uint32_t* sh /*[4]*/, 
   return off + x - v;
 }
 
+// Per-tile digit counts: one LDS histogram per wave (an atomic add per item,
+// spread over 256 bins), summed at the end.
 template <typename K>
 __global__ __launch_bounds__(RS_THREADS) void k_rs_hist(const K* __restrict__ keys, uint64_t m,
                                                         uint32_t shift, uint32_t* __restrict__ cnt,
                                                         uint32_t tiles) {
-  __shared__ uint32_t s_h[256];
-  s_h[threadIdx.x] = 0;
+  constexpr uint32_t W = RS_THREADS / 64;
+  __shared__ uint32_t s_h[W][256];
+  const uint32_t wv = threadIdx.x >> 6;
+#pragma unroll
+  for (uint32_t w = 0; w < W; w++) s_h[w][threadIdx.x] = 0;
   __syncthreads();
   const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
   K k[RS_ITEMS];
@@ -57,16 +62,16 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_hist(const K* __restrict__ ke
     const uint64_t p = base + it * RS_THREADS + threadIdx.x;
     k[it] = p < m ? keys[p] : (K)0;
   }
-  const uint64_t lt = lanemask_lt();
 #pragma unroll
   for (uint32_t it = 0; it < RS_ITEMS; it++) {
     const uint64_t p = base + it * RS_THREADS + threadIdx.x;
-    const uint32_t d = (uint32_t)(k[it] >> shift) & 255u;
-    const uint64_t peers = digit_peers(d, p < m);
-    if (peers && (peers & lt) == 0) atomicAdd(&s_h[d], (uint32_t)__builtin_popcountll(peers));
+    if (p < m) atomicAdd(&s_h[wv][(uint32_t)(k[it] >> shift) & 255u], 1u);
   }
   __syncthreads();
-  cnt[(uint64_t)threadIdx.x * tiles + blockIdx.x] = s_h[threadIdx.x];
+  uint32_t c = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < W; w++) c += s_h[w][threadIdx.x];
+  cnt[(uint64_t)threadIdx.x * tiles + blockIdx.x] = c;
 }
 
 // One workgroup per digit: exclusive scan of cnt[d][0..tiles) in place,
