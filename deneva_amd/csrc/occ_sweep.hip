@@ -221,7 +221,7 @@ __device__ inline uint32_t sw_tiles_per_wg(uint32_t n64, uint32_t nblocks) {
 // only its first access touches the level's global key table, so a hot key
 // costs one global CAS per tile rather than one per access.
 constexpr uint32_t PRE_MAP = 4096;       // LDS map slots (<= 2048 distinct keys per pass)
-constexpr uint32_t PRE_B = 512;           // threads per workgroup
+constexpr uint32_t PRE_B = 1024;          // threads per workgroup
 
 __device__ inline uint32_t pre_map_insert(uint64_t* mkey, uint64_t key, bool& first) {
   uint32_t h = sw_hash(key, 12);
@@ -475,9 +475,9 @@ __global__ __launch_bounds__(PRE_B) void k_sw_pre(SwPreArgs a) {
       if (j < SW_T) R.meta[j] = SWM_STOP;
       return;
     }
-    if (cnt <= 2 * PRE_B) pre_tile<2>(a, L, k, j, nt, A0, cnt, off0);
-    else if (cnt <= 4 * PRE_B) pre_tile<4>(a, L, k, j, nt, A0, cnt, off0);
-    else pre_tile<8>(a, L, k, j, nt, A0, cnt, off0);
+    if (cnt <= PRE_B) pre_tile<1>(a, L, k, j, nt, A0, cnt, off0);
+    else if (cnt <= 2 * PRE_B) pre_tile<2>(a, L, k, j, nt, A0, cnt, off0);
+    else pre_tile<4>(a, L, k, j, nt, A0, cnt, off0);
     // the per-txn words (k_sw_rows adds the row length)
     if (j < SW_T) {
       uint32_t mt = s_meta[j];
