@@ -558,65 +558,101 @@ __global__ __launch_bounds__(256) void k_sw_rows(SwPreArgs a) {
       const uint32_t x = x0 + j + 256 * u;
       if (x >= cnt) continue;
       const bool in = sw_aid(e[u]) < idlim;
+      // live | needed << 1 | the access's txn in the tile << 2
       const uint32_t f = (in && fw[u] < pp[u] ? 1u : 0u) |
-                         (in && (e[u] & 32u) && la[u] > pp[u] ? 2u : 0u);
+                         (in && (e[u] & 32u) && la[u] > pp[u] ? 2u : 0u) | ((pp[u] & 63u) << 2);
       s_ent[x] = e[u];
       s_flag[x] = (uint8_t)f;
     }
   }
   __syncthreads();
   if (dbg && j == 0) dbg[10] = __builtin_amdgcn_s_memrealtime();
-  if (j >= 64) return;
-  // (2) wave 0, lane = txn: counts, prefix sums, the two lists from LDS
+  // (2) the two lists in access order, which is txn order (so the probes
+  // come grouped by txn): per 64-access chunk the live / needed ballots and
+  // counts (the four waves take every fourth chunk), an exclusive scan of the
+  // chunk counts (wave 0: at most 64 chunks), then every wave writes its
+  // chunks' entries in place
+  __shared__ uint64_t s_bl[SW_TA / 64 + 1];  // live ballot per chunk (+ a zero word)
+  __shared__ uint32_t s_cp[SW_TA / 64 + 1], s_ci[SW_TA / 64 + 1];
+  const uint32_t wv = j >> 6;
+  const uint32_t nch = (cnt + 63) / 64;
+  const uint64_t lt = lanemask_lt();
+  for (uint32_t c = wv; c < nch; c += 4) {
+    const uint32_t x = c * 64 + lane;
+    const uint32_t f = x < cnt ? s_flag[x] : 0u;
+    const uint64_t bl = ballot64(f & 1u), bn = ballot64((f >> 1) & 1u);
+    if (lane == 0) {
+      s_bl[c] = bl;
+      s_cp[c] = (uint32_t)__popcll(bl);
+      s_ci[c] = (uint32_t)__popcll(bn);
+    }
+  }
+  __syncthreads();
+  if (wv == 0) {
+    const uint32_t vp = lane < nch ? s_cp[lane] : 0u, vi = lane < nch ? s_ci[lane] : 0u;
+    uint32_t tp, ti;
+    const uint32_t ep = wave_excl_u32(vp, tp), ei = wave_excl_u32(vi, ti);
+    if (lane < nch) {
+      s_cp[lane] = ep;
+      s_ci[lane] = ei;
+    }
+    if (lane == 0) {
+      s_cp[nch] = tp;
+      s_ci[nch] = ti;
+      s_bl[nch] = 0;
+    }
+  }
+  __syncthreads();
+  const uint32_t np = s_cp[nch], ni = s_ci[nch];
+  uint32_t* ovf = a.lst_ovf + (uint64_t)k * SW_OVF;
+  for (uint32_t c = wv; c < nch; c += 4) {
+    const uint32_t x = c * 64 + lane;
+    const uint32_t f = x < cnt ? s_flag[x] : 0u;
+    const uint64_t bn = ballot64((f >> 1) & 1u);
+    if (!(f & 3u)) continue;
+    const uint32_t id = sw_aid(s_ent[x]);
+    if (f & 1u) {
+      const uint32_t q = s_cp[c] + (uint32_t)__popcll(s_bl[c] & lt);
+      const uint32_t e = sw_ppack(id);
+      if (q < SW_PL) R.probe[q] = e;
+      else ovf[q - SW_PL] = e;
+    }
+    if (f & 2u) {
+      const uint32_t q = s_ci[c] + (uint32_t)__popcll(bn & lt);
+      const uint32_t e = sw_ipack(id, f >> 2);
+      if (q < SW_IL) R.ins[q] = e;
+      else ovf[SW_TA + q - SW_IL] = e;
+    }
+  }
+  if (wv != 0) return;
+  // lane = txn: its probe span (the live accesses before its first and past
+  // its last access), the register-chunk masks, no-op padding, the header
   const uint32_t t = lane;
-  uint32_t s = 0, len = 0;
+  uint32_t xlo = cnt, xhi = cnt;
   if (t < nt) {
-    s = s_off[t] - A0;
-    len = s_off[t + 1] > s_off[t] ? min(s_off[t + 1] - s_off[t], MAX_TXN_LEN) : 0u;
-    if (s + len > cnt) len = s < cnt ? cnt - s : 0u;
+    const uint32_t s0 = s_off[t] - A0;
+    const uint32_t len = s_off[t + 1] > s_off[t] ? min(s_off[t + 1] - s_off[t], MAX_TXN_LEN) : 0u;
+    xlo = min(s0, cnt);
+    xhi = min(s0 + len, cnt);
   }
-  uint32_t cp = 0, ci = 0;
-  for (uint32_t q = 0; q < len; q++) {
-    const uint32_t f = s_flag[s + q];
-    cp += f & 1u;
-    ci += f >> 1;
-  }
-  uint32_t np, ni;
-  uint32_t ps = wave_excl_u32(cp, np);
-  uint32_t is = wave_excl_u32(ci, ni);
-  R.pspan[t] = ps | ((ps + cp) << 16);
+  auto live_before = [&](uint32_t x) {
+    const uint32_t w = x >> 6, b = x & 63u;
+    return s_cp[w] + (uint32_t)__popcll(s_bl[w] & (b ? ~0ull >> (64 - b) : 0ull));
+  };
+  const uint32_t ps = live_before(xlo), pe = live_before(xhi);
+  R.pspan[t] = ps | (pe << 16);
   if (t == 0) {
     R.np = np;
     R.ni = ni;
     R.hdr = (np > SW_RC * 64 ? SWH_PLONG : 0u) | (ni > SW_RC * 64 ? SWH_ILONG : 0u);
   }
-  // the register chunks: per txn its entries in each, no-op padding
 #pragma unroll
   for (uint32_t c = 0; c < SW_RC; c++) {
-    const uint32_t lo = max(ps, c * 64), hi = min(ps + cp, c * 64 + 64);
+    const uint32_t lo = max(ps, c * 64), hi = min(pe, c * 64 + 64);
     const uint32_t nb = hi > lo ? hi - lo : 0u;
     R.seg[c][t] = nb ? (nb >= 64 ? ~0ull : ((1ull << nb) - 1ull)) << (lo - c * 64) : 0ull;
     if (c * 64 + t >= np) R.probe[c * 64 + t] = SW_P_NONE;
     if (c * 64 + t >= ni) R.ins[c * 64 + t] = sw_idummy(t);
-  }
-  uint32_t* ovf = a.lst_ovf + (uint64_t)k * SW_OVF;
-  for (uint32_t q = 0; q < len; q++) {
-    const uint32_t f = s_flag[s + q];
-    if (!f) continue;
-    const uint32_t ent = s_ent[s + q];
-    const uint32_t id = sw_aid(ent);
-    if (f & 1u) {
-      const uint32_t e = sw_ppack(id);
-      if (ps < SW_PL) R.probe[ps] = e;
-      else ovf[ps - SW_PL] = e;
-      ps++;
-    }
-    if (f & 2u) {
-      const uint32_t e = sw_ipack(id, t);
-      if (is < SW_IL) R.ins[is] = e;
-      else ovf[SW_TA + is - SW_IL] = e;
-      is++;
-    }
   }
   if (dbg && t == 0) {
     __builtin_amdgcn_s_waitcnt(0);
