@@ -400,6 +400,13 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1, const SwShard* shl
                  cbits_d, ckeys_d, bloom_d, lv, lv + 1, (uint32_t*)out.off.p, (uint64_t*)sw_mg.p,
                  abandon, err, nullptr};
     if (sw_debug && l < 4) sa.dbg = (uint64_t*)sw_dbg.p + (size_t)l * 1024;
+    if (top) {  // the epoch's validation pass rides along the level-0 serial pass
+      sa.prep_off = d.off;
+      sa.prep_n = d.n;
+      sa.prep_at = d.acctype;
+      sa.prep_nnz = d.nnz;
+      sa.prep_part = (PrepPart*)((char*)hpart_dev + SW_PREP_OFF);
+    }
     if (serial_part) launch_sw_seq(sa, stream);
     // the last level of a graph-captured epoch usually decides its whole list
     // serially: its listing, filter and compaction are enqueued only when the
@@ -631,11 +638,7 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
       fa.job[fa.n++] = FillJob{(uint32_t*)sw_fw.p, 1ull << sw_gbits(0), 0xFFFFFFFFu};
       fa.job[fa.n++] = FillJob{(uint32_t*)sw_fw.p + (1u << SW_GBITS_MAX), 1ull << sw_gbits(0), 0u};
     }
-    if (sweep)
-      launch_fill_prep(fa, d.off, d.n, d.acctype, d.nnz,
-                       (PrepPart*)((char*)hpart_dev + SW_PREP_OFF), stream);
-    else
-      launch_fill(fa, stream);
+    launch_fill(fa, stream);  // the sweep's prep runs inside its level-0 serial pass
   }
 
   // ---- history window pre-pass (occ.cpp:160-180)
@@ -731,9 +734,9 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   if (sweep) {
     // prep results: the batch is rejected exactly as device_prep would
     const PrepPart* pp = (const PrepPart*)((const char*)hpart + SW_PREP_OFF);
-    static_assert(SW_PREP_OFF + SW_PREP_BLOCKS * sizeof(PrepPart) <= (1u << 16), "hpart holds them");
+    static_assert(SW_PREP_OFF + SW_SEQ_PREP_BLOCKS * sizeof(PrepPart) <= (1u << 16), "hpart holds them");
     uint32_t perr = 0;
-    for (unsigned q = 0; q < SW_PREP_BLOCKS; q++) {
+    for (unsigned q = 0; q < SW_SEQ_PREP_BLOCKS; q++) {
       perr |= pp[q].err;
       maxlen = std::max(maxlen, pp[q].maxlen);
       nnz_w += pp[q].nw;

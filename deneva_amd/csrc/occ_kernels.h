@@ -31,7 +31,6 @@ constexpr uint32_t ERR_UNDECIDED = 16;
 constexpr uint32_t ERR_SPIN = 128;  // sweep filter: look-back spin limit reached
 
 constexpr unsigned PREP_BLOCKS = 512;
-constexpr unsigned SW_PREP_BLOCKS = 2048;  // the sweep's prep (inside the fill launch)
 constexpr unsigned FINAL_BLOCKS = 512;
 struct PrepPart {
   uint32_t err, maxlen, nw, nw_prefix;
@@ -248,7 +247,15 @@ struct SwSeqArgs {
   const uint32_t* abandon;
   uint32_t* err;
   uint64_t* dbg;          // per-tile clock stamps (DCC_SW_DEBUG) or null
+  // the epoch's batch validation (prep_body.h), run by workgroups 1.. of the
+  // level-0 launch beside the one-CU serial pass (prep_part null: none)
+  const uint32_t* prep_off;
+  uint64_t prep_n;
+  const uint8_t* prep_at;
+  uint64_t prep_nnz;
+  PrepPart* prep_part;    // [SW_SEQ_PREP_BLOCKS] (pinned host memory)
 };
+constexpr unsigned SW_SEQ_PREP_BLOCKS = 240;  // prep workgroups beside the level-0 serial pass
 struct SwCoutArgs {
   SwList in;
   const uint32_t* aent;
@@ -338,8 +345,6 @@ struct FillArgs {
   uint32_t n;
 };
 void launch_fill(const FillArgs& a, hipStream_t st);
-void launch_fill_prep(const FillArgs& a, const uint32_t* off, uint64_t n, const uint8_t* at,
-                      uint64_t nnz, PrepPart* part, hipStream_t st);
 // Several small device -> pinned-host copies in one launch (word granular):
 // the control words, counters and partials the host reads after an epoch.
 struct CopyJob {

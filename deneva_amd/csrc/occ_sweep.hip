@@ -42,6 +42,7 @@
 
 #include "dcc_device.h"
 #include "occ_kernels.h"
+#include "prep_body.h"
 
 namespace dcc {
 
@@ -723,6 +724,13 @@ __global__ __launch_bounds__(SEQ_B) void k_sw_seq(SwSeqArgs a) {
     SwRec ring[SEQ_RING];
   };
   __shared__ __attribute__((aligned(16))) Lds L;
+  // workgroups 1.. (level 0 only): the batch validation pass on the CUs the
+  // serial pass leaves idle -- the host reads its partials after the epoch
+  if (blockIdx.x) {
+    prep_body(a.prep_off, a.prep_n, a.prep_at, a.prep_nnz, 0, a.prep_part, blockIdx.x - 1,
+              gridDim.x - 1);
+    return;
+  }
   uint32_t* const cbits = L.cbits;
   uint32_t* const s_ready = L.s_ready;
   uint32_t &s_done = L.s_done, &s_stop = L.s_stop, &s_k = L.s_k;
@@ -1637,7 +1645,9 @@ __global__ __launch_bounds__(SW_CHUNK) void k_sw_compact(SwFilterArgs a) {
 void launch_sw_pre(const SwPreArgs& a, unsigned grid, hipStream_t st) {
   k_sw_pre<<<grid ? grid : 1u, PRE_B, 0, st>>>(a);
 }
-void launch_sw_seq(const SwSeqArgs& a, hipStream_t st) { k_sw_seq<<<1, SEQ_B, 0, st>>>(a); }
+void launch_sw_seq(const SwSeqArgs& a, hipStream_t st) {
+  k_sw_seq<<<a.prep_part ? 1 + SW_SEQ_PREP_BLOCKS : 1, SEQ_B, 0, st>>>(a);
+}
 void launch_sw_rows(const SwPreArgs& a, unsigned grid, hipStream_t st) {
   k_sw_rows<<<grid ? grid : 1u, 256, 0, st>>>(a);  // one workgroup per tile
 }

@@ -2,7 +2,7 @@
 """HBM traffic of one whole OCC epoch from rocprofv3 --pmc passes
 (tools/gpu_pmc_epoch.sh): FETCH_SIZE and WRITE_SIZE (kB, one pass each)
 summed over every dispatch of an epoch (an epoch = the dispatches from one
-k_fill_prep (k_prep in older builds) to the next), median over the run's epochs.  gfx950 correction
+k_fill (k_fill_prep / k_prep in older builds) to the next), median over the run's epochs.  gfx950 correction
 (MI355X_MICROARCH.md, HBM / rocprofv3 section): FETCH_SIZE counts 128-B
 requests at 64 B, so it is doubled.  Also reports the level-0 filter alone.
 Writes <out json>[key] = {"bytes_per_epoch", "source", ...} for bench.py.
@@ -31,7 +31,7 @@ def load(root, pas):
 def epochs(disp):
     out, cur = [], None
     for d in disp:
-        if "k_prep" in d["name"] or "k_fill_prep" in d["name"]:
+        if "k_prep" in d["name"] or "k_fill" in d["name"]:
             if cur:
                 out.append(cur)
             cur = []

@@ -2,7 +2,7 @@
 """Print the kernel timeline of one OCC epoch from a rocprofv3 kernel trace
 (csv): every dispatch of the epoch, with its duration and the idle gap before
 it.  An epoch ends with the k_stage_final dispatch (stage solver) or starts
-with k_prep (older solvers).
+with k_fill (k_fill_prep / k_prep in older builds).
 
     trace_epoch.py <kernel_trace.csv> [epoch_index]   (default: the second to last)
 """
@@ -17,7 +17,7 @@ def main():
     if ends:
         bounds = [(ends[i - 1] + 1 if i else 0, ends[i] + 1) for i in range(len(ends))]
     else:
-        starts = [i for i, r in enumerate(rows) if "k_prep" in r["Kernel_Name"] or "k_fill_prep" in r["Kernel_Name"]]
+        starts = [i for i, r in enumerate(rows) if "k_prep" in r["Kernel_Name"] or "k_fill" in r["Kernel_Name"]]
         bounds = [(s, starts[i + 1] if i + 1 < len(starts) else len(rows)) for i, s in enumerate(starts)]
     e = int(sys.argv[2]) if len(sys.argv) > 2 else max(0, len(bounds) - 2)
     a, b = bounds[e]
