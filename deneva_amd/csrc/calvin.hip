@@ -61,6 +61,7 @@ constexpr uint32_t CV_MAX_TXN = 1u << 25;  // value = txn:25 | j:6 | EX:1
 constexpr unsigned CV_PREP_BLOCKS = 1024;
 constexpr uint32_t CV_ITEMS = 16;                  // scan elements per thread
 constexpr uint32_t CV_TILE = 256 * CV_ITEMS;       // scan elements per workgroup
+constexpr uint64_t CV_PUT_MIN = 1ull << 21;        // requests from which groups go out windowed
 constexpr uint32_t ERR_WAVE_TIMEOUT = 1u << 8;
 
 struct CvPart {
@@ -625,7 +626,8 @@ __global__ __launch_bounds__(256) void k_cv_top_l(uint32_t* __restrict__ agg, ui
 template <typename K>
 __global__ __launch_bounds__(256) void k_cv_down_l(const K* __restrict__ sk,
                                                    const uint32_t* __restrict__ sv, uint64_t m,
-                                                   const uint32_t* __restrict__ pre, ScanOut o) {
+                                                   const uint32_t* __restrict__ pre, ScanOut o,
+                                                   uint32_t* __restrict__ gs) {
   __shared__ uint32_t s_w[4];
   __shared__ K lk[CV_LDS];
   __shared__ uint32_t lv[CV_LDS];
@@ -648,6 +650,28 @@ __global__ __launch_bounds__(256) void k_cv_down_l(const K* __restrict__ sk,
   }
   uint32_t total;
   uint32_t run = gl_combine(pre[blockIdx.x], gl_block_excl(acc, s_w, total));
+  if (gs) {  // groups in sorted order, staged through LDS: coalesced stores
+    K pk = pk0;
+    uint32_t pv = pv0;
+    const uint32_t b = threadIdx.x * (CV_ITEMS + 1);
+#pragma unroll
+    for (uint32_t i = 0; i < CV_ITEMS; i++) {
+      uint32_t g = 0;
+      if (p0 + i < m) {
+        const uint32_t e = gl_element(p0 + i, k[i], v[i], pk, pv);
+        run = gl_combine(run, e);
+        g = e == GL_ID ? DCC_GROUP_NONE : run >> 5;
+      }
+      pk = k[i];
+      pv = v[i];
+      lv[b + i] = g;  // every read of lv (load_run) precedes the scan's barriers
+    }
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * CV_TILE;
+    for (uint32_t i = threadIdx.x; i < CV_TILE; i += 256)
+      if (base + i < m) gs[base + i] = lv[i + (i >> 4)];
+    return;
+  }
   if (p0 >= m) return;
   uint32_t xo[CV_ITEMS];
 #pragma unroll
@@ -668,6 +692,57 @@ __global__ __launch_bounds__(256) void k_cv_down_l(const K* __restrict__ sk,
     if (t >= o.n) continue;  // held-prefix request: part of the scan only
     o.group[xo[i] + j] = e == GL_ID ? DCC_GROUP_NONE : run >> 5;
   }
+}
+
+// The windowed group write-out (uniform request counts, large epochs).  The
+// direct store from k_cv_down_l puts each request's group at a random place:
+// one 32-B sector write per 4-B store (PMC: 521 MB written for 67 MB).
+// Instead the sorted values (txn, request) and their groups are partitioned
+// by the txn's top 8 bits (one counting pass), and each workgroup here owns
+// a window of the group array (a bucket's requests are contiguous there):
+// it places its bucket's groups into the window in LDS and stores the window
+// with coalesced stores.
+constexpr uint32_t CV_WIN = 40448;  // u32 window per workgroup (158 KiB of LDS)
+__global__ __launch_bounds__(1024) void k_cv_put(const uint32_t* __restrict__ sv,
+                                                 const uint32_t* __restrict__ sg,
+                                                 const uint32_t* __restrict__ tot, uint32_t n,
+                                                 uint32_t ulen, uint32_t tsh, uint32_t H,
+                                                 uint32_t wh, uint32_t* __restrict__ group) {
+  __shared__ uint32_t win[CV_WIN];
+  __shared__ uint32_t s_rng[2];
+  const uint32_t bkt = blockIdx.x / H, h = blockIdx.x % H;
+  const uint64_t t_lo = (uint64_t)bkt << tsh;
+  if (t_lo >= n) return;  // whole workgroup
+  const uint64_t d_lo = t_lo * ulen + (uint64_t)h * wh;
+  const uint64_t d_end = min<uint64_t>(t_lo + (1ull << tsh), n) * ulen;
+  if (d_lo >= d_end) return;  // whole workgroup
+  const uint32_t w = (uint32_t)min<uint64_t>(wh, d_end - d_lo);
+  // the bucket's pairs: the digit totals before it (counting pass order)
+  if (threadIdx.x < 2) s_rng[threadIdx.x] = 0;
+  __syncthreads();
+  if (threadIdx.x < bkt) atomicAdd(&s_rng[0], tot[threadIdx.x]);
+  if (threadIdx.x == bkt) s_rng[1] = tot[bkt];
+  __syncthreads();
+  const uint32_t p_lo = s_rng[0], p_hi = s_rng[0] + s_rng[1];
+  constexpr uint32_t U = 8;  // pairs in flight per thread
+  for (uint32_t p0 = p_lo + threadIdx.x; p0 < p_hi; p0 += 1024 * U) {
+    uint32_t vv[U], gg[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++) {
+      const uint32_t p = p0 + u * 1024;
+      vv[u] = p < p_hi ? sv[p] : 0xFFFFFFFFu;  // txn 2^25 - 1 >= n: skipped
+      gg[u] = p < p_hi ? sg[p] : 0u;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++) {
+      const uint32_t t = vv[u] >> 7;
+      if (t >= n) continue;  // held-prefix request (or past the bucket)
+      const uint64_t x = (uint64_t)t * ulen + ((vv[u] >> 1) & 63u);
+      if (x >= d_lo && x < d_lo + w) win[x - d_lo] = gg[u];
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < w; i += 1024) group[d_lo + i] = win[i];
 }
 
 // acquire_locks' return (ycsb_txn.cpp:76-79): RCOK iff every request of the
@@ -834,7 +909,26 @@ static int calvin_sort_and_scan(dcc_ctx* ctx, const DevBatch& d, const uint32_t*
     uint32_t* agg = (uint32_t*)ctx->cv_agg.p;
     k_cv_up_l<K><<<(unsigned)tiles, 256, 0, st>>>(kb[cur], vb[cur], m, agg);
     k_cv_top_l<<<1, 256, 0, st>>>(agg, (uint32_t)tiles);
-    k_cv_down_l<K><<<(unsigned)tiles, 256, 0, st>>>(kb[cur], vb[cur], m, agg, so);
+    if (so.ulen && d.nnz >= CV_PUT_MIN) {
+      // groups in sorted order into the idle value buffer; one counting pass
+      // of (value, group) on the txn's top 8 bits; the windowed put
+      uint32_t* gs = vb[1 - cur];
+      k_cv_down_l<K><<<(unsigned)tiles, 256, 0, st>>>(kb[cur], vb[cur], m, agg, so, gs);
+      const uint64_t tmax = d.n + nh - 1;
+      const uint32_t tb = tmax ? 64u - (uint32_t)__builtin_clzll(tmax) : 1u;
+      const uint32_t tsh = tb > 8 ? tb - 8 : 0;
+      uint32_t* ko = (uint32_t*)kb[1 - cur];
+      uint32_t* go = (uint32_t*)kb[cur];
+      uint32_t* scratch = (uint32_t*)ctx->cv_scratch.p;
+      radix_pass_u32(vb[cur], gs, ko, go, m, 7 + tsh, scratch, st);
+      const uint64_t span = (1ull << tsh) * so.ulen;
+      const uint32_t H = (uint32_t)((span + CV_WIN - 1) / CV_WIN);
+      const uint32_t wh = (uint32_t)((span + H - 1) / H);
+      k_cv_put<<<256 * H, 1024, 0, st>>>(ko, go, scratch + 256 * rs_tiles(m), (uint32_t)d.n,
+                                         so.ulen, tsh, H, wh, so.group);
+    } else {
+      k_cv_down_l<K><<<(unsigned)tiles, 256, 0, st>>>(kb[cur], vb[cur], m, agg, so, nullptr);
+    }
   }
   CK(hipGetLastError());
   return DCC_OK;
