@@ -38,6 +38,7 @@ OPT_BATCH_MAX = 2
 OPT_SOLVER = 5
 OPT_SWEEP_LEVELS = 6
 OPT_HIST_MERGE = 7
+OPT_FAIL_RANK = 8
 
 
 class Batch(C.Structure):
@@ -180,6 +181,7 @@ _SIGS = [
     ("dcc_comm_size", C.c_int, [_P]),
     ("dcc_comm_destroy", C.c_int, [_P]),
     ("dcc_key_shard", C.c_uint32, [C.c_uint64, C.c_uint32]),
+    ("dcc_key_shard_n", C.c_int, [_P, C.c_uint64, C.c_uint32, _P]),
     ("dcc_shard_filter", C.c_int, [C.POINTER(Batch), C.c_uint32, C.c_uint32, _P, _P, _P,
                                    C.POINTER(C.c_uint64)]),
     ("dcc_occ_validate_epoch", C.c_int, [_P, C.POINTER(Batch), _P, _P, C.POINTER(Stats)]),

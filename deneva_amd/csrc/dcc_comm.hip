@@ -28,6 +28,7 @@ struct dcc_comm_state {
   void* user = nullptr;
   uint8_t* hbuf = nullptr;  // pinned staging for the host backend
   uint64_t hcap = 0;
+  bool aborted = false;     // ncclCommAbort ran (a peer rank failed)
 };
 
 int dcc_ctx::comm_ranks() const { return comm ? comm->nranks : 1; }
@@ -36,6 +37,7 @@ int dcc_ctx::comm_rank() const { return comm ? comm->rank : 0; }
 int dcc_ctx::comm_allreduce_max_u8(uint8_t* dev, uint64_t n) {
   dcc_ctx* ctx = this;
   if (!comm || comm->nranks <= 1 || n == 0) return DCC_OK;
+  if (comm->aborted) return fail(DCC_ECOMM, "communicator aborted (a peer rank failed)");
   if (comm->nccl) {
     const ncclResult_t r = ncclAllReduce(dev, dev, n, ncclUint8, ncclMax, comm->nccl, stream);
     if (r != ncclSuccess) return fail(DCC_ECOMM, "ncclAllReduce: %s", ncclGetErrorString(r));
@@ -65,6 +67,7 @@ int dcc_ctx::comm_allgather_u8(const uint8_t* send, uint8_t* recv, uint64_t byte
     const hipError_t e = hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, stream);
     return e == hipSuccess ? DCC_OK : hip_fail(e, "allgather copy");
   }
+  if (comm->aborted) return fail(DCC_ECOMM, "communicator aborted (a peer rank failed)");
   if (comm->nccl) {
     const ncclResult_t r = ncclAllGather(send, recv, bytes, ncclUint8, comm->nccl, stream);
     if (r != ncclSuccess) return fail(DCC_ECOMM, "ncclAllGather: %s", ncclGetErrorString(r));
@@ -116,12 +119,23 @@ extern "C" int dcc_comm_init(dcc_ctx* ctx, int rank, int nranks, const void* uni
 
 // dcc_init_multi: a sub-context joins the clique ncclCommInitAll made
 int dcc_comm_attach(dcc_ctx* ctx, int rank, int nranks, void* nccl_comm) {
+  if (!ctx || !nccl_comm || ctx->comm) return DCC_EINVAL;
   auto* c = new dcc_comm_state;
   c->rank = rank;
   c->nranks = nranks;
   c->nccl = (ncclComm_t)nccl_comm;
   ctx->comm = c;
   return DCC_OK;
+}
+
+// a peer failed: end this rank's pending RCCL collectives (multi context)
+void dcc_comm_abort(dcc_ctx* ctx) {
+  if (!ctx || !ctx->comm || ctx->comm->aborted) return;
+  ctx->comm->aborted = true;
+  if (ctx->comm->nccl) {
+    (void)ncclCommAbort(ctx->comm->nccl);
+    ctx->comm->nccl = nullptr;
+  }
 }
 
 extern "C" int dcc_comm_init_host(dcc_ctx* ctx, int rank, int nranks, dcc_exchange_fn fn,

@@ -84,8 +84,13 @@ struct dcc_ctx {
   uint64_t recheck_max = 16384;   // fold the kill wave into rounds with lists <= this
   uint32_t batch_max = 8;       // rounds enqueued between host synchronisations
   bool bars_used = false;       // this epoch's rounds used grid-barrier words
-  int solver = 0;               // 0 auto (sweep), 1 fixed-point rounds, 3 sweep
+  int solver = 0;               // 0 auto (= 4), 1 fixed-point rounds, 3 sweep, 4 level-0 sweep +
+                                // commit/kill rounds
   bool use_sweep() const { return solver != 1; }
+  bool use_ck() const { return solver == 0 || solver == 4; }
+  uint32_t ck_graph_rounds = 10;  // commit/kill rounds in the captured epoch
+  uint64_t ck_clean = 0;          // table slots known clean
+  bool ck_dirty = false;          // an epoch stopped before k_final reset its slots
   uint32_t sw_levels = 4;
   bool sw_debug = false;        // DCC_SW_DEBUG: per-tile clock stamps of the serial pass       // sweep levels enqueued between host synchronisations
   hipEvent_t pev[8] = {};  // phase boundary events (profiling only)
@@ -125,6 +130,7 @@ struct dcc_ctx {
   DevBuf sw_rec, sw_rk, sw_gtab, sw_fw, sw_aent, sw_mg;
   DevBuf sw_xcnt, sw_xsend, sw_xrec, sw_mcnt, sw_moff, sw_mkeys, sw_mat, sw_kill;  // key-sharded sweep  // sweep tile records
   SubBufs sw_list[2];                            // sweep level lists (ping-pong)
+  DevBuf ck_tab, ck_ctl, ck_aslot, ck_lst[2];    // commit/kill solver (occ_ck.hip)
   DevBuf l_tid[2], l_coff[2], l_cent[2];         // ping-pong undecided lists
   // OCC history (occ.h:62-64) on the device: base + delta levels
   HistStore hs[2];
@@ -141,7 +147,7 @@ struct dcc_ctx {
   DevBuf mt_misc, mt_slot, mt_sval, mt_slot2, mt_sval2, mt_sfl, mt_stx, mt_txn, mt_agg;
   DevBuf mt_sflB, mt_stxB, mt_k1, mt_tcnt;
   // GPU index (index.hip): key table, newest insert ordinal per key, rows
-  DevBuf ix_keys, ix_ord, ix_rows, ix_cnt, wv_buf;
+  DevBuf ix_keys, ix_ord, ix_rows, ix_cnt, wv_buf, ix_scr, wv_hbuf, wv_obuf;
   uint32_t ix_bits = 0;
   uint64_t ix_nkeys = 0, ix_nrows = 0;
   double ix_last_ms = 0;
@@ -183,6 +189,9 @@ struct dcc_ctx {
   int sweep_enqueue(const DevBatch& d, int l0, int l1, const dcc::SwShard* shard = nullptr,
                     bool resume = false, bool tail_serial = false);
   int sweep_sharded(const DevBatch& d, int& next_level);
+  int ck_reserve(const DevBatch& d);
+  int ck_enqueue(const DevBatch& d, uint32_t r0, uint32_t r1, bool build);  // rounds [r0, r1]
+  uint32_t ck_cap_bits = 0;
   int occ_sweep_finish(const DevBatch& d, int& next_level, bool& done, uint32_t maxlen);
   int occ_snapshot(const dcc_batch* b, const dcc_occ_snapshot* s, uint8_t* out_rc, dcc_stats* st);
   // MaaT (maat.hip): row timestamp table + epoch workspaces

@@ -176,8 +176,14 @@ extern "C" int dcc_set_profiling(dcc_ctx* ctx, int enable) {
   return DCC_OK;
 }
 
+int dcc_multi_set_fail_rank(dcc_ctx* ctx, int rank);  // dcc_multi.cpp
+
 extern "C" int dcc_set_option(dcc_ctx* ctx, int option, int64_t value) {
   if (!ctx) return DCC_EINVAL;
+  if (option == DCC_OPT_FAIL_RANK) {
+    if (!ctx->multi) return ctx->fail(DCC_EINVAL, "DCC_OPT_FAIL_RANK: multi-GPU contexts only");
+    return dcc_multi_set_fail_rank(ctx, (int)value);
+  }
   if (ctx->multi)
     for (int r = 0; r < dcc_multi_size(ctx); r++) {
       const int e = dcc_set_option(dcc_multi_sub(ctx, r), option, value);
@@ -189,7 +195,7 @@ extern "C" int dcc_set_option(dcc_ctx* ctx, int option, int64_t value) {
       ctx->recheck_max = (uint64_t)value;
       return DCC_OK;
     case DCC_OPT_SOLVER:
-      if (value != 0 && value != 1 && value != 3) return DCC_EINVAL;
+      if (value != 0 && value != 1 && value != 3 && value != 4) return DCC_EINVAL;
       ctx->solver = (int)value;
       return DCC_OK;
     case DCC_OPT_SWEEP_LEVELS:
@@ -226,8 +232,9 @@ std::vector<DevBuf*> dcc_ctx::all_bufs() {
                             &sw_xrec, &sw_mcnt, &sw_moff, &sw_mkeys, &sw_mat, &sw_kill,
                             &snap_top, &snap_aoff, &snap_aidx, &snap_cnt, &mt_rk, &mt_rlr, &mt_rlw,
                             &mt_misc, &mt_slot, &mt_sval, &mt_slot2, &mt_sval2, &mt_sfl,
-                            &mt_stx, &mt_txn, &mt_agg, &mt_sflB, &mt_stxB, &mt_k1, &mt_tcnt, &ix_keys, &ix_ord, &ix_rows, &ix_cnt, &wv_buf,
-                            &h_K[0], &h_K[1], &h_V[0], &h_V[1], &h_scr, &h_bsum};
+                            &mt_stx, &mt_txn, &mt_agg, &mt_sflB, &mt_stxB, &mt_k1, &mt_tcnt, &ix_keys, &ix_ord, &ix_rows, &ix_cnt, &wv_buf, &ix_scr, &wv_hbuf, &wv_obuf,
+                            &h_K[0], &h_K[1], &h_V[0], &h_V[1], &h_scr, &h_bsum,
+                            &ck_tab, &ck_ctl, &ck_aslot, &ck_lst[0], &ck_lst[1]};
   for (auto& h : hs)
     for (DevBuf* b : {&h.fk, &h.ft, &h.skey, &h.stn, &h.hash}) v.push_back(b);
   for (auto& sb : sw_list)

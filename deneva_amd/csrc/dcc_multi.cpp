@@ -27,18 +27,42 @@
 #include "dcc_ctx.h"
 
 int dcc_comm_attach(dcc_ctx* ctx, int rank, int nranks, void* nccl_comm);  // dcc_comm.hip
+void dcc_comm_abort(dcc_ctx* ctx);                                          // dcc_comm.hip
 
 namespace {
 
-// Byte-wise MAX all-reduce among the host threads of one process.
+// Byte-wise MAX all-reduce among the host threads of one process.  Each
+// generation's result (and its size-mismatch flag) lives in the slot of the
+// generation's parity: a slow waiter of generation g reads slot g & 1, which
+// only generation g + 2 rewrites -- and g + 1 cannot complete before that
+// waiter arrives at it.  A failing rank poisons the exchange: every waiter
+// and every later arrival returns at once with an error, so no rank blocks
+// on a peer that will never arrive.
 struct LocalExchange {
   int n = 0;
   std::mutex mu;
   std::condition_variable cv;
   uint64_t gen = 0;
   int arrived = 0;
-  bool bad = false;
-  std::vector<uint8_t> acc, result;
+  bool bad = false;        // the open generation's size mismatch
+  bool poisoned = false;   // a rank failed this epoch
+  std::vector<uint8_t> acc;
+  std::vector<uint8_t> result[2];
+  bool result_bad[2] = {false, false};
+  void poison() {
+    std::lock_guard<std::mutex> lk(mu);
+    poisoned = true;
+    cv.notify_all();
+  }
+  // between epochs (no rank inside): a clean exchange
+  void reset() {
+    std::lock_guard<std::mutex> lk(mu);
+    poisoned = false;
+    arrived = 0;
+    bad = false;
+    acc.clear();
+    gen += 2;  // keeps the slot parity meaning of any stale waiter moot
+  }
 };
 struct LocalPart {
   LocalExchange* x;
@@ -49,6 +73,7 @@ int local_exchange(void* user, uint8_t* buf, uint64_t nb) {
   LocalPart* p = (LocalPart*)user;
   LocalExchange* X = p->x;
   std::unique_lock<std::mutex> lk(X->mu);
+  if (X->poisoned) return 1;
   const uint64_t g = X->gen;
   if (X->arrived == 0) {
     X->acc.assign(buf, buf + nb);
@@ -59,15 +84,18 @@ int local_exchange(void* user, uint8_t* buf, uint64_t nb) {
     for (uint64_t i = 0; i < nb; i++) X->acc[i] = std::max(X->acc[i], buf[i]);
   }
   if (++X->arrived == X->n) {
-    X->result.swap(X->acc);
+    X->result[g & 1].swap(X->acc);
+    X->result_bad[g & 1] = X->bad;
     X->arrived = 0;
     X->gen++;
     X->cv.notify_all();
   } else {
-    X->cv.wait(lk, [&] { return X->gen != g; });
+    X->cv.wait(lk, [&] { return X->gen != g || X->poisoned; });
+    if (X->gen == g) return 1;  // poisoned before the generation completed
   }
-  if (X->bad || X->result.size() != nb) return 1;
-  memcpy(buf, X->result.data(), nb);
+  const std::vector<uint8_t>& res = X->result[g & 1];
+  if (X->result_bad[g & 1] || res.size() != nb) return 1;
+  memcpy(buf, res.data(), nb);
   return 0;
 }
 
@@ -113,30 +141,70 @@ struct dcc_multi {
   std::vector<dcc_ctx*> sub;
   LocalExchange lx;
   std::vector<LocalPart> parts;
+  bool rccl = false;        // the sub-contexts share an RCCL clique
+  bool broken = false;      // the clique was aborted after a rank failed
+  int fail_rank = -1;       // DCC_OPT_FAIL_RANK (fault injection, tests)
+  std::mutex fail_mu;
+  bool failing = false;     // a rank of the running epoch failed
 };
 
+// A rank failed: its peers must not wait for it.  The host exchange is
+// poisoned (waiters return an error at once); the RCCL clique is aborted
+// (ncclCommAbort ends the peers' pending collectives) and the context stays
+// unusable until it is destroyed.
+static void fail_fast(dcc_multi* M) {
+  std::lock_guard<std::mutex> lk(M->fail_mu);
+  if (M->failing) return;
+  M->failing = true;
+  M->lx.poison();
+  if (M->rccl) {
+    for (dcc_ctx* s : M->sub) dcc_comm_abort(s);
+    M->broken = true;
+  }
+}
+
 // Runs fn(rank) on one host thread per sub-context; the first failure's code
-// and message become the multi context's.
+// and message become the multi context's.  A failing rank makes every other
+// rank fail too (fail_fast) instead of leaving it blocked in an exchange.
 template <typename F>
 static int run_ranks(dcc_ctx* ctx, F fn) {
   dcc_multi* M = ctx->multi;
+  if (M->broken)
+    return ctx->fail(DCC_ECOMM, "multi-GPU: the RCCL clique was aborted after a rank failed; "
+                                "destroy and re-create the context");
   const int R = (int)M->sub.size();
+  M->lx.reset();
+  M->failing = false;
+  const int inject = M->fail_rank;
+  M->fail_rank = -1;  // one-shot
   std::vector<int> rc(R, DCC_OK);
   std::vector<std::thread> th;
   for (int r = 0; r < R; r++)
     th.emplace_back([&, r] {
       if (hipSetDevice(M->sub[r]->device) != hipSuccess) {
         rc[r] = DCC_ENODEV;
-        return;
+      } else if (r == inject) {
+        rc[r] = M->sub[r]->fail(DCC_EIO, "injected failure (DCC_OPT_FAIL_RANK)");
+      } else {
+        rc[r] = fn(r, M->sub[r]);
       }
-      rc[r] = fn(r, M->sub[r]);
+      if (rc[r] != DCC_OK) fail_fast(M);
     });
   for (auto& t : th) t.join();
+  // the first rank that failed on its own (the others report the poisoning)
+  int first = -1;
   for (int r = 0; r < R; r++)
-    if (rc[r] != DCC_OK) {
-      ctx->last_error = "rank " + std::to_string(r) + ": " + M->sub[r]->last_error;
-      return rc[r];
-    }
+    if (rc[r] != DCC_OK && (first < 0 || (rc[first] == DCC_ECOMM && rc[r] != DCC_ECOMM))) first = r;
+  if (first >= 0) {
+    ctx->last_error = "rank " + std::to_string(first) + ": " + M->sub[first]->last_error;
+    return rc[first];
+  }
+  return DCC_OK;
+}
+
+int dcc_multi_set_fail_rank(dcc_ctx* ctx, int rank) {
+  if (!ctx->multi || rank < -1 || rank >= (int)ctx->multi->sub.size()) return DCC_EINVAL;
+  ctx->multi->fail_rank = rank;
   return DCC_OK;
 }
 
@@ -161,6 +229,7 @@ extern "C" int dcc_init_multi(dcc_ctx** out, int n_gpus, const int* device_ids) 
     const std::set<int> distinct(device_ids, device_ids + n_gpus);
     if ((int)distinct.size() == n_gpus) {
       // one RCCL clique over the node's GPUs (xGMI), one communicator per rank
+      // (unverified on hardware: the test box has one GPU)
       std::vector<ncclComm_t> comms(n_gpus);
       const ncclResult_t e = ncclCommInitAll(comms.data(), n_gpus, device_ids);
       if (e != ncclSuccess) {
@@ -168,7 +237,16 @@ extern "C" int dcc_init_multi(dcc_ctx** out, int n_gpus, const int* device_ids) 
         dcc_destroy(root);
         return DCC_ECOMM;
       }
-      for (int i = 0; i < n_gpus; i++) dcc_comm_attach(M->sub[i], i, n_gpus, comms[i]);
+      M->rccl = true;
+      for (int i = 0; i < n_gpus; i++) {
+        r = dcc_comm_attach(M->sub[i], i, n_gpus, comms[i]);
+        if (r != DCC_OK) {
+          // the attached ones go with their sub-contexts; the rest here
+          for (int j = i; j < n_gpus; j++) (void)ncclCommDestroy(comms[j]);
+          dcc_destroy(root);
+          return r;
+        }
+      }
     } else {
       // shards sharing a GPU: the in-process host exchange
       M->lx.n = n_gpus;

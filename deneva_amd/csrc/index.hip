@@ -177,7 +177,15 @@ int dcc_ctx::index_reserve(uint64_t want) {
   while ((1ull << bits) < 2 * want) bits++;
   if (bits > 34) return fail(DCC_ERANGE, "index: more than 2^33 keys");
   const uint64_t cap = 1ull << bits;
+  // the new table: released on every error return, moved in on success
   DevBuf nk, no;
+  struct Guard {
+    DevBuf *a, *b;
+    ~Guard() {
+      if (a) a->release();
+      if (b) b->release();
+    }
+  } guard{&nk, &no};
   CR(nk.ensure(this, cap * 8, "index keys"));
   CR(no.ensure(this, cap * 8, "index ordinals"));
   CK(hipMemsetAsync(nk.p, 0xFF, cap * 8, stream));
@@ -192,6 +200,7 @@ int dcc_ctx::index_reserve(uint64_t want) {
   ix_ord.release();
   ix_keys = nk;
   ix_ord = no;
+  guard.a = guard.b = nullptr;
   ix_bits = bits;
   return DCC_OK;
 }
@@ -212,7 +221,8 @@ extern "C" int dcc_index_insert(dcc_ctx* ctx, const uint64_t* keys, const uint64
     ctx->ix_rows.release();
     ctx->ix_rows = nr;
   }
-  DevBuf tk;
+  // host keys staged in the context's grow-only scratch (no per-call allocation)
+  DevBuf& tk = ctx->ix_scr;
   CR(tk.ensure(ctx, n * 8, "index insert keys"));
   CR(ctx->ix_cnt.ensure(ctx, 64, "index counters"));
   CK(hipMemcpyAsync(tk.p, keys, n * 8, hipMemcpyHostToDevice, ctx->stream));
@@ -226,7 +236,6 @@ extern "C" int dcc_index_insert(dcc_ctx* ctx, const uint64_t* keys, const uint64
   uint32_t c[2];
   CK(hipMemcpyAsync(c, ctx->ix_cnt.p, 8, hipMemcpyDeviceToHost, ctx->stream));
   CK(hipStreamSynchronize(ctx->stream));
-  tk.release();
   ctx->ix_nkeys += c[0];
   ctx->ix_nrows += n;
   if (c[1]) return ctx->fail(DCC_EINVAL, "index: key equal to DCC_KEY_RESERVED");
@@ -246,13 +255,12 @@ extern "C" int dcc_index_probe(dcc_ctx* ctx, const uint64_t* keys, uint64_t n, u
   if (!ctx->ix_rows.p) CR(ctx->ix_rows.ensure(ctx, 4096, "index rows"));
   const uint64_t* dk = keys;
   uint64_t* dout = out_rows;
-  DevBuf tk, to;
-  if (!dev) {
-    CR(tk.ensure(ctx, n * 8, "probe keys"));
-    CR(to.ensure(ctx, n * 8, "probe rows"));
-    CK(hipMemcpyAsync(tk.p, keys, n * 8, hipMemcpyHostToDevice, ctx->stream));
-    dk = (const uint64_t*)tk.p;
-    dout = (uint64_t*)to.p;
+  if (!dev) {  // host pointers: keys and rows staged in the grow-only scratch
+    CR(ctx->ix_scr.ensure(ctx, n * 16, "probe keys + rows"));
+    uint64_t* tk = (uint64_t*)ctx->ix_scr.p;
+    CK(hipMemcpyAsync(tk, keys, n * 8, hipMemcpyHostToDevice, ctx->stream));
+    dk = tk;
+    dout = tk + n;
   }
   CK(hipMemsetAsync(ctx->ix_cnt.p, 0, 16, ctx->stream));
   CK(hipEventRecord(ctx->ev0, ctx->stream));
@@ -310,15 +318,16 @@ extern "C" int dcc_calvin_dispatch(dcc_ctx* ctx, const uint32_t* wave, const uin
   uint32_t* mx = w + 5 * n;
   const uint32_t* dwave = wave;
   const uint64_t* dorder = order;
-  DevBuf tw, to;
+  // host pointers: order and waves staged in the grow-only scratch
   if (!dev) {
-    CR(tw.ensure(ctx, n * 4, "dispatch waves"));
-    CK(hipMemcpyAsync(tw.p, wave, n * 4, hipMemcpyHostToDevice, st));
-    dwave = (const uint32_t*)tw.p;
+    CR(ctx->wv_hbuf.ensure(ctx, n * 8 + n * 4 + 64, "dispatch staging"));
+    uint64_t* to = (uint64_t*)ctx->wv_hbuf.p;
+    uint32_t* tw = (uint32_t*)(to + n);
+    CK(hipMemcpyAsync(tw, wave, n * 4, hipMemcpyHostToDevice, st));
+    dwave = tw;
     if (order) {
-      CR(to.ensure(ctx, n * 8, "dispatch order"));
-      CK(hipMemcpyAsync(to.p, order, n * 8, hipMemcpyHostToDevice, st));
-      dorder = (const uint64_t*)to.p;
+      CK(hipMemcpyAsync(to, order, n * 8, hipMemcpyHostToDevice, st));
+      dorder = to;
     }
   }
   CR(ctx->cv_scratch.ensure(ctx, rs_scratch_words(n) * 4 + 64, "radix scratch"));
@@ -343,11 +352,10 @@ extern "C" int dcc_calvin_dispatch(dcc_ctx* ctx, const uint32_t* wave, const uin
   uint32_t bits = 0;
   while (bits < 32 && (1ull << bits) <= hmx) bits++;
   const int c = radix_sort_u32(kb, vb, n, bits, (uint32_t*)ctx->cv_scratch.p, st);
-  DevBuf toff;
   uint32_t* doff = dev ? out_wave_off : nullptr;
   if (out_wave_off && !dev) {
-    CR(toff.ensure(ctx, ((uint64_t)nw + 1) * 4, "dispatch offsets"));
-    doff = (uint32_t*)toff.p;
+    CR(ctx->wv_obuf.ensure(ctx, ((uint64_t)nw + 1) * 4, "dispatch offsets"));
+    doff = (uint32_t*)ctx->wv_obuf.p;
   }
   if (doff) k_wv_off<<<g256(n), 256, 0, st>>>(kb[c], n, nw, doff);
   CK(hipGetLastError());

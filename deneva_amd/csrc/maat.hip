@@ -165,6 +165,25 @@ __global__ __launch_bounds__(256) void k_mt_get(const uint64_t* keys, uint64_t n
   }
 }
 
+// ---------------------------------------------------------------- check
+// The batch's validity before the persistent row table changes: offsets
+// (monotone, 0 .. nnz, <= MAX_ROW_PER_TXN per txn) and no reserved key.  A
+// rejected epoch leaves the row table (rows and timestamps) untouched.
+__global__ __launch_bounds__(256) void k_mt_check(const uint32_t* off, uint64_t n,
+                                                  const uint64_t* keys, uint64_t nnz,
+                                                  uint32_t* err) {
+  uint32_t e = 0;
+  const uint64_t t0 = (uint64_t)blockIdx.x * 256 + threadIdx.x, stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t t = t0; t < n; t += stride) {
+    const uint32_t o0 = off[t], o1 = off[t + 1];
+    if (o1 < o0 || o1 - o0 > MAX_TXN_LEN) e |= MT_ERR_OFF;
+    if ((t == 0 && o0 != 0) || (t + 1 == n && o1 != nnz)) e |= MT_ERR_OFF;
+  }
+  for (uint64_t x = t0; x < nnz; x += stride)
+    if (keys[x] == DCC_KEY_RESERVED) e |= MT_ERR_KEY;
+  if (e) atomicOr(err, e);
+}
+
 // ---------------------------------------------------------------- base
 // Access-parallel: every access enters its row (slot id) in the table.
 __global__ __launch_bounds__(256) void k_mt_slots(const uint64_t* keys, uint64_t nnz, uint64_t* rk,
@@ -713,6 +732,16 @@ int dcc_ctx::maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, 
     }
   }
 
+  // reject a malformed batch before the row table changes (one small sync)
+  k_mt_check<<<g1(std::max<uint64_t>(n, m), 2048), 256, 0, stream>>>(d.off, n, d.keys, m, cnt + 1);
+  CK(hipGetLastError());
+  CK(hipMemcpyAsync(hmisc, cnt + 1, 4, hipMemcpyDeviceToHost, stream));
+  CK(hipStreamSynchronize(stream));
+  {
+    const uint32_t e = *(const uint32_t*)hmisc;
+    if (e & MT_ERR_OFF) return fail(DCC_EINVAL, "batch: malformed offsets");
+    if (e & MT_ERR_KEY) return fail(DCC_EINVAL, "batch: key equal to DCC_KEY_RESERVED");
+  }
   CK(hipEventRecord(ev0, stream));
   // every access gets a slot / owner / sort value even in a malformed batch
   CK(hipMemsetAsync(mt_slot.p, 0, mm * 4, stream));
@@ -800,11 +829,11 @@ int dcc_ctx::maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, 
   CK(hipMemcpyAsync(hmisc, cnt, 32, hipMemcpyDeviceToHost, stream));
   CK(hipStreamSynchronize(stream));
   const uint32_t* hc = (const uint32_t*)hmisc;
+  mt_rows = hc[0];  // rows inserted this epoch stay in the table whatever follows
   if (hc[1] & MT_ERR_OFF) return fail(DCC_EINVAL, "batch: malformed offsets");
   if (hc[1] & MT_ERR_KEY) return fail(DCC_EINVAL, "batch: key equal to DCC_KEY_RESERVED");
   if (hc[1] & MT_ERR_FULL) return fail(DCC_EIO, "maat: row table full");
   if (hc[3]) return fail(DCC_EIO, "maat: %u undecided transactions", hc[3]);
-  mt_rows = hc[0];
   float ms = 0;
   CK(hipEventElapsedTime(&ms, ev0, ev1));
   S.rounds = rounds;

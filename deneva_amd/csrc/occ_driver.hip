@@ -552,6 +552,65 @@ int dcc_ctx::sweep_sharded(const DevBatch& d, int& next_level) {
 }
 
 
+// ---------------------------------------------------------------------------
+// Commit/kill round solver (occ_ck.hip) over level 0's survivors.  The key
+// table is sized for every access of the epoch at <= 50 % load (a list that
+// does not fit goes to the round solver) and kept clean between epochs by
+// k_final, so only a new, grown or abandoned table is filled here (before any
+// capture).
+static constexpr size_t CK_HCTL = 15360;  // ck counter ring copy inside `hmisc`
+int dcc_ctx::ck_reserve(const DevBatch& d) {
+  dcc_ctx* ctx = this;
+  uint32_t bits = 10;
+  while (bits < 30 && (1ull << bits) < std::max<uint64_t>(1024, d.nnz)) bits++;
+  const uint64_t slots = 1ull << bits;
+  const void* old = ck_tab.p;
+  CR(ck_tab.ensure(this, slots * sizeof(CkSlot), "commit/kill key table"));
+  if (ck_tab.p != old) ck_clean = 0;
+  CR(ck_ctl.ensure(this, CK_CTL_WORDS * 4, "commit/kill control"));
+  CR(ck_aslot.ensure(this, std::max<uint64_t>(64, d.nnz * 4), "commit/kill access slots"));
+  for (DevBuf& l : ck_lst) CR(l.ensure(this, d.n * 4 + 64, "commit/kill lists"));
+  const uint64_t have = ck_tab.cap / sizeof(CkSlot);
+  ck_cap_bits = 0;
+  while ((2ull << ck_cap_bits) <= have) ck_cap_bits++;
+  if (ck_dirty || ck_clean < have) {
+    launch_ck_fill((CkSlot*)ck_tab.p, have, stream);
+    CK(hipGetLastError());
+    ck_clean = have;
+    ck_dirty = false;
+  }
+  return DCC_OK;
+}
+
+// build (round 1's inputs) and rounds [r0, r1] on the engine stream
+int dcc_ctx::ck_enqueue(const DevBatch& d, uint32_t r0, uint32_t r1, bool build) {
+  dcc_ctx* ctx = this;
+  (void)d;
+  SwLevel* ctl = (SwLevel*)sw_ctl.p;
+  const SubBufs& b = sw_list[0];  // level 0's filter writes list 1 here
+  CkArgs a{};
+  a.tid1 = (const uint32_t*)b.tid.p;
+  a.off1 = (const uint32_t*)b.off.p;
+  a.keys1 = (const uint64_t*)b.keys.p;
+  a.at1 = (const uint8_t*)b.acctype.p;
+  a.lv1 = ctl + 1;
+  a.abandon = (const uint32_t*)(ctl + SW_MAX_LEVEL + 1);
+  a.abandon_out = (uint32_t*)(ctl + SW_MAX_LEVEL + 1);
+  a.tab = (CkSlot*)ck_tab.p;
+  a.cap_bits = ck_cap_bits;
+  a.ctl = (uint32_t*)ck_ctl.p;
+  a.aslot = (uint32_t*)ck_aslot.p;
+  a.lst[0] = (uint32_t*)ck_lst[0].p;
+  a.lst[1] = (uint32_t*)ck_lst[1].p;
+  a.state = (uint8_t*)state.p;
+  a.err = (uint32_t*)misc.p;
+  if (build) launch_ck_build(a, (unsigned)n_cu * 2, stream);
+  for (uint32_t r = r0; r <= r1; r++)
+    launch_ck_round(a, r, r <= 2 ? (unsigned)n_cu * 2 : (unsigned)n_cu / 2, stream);
+  CK(hipGetLastError());
+  return DCC_OK;
+}
+
 int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dcc_stats* st) {
   dcc_ctx* ctx = this;
   // key-sharded across ranks: this rank holds only its keys
@@ -570,6 +629,9 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   CR(stage_batch(b, d));
   const bool sweep = use_sweep();
   if (sweep) CR(sweep_reserve(d));
+  // level 0 of the sweep, then the commit/kill rounds (single GPU)
+  const bool ck = sweep && use_ck() && !sh;
+  if (ck) CR(ck_reserve(d));
   CR(state.ensure(this, d.n + 16, "state"));
   CR(hasw.ensure(this, d.n + 16, "hasw"));
   CR(rc.ensure(this, d.n + 16, "rc"));
@@ -586,7 +648,8 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   const bool hist_on = d.start_tn && hist_size() > 0;
   const bool graph_ok = sweep && !profiling && !sw_debug && !want_tn && !hist_on && !sh &&
                         !getenv("DCC_NO_GRAPH");
-  const GraphKey gkey{d.off, d.keys, d.acctype, d.n, d.nnz, out_rc, dev_out, sw_levels, buf_gen};
+  const GraphKey gkey{d.off, d.keys, d.acctype, d.n, d.nnz, out_rc, dev_out,
+                      ck ? 1000u + ck_graph_rounds : sw_levels, buf_gen};
   bool replay = graph_ok && graph_exec && gkey == graph_key;
   bool capturing = false;
   // a failure while capturing must still end the capture
@@ -669,10 +732,15 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   int serial_tail = -1;  // level enqueued without its filter (sweep_enqueue tail_serial)
   if (sweep) {
     if (profiling) CK(hipEventRecord(pev[0], stream));
-    next_level = (int)std::min<uint32_t>(sw_levels, SW_MAX_LEVEL - 1);
-    if (!sh && next_level >= 2) serial_tail = next_level - 1;
-    if (sh) CR(sweep_sharded(d, next_level));
-    else if (!replay) CR(sweep_enqueue(d, 0, next_level, nullptr, false, serial_tail >= 0));
+    next_level = ck ? 1 : (int)std::min<uint32_t>(sw_levels, SW_MAX_LEVEL - 1);
+    if (!sh && !ck && next_level >= 2) serial_tail = next_level - 1;
+    if (ck) ck_dirty = true;  // until k_final has reset the table's slots
+    if (sh) {
+      CR(sweep_sharded(d, next_level));
+    } else if (!replay) {
+      CR(sweep_enqueue(d, 0, next_level, nullptr, false, serial_tail >= 0));
+      if (ck) CR(ck_enqueue(d, 1, ck_graph_rounds, true));
+    }
   } else {
     CR(occ_rounds(top, maxlen, profiling, rounds));
   }
@@ -682,6 +750,9 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   uint8_t* rc_dev = (dev_out && out_rc) ? out_rc : (uint8_t*)rc.p;
   uint32_t* cf = want_tn ? (uint32_t*)cflag.p : nullptr;
   uint64_t* tn_dev = want_tn ? ((dev_out && out_tn) ? out_tn : (uint64_t*)tn.p) : nullptr;
+  uint32_t ck_last = ck_graph_rounds;  // the last commit/kill round enqueued
+  SwLevel* const ctl_d = (SwLevel*)sw_ctl.p;
+  uint32_t* const ck_cnt_d = (uint32_t*)ck_ctl.p + CK_CTL_RING;
   auto enqueue_final = [&]() -> int {
     if (replay) {  // once: a second finalize (after more levels) runs directly
       replay = false;
@@ -701,8 +772,16 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
     job(hmisc_dev, misc.p, 64);
     job((char*)hmisc_dev + MISC_BARS, (char*)misc.p + MISC_BARS, CTR_RING * 16);
     if (sweep) job((char*)hmisc_dev + SW_HCTL, sw_ctl.p, sw_ctl_bytes());
+    if (ck) job((char*)hmisc_dev + CK_HCTL, ck_ctl.p, CK_CTL_WORDS * 4);
     FinalArgs fa{d.n, (const uint8_t*)state.p, (const uint8_t*)hasw.p, rc_dev, cf,
                  (FinalPart*)hpart_dev};
+    if (ck) {
+      fa.ck_tab = (CkSlot*)ck_tab.p;
+      fa.ck_aslot = (const uint32_t*)ck_aslot.p;
+      fa.ck_acc = &ctl_d[1].acc;
+      fa.ck_live = ck_cnt_d + (ck_last + 1) % CK_RING;
+      fa.ck_abandon = (const uint32_t*)(ctl_d + SW_MAX_LEVEL + 1);
+    }
     launch_final(fa, ga, stream);
     if (want_tn) launch_commit_tn(cf, d.n, (uint64_t*)bsum.p, tnc, tn_dev, stream);
     CK(hipGetLastError());
@@ -747,7 +826,45 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
                   MAX_TXN_LEN);
     // more levels, or hand the remaining list to the round solver
     bool again = false;
-    for (;;) {
+    uint32_t ck_rounds = 0;
+    bool ck_done = false;
+    if (ck) {
+      // the commit/kill rounds: the captured ones, then more in batches
+      // until the list is empty (unless level 0 or the build handed it off)
+      const SwLevel* hc = (const SwLevel*)((const char*)hmisc + SW_HCTL);
+      const uint32_t ab = *(const uint32_t*)(hc + SW_MAX_LEVEL + 1);
+      const uint32_t e = *(const uint32_t*)hmisc;
+      if (!ab && !(e & (ERR_SPIN | ERR_TILE | ERR_FULL))) {
+        ck_done = true;
+        const uint32_t* hcnt = (const uint32_t*)((const char*)hmisc + CK_HCTL) + CK_CTL_RING;
+        const uint32_t m1 = hc[1].m;
+        auto count = [&](uint32_t r0, uint32_t r1) {  // rounds in [r0, r1] with a list
+          for (uint32_t r = r0; r <= r1; r++)
+            if (r == 1 ? m1 > 0 : hcnt[r % CK_RING] > 0) ck_rounds++;
+        };
+        uint32_t R = ck_graph_rounds;
+        count(1, R);
+        while (hcnt[(R + 1) % CK_RING]) {
+          const uint32_t B = 32;  // <= CK_RING - 2: the batch's counters stay intact
+          CR(ck_enqueue(d, R + 1, R + B, false));
+          GatherArgs ga{};
+          ga.job[ga.n++] = CopyJob{(const uint32_t*)ck_ctl.p,
+                                   (uint32_t*)((char*)hmisc_dev + CK_HCTL), CK_CTL_WORDS};
+          ga.job[ga.n++] = CopyJob{(const uint32_t*)misc.p, (uint32_t*)hmisc_dev, 16};
+          launch_gather(ga, stream);
+          CK(hipGetLastError());
+          CK(hipStreamSynchronize(stream));
+          count(R + 1, R + B);
+          R += B;
+          if (R > m1 + 2 * B) return fail(DCC_EIO, "commit/kill rounds did not converge");
+        }
+        if (R != ck_last) {
+          ck_last = R;
+          again = true;  // finalize again: the captured k_final ran before these rounds
+        }
+      }
+    }
+    for (; !ck_done;) {
       const SwLevel* hc = (const SwLevel*)((const char*)hmisc + SW_HCTL);
       const uint32_t ab = *(const uint32_t*)(hc + SW_MAX_LEVEL + 1);
       const uint32_t e = *(const uint32_t*)hmisc;
@@ -887,6 +1004,7 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
     info.prefix = hc[0].pos;
     info.survivors = hc[1].m;
     for (int l = 0; l < next_level && (l == 0 || hc[l].m); l++) rounds++;
+    rounds += ck_rounds;
   }
 
   const uint32_t e = *(const uint32_t*)hmisc;
@@ -912,6 +1030,7 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   }
   if (n_und) return fail(DCC_EIO, "%llu undecided transactions after convergence",
                          (unsigned long long)n_und);
+  if (ck) ck_dirty = false;  // k_final reset the slots (or the list never used them)
   float ms = 0;
   CK(hipEventElapsedTime(&ms, ev0, ev1));
   S.rounds = rounds;

@@ -7,6 +7,7 @@
 namespace dcc {
 
 struct Slot;
+struct CkSlot;
 
 constexpr int TILE_CAP = 1024;  // accesses staged per wave (LDS), build kernel
 constexpr int ROUND_CAP = 512;  // accesses staged per wave, round / publish kernels
@@ -122,6 +123,13 @@ struct FinalArgs {
   uint8_t* rc;
   uint32_t* cflag;
   FinalPart* part;  // [FINAL_BLOCKS] (pinned host memory: read back directly)
+  // commit/kill solver: reset the table slots its list used, once every
+  // round has run (ck_live: the undecided count after the last enqueued round)
+  struct CkSlot* ck_tab;
+  const uint32_t* ck_aslot;
+  const uint32_t* ck_acc;
+  const uint32_t* ck_live;
+  const uint32_t* ck_abandon;
 };
 
 // sub-list decisions back to the epoch's state bytes (round-solver hand-off)
@@ -332,6 +340,40 @@ void launch_sw_share(const uint32_t* m_dev, uint32_t m_host, const uint32_t* aba
 void launch_sw_merge(const SwList& in, uint32_t P, uint32_t* xbuf, uint32_t xoff_words,
                      uint32_t n_all, uint32_t* cnt, uint32_t* cur, uint32_t* moff,
                      uint64_t* mkeys, uint8_t* mat, bool export_only, hipStream_t st);
+
+// ---- commit/kill round solver over the level-0 survivors (occ_ck.hip)
+struct __attribute__((aligned(32))) CkSlot {
+  uint64_t key;   // KEY_EMPTY: free
+  uint32_t c;     // the key's committed writer (list position), ~0u: none
+  uint32_t pad;
+  uint64_t u[2];  // smallest undecided writer at the start of round r: u[r & 1]
+};
+constexpr uint32_t CK_WR = 0x80000000u;   // aslot: the access is a write
+constexpr uint32_t CK_NONE = 0x7FFFFFFFu; // aslot: no slot (reserved key)
+constexpr uint32_t CK_RING = 64;          // per-round list counters kept on the device
+constexpr uint32_t CK_CTL_MASK = 0;       // ctl word: the table's slot mask this epoch
+constexpr uint32_t CK_CTL_RING = 16;      // ctl words [16, 16 + CK_RING): list counters
+constexpr uint32_t CK_CTL_WORDS = CK_CTL_RING + CK_RING;
+constexpr uint32_t CK_U = 4;              // slot loads in flight per lane
+struct CkArgs {
+  const uint32_t* tid1;   // the list (level 0's survivors, index order): txn ids,
+  const uint32_t* off1;   // offsets (0-based), keys and access types
+  const uint64_t* keys1;
+  const uint8_t* at1;
+  const SwLevel* lv1;     // its length and access count (device)
+  const uint32_t* abandon;
+  uint32_t* abandon_out;  // = 1: the list goes to the fixed-point round solver
+  CkSlot* tab;            // [1 << cap_bits] clean slots
+  uint32_t cap_bits;
+  uint32_t* ctl;          // [CK_CTL_WORDS]
+  uint32_t* aslot;        // [list accesses] slot | CK_WR
+  uint32_t* lst[2];       // undecided list positions, by round parity
+  uint8_t* state;         // the epoch's state bytes
+  uint32_t* err;
+};
+void launch_ck_build(const CkArgs& a, unsigned grid, hipStream_t st);
+void launch_ck_round(const CkArgs& a, uint32_t r, unsigned grid, hipStream_t st);
+void launch_ck_fill(CkSlot* tab, uint64_t n, hipStream_t st);
 
 // Several word fills in one launch (replaces a run of hipMemsetAsync calls,
 // each of which costs a dispatch and an idle gap on the stream).

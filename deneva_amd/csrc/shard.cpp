@@ -13,6 +13,12 @@ extern "C" uint32_t dcc_key_shard(uint64_t key, uint32_t nranks) {
   return (uint32_t)((((unsigned __int128)h) * nranks) >> 64);
 }
 
+extern "C" int dcc_key_shard_n(const uint64_t* keys, uint64_t n, uint32_t nranks, uint32_t* out) {
+  if ((n && (!keys || !out)) || nranks == 0) return DCC_EINVAL;
+  for (uint64_t i = 0; i < n; i++) out[i] = dcc_key_shard(keys[i], nranks);
+  return DCC_OK;
+}
+
 extern "C" int dcc_shard_filter(const dcc_batch* in, uint32_t rank, uint32_t nranks,
                                 uint32_t* out_offsets, uint64_t* out_keys, uint8_t* out_acctype,
                                 uint64_t* out_nnz) {

@@ -414,6 +414,14 @@ def key_shard(key: int, nranks: int) -> int:
     return int(lib.dcc_key_shard(key, nranks))
 
 
+def shard_of_keys(keys, nranks: int) -> np.ndarray:
+    """dcc_key_shard of every key (u32 array)."""
+    k = np.ascontiguousarray(keys, dtype=np.uint64)
+    out = np.empty(max(k.size, 1), np.uint32)
+    _check(lib.dcc_key_shard_n(_ptr(k), k.size, nranks, _ptr(out)))
+    return out[: k.size]
+
+
 def shard_filter(batch: EpochBatch, rank: int, nranks: int) -> EpochBatch:
     n, nnz = batch.n_txn, batch.nnz
     off = np.empty(n + 1, np.uint32)

@@ -148,12 +148,16 @@ int dcc_set_profiling(dcc_ctx* ctx, int enable);
 /* Tuning knobs (defaults are the tuned values; for A/B measurement). */
 #define DCC_OPT_RECHECK 1     /* fold kill waves into rounds whose list has <= value txns */
 #define DCC_OPT_BATCH_MAX 2   /* max rounds enqueued between host synchronisations        */
-#define DCC_OPT_SOLVER 5      /* OCC solver: 0 auto (= 3), 1 fixed-point rounds only, 3 sweep
-                                 (key-sharded too; hands lists that stop shrinking to the
-                                 round solver)                                             */
+#define DCC_OPT_SOLVER 5      /* OCC solver: 0 auto (= 4; 3 when key-sharded), 1 fixed-point
+                                 rounds only, 3 sweep (levels of serial passes + filters;
+                                 hands lists that stop shrinking to the round solver), 4 the
+                                 sweep's level 0, then commit/kill rounds over its survivors */
 #define DCC_OPT_SWEEP_LEVELS 6 /* sweep levels enqueued between host synchronisations       */
 #define DCC_OPT_HIST_MERGE 7  /* device history: delta pairs above which the delta merges into
                                  the base (default 65536; the base/4 rule also applies)      */
+#define DCC_OPT_FAIL_RANK 8   /* fault injection (tests): rank `value` of a multi-GPU context
+                                 fails its next epoch before its first exchange; the other
+                                 ranks must return DCC_ECOMM instead of waiting for it      */
 int dcc_set_option(dcc_ctx* ctx, int option, int64_t value);
 /* Pre-size device workspaces so a later call performs no allocation. */
 int dcc_reserve(dcc_ctx* ctx, uint64_t max_txn, uint64_t max_nnz);
@@ -177,6 +181,8 @@ int dcc_comm_destroy(dcc_ctx* ctx);
 int dcc_comm_rank(const dcc_ctx* ctx);
 int dcc_comm_size(const dcc_ctx* ctx);
 uint32_t dcc_key_shard(uint64_t key, uint32_t nranks);
+/* dcc_key_shard of n keys (host arrays): out[i] = shard of keys[i] */
+int dcc_key_shard_n(const uint64_t* keys, uint64_t n, uint32_t nranks, uint32_t* out);
 /* Host helper: keep only the accesses of `rank` (same n_txn, same order).
  * out_offsets [n_txn+1]; out_keys/out_acctype sized >= in nnz; *out_nnz set. */
 int dcc_shard_filter(const dcc_batch* in, uint32_t rank, uint32_t nranks,

@@ -48,3 +48,21 @@ def chain_batch(n: int) -> EpochBatch:
     point needs ~n rounds (exercises the round-tag wrap)."""
     txns = [[(0, WR)]] + [[(i - 1, RD), (i, WR)] for i in range(1, n)]
     return make_batch(txns)
+
+
+def c4_batch(n_txn: int = 1 << 20, seed=None):
+    """BASELINE config C4: YCSB theta 0.9, 16 partitions (keys row*16+part),
+    65,536-txn generator chunks, each txn's home partition its origin node and
+    the sequencer order (origin, FIFO within the origin) -- sched_dequeue's
+    (epoch, origin, FIFO) order (work_queue.cpp:105-151)."""
+    import deneva_amd as d
+    kw = {} if seed is None else {"seed": seed}
+    b = d.gen_ycsb(n_txn=n_txn, zipf_theta=0.9, part_cnt=16, chunk_txns=65536, want_home=True,
+                   **kw)
+    home = b.meta["home"].astype(np.uint64)
+    seq = np.zeros(b.n_txn, np.uint64)
+    for h in np.unique(home):
+        idx = np.nonzero(home == h)[0]
+        seq[idx] = np.arange(idx.size, dtype=np.uint64)
+    b.order = (home << np.uint64(32)) | seq
+    return b

@@ -73,3 +73,29 @@ def test_dispatch_lists(engine, ordered):
     assert np.array_equal(np.diff(np.asarray(off, np.int64)), counts)
     # every txn of wave w+1 has a predecessor in wave w (the schedule is tight)
     assert off[0] == 0 and off[-1] == b.n_txn
+
+
+def test_repeated_host_calls_keep_memory_flat():
+    """Probe and dispatch with host pointers stage through the context's
+    grow-only scratch: after the first call, repeated calls allocate nothing
+    (device free memory stays flat)."""
+    import torch
+    rng = np.random.default_rng(9)
+    with d.Engine(0) as eng:
+        k = rng.integers(0, 1 << 20, size=200000).astype(np.uint64)
+        eng.index_insert(k, k * 3)
+        probe = rng.integers(0, 1 << 21, size=1 << 20).astype(np.uint64)
+        wave = rng.integers(0, 500, size=1 << 18).astype(np.uint32)
+        order = rng.permutation(wave.size).astype(np.uint64)
+        eng.index_probe(probe)
+        eng.calvin_dispatch(wave, order)
+        torch.cuda.synchronize()
+        free0 = torch.cuda.mem_get_info(0)[0]
+        for _ in range(40):
+            eng.index_probe(probe)
+            eng.calvin_dispatch(wave, order)
+            eng.index_insert(k[:1000], k[:1000])
+        torch.cuda.synchronize()
+        free1 = torch.cuda.mem_get_info(0)[0]
+        # 40 leaked probe buffers alone would be 40 x 16 MiB
+        assert free0 - free1 < (8 << 20), (free0, free1)

@@ -111,3 +111,28 @@ def test_row_table_growth(engine):
     glr, glw = engine.maat_rows_get(k)
     assert np.array_equal(glr, lr) and np.array_equal(glw, lw)
     engine.maat_rows_clear()
+
+
+def test_rejected_batch_leaves_rows_unchanged(engine):
+    """A batch the engine rejects (reserved key, malformed offsets) changes
+    neither the row table's rows nor its timestamps."""
+    from deneva_amd._abi import DccError
+    engine.maat_rows_clear()
+    b = d.gen_ycsb(n_txn=4096, zipf_theta=0.9, table_size=1 << 12, seed=77)
+    engine.maat_validate_epoch(b)
+    rk = np.unique(np.asarray(b.keys))
+    lr0, lw0 = engine.maat_rows_get(rk)
+    size0 = engine.maat_rows_size
+    c = d.gen_ycsb(n_txn=4096, zipf_theta=0.9, table_size=1 << 16, seed=78)
+    keys = np.asarray(c.keys).copy()
+    keys[-1] = 0xFFFFFFFFFFFFFFFF
+    with pytest.raises(DccError):
+        engine.maat_validate_epoch(d.EpochBatch(c.offsets, keys, c.acctype))
+    off = np.asarray(c.offsets).copy()
+    off[5], off[6] = off[6], off[5]
+    with pytest.raises(DccError):
+        engine.maat_validate_epoch(d.EpochBatch(off, c.keys, c.acctype))
+    assert engine.maat_rows_size == size0
+    lr1, lw1 = engine.maat_rows_get(rk)
+    assert np.array_equal(lr0, lr1) and np.array_equal(lw0, lw1)
+    engine.maat_rows_clear()

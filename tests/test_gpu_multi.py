@@ -76,3 +76,53 @@ def test_multi_rejects_device_batches_and_snapshot():
             eng.occ_validate_epoch(b.to_torch("cuda:0"))
         with pytest.raises(d.DccError):
             eng.maat_validate_epoch(b)
+
+
+@pytest.fixture(scope="module")
+def c4():
+    from helpers import c4_batch
+    b = c4_batch()
+    eg, erc, _ = orc.calvin(b)
+    return b, eg, erc
+
+
+def test_multi_calvin_c4_full_8_shards(c4):
+    """BASELINE config C4 at full size, key-sharded 8 ways in one multi-GPU
+    context (each shard locks only its own rows, ycsb_txn.cpp:62-63); the
+    scattered grant groups and the all-reduced readiness equal the oracle's
+    literal Row_lock order and the one-GPU engine's."""
+    b, eg, erc = c4
+    with d.Engine(0) as one:
+        g1, rc1, _, _ = one.calvin_order_epoch(b, want_group=True)
+    g1 = np.asarray(g1).astype(np.uint32)
+    assert np.array_equal(g1, eg) and np.array_equal(np.asarray(rc1), erc)
+    with d.Engine(devices=[0] * 8) as eng:
+        assert eng.comm_size == 8
+        g, rc, _, st = eng.calvin_order_epoch(b, want_group=True)
+        assert np.array_equal(np.asarray(g).astype(np.uint32), eg)
+        assert np.array_equal(np.asarray(rc), erc)
+        assert st["n_shards"] == 8 and st["n_commit"] == int((erc == 0).sum())
+
+
+@pytest.mark.parametrize("bad_rank", [0, 2])
+def test_multi_rank_failure_does_not_hang(bad_rank):
+    """One rank fails before its first exchange (fault injection): every
+    rank returns instead of waiting for it (the exchange is poisoned), the
+    failing rank's error is reported, and the next epoch runs normally."""
+    from deneva_amd._abi import OPT_FAIL_RANK
+    b = d.gen_ycsb(n_txn=30000, zipf_theta=0.9, table_size=1 << 16)
+    erc, _, _ = orc.occ(b)
+    c = d.gen_ycsb(n_txn=20000, zipf_theta=0.9, part_cnt=4, chunk_txns=4096)
+    eg, ecrc, _ = orc.calvin(c)
+    with d.Engine(devices=[0] * 4) as eng:
+        eng.set_option(OPT_FAIL_RANK, bad_rank)
+        with pytest.raises(d.DccError, match="injected"):
+            eng.occ_validate_epoch(b)
+        rc, _, _ = eng.occ_validate_epoch(b)
+        assert np.array_equal(np.asarray(rc), erc)
+        eng.set_option(OPT_FAIL_RANK, 3)
+        with pytest.raises(d.DccError, match="injected"):
+            eng.calvin_order_epoch(c, want_group=True)
+        g, crc, _, _ = eng.calvin_order_epoch(c, want_group=True)
+        assert np.array_equal(np.asarray(g).astype(np.uint32), eg)
+        assert np.array_equal(np.asarray(crc), ecrc)

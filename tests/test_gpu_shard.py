@@ -158,3 +158,48 @@ def test_sharded_c5_full_size(world):
         assert nsh == world and tnc == etnc
         assert np.array_equal(rc, erc), f"rank {r}: rc differs from the oracle"
         assert np.array_equal(tn.astype(np.uint64), etn), f"rank {r}: tn differs"
+
+
+def _c4_worker(rank, world, port, out):
+    import torch
+    import torch.distributed as dist
+    from helpers import c4_batch
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def allreduce_max(buf):
+        t = torch.from_numpy(buf)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+
+    eng = d.Engine(0)
+    eng.comm_init_host(rank, world, allreduce_max)
+    b = c4_batch()
+    g, crc, _, st = eng.calvin_order_epoch(d.shard_filter(b, rank, world), want_group=True)
+    out[rank] = (np.asarray(g).astype(np.uint32).copy(), np.asarray(crc).copy(), st["n_shards"])
+    eng.close()
+    dist.destroy_process_group()
+
+
+def test_sharded_calvin_c4_full_size_8_ranks():
+    """BASELINE config C4 (1,048,576 txns, 16 partitions, sequencer (origin,
+    FIFO) order) key-sharded over 8 rank processes: each locks only its own
+    rows (ycsb_txn.cpp:62-63), readiness is the MAX all-reduce of the WAIT
+    bytes; the scattered groups and readiness equal the oracle's literal
+    Row_lock order (row_lock.cpp:52-216)."""
+    import torch.multiprocessing as mp
+    from helpers import c4_batch
+    world = 8
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_c4_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    b = c4_batch()
+    eg, erc, _ = orc.calvin(b)
+    owner = d.shard_of_keys(np.asarray(b.keys), world)
+    got = np.full(b.nnz, 0xFFFFFFFE, np.uint32)
+    for r in range(world):
+        g, crc, nsh = out[r]
+        assert nsh == world
+        got[owner == r] = g[: int((owner == r).sum())]
+        assert np.array_equal(crc, erc), f"rank {r}: calvin readiness differs"
+    assert np.array_equal(got, eg), "calvin grant groups differ"
