@@ -45,7 +45,10 @@ def parse():
                     help="comma-separated secondary configs to run INSTEAD of the headline "
                          "(profiling aid): " + ",".join(CONFIGS))
     ap.add_argument("--solver", type=int, default=0,
-                    help="OCC solver: 0 auto (sweep), 1 fixed-point rounds only, 3 sweep")
+                    help="OCC solver: 0 auto (= 4), 1 fixed-point rounds only, 3 sweep levels, "
+                         "4 sweep levels then commit/kill rounds")
+    ap.add_argument("--ck-level", type=int, default=0,
+                    help="solver 4: full sweep levels before the commit/kill rounds (0: default)")
     ap.add_argument("--strong", action="store_true",
                     help="strong scaling: one fixed batch of --txns txns key-sharded over the "
                          "N ranks (BASELINE config C5 with --theta 0.99 --seed 0xD3E7A002); "
@@ -91,6 +94,36 @@ def _cpu_model() -> str:
     return "unknown"
 
 
+def host_threads() -> int:
+    """Host threads this process may run on (its CPU affinity), not
+    OMP_NUM_THREADS: the multi-threaded CPU baseline uses all of them."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
+
+
+def prefix_batch(b, n):
+    """The first n txns of a batch (a valid epoch of its own: the decisions
+    of a prefix never depend on later txns)."""
+    from deneva_amd import EpochBatch
+    n = min(n, b.n_txn)
+    off = np.asarray(b.offsets)[: n + 1].copy()
+    cut = lambda a: None if a is None else np.asarray(a)[:n].copy()
+    return EpochBatch(off, np.asarray(b.keys)[: off[-1]], np.asarray(b.acctype)[: off[-1]],
+                      cut(b.start_tn), cut(b.finish_tn), cut(b.order))
+
+
+def cpu_leg(fn, n, variant, sample_note):
+    """Time one single-threaded CPU restatement of the reference algorithm
+    (the checker's code, outside every GPU timing) on n txns."""
+    t0 = time.perf_counter()
+    out = fn()
+    dt = time.perf_counter() - t0
+    return out, {"txns_per_s": n / dt, "txns": n, "seconds": dt, "threads": 1, "kind": "port",
+                 "variant": variant, "sample": sample_note}
+
+
 def cpu_baseline(batch, sample: int):
     """The reference CPU path and its two faster restatements, timed on this
     host, on the same batch:
@@ -108,7 +141,7 @@ def cpu_baseline(batch, sample: int):
     import _oracle as orc  # checker / CPU baseline only
     from deneva_amd import EpochBatch
 
-    threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or (os.cpu_count() or 1)
+    threads = host_threads()
     n = min(sample, batch.n_txn)
     off = batch.offsets[: n + 1].copy()
     sub = EpochBatch(off, batch.keys[: off[-1]], batch.acctype[: off[-1]])
@@ -180,7 +213,16 @@ def occ_config(eng, dev, timed, orc, tag):
     rc = torch.empty(b.n_txn, dtype=torch.uint8, device=dev)
     dt, st = timed(lambda: eng.occ_validate_epoch(db, out_rc=rc)[2])
     erc, _, _ = orc.occ(b)
+    # the reference algorithm on the host: the literal OptCC epoch replay
+    # (occ.cpp:116-327, oracle/occ_ref.c), on a prefix sized to ~5-10 s
+    ns = {"C2": 65536, "C3": 65536, "C5": 262144}[tag]
+    sub = prefix_batch(b, ns)
+    (lrc, _, _), cpu = cpu_leg(lambda: orc.occ(sub, literal=True), sub.n_txn,
+                               "REF-LITERAL (literal OptCC epoch replay, oracle/occ_ref.c)",
+                               f"first {sub.n_txn} of {b.n_txn} txns")
+    cpu["parity_vs_gpu"] = bool(np.array_equal(lrc, rc[: sub.n_txn].cpu().numpy()))
     return {"workload": desc, "txns_per_s": b.n_txn / dt, "ms_per_epoch": dt * 1e3,
+            "cpu_baseline": cpu,
             "device_ms": st["device_ms"], "rounds": int(st["rounds"]),
             "commits": int(st["n_commit"]), "peel_prefix": int(st["peel_prefix"]),
             "survivors": int(st["n_survivors"]),
@@ -204,9 +246,16 @@ def calvin_config(eng, dev, timed, orc, tag="C4"):
     eg, erc, _ = orc.calvin(b)
     par = bool(np.array_equal(res["g"].cpu().numpy().astype(np.uint32)[:b.nnz], eg) and
                np.array_equal(res["rc"].cpu().numpy()[:b.n_txn], erc))
+    # the reference's lock table on the host: the literal Row_lock CALVIN
+    # replay (FIFO waiters, no barging, promotion on release; row_lock.cpp:
+    # 52-381, oracle/calvin_ref.c) of the sequenced epoch's first txns
+    sub = prefix_batch(b, 262144)
+    _, cpu = cpu_leg(lambda: orc.calvin(sub, literal=True), sub.n_txn,
+                     "REF-LITERAL (literal Row_lock CALVIN replay, oracle/calvin_ref.c)",
+                     f"first {sub.n_txn} of {b.n_txn} txns (index order; sequenced by `order`)")
     return {"workload": "Calvin lock ordering, YCSB theta=0.9, 16 partitions, "
                         "1,048,576 txns x 16 keys, sequencer (origin, FIFO) order",
-            "txns_per_s": b.n_txn / dt, "ms_per_epoch": dt * 1e3,
+            "txns_per_s": b.n_txn / dt, "ms_per_epoch": dt * 1e3, "cpu_baseline": cpu,
             "device_ms": st["device_ms"], "ready_at_acquire": int(st["n_commit"]),
             "alg_GBps": st["alg_bytes"] / (st["device_ms"] * 1e-3) / 1e9,
             "hbm_frac": st["alg_bytes"] / (st["device_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
@@ -228,9 +277,17 @@ def maat_config(eng, dev, timed, orc, tag="MAAT_C2"):
         return eng.maat_validate_epoch(db, want_cts=False, out_rc=rc)[2]
     dt, st = timed(step)
     erc, _, _ = orc.maat(b)
+    # the reference algorithm on the host: the literal MaaT epoch replay
+    # (Maat::validate / find_bound, Row_maat soft locks; maat.cpp:29-191,
+    # row_maat.cpp:38-314, oracle/maat_ref.c) on the first 65,536 txns
+    sub = prefix_batch(b, 65536)
+    _, cpu = cpu_leg(lambda: orc.maat(sub, literal=True), sub.n_txn,
+                     "REF-LITERAL (literal MaaT epoch replay, oracle/maat_ref.c)",
+                     f"first {sub.n_txn} of {n} txns")
     return {"workload": f"MaaT epoch validation, YCSB {n} txns x 16 keys, theta=0.9, empty row "
                         f"timestamps",
             "txns_per_s": n / dt, "ms_per_epoch": dt * 1e3, "device_ms": st["device_ms"],
+            "cpu_baseline": cpu,
             "rounds": int(st["rounds"]), "commits": int(st["n_commit"]),
             "alg_GBps": st["alg_bytes"] / (st["device_ms"] * 1e-3) / 1e9,
             "parity_vs_oracle": bool(np.array_equal(rc.cpu().numpy(), erc))}
@@ -291,8 +348,53 @@ def history_config(eng, dev, timed, orc, tag="HIST", n=1 << 18, epochs=8):
             "parity_vs_oracle": bool(par)}
 
 
+def shim_config(eng, dev, timed, orc, tag="SHIM", n=1 << 20, steps=6):
+    """The shipped shim path at the headline size: what OccEpoch::close
+    (deneva_amd/csrc/host/occ_epoch.h) hands the engine -- HOST arrays (H2D
+    of the CSR and D2H of the decisions inside the call), per-txn TS_CAS
+    windows (start_tn, finish_tn], commit tn wanted and the committed writes
+    appended to the device history (DCC_OCC_APPEND_HISTORY, central_finish,
+    occ.cpp:277-286).  Each step starts from the same history: the committed
+    writes of the previous epoch of the same shape (tn 1..).  Wall time per
+    call (host-synchronous API) and the call's device time."""
+    import deneva_amd as d
+    rng = np.random.default_rng(0xD3E7A00C)
+    prev = d.gen_ycsb(n_txn=n, zipf_theta=0.9, seed=0xD3E7A00D)
+    _, ptn, ptnc = orc.occ(prev)
+    off = np.asarray(prev.offsets, np.int64)
+    owner = np.repeat(np.arange(n), np.diff(off))
+    sel = (np.asarray(prev.acctype) == d.WR) & (ptn[owner] != 0)
+    hk, ht = np.asarray(prev.keys, np.uint64)[sel].copy(), ptn[owner[sel]].astype(np.uint64)
+    b = d.gen_ycsb(n_txn=n, zipf_theta=0.9)
+    b.start_tn = (ptnc - rng.integers(0, ptnc + 1, size=n)).astype(np.uint64)
+    b.finish_tn = (ptnc + rng.integers(0, 64, size=n)).astype(np.uint64)
+    erc, etn, _ = orc.occ(b, hist_keys=hk, hist_tn=ht, tnc=ptnc)
+    walls, devs, res = [], [], None
+    for i in range(steps + 2):
+        eng.history_clear()
+        eng.history_append(hk, ht)
+        eng.tnc = ptnc
+        t0 = time.perf_counter()
+        rc, tn, st = eng.occ_validate_epoch(b, want_tn=True, append_history=True)
+        w = time.perf_counter() - t0
+        if i >= 2:  # warmup
+            walls.append(w)
+            devs.append(st["device_ms"])
+        res = (rc, tn)
+    eng.history_clear()
+    eng.tnc = 0
+    par = bool(np.array_equal(np.asarray(res[0]), erc) and np.array_equal(np.asarray(res[1]), etn))
+    wall = float(np.median(walls))
+    return {"workload": f"OCC epoch of {n} YCSB txns x 16 keys (theta=0.9) through the shim's path: "
+                        f"host arrays, TS_CAS windows against a {hk.size}-pair history, commit tn, "
+                        f"history append",
+            "txns_per_s": n / wall, "ms_per_epoch": wall * 1e3,
+            "device_ms": float(np.median(devs)), "note": "wall includes H2D of the CSR, D2H of rc + tn",
+            "parity_vs_oracle": par}
+
+
 CONFIGS = {"C2": occ_config, "C3": occ_config, "C5": occ_config, "C4": calvin_config,
-           "C6": None, "HIST": history_config, "MAAT_C2": maat_config,
+           "C6": None, "HIST": history_config, "SHIM": shim_config, "MAAT_C2": maat_config,
            "MAAT_1M": maat_config}
 
 
@@ -371,6 +473,9 @@ def main():
     if args.only:
         torch.cuda.set_device(0)
         with d.Engine(0) as eng:
+            eng.set_option(d._abi.OPT_SOLVER, args.solver)
+            if args.ck_level:
+                eng.set_option(d._abi.OPT_CK_LEVEL, args.ck_level)
             print(json.dumps(secondary_configs(eng, 0, steps=args.steps, warmup=args.warmup,
                                                only=args.only.split(","))), flush=True)
         return
@@ -396,6 +501,8 @@ def main():
                        seed=args.seed)
     eng = d.Engine(local)
     eng.set_option(d._abi.OPT_SOLVER, args.solver)
+    if args.ck_level:
+        eng.set_option(d._abi.OPT_CK_LEVEL, args.ck_level)
     if world > 1:
         if args.exchange == "rccl":
             uid = d.comm_unique_id() if rank == 0 else bytes(d._abi.UNIQUE_ID_BYTES)

@@ -39,6 +39,7 @@ OPT_SOLVER = 5
 OPT_SWEEP_LEVELS = 6
 OPT_HIST_MERGE = 7
 OPT_FAIL_RANK = 8
+OPT_CK_LEVEL = 9
 
 
 class Batch(C.Structure):

@@ -84,11 +84,12 @@ struct dcc_ctx {
   uint64_t recheck_max = 16384;   // fold the kill wave into rounds with lists <= this
   uint32_t batch_max = 8;       // rounds enqueued between host synchronisations
   bool bars_used = false;       // this epoch's rounds used grid-barrier words
-  int solver = 0;               // 0 auto (= 4), 1 fixed-point rounds, 3 sweep, 4 level-0 sweep +
-                                // commit/kill rounds
+  int solver = 0;               // 0 auto (= 3), 1 fixed-point rounds, 3 sweep, 4 sweep levels +
+                                // commit/kill rounds (measured slower)
   bool use_sweep() const { return solver != 1; }
-  bool use_ck() const { return solver == 0 || solver == 4; }
+  bool use_ck() const { return solver == 4; }
   uint32_t ck_graph_rounds = 10;  // commit/kill rounds in the captured epoch
+  uint32_t ck_level = 2;          // full sweep levels before the commit/kill rounds
   uint64_t ck_clean = 0;          // table slots known clean
   bool ck_dirty = false;          // an epoch stopped before k_final reset its slots
   uint32_t sw_levels = 4;

@@ -202,6 +202,10 @@ extern "C" int dcc_set_option(dcc_ctx* ctx, int option, int64_t value) {
       if (value < 1 || value > SW_MAX_LEVEL) return DCC_EINVAL;
       ctx->sw_levels = (uint32_t)value;
       return DCC_OK;
+    case DCC_OPT_CK_LEVEL:
+      if (value < 1 || value > SW_MAX_LEVEL - 2) return DCC_EINVAL;
+      ctx->ck_level = (uint32_t)value;
+      return DCC_OK;
     case DCC_OPT_HIST_MERGE:
       if (value < 1) return DCC_EINVAL;
       ctx->hist_merge_min = (uint64_t)value;

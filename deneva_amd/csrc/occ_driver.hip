@@ -587,26 +587,30 @@ int dcc_ctx::ck_enqueue(const DevBatch& d, uint32_t r0, uint32_t r1, bool build)
   dcc_ctx* ctx = this;
   (void)d;
   SwLevel* ctl = (SwLevel*)sw_ctl.p;
-  const SubBufs& b = sw_list[0];  // level 0's filter writes list 1 here
+  const uint32_t L = ck_level;                  // the list the rounds decide:
+  const SubBufs& b = sw_list[(L - 1) & 1];      // level L-1's filter writes it here
   CkArgs a{};
   a.tid1 = (const uint32_t*)b.tid.p;
   a.off1 = (const uint32_t*)b.off.p;
   a.keys1 = (const uint64_t*)b.keys.p;
   a.at1 = (const uint8_t*)b.acctype.p;
-  a.lv1 = ctl + 1;
+  a.lv1 = ctl + L;
   a.abandon = (const uint32_t*)(ctl + SW_MAX_LEVEL + 1);
   a.abandon_out = (uint32_t*)(ctl + SW_MAX_LEVEL + 1);
+  a.abandon_level = L;
   a.tab = (CkSlot*)ck_tab.p;
   a.cap_bits = ck_cap_bits;
   a.ctl = (uint32_t*)ck_ctl.p;
   a.aslot = (uint32_t*)ck_aslot.p;
-  a.lst[0] = (uint32_t*)ck_lst[0].p;
-  a.lst[1] = (uint32_t*)ck_lst[1].p;
+  a.s1 = (uint32_t*)ck_lst[0].p;
   a.state = (uint8_t*)state.p;
   a.err = (uint32_t*)misc.p;
-  if (build) launch_ck_build(a, (unsigned)n_cu * 2, stream);
+  // grid-stride over the list with the chip's resident capacity (8 workgroups
+  // of 256 per CU) while it is long: a group of 16 lanes per txn; later
+  // rounds decide a few thousand txns and mostly skip decided ones
+  if (build) launch_ck_build(a, (unsigned)n_cu * 8, stream);
   for (uint32_t r = r0; r <= r1; r++)
-    launch_ck_round(a, r, r <= 2 ? (unsigned)n_cu * 2 : (unsigned)n_cu / 2, stream);
+    launch_ck_round(a, r, r <= 2 ? (unsigned)n_cu * 8 : (unsigned)n_cu * 2, stream);
   CK(hipGetLastError());
   return DCC_OK;
 }
@@ -649,7 +653,7 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   const bool graph_ok = sweep && !profiling && !sw_debug && !want_tn && !hist_on && !sh &&
                         !getenv("DCC_NO_GRAPH");
   const GraphKey gkey{d.off, d.keys, d.acctype, d.n, d.nnz, out_rc, dev_out,
-                      ck ? 1000u + ck_graph_rounds : sw_levels, buf_gen};
+                      ck ? 1000u + 100u * ck_level + ck_graph_rounds : sw_levels, buf_gen};
   bool replay = graph_ok && graph_exec && gkey == graph_key;
   bool capturing = false;
   // a failure while capturing must still end the capture
@@ -732,7 +736,7 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   int serial_tail = -1;  // level enqueued without its filter (sweep_enqueue tail_serial)
   if (sweep) {
     if (profiling) CK(hipEventRecord(pev[0], stream));
-    next_level = ck ? 1 : (int)std::min<uint32_t>(sw_levels, SW_MAX_LEVEL - 1);
+    next_level = ck ? (int)ck_level : (int)std::min<uint32_t>(sw_levels, SW_MAX_LEVEL - 1);
     if (!sh && !ck && next_level >= 2) serial_tail = next_level - 1;
     if (ck) ck_dirty = true;  // until k_final has reset the table's slots
     if (sh) {
@@ -778,7 +782,7 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
     if (ck) {
       fa.ck_tab = (CkSlot*)ck_tab.p;
       fa.ck_aslot = (const uint32_t*)ck_aslot.p;
-      fa.ck_acc = &ctl_d[1].acc;
+      fa.ck_acc = &ctl_d[ck_level].acc;
       fa.ck_live = ck_cnt_d + (ck_last + 1) % CK_RING;
       fa.ck_abandon = (const uint32_t*)(ctl_d + SW_MAX_LEVEL + 1);
     }
@@ -836,8 +840,9 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
       const uint32_t e = *(const uint32_t*)hmisc;
       if (!ab && !(e & (ERR_SPIN | ERR_TILE | ERR_FULL))) {
         ck_done = true;
+        // per-round live flags: round r ran on a non-empty list
         const uint32_t* hcnt = (const uint32_t*)((const char*)hmisc + CK_HCTL) + CK_CTL_RING;
-        const uint32_t m1 = hc[1].m;
+        const uint32_t m1 = hc[ck_level].m;
         auto count = [&](uint32_t r0, uint32_t r1) {  // rounds in [r0, r1] with a list
           for (uint32_t r = r0; r <= r1; r++)
             if (r == 1 ? m1 > 0 : hcnt[r % CK_RING] > 0) ck_rounds++;
@@ -845,7 +850,7 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
         uint32_t R = ck_graph_rounds;
         count(1, R);
         while (hcnt[(R + 1) % CK_RING]) {
-          const uint32_t B = 32;  // <= CK_RING - 2: the batch's counters stay intact
+          const uint32_t B = 32;  // <= CK_RING - 2: the batch's flags stay intact
           CR(ck_enqueue(d, R + 1, R + B, false));
           GatherArgs ga{};
           ga.job[ga.n++] = CopyJob{(const uint32_t*)ck_ctl.p,
@@ -862,6 +867,10 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
           ck_last = R;
           again = true;  // finalize again: the captured k_final ran before these rounds
         }
+        // the next epoch captures one round more than this one needed (the
+        // last captured round then finds its list empty): a steady workload
+        // settles on a graph without host round trips or idle rounds
+        ck_graph_rounds = std::max<uint32_t>(4, std::min<uint32_t>(24, ck_rounds + 1));
       }
     }
     for (; !ck_done;) {

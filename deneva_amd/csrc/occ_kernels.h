@@ -352,22 +352,25 @@ constexpr uint32_t CK_WR = 0x80000000u;   // aslot: the access is a write
 constexpr uint32_t CK_NONE = 0x7FFFFFFFu; // aslot: no slot (reserved key)
 constexpr uint32_t CK_RING = 64;          // per-round list counters kept on the device
 constexpr uint32_t CK_CTL_MASK = 0;       // ctl word: the table's slot mask this epoch
-constexpr uint32_t CK_CTL_RING = 16;      // ctl words [16, 16 + CK_RING): list counters
+constexpr uint32_t CK_CTL_RING = 16;      // ctl words [16, 16 + CK_RING): per-round live flags
 constexpr uint32_t CK_CTL_WORDS = CK_CTL_RING + CK_RING;
-constexpr uint32_t CK_U = 4;              // slot loads in flight per lane
+constexpr uint32_t CK_G = 16;             // lanes per txn (k_ck_build / k_ck_round)
+constexpr uint32_t CK_C = MAX_TXN_LEN / CK_G;  // accesses per lane
 struct CkArgs {
-  const uint32_t* tid1;   // the list (level 0's survivors, index order): txn ids,
+  const uint32_t* tid1;   // the list (the survivors of the sweep's first levels, index
+                          // order): txn ids,
   const uint32_t* off1;   // offsets (0-based), keys and access types
   const uint64_t* keys1;
   const uint8_t* at1;
   const SwLevel* lv1;     // its length and access count (device)
   const uint32_t* abandon;
-  uint32_t* abandon_out;  // = 1: the list goes to the fixed-point round solver
+  uint32_t* abandon_out;  // = abandon_level: the list goes to the fixed-point round solver
+  uint32_t abandon_level; // the list's level (level L-1's filter wrote it)
   CkSlot* tab;            // [1 << cap_bits] clean slots
   uint32_t cap_bits;
   uint32_t* ctl;          // [CK_CTL_WORDS]
   uint32_t* aslot;        // [list accesses] slot | CK_WR
-  uint32_t* lst[2];       // undecided list positions, by round parity
+  uint32_t* s1;           // [list txns] state words by list position
   uint8_t* state;         // the epoch's state bytes
   uint32_t* err;
 };

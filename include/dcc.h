@@ -148,13 +148,15 @@ int dcc_set_profiling(dcc_ctx* ctx, int enable);
 /* Tuning knobs (defaults are the tuned values; for A/B measurement). */
 #define DCC_OPT_RECHECK 1     /* fold kill waves into rounds whose list has <= value txns */
 #define DCC_OPT_BATCH_MAX 2   /* max rounds enqueued between host synchronisations        */
-#define DCC_OPT_SOLVER 5      /* OCC solver: 0 auto (= 4; 3 when key-sharded), 1 fixed-point
-                                 rounds only, 3 sweep (levels of serial passes + filters;
-                                 hands lists that stop shrinking to the round solver), 4 the
-                                 sweep's level 0, then commit/kill rounds over its survivors */
+#define DCC_OPT_SOLVER 5      /* OCC solver: 0 auto (= 3), 1 fixed-point rounds only, 3 sweep
+                                 (levels of serial passes + filters; hands lists that stop
+                                 shrinking to the round solver), 4 the sweep's first levels,
+                                 then commit/kill rounds over their survivors (single GPU)   */
 #define DCC_OPT_SWEEP_LEVELS 6 /* sweep levels enqueued between host synchronisations       */
 #define DCC_OPT_HIST_MERGE 7  /* device history: delta pairs above which the delta merges into
                                  the base (default 65536; the base/4 rule also applies)      */
+#define DCC_OPT_CK_LEVEL 9    /* solver 4: full sweep levels before the commit/kill rounds
+                                 (default 2)                                                 */
 #define DCC_OPT_FAIL_RANK 8   /* fault injection (tests): rank `value` of a multi-GPU context
                                  fails its next epoch before its first exchange; the other
                                  ranks must return DCC_ECOMM instead of waiting for it      */
