@@ -53,9 +53,10 @@ def parse():
                     help="strong scaling: one fixed batch of --txns txns key-sharded over the "
                          "N ranks (BASELINE config C5 with --theta 0.99 --seed 0xD3E7A002); "
                          "default is weak scaling (N x --txns txns)")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r02", "traffic.json"),
-                    help="PMC traffic summary (tools/gpu_pmc.sh) the roofline.traffic field "
-                         "is read from; null when it holds no entry for this workload")
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r03", "pmc.json"),
+                    help="PMC summary (tools/gpu_pmc_r03.sh -> tools/pmc_r03.py) the "
+                         "roofline.traffic and l2_hit fields are read from (headline and C4 "
+                         "workloads at N=1; null otherwise)")
     ap.add_argument("--exchange", choices=["rccl", "host"], default="rccl",
                     help="N>1 status all-reduce: RCCL over xGMI (one GPU per rank), or "
                          "host/gloo (rehearsal: ranks may share one GPU)")
@@ -579,19 +580,32 @@ def main():
         secondary = secondary_configs(eng, local)
 
     if rank == 0:
-        # HBM traffic of one epoch (PMC FETCH_SIZE x2 + WRITE_SIZE summed over the
-        # epoch's kernels, tools/gpu_pmc.sh), read from the committed summary
-        # named by --traffic; null when it has no entry for this workload
-        traffic, traffic_src = None, None
-        if os.path.exists(args.traffic):
+        # HBM traffic and L2 hit rates of one epoch (PMC FETCH_SIZE x2 +
+        # WRITE_SIZE, TCC_HIT / (HIT + MISS), per dispatch, tools/gpu_pmc_r03.sh),
+        # read from the committed summary named by --pmc: null for workloads
+        # it does not describe (N > 1, other sizes)
+        pmc = None
+        if (os.path.exists(args.pmc) and world == 1 and n_total == 1 << 20 and args.theta == 0.9
+                and args.keys == 16):
             try:
-                tj = json.load(open(args.traffic))
-                ent = tj.get(f"{n_total}:{args.theta}:{args.keys}:{world}")
-                if ent:
-                    traffic = ent["bytes_per_epoch"]
-                    traffic_src = f"{os.path.relpath(args.traffic, ROOT)} ({ent.get('source', '')})"
-            except (OSError, ValueError, KeyError):
-                traffic = None
+                pmc = json.load(open(args.pmc))
+            except (OSError, ValueError):
+                pmc = None
+        hp = (pmc or {}).get("headline") or {}
+        traffic = hp.get("epoch_bytes")
+        traffic_src = (f"{os.path.relpath(args.pmc, ROOT)} ({pmc.get('source', '')}; "
+                       f"{pmc.get('correction', '')})") if pmc else None
+        if pmc and secondary and "C4" in secondary:
+            c4 = pmc.get("C4") or {}
+            ks = c4.get("kernels") or {}
+            secondary["C4"]["pmc"] = {
+                "source": traffic_src,
+                "epoch_traffic_bytes": c4.get("epoch_bytes"),
+                "epoch_l2_hit": c4.get("epoch_l2_hit"),
+                "l2_hit": {k: v.get("l2_hit") for k, v in ks.items()
+                           if "k_rs_" in k or "k_cv_" in k},
+                "sort_scatter_write_bytes": (ks.get("dcc::k_rs_scatter<unsigned int>") or {}).get(
+                    "write_bytes_max")}
         line = {
             "metric": "OCC-validated txns/sec, YCSB theta=0.9",
             "value": value,
@@ -626,6 +640,10 @@ def main():
                 "frac_of_stream_copy": epoch_gbs / copy_gbps if copy_gbps else None,
                 "traffic": traffic,
                 "traffic_source": traffic_src,
+                "l2_hit": {"epoch": hp.get("epoch_l2_hit"),
+                           "level0_filter": (hp.get("filter_l0") or {}).get("l2_hit"),
+                           "serial_pass": hp.get("serial_pass_l2_hit"),
+                           "pre_pass": hp.get("pre_pass_l2_hit")} if hp else None,
                 "alg_bytes_per_launch": int(s0["alg_bytes"]),
                 "avg_launch_ms": dev_ms,
                 "streaming_kernel": filt,
