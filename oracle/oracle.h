@@ -52,6 +52,15 @@ int oracle_occ_rounds_mt(uint64_t n, const uint32_t* off, const uint64_t* keys,
                          const uint8_t* acctype, int nthreads, uint64_t* tnc, uint8_t* out_rc,
                          uint64_t* out_tn, uint32_t* out_rounds);
 
+/* SWEEP-MT (occ_sweep_mt.c): the CPU form of the GPU sweep on `nthreads`
+ * host threads -- per level a serial prefix (one thread) building the
+ * committed write-key set, then a parallel read-only filter of the rest.
+ * Same decisions and out_tn / *tnc as oracle_occ_hash without a history
+ * window; *out_levels = levels run.  Returns 0, -1 on allocation failure. */
+int oracle_occ_sweep_mt(uint64_t n, const uint32_t* off, const uint64_t* keys,
+                        const uint8_t* acctype, int nthreads, uint64_t* tnc, uint8_t* out_rc,
+                        uint64_t* out_tn, uint32_t* out_levels);
+
 /* Captured-snapshot validation, literal (central_validate, occ.cpp:116-239,
  * against each txn's captured critical-section view, occ.cpp:137-158):
  * hist_top[t] = tn of the history head t saw (NULL = all visible);

@@ -17,7 +17,7 @@ LIB = os.path.join(ORACLE_DIR, "liboracle.so")
 
 
 def _load():
-    srcs = [os.path.join(ORACLE_DIR, f) for f in ("occ_ref.c", "occ_mt.c", "calvin_ref.c", "maat_ref.c", "oracle.h", "kmap.h")]
+    srcs = [os.path.join(ORACLE_DIR, f) for f in ("occ_ref.c", "occ_mt.c", "occ_sweep_mt.c", "calvin_ref.c", "maat_ref.c", "oracle.h", "kmap.h")]
     if not os.path.exists(LIB) or any(os.path.getmtime(s) > os.path.getmtime(LIB) for s in srcs
                                       if os.path.exists(s)):
         subprocess.run(["make", "-C", ORACLE_DIR], check=True, capture_output=True)
@@ -31,6 +31,8 @@ def _load():
     lib.oracle_occ_rounds_mt.argtypes = [C.c_uint64, P, P, P, C.c_int, C.POINTER(C.c_uint64), P,
                                          P, C.POINTER(C.c_uint32)]
     lib.oracle_occ_rounds_mt.restype = C.c_int
+    lib.oracle_occ_sweep_mt.argtypes = lib.oracle_occ_rounds_mt.argtypes
+    lib.oracle_occ_sweep_mt.restype = C.c_int
     lib.oracle_occ_round_status.argtypes = [C.c_uint64, P, P, P, P, P]
     lib.oracle_calvin_replay.argtypes = [C.c_uint64, P, P, P, P, P, P, P]
     lib.oracle_calvin_formula.argtypes = lib.oracle_calvin_replay.argtypes
@@ -91,6 +93,23 @@ def occ_rounds_mt(batch, nthreads, tnc=0):
     if r != 0:
         raise RuntimeError(f"oracle rounds-mt failed: {r}")
     return rc[:n], tn[:n], t.value, rounds.value
+
+
+def occ_sweep_mt(batch, nthreads, tnc=0):
+    """SWEEP-MT CPU baseline: returns (rc u8[n], tn u64[n], tnc_after, levels)."""
+    n = batch.n_txn
+    off = _arr(batch.offsets, np.uint32)
+    keys = _arr(batch.keys, np.uint64)
+    at = _arr(batch.acctype, np.uint8)
+    rc = np.empty(max(n, 1), np.uint8)
+    tn = np.empty(max(n, 1), np.uint64)
+    t = C.c_uint64(tnc)
+    lv = C.c_uint32(0)
+    r = lib.oracle_occ_sweep_mt(n, _p(off), _p(keys), _p(at), int(nthreads), C.byref(t),
+                                rc.ctypes.data, tn.ctypes.data, C.byref(lv))
+    if r != 0:
+        raise RuntimeError(f"oracle sweep-mt failed: {r}")
+    return rc[:n], tn[:n], t.value, lv.value
 
 
 def occ_snapshot(batch, active_off, active_idx, hist_top=None, hist_keys=None, hist_tn=None):

@@ -126,6 +126,22 @@ def test_rounds_mt_equals_serial(threads):
         assert rounds <= b.n_txn + 1
 
 
+@pytest.mark.parametrize("threads", [1, 4, 8])
+def test_sweep_mt_equals_serial(threads):
+    """SWEEP-MT (the multi-core CPU baseline: serial prefixes + parallel
+    filters) decides exactly like the serial scan, tn numbering included."""
+    rng = np.random.default_rng(12)
+    for b in (d.gen_ycsb(n_txn=60000, zipf_theta=0.9, table_size=1 << 16),
+              d.gen_ycsb(n_txn=30000, zipf_theta=0.0),
+              d.gen_ycsb(n_txn=20000, zipf_theta=0.99),
+              random_batch(rng, 3000, 16, 300, types=(RD, WR, XP, SCAN)), chain_batch(3000),
+              make_batch([]), make_batch([[], [(1, WR)], [(1, RD)]])):
+        rc, tn, tnc = orc.occ(b, tnc=7)
+        rc2, tn2, tnc2, levels = orc.occ_sweep_mt(b, threads, tnc=7)
+        assert np.array_equal(rc, rc2) and np.array_equal(tn, tn2) and tnc == tnc2
+        assert levels >= (1 if b.n_txn else 0)
+
+
 # ---------------------------------------------------------------- Calvin
 def calvin_both(b):
     g1, r1, w1 = orc.calvin(b, literal=True)
