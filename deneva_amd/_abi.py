@@ -28,6 +28,7 @@ KEY_RESERVED = 0xFFFFFFFFFFFFFFFF
 GROUP_NONE = 0xFFFFFFFF
 DEVICE_PTRS = 0x1
 OCC_APPEND_HISTORY = 0x2
+OCC_DEFER_FINISH = 0x8
 MAAT_READ_AND_PREWRITE = 0x4
 ROW_NONE = 0xFFFFFFFFFFFFFFFF
 UNIQUE_ID_BYTES = 128
@@ -186,6 +187,7 @@ _SIGS = [
     ("dcc_shard_filter", C.c_int, [C.POINTER(Batch), C.c_uint32, C.c_uint32, _P, _P, _P,
                                    C.POINTER(C.c_uint64)]),
     ("dcc_occ_validate_epoch", C.c_int, [_P, C.POINTER(Batch), _P, _P, C.POINTER(Stats)]),
+    ("dcc_occ_finish_epoch", C.c_int, [_P, _P, _P, C.c_uint32]),
     ("dcc_occ_validate_snapshot", C.c_int,
      [_P, C.POINTER(Batch), C.POINTER(Snapshot), _P, C.POINTER(Stats)]),
     ("dcc_occ_history_append", C.c_int, [_P, _P, _P, C.c_uint64]),

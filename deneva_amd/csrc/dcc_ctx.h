@@ -183,6 +183,13 @@ struct dcc_ctx {
                   uint64_t* nnz_w_prefix = nullptr);
   int read_partials(size_t bytes);
   int occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dcc_stats* st);
+  // DCC_OCC_DEFER_FINISH: the decided epoch waiting for its global RC
+  bool fin_pending = false;
+  DevBatch fin_d;
+  uint64_t fin_nnz_w = 0;
+  DevBuf fin_off, fin_keys, fin_at, fin_state, fin_hasw, fin_rc, fin_cnt;
+  int fin_save(const DevBatch& d, bool host_batch, uint64_t nnz_w);
+  int occ_finish(const uint8_t* final_rc, uint64_t* out_tn, uint32_t flags);
   int occ_rounds(const SubProb& sp, uint32_t maxlen, bool prof, uint32_t& rounds);
   int sweep_reserve(const DevBatch& d);
   // levels [l0, l1); resume: level l0's serial part already ran (start at its

@@ -238,7 +238,8 @@ std::vector<DevBuf*> dcc_ctx::all_bufs() {
                             &mt_misc, &mt_slot, &mt_sval, &mt_slot2, &mt_sval2, &mt_sfl,
                             &mt_stx, &mt_txn, &mt_agg, &mt_sflB, &mt_stxB, &mt_k1, &mt_tcnt, &ix_keys, &ix_ord, &ix_rows, &ix_cnt, &wv_buf, &ix_scr, &wv_hbuf, &wv_obuf,
                             &h_K[0], &h_K[1], &h_V[0], &h_V[1], &h_scr, &h_bsum,
-                            &ck_tab, &ck_ctl, &ck_aslot, &ck_lst[0], &ck_lst[1]};
+                            &ck_tab, &ck_ctl, &ck_aslot, &ck_lst[0], &ck_lst[1],
+                            &fin_off, &fin_keys, &fin_at, &fin_state, &fin_hasw, &fin_rc, &fin_cnt};
   for (auto& h : hs)
     for (DevBuf* b : {&h.fk, &h.ft, &h.skey, &h.stn, &h.hash}) v.push_back(b);
   for (auto& sb : sw_list)
@@ -622,4 +623,24 @@ extern "C" int dcc_occ_validate_epoch(dcc_ctx* ctx, const dcc_batch* batch, uint
   if (ctx->multi) return dcc_multi_occ_epoch(ctx, batch, out_rc, out_commit_tn, out_stats);
   if (hipSetDevice(ctx->device) != hipSuccess) return DCC_ENODEV;
   return ctx->occ_epoch(batch, out_rc, out_commit_tn, out_stats);
+}
+
+extern "C" int dcc_occ_finish_epoch(dcc_ctx* ctx, const uint8_t* final_rc, uint64_t* out_commit_tn,
+                                    uint32_t flags) {
+  if (!ctx) return DCC_EINVAL;
+  if (ctx->multi) {
+    // every shard appends its own keys' writes; tn numbering is alike on all
+    for (int r = 0; r < dcc_multi_size(ctx); r++) {
+      dcc_ctx* s = dcc_multi_sub(ctx, r);
+      if (hipSetDevice(s->device) != hipSuccess) return DCC_ENODEV;
+      const int e = s->occ_finish(final_rc, r == 0 ? out_commit_tn : nullptr, flags);
+      if (e != DCC_OK) {
+        ctx->last_error = "rank " + std::to_string(r) + ": " + s->last_error;
+        return e;
+      }
+    }
+    return DCC_OK;
+  }
+  if (hipSetDevice(ctx->device) != hipSuccess) return DCC_ENODEV;
+  return ctx->occ_finish(final_rc, out_commit_tn, flags);
 }

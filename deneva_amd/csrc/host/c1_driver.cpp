@@ -40,6 +40,7 @@ struct Cfg {
   int max_retries = 1000;
   bool calvin = false;
   bool live = false;           // live OptCC run on the workers, capture replayed on the GPU
+  bool overlap = true;         // OccEpoch fills epoch N+1 while N is on the GPU
   std::string capture;
 };
 
@@ -47,7 +48,7 @@ static void usage() {
   fprintf(stderr,
           "c1_driver [--threads N] [--txns N] [--theta T] [--req N] [--table N]\n"
           "          [--epoch-max N] [--timer-ms T] [--seed S] [--device D] [--gpus N]\n"
-          "          [--capture DIR] [--calvin | --live]\n");
+          "          [--capture DIR] [--calvin | --live] [--no-overlap]\n");
 }
 
 static int parse(int argc, char** argv, Cfg& c) {
@@ -58,6 +59,7 @@ static int parse(int argc, char** argv, Cfg& c) {
     if (a == "--help" || a == "-h") return 1;
     if (a == "--calvin") { c.calvin = true; continue; }
     if (a == "--live") { c.live = true; continue; }
+    if (a == "--no-overlap") { c.overlap = false; continue; }
     if (!(v = val())) return 2;
     if (a == "--threads") c.threads = atoi(v);
     else if (a == "--txns") c.txns = strtoull(v, nullptr, 0);
@@ -183,6 +185,7 @@ int main(int argc, char** argv) {
     o.n_workers = c.threads;
     o.timer_ms = c.timer_ms;
     o.capture_dir = c.capture;
+    o.overlap = c.overlap;
     OccEpoch occ(ctx, o);
     std::vector<std::thread> ws;
     for (int w = 0; w < c.threads; w++)
@@ -249,12 +252,12 @@ int main(int argc, char** argv) {
   printf("{\"driver\": \"c1\", \"cc\": \"%s\", \"threads\": %d, \"txns\": %llu, "
          "\"epochs\": %llu, \"commits\": %llu, \"restarts\": %llu, \"ready\": %llu, "
          "\"waits\": %llu, \"device_ms\": %.3f, \"wall_s\": %.3f, \"txns_per_s\": %.1f, "
-         "\"live_mismatch\": %lld, \"gave_up\": %llu, \"failed\": %d}\n",
+         "\"live_mismatch\": %lld, \"gave_up\": %llu, \"overlap\": %d, \"failed\": %d}\n",
          c.calvin ? "CALVIN" : (c.live ? "OCC-live" : "OCC"), c.threads, (unsigned long long)total,
          (unsigned long long)epochs, (unsigned long long)commits.load(),
          (unsigned long long)restarts.load(), (unsigned long long)ready.load(),
          (unsigned long long)waits.load(), device_ms, wall, total / wall, live_mismatch,
-         (unsigned long long)gave_up.load(), failed.load());
+         (unsigned long long)gave_up.load(), c.overlap ? 1 : 0, failed.load());
   dcc_destroy(ctx);
   return failed ? 1 : 0;
 }

@@ -15,6 +15,14 @@
 // has waited timer_ms.  Decided epochs can be captured as .dccb files
 // (dcc_file_write) with their decisions, for offline parity checks.
 //
+// Capture and validation overlap: the closing thread swaps the open epoch's
+// CSR into the in-flight buffer and releases the mutex for the engine call,
+// so workers fill epoch N+1 while epoch N is on the GPU.  Engine calls stay
+// serialized (one in flight; the context is thread-compatible), and an epoch
+// closes only when the previous one is decided, which keeps tnc and the
+// history in epoch order.  Options::overlap = false holds the mutex across
+// the call (the pre-overlap behaviour, kept for A/B measurement).
+//
 // Timestamps: with the reference's default TS_CLOCK (config.h:124) the history
 // window of central_validate never fires, so by
 // default the shim passes no start/finish timestamps and keeps no history (the
@@ -53,6 +61,7 @@ class OccEpoch {
     double timer_ms = 5.0;       // SEQ_BATCH_TIMER-like close timer (config.h:348)
     std::string capture_dir;     // "" = no capture
     bool ts_window = false;      // pass start/finish tn and keep the history
+    bool overlap = true;         // fill epoch N+1 while epoch N is decided
   };
   struct Stats {
     uint64_t epochs = 0, txns = 0, commits = 0, aborts = 0;
@@ -60,7 +69,7 @@ class OccEpoch {
     double device_ms = 0, wall_ms = 0;
   };
 
-  OccEpoch(dcc_ctx* ctx, const Options& o) : ctx_(ctx), opt_(o) { off_.push_back(0); }
+  OccEpoch(dcc_ctx* ctx, const Options& o) : ctx_(ctx), opt_(o) { open_.off.push_back(0); }
 
   // TxnManager::validate for CC_ALG == OCC: DCC_RC_RCOK or DCC_RC_ABORT in *rc.
   // start_tn / finish_tn are read only with Options::ts_window.
@@ -69,27 +78,27 @@ class OccEpoch {
                uint64_t finish_tn = 0) {
     std::unique_lock<std::mutex> lk(mu_);
     const uint64_t ep = epoch_;
-    const uint64_t slot = off_.size() - 1;
+    const uint64_t slot = open_.off.size() - 1;
     for (size_t i = 0; i < n; i++) {
-      keys_.push_back(acc[i].key);
-      at_.push_back(acc[i].type);
+      open_.keys.push_back(acc[i].key);
+      open_.at.push_back(acc[i].type);
     }
-    off_.push_back((uint32_t)keys_.size());
+    open_.off.push_back((uint32_t)open_.keys.size());
     if (opt_.ts_window) {
-      start_.push_back(start_tn);
-      finish_.push_back(finish_tn);
+      open_.start.push_back(start_tn);
+      open_.finish.push_back(finish_tn);
     }
     if (slot == 0) opened_ = std::chrono::steady_clock::now();
-    waiting_++;
+    waiting_++;  // in validate(), for the open or the in-flight epoch
     int err = 0;
     while (decided_.find(ep) == decided_.end()) {
-      const bool full = off_.size() - 1 >= opt_.max_txns;
+      const bool full = open_.off.size() - 1 >= opt_.max_txns;
       const bool all_in = waiting_ >= opt_.n_workers;
       const auto age = std::chrono::duration<double, std::milli>(
                            std::chrono::steady_clock::now() - opened_).count();
-      if (ep == epoch_ && (full || all_in || age >= opt_.timer_ms)) {
-        err = close_locked();
-        break;
+      if (ep == epoch_ && !busy_ && (full || all_in || age >= opt_.timer_ms)) {
+        err = close(lk);
+        continue;  // decided (or failed) now
       }
       // a system_clock deadline (pthread_cond_timedwait: the wait ThreadSanitizer
       // intercepts; a 200 us poll does not care about clock steps)
@@ -124,21 +133,39 @@ class OccEpoch {
     int err = 0;
   };
 
-  // decide the open epoch (mutex held): one engine call, then wake everyone
-  int close_locked() {
-    const uint64_t n = off_.size() - 1;
+  struct Csr {  // an epoch's access sets
+    std::vector<uint32_t> off;
+    std::vector<uint64_t> keys;
+    std::vector<uint8_t> at;
+    std::vector<uint64_t> start, finish;
+  };
+
+  // decide the open epoch: it moves to the in-flight buffer, the mutex is
+  // released for the engine call (Options::overlap), then everyone wakes.
+  // Called with lk held and no call in flight; returns with lk held.
+  int close(std::unique_lock<std::mutex>& lk) {
+    std::swap(open_, fly_);
+    open_.off.assign(1, 0);
+    open_.keys.clear();
+    open_.at.clear();
+    open_.start.clear();
+    open_.finish.clear();
+    const uint64_t id = epoch_++;
+    busy_ = true;
+    if (opt_.overlap) lk.unlock();
+    const uint64_t n = fly_.off.size() - 1;
     Decided d;
     d.rc.assign(n, DCC_RC_ABORT);
     d.readers = n;
     dcc_batch b{};
     b.n_txn = n;
-    b.nnz = keys_.size();
-    b.offsets = off_.data();
-    b.keys = keys_.data();
-    b.acctype = at_.data();
+    b.nnz = fly_.keys.size();
+    b.offsets = fly_.off.data();
+    b.keys = fly_.keys.data();
+    b.acctype = fly_.at.data();
     if (opt_.ts_window) {
-      b.start_tn = start_.data();
-      b.finish_tn = finish_.data();
+      b.start_tn = fly_.start.data();
+      b.finish_tn = fly_.finish.data();
       b.flags = DCC_OCC_APPEND_HISTORY;  // central_finish: commit tn + history
     }
     dcc_stats st{};
@@ -146,32 +173,29 @@ class OccEpoch {
     const auto t0 = std::chrono::steady_clock::now();
     d.err = n ? dcc_occ_validate_epoch(ctx_, &b, d.rc.data(), nullptr, &st) : 0;
     const auto t1 = std::chrono::steady_clock::now();
+    bool cap_err = false;
     if (!d.err && !opt_.capture_dir.empty()) {
       dcc_file_info fi{};
       fi.kind = DCC_FILE_OCC;
-      fi.epoch = epoch_;
+      fi.epoch = id;
       fi.tnc_before = tnc0;
       char path[4096];
       snprintf(path, sizeof path, "%s/epoch_%06llu.dccb", opt_.capture_dir.c_str(),
-               (unsigned long long)epoch_);
+               (unsigned long long)id);
       // the epoch is decided (tnc and history advanced): a failed capture is
       // counted, never turned into aborts
-      if (dcc_file_write(path, &fi, &b, d.rc.data(), nullptr, nullptr, nullptr) != DCC_OK)
-        stats_.capture_errors++;
+      cap_err = dcc_file_write(path, &fi, &b, d.rc.data(), nullptr, nullptr, nullptr) != DCC_OK;
     }
+    if (opt_.overlap) lk.lock();
+    busy_ = false;
+    stats_.capture_errors += cap_err ? 1 : 0;
     stats_.epochs++;
     stats_.txns += n;
     for (uint8_t r : d.rc) (r == DCC_RC_RCOK ? stats_.commits : stats_.aborts)++;
     stats_.device_ms += st.device_ms;
     stats_.wall_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
     const int err = d.err;
-    decided_.emplace(epoch_, std::move(d));
-    epoch_++;
-    off_.assign(1, 0);
-    keys_.clear();
-    at_.clear();
-    start_.clear();
-    finish_.clear();
+    decided_.emplace(id, std::move(d));
     cv_.notify_all();
     return err;
   }
@@ -180,10 +204,8 @@ class OccEpoch {
   Options opt_;
   std::mutex mu_;
   std::condition_variable cv_;
-  std::vector<uint32_t> off_;
-  std::vector<uint64_t> keys_;
-  std::vector<uint8_t> at_;
-  std::vector<uint64_t> start_, finish_;
+  Csr open_, fly_;     // the epoch workers fill; the one on the GPU
+  bool busy_ = false;  // an engine call is in flight
   std::chrono::steady_clock::time_point opened_{};
   uint64_t epoch_ = 0;
   int waiting_ = 0;

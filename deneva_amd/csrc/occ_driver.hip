@@ -553,6 +553,76 @@ int dcc_ctx::sweep_sharded(const DevBatch& d, int& next_level) {
 
 
 // ---------------------------------------------------------------------------
+// Deferred central_finish (DCC_OCC_DEFER_FINISH): the decided epoch is kept --
+// its local state and has-write bytes, and the batch itself when it was a
+// host batch (the staging buffers belong to the next call) -- until
+// dcc_occ_finish_epoch brings the global RC.
+int dcc_ctx::fin_save(const DevBatch& d, bool host_batch, uint64_t nnz_w) {
+  dcc_ctx* ctx = this;
+  CR(fin_state.ensure(this, d.n + 16, "deferred finish state"));
+  CR(fin_hasw.ensure(this, d.n + 16, "deferred finish has-write"));
+  CK(hipMemcpyAsync(fin_state.p, state.p, d.n, hipMemcpyDeviceToDevice, stream));
+  CK(hipMemcpyAsync(fin_hasw.p, hasw.p, d.n, hipMemcpyDeviceToDevice, stream));
+  fin_d = d;
+  if (host_batch) {
+    CR(fin_off.ensure(this, (d.n + 1) * 4, "deferred finish offsets"));
+    CR(fin_keys.ensure(this, std::max<uint64_t>(8, d.nnz * 8), "deferred finish keys"));
+    CR(fin_at.ensure(this, std::max<uint64_t>(16, d.nnz), "deferred finish types"));
+    CK(hipMemcpyAsync(fin_off.p, d.off, (d.n + 1) * 4, hipMemcpyDeviceToDevice, stream));
+    if (d.nnz) {
+      CK(hipMemcpyAsync(fin_keys.p, d.keys, d.nnz * 8, hipMemcpyDeviceToDevice, stream));
+      CK(hipMemcpyAsync(fin_at.p, d.acctype, d.nnz, hipMemcpyDeviceToDevice, stream));
+    }
+    fin_d.off = (const uint32_t*)fin_off.p;
+    fin_d.keys = (const uint64_t*)fin_keys.p;
+    fin_d.acctype = (const uint8_t*)fin_at.p;
+  }
+  CK(hipStreamSynchronize(stream));
+  fin_nnz_w = nnz_w;
+  fin_pending = true;
+  return DCC_OK;
+}
+
+int dcc_ctx::occ_finish(const uint8_t* final_rc, uint64_t* out_tn, uint32_t flags) {
+  dcc_ctx* ctx = this;
+  if (!fin_pending) return fail(DCC_EINVAL, "no epoch awaits dcc_occ_finish_epoch");
+  const uint64_t n = fin_d.n;
+  if (n == 0) {
+    fin_pending = false;
+    return DCC_OK;
+  }
+  if (!final_rc) return fail(DCC_EINVAL, "null final_rc");
+  const bool dev = (flags & DCC_DEVICE_PTRS) != 0;
+  const uint8_t* frc = final_rc;
+  if (!dev) {
+    CR(fin_rc.ensure(this, n + 16, "final rc"));
+    CK(hipMemcpyAsync(fin_rc.p, final_rc, n, hipMemcpyHostToDevice, stream));
+    frc = (const uint8_t*)fin_rc.p;
+  }
+  CR(cflag.ensure(this, n * 4, "cflag"));
+  CR(bsum.ensure(this, ((n + 1023) / 1024 + 1) * 8, "bsum"));
+  CR(tn.ensure(this, n * 8, "tn"));
+  CR(fin_cnt.ensure(this, 64, "finish counts"));
+  uint64_t* tn_dev = (dev && out_tn) ? out_tn : (uint64_t*)tn.p;
+  CK(hipMemsetAsync(fin_cnt.p, 0, 8, stream));
+  launch_finish_flags(frc, (const uint8_t*)fin_state.p, (const uint8_t*)fin_hasw.p, n,
+                      (uint32_t*)cflag.p, (uint32_t*)fin_cnt.p, stream);
+  launch_commit_tn((const uint32_t*)cflag.p, n, (uint64_t*)bsum.p, tnc, tn_dev, stream);
+  CK(hipGetLastError());
+  CK(hipMemcpyAsync(hmisc, fin_cnt.p, 8, hipMemcpyDeviceToHost, stream));
+  CK(hipStreamSynchronize(stream));
+  const uint32_t n_cw = ((const uint32_t*)hmisc)[0], bad = ((const uint32_t*)hmisc)[1];
+  if (bad)
+    return fail(DCC_EINVAL, "final_rc: %u txns with global RCOK aborted locally (2PC never commits them)",
+                bad);
+  CR(hist_append_epoch(fin_d, tn_dev, fin_nnz_w, n_cw));
+  tnc += n_cw;
+  if (out_tn && !dev) CK(hipMemcpy(out_tn, tn_dev, n * 8, hipMemcpyDeviceToHost));
+  fin_pending = false;
+  return DCC_OK;
+}
+
+// ---------------------------------------------------------------------------
 // Commit/kill round solver (occ_ck.hip) over level 0's survivors.  The key
 // table is sized for every access of the epoch at <= 50 % load (a list that
 // does not fit goes to the round solver) and kept clean between epochs by
@@ -622,10 +692,20 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   const auto t_wall0 = std::chrono::steady_clock::now();
   CR(check_batch(b));
   const bool dev_out = (b->flags & DCC_DEVICE_PTRS) != 0;
+  const bool defer = (b->flags & DCC_OCC_DEFER_FINISH) != 0;
+  if (fin_pending)
+    return fail(DCC_EINVAL, "an epoch validated with DCC_OCC_DEFER_FINISH awaits dcc_occ_finish_epoch");
+  if (defer && (out_tn || (b->flags & DCC_OCC_APPEND_HISTORY)))
+    return fail(DCC_EINVAL, "DCC_OCC_DEFER_FINISH: commit tn and history come from dcc_occ_finish_epoch");
   dcc_stats S;
   memset(&S, 0, sizeof S);
   S.n_shards = (uint32_t)comm_ranks();
   if (b->n_txn == 0) {
+    if (defer) {
+      fin_d = DevBatch{};
+      fin_nnz_w = 0;
+      fin_pending = true;
+    }
     if (st) *st = S;
     return DCC_OK;
   }
@@ -1085,8 +1165,13 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   }
 
   // central_finish (occ.cpp:277-286): committed write sets join the history
-  if (b->flags & DCC_OCC_APPEND_HISTORY) CR(hist_append_epoch(d, tn_dev, nnz_w, n_cw));
-  tnc += n_cw;
+  // -- or, deferred, with the global RC (dcc_occ_finish_epoch)
+  if (defer) {
+    CR(fin_save(d, !dev_out, nnz_w));
+  } else {
+    if (b->flags & DCC_OCC_APPEND_HISTORY) CR(hist_append_epoch(d, tn_dev, nnz_w, n_cw));
+    tnc += n_cw;
+  }
   const auto t_wall1 = std::chrono::steady_clock::now();
   S.total_ms = std::chrono::duration<double, std::milli>(t_wall1 - t_wall0).count();
   if (st) *st = S;

@@ -420,5 +420,10 @@ void launch_decide(uint8_t* state, uint8_t* gst, uint64_t n, uint8_t abort_byte,
                    uint32_t* und_next, hipStream_t st);
 void launch_commit_tn(const uint32_t* cflag, uint64_t n, uint64_t* bsum, uint64_t tnc,
                       uint64_t* tn, hipStream_t st);
+// deferred central_finish: cflag[t] = global RCOK && local commit && has a
+// write; cnt[0] += their number, cnt[1] += txns with global RCOK that
+// aborted locally
+void launch_finish_flags(const uint8_t* final_rc, const uint8_t* state, const uint8_t* hasw,
+                         uint64_t n, uint32_t* cflag, uint32_t* cnt, hipStream_t st);
 
 }  // namespace dcc

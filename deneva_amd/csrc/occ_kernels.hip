@@ -900,6 +900,34 @@ void launch_commit_tn(const uint32_t* cflag, uint64_t n, uint64_t* bsum, uint64_
 }
 
 // ---------------------------------------------------------------------------
+// k_finish_flags: the commit flags of a deferred central_finish (global RC).
+__global__ __launch_bounds__(256) void k_finish_flags(const uint8_t* __restrict__ frc,
+                                                      const uint8_t* __restrict__ state,
+                                                      const uint8_t* __restrict__ hasw, uint64_t n,
+                                                      uint32_t* __restrict__ cflag,
+                                                      uint32_t* __restrict__ cnt) {
+  __shared__ uint32_t sh[4];
+  uint32_t c = 0, bad = 0;
+  for (uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x; t < n; t += (uint64_t)gridDim.x * 256) {
+    const bool g = frc[t] == 0 /* DCC_RC_RCOK */, local = state[t] == ST_COMMIT;
+    const uint32_t f = (g && local && hasw[t]) ? 1u : 0u;
+    cflag[t] = f;
+    c += f;
+    bad += (g && !local) ? 1u : 0u;
+  }
+  const uint32_t sc = block_sum_u32(c, sh), sb = block_sum_u32(bad, sh);
+  if (threadIdx.x == 0) {
+    if (sc) atomicAdd(&cnt[0], sc);
+    if (sb) atomicAdd(&cnt[1], sb);
+  }
+}
+void launch_finish_flags(const uint8_t* final_rc, const uint8_t* state, const uint8_t* hasw,
+                         uint64_t n, uint32_t* cflag, uint32_t* cnt, hipStream_t st) {
+  k_finish_flags<<<grid_for(n, 256) < 1024 ? grid_for(n, 256) : 1024, 256, 0, st>>>(
+      final_rc, state, hasw, n, cflag, cnt);
+}
+
+// ---------------------------------------------------------------------------
 // k_scatter: sub-batch decisions back to the epoch's state bytes.
 __global__ __launch_bounds__(256) void k_scatter(const uint8_t* __restrict__ sub_state,
                                                  const uint32_t* __restrict__ sub_tid,

@@ -143,8 +143,11 @@ class Engine:
 
     # ------------------------------------------------------------ OCC
     def occ_validate_epoch(self, batch: EpochBatch, want_tn: bool = False,
-                           append_history: bool = False, out_rc=None, out_tn=None):
-        """Decide every txn of the epoch; returns (rc u8[n], tn u64[n] | None, stats)."""
+                           append_history: bool = False, out_rc=None, out_tn=None,
+                           defer_finish: bool = False):
+        """Decide every txn of the epoch; returns (rc u8[n], tn u64[n] | None, stats).
+        defer_finish: 2PC participant -- rc is the local vote; commit tn and
+        history wait for ``occ_finish_epoch(global_rc)``."""
         n = batch.n_txn
         dev = batch.on_device
         if out_rc is None:
@@ -161,10 +164,41 @@ class Engine:
                 out_tn = np.empty(max(n, 1), np.uint64)
         st = _abi.Stats()
         flags = _abi.OCC_APPEND_HISTORY if append_history else 0
+        if defer_finish:
+            flags |= _abi.OCC_DEFER_FINISH
         b = batch.to_c(flags)
         _check(lib.dcc_occ_validate_epoch(self._h, C.byref(b), _ptr(out_rc), _ptr(out_tn),
                                           C.byref(st)), self._h)
+        if defer_finish:
+            self._fin_n = n
         return out_rc[:n], (out_tn[:n] if want_tn else None), st.as_dict()
+
+    @property
+    def pending_finish(self) -> Optional[int]:
+        """n_txn of the epoch awaiting occ_finish_epoch, or None."""
+        return getattr(self, "_fin_n", None)
+
+    def occ_finish_epoch(self, final_rc, want_tn: bool = True, out_tn=None):
+        """central_finish with the global RC of a deferred epoch
+        (dcc_occ_finish_epoch; OptCC::finish after RFIN, occ.cpp:248-294):
+        globally committed writers take tn = tnc+1.. and join the history.
+        Returns tn u64[n] | None."""
+        dev = _is_device(final_rc)
+        n = int(final_rc.shape[0])
+        if self.pending_finish is not None and n != self.pending_finish:
+            raise ValueError(f"final_rc holds {n} txns, the pending epoch {self.pending_finish}")
+        if not dev:
+            final_rc = np.ascontiguousarray(final_rc, dtype=np.uint8)
+        if want_tn and out_tn is None:
+            if dev:
+                import torch
+                out_tn = torch.empty(max(n, 1), dtype=torch.int64, device=final_rc.device)
+            else:
+                out_tn = np.empty(max(n, 1), np.uint64)
+        _check(lib.dcc_occ_finish_epoch(self._h, _ptr(final_rc), _ptr(out_tn),
+                                        _abi.DEVICE_PTRS if dev else 0), self._h)
+        self._fin_n = None
+        return out_tn[:n] if want_tn else None
 
     # ----------------------------------------------------------------- MaaT
     def maat_validate_epoch(self, batch: EpochBatch, want_cts: bool = True,

@@ -71,6 +71,11 @@ extern "C" {
                                      of this epoch are appended to the history with
                                      tn = tnc+1, tnc+2, ... in index order
                                      (occ.cpp:248-294) */
+#define DCC_OCC_DEFER_FINISH 0x8u   /* 2PC participants: decide only.  Commit tn and the
+                                     history follow the GLOBAL RC passed later to
+                                     dcc_occ_finish_epoch (OptCC::finish after RFIN,
+                                     worker_thread.cpp:286-297, occ.cpp:248-294).  Not
+                                     with DCC_OCC_APPEND_HISTORY or out_commit_tn. */
 
 /* One epoch as a CSR of per-transaction access lists in capture order
  * (Access list of TxnManager, system/txn.h:39-70; txn.cpp:818-847). */
@@ -200,6 +205,20 @@ int dcc_shard_filter(const dcc_batch* in, uint32_t rank, uint32_t nranks,
  *                      (tnc++ / wset->tn = tnc, occ.cpp:283-284); may be NULL. */
 int dcc_occ_validate_epoch(dcc_ctx* ctx, const dcc_batch* batch, uint8_t* out_rc,
                            uint64_t* out_commit_tn, dcc_stats* out_stats);
+/* central_finish with the global decision, for an epoch validated with
+ * DCC_OCC_DEFER_FINISH (each node votes with its local RC; 2PC's coordinator
+ * commits only if every participant voted RCOK, worker_thread.cpp:328-334,
+ * and RFIN carries that RC back, worker_thread.cpp:286-297):
+ *   final_rc[i] = DCC_RC_RCOK or DCC_RC_ABORT, the global RC of txn i;
+ * committed non-read-only txns (global RCOK) take tn = tnc+1, tnc+2, ... in
+ * index order and their write sets join the history; a txn aborted globally
+ * leaves no trace even if it validated locally.  DCC_EINVAL if a txn has
+ * final RCOK but aborted locally (2PC never commits it) or no epoch is
+ * pending.  flags: DCC_DEVICE_PTRS when final_rc / out_commit_tn are device
+ * memory.  The deferred epoch's device batch (DCC_DEVICE_PTRS) must stay
+ * valid until this call; every other OCC epoch is refused meanwhile. */
+int dcc_occ_finish_epoch(dcc_ctx* ctx, const uint8_t* final_rc, uint64_t* out_commit_tn,
+                         uint32_t flags);
 /* Committed write sets of earlier epochs (the `history` list, occ.h:62-64).
  * keys/tn are host arrays of n (key, tn) pairs; each pair is one write of the
  * committed txn numbered tn.  The history is device-resident: epochs with

@@ -33,8 +33,9 @@ static int fails = 0;
     }                                                                   \
   } while (0)
 
-static void shim_threads(const char* dir) {
+static void shim_threads(const char* dir, bool overlap) {
   dcc_host::OccEpoch::Options o;
+  o.overlap = overlap;
   o.max_txns = 64;
   o.n_workers = 4;
   o.timer_ms = 1.0;
@@ -187,7 +188,8 @@ static void oracles() {
 
 int main(int argc, char** argv) {
   const char* dir = argc > 1 ? argv[1] : ".";
-  shim_threads(dir);
+  shim_threads(dir, true);
+  shim_threads(dir, false);
   batch_files(dir);
   oracles();
   if (fails) {
