@@ -15,7 +15,7 @@ timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > "$O/sm
 tail -3 "$O/smoke.log"
 fi
 T0=$(date +%s.%N); timeout -k 10 600 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 > "$O/bench.json" 2> "$O/bench.err" || { tail -20 "$O/bench.err"; exit 1; }
-echo "bench wall s: $(echo "$(date +%s.%N) - $T0" | bc)"
+echo "bench wall s: $(python3 -c "print(round($(date +%s.%N) - $T0, 1))")"
 python3 -c "
 import json;j=json.load(open('$O/bench.json'));e=j['epoch'];r=j['roofline']
 print('value',round(j['value']/1e9,3),'G txns/s  ms',round(j['ms_per_step'],4),'dev',round(e['device_ms'],4),'frac',round(r['frac'],3),'traffic',r['traffic'],'l2',r['l2_hit'])
