@@ -47,6 +47,11 @@ def parse():
     ap.add_argument("--solver", type=int, default=0,
                     help="OCC solver: 0 auto (= 4), 1 fixed-point rounds only, 3 sweep levels, "
                          "4 sweep levels then commit/kill rounds")
+    ap.add_argument("--sweep-levels", type=int, default=0,
+                    help="sweep levels per captured epoch (DCC_OPT_SWEEP_LEVELS; 0: the engine's "
+                         "default)")
+    ap.add_argument("--ro-split", type=int, default=-1,
+                    help="DCC_OPT_RO_SPLIT (-1: the engine's default)")
     ap.add_argument("--ck-level", type=int, default=0,
                     help="solver 4: full sweep levels before the commit/kill rounds (0: default)")
     ap.add_argument("--strong", action="store_true",
@@ -517,6 +522,10 @@ def main():
                        seed=args.seed)
     eng = d.Engine(local)
     eng.set_option(d._abi.OPT_SOLVER, args.solver)
+    if args.sweep_levels:
+        eng.set_option(d._abi.OPT_SWEEP_LEVELS, args.sweep_levels)
+    if args.ro_split >= 0:
+        eng.set_option(d._abi.OPT_RO_SPLIT, args.ro_split)
     if args.ck_level:
         eng.set_option(d._abi.OPT_CK_LEVEL, args.ck_level)
     if world > 1:

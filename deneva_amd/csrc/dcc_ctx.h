@@ -92,7 +92,11 @@ struct dcc_ctx {
   uint32_t ck_level = 2;          // full sweep levels before the commit/kill rounds
   uint64_t ck_clean = 0;          // table slots known clean
   bool ck_dirty = false;          // an epoch stopped before k_final reset its slots
-  uint32_t sw_levels = 4;
+  bool ro_split = true;           // DCC_OPT_RO_SPLIT
+  bool ro_on = false;             // this epoch splits read-only txns off (sweep, one GPU)
+  uint32_t wt_bits = 18;          // committed-writer table slots (WT_BITS_DEFAULT; grows after an overflow)
+  uint32_t wf_bits = 0;           // fallback table (k_sw_wall) slots
+  uint32_t sw_levels = 0;          // DCC_OPT_SWEEP_LEVELS (0: auto)
   bool sw_debug = false;        // DCC_SW_DEBUG: per-tile clock stamps of the serial pass       // sweep levels enqueued between host synchronisations
   hipEvent_t pev[8] = {};  // phase boundary events (profiling only)
   std::string last_error;
@@ -129,6 +133,8 @@ struct dcc_ctx {
   DevBuf hasw_scr;                               // round-solver hand-off
   DevBuf sw_ctl, sw_status, sw_ckeys, sw_dbg;            // sweep solver: level control, look-back, C
   DevBuf sw_rec, sw_rk, sw_gtab, sw_fw, sw_aent, sw_mg;
+  DevBuf sw_rflag, sw_ro, sw_wtab, sw_cw, sw_wtab_big;  // read-only split: survivor bits, RO
+                                                        // list, writer tables, committed writers
   DevBuf sw_xcnt, sw_xsend, sw_xrec, sw_mcnt, sw_moff, sw_mkeys, sw_mat, sw_kill;  // key-sharded sweep  // sweep tile records
   SubBufs sw_list[2];                            // sweep level lists (ping-pong)
   DevBuf ck_tab, ck_ctl, ck_aslot, ck_lst[2];    // commit/kill solver (occ_ck.hip)
@@ -200,6 +206,7 @@ struct dcc_ctx {
   int ck_reserve(const DevBatch& d);
   int ck_enqueue(const DevBatch& d, uint32_t r0, uint32_t r1, bool build);  // rounds [r0, r1]
   uint32_t ck_cap_bits = 0;
+  int sweep_ro(const DevBatch& d, bool big, bool scan, uint64_t nnz_w);  // decide the RO list
   int occ_sweep_finish(const DevBatch& d, int& next_level, bool& done, uint32_t maxlen);
   int occ_snapshot(const dcc_batch* b, const dcc_occ_snapshot* s, uint8_t* out_rc, dcc_stats* st);
   // MaaT (maat.hip): row timestamp table + epoch workspaces

@@ -199,12 +199,19 @@ extern "C" int dcc_set_option(dcc_ctx* ctx, int option, int64_t value) {
       ctx->solver = (int)value;
       return DCC_OK;
     case DCC_OPT_SWEEP_LEVELS:
-      if (value < 1 || value > SW_MAX_LEVEL) return DCC_EINVAL;
+      if (value < 0 || value > SW_MAX_LEVEL) return DCC_EINVAL;
       ctx->sw_levels = (uint32_t)value;
       return DCC_OK;
     case DCC_OPT_CK_LEVEL:
       if (value < 1 || value > SW_MAX_LEVEL - 2) return DCC_EINVAL;
       ctx->ck_level = (uint32_t)value;
+      return DCC_OK;
+    case DCC_OPT_RO_SPLIT:
+      // 0 off, 1 on; 4..24: on with a writer table of 2^value slots (tests
+      // drive the overflow fallback with small tables)
+      if (value != 0 && value != 1 && (value < 4 || value > 24)) return DCC_EINVAL;
+      ctx->ro_split = value != 0;
+      ctx->wt_bits = value >= 4 ? (uint32_t)value : WT_BITS_DEFAULT;
       return DCC_OK;
     case DCC_OPT_HIST_MERGE:
       if (value < 1) return DCC_EINVAL;
@@ -234,6 +241,7 @@ std::vector<DevBuf*> dcc_ctx::all_bufs() {
                             &cv_off2, &cv_tsum, &cv_hkeys, &cv_hat, &gst, &hasw_scr, &sw_ctl, &sw_status, &sw_dbg,
                             &sw_ckeys, &sw_gtab, &sw_rec, &sw_rk, &sw_fw, &sw_aent, &sw_mg, &sw_xcnt, &sw_xsend,
                             &sw_xrec, &sw_mcnt, &sw_moff, &sw_mkeys, &sw_mat, &sw_kill,
+                            &sw_rflag, &sw_ro, &sw_wtab, &sw_cw, &sw_wtab_big,
                             &snap_top, &snap_aoff, &snap_aidx, &snap_cnt, &mt_rk, &mt_rlr, &mt_rlw,
                             &mt_misc, &mt_slot, &mt_sval, &mt_slot2, &mt_sval2, &mt_sfl,
                             &mt_stx, &mt_txn, &mt_agg, &mt_sflB, &mt_stxB, &mt_k1, &mt_tcnt, &ix_keys, &ix_ord, &ix_rows, &ix_cnt, &wv_buf, &ix_scr, &wv_hbuf, &wv_obuf,

@@ -271,7 +271,11 @@ static constexpr size_t SW_PREP_OFF = 32768;  // prep partials inside `part` / `
 static constexpr size_t SW_HCTL = 13312;      // control-block copy inside `hmisc`
 static constexpr uint32_t SW_PMAX_TOP = 65536;
                                                           // the serial pass's LDS set)
-static uint32_t sw_pmax(int level) {
+// the serial prefixes per level: 1,024 txns at level 0; with the read-only
+// split (lists of write txns only after level 0) 3,072 and 8,192 next, so the
+// headline epoch ends in three levels (tools/sweep_model.py, measured A/B in
+// DESIGN.md §3); without it 1,024 << level
+static uint32_t sw_pmax(int level, bool split) {
   // DCC_SW_PMAX="p0,p1,...": per-level serial prefixes (tuning experiments)
   static const std::vector<uint32_t> ov = [] {
     std::vector<uint32_t> v;
@@ -286,28 +290,33 @@ static uint32_t sw_pmax(int level) {
     return v;
   }();
   if (level < (int)ov.size()) return ov[level];
+  if (split) {
+    if (level == 0) return 1024u;
+    if (level == 1) return 3072u;
+    return level >= 5 ? SW_PMAX_TOP : (8192u << (level - 2));
+  }
   return level >= 6 ? SW_PMAX_TOP : (1024u << level);
 }
 static size_t sw_ctl_bytes() { return (SW_MAX_LEVEL + 2) * sizeof(SwLevel) + 64; }
 // the access budget of a level's serial range: a quarter of the smallest
 // table with four slots per access of p_max 16-access txns
-static uint32_t sw_budget_bits(int level) {
+static uint32_t sw_budget_bits(int level, bool split) {
   uint32_t b = 12;
-  while (b < SW_GBITS_MAX && (1ull << b) < 4ull * sw_pmax(level) * 16) b++;
+  while (b < SW_GBITS_MAX && (1ull << b) < 4ull * sw_pmax(level, split) * 16) b++;
   return b;
 }
-static uint32_t sw_budget(int level) { return 1u << (sw_budget_bits(level) - 2); }
+static uint32_t sw_budget(int level, bool split) { return 1u << (sw_budget_bits(level, split) - 2); }
 // key-table slots of a level: sparse (2^18 at level 0, 2^19 after; the
 // DCC_SW_GBITS override for experiments), so a pre-pass workgroup's ~500
 // first inserts almost never meet another key at their first slot -- each
 // lost slot is one more dependent round trip for the whole workgroup
-static uint32_t sw_gbits(int level) {
+static uint32_t sw_gbits(int level, bool split) {
   static const int ov = [] {
     const char* c = getenv("DCC_SW_GBITS");
     return c ? atoi(c) : 0;
   }();
   uint32_t b = ov > 0 ? (uint32_t)ov : (level == 0 ? 18u : 19u);
-  b = std::max(b, sw_budget_bits(level));
+  b = std::max(b, sw_budget_bits(level, split));
   return std::min<uint32_t>(b, SW_GBITS_MAX);
 }
 
@@ -331,6 +340,13 @@ int dcc_ctx::sweep_reserve(const DevBatch& d) {
   CR(sw_fw.ensure(this, 2 * (1ull << SW_GBITS_MAX) * 4, "sweep first writer / last accessor"));
   CR(sw_aent.ensure(this, 2 * (1ull << (SW_GBITS_MAX - 1)) * 4, "sweep access entries"));
   CR(sw_mg.ensure(this, SW_PMAX_TILES * 8, "sweep tile commit masks"));
+  if (ro_on) {
+    const uint64_t n64 = (d.n + 63) / 64 + 32;
+    CR(sw_rflag.ensure(this, (2 * n64 + 4ull * n_cu + 64) * 8, "sweep read-only survivor bits"));
+    CR(sw_ro.ensure(this, d.n * sizeof(RoEnt) + 64, "sweep read-only list"));
+    CR(sw_wtab.ensure(this, sizeof(WrSlot) << wt_bits, "committed-writer table"));
+    CR(sw_cw.ensure(this, d.n * 4 + 64, "committed writers"));
+  }
   for (SubBufs& b : sw_list) {
     CR(b.tid.ensure(this, d.n * 4 + 16, "sweep list tid"));
     CR(b.off.ensure(this, (d.n + 1) * 4 + 16, "sweep list offsets"));
@@ -360,6 +376,10 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1, const SwShard* shl
   uint64_t* sflag_d = (uint64_t*)sw_status.p;
   unsigned long long* tcount_d = (unsigned long long*)(sflag_d + n64 + 32);
   unsigned long long* bsum_d = tcount_d + n64 + 32;
+  // read-only split (one GPU): level 0 moves its read-only survivors to the
+  // RO list (decided after the levels, sweep_ro)
+  const bool ros = ro_on && !shl;
+  uint32_t* const wctl = abandon;  // [0] abandon [1] writer table full [2] RO count
   for (int l = l0; l < l1; l++) {
     const bool top = l == 0;
     SwList in;
@@ -373,7 +393,7 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1, const SwShard* shl
     SubBufs& out = sw_list[l & 1];
     SwLevel* lv = ctl + l;
     const uint32_t* mdev = top ? nullptr : &lv->m;
-    const uint32_t pmax = sw_pmax(l);
+    const uint32_t pmax = sw_pmax(l, ros);
     const uint64_t tiles = (std::min<uint64_t>(pmax, d.n) + SW_T - 1) / SW_T;
     uint32_t* fw = (uint32_t*)sw_fw.p;
     uint32_t* la = fw + (1u << SW_GBITS_MAX);
@@ -386,8 +406,8 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1, const SwShard* shl
     const uint32_t sm_host = shl ? shl->P : n;
     SwPreArgs pa{sin, smdev, sm_host, pmax, top ? (const uint8_t*)state.p : nullptr,
                  (SwRec*)sw_rec.p, (uint32_t*)sw_rk.p,
-                 gtab0 + (size_t)(l & 1) * (1ull << SW_GBITS_MAX), sw_gbits(l),
-                 sw_budget(l), fw, la, aent, apos, abandon, err, nullptr};
+                 gtab0 + (size_t)(l & 1) * (1ull << SW_GBITS_MAX), sw_gbits(l, ros),
+                 sw_budget(l, ros), fw, la, aent, apos, abandon, err, nullptr};
     if (sw_debug && l < 4) pa.dbg = (uint64_t*)sw_dbg.p + 4096 + 4 * 256 * 8 + (size_t)l * 64 * 8;
     const bool serial_part = !(resume && l == l0);
     if (serial_part) {
@@ -395,11 +415,15 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1, const SwShard* shl
       launch_sw_rows(pa, (unsigned)tiles, stream);
     }
     SwSeqArgs sa{smdev, sm_host, pmax, top ? 1 : 0, (const SwRec*)sw_rec.p, (const uint32_t*)sw_rk.p,
-                 gtab0 + (size_t)(l & 1) * (1ull << SW_GBITS_MAX), sw_gbits(l),
+                 gtab0 + (size_t)(l & 1) * (1ull << SW_GBITS_MAX), sw_gbits(l, ros),
                  (uint8_t*)state.p, (uint8_t*)hasw.p,
                  cbits_d, ckeys_d, bloom_d, lv, lv + 1, (uint32_t*)out.off.p, (uint64_t*)sw_mg.p,
                  abandon, err, nullptr};
     if (sw_debug && l < 4) sa.dbg = (uint64_t*)sw_dbg.p + (size_t)l * 1024;
+    if (ros) {
+      sa.cw_list = (uint32_t*)sw_cw.p;
+      sa.cw_count = wctl + 4;
+    }
     if (top) {  // the epoch's validation pass rides along the level-0 serial pass
       sa.prep_off = d.off;
       sa.prep_n = d.n;
@@ -420,10 +444,9 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1, const SwShard* shl
     fa.m_dev = mdev;
     fa.m_host = n;
     fa.cand_state = top ? 1 : 0;
-    fa.write_hasw = top ? 1 : 0;
     fa.level = (uint32_t)l;
     fa.gtab = gtab0 + (size_t)(l & 1) * (1ull << SW_GBITS_MAX);
-    fa.gbits = sw_gbits(l);
+    fa.gbits = sw_gbits(l, ros);
     fa.cbits = cbits_d;
     fa.bloom = bloom_d;
     fa.ckeys = ckeys_d;
@@ -447,7 +470,7 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1, const SwShard* shl
     fa.abandon_num = top ? 1 : 3;
     fa.abandon_den = 4;
     fa.gclear = gtab0 + (size_t)((l + 1) & 1) * (1ull << SW_GBITS_MAX);
-    fa.gclear_n = 1ull << sw_gbits(l + 1);
+    fa.gclear_n = 1ull << sw_gbits(l + 1, ros);
     fa.fw_clear = fw;
     fa.la_clear = la;
     fa.err = err;
@@ -455,6 +478,12 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1, const SwShard* shl
     fa.cdbg = pa.dbg ? pa.dbg + 32 : nullptr;
     fa.kill_out = shl ? shl->kill : nullptr;
     fa.kill_in = shl ? shl->kill : nullptr;
+    fa.ro_split = (ros && top) ? 1 : 0;
+    fa.rflag = (uint64_t*)sw_rflag.p;
+    fa.rtcount = (unsigned long long*)(fa.rflag + n64 + 32);
+    fa.rbsum = fa.rtcount + n64 + 32;
+    fa.ro_out = (RoEnt*)sw_ro.p;
+    fa.ro_count = wctl + 2;
     // phase 1 of the profile is exactly the level-0 streaming filter
     if (top && profiling) CK(hipEventRecord(pev[1], stream));
     launch_sw_filter(fa, fgrid, stream);
@@ -500,7 +529,7 @@ int dcc_ctx::sweep_sharded(const DevBatch& d, int& next_level) {
     uint32_t* cnt = (uint32_t*)sw_xcnt.p;
     CK(hipMemsetAsync(cnt, 0, 4ull * (R + 2), stream));
     launch_sw_share(top ? nullptr : &ctl[l].m, (uint32_t)d.n, abandon, top ? d.off : in.off,
-                    sw_pmax(l), (uint32_t)me, cnt, stream);
+                    sw_pmax(l, false), (uint32_t)me, cnt, stream);
     CR(comm_allreduce_max_u8((uint8_t*)cnt, 4ull * (R + 2)));
     std::vector<uint32_t> hc(R + 2);
     CK(hipMemcpyAsync(hc.data(), cnt, 4ull * (R + 2), hipMemcpyDeviceToHost, stream));
@@ -508,7 +537,7 @@ int dcc_ctx::sweep_sharded(const DevBatch& d, int& next_level) {
     const uint32_t m = hc[0];
     if (hc[1]) return DCC_OK;  // an earlier level handed off
     if (m == 0) return DCC_OK;
-    const uint32_t P = std::min<uint32_t>(sw_pmax(l), m);
+    const uint32_t P = std::min<uint32_t>(sw_pmax(l, false), m);
     const uint32_t* share = hc.data() + 2;
     uint64_t total = 0, before = 0;
     for (int r = 0; r < R; r++) {
@@ -685,6 +714,33 @@ int dcc_ctx::ck_enqueue(const DevBatch& d, uint32_t r0, uint32_t r1, bool build)
   return DCC_OK;
 }
 
+// The read-only list of a split epoch, once every writer is decided: the
+// writer table of the committed writes (k_sw_wall: the committed writers the
+// serial passes listed, or after a hand-off to the round solver every
+// committed writer of the epoch), then the list against it (k_sw_ro).  `big`:
+// after an overflow, a table sized for every write of the epoch (<= 50 %
+// load, unbounded probes).
+int dcc_ctx::sweep_ro(const DevBatch& d, bool big, bool scan, uint64_t nnz_w) {
+  dcc_ctx* ctx = this;
+  uint32_t* wctl = (uint32_t*)((SwLevel*)sw_ctl.p + SW_MAX_LEVEL + 1);
+  WrTab wt{(WrSlot*)sw_wtab.p, wt_bits, WT_PROBES, wctl + 1};
+  if (big) {
+    uint32_t bits = 10;
+    while (bits < 31 && (1ull << bits) < 2 * std::max<uint64_t>(nnz_w, 1)) bits++;
+    CR(sw_wtab_big.ensure(this, sizeof(WrSlot) << bits, "committed-writer fallback table"));
+    CK(hipMemsetAsync(sw_wtab_big.p, 0xFF, sizeof(WrSlot) << bits, stream));
+    wt = WrTab{(WrSlot*)sw_wtab_big.p, bits, 1u << bits, wctl + 3};
+  }
+  SwWallArgs wa{d.n, d.off, d.keys, d.acctype, d.nnz, (const uint8_t*)state.p,
+                (const uint8_t*)hasw.p, scan ? nullptr : (const uint32_t*)sw_cw.p, wctl + 4, wt};
+  launch_sw_wall(wa, (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(scan ? 4096 : 256, (d.n + 255) / 256)),
+                 stream);
+  SwRoArgs ra{(const RoEnt*)sw_ro.p, wctl + 2, d.keys, wt, (uint8_t*)state.p};
+  launch_sw_ro(ra, (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(4096, (d.n + 63) / 64)), stream);
+  CK(hipGetLastError());
+  return DCC_OK;
+}
+
 int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dcc_stats* st) {
   dcc_ctx* ctx = this;
   // key-sharded across ranks: this rank holds only its keys
@@ -712,9 +768,10 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   DevBatch d;
   CR(stage_batch(b, d));
   const bool sweep = use_sweep();
-  if (sweep) CR(sweep_reserve(d));
   // level 0 of the sweep, then the commit/kill rounds (single GPU)
   const bool ck = sweep && use_ck() && !sh;
+  ro_on = sweep && ro_split && !sh && !ck;
+  if (sweep) CR(sweep_reserve(d));
   if (ck) CR(ck_reserve(d));
   CR(state.ensure(this, d.n + 16, "state"));
   CR(hasw.ensure(this, d.n + 16, "hasw"));
@@ -732,8 +789,13 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   const bool hist_on = d.start_tn && hist_size() > 0;
   const bool graph_ok = sweep && !profiling && !sw_debug && !want_tn && !hist_on && !sh &&
                         !getenv("DCC_NO_GRAPH");
+  // levels per captured epoch (DCC_OPT_SWEEP_LEVELS; 0 = auto: 3 with the
+  // read-only split, 4 without)
+  const uint32_t glv = sw_levels ? sw_levels : (ro_on ? 3u : 4u);
   const GraphKey gkey{d.off, d.keys, d.acctype, d.n, d.nnz, out_rc, dev_out,
-                      ck ? 1000u + 100u * ck_level + ck_graph_rounds : sw_levels, buf_gen};
+                      ck ? 1000u + 100u * ck_level + ck_graph_rounds
+                         : glv | (ro_on ? 0x80u | (wt_bits << 8) : 0u),
+                      buf_gen};
   bool replay = graph_ok && graph_exec && gkey == graph_key;
   bool capturing = false;
   // a failure while capturing must still end the capture
@@ -781,9 +843,10 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
     fa.job[fa.n++] = FillJob{(uint32_t*)state.p, (d.n + 3) / 4, 0u};  // state holds n + 16
     if (sweep) {
       fa.job[fa.n++] = FillJob{(uint32_t*)sw_ctl.p, sw_ctl_bytes() / 4, 0u};
-      fa.job[fa.n++] = FillJob{(uint32_t*)sw_gtab.p, (1ull << sw_gbits(0)) * 2, 0xFFFFFFFFu};
-      fa.job[fa.n++] = FillJob{(uint32_t*)sw_fw.p, 1ull << sw_gbits(0), 0xFFFFFFFFu};
-      fa.job[fa.n++] = FillJob{(uint32_t*)sw_fw.p + (1u << SW_GBITS_MAX), 1ull << sw_gbits(0), 0u};
+      fa.job[fa.n++] = FillJob{(uint32_t*)sw_gtab.p, (1ull << sw_gbits(0, ro_on)) * 2, 0xFFFFFFFFu};
+      fa.job[fa.n++] = FillJob{(uint32_t*)sw_fw.p, 1ull << sw_gbits(0, ro_on), 0xFFFFFFFFu};
+      fa.job[fa.n++] = FillJob{(uint32_t*)sw_fw.p + (1u << SW_GBITS_MAX), 1ull << sw_gbits(0, ro_on), 0u};
+      if (ro_on) fa.job[fa.n++] = FillJob{(uint32_t*)sw_wtab.p, 4ull << wt_bits, 0xFFFFFFFFu};
     }
     launch_fill(fa, stream);  // the sweep's prep runs inside its level-0 serial pass
   }
@@ -816,7 +879,7 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   int serial_tail = -1;  // level enqueued without its filter (sweep_enqueue tail_serial)
   if (sweep) {
     if (profiling) CK(hipEventRecord(pev[0], stream));
-    next_level = ck ? (int)ck_level : (int)std::min<uint32_t>(sw_levels, SW_MAX_LEVEL - 1);
+    next_level = ck ? (int)ck_level : (int)std::min<uint32_t>(glv, SW_MAX_LEVEL - 1);
     if (!sh && !ck && next_level >= 2) serial_tail = next_level - 1;
     if (ck) ck_dirty = true;  // until k_final has reset the table's slots
     if (sh) {
@@ -824,6 +887,7 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
     } else if (!replay) {
       CR(sweep_enqueue(d, 0, next_level, nullptr, false, serial_tail >= 0));
       if (ck) CR(ck_enqueue(d, 1, ck_graph_rounds, true));
+      if (ro_on) CR(sweep_ro(d, false, false, 0));
     }
   } else {
     CR(occ_rounds(top, maxlen, profiling, rounds));
@@ -909,7 +973,7 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
       return fail(DCC_ERANGE, "batch: a txn has %u accesses (> MAX_ROW_PER_TXN=%u)", maxlen,
                   MAX_TXN_LEN);
     // more levels, or hand the remaining list to the round solver
-    bool again = false;
+    bool again = false, ro_fast_rerun = false;
     uint32_t ck_rounds = 0;
     bool ck_done = false;
     if (ck) {
@@ -965,7 +1029,7 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
         const int lt = serial_tail;
         serial_tail = -1;
         if (!ab && t.m > 0 && t.pos < t.m) {
-          const int l1 = std::min(lt + 1 + (int)sw_levels, SW_MAX_LEVEL - 1);
+          const int l1 = std::min(lt + 1 + (int)glv, SW_MAX_LEVEL - 1);
           CR(sweep_enqueue(d, lt, l1, nullptr, true, false));
           next_level = l1;
           GatherArgs ga{};
@@ -983,9 +1047,9 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
       int L = -1;
       if (ab) L = (int)ab;
       else if (hc[next_level].m == 0) break;  // every list decided
-      else if (sh || next_level + (int)sw_levels >= SW_MAX_LEVEL) L = next_level;
+      else if (sh || next_level + (int)glv >= SW_MAX_LEVEL) L = next_level;
       if (L < 0) {
-        const int l1 = next_level + (int)sw_levels;
+        const int l1 = next_level + (int)glv;
         CR(sweep_enqueue(d, next_level, l1));
         next_level = l1;
         GatherArgs ga{};
@@ -1023,9 +1087,35 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
       again = true;
       break;
     }
+    if (ro_on) {
+      // the RO list: decided again after more levels (their commits joined
+      // the writer table), or from the whole decided epoch when a list went
+      // to the round solver (its commits never reach the table) or the table
+      // overflowed (and the next epochs get a larger one)
+      const uint32_t* w = (const uint32_t*)((const SwLevel*)((const char*)hmisc + SW_HCTL) +
+                                            SW_MAX_LEVEL + 1);
+      const bool full = w[1] != 0, ro_n = w[2] != 0;
+      if (full && wt_bits < 24) wt_bits += 2;
+      if (ro_n && (full || again)) {
+        CR(sweep_ro(d, full, handoffs > 0, nnz_w));
+        ro_fast_rerun = !full;
+        again = true;
+      }
+    }
     if (again) {
       if (profiling) CK(hipEventRecord(pev[3], stream));
       CR(enqueue_final());
+    }
+    if (ro_fast_rerun) {
+      // the rerun's table may have overflowed in turn (more commits than the
+      // graph pass saw): then once more with the table sized for every write
+      const uint32_t* w = (const uint32_t*)((const SwLevel*)((const char*)hmisc + SW_HCTL) +
+                                            SW_MAX_LEVEL + 1);
+      if (w[1]) {
+        if (wt_bits < 24) wt_bits += 2;
+        CR(sweep_ro(d, true, handoffs > 0, nnz_w));
+        CR(enqueue_final());
+      }
     }
     const SwLevel* hc = (const SwLevel*)((const char*)hmisc + SW_HCTL);
     if (sw_debug) {

@@ -215,6 +215,57 @@ struct SwList {
   const uint8_t* acctype;
   uint64_t nnz;         // accesses addressable through keys/acctype
 };
+// The epoch's committed writers: key -> the txn id of its committed writer.
+// A key has at most one (the first committed writer of a key kills every
+// later accessor, occ.cpp:185-199), so a slot is written once.  Open
+// addressing, linear probes over 16-B slots (key and writer read together),
+// KEY_EMPTY-filled per epoch; an insert that finds no slot within `probes`
+// sets *full (the host then rebuilds a table sized for every write).
+struct __attribute__((aligned(16))) WrSlot {
+  uint64_t key;
+  uint32_t tid;
+  uint32_t pad;
+};
+struct WrTab {
+  WrSlot* slot;     // [1 << bits]
+  uint32_t bits;
+  uint32_t probes;  // longest probe sequence (WT_PROBES; the whole table for the fallback)
+  uint32_t* full;
+};
+constexpr uint32_t WT_PROBES = 64;
+constexpr uint32_t WT_BITS_DEFAULT = 18;  // 2^18 slots (4 MiB): ~10 % load at the headline
+// A read-only txn the level-0 compaction split off: its id and access range.
+struct RoEnt {
+  uint32_t tid, s, e, pad;
+};
+// k_sw_ro: the split-off read-only txns, decided once every writer is: abort
+// iff a key has a committed writer with a smaller txn id (occ.cpp:185-199
+// with only earlier txns' writes in `active`; read-only txns never enter it).
+struct SwRoArgs {
+  const RoEnt* ro;
+  const uint32_t* ro_count;
+  const uint64_t* keys;
+  WrTab wt;
+  uint8_t* state;
+};
+// k_sw_wall: the committed writers' writes into wt -- the txns the serial
+// passes listed (cw_list, cw_count), or (cw_list null) every committed txn
+// with a write of the decided epoch (after a hand-off to the round solver)
+struct SwWallArgs {
+  uint64_t n;
+  const uint32_t* off;
+  const uint64_t* keys;
+  const uint8_t* acctype;
+  uint64_t nnz;
+  const uint8_t* state;
+  const uint8_t* hasw;
+  const uint32_t* cw_list;
+  const uint32_t* cw_count;
+  WrTab wt;
+};
+void launch_sw_ro(const SwRoArgs& a, unsigned grid, hipStream_t st);
+void launch_sw_wall(const SwWallArgs& a, unsigned grid, hipStream_t st);
+
 struct SwPreArgs {
   SwList in;
   const uint32_t* m_dev;  // list length on the device (null: m_host)
@@ -256,12 +307,17 @@ struct SwSeqArgs {
   uint32_t* err;
   uint64_t* dbg;          // per-tile clock stamps (DCC_SW_DEBUG) or null
   // the epoch's batch validation (prep_body.h), run by workgroups 1.. of the
-  // level-0 launch beside the one-CU serial pass (prep_part null: none)
+  // level-0 launch beside the one-CU serial pass (prep_part null: none); it
+  // also writes every txn's has-write byte into `hasw`
   const uint32_t* prep_off;
   uint64_t prep_n;
   const uint8_t* prep_at;
   uint64_t prep_nnz;
   PrepPart* prep_part;    // [SW_SEQ_PREP_BLOCKS] (pinned host memory)
+  // read-only split: committed txns with a write are appended here (their
+  // writes enter the writer table after the levels, k_sw_wall); null: none
+  uint32_t* cw_list;
+  uint32_t* cw_count;
 };
 constexpr unsigned SW_SEQ_PREP_BLOCKS = 240;  // prep workgroups beside the level-0 serial pass
 struct SwCoutArgs {
@@ -284,7 +340,6 @@ struct SwFilterArgs {
   const uint32_t* m_dev;
   uint32_t m_host;
   int cand_state;         // identity list: only UNDECIDED txns are candidates
-  int write_hasw;
   uint32_t level;
   const uint64_t* gtab;   // the level's key table / committed ids / Bloom filter /
   uint32_t gbits;         // committed keys (k_sw_seq's outputs): the committed set C
@@ -308,6 +363,15 @@ struct SwFilterArgs {
   uint32_t abandon_min, abandon_num, abandon_den;
   uint8_t* kill_out;      // key-sharded: per list position, this shard's kill bit (else null)
   const uint8_t* kill_in; // key-sharded: the all-reduced kill bits (k_sw_apply)
+  // read-only split (level 0, one GPU): read-only survivors (hasw[txn] == 0)
+  // go to ro_out (txn ids, any order) instead of the next list -- no later
+  // level holds them; k_sw_ro decides them once every writer is decided
+  int ro_split;
+  uint64_t* rflag;        // read-only survivor bits per tile
+  unsigned long long* rtcount;  // per tile: read-only survivors << 34 | their accesses
+  unsigned long long* rbsum;    // per filter workgroup: read-only total
+  RoEnt* ro_out;
+  uint32_t* ro_count;     // out: length of ro_out (0 when the level hands off)
   uint64_t* gclear;       // the next level's key table, KEY_EMPTY-filled here
   uint64_t gclear_n;
   uint32_t* fw_clear;     // the next level's first-writer / last-accessor words
@@ -329,7 +393,6 @@ void launch_sw_seq(const SwSeqArgs& a, hipStream_t st);
 void launch_sw_rows(const SwPreArgs& a, unsigned grid, hipStream_t st);
 void launch_sw_cout(const SwCoutArgs& a, unsigned grid, hipStream_t st);
 void launch_sw_filter(const SwFilterArgs& a, unsigned grid, hipStream_t st);
-void launch_sw_scan(const SwFilterArgs& a, hipStream_t st);
 void launch_sw_compact(const SwFilterArgs& a, unsigned grid, hipStream_t st);
 void launch_sw_apply(const SwFilterArgs& a, unsigned grid, hipStream_t st);
 void launch_sw_share(const uint32_t* m_dev, uint32_t m_host, const uint32_t* abandon,

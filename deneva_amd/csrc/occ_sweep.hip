@@ -89,6 +89,34 @@ __device__ inline void bloom_bits(uint64_t key, uint32_t& b1, uint32_t& b2) {
   b2 = (h * 0xC2B2AE35u + 0x27D4EB2Fu) >> (32 - SW_BLOOM_LOG);
 }
 
+// The epoch's committed-writer table (WrTab, occ_kernels.h): linear probes
+// from the key's hash, at most wt.probes slots.
+__device__ inline void wt_insert(const WrTab& wt, uint64_t key, uint32_t tid) {
+  const uint32_t mask = (1u << wt.bits) - 1u;
+  uint32_t s = sw_hash(key, wt.bits);
+  for (uint32_t q = 0; q < wt.probes; q++, s = (s + 1) & mask) {
+    const unsigned long long prev = atomicCAS((unsigned long long*)&wt.slot[s].key,
+                                              (unsigned long long)KEY_EMPTY, (unsigned long long)key);
+    if (prev == KEY_EMPTY || prev == key) {
+      wt.slot[s].tid = tid;  // one committed writer per key: a single value
+      return;
+    }
+  }
+  atomicOr(wt.full, 1u);
+}
+// the key's committed writer, or ~0u (one 16-B load per probe)
+__device__ inline uint32_t wt_find(const WrTab& wt, uint64_t key) {
+  const uint32_t mask = (1u << wt.bits) - 1u;
+  uint32_t s = sw_hash(key, wt.bits);
+  for (uint32_t q = 0; q < wt.probes; q++, s = (s + 1) & mask) {
+    const uint4 v = *(const uint4*)&wt.slot[s];
+    const uint64_t k = ((uint64_t)v.y << 32) | v.x;
+    if (k == key) return v.z;
+    if (k == KEY_EMPTY) break;
+  }
+  return ~0u;
+}
+
 // LDS set of u64 keys in 4-slot buckets (32 B, two ds_read_b128 per bucket).
 // A bucket fills in slot order and a key moves to the next bucket only when
 // its bucket is full, so a bucket with a free last slot ends every chain:
@@ -727,8 +755,8 @@ __global__ __launch_bounds__(SEQ_B) void k_sw_seq(SwSeqArgs a) {
   // workgroups 1.. (level 0 only): the batch validation pass on the CUs the
   // serial pass leaves idle -- the host reads its partials after the epoch
   if (blockIdx.x) {
-    prep_body(a.prep_off, a.prep_n, a.prep_at, a.prep_nnz, 0, a.prep_part, blockIdx.x - 1,
-              gridDim.x - 1);
+    prep_body_hasw(a.prep_off, a.prep_n, a.prep_at, a.prep_nnz, a.hasw, a.prep_part,
+                   blockIdx.x - 1, gridDim.x - 1);
     return;
   }
   uint32_t* const cbits = L.cbits;
@@ -923,13 +951,28 @@ __global__ __launch_bounds__(SEQ_B) void k_sw_seq(SwSeqArgs a) {
   __syncthreads();
   const uint32_t k = s_k;
   // ---- write-out: decisions of tiles [0, k), the level's committed keys
-  for (uint32_t q = j; q < k * SW_T; q += SEQ_B) {
-    const uint32_t kk = q / SW_T, t = q % SW_T;
-    const uint32_t mt = a.rec[kk].meta[t];
-    if (!(mt & SWM_VALID)) continue;
-    const uint32_t tid = a.rec[kk].rtid[t];
-    if (!(mt & SWM_PRE)) a.state[tid] = ((s_M[kk] >> t) & 1ull) ? ST_COMMIT : ST_ABORT;
-    if (a.write_hasw) a.hasw[tid] = (mt & SWM_HASW) ? 1 : 0;
+  for (uint32_t q0 = 0; q0 < k * SW_T; q0 += SEQ_B) {  // uniform trip count (ballots below)
+    const uint32_t q = q0 + j;
+    bool cw = false;
+    uint32_t tid = 0;
+    if (q < k * SW_T) {
+      const uint32_t kk = q / SW_T, t = q % SW_T;
+      const uint32_t mt = a.rec[kk].meta[t];
+      if (mt & SWM_VALID) {
+        tid = a.rec[kk].rtid[t];
+        const bool com = (s_M[kk] >> t) & 1ull;
+        if (!(mt & SWM_PRE)) a.state[tid] = com ? ST_COMMIT : ST_ABORT;
+        if (a.write_hasw) a.hasw[tid] = (mt & SWM_HASW) ? 1 : 0;
+        cw = com && !(mt & SWM_PRE) && (mt & SWM_HASW);
+      }
+    }
+    if (a.cw_list) {  // the committed writers, for the writer table (k_sw_wall)
+      const uint64_t bm = ballot64(cw);
+      uint32_t base = 0;
+      if (lane == 0 && bm) base = atomicAdd(a.cw_count, (uint32_t)__popcll(bm));
+      base = __shfl(base, 0);
+      if (cw) a.cw_list[base + (uint32_t)__popcll(bm & lanemask_lt())] = tid;
+    }
   }
   if (dbg) {
     __syncthreads();
@@ -1079,7 +1122,6 @@ __global__ __launch_bounds__(SW_CHUNK) void k_sw_filter(SwFilterArgs a) {
   uint32_t* const bl = fs.bl;     // both modes' bitmaps start the union
   uint64_t* const cex = fs.x.cex;
   __shared__ uint64_t s_hit[FW][SW_WA / 64];
-  __shared__ uint64_t s_wr[FW][SW_WA / 64];
   __shared__ uint64_t s_stash[FW][F_STASH];
   __shared__ uint32_t s_wpre[FW][SW_WA / 64];
   const uint32_t j = threadIdx.x, lane = lane_id(), wv = j >> 6;
@@ -1111,7 +1153,10 @@ __global__ __launch_bounds__(SW_CHUNK) void k_sw_filter(SwFilterArgs a) {
   const uint32_t R = sw_tiles_per_wg(n64, gridDim.x);
   const uint32_t t_lo = min(blockIdx.x * R, n64), t_hi = min(t_lo + R, n64);
   if (t_lo >= t_hi) {  // idle: no setup
-    if (!a.kill_out && j == 0) a.bsum[blockIdx.x] = 0;
+    if (!a.kill_out && j == 0) {
+      a.bsum[blockIdx.x] = 0;
+      if (a.ro_split) a.rbsum[blockIdx.x] = 0;
+    }
     return;
   }
   const bool small = X;  // exact checks in LDS
@@ -1141,31 +1186,32 @@ __global__ __launch_bounds__(SW_CHUNK) void k_sw_filter(SwFilterArgs a) {
   }
   if (dbg) dbg[1] = __builtin_amdgcn_s_memrealtime();
   uint64_t* hit = s_hit[wv];
-  uint64_t* wr = s_wr[wv];
   uint64_t* stash = s_stash[wv];
-  uint64_t wsum = 0;
+  uint64_t wsum = 0, rsum = 0;
   // the per-txn words of a wave's next tile are loaded while the current
   // tile's keys are in flight (branch-free, clamped: they issue together)
-  uint32_t ns = 0, ne = 0, ntid = 0, nst = 0;
+  uint32_t ns = 0, ne = 0, ntid = 0, nst = 0, nhw = 1;
   auto prefetch = [&](uint32_t wt) {
     const uint32_t pc = min(pos + wt * 64 + lane, m - 1);
     ns = a.in.off[pc];
     ne = a.in.off[pc + 1];
     ntid = a.in.tid ? a.in.tid[pc] : pc;
     nst = a.cand_state ? a.state[pc] : 0u;
+    if (a.ro_split) nhw = a.hasw[pc];  // identity list: pc is the txn
   };
   if (t_lo + wv < t_hi) prefetch(t_lo + wv);
   for (uint32_t wt = t_lo + wv; wt < t_hi; wt += FW) {
     const uint32_t p = pos + wt * 64 + lane;
     const bool valid = p < m;
     uint32_t s = 0, e = 0, tid = 0;
-    bool cand = false;
+    bool cand = false, ro = false;
     if (valid) {
       s = (uint32_t)min((uint64_t)ns, nnz);
       e = (uint32_t)min((uint64_t)ne, nnz);
       if (e < s) e = s;
       tid = ntid;
       cand = nst == ST_UNDECIDED;
+      ro = nhw == 0;
     }
     bool pref = false;
     const uint64_t vm = ballot64(valid);
@@ -1183,13 +1229,11 @@ __global__ __launch_bounds__(SW_CHUNK) void k_sw_filter(SwFilterArgs a) {
     bool bad_key = false;
     for (uint32_t b0 = 0; b0 < span; b0 += 64 * FK) {
       uint64_t key[FK];
-      uint32_t at[FK];
 #pragma unroll
       for (uint32_t u = 0; u < FK; u++) {
         const uint32_t xr = b0 + 64 * u + lane;
         const uint32_t x = A0 + (xr < span ? xr : 0u);
         key[u] = a.in.keys[x];
-        at[u] = a.in.acctype[x];
       }
       if (!pref) {
         pref = true;
@@ -1211,16 +1255,13 @@ __global__ __launch_bounds__(SW_CHUNK) void k_sw_filter(SwFilterArgs a) {
           const uint32_t wa = bl[b1 >> 5], wb = bl[b2 >> 5];
           h = in && (((wa >> (b1 & 31u)) & (wb >> (b2 & 31u)) & 1u) != 0);
         }
-        const uint64_t hb = ballot64(h), wbm = ballot64(in && at[u] == 1);
+        const uint64_t hb = ballot64(h);
         if (h) {
           const uint32_t ci = npos + (uint32_t)__popcll(hb & lanemask_lt());
           if (ci < F_STASH) stash[ci] = key[u];
         }
         npos += (uint32_t)__popcll(hb);
-        if (lane == 0) {
-          hit[(b0 >> 6) + u] = hb;
-          wr[(b0 >> 6) + u] = wbm;
-        }
+        if (lane == 0) hit[(b0 >> 6) + u] = hb;
       }
     }
     if (!pref && wt + FW < t_hi) prefetch(wt + FW);  // a tile without accesses
@@ -1256,7 +1297,6 @@ __global__ __launch_bounds__(SW_CHUNK) void k_sw_filter(SwFilterArgs a) {
     }
     if (dbg && wt == t_lo) dbg[3] = __builtin_amdgcn_s_memrealtime();
     if (dbg) dbg[6]++;
-    if (valid && a.write_hasw) a.hasw[tid] = ok && rlen && range_any(wr, rlo, rlen) ? 1 : 0;
     if (a.kill_out) {  // key-sharded: this shard's kill bit only (k_sw_apply decides)
       if (valid) a.kill_out[p] = killed ? 1 : 0;
       continue;
@@ -1272,19 +1312,36 @@ __global__ __launch_bounds__(SW_CHUNK) void k_sw_filter(SwFilterArgs a) {
       a.sflag[wt] = sm;
       a.tcount[wt] = cnt;
     }
+    if (a.ro_split) {  // read-only survivors, counted apart (k_sw_compact splits them off)
+      const uint64_t rm = ballot64(surv && ro);
+      const uint64_t racc = wave_sum64(surv && ro ? rlen : 0u);
+      const uint64_t rc = ((uint64_t)__popcll(rm) << LB_ACC_BITS) | racc;
+      rsum += rc;
+      if (lane == 0) {
+        a.rflag[wt] = rm;
+        a.rtcount[wt] = rc;
+      }
+    }
     if (dbg && wt == t_lo) {
       __builtin_amdgcn_s_waitcnt(0);
       dbg[4] = __builtin_amdgcn_s_memrealtime();
     }
   }
   if (a.kill_out) return;
-  __shared__ unsigned long long s_bs[FW];
-  if (lane == 0) s_bs[wv] = wsum;
+  __shared__ unsigned long long s_bs[FW][2];
+  if (lane == 0) {
+    s_bs[wv][0] = wsum;
+    s_bs[wv][1] = rsum;
+  }
   __syncthreads();
   if (j == 0) {
-    uint64_t t = 0;
-    for (uint32_t w = 0; w < FW; w++) t += s_bs[w];
+    uint64_t t = 0, r = 0;
+    for (uint32_t w = 0; w < FW; w++) {
+      t += s_bs[w][0];
+      r += s_bs[w][1];
+    }
     a.bsum[blockIdx.x] = t;
+    if (a.ro_split) a.rbsum[blockIdx.x] = r;
   }
   if (dbg) {
     __builtin_amdgcn_s_waitcnt(0);
@@ -1430,62 +1487,6 @@ __global__ __launch_bounds__(256) void k_sw_mscatter(const uint32_t* rec, uint32
 }
 
 // ---------------------------------------------------------------------------
-// k_sw_scan (one workgroup): exclusive scan of the filter workgroups' totals
-// (16 per thread, loaded together); the next list's length, closing offset
-// and the hand-off decision.
-__global__ __launch_bounds__(1024) void k_sw_scan(SwFilterArgs a) {
-  constexpr uint32_t PT = 16;
-  __shared__ unsigned long long s_w[16];
-  __shared__ unsigned long long s_carry;
-  const uint32_t j = threadIdx.x, lane = lane_id(), wv = j >> 6;
-  if (*a.abandon) return;
-  const uint32_t m = list_len(a.m_dev, a.m_host);
-  const uint32_t pos = a.lv->pos;
-  if (pos >= m) return;
-  const uint32_t nb = a.nblocks;
-  if (j == 0) s_carry = 0;
-  __syncthreads();
-  for (uint32_t c0 = 0; c0 < nb; c0 += 1024 * PT) {
-    const uint32_t q0 = c0 + j * PT;
-    uint64_t v[PT], t = 0;
-#pragma unroll
-    for (uint32_t i = 0; i < PT; i++) v[i] = q0 + i < nb ? a.bsum[q0 + i] : 0ull;
-#pragma unroll
-    for (uint32_t i = 0; i < PT; i++) t += v[i];
-    uint64_t x = t;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint64_t y = __shfl_up(x, d);
-      if (lane >= (uint32_t)d) x += y;
-    }
-    if (lane == 63) s_w[wv] = x;
-    __syncthreads();
-    uint64_t base = s_carry;
-    for (uint32_t w = 0; w < wv; w++) base += s_w[w];
-    uint64_t run = base + x - t;  // exclusive prefix of this thread's first block
-#pragma unroll
-    for (uint32_t i = 0; i < PT; i++) {
-      if (q0 + i < nb) a.bsum[q0 + i] = run;
-      run += v[i];
-    }
-    __syncthreads();
-    if (j == 1023) s_carry = base + x;
-    __syncthreads();
-  }
-  if (j == 0) {
-    const uint64_t inc = s_carry;
-    const uint32_t tot = (uint32_t)(inc >> LB_ACC_BITS);
-    const uint64_t acc = inc & ((1ull << LB_ACC_BITS) - 1);
-    a.lv_next->m = tot;
-    a.lv_next->acc = (uint32_t)acc;
-    a.off_out[tot] = (uint32_t)acc;
-    const uint32_t in_n = m - pos;
-    if (tot > a.abandon_min && (uint64_t)tot * a.abandon_den > (uint64_t)in_n * a.abandon_num)
-      atomicMax(a.abandon_out, a.level + 1);
-  }
-}
-
-// ---------------------------------------------------------------------------
 // k_sw_compact: the survivors, in index order, into the next level's list.
 __global__ __launch_bounds__(SW_CHUNK) void k_sw_compact(SwFilterArgs a) {
   const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
@@ -1505,53 +1506,76 @@ __global__ __launch_bounds__(SW_CHUNK) void k_sw_compact(SwFilterArgs a) {
   uint64_t* dbg = (a.cdbg && blockIdx.x == 0 && threadIdx.x == 0) ? a.cdbg : nullptr;
   if (dbg) dbg[0] = __builtin_amdgcn_s_memrealtime();
   __shared__ unsigned long long s_tb[SW_CMP_MAXR];
-  __shared__ unsigned long long s_part[SW_CHUNK / 64][2];
+  __shared__ unsigned long long s_part[SW_CHUNK / 64][4];
+  __shared__ uint32_t s_split, s_rnext;  // RO list: next position of this workgroup's block
   if (R > SW_CMP_MAXR) {
     if (threadIdx.x == 0) atomicOr(a.err, ERR_TILE);
     return;
   }
   // this workgroup's base: the filter workgroups' totals before it (no
-  // separate scan pass); workgroup 0 also closes the level with the total
+  // separate scan pass); workgroup 0 also closes the level with the total.
+  // Read-only survivors (ro_split) leave the list for the RO list unless the
+  // level hands off (every workgroup takes the same decision from the same
+  // totals): packed count|accesses words subtract field by field.
   {
-    uint64_t pre = 0, all = 0;
+    uint64_t pre = 0, all = 0, rpre = 0, rall = 0;
     for (uint32_t q = threadIdx.x; q < a.nblocks; q += SW_CHUNK) {
       const uint64_t v = a.bsum[q];
       all += v;
       if (q < blockIdx.x) pre += v;
+      if (a.ro_split) {
+        const uint64_t r = a.rbsum[q];
+        rall += r;
+        if (q < blockIdx.x) rpre += r;
+      }
     }
     pre = wave_sum64(pre);
     all = wave_sum64(all);
+    rpre = wave_sum64(rpre);
+    rall = wave_sum64(rall);
     if (lane == 0) {
       s_part[wv][0] = pre;
       s_part[wv][1] = all;
+      s_part[wv][2] = rpre;
+      s_part[wv][3] = rall;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-      uint64_t p0 = 0, a0 = 0;
+      uint64_t p0 = 0, a0 = 0, rp = 0, ra = 0;
       for (uint32_t w = 0; w < SW_CHUNK / 64; w++) {
         p0 += s_part[w][0];
         a0 += s_part[w][1];
+        rp += s_part[w][2];
+        ra += s_part[w][3];
       }
-      s_part[0][0] = p0;
+      const uint32_t tot = (uint32_t)(a0 >> LB_ACC_BITS);
+      const uint32_t in_n = m - pos;
+      const bool handoff =
+          tot > a.abandon_min && (uint64_t)tot * a.abandon_den > (uint64_t)in_n * a.abandon_num;
+      const bool split = a.ro_split && !handoff;
+      s_split = split ? 1u : 0u;
+      s_part[0][0] = split ? p0 - rp : p0;
+      s_rnext = (uint32_t)(rp >> LB_ACC_BITS);
       if (blockIdx.x == 0) {
-        const uint32_t tot = (uint32_t)(a0 >> LB_ACC_BITS);
-        const uint64_t acc = a0 & ((1ull << LB_ACC_BITS) - 1);
-        a.lv_next->m = tot;
+        const uint64_t keep = split ? a0 - ra : a0;
+        const uint32_t kt = (uint32_t)(keep >> LB_ACC_BITS);
+        const uint64_t acc = keep & ((1ull << LB_ACC_BITS) - 1);
+        a.lv_next->m = kt;
         a.lv_next->acc = (uint32_t)acc;
-        a.off_out[tot] = (uint32_t)acc;
-        const uint32_t in_n = m - pos;
-        if (tot > a.abandon_min && (uint64_t)tot * a.abandon_den > (uint64_t)in_n * a.abandon_num)
-          atomicMax(a.abandon_out, a.level + 1);
+        a.off_out[kt] = (uint32_t)acc;
+        if (a.ro_split) *a.ro_count = split ? (uint32_t)(ra >> LB_ACC_BITS) : 0u;
+        if (handoff) atomicMax(a.abandon_out, a.level + 1);
       }
     }
     __syncthreads();
   }
+  const bool split = s_split != 0;
   if (dbg) dbg[1] = __builtin_amdgcn_s_memrealtime();
   if (wv == 0) {
     uint64_t run = s_part[0][0];
     for (uint32_t c0 = t_lo; c0 < t_hi; c0 += 64) {
       const uint32_t q = c0 + lane;
-      const uint64_t v = q < t_hi ? a.tcount[q] : 0ull;
+      const uint64_t v = (q < t_hi ? a.tcount[q] : 0ull) - ((split && q < t_hi) ? a.rtcount[q] : 0ull);
       uint64_t x = v;
 #pragma unroll
       for (int d = 1; d < 64; d <<= 1) {
@@ -1568,13 +1592,14 @@ __global__ __launch_bounds__(SW_CHUNK) void k_sw_compact(SwFilterArgs a) {
   // of the CB tiles in flight together, then each tile's moves
   constexpr uint32_t CB = 4;
   for (uint32_t w0 = t_lo + wv; w0 < t_hi; w0 += FW * CB) {
-    uint64_t wordv[CB];
+    uint64_t wordv[CB], rwordv[CB];
     uint32_t sv[CB], ev[CB], tv[CB];
 #pragma unroll
     for (uint32_t i = 0; i < CB; i++) {
       const uint32_t wt = w0 + FW * i;
       const uint32_t pc = min(pos + min(wt, n64 - 1) * 64 + lane, m - 1);
       wordv[i] = wt < t_hi ? a.sflag[wt] : 0ull;
+      rwordv[i] = (split && wt < t_hi) ? a.rflag[wt] : 0ull;
       sv[i] = a.in.off[pc];
       ev[i] = a.in.off[pc + 1];
       tv[i] = a.in.tid ? a.in.tid[pc] : pc;
@@ -1582,7 +1607,18 @@ __global__ __launch_bounds__(SW_CHUNK) void k_sw_compact(SwFilterArgs a) {
 #pragma unroll
     for (uint32_t i = 0; i < CB; i++) {
       const uint32_t wt = w0 + FW * i;
-      const uint64_t word = wordv[i];
+      const uint64_t rword = rwordv[i];
+      const uint64_t word = wordv[i] & ~rword;
+      if (rword) {  // uniform: the RO list's order is free (its txns are decided alone)
+        uint32_t rb = 0;
+        if (lane == 0) rb = atomicAdd(&s_rnext, (uint32_t)__popcll(rword));
+        rb = __shfl(rb, 0);
+        if ((rword >> lane) & 1ull) {
+          const uint32_t rs = (uint32_t)min((uint64_t)sv[i], nnz);
+          a.ro_out[rb + (uint32_t)__popcll(rword & lanemask_lt())] =
+              RoEnt{tv[i], rs, max(rs, (uint32_t)min((uint64_t)ev[i], nnz)), 0u};
+        }
+      }
       if (!word) continue;  // uniform
       const uint64_t base = s_tb[wt - t_lo];
       const uint32_t tb = (uint32_t)(base >> LB_ACC_BITS);
@@ -1642,6 +1678,64 @@ __global__ __launch_bounds__(SW_CHUNK) void k_sw_compact(SwFilterArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// k_sw_ro: the read-only txns level 0 split off, 16 lanes per txn (a lane per
+// access, then every 16th): a key whose committed writer precedes the txn
+// kills it.  Read-only txns never kill or block anyone, so each is decided
+// alone once every writer is.
+__global__ __launch_bounds__(256) void k_sw_ro(SwRoArgs a) {
+  const uint32_t cnt = *a.ro_count;
+  const uint32_t lane = lane_id(), g = lane >> 4, sl = lane & 15u;
+  const uint32_t ng = gridDim.x * 16;
+  for (uint32_t i = (blockIdx.x * 256 + threadIdx.x) >> 4; i < cnt; i += ng) {
+    const uint4 r = *(const uint4*)&a.ro[i];  // tid, first access, end
+    bool kill = false;
+    for (uint32_t x = r.y + sl; x < r.z && !kill; x += 16) kill = wt_find(a.wt, a.keys[x]) < r.x;
+    const uint64_t b = ballot64(kill);
+    if (sl == 0) a.state[r.x] = ((b >> (16 * g)) & 0xFFFFull) ? ST_ABORT : ST_COMMIT;
+  }
+}
+
+// k_sw_wall: the committed writers' writes into the writer table, 16 lanes
+// per txn, four txns per wave step: the txns the serial passes listed, or
+// (fallback) every committed txn with a write found in the epoch's state and
+// has-write bytes (64 per wave).
+__device__ inline void wall_txn(const SwWallArgs& a, uint64_t tt, uint32_t sl) {
+  const uint64_t s = min((uint64_t)a.off[tt], a.nnz), e = min((uint64_t)a.off[tt + 1], a.nnz);
+  for (uint64_t x = s + sl; x < e; x += 16)
+    if (a.acctype[x] == 1) wt_insert(a.wt, a.keys[x], (uint32_t)tt);
+}
+__global__ __launch_bounds__(256) void k_sw_wall(SwWallArgs a) {
+  const uint32_t lane = lane_id(), g = lane >> 4, sl = lane & 15u;
+  if (a.cw_list) {
+    const uint32_t cnt = *a.cw_count;
+    for (uint32_t i = (blockIdx.x * 256 + threadIdx.x) >> 4; i < cnt; i += gridDim.x * 16)
+      wall_txn(a, a.cw_list[i], sl);
+    return;
+  }
+  for (uint64_t t0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) & ~63ull; t0 < a.n;
+       t0 += (uint64_t)gridDim.x * 256) {
+    const uint64_t t = t0 + lane;
+    const bool cw = t < a.n && a.state[t] == ST_COMMIT && a.hasw[t];
+    uint64_t w = ballot64(cw);
+    while (w) {  // uniform: up to four committed writers per step
+      uint32_t pick[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        pick[q] = w ? (uint32_t)__builtin_ctzll(w) : 64u;
+        if (w) w &= w - 1;
+      }
+      if (pick[g] < 64) wall_txn(a, t0 + pick[g], sl);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+void launch_sw_ro(const SwRoArgs& a, unsigned grid, hipStream_t st) {
+  k_sw_ro<<<grid ? grid : 1u, 256, 0, st>>>(a);
+}
+void launch_sw_wall(const SwWallArgs& a, unsigned grid, hipStream_t st) {
+  k_sw_wall<<<grid ? grid : 1u, 256, 0, st>>>(a);
+}
 void launch_sw_pre(const SwPreArgs& a, unsigned grid, hipStream_t st) {
   k_sw_pre<<<grid ? grid : 1u, PRE_B, 0, st>>>(a);
 }
@@ -1657,7 +1751,6 @@ void launch_sw_cout(const SwCoutArgs& a, unsigned grid, hipStream_t st) {
 void launch_sw_filter(const SwFilterArgs& a, unsigned grid, hipStream_t st) {
   k_sw_filter<<<grid ? grid : 1u, SW_CHUNK, 0, st>>>(a);
 }
-void launch_sw_scan(const SwFilterArgs& a, hipStream_t st) { k_sw_scan<<<1, 1024, 0, st>>>(a); }
 void launch_sw_share(const uint32_t* m_dev, uint32_t m_host, const uint32_t* abandon,
                      const uint32_t* off, uint32_t p_max, uint32_t rank, uint32_t* cnt,
                      hipStream_t st) {

@@ -157,11 +157,17 @@ int dcc_set_profiling(dcc_ctx* ctx, int enable);
                                  (levels of serial passes + filters; hands lists that stop
                                  shrinking to the round solver), 4 the sweep's first levels,
                                  then commit/kill rounds over their survivors (single GPU)   */
-#define DCC_OPT_SWEEP_LEVELS 6 /* sweep levels enqueued between host synchronisations       */
+#define DCC_OPT_SWEEP_LEVELS 6 /* sweep levels enqueued between host synchronisations (0:
+                                  auto, 3 with DCC_OPT_RO_SPLIT, 4 without)                  */
 #define DCC_OPT_HIST_MERGE 7  /* device history: delta pairs above which the delta merges into
                                  the base (default 65536; the base/4 rule also applies)      */
 #define DCC_OPT_CK_LEVEL 9    /* solver 4: full sweep levels before the commit/kill rounds
                                  (default 2)                                                 */
+#define DCC_OPT_RO_SPLIT 10   /* sweep: read-only txns that survive the first level's filter
+                                 leave the level lists and are decided once every writer is
+                                 (1, default) or stay in the lists (0); one-GPU epochs only.
+                                 4..24: on, with 2^value committed-writer table slots (the
+                                 table grows after an overflow; tests use small ones)        */
 #define DCC_OPT_FAIL_RANK 8   /* fault injection (tests): rank `value` of a multi-GPU context
                                  fails its next epoch before its first exchange; the other
                                  ranks must return DCC_ECOMM instead of waiting for it      */

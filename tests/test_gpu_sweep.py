@@ -23,7 +23,7 @@ def sw(engine):
     engine.set_option(OPT_SOLVER, 3)
     yield engine
     engine.set_option(OPT_SOLVER, 0)
-    engine.set_option(OPT_SWEEP_LEVELS, 4)
+    engine.set_option(OPT_SWEEP_LEVELS, 0)
 
 
 def run(engine, b, levels=4, hist=None, tnc=0):
