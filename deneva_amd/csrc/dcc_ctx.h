@@ -215,6 +215,11 @@ struct dcc_ctx {
   int maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, dcc_stats* st);
   int calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint32_t* out_group,
                    uint8_t* out_rc, uint32_t* out_wave, dcc_stats* st);
+  // device-side key-shard partition (shard_dev.hip): rank `rank` of R of a
+  // multi-GPU context; sb is the shard as a device batch
+  DevBuf sh_off, sh_keys, sh_at, sh_src, sh_cnt, sh_bsum, sh_rc, sh_tn, sh_grp;
+  int shard_stage(const dcc_batch* b, uint32_t rank, uint32_t R, dcc_batch& sb);
+  int shard_groups(const uint32_t* grp, uint64_t m, uint32_t* out_dev);  // groups to batch order
 };
 
 // multi-GPU context (dcc_multi.cpp)

@@ -4,8 +4,8 @@
 // that one process drives every GPU of the node.
 //
 // The context owns one per-device sub-context per GPU, key-sharded exactly
-// like the one-process-per-GPU path (dcc_key_shard; each sub-context holds
-// only its shard's accesses).  The sub-contexts talk over one RCCL clique
+// like the one-process-per-GPU path (dcc_key_shard; each sub-context keeps
+// only its shard's accesses, partitioned on its own GPU: shard_dev.hip).  The sub-contexts talk over one RCCL clique
 // made with ncclCommInitAll when the device ids are distinct; when ids repeat
 // (several shards on one GPU: tests, or a node with fewer GPUs than shards)
 // over an in-process host exchange.  One host thread per sub-context runs its
@@ -97,42 +97,6 @@ int local_exchange(void* user, uint8_t* buf, uint64_t nb) {
   if (X->result_bad[g & 1] || res.size() != nb) return 1;
   memcpy(buf, res.data(), nb);
   return 0;
-}
-
-// The shard of one rank: its accesses, and where each sat in the batch.
-struct Shard {
-  std::vector<uint32_t> off;
-  std::vector<uint64_t> keys;
-  std::vector<uint8_t> at;
-  std::vector<uint32_t> src;  // batch access index of each shard access
-};
-
-void make_shards(const dcc_batch* b, int R, std::vector<Shard>& sh) {
-  sh.assign(R, Shard{});
-  for (int r = 0; r < R; r++) {
-    sh[r].off.assign(b->n_txn + 1, 0);
-    sh[r].keys.reserve(b->nnz / R + 16);
-    sh[r].at.reserve(b->nnz / R + 16);
-    sh[r].src.reserve(b->nnz / R + 16);
-  }
-  for (uint64_t t = 0; t < b->n_txn; t++) {
-    for (uint32_t x = b->offsets[t]; x < b->offsets[t + 1]; x++) {
-      const int r = (int)dcc_key_shard(b->keys[x], (uint32_t)R);
-      sh[r].keys.push_back(b->keys[x]);
-      sh[r].at.push_back(b->acctype[x]);
-      sh[r].src.push_back(x);
-    }
-    for (int r = 0; r < R; r++) sh[r].off[t + 1] = (uint32_t)sh[r].keys.size();
-  }
-}
-
-dcc_batch shard_batch(const dcc_batch* b, const Shard& s) {
-  dcc_batch o = *b;
-  o.nnz = s.keys.size();
-  o.offsets = s.off.data();
-  o.keys = s.keys.data();
-  o.acctype = s.at.data();
-  return o;
 }
 
 }  // namespace
@@ -238,6 +202,19 @@ extern "C" int dcc_init_multi(dcc_ctx** out, int n_gpus, const int* device_ids) 
         return DCC_ECOMM;
       }
       M->rccl = true;
+      // peer access both ways between every pair: a rank's shard kernels read
+      // a caller's device batch, and Calvin groups are written, over xGMI
+      for (int i = 0; i < n_gpus; i++) {
+        if (hipSetDevice(device_ids[i]) != hipSuccess) continue;
+        for (int j = 0; j < n_gpus; j++) {
+          if (i == j) continue;
+          int can = 0;
+          if (hipDeviceCanAccessPeer(&can, device_ids[i], device_ids[j]) == hipSuccess && can) {
+            const hipError_t pe = hipDeviceEnablePeerAccess(device_ids[j], 0);
+            if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+          }
+        }
+      }
       for (int i = 0; i < n_gpus; i++) {
         r = dcc_comm_attach(M->sub[i], i, n_gpus, comms[i]);
         if (r != DCC_OK) {
@@ -274,36 +251,60 @@ void dcc_multi_destroy(dcc_ctx* ctx) {
   ctx->multi = nullptr;
 }
 
+// Every rank stages the batch (host: its own H2D copy; device: the caller's
+// arrays, read over xGMI when they sit on a peer) and keeps its key shard on
+// its GPU (dcc_ctx::shard_stage, shard_dev.hip); its epoch runs on that device
+// batch into device outputs.  Rank 0's decisions are returned (host outputs:
+// every rank's are compared first).
 int dcc_multi_occ_epoch(dcc_ctx* ctx, const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn,
                         dcc_stats* st) {
   if (!b) return ctx->fail(DCC_EINVAL, "null batch");
-  if (b->flags & DCC_DEVICE_PTRS)
-    return ctx->fail(DCC_ENOTSUP, "multi-GPU context: host batches (it shards them itself)");
   // the whole batch is validated before it is sharded: every rank then
   // runs the same collectives (no rank may fail alone mid-exchange)
   if (int e = ctx->check_batch(b)) return e;
+  const bool dev = (b->flags & DCC_DEVICE_PTRS) != 0;
+  const uint64_t n = b->n_txn;
   const int R = (int)ctx->multi->sub.size();
-  std::vector<Shard> sh;
-  make_shards(b, R, sh);
-  std::vector<std::vector<uint8_t>> rc(R, std::vector<uint8_t>(b->n_txn + 1));
-  std::vector<std::vector<uint64_t>> tn(R, std::vector<uint64_t>(out_tn ? b->n_txn + 1 : 0));
+  std::vector<std::vector<uint8_t>> rc(R);
+  std::vector<uint64_t> tn0;
   std::vector<dcc_stats> S(R);
-  const int e = run_ranks(ctx, [&](int r, dcc_ctx* s) {
-    const dcc_batch sb = shard_batch(b, sh[r]);
-    return dcc_occ_validate_epoch(s, &sb, rc[r].data(), out_tn ? tn[r].data() : nullptr, &S[r]);
+  const int e = run_ranks(ctx, [&](int r, dcc_ctx* s) -> int {
+    dcc_batch sb;
+    int x = s->shard_stage(b, (uint32_t)r, (uint32_t)R, sb);
+    if (x != DCC_OK) return x;
+    if ((x = s->sh_rc.ensure(s, n + 16, "shard rc")) != DCC_OK) return x;
+    if (out_tn && (x = s->sh_tn.ensure(s, n * 8 + 16, "shard tn")) != DCC_OK) return x;
+    uint8_t* drc = (uint8_t*)s->sh_rc.p;
+    uint64_t* dtn = out_tn ? (uint64_t*)s->sh_tn.p : nullptr;
+    if ((x = s->occ_epoch(&sb, drc, dtn, &S[r])) != DCC_OK) return x;
+    hipError_t he = hipSuccess;
+    if (!dev) {
+      rc[r].resize(n + 1);
+      he = hipMemcpy(rc[r].data(), drc, n, hipMemcpyDeviceToHost);
+      if (he == hipSuccess && r == 0 && dtn) {
+        tn0.resize(n);
+        he = hipMemcpy(tn0.data(), dtn, n * 8, hipMemcpyDeviceToHost);
+      }
+    } else if (r == 0) {  // the caller's device arrays (this GPU or a peer)
+      if (out_rc) he = hipMemcpy(out_rc, drc, n, hipMemcpyDeviceToDevice);
+      if (he == hipSuccess && out_tn) he = hipMemcpy(out_tn, dtn, n * 8, hipMemcpyDeviceToDevice);
+    }
+    return he == hipSuccess ? DCC_OK : s->hip_fail(he, "multi-GPU: decisions out");
   });
   if (e != DCC_OK) return e;
-  for (int r = 1; r < R; r++)
-    if (memcmp(rc[r].data(), rc[0].data(), b->n_txn) != 0)
-      return ctx->fail(DCC_EIO, "multi-GPU: ranks 0 and %d decided differently", r);
-  if (out_rc) memcpy(out_rc, rc[0].data(), b->n_txn);
-  if (out_tn) memcpy(out_tn, tn[0].data(), b->n_txn * 8);
+  if (!dev) {
+    for (int r = 1; r < R; r++)
+      if (memcmp(rc[r].data(), rc[0].data(), n) != 0)
+        return ctx->fail(DCC_EIO, "multi-GPU: ranks 0 and %d decided differently", r);
+    if (out_rc) memcpy(out_rc, rc[0].data(), n);
+    if (out_tn) memcpy(out_tn, tn0.data(), n * 8);
+  }
   if (st) {
     *st = S[0];
     for (int r = 1; r < R; r++) st->device_ms = std::max(st->device_ms, S[r].device_ms);
     st->nnz_w = 0;
     for (int r = 0; r < R; r++) st->nnz_w += S[r].nnz_w;
-    st->alg_bytes = dcc_alg_bytes(b->n_txn, b->nnz, st->nnz_w);
+    st->alg_bytes = dcc_alg_bytes(n, b->nnz, st->nnz_w);
   }
   return DCC_OK;
 }
@@ -312,16 +313,16 @@ int dcc_multi_calvin_epoch(dcc_ctx* ctx, const dcc_batch* b, const dcc_calvin_he
                            uint32_t* out_group, uint8_t* out_rc, uint32_t* out_wave,
                            dcc_stats* st) {
   if (!b) return ctx->fail(DCC_EINVAL, "null batch");
-  if (b->flags & DCC_DEVICE_PTRS)
-    return ctx->fail(DCC_ENOTSUP, "multi-GPU context: host batches (it shards them itself)");
   if (out_wave) return ctx->fail(DCC_ENOTSUP, "calvin: wave levels need the whole epoch on one GPU");
   if (int e = ctx->check_batch(b)) return e;
   if (held && held->n && (!held->keys || !held->acctype))
     return ctx->fail(DCC_EINVAL, "calvin: null held arrays");
+  const bool dev = (b->flags & DCC_DEVICE_PTRS) != 0;
+  if (dev && held && held->n)
+    return ctx->fail(DCC_ENOTSUP, "multi-GPU calvin: held rows with host arrays only");
+  const uint64_t n = b->n_txn;
   const int R = (int)ctx->multi->sub.size();
-  std::vector<Shard> sh;
-  make_shards(b, R, sh);
-  // the held prefix is sharded by row as well
+  // the held prefix is sharded by row as well (host)
   std::vector<std::vector<uint64_t>> hk(R);
   std::vector<std::vector<uint8_t>> ha(R);
   if (held)
@@ -330,29 +331,68 @@ int dcc_multi_calvin_epoch(dcc_ctx* ctx, const dcc_batch* b, const dcc_calvin_he
       hk[r].push_back(held->keys[i]);
       ha[r].push_back(held->acctype[i]);
     }
-  std::vector<std::vector<uint8_t>> rc(R, std::vector<uint8_t>(b->n_txn + 1));
-  std::vector<std::vector<uint32_t>> grp(R);
+  std::vector<std::vector<uint8_t>> rc(R);
+  std::vector<std::vector<uint32_t>> grp(R), src(R);
   std::vector<dcc_stats> S(R);
-  const int e = run_ranks(ctx, [&](int r, dcc_ctx* s) {
-    const dcc_batch sb = shard_batch(b, sh[r]);
-    grp[r].resize(sh[r].keys.size() + 1);
-    if (held) {
-      const dcc_calvin_held h{hk[r].size(), hk[r].data(), ha[r].data()};
-      return dcc_calvin_order_epoch_held(s, &sb, &h, grp[r].data(), rc[r].data(), nullptr, &S[r]);
+  const int e = run_ranks(ctx, [&](int r, dcc_ctx* s) -> int {
+    dcc_batch sb;
+    int x = s->shard_stage(b, (uint32_t)r, (uint32_t)R, sb);
+    if (x != DCC_OK) return x;
+    const uint64_t m = sb.nnz;
+    if ((x = s->sh_rc.ensure(s, n + 16, "shard rc")) != DCC_OK) return x;
+    if ((x = s->sh_grp.ensure(s, (m + 16) * 4, "shard groups")) != DCC_OK) return x;
+    uint8_t* drc = (uint8_t*)s->sh_rc.p;
+    uint32_t* dgrp = out_group ? (uint32_t*)s->sh_grp.p : nullptr;
+    if (held && held->n) {
+      // the shard's held rows go to its GPU beside its device batch
+      const uint64_t nh = hk[r].size();
+      if ((x = s->cv_hkeys.ensure(s, std::max<uint64_t>(8, nh * 8), "calvin held keys")) != DCC_OK ||
+          (x = s->cv_hat.ensure(s, std::max<uint64_t>(16, nh), "calvin held types")) != DCC_OK)
+        return x;
+      hipError_t he = hipSuccess;
+      if (nh) {
+        he = hipMemcpy(s->cv_hkeys.p, hk[r].data(), nh * 8, hipMemcpyHostToDevice);
+        if (he == hipSuccess) he = hipMemcpy(s->cv_hat.p, ha[r].data(), nh, hipMemcpyHostToDevice);
+      }
+      if (he != hipSuccess) return s->hip_fail(he, "multi-GPU calvin: held rows in");
+      const dcc_calvin_held h{nh, (const uint64_t*)s->cv_hkeys.p, (const uint8_t*)s->cv_hat.p};
+      x = s->calvin_epoch(&sb, &h, dgrp, drc, nullptr, &S[r]);
+    } else {
+      x = s->calvin_epoch(&sb, nullptr, dgrp, drc, nullptr, &S[r]);
     }
-    return dcc_calvin_order_epoch(s, &sb, grp[r].data(), rc[r].data(), nullptr, &S[r]);
+    if (x != DCC_OK) return x;
+    hipError_t he = hipSuccess;
+    if (!dev) {
+      if (r == 0) {
+        rc[0].resize(n + 1);
+        he = hipMemcpy(rc[0].data(), drc, n, hipMemcpyDeviceToHost);
+      }
+      if (he == hipSuccess && dgrp && m) {
+        grp[r].resize(m);
+        src[r].resize(m);
+        he = hipMemcpy(grp[r].data(), dgrp, m * 4, hipMemcpyDeviceToHost);
+        if (he == hipSuccess) he = hipMemcpy(src[r].data(), s->sh_src.p, m * 4, hipMemcpyDeviceToHost);
+      }
+    } else {
+      if (r == 0 && out_rc) he = hipMemcpy(out_rc, drc, n, hipMemcpyDeviceToDevice);
+      if (he == hipSuccess && dgrp && (x = s->shard_groups(dgrp, m, out_group)) != DCC_OK) return x;
+      if (he == hipSuccess) he = hipStreamSynchronize(s->stream);
+    }
+    return he == hipSuccess ? DCC_OK : s->hip_fail(he, "multi-GPU calvin: results out");
   });
   if (e != DCC_OK) return e;
-  if (out_rc) memcpy(out_rc, rc[0].data(), b->n_txn);
-  if (out_group)
-    for (int r = 0; r < R; r++)
-      for (size_t j = 0; j < sh[r].src.size(); j++) out_group[sh[r].src[j]] = grp[r][j];
+  if (!dev) {
+    if (out_rc) memcpy(out_rc, rc[0].data(), n);
+    if (out_group)
+      for (int r = 0; r < R; r++)
+        for (size_t j = 0; j < src[r].size(); j++) out_group[src[r][j]] = grp[r][j];
+  }
   if (st) {
     *st = S[0];
     for (int r = 1; r < R; r++) st->device_ms = std::max(st->device_ms, S[r].device_ms);
     st->nnz_w = 0;
     for (int r = 0; r < R; r++) st->nnz_w += S[r].nnz_w;
-    st->alg_bytes = dcc_calvin_alg_bytes(b->n_txn, b->nnz, b->order != nullptr, 0);
+    st->alg_bytes = dcc_calvin_alg_bytes(n, b->nnz, b->order != nullptr, 0);
   }
   return DCC_OK;
 }

@@ -135,9 +135,13 @@ int dcc_init(dcc_ctx** out, int device_id);
  * the context key-shards every epoch over n per-device sub-contexts
  * (dcc_key_shard) that exchange over one RCCL clique (ncclCommInitAll) when
  * the ids are distinct, else over an in-process host exchange (shards sharing
- * a GPU).  OCC and Calvin epochs take host batches and return the same
- * decisions as one GPU; options, tnc and history apply to every shard.
- * Snapshot validation, MaaT and dcc_set_stream are DCC_ENOTSUP on it. */
+ * a GPU).  Each sub-context partitions the batch on its own GPU (a host batch
+ * is copied to every GPU; a device batch, DCC_DEVICE_PTRS, is read where it
+ * lies -- peer access between distinct GPUs is enabled here).  OCC and Calvin
+ * epochs return the same decisions as one GPU (device outputs are written by
+ * rank 0); options, tnc and history apply to every shard.  Snapshot
+ * validation, MaaT, Calvin waves, held rows with a device batch and
+ * dcc_set_stream are DCC_ENOTSUP on it. */
 int dcc_init_multi(dcc_ctx** out, int n_gpus, const int* device_ids);
 void dcc_destroy(dcc_ctx* ctx);
 const char* dcc_strerror(int code);

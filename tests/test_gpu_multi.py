@@ -68,14 +68,40 @@ def test_multi_history_and_calvin():
         assert np.array_equal(np.asarray(crc), erc2)
 
 
-def test_multi_rejects_device_batches_and_snapshot():
-    import torch
+def test_multi_rejects_maat():
     b = d.gen_ycsb(n_txn=1000, zipf_theta=0.9)
     with d.Engine(devices=[0, 0]) as eng:
         with pytest.raises(d.DccError):
-            eng.occ_validate_epoch(b.to_torch("cuda:0"))
-        with pytest.raises(d.DccError):
             eng.maat_validate_epoch(b)
+
+
+@pytest.mark.parametrize("shards", [2, 4])
+def test_multi_device_batch_occ(c5, shards):
+    """A device batch (DCC_DEVICE_PTRS): every rank partitions it on its own
+    GPU (shard_dev.hip) instead of the host splitting it; decisions and commit
+    tns land in the caller's device arrays, equal to the oracle's."""
+    import torch
+    b, erc, etn, etnc = c5
+    db = b.to_torch("cuda:0")
+    with d.Engine(devices=[0] * shards) as eng:
+        eng.tnc = 0
+        rc, tn, st = eng.occ_validate_epoch(db, want_tn=True)
+        torch.cuda.synchronize()
+        assert np.array_equal(rc.cpu().numpy(), erc)
+        assert np.array_equal(tn.cpu().numpy().view(np.uint64), etn)
+        assert eng.tnc == etnc and st["n_shards"] == shards
+
+
+def test_multi_device_batch_calvin():
+    import torch
+    c = d.gen_ycsb(n_txn=60000, zipf_theta=0.9, part_cnt=4, chunk_txns=4096)
+    c.order = np.random.default_rng(5).integers(0, 1 << 20, size=c.n_txn).astype(np.uint64)
+    eg, erc, _ = orc.calvin(c)
+    with d.Engine(devices=[0, 0, 0]) as eng:
+        g, rc, _, _ = eng.calvin_order_epoch(c.to_torch("cuda:0"), want_group=True)
+        torch.cuda.synchronize()
+        assert np.array_equal(g.cpu().numpy().view(np.uint32), eg)
+        assert np.array_equal(rc.cpu().numpy(), erc)
 
 
 @pytest.fixture(scope="module")
