@@ -423,6 +423,10 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1, const SwShard* shl
     if (ros) {
       sa.cw_list = (uint32_t*)sw_cw.p;
       sa.cw_count = wctl + 4;
+      if (top) {
+        sa.wclear = (uint4*)sw_wtab.p;
+        sa.wclear_n16 = (sizeof(WrSlot) << wt_bits) / 16;
+      }
     }
     if (top) {  // the epoch's validation pass rides along the level-0 serial pass
       sa.prep_off = d.off;
@@ -846,7 +850,6 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
       fa.job[fa.n++] = FillJob{(uint32_t*)sw_gtab.p, (1ull << sw_gbits(0, ro_on)) * 2, 0xFFFFFFFFu};
       fa.job[fa.n++] = FillJob{(uint32_t*)sw_fw.p, 1ull << sw_gbits(0, ro_on), 0xFFFFFFFFu};
       fa.job[fa.n++] = FillJob{(uint32_t*)sw_fw.p + (1u << SW_GBITS_MAX), 1ull << sw_gbits(0, ro_on), 0u};
-      if (ro_on) fa.job[fa.n++] = FillJob{(uint32_t*)sw_wtab.p, 4ull << wt_bits, 0xFFFFFFFFu};
     }
     launch_fill(fa, stream);  // the sweep's prep runs inside its level-0 serial pass
   }

@@ -318,6 +318,8 @@ struct SwSeqArgs {
   // writes enter the writer table after the levels, k_sw_wall); null: none
   uint32_t* cw_list;
   uint32_t* cw_count;
+  uint4* wclear;          // level 0: the writer table, cleared by the prep workgroups
+  uint64_t wclear_n16;    // its size in 16-B words (0: none)
 };
 constexpr unsigned SW_SEQ_PREP_BLOCKS = 240;  // prep workgroups beside the level-0 serial pass
 struct SwCoutArgs {

@@ -757,6 +757,12 @@ __global__ __launch_bounds__(SEQ_B) void k_sw_seq(SwSeqArgs a) {
   if (blockIdx.x) {
     prep_body_hasw(a.prep_off, a.prep_n, a.prep_at, a.prep_nnz, a.hasw, a.prep_part,
                    blockIdx.x - 1, gridDim.x - 1);
+    // the epoch's committed-writer table, KEY_EMPTY-filled here (used only
+    // after the last level)
+    const uint4 e = make_uint4(~0u, ~0u, ~0u, ~0u);
+    for (uint64_t q = (uint64_t)(blockIdx.x - 1) * SEQ_B + threadIdx.x; q < a.wclear_n16;
+         q += (uint64_t)(gridDim.x - 1) * SEQ_B)
+      a.wclear[q] = e;
     return;
   }
   uint32_t* const cbits = L.cbits;
@@ -950,28 +956,50 @@ __global__ __launch_bounds__(SEQ_B) void k_sw_seq(SwSeqArgs a) {
   }
   __syncthreads();
   const uint32_t k = s_k;
-  // ---- write-out: decisions of tiles [0, k), the level's committed keys
-  for (uint32_t q0 = 0; q0 < k * SW_T; q0 += SEQ_B) {  // uniform trip count (ballots below)
-    const uint32_t q = q0 + j;
-    bool cw = false;
-    uint32_t tid = 0;
-    if (q < k * SW_T) {
-      const uint32_t kk = q / SW_T, t = q % SW_T;
-      const uint32_t mt = a.rec[kk].meta[t];
-      if (mt & SWM_VALID) {
-        tid = a.rec[kk].rtid[t];
-        const bool com = (s_M[kk] >> t) & 1ull;
-        if (!(mt & SWM_PRE)) a.state[tid] = com ? ST_COMMIT : ST_ABORT;
-        if (a.write_hasw) a.hasw[tid] = (mt & SWM_HASW) ? 1 : 0;
-        cw = com && !(mt & SWM_PRE) && (mt & SWM_HASW);
+  // ---- write-out: decisions of tiles [0, k), the level's committed keys.
+  // WO_U positions per thread and step, their record words loaded together
+  // (one round trip per step instead of one per position)
+  constexpr uint32_t WO_U = 8;
+  for (uint32_t q0 = 0; q0 < k * SW_T; q0 += SEQ_B * WO_U) {  // uniform trip count (ballots)
+    uint32_t mt[WO_U], tid[WO_U];
+#pragma unroll
+    for (uint32_t u = 0; u < WO_U; u++) {
+      const uint32_t q = q0 + u * SEQ_B + j;
+      mt[u] = 0;
+      tid[u] = 0;
+      if (q < k * SW_T) {
+        mt[u] = a.rec[q / SW_T].meta[q % SW_T];
+        tid[u] = a.rec[q / SW_T].rtid[q % SW_T];
+      }
+    }
+    bool cw[WO_U];
+#pragma unroll
+    for (uint32_t u = 0; u < WO_U; u++) {
+      const uint32_t q = q0 + u * SEQ_B + j;
+      cw[u] = false;
+      if (mt[u] & SWM_VALID) {
+        const bool com = (s_M[q / SW_T] >> (q % SW_T)) & 1ull;
+        if (!(mt[u] & SWM_PRE)) a.state[tid[u]] = com ? ST_COMMIT : ST_ABORT;
+        if (a.write_hasw) a.hasw[tid[u]] = (mt[u] & SWM_HASW) ? 1 : 0;
+        cw[u] = com && !(mt[u] & SWM_PRE) && (mt[u] & SWM_HASW);
       }
     }
     if (a.cw_list) {  // the committed writers, for the writer table (k_sw_wall)
-      const uint64_t bm = ballot64(cw);
+      uint64_t bm[WO_U];
+      uint32_t tot = 0;
+#pragma unroll
+      for (uint32_t u = 0; u < WO_U; u++) {
+        bm[u] = ballot64(cw[u]);
+        tot += (uint32_t)__popcll(bm[u]);
+      }
       uint32_t base = 0;
-      if (lane == 0 && bm) base = atomicAdd(a.cw_count, (uint32_t)__popcll(bm));
+      if (lane == 0 && tot) base = atomicAdd(a.cw_count, tot);
       base = __shfl(base, 0);
-      if (cw) a.cw_list[base + (uint32_t)__popcll(bm & lanemask_lt())] = tid;
+#pragma unroll
+      for (uint32_t u = 0; u < WO_U; u++) {
+        if (cw[u]) a.cw_list[base + (uint32_t)__popcll(bm[u] & lanemask_lt())] = tid[u];
+        base += (uint32_t)__popcll(bm[u]);
+      }
     }
   }
   if (dbg) {
