@@ -152,7 +152,7 @@ struct dcc_ctx {
   uint64_t mt_rows = 0;                          // rows in the table
   uint32_t mt_rows32 = 0;                        // upload source of the row counter
   DevBuf mt_misc, mt_slot, mt_sval, mt_slot2, mt_sval2, mt_sfl, mt_stx, mt_txn, mt_agg;
-  DevBuf mt_sflB, mt_stxB, mt_k1, mt_tcnt;
+  DevBuf mt_sflB, mt_stxB, mt_k1, mt_tcnt, mt_ul;
   // GPU index (index.hip): key table, newest insert ordinal per key, rows
   DevBuf ix_keys, ix_ord, ix_rows, ix_cnt, wv_buf, ix_scr, wv_hbuf, wv_obuf;
   uint32_t ix_bits = 0;

@@ -30,6 +30,8 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "dcc.h"
@@ -58,6 +60,7 @@ constexpr uint32_t MT_ITEMS = 16;
 constexpr uint32_t MT_TILE = 256 * MT_ITEMS;
 constexpr uint32_t MT_RING = 64;          // per-round undecided counters
 constexpr uint32_t MT_BATCH = 4;          // rounds enqueued per host check
+constexpr uint64_t MT_LONG = 1u << 21;    // scans longer than this: a check after every round
 constexpr uint8_t ST_UND = 0, ST_COM = 1, ST_ABO = 2;
 // sorted-position flags
 constexpr uint8_t F_R = 1, F_W = 2, F_LAST = 4, F_START = 8;
@@ -362,49 +365,110 @@ struct MtRoundArgs {
   Ms* agg;
 };
 
-__device__ inline Ms block_reduce_ms(Ms v, Ms* s) {
-  s[threadIdx.x] = v;
-  __syncthreads();
-  for (uint32_t w = 1; w < 256; w <<= 1) {
-    if ((threadIdx.x & (2 * w - 1)) == 0) s[threadIdx.x] = ms_comb(s[threadIdx.x], s[threadIdx.x + w]);
-    __syncthreads();
+// wave shuffles of the four fields, then the four waves' totals through LDS
+__device__ inline Ms ms_shfl_up(const Ms& v, uint32_t d) {
+  Ms r;
+  r.flag = __shfl_up(v.flag, d);
+  r.und = __shfl_up(v.und, d);
+  r.rmax = __shfl_up(v.rmax, d);
+  r.wmin = __shfl_up(v.wmin, d);
+  return r;
+}
+__device__ inline Ms wave_incl_ms(Ms x) {
+  const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const Ms y = ms_shfl_up(x, d);
+    if (lane >= d) x = ms_comb(y, x);
   }
-  return s[0];
+  return x;
+}
+__device__ inline Ms block_reduce_ms(Ms v, Ms* s) {
+  const Ms x = wave_incl_ms(v);
+  if ((threadIdx.x & 63) == 63) s[threadIdx.x >> 6] = x;
+  __syncthreads();
+  Ms r = s[0];
+  for (uint32_t w = 1; w < 4; w++) r = ms_comb(r, s[w]);
+  __syncthreads();
+  return r;
 }
 __device__ inline Ms block_excl_ms(Ms v, Ms* s) {
-  s[threadIdx.x] = v;
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const Ms x = wave_incl_ms(v);
+  if (lane == 63) s[wv] = x;
   __syncthreads();
-  for (uint32_t d = 1; d < 256; d <<= 1) {
-    Ms r = s[threadIdx.x];
-    if (threadIdx.x >= d) r = ms_comb(s[threadIdx.x - d], r);
-    __syncthreads();
-    s[threadIdx.x] = r;
-    __syncthreads();
+  Ms pre = ms_id();
+  for (uint32_t w = 0; w < wv; w++) pre = ms_comb(pre, s[w]);
+  Ms ex = ms_shfl_up(x, 1);
+  if (lane == 0) ex = ms_id();
+  __syncthreads();
+  return ms_comb(pre, ex);
+}
+
+// A tile's flags and txns in the blocked arrangement the scans need (thread
+// t: positions 16t .. 16t + 15 of the tile), loaded with coalesced 16-B loads
+// (flags: 4 per thread, txns: 16 words per thread as 4 loads) through LDS --
+// a thread reading its own 16 consecutive positions straight from memory
+// spreads every wave instruction over 64 lines.  Past the end: flags 0, an
+// identity element of every scan.
+struct MtTileLds {
+  uint4 f[MT_TILE / 16];
+  uint4 x[MT_TILE / 4];
+};
+__device__ inline void mt_load_tile(const uint8_t* sfl, const uint32_t* stx, uint64_t m, uint64_t base,
+                                    MtTileLds& L, uint8_t (&f)[MT_ITEMS], uint32_t (&tx)[MT_ITEMS]) {
+  const uint32_t tid = threadIdx.x;
+  const uint64_t n_here = m > base ? min<uint64_t>(MT_TILE, m - base) : 0;
+  const bool full = n_here == MT_TILE && ((uintptr_t)(sfl + base) & 15) == 0 &&
+                    ((uintptr_t)(stx + base) & 15) == 0;
+  if (full) {
+    L.f[tid] = ((const uint4*)(sfl + base))[tid];
+#pragma unroll
+    for (uint32_t i = 0; i < 4; i++) L.x[i * 256 + tid] = ((const uint4*)(stx + base))[i * 256 + tid];
+  } else {
+    uint8_t* lf = (uint8_t*)L.f;
+    uint32_t* lx = (uint32_t*)L.x;
+    for (uint32_t q = tid; q < MT_TILE; q += 256) {
+      lf[q] = q < n_here ? sfl[base + q] : (uint8_t)0;
+      lx[q] = q < n_here ? stx[base + q] : 0u;
+    }
   }
-  const Ms ex = threadIdx.x ? s[threadIdx.x - 1] : ms_id();
   __syncthreads();
-  return ex;
+  const uint4 fw = L.f[tid];
+  const uint32_t w4[4] = {fw.x, fw.y, fw.z, fw.w};
+#pragma unroll
+  for (uint32_t i = 0; i < MT_ITEMS; i++) f[i] = (uint8_t)(w4[i >> 2] >> (8 * (i & 3)));
+#pragma unroll
+  for (uint32_t i = 0; i < 4; i++) {
+    const uint4 v = L.x[tid * 4 + i];
+    tx[4 * i] = v.x;
+    tx[4 * i + 1] = v.y;
+    tx[4 * i + 2] = v.z;
+    tx[4 * i + 3] = v.w;
+  }
+  __syncthreads();  // the caller may reuse L
 }
 
 __global__ __launch_bounds__(256) void k_mt_up(MtRoundArgs a) {
   __shared__ Ms s[256];
-  const uint64_t p0 = (uint64_t)blockIdx.x * MT_TILE + (uint64_t)threadIdx.x * MT_ITEMS;
+  __shared__ MtTileLds L;
+  const uint64_t base = (uint64_t)blockIdx.x * MT_TILE;
+  uint8_t f[MT_ITEMS];
+  uint32_t tx[MT_ITEMS];
+  mt_load_tile(a.sfl, a.stx, a.m, base, L, f, tx);
+  uint8_t st[MT_ITEMS];
+  uint64_t c[MT_ITEMS];
+#pragma unroll
+  for (uint32_t i = 0; i < MT_ITEMS; i++) {  // the gathers of a thread's group ends together
+    st[i] = (f[i] & F_LAST) ? a.state[tx[i]] : ST_ABO;
+    c[i] = 0;
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < MT_ITEMS; i++)
+    if (st[i] == ST_COM) c[i] = a.cts[tx[i]];
   Ms acc = ms_id();
 #pragma unroll
-  for (uint32_t i = 0; i < MT_ITEMS; i++) {
-    const uint64_t p = p0 + i;
-    if (p < a.m) {
-      const uint8_t f = a.sfl[p];
-      uint8_t st = ST_ABO;
-      uint64_t c = 0;
-      if (f & F_LAST) {
-        const uint32_t t = a.stx[p];
-        st = a.state[t];
-        if (st == ST_COM) c = a.cts[t];
-      }
-      acc = ms_comb(acc, ms_elem(f, st, c));
-    }
-  }
+  for (uint32_t i = 0; i < MT_ITEMS; i++) acc = ms_comb(acc, ms_elem(f[i], st[i], c[i]));
   const Ms r = block_reduce_ms(acc, s);
   if (threadIdx.x == 0) a.agg[blockIdx.x] = r;
 }
@@ -431,28 +495,24 @@ __global__ __launch_bounds__(256) void k_mt_top(Ms* agg, uint32_t tiles) {
 // row it touches, pending from undecided ones
 __global__ __launch_bounds__(256) void k_mt_down(MtRoundArgs a) {
   __shared__ Ms s[256];
-  const uint64_t p0 = (uint64_t)blockIdx.x * MT_TILE + (uint64_t)threadIdx.x * MT_ITEMS;
+  __shared__ MtTileLds L;
+  const uint64_t base = (uint64_t)blockIdx.x * MT_TILE;
+  const uint64_t p0 = base + (uint64_t)threadIdx.x * MT_ITEMS;
   uint8_t f[MT_ITEMS], st[MT_ITEMS];
   uint32_t tx[MT_ITEMS];
   uint64_t c[MT_ITEMS];
-  Ms acc = ms_id();
+  mt_load_tile(a.sfl, a.stx, a.m, base, L, f, tx);
 #pragma unroll
   for (uint32_t i = 0; i < MT_ITEMS; i++) {
-    const uint64_t p = p0 + i;
-    f[i] = 0;
-    st[i] = ST_ABO;
-    tx[i] = 0;
+    st[i] = (f[i] & F_LAST) ? a.state[tx[i]] : ST_ABO;
     c[i] = 0;
-    if (p < a.m) {
-      f[i] = a.sfl[p];
-      if (f[i] & F_LAST) {
-        tx[i] = a.stx[p];
-        st[i] = a.state[tx[i]];
-        if (st[i] == ST_COM) c[i] = a.cts[tx[i]];
-      }
-      acc = ms_comb(acc, ms_elem(f[i], st[i], c[i]));
-    }
   }
+#pragma unroll
+  for (uint32_t i = 0; i < MT_ITEMS; i++)
+    if (st[i] == ST_COM) c[i] = a.cts[tx[i]];
+  Ms acc = ms_id();
+#pragma unroll
+  for (uint32_t i = 0; i < MT_ITEMS; i++) acc = ms_comb(acc, ms_elem(f[i], st[i], c[i]));
   Ms run = ms_comb(a.agg[blockIdx.x], block_excl_ms(acc, s));
 #pragma unroll
   for (uint32_t i = 0; i < MT_ITEMS; i++) {
@@ -464,7 +524,8 @@ __global__ __launch_bounds__(256) void k_mt_down(MtRoundArgs a) {
       const uint32_t t = tx[i];
       if ((f[i] & F_W) && run.rmax) atomicMax((unsigned long long*)&a.lacc[t], run.rmax + 1);
       if (run.wmin != U64MAX) atomicMin((unsigned long long*)&a.uacc[t], run.wmin - 1);
-      if ((run.und & 2u) || ((f[i] & F_W) && (run.und & 1u))) atomicOr(&a.pend[t], 1u);
+      // a plain store: every writer of the word stores the same 1 (decide resets it)
+      if ((run.und & 2u) || ((f[i] & F_W) && (run.und & 1u))) a.pend[t] = 1u;
     }
     run = ms_comb(run, ms_elem(f[i] & ~F_START, st[i], c[i]));
   }
@@ -472,13 +533,17 @@ __global__ __launch_bounds__(256) void k_mt_down(MtRoundArgs a) {
 
 // decide: abort when the known bounds are already empty, commit when no
 // relevant predecessor is undecided; reset the accumulators
-__global__ __launch_bounds__(256) void k_mt_decide(uint64_t n, const uint64_t* base, uint8_t* state,
+// (over the undecided-txn list ul[0, *ulen) when given, else txns [0, n))
+__global__ __launch_bounds__(256) void k_mt_decide(uint64_t n, const uint32_t* ul, const uint32_t* ulen,
+                                                   const uint64_t* base, uint8_t* state,
                                                    uint64_t* cts, uint64_t* lacc, uint64_t* uacc,
                                                    uint32_t* pend, uint32_t* und_out,
                                                    uint32_t* und_zero) {
   __shared__ uint32_t sh[4];
   uint32_t und = 0;
-  for (uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x; t < n; t += (uint64_t)gridDim.x * 256) {
+  const uint64_t cnt = ul ? *ulen : n;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < cnt; i += (uint64_t)gridDim.x * 256) {
+    const uint64_t t = ul ? ul[i] : i;
     if (state[t] != ST_UND) continue;
     const uint64_t L = max(base[t], lacc[t]);
     const uint64_t U = uacc[t];
@@ -504,6 +569,38 @@ __global__ __launch_bounds__(256) void k_mt_decide(uint64_t n, const uint64_t* b
   }
 }
 
+// the undecided txns of a list (any order: each is decided on its own)
+__global__ __launch_bounds__(256) void k_mt_ucompact(const uint32_t* ul, const uint32_t* ulen, uint64_t n,
+                                                     const uint8_t* state, uint32_t* out,
+                                                     uint32_t* out_len) {
+  // one counter atomic per workgroup and step (same-address atomics
+  // serialise: one per wave cost 190 us over a 1M-txn list)
+  __shared__ uint32_t s_n[4], s_b;
+  const uint64_t cnt = ul ? *ulen : n;
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (uint64_t i0 = (uint64_t)blockIdx.x * 256; i0 < cnt; i0 += (uint64_t)gridDim.x * 256) {
+    const uint64_t i = i0 + threadIdx.x;
+    uint32_t t = 0;
+    bool keep = false;
+    if (i < cnt) {
+      t = ul ? ul[i] : (uint32_t)i;
+      keep = state[t] == ST_UND;
+    }
+    const uint64_t bm = ballot64(keep);
+    if (lane == 0) s_n[wv] = (uint32_t)__popcll(bm);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint32_t tot = s_n[0] + s_n[1] + s_n[2] + s_n[3];
+      s_b = tot ? atomicAdd(out_len, tot) : 0u;
+    }
+    __syncthreads();
+    uint32_t b = s_b;
+    for (uint32_t w = 0; w < wv; w++) b += s_n[w];
+    if (keep) out[b + (uint32_t)__popcll(bm & ((1ull << lane) - 1ull))] = t;
+    __syncthreads();
+  }
+}
+
 // ---------------------------------------------------------------- compaction
 // Between rounds the scan input shrinks to what can still matter: the last
 // position of every group of an undecided or committed txn (aborted txns
@@ -517,11 +614,12 @@ __global__ __launch_bounds__(256) void k_mt_keep_count(uint64_t m, const uint8_t
                                                        const uint32_t* stx, const uint8_t* state,
                                                        uint32_t* tcnt) {
   __shared__ uint32_t s_c[4];
-  const uint64_t p0 = (uint64_t)blockIdx.x * MT_TILE + (uint64_t)threadIdx.x * MT_ITEMS;
+  // the count only: positions in the striped order (coalesced loads)
+  const uint64_t base = (uint64_t)blockIdx.x * MT_TILE;
   uint32_t c = 0;
 #pragma unroll
   for (uint32_t i = 0; i < MT_ITEMS; i++) {
-    const uint64_t p = p0 + i;
+    const uint64_t p = base + i * 256 + threadIdx.x;
     if (p < m) {
       const uint8_t f = sfl[p];
       if ((f & F_LAST) && mt_keep(f, state[stx[p]])) c++;
@@ -532,24 +630,29 @@ __global__ __launch_bounds__(256) void k_mt_keep_count(uint64_t m, const uint8_t
   __syncthreads();
   if (threadIdx.x == 0) tcnt[blockIdx.x] = s_c[0] + s_c[1] + s_c[2] + s_c[3];
 }
+// the kept positions of a tile, in order: blocked arrangement for the
+// prefix (loads through LDS), the kept ones staged in LDS at their tile
+// offsets, then stored with coalesced stores
 __global__ __launch_bounds__(256) void k_mt_keep_scatter(uint64_t m, const uint8_t* sfl,
                                                          const uint32_t* stx, const uint32_t* ss,
                                                          const uint8_t* state, const uint32_t* tpre,
                                                          uint8_t* sfl2, uint32_t* stx2, uint32_t* ss2) {
   __shared__ uint32_t s_w[4];
-  const uint64_t p0 = (uint64_t)blockIdx.x * MT_TILE + (uint64_t)threadIdx.x * MT_ITEMS;
+  __shared__ MtTileLds L;
+  __shared__ uint32_t s_ss[MT_TILE];
+  const uint64_t base = (uint64_t)blockIdx.x * MT_TILE;
+  const uint64_t n_here = m > base ? min<uint64_t>(MT_TILE, m - base) : 0;
+  for (uint32_t q = threadIdx.x; q < MT_TILE; q += 256) s_ss[q] = q < n_here ? ss[base + q] : 0u;
+  uint8_t f[MT_ITEMS];
+  uint32_t tx[MT_ITEMS];
+  mt_load_tile(sfl, stx, m, base, L, f, tx);  // (its barriers also cover s_ss)
   uint32_t keep = 0, c = 0;
 #pragma unroll
-  for (uint32_t i = 0; i < MT_ITEMS; i++) {
-    const uint64_t p = p0 + i;
-    if (p < m) {
-      const uint8_t f = sfl[p];
-      if ((f & F_LAST) && mt_keep(f, state[stx[p]])) {
-        keep |= 1u << i;
-        c++;
-      }
+  for (uint32_t i = 0; i < MT_ITEMS; i++)
+    if ((f[i] & F_LAST) && mt_keep(f[i], state[tx[i]])) {
+      keep |= 1u << i;
+      c++;
     }
-  }
   // exclusive scan of c over the workgroup (thread order = position order)
   const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   uint32_t x = c;
@@ -559,16 +662,33 @@ __global__ __launch_bounds__(256) void k_mt_keep_scatter(uint64_t m, const uint8
   }
   if (lane == 63) s_w[w] = x;
   __syncthreads();
-  uint32_t q = tpre[blockIdx.x] + x - c;
-  for (uint32_t v = 0; v < w; v++) q += s_w[v];
+  uint32_t q = x - c, tot = 0;
+  for (uint32_t v = 0; v < 4; v++) {
+    if (v < w) q += s_w[v];
+    tot += s_w[v];
+  }
+  // stage the kept positions at their tile offsets (flags in L.f, txns in
+  // L.x, slots back in s_ss once every thread holds its own)
+  uint32_t sv[MT_ITEMS];
+#pragma unroll
+  for (uint32_t i = 0; i < MT_ITEMS; i++) sv[i] = s_ss[threadIdx.x * MT_ITEMS + i];
+  __syncthreads();
+  uint8_t* of = (uint8_t*)L.f;
+  uint32_t* ox = (uint32_t*)L.x;
 #pragma unroll
   for (uint32_t i = 0; i < MT_ITEMS; i++) {
     if (!((keep >> i) & 1u)) continue;
-    const uint64_t p = p0 + i;
-    sfl2[q] = sfl[p] & (F_R | F_W | F_LAST);
-    stx2[q] = stx[p];
-    ss2[q] = ss[p];
+    of[q] = f[i] & (F_R | F_W | F_LAST);
+    ox[q] = tx[i];
+    s_ss[q] = sv[i];
     q++;
+  }
+  __syncthreads();
+  const uint32_t ob = tpre[blockIdx.x];
+  for (uint32_t j = threadIdx.x; j < tot; j += 256) {
+    sfl2[ob + j] = of[j];
+    stx2[ob + j] = ox[j];
+    ss2[ob + j] = s_ss[j];
   }
 }
 __global__ __launch_bounds__(256) void k_mt_starts(uint64_t m, const uint32_t* ss, uint8_t* sfl) {
@@ -772,6 +892,16 @@ int dcc_ctx::maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, 
   // the scan input is compacted to the groups that can still matter
   uint32_t rounds = 0;
   bool done = false;
+  const bool mt_debug = getenv("DCC_MT_DEBUG") != nullptr;
+  // the undecided txns: all of them at first (identity), then a compacted
+  // list whenever the undecided count falls well below it
+  CR(mt_ul.ensure(this, 2 * n * 4 + 64, "maat undecided lists"));
+  uint32_t* ul_buf[2] = {(uint32_t*)mt_ul.p, (uint32_t*)mt_ul.p + n};
+  uint32_t* ulen_w = cnt + 5;  // two count words: cnt[5], cnt[6]
+  const uint32_t* ul_cur = nullptr;
+  const uint32_t* ulen_cur = nullptr;
+  uint64_t ulen_host = n;
+  int ub = 0;
   uint64_t mc = m;  // current scan length
   int cb = 0;       // current buffer set
   uint32_t* tcnt = (uint32_t*)mt_tcnt.p;
@@ -779,14 +909,17 @@ int dcc_ctx::maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, 
     const uint32_t k0 = rounds;
     const uint64_t tiles_c = (mc + MT_TILE - 1) / MT_TILE;
     MtRoundArgs ra{mc, n, sflb[cb], stxb[cb], state, cts, lacc, uacc, pend, (Ms*)mt_agg.p};
-    const uint32_t nb = rounds == 0 ? 1u : MT_BATCH;
+    // one round per host check while the scan is long (each check may
+    // compact it), MT_BATCH once it is short
+    const uint32_t nb = (rounds == 0 || mc > MT_LONG) ? 1u : MT_BATCH;
     for (uint32_t q = 0; q < nb; q++, rounds++) {
       if (mc) {
         k_mt_up<<<(unsigned)tiles_c, 256, 0, stream>>>(ra);
         k_mt_top<<<1, 256, 0, stream>>>((Ms*)mt_agg.p, (uint32_t)tiles_c);
         k_mt_down<<<(unsigned)tiles_c, 256, 0, stream>>>(ra);
       }
-      k_mt_decide<<<g1(n, 2048), 256, 0, stream>>>(n, base, state, cts, lacc, uacc, pend,
+      k_mt_decide<<<g1(ulen_host, 2048), 256, 0, stream>>>(n, ul_cur, ulen_cur, base, state, cts,
+                                                            lacc, uacc, pend,
                                                    &ring[rounds % MT_RING],
                                                    &ring[(rounds + 1) % MT_RING]);
     }
@@ -799,6 +932,10 @@ int dcc_ctx::maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, 
     if (mc) CK(hipMemcpyAsync((char*)hmisc + MT_RING * 4, tcnt + tiles_c, 4, hipMemcpyDeviceToHost, stream));
     CK(hipStreamSynchronize(stream));
     const uint32_t* hr = (const uint32_t*)hmisc;
+    if (mt_debug)  // DCC_MT_DEBUG: undecided txns after each round, scan length
+      for (uint32_t q = k0; q < rounds; q++)
+        fprintf(stderr, "maat round %u: undecided %u, scan positions %llu\n", q + 1, hr[q % MT_RING],
+                (unsigned long long)mc);
     for (uint32_t q = k0; q < rounds; q++)
       if (hr[q % MT_RING] == 0) {
         rounds = q + 1;
@@ -806,7 +943,19 @@ int dcc_ctx::maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, 
         break;
       }
     if (!done && rounds > n + 8) return fail(DCC_EIO, "maat: rounds did not converge");
-    if (!done && mc) {
+    if (!done) {
+      const uint32_t und = hr[(rounds - 1) % MT_RING];
+      if ((uint64_t)und * 10 < ulen_host * 3) {  // shrinks to < 30 %: worth a pass
+        CK(hipMemsetAsync(ulen_w + ub, 0, 4, stream));
+        k_mt_ucompact<<<g1(ulen_host, 2048), 256, 0, stream>>>(ul_cur, ulen_cur, n, state, ul_buf[ub],
+                                                              ulen_w + ub);
+        ul_cur = ul_buf[ub];
+        ulen_cur = ulen_w + ub;
+        ulen_host = und;
+        ub ^= 1;
+      }
+    }
+    if (!done && mc && (uint64_t)hr[MT_RING] * 10 <= mc * 9) {  // compact when it drops >= 10 %
       const uint64_t m2 = hr[MT_RING];
       k_mt_keep_scatter<<<(unsigned)tiles_c, 256, 0, stream>>>(mc, sflb[cb], stxb[cb], ssb[cb], state,
                                                              tcnt, sflb[cb ^ 1], stxb[cb ^ 1],
