@@ -147,7 +147,7 @@ struct dcc_ctx {
   DevBuf cv_scratch, cv_agg, cv_group, cv_wave, cv_pgx, cv_gsx, cv_gsize, cv_done, cv_maxl;
   DevBuf cv_seq_b, cv_ok, cv_len, cv_off2, cv_tsum, cv_hkeys, cv_hat;
   DevBuf snap_top, snap_aoff, snap_aidx, snap_cnt;  // captured-snapshot validation
-  DevBuf mt_rk, mt_rlr, mt_rlw;                  // MaaT row table: key, last read / write ts
+  DevBuf mt_rk;                                  // MaaT row table: 32-B {key, last read, last write} slots
   uint32_t mt_bits = 0;                          // log2 row-table slots (0: none yet)
   uint64_t mt_rows = 0;                          // rows in the table
   uint32_t mt_rows32 = 0;                        // upload source of the row counter

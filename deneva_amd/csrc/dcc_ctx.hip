@@ -242,7 +242,7 @@ std::vector<DevBuf*> dcc_ctx::all_bufs() {
                             &sw_ckeys, &sw_gtab, &sw_rec, &sw_rk, &sw_fw, &sw_aent, &sw_mg, &sw_xcnt, &sw_xsend,
                             &sw_xrec, &sw_mcnt, &sw_moff, &sw_mkeys, &sw_mat, &sw_kill,
                             &sw_rflag, &sw_ro, &sw_wtab, &sw_cw, &sw_wtab_big,
-                            &snap_top, &snap_aoff, &snap_aidx, &snap_cnt, &mt_rk, &mt_rlr, &mt_rlw,
+                            &snap_top, &snap_aoff, &snap_aidx, &snap_cnt, &mt_rk,
                             &mt_misc, &mt_slot, &mt_sval, &mt_slot2, &mt_sval2, &mt_sfl,
                             &mt_stx, &mt_txn, &mt_agg, &mt_sflB, &mt_stxB, &mt_k1, &mt_tcnt, &mt_ul, &ix_keys, &ix_ord, &ix_rows, &ix_cnt, &wv_buf, &ix_scr, &wv_hbuf, &wv_obuf,
                             &h_K[0], &h_K[1], &h_V[0], &h_V[1], &h_scr, &h_bsum,

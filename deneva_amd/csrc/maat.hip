@@ -71,18 +71,25 @@ __device__ inline uint64_t mt_hash(uint64_t key, uint32_t bits) {
 }
 
 // ---------------------------------------------------------------- row table
+// One 32-B slot per row: the key and its two timestamps side by side, so the
+// access that finds a row has its timestamps in the same 64-B line (three
+// separate arrays cost three random HBM lines per access).
+struct __attribute__((aligned(32))) MtSlot {
+  uint64_t key, lr, lw, pad;
+};
+static_assert(sizeof(MtSlot) == 32, "row slot");
 // insert-or-find the row of `key` (ins: this call created it); its lr / lw
 // stay 0 until an epoch commits
-__device__ inline uint32_t mt_row(uint64_t* rk, uint32_t bits, uint64_t key, bool& ins,
+__device__ inline uint32_t mt_row(MtSlot* rt, uint32_t bits, uint64_t key, bool& ins,
                                   uint32_t* err) {
   const uint64_t mask = (1ull << bits) - 1;
   uint64_t s = mt_hash(key, bits);
   ins = false;
   for (uint64_t q = 0; q <= mask; q++) {
-    const uint64_t v = rk[s];
+    const uint64_t v = rt[s].key;
     if (v == key) return (uint32_t)s;
     if (v == DCC_KEY_RESERVED) {
-      const unsigned long long prev = atomicCAS((unsigned long long*)&rk[s],
+      const unsigned long long prev = atomicCAS((unsigned long long*)&rt[s].key,
                                                 (unsigned long long)DCC_KEY_RESERVED,
                                                 (unsigned long long)key);
       if (prev == DCC_KEY_RESERVED) {
@@ -110,28 +117,30 @@ __device__ inline void block_add(uint32_t c, uint32_t* ctr) {
 }
 
 // rehash: every row of the old table into the new one (values carried)
-__global__ __launch_bounds__(256) void k_mt_rehash(const uint64_t* ok, const uint64_t* olr,
-                                                   const uint64_t* olw, uint64_t ocap, uint64_t* nk,
-                                                   uint64_t* nlr, uint64_t* nlw, uint32_t nbits,
-                                                   uint32_t* nrows, uint32_t* err) {
+__global__ __launch_bounds__(256) void k_mt_rehash(const MtSlot* ot, uint64_t ocap, MtSlot* nt,
+                                                   uint32_t nbits, uint32_t* nrows, uint32_t* err) {
   uint32_t c = 0;
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < ocap; i += (uint64_t)gridDim.x * 256) {
-    const uint64_t k = ok[i];
-    if (k == DCC_KEY_RESERVED) continue;
+    const MtSlot o = ot[i];
+    if (o.key == DCC_KEY_RESERVED) continue;
     bool ins;
-    const uint32_t s = mt_row(nk, nbits, k, ins, err);
+    const uint32_t s = mt_row(nt, nbits, o.key, ins, err);
     c += ins;
-    nlr[s] = olr[i];
-    nlw[s] = olw[i];
+    nt[s].lr = o.lr;
+    nt[s].lw = o.lw;
   }
   block_add(c, nrows);
+}
+// an empty table: every key KEY_RESERVED, timestamps 0
+__global__ __launch_bounds__(256) void k_mt_clear(MtSlot* rt, uint64_t cap) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < cap; i += (uint64_t)gridDim.x * 256)
+    rt[i] = MtSlot{DCC_KEY_RESERVED, 0, 0, 0};
 }
 
 // host-seeded rows (dcc_maat_rows_set): insert and overwrite the timestamps
 __global__ __launch_bounds__(256) void k_mt_seed(const uint64_t* keys, const uint64_t* lr,
-                                                 const uint64_t* lw, uint64_t n, uint64_t* rk,
-                                                 uint64_t* rlr, uint64_t* rlw, uint32_t bits,
-                                                 uint32_t* nrows, uint32_t* err) {
+                                                 const uint64_t* lw, uint64_t n, MtSlot* rt,
+                                                 uint32_t bits, uint32_t* nrows, uint32_t* err) {
   uint32_t c = 0;
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
     if (keys[i] == DCC_KEY_RESERVED) {
@@ -139,25 +148,24 @@ __global__ __launch_bounds__(256) void k_mt_seed(const uint64_t* keys, const uin
       continue;
     }
     bool ins;
-    const uint32_t s = mt_row(rk, bits, keys[i], ins, err);
+    const uint32_t s = mt_row(rt, bits, keys[i], ins, err);
     c += ins;
-    rlr[s] = lr[i];
-    rlw[s] = lw[i];
+    rt[s].lr = lr[i];
+    rt[s].lw = lw[i];
   }
   block_add(c, nrows);
 }
-__global__ __launch_bounds__(256) void k_mt_get(const uint64_t* keys, uint64_t n, const uint64_t* rk,
-                                                const uint64_t* rlr, const uint64_t* rlw,
+__global__ __launch_bounds__(256) void k_mt_get(const uint64_t* keys, uint64_t n, const MtSlot* rt,
                                                 uint32_t bits, uint64_t* lr, uint64_t* lw) {
   const uint64_t mask = (1ull << bits) - 1;
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
     const uint64_t key = keys[i];
     uint64_t s = mt_hash(key, bits), a = 0, b = 0;
     for (uint64_t q = 0; q <= mask; q++) {
-      const uint64_t v = rk[s];
+      const uint64_t v = rt[s].key;
       if (v == key) {
-        a = rlr[s];
-        b = rlw[s];
+        a = rt[s].lr;
+        b = rt[s].lw;
         break;
       }
       if (v == DCC_KEY_RESERVED) break;
@@ -188,31 +196,14 @@ __global__ __launch_bounds__(256) void k_mt_check(const uint32_t* off, uint64_t 
 }
 
 // ---------------------------------------------------------------- base
-// Access-parallel: every access enters its row (slot id) in the table.
-__global__ __launch_bounds__(256) void k_mt_slots(const uint64_t* keys, uint64_t nnz, uint64_t* rk,
-                                                  uint32_t bits, uint32_t* slot, uint32_t* nrows,
-                                                  uint32_t* err) {
-  uint32_t c = 0;
-  for (uint64_t x = (uint64_t)blockIdx.x * 256 + threadIdx.x; x < nnz; x += (uint64_t)gridDim.x * 256) {
-    const uint64_t key = keys[x];
-    uint32_t sl = 0;
-    if (key == DCC_KEY_RESERVED) {
-      atomicOr(err, MT_ERR_KEY);
-    } else {
-      bool ins;
-      sl = mt_row(rk, bits, key, ins, err);
-      c += ins;
-    }
-    slot[x] = sl;
-  }
-  block_add(c, nrows);
-}
-
 // The txn's lower bound from the row timestamps copied at access time: gwts
 // over rows read or written, grts over rows written (Row_maat::read /
 // prewrite, row_maat.cpp:115-117, 150-156; Maat::validate raises lower past
-// them, maat.cpp:46-49, 69-72).  A wave per 64 txns walks their contiguous
-// accesses 64 at a time (coalesced slot / type loads, four rounds in flight),
+// them, maat.cpp:46-49, 69-72).  Every access first finds or enters its row
+// in the table (its slot id, written twice: the sort's key buffer and the
+// finish's copy) and reads the row's timestamps from the same slot.  A wave
+// per 64 txns walks their contiguous accesses 64 at a time (coalesced key /
+// type loads, four rounds in flight),
 // finds each access's txn in the wave's LDS offset prefix and folds the row
 // timestamps per txn with LDS atomicMax.  Each access's sort value packs its
 // txn and R / W bits, so the sorted groups need no gathers.
@@ -221,10 +212,13 @@ struct BaseArgs {
   const uint32_t* off;
   const uint8_t* at;
   uint32_t rw_all;
-  const uint64_t* rlr;
-  const uint64_t* rlw;
-  const uint32_t* slot;
-  uint32_t* sval;   // [nnz] txn << 2 | R << 1 | W (pre-zeroed)
+  const uint64_t* keys;
+  MtSlot* rt;
+  uint32_t bits;
+  uint32_t* slot;   // [nnz] row slot per access
+  uint32_t* slot2;  // [nnz] the same (the sort's first key buffer)
+  uint32_t* nrows;
+  uint32_t* sval;   // [nnz] txn << 2 | R << 1 | W
   uint64_t* base;   // [n]
   uint8_t* state;   // [n] zeroed here
   uint64_t* lacc;   // [n] 0
@@ -261,25 +255,38 @@ __global__ __launch_bounds__(256) void k_mt_base(BaseArgs a) {
     s_o[w][64] = max(s_o[w][63], (uint32_t)min<uint64_t>(a.off[t0 + 64], a.nnz));
   __builtin_amdgcn_wave_barrier();
   const uint32_t a0 = s_o[w][0], a1 = s_o[w][nt];
+  uint32_t nins = 0;
   for (uint32_t x0 = a0; x0 < a1; x0 += 4 * 64) {
-    uint32_t sl[4];
+    uint64_t key[4];
     uint8_t ty[4];
 #pragma unroll
     for (uint32_t u = 0; u < 4; u++) {
       const uint32_t x = min(x0 + 64 * u + lane, a1 - 1);
-      sl[u] = a.slot[x];
+      key[u] = a.keys[x];
       ty[u] = a.at[x];
+    }
+    uint32_t sl[4];
+#pragma unroll
+    for (uint32_t u = 0; u < 4; u++) {
+      sl[u] = 0;
+      if (x0 + 64 * u + lane < a1 && key[u] != DCC_KEY_RESERVED) {  // the check rejected reserved keys
+        bool ins;
+        sl[u] = mt_row(a.rt, a.bits, key[u], ins, a.err);
+        nins += ins;
+      }
     }
     uint64_t lw[4], lr[4];
 #pragma unroll
     for (uint32_t u = 0; u < 4; u++) {
-      lw[u] = a.rlw[sl[u]];
-      lr[u] = a.rlr[sl[u]];
+      lw[u] = a.rt[sl[u]].lw;
+      lr[u] = a.rt[sl[u]].lr;
     }
 #pragma unroll
     for (uint32_t u = 0; u < 4; u++) {
       const uint32_t x = x0 + 64 * u + lane;
       if (x >= a1) continue;
+      a.slot[x] = sl[u];
+      a.slot2[x] = sl[u];
       uint32_t lo = 0, hi = nt;  // largest k < nt with s_o[k] <= x
       while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
@@ -292,6 +299,8 @@ __global__ __launch_bounds__(256) void k_mt_base(BaseArgs a) {
       a.sval[x] = ((uint32_t)(t0 + lo) << 2) | (rd ? SV_R : 0u) | (wr ? SV_W : 0u);
     }
   }
+  for (int d = 32; d > 0; d >>= 1) nins += __shfl_xor(nins, d);
+  if (lane == 0 && nins) atomicAdd(a.nrows, nins);
   __builtin_amdgcn_wave_barrier();
   if (lane < nt) {
     a.base[t] = max(s_gw[w][lane], s_gr[w][lane]) + 1;
@@ -707,8 +716,7 @@ struct FinArgs {
   const uint8_t* state;
   const uint64_t* cts;
   const uint32_t* slot;
-  uint64_t* rlr;
-  uint64_t* rlw;
+  MtSlot* rt;
   uint8_t* rc;
   uint64_t* cts_out;
   uint32_t* cnt;  // [0] commits, [1] undecided, [2] write accesses
@@ -730,8 +738,8 @@ __global__ __launch_bounds__(256) void k_mt_finish(FinArgs a) {
       nw += ty == DCC_WR;
       if (!ok) continue;
       const uint32_t sl = a.slot[x];
-      if (a.rw_all || ty == DCC_RD) atomicMax((unsigned long long*)&a.rlr[sl], c);
-      if (a.rw_all || ty == DCC_WR) atomicMax((unsigned long long*)&a.rlw[sl], c);
+      if (a.rw_all || ty == DCC_RD) atomicMax((unsigned long long*)&a.rt[sl].lr, c);
+      if (a.rw_all || ty == DCC_WR) atomicMax((unsigned long long*)&a.rt[sl].lw, c);
     }
   }
   for (int d = 32; d > 0; d >>= 1) {
@@ -768,28 +776,19 @@ int dcc_ctx::maat_rows_reserve(uint64_t want) {
   while ((1ull << bits) < 2 * want) bits++;
   if (bits > 31) return fail(DCC_ERANGE, "maat: row table exceeds 2^31 slots");
   const uint64_t cap = 1ull << bits;
-  DevBuf nk, nlr, nlw;
-  CR(nk.ensure(this, cap * 8, "maat row keys"));
-  CR(nlr.ensure(this, cap * 8, "maat row lr"));
-  CR(nlw.ensure(this, cap * 8, "maat row lw"));
-  CK(hipMemsetAsync(nk.p, 0xFF, cap * 8, stream));
-  CK(hipMemsetAsync(nlr.p, 0, cap * 8, stream));
-  CK(hipMemsetAsync(nlw.p, 0, cap * 8, stream));
+  DevBuf nt;
+  CR(nt.ensure(this, cap * sizeof(MtSlot), "maat row table"));
+  k_mt_clear<<<g1(cap, 16384), 256, 0, stream>>>((MtSlot*)nt.p, cap);
   CK(hipMemsetAsync(cnt, 0, 4, stream));
   if (mt_bits) {
     const uint64_t ocap = 1ull << mt_bits;
-    k_mt_rehash<<<g1(ocap), 256, 0, stream>>>((const uint64_t*)mt_rk.p, (const uint64_t*)mt_rlr.p,
-                                              (const uint64_t*)mt_rlw.p, ocap, (uint64_t*)nk.p,
-                                              (uint64_t*)nlr.p, (uint64_t*)nlw.p, bits, cnt, cnt + 1);
-    CK(hipGetLastError());
+    k_mt_rehash<<<g1(ocap), 256, 0, stream>>>((const MtSlot*)mt_rk.p, ocap, (MtSlot*)nt.p, bits, cnt,
+                                              cnt + 1);
   }
+  CK(hipGetLastError());
   CK(hipStreamSynchronize(stream));
   mt_rk.release();
-  mt_rlr.release();
-  mt_rlw.release();
-  mt_rk = nk;
-  mt_rlr = nlr;
-  mt_rlw = nlw;
+  mt_rk = nt;
   mt_bits = bits;
   return DCC_OK;
 }
@@ -863,13 +862,10 @@ int dcc_ctx::maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, 
     if (e & MT_ERR_KEY) return fail(DCC_EINVAL, "batch: key equal to DCC_KEY_RESERVED");
   }
   CK(hipEventRecord(ev0, stream));
-  // every access gets a slot / owner / sort value even in a malformed batch
-  CK(hipMemsetAsync(mt_slot.p, 0, mm * 4, stream));
-  CK(hipMemsetAsync(mt_sval.p, 0, mm * 4, stream));
-  k_mt_slots<<<g1(mm, 16384), 256, 0, stream>>>(d.keys, m, (uint64_t*)mt_rk.p, mt_bits,
-                                                 (uint32_t*)mt_slot.p, cnt, cnt + 1);
-  BaseArgs ba{n,     m,     d.off, d.acctype, rw_all, (const uint64_t*)mt_rlr.p,
-              (const uint64_t*)mt_rlw.p, (const uint32_t*)mt_slot.p, (uint32_t*)mt_sval.p,
+  // the check passed: the offsets cover every access once, so the base pass
+  // writes every slot and sort value (no clears)
+  BaseArgs ba{n,     m,     d.off, d.acctype, rw_all, d.keys, (MtSlot*)mt_rk.p, mt_bits,
+              (uint32_t*)mt_slot.p, (uint32_t*)mt_slot2.p, cnt, (uint32_t*)mt_sval.p,
               base,  state, lacc,  uacc,      pend,   cnt + 1};
   k_mt_base<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(ba);  // a wave per 64 txns
   // rows sorted by slot (stable: index order within a row); the sorted slots
@@ -878,7 +874,6 @@ int dcc_ctx::maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, 
   uint32_t* stxb[2] = {(uint32_t*)mt_stx.p, (uint32_t*)mt_stxB.p};
   uint32_t* ssb[2] = {(uint32_t*)mt_slot2.p, (uint32_t*)mt_k1.p};
   if (m) {
-    CK(hipMemcpyAsync(mt_slot2.p, mt_slot.p, m * 4, hipMemcpyDeviceToDevice, stream));
     uint32_t* kk[2] = {(uint32_t*)mt_slot2.p, (uint32_t*)mt_k1.p};
     uint32_t* vb[2] = {(uint32_t*)mt_sval.p, (uint32_t*)mt_sval2.p};
     const int cur = radix_sort_u32(kk, vb, m, mt_bits, (uint32_t*)cv_scratch.p, stream);
@@ -967,7 +962,7 @@ int dcc_ctx::maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, 
     }
   }
   FinArgs fa{n, m, d.off, d.acctype, rw_all, state, cts, (const uint32_t*)mt_slot.p,
-             (uint64_t*)mt_rlr.p, (uint64_t*)mt_rlw.p, rc_dev, cts_dev, cnt + 2};
+             (MtSlot*)mt_rk.p, rc_dev, cts_dev, cnt + 2};
   k_mt_finish<<<g1(n, 2048), 256, 0, stream>>>(fa);
   CK(hipGetLastError());
   CK(hipEventRecord(ev1, stream));
@@ -1017,10 +1012,8 @@ extern "C" int dcc_maat_rows_clear(dcc_ctx* ctx) {
   if (hipSetDevice(ctx->device) != hipSuccess) return DCC_ENODEV;
   if (ctx->mt_bits) {
     const uint64_t cap = 1ull << ctx->mt_bits;
-    if (hipMemsetAsync(ctx->mt_rk.p, 0xFF, cap * 8, ctx->stream) != hipSuccess ||
-        hipMemsetAsync(ctx->mt_rlr.p, 0, cap * 8, ctx->stream) != hipSuccess ||
-        hipMemsetAsync(ctx->mt_rlw.p, 0, cap * 8, ctx->stream) != hipSuccess ||
-        hipStreamSynchronize(ctx->stream) != hipSuccess)
+    k_mt_clear<<<g1(cap, 16384), 256, 0, ctx->stream>>>((MtSlot*)ctx->mt_rk.p, cap);
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(ctx->stream) != hipSuccess)
       return ctx->hip_fail(hipGetLastError(), "maat rows clear");
   }
   ctx->mt_rows = 0;
@@ -1045,8 +1038,7 @@ extern "C" int dcc_maat_rows_set(dcc_ctx* ctx, const uint64_t* keys, const uint6
   CK(hipMemcpyAsync(t, keys, n * 8, hipMemcpyHostToDevice, ctx->stream));
   CK(hipMemcpyAsync(t + n, last_read, n * 8, hipMemcpyHostToDevice, ctx->stream));
   CK(hipMemcpyAsync(t + 2 * n, last_write, n * 8, hipMemcpyHostToDevice, ctx->stream));
-  k_mt_seed<<<g1(n), 256, 0, ctx->stream>>>(t, t + n, t + 2 * n, n, (uint64_t*)ctx->mt_rk.p,
-                                            (uint64_t*)ctx->mt_rlr.p, (uint64_t*)ctx->mt_rlw.p,
+  k_mt_seed<<<g1(n), 256, 0, ctx->stream>>>(t, t + n, t + 2 * n, n, (MtSlot*)ctx->mt_rk.p,
                                             ctx->mt_bits, cnt, cnt + 1);
   CK(hipGetLastError());
   uint32_t hc[2];
@@ -1074,10 +1066,8 @@ extern "C" int dcc_maat_rows_get(dcc_ctx* ctx, const uint64_t* keys, uint64_t* l
   CR(tmp.ensure(ctx, n * 24, "maat get"));
   uint64_t* t = (uint64_t*)tmp.p;
   CK(hipMemcpyAsync(t, keys, n * 8, hipMemcpyHostToDevice, ctx->stream));
-  k_mt_get<<<g1(n), 256, 0, ctx->stream>>>(t, n, (const uint64_t*)ctx->mt_rk.p,
-                                           (const uint64_t*)ctx->mt_rlr.p,
-                                           (const uint64_t*)ctx->mt_rlw.p, ctx->mt_bits, t + n,
-                                           t + 2 * n);
+  k_mt_get<<<g1(n), 256, 0, ctx->stream>>>(t, n, (const MtSlot*)ctx->mt_rk.p, ctx->mt_bits,
+                                           t + n, t + 2 * n);
   CK(hipGetLastError());
   CK(hipMemcpyAsync(last_read, t + n, n * 8, hipMemcpyDeviceToHost, ctx->stream));
   CK(hipMemcpyAsync(last_write, t + 2 * n, n * 8, hipMemcpyDeviceToHost, ctx->stream));
