@@ -17,9 +17,9 @@
 
 namespace dcc {
 
-constexpr uint32_t RS_THREADS = 256;
+constexpr uint32_t RS_THREADS = 512;
 constexpr uint32_t RS_ITEMS = 16;
-constexpr uint32_t RS_TILE = RS_THREADS * RS_ITEMS;  // 4096 pairs per workgroup
+constexpr uint32_t RS_TILE = RS_THREADS * RS_ITEMS;  // 8192 pairs per workgroup
 
 inline uint64_t rs_tiles(uint64_t m) { return (m + RS_TILE - 1) / RS_TILE; }
 // u32 words of scratch a sort of m pairs needs: counts [256][tiles] + totals [256]

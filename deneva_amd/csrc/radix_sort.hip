@@ -22,8 +22,11 @@ __device__ inline uint64_t lanemask_lt() {
   return l == 0 ? 0ull : (~0ull >> (64 - l));
 }
 
-// Exclusive scan of one u32 per thread over a 256-thread workgroup.
-__device__ inline uint32_t block_excl_scan256(uint32_t v, uint32_t* sh /*[4]*/, uint32_t& total) {
+constexpr uint32_t RS_W = RS_THREADS / 64;  // waves per workgroup
+static_assert(RS_THREADS >= 256, "one thread per digit");
+
+// Exclusive scan of one u32 per thread over the workgroup.
+__device__ inline uint32_t block_excl_scan(uint32_t v, uint32_t* sh /*[RS_W]*/, uint32_t& total) {
   const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
   uint32_t x = v;
 #pragma unroll
@@ -36,49 +39,73 @@ __device__ inline uint32_t block_excl_scan256(uint32_t v, uint32_t* sh /*[4]*/, 
   __syncthreads();
   uint32_t off = 0;
   total = 0;
-  for (uint32_t w = 0; w < 4; w++) {
+#pragma unroll
+  for (uint32_t w = 0; w < RS_W; w++) {
     if (w < wv) off += sh[w];
     total += sh[w];
   }
   return off + x - v;
 }
 
-// Per-tile digit counts: one LDS histogram per wave (an atomic add per item,
-// spread over 256 bins), summed at the end.
+// Per-tile digit counts: one LDS histogram per wave, summed at the end.
+// Thread t counts the tile's items [16t, 16t + 16) (16-B loads): a run of
+// equal digits -- a hot row's requests are adjacent once the lower digits
+// are sorted -- costs one LDS atomic, not one per item (the skewed top-digit
+// pass of a YCSB key sort took 34 us with an atomic per item, the others
+// ~16-19; adding once per digit per wave instruction, via digit_peers, 41).
 template <typename K>
 __global__ __launch_bounds__(RS_THREADS) void k_rs_hist(const K* __restrict__ keys, uint64_t m,
                                                         uint32_t shift, uint32_t* __restrict__ cnt,
                                                         uint32_t tiles) {
-  constexpr uint32_t W = RS_THREADS / 64;
+  constexpr uint32_t W = RS_W;
+  constexpr uint32_t V = 16 / sizeof(K);  // keys per 16-B load
   __shared__ uint32_t s_h[W][256];
   const uint32_t wv = threadIdx.x >> 6;
-#pragma unroll
-  for (uint32_t w = 0; w < W; w++) s_h[w][threadIdx.x] = 0;
+  for (uint32_t q = threadIdx.x; q < W * 256; q += RS_THREADS) (&s_h[0][0])[q] = 0;
   __syncthreads();
-  const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
+  const uint64_t p0 = (uint64_t)blockIdx.x * RS_TILE + (uint64_t)threadIdx.x * RS_ITEMS;
   K k[RS_ITEMS];
+  if (p0 + RS_ITEMS <= m && ((uintptr_t)(keys + p0) & 15) == 0) {
 #pragma unroll
-  for (uint32_t it = 0; it < RS_ITEMS; it++) {
-    const uint64_t p = base + it * RS_THREADS + threadIdx.x;
-    k[it] = p < m ? keys[p] : (K)0;
-  }
+    for (uint32_t q = 0; q < RS_ITEMS / V; q++) {
+      const uint4 x = ((const uint4*)(keys + p0))[q];
+      const K* xk = (const K*)&x;
 #pragma unroll
-  for (uint32_t it = 0; it < RS_ITEMS; it++) {
-    const uint64_t p = base + it * RS_THREADS + threadIdx.x;
-    if (p < m) atomicAdd(&s_h[wv][(uint32_t)(k[it] >> shift) & 255u], 1u);
+      for (uint32_t i = 0; i < V; i++) k[q * V + i] = xk[i];
+    }
+  } else {
+#pragma unroll
+    for (uint32_t i = 0; i < RS_ITEMS; i++) k[i] = p0 + i < m ? keys[p0 + i] : (K)0;
   }
+  const uint32_t n = p0 >= m ? 0u : (uint32_t)min<uint64_t>(RS_ITEMS, m - p0);
+  uint32_t run_d = (uint32_t)(k[0] >> shift) & 255u, run_n = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < RS_ITEMS; i++) {
+    const uint32_t d = (uint32_t)(k[i] >> shift) & 255u;
+    if (i < n) {
+      if (d != run_d) {
+        if (run_n) atomicAdd(&s_h[wv][run_d], run_n);
+        run_d = d;
+        run_n = 0;
+      }
+      run_n++;
+    }
+  }
+  if (run_n) atomicAdd(&s_h[wv][run_d], run_n);
   __syncthreads();
-  uint32_t c = 0;
+  if (threadIdx.x < 256) {
+    uint32_t c = 0;
 #pragma unroll
-  for (uint32_t w = 0; w < W; w++) c += s_h[w][threadIdx.x];
-  cnt[(uint64_t)threadIdx.x * tiles + blockIdx.x] = c;
+    for (uint32_t w = 0; w < W; w++) c += s_h[w][threadIdx.x];
+    cnt[(uint64_t)threadIdx.x * tiles + blockIdx.x] = c;
+  }
 }
 
 // One workgroup per digit: exclusive scan of cnt[d][0..tiles) in place,
 // digit total to tot[d].
 __global__ __launch_bounds__(RS_THREADS) void k_rs_scan(uint32_t* __restrict__ cnt, uint32_t tiles,
                                                         uint32_t* __restrict__ tot) {
-  __shared__ uint32_t sh[4];
+  __shared__ uint32_t sh[RS_W];
   uint32_t* row = cnt + (uint64_t)blockIdx.x * tiles;
   uint32_t run = 0;
   for (uint32_t c0 = 0; c0 < tiles; c0 += RS_THREADS * 4) {
@@ -90,7 +117,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scan(uint32_t* __restrict__ c
       s += v[q];
     }
     uint32_t total;
-    uint32_t pre = run + block_excl_scan256(s, sh, total);
+    uint32_t pre = run + block_excl_scan(s, sh, total);
 #pragma unroll
     for (int q = 0; q < 4; q++) {
       const uint32_t i = c0 + threadIdx.x * 4 + q;
@@ -118,14 +145,15 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(const K* __restrict__
                                                            const uint32_t* __restrict__ cnt,
                                                            const uint32_t* __restrict__ tot,
                                                            uint32_t tiles) {
-  constexpr uint32_t W = RS_THREADS / 64, WI = RS_TILE / W;  // waves, items per wave
+  constexpr uint32_t W = RS_W, WI = RS_TILE / W;  // waves, items per wave
   __shared__ K s_key[RS_TILE];
   __shared__ uint32_t s_val[RS_TILE];
   __shared__ uint32_t s_wc[W][256];  // per wave: running digit count, then its base in the tile
   __shared__ uint32_t s_gb[256];     // global destination base per digit
   __shared__ uint32_t s_tb[256];     // tile-local base per digit
-  __shared__ uint32_t sh[4];
+  __shared__ uint32_t sh[RS_W];
   const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
+  const bool dig = tid < 256;  // this thread owns digit tid
   const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
   const uint64_t wbase = base + (uint64_t)wv * WI;
 
@@ -139,11 +167,10 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(const K* __restrict__
   }
   {
     uint32_t total;
-    const uint32_t g = block_excl_scan256(tot[tid], sh, total);
-    s_gb[tid] = g + cnt[(uint64_t)tid * tiles + blockIdx.x];
+    const uint32_t g = block_excl_scan(dig ? tot[tid] : 0u, sh, total);
+    if (dig) s_gb[tid] = g + cnt[(uint64_t)tid * tiles + blockIdx.x];
   }
-#pragma unroll
-  for (uint32_t w = 0; w < W; w++) s_wc[w][tid] = 0;
+  for (uint32_t q = tid; q < W * 256; q += RS_THREADS) (&s_wc[0][0])[q] = 0;
   __syncthreads();
 
   const uint64_t lt = lanemask_lt();
@@ -167,16 +194,19 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(const K* __restrict__
     uint32_t c[W], t = 0;
 #pragma unroll
     for (uint32_t w = 0; w < W; w++) {
-      c[w] = s_wc[w][tid];
+      c[w] = dig ? s_wc[w][tid] : 0u;
       t += c[w];
     }
     uint32_t total;
-    uint32_t b = block_excl_scan256(t, sh, total);
-    s_tb[tid] = b;
+    uint32_t b = block_excl_scan(t, sh, total);
+    __syncthreads();  // every wave's counts read before they become bases
+    if (dig) {
+      s_tb[tid] = b;
 #pragma unroll
-    for (uint32_t w = 0; w < W; w++) {
-      s_wc[w][tid] = b;
-      b += c[w];
+      for (uint32_t w = 0; w < W; w++) {
+        s_wc[w][tid] = b;
+        b += c[w];
+      }
     }
   }
   __syncthreads();
