@@ -258,9 +258,12 @@ def calvin_config(eng, dev, timed, orc, tag="C4"):
     b.order = c4_order(b)
     db = b.to_torch(dev)
     res = {}
+    import torch
+    g_out = torch.empty(b.nnz, dtype=torch.int32, device=dev)  # reused across epochs
+    rc_out = torch.empty(b.n_txn, dtype=torch.uint8, device=dev)
 
     def cv():
-        g, rc, _, st = eng.calvin_order_epoch(db, want_group=True)
+        g, rc, _, st = eng.calvin_order_epoch(db, want_group=True, out_group=g_out, out_rc=rc_out)
         res["g"], res["rc"] = g, rc
         return st
     dt, st = timed(cv)

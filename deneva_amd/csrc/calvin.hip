@@ -1048,13 +1048,63 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint3
     so.gsize = (uint32_t*)cv_gsize.p;
   }
   uint32_t* err = (uint32_t*)misc.p;
+
+  // ---- the rest of the epoch as one captured HIP graph: the launches below
+  // depend only on the batch's buffers and shape, the key / order packings
+  // and the outputs, so the second epoch of a shape is captured and later
+  // ones replay it (the host enqueued ~30 launches after the prep read-back,
+  // and the first, short ones left the GPU waiting for the host)
+  const bool have_seq = d.order && (oor ^ oand);
+  const KeyPack op = have_seq ? make_keypack(oor ^ oand) : KeyPack{};
+  static_assert(sizeof(KeyPack) <= sizeof(CvGraphKey::kp), "key image");
+  const bool cv_graph_ok = !profiling && !waves && nh == 0 && comm_ranks() == 1 &&
+                           !getenv("DCC_NO_GRAPH");
+  CvGraphKey gk;
+  memset(&gk, 0, sizeof gk);
+  gk.off = d.off;
+  gk.keys = d.keys;
+  gk.acc = d.acctype;
+  gk.order = d.order;
+  gk.grp = grp_dev;
+  gk.rc = rc_dev;
+  gk.n = d.n;
+  gk.nnz = d.nnz;
+  gk.gen = buf_gen;
+  gk.ulen = ulen;
+  gk.have_seq = have_seq ? 1u : 0u;
+  memcpy(gk.kp, &kp, sizeof kp);
+  memcpy(gk.op, &op, sizeof op);
+  const bool cv_replay = cv_graph_ok && cv_graph_exec && !memcmp(&gk, &cv_graph_key, sizeof gk);
+  const bool cv_cap = cv_graph_ok && !cv_replay && cv_seen && !memcmp(&gk, &cv_seen_key, sizeof gk);
+  struct CvCapture {  // a failure while capturing still ends the capture
+    hipStream_t s;
+    bool on;
+    ~CvCapture() {
+      if (on) {
+        hipGraph_t g = nullptr;
+        (void)hipStreamEndCapture(s, &g);
+        if (g) (void)hipGraphDestroy(g);
+        (void)hipGetLastError();
+      }
+    }
+  } cap{stream, false};
+  if (cv_replay) {
+    CK(hipGraphLaunch(cv_graph_exec, stream));
+  } else {
+  if (cv_cap) {
+    if (cv_graph_exec) {
+      (void)hipGraphExecDestroy(cv_graph_exec);
+      cv_graph_exec = nullptr;
+    }
+    CK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+    cap.on = true;
+  }
   CK(hipMemsetAsync(err, 0, 4, stream));
 
   // ---- rank: seq[q] = txn at sequence position q (stable in index order)
   const uint32_t* seq = nullptr;
   const uint32_t* off2 = nullptr;
-  if (d.order && (oor ^ oand)) {
-    const KeyPack op = make_keypack(oor ^ oand);
+  if (have_seq) {
     CR(perm.ensure(this, d.n * 4 + 16, "calvin seq a"));
     CR(cv_seq_b.ensure(this, d.n * 4 + 16, "calvin seq b"));
     CR(cv_ok.ensure(this, d.n * 8 * 2 + 32, "calvin order keys"));
@@ -1118,6 +1168,25 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint3
   CvCount* cc = (CvCount*)part.p;
   k_cv_count<<<CV_PREP_BLOCKS, 256, 0, stream>>>(rc_dev, wave_dev, d.n, cc);
   CK(hipGetLastError());
+  if (cv_cap) {
+    cap.on = false;
+    hipGraph_t g = nullptr;
+    CK(hipStreamEndCapture(stream, &g));
+    const hipError_t ie = hipGraphInstantiate(&cv_graph_exec, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (ie != hipSuccess) {
+      cv_graph_exec = nullptr;
+      return fail(DCC_EIO, "hipGraphInstantiate: %s", hipGetErrorString(ie));
+    }
+    cv_graph_key = gk;
+    CK(hipGraphLaunch(cv_graph_exec, stream));
+  }
+  if (cv_graph_ok) {  // the shape this call enqueued, with the workspaces it left
+    cv_seen_key = gk;
+    cv_seen_key.gen = buf_gen;
+    cv_seen = true;
+  }
+  }  // not replayed
   CK(hipEventRecord(ev1, stream));
   if (!dev_out) {
     if (out_rc) CK(hipMemcpyAsync(out_rc, rc_dev, d.n, hipMemcpyDeviceToHost, stream));

@@ -117,6 +117,17 @@ struct dcc_ctx {
     }
   };
   hipGraphExec_t graph_exec = nullptr;
+  // the Calvin epoch's launch sequence after its prep read-back (calvin.hip):
+  // captured the second time a shape is seen, replayed while it repeats
+  struct CvGraphKey {
+    const void *off, *keys, *acc, *order, *grp, *rc;
+    uint64_t n, nnz, gen;
+    uint32_t ulen, have_seq;
+    uint8_t kp[112], op[112];  // KeyPack images (memcmp)
+  };
+  hipGraphExec_t cv_graph_exec = nullptr;
+  CvGraphKey cv_graph_key{}, cv_seen_key{};
+  bool cv_seen = false;
   GraphKey graph_key{};
   uint64_t buf_gen = 0;
   void* hmisc_dev = nullptr;  // device-visible addresses of the two (k_gather targets)

@@ -156,6 +156,7 @@ extern "C" void dcc_destroy(dcc_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->graph_exec) (void)hipGraphExecDestroy(ctx->graph_exec);
+  if (ctx->cv_graph_exec) (void)hipGraphExecDestroy(ctx->cv_graph_exec);
   dcc_comm_destroy(ctx);
   for (DevBuf* b : ctx->all_bufs()) b->release();
   if (ctx->hmisc) (void)hipHostFree(ctx->hmisc);

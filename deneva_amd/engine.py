@@ -314,22 +314,31 @@ class Engine:
 
     # ------------------------------------------------------------ Calvin
     def calvin_order_epoch(self, batch: EpochBatch, want_group: bool = True,
-                           want_wave: bool = False, held=None):
+                           want_wave: bool = False, held=None, out_group=None, out_rc=None):
         """Returns (group u32[nnz] | None, rc u8[n], wave u32[n] | None, stats).
         held = (keys u64[h], acctype u8[h]): rows still locked at the epoch's
-        start, per row owners first then waiters (dcc_calvin_order_epoch_held)."""
+        start, per row owners first then waiters (dcc_calvin_order_epoch_held).
+        out_group / out_rc: caller-owned output buffers (reused across epochs,
+        the engine then replays the epoch's captured launches)."""
         n, nnz = batch.n_txn, batch.nnz
         dev = batch.on_device
         if dev:
             import torch
             d = batch.offsets.device
-            rc = torch.empty(max(n, 1), dtype=torch.uint8, device=d)
-            grp = torch.empty(max(nnz, 1), dtype=torch.int32, device=d) if want_group else None
+            rc = out_rc if out_rc is not None else torch.empty(max(n, 1), dtype=torch.uint8, device=d)
+            grp = None
+            if want_group:
+                grp = out_group if out_group is not None else torch.empty(max(nnz, 1), dtype=torch.int32,
+                                                                          device=d)
             wav = torch.empty(max(n, 1), dtype=torch.int32, device=d) if want_wave else None
         else:
-            rc = np.empty(max(n, 1), np.uint8)
-            grp = np.empty(max(nnz, 1), np.uint32) if want_group else None
+            rc = out_rc if out_rc is not None else np.empty(max(n, 1), np.uint8)
+            grp = None
+            if want_group:
+                grp = out_group if out_group is not None else np.empty(max(nnz, 1), np.uint32)
             wav = np.empty(max(n, 1), np.uint32) if want_wave else None
+        if rc.shape[0] < n or (grp is not None and grp.shape[0] < nnz):
+            raise ValueError("calvin_order_epoch: output buffer shorter than the epoch")
         st = _abi.Stats()
         b = batch.to_c()
         if held is None:
