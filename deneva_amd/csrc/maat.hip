@@ -59,8 +59,8 @@ constexpr uint64_t U64MAX = ~0ull;
 constexpr uint32_t MT_ITEMS = 16;
 constexpr uint32_t MT_TILE = 256 * MT_ITEMS;
 constexpr uint32_t MT_RING = 64;          // per-round undecided counters
-constexpr uint32_t MT_BATCH = 4;          // rounds enqueued per host check
-constexpr uint64_t MT_LONG = 1u << 21;    // scans longer than this: a check after every round
+constexpr uint32_t MT_BATCH = 8;          // rounds enqueued per host check (A/B: profiles/r03/maat_batch/)
+constexpr uint64_t MT_LONG = 1u << 22;    // scans longer than this: a check after every round
 constexpr uint8_t ST_UND = 0, ST_COM = 1, ST_ABO = 2;
 // sorted-position flags
 constexpr uint8_t F_R = 1, F_W = 2, F_LAST = 4, F_START = 8;
@@ -906,7 +906,15 @@ int dcc_ctx::maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, 
     MtRoundArgs ra{mc, n, sflb[cb], stxb[cb], state, cts, lacc, uacc, pend, (Ms*)mt_agg.p};
     // one round per host check while the scan is long (each check may
     // compact it), MT_BATCH once it is short
-    const uint32_t nb = (rounds == 0 || mc > MT_LONG) ? 1u : MT_BATCH;
+    static const uint32_t batch = [] {  // DCC_MT_BATCH / DCC_MT_LONG: tuning experiments
+      const char* e = getenv("DCC_MT_BATCH");
+      return e && atoi(e) > 0 ? (uint32_t)atoi(e) : MT_BATCH;
+    }();
+    static const uint64_t long_scan = [] {
+      const char* e = getenv("DCC_MT_LONG");
+      return e && atoll(e) > 0 ? (uint64_t)atoll(e) : MT_LONG;
+    }();
+    const uint32_t nb = (rounds == 0 || mc > long_scan) ? 1u : batch;
     for (uint32_t q = 0; q < nb; q++, rounds++) {
       if (mc) {
         k_mt_up<<<(unsigned)tiles_c, 256, 0, stream>>>(ra);
