@@ -179,9 +179,13 @@ __host__ __device__ constexpr uint32_t sw_idummy(uint32_t q) {
 // per-txn meta word of a tile record
 constexpr uint32_t SWM_VALID = 1, SWM_PRE = 2, SWM_HASW = 4, SWM_STOP = 16;
 // list chunks the serial pass holds in registers: the first SW_RC * 64
-// entries of each list (padded with no-op entries by k_sw_rows)
-constexpr uint32_t SW_RC = 2;
-// One 64-txn tile of a level's serial range as k_sw_seq reads it (6,144 B).
+// entries of each list (padded with no-op entries by k_sw_rows).  Three: the
+// headline's serial ranges hold 107-161 probes per 64-txn tile on average,
+// and a tile past the register chunks takes the long path (an LDS loop per
+// chunk); 2 -> 3 took the passes from 17 / 33 / 55 to 14 / 25 / 48 us, 4 was
+// slower again at level 2 (14 / 28 / 54).
+constexpr uint32_t SW_RC = 3;
+// One 64-txn tile of a level's serial range as k_sw_seq reads it (7,168 B).
 // Only the accesses the serial pass must look at, as two tile-wide lists:
 // probes (accesses whose key an earlier txn of the range writes), grouped by
 // txn (txn t's are [pspan & 0xFFFF, pspan >> 16)), and inserts (writes whose
@@ -197,7 +201,7 @@ struct SwRec {
   uint64_t seg[SW_RC][SW_T];
   uint32_t np, ni;
   uint32_t hdr;  // SWH_*: the serial pass's per-tile branches
-  uint32_t pad[5];
+  uint32_t pad[5 + 128];  // whole KiB (the ring copy moves 16 B per lane)
 };
 constexpr uint32_t SWH_PLONG = 1, SWH_ILONG = 2, SWH_STOP = 4;
 struct SwLevel {     // device control words of one level
