@@ -185,6 +185,9 @@ constexpr uint32_t SWM_VALID = 1, SWM_PRE = 2, SWM_HASW = 4, SWM_STOP = 16;
 // chunk); 2 -> 3 took the passes from 17 / 33 / 55 to 14 / 25 / 48 us, 4 was
 // slower again at level 2 (14 / 28 / 54).
 constexpr uint32_t SW_RC = 3;
+// insert chunks held in registers (the needed writes are fewer: 58-92 per
+// tile at the headline's levels; a third insert chunk is a dummy atomic)
+constexpr uint32_t SW_RC_I = 2;
 // One 64-txn tile of a level's serial range as k_sw_seq reads it (7,168 B).
 // Only the accesses the serial pass must look at, as two tile-wide lists:
 // probes (accesses whose key an earlier txn of the range writes), grouped by

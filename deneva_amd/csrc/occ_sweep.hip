@@ -673,7 +673,7 @@ __global__ __launch_bounds__(256) void k_sw_rows(SwPreArgs a) {
   if (t == 0) {
     R.np = np;
     R.ni = ni;
-    R.hdr = (np > SW_RC * 64 ? SWH_PLONG : 0u) | (ni > SW_RC * 64 ? SWH_ILONG : 0u);
+    R.hdr = (np > SW_RC * 64 ? SWH_PLONG : 0u) | (ni > SW_RC_I * 64 ? SWH_ILONG : 0u);
   }
 #pragma unroll
   for (uint32_t c = 0; c < SW_RC; c++) {
@@ -701,7 +701,7 @@ constexpr uint32_t SEQ_RING = 12;  // LDS record slots (73,728 B)
 constexpr uint32_t SEQ_B = 1024;   // threads of the serial pass's workgroup
 constexpr uint32_t SEQ_PROD = SEQ_B / 64 - 1;  // producer waves
 constexpr uint32_t SEQ_V4 = sizeof(SwRec) / 16;  // uint4 per record
-static_assert(SW_RC * 64 <= SW_IL, "register chunks inside the record");
+static_assert(SW_RC * 64 <= SW_PL && SW_RC_I * 64 <= SW_IL, "register chunks inside the record");
 static_assert(sizeof(SwRec) % (16 * 64) == 0, "record copy: whole uint4 per lane");
 
 // A load the compiler's wait-count tracking does not see: it completes inside
@@ -835,7 +835,7 @@ __global__ __launch_bounds__(SEQ_B) void k_sw_seq(SwSeqArgs a) {
       __builtin_amdgcn_s_sleep(1);
     }
     uint64_t cdep, cseg[SW_RC];
-    uint32_t cmeta, chdr, cpe[SW_RC], cie[SW_RC];
+    uint32_t cmeta, chdr, cpe[SW_RC], cie[SW_RC_I];
     auto read_rec = [&](const SwRec& T) {
       cdep = T.dep[lane];
       cmeta = T.meta[lane];
@@ -843,9 +843,10 @@ __global__ __launch_bounds__(SEQ_B) void k_sw_seq(SwSeqArgs a) {
 #pragma unroll
       for (uint32_t c = 0; c < SW_RC; c++) {
         cpe[c] = T.probe[c * 64 + lane];
-        cie[c] = T.ins[c * 64 + lane];
         cseg[c] = T.seg[c][lane];
       }
+#pragma unroll
+      for (uint32_t c = 0; c < SW_RC_I; c++) cie[c] = T.ins[c * 64 + lane];
     };
     read_rec(ring[0]);
     if (ntiles > 1)
@@ -860,13 +861,14 @@ __global__ __launch_bounds__(SEQ_B) void k_sw_seq(SwSeqArgs a) {
       const uint64_t dep = cdep;
       const uint32_t meta = cmeta;
       uint64_t seg[SW_RC];
-      uint32_t pe[SW_RC], ie[SW_RC];
+      uint32_t pe[SW_RC], ie[SW_RC_I];
 #pragma unroll
       for (uint32_t c = 0; c < SW_RC; c++) {
         seg[c] = cseg[c];
         pe[c] = cpe[c];
-        ie[c] = cie[c];
       }
+#pragma unroll
+      for (uint32_t c = 0; c < SW_RC_I; c++) ie[c] = cie[c];
       const uint32_t kn = k + 1, sn = slot + 1 == SEQ_RING ? 0u : slot + 1;
       // (1) probe C with the register chunks: a txn touching a committed key
       // is dead (padding entries read the always-zero word)
@@ -924,11 +926,11 @@ __global__ __launch_bounds__(SEQ_B) void k_sw_seq(SwSeqArgs a) {
       // (3) needed writes of committed txns join C: a fixed number of LDS
       // operations per tile, so the next tile's wait counts stay exact
 #pragma unroll
-      for (uint32_t c = 0; c < SW_RC; c++) cb_insert_m(cbits, ie[c], M);
+      for (uint32_t c = 0; c < SW_RC_I; c++) cb_insert_m(cbits, ie[c], M);
       if (hdr & SWH_ILONG) {  // long insert lists (rare)
         const uint32_t ni = __builtin_amdgcn_readfirstlane(ring[slot].ni);
         const uint32_t* ovf = a.lst_ovf + (uint64_t)k * SW_OVF;
-        for (uint32_t q0 = SW_RC * 64; q0 < ni; q0 += 64) {
+        for (uint32_t q0 = SW_RC_I * 64; q0 < ni; q0 += 64) {
           const uint32_t q = q0 + lane;
           uint32_t e = sw_idummy(lane);
           if (q < ni) e = q < SW_IL ? ring[slot].ins[q] : ld_sync(ovf + SW_TA + (q - SW_IL));
