@@ -223,7 +223,7 @@ __global__ __launch_bounds__(256) void k_cv_layout(const uint32_t* __restrict__ 
                                                    const uint32_t* __restrict__ off2, uint64_t n,
                                                    const uint64_t* __restrict__ keys,
                                                    const uint8_t* __restrict__ at, KeyPack kp,
-                                                   uint32_t base, K* __restrict__ ak,
+                                                   uint32_t base, uint32_t ulen, K* __restrict__ ak,
                                                    uint32_t* __restrict__ av) {
   __shared__ uint32_t s_src[4][64], s_pre[4][65], s_t[4][64];
   const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -249,7 +249,9 @@ __global__ __launch_bounds__(256) void k_cv_layout(const uint32_t* __restrict__ 
   if (lane == 0) s_pre[w][64] = total;
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  const uint64_t d0 = (uint64_t)base + (off2 ? off2[q0] : off[q0]);
+  // the wave's first request in sequence order: q0 * len for uniform txns,
+  // else the sequence-order offsets (identity order: the batch's own)
+  const uint64_t d0 = (uint64_t)base + (ulen ? q0 * ulen : (off2 ? off2[q0] : off[q0]));
   for (uint32_t jj = lane; jj < total; jj += 64) {
     // largest k with pre[k] <= jj (empty txns share a prefix value: take the last)
     uint32_t lo = 0, hi = 64;
@@ -892,7 +894,7 @@ static int calvin_sort_and_scan(dcc_ctx* ctx, const DevBatch& d, const uint32_t*
     k_cv_layout_held<K><<<grid1(nh, 256), 256, 0, st>>>(hkeys, hat, nh, (uint32_t)d.n, kp, kb[0],
                                                          vb[0]);
   k_cv_layout<K><<<grid1(d.n, 256), 256, 0, st>>>(d.off, seq, off2, d.n, d.keys, d.acctype, kp,
-                                                  (uint32_t)nh, kb[0], vb[0]);  // 4 waves x 64
+                                                  (uint32_t)nh, so.ulen, kb[0], vb[0]);  // 4 waves x 64
   if (prof) CK(hipEventRecord(ctx->pev[1], st));
   int cur;
   if (sizeof(K) == 4)
@@ -1122,7 +1124,9 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint3
       cur = radix_sort_u64(kb, vb, d.n, op.bits, (uint32_t*)cv_scratch.p, stream);
     }
     seq = vb[cur];
-    // request offsets in sequence order
+  }
+  // request offsets in sequence order (uniform txns: q * len, no pass)
+  if (have_seq && !ulen) {
     const uint64_t lt = (d.n + CV_TILE - 1) / CV_TILE;
     CR(cv_len.ensure(this, d.n * 4 + 16, "calvin len"));
     CR(cv_off2.ensure(this, (d.n + 1) * 4 + 16, "calvin off2"));
