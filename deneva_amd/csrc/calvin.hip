@@ -38,6 +38,7 @@
 #include "dcc_ctx.h"
 #include "dcc_device.h"
 #include "occ_kernels.h"
+#include "prep_body.h"
 #include "radix_sort.h"
 
 using namespace dcc;
@@ -70,17 +71,25 @@ struct CvPart {
 };
 
 // ---------------------------------------------------------------- prep
+// Workgroups [0, CV_PREP_BLOCKS): the key / order bit reductions; the rest
+// run the batch validation (prep_body.h: offsets, lengths) beside them in the
+// same launch.
 __global__ __launch_bounds__(256) void k_cv_prep(const uint64_t* __restrict__ keys, uint64_t nnz,
                                                  const uint8_t* __restrict__ at,
                                                  const uint64_t* __restrict__ order, uint64_t n,
                                                  const uint64_t* __restrict__ hkeys, uint64_t nh,
-                                                 CvPart* __restrict__ part) {
+                                                 CvPart* __restrict__ part, const uint32_t* off,
+                                                 PrepPart* pp) {
+  if (blockIdx.x >= CV_PREP_BLOCKS) {
+    prep_body(off, n, at, nnz, 0, pp, blockIdx.x - CV_PREP_BLOCKS, gridDim.x - CV_PREP_BLOCKS);
+    return;
+  }
   __shared__ uint64_t s[4][4];
   __shared__ uint32_t s_ex[4];
   uint64_t kor = 0, kand = ~0ull, oor = 0, oand = ~0ull;
   uint32_t nex = 0;
   const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t stride = (uint64_t)CV_PREP_BLOCKS * blockDim.x;
   // 16-B loads: two keys, sixteen access types per load (when aligned)
   const uint64_t n2 = ((uintptr_t)keys & 15) ? 0 : nnz / 2;
   const uint64_t n16 = ((uintptr_t)at & 15) ? 0 : nnz / 16;
@@ -981,10 +990,9 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint3
   if (profiling) CK(hipEventRecord(pev[0], stream));
 
   // ---- prep: offsets/length validation + which key / order bits vary
-  launch_prep(d.off, d.n, d.acctype, d.nnz, 0, (PrepPart*)part.p, stream);
   CvPart* cvp = (CvPart*)((char*)part.p + 16384);
-  k_cv_prep<<<CV_PREP_BLOCKS, 256, 0, stream>>>(d.keys, d.nnz, d.acctype, d.order, d.n, hkeys, nh,
-                                                cvp);
+  k_cv_prep<<<CV_PREP_BLOCKS + PREP_BLOCKS, 256, 0, stream>>>(d.keys, d.nnz, d.acctype, d.order, d.n,
+                                                              hkeys, nh, cvp, d.off, (PrepPart*)part.p);
   CK(hipGetLastError());
   CK(hipMemcpyAsync(hpart, part.p, 16384 + CV_PREP_BLOCKS * sizeof(CvPart), hipMemcpyDeviceToHost,
                     stream));

@@ -261,3 +261,19 @@ def test_graph_replay_new_contents(engine, sequenced):
         assert np.array_equal(g.cpu().numpy().astype(np.uint32), eg), f"groups, call {i}"
         assert np.array_equal(rc.cpu().numpy(), erc), f"readiness, call {i}"
         assert st["n_commit"] == int((erc == 0).sum())
+
+
+def test_rejects_malformed_batches(engine):
+    """The batch validation (offsets monotone and inside the accesses, at most
+    MAX_ROW_PER_TXN per txn) rides in the key-bit reduction's launch; a bad
+    batch is rejected before any ordering work."""
+    b = make_batch([[(1, RD), (2, WR)], [(3, WR)], [(4, RD)]])
+    off = np.asarray(b.offsets).copy()
+    off[1], off[2] = 3, 2  # not monotone
+    with pytest.raises(d.DccError):
+        engine.calvin_order_epoch(d.EpochBatch(off, b.keys, b.acctype))
+    big = make_batch([[(k + 1, RD) for k in range(70)]])  # > MAX_ROW_PER_TXN
+    with pytest.raises(d.DccError):
+        engine.calvin_order_epoch(big)
+    # the engine still decides a good batch afterwards
+    run(engine, random_batch(np.random.default_rng(5), 300, 12, 200), waves=False)
