@@ -587,8 +587,10 @@ __device__ inline uint32_t gl_block_excl(uint32_t v, uint32_t* s_w, uint32_t& to
 template <typename K>
 __global__ __launch_bounds__(256) void k_cv_up_l(const K* __restrict__ sk,
                                                  const uint32_t* __restrict__ sv, uint64_t m,
-                                                 uint32_t* __restrict__ agg) {
+                                                 uint32_t* __restrict__ agg, uint32_t dshift,
+                                                 uint32_t* __restrict__ hcnt) {
   __shared__ uint32_t s_w[4];
+  __shared__ uint32_t s_h[256];
   __shared__ K lk[CV_LDS];
   __shared__ uint32_t lv[CV_LDS];
   const uint64_t p0 = (uint64_t)blockIdx.x * CV_TILE + (uint64_t)threadIdx.x * CV_ITEMS;
@@ -609,6 +611,15 @@ __global__ __launch_bounds__(256) void k_cv_up_l(const K* __restrict__ sk,
   uint32_t total;
   (void)gl_block_excl(acc, s_w, total);
   if (threadIdx.x == 0) agg[blockIdx.x] = total;
+  if (hcnt) {  // the tile's counts of the write-out partition digit (txn's top bits)
+    s_h[threadIdx.x] = 0;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t i = 0; i < CV_ITEMS; i++)
+      if (p0 + i < m) atomicAdd(&s_h[(v[i] >> dshift) & 255u], 1u);
+    __syncthreads();
+    hcnt[(uint64_t)threadIdx.x * gridDim.x + blockIdx.x] = s_h[threadIdx.x];
+  }
 }
 
 // one workgroup: exclusive scan of the tile aggregates in place (16 per thread)
@@ -634,12 +645,26 @@ __global__ __launch_bounds__(256) void k_cv_top_l(uint32_t* __restrict__ agg, ui
   }
 }
 
+// The windowed put's partition, written by the scan itself: (value, group)
+// pairs into 256 buckets of the txn's top bits (the order inside a bucket is
+// free: every pair carries its destination); hcnt holds the per-digit
+// exclusive prefix over tiles (k_cv_up_l's counts, scanned), tot the digit
+// totals.
+struct PartOut {
+  uint32_t dshift;
+  const uint32_t* hcnt;
+  const uint32_t* tot;
+  uint32_t* ko;
+  uint32_t* go;
+};
+
 template <typename K>
 __global__ __launch_bounds__(256) void k_cv_down_l(const K* __restrict__ sk,
                                                    const uint32_t* __restrict__ sv, uint64_t m,
                                                    const uint32_t* __restrict__ pre, ScanOut o,
-                                                   uint32_t* __restrict__ gs) {
+                                                   PartOut po) {
   __shared__ uint32_t s_w[4];
+  __shared__ uint32_t s_tb[256], s_gb[256], s_run[256];
   __shared__ K lk[CV_LDS];
   __shared__ uint32_t lv[CV_LDS];
   const uint64_t p0 = (uint64_t)blockIdx.x * CV_TILE + (uint64_t)threadIdx.x * CV_ITEMS;
@@ -661,26 +686,79 @@ __global__ __launch_bounds__(256) void k_cv_down_l(const K* __restrict__ sk,
   }
   uint32_t total;
   uint32_t run = gl_combine(pre[blockIdx.x], gl_block_excl(acc, s_w, total));
-  if (gs) {  // groups in sorted order, staged through LDS: coalesced stores
-    K pk = pk0;
-    uint32_t pv = pv0;
-    const uint32_t b = threadIdx.x * (CV_ITEMS + 1);
+  if (po.ko) {
+    // (1) per digit: the tile's count (LDS), its tile-local base (scan over
+    // digits) and its global base (digit totals before it + this tile's
+    // prefix among the tiles)
+    const uint32_t tid = threadIdx.x;
+    s_run[tid] = 0;
+    __syncthreads();
+    uint32_t g[CV_ITEMS], dg[CV_ITEMS];
+    {
+      K pk = pk0;
+      uint32_t pv = pv0;
 #pragma unroll
-    for (uint32_t i = 0; i < CV_ITEMS; i++) {
-      uint32_t g = 0;
-      if (p0 + i < m) {
-        const uint32_t e = gl_element(p0 + i, k[i], v[i], pk, pv);
-        run = gl_combine(run, e);
-        g = e == GL_ID ? DCC_GROUP_NONE : run >> 5;
+      for (uint32_t i = 0; i < CV_ITEMS; i++) {
+        g[i] = 0;
+        dg[i] = (v[i] >> po.dshift) & 255u;
+        if (p0 + i < m) {
+          const uint32_t e = gl_element(p0 + i, k[i], v[i], pk, pv);
+          run = gl_combine(run, e);
+          g[i] = e == GL_ID ? DCC_GROUP_NONE : run >> 5;
+          atomicAdd(&s_run[dg[i]], 1u);
+        }
+        pk = k[i];
+        pv = v[i];
       }
-      pk = k[i];
-      pv = v[i];
-      lv[b + i] = g;  // every read of lv (load_run) precedes the scan's barriers
     }
     __syncthreads();
+    {
+      const uint32_t c = s_run[tid], t = po.tot[tid];
+      uint32_t x = c, y = t;  // inclusive wave scans of the tile counts and the totals
+#pragma unroll
+      for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t xu = __shfl_up(x, d), yu = __shfl_up(y, d);
+        if ((tid & 63u) >= d) {
+          x += xu;
+          y += yu;
+        }
+      }
+      __shared__ uint32_t s_wx[4], s_wy[4];
+      if ((tid & 63u) == 63u) {
+        s_wx[tid >> 6] = x;
+        s_wy[tid >> 6] = y;
+      }
+      __syncthreads();
+      uint32_t bx = 0, by = 0;
+      for (uint32_t w = 0; w < (tid >> 6); w++) {
+        bx += s_wx[w];
+        by += s_wy[w];
+      }
+      s_tb[tid] = bx + x - c;
+      s_gb[tid] = by + y - t + po.hcnt[(uint64_t)tid * gridDim.x + blockIdx.x];
+      s_run[tid] = bx + x - c;
+    }
+    __syncthreads();
+    // (2) the tile's pairs in digit order through LDS (any order within a digit)
+    uint32_t* lvv = lv;
+    uint32_t* lgg = (uint32_t*)lk;
+#pragma unroll
+    for (uint32_t i = 0; i < CV_ITEMS; i++)
+      if (p0 + i < m) {
+        const uint32_t q = atomicAdd(&s_run[dg[i]], 1u);
+        lvv[q] = v[i];
+        lgg[q] = g[i];
+      }
+    __syncthreads();
+    // (3) coalesced runs per digit
     const uint64_t base = (uint64_t)blockIdx.x * CV_TILE;
-    for (uint32_t i = threadIdx.x; i < CV_TILE; i += 256)
-      if (base + i < m) gs[base + i] = lv[i + (i >> 4)];
+    const uint32_t n_here = (uint32_t)min<uint64_t>(CV_TILE, m - base);
+    for (uint32_t j = tid; j < n_here; j += 256) {
+      const uint32_t vv = lvv[j], d = (vv >> po.dshift) & 255u;
+      const uint32_t dst = s_gb[d] + (j - s_tb[d]);
+      po.ko[dst] = vv;
+      po.go[dst] = lgg[j];
+    }
     return;
   }
   if (p0 >= m) return;
@@ -708,8 +786,9 @@ __global__ __launch_bounds__(256) void k_cv_down_l(const K* __restrict__ sk,
 // The windowed group write-out (uniform request counts, large epochs).  The
 // direct store from k_cv_down_l puts each request's group at a random place:
 // one 32-B sector write per 4-B store (PMC: 521 MB written for 67 MB).
-// Instead the sorted values (txn, request) and their groups are partitioned
-// by the txn's top 8 bits (one counting pass), and each workgroup here owns
+// Instead k_cv_down_l writes the (value, group) pairs already partitioned by
+// the txn's top 8 bits (bucket offsets from k_cv_up_l's per-tile digit counts
+// scanned by rs_scan_rows), and each workgroup here owns
 // a window of the group array (a bucket's requests are contiguous there):
 // it places its bucket's groups into the window in LDS and stores the window
 // with coalesced stores.
@@ -728,7 +807,7 @@ __global__ __launch_bounds__(1024) void k_cv_put(const uint32_t* __restrict__ sv
   const uint64_t d_end = min<uint64_t>(t_lo + (1ull << tsh), n) * ulen;
   if (d_lo >= d_end) return;  // whole workgroup
   const uint32_t w = (uint32_t)min<uint64_t>(wh, d_end - d_lo);
-  // the bucket's pairs: the digit totals before it (counting pass order)
+  // the bucket's pairs: the digit totals before it (bucket order)
   if (threadIdx.x < 2) s_rng[threadIdx.x] = 0;
   __syncthreads();
   if (threadIdx.x < bkt) atomicAdd(&s_rng[0], tot[threadIdx.x]);
@@ -894,8 +973,11 @@ static int calvin_sort_and_scan(dcc_ctx* ctx, const DevBatch& d, const uint32_t*
   CR(ctx->calvin_b.ensure(ctx, std::max<uint64_t>(16, m * sizeof(K)), "calvin keys b"));
   CR(ctx->calvin_c.ensure(ctx, std::max<uint64_t>(16, m * 4), "calvin vals a"));
   CR(ctx->calvin_d.ensure(ctx, std::max<uint64_t>(16, m * 4), "calvin vals b"));
-  CR(ctx->cv_scratch.ensure(ctx, rs_scratch_words(m) * 4 + 64, "radix scratch"));
   const uint64_t tiles = (m + CV_TILE - 1) / CV_TILE;
+  // the radix passes' counts, or the scan's write-out partition counts
+  // ([256][tiles] + 256 totals)
+  CR(ctx->cv_scratch.ensure(ctx, std::max<uint64_t>(rs_scratch_words(m), 256 * (tiles + 1)) * 4 + 64,
+                            "radix scratch"));
   CR(ctx->cv_agg.ensure(ctx, std::max<uint64_t>(1, tiles) * sizeof(Gs), "calvin scan"));
   K* kb[2] = {(K*)ctx->calvin_a.p, (K*)ctx->calvin_b.p};
   uint32_t* vb[2] = {(uint32_t*)ctx->calvin_c.p, (uint32_t*)ctx->calvin_d.p};
@@ -918,27 +1000,31 @@ static int calvin_sort_and_scan(dcc_ctx* ctx, const DevBatch& d, const uint32_t*
     k_cv_down<K><<<(unsigned)tiles, 256, 0, st>>>(kb[cur], vb[cur], m, agg, so);
   } else {  // grant groups only: the one-word state
     uint32_t* agg = (uint32_t*)ctx->cv_agg.p;
-    k_cv_up_l<K><<<(unsigned)tiles, 256, 0, st>>>(kb[cur], vb[cur], m, agg);
+    const bool put = so.ulen && d.nnz >= CV_PUT_MIN;
+    const uint64_t tmax = d.n + nh - 1;
+    const uint32_t tb = tmax ? 64u - (uint32_t)__builtin_clzll(tmax) : 1u;
+    const uint32_t tsh = tb > 8 ? tb - 8 : 0;
+    uint32_t* hcnt = (uint32_t*)ctx->cv_scratch.p;
+    uint32_t* htot = hcnt + 256 * tiles;
+    k_cv_up_l<K><<<(unsigned)tiles, 256, 0, st>>>(kb[cur], vb[cur], m, agg, 7 + tsh,
+                                                  put ? hcnt : nullptr);
     k_cv_top_l<<<1, 256, 0, st>>>(agg, (uint32_t)tiles);
-    if (so.ulen && d.nnz >= CV_PUT_MIN) {
-      // groups in sorted order into the idle value buffer; one counting pass
-      // of (value, group) on the txn's top 8 bits; the windowed put
-      uint32_t* gs = vb[1 - cur];
-      k_cv_down_l<K><<<(unsigned)tiles, 256, 0, st>>>(kb[cur], vb[cur], m, agg, so, gs);
-      const uint64_t tmax = d.n + nh - 1;
-      const uint32_t tb = tmax ? 64u - (uint32_t)__builtin_clzll(tmax) : 1u;
-      const uint32_t tsh = tb > 8 ? tb - 8 : 0;
+    if (put) {
+      // the scan writes (value, group) pairs straight into 256 buckets of the
+      // txn's top 8 bits (counted by the up pass); the windowed put places
+      // each bucket's groups in request order
+      rs_scan_rows(hcnt, 256, (uint32_t)tiles, htot, st);
       uint32_t* ko = (uint32_t*)kb[1 - cur];
-      uint32_t* go = (uint32_t*)kb[cur];
-      uint32_t* scratch = (uint32_t*)ctx->cv_scratch.p;
-      radix_pass_u32(vb[cur], gs, ko, go, m, 7 + tsh, scratch, st);
+      uint32_t* go = vb[1 - cur];
+      k_cv_down_l<K><<<(unsigned)tiles, 256, 0, st>>>(kb[cur], vb[cur], m, agg, so,
+                                                      PartOut{7 + tsh, hcnt, htot, ko, go});
       const uint64_t span = (1ull << tsh) * so.ulen;
       const uint32_t H = (uint32_t)((span + CV_WIN - 1) / CV_WIN);
       const uint32_t wh = (uint32_t)((span + H - 1) / H);
-      k_cv_put<<<256 * H, 1024, 0, st>>>(ko, go, scratch + 256 * rs_tiles(m), (uint32_t)d.n,
-                                         so.ulen, tsh, H, wh, so.group);
+      k_cv_put<<<256 * H, 1024, 0, st>>>(ko, go, htot, (uint32_t)d.n, so.ulen, tsh, H, wh, so.group);
     } else {
-      k_cv_down_l<K><<<(unsigned)tiles, 256, 0, st>>>(kb[cur], vb[cur], m, agg, so, nullptr);
+      k_cv_down_l<K><<<(unsigned)tiles, 256, 0, st>>>(kb[cur], vb[cur], m, agg, so,
+                                                      PartOut{0, nullptr, nullptr, nullptr, nullptr});
     }
   }
   CK(hipGetLastError());

@@ -33,13 +33,10 @@ int radix_sort_u32(uint32_t* k[2], uint32_t* v[2], uint64_t m, uint32_t bits, ui
 int radix_sort_u64(uint64_t* k[2], uint32_t* v[2], uint64_t m, uint32_t bits, uint32_t* scratch,
                    hipStream_t st);
 
-// One stable counting pass on digit (key >> shift) & 255 (a partition into
-// 256 buckets), kin/vin -> kout/vout.
-void radix_pass_u32(const uint32_t* kin, const uint32_t* vin, uint32_t* kout, uint32_t* vout,
-                    uint64_t m, uint32_t shift, uint32_t* scratch, hipStream_t st);
-
 // Exclusive scan of one u32 row in place (one workgroup); *total = its sum.
 void rs_scan_one(uint32_t* row, uint32_t len, uint32_t* total, hipStream_t st);
+// The same for `rows` rows of `len` (row r at cnt + r * len); tot[r] = row sums.
+void rs_scan_rows(uint32_t* cnt, uint32_t rows, uint32_t len, uint32_t* tot, hipStream_t st);
 
 // Bit-gather: the positions where a batch's keys differ (OR ^ AND over every
 // key) packed into the low bits, as at most 32 runs of contiguous bits.

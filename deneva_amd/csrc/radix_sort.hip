@@ -258,20 +258,11 @@ int radix_sort_u64(uint64_t* k[2], uint32_t* v[2], uint64_t m, uint32_t bits, ui
   return radix_sort_impl<uint64_t>(k, v, m, bits > 64 ? 64 : bits, scratch, st);
 }
 
-void radix_pass_u32(const uint32_t* kin, const uint32_t* vin, uint32_t* kout, uint32_t* vout,
-                    uint64_t m, uint32_t shift, uint32_t* scratch, hipStream_t st) {
-  if (m == 0) return;
-  const uint32_t tiles = (uint32_t)rs_tiles(m);
-  uint32_t* cnt = scratch;
-  uint32_t* tot = scratch + 256ull * tiles;
-  k_rs_hist<uint32_t><<<tiles, RS_THREADS, 0, st>>>(kin, m, shift, cnt, tiles);
-  k_rs_scan<<<256, RS_THREADS, 0, st>>>(cnt, tiles, tot);
-  k_rs_scatter<uint32_t><<<tiles, RS_THREADS, 0, st>>>(kin, vin, kout, vout, m, shift, cnt, tot,
-                                                       tiles);
-}
-
 void rs_scan_one(uint32_t* row, uint32_t len, uint32_t* total, hipStream_t st) {
   k_rs_scan<<<1, RS_THREADS, 0, st>>>(row, len, total);
+}
+void rs_scan_rows(uint32_t* cnt, uint32_t rows, uint32_t len, uint32_t* tot, hipStream_t st) {
+  k_rs_scan<<<rows, RS_THREADS, 0, st>>>(cnt, len, tot);
 }
 
 KeyPack make_keypack(uint64_t varying) {
