@@ -16,3 +16,5 @@ python3 -c "import json;j=json.load(open('$O/c4.json'))['C4'];print('C4 dev',j['
 f=$(find "$O/prof" -name '*kernel_stats.csv' | head -1)
 head -20 "$f" | cut -d, -f1-4 | sed 's/(.*)"/"/'
 python3 "$R/tools/kstats.py" "$O/prof" 20
+t=$(find "$O/prof" -name '*kernel_trace.csv' | head -1)
+python3 "$R/tools/trace_epoch.py" "$t" > "$O/trace.txt" && cat "$O/trace.txt"

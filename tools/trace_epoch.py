@@ -17,7 +17,7 @@ def main():
     if ends:
         bounds = [(ends[i - 1] + 1 if i else 0, ends[i] + 1) for i in range(len(ends))]
     else:
-        starts = [i for i, r in enumerate(rows) if "k_prep" in r["Kernel_Name"] or "k_fill" in r["Kernel_Name"]]
+        starts = [i for i, r in enumerate(rows) if any(k in r["Kernel_Name"] for k in ("k_prep", "k_fill", "k_cv_prep"))]
         bounds = [(s, starts[i + 1] if i + 1 < len(starts) else len(rows)) for i, s in enumerate(starts)]
     e = int(sys.argv[2]) if len(sys.argv) > 2 else max(0, len(bounds) - 2)
     a, b = bounds[e]
