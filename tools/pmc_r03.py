@@ -4,7 +4,7 @@
 epoch; FETCH_SIZE is doubled (gfx950 counts 128-B requests at 64 B,
 MI355X_MICROARCH.md HBM section), WRITE_SIZE taken as is; L2 hit rate =
 TCC_HIT_sum / (TCC_HIT_sum + TCC_MISS_sum).  An OCC epoch is the dispatches
-from one k_fill to the next; a Calvin epoch from one k_prep to the next.
+from one k_fill to the next; a Calvin epoch from one k_cv_prep to the next.
     pmc_r03.py <pass dir root> <out json>"""
 import csv
 import glob
@@ -82,7 +82,7 @@ def main():
         "serial_pass_l2_hit": first(l2, "k_sw_seq", hit),
         "pre_pass_l2_hit": first(l2, "k_sw_pre", hit)}
     # ---- C4 Calvin epoch: per-kernel sums and hit rates
-    cfe, cwr, cl2 = (epochs(dispatches(root, p), "k_prep") for p in ("c_fetch", "c_write", "c_l2"))
+    cfe, cwr, cl2 = (epochs(dispatches(root, p), "k_cv_prep") for p in ("c_fetch", "c_write", "c_l2"))
 
     def per_kernel(es, fn):
         acc = defaultdict(list)
