@@ -45,15 +45,13 @@ def parse():
                     help="comma-separated secondary configs to run INSTEAD of the headline "
                          "(profiling aid): " + ",".join(CONFIGS))
     ap.add_argument("--solver", type=int, default=0,
-                    help="OCC solver: 0 auto (= 4), 1 fixed-point rounds only, 3 sweep levels, "
-                         "4 sweep levels then commit/kill rounds")
+                    help="OCC solver: 0 auto, 1 fixed-point rounds only, 3 sweep levels, "
+                         "4 level 0 of the sweep then the dataflow solver")
     ap.add_argument("--sweep-levels", type=int, default=0,
                     help="sweep levels per captured epoch (DCC_OPT_SWEEP_LEVELS; 0: the engine's "
                          "default)")
     ap.add_argument("--ro-split", type=int, default=-1,
                     help="DCC_OPT_RO_SPLIT (-1: the engine's default)")
-    ap.add_argument("--ck-level", type=int, default=0,
-                    help="solver 4: full sweep levels before the commit/kill rounds (0: default)")
     ap.add_argument("--strong", action="store_true",
                     help="strong scaling: one fixed batch of --txns txns key-sharded over the "
                          "N ranks (BASELINE config C5 with --theta 0.99 --seed 0xD3E7A002); "
@@ -498,8 +496,6 @@ def main():
         torch.cuda.set_device(0)
         with d.Engine(0) as eng:
             eng.set_option(d._abi.OPT_SOLVER, args.solver)
-            if args.ck_level:
-                eng.set_option(d._abi.OPT_CK_LEVEL, args.ck_level)
             print(json.dumps(secondary_configs(eng, 0, steps=args.steps, warmup=args.warmup,
                                                only=args.only.split(","))), flush=True)
         return
@@ -529,8 +525,6 @@ def main():
         eng.set_option(d._abi.OPT_SWEEP_LEVELS, args.sweep_levels)
     if args.ro_split >= 0:
         eng.set_option(d._abi.OPT_RO_SPLIT, args.ro_split)
-    if args.ck_level:
-        eng.set_option(d._abi.OPT_CK_LEVEL, args.ck_level)
     if world > 1:
         if args.exchange == "rccl":
             uid = d.comm_unique_id() if rank == 0 else bytes(d._abi.UNIQUE_ID_BYTES)

@@ -40,7 +40,6 @@ OPT_SOLVER = 5
 OPT_SWEEP_LEVELS = 6
 OPT_HIST_MERGE = 7
 OPT_FAIL_RANK = 8
-OPT_CK_LEVEL = 9
 OPT_RO_SPLIT = 10
 
 

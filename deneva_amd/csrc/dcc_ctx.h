@@ -14,6 +14,7 @@
 
 namespace dcc {
 struct SwShard;  // occ_kernels.h: one key-sharded sweep level's serial range
+struct DfArgs;   // occ_kernels.h: the dataflow solver's buffers
 }
 
 struct dcc_ctx;
@@ -84,14 +85,17 @@ struct dcc_ctx {
   uint64_t recheck_max = 16384;   // fold the kill wave into rounds with lists <= this
   uint32_t batch_max = 8;       // rounds enqueued between host synchronisations
   bool bars_used = false;       // this epoch's rounds used grid-barrier words
-  int solver = 0;               // 0 auto (= 3), 1 fixed-point rounds, 3 sweep, 4 sweep levels +
-                                // commit/kill rounds (measured slower)
+  int solver = 0;               // 0 auto (= 3), 1 fixed-point rounds, 3 sweep, 4 level 0 of the
+                                // sweep + the dataflow solver (occ_dataflow.hip)
   bool use_sweep() const { return solver != 1; }
-  bool use_ck() const { return solver == 4; }
-  uint32_t ck_graph_rounds = 10;  // commit/kill rounds in the captured epoch
-  uint32_t ck_level = 2;          // full sweep levels before the commit/kill rounds
-  uint64_t ck_clean = 0;          // table slots known clean
-  bool ck_dirty = false;          // an epoch stopped before k_final reset its slots
+  bool use_df() const { return solver == 4; }
+  bool df_on = false;             // this epoch: level 0's compaction launch is k_df_list
+  uint64_t df_clean = 0;          // dataflow key-table slots known clean
+  bool df_dirty = false;          // an epoch stopped before its solver reset the slots it used
+  uint32_t df_max_bits = 0;       // dataflow key table: 1 << df_max_bits slots allocated
+  uint64_t df_cap_acc = 0, df_cap_txn = 0;
+  uint32_t df_grid = 0;           // k_df_solve workgroups (all resident)
+  uint64_t df_limit_ticks = 50000000;  // the solver's time limit (0.5 s; DCC_DF_LIMIT_US)
   bool ro_split = true;           // DCC_OPT_RO_SPLIT
   bool ro_on = false;             // this epoch splits read-only txns off (sweep, one GPU)
   uint32_t wt_bits = 18;          // committed-writer table slots (WT_BITS_DEFAULT; grows after an overflow)
@@ -148,7 +152,8 @@ struct dcc_ctx {
                                                         // list, writer tables, committed writers
   DevBuf sw_xcnt, sw_xsend, sw_xrec, sw_mcnt, sw_moff, sw_mkeys, sw_mat, sw_kill;  // key-sharded sweep  // sweep tile records
   SubBufs sw_list[2];                            // sweep level lists (ping-pong)
-  DevBuf ck_tab, ck_ctl, ck_aslot, ck_lst[2];    // commit/kill solver (occ_ck.hip)
+  DevBuf df_ctl, df_tkey, df_tnw, df_trec;       // dataflow solver: control, key table
+  DevBuf df_tid, df_aoff, df_cfirst, df_slot, df_rank, df_x, df_wtid, df_words;  // list, entries
   DevBuf l_tid[2], l_coff[2], l_cent[2];         // ping-pong undecided lists
   // OCC history (occ.h:62-64) on the device: base + delta levels
   HistStore hs[2];
@@ -207,6 +212,8 @@ struct dcc_ctx {
   DevBuf fin_off, fin_keys, fin_at, fin_state, fin_hasw, fin_rc, fin_cnt;
   int fin_save(const DevBatch& d, bool host_batch, uint64_t nnz_w);
   int occ_finish(const uint8_t* final_rc, uint64_t* out_tn, uint32_t flags);
+  int occ_finish_prepare(const uint8_t* final_rc, uint32_t flags, uint32_t& n_cw);
+  int occ_finish_commit(uint32_t n_cw, uint64_t* out_tn, uint32_t flags);
   int occ_rounds(const SubProb& sp, uint32_t maxlen, bool prof, uint32_t& rounds);
   int sweep_reserve(const DevBatch& d);
   // levels [l0, l1); resume: level l0's serial part already ran (start at its
@@ -214,9 +221,9 @@ struct dcc_ctx {
   int sweep_enqueue(const DevBatch& d, int l0, int l1, const dcc::SwShard* shard = nullptr,
                     bool resume = false, bool tail_serial = false);
   int sweep_sharded(const DevBatch& d, int& next_level);
-  int ck_reserve(const DevBatch& d);
-  int ck_enqueue(const DevBatch& d, uint32_t r0, uint32_t r1, bool build);  // rounds [r0, r1]
-  uint32_t ck_cap_bits = 0;
+  int df_reserve(const DevBatch& d);
+  dcc::DfArgs df_args(const DevBatch& d);
+  int df_enqueue(const DevBatch& d);  // k_df_alloc, k_df_scatter, k_df_solve
   int sweep_ro(const DevBatch& d, bool big, bool scan, uint64_t nnz_w);  // decide the RO list
   int occ_sweep_finish(const DevBatch& d, int& next_level, bool& done, uint32_t maxlen);
   int occ_snapshot(const dcc_batch* b, const dcc_occ_snapshot* s, uint8_t* out_rc, dcc_stats* st);

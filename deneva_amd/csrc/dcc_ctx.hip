@@ -203,10 +203,6 @@ extern "C" int dcc_set_option(dcc_ctx* ctx, int option, int64_t value) {
       if (value < 0 || value > SW_MAX_LEVEL) return DCC_EINVAL;
       ctx->sw_levels = (uint32_t)value;
       return DCC_OK;
-    case DCC_OPT_CK_LEVEL:
-      if (value < 1 || value > SW_MAX_LEVEL - 2) return DCC_EINVAL;
-      ctx->ck_level = (uint32_t)value;
-      return DCC_OK;
     case DCC_OPT_RO_SPLIT:
       // 0 off, 1 on; 4..24: on with a writer table of 2^value slots (tests
       // drive the overflow fallback with small tables)
@@ -247,7 +243,8 @@ std::vector<DevBuf*> dcc_ctx::all_bufs() {
                             &mt_misc, &mt_slot, &mt_sval, &mt_slot2, &mt_sval2, &mt_sfl,
                             &mt_stx, &mt_txn, &mt_agg, &mt_sflB, &mt_stxB, &mt_k1, &mt_tcnt, &mt_ul, &ix_keys, &ix_ord, &ix_rows, &ix_cnt, &wv_buf, &ix_scr, &wv_hbuf, &wv_obuf,
                             &h_K[0], &h_K[1], &h_V[0], &h_V[1], &h_scr, &h_bsum,
-                            &ck_tab, &ck_ctl, &ck_aslot, &ck_lst[0], &ck_lst[1],
+                            &df_ctl, &df_tkey, &df_tnw, &df_trec, &df_tid, &df_aoff, &df_cfirst,
+                            &df_slot, &df_rank, &df_x, &df_wtid, &df_words,
                             &fin_off, &fin_keys, &fin_at, &fin_state, &fin_hasw, &fin_rc, &fin_cnt,
                             &sh_off, &sh_keys, &sh_at, &sh_src, &sh_cnt, &sh_bsum, &sh_rc, &sh_tn, &sh_grp};
   for (auto& h : hs)
@@ -639,16 +636,24 @@ extern "C" int dcc_occ_finish_epoch(dcc_ctx* ctx, const uint8_t* final_rc, uint6
                                     uint32_t flags) {
   if (!ctx) return DCC_EINVAL;
   if (ctx->multi) {
-    // every shard appends its own keys' writes; tn numbering is alike on all
-    for (int r = 0; r < dcc_multi_size(ctx); r++) {
-      dcc_ctx* s = dcc_multi_sub(ctx, r);
-      if (hipSetDevice(s->device) != hipSuccess) return DCC_ENODEV;
-      const int e = s->occ_finish(final_rc, r == 0 ? out_commit_tn : nullptr, flags);
-      if (e != DCC_OK) {
-        ctx->last_error = "rank " + std::to_string(r) + ": " + s->last_error;
-        return e;
+    // every shard appends its own keys' writes; tn numbering is alike on all.
+    // Every rank is checked first (allocations, the votes): a failure there
+    // leaves every rank's epoch pending, so the call can be repeated.  Only
+    // the history appends follow (an allocation failure there leaves the
+    // shards disagreeing: the context must then be re-created).
+    const int R = dcc_multi_size(ctx);
+    std::vector<uint32_t> n_cw(R, 0);
+    for (int pass = 0; pass < 2; pass++)
+      for (int r = 0; r < R; r++) {
+        dcc_ctx* s = dcc_multi_sub(ctx, r);
+        if (hipSetDevice(s->device) != hipSuccess) return DCC_ENODEV;
+        const int e = pass == 0 ? s->occ_finish_prepare(final_rc, flags, n_cw[r])
+                                : s->occ_finish_commit(n_cw[r], r == 0 ? out_commit_tn : nullptr, flags);
+        if (e != DCC_OK) {
+          ctx->last_error = "rank " + std::to_string(r) + ": " + s->last_error;
+          return e;
+        }
       }
-    }
     return DCC_OK;
   }
   if (hipSetDevice(ctx->device) != hipSuccess) return DCC_ENODEV;

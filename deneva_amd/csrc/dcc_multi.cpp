@@ -251,6 +251,29 @@ void dcc_multi_destroy(dcc_ctx* ctx) {
   ctx->multi = nullptr;
 }
 
+// A device batch (DCC_DEVICE_PTRS) is validated whole before it is sharded:
+// check_batch only sees host arrays, and the ranks' shards always have
+// well-formed offsets, so a malformed device batch would otherwise be decided
+// silently (or fail on some ranks and not others, breaking the "every rank
+// runs the same collectives" rule).  Rank 0's sub-context runs the offsets /
+// length pass (prep_body) on the caller's arrays (over xGMI when they sit on a
+// peer) and the batch is rejected before any rank starts.
+static int multi_check_device_batch(dcc_ctx* ctx, const dcc_batch* b) {
+  if (!(b->flags & DCC_DEVICE_PTRS) || b->n_txn == 0) return DCC_OK;
+  dcc_ctx* s = ctx->multi->sub[0];
+  int prev = 0;
+  if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(s->device) != hipSuccess)
+    return ctx->fail(DCC_ENODEV, "multi-GPU: cannot select rank 0's device");
+  DevBatch d;
+  uint32_t maxlen = 0;
+  uint64_t nnz_w = 0;
+  int e = s->stage_batch(b, d);
+  if (e == DCC_OK) e = s->device_prep(d, maxlen, nnz_w);
+  (void)hipSetDevice(prev);
+  if (e != DCC_OK) return ctx->fail(e, "%s", s->last_error.c_str());
+  return DCC_OK;
+}
+
 // Every rank stages the batch (host: its own H2D copy; device: the caller's
 // arrays, read over xGMI when they sit on a peer) and keeps its key shard on
 // its GPU (dcc_ctx::shard_stage, shard_dev.hip); its epoch runs on that device
@@ -262,6 +285,7 @@ int dcc_multi_occ_epoch(dcc_ctx* ctx, const dcc_batch* b, uint8_t* out_rc, uint6
   // the whole batch is validated before it is sharded: every rank then
   // runs the same collectives (no rank may fail alone mid-exchange)
   if (int e = ctx->check_batch(b)) return e;
+  if (int e = multi_check_device_batch(ctx, b)) return e;
   const bool dev = (b->flags & DCC_DEVICE_PTRS) != 0;
   const uint64_t n = b->n_txn;
   const int R = (int)ctx->multi->sub.size();
@@ -315,6 +339,7 @@ int dcc_multi_calvin_epoch(dcc_ctx* ctx, const dcc_batch* b, const dcc_calvin_he
   if (!b) return ctx->fail(DCC_EINVAL, "null batch");
   if (out_wave) return ctx->fail(DCC_ENOTSUP, "calvin: wave levels need the whole epoch on one GPU");
   if (int e = ctx->check_batch(b)) return e;
+  if (int e = multi_check_device_batch(ctx, b)) return e;
   if (held && held->n && (!held->keys || !held->acctype))
     return ctx->fail(DCC_EINVAL, "calvin: null held arrays");
   const bool dev = (b->flags & DCC_DEVICE_PTRS) != 0;

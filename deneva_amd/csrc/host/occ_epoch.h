@@ -89,11 +89,16 @@ class OccEpoch {
       open_.finish.push_back(finish_tn);
     }
     if (slot == 0) opened_ = std::chrono::steady_clock::now();
-    waiting_++;  // in validate(), for the open or the in-flight epoch
+    // waiting for the OPEN epoch: a worker blocked on the in-flight one will
+    // add its next txn to the open epoch once that one is decided, so it does
+    // not count towards "every worker is in" (the open epoch would otherwise
+    // close early, right after the in-flight call returns and before its
+    // waiters have woken)
+    open_waiting_++;
     int err = 0;
     while (decided_.find(ep) == decided_.end()) {
       const bool full = open_.off.size() - 1 >= opt_.max_txns;
-      const bool all_in = waiting_ >= opt_.n_workers;
+      const bool all_in = open_waiting_ >= opt_.n_workers;
       const auto age = std::chrono::duration<double, std::milli>(
                            std::chrono::steady_clock::now() - opened_).count();
       if (ep == epoch_ && !busy_ && (full || all_in || age >= opt_.timer_ms)) {
@@ -104,7 +109,6 @@ class OccEpoch {
       // intercepts; a 200 us poll does not care about clock steps)
       cv_.wait_until(lk, std::chrono::system_clock::now() + std::chrono::microseconds(200));
     }
-    waiting_--;
     auto it = decided_.find(ep);
     if (it == decided_.end()) return err ? err : DCC_EIO;
     if (it->second.err) err = it->second.err;
@@ -151,6 +155,7 @@ class OccEpoch {
     open_.start.clear();
     open_.finish.clear();
     const uint64_t id = epoch_++;
+    open_waiting_ = 0;  // they wait for the closed epoch now
     busy_ = true;
     if (opt_.overlap) lk.unlock();
     const uint64_t n = fly_.off.size() - 1;
@@ -208,7 +213,7 @@ class OccEpoch {
   bool busy_ = false;  // an engine call is in flight
   std::chrono::steady_clock::time_point opened_{};
   uint64_t epoch_ = 0;
-  int waiting_ = 0;
+  int open_waiting_ = 0;  // workers in validate() for the open epoch
   std::map<uint64_t, Decided> decided_;
   Stats stats_;
 };

@@ -498,7 +498,8 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1, const SwShard* shl
       if (top) CR(comm_allreduce_max_u8((uint8_t*)hasw.p, d.n));
       launch_sw_apply(fa, fgrid, stream);
     }
-    launch_sw_compact(fa, fgrid, stream);
+    if (top && df_on) launch_df_list(fa, df_args(d), fgrid, stream);
+    else launch_sw_compact(fa, fgrid, stream);
   }
   CK(hipGetLastError());
   return DCC_OK;
@@ -597,7 +598,12 @@ int dcc_ctx::fin_save(const DevBatch& d, bool host_batch, uint64_t nnz_w) {
   CK(hipMemcpyAsync(fin_state.p, state.p, d.n, hipMemcpyDeviceToDevice, stream));
   CK(hipMemcpyAsync(fin_hasw.p, hasw.p, d.n, hipMemcpyDeviceToDevice, stream));
   fin_d = d;
-  if (host_batch) {
+  // the batch must outlive this call: a host batch sits in the staging
+  // buffers of the next call, and a multi-GPU rank's shard (a "device" batch
+  // in this context's own sh_* buffers) is rewritten by the next epoch of any
+  // kind (e.g. a Calvin epoch before dcc_occ_finish_epoch) -- copy both
+  const bool own = d.off == (const uint32_t*)sh_off.p || d.keys == (const uint64_t*)sh_keys.p;
+  if (host_batch || own) {
     CR(fin_off.ensure(this, (d.n + 1) * 4, "deferred finish offsets"));
     CR(fin_keys.ensure(this, std::max<uint64_t>(8, d.nnz * 8), "deferred finish keys"));
     CR(fin_at.ensure(this, std::max<uint64_t>(16, d.nnz), "deferred finish types"));
@@ -616,14 +622,16 @@ int dcc_ctx::fin_save(const DevBatch& d, bool host_batch, uint64_t nnz_w) {
   return DCC_OK;
 }
 
-int dcc_ctx::occ_finish(const uint8_t* final_rc, uint64_t* out_tn, uint32_t flags) {
+// Two phases, so a multi-GPU context can check every rank before any rank
+// changes state: prepare (allocations, the finish flags, the tn numbering and
+// the bad-vote check -- device scratch only) and commit (the history append,
+// tnc, the tn copy-out).
+int dcc_ctx::occ_finish_prepare(const uint8_t* final_rc, uint32_t flags, uint32_t& n_cw) {
   dcc_ctx* ctx = this;
+  n_cw = 0;
   if (!fin_pending) return fail(DCC_EINVAL, "no epoch awaits dcc_occ_finish_epoch");
   const uint64_t n = fin_d.n;
-  if (n == 0) {
-    fin_pending = false;
-    return DCC_OK;
-  }
+  if (n == 0) return DCC_OK;
   if (!final_rc) return fail(DCC_EINVAL, "null final_rc");
   const bool dev = (flags & DCC_DEVICE_PTRS) != 0;
   const uint8_t* frc = final_rc;
@@ -636,84 +644,125 @@ int dcc_ctx::occ_finish(const uint8_t* final_rc, uint64_t* out_tn, uint32_t flag
   CR(bsum.ensure(this, ((n + 1023) / 1024 + 1) * 8, "bsum"));
   CR(tn.ensure(this, n * 8, "tn"));
   CR(fin_cnt.ensure(this, 64, "finish counts"));
-  uint64_t* tn_dev = (dev && out_tn) ? out_tn : (uint64_t*)tn.p;
   CK(hipMemsetAsync(fin_cnt.p, 0, 8, stream));
   launch_finish_flags(frc, (const uint8_t*)fin_state.p, (const uint8_t*)fin_hasw.p, n,
                       (uint32_t*)cflag.p, (uint32_t*)fin_cnt.p, stream);
-  launch_commit_tn((const uint32_t*)cflag.p, n, (uint64_t*)bsum.p, tnc, tn_dev, stream);
+  launch_commit_tn((const uint32_t*)cflag.p, n, (uint64_t*)bsum.p, tnc, (uint64_t*)tn.p, stream);
   CK(hipGetLastError());
   CK(hipMemcpyAsync(hmisc, fin_cnt.p, 8, hipMemcpyDeviceToHost, stream));
   CK(hipStreamSynchronize(stream));
-  const uint32_t n_cw = ((const uint32_t*)hmisc)[0], bad = ((const uint32_t*)hmisc)[1];
+  n_cw = ((const uint32_t*)hmisc)[0];
+  const uint32_t bad = ((const uint32_t*)hmisc)[1];
   if (bad)
     return fail(DCC_EINVAL, "final_rc: %u txns with global RCOK aborted locally (2PC never commits them)",
                 bad);
-  CR(hist_append_epoch(fin_d, tn_dev, fin_nnz_w, n_cw));
-  tnc += n_cw;
-  if (out_tn && !dev) CK(hipMemcpy(out_tn, tn_dev, n * 8, hipMemcpyDeviceToHost));
+  return DCC_OK;
+}
+
+int dcc_ctx::occ_finish_commit(uint32_t n_cw, uint64_t* out_tn, uint32_t flags) {
+  dcc_ctx* ctx = this;
+  const uint64_t n = fin_d.n;
+  if (n) {
+    CR(hist_append_epoch(fin_d, (const uint64_t*)tn.p, fin_nnz_w, n_cw));
+    tnc += n_cw;
+    if (out_tn) {
+      const bool dev = (flags & DCC_DEVICE_PTRS) != 0;
+      CK(hipMemcpy(out_tn, tn.p, n * 8, dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost));
+    }
+  }
   fin_pending = false;
   return DCC_OK;
 }
 
+int dcc_ctx::occ_finish(const uint8_t* final_rc, uint64_t* out_tn, uint32_t flags) {
+  uint32_t n_cw = 0;
+  CR(occ_finish_prepare(final_rc, flags, n_cw));
+  return occ_finish_commit(n_cw, out_tn, flags);
+}
+
 // ---------------------------------------------------------------------------
-// Commit/kill round solver (occ_ck.hip) over level 0's survivors.  The key
-// table is sized for every access of the epoch at <= 50 % load (a list that
-// does not fit goes to the round solver) and kept clean between epochs by
-// k_final, so only a new, grown or abandoned table is filled here (before any
-// capture).
-static constexpr size_t CK_HCTL = 15360;  // ck counter ring copy inside `hmisc`
-int dcc_ctx::ck_reserve(const DevBatch& d) {
+// Dataflow solver (occ_dataflow.hip) over level 0's survivors.  Buffers are
+// sized for survivors of up to half the epoch's accesses (a larger list goes
+// to the round solver); the key table is kept clean between epochs by the
+// solver itself (each decided writer resets its key's slot), so only a new,
+// grown or abandoned table is filled here (before any capture).
+static constexpr size_t DF_HCTL = 15360;  // dataflow control copy inside `hmisc`
+int dcc_ctx::df_reserve(const DevBatch& d) {
   dcc_ctx* ctx = this;
-  uint32_t bits = 10;
-  while (bits < 30 && (1ull << bits) < std::max<uint64_t>(1024, d.nnz)) bits++;
+  const uint64_t cap_acc = std::max<uint64_t>(65536, d.nnz / 2);
+  uint32_t bits = DF_MIN_BITS;
+  while (bits < 31 && (1ull << bits) < cap_acc + cap_acc / 4) bits++;
   const uint64_t slots = 1ull << bits;
-  const void* old = ck_tab.p;
-  CR(ck_tab.ensure(this, slots * sizeof(CkSlot), "commit/kill key table"));
-  if (ck_tab.p != old) ck_clean = 0;
-  CR(ck_ctl.ensure(this, CK_CTL_WORDS * 4, "commit/kill control"));
-  CR(ck_aslot.ensure(this, std::max<uint64_t>(64, d.nnz * 4), "commit/kill access slots"));
-  for (DevBuf& l : ck_lst) CR(l.ensure(this, d.n * 4 + 64, "commit/kill lists"));
-  const uint64_t have = ck_tab.cap / sizeof(CkSlot);
-  ck_cap_bits = 0;
-  while ((2ull << ck_cap_bits) <= have) ck_cap_bits++;
-  if (ck_dirty || ck_clean < have) {
-    launch_ck_fill((CkSlot*)ck_tab.p, have, stream);
+  const void* old = df_tkey.p;
+  CR(df_ctl.ensure(this, sizeof(DfCtl), "dataflow control"));
+  CR(df_tkey.ensure(this, slots * 8, "dataflow key table"));
+  CR(df_tnw.ensure(this, slots * 4, "dataflow writer counts"));
+  CR(df_trec.ensure(this, slots * 16, "dataflow key records"));
+  if (df_tkey.p != old) df_clean = 0;
+  CR(df_tid.ensure(this, d.n * 4 + 64, "dataflow list txns"));
+  CR(df_aoff.ensure(this, d.n * 4 + 64, "dataflow list offsets"));
+  CR(df_cfirst.ensure(this, (cap_acc / 64 + 4) * 4, "dataflow chunks"));
+  CR(df_slot.ensure(this, cap_acc * 4 + 64, "dataflow access slots"));
+  CR(df_rank.ensure(this, cap_acc * 4 + 64, "dataflow access ranks"));
+  CR(df_x.ensure(this, cap_acc * 4 + 64, "dataflow access refs"));
+  CR(df_wtid.ensure(this, cap_acc * 4 + 64, "dataflow writer entries"));
+  CR(df_words.ensure(this, cap_acc * 8 + 64, "dataflow group words"));
+  uint64_t have = std::min<uint64_t>(df_tkey.cap / 8, df_tnw.cap / 4);
+  have = std::min<uint64_t>(have, df_trec.cap / 16);
+  df_max_bits = 0;
+  while ((2ull << df_max_bits) <= have) df_max_bits++;
+  df_cap_acc = std::min<uint64_t>({df_slot.cap / 4, df_rank.cap / 4, df_x.cap / 4, df_wtid.cap / 4,
+                                   df_words.cap / 8, (df_cfirst.cap / 4 - 4) * 64}) - 16;
+  df_cap_txn = std::min<uint64_t>(df_tid.cap / 4, df_aoff.cap / 4) - 16;
+  if (!df_grid) {
+    const int per = df_solve_blocks_per_cu();
+    df_grid = (unsigned)n_cu * (unsigned)std::max(1, std::min(per, 3));
+  }
+  if (const char* e = getenv("DCC_DF_LIMIT_US")) df_limit_ticks = strtoull(e, nullptr, 10) * 100ull;
+  if (df_dirty || df_clean < (1ull << df_max_bits)) {
+    const DfArgs a = df_args(d);
+    launch_df_clear(a, 1ull << df_max_bits, stream);
     CK(hipGetLastError());
-    ck_clean = have;
-    ck_dirty = false;
+    df_clean = 1ull << df_max_bits;
+    df_dirty = false;
   }
   return DCC_OK;
 }
 
-// build (round 1's inputs) and rounds [r0, r1] on the engine stream
-int dcc_ctx::ck_enqueue(const DevBatch& d, uint32_t r0, uint32_t r1, bool build) {
-  dcc_ctx* ctx = this;
-  (void)d;
-  SwLevel* ctl = (SwLevel*)sw_ctl.p;
-  const uint32_t L = ck_level;                  // the list the rounds decide:
-  const SubBufs& b = sw_list[(L - 1) & 1];      // level L-1's filter writes it here
-  CkArgs a{};
-  a.tid1 = (const uint32_t*)b.tid.p;
-  a.off1 = (const uint32_t*)b.off.p;
-  a.keys1 = (const uint64_t*)b.keys.p;
-  a.at1 = (const uint8_t*)b.acctype.p;
-  a.lv1 = ctl + L;
-  a.abandon = (const uint32_t*)(ctl + SW_MAX_LEVEL + 1);
-  a.abandon_out = (uint32_t*)(ctl + SW_MAX_LEVEL + 1);
-  a.abandon_level = L;
-  a.tab = (CkSlot*)ck_tab.p;
-  a.cap_bits = ck_cap_bits;
-  a.ctl = (uint32_t*)ck_ctl.p;
-  a.aslot = (uint32_t*)ck_aslot.p;
-  a.s1 = (uint32_t*)ck_lst[0].p;
+DfArgs dcc_ctx::df_args(const DevBatch& d) {
+  DfArgs a{};
+  a.ctl = (DfCtl*)df_ctl.p;
+  a.off = d.off;
+  a.keys = d.keys;
+  a.acctype = d.acctype;
+  a.nnz = d.nnz;
   a.state = (uint8_t*)state.p;
+  a.tkey = (uint64_t*)df_tkey.p;
+  a.tnw = (uint32_t*)df_tnw.p;
+  a.trec = (uint4*)df_trec.p;
+  a.max_bits = df_max_bits;
+  a.cap_acc = df_cap_acc;
+  a.cap_txn = df_cap_txn;
+  a.s_tid = (uint32_t*)df_tid.p;
+  a.s_aoff = (uint32_t*)df_aoff.p;
+  a.cfirst = (uint32_t*)df_cfirst.p;
+  a.s_slot = (uint32_t*)df_slot.p;
+  a.s_rank = (uint32_t*)df_rank.p;
+  a.s_x = (uint32_t*)df_x.p;
+  a.wtid = (uint32_t*)df_wtid.p;
+  a.words = (unsigned long long*)df_words.p;
+  a.abandon = (const uint32_t*)((SwLevel*)sw_ctl.p + SW_MAX_LEVEL + 1);
   a.err = (uint32_t*)misc.p;
-  // grid-stride over the list with the chip's resident capacity (8 workgroups
-  // of 256 per CU) while it is long: a group of 16 lanes per txn; later
-  // rounds decide a few thousand txns and mostly skip decided ones
-  if (build) launch_ck_build(a, (unsigned)n_cu * 8, stream);
-  for (uint32_t r = r0; r <= r1; r++)
-    launch_ck_round(a, r, r <= 2 ? (unsigned)n_cu * 8 : (unsigned)n_cu * 2, stream);
+  a.limit_ticks = df_limit_ticks;
+  return a;
+}
+
+int dcc_ctx::df_enqueue(const DevBatch& d) {
+  dcc_ctx* ctx = this;
+  const DfArgs a = df_args(d);
+  launch_df_alloc(a, stream);
+  launch_df_scatter(a, (unsigned)n_cu * 8, stream);
+  launch_df_solve(a, df_grid, stream);
   CK(hipGetLastError());
   return DCC_OK;
 }
@@ -772,11 +821,12 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   DevBatch d;
   CR(stage_batch(b, d));
   const bool sweep = use_sweep();
-  // level 0 of the sweep, then the commit/kill rounds (single GPU)
-  const bool ck = sweep && use_ck() && !sh;
-  ro_on = sweep && ro_split && !sh && !ck;
+  // level 0 of the sweep, then the dataflow solver (single GPU)
+  const bool df = sweep && use_df() && !sh;
+  df_on = df;
+  ro_on = sweep && ro_split && !sh && !df;
   if (sweep) CR(sweep_reserve(d));
-  if (ck) CR(ck_reserve(d));
+  if (df) CR(df_reserve(d));
   CR(state.ensure(this, d.n + 16, "state"));
   CR(hasw.ensure(this, d.n + 16, "hasw"));
   CR(rc.ensure(this, d.n + 16, "rc"));
@@ -797,7 +847,7 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   // read-only split, 4 without)
   const uint32_t glv = sw_levels ? sw_levels : (ro_on ? 3u : 4u);
   const GraphKey gkey{d.off, d.keys, d.acctype, d.n, d.nnz, out_rc, dev_out,
-                      ck ? 1000u + 100u * ck_level + ck_graph_rounds
+                      df ? 2000u + df_max_bits
                          : glv | (ro_on ? 0x80u | (wt_bits << 8) : 0u),
                       buf_gen};
   bool replay = graph_ok && graph_exec && gkey == graph_key;
@@ -850,6 +900,9 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
       fa.job[fa.n++] = FillJob{(uint32_t*)sw_gtab.p, (1ull << sw_gbits(0, ro_on)) * 2, 0xFFFFFFFFu};
       fa.job[fa.n++] = FillJob{(uint32_t*)sw_fw.p, 1ull << sw_gbits(0, ro_on), 0xFFFFFFFFu};
       fa.job[fa.n++] = FillJob{(uint32_t*)sw_fw.p + (1u << SW_GBITS_MAX), 1ull << sw_gbits(0, ro_on), 0u};
+      // the dataflow control words (a level 0 that decides the whole epoch
+      // never reaches k_df_list, so nothing may read a stale `live`)
+      if (df) fa.job[fa.n++] = FillJob{(uint32_t*)df_ctl.p, 16, 0u};
     }
     launch_fill(fa, stream);  // the sweep's prep runs inside its level-0 serial pass
   }
@@ -882,14 +935,14 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   int serial_tail = -1;  // level enqueued without its filter (sweep_enqueue tail_serial)
   if (sweep) {
     if (profiling) CK(hipEventRecord(pev[0], stream));
-    next_level = ck ? (int)ck_level : (int)std::min<uint32_t>(glv, SW_MAX_LEVEL - 1);
-    if (!sh && !ck && next_level >= 2) serial_tail = next_level - 1;
-    if (ck) ck_dirty = true;  // until k_final has reset the table's slots
+    next_level = df ? 1 : (int)std::min<uint32_t>(glv, SW_MAX_LEVEL - 1);
+    if (!sh && !df && next_level >= 2) serial_tail = next_level - 1;
+    if (df) df_dirty = true;  // until the solver has reset the table's slots
     if (sh) {
       CR(sweep_sharded(d, next_level));
     } else if (!replay) {
       CR(sweep_enqueue(d, 0, next_level, nullptr, false, serial_tail >= 0));
-      if (ck) CR(ck_enqueue(d, 1, ck_graph_rounds, true));
+      if (df) CR(df_enqueue(d));
       if (ro_on) CR(sweep_ro(d, false, false, 0));
     }
   } else {
@@ -901,9 +954,6 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   uint8_t* rc_dev = (dev_out && out_rc) ? out_rc : (uint8_t*)rc.p;
   uint32_t* cf = want_tn ? (uint32_t*)cflag.p : nullptr;
   uint64_t* tn_dev = want_tn ? ((dev_out && out_tn) ? out_tn : (uint64_t*)tn.p) : nullptr;
-  uint32_t ck_last = ck_graph_rounds;  // the last commit/kill round enqueued
-  SwLevel* const ctl_d = (SwLevel*)sw_ctl.p;
-  uint32_t* const ck_cnt_d = (uint32_t*)ck_ctl.p + CK_CTL_RING;
   auto enqueue_final = [&]() -> int {
     if (replay) {  // once: a second finalize (after more levels) runs directly
       replay = false;
@@ -923,16 +973,9 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
     job(hmisc_dev, misc.p, 64);
     job((char*)hmisc_dev + MISC_BARS, (char*)misc.p + MISC_BARS, CTR_RING * 16);
     if (sweep) job((char*)hmisc_dev + SW_HCTL, sw_ctl.p, sw_ctl_bytes());
-    if (ck) job((char*)hmisc_dev + CK_HCTL, ck_ctl.p, CK_CTL_WORDS * 4);
+    if (df) job((char*)hmisc_dev + DF_HCTL, df_ctl.p, 64);
     FinalArgs fa{d.n, (const uint8_t*)state.p, (const uint8_t*)hasw.p, rc_dev, cf,
                  (FinalPart*)hpart_dev};
-    if (ck) {
-      fa.ck_tab = (CkSlot*)ck_tab.p;
-      fa.ck_aslot = (const uint32_t*)ck_aslot.p;
-      fa.ck_acc = &ctl_d[ck_level].acc;
-      fa.ck_live = ck_cnt_d + (ck_last + 1) % CK_RING;
-      fa.ck_abandon = (const uint32_t*)(ctl_d + SW_MAX_LEVEL + 1);
-    }
     launch_final(fa, ga, stream);
     if (want_tn) launch_commit_tn(cf, d.n, (uint64_t*)bsum.p, tnc, tn_dev, stream);
     CK(hipGetLastError());
@@ -975,52 +1018,24 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
     if (maxlen > MAX_TXN_LEN)
       return fail(DCC_ERANGE, "batch: a txn has %u accesses (> MAX_ROW_PER_TXN=%u)", maxlen,
                   MAX_TXN_LEN);
-    // more levels, or hand the remaining list to the round solver
-    bool again = false, ro_fast_rerun = false;
-    uint32_t ck_rounds = 0;
-    bool ck_done = false;
-    if (ck) {
-      // the commit/kill rounds: the captured ones, then more in batches
-      // until the list is empty (unless level 0 or the build handed it off)
-      const SwLevel* hc = (const SwLevel*)((const char*)hmisc + SW_HCTL);
-      const uint32_t ab = *(const uint32_t*)(hc + SW_MAX_LEVEL + 1);
-      const uint32_t e = *(const uint32_t*)hmisc;
-      if (!ab && !(e & (ERR_SPIN | ERR_TILE | ERR_FULL))) {
-        ck_done = true;
-        // per-round live flags: round r ran on a non-empty list
-        const uint32_t* hcnt = (const uint32_t*)((const char*)hmisc + CK_HCTL) + CK_CTL_RING;
-        const uint32_t m1 = hc[ck_level].m;
-        auto count = [&](uint32_t r0, uint32_t r1) {  // rounds in [r0, r1] with a list
-          for (uint32_t r = r0; r <= r1; r++)
-            if (r == 1 ? m1 > 0 : hcnt[r % CK_RING] > 0) ck_rounds++;
-        };
-        uint32_t R = ck_graph_rounds;
-        count(1, R);
-        while (hcnt[(R + 1) % CK_RING]) {
-          const uint32_t B = 32;  // <= CK_RING - 2: the batch's flags stay intact
-          CR(ck_enqueue(d, R + 1, R + B, false));
-          GatherArgs ga{};
-          ga.job[ga.n++] = CopyJob{(const uint32_t*)ck_ctl.p,
-                                   (uint32_t*)((char*)hmisc_dev + CK_HCTL), CK_CTL_WORDS};
-          ga.job[ga.n++] = CopyJob{(const uint32_t*)misc.p, (uint32_t*)hmisc_dev, 16};
-          launch_gather(ga, stream);
-          CK(hipGetLastError());
-          CK(hipStreamSynchronize(stream));
-          count(R + 1, R + B);
-          R += B;
-          if (R > m1 + 2 * B) return fail(DCC_EIO, "commit/kill rounds did not converge");
-        }
-        if (R != ck_last) {
-          ck_last = R;
-          again = true;  // finalize again: the captured k_final ran before these rounds
-        }
-        // the next epoch captures one round more than this one needed (the
-        // last captured round then finds its list empty): a steady workload
-        // settles on a graph without host round trips or idle rounds
-        ck_graph_rounds = std::max<uint32_t>(4, std::min<uint32_t>(24, ck_rounds + 1));
+    // the dataflow solver gave up (its time limit, or a look-back that never
+    // completed): the epoch again with the sweep's levels; the table is
+    // cleaned before the next dataflow epoch
+    if (df) {
+      const DfCtl* hd = (const DfCtl*)((const char*)hmisc + DF_HCTL);
+      if (hd->err) {
+        df_dirty = true;
+        const int saved = solver;
+        solver = 3;
+        const int e = occ_epoch(b, out_rc, out_tn, st);
+        solver = saved;
+        if (st) st->fallback += 1;
+        return e;
       }
     }
-    for (; !ck_done;) {
+    // more levels, or hand the remaining list to the round solver
+    bool again = false, ro_fast_rerun = false;
+    for (;;) {
       const SwLevel* hc = (const SwLevel*)((const char*)hmisc + SW_HCTL);
       const uint32_t ab = *(const uint32_t*)(hc + SW_MAX_LEVEL + 1);
       const uint32_t e = *(const uint32_t*)hmisc;
@@ -1186,7 +1201,13 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
     info.prefix = hc[0].pos;
     info.survivors = hc[1].m;
     for (int l = 0; l < next_level && (l == 0 || hc[l].m); l++) rounds++;
-    rounds += ck_rounds;
+    if (df) {
+      const DfCtl* hd = (const DfCtl*)((const char*)hmisc + DF_HCTL);
+      if (hd->live) {
+        info.survivors = hd->m;
+        rounds++;
+      }
+    }
   }
 
   const uint32_t e = *(const uint32_t*)hmisc;
@@ -1212,7 +1233,7 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   }
   if (n_und) return fail(DCC_EIO, "%llu undecided transactions after convergence",
                          (unsigned long long)n_und);
-  if (ck) ck_dirty = false;  // k_final reset the slots (or the list never used them)
+  if (df) df_dirty = false;  // the solver reset the slots it used (or the list never used them)
   float ms = 0;
   CK(hipEventElapsedTime(&ms, ev0, ev1));
   S.rounds = rounds;

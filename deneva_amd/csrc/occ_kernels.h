@@ -7,7 +7,6 @@
 namespace dcc {
 
 struct Slot;
-struct CkSlot;
 
 constexpr int TILE_CAP = 1024;  // accesses staged per wave (LDS), build kernel
 constexpr int ROUND_CAP = 512;  // accesses staged per wave, round / publish kernels
@@ -123,13 +122,6 @@ struct FinalArgs {
   uint8_t* rc;
   uint32_t* cflag;
   FinalPart* part;  // [FINAL_BLOCKS] (pinned host memory: read back directly)
-  // commit/kill solver: reset the table slots its list used, once every
-  // round has run (ck_live: the undecided count after the last enqueued round)
-  struct CkSlot* ck_tab;
-  const uint32_t* ck_aslot;
-  const uint32_t* ck_acc;
-  const uint32_t* ck_live;
-  const uint32_t* ck_abandon;
 };
 
 // sub-list decisions back to the epoch's state bytes (round-solver hand-off)
@@ -402,7 +394,12 @@ void launch_sw_seq(const SwSeqArgs& a, hipStream_t st);
 void launch_sw_rows(const SwPreArgs& a, unsigned grid, hipStream_t st);
 void launch_sw_cout(const SwCoutArgs& a, unsigned grid, hipStream_t st);
 void launch_sw_filter(const SwFilterArgs& a, unsigned grid, hipStream_t st);
+// the level-0 compaction; with df.ctl set (the dataflow solver) it lists the
+// survivors by reference and builds the key table instead, unless the level
+// hands off to the round solver
+struct DfArgs;
 void launch_sw_compact(const SwFilterArgs& a, unsigned grid, hipStream_t st);
+void launch_df_list(const SwFilterArgs& a, const DfArgs& d, unsigned grid, hipStream_t st);
 void launch_sw_apply(const SwFilterArgs& a, unsigned grid, hipStream_t st);
 void launch_sw_share(const uint32_t* m_dev, uint32_t m_host, const uint32_t* abandon,
                      const uint32_t* off, uint32_t p_max, uint32_t rank, uint32_t* cnt,
@@ -413,42 +410,70 @@ void launch_sw_merge(const SwList& in, uint32_t P, uint32_t* xbuf, uint32_t xoff
                      uint32_t n_all, uint32_t* cnt, uint32_t* cur, uint32_t* moff,
                      uint64_t* mkeys, uint8_t* mat, bool export_only, hipStream_t st);
 
-// ---- commit/kill round solver over the level-0 survivors (occ_ck.hip)
-struct __attribute__((aligned(32))) CkSlot {
-  uint64_t key;   // KEY_EMPTY: free
-  uint32_t c;     // the key's committed writer (list position), ~0u: none
-  uint32_t pad;
-  uint64_t u[2];  // smallest undecided writer at the start of round r: u[r & 1]
+// ---- dataflow solver over the level-0 survivors (occ_dataflow.hip)
+// Level 0 of the sweep decides its serial prefix and kills every txn touching
+// its committed writes; the survivors (write and read-only txns, index order)
+// are then decided with no further levels: per write key, the list of its
+// writers (txn ids, any order) and one 64-bit word per 32 writers
+//   bits [0, 32)   writer s % 32 of the group is decided (commit or abort)
+//   bits [32, 64)  ~txn id of the group's committed writer (0: none yet)
+// A txn commits once, on each of its keys, every writer with a smaller id is
+// decided and none committed; it aborts once one of them committed.  Each
+// decision is one atomicOr of the writer's bit (with ~id on commit), so readers
+// learn decisions without barriers, rounds or levels.
+constexpr uint32_t DF_NONE = 0xFFFFFFFFu;  // s_slot: no list txn writes the key
+constexpr uint32_t DF_PEND = 0xFFFFFFFEu;  // s_slot after k_df_list: a read, looked up later
+constexpr uint32_t DF_SCAN_WG = 256;       // k_df_alloc workgroups (all resident)
+constexpr uint32_t DF_QW = 4;              // chunks in a solver wave's window
+constexpr uint32_t DF_MIN_BITS = 10;
+// control block (device; copied to the host with the epoch's read-back)
+struct DfCtl {
+  uint32_t m;        // survivors (list txns)
+  uint32_t acc;      // their accesses
+  uint32_t bits;     // key-table slots this epoch: 1 << bits
+  uint32_t nchunks;  // solver chunks: txns whose first access is in [64c, 64c + 64)
+  uint32_t live;     // 1: the dataflow path runs this epoch (0: nothing / hand-off)
+  uint32_t err;      // DF_E_* (the host falls back to the sweep levels)
+  uint32_t npos;     // writer entries (k_df_alloc)
+  uint32_t nwords;   // group words
+  uint32_t passes;   // the solver's most passes by one wave
+  uint32_t pad[7];
+  unsigned long long gran[DF_SCAN_WG];  // k_df_alloc look-back: flag << 63 | words << 32 | entries
 };
-constexpr uint32_t CK_WR = 0x80000000u;   // aslot: the access is a write
-constexpr uint32_t CK_NONE = 0x7FFFFFFFu; // aslot: no slot (reserved key)
-constexpr uint32_t CK_RING = 64;          // per-round list counters kept on the device
-constexpr uint32_t CK_CTL_MASK = 0;       // ctl word: the table's slot mask this epoch
-constexpr uint32_t CK_CTL_RING = 16;      // ctl words [16, 16 + CK_RING): per-round live flags
-constexpr uint32_t CK_CTL_WORDS = CK_CTL_RING + CK_RING;
-constexpr uint32_t CK_G = 16;             // lanes per txn (k_ck_build / k_ck_round)
-constexpr uint32_t CK_C = MAX_TXN_LEN / CK_G;  // accesses per lane
-struct CkArgs {
-  const uint32_t* tid1;   // the list (the survivors of the sweep's first levels, index
-                          // order): txn ids,
-  const uint32_t* off1;   // offsets (0-based), keys and access types
-  const uint64_t* keys1;
-  const uint8_t* at1;
-  const SwLevel* lv1;     // its length and access count (device)
+constexpr uint32_t DF_E_SPIN = 1, DF_E_SCAN = 2, DF_E_FULL = 4;
+struct DfArgs {
+  DfCtl* ctl;
+  const uint32_t* off;
+  const uint64_t* keys;
+  const uint8_t* acctype;
+  uint64_t nnz;
+  uint8_t* state;
+  // key table of the survivors' write keys (clean between epochs: the solver
+  // resets every slot it used)
+  uint64_t* tkey;    // [1 << max_bits] KEY_EMPTY
+  uint32_t* tnw;     // [1 << max_bits] writers per key, 0
+  uint4* trec;       // [1 << max_bits] {first entry, first word, writers, committed writer}
+  uint32_t max_bits;
+  uint64_t cap_acc;  // survivor accesses the per-access arrays hold
+  uint64_t cap_txn;
+  // the list (k_df_list)
+  uint32_t* s_tid;   // [m] txn id
+  uint32_t* s_aoff;  // [m + 1] first access (list access index)
+  uint32_t* cfirst;  // [nchunks + 1] first list txn of each chunk
+  uint32_t* s_slot;  // [acc] key slot (DF_NONE: no list writer)
+  uint32_t* s_rank;  // [acc] a write's rank among its key's writers (DF_NONE: a read)
+  uint32_t* s_x;     // [acc] writes: txn id; reads: batch access index
+  uint32_t* wtid;    // [npos] writer txn ids per key (k_df_scatter)
+  unsigned long long* words;  // [nwords]
   const uint32_t* abandon;
-  uint32_t* abandon_out;  // = abandon_level: the list goes to the fixed-point round solver
-  uint32_t abandon_level; // the list's level (level L-1's filter wrote it)
-  CkSlot* tab;            // [1 << cap_bits] clean slots
-  uint32_t cap_bits;
-  uint32_t* ctl;          // [CK_CTL_WORDS]
-  uint32_t* aslot;        // [list accesses] slot | CK_WR
-  uint32_t* s1;           // [list txns] state words by list position
-  uint8_t* state;         // the epoch's state bytes
   uint32_t* err;
+  uint64_t limit_ticks;  // the solver gives up after this long (s_memrealtime, 100 MHz)
 };
-void launch_ck_build(const CkArgs& a, unsigned grid, hipStream_t st);
-void launch_ck_round(const CkArgs& a, uint32_t r, unsigned grid, hipStream_t st);
-void launch_ck_fill(CkSlot* tab, uint64_t n, hipStream_t st);
+void launch_df_alloc(const DfArgs& a, hipStream_t st);
+void launch_df_scatter(const DfArgs& a, unsigned grid, hipStream_t st);
+void launch_df_solve(const DfArgs& a, unsigned grid, hipStream_t st);
+void launch_df_clear(const DfArgs& a, uint64_t slots, hipStream_t st);
+int df_solve_blocks_per_cu();  // resident k_df_solve workgroups per CU (occupancy query)
 
 // Several word fills in one launch (replaces a run of hipMemsetAsync calls,
 // each of which costs a dispatch and an idle gap on the stream).

@@ -736,20 +736,6 @@ __global__ __launch_bounds__(256) void k_final(FinalArgs a, GatherArgs g) {
     a.rc[t] = st == ST_COMMIT ? 0 /* RCOK */ : 2 /* Abort */;
     if (a.cflag) a.cflag[t] = f;
   }
-  // the commit/kill solver's table back to clean: every slot its list used
-  if (a.ck_tab && *a.ck_abandon == 0 && *a.ck_live == 0) {
-    const uint32_t acc = *a.ck_acc;
-    CkSlot cs;
-    cs.key = KEY_EMPTY;
-    cs.c = ~0u;
-    cs.pad = 0;
-    cs.u[0] = ~0ull;
-    cs.u[1] = ~0ull;
-    for (uint64_t x = tid; x < acc; x += stride) {
-      const uint32_t as = a.ck_aslot[x];
-      if (as != CK_NONE) a.ck_tab[as & ~CK_WR] = cs;
-    }
-  }
   const uint32_t s0 = block_sum_u32(c, sh), s1 = block_sum_u32(ab, sh),
                  s2 = block_sum_u32(ro, sh), s3 = block_sum_u32(cw, sh),
                  s4 = block_sum_u32(und, sh);

@@ -40,7 +40,7 @@ extern "C" {
 
 /* ------------------------------------------------------ reference enums */
 /* access_t, system/global.h:287  {RD, WR, XP, SCAN}.  OCC puts only WR into
- * the write set (concurrency_control/occ.cpp:379-383, get_rw_set); Calvin
+ * the write set (concurrency_control/occ.cpp:296-317, get_rw_set: `get_access_type(i) == WR`, line 308); Calvin
  * maps RD/SCAN to LOCK_SH and everything else to LOCK_EX (storage/row.cpp:191). */
 #define DCC_RD 0
 #define DCC_WR 1
@@ -159,14 +159,13 @@ int dcc_set_profiling(dcc_ctx* ctx, int enable);
 #define DCC_OPT_BATCH_MAX 2   /* max rounds enqueued between host synchronisations        */
 #define DCC_OPT_SOLVER 5      /* OCC solver: 0 auto (= 3), 1 fixed-point rounds only, 3 sweep
                                  (levels of serial passes + filters; hands lists that stop
-                                 shrinking to the round solver), 4 the sweep's first levels,
-                                 then commit/kill rounds over their survivors (single GPU)   */
+                                 shrinking to the round solver), 4 level 0 of the sweep, then
+                                 the dataflow solver over its survivors (single GPU; falls
+                                 back to 3 on its time limit)                                */
 #define DCC_OPT_SWEEP_LEVELS 6 /* sweep levels enqueued between host synchronisations (0:
                                   auto, 3 with DCC_OPT_RO_SPLIT, 4 without)                  */
 #define DCC_OPT_HIST_MERGE 7  /* device history: delta pairs above which the delta merges into
                                  the base (default 65536; the base/4 rule also applies)      */
-#define DCC_OPT_CK_LEVEL 9    /* solver 4: full sweep levels before the commit/kill rounds
-                                 (default 2)                                                 */
 #define DCC_OPT_RO_SPLIT 10   /* sweep: read-only txns that survive the first level's filter
                                  leave the level lists and are decided once every writer is
                                  (1, default) or stay in the lists (0); one-GPU epochs only.

@@ -152,3 +152,34 @@ def test_multi_rank_failure_does_not_hang(bad_rank):
         g, crc, _, _ = eng.calvin_order_epoch(c, want_group=True)
         assert np.array_equal(np.asarray(g).astype(np.uint32), eg)
         assert np.array_equal(np.asarray(crc), ecrc)
+
+
+@pytest.mark.parametrize("fault", ["decreasing", "first", "last", "too_long"])
+def test_multi_rejects_malformed_device_batch(fault):
+    """A malformed device batch is rejected by every rank before any exchange
+    (rank 0 validates the caller's arrays; the shards' own offsets are always
+    well formed, so no rank could notice alone); the context stays usable."""
+    import torch
+    b = d.gen_ycsb(n_txn=4096, zipf_theta=0.9, table_size=1 << 14)
+    off = np.asarray(b.offsets, np.uint32).copy()
+    keys, at = np.asarray(b.keys), np.asarray(b.acctype)
+    if fault == "decreasing":
+        off[100] = off[99] - 1
+    elif fault == "first":
+        off[0] = 1
+    elif fault == "last":
+        off[-1] = off[-1] - 3
+    else:  # one txn of 80 accesses (> MAX_ROW_PER_TXN)
+        off = np.concatenate([[0], np.arange(80, keys.size + 1, 16, dtype=np.int64)])
+        off[-1] = keys.size
+        off = off.astype(np.uint32)
+    bad = d.EpochBatch(off, keys, at).to_torch("cuda:0")
+    erc, _, _ = orc.occ(b)
+    with d.Engine(devices=[0, 0, 0]) as eng:
+        with pytest.raises(d.DccError):
+            eng.occ_validate_epoch(bad)
+        with pytest.raises(d.DccError):
+            eng.calvin_order_epoch(bad, want_group=True)
+        rc, _, _ = eng.occ_validate_epoch(b.to_torch("cuda:0"))
+        torch.cuda.synchronize()
+        assert np.array_equal(rc.cpu().numpy(), erc)

@@ -57,7 +57,7 @@ def test_empty_batch(engine):
 def test_empty_and_readonly_txns(engine):
     b = make_batch([[], [(5, RD)], [], [(5, WR)], [(5, RD)], [], [(5, SCAN), (6, XP)]])
     rc, _ = run(engine, b)
-    # XP is not WR: the last txn is read-only for OCC (occ.cpp:379-383)
+    # XP is not WR: the last txn is read-only for OCC (get_rw_set, occ.cpp:296-317: only WR joins the write set)
     assert list(rc) == [0, 0, 0, 0, 2, 0, 2]
 
 

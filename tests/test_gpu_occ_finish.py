@@ -183,3 +183,34 @@ def test_sharded_context(eng):
         rc2, _, _ = m.occ_validate_epoch(b2)
         erc2, _, _ = orc.occ(b2, hist_keys=hk, hist_tn=ht, tnc=etnc)
         assert np.array_equal(np.asarray(rc2), erc2)
+
+
+def test_sharded_device_batch_calvin_between(eng):
+    # a device batch on a key-sharded context: each rank's shard lives in the
+    # context's own buffers, which the Calvin epoch run between the deferred
+    # validate and the finish rewrites -- the finish must still append the
+    # validated epoch's writes (the shard is kept aside), not the Calvin batch's
+    import torch
+    rng = np.random.default_rng(23)
+    b = random_batch(rng, 20000, 10, 4000, p_write=0.4)
+    c = d.gen_ycsb(n_txn=30000, zipf_theta=0.9, part_cnt=4, chunk_txns=4096, seed=77)
+    with d.Engine(devices=[0, 0, 0]) as m:
+        rc, _, _ = m.occ_validate_epoch(b.to_torch("cuda:0"), defer_finish=True)
+        torch.cuda.synchronize()
+        rc = rc.cpu().numpy()
+        erc, _, _ = orc.occ(b)
+        assert np.array_equal(rc, erc)
+        g, crc, _, _ = m.calvin_order_epoch(c, want_group=True)
+        eg, ecrc, _ = orc.calvin(c)
+        assert np.array_equal(np.asarray(g).astype(np.uint32), eg)
+        gl = global_rc(rc, rng, 0.25)
+        tn = m.occ_finish_epoch(gl)
+        etn, hk, ht, etnc = expected_finish(b, gl, 0)
+        assert np.array_equal(np.asarray(tn).astype(np.uint64), etn)
+        # the history holds b's committed writes: a later epoch's window sees them
+        b2 = random_batch(rng, 20000, 8, 4000, p_write=0.3)
+        b2.start_tn = np.zeros(b2.n_txn, np.uint64)
+        b2.finish_tn = np.full(b2.n_txn, etnc, np.uint64)
+        rc2, _, _ = m.occ_validate_epoch(b2)
+        erc2, _, _ = orc.occ(b2, hist_keys=hk, hist_tn=ht, tnc=etnc)
+        assert np.array_equal(np.asarray(rc2), erc2)

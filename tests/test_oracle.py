@@ -41,7 +41,7 @@ def test_kat_write_write_conflict():
 
 
 def test_kat_xp_and_scan_are_reads():
-    # get_rw_set puts every non-WR access into the read set (occ.cpp:379-383)
+    # get_rw_set puts every non-WR access into the read set (occ.cpp:296-317)
     rc, tn, _ = both(make_batch([[(7, XP)], [(7, WR)], [(7, SCAN)], [(7, XP)]]))
     assert list(rc) == [0, 0, 2, 2]
     assert list(tn) == [0, 1, 0, 0]
