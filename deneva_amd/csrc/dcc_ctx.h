@@ -90,12 +90,13 @@ struct dcc_ctx {
   bool use_sweep() const { return solver != 1; }
   bool use_df() const { return solver == 4; }
   bool df_on = false;             // this epoch: level 0's compaction launch is k_df_list
-  uint64_t df_clean = 0;          // dataflow key-table slots known clean
-  bool df_dirty = false;          // an epoch stopped before its solver reset the slots it used
-  uint32_t df_max_bits = 0;       // dataflow key table: 1 << df_max_bits slots allocated
+  uint64_t df_clean = 0;          // dataflow bucket counts known zero
+  bool df_dirty = false;          // an epoch stopped before k_df_alloc cleared the counts
+  uint32_t df_max_bits = 0;       // dataflow buckets: 1 << df_max_bits allocated
   uint64_t df_cap_acc = 0, df_cap_txn = 0;
   uint32_t df_grid = 0;           // k_df_solve workgroups (all resident)
   uint64_t df_limit_ticks = 50000000;  // the solver's time limit (0.5 s; DCC_DF_LIMIT_US)
+  bool df_debug = false;          // DCC_DF_DEBUG: per-wave stamps of the solver (no graph)
   bool ro_split = true;           // DCC_OPT_RO_SPLIT
   bool ro_on = false;             // this epoch splits read-only txns off (sweep, one GPU)
   uint32_t wt_bits = 18;          // committed-writer table slots (WT_BITS_DEFAULT; grows after an overflow)
@@ -152,8 +153,9 @@ struct dcc_ctx {
                                                         // list, writer tables, committed writers
   DevBuf sw_xcnt, sw_xsend, sw_xrec, sw_mcnt, sw_moff, sw_mkeys, sw_mat, sw_kill;  // key-sharded sweep  // sweep tile records
   SubBufs sw_list[2];                            // sweep level lists (ping-pong)
-  DevBuf df_ctl, df_tkey, df_tnw, df_trec;       // dataflow solver: control, key table
-  DevBuf df_tid, df_aoff, df_cfirst, df_slot, df_rank, df_x, df_wtid, df_words;  // list, entries
+  DevBuf df_ctl, df_bcnt, df_bcur, df_brec, df_ent, df_words;  // dataflow solver: buckets, entries
+  DevBuf df_tid, df_aoff, df_cfirst, df_x, df_pub, df_rx, df_rt;  // write list, read-only list
+  DevBuf df_dbg;
   DevBuf l_tid[2], l_coff[2], l_cent[2];         // ping-pong undecided lists
   // OCC history (occ.h:62-64) on the device: base + delta levels
   HistStore hs[2];

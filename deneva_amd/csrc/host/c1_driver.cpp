@@ -220,7 +220,7 @@ int main(int argc, char** argv) {
     device_ms = s.device_ms;
   } else {
     // each worker is an origin node; an epoch is every worker's next chunk
-    CalvinEpoch cal(ctx);
+    CalvinEpoch cal(ctx, c.capture);
     const uint64_t chunk = std::max<uint64_t>(1, c.epoch_max / (uint64_t)c.threads);
     for (uint64_t base = 0; base < c.txns && !failed; base += chunk) {
       std::vector<std::thread> ws;
@@ -241,6 +241,7 @@ int main(int argc, char** argv) {
         failed = 1;
         break;
       }
+      if (r.capture_err) fprintf(stderr, "calvin capture: .dccb write failed\n");
       for (uint8_t x : r.rc) (x == DCC_RC_RCOK ? ready : waits)++;
       epochs++;
       device_ms += r.stats.device_ms;

@@ -13,7 +13,9 @@
 #pragma once
 
 #include <cstdint>
+#include <cstdio>
 #include <mutex>
+#include <string>
 #include <vector>
 
 #include "dcc.h"
@@ -27,11 +29,19 @@ class CalvinEpoch {
     std::vector<uint32_t> origin, seq;  // per txn of the epoch, submission order
     std::vector<uint8_t> rc;            // DCC_RC_RCOK / DCC_RC_WAIT
     std::vector<uint32_t> wave;
+    std::vector<uint32_t> group;        // grant group per request (capture only)
     dcc_stats stats{};
     int err = 0;
+    bool capture_err = false;           // the .dccb write failed (decisions unaffected)
   };
 
-  explicit CalvinEpoch(dcc_ctx* ctx) : ctx_(ctx) { off_.push_back(0); }
+  // capture_dir: every closed epoch is written as a .dccb file (batch in
+  // submission order with the sequencer order, grant groups, readiness and
+  // wave levels) for offline parity checks against the Row_lock replay
+  explicit CalvinEpoch(dcc_ctx* ctx, std::string capture_dir = "")
+      : ctx_(ctx), capture_(std::move(capture_dir)) {
+    off_.push_back(0);
+  }
 
   // Sequencer::process_txn: the txn joins its origin's FIFO for this epoch.
   void submit(uint32_t origin, const Access* acc, size_t n) {
@@ -62,7 +72,21 @@ class CalvinEpoch {
     b.keys = keys_.data();
     b.acctype = at_.data();
     b.order = order.data();
-    if (n) r.err = dcc_calvin_order_epoch(ctx_, &b, nullptr, r.rc.data(), r.wave.data(), &r.stats);
+    const bool cap = !capture_.empty();
+    if (cap) r.group.assign(b.nnz ? b.nnz : 1, 0);
+    if (n)
+      r.err = dcc_calvin_order_epoch(ctx_, &b, cap ? r.group.data() : nullptr, r.rc.data(), r.wave.data(),
+                                     &r.stats);
+    if (n && cap && !r.err) {
+      dcc_file_info fi{};
+      fi.kind = DCC_FILE_CALVIN;
+      fi.epoch = epoch_;
+      char path[4096];
+      snprintf(path, sizeof path, "%s/calvin_%06llu.dccb", capture_.c_str(), (unsigned long long)epoch_);
+      r.capture_err =
+          dcc_file_write(path, &fi, &b, r.rc.data(), nullptr, r.group.data(), r.wave.data()) != DCC_OK;
+    }
+    epoch_++;
     r.origin.swap(origin_);
     r.seq.swap(seq_);
     off_.assign(1, 0);
@@ -74,6 +98,8 @@ class CalvinEpoch {
 
  private:
   dcc_ctx* ctx_;
+  std::string capture_;
+  uint64_t epoch_ = 0;
   std::mutex mu_;
   std::vector<uint32_t> off_, origin_, seq_, next_seq_;
   std::vector<uint64_t> keys_;

@@ -15,25 +15,28 @@
 // commits when all its keys are clear.  The survivors of level 0 touch no key
 // level 0 committed, so only list txns matter.
 //
-//   k_df_list     (the level-0 compaction launch, occ_sweep.hip) the
-//                 survivors by reference -- txn ids and access offsets into the
-//                 batch's CSR, no keys copied -- and every write key entered in
-//                 the table (tkey), its writers counted (tnw: the write's rank)
-//   k_df_alloc    one exclusive scan over the table (decoupled look-back, one
-//                 workgroup per CU, all resident): each key's writer entries and
-//                 group words (one 64-bit word per 32 writers)
-//   k_df_scatter  writers' txn ids into their key's entries; reads find their
-//                 key's slot (a key no list txn writes cannot conflict)
-//   k_df_solve    persistent: each wave keeps a window of chunks (the txns whose
-//                 first access lies in a 64-access window of the list), a lane
-//                 per access.  An access's relevant writers are a mask over its
-//                 key's group words (writers with a smaller txn id); it polls
-//                 the word until the mask is all decided or a committed writer
-//                 shows.  A decided txn ORs its bit into each of its write
-//                 keys' words (with ~txn id on commit): one atomic per write,
+//   k_df_list     (the level-0 compaction launch, occ_sweep.hip) the write and
+//                 the read-only survivors as two lists by reference -- txn ids
+//                 and batch access indices, no keys copied -- and one count per
+//                 write access into its key's hash bucket (no key table: a
+//                 bucket holds the writes of every key hashing to it)
+//   k_df_alloc    one exclusive scan over the buckets (decoupled look-back, one
+//                 workgroup per CU, all resident): each bucket's entries and
+//                 group words; the counts are cleared for the next epoch
+//   k_df_scatter  each write access becomes an entry {key, txn id} of its
+//                 bucket (a cursor per bucket) and learns its word and bit
+//   k_df_solve    persistent: each wave keeps a window of chunks (the write
+//                 txns whose first access lies in a 64-access window of the
+//                 list), a lane per access.  An access's relevant writers are a
+//                 mask over its bucket's group words (entries of its key with a
+//                 smaller txn id); it polls the word until the mask is all
+//                 decided or a committed entry shows.  A decided txn ORs its
+//                 bits into each of its writes' words: one atomic per write,
 //                 seen by every later accessor.  The smallest undecided txn can
 //                 always decide and its wave is resident, so the solver drains;
 //                 a time limit hands a pathological epoch back to the levels.
+//   k_df_ro       the read-only survivors: one with a committed entry of one
+//                 of its keys with a smaller txn id aborts.
 #include <hip/hip_runtime.h>
 
 #include "dcc_device.h"
@@ -77,38 +80,37 @@ __device__ inline void df_block_scan2(uint32_t p, uint32_t w, uint32_t& ep, uint
   __syncthreads();
 }
 
-// k_df_alloc: the table's writer counts -> each key's first entry and first
-// group word (slot order).  DF_SCAN_WG workgroups, one per CU: each scans its
-// slot range, publishes its total, and sums the totals of the workgroups
-// before it (they are all resident, so the look-back is one round trip).
+// k_df_alloc: bucket counts -> each bucket's first entry and first group word.
+// DF_SCAN_WG workgroups, one per CU: each sums its bucket range (coalesced,
+// bucket lo + 256 k + thread), publishes its total, sums the totals of the
+// workgroups before it (all resident: the look-back is one round trip), then
+// assigns its buckets in the same order, 256 per step.  The order of
+// allocation is free: a bucket only needs a contiguous range.
 __global__ __launch_bounds__(256) void k_df_alloc(DfArgs d) {
   __shared__ uint32_t sh[8];
-  __shared__ uint32_t s_base[2];
   DfCtl* c = d.ctl;
-  if (!c->live) return;
+  if (!c->live || !c->m) return;
+  const uint32_t t = threadIdx.x;
   const uint32_t bits = c->bits;
-  const uint64_t cap = 1ull << bits;
-  const uint64_t per = cap / DF_SCAN_WG;  // cap >= 2^DF_MIN_BITS
-  const uint64_t lo = (uint64_t)blockIdx.x * per;
-  const uint32_t T = (uint32_t)((per + 255) / 256);
-  const uint64_t s0 = min(lo + (uint64_t)threadIdx.x * T, lo + per), s1 = min(s0 + T, lo + per);
+  const uint32_t per = (1u << bits) / DF_SCAN_WG;  // 2^bits >= 2^DF_MIN_BITS
+  const uint32_t lo = blockIdx.x * per;
   uint32_t np = 0, nw = 0;
-  for (uint64_t q = s0; q < s1; q++) {
-    const uint32_t v = d.tnw[q];
+  for (uint32_t k = t; k < per; k += 256) {
+    const uint32_t v = d.bcnt[lo + k];
     np += v;
     nw += (v + 31u) / 32u;
   }
   uint32_t ep, ew, tp, tw;
   df_block_scan2(np, nw, ep, ew, tp, tw, sh);
-  if (threadIdx.x == 0)
+  if (t == 0)
     __hip_atomic_store(&c->gran[blockIdx.x], (1ull << 63) | ((unsigned long long)tw << 32) | tp,
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // look-back: thread t < blockIdx.x waits for workgroup t's total
   uint32_t gp = 0, gw = 0;
-  if (threadIdx.x < blockIdx.x) {
+  if (t < blockIdx.x) {
     unsigned long long g = 0;
     for (uint32_t spin = 0;; spin++) {
-      g = __hip_atomic_load(&c->gran[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      g = __hip_atomic_load(&c->gran[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (g >> 63) break;
       if (spin > (1u << 22)) {  // a predecessor never ran (not resident): give up
         atomicOr(&c->err, DF_E_SCAN);
@@ -123,43 +125,47 @@ __global__ __launch_bounds__(256) void k_df_alloc(DfArgs d) {
   df_block_scan2(gp, gw, bp_, bw_, tbp, tbw, sh);
   (void)bp_;
   (void)bw_;
-  if (threadIdx.x == 0) {
-    s_base[0] = tbp;
-    s_base[1] = tbw;
-    if (blockIdx.x == DF_SCAN_WG - 1) {
-      c->npos = tbp + tp;
-      c->nwords = tbw + tw;
-      // group words are addressed by 27 bits in the solver
-      if (tbw + tw >= (1u << 27)) atomicOr(&c->err, DF_E_FULL);
-    }
+  if (t == 0 && blockIdx.x == DF_SCAN_WG - 1) {
+    c->nent = tbp + tp;
+    c->nwords = tbw + tw;
+    // group words are addressed by 27 bits in the solver
+    if (tbw + tw >= (1u << 27)) atomicOr(&c->err, DF_E_FULL);
   }
-  __syncthreads();
-  uint32_t rp = s_base[0] + ep, rw = s_base[1] + ew;
-  for (uint64_t q = s0; q < s1; q++) {
-    const uint32_t v = d.tnw[q];
-    if (!v) continue;
+  uint32_t rp = tbp, rw = tbw;
+  for (uint32_t k0 = 0; k0 < per; k0 += 256) {  // uniform trip count
+    const uint32_t q = lo + k0 + t;
+    const uint32_t v = k0 + t < per ? d.bcnt[q] : 0u;
     const uint32_t ng = (v + 31u) / 32u;
-    d.trec[q] = make_uint4(rp, rw, v, ~0u);
-    for (uint32_t k = 0; k < ng; k++) d.words[rw + k] = 0ull;
-    rp += v;
-    rw += ng;
+    uint32_t xp, xw, sp, sw;
+    df_block_scan2(v, ng, xp, xw, sp, sw, sh);
+    if (k0 + t < per) {
+      const uint32_t seg = rp + xp, gb = rw + xw;
+      d.brec[q] = make_uint4(seg, gb, v, 0u);
+      d.bcur[q] = seg;
+      for (uint32_t g = 0; g < ng; g++) d.words[gb + g] = 0ull;
+      if (v) d.bcnt[q] = 0u;  // clean for the next epoch
+    }
+    rp += sp;
+    rw += sw;
   }
 }
 
-// k_df_scatter: every list access -- a write's txn id into its key's writer
-// entries; a read's key slot (DF_NONE: no list txn writes the key)
+// k_df_scatter: each write access of the list becomes an entry of its bucket
+// and learns its group word and bit (s_pub)
 __global__ __launch_bounds__(256) void k_df_scatter(DfArgs d) {
   DfCtl* c = d.ctl;
-  if (!c->live) return;
+  if (!c->live || !c->m) return;
   const uint32_t acc = c->acc, bits = c->bits;
   for (uint32_t a = blockIdx.x * 256 + threadIdx.x; a < acc; a += gridDim.x * 256) {
-    const uint32_t sl = d.s_slot[a];
-    if (sl == DF_PEND) {
-      d.s_slot[a] = df_find(d.tkey, bits, d.keys[d.s_x[a]]);
-    } else if (sl != DF_NONE) {
-      const uint32_t r = d.s_rank[a];
-      d.wtid[d.trec[sl].x + r] = d.s_x[a];
-    }
+    const uint32_t tid = d.s_pub[a];
+    if (tid == DF_NONE) continue;  // a read
+    const uint64_t key = d.keys[d.s_x[a]];
+    const uint32_t b = df_bucket(key, bits);
+    const uint32_t pos = atomicAdd(&d.bcur[b], 1u);
+    const uint4 r = d.brec[b];
+    const uint32_t j = pos - r.x;
+    d.ent[pos] = make_uint4((uint32_t)key, (uint32_t)(key >> 32), tid, 0u);
+    d.s_pub[a] = ((r.y + j / 32u) << 5) | (j & 31u);
   }
 }
 
@@ -168,27 +174,30 @@ __global__ __launch_bounds__(256) void k_df_scatter(DfArgs d) {
 // holds the txns whose first access is in a 64-access window, so at most 127
 // accesses) the wave keeps six words in LDS (struct of arrays):
 constexpr uint32_t DF_F = 6;
-enum : uint32_t { F_TID = 0, F_WORD = 1, F_MASK = 2, F_INFO = 3, F_PUB = 4, F_SLOT = 5 };
+enum : uint32_t { F_TID = 0, F_WORD = 1, F_MASK = 2, F_INFO = 3, F_PUB = 4, F_BX = 5 };
 // F_INFO: txn's lane-slots [x0, x1) | flags | group
 constexpr uint32_t I_LIVE = 1u << 16;   // the lane-slot holds an access
-constexpr uint32_t I_DONE = 1u << 17;   // every relevant writer decided, none committed
-constexpr uint32_t I_MULTI = 1u << 18;  // the key has > 32 writers (groups, committed-writer word)
+constexpr uint32_t I_DONE = 1u << 17;   // every relevant entry decided, none committed
 constexpr uint32_t I_FIN = 1u << 19;    // the txn is decided
 constexpr uint32_t I_GSHIFT = 20;       // current group (12 bits)
 constexpr uint32_t DF_MAX_GROUPS = 1u << 12;
 
-// relevant-writer mask of a group: entries with a smaller txn id
-__device__ inline uint32_t df_mask(const uint32_t* e, uint32_t cnt, uint32_t tid) {
+// relevant-entry mask of a group: entries of the key with a smaller txn id
+__device__ inline uint32_t df_mask(const uint4* e, uint32_t cnt, uint64_t key, uint32_t tid) {
   uint32_t m = 0;
-#pragma unroll 8
-  for (uint32_t j = 0; j < cnt; j++) m |= (e[j] < tid ? 1u : 0u) << j;
+#pragma unroll 4
+  for (uint32_t j = 0; j < cnt; j++) {
+    const uint4 v = e[j];
+    m |= ((((uint64_t)v.y << 32) | v.x) == key && v.z < tid ? 1u : 0u) << j;
+  }
   return m;
 }
-// first group >= g with a relevant writer; false: none left (the key is clear)
-__device__ inline bool df_group(const DfArgs& d, uint4 r, uint32_t tid, uint32_t& g, uint32_t& m) {
+// first group >= g with a relevant entry; false: none left (the key is clear)
+__device__ inline bool df_group(const DfArgs& d, uint4 r, uint64_t key, uint32_t tid, uint32_t& g,
+                                uint32_t& m) {
   const uint32_t ng = (r.z + 31u) / 32u;
   for (; g < ng; g++) {
-    m = df_mask(d.wtid + r.x + 32u * g, min(32u, r.z - 32u * g), tid);
+    m = df_mask(d.ent + r.x + 32u * g, min(32u, r.z - 32u * g), key, tid);
     if (m) return true;
   }
   return false;
@@ -198,8 +207,8 @@ __global__ __launch_bounds__(256) void k_df_solve(DfArgs d) {
   __shared__ uint32_t ls[4][DF_QW][DF_F][128];
   const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
   DfCtl* c = d.ctl;
-  if (!c->live) return;
-  const uint32_t nch = c->nchunks;
+  if (!c->live || !c->m) return;
+  const uint32_t nch = c->nchunks, bits = c->bits;
   const uint32_t W = gridDim.x * 4, wid = blockIdx.x * 4 + wv;
   uint32_t (*L)[DF_F][128] = ls[wv];
   uint32_t cid[DF_QW];
@@ -207,7 +216,9 @@ __global__ __launch_bounds__(256) void k_df_solve(DfArgs d) {
   for (uint32_t w = 0; w < DF_QW; w++) cid[w] = DF_NONE;
   uint32_t next = wid;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  uint32_t passes = 0;
+  uint32_t passes = 0, refills = 0, polls = 0;
+  uint64_t t_ready = 0;
+  unsigned long long* dbg = (d.dbg && wid < DF_DBG_WAVES) ? d.dbg + 8 * wid : nullptr;
   bool bail = false;
   for (;;) {
     // ---- refill empty window slots (their loads overlap)
@@ -217,6 +228,7 @@ __global__ __launch_bounds__(256) void k_df_solve(DfArgs d) {
       if (cid[w] == DF_NONE && next < nch) {
         cid[w] = next;
         next += W;
+        refills++;
         const uint32_t ch = cid[w];
         const uint32_t p0 = d.cfirst[ch], p1 = d.cfirst[ch + 1];
         const uint32_t nt = p1 - p0;
@@ -239,28 +251,23 @@ __global__ __launch_bounds__(256) void k_df_solve(DfArgs d) {
           const uint32_t x1 = l + 1 < nt ? x1n : na;
           const uint32_t tid = __shfl(tt, l);
           const bool live = x < na;
-          uint32_t info = 0, word = 0, mask = 0, pub = DF_NONE, slot = DF_NONE;
+          uint32_t info = 0, word = 0, mask = 0, pub = DF_NONE, bx = 0;
           if (live) {
             info = x0 | (x1 << 8) | I_LIVE;
-            slot = d.s_slot[a0 + x];
-            const uint32_t rk = d.s_rank[a0 + x];
-            if (slot == DF_NONE) {
+            bx = d.s_x[a0 + x];
+            pub = d.s_pub[a0 + x];
+            const uint64_t key = d.keys[bx];
+            const uint4 r = d.brec[df_bucket(key, bits)];
+            uint32_t g = 0, m = 0;
+            if ((r.z + 31u) / 32u > DF_MAX_GROUPS) {
+              atomicOr(&c->err, DF_E_FULL);
               info |= I_DONE;
+            } else if (df_group(d, r, key, tid, g, m)) {
+              word = r.y + g;
+              mask = m;
+              info |= g << I_GSHIFT;
             } else {
-              const uint4 r = d.trec[slot];
-              if (rk != DF_NONE) pub = ((r.y + rk / 32u) << 5) | (rk & 31u);
-              if (r.z > 32u) info |= I_MULTI;
-              uint32_t g = 0, m = 0;
-              if ((r.z + 31u) / 32u > DF_MAX_GROUPS) {
-                atomicOr(&c->err, DF_E_FULL);
-                info |= I_DONE;
-              } else if (df_group(d, r, tid, g, m)) {
-                word = r.y + g;
-                mask = m;
-                info |= g << I_GSHIFT;
-              } else {
-                info |= I_DONE;
-              }
+              info |= I_DONE;
             }
           }
           L[w][F_TID][x] = tid;
@@ -268,32 +275,28 @@ __global__ __launch_bounds__(256) void k_df_solve(DfArgs d) {
           L[w][F_MASK][x] = mask;
           L[w][F_INFO][x] = info;
           L[w][F_PUB][x] = pub;
-          L[w][F_SLOT][x] = slot;
+          L[w][F_BX][x] = bx;
         }
       }
       any |= cid[w] != DF_NONE;
     }
     if (!any || bail) break;
-    // ---- poll: every pending access's group word (and, for keys with more
-    // than 32 writers, the committed-writer word), all in flight together
+    if (dbg && !t_ready) t_ready = __builtin_amdgcn_s_memrealtime();
+    // ---- poll every pending access's group word, all in flight together
     unsigned long long pv[DF_QW][2];
-    uint32_t cw[DF_QW][2];
 #pragma unroll
     for (uint32_t w = 0; w < DF_QW; w++)
 #pragma unroll
       for (uint32_t k = 0; k < 2; k++) {
         pv[w][k] = 0;
-        cw[w][k] = ~0u;
         if (cid[w] == DF_NONE) continue;
         const uint32_t x = lane + 64 * k;
         const uint32_t info = L[w][F_INFO][x];
         if ((info & (I_LIVE | I_DONE | I_FIN)) != I_LIVE) continue;
         pv[w][k] = __hip_atomic_load(&d.words[L[w][F_WORD][x]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (info & I_MULTI)
-          cw[w][k] = __hip_atomic_load(&d.trec[L[w][F_SLOT][x]].w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        polls++;
       }
     // ---- evaluate
-    bool progress = false;
 #pragma unroll
     for (uint32_t w = 0; w < DF_QW; w++) {
       if (cid[w] == DF_NONE) continue;
@@ -304,30 +307,23 @@ __global__ __launch_bounds__(256) void k_df_solve(DfArgs d) {
         uint32_t info = L[w][F_INFO][x];
         kill[k] = false;
         if ((info & (I_LIVE | I_DONE | I_FIN)) == I_LIVE) {
-          const uint32_t tid = L[w][F_TID][x];
           const unsigned long long v = pv[w][k];
-          const uint32_t hi = (uint32_t)(v >> 32);
-          if ((hi && ~hi < tid) || cw[w][k] < tid) {
+          const uint32_t m = L[w][F_MASK][x];
+          if ((uint32_t)(v >> 32) & m) {  // a committed entry of the key precedes the txn
             kill[k] = true;
-          } else {
-            const uint32_t m = L[w][F_MASK][x];
-            if (((uint32_t)v & m) == m) {  // this group is clear: the next one
-              uint32_t g = (info >> I_GSHIFT) + 1u, nm = 0;
-              bool more = false;
-              uint4 r = make_uint4(0, 0, 0, 0);
-              if (info & I_MULTI) {
-                r = d.trec[L[w][F_SLOT][x]];
-                more = df_group(d, r, tid, g, nm);
-              }
-              if (more) {
-                L[w][F_WORD][x] = r.y + g;
-                L[w][F_MASK][x] = nm;
-                info = (info & ((1u << I_GSHIFT) - 1u)) | (g << I_GSHIFT);
-              } else {
-                info |= I_DONE;
-              }
-              L[w][F_INFO][x] = info;
+          } else if (((uint32_t)v & m) == m) {  // this group is clear: the next one
+            const uint32_t tid = L[w][F_TID][x];
+            const uint64_t key = d.keys[L[w][F_BX][x]];
+            const uint4 r = d.brec[df_bucket(key, bits)];
+            uint32_t g = (info >> I_GSHIFT) + 1u, nm = 0;
+            if (df_group(d, r, key, tid, g, nm)) {
+              L[w][F_WORD][x] = r.y + g;
+              L[w][F_MASK][x] = nm;
+              info = (info & ((1u << I_GSHIFT) - 1u)) | (g << I_GSHIFT);
+            } else {
+              info |= I_DONE;
             }
+            L[w][F_INFO][x] = info;
           }
         }
         done[k] = (info & I_DONE) != 0;
@@ -350,23 +346,15 @@ __global__ __launch_bounds__(256) void k_df_solve(DfArgs d) {
           const bool td = (D0 & R0) == R0 && (D1 & R1) == R1;
           if (tk || td) {
             const bool commit = !tk;
-            const uint32_t tid = L[w][F_TID][x];
-            if (x == x0) d.state[tid] = commit ? ST_COMMIT : ST_ABORT;
+            if (x == x0) d.state[L[w][F_TID][x]] = commit ? ST_COMMIT : ST_ABORT;
             const uint32_t pub = L[w][F_PUB][x];
             if (pub != DF_NONE) {
-              const uint32_t slot = L[w][F_SLOT][x];
-              const unsigned long long bit = (1ull << (pub & 31u)) |
-                                             (commit ? ((unsigned long long)(~tid) << 32) : 0ull);
-              if (commit && (info & I_MULTI)) atomicMin(&d.trec[slot].w, tid);
-              __hip_atomic_fetch_or(&d.words[pub >> 5], bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              // the table back to clean for the next epoch (no reader of this
-              // launch looks at tkey / tnw)
-              d.tkey[slot] = KEY_EMPTY;
-              d.tnw[slot] = 0u;
+              const unsigned long long bit = 1ull << (pub & 31u);
+              __hip_atomic_fetch_or(&d.words[pub >> 5], commit ? (bit | (bit << 32)) : bit,
+                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             info |= I_FIN;
             L[w][F_INFO][x] = info;
-            progress = true;
           }
         }
         if ((info & (I_LIVE | I_FIN)) == I_LIVE) fin_all = false;
@@ -374,7 +362,6 @@ __global__ __launch_bounds__(256) void k_df_solve(DfArgs d) {
       if (!ballot64(!fin_all)) cid[w] = DF_NONE;  // the chunk is decided
     }
     passes++;
-    (void)progress;
     if ((passes & 15u) == 1) {  // the first pass too (a 0 limit gives up at once)
       const bool late = __builtin_amdgcn_s_memrealtime() - t0 > d.limit_ticks;
       const uint32_t e = __hip_atomic_load(&c->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -383,15 +370,50 @@ __global__ __launch_bounds__(256) void k_df_solve(DfArgs d) {
     }
   }
   if (wid == 0 && lane == 0) c->passes = passes;
+  if (dbg) {
+    // polls summed over the wave's lanes
+    uint32_t p = polls;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) p += __shfl_xor(p, o);
+    if (lane == 0) {
+      dbg[0] = t0;
+      dbg[1] = t_ready;
+      dbg[2] = __builtin_amdgcn_s_memrealtime();
+      dbg[3] = passes;
+      dbg[4] = refills;
+      dbg[5] = p;
+      dbg[6] = 1;
+    }
+  }
 }
 
-// k_df_clear: the whole table clean (first use, growth, or after an epoch
-// that stopped before its solver reset the slots it used)
-__global__ __launch_bounds__(256) void k_df_clear(DfArgs d, uint64_t slots) {
-  for (uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x; q < slots; q += (uint64_t)gridDim.x * 256) {
-    d.tkey[q] = KEY_EMPTY;
-    d.tnw[q] = 0u;
+// k_df_ro: the read-only survivors, an access per thread: a committed entry
+// of the access's key with a smaller txn id aborts the txn (k_df_list started
+// it as committed; only aborts are stored here, so threads of one txn never
+// disagree).  Every writer is decided: plain loads.
+__global__ __launch_bounds__(256) void k_df_ro(DfArgs d) {
+  DfCtl* c = d.ctl;
+  if (!c->live || !c->m) return;  // no write survivors: every read-only one commits
+  const uint32_t acc = c->acc_r, bits = c->bits;
+  for (uint32_t a = blockIdx.x * 256 + threadIdx.x; a < acc; a += gridDim.x * 256) {
+    const uint32_t tid = d.r_t[a];
+    const uint64_t key = d.keys[d.r_x[a]];
+    const uint4 r = d.brec[df_bucket(key, bits)];
+    bool kill = false;
+    for (uint32_t j = 0; j < r.z && !kill; j++) {
+      const uint4 e = d.ent[r.x + j];
+      if ((((uint64_t)e.y << 32) | e.x) == key && e.z < tid)
+        kill = (d.words[r.y + j / 32u] >> (32u + (j & 31u))) & 1ull;
+    }
+    if (kill) d.state[tid] = ST_ABORT;
   }
+}
+
+// k_df_clear: the bucket counts clean (first use, growth, or after an epoch
+// that stopped before k_df_alloc cleared them)
+__global__ __launch_bounds__(256) void k_df_clear(DfArgs d, uint64_t buckets) {
+  for (uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x; q < buckets; q += (uint64_t)gridDim.x * 256)
+    d.bcnt[q] = 0u;
 }
 
 void launch_df_alloc(const DfArgs& a, hipStream_t st) { k_df_alloc<<<DF_SCAN_WG, 256, 0, st>>>(a); }
@@ -401,14 +423,17 @@ void launch_df_scatter(const DfArgs& a, unsigned grid, hipStream_t st) {
 void launch_df_solve(const DfArgs& a, unsigned grid, hipStream_t st) {
   k_df_solve<<<grid ? grid : 1u, 256, 0, st>>>(a);
 }
+void launch_df_ro(const DfArgs& a, unsigned grid, hipStream_t st) {
+  k_df_ro<<<grid ? grid : 1u, 256, 0, st>>>(a);
+}
 int df_solve_blocks_per_cu() {
   int nb = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_df_solve, 256, 0) != hipSuccess) nb = 1;
   return nb;
 }
-void launch_df_clear(const DfArgs& a, uint64_t slots, hipStream_t st) {
-  const uint64_t g = (slots + 255) / 256;
-  k_df_clear<<<(unsigned)(g < 8192 ? (g ? g : 1) : 8192), 256, 0, st>>>(a, slots);
+void launch_df_clear(const DfArgs& a, uint64_t buckets, hipStream_t st) {
+  const uint64_t g = (buckets + 255) / 256;
+  k_df_clear<<<(unsigned)(g < 8192 ? (g ? g : 1) : 8192), 256, 0, st>>>(a, buckets);
 }
 
 }  // namespace dcc

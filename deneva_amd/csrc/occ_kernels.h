@@ -412,32 +412,36 @@ void launch_sw_merge(const SwList& in, uint32_t P, uint32_t* xbuf, uint32_t xoff
 
 // ---- dataflow solver over the level-0 survivors (occ_dataflow.hip)
 // Level 0 of the sweep decides its serial prefix and kills every txn touching
-// its committed writes; the survivors (write and read-only txns, index order)
-// are then decided with no further levels: per write key, the list of its
-// writers (txn ids, any order) and one 64-bit word per 32 writers
-//   bits [0, 32)   writer s % 32 of the group is decided (commit or abort)
-//   bits [32, 64)  ~txn id of the group's committed writer (0: none yet)
-// A txn commits once, on each of its keys, every writer with a smaller id is
-// decided and none committed; it aborts once one of them committed.  Each
-// decision is one atomicOr of the writer's bit (with ~id on commit), so readers
-// learn decisions without barriers, rounds or levels.
-constexpr uint32_t DF_NONE = 0xFFFFFFFFu;  // s_slot: no list txn writes the key
-constexpr uint32_t DF_PEND = 0xFFFFFFFEu;  // s_slot after k_df_list: a read, looked up later
+// its committed writes; the survivors are then decided with no further levels,
+// rounds or grid barriers.  The survivors' write accesses are laid out per
+// hash bucket of their key (bucket = fmix64(key) >> (64 - bits), any order
+// inside a bucket), each bucket with one 64-bit word per 32 entries:
+//   bits [0, 32)   entry j % 32 of the group is decided (its txn committed or aborted)
+//   bits [32, 64)  entry j % 32 of the group committed
+// A write txn commits once, on each of its keys, every entry of that key with a
+// smaller txn id is decided and none committed (occ.cpp:185-199: the first
+// committed writer of a key kills every later accessor); it aborts once one of
+// them committed.  A decision is one atomicOr per write access.  Read-only
+// survivors never block anyone (occ.cpp:151-154): they are decided after every
+// writer, against the committed bits.
+constexpr uint32_t DF_NONE = 0xFFFFFFFFu;
 constexpr uint32_t DF_SCAN_WG = 256;       // k_df_alloc workgroups (all resident)
 constexpr uint32_t DF_QW = 4;              // chunks in a solver wave's window
 constexpr uint32_t DF_MIN_BITS = 10;
 // control block (device; copied to the host with the epoch's read-back)
 struct DfCtl {
-  uint32_t m;        // survivors (list txns)
+  uint32_t m;        // write survivors (the solver's list)
   uint32_t acc;      // their accesses
-  uint32_t bits;     // key-table slots this epoch: 1 << bits
-  uint32_t nchunks;  // solver chunks: txns whose first access is in [64c, 64c + 64)
+  uint32_t m_r;      // read-only survivors
+  uint32_t acc_r;    // their accesses
+  uint32_t bits;     // buckets this epoch: 1 << bits
+  uint32_t nchunks;  // solver chunks: write txns whose first access is in [64c, 64c + 64)
   uint32_t live;     // 1: the dataflow path runs this epoch (0: nothing / hand-off)
   uint32_t err;      // DF_E_* (the host falls back to the sweep levels)
-  uint32_t npos;     // writer entries (k_df_alloc)
+  uint32_t nent;     // bucket entries (write accesses of the list, k_df_alloc)
   uint32_t nwords;   // group words
-  uint32_t passes;   // the solver's most passes by one wave
-  uint32_t pad[7];
+  uint32_t passes;   // wave 0's solver passes
+  uint32_t pad[5];
   unsigned long long gran[DF_SCAN_WG];  // k_df_alloc look-back: flag << 63 | words << 32 | entries
 };
 constexpr uint32_t DF_E_SPIN = 1, DF_E_SCAN = 2, DF_E_FULL = 4;
@@ -448,31 +452,37 @@ struct DfArgs {
   const uint8_t* acctype;
   uint64_t nnz;
   uint8_t* state;
-  // key table of the survivors' write keys (clean between epochs: the solver
-  // resets every slot it used)
-  uint64_t* tkey;    // [1 << max_bits] KEY_EMPTY
-  uint32_t* tnw;     // [1 << max_bits] writers per key, 0
-  uint4* trec;       // [1 << max_bits] {first entry, first word, writers, committed writer}
+  // buckets: entry counts (zero between epochs: k_df_alloc clears what it
+  // read), fill cursors, {first entry, first word, entries}
+  uint32_t* bcnt;    // [1 << max_bits]
+  uint32_t* bcur;    // [1 << max_bits]
+  uint4* brec;       // [1 << max_bits]
+  uint4* ent;        // [cap_acc] {key lo, key hi, txn id, 0} per write access
+  unsigned long long* words;  // [cap_acc]
   uint32_t max_bits;
-  uint64_t cap_acc;  // survivor accesses the per-access arrays hold
+  uint64_t cap_acc;  // list accesses the per-access arrays hold (each list)
   uint64_t cap_txn;
-  // the list (k_df_list)
+  // the write list (k_df_list)
   uint32_t* s_tid;   // [m] txn id
   uint32_t* s_aoff;  // [m + 1] first access (list access index)
   uint32_t* cfirst;  // [nchunks + 1] first list txn of each chunk
-  uint32_t* s_slot;  // [acc] key slot (DF_NONE: no list writer)
-  uint32_t* s_rank;  // [acc] a write's rank among its key's writers (DF_NONE: a read)
-  uint32_t* s_x;     // [acc] writes: txn id; reads: batch access index
-  uint32_t* wtid;    // [npos] writer txn ids per key (k_df_scatter)
-  unsigned long long* words;  // [nwords]
-  const uint32_t* abandon;
+  uint32_t* s_x;     // [acc] batch access index
+  uint32_t* s_pub;   // [acc] writes: txn id (k_df_list), then word << 5 | bit (k_df_scatter); reads DF_NONE
+  // the read-only list: per access its batch index and txn id
+  uint32_t* r_x;
+  uint32_t* r_t;
   uint32_t* err;
   uint64_t limit_ticks;  // the solver gives up after this long (s_memrealtime, 100 MHz)
+  // DCC_DF_DEBUG: per-wave stamps of the first DF_DBG_WAVES waves (start,
+  // first window ready, end, passes, refills, polls)
+  unsigned long long* dbg;
 };
+constexpr uint32_t DF_DBG_WAVES = 4096;
 void launch_df_alloc(const DfArgs& a, hipStream_t st);
 void launch_df_scatter(const DfArgs& a, unsigned grid, hipStream_t st);
 void launch_df_solve(const DfArgs& a, unsigned grid, hipStream_t st);
-void launch_df_clear(const DfArgs& a, uint64_t slots, hipStream_t st);
+void launch_df_ro(const DfArgs& a, unsigned grid, hipStream_t st);
+void launch_df_clear(const DfArgs& a, uint64_t buckets, hipStream_t st);
 int df_solve_blocks_per_cu();  // resident k_df_solve workgroups per CU (occupancy query)
 
 // Several word fills in one launch (replaces a run of hipMemsetAsync calls,

@@ -59,11 +59,37 @@ def test_c1_occ_epochs_match_oracle(tmp_path, gpus):
 
 
 @pytest.mark.gpu
-def test_c1_calvin_handoff():
+def test_c1_calvin_handoff(tmp_path):
+    # four origin nodes submit concurrently (CalvinEpoch::submit, the
+    # sequencer's per-origin FIFO numbering); every closed epoch is captured
+    # with its sequencer order and checked against the literal Row_lock replay
+    # (grant groups per request, readiness and wave level per txn) -- the
+    # epochs the concurrent submitters formed, not a regenerated batch
+    cap = tmp_path / "cal"
+    cap.mkdir()
     out = run_driver("--calvin", "--threads", "4", "--txns", "1000", "--theta", "0.6",
-                     "--epoch-max", "512")
+                     "--epoch-max", "512", "--capture", str(cap))
     assert out["failed"] == 0 and out["ready"] + out["waits"] == 4 * 1000
     assert out["epochs"] == (1000 + 127) // 128 and out["ready"] > 0
+    files = sorted(glob.glob(str(cap / "calvin_*.dccb")))
+    assert len(files) == out["epochs"]
+    seen = ready = 0
+    for f in files:
+        b, meta, dec = d.read_batch_file(f)
+        assert meta["kind"] == d._abi.FILE_CALVIN and b.order is not None
+        order = np.asarray(b.order, np.uint64)
+        # sequencer order: origin << 32 | FIFO number within the origin, every
+        # origin numbered 0.. in this epoch (sequencer.cpp:283-326)
+        for o in np.unique(order >> np.uint64(32)):
+            sq = np.sort(order[(order >> np.uint64(32)) == o] & np.uint64(0xFFFFFFFF))
+            assert np.array_equal(sq, np.arange(sq.size, dtype=np.uint64)), f
+        eg, erc, ew = orc.calvin(b, literal=True)
+        assert np.array_equal(dec["group"], eg), f
+        assert np.array_equal(dec["rc"], erc), f
+        assert np.array_equal(dec["wave"], ew), f
+        seen += b.n_txn
+        ready += int((erc == 0).sum())
+    assert seen == 4 * 1000 and ready == out["ready"]
 
 
 @pytest.mark.gpu
