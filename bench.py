@@ -45,8 +45,7 @@ def parse():
                     help="comma-separated secondary configs to run INSTEAD of the headline "
                          "(profiling aid): " + ",".join(CONFIGS))
     ap.add_argument("--solver", type=int, default=0,
-                    help="OCC solver: 0 auto, 1 fixed-point rounds only, 3 sweep levels, "
-                         "4 level 0 of the sweep then the dataflow solver")
+                    help="OCC solver: 0 auto (= 3), 1 fixed-point rounds only, 3 sweep levels")
     ap.add_argument("--sweep-levels", type=int, default=0,
                     help="sweep levels per captured epoch (DCC_OPT_SWEEP_LEVELS; 0: the engine's "
                          "default)")

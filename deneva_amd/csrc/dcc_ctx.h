@@ -14,7 +14,6 @@
 
 namespace dcc {
 struct SwShard;  // occ_kernels.h: one key-sharded sweep level's serial range
-struct DfArgs;   // occ_kernels.h: the dataflow solver's buffers
 }
 
 struct dcc_ctx;
@@ -85,18 +84,8 @@ struct dcc_ctx {
   uint64_t recheck_max = 16384;   // fold the kill wave into rounds with lists <= this
   uint32_t batch_max = 8;       // rounds enqueued between host synchronisations
   bool bars_used = false;       // this epoch's rounds used grid-barrier words
-  int solver = 0;               // 0 auto (= 3), 1 fixed-point rounds, 3 sweep, 4 level 0 of the
-                                // sweep + the dataflow solver (occ_dataflow.hip)
+  int solver = 0;               // 0 auto (= 3), 1 fixed-point rounds, 3 sweep
   bool use_sweep() const { return solver != 1; }
-  bool use_df() const { return solver == 4; }
-  bool df_on = false;             // this epoch: level 0's compaction launch is k_df_list
-  uint64_t df_clean = 0;          // dataflow bucket counts known zero
-  bool df_dirty = false;          // an epoch stopped before k_df_alloc cleared the counts
-  uint32_t df_max_bits = 0;       // dataflow buckets: 1 << df_max_bits allocated
-  uint64_t df_cap_acc = 0, df_cap_txn = 0;
-  uint32_t df_grid = 0;           // k_df_solve workgroups (all resident)
-  uint64_t df_limit_ticks = 50000000;  // the solver's time limit (0.5 s; DCC_DF_LIMIT_US)
-  bool df_debug = false;          // DCC_DF_DEBUG: per-wave stamps of the solver (no graph)
   bool ro_split = true;           // DCC_OPT_RO_SPLIT
   bool ro_on = false;             // this epoch splits read-only txns off (sweep, one GPU)
   uint32_t wt_bits = 18;          // committed-writer table slots (WT_BITS_DEFAULT; grows after an overflow)
@@ -153,9 +142,6 @@ struct dcc_ctx {
                                                         // list, writer tables, committed writers
   DevBuf sw_xcnt, sw_xsend, sw_xrec, sw_mcnt, sw_moff, sw_mkeys, sw_mat, sw_kill;  // key-sharded sweep  // sweep tile records
   SubBufs sw_list[2];                            // sweep level lists (ping-pong)
-  DevBuf df_ctl, df_bcnt, df_bcur, df_brec, df_ent, df_words;  // dataflow solver: buckets, entries
-  DevBuf df_tid, df_aoff, df_cfirst, df_x, df_pub, df_rx, df_rt;  // write list, read-only list
-  DevBuf df_dbg;
   DevBuf l_tid[2], l_coff[2], l_cent[2];         // ping-pong undecided lists
   // OCC history (occ.h:62-64) on the device: base + delta levels
   HistStore hs[2];
@@ -223,9 +209,6 @@ struct dcc_ctx {
   int sweep_enqueue(const DevBatch& d, int l0, int l1, const dcc::SwShard* shard = nullptr,
                     bool resume = false, bool tail_serial = false);
   int sweep_sharded(const DevBatch& d, int& next_level);
-  int df_reserve(const DevBatch& d);
-  dcc::DfArgs df_args(const DevBatch& d);
-  int df_enqueue(const DevBatch& d);  // k_df_alloc, k_df_scatter, k_df_solve
   int sweep_ro(const DevBatch& d, bool big, bool scan, uint64_t nnz_w);  // decide the RO list
   int occ_sweep_finish(const DevBatch& d, int& next_level, bool& done, uint32_t maxlen);
   int occ_snapshot(const dcc_batch* b, const dcc_occ_snapshot* s, uint8_t* out_rc, dcc_stats* st);

@@ -196,7 +196,7 @@ extern "C" int dcc_set_option(dcc_ctx* ctx, int option, int64_t value) {
       ctx->recheck_max = (uint64_t)value;
       return DCC_OK;
     case DCC_OPT_SOLVER:
-      if (value != 0 && value != 1 && value != 3 && value != 4) return DCC_EINVAL;
+      if (value != 0 && value != 1 && value != 3) return DCC_EINVAL;
       ctx->solver = (int)value;
       return DCC_OK;
     case DCC_OPT_SWEEP_LEVELS:
@@ -243,8 +243,6 @@ std::vector<DevBuf*> dcc_ctx::all_bufs() {
                             &mt_misc, &mt_slot, &mt_sval, &mt_slot2, &mt_sval2, &mt_sfl,
                             &mt_stx, &mt_txn, &mt_agg, &mt_sflB, &mt_stxB, &mt_k1, &mt_tcnt, &mt_ul, &ix_keys, &ix_ord, &ix_rows, &ix_cnt, &wv_buf, &ix_scr, &wv_hbuf, &wv_obuf,
                             &h_K[0], &h_K[1], &h_V[0], &h_V[1], &h_scr, &h_bsum,
-                            &df_ctl, &df_bcnt, &df_bcur, &df_brec, &df_ent, &df_words, &df_tid,
-                            &df_aoff, &df_cfirst, &df_x, &df_pub, &df_rx, &df_rt, &df_dbg,
                             &fin_off, &fin_keys, &fin_at, &fin_state, &fin_hasw, &fin_rc, &fin_cnt,
                             &sh_off, &sh_keys, &sh_at, &sh_src, &sh_cnt, &sh_bsum, &sh_rc, &sh_tn, &sh_grp};
   for (auto& h : hs)

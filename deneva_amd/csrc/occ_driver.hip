@@ -340,11 +340,9 @@ int dcc_ctx::sweep_reserve(const DevBatch& d) {
   CR(sw_fw.ensure(this, 2 * (1ull << SW_GBITS_MAX) * 4, "sweep first writer / last accessor"));
   CR(sw_aent.ensure(this, 2 * (1ull << (SW_GBITS_MAX - 1)) * 4, "sweep access entries"));
   CR(sw_mg.ensure(this, SW_PMAX_TILES * 8, "sweep tile commit masks"));
-  if (ro_on || df_on) {
+  if (ro_on) {
     const uint64_t n64 = (d.n + 63) / 64 + 32;
     CR(sw_rflag.ensure(this, (2 * n64 + 4ull * n_cu + 64) * 8, "sweep read-only survivor bits"));
-  }
-  if (ro_on) {
     CR(sw_ro.ensure(this, d.n * sizeof(RoEnt) + 64, "sweep read-only list"));
     CR(sw_wtab.ensure(this, sizeof(WrSlot) << wt_bits, "committed-writer table"));
     CR(sw_cw.ensure(this, d.n * 4 + 64, "committed writers"));
@@ -484,9 +482,7 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1, const SwShard* shl
     fa.cdbg = pa.dbg ? pa.dbg + 32 : nullptr;
     fa.kill_out = shl ? shl->kill : nullptr;
     fa.kill_in = shl ? shl->kill : nullptr;
-    // the dataflow path counts the read-only survivors apart as well (its own
-    // read-only list), without the RO split's serial-pass bookkeeping
-    fa.ro_split = ((ros || df_on) && top) ? 1 : 0;
+    fa.ro_split = (ros && top) ? 1 : 0;
     fa.rflag = (uint64_t*)sw_rflag.p;
     fa.rtcount = (unsigned long long*)(fa.rflag + n64 + 32);
     fa.rbsum = fa.rtcount + n64 + 32;
@@ -502,8 +498,7 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1, const SwShard* shl
       if (top) CR(comm_allreduce_max_u8((uint8_t*)hasw.p, d.n));
       launch_sw_apply(fa, fgrid, stream);
     }
-    if (top && df_on) launch_df_list(fa, df_args(d), fgrid, stream);
-    else launch_sw_compact(fa, fgrid, stream);
+    launch_sw_compact(fa, fgrid, stream);
   }
   CK(hipGetLastError());
   return DCC_OK;
@@ -684,101 +679,6 @@ int dcc_ctx::occ_finish(const uint8_t* final_rc, uint64_t* out_tn, uint32_t flag
   return occ_finish_commit(n_cw, out_tn, flags);
 }
 
-// ---------------------------------------------------------------------------
-// Dataflow solver (occ_dataflow.hip) over level 0's survivors.  Buffers are
-// sized for lists of up to half the epoch's accesses (a larger list goes to
-// the round solver); the bucket counts are kept zero between epochs by
-// k_df_alloc (it clears what it read), so only new, grown or abandoned counts
-// are cleared here (before any capture).
-static constexpr size_t DF_HCTL = 15360;  // dataflow control copy inside `hmisc`
-int dcc_ctx::df_reserve(const DevBatch& d) {
-  dcc_ctx* ctx = this;
-  const uint64_t cap_acc = std::max<uint64_t>(65536, d.nnz / 2);
-  uint32_t bits = DF_MIN_BITS;
-  while (bits < 31 && (2ull << bits) < cap_acc) bits++;
-  const uint64_t buckets = 1ull << bits;
-  const void* old = df_bcnt.p;
-  CR(df_ctl.ensure(this, sizeof(DfCtl), "dataflow control"));
-  CR(df_bcnt.ensure(this, buckets * 4, "dataflow bucket counts"));
-  CR(df_bcur.ensure(this, buckets * 4, "dataflow bucket cursors"));
-  CR(df_brec.ensure(this, buckets * 16, "dataflow buckets"));
-  if (df_bcnt.p != old) df_clean = 0;
-  CR(df_ent.ensure(this, cap_acc * 16 + 64, "dataflow bucket entries"));
-  CR(df_words.ensure(this, cap_acc * 8 + 64, "dataflow group words"));
-  CR(df_tid.ensure(this, d.n * 4 + 64, "dataflow list txns"));
-  CR(df_aoff.ensure(this, d.n * 4 + 64, "dataflow list offsets"));
-  CR(df_cfirst.ensure(this, (cap_acc / 64 + 4) * 4, "dataflow chunks"));
-  CR(df_x.ensure(this, cap_acc * 4 + 64, "dataflow access refs"));
-  CR(df_pub.ensure(this, cap_acc * 4 + 64, "dataflow access words"));
-  CR(df_rx.ensure(this, cap_acc * 4 + 64, "dataflow read-only refs"));
-  CR(df_rt.ensure(this, cap_acc * 4 + 64, "dataflow read-only txns"));
-  uint64_t have = std::min<uint64_t>({df_bcnt.cap / 4, df_bcur.cap / 4, df_brec.cap / 16});
-  df_max_bits = 0;
-  while ((2ull << df_max_bits) <= have) df_max_bits++;
-  df_cap_acc = std::min<uint64_t>({df_ent.cap / 16, df_words.cap / 8, df_x.cap / 4, df_pub.cap / 4,
-                                   df_rx.cap / 4, df_rt.cap / 4, (df_cfirst.cap / 4 - 4) * 64}) - 16;
-  df_cap_txn = std::min<uint64_t>(df_tid.cap / 4, df_aoff.cap / 4) - 16;
-  if (!df_grid) {
-    const int per = df_solve_blocks_per_cu();
-    df_grid = (unsigned)n_cu * (unsigned)std::max(1, std::min(per, 3));
-  }
-  if (const char* e = getenv("DCC_DF_LIMIT_US")) df_limit_ticks = strtoull(e, nullptr, 10) * 100ull;
-  df_debug = getenv("DCC_DF_DEBUG") != nullptr;
-  if (df_debug) {
-    const size_t bytes = 8ull * DF_DBG_WAVES * 8;
-    CR(df_dbg.ensure(this, bytes, "dataflow debug"));
-    CK(hipMemsetAsync(df_dbg.p, 0, bytes, stream));
-  }
-  if (df_dirty || df_clean < (1ull << df_max_bits)) {
-    const DfArgs a = df_args(d);
-    launch_df_clear(a, 1ull << df_max_bits, stream);
-    CK(hipGetLastError());
-    df_clean = 1ull << df_max_bits;
-    df_dirty = false;
-  }
-  return DCC_OK;
-}
-
-DfArgs dcc_ctx::df_args(const DevBatch& d) {
-  DfArgs a{};
-  a.ctl = (DfCtl*)df_ctl.p;
-  a.off = d.off;
-  a.keys = d.keys;
-  a.acctype = d.acctype;
-  a.nnz = d.nnz;
-  a.state = (uint8_t*)state.p;
-  a.bcnt = (uint32_t*)df_bcnt.p;
-  a.bcur = (uint32_t*)df_bcur.p;
-  a.brec = (uint4*)df_brec.p;
-  a.ent = (uint4*)df_ent.p;
-  a.words = (unsigned long long*)df_words.p;
-  a.max_bits = df_max_bits;
-  a.cap_acc = df_cap_acc;
-  a.cap_txn = df_cap_txn;
-  a.s_tid = (uint32_t*)df_tid.p;
-  a.s_aoff = (uint32_t*)df_aoff.p;
-  a.cfirst = (uint32_t*)df_cfirst.p;
-  a.s_x = (uint32_t*)df_x.p;
-  a.s_pub = (uint32_t*)df_pub.p;
-  a.r_x = (uint32_t*)df_rx.p;
-  a.r_t = (uint32_t*)df_rt.p;
-  a.err = (uint32_t*)misc.p;
-  a.limit_ticks = df_limit_ticks;
-  a.dbg = df_debug ? (unsigned long long*)df_dbg.p : nullptr;
-  return a;
-}
-
-int dcc_ctx::df_enqueue(const DevBatch& d) {
-  dcc_ctx* ctx = this;
-  const DfArgs a = df_args(d);
-  launch_df_alloc(a, stream);
-  launch_df_scatter(a, (unsigned)n_cu * 8, stream);
-  launch_df_solve(a, df_grid, stream);
-  launch_df_ro(a, (unsigned)n_cu * 8, stream);
-  CK(hipGetLastError());
-  return DCC_OK;
-}
-
 // The read-only list of a split epoch, once every writer is decided: the
 // writer table of the committed writes (k_sw_wall: the committed writers the
 // serial passes listed, or after a hand-off to the round solver every
@@ -833,12 +733,8 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   DevBatch d;
   CR(stage_batch(b, d));
   const bool sweep = use_sweep();
-  // level 0 of the sweep, then the dataflow solver (single GPU)
-  const bool df = sweep && use_df() && !sh;
-  df_on = df;
-  ro_on = sweep && ro_split && !sh && !df;
+  ro_on = sweep && ro_split && !sh;
   if (sweep) CR(sweep_reserve(d));
-  if (df) CR(df_reserve(d));
   CR(state.ensure(this, d.n + 16, "state"));
   CR(hasw.ensure(this, d.n + 16, "hasw"));
   CR(rc.ensure(this, d.n + 16, "rc"));
@@ -853,14 +749,13 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   // the ones it was captured with: one graph launch instead of ~30 kernel
   // launches, so the device never waits for the host between kernels.
   const bool hist_on = d.start_tn && hist_size() > 0;
-  const bool graph_ok = sweep && !profiling && !sw_debug && !(df && df_debug) && !want_tn && !hist_on && !sh &&
+  const bool graph_ok = sweep && !profiling && !sw_debug && !want_tn && !hist_on && !sh &&
                         !getenv("DCC_NO_GRAPH");
   // levels per captured epoch (DCC_OPT_SWEEP_LEVELS; 0 = auto: 3 with the
   // read-only split, 4 without)
   const uint32_t glv = sw_levels ? sw_levels : (ro_on ? 3u : 4u);
   const GraphKey gkey{d.off, d.keys, d.acctype, d.n, d.nnz, out_rc, dev_out,
-                      df ? 2000u + df_max_bits
-                         : glv | (ro_on ? 0x80u | (wt_bits << 8) : 0u),
+                      glv | (ro_on ? 0x80u | (wt_bits << 8) : 0u),
                       buf_gen};
   bool replay = graph_ok && graph_exec && gkey == graph_key;
   bool capturing = false;
@@ -912,9 +807,6 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
       fa.job[fa.n++] = FillJob{(uint32_t*)sw_gtab.p, (1ull << sw_gbits(0, ro_on)) * 2, 0xFFFFFFFFu};
       fa.job[fa.n++] = FillJob{(uint32_t*)sw_fw.p, 1ull << sw_gbits(0, ro_on), 0xFFFFFFFFu};
       fa.job[fa.n++] = FillJob{(uint32_t*)sw_fw.p + (1u << SW_GBITS_MAX), 1ull << sw_gbits(0, ro_on), 0u};
-      // the dataflow control words (a level 0 that decides the whole epoch
-      // never reaches k_df_list, so nothing may read a stale `live`)
-      if (df) fa.job[fa.n++] = FillJob{(uint32_t*)df_ctl.p, 16, 0u};
     }
     launch_fill(fa, stream);  // the sweep's prep runs inside its level-0 serial pass
   }
@@ -947,14 +839,12 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   int serial_tail = -1;  // level enqueued without its filter (sweep_enqueue tail_serial)
   if (sweep) {
     if (profiling) CK(hipEventRecord(pev[0], stream));
-    next_level = df ? 1 : (int)std::min<uint32_t>(glv, SW_MAX_LEVEL - 1);
-    if (!sh && !df && next_level >= 2) serial_tail = next_level - 1;
-    if (df) df_dirty = true;  // until k_df_alloc has cleared the bucket counts
+    next_level = (int)std::min<uint32_t>(glv, SW_MAX_LEVEL - 1);
+    if (!sh && next_level >= 2) serial_tail = next_level - 1;
     if (sh) {
       CR(sweep_sharded(d, next_level));
     } else if (!replay) {
       CR(sweep_enqueue(d, 0, next_level, nullptr, false, serial_tail >= 0));
-      if (df) CR(df_enqueue(d));
       if (ro_on) CR(sweep_ro(d, false, false, 0));
     }
   } else {
@@ -985,7 +875,6 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
     job(hmisc_dev, misc.p, 64);
     job((char*)hmisc_dev + MISC_BARS, (char*)misc.p + MISC_BARS, CTR_RING * 16);
     if (sweep) job((char*)hmisc_dev + SW_HCTL, sw_ctl.p, sw_ctl_bytes());
-    if (df) job((char*)hmisc_dev + DF_HCTL, df_ctl.p, 64);
     FinalArgs fa{d.n, (const uint8_t*)state.p, (const uint8_t*)hasw.p, rc_dev, cf,
                  (FinalPart*)hpart_dev};
     launch_final(fa, ga, stream);
@@ -1030,53 +919,6 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
     if (maxlen > MAX_TXN_LEN)
       return fail(DCC_ERANGE, "batch: a txn has %u accesses (> MAX_ROW_PER_TXN=%u)", maxlen,
                   MAX_TXN_LEN);
-    if (df && df_debug) {
-      const DfCtl* hd = (const DfCtl*)((const char*)hmisc + DF_HCTL);
-      std::vector<unsigned long long> v(8ull * DF_DBG_WAVES);
-      CK(hipMemcpy(v.data(), df_dbg.p, v.size() * 8, hipMemcpyDeviceToHost));
-      uint64_t t0 = ~0ull, nw = 0;
-      for (uint32_t w = 0; w < DF_DBG_WAVES; w++)
-        if (v[8 * w + 6]) t0 = std::min<uint64_t>(t0, v[8 * w]), nw++;
-      std::vector<double> ready, end, passes, refills, polls;
-      for (uint32_t w = 0; w < DF_DBG_WAVES; w++) {
-        const unsigned long long* x = &v[8 * w];
-        if (!x[6]) continue;
-        ready.push_back((x[1] - t0) * 0.01);
-        end.push_back((x[2] - t0) * 0.01);
-        passes.push_back((double)x[3]);
-        refills.push_back((double)x[4]);
-        polls.push_back((double)x[5]);
-      }
-      auto q = [](std::vector<double> a, double f) {
-        if (a.empty()) return 0.0;
-        std::sort(a.begin(), a.end());
-        return a[(size_t)(f * (a.size() - 1))];
-      };
-      double tp = 0;
-      for (double p : polls) tp += p;
-      fprintf(stderr, "df: m %u acc %u (read-only %u / %u) bits %u chunks %u entries %u words %u; %llu waves: "
-                      "ready us p50 %.1f max %.1f | end us p50 %.1f p90 %.1f max %.1f | passes p50 %.0f max %.0f | "
-                      "refills max %.0f | polls total %.0f\n",
-              hd->m, hd->acc, hd->m_r, hd->acc_r, hd->bits, hd->nchunks, hd->nent, hd->nwords,
-              (unsigned long long)nw,
-              q(ready, 0.5), q(ready, 1), q(end, 0.5), q(end, 0.9), q(end, 1), q(passes, 0.5), q(passes, 1),
-              q(refills, 1), tp);
-    }
-    // the dataflow solver gave up (its time limit, or a look-back that never
-    // completed): the epoch again with the sweep's levels; the table is
-    // cleaned before the next dataflow epoch
-    if (df) {
-      const DfCtl* hd = (const DfCtl*)((const char*)hmisc + DF_HCTL);
-      if (hd->err) {
-        df_dirty = true;
-        const int saved = solver;
-        solver = 3;
-        const int e = occ_epoch(b, out_rc, out_tn, st);
-        solver = saved;
-        if (st) st->fallback += 1;
-        return e;
-      }
-    }
     // more levels, or hand the remaining list to the round solver
     bool again = false, ro_fast_rerun = false;
     for (;;) {
@@ -1245,13 +1087,6 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
     info.prefix = hc[0].pos;
     info.survivors = hc[1].m;
     for (int l = 0; l < next_level && (l == 0 || hc[l].m); l++) rounds++;
-    if (df) {
-      const DfCtl* hd = (const DfCtl*)((const char*)hmisc + DF_HCTL);
-      if (hd->live) {
-        info.survivors = hd->m;
-        rounds++;
-      }
-    }
   }
 
   const uint32_t e = *(const uint32_t*)hmisc;
@@ -1277,7 +1112,6 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   }
   if (n_und) return fail(DCC_EIO, "%llu undecided transactions after convergence",
                          (unsigned long long)n_und);
-  if (df) df_dirty = false;  // k_df_alloc cleared the counts (or the epoch never counted)
   float ms = 0;
   CK(hipEventElapsedTime(&ms, ev0, ev1));
   S.rounds = rounds;

@@ -394,12 +394,7 @@ void launch_sw_seq(const SwSeqArgs& a, hipStream_t st);
 void launch_sw_rows(const SwPreArgs& a, unsigned grid, hipStream_t st);
 void launch_sw_cout(const SwCoutArgs& a, unsigned grid, hipStream_t st);
 void launch_sw_filter(const SwFilterArgs& a, unsigned grid, hipStream_t st);
-// the level-0 compaction; with df.ctl set (the dataflow solver) it lists the
-// survivors by reference and builds the key table instead, unless the level
-// hands off to the round solver
-struct DfArgs;
 void launch_sw_compact(const SwFilterArgs& a, unsigned grid, hipStream_t st);
-void launch_df_list(const SwFilterArgs& a, const DfArgs& d, unsigned grid, hipStream_t st);
 void launch_sw_apply(const SwFilterArgs& a, unsigned grid, hipStream_t st);
 void launch_sw_share(const uint32_t* m_dev, uint32_t m_host, const uint32_t* abandon,
                      const uint32_t* off, uint32_t p_max, uint32_t rank, uint32_t* cnt,
@@ -409,81 +404,6 @@ void launch_sw_share(const uint32_t* m_dev, uint32_t m_host, const uint32_t* aba
 void launch_sw_merge(const SwList& in, uint32_t P, uint32_t* xbuf, uint32_t xoff_words,
                      uint32_t n_all, uint32_t* cnt, uint32_t* cur, uint32_t* moff,
                      uint64_t* mkeys, uint8_t* mat, bool export_only, hipStream_t st);
-
-// ---- dataflow solver over the level-0 survivors (occ_dataflow.hip)
-// Level 0 of the sweep decides its serial prefix and kills every txn touching
-// its committed writes; the survivors are then decided with no further levels,
-// rounds or grid barriers.  The survivors' write accesses are laid out per
-// hash bucket of their key (bucket = fmix64(key) >> (64 - bits), any order
-// inside a bucket), each bucket with one 64-bit word per 32 entries:
-//   bits [0, 32)   entry j % 32 of the group is decided (its txn committed or aborted)
-//   bits [32, 64)  entry j % 32 of the group committed
-// A write txn commits once, on each of its keys, every entry of that key with a
-// smaller txn id is decided and none committed (occ.cpp:185-199: the first
-// committed writer of a key kills every later accessor); it aborts once one of
-// them committed.  A decision is one atomicOr per write access.  Read-only
-// survivors never block anyone (occ.cpp:151-154): they are decided after every
-// writer, against the committed bits.
-constexpr uint32_t DF_NONE = 0xFFFFFFFFu;
-constexpr uint32_t DF_SCAN_WG = 256;       // k_df_alloc workgroups (all resident)
-constexpr uint32_t DF_QW = 4;              // chunks in a solver wave's window
-constexpr uint32_t DF_MIN_BITS = 10;
-// control block (device; copied to the host with the epoch's read-back)
-struct DfCtl {
-  uint32_t m;        // write survivors (the solver's list)
-  uint32_t acc;      // their accesses
-  uint32_t m_r;      // read-only survivors
-  uint32_t acc_r;    // their accesses
-  uint32_t bits;     // buckets this epoch: 1 << bits
-  uint32_t nchunks;  // solver chunks: write txns whose first access is in [64c, 64c + 64)
-  uint32_t live;     // 1: the dataflow path runs this epoch (0: nothing / hand-off)
-  uint32_t err;      // DF_E_* (the host falls back to the sweep levels)
-  uint32_t nent;     // bucket entries (write accesses of the list, k_df_alloc)
-  uint32_t nwords;   // group words
-  uint32_t passes;   // wave 0's solver passes
-  uint32_t pad[5];
-  unsigned long long gran[DF_SCAN_WG];  // k_df_alloc look-back: flag << 63 | words << 32 | entries
-};
-constexpr uint32_t DF_E_SPIN = 1, DF_E_SCAN = 2, DF_E_FULL = 4;
-struct DfArgs {
-  DfCtl* ctl;
-  const uint32_t* off;
-  const uint64_t* keys;
-  const uint8_t* acctype;
-  uint64_t nnz;
-  uint8_t* state;
-  // buckets: entry counts (zero between epochs: k_df_alloc clears what it
-  // read), fill cursors, {first entry, first word, entries}
-  uint32_t* bcnt;    // [1 << max_bits]
-  uint32_t* bcur;    // [1 << max_bits]
-  uint4* brec;       // [1 << max_bits]
-  uint4* ent;        // [cap_acc] {key lo, key hi, txn id, 0} per write access
-  unsigned long long* words;  // [cap_acc]
-  uint32_t max_bits;
-  uint64_t cap_acc;  // list accesses the per-access arrays hold (each list)
-  uint64_t cap_txn;
-  // the write list (k_df_list)
-  uint32_t* s_tid;   // [m] txn id
-  uint32_t* s_aoff;  // [m + 1] first access (list access index)
-  uint32_t* cfirst;  // [nchunks + 1] first list txn of each chunk
-  uint32_t* s_x;     // [acc] batch access index
-  uint32_t* s_pub;   // [acc] writes: txn id (k_df_list), then word << 5 | bit (k_df_scatter); reads DF_NONE
-  // the read-only list: per access its batch index and txn id
-  uint32_t* r_x;
-  uint32_t* r_t;
-  uint32_t* err;
-  uint64_t limit_ticks;  // the solver gives up after this long (s_memrealtime, 100 MHz)
-  // DCC_DF_DEBUG: per-wave stamps of the first DF_DBG_WAVES waves (start,
-  // first window ready, end, passes, refills, polls)
-  unsigned long long* dbg;
-};
-constexpr uint32_t DF_DBG_WAVES = 4096;
-void launch_df_alloc(const DfArgs& a, hipStream_t st);
-void launch_df_scatter(const DfArgs& a, unsigned grid, hipStream_t st);
-void launch_df_solve(const DfArgs& a, unsigned grid, hipStream_t st);
-void launch_df_ro(const DfArgs& a, unsigned grid, hipStream_t st);
-void launch_df_clear(const DfArgs& a, uint64_t buckets, hipStream_t st);
-int df_solve_blocks_per_cu();  // resident k_df_solve workgroups per CU (occupancy query)
 
 // Several word fills in one launch (replaces a run of hipMemsetAsync calls,
 // each of which costs a dispatch and an idle gap on the stream).

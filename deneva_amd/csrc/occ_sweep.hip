@@ -41,7 +41,6 @@
 #include <algorithm>
 
 #include "dcc_device.h"
-#include "occ_dataflow.h"
 #include "occ_kernels.h"
 #include "prep_body.h"
 
@@ -230,88 +229,6 @@ __device__ inline uint32_t wave_excl_u32(uint32_t v, uint32_t& total) {
 __device__ inline uint64_t lanemask_lt() {
   const uint32_t l = lane_id();
   return l ? (~0ull >> (64 - l)) : 0ull;
-}
-
-// k_df_list's body for one surviving tile (called from the level-0
-// compaction, below): lane = txn of the tile; `base` = the tile's first list
-// position << LB_ACC_BITS | first list access.  RO = false: the write list
-// (txn ids, offsets, chunk starts, per access its batch index; a write also
-// counts into its key's bucket); RO = true: the read-only list (per access its
-// batch index and txn id; the txn starts as committed, k_df_ro aborts it).
-template <bool RO>
-__device__ void df_list_tile(const DfArgs& d, uint64_t word, uint64_t base, uint32_t sv, uint32_t ev,
-                             uint32_t tv, uint64_t nnz, uint32_t bits) {
-  const uint32_t lane = lane_id();
-  const uint32_t tb = (uint32_t)(base >> LB_ACC_BITS);
-  const uint32_t abase = (uint32_t)(base & ((1ull << LB_ACC_BITS) - 1));
-  const bool surv = (word >> lane) & 1ull;
-  uint32_t s = 0, len = 0;
-  if (surv) {
-    s = (uint32_t)min((uint64_t)sv, nnz);
-    len = (uint32_t)min((uint64_t)ev, nnz) - s;
-  }
-  uint32_t atot;
-  const uint32_t aex = wave_excl_u32(len, atot);
-  if (surv) {
-    if (RO) {
-      d.state[tv] = ST_COMMIT;
-    } else {
-      const uint32_t r = tb + (uint32_t)__popcll(word & lanemask_lt());
-      const uint32_t x = abase + aex, y = x + len;
-      d.s_tid[r] = tv;
-      d.s_aoff[r] = x;
-      // chunk c starts at the first txn whose first access is >= 64 c: the
-      // txn whose span (x, y] holds 64 c is the one before it
-      for (uint32_t c = x / 64 + 1; c <= y / 64; c++) d.cfirst[c] = r + 1;
-    }
-  }
-  const uint32_t incl = aex + len;
-  for (uint32_t q0 = 0; q0 < atot; q0 += 64 * 4) {
-    uint32_t src[4], own[4];
-    bool in[4];
-#pragma unroll
-    for (uint32_t r = 0; r < 4; r++) {
-      const uint32_t q = q0 + 64 * r + lane;
-      uint32_t lo = 0;  // first lane l with incl[l] > q (all lanes take part)
-#pragma unroll
-      for (uint32_t st = 32; st > 0; st >>= 1) {
-        const uint32_t v = __shfl(incl, lo + st - 1);
-        if (v <= q) lo += st;
-      }
-      in[r] = q < atot;
-      src[r] = __shfl(s, lo) + (q - __shfl(aex, lo));
-      own[r] = __shfl(tv, lo);
-    }
-    if (RO) {
-#pragma unroll
-      for (uint32_t r = 0; r < 4; r++) {
-        if (!in[r]) continue;
-        const uint32_t a = abase + q0 + 64 * r + lane;
-        d.r_x[a] = src[r];
-        d.r_t[a] = own[r];
-      }
-      continue;
-    }
-    uint64_t kk[4];
-    uint8_t aa[4];
-#pragma unroll
-    for (uint32_t r = 0; r < 4; r++) {
-      kk[r] = in[r] ? d.keys[src[r]] : 0ull;
-      aa[r] = in[r] ? d.acctype[src[r]] : (uint8_t)0;
-    }
-#pragma unroll
-    for (uint32_t r = 0; r < 4; r++) {
-      if (!in[r]) continue;
-      const uint32_t a = abase + q0 + 64 * r + lane;
-      d.s_x[a] = src[r];
-      // a write (the reserved key, which the filter reported, is ignored):
-      // its txn id until k_df_scatter places it; one count into its bucket
-      const bool w = aa[r] == 1 /* WR */ && kk[r] != KEY_EMPTY;
-      d.s_pub[a] = w ? own[r] : DF_NONE;
-      if (w) __hip_atomic_fetch_add(&d.bcnt[df_bucket(kk[r], bits)], 1u, __ATOMIC_RELAXED,
-                                    __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
 }
 
 __device__ inline uint32_t list_len(const uint32_t* m_dev, uint32_t m_host) {
@@ -1601,12 +1518,7 @@ __global__ __launch_bounds__(256) void k_sw_mscatter(const uint32_t* rec, uint32
 
 // ---------------------------------------------------------------------------
 // k_sw_compact: the survivors, in index order, into the next level's list.
-// With the dataflow solver (DF, level 0 only, no read-only split) the same
-// launch is k_df_list: unless the level hands off to the round solver, the
-// survivors are listed by reference and their write keys enter the dataflow
-// table (df_list_tile) instead of being copied.
-template <bool DF>
-__device__ inline void sw_compact_body(const SwFilterArgs& a, const DfArgs* d) {
+__global__ __launch_bounds__(SW_CHUNK) void k_sw_compact(SwFilterArgs a) {
   const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
   // an earlier level's hand-off: nothing to compact (this level's own
   // decision is made below and still needs its list)
@@ -1626,9 +1538,6 @@ __device__ inline void sw_compact_body(const SwFilterArgs& a, const DfArgs* d) {
   __shared__ unsigned long long s_tb[SW_CMP_MAXR];
   __shared__ unsigned long long s_part[SW_CHUNK / 64][4];
   __shared__ uint32_t s_split, s_rnext;  // RO list: next position of this workgroup's block
-  __shared__ uint32_t s_df, s_bits;       // DF: the dataflow path runs; its bucket count
-  __shared__ unsigned long long s_rb;     // DF: the read-only list's base of this workgroup
-  __shared__ unsigned long long s_tbr[DF ? SW_CMP_MAXR : 1];  // DF: read-only tile bases
   if (R > SW_CMP_MAXR) {
     if (threadIdx.x == 0) atomicOr(a.err, ERR_TILE);
     return;
@@ -1671,55 +1580,13 @@ __device__ inline void sw_compact_body(const SwFilterArgs& a, const DfArgs* d) {
       }
       const uint32_t tot = (uint32_t)(a0 >> LB_ACC_BITS);
       const uint32_t in_n = m - pos;
-      bool handoff =
+      const bool handoff =
           tot > a.abandon_min && (uint64_t)tot * a.abandon_den > (uint64_t)in_n * a.abandon_num;
-      bool df_go = false;
-      uint32_t bits = DF_MIN_BITS;
-      if (DF) {
-        // the dataflow path takes the survivors unless the level hands off or
-        // they exceed its buffers (then the round solver takes them); the
-        // write and read-only survivors form two lists
-        const uint64_t acc = a0 & ((1ull << LB_ACC_BITS) - 1);
-        const uint64_t acc_r = ra & ((1ull << LB_ACC_BITS) - 1);
-        const uint64_t acc_w = acc - acc_r;
-        const uint32_t m_r = (uint32_t)(ra >> LB_ACC_BITS), m_w = tot - m_r;
-        while (bits < 31 && (2ull << bits) < acc_w) bits++;  // <= 2 entries per bucket on average
-        const bool fits = acc_w <= d->cap_acc && acc_r <= d->cap_acc && tot <= d->cap_txn &&
-                          bits <= d->max_bits;
-        if (tot && !fits) handoff = true;
-        df_go = tot && !handoff;
-        if (blockIdx.x == 0) {
-          DfCtl* c = d->ctl;
-          c->m = df_go ? m_w : 0u;
-          c->acc = df_go ? (uint32_t)acc_w : 0u;
-          c->m_r = df_go ? m_r : 0u;
-          c->acc_r = df_go ? (uint32_t)acc_r : 0u;
-          c->bits = bits;
-          c->nchunks = df_go ? (uint32_t)((acc_w + 63) / 64) : 0u;
-          c->live = df_go ? 1u : 0u;
-          c->err = 0u;
-          c->nent = c->nwords = c->passes = 0u;
-        }
-      }
-      s_df = df_go ? 1u : 0u;
-      s_bits = bits;
-      // the dataflow path splits the lists itself (s_rb: the read-only base)
-      const bool split = a.ro_split && !handoff && !df_go;
+      const bool split = a.ro_split && !handoff;
       s_split = split ? 1u : 0u;
-      s_part[0][0] = (split || df_go) ? p0 - rp : p0;
-      s_rb = rp;
+      s_part[0][0] = split ? p0 - rp : p0;
       s_rnext = (uint32_t)(rp >> LB_ACC_BITS);
-      if (blockIdx.x == 0 && df_go) {
-        // no list for a next level: the dataflow solver decides the survivors
-        const uint64_t acc_w = (a0 - ra) & ((1ull << LB_ACC_BITS) - 1);
-        const uint32_t m_w = (uint32_t)((a0 - ra) >> LB_ACC_BITS);
-        a.lv_next->m = 0;
-        a.lv_next->acc = 0;
-        if (a.ro_split) *a.ro_count = 0u;
-        d->s_aoff[m_w] = (uint32_t)acc_w;
-        d->cfirst[0] = 0;
-        d->cfirst[(acc_w + 63) / 64] = m_w;
-      } else if (blockIdx.x == 0) {
+      if (blockIdx.x == 0) {
         const uint64_t keep = split ? a0 - ra : a0;
         const uint32_t kt = (uint32_t)(keep >> LB_ACC_BITS);
         const uint64_t acc = keep & ((1ull << LB_ACC_BITS) - 1);
@@ -1733,37 +1600,19 @@ __device__ inline void sw_compact_body(const SwFilterArgs& a, const DfArgs* d) {
     __syncthreads();
   }
   const bool split = s_split != 0;
-  const bool df = DF && s_df != 0;
-  if (df && blockIdx.x == 0)  // k_df_alloc's look-back words
-    for (uint32_t q = threadIdx.x; q < DF_SCAN_WG; q += SW_CHUNK) d->ctl->gran[q] = 0ull;
   if (dbg) dbg[1] = __builtin_amdgcn_s_memrealtime();
   if (wv == 0) {
     uint64_t run = s_part[0][0];
-    const bool sub = split || df;
     for (uint32_t c0 = t_lo; c0 < t_hi; c0 += 64) {
       const uint32_t q = c0 + lane;
-      const uint64_t v = (q < t_hi ? a.tcount[q] : 0ull) - ((sub && q < t_hi) ? a.rtcount[q] : 0ull);
+      const uint64_t v = (q < t_hi ? a.tcount[q] : 0ull) - ((split && q < t_hi) ? a.rtcount[q] : 0ull);
       uint64_t x = v;
 #pragma unroll
-      for (int dd = 1; dd < 64; dd <<= 1) {
-        const uint64_t y = __shfl_up(x, dd);
-        if (lane >= (uint32_t)dd) x += y;
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t y = __shfl_up(x, d);
+        if (lane >= (uint32_t)d) x += y;
       }
       if (q < t_hi) s_tb[q - t_lo] = run + x - v;
-      run += __shfl(x, 63);
-    }
-  } else if (DF && wv == 1 && df) {  // the read-only list's tile bases
-    uint64_t run = s_rb;
-    for (uint32_t c0 = t_lo; c0 < t_hi; c0 += 64) {
-      const uint32_t q = c0 + lane;
-      const uint64_t v = q < t_hi ? a.rtcount[q] : 0ull;
-      uint64_t x = v;
-#pragma unroll
-      for (int dd = 1; dd < 64; dd <<= 1) {
-        const uint64_t y = __shfl_up(x, dd);
-        if (lane >= (uint32_t)dd) x += y;
-      }
-      if (q < t_hi) s_tbr[q - t_lo] = run + x - v;
       run += __shfl(x, 63);
     }
   }
@@ -1780,20 +1629,10 @@ __device__ inline void sw_compact_body(const SwFilterArgs& a, const DfArgs* d) {
       const uint32_t wt = w0 + FW * i;
       const uint32_t pc = min(pos + min(wt, n64 - 1) * 64 + lane, m - 1);
       wordv[i] = wt < t_hi ? a.sflag[wt] : 0ull;
-      rwordv[i] = ((split || df) && wt < t_hi) ? a.rflag[wt] : 0ull;
+      rwordv[i] = (split && wt < t_hi) ? a.rflag[wt] : 0ull;
       sv[i] = a.in.off[pc];
       ev[i] = a.in.off[pc + 1];
       tv[i] = a.in.tid ? a.in.tid[pc] : pc;
-    }
-    if (DF && df) {  // uniform
-#pragma unroll
-      for (uint32_t i = 0; i < CB; i++) {
-        const uint32_t wt = w0 + FW * i;
-        const uint64_t ww = wordv[i] & ~rwordv[i];
-        if (ww) df_list_tile<false>(*d, ww, s_tb[wt - t_lo], sv[i], ev[i], tv[i], nnz, s_bits);
-        if (rwordv[i]) df_list_tile<true>(*d, rwordv[i], s_tbr[wt - t_lo], sv[i], ev[i], tv[i], nnz, s_bits);
-      }
-      continue;
     }
 #pragma unroll
     for (uint32_t i = 0; i < CB; i++) {
@@ -1866,12 +1705,6 @@ __device__ inline void sw_compact_body(const SwFilterArgs& a, const DfArgs* d) {
     __builtin_amdgcn_s_waitcnt(0);
     dbg[4] = __builtin_amdgcn_s_memrealtime();
   }
-}
-__global__ __launch_bounds__(SW_CHUNK) void k_sw_compact(SwFilterArgs a) {
-  sw_compact_body<false>(a, nullptr);
-}
-__global__ __launch_bounds__(SW_CHUNK) void k_df_list(SwFilterArgs a, DfArgs d) {
-  sw_compact_body<true>(a, &d);
 }
 
 // ---------------------------------------------------------------------------
@@ -1970,9 +1803,6 @@ void launch_sw_merge(const SwList& in, uint32_t P, uint32_t* xbuf, uint32_t xoff
 }
 void launch_sw_compact(const SwFilterArgs& a, unsigned grid, hipStream_t st) {
   k_sw_compact<<<grid ? grid : 1u, SW_CHUNK, 0, st>>>(a);
-}
-void launch_df_list(const SwFilterArgs& a, const DfArgs& d, unsigned grid, hipStream_t st) {
-  k_df_list<<<grid ? grid : 1u, SW_CHUNK, 0, st>>>(a, d);
 }
 
 }  // namespace dcc

@@ -159,9 +159,7 @@ int dcc_set_profiling(dcc_ctx* ctx, int enable);
 #define DCC_OPT_BATCH_MAX 2   /* max rounds enqueued between host synchronisations        */
 #define DCC_OPT_SOLVER 5      /* OCC solver: 0 auto (= 3), 1 fixed-point rounds only, 3 sweep
                                  (levels of serial passes + filters; hands lists that stop
-                                 shrinking to the round solver), 4 level 0 of the sweep, then
-                                 the dataflow solver over its survivors (single GPU; falls
-                                 back to 3 on its time limit)                                */
+                                 shrinking to the round solver)                              */
 #define DCC_OPT_SWEEP_LEVELS 6 /* sweep levels enqueued between host synchronisations (0:
                                   auto, 3 with DCC_OPT_RO_SPLIT, 4 without)                  */
 #define DCC_OPT_HIST_MERGE 7  /* device history: delta pairs above which the delta merges into

@@ -11,7 +11,7 @@ from kat_branches import cases, hist, rows
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("solver", [0, 1, 3, 4])
+@pytest.mark.parametrize("solver", [0, 1, 3])
 @pytest.mark.parametrize("name,b,c", cases("occ"), ids=[n for n, _, _ in cases("occ")])
 def test_occ_branch(engine, name, b, c, solver):
     hk, ht = hist(c)

@@ -1,6 +1,6 @@
 #!/bin/bash
 # rocprofv3 kernel stats + one epoch's timeline of the headline bench:
-#   TAG=x [ARGS="--solver 4"] tools/gpu_prof_head.sh
+#   TAG=x [ARGS="--solver 3"] tools/gpu_prof_head.sh
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/${TAG:-head}
