@@ -29,6 +29,9 @@ GROUP_NONE = 0xFFFFFFFF
 DEVICE_PTRS = 0x1
 OCC_APPEND_HISTORY = 0x2
 OCC_DEFER_FINISH = 0x8
+KEYS_U32 = 0x10
+ACCTYPE_2BIT = 0x20
+TN_U32 = 0x40
 MAAT_READ_AND_PREWRITE = 0x4
 ROW_NONE = 0xFFFFFFFFFFFFFFFF
 UNIQUE_ID_BYTES = 128
@@ -176,6 +179,8 @@ _SIGS = [
     ("dcc_set_profiling", C.c_int, [_P, C.c_int]),
     ("dcc_set_option", C.c_int, [_P, C.c_int, C.c_int64]),
     ("dcc_reserve", C.c_int, [_P, C.c_uint64, C.c_uint64]),
+    ("dcc_host_alloc", C.c_int, [_P, C.c_uint64, C.POINTER(C.c_void_p)]),
+    ("dcc_host_free", C.c_int, [_P, C.c_void_p]),
     ("dcc_comm_unique_id", C.c_int, [_P]),
     ("dcc_comm_init", C.c_int, [_P, C.c_int, C.c_int, _P]),
     ("dcc_comm_init_host", C.c_int, [_P, C.c_int, C.c_int, C.c_void_p, _P]),

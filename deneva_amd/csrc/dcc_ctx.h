@@ -131,6 +131,7 @@ struct dcc_ctx {
   DevBuf misc;                                   // counters / error words
   DevBuf part;                                   // per-block partial reductions
   DevBuf off, keys, acctype, start_tn, finish_tn, order;  // staged host batch
+  DevBuf nar_keys, nar_at, nar_tn;                 // compact forms before widening (host batches)
   DevBuf table;                                  // Slot[cap]
   DevBuf state, hasw, rc, stat;                  // per-txn bytes
   DevBuf cflag, bsum, tn;                        // commit-tn scan
@@ -187,7 +188,9 @@ struct dcc_ctx {
   int hist_prepare();  // merge policy + rebuild: call before a window check
   dcc::HistView hist_view() const;
   int hist_append_epoch(const DevBatch& d, const uint64_t* tn_dev, uint64_t nnz_w, uint64_t n_cw);
-  int check_batch(const dcc_batch* b);
+  // scan_offsets: the O(n) host pass over a host batch's offsets (the sweep
+  // validates them on the device instead, inside its level-0 launch)
+  int check_batch(const dcc_batch* b, bool scan_offsets = true);
   int stage_batch(const dcc_batch* b, DevBatch& d);
   int device_prep(const DevBatch& d, uint32_t& maxlen, uint64_t& nnz_w, uint64_t p = 0,
                   uint64_t* nnz_w_prefix = nullptr);

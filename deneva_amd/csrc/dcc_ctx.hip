@@ -243,7 +243,7 @@ std::vector<DevBuf*> dcc_ctx::all_bufs() {
                             &mt_misc, &mt_slot, &mt_sval, &mt_slot2, &mt_sval2, &mt_sfl,
                             &mt_stx, &mt_txn, &mt_agg, &mt_sflB, &mt_stxB, &mt_k1, &mt_tcnt, &mt_ul, &ix_keys, &ix_ord, &ix_rows, &ix_cnt, &wv_buf, &ix_scr, &wv_hbuf, &wv_obuf,
                             &h_K[0], &h_K[1], &h_V[0], &h_V[1], &h_scr, &h_bsum,
-                            &fin_off, &fin_keys, &fin_at, &fin_state, &fin_hasw, &fin_rc, &fin_cnt,
+                            &nar_keys, &nar_at, &nar_tn, &fin_off, &fin_keys, &fin_at, &fin_state, &fin_hasw, &fin_rc, &fin_cnt,
                             &sh_off, &sh_keys, &sh_at, &sh_src, &sh_cnt, &sh_bsum, &sh_rc, &sh_tn, &sh_grp};
   for (auto& h : hs)
     for (DevBuf* b : {&h.fk, &h.ft, &h.skey, &h.stn, &h.hash}) v.push_back(b);
@@ -552,7 +552,7 @@ extern "C" uint64_t dcc_occ_get_tnc(const dcc_ctx* ctx) {
 }
 
 // ---------------------------------------------------------------- batch checks
-int dcc_ctx::check_batch(const dcc_batch* b) {
+int dcc_ctx::check_batch(const dcc_batch* b, bool scan_offsets) {
   if (!b) return fail(DCC_EINVAL, "null batch");
   if (b->n_txn == 0) return DCC_OK;
   if (!b->offsets || (b->nnz && (!b->keys || !b->acctype)))
@@ -568,7 +568,7 @@ int dcc_ctx::check_batch(const dcc_batch* b) {
     const uint32_t* o = b->offsets;
     if (o[0] != 0 || o[b->n_txn] != b->nnz)
       return fail(DCC_EINVAL, "batch: offsets[0] must be 0 and offsets[n_txn] == nnz");
-    for (uint64_t t = 0; t < b->n_txn; t++) {
+    for (uint64_t t = 0; scan_offsets && t < b->n_txn; t++) {
       if (o[t + 1] < o[t]) return fail(DCC_EINVAL, "batch: offsets decrease at txn %llu",
                                        (unsigned long long)t);
       if (o[t + 1] - o[t] > MAX_TXN_LEN)
@@ -580,11 +580,20 @@ int dcc_ctx::check_batch(const dcc_batch* b) {
 }
 
 // Upload a host batch into ctx buffers (or alias a device batch); fills `d`.
+// A host batch is copied to the context's device buffers (asynchronously on
+// the engine stream: from pinned memory, dcc_host_alloc, at DMA speed); a
+// device batch is read in place.  Compact forms (DCC_KEYS_U32,
+// DCC_ACCTYPE_2BIT, DCC_TN_U32) move their narrow arrays and are widened on
+// the device (k_widen) into the context's buffers, so every engine below sees
+// u64 keys, byte access types and u64 timestamps.
 int dcc_ctx::stage_batch(const dcc_batch* b, DevBatch& d) {
   dcc_ctx* ctx = this;
   d.n = b->n_txn;
   d.nnz = b->nnz;
-  if (b->flags & DCC_DEVICE_PTRS) {
+  const bool dev = (b->flags & DCC_DEVICE_PTRS) != 0;
+  const bool k32 = (b->flags & DCC_KEYS_U32) != 0, a2 = (b->flags & DCC_ACCTYPE_2BIT) != 0,
+             t32 = (b->flags & DCC_TN_U32) != 0;
+  if (dev && !k32 && !a2 && !t32) {
     d.off = b->offsets;
     d.keys = b->keys;
     d.acctype = b->acctype;
@@ -593,32 +602,113 @@ int dcc_ctx::stage_batch(const dcc_batch* b, DevBatch& d) {
     d.order = b->order;
     return DCC_OK;
   }
-  CR(off.ensure(this, (d.n + 1) * 4, "offsets"));
+  const hipMemcpyKind kind = dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+  WidenArgs w{};
+  w.nnz = d.nnz;
+  w.n = d.n;
+  // offsets: never compact (read in place from a device batch)
+  if (dev) {
+    d.off = b->offsets;
+  } else {
+    CR(off.ensure(this, (d.n + 1) * 4, "offsets"));
+    CK(hipMemcpyAsync(off.p, b->offsets, (d.n + 1) * 4, kind, stream));
+    d.off = (const uint32_t*)off.p;
+  }
   CR(keys.ensure(this, std::max<uint64_t>(8, d.nnz * 8), "keys"));
   CR(acctype.ensure(this, std::max<uint64_t>(16, d.nnz), "acctype"));
-  CK(hipMemcpyAsync(off.p, b->offsets, (d.n + 1) * 4, hipMemcpyHostToDevice, stream));
-  if (d.nnz) {
-    CK(hipMemcpyAsync(keys.p, b->keys, d.nnz * 8, hipMemcpyHostToDevice, stream));
-    CK(hipMemcpyAsync(acctype.p, b->acctype, d.nnz, hipMemcpyHostToDevice, stream));
-  }
-  d.off = (const uint32_t*)off.p;
   d.keys = (const uint64_t*)keys.p;
   d.acctype = (const uint8_t*)acctype.p;
+  if (d.nnz) {
+    if (k32) {
+      const void* src = b->keys;
+      if (!dev) {
+        CR(nar_keys.ensure(this, d.nnz * 4, "compact keys"));
+        CK(hipMemcpyAsync(nar_keys.p, b->keys, d.nnz * 4, kind, stream));
+        src = nar_keys.p;
+      }
+      w.k32 = (const uint32_t*)src;
+      w.k64 = (uint64_t*)keys.p;
+    } else if (dev) {
+      d.keys = b->keys;
+    } else {
+      CK(hipMemcpyAsync(keys.p, b->keys, d.nnz * 8, kind, stream));
+    }
+    if (a2) {
+      const uint64_t pb = (d.nnz + 3) / 4;
+      const void* src = b->acctype;
+      if (!dev) {
+        CR(nar_at.ensure(this, pb + 16, "compact access types"));
+        CK(hipMemcpyAsync(nar_at.p, b->acctype, pb, kind, stream));
+        src = nar_at.p;
+      }
+      w.a2 = (const uint8_t*)src;
+      w.a8 = (uint8_t*)acctype.p;
+    } else if (dev) {
+      d.acctype = b->acctype;
+    } else {
+      CK(hipMemcpyAsync(acctype.p, b->acctype, d.nnz, kind, stream));
+    }
+  }
   d.start_tn = d.finish_tn = nullptr;
   if (b->start_tn) {
     CR(start_tn.ensure(this, d.n * 8, "start_tn"));
     CR(finish_tn.ensure(this, d.n * 8, "finish_tn"));
-    CK(hipMemcpyAsync(start_tn.p, b->start_tn, d.n * 8, hipMemcpyHostToDevice, stream));
-    CK(hipMemcpyAsync(finish_tn.p, b->finish_tn, d.n * 8, hipMemcpyHostToDevice, stream));
     d.start_tn = (const uint64_t*)start_tn.p;
     d.finish_tn = (const uint64_t*)finish_tn.p;
+    if (t32) {
+      const void *s0 = b->start_tn, *f0 = b->finish_tn;
+      if (!dev) {
+        CR(nar_tn.ensure(this, d.n * 8 + 16, "compact timestamps"));
+        CK(hipMemcpyAsync(nar_tn.p, b->start_tn, d.n * 4, kind, stream));
+        CK(hipMemcpyAsync((char*)nar_tn.p + d.n * 4, b->finish_tn, d.n * 4, kind, stream));
+        s0 = nar_tn.p;
+        f0 = (const char*)nar_tn.p + d.n * 4;
+      }
+      w.s32 = (const uint32_t*)s0;
+      w.f32 = (const uint32_t*)f0;
+      w.s64 = (uint64_t*)start_tn.p;
+      w.f64 = (uint64_t*)finish_tn.p;
+    } else if (dev) {
+      d.start_tn = b->start_tn;
+      d.finish_tn = b->finish_tn;
+    } else {
+      CK(hipMemcpyAsync(start_tn.p, b->start_tn, d.n * 8, kind, stream));
+      CK(hipMemcpyAsync(finish_tn.p, b->finish_tn, d.n * 8, kind, stream));
+    }
   }
   d.order = nullptr;
   if (b->order) {
-    CR(order.ensure(this, d.n * 8, "order"));
-    CK(hipMemcpyAsync(order.p, b->order, d.n * 8, hipMemcpyHostToDevice, stream));
-    d.order = (const uint64_t*)order.p;
+    if (dev) {
+      d.order = b->order;
+    } else {
+      CR(order.ensure(this, d.n * 8, "order"));
+      CK(hipMemcpyAsync(order.p, b->order, d.n * 8, kind, stream));
+      d.order = (const uint64_t*)order.p;
+    }
   }
+  if (w.k32 || w.a2 || w.s32) {
+    launch_widen(w, n_cu, stream);
+    CK(hipGetLastError());
+  }
+  return DCC_OK;
+}
+
+extern "C" int dcc_host_alloc(dcc_ctx* ctx, uint64_t bytes, void** out) {
+  if (!ctx || !out) return DCC_EINVAL;
+  *out = nullptr;
+  if (!bytes) return DCC_OK;
+  const hipError_t e = hipHostMalloc(out, bytes, hipHostMallocDefault);
+  if (e != hipSuccess) {
+    *out = nullptr;
+    return ctx->fail(DCC_ENOMEM, "hipHostMalloc(%llu): %s", (unsigned long long)bytes, hipGetErrorString(e));
+  }
+  return DCC_OK;
+}
+
+// ctx may be NULL (memory outliving its context)
+extern "C" int dcc_host_free(dcc_ctx* ctx, void* p) {
+  if (p && hipHostFree(p) != hipSuccess)
+    return ctx ? ctx->fail(DCC_EINVAL, "dcc_host_free: not a dcc_host_alloc pointer") : DCC_EINVAL;
   return DCC_OK;
 }
 

@@ -39,9 +39,13 @@
 #include <condition_variable>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #include <map>
 #include <mutex>
+#include <new>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "dcc.h"
@@ -51,6 +55,78 @@ namespace dcc_host {
 struct Access {   // one entry of a txn's access list
   uint64_t key;   // canonical row key
   uint8_t type;   // access_t: DCC_RD / DCC_WR / DCC_XP / DCC_SCAN
+};
+
+// A growable array in pinned host memory (dcc_host_alloc): the epoch's CSR is
+// built in place, so the engine's H2D copy runs at DMA speed with no staging
+// copy.  Falls back to ordinary memory if pinning fails (slower copy, same
+// result).
+template <class T>
+class PinnedVec {
+ public:
+  explicit PinnedVec(dcc_ctx* ctx = nullptr) : ctx_(ctx) {}
+  ~PinnedVec() { release(); }
+  PinnedVec(const PinnedVec&) = delete;
+  PinnedVec& operator=(const PinnedVec&) = delete;
+  PinnedVec(PinnedVec&& o) noexcept { take(o); }
+  PinnedVec& operator=(PinnedVec&& o) noexcept {
+    if (this != &o) {
+      release();
+      take(o);
+    }
+    return *this;
+  }
+  void push_back(T v) {
+    if (n_ == cap_) grow(n_ ? 2 * n_ : 4096);
+    p_[n_++] = v;
+  }
+  void resize(size_t n) {
+    if (n > cap_) grow(n);
+    n_ = n;
+  }
+  void clear() { n_ = 0; }
+  size_t size() const { return n_; }
+  T* data() { return p_; }
+  const T* data() const { return p_; }
+  T& operator[](size_t i) { return p_[i]; }
+  const T& operator[](size_t i) const { return p_[i]; }
+  T& back() { return p_[n_ - 1]; }
+
+ private:
+  void grow(size_t cap) {
+    void* q = nullptr;
+    bool pinned = ctx_ && dcc_host_alloc(ctx_, cap * sizeof(T), &q) == DCC_OK && q;
+    if (!pinned) {
+      q = std::malloc(cap * sizeof(T));
+      if (!q) throw std::bad_alloc();
+    }
+    if (n_) std::memcpy(q, p_, n_ * sizeof(T));
+    release();
+    p_ = (T*)q;
+    cap_ = cap;
+    pinned_ = pinned;
+  }
+  void release() {
+    if (p_) {
+      if (pinned_) (void)dcc_host_free(ctx_, p_);
+      else std::free(p_);
+    }
+    p_ = nullptr;
+    cap_ = 0;
+  }
+  void take(PinnedVec& o) {
+    ctx_ = o.ctx_;
+    p_ = o.p_;
+    n_ = o.n_;
+    cap_ = o.cap_;
+    pinned_ = o.pinned_;
+    o.p_ = nullptr;
+    o.n_ = o.cap_ = 0;
+  }
+  dcc_ctx* ctx_ = nullptr;
+  T* p_ = nullptr;
+  size_t n_ = 0, cap_ = 0;
+  bool pinned_ = false;
 };
 
 class OccEpoch {
@@ -69,7 +145,9 @@ class OccEpoch {
     double device_ms = 0, wall_ms = 0;
   };
 
-  OccEpoch(dcc_ctx* ctx, const Options& o) : ctx_(ctx), opt_(o) { open_.off.push_back(0); }
+  OccEpoch(dcc_ctx* ctx, const Options& o) : ctx_(ctx), opt_(o), open_(ctx), fly_(ctx) {
+    open_.off.push_back(0);
+  }
 
   // TxnManager::validate for CC_ALG == OCC: DCC_RC_RCOK or DCC_RC_ABORT in *rc.
   // start_tn / finish_tn are read only with Options::ts_window.
@@ -79,15 +157,9 @@ class OccEpoch {
     std::unique_lock<std::mutex> lk(mu_);
     const uint64_t ep = epoch_;
     const uint64_t slot = open_.off.size() - 1;
-    for (size_t i = 0; i < n; i++) {
-      open_.keys.push_back(acc[i].key);
-      open_.at.push_back(acc[i].type);
-    }
-    open_.off.push_back((uint32_t)open_.keys.size());
-    if (opt_.ts_window) {
-      open_.start.push_back(start_tn);
-      open_.finish.push_back(finish_tn);
-    }
+    for (size_t i = 0; i < n; i++) open_.add(acc[i].key, acc[i].type);
+    open_.off.push_back((uint32_t)open_.nnz);
+    if (opt_.ts_window) open_.add_tn(start_tn, finish_tn);
     if (slot == 0) opened_ = std::chrono::steady_clock::now();
     // waiting for the OPEN epoch: a worker blocked on the in-flight one will
     // add its next txn to the open epoch once that one is decided, so it does
@@ -137,11 +209,96 @@ class OccEpoch {
     int err = 0;
   };
 
-  struct Csr {  // an epoch's access sets
-    std::vector<uint32_t> off;
-    std::vector<uint64_t> keys;
-    std::vector<uint8_t> at;
-    std::vector<uint64_t> start, finish;
+  // An epoch's access sets in pinned memory and in the engine's compact
+  // transfer form (dcc.h): u32 keys while every key fits (widened in place on
+  // the first one that does not), 2-bit access types four per byte, u32
+  // timestamps while they fit -- a third of the full-width PCIe bytes for YCSB.
+  struct Csr {
+    explicit Csr(dcc_ctx* c)
+        : off(c), k32(c), k64(c), at2(c), s32(c), f32(c), s64(c), f64(c) {}
+    PinnedVec<uint32_t> off;
+    PinnedVec<uint32_t> k32;
+    PinnedVec<uint64_t> k64;
+    PinnedVec<uint8_t> at2;
+    PinnedVec<uint32_t> s32, f32;
+    PinnedVec<uint64_t> s64, f64;
+    uint64_t nnz = 0, ntn = 0;
+    bool wide = false, tn_wide = false;
+
+    void add(uint64_t key, uint8_t type) {
+      if (!wide && (key >> 32)) {
+        k64.resize(k32.size());
+        for (size_t i = 0; i < k32.size(); i++) k64[i] = k32[i];
+        wide = true;
+      }
+      if (wide) k64.push_back(key);
+      else k32.push_back((uint32_t)key);
+      if ((nnz & 3) == 0) at2.push_back(0);
+      at2.back() = (uint8_t)(at2.back() | ((type & 3u) << (2 * (nnz & 3))));
+      nnz++;
+    }
+    void add_tn(uint64_t s, uint64_t f) {
+      if (!tn_wide && ((s | f) >> 32)) {
+        s64.resize(s32.size());
+        f64.resize(f32.size());
+        for (size_t i = 0; i < s32.size(); i++) {
+          s64[i] = s32[i];
+          f64[i] = f32[i];
+        }
+        tn_wide = true;
+      }
+      if (tn_wide) {
+        s64.push_back(s);
+        f64.push_back(f);
+      } else {
+        s32.push_back((uint32_t)s);
+        f32.push_back((uint32_t)f);
+      }
+      ntn++;
+    }
+    void clear() {
+      off.clear();
+      off.push_back(0);
+      k32.clear();
+      k64.clear();
+      at2.clear();
+      s32.clear();
+      f32.clear();
+      s64.clear();
+      f64.clear();
+      nnz = ntn = 0;
+      wide = tn_wide = false;
+    }
+    void to_batch(dcc_batch& b) const {
+      b.n_txn = off.size() - 1;
+      b.nnz = nnz;
+      b.offsets = off.data();
+      b.keys = wide ? k64.data() : (const uint64_t*)(const void*)k32.data();
+      b.acctype = at2.data();
+      b.flags |= DCC_ACCTYPE_2BIT | (wide ? 0u : DCC_KEYS_U32);
+      if (ntn) {
+        b.start_tn = tn_wide ? s64.data() : (const uint64_t*)(const void*)s32.data();
+        b.finish_tn = tn_wide ? f64.data() : (const uint64_t*)(const void*)f32.data();
+        b.flags |= tn_wide ? 0u : DCC_TN_U32;
+      }
+    }
+    // full-width copies for a .dccb capture (the file holds the engine's
+    // canonical layout)
+    void full(std::vector<uint64_t>& keys, std::vector<uint8_t>& at, std::vector<uint64_t>& st,
+              std::vector<uint64_t>& ft) const {
+      keys.resize(nnz);
+      at.resize(nnz);
+      for (uint64_t x = 0; x < nnz; x++) {
+        keys[x] = wide ? k64[x] : k32[x];
+        at[x] = (uint8_t)((at2[x >> 2] >> (2 * (x & 3))) & 3u);
+      }
+      st.resize(ntn);
+      ft.resize(ntn);
+      for (uint64_t t = 0; t < ntn; t++) {
+        st[t] = tn_wide ? s64[t] : s32[t];
+        ft[t] = tn_wide ? f64[t] : f32[t];
+      }
+    }
   };
 
   // decide the open epoch: it moves to the in-flight buffer, the mutex is
@@ -149,11 +306,7 @@ class OccEpoch {
   // Called with lk held and no call in flight; returns with lk held.
   int close(std::unique_lock<std::mutex>& lk) {
     std::swap(open_, fly_);
-    open_.off.assign(1, 0);
-    open_.keys.clear();
-    open_.at.clear();
-    open_.start.clear();
-    open_.finish.clear();
+    open_.clear();
     const uint64_t id = epoch_++;
     open_waiting_ = 0;  // they wait for the closed epoch now
     busy_ = true;
@@ -163,16 +316,8 @@ class OccEpoch {
     d.rc.assign(n, DCC_RC_ABORT);
     d.readers = n;
     dcc_batch b{};
-    b.n_txn = n;
-    b.nnz = fly_.keys.size();
-    b.offsets = fly_.off.data();
-    b.keys = fly_.keys.data();
-    b.acctype = fly_.at.data();
-    if (opt_.ts_window) {
-      b.start_tn = fly_.start.data();
-      b.finish_tn = fly_.finish.data();
-      b.flags = DCC_OCC_APPEND_HISTORY;  // central_finish: commit tn + history
-    }
+    if (opt_.ts_window) b.flags = DCC_OCC_APPEND_HISTORY;  // central_finish: commit tn + history
+    fly_.to_batch(b);
     dcc_stats st{};
     const uint64_t tnc0 = dcc_occ_get_tnc(ctx_);
     const auto t0 = std::chrono::steady_clock::now();
@@ -189,7 +334,18 @@ class OccEpoch {
                (unsigned long long)id);
       // the epoch is decided (tnc and history advanced): a failed capture is
       // counted, never turned into aborts
-      cap_err = dcc_file_write(path, &fi, &b, d.rc.data(), nullptr, nullptr, nullptr) != DCC_OK;
+      std::vector<uint64_t> fk, fs, ff;
+      std::vector<uint8_t> fa;
+      fly_.full(fk, fa, fs, ff);
+      dcc_batch fb = b;
+      fb.flags &= ~DCC_COMPACT_FLAGS;
+      fb.keys = fk.data();
+      fb.acctype = fa.data();
+      if (fly_.ntn) {
+        fb.start_tn = fs.data();
+        fb.finish_tn = ff.data();
+      }
+      cap_err = dcc_file_write(path, &fi, &fb, d.rc.data(), nullptr, nullptr, nullptr) != DCC_OK;
     }
     if (opt_.overlap) lk.lock();
     busy_ = false;

@@ -711,7 +711,10 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   // key-sharded across ranks: this rank holds only its keys
   const bool sh = comm_ranks() > 1;
   const auto t_wall0 = std::chrono::steady_clock::now();
-  CR(check_batch(b));
+  // the one-GPU sweep validates a host batch's offsets on the device (its
+  // level-0 launch, prep_body; every kernel before clamps its indices), so the
+  // O(n) host pass is skipped there
+  CR(check_batch(b, !(use_sweep() && !sh)));
   const bool dev_out = (b->flags & DCC_DEVICE_PTRS) != 0;
   const bool defer = (b->flags & DCC_OCC_DEFER_FINISH) != 0;
   if (fin_pending)

@@ -405,6 +405,20 @@ void launch_sw_merge(const SwList& in, uint32_t P, uint32_t* xbuf, uint32_t xoff
                      uint32_t n_all, uint32_t* cnt, uint32_t* cur, uint32_t* moff,
                      uint64_t* mkeys, uint8_t* mat, bool export_only, hipStream_t st);
 
+// Compact transfer forms widened on the device (dcc_ctx::stage_batch): u32
+// keys -> u64, 2-bit packed access types -> bytes, u32 timestamps -> u64.
+// A null source skips that part.
+struct WidenArgs {
+  uint64_t n, nnz;
+  const uint32_t* k32;
+  uint64_t* k64;
+  const uint8_t* a2;
+  uint8_t* a8;
+  const uint32_t *s32, *f32;
+  uint64_t *s64, *f64;
+};
+void launch_widen(const WidenArgs& a, unsigned n_cu, hipStream_t st);
+
 // Several word fills in one launch (replaces a run of hipMemsetAsync calls,
 // each of which costs a dispatch and an idle gap on the stream).
 struct FillJob {

@@ -933,4 +933,45 @@ void launch_scatter(const uint8_t* sub_state, const uint32_t* sub_tid, const uin
   k_scatter<<<g ? g : 1, 256, 0, st>>>(sub_state, sub_tid, n_sub, state);
 }
 
+
+// --------------------------------------------------------------------------
+// k_widen: the compact transfer forms (dcc.h DCC_KEYS_U32 / DCC_ACCTYPE_2BIT /
+// DCC_TN_U32) back to the engine's layout.  Four accesses per thread and step
+// (one 16-B key load, two 16-B key stores, one packed type byte in, one 4-byte
+// type word out) when the arrays are 16-B aligned, else one.
+__global__ __launch_bounds__(256) void k_widen(WidenArgs a) {
+  const uint64_t tid = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  if (a.k32) {
+    const bool vec = (((uintptr_t)a.k32 | (uintptr_t)a.k64) & 15u) == 0;
+    const uint64_t n4 = vec ? a.nnz / 4 : 0;
+    for (uint64_t q = tid; q < n4; q += stride) {
+      const uint4 v = ((const uint4*)a.k32)[q];
+      ((uint4*)a.k64)[2 * q] = make_uint4(v.x, 0u, v.y, 0u);
+      ((uint4*)a.k64)[2 * q + 1] = make_uint4(v.z, 0u, v.w, 0u);
+    }
+    for (uint64_t x = 4 * n4 + tid; x < a.nnz; x += stride) a.k64[x] = a.k32[x];
+  }
+  if (a.a2) {
+    const bool vec = ((uintptr_t)a.a8 & 3u) == 0;
+    const uint64_t n4 = vec ? a.nnz / 4 : 0;
+    for (uint64_t q = tid; q < n4; q += stride) {
+      const uint32_t p = a.a2[q];
+      ((uint32_t*)a.a8)[q] = (p & 3u) | ((p >> 2) & 3u) << 8 | ((p >> 4) & 3u) << 16 | ((p >> 6) & 3u) << 24;
+    }
+    for (uint64_t x = 4 * n4 + tid; x < a.nnz; x += stride) a.a8[x] = (a.a2[x >> 2] >> (2 * (x & 3))) & 3u;
+  }
+  if (a.s32)
+    for (uint64_t t = tid; t < a.n; t += stride) {
+      a.s64[t] = a.s32[t];
+      a.f64[t] = a.f32[t];
+    }
+}
+
+void launch_widen(const WidenArgs& a, unsigned n_cu, hipStream_t st) {
+  const uint64_t work = std::max<uint64_t>(a.nnz / 4, a.n);
+  const uint64_t g = std::min<uint64_t>((work + 255) / 256, 8ull * n_cu);
+  k_widen<<<(unsigned)std::max<uint64_t>(g, 1), 256, 0, st>>>(a);
+}
+
 }  // namespace dcc

@@ -140,7 +140,7 @@ int dcc_ctx::shard_stage(const dcc_batch* b, uint32_t rank, uint32_t R, dcc_batc
   CK(hipMemcpyAsync(hmisc, bs + nb, 4, hipMemcpyDeviceToHost, stream));
   CK(hipStreamSynchronize(stream));
   sb = *b;
-  sb.flags = b->flags | DCC_DEVICE_PTRS;
+  sb.flags = (b->flags | DCC_DEVICE_PTRS) & ~DCC_COMPACT_FLAGS;  // stage_batch widened them
   sb.n_txn = n;
   sb.nnz = *(const uint32_t*)hmisc;
   sb.offsets = (const uint32_t*)sh_off.p;

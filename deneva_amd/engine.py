@@ -31,6 +31,18 @@ def _ptr(a) -> Optional[int]:
     return int(a.data_ptr())  # torch tensor
 
 
+def _itemsize(a) -> int:
+    return int(a.itemsize) if isinstance(a, np.ndarray) else int(a.element_size())
+
+
+def pack_acctype(at) -> np.ndarray:
+    """access_t bytes -> 2-bit codes, four per byte (DCC_ACCTYPE_2BIT)."""
+    at = np.asarray(at, np.uint8)
+    pad = np.zeros((-at.size) % 4, np.uint8)
+    q = np.concatenate([at, pad]).reshape(-1, 4) & 3
+    return (q[:, 0] | (q[:, 1] << 2) | (q[:, 2] << 4) | (q[:, 3] << 6)).astype(np.uint8)
+
+
 def _is_device(a) -> bool:
     return a is not None and not isinstance(a, np.ndarray) and bool(getattr(a, "is_cuda", False))
 
@@ -70,6 +82,13 @@ class EpochBatch:
         b.finish_tn = _ptr(self.finish_tn)
         b.order = _ptr(self.order)
         b.flags = flags | (_abi.DEVICE_PTRS if self.on_device else 0)
+        # compact transfer forms (dcc.h): 4-byte keys / timestamps, packed types
+        if _itemsize(self.keys) == 4:
+            b.flags |= _abi.KEYS_U32
+        if self.meta.get("acctype_2bit"):
+            b.flags |= _abi.ACCTYPE_2BIT
+        if self.start_tn is not None and _itemsize(self.start_tn) == 4:
+            b.flags |= _abi.TN_U32
         return b
 
     def to_torch(self, device="cuda"):
@@ -140,6 +159,45 @@ class Engine:
 
     def reserve(self, max_txn: int, max_nnz: int) -> None:
         _check(lib.dcc_reserve(self._h, max_txn, max_nnz), self._h)
+
+    def host_empty(self, n: int, dtype) -> np.ndarray:
+        """A numpy array in pinned host memory (dcc_host_alloc): host batches
+        and outputs in it move at DMA speed with no staging copy.  Freed with
+        the array."""
+        import weakref
+        dt = np.dtype(dtype)
+        nbytes = max(int(n), 1) * dt.itemsize
+        p = C.c_void_p()
+        _check(lib.dcc_host_alloc(self._h, nbytes, C.byref(p)), self._h)
+        buf = (C.c_uint8 * nbytes).from_address(p.value)
+        arr = np.frombuffer(buf, dtype=dt, count=max(int(n), 1))[:int(n)]
+        # freed with the buffer (no context needed: the engine may be gone)
+        weakref.finalize(buf, lib.dcc_host_free, None, p.value)
+        return arr
+
+    def compact_host_batch(self, b: "EpochBatch") -> "EpochBatch":
+        """The batch in pinned host memory and its compact transfer form:
+        u32 keys when every key fits, 2-bit access types, u32 timestamps when
+        they fit (dcc.h DCC_KEYS_U32 / DCC_ACCTYPE_2BIT / DCC_TN_U32) -- what a
+        host shim builds directly (OccEpoch) to cut the PCIe bytes."""
+        def pin(a, dtype):
+            a = np.asarray(a)
+            out = self.host_empty(a.size, dtype)
+            out[...] = a
+            return out
+        keys = np.asarray(b.keys, np.uint64)
+        k = pin(keys, np.uint32) if (keys.size == 0 or int(keys.max()) < (1 << 32)) else pin(keys, np.uint64)
+        at = pin(pack_acctype(b.acctype), np.uint8)
+        st = ft = None
+        if b.start_tn is not None:
+            big = max(int(np.max(b.start_tn, initial=0)), int(np.max(b.finish_tn, initial=0)))
+            dt = np.uint32 if big < (1 << 32) else np.uint64
+            st, ft = pin(b.start_tn, dt), pin(b.finish_tn, dt)
+        od = None if b.order is None else pin(b.order, np.uint64)
+        meta = dict(b.meta)
+        meta["acctype_2bit"] = True
+        meta["nnz"] = int(keys.size)
+        return EpochBatch(pin(b.offsets, np.uint32), k, at, st, ft, od, meta)
 
     # ------------------------------------------------------------ OCC
     def occ_validate_epoch(self, batch: EpochBatch, want_tn: bool = False,

@@ -77,6 +77,16 @@ extern "C" {
                                      worker_thread.cpp:286-297, occ.cpp:248-294).  Not
                                      with DCC_OCC_APPEND_HISTORY or out_commit_tn. */
 
+/* Compact transfer forms (host or device batches; widened on the device before
+ * any kernel reads them).  They shrink what a host batch moves over PCIe:
+ * u32 keys halve the largest array when the key universe fits (YCSB row ids),
+ * packed access types and u32 timestamps cut the rest. */
+#define DCC_KEYS_U32 0x10u      /* keys points to uint32_t keys                            */
+#define DCC_ACCTYPE_2BIT 0x20u  /* acctype holds 2-bit access types, four per byte: access x
+                                   in bits 2(x%4)..2(x%4)+1 of byte x/4                     */
+#define DCC_TN_U32 0x40u        /* start_tn / finish_tn point to uint32_t timestamps        */
+#define DCC_COMPACT_FLAGS (DCC_KEYS_U32 | DCC_ACCTYPE_2BIT | DCC_TN_U32)
+
 /* One epoch as a CSR of per-transaction access lists in capture order
  * (Access list of TxnManager, system/txn.h:39-70; txn.cpp:818-847). */
 typedef struct dcc_batch {
@@ -175,6 +185,10 @@ int dcc_set_profiling(dcc_ctx* ctx, int enable);
 int dcc_set_option(dcc_ctx* ctx, int option, int64_t value);
 /* Pre-size device workspaces so a later call performs no allocation. */
 int dcc_reserve(dcc_ctx* ctx, uint64_t max_txn, uint64_t max_nnz);
+/* Pinned (page-locked) host memory for batches and outputs: a host batch in it
+ * is copied at DMA speed with no staging copy.  Free with dcc_host_free. */
+int dcc_host_alloc(dcc_ctx* ctx, uint64_t bytes, void** out);
+int dcc_host_free(dcc_ctx* ctx, void* p);  /* ctx may be NULL */
 
 /* ------------------------------------------------------- multi-GPU     */
 /* Key sharding across the GPUs of one node, one process per GPU

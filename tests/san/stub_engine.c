@@ -4,6 +4,7 @@
  * shim's mutex / condition-variable epoch map run under ThreadSanitizer and
  * AddressSanitizer on a machine without a GPU.  Never part of libdcc. */
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 #include <time.h>
 
@@ -45,9 +46,40 @@ int dcc_occ_validate_epoch(dcc_ctx* ctx, const dcc_batch* b, uint8_t* out_rc,
     tn = buf;
   }
   (void)tn_scratch;
-  int r = oracle_occ_hash(n, b->offsets, b->keys, b->acctype, b->start_tn, b->finish_tn, 0, NULL,
-                          NULL, &ctx->tnc, out_rc, tn);
+  /* the shim hands the engine its compact transfer form (dcc.h): widen it */
+  const uint64_t nnz = b->nnz;
+  uint64_t* keys = (uint64_t*)malloc((nnz + 1) * 8);
+  uint8_t* at = (uint8_t*)malloc(nnz + 1);
+  uint64_t* s_tn = b->start_tn ? (uint64_t*)malloc((n + 1) * 8) : NULL;
+  uint64_t* f_tn = b->start_tn ? (uint64_t*)malloc((n + 1) * 8) : NULL;
+  for (uint64_t x = 0; x < nnz; x++) {
+    keys[x] = (b->flags & DCC_KEYS_U32) ? ((const uint32_t*)(const void*)b->keys)[x] : b->keys[x];
+    at[x] = (b->flags & DCC_ACCTYPE_2BIT) ? (uint8_t)((b->acctype[x >> 2] >> (2 * (x & 3))) & 3u)
+                                          : b->acctype[x];
+  }
+  for (uint64_t t = 0; s_tn && t < n; t++) {
+    s_tn[t] = (b->flags & DCC_TN_U32) ? ((const uint32_t*)(const void*)b->start_tn)[t] : b->start_tn[t];
+    f_tn[t] = (b->flags & DCC_TN_U32) ? ((const uint32_t*)(const void*)b->finish_tn)[t] : b->finish_tn[t];
+  }
+  int r = oracle_occ_hash(n, b->offsets, keys, at, s_tn, f_tn, 0, NULL, NULL, &ctx->tnc, out_rc, tn);
+  free(keys);
+  free(at);
+  free(s_tn);
+  free(f_tn);
   if (st) memset(st, 0, sizeof *st);
   __atomic_fetch_sub(&inflight, 1, __ATOMIC_ACQ_REL);
   return r ? DCC_EIO : DCC_OK;
+}
+
+/* pinned host memory (dcc_host_alloc): plain malloc in the stub */
+int dcc_host_alloc(dcc_ctx* ctx, uint64_t bytes, void** out) {
+  (void)ctx;
+  if (!out) return DCC_EINVAL;
+  *out = bytes ? malloc(bytes) : NULL;
+  return (bytes && !*out) ? DCC_ENOMEM : DCC_OK;
+}
+int dcc_host_free(dcc_ctx* ctx, void* p) {
+  (void)ctx;
+  free(p);
+  return DCC_OK;
 }
