@@ -180,6 +180,7 @@ _SIGS = [
     ("dcc_set_option", C.c_int, [_P, C.c_int, C.c_int64]),
     ("dcc_reserve", C.c_int, [_P, C.c_uint64, C.c_uint64]),
     ("dcc_host_alloc", C.c_int, [_P, C.c_uint64, C.POINTER(C.c_void_p)]),
+    ("dcc_copy_bandwidth", C.c_int, [_P, C.c_uint64, C.c_int, C.POINTER(C.c_double)]),
     ("dcc_host_free", C.c_int, [_P, C.c_void_p]),
     ("dcc_comm_unique_id", C.c_int, [_P]),
     ("dcc_comm_init", C.c_int, [_P, C.c_int, C.c_int, _P]),

@@ -693,6 +693,28 @@ int dcc_ctx::stage_batch(const dcc_batch* b, DevBatch& d) {
   return DCC_OK;
 }
 
+extern "C" int dcc_copy_bandwidth(dcc_ctx* ctx, uint64_t bytes, int reps, double* gbps) {
+  if (!ctx || !gbps || bytes < 16 || reps < 1) return DCC_EINVAL;
+  if (ctx->multi) ctx = dcc_multi_sub(ctx, 0);
+  if (hipSetDevice(ctx->device) != hipSuccess) return DCC_ENODEV;
+  bytes &= ~15ull;
+  DevBuf a, b;
+  CR(a.ensure(ctx, bytes, "copy source"));
+  CR(b.ensure(ctx, bytes, "copy destination"));
+  CK(hipMemsetAsync(a.p, 1, bytes, ctx->stream));
+  // one launch of 8 workgroups per CU: every CU streams, loads in flight
+  const unsigned grid = (unsigned)ctx->n_cu * 8;
+  for (int i = 0; i < 2; i++) launch_copy16(a.p, b.p, bytes, grid, ctx->stream);
+  CK(hipEventRecord(ctx->ev0, ctx->stream));
+  for (int i = 0; i < reps; i++) launch_copy16(a.p, b.p, bytes, grid, ctx->stream);
+  CK(hipEventRecord(ctx->ev1, ctx->stream));
+  CK(hipEventSynchronize(ctx->ev1));
+  float ms = 0;
+  CK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+  *gbps = 2.0 * (double)bytes * reps / (ms * 1e-3) / 1e9;
+  return DCC_OK;
+}
+
 extern "C" int dcc_host_alloc(dcc_ctx* ctx, uint64_t bytes, void** out) {
   if (!ctx || !out) return DCC_EINVAL;
   *out = nullptr;

@@ -974,4 +974,25 @@ void launch_widen(const WidenArgs& a, unsigned n_cu, hipStream_t st) {
   k_widen<<<(unsigned)std::max<uint64_t>(g, 1), 256, 0, st>>>(a);
 }
 
+
+// --------------------------------------------------------------------------
+// k_copy16: the bandwidth reference (dcc_copy_bandwidth): 16 B per lane per
+// load, four loads in flight per thread before their stores, grid-stride.
+__global__ __launch_bounds__(256) void k_copy16(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                uint64_t n16) {
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  for (; q + 3 * stride < n16; q += 4 * stride) {
+    const uint4 a = src[q], b = src[q + stride], c = src[q + 2 * stride], d = src[q + 3 * stride];
+    dst[q] = a;
+    dst[q + stride] = b;
+    dst[q + 2 * stride] = c;
+    dst[q + 3 * stride] = d;
+  }
+  for (; q < n16; q += stride) dst[q] = src[q];
+}
+void launch_copy16(const void* src, void* dst, uint64_t bytes, unsigned grid, hipStream_t st) {
+  k_copy16<<<grid ? grid : 1u, 256, 0, st>>>((const uint4*)src, (uint4*)dst, bytes / 16);
+}
+
 }  // namespace dcc
