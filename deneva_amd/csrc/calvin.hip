@@ -34,6 +34,8 @@
 #include <chrono>
 #include <cstring>
 
+#include "calvin_bucket.h"
+#include "calvin_gl.h"
 #include "dcc.h"
 #include "dcc_ctx.h"
 #include "dcc_device.h"
@@ -56,7 +58,6 @@ using namespace dcc;
 
 namespace {
 
-constexpr uint32_t CV_SH = 0, CV_EX = 1, CV_NONE = 2;
 constexpr uint32_t NOPOS = 0xFFFFFFFFu;
 constexpr uint32_t CV_MAX_TXN = 1u << 25;  // value = txn:25 | j:6 | EX:1
 constexpr unsigned CV_PREP_BLOCKS = 1024;
@@ -538,23 +539,9 @@ __global__ __launch_bounds__(256) void k_cv_down(const K* __restrict__ sk,
 }
 
 // ---- the same scan when no wave levels are asked for: only the grant group
-// count is needed, so the state packs into one word -- segment start (bit 0),
-// first and last lock type of the run (2 bits each: SH, EX, NONE) and the
-// groups started since the segment's first request (27 bits) -- and the block
-// scans are wave shuffles instead of 10-word LDS trees.  Same monoid as Gs
-// restricted to (flag, ft, lt, cnt).
-__host__ __device__ constexpr uint32_t gl_pack(uint32_t flag, uint32_t ft, uint32_t lt, uint32_t cnt) {
-  return flag | (ft << 1) | (lt << 3) | (cnt << 5);
-}
-constexpr uint32_t GL_ID = gl_pack(0, CV_NONE, CV_NONE, 0);
-__device__ inline uint32_t gl_combine(uint32_t A, uint32_t B) {
-  if (B & 1u) return B;
-  const uint32_t aft = (A >> 1) & 3u, alt = (A >> 3) & 3u, bft = (B >> 1) & 3u, blt = (B >> 3) & 3u;
-  const bool bnd = alt != CV_NONE && bft != CV_NONE && (alt == CV_EX || bft == CV_EX);
-  const uint32_t ft = aft != CV_NONE ? aft : bft;
-  const uint32_t lt = blt != CV_NONE ? blt : alt;
-  return (A & 1u) | (ft << 1) | (lt << 3) | (((A >> 5) + (B >> 5) + (bnd ? 1u : 0u)) << 5);
-}
+// count is needed, so the state packs into one word (calvin_gl.h) and the
+// block scans are wave shuffles instead of 10-word LDS trees.  Same monoid as
+// Gs restricted to (flag, ft, lt, cnt).
 template <typename K>
 __device__ inline uint32_t gl_element(uint64_t p, K key, uint32_t val, K pkey, uint32_t pval) {
   const bool start = p == 0 || key != pkey;
@@ -563,27 +550,6 @@ __device__ inline uint32_t gl_element(uint64_t p, K key, uint32_t val, K pkey, u
   if ((val >> 7) == (pval >> 7)) return GL_ID;  // duplicate row of the same txn
   return gl_pack(0, typ, typ, 0);
 }
-// inclusive scan of a wave, then the block's exclusive prefix of each thread
-// (4 waves; the wave totals through LDS); returns the exclusive prefix and
-// the block total
-__device__ inline uint32_t gl_block_excl(uint32_t v, uint32_t* s_w, uint32_t& total) {
-  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-  uint32_t x = v;
-#pragma unroll
-  for (uint32_t d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(x, d);
-    if (lane >= d) x = gl_combine(y, x);
-  }
-  if (lane == 63) s_w[w] = x;
-  __syncthreads();
-  uint32_t wp = GL_ID;
-  for (uint32_t q = 0; q < w; q++) wp = gl_combine(wp, s_w[q]);
-  total = gl_combine(gl_combine(gl_combine(s_w[0], s_w[1]), s_w[2]), s_w[3]);
-  const uint32_t ex_in = __shfl_up(x, 1);
-  __syncthreads();
-  return gl_combine(wp, lane ? ex_in : GL_ID);
-}
-
 template <typename K>
 __global__ __launch_bounds__(256) void k_cv_up_l(const K* __restrict__ sk,
                                                  const uint32_t* __restrict__ sv, uint64_t m,
@@ -1155,6 +1121,14 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint3
   static_assert(sizeof(KeyPack) <= sizeof(CvGraphKey::kp), "key image");
   const bool cv_graph_ok = !profiling && !waves && nh == 0 && comm_ranks() == 1 &&
                            !getenv("DCC_NO_GRAPH");
+  // the bucket path (calvin_bucket.h) for large epochs of uniform txns;
+  // DCC_CV_BUCKET=0 keeps the global sort + scan, =1 takes the bucket path at
+  // every size it applies to
+  const char* cbe = getenv("DCC_CV_BUCKET");
+  const int cb_mode = cbe ? atoi(cbe) : -1;
+  CbPlan cbp{};
+  const bool use_cb = d.nnz && cb_mode != 0 && !waves && nh == 0 && ulen &&
+                      (cb_mode == 1 || d.nnz >= CV_PUT_MIN) && cb_plan(d.n, d.nnz, ulen, kp.bits, &cbp);
   CvGraphKey gk;
   memset(&gk, 0, sizeof gk);
   gk.off = d.off;
@@ -1168,6 +1142,7 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint3
   gk.gen = buf_gen;
   gk.ulen = ulen;
   gk.have_seq = have_seq ? 1u : 0u;
+  gk.bucket = use_cb ? 1u : 0u;
   memcpy(gk.kp, &kp, sizeof kp);
   memcpy(gk.op, &op, sizeof op);
   const bool cv_replay = cv_graph_ok && cv_graph_exec && !memcmp(&gk, &cv_graph_key, sizeof gk);
@@ -1235,7 +1210,15 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint3
   CK(hipGetLastError());
 
   // ---- requests in sequence order -> sorted by row -> group scan
-  if (d.nnz) {
+  if (use_cb) {
+    CR(cb_e.ensure(this, cbp.elem_bytes, "calvin bucket requests"));
+    CR(cb_out.ensure(this, cbp.out_bytes, "calvin bucket pairs"));
+    CR(cb_cnt.ensure(this, cbp.cnt_bytes, "calvin bucket counts"));
+    CR(cb_small.ensure(this, cbp.small_bytes, "calvin bucket totals"));
+    const CbArgs ca{d.keys, d.acctype, seq, d.n, d.nnz, ulen, kp, (uint64_t*)cb_e.p,
+                    (uint64_t*)cb_out.p, (uint32_t*)cb_cnt.p, (uint32_t*)cb_small.p, grp_dev, rc_dev};
+    CK(cb_run(cbp, ca, stream, profiling ? pev[1] : nullptr, profiling ? pev[2] : nullptr));
+  } else if (d.nnz) {
     if (kp.bits <= 32)
       CR(calvin_sort_and_scan<uint32_t>(this, d, seq, off2, kp, so, hkeys, hat, nh, profiling));
     else
@@ -1244,8 +1227,13 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint3
     CK(hipEventRecord(pev[1], stream));
     CK(hipEventRecord(pev[2], stream));
   }
-  if (d.nnz) k_cv_ready<<<grid1(d.n, 256), 256, 0, stream>>>(d.off, d.n, grp_dev, rc_dev);
-  else CK(hipMemsetAsync(rc_dev, DCC_RC_RCOK, d.n, stream));
+  if (use_cb) {
+    // readiness came with the bucket path's window stores
+  } else if (d.nnz) {
+    k_cv_ready<<<grid1(d.n, 256), 256, 0, stream>>>(d.off, d.n, grp_dev, rc_dev);
+  } else {
+    CK(hipMemsetAsync(rc_dev, DCC_RC_RCOK, d.n, stream));
+  }
   CK(hipGetLastError());
   if (profiling) CK(hipEventRecord(pev[3], stream));
 

@@ -1,0 +1,570 @@
+// Calvin grant groups by key buckets on gfx950 (see calvin_bucket.h).
+//
+// Same result as calvin.hip's key sort + group scan + windowed put (grant
+// group = group boundaries before the request on its row, in sequence order;
+// row_lock.cpp:78-81, 152-170, 317-357), with the data moved fewer times:
+//
+//   k_cb_count   requests in sequence order, per tile of 65,536: counts of
+//                the 2^bb buckets (low packed-key bits)
+//   k_cb_scan    per bucket, exclusive scan of its tile counts
+//   k_cb_part    the stable partition: each tile's requests -- packed key and
+//                (txn, j, EX) -- ranked per wave, staged in LDS by bucket and
+//                written to the buckets' runs (bucket order = sequence order)
+//   k_cb_bucket  one workgroup per bucket, 4,096-request chunks in order: an
+//                LDS radix sort of the chunk by the row bits above the bucket
+//                bits (stable, so a row's requests stay in sequence order),
+//                the grant-group scan with each row's state carried across
+//                chunks in an LDS table indexed by those bits, and the
+//                (request, group) pairs staged by output window and appended
+//                to the window's region (one returning atomic per window and
+//                chunk, on one of R replicated counters)
+//   k_cb_put     one workgroup per window of 2^tsh txns: the window's groups
+//                placed in LDS, stored whole, and the txns' readiness
+//                (acquire_locks' RCOK iff every request is in group 0,
+//                ycsb_txn.cpp:76-79)
+#include "calvin_bucket.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "calvin_gl.h"
+#include "dcc.h"
+#include "dcc_device.h"
+
+namespace dcc {
+namespace {
+
+constexpr uint32_t CB_PT = 512;                 // count / partition threads (8 waves)
+constexpr uint32_t CB_SUB = CB_PT * 16;         // requests per partition sub-tile (LDS staging)
+constexpr uint32_t CB_NSUB = 8;                 // sub-tiles per tile
+constexpr uint32_t CB_TILE = CB_SUB * CB_NSUB;  // requests per tile (one count column)
+constexpr uint32_t CB_BB_MAX = 11;              // bucket bits
+constexpr uint32_t CB_LB_MAX = 13;              // row bits inside a bucket
+constexpr uint32_t CB_BT = 256;                 // bucket workgroup
+constexpr uint32_t CB_IT = 16;                  // requests per thread per chunk
+constexpr uint32_t CB_CHUNK = CB_BT * CB_IT;
+constexpr uint32_t CB_STG = CB_CHUNK + CB_CHUNK / 16;  // one pad word per 16 (bank spread)
+constexpr uint32_t CB_NDIG_MAX = 760;           // output windows (LDS: two bucket workgroups per CU)
+constexpr uint32_t CB_WIN = 32768;              // groups per output window (128 KiB of LDS)
+constexpr uint32_t CB_R = 8;                    // reservation-counter replicas
+constexpr uint32_t NOTXN = 0xFFFFFFFFu;
+// carry-table word: bit 0 "the row's last request is the chunk's last txn",
+// bits 1-2 its lock type (CV_NONE: row not seen yet), bits 3.. its group count
+constexpr uint32_t TAB_EMPTY = CV_NONE << 1;
+
+__device__ inline uint32_t stg_ix(uint32_t p) { return p + (p >> 4); }
+
+// LDS-only workgroup barrier: waits for this wave's LDS operations, not for
+// its outstanding global loads, stores or returning atomics.
+__device__ inline void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Exclusive add-scan of one u32 per thread over the workgroup (LDS barriers
+// only); s_w holds one word per wave.
+__device__ inline uint32_t blk_excl_add(uint32_t v, uint32_t* s_w, uint32_t& total) {
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d);
+    if (lane >= d) x += y;
+  }
+  lds_barrier();  // s_w free (an earlier call's readers are done)
+  if (lane == 63) s_w[w] = x;
+  lds_barrier();
+  uint32_t off = 0;
+  total = 0;
+  for (uint32_t q = 0; q < nw; q++) {
+    const uint32_t s = s_w[q];
+    if (q < w) off += s;
+    total += s;
+  }
+  return off + x - v;
+}
+
+// Lanes of the wave whose nbits-bit bucket equals this lane's.
+__device__ inline uint64_t bucket_peers(uint32_t d, bool act, uint32_t nbits) {
+  uint64_t m = ballot64(act);
+  for (uint32_t b = 0; b < nbits; b++) {
+    const bool bit = (d >> b) & 1u;
+    const uint64_t bb = ballot64(bit);
+    m &= bit ? bb : ~bb;
+  }
+  return act ? m : 0ull;
+}
+
+struct CbSrc {
+  const uint64_t* keys;
+  const uint8_t* at;
+  const uint32_t* seq;
+  uint64_t nnz;
+  uint32_t ulen;
+  KeyPack kp;
+};
+
+// Request p of the sequence-order stream: packed key (high word) and
+// txn:25 | j:6 | EX:1 (low word).
+__device__ inline uint64_t cb_elem(const CbSrc& s, uint32_t p) {
+  const uint32_t q = p / s.ulen, j = p - q * s.ulen;
+  const uint32_t t = s.seq ? s.seq[q] : q;
+  const uint64_t x = (uint64_t)t * s.ulen + j;
+  const uint32_t pk = (uint32_t)keypack_apply(s.kp, s.keys[x]);
+  const uint8_t a = s.at[x];
+  return ((uint64_t)pk << 32) | (t << 7) | (j << 1) | ((a != DCC_RD && a != DCC_SCAN) ? 1u : 0u);
+}
+__device__ inline uint32_t cb_pk(const CbSrc& s, uint32_t p) {
+  const uint32_t q = p / s.ulen, j = p - q * s.ulen;
+  const uint32_t t = s.seq ? s.seq[q] : q;
+  return (uint32_t)keypack_apply(s.kp, s.keys[(uint64_t)t * s.ulen + j]);
+}
+
+// ---------------------------------------------------------------- count
+// cnt[tile][b] = requests of the tile in bucket b (tile-major: coalesced).
+__global__ __launch_bounds__(CB_PT) void k_cb_count(CbSrc s, uint32_t bmask, uint32_t* __restrict__ cnt) {
+  __shared__ uint32_t s_h[1u << CB_BB_MAX];
+  const uint32_t B = bmask + 1;
+  for (uint32_t i = threadIdx.x; i < B; i += CB_PT) s_h[i] = 0;
+  __syncthreads();
+  const uint64_t base = (uint64_t)blockIdx.x * CB_TILE;
+  const uint32_t n_here = (uint32_t)min<uint64_t>(CB_TILE, s.nnz - base);
+  constexpr uint32_t U = 8;
+  for (uint32_t i0 = threadIdx.x; i0 < n_here; i0 += CB_PT * U) {
+    uint32_t pk[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++) {
+      const uint32_t i = i0 + u * CB_PT;
+      pk[u] = i < n_here ? cb_pk(s, (uint32_t)(base + i)) : 0u;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++)
+      if (i0 + u * CB_PT < n_here) atomicAdd(&s_h[pk[u] & bmask], 1u);
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < B; i += CB_PT) cnt[(uint64_t)blockIdx.x * B + i] = s_h[i];
+}
+
+// ---------------------------------------------------------------- scan
+// Per bucket (a lane each, 64 per workgroup), the exclusive scan of its tile
+// counts in place, the four waves taking a quarter of the tiles each; tot[b]
+// = the bucket's size.
+__global__ __launch_bounds__(256) void k_cb_scan(uint32_t* __restrict__ cnt, uint32_t ntile, uint32_t B,
+                                                 uint32_t* __restrict__ tot) {
+  __shared__ uint32_t s_p[4][64];
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  const uint32_t b = blockIdx.x * 64 + lane;
+  const uint32_t per = (ntile + 3) / 4, t0 = min(ntile, w * per), t1 = min(ntile, t0 + per);
+  uint32_t s = 0;
+  if (b < B) {
+#pragma unroll 8
+    for (uint32_t t = t0; t < t1; t++) s += cnt[(uint64_t)t * B + b];
+  }
+  s_p[w][lane] = s;
+  __syncthreads();
+  uint32_t run = 0;
+  for (uint32_t q = 0; q < w; q++) run += s_p[q][lane];
+  if (b < B) {
+#pragma unroll 8
+    for (uint32_t t = t0; t < t1; t++) {
+      const uint32_t c = cnt[(uint64_t)t * B + b];
+      cnt[(uint64_t)t * B + b] = run;
+      run += c;
+    }
+    if (w == 3) tot[b] = run;
+  }
+}
+
+// ---------------------------------------------------------------- partition
+// One workgroup per tile, its 8 sub-tiles in order.  In a sub-tile wave w
+// produces requests [w * 1024, w * 1024 + 1024) (round it, lane l at
+// w * 1024 + 64 it + l: sequence order is (wave, round, lane)) and ranks each
+// among the wave's earlier requests of its bucket with a running per-bucket
+// count in its own LDS row; the waves' counts become per-(bucket, wave) bases
+// of a bucket-ordered LDS staging, written out as one run per bucket at the
+// bucket's cursor.  Workgroup 0 also stores the buckets' bases for the bucket
+// pass.
+__global__ __launch_bounds__(CB_PT) void k_cb_part(CbSrc s, uint32_t bb, const uint32_t* __restrict__ cnt,
+                                                   const uint32_t* __restrict__ tot,
+                                                   uint32_t* __restrict__ bbase_out,
+                                                   uint64_t* __restrict__ out) {
+  constexpr uint32_t BM = 1u << CB_BB_MAX, W = CB_PT / 64;
+  __shared__ uint64_t s_stg[CB_SUB];
+  __shared__ uint32_t s_cur[BM];  // global cursor of the bucket
+  __shared__ uint32_t s_gof[BM];  // global destination minus staging index
+  __shared__ uint16_t s_wc[W][BM];
+  __shared__ uint32_t s_w[W];
+  const uint32_t B = 1u << bb, bmask = B - 1;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+  const uint32_t per = (B + CB_PT - 1) / CB_PT;  // buckets per thread
+  const uint32_t b0 = min(B, tid * per), b1 = min(B, b0 + per);
+  {
+    uint32_t ls = 0;
+    for (uint32_t b = b0; b < b1; b++) ls += tot[b];
+    uint32_t total;
+    uint32_t run = blk_excl_add(ls, s_w, total);
+    for (uint32_t b = b0; b < b1; b++) {
+      s_cur[b] = run + cnt[(uint64_t)blockIdx.x * B + b];
+      if (blockIdx.x == 0) bbase_out[b] = run;
+      run += tot[b];
+    }
+  }
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  for (uint32_t sub = 0; sub < CB_NSUB; sub++) {
+    const uint64_t sbase = (uint64_t)blockIdx.x * CB_TILE + (uint64_t)sub * CB_SUB;
+    if (sbase >= s.nnz) break;  // whole workgroup
+    const uint32_t n_sub = (uint32_t)min<uint64_t>(CB_SUB, s.nnz - sbase);
+    for (uint32_t i = tid; i < W * BM; i += CB_PT) (&s_wc[0][0])[i] = 0;
+    uint64_t e[16];
+#pragma unroll
+    for (uint32_t it = 0; it < 16; it++) {
+      const uint32_t i = wv * 1024 + it * 64 + lane;
+      e[it] = i < n_sub ? cb_elem(s, (uint32_t)(sbase + i)) : 0ull;
+    }
+    __syncthreads();
+    uint16_t loc[16];
+    uint16_t* my = s_wc[wv];
+#pragma unroll
+    for (uint32_t it = 0; it < 16; it++) {
+      const bool act = wv * 1024 + it * 64 + lane < n_sub;
+      const uint32_t b = (uint32_t)(e[it] >> 32) & bmask;
+      const uint64_t peers = bucket_peers(b, act, bb);
+      const uint32_t lr = (uint32_t)__builtin_popcountll(peers & lt);
+      const uint32_t before = my[b];
+      loc[it] = (uint16_t)(before + lr);
+      // the bucket's first lane advances the count (same wave: in order)
+      if (act && lr == 0) my[b] = (uint16_t)(before + (uint32_t)__builtin_popcountll(peers));
+    }
+    __syncthreads();
+    {
+      uint32_t ls = 0;
+      for (uint32_t b = b0; b < b1; b++)
+#pragma unroll
+        for (uint32_t w = 0; w < W; w++) ls += s_wc[w][b];
+      uint32_t total;
+      uint32_t run = blk_excl_add(ls, s_w, total);
+      for (uint32_t b = b0; b < b1; b++) {
+        const uint32_t lb = run;
+#pragma unroll
+        for (uint32_t w = 0; w < W; w++) {
+          const uint32_t c = s_wc[w][b];
+          s_wc[w][b] = (uint16_t)run;
+          run += c;
+        }
+        s_gof[b] = s_cur[b] - lb;  // mod 2^32: dst = s_gof[b] + staging index
+        s_cur[b] += run - lb;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t it = 0; it < 16; it++) {
+      if (wv * 1024 + it * 64 + lane < n_sub) {
+        const uint32_t b = (uint32_t)(e[it] >> 32) & bmask;
+        s_stg[my[b] + loc[it]] = e[it];
+      }
+    }
+    __syncthreads();
+    for (uint32_t j = tid; j < n_sub; j += CB_PT) {
+      const uint64_t x = s_stg[j];
+      out[s_gof[(uint32_t)(x >> 32) & bmask] + j] = x;
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------- bucket
+struct CbBucket {
+  const uint64_t* in;
+  const uint32_t* tot;
+  const uint32_t* bbase;
+  uint32_t bb, lbits, tsh, ndig;
+  uint64_t span;
+  uint32_t* gcnt;  // [R][ndig]
+  uint64_t* out;   // [R][ndig][span]
+};
+
+__global__ __launch_bounds__(CB_BT) void k_cb_bucket(CbBucket a) {
+  __shared__ uint32_t s_tab[1u << CB_LB_MAX];
+  __shared__ uint64_t s_stg[CB_STG];
+  __shared__ uint16_t s_rc[16 * CB_BT];       // radix counts [digit][thread]
+  __shared__ uint32_t s_dc[CB_NDIG_MAX];      // window counts, then cursors
+  __shared__ uint32_t s_dg[CB_NDIG_MAX];      // window region offset minus staging index
+  __shared__ uint32_t s_w[CB_BT / 64];
+  __shared__ uint32_t s_tl;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t size = a.tot[blockIdx.x];
+  if (size == 0) return;  // whole workgroup
+  const uint64_t base = a.bbase[blockIdx.x];
+  const uint32_t r = blockIdx.x % CB_R;
+  const uint32_t ntab = 1u << a.lbits;
+  for (uint32_t i = tid; i < ntab; i += CB_BT) s_tab[i] = TAB_EMPTY;
+  for (uint32_t d = tid; d < a.ndig; d += CB_BT) s_dc[d] = 0;
+  const uint32_t npass = (a.lbits + 3) / 4;
+  const uint32_t dpt = (a.ndig + CB_BT - 1) / CB_BT;  // windows per thread (<= 3)
+  const uint32_t d0 = min(a.ndig, tid * dpt), d1 = min(a.ndig, d0 + dpt);
+  uint32_t t_prev = NOTXN;  // the previous chunk's last txn
+  lds_barrier();
+  for (uint32_t c0 = 0; c0 < size; c0 += CB_CHUNK) {
+    const uint32_t nc = min(CB_CHUNK, size - c0);
+    const uint64_t* src = a.in + base + c0;
+    // (1) this thread's 16 consecutive requests (padding sorts last: all-ones key)
+    uint64_t e[CB_IT];
+    const uint32_t p0 = tid * CB_IT;
+    if (p0 + CB_IT <= nc && (((uintptr_t)(src + p0)) & 15) == 0) {
+#pragma unroll
+      for (uint32_t q = 0; q < CB_IT / 2; q++) {
+        const ulonglong2 x = ((const ulonglong2*)(src + p0))[q];
+        e[2 * q] = x.x;
+        e[2 * q + 1] = x.y;
+      }
+    } else {
+#pragma unroll
+      for (uint32_t i = 0; i < CB_IT; i++) e[i] = p0 + i < nc ? src[p0 + i] : ~0ull;
+    }
+    if (tid == 0) s_tl = (uint32_t)src[nc - 1] >> 7;
+    // (2) window counts, then one reservation per window (used after the sort)
+#pragma unroll
+    for (uint32_t i = 0; i < CB_IT; i++)
+      if (p0 + i < nc) atomicAdd(&s_dc[((uint32_t)e[i] >> 7) >> a.tsh], 1u);
+    lds_barrier();
+    const uint32_t t_last = s_tl;
+    uint32_t resv[3] = {0, 0, 0}, dcn[3] = {0, 0, 0};
+#pragma unroll
+    for (uint32_t k = 0; k < 3; k++) {
+      const uint32_t d = d0 + k;
+      if (d < d1) {
+        dcn[k] = s_dc[d];
+        if (dcn[k]) resv[k] = atomicAdd(&a.gcnt[r * a.ndig + d], dcn[k]);
+      }
+    }
+    // (3) stable LDS radix sort of the chunk by the row bits, 4 per pass
+    for (uint32_t ps = 0; ps < npass; ps++) {
+      const uint32_t sh = 32 + a.bb + 4 * ps;
+      uint64_t clo = 0, chi = 0;  // 8-bit running counts of digits 0-7 / 8-15
+      uint32_t rk[CB_IT];
+#pragma unroll
+      for (uint32_t i = 0; i < CB_IT; i++) {
+        const uint32_t d = (uint32_t)(e[i] >> sh) & 15u;
+        const uint32_t fs = (d & 7u) * 8u;
+        if (d < 8) {
+          rk[i] = (uint32_t)(clo >> fs) & 255u;
+          clo += 1ull << fs;
+        } else {
+          rk[i] = (uint32_t)(chi >> fs) & 255u;
+          chi += 1ull << fs;
+        }
+      }
+#pragma unroll
+      for (uint32_t d = 0; d < 16; d++)
+        s_rc[d * CB_BT + tid] = (uint16_t)(((d < 8 ? clo : chi) >> ((d & 7u) * 8u)) & 255u);
+      lds_barrier();
+      {  // digit-major exclusive scan of the 16 x 256 counts
+        uint32_t v[16], ls = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 16; k++) {
+          v[k] = s_rc[tid * 16 + k];
+          ls += v[k];
+        }
+        uint32_t total;
+        uint32_t run = blk_excl_add(ls, s_w, total);
+#pragma unroll
+        for (uint32_t k = 0; k < 16; k++) {
+          s_rc[tid * 16 + k] = (uint16_t)run;
+          run += v[k];
+        }
+      }
+      lds_barrier();
+#pragma unroll
+      for (uint32_t i = 0; i < CB_IT; i++) {
+        const uint32_t d = (uint32_t)(e[i] >> sh) & 15u;
+        s_stg[stg_ix(s_rc[d * CB_BT + tid] + rk[i])] = e[i];
+      }
+      lds_barrier();
+#pragma unroll
+      for (uint32_t i = 0; i < CB_IT; i++) e[i] = s_stg[stg_ix(p0 + i)];
+      lds_barrier();
+    }
+    if (npass == 0) {  // one row per bucket: position order is row order
+#pragma unroll
+      for (uint32_t i = 0; i < CB_IT; i++) s_stg[stg_ix(p0 + i)] = e[i];
+      lds_barrier();
+    }
+    // (4) grant-group scan; a row's first request in the chunk continues from
+    // the carry table, its last one stores the row's state back
+    const uint32_t lsh = 32 + a.bb;
+    const uint64_t prev_e = p0 ? s_stg[stg_ix(p0 - 1)] : ~0ull;
+    const uint64_t next_e = p0 + CB_IT < nc ? s_stg[stg_ix(p0 + CB_IT)] : ~0ull;
+    uint32_t st[CB_IT];
+    uint32_t dupm = 0;
+    uint32_t acc = GL_ID;
+#pragma unroll
+    for (uint32_t i = 0; i < CB_IT; i++) {
+      const uint64_t pe = i ? e[i - 1] : prev_e;
+      const uint32_t lk = (uint32_t)(e[i] >> lsh), plk = (uint32_t)(pe >> lsh);
+      const uint32_t v = (uint32_t)e[i], tx = v >> 7;
+      const uint32_t typ = (v & 1u) ? CV_EX : CV_SH;
+      uint32_t x;
+      if (p0 + i >= nc) {
+        x = GL_ID;
+      } else if (p0 + i == 0 || lk != plk) {
+        const uint32_t c = s_tab[lk];
+        const uint32_t cl = (c >> 1) & 3u, cc = c >> 3;
+        if (cl == CV_NONE) {
+          x = gl_pack(1, typ, typ, 0);
+        } else if ((c & 1u) && tx == t_prev) {  // same txn as the row's last request
+          x = gl_pack(1, cl, cl, cc);
+          dupm |= 1u << i;
+        } else {
+          x = gl_pack(1, cl, typ, cc + ((cl == CV_EX || typ == CV_EX) ? 1u : 0u));
+        }
+      } else if (tx == (uint32_t)pe >> 7) {  // duplicate row of the same txn
+        x = GL_ID;
+        dupm |= 1u << i;
+      } else {
+        x = gl_pack(0, typ, typ, 0);
+      }
+      st[i] = x;
+      acc = gl_combine(acc, x);
+    }
+    uint32_t total;
+    uint32_t run = gl_block_excl(acc, s_w, total);  // every table read is done past this
+    uint32_t grp[CB_IT];
+#pragma unroll
+    for (uint32_t i = 0; i < CB_IT; i++) {
+      run = gl_combine(run, st[i]);
+      grp[i] = ((dupm >> i) & 1u) ? DCC_GROUP_NONE : run >> 5;
+      if (p0 + i < nc) {
+        const uint64_t ne = i + 1 < CB_IT ? e[i + 1] : next_e;
+        const uint32_t lk = (uint32_t)(e[i] >> lsh);
+        if (p0 + i + 1 == nc || (uint32_t)(ne >> lsh) != lk) {
+          const uint32_t tx = (uint32_t)e[i] >> 7;
+          s_tab[lk] = ((run >> 5) << 3) | (((run >> 3) & 3u) << 1) | (tx == t_last ? 1u : 0u);
+        }
+      }
+    }
+    // (5) the (request, group) pairs staged by window, appended to the regions
+    {
+      uint32_t ls = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < 3; k++) ls += dcn[k];
+      uint32_t tt;
+      uint32_t lb = blk_excl_add(ls, s_w, tt);
+#pragma unroll
+      for (uint32_t k = 0; k < 3; k++) {
+        const uint32_t d = d0 + k;
+        if (d < d1) {
+          s_dc[d] = lb;
+          s_dg[d] = resv[k] - lb;
+          lb += dcn[k];
+        }
+      }
+    }
+    lds_barrier();
+#pragma unroll
+    for (uint32_t i = 0; i < CB_IT; i++) {
+      if (p0 + i < nc) {
+        const uint32_t v = (uint32_t)e[i];
+        const uint32_t q = atomicAdd(&s_dc[(v >> 7) >> a.tsh], 1u);
+        s_stg[q] = ((uint64_t)grp[i] << 32) | v;
+      }
+    }
+    lds_barrier();
+    for (uint32_t j = tid; j < nc; j += CB_BT) {
+      const uint64_t x = s_stg[j];
+      const uint32_t d = ((uint32_t)x >> 7) >> a.tsh;
+      a.out[((uint64_t)r * a.ndig + d) * a.span + (uint32_t)(s_dg[d] + j)] = x;
+    }
+    lds_barrier();
+    for (uint32_t d = tid; d < a.ndig; d += CB_BT) s_dc[d] = 0;
+    t_prev = t_last;
+    lds_barrier();
+  }
+}
+
+// ---------------------------------------------------------------- put
+__global__ __launch_bounds__(1024) void k_cb_put(const uint64_t* __restrict__ in,
+                                                 const uint32_t* __restrict__ gcnt, uint32_t ndig,
+                                                 uint64_t span, uint32_t n, uint32_t ulen, uint32_t tsh,
+                                                 uint32_t* __restrict__ group, uint8_t* __restrict__ rc) {
+  __shared__ uint32_t win[CB_WIN];
+  __shared__ uint32_t s_wait[CB_WIN / 32];
+  const uint32_t d = blockIdx.x, tid = threadIdx.x;
+  const uint32_t t_lo = d << tsh, ntx = min(n - t_lo, 1u << tsh);
+  const uint32_t w = ntx * ulen;
+  const uint64_t x_lo = (uint64_t)t_lo * ulen;
+  for (uint32_t i = tid; i < (ntx + 31) / 32; i += 1024) s_wait[i] = 0;
+  constexpr uint32_t U = 8;
+  for (uint32_t r = 0; r < CB_R; r++) {
+    const uint32_t m = gcnt[r * ndig + d];
+    const uint64_t* src = in + ((uint64_t)r * ndig + d) * span;
+    for (uint32_t p0 = tid; p0 < m; p0 += 1024 * U) {
+      uint64_t x[U];
+#pragma unroll
+      for (uint32_t u = 0; u < U; u++) x[u] = p0 + u * 1024 < m ? src[p0 + u * 1024] : ~0ull;
+#pragma unroll
+      for (uint32_t u = 0; u < U; u++) {
+        if (p0 + u * 1024 >= m) continue;
+        const uint32_t v = (uint32_t)x[u];
+        win[((v >> 7) - t_lo) * ulen + ((v >> 1) & 63u)] = (uint32_t)(x[u] >> 32);
+      }
+    }
+  }
+  __syncthreads();
+  uint32_t* dst = group + x_lo;
+  for (uint32_t i = tid; i < w; i += 1024) {
+    const uint32_t g = win[i];
+    dst[i] = g;
+    if (g != 0 && g != DCC_GROUP_NONE) {
+      const uint32_t tt = i / ulen;
+      atomicOr(&s_wait[tt >> 5], 1u << (tt & 31u));
+    }
+  }
+  __syncthreads();
+  for (uint32_t tt = tid; tt < ntx; tt += 1024)
+    rc[t_lo + tt] = ((s_wait[tt >> 5] >> (tt & 31u)) & 1u) ? DCC_RC_WAIT : DCC_RC_RCOK;
+}
+
+}  // namespace
+
+bool cb_plan(uint64_t n, uint64_t nnz, uint32_t ulen, uint32_t kbits, CbPlan* p) {
+  if (!ulen || ulen > 64 || nnz == 0 || nnz != n * ulen || nnz >= 0xFFFFFFFFull) return false;
+  if (kbits > CB_BB_MAX + CB_LB_MAX) return false;
+  CbPlan q{};
+  q.bb = std::min(CB_BB_MAX, kbits);
+  q.lbits = kbits - q.bb;
+  q.tsh = 0;
+  while ((2ull << q.tsh) * ulen <= CB_WIN) q.tsh++;
+  q.span = (1ull << q.tsh) * ulen;
+  q.ndig = (uint32_t)((n + (1ull << q.tsh) - 1) >> q.tsh);
+  if (q.ndig > CB_NDIG_MAX) return false;
+  q.ntile = (uint32_t)((nnz + CB_TILE - 1) / CB_TILE);
+  q.R = CB_R;
+  const uint64_t B = 1ull << q.bb;
+  q.elem_bytes = nnz * 8;
+  q.out_bytes = (uint64_t)q.R * q.ndig * q.span * 8;
+  q.cnt_bytes = (uint64_t)q.ntile * B * 4;
+  q.small_bytes = (2 * B + (uint64_t)q.R * q.ndig) * 4;
+  *p = q;
+  return true;
+}
+
+hipError_t cb_run(const CbPlan& p, const CbArgs& a, hipStream_t st, hipEvent_t ev_part,
+                  hipEvent_t ev_bucket) {
+  const uint32_t B = 1u << p.bb;
+  uint32_t* tot = a.small;
+  uint32_t* bbase = tot + B;
+  uint32_t* gcnt = bbase + B;
+  const CbSrc s{a.keys, a.acctype, a.seq, a.nnz, a.ulen, a.kp};
+  hipError_t e = hipMemsetAsync(gcnt, 0, (size_t)p.R * p.ndig * 4, st);
+  if (e != hipSuccess) return e;
+  k_cb_count<<<p.ntile, CB_PT, 0, st>>>(s, B - 1, a.cnt);
+  k_cb_scan<<<(B + 63) / 64, 256, 0, st>>>(a.cnt, p.ntile, B, tot);
+  k_cb_part<<<p.ntile, CB_PT, 0, st>>>(s, p.bb, a.cnt, tot, bbase, a.elems);
+  if (ev_part && (e = hipEventRecord(ev_part, st)) != hipSuccess) return e;
+  k_cb_bucket<<<B, CB_BT, 0, st>>>(
+      CbBucket{a.elems, tot, bbase, p.bb, p.lbits, p.tsh, p.ndig, p.span, gcnt, a.out});
+  if (ev_bucket && (e = hipEventRecord(ev_bucket, st)) != hipSuccess) return e;
+  k_cb_put<<<p.ndig, 1024, 0, st>>>(a.out, gcnt, p.ndig, p.span, (uint32_t)a.n, a.ulen, p.tsh, a.group,
+                                    a.rc);
+  return hipGetLastError();
+}
+
+}  // namespace dcc

@@ -116,7 +116,7 @@ struct dcc_ctx {
   struct CvGraphKey {
     const void *off, *keys, *acc, *order, *grp, *rc;
     uint64_t n, nnz, gen;
-    uint32_t ulen, have_seq;
+    uint32_t ulen, have_seq, bucket;
     uint8_t kp[112], op[112];  // KeyPack images (memcmp)
   };
   hipGraphExec_t cv_graph_exec = nullptr;
@@ -151,6 +151,7 @@ struct dcc_ctx {
   DevBuf perm, calvin_a, calvin_b, calvin_c, calvin_d;  // Calvin workspaces
   DevBuf cv_scratch, cv_agg, cv_group, cv_wave, cv_pgx, cv_gsx, cv_gsize, cv_done, cv_maxl;
   DevBuf cv_seq_b, cv_ok, cv_len, cv_off2, cv_tsum, cv_hkeys, cv_hat;
+  DevBuf cb_e, cb_out, cb_cnt, cb_small;           // Calvin bucket path (calvin_bucket.h)
   DevBuf snap_top, snap_aoff, snap_aidx, snap_cnt;  // captured-snapshot validation
   DevBuf mt_rk;                                  // MaaT row table: 32-B {key, last read, last write} slots
   uint32_t mt_bits = 0;                          // log2 row-table slots (0: none yet)
