@@ -55,10 +55,12 @@ def parse():
                     help="strong scaling: one fixed batch of --txns txns key-sharded over the "
                          "N ranks (BASELINE config C5 with --theta 0.99 --seed 0xD3E7A002); "
                          "default is weak scaling (N x --txns txns)")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r03", "pmc.json"),
-                    help="PMC summary (tools/gpu_pmc_r03.sh -> tools/pmc_r03.py) the "
-                         "roofline.traffic and l2_hit fields are read from (headline and C4 "
-                         "workloads at N=1; null otherwise)")
+    ap.add_argument("--pmc", default=next((p for p in (os.path.join(ROOT, "profiles", r, "pmc.json")
+                                                       for r in ("r04", "r03")) if os.path.exists(p)),
+                                          os.path.join(ROOT, "profiles", "r04", "pmc.json")),
+                    help="PMC summary (tools/gpu_pmc_r04.sh -> tools/pmc_r04.py) the "
+                         "roofline.traffic / l2_hit fields and each config's pmc block are read "
+                         "from (the workloads it describes at N=1; null otherwise)")
     ap.add_argument("--exchange", choices=["rccl", "host"], default="rccl",
                     help="N>1 status all-reduce: RCCL over xGMI (one GPU per rank), or "
                          "host/gloo (rehearsal: ranks may share one GPU)")
@@ -132,6 +134,15 @@ def prefix_batch(b, n):
     cut = lambda a: None if a is None else np.asarray(a)[:n].copy()
     return EpochBatch(off, np.asarray(b.keys)[: off[-1]], np.asarray(b.acctype)[: off[-1]],
                       cut(b.start_tn), cut(b.finish_tn), cut(b.order))
+
+
+def _kern_l2(pw, name):
+    """L2 hit rate of the first kernel of a PMC workload summary whose name
+    holds `name` (profiles/r04/pmc.json), or null."""
+    for k, v in ((pw or {}).get("kernels") or {}).items():
+        if name in k:
+            return v.get("l2_hit")
+    return None
 
 
 def cpu_leg(fn, n, variant, sample_note):
@@ -664,17 +675,24 @@ def main():
         traffic = hp.get("epoch_bytes")
         traffic_src = (f"{os.path.relpath(args.pmc, ROOT)} ({pmc.get('source', '')}; "
                        f"{pmc.get('correction', '')})") if pmc else None
-        if pmc and secondary and "C4" in secondary:
-            c4 = pmc.get("C4") or {}
-            ks = c4.get("kernels") or {}
-            secondary["C4"]["pmc"] = {
-                "source": traffic_src,
-                "epoch_traffic_bytes": c4.get("epoch_bytes"),
-                "epoch_l2_hit": c4.get("epoch_l2_hit"),
-                "l2_hit": {k: v.get("l2_hit") for k, v in ks.items()
-                           if "k_rs_" in k or "k_cv_" in k},
-                "sort_scatter_write_bytes": (ks.get("dcc::k_rs_scatter<unsigned int>") or {}).get(
-                    "write_bytes_max")}
+        if pmc and secondary:
+            # per-workload traffic next to each config's own device time
+            for tag, sec in secondary.items():
+                pw = pmc.get(tag) or {}
+                if not pw.get("epoch_bytes") or not isinstance(sec, dict):
+                    continue
+                ks = pw.get("kernels") or {}
+                top = sorted(ks.items(), key=lambda kv: -(kv[1].get("fetch_bytes", kv[1].get("fetch_bytes_max", 0)) +
+                                                          kv[1].get("write_bytes", kv[1].get("write_bytes_max", 0))))[:6]
+                dms = sec.get("device_ms")
+                sec["pmc"] = {
+                    "source": traffic_src,
+                    "epoch_traffic_bytes": pw.get("epoch_bytes"),
+                    "epoch_l2_hit": pw.get("epoch_l2_hit"),
+                    "actual_GBps": pw["epoch_bytes"] / (dms * 1e-3) / 1e9 if dms else None,
+                    "top_kernels": {k: {"fetch_bytes": v.get("fetch_bytes", v.get("fetch_bytes_max")),
+                                        "write_bytes": v.get("write_bytes", v.get("write_bytes_max")),
+                                        "l2_hit": v.get("l2_hit")} for k, v in top}}
         line = {
             "metric": "OCC-validated txns/sec, YCSB theta=0.9",
             "value": value,
@@ -713,9 +731,9 @@ def main():
                 "actual_GBps": (traffic / (dev_ms * 1e-3) / 1e9) if traffic else None,
                 "traffic_source": traffic_src,
                 "l2_hit": {"epoch": hp.get("epoch_l2_hit"),
-                           "level0_filter": (hp.get("filter_l0") or {}).get("l2_hit"),
-                           "serial_pass": hp.get("serial_pass_l2_hit"),
-                           "pre_pass": hp.get("pre_pass_l2_hit")} if hp else None,
+                           "filter": _kern_l2(hp, "k_sw_filter"),
+                           "serial_pass": _kern_l2(hp, "k_sw_seq"),
+                           "pre_pass": _kern_l2(hp, "k_sw_pre")} if hp else None,
                 "alg_bytes_per_launch": int(s0["alg_bytes"]),
                 "avg_launch_ms": dev_ms,
                 "streaming_kernel": filt,
