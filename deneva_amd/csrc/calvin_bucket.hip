@@ -4,8 +4,8 @@
 // group = group boundaries before the request on its row, in sequence order;
 // row_lock.cpp:78-81, 152-170, 317-357), with the data moved fewer times:
 //
-//   k_cb_count   requests in sequence order, per tile of 65,536: counts of
-//                the 2^bb buckets (low packed-key bits)
+//   k_cb_count   requests in sequence order, per tile of 64 x 1024 / ulen
+//                txns: counts of the 2^bb buckets (low packed-key bits)
 //   k_cb_scan    per bucket, exclusive scan of its tile counts
 //   k_cb_part    the stable partition: each tile's requests -- packed key and
 //                (txn, j, EX) -- ranked per wave, staged in LDS by bucket and
@@ -38,13 +38,12 @@ namespace {
 constexpr uint32_t CB_PT = 512;                 // count / partition threads (8 waves)
 constexpr uint32_t CB_SUB = CB_PT * 16;         // requests per partition sub-tile (LDS staging)
 constexpr uint32_t CB_NSUB = 8;                 // sub-tiles per tile
-constexpr uint32_t CB_TILE = CB_SUB * CB_NSUB;  // requests per tile (one count column)
 constexpr uint32_t CB_BB_MAX = 11;              // bucket bits
 constexpr uint32_t CB_LB_MAX = 13;              // row bits inside a bucket
 constexpr uint32_t CB_BT = 256;                 // bucket workgroup
 constexpr uint32_t CB_IT = 16;                  // requests per thread per chunk
 constexpr uint32_t CB_CHUNK = CB_BT * CB_IT;
-constexpr uint32_t CB_STG = CB_CHUNK + CB_CHUNK / 16;  // one pad word per 16 (bank spread)
+constexpr uint32_t CB_STG = CB_CHUNK + CB_CHUNK / 32;  // one pad slot per 32 (bank spread)
 constexpr uint32_t CB_NDIG_MAX = 760;           // output windows (LDS: two bucket workgroups per CU)
 constexpr uint32_t CB_WIN = 32768;              // groups per output window (128 KiB of LDS)
 constexpr uint32_t CB_R = 8;                    // reservation-counter replicas
@@ -53,7 +52,7 @@ constexpr uint32_t NOTXN = 0xFFFFFFFFu;
 // bits 1-2 its lock type (CV_NONE: row not seen yet), bits 3.. its group count
 constexpr uint32_t TAB_EMPTY = CV_NONE << 1;
 
-__device__ inline uint32_t stg_ix(uint32_t p) { return p + (p >> 4); }
+__device__ inline uint32_t stg_ix(uint32_t p) { return p + (p >> 5); }
 
 // LDS-only workgroup barrier: waits for this wave's LDS operations, not for
 // its outstanding global loads, stores or returning atomics.
@@ -82,13 +81,24 @@ __device__ inline uint32_t blk_excl_add(uint32_t v, uint32_t* s_w, uint32_t& tot
   return off + x - v;
 }
 
-// Lanes of the wave whose nbits-bit bucket equals this lane's.
+// Lanes of the wave whose nbits-bit bucket equals this lane's (NB > 0: a
+// compile-time bit count, the loop unrolled).
+template <uint32_t NB>
 __device__ inline uint64_t bucket_peers(uint32_t d, bool act, uint32_t nbits) {
   uint64_t m = ballot64(act);
-  for (uint32_t b = 0; b < nbits; b++) {
-    const bool bit = (d >> b) & 1u;
-    const uint64_t bb = ballot64(bit);
-    m &= bit ? bb : ~bb;
+  if (NB) {
+#pragma unroll
+    for (uint32_t b = 0; b < NB; b++) {
+      const bool bit = (d >> b) & 1u;
+      const uint64_t bb = ballot64(bit);
+      m &= bit ? bb : ~bb;
+    }
+  } else {
+    for (uint32_t b = 0; b < nbits; b++) {
+      const bool bit = (d >> b) & 1u;
+      const uint64_t bb = ballot64(bit);
+      m &= bit ? bb : ~bb;
+    }
   }
   return act ? m : 0ull;
 }
@@ -97,47 +107,84 @@ struct CbSrc {
   const uint64_t* keys;
   const uint8_t* at;
   const uint32_t* seq;
-  uint64_t nnz;
-  uint32_t ulen;
+  uint32_t n;     // txns
+  uint32_t ulen;  // requests per txn
+  uint32_t um;    // (2^20 + ulen - 1) / ulen: e / ulen == (e * um) >> 20 for e <= 1024
+  uint32_t wt;    // txns per wave and sub-tile (1024 / ulen)
   KeyPack kp;
 };
 
-// Request p of the sequence-order stream: packed key (high word) and
-// txn:25 | j:6 | EX:1 (low word).
-__device__ inline uint64_t cb_elem(const CbSrc& s, uint32_t p) {
-  const uint32_t q = p / s.ulen, j = p - q * s.ulen;
-  const uint32_t t = s.seq ? s.seq[q] : q;
-  const uint64_t x = (uint64_t)t * s.ulen + j;
-  const uint32_t pk = (uint32_t)keypack_apply(s.kp, s.keys[x]);
-  const uint8_t a = s.at[x];
-  return ((uint64_t)pk << 32) | (t << 7) | (j << 1) | ((a != DCC_RD && a != DCC_SCAN) ? 1u : 0u);
-}
-__device__ inline uint32_t cb_pk(const CbSrc& s, uint32_t p) {
-  const uint32_t q = p / s.ulen, j = p - q * s.ulen;
-  const uint32_t t = s.seq ? s.seq[q] : q;
-  return (uint32_t)keypack_apply(s.kp, s.keys[(uint64_t)t * s.ulen + j]);
+// Wave w's share of a sub-tile: sequence positions [q0, q0 + nq), nq <= wt.
+// Their txn ids are staged in LDS (s_t, this wave's 1024 words; one round
+// trip for nq <= 64), then element e = 64 it + lane (< nq * ulen) is request
+// e % ulen of txn e / ulen: every key (and type) load of the wave is issued
+// before the first is used.  FULL: the element (packed key high, txn:25 |
+// j:6 | EX:1 low), else the packed key alone; past the end ~0 (sorts last).
+template <bool FULL>
+__device__ inline uint32_t cb_wave_elems(const CbSrc& s, uint32_t q0, uint32_t nq, uint32_t* s_t,
+                                         uint64_t (&el)[16]) {
+  const uint32_t lane = threadIdx.x & 63u;
+  if (nq == 0) {
+#pragma unroll
+    for (uint32_t it = 0; it < 16; it++) el[it] = ~0ull;
+    return 0;
+  }
+  const uint32_t nk = (nq + 63) / 64;
+  for (uint32_t k = 0; k < nk; k++) {
+    const uint32_t i = k * 64 + lane;
+    if (i < nq) s_t[i] = s.seq ? s.seq[q0 + i] : q0 + i;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const uint32_t ne = nq * s.ulen;
+  uint64_t kk[16];
+  uint32_t tj[16];
+  uint8_t aa[16];
+#pragma unroll
+  for (uint32_t it = 0; it < 16; it++) {
+    const uint32_t e = min(it * 64 + lane, ne - 1);
+    const uint32_t i = (e * s.um) >> 20, j = e - i * s.ulen;
+    const uint32_t t = s_t[i];
+    const uint64_t x = (uint64_t)t * s.ulen + j;
+    kk[it] = s.keys[x];
+    if (FULL) aa[it] = s.at[x];
+    tj[it] = (t << 7) | (j << 1);
+  }
+#pragma unroll
+  for (uint32_t it = 0; it < 16; it++) {
+    const uint32_t pk = (uint32_t)keypack_apply(s.kp, kk[it]);
+    if (it * 64 + lane >= ne)
+      el[it] = ~0ull;
+    else if (FULL)
+      el[it] = ((uint64_t)pk << 32) | tj[it] | ((aa[it] != DCC_RD && aa[it] != DCC_SCAN) ? 1u : 0u);
+    else
+      el[it] = pk;
+  }
+  return ne;
 }
 
 // ---------------------------------------------------------------- count
-// cnt[tile][b] = requests of the tile in bucket b (tile-major: coalesced).
+// A tile is CB_NSUB sub-tiles of 8 waves x wt txns in sequence order (wave w
+// of sub-tile u: positions tile_q0 + (8u + w) * wt ...).  cnt[tile][b] =
+// requests of the tile in bucket b (tile-major: coalesced).
 __global__ __launch_bounds__(CB_PT) void k_cb_count(CbSrc s, uint32_t bmask, uint32_t* __restrict__ cnt) {
+  constexpr uint32_t W = CB_PT / 64;
   __shared__ uint32_t s_h[1u << CB_BB_MAX];
-  const uint32_t B = bmask + 1;
+  __shared__ uint32_t s_t[W][1024];
+  const uint32_t B = bmask + 1, lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   for (uint32_t i = threadIdx.x; i < B; i += CB_PT) s_h[i] = 0;
   __syncthreads();
-  const uint64_t base = (uint64_t)blockIdx.x * CB_TILE;
-  const uint32_t n_here = (uint32_t)min<uint64_t>(CB_TILE, s.nnz - base);
-  constexpr uint32_t U = 8;
-  for (uint32_t i0 = threadIdx.x; i0 < n_here; i0 += CB_PT * U) {
-    uint32_t pk[U];
+  const uint64_t tq0 = (uint64_t)blockIdx.x * CB_NSUB * W * s.wt;
+  for (uint32_t sub = 0; sub < CB_NSUB; sub++) {
+    const uint64_t q0 = tq0 + (uint64_t)(sub * W + wv) * s.wt;
+    if (q0 >= s.n) break;  // this wave (no barrier in the loop)
+    const uint32_t nq = (uint32_t)min<uint64_t>(s.wt, s.n - q0);
+    uint64_t el[16];
+    const uint32_t ne = cb_wave_elems<false>(s, (uint32_t)q0, nq, s_t[wv], el);
 #pragma unroll
-    for (uint32_t u = 0; u < U; u++) {
-      const uint32_t i = i0 + u * CB_PT;
-      pk[u] = i < n_here ? cb_pk(s, (uint32_t)(base + i)) : 0u;
-    }
-#pragma unroll
-    for (uint32_t u = 0; u < U; u++)
-      if (i0 + u * CB_PT < n_here) atomicAdd(&s_h[pk[u] & bmask], 1u);
+    for (uint32_t it = 0; it < 16; it++)
+      if (it * 64 + lane < ne) atomicAdd(&s_h[(uint32_t)el[it] & bmask], 1u);
   }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < B; i += CB_PT) cnt[(uint64_t)blockIdx.x * B + i] = s_h[i];
@@ -174,22 +221,29 @@ __global__ __launch_bounds__(256) void k_cb_scan(uint32_t* __restrict__ cnt, uin
 }
 
 // ---------------------------------------------------------------- partition
-// One workgroup per tile, its 8 sub-tiles in order.  In a sub-tile wave w
-// produces requests [w * 1024, w * 1024 + 1024) (round it, lane l at
-// w * 1024 + 64 it + l: sequence order is (wave, round, lane)) and ranks each
-// among the wave's earlier requests of its bucket with a running per-bucket
-// count in its own LDS row; the waves' counts become per-(bucket, wave) bases
-// of a bucket-ordered LDS staging, written out as one run per bucket at the
-// bucket's cursor.  Workgroup 0 also stores the buckets' bases for the bucket
-// pass.
+// One workgroup per tile, its sub-tiles in order.  In a sub-tile wave w
+// produces its wt txns' requests (cb_wave_elems: element 64 it + lane, so
+// sequence order is (wave, round, lane)) and ranks each among the wave's
+// earlier requests of its bucket with a running per-bucket count in its own
+// LDS row; the waves' counts become per-(bucket, wave) bases of a
+// bucket-ordered LDS staging, written out as one run per bucket at the
+// bucket's cursor.  Workgroup 0 also stores the buckets' bases for the
+// bucket pass.
+template <uint32_t NB>  // bucket bits at compile time (0: bb at run time)
 __global__ __launch_bounds__(CB_PT) void k_cb_part(CbSrc s, uint32_t bb, const uint32_t* __restrict__ cnt,
                                                    const uint32_t* __restrict__ tot,
                                                    uint32_t* __restrict__ bbase_out,
-                                                   uint64_t* __restrict__ out) {
+                                                   uint64_t* __restrict__ out, uint32_t ntile) {
   constexpr uint32_t BM = 1u << CB_BB_MAX, W = CB_PT / 64;
-  __shared__ uint64_t s_stg[CB_SUB];
-  __shared__ uint32_t s_cur[BM];  // global cursor of the bucket
-  __shared__ uint32_t s_gof[BM];  // global destination minus staging index
+  // XCD-contiguous tiles: workgroup b runs on XCD b % 8, which takes tiles
+  // [x * per, (x + 1) * per) -- a bucket's runs from consecutive tiles then
+  // meet in one L2 and leave it as whole lines
+  const uint32_t tpx = (ntile + 7) / 8;
+  const uint32_t tile = (blockIdx.x % 8) * tpx + blockIdx.x / 8;
+  if (tile >= ntile) return;  // whole workgroup (tile 0 is workgroup 0's)
+  __shared__ uint64_t s_stg[CB_SUB];  // also the waves' txn ids while the elements load
+  __shared__ uint32_t s_cur[BM];      // global cursor of the bucket
+  __shared__ uint32_t s_gof[BM];      // global destination minus staging index
   __shared__ uint16_t s_wc[W][BM];
   __shared__ uint32_t s_w[W];
   const uint32_t B = 1u << bb, bmask = B - 1;
@@ -202,31 +256,28 @@ __global__ __launch_bounds__(CB_PT) void k_cb_part(CbSrc s, uint32_t bb, const u
     uint32_t total;
     uint32_t run = blk_excl_add(ls, s_w, total);
     for (uint32_t b = b0; b < b1; b++) {
-      s_cur[b] = run + cnt[(uint64_t)blockIdx.x * B + b];
-      if (blockIdx.x == 0) bbase_out[b] = run;
+      s_cur[b] = run + cnt[(uint64_t)tile * B + b];
+      if (tile == 0) bbase_out[b] = run;
       run += tot[b];
     }
   }
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  const uint64_t tq0 = (uint64_t)tile * CB_NSUB * W * s.wt;
   for (uint32_t sub = 0; sub < CB_NSUB; sub++) {
-    const uint64_t sbase = (uint64_t)blockIdx.x * CB_TILE + (uint64_t)sub * CB_SUB;
-    if (sbase >= s.nnz) break;  // whole workgroup
-    const uint32_t n_sub = (uint32_t)min<uint64_t>(CB_SUB, s.nnz - sbase);
+    if (tq0 + (uint64_t)sub * W * s.wt >= s.n) break;  // whole workgroup
+    const uint64_t q0 = tq0 + (uint64_t)(sub * W + wv) * s.wt;
+    const uint32_t nq = q0 < s.n ? (uint32_t)min<uint64_t>(s.wt, s.n - q0) : 0u;
     for (uint32_t i = tid; i < W * BM; i += CB_PT) (&s_wc[0][0])[i] = 0;
     uint64_t e[16];
-#pragma unroll
-    for (uint32_t it = 0; it < 16; it++) {
-      const uint32_t i = wv * 1024 + it * 64 + lane;
-      e[it] = i < n_sub ? cb_elem(s, (uint32_t)(sbase + i)) : 0ull;
-    }
+    const uint32_t ne = cb_wave_elems<true>(s, (uint32_t)q0, nq, (uint32_t*)s_stg + wv * 1024, e);
     __syncthreads();
     uint16_t loc[16];
     uint16_t* my = s_wc[wv];
 #pragma unroll
     for (uint32_t it = 0; it < 16; it++) {
-      const bool act = wv * 1024 + it * 64 + lane < n_sub;
+      const bool act = it * 64 + lane < ne;
       const uint32_t b = (uint32_t)(e[it] >> 32) & bmask;
-      const uint64_t peers = bucket_peers(b, act, bb);
+      const uint64_t peers = bucket_peers<NB>(b, act, bb);
       const uint32_t lr = (uint32_t)__builtin_popcountll(peers & lt);
       const uint32_t before = my[b];
       loc[it] = (uint16_t)(before + lr);
@@ -234,13 +285,13 @@ __global__ __launch_bounds__(CB_PT) void k_cb_part(CbSrc s, uint32_t bb, const u
       if (act && lr == 0) my[b] = (uint16_t)(before + (uint32_t)__builtin_popcountll(peers));
     }
     __syncthreads();
+    uint32_t n_sub;
     {
       uint32_t ls = 0;
       for (uint32_t b = b0; b < b1; b++)
 #pragma unroll
         for (uint32_t w = 0; w < W; w++) ls += s_wc[w][b];
-      uint32_t total;
-      uint32_t run = blk_excl_add(ls, s_w, total);
+      uint32_t run = blk_excl_add(ls, s_w, n_sub);
       for (uint32_t b = b0; b < b1; b++) {
         const uint32_t lb = run;
 #pragma unroll
@@ -256,7 +307,7 @@ __global__ __launch_bounds__(CB_PT) void k_cb_part(CbSrc s, uint32_t bb, const u
     __syncthreads();
 #pragma unroll
     for (uint32_t it = 0; it < 16; it++) {
-      if (wv * 1024 + it * 64 + lane < n_sub) {
+      if (it * 64 + lane < ne) {
         const uint32_t b = (uint32_t)(e[it] >> 32) & bmask;
         s_stg[my[b] + loc[it]] = e[it];
       }
@@ -281,6 +332,41 @@ struct CbBucket {
   uint64_t* out;   // [R][ndig][span]
 };
 
+// Thread p0 / 16's 16 consecutive requests of a chunk of nc, clamped to the
+// chunk (straight-line loads, so a prefetch stays in flight); cb_mask_chunk
+// then sets the ones past nc to all-ones (they sort last).
+__device__ inline void cb_load_chunk(const uint64_t* src, uint32_t nc, uint32_t p0, uint64_t (&e)[CB_IT]) {
+#pragma unroll
+  for (uint32_t i = 0; i < CB_IT; i++) e[i] = src[min(p0 + i, nc - 1)];
+}
+__device__ inline void cb_mask_chunk(uint32_t nc, uint32_t p0, uint64_t (&e)[CB_IT]) {
+#pragma unroll
+  for (uint32_t i = 0; i < CB_IT; i++) e[i] = p0 + i < nc ? e[i] : ~0ull;
+}
+
+// calvin_gl.h's block scan with LDS-only barriers (the outstanding
+// reservations and next-chunk loads stay in flight)
+__device__ inline uint32_t gl_block_excl_lds(uint32_t v, uint32_t* s_w, uint32_t& total) {
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d);
+    if (lane >= d) x = gl_combine(y, x);
+  }
+  lds_barrier();  // s_w free
+  if (lane == 63) s_w[w] = x;
+  lds_barrier();
+  uint32_t wp = GL_ID;
+  total = GL_ID;
+  for (uint32_t q = 0; q < nw; q++) {
+    if (q < w) wp = gl_combine(wp, s_w[q]);
+    total = gl_combine(total, s_w[q]);
+  }
+  const uint32_t ex_in = __shfl_up(x, 1);
+  return gl_combine(wp, lane ? ex_in : GL_ID);
+}
+
 __global__ __launch_bounds__(CB_BT) void k_cb_bucket(CbBucket a) {
   __shared__ uint32_t s_tab[1u << CB_LB_MAX];
   __shared__ uint64_t s_stg[CB_STG];
@@ -289,6 +375,7 @@ __global__ __launch_bounds__(CB_BT) void k_cb_bucket(CbBucket a) {
   __shared__ uint32_t s_dg[CB_NDIG_MAX];      // window region offset minus staging index
   __shared__ uint32_t s_w[CB_BT / 64];
   __shared__ uint32_t s_tl;
+  __shared__ uint32_t s_fl[2][64], s_fln[2];  // rows flagged per chunk (parity)
   const uint32_t tid = threadIdx.x;
   const uint32_t size = a.tot[blockIdx.x];
   if (size == 0) return;  // whole workgroup
@@ -301,39 +388,41 @@ __global__ __launch_bounds__(CB_BT) void k_cb_bucket(CbBucket a) {
   const uint32_t dpt = (a.ndig + CB_BT - 1) / CB_BT;  // windows per thread (<= 3)
   const uint32_t d0 = min(a.ndig, tid * dpt), d1 = min(a.ndig, d0 + dpt);
   uint32_t t_prev = NOTXN;  // the previous chunk's last txn
+  const uint32_t p0 = tid * CB_IT;
+  uint64_t e[CB_IT];  // this thread's 16 consecutive requests (padding: all-ones, sorts last)
+  cb_load_chunk(a.in + base, min(CB_CHUNK, size), p0, e);
   lds_barrier();
+  if (tid < 2) s_fln[tid] = 0;
   for (uint32_t c0 = 0; c0 < size; c0 += CB_CHUNK) {
     const uint32_t nc = min(CB_CHUNK, size - c0);
-    const uint64_t* src = a.in + base + c0;
-    // (1) this thread's 16 consecutive requests (padding sorts last: all-ones key)
-    uint64_t e[CB_IT];
-    const uint32_t p0 = tid * CB_IT;
-    if (p0 + CB_IT <= nc && (((uintptr_t)(src + p0)) & 15) == 0) {
+    const uint32_t pc = (c0 / CB_CHUNK) & 1u;
+    if (tid == 0 && c0) s_fln[pc] = 0;  // its flags were cleared in the last chunk
+    cb_mask_chunk(nc, p0, e);
 #pragma unroll
-      for (uint32_t q = 0; q < CB_IT / 2; q++) {
-        const ulonglong2 x = ((const ulonglong2*)(src + p0))[q];
-        e[2 * q] = x.x;
-        e[2 * q + 1] = x.y;
-      }
-    } else {
-#pragma unroll
-      for (uint32_t i = 0; i < CB_IT; i++) e[i] = p0 + i < nc ? src[p0 + i] : ~0ull;
-    }
-    if (tid == 0) s_tl = (uint32_t)src[nc - 1] >> 7;
+    for (uint32_t i = 0; i < CB_IT; i++)
+      if (p0 + i == nc - 1) s_tl = (uint32_t)e[i] >> 7;
     // (2) window counts, then one reservation per window (used after the sort)
 #pragma unroll
     for (uint32_t i = 0; i < CB_IT; i++)
       if (p0 + i < nc) atomicAdd(&s_dc[((uint32_t)e[i] >> 7) >> a.tsh], 1u);
     lds_barrier();
     const uint32_t t_last = s_tl;
-    uint32_t resv[3] = {0, 0, 0}, dcn[3] = {0, 0, 0};
+    // straight-line: a window past this thread's range adds 0 to its last one
+    uint32_t resv[3], dcn[3];
 #pragma unroll
     for (uint32_t k = 0; k < 3; k++) {
       const uint32_t d = d0 + k;
-      if (d < d1) {
-        dcn[k] = s_dc[d];
-        if (dcn[k]) resv[k] = atomicAdd(&a.gcnt[r * a.ndig + d], dcn[k]);
-      }
+      dcn[k] = d < d1 ? s_dc[min(d, a.ndig - 1)] : 0u;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 3; k++)
+      resv[k] = k < dpt ? atomicAdd(&a.gcnt[r * a.ndig + min(d0 + k, a.ndig - 1)], dcn[k]) : 0u;
+    // the next chunk's requests, in flight behind the reservations through the
+    // sort and the scan (the last chunk reloads itself: no branch)
+    uint64_t en[CB_IT];
+    {
+      const uint32_t cn = c0 + CB_CHUNK < size ? c0 + CB_CHUNK : c0;
+      cb_load_chunk(a.in + base + cn, min(CB_CHUNK, size - cn), p0, en);
     }
     // (3) stable LDS radix sort of the chunk by the row bits, 4 per pass
     for (uint32_t ps = 0; ps < npass; ps++) {
@@ -425,7 +514,14 @@ __global__ __launch_bounds__(CB_BT) void k_cb_bucket(CbBucket a) {
       acc = gl_combine(acc, x);
     }
     uint32_t total;
-    uint32_t run = gl_block_excl(acc, s_w, total);  // every table read is done past this
+    uint32_t run = gl_block_excl_lds(acc, s_w, total);  // every table read is done past this
+    // a "same txn" flag lives one chunk: the rows flagged by the previous
+    // chunk lose it before this chunk's row states go in
+    {
+      const uint32_t po = pc ^ 1u;
+      if (tid < s_fln[po]) atomicAnd(&s_tab[s_fl[po][tid]], ~1u);
+      lds_barrier();
+    }
     uint32_t grp[CB_IT];
 #pragma unroll
     for (uint32_t i = 0; i < CB_IT; i++) {
@@ -437,6 +533,7 @@ __global__ __launch_bounds__(CB_BT) void k_cb_bucket(CbBucket a) {
         if (p0 + i + 1 == nc || (uint32_t)(ne >> lsh) != lk) {
           const uint32_t tx = (uint32_t)e[i] >> 7;
           s_tab[lk] = ((run >> 5) << 3) | (((run >> 3) & 3u) << 1) | (tx == t_last ? 1u : 0u);
+          if (tx == t_last) s_fl[pc][atomicAdd(&s_fln[pc], 1u)] = lk;  // <= 64: one txn's requests
         }
       }
     }
@@ -475,6 +572,8 @@ __global__ __launch_bounds__(CB_BT) void k_cb_bucket(CbBucket a) {
     lds_barrier();
     for (uint32_t d = tid; d < a.ndig; d += CB_BT) s_dc[d] = 0;
     t_prev = t_last;
+#pragma unroll
+    for (uint32_t i = 0; i < CB_IT; i++) e[i] = en[i];
     lds_barrier();
   }
 }
@@ -498,7 +597,7 @@ __global__ __launch_bounds__(1024) void k_cb_put(const uint64_t* __restrict__ in
     for (uint32_t p0 = tid; p0 < m; p0 += 1024 * U) {
       uint64_t x[U];
 #pragma unroll
-      for (uint32_t u = 0; u < U; u++) x[u] = p0 + u * 1024 < m ? src[p0 + u * 1024] : ~0ull;
+      for (uint32_t u = 0; u < U; u++) x[u] = src[min(p0 + u * 1024, m - 1)];
 #pragma unroll
       for (uint32_t u = 0; u < U; u++) {
         if (p0 + u * 1024 >= m) continue;
@@ -535,7 +634,8 @@ bool cb_plan(uint64_t n, uint64_t nnz, uint32_t ulen, uint32_t kbits, CbPlan* p)
   q.span = (1ull << q.tsh) * ulen;
   q.ndig = (uint32_t)((n + (1ull << q.tsh) - 1) >> q.tsh);
   if (q.ndig > CB_NDIG_MAX) return false;
-  q.ntile = (uint32_t)((nnz + CB_TILE - 1) / CB_TILE);
+  const uint64_t tile_txn = (uint64_t)CB_NSUB * (CB_PT / 64) * (1024 / ulen);
+  q.ntile = (uint32_t)((n + tile_txn - 1) / tile_txn);
   q.R = CB_R;
   const uint64_t B = 1ull << q.bb;
   q.elem_bytes = nnz * 8;
@@ -552,12 +652,17 @@ hipError_t cb_run(const CbPlan& p, const CbArgs& a, hipStream_t st, hipEvent_t e
   uint32_t* tot = a.small;
   uint32_t* bbase = tot + B;
   uint32_t* gcnt = bbase + B;
-  const CbSrc s{a.keys, a.acctype, a.seq, a.nnz, a.ulen, a.kp};
+  const CbSrc s{a.keys, a.acctype, a.seq, (uint32_t)a.n, a.ulen, ((1u << 20) + a.ulen - 1) / a.ulen,
+                1024 / a.ulen, a.kp};
   hipError_t e = hipMemsetAsync(gcnt, 0, (size_t)p.R * p.ndig * 4, st);
   if (e != hipSuccess) return e;
   k_cb_count<<<p.ntile, CB_PT, 0, st>>>(s, B - 1, a.cnt);
   k_cb_scan<<<(B + 63) / 64, 256, 0, st>>>(a.cnt, p.ntile, B, tot);
-  k_cb_part<<<p.ntile, CB_PT, 0, st>>>(s, p.bb, a.cnt, tot, bbase, a.elems);
+  if (p.bb == CB_BB_MAX)
+    k_cb_part<CB_BB_MAX><<<8 * ((p.ntile + 7) / 8), CB_PT, 0, st>>>(s, p.bb, a.cnt, tot, bbase, a.elems,
+                                                                    p.ntile);
+  else
+    k_cb_part<0><<<8 * ((p.ntile + 7) / 8), CB_PT, 0, st>>>(s, p.bb, a.cnt, tot, bbase, a.elems, p.ntile);
   if (ev_part && (e = hipEventRecord(ev_part, st)) != hipSuccess) return e;
   k_cb_bucket<<<B, CB_BT, 0, st>>>(
       CbBucket{a.elems, tot, bbase, p.bb, p.lbits, p.tsh, p.ndig, p.span, gcnt, a.out});

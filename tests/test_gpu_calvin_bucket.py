@@ -69,6 +69,20 @@ def test_chunk_straddling_duplicates(engine, bucket):
     check(engine, uniform_batch(rng, 60000, 16, 4096, types=(RD, WR), order=True))
 
 
+@pytest.mark.parametrize("n,L,nrow", [(40000, 2, 200), (20000, 4, 64), (30000, 3, 500)])
+def test_rows_of_one_class(engine, bucket, n, L, nrow):
+    # every row in bucket 0 and row class 0 (keys i * 8192 with all 21 low
+    # bits varying): rows go untouched for whole 64-request rounds while txns
+    # straddle the round boundaries -- the carry table's one-round "same txn"
+    # flag must not outlive its round
+    rng = np.random.default_rng(n + nrow)
+    keys = rng.choice(np.arange(nrow, dtype=np.uint64) * np.uint64(8192), size=n * L)
+    keys[0] = (1 << 21) - 1
+    at = rng.choice(np.array([RD, WR, SCAN, XP], np.uint8), size=n * L, p=[0.6, 0.2, 0.1, 0.1])
+    od = rng.integers(0, n // 8, size=n).astype(np.uint64)
+    check(engine, d.EpochBatch((np.arange(n + 1) * L).astype(np.uint32), keys, at, None, None, od))
+
+
 def test_single_hot_row(engine, bucket):
     rng = np.random.default_rng(14)
     at = np.where(rng.random(20000) < 0.3, WR, RD).astype(np.uint8)

@@ -22,7 +22,7 @@ def main():
             per[k] += float(r["Counter_Value"])
             names[r["Dispatch_Id"]] = r["Kernel_Name"]
         for (disp, cn), v in per.items():
-            kn = names[disp].split("(")[0]
+            kn = names[disp].replace("(anonymous namespace)::", "").split("(")[0]
             acc[kn][cn].append(v)
     for kn in sorted(acc):
         if want and not any(w in kn for w in want):
