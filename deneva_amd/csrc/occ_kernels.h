@@ -419,6 +419,7 @@ struct WidenArgs {
 };
 void launch_widen(const WidenArgs& a, unsigned n_cu, hipStream_t st);
 void launch_copy16(const void* src, void* dst, uint64_t bytes, unsigned grid, hipStream_t st);
+void launch_copy16_chunk(const void* src, void* dst, uint64_t bytes, unsigned grid, hipStream_t st);
 
 // Several word fills in one launch (replaces a run of hipMemsetAsync calls,
 // each of which costs a dispatch and an idle gap on the stream).

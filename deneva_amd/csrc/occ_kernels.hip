@@ -977,7 +977,10 @@ void launch_widen(const WidenArgs& a, unsigned n_cu, hipStream_t st) {
 
 // --------------------------------------------------------------------------
 // k_copy16: the bandwidth reference (dcc_copy_bandwidth): 16 B per lane per
-// load, four loads in flight per thread before their stores, grid-stride.
+// load.  Grid-stride form: four loads in flight per thread before their
+// stores.  Chunked form: each workgroup copies one contiguous range (DRAM
+// pages stay open), eight loads in flight per thread, non-temporal loads and
+// stores (the copy is read and written once).
 __global__ __launch_bounds__(256) void k_copy16(const uint4* __restrict__ src, uint4* __restrict__ dst,
                                                 uint64_t n16) {
   const uint64_t stride = (uint64_t)gridDim.x * 256;
@@ -991,8 +994,29 @@ __global__ __launch_bounds__(256) void k_copy16(const uint4* __restrict__ src, u
   }
   for (; q < n16; q += stride) dst[q] = src[q];
 }
+__global__ __launch_bounds__(256) void k_copy16_chunk(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                      uint64_t n16) {
+  constexpr uint32_t U = 8;
+  const uint64_t per = (n16 + gridDim.x - 1) / gridDim.x;
+  const uint64_t lo = (uint64_t)blockIdx.x * per, hi = min(n16, lo + per);
+  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+  const v4u* s4 = (const v4u*)src;
+  v4u* d4 = (v4u*)dst;
+  uint64_t q = lo + threadIdx.x;
+  for (; q + (U - 1) * 256 < hi; q += U * 256) {
+    v4u v[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++) v[u] = __builtin_nontemporal_load(s4 + q + u * 256);
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++) __builtin_nontemporal_store(v[u], d4 + q + u * 256);
+  }
+  for (; q < hi; q += 256) dst[q] = src[q];
+}
 void launch_copy16(const void* src, void* dst, uint64_t bytes, unsigned grid, hipStream_t st) {
   k_copy16<<<grid ? grid : 1u, 256, 0, st>>>((const uint4*)src, (uint4*)dst, bytes / 16);
+}
+void launch_copy16_chunk(const void* src, void* dst, uint64_t bytes, unsigned grid, hipStream_t st) {
+  k_copy16_chunk<<<grid ? grid : 1u, 256, 0, st>>>((const uint4*)src, (uint4*)dst, bytes / 16);
 }
 
 }  // namespace dcc

@@ -185,9 +185,11 @@ int dcc_set_profiling(dcc_ctx* ctx, int enable);
 int dcc_set_option(dcc_ctx* ctx, int option, int64_t value);
 /* Pre-size device workspaces so a later call performs no allocation. */
 int dcc_reserve(dcc_ctx* ctx, uint64_t max_txn, uint64_t max_nnz);
-/* Achievable HBM bandwidth on this device (measurement aid): a
- * hand-written 16-byte-per-lane copy kernel over two `bytes`-sized device
- * buffers, `reps` launches timed with HIP events; *gbps = 2 * bytes / time. */
+/* Achievable HBM bandwidth on this device (measurement aid):
+ * hand-written 16-byte-per-lane copy kernels over two `bytes`-sized device
+ * buffers (grid-stride; one contiguous range per workgroup with non-temporal
+ * loads and stores at 2 / 4 / 8 workgroups per CU), `reps` launches of each
+ * timed with HIP events; *gbps = 2 * bytes / time of the fastest form. */
 int dcc_copy_bandwidth(dcc_ctx* ctx, uint64_t bytes, int reps, double* gbps);
 /* Pinned (page-locked) host memory for batches and outputs: a host batch in it
  * is copied at DMA speed with no staging copy.  Free with dcc_host_free. */
