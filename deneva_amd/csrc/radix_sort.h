@@ -15,15 +15,27 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 namespace dcc {
 
 constexpr uint32_t RS_THREADS = 512;
 constexpr uint32_t RS_ITEMS = 16;
 constexpr uint32_t RS_TILE = RS_THREADS * RS_ITEMS;  // 8192 pairs per workgroup
 
-inline uint64_t rs_tiles(uint64_t m) { return (m + RS_TILE - 1) / RS_TILE; }
-// u32 words of scratch a sort of m pairs needs: counts [256][tiles] + totals [256]
-inline uint64_t rs_scratch_words(uint64_t m) { return 256 * (rs_tiles(m) + 1); }
+constexpr uint32_t RS_ITEMS_SMALL = 4;           // sorts of <= RS_SMALL pairs: 2,048-pair tiles
+constexpr uint64_t RS_SMALL = 2ull << 20;
+
+inline uint64_t rs_tiles(uint64_t m) {
+  const uint64_t t = m <= RS_SMALL ? (uint64_t)RS_THREADS * RS_ITEMS_SMALL : RS_TILE;
+  return (m + t - 1) / t;
+}
+// u32 words of scratch a sort of up to m pairs needs: counts [256][tiles] +
+// totals [256] (monotone in m: covers either tiling of any m' <= m)
+inline uint64_t rs_scratch_words(uint64_t m) {
+  const uint64_t ts = (uint64_t)RS_THREADS * RS_ITEMS_SMALL;
+  return 256 * ((std::min<uint64_t>(m, RS_SMALL) + ts - 1) / ts + (m + RS_TILE - 1) / RS_TILE + 1);
+}
 
 // Sorts m pairs by the low `bits` key bits.  Input in k[0]/v[0]; k[1]/v[1] are
 // equal-sized ping-pong buffers.  Returns the index (0 or 1) of the buffer

@@ -1,6 +1,8 @@
 // gfx950 stable LSD radix sort of (key, u32 value) pairs — see radix_sort.h.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "dcc_device.h"
 #include "radix_sort.h"
 
@@ -53,7 +55,7 @@ __device__ inline uint32_t block_excl_scan(uint32_t v, uint32_t* sh /*[RS_W]*/, 
 // are sorted -- costs one LDS atomic, not one per item (the skewed top-digit
 // pass of a YCSB key sort took 34 us with an atomic per item, the others
 // ~16-19; adding once per digit per wave instruction, via digit_peers, 41).
-template <typename K>
+template <typename K, uint32_t IT>
 __global__ __launch_bounds__(RS_THREADS) void k_rs_hist(const K* __restrict__ keys, uint64_t m,
                                                         uint32_t shift, uint32_t* __restrict__ cnt,
                                                         uint32_t tiles) {
@@ -63,11 +65,11 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_hist(const K* __restrict__ ke
   const uint32_t wv = threadIdx.x >> 6;
   for (uint32_t q = threadIdx.x; q < W * 256; q += RS_THREADS) (&s_h[0][0])[q] = 0;
   __syncthreads();
-  const uint64_t p0 = (uint64_t)blockIdx.x * RS_TILE + (uint64_t)threadIdx.x * RS_ITEMS;
-  K k[RS_ITEMS];
-  if (p0 + RS_ITEMS <= m && ((uintptr_t)(keys + p0) & 15) == 0) {
+  const uint64_t p0 = (uint64_t)blockIdx.x * (RS_THREADS * IT) + (uint64_t)threadIdx.x * IT;
+  K k[IT];
+  if (p0 + IT <= m && ((uintptr_t)(keys + p0) & 15) == 0) {
 #pragma unroll
-    for (uint32_t q = 0; q < RS_ITEMS / V; q++) {
+    for (uint32_t q = 0; q < IT / V; q++) {
       const uint4 x = ((const uint4*)(keys + p0))[q];
       const K* xk = (const K*)&x;
 #pragma unroll
@@ -75,12 +77,12 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_hist(const K* __restrict__ ke
     }
   } else {
 #pragma unroll
-    for (uint32_t i = 0; i < RS_ITEMS; i++) k[i] = p0 + i < m ? keys[p0 + i] : (K)0;
+    for (uint32_t i = 0; i < IT; i++) k[i] = p0 + i < m ? keys[p0 + i] : (K)0;
   }
-  const uint32_t n = p0 >= m ? 0u : (uint32_t)min<uint64_t>(RS_ITEMS, m - p0);
+  const uint32_t n = p0 >= m ? 0u : (uint32_t)min<uint64_t>(IT, m - p0);
   uint32_t run_d = (uint32_t)(k[0] >> shift) & 255u, run_n = 0;
 #pragma unroll
-  for (uint32_t i = 0; i < RS_ITEMS; i++) {
+  for (uint32_t i = 0; i < IT; i++) {
     const uint32_t d = (uint32_t)(k[i] >> shift) & 255u;
     if (i < n) {
       if (d != run_d) {
@@ -136,7 +138,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scan(uint32_t* __restrict__ c
 // round (a wave's LDS operations execute in order) -- and the waves' counts
 // are combined once.  Then the tile is staged in LDS in digit order and
 // written out with coalesced runs per digit.
-template <typename K>
+template <typename K, uint32_t IT>
 __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(const K* __restrict__ kin,
                                                            const uint32_t* __restrict__ vin,
                                                            K* __restrict__ kout,
@@ -145,22 +147,23 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(const K* __restrict__
                                                            const uint32_t* __restrict__ cnt,
                                                            const uint32_t* __restrict__ tot,
                                                            uint32_t tiles) {
-  constexpr uint32_t W = RS_W, WI = RS_TILE / W;  // waves, items per wave
-  __shared__ K s_key[RS_TILE];
-  __shared__ uint32_t s_val[RS_TILE];
+  constexpr uint32_t TILE = RS_THREADS * IT;
+  constexpr uint32_t W = RS_W, WI = TILE / W;  // waves, items per wave
+  __shared__ K s_key[TILE];
+  __shared__ uint32_t s_val[TILE];
   __shared__ uint32_t s_wc[W][256];  // per wave: running digit count, then its base in the tile
   __shared__ uint32_t s_gb[256];     // global destination base per digit
   __shared__ uint32_t s_tb[256];     // tile-local base per digit
   __shared__ uint32_t sh[RS_W];
   const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
   const bool dig = tid < 256;  // this thread owns digit tid
-  const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
+  const uint64_t base = (uint64_t)blockIdx.x * TILE;
   const uint64_t wbase = base + (uint64_t)wv * WI;
 
-  K k[RS_ITEMS];
-  uint32_t v[RS_ITEMS];
+  K k[IT];
+  uint32_t v[IT];
 #pragma unroll
-  for (uint32_t it = 0; it < RS_ITEMS; it++) {
+  for (uint32_t it = 0; it < IT; it++) {
     const uint64_t p = wbase + it * 64 + lane;
     k[it] = p < m ? kin[p] : (K)0;
     v[it] = p < m ? vin[p] : 0u;
@@ -174,10 +177,10 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(const K* __restrict__
   __syncthreads();
 
   const uint64_t lt = lanemask_lt();
-  uint32_t loc[RS_ITEMS];
+  uint32_t loc[IT];
   uint32_t* wc = s_wc[wv];
 #pragma unroll
-  for (uint32_t it = 0; it < RS_ITEMS; it++) {
+  for (uint32_t it = 0; it < IT; it++) {
     const uint64_t p = wbase + it * 64 + lane;
     const bool act = p < m;
     const uint32_t d = (uint32_t)(k[it] >> shift) & 255u;
@@ -211,7 +214,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(const K* __restrict__
   }
   __syncthreads();
 #pragma unroll
-  for (uint32_t it = 0; it < RS_ITEMS; it++) {
+  for (uint32_t it = 0; it < IT; it++) {
     const uint64_t p = wbase + it * 64 + lane;
     if (p < m) {
       const uint32_t d = (uint32_t)(k[it] >> shift) & 255u;
@@ -221,7 +224,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(const K* __restrict__
     }
   }
   __syncthreads();
-  const uint32_t n_here = (uint32_t)min<uint64_t>(RS_TILE, m - base);
+  const uint32_t n_here = (uint32_t)min<uint64_t>(TILE, m - base);
   for (uint32_t j = tid; j < n_here; j += RS_THREADS) {
     const K kk = s_key[j];
     const uint32_t d = (uint32_t)(kk >> shift) & 255u;
@@ -231,22 +234,35 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(const K* __restrict__
   }
 }
 
-template <typename K>
-static int radix_sort_impl(K* k[2], uint32_t* v[2], uint64_t m, uint32_t bits, uint32_t* scratch,
-                           hipStream_t st) {
+template <typename K, uint32_t IT>
+static int radix_sort_run(K* k[2], uint32_t* v[2], uint64_t m, uint32_t bits, uint32_t* scratch,
+                          hipStream_t st) {
   int cur = 0;
-  if (m <= 1 || bits == 0) return cur;
-  const uint32_t tiles = (uint32_t)rs_tiles(m);
+  const uint32_t tiles = (uint32_t)((m + RS_THREADS * IT - 1) / (RS_THREADS * IT));
   uint32_t* cnt = scratch;
   uint32_t* tot = scratch + 256ull * tiles;
   for (uint32_t shift = 0; shift < bits; shift += 8) {
-    k_rs_hist<K><<<tiles, RS_THREADS, 0, st>>>(k[cur], m, shift, cnt, tiles);
+    k_rs_hist<K, IT><<<tiles, RS_THREADS, 0, st>>>(k[cur], m, shift, cnt, tiles);
     k_rs_scan<<<256, RS_THREADS, 0, st>>>(cnt, tiles, tot);
-    k_rs_scatter<K><<<tiles, RS_THREADS, 0, st>>>(k[cur], v[cur], k[cur ^ 1], v[cur ^ 1], m, shift,
-                                                  cnt, tot, tiles);
+    k_rs_scatter<K, IT><<<tiles, RS_THREADS, 0, st>>>(k[cur], v[cur], k[cur ^ 1], v[cur ^ 1], m, shift,
+                                                      cnt, tot, tiles);
     cur ^= 1;
   }
   return cur;
+}
+// small sorts (the Calvin rank of 1M orders, index builds) take 2,048-pair
+// tiles: four times the workgroups of the 8,192-pair tiles, each with a
+// quarter of the latency-bound chain
+template <typename K>
+static int radix_sort_impl(K* k[2], uint32_t* v[2], uint64_t m, uint32_t bits, uint32_t* scratch,
+                           hipStream_t st) {
+  if (m <= 1 || bits == 0) return 0;
+  static const bool small_on = [] {  // DCC_RS_SMALL=0: 8,192-pair tiles at every size (A/B)
+    const char* e = getenv("DCC_RS_SMALL");
+    return !(e && e[0] == '0');
+  }();
+  if (small_on && m <= RS_SMALL) return radix_sort_run<K, RS_ITEMS_SMALL>(k, v, m, bits, scratch, st);
+  return radix_sort_run<K, RS_ITEMS>(k, v, m, bits, scratch, st);
 }
 
 int radix_sort_u32(uint32_t* k[2], uint32_t* v[2], uint64_t m, uint32_t bits, uint32_t* scratch,
