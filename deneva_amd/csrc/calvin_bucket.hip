@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "calvin_gl.h"
 #include "dcc.h"
@@ -111,6 +112,8 @@ struct CbSrc {
   uint32_t ulen;  // requests per txn
   uint32_t um;    // (2^20 + ulen - 1) / ulen: e / ulen == (e * um) >> 20 for e <= 1024
   uint32_t wt;    // txns per wave and sub-tile (1024 / ulen)
+  uint32_t var;   // DCC_CB_VARIANT timing variants (wrong results): 1 no partition stores,
+                  // 2 no ranking, 4 no element loads
   KeyPack kp;
 };
 
@@ -269,7 +272,16 @@ __global__ __launch_bounds__(CB_PT) void k_cb_part(CbSrc s, uint32_t bb, const u
     const uint32_t nq = q0 < s.n ? (uint32_t)min<uint64_t>(s.wt, s.n - q0) : 0u;
     for (uint32_t i = tid; i < W * BM; i += CB_PT) (&s_wc[0][0])[i] = 0;
     uint64_t e[16];
-    const uint32_t ne = cb_wave_elems<true>(s, (uint32_t)q0, nq, (uint32_t*)s_stg + wv * 1024, e);
+    uint32_t ne;
+    if (s.var & 4u) {
+      ne = nq * s.ulen;
+#pragma unroll
+      for (uint32_t it = 0; it < 16; it++)
+        e[it] = ((uint64_t)((((uint32_t)q0 * 16 + it * 64 + lane) * 2654435761u) >> 8) << 32) |
+                ((uint32_t)min<uint64_t>(q0, s.n - 1) << 7);  // in-range row and txn
+    } else {
+      ne = cb_wave_elems<true>(s, (uint32_t)q0, nq, (uint32_t*)s_stg + wv * 1024, e);
+    }
     __syncthreads();
     uint16_t loc[16];
     uint16_t* my = s_wc[wv];
@@ -277,7 +289,7 @@ __global__ __launch_bounds__(CB_PT) void k_cb_part(CbSrc s, uint32_t bb, const u
     for (uint32_t it = 0; it < 16; it++) {
       const bool act = it * 64 + lane < ne;
       const uint32_t b = (uint32_t)(e[it] >> 32) & bmask;
-      const uint64_t peers = bucket_peers<NB>(b, act, bb);
+      const uint64_t peers = (s.var & 2u) ? (act ? 1ull << lane : 0ull) : bucket_peers<NB>(b, act, bb);
       const uint32_t lr = (uint32_t)__builtin_popcountll(peers & lt);
       const uint32_t before = my[b];
       loc[it] = (uint16_t)(before + lr);
@@ -315,7 +327,7 @@ __global__ __launch_bounds__(CB_PT) void k_cb_part(CbSrc s, uint32_t bb, const u
     __syncthreads();
     for (uint32_t j = tid; j < n_sub; j += CB_PT) {
       const uint64_t x = s_stg[j];
-      out[s_gof[(uint32_t)(x >> 32) & bmask] + j] = x;
+      if (!(s.var & 1u)) out[s_gof[(uint32_t)(x >> 32) & bmask] + j] = x;
     }
     __syncthreads();
   }
@@ -330,6 +342,8 @@ struct CbBucket {
   uint64_t span;
   uint32_t* gcnt;  // [R][ndig]
   uint64_t* out;   // [R][ndig][span]
+  uint32_t var;    // DCC_CB_VARIANT (wrong results): 8 no radix passes, 16 no pair stores,
+                   // 32 no grant-group scan, 64 no staging/output
 };
 
 // Thread p0 / 16's 16 consecutive requests of a chunk of nc, clamped to the
@@ -371,7 +385,7 @@ __global__ __launch_bounds__(CB_BT) void k_cb_bucket(CbBucket a) {
   __shared__ uint32_t s_tab[1u << CB_LB_MAX];
   __shared__ uint64_t s_stg[CB_STG];
   __shared__ uint16_t s_rc[16 * CB_BT];       // radix counts [digit][thread]
-  __shared__ uint32_t s_dc[CB_NDIG_MAX];      // window counts, then cursors
+  __shared__ uint32_t s_dc[CB_NDIG_MAX + 1];  // window counts, then cursors (+ a spare)
   __shared__ uint32_t s_dg[CB_NDIG_MAX];      // window region offset minus staging index
   __shared__ uint32_t s_w[CB_BT / 64];
   __shared__ uint32_t s_tl;
@@ -384,7 +398,7 @@ __global__ __launch_bounds__(CB_BT) void k_cb_bucket(CbBucket a) {
   const uint32_t ntab = 1u << a.lbits;
   for (uint32_t i = tid; i < ntab; i += CB_BT) s_tab[i] = TAB_EMPTY;
   for (uint32_t d = tid; d < a.ndig; d += CB_BT) s_dc[d] = 0;
-  const uint32_t npass = (a.lbits + 3) / 4;
+  const uint32_t npass = (a.var & 8u) ? 0u : (a.lbits + 3) / 4;
   const uint32_t dpt = (a.ndig + CB_BT - 1) / CB_BT;  // windows per thread (<= 3)
   const uint32_t d0 = min(a.ndig, tid * dpt), d1 = min(a.ndig, d0 + dpt);
   uint32_t t_prev = NOTXN;  // the previous chunk's last txn
@@ -426,12 +440,12 @@ __global__ __launch_bounds__(CB_BT) void k_cb_bucket(CbBucket a) {
     }
     // (3) stable LDS radix sort of the chunk by the row bits, 4 per pass
     for (uint32_t ps = 0; ps < npass; ps++) {
-      const uint32_t sh = 32 + a.bb + 4 * ps;
+      const uint32_t sh = a.bb + 4 * ps;  // in the high word
       uint64_t clo = 0, chi = 0;  // 8-bit running counts of digits 0-7 / 8-15
       uint32_t rk[CB_IT];
 #pragma unroll
       for (uint32_t i = 0; i < CB_IT; i++) {
-        const uint32_t d = (uint32_t)(e[i] >> sh) & 15u;
+        const uint32_t d = ((uint32_t)(e[i] >> 32) >> sh) & 15u;
         const uint32_t fs = (d & 7u) * 8u;
         if (d < 8) {
           rk[i] = (uint32_t)(clo >> fs) & 255u;
@@ -463,7 +477,7 @@ __global__ __launch_bounds__(CB_BT) void k_cb_bucket(CbBucket a) {
       lds_barrier();
 #pragma unroll
       for (uint32_t i = 0; i < CB_IT; i++) {
-        const uint32_t d = (uint32_t)(e[i] >> sh) & 15u;
+        const uint32_t d = ((uint32_t)(e[i] >> 32) >> sh) & 15u;
         s_stg[stg_ix(s_rc[d * CB_BT + tid] + rk[i])] = e[i];
       }
       lds_barrier();
@@ -478,64 +492,107 @@ __global__ __launch_bounds__(CB_BT) void k_cb_bucket(CbBucket a) {
     }
     // (4) grant-group scan; a row's first request in the chunk continues from
     // the carry table, its last one stores the row's state back
-    const uint32_t lsh = 32 + a.bb;
+    // Row of a request: its high word past the bucket bits (32-bit shifts).
+    const uint32_t bsh = a.bb;
     const uint64_t prev_e = p0 ? s_stg[stg_ix(p0 - 1)] : ~0ull;
     const uint64_t next_e = p0 + CB_IT < nc ? s_stg[stg_ix(p0 + CB_IT)] : ~0ull;
-    uint32_t st[CB_IT];
     uint32_t dupm = 0;
-    uint32_t acc = GL_ID;
-#pragma unroll
-    for (uint32_t i = 0; i < CB_IT; i++) {
-      const uint64_t pe = i ? e[i - 1] : prev_e;
-      const uint32_t lk = (uint32_t)(e[i] >> lsh), plk = (uint32_t)(pe >> lsh);
-      const uint32_t v = (uint32_t)e[i], tx = v >> 7;
-      const uint32_t typ = (v & 1u) ? CV_EX : CV_SH;
-      uint32_t x;
-      if (p0 + i >= nc) {
-        x = GL_ID;
-      } else if (p0 + i == 0 || lk != plk) {
-        const uint32_t c = s_tab[lk];
-        const uint32_t cl = (c >> 1) & 3u, cc = c >> 3;
-        if (cl == CV_NONE) {
-          x = gl_pack(1, typ, typ, 0);
-        } else if ((c & 1u) && tx == t_prev) {  // same txn as the row's last request
-          x = gl_pack(1, cl, cl, cc);
-          dupm |= 1u << i;
-        } else {
-          x = gl_pack(1, cl, typ, cc + ((cl == CV_EX || typ == CV_EX) ? 1u : 0u));
-        }
-      } else if (tx == (uint32_t)pe >> 7) {  // duplicate row of the same txn
-        x = GL_ID;
-        dupm |= 1u << i;
-      } else {
-        x = gl_pack(0, typ, typ, 0);
-      }
-      st[i] = x;
-      acc = gl_combine(acc, x);
-    }
-    uint32_t total;
-    uint32_t run = gl_block_excl_lds(acc, s_w, total);  // every table read is done past this
-    // a "same txn" flag lives one chunk: the rows flagged by the previous
-    // chunk lose it before this chunk's row states go in
-    {
-      const uint32_t po = pc ^ 1u;
-      if (tid < s_fln[po]) atomicAnd(&s_tab[s_fl[po][tid]], ~1u);
-      lds_barrier();
-    }
     uint32_t grp[CB_IT];
+    if (a.var & 32u) {
 #pragma unroll
-    for (uint32_t i = 0; i < CB_IT; i++) {
-      run = gl_combine(run, st[i]);
-      grp[i] = ((dupm >> i) & 1u) ? DCC_GROUP_NONE : run >> 5;
-      if (p0 + i < nc) {
-        const uint64_t ne = i + 1 < CB_IT ? e[i + 1] : next_e;
-        const uint32_t lk = (uint32_t)(e[i] >> lsh);
-        if (p0 + i + 1 == nc || (uint32_t)(ne >> lsh) != lk) {
-          const uint32_t tx = (uint32_t)e[i] >> 7;
-          s_tab[lk] = ((run >> 5) << 3) | (((run >> 3) & 3u) << 1) | (tx == t_last ? 1u : 0u);
-          if (tx == t_last) s_fl[pc][atomicAdd(&s_fln[pc], 1u)] = lk;  // <= 64: one txn's requests
+      for (uint32_t i = 0; i < CB_IT; i++) grp[i] = (uint32_t)(e[i] >> 32) >> bsh;
+      goto staged;
+    }
+    {
+      // every item's carry word read up front (one LDS round trip, not one per
+      // row start inside the branches below)
+      uint32_t cw[CB_IT];
+#pragma unroll
+      for (uint32_t i = 0; i < CB_IT; i++) cw[i] = s_tab[min((uint32_t)(e[i] >> 32) >> bsh, ntab - 1)];
+      // The thread's 16 requests folded left to right into the gl state
+      // (flag, ft, lt, cnt) in separate registers; per request the inclusive
+      // local count lc[i], and bit masks: a row start at or before i (startm),
+      // a non-identity request at or before i (seenm), the local last type
+      // after i (ltp, 2 bits each).  A row start resets the state.
+      uint32_t lc[CB_IT];
+      uint32_t startm = 0, seenm = 0, ltp = 0;
+      uint32_t lflag = 0, lft = CV_NONE, llt = CV_NONE, lcnt = 0;
+#pragma unroll
+      for (uint32_t i = 0; i < CB_IT; i++) {
+        const uint64_t pe = i ? e[i - 1] : prev_e;
+        const uint32_t lk = (uint32_t)(e[i] >> 32) >> bsh, plk = (uint32_t)(pe >> 32) >> bsh;
+        const uint32_t v = (uint32_t)e[i], tx = v >> 7;
+        const uint32_t typ = (v & 1u) ? CV_EX : CV_SH;
+        if (p0 + i < nc) {
+          if (p0 + i == 0 || lk != plk) {
+            const uint32_t c = cw[i];
+            const uint32_t cl = (c >> 1) & 3u, cc = c >> 3;
+            uint32_t ft;
+            if (cl == CV_NONE) {
+              ft = typ;
+              llt = typ;
+              lcnt = 0;
+            } else if ((c & 1u) && tx == t_prev) {  // same txn as the row's last request
+              ft = cl;
+              llt = cl;
+              lcnt = cc;
+              dupm |= 1u << i;
+            } else {
+              ft = cl;
+              llt = typ;
+              lcnt = cc + ((cl == CV_EX || typ == CV_EX) ? 1u : 0u);
+            }
+            lflag = 1;
+            lft = lft == CV_NONE ? ft : lft;
+          } else if (tx == (uint32_t)pe >> 7) {  // duplicate row of the same txn: identity
+            dupm |= 1u << i;
+          } else {
+            lcnt += (llt == CV_EX || (llt == CV_SH && typ == CV_EX)) ? 1u : 0u;
+            lft = lft == CV_NONE ? typ : lft;
+            llt = typ;
+          }
+        }
+        lc[i] = lcnt;
+        startm |= lflag << i;
+        seenm |= (lft != CV_NONE ? 1u : 0u) << i;
+        ltp |= llt << (2 * i);
+      }
+      uint32_t total;
+      const uint32_t run =  // every table read is done past this
+          gl_block_excl_lds(gl_pack(lflag, lft, llt, lcnt), s_w, total);
+      // a "same txn" flag lives one chunk: the rows flagged by the previous
+      // chunk lose it before this chunk's row states go in
+      {
+        const uint32_t po = pc ^ 1u;
+        if (tid < s_fln[po]) atomicAnd(&s_tab[s_fl[po][tid]], ~1u);
+        lds_barrier();
+      }
+      // inclusive state at i = prefix (x) local state at i
+      const uint32_t pcnt = run >> 5, plt = (run >> 3) & 3u;
+      const uint32_t pb = (plt != CV_NONE && lft != CV_NONE && (plt == CV_EX || lft == CV_EX)) ? 1u : 0u;
+#pragma unroll
+      for (uint32_t i = 0; i < CB_IT; i++) {
+        const uint32_t cnt = ((startm >> i) & 1u) ? lc[i] : pcnt + lc[i] + (pb & (seenm >> i));
+        grp[i] = ((dupm >> i) & 1u) ? DCC_GROUP_NONE : cnt;
+        if (p0 + i < nc) {
+          const uint64_t ne = i + 1 < CB_IT ? e[i + 1] : next_e;
+          const uint32_t lk = (uint32_t)(e[i] >> 32) >> bsh;
+          if (p0 + i + 1 == nc || (uint32_t)(ne >> 32) >> bsh != lk) {
+            const uint32_t tx = (uint32_t)e[i] >> 7;
+            const uint32_t lt_i = (ltp >> (2 * i)) & 3u;
+            s_tab[lk] = (cnt << 3) | ((lt_i != CV_NONE ? lt_i : plt) << 1) | (tx == t_last ? 1u : 0u);
+            if (tx == t_last) s_fl[pc][atomicAdd(&s_fln[pc], 1u)] = lk;  // <= 64: one txn's requests
+          }
         }
       }
+    }
+  staged:
+    if (a.var & 64u) {
+      uint32_t x = 0;
+#pragma unroll
+      for (uint32_t i = 0; i < CB_IT; i++) x ^= grp[i];
+      if (x == 0x9e3779b9u) a.gcnt[0] = resv[0] + resv[1] + resv[2];
+      goto next_chunk;
     }
     // (5) the (request, group) pairs staged by window, appended to the regions
     {
@@ -555,21 +612,23 @@ __global__ __launch_bounds__(CB_BT) void k_cb_bucket(CbBucket a) {
       }
     }
     lds_barrier();
+    {  // every position drawn before the first store (padding draws from a spare counter)
+      uint32_t q[CB_IT];
 #pragma unroll
-    for (uint32_t i = 0; i < CB_IT; i++) {
-      if (p0 + i < nc) {
-        const uint32_t v = (uint32_t)e[i];
-        const uint32_t q = atomicAdd(&s_dc[(v >> 7) >> a.tsh], 1u);
-        s_stg[q] = ((uint64_t)grp[i] << 32) | v;
-      }
+      for (uint32_t i = 0; i < CB_IT; i++)
+        q[i] = atomicAdd(&s_dc[p0 + i < nc ? ((uint32_t)e[i] >> 7) >> a.tsh : CB_NDIG_MAX], 1u);
+#pragma unroll
+      for (uint32_t i = 0; i < CB_IT; i++)
+        if (p0 + i < nc) s_stg[q[i]] = ((uint64_t)grp[i] << 32) | (uint32_t)e[i];
     }
     lds_barrier();
     for (uint32_t j = tid; j < nc; j += CB_BT) {
       const uint64_t x = s_stg[j];
       const uint32_t d = ((uint32_t)x >> 7) >> a.tsh;
-      a.out[((uint64_t)r * a.ndig + d) * a.span + (uint32_t)(s_dg[d] + j)] = x;
+      if (!(a.var & 16u)) a.out[((uint64_t)r * a.ndig + d) * a.span + (uint32_t)(s_dg[d] + j)] = x;
     }
     lds_barrier();
+  next_chunk:
     for (uint32_t d = tid; d < a.ndig; d += CB_BT) s_dc[d] = 0;
     t_prev = t_last;
 #pragma unroll
@@ -652,8 +711,12 @@ hipError_t cb_run(const CbPlan& p, const CbArgs& a, hipStream_t st, hipEvent_t e
   uint32_t* tot = a.small;
   uint32_t* bbase = tot + B;
   uint32_t* gcnt = bbase + B;
+  static const uint32_t var = [] {
+    const char* e = getenv("DCC_CB_VARIANT");
+    return e ? (uint32_t)atoi(e) : 0u;
+  }();
   const CbSrc s{a.keys, a.acctype, a.seq, (uint32_t)a.n, a.ulen, ((1u << 20) + a.ulen - 1) / a.ulen,
-                1024 / a.ulen, a.kp};
+                1024 / a.ulen, var, a.kp};
   hipError_t e = hipMemsetAsync(gcnt, 0, (size_t)p.R * p.ndig * 4, st);
   if (e != hipSuccess) return e;
   k_cb_count<<<p.ntile, CB_PT, 0, st>>>(s, B - 1, a.cnt);
@@ -665,7 +728,7 @@ hipError_t cb_run(const CbPlan& p, const CbArgs& a, hipStream_t st, hipEvent_t e
     k_cb_part<0><<<8 * ((p.ntile + 7) / 8), CB_PT, 0, st>>>(s, p.bb, a.cnt, tot, bbase, a.elems, p.ntile);
   if (ev_part && (e = hipEventRecord(ev_part, st)) != hipSuccess) return e;
   k_cb_bucket<<<B, CB_BT, 0, st>>>(
-      CbBucket{a.elems, tot, bbase, p.bb, p.lbits, p.tsh, p.ndig, p.span, gcnt, a.out});
+      CbBucket{a.elems, tot, bbase, p.bb, p.lbits, p.tsh, p.ndig, p.span, gcnt, a.out, var});
   if (ev_bucket && (e = hipEventRecord(ev_bucket, st)) != hipSuccess) return e;
   k_cb_put<<<p.ndig, 1024, 0, st>>>(a.out, gcnt, p.ndig, p.span, (uint32_t)a.n, a.ulen, p.tsh, a.group,
                                     a.rc);
