@@ -159,6 +159,9 @@ struct dcc_ctx {
   uint32_t mt_rows32 = 0;                        // upload source of the row counter
   DevBuf mt_misc, mt_slot, mt_sval, mt_slot2, mt_sval2, mt_sfl, mt_stx, mt_txn, mt_agg;
   DevBuf mt_sflB, mt_stxB, mt_k1, mt_tcnt, mt_ul;
+  DevBuf mt_lb;          // fused round scan: look-back status per tile (k_mt_round)
+  uint32_t mt_tag = 0;   // its round tag (monotone; the buffer is zeroed when it wraps)
+  int mt_fused = -1;     // DCC_MT_FUSED: 1 fused round scan (default), 0 up / top / down
   // GPU index (index.hip): key table, newest insert ordinal per key, rows
   DevBuf ix_keys, ix_ord, ix_rows, ix_cnt, wv_buf, ix_scr, wv_hbuf, wv_obuf;
   uint32_t ix_bits = 0;

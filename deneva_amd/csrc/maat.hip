@@ -540,6 +540,158 @@ __global__ __launch_bounds__(256) void k_mt_down(MtRoundArgs a) {
   }
 }
 
+// ---------------------------------------------------------------- fused round
+// k_mt_up + k_mt_top + k_mt_down in one launch (one read of each tile, no
+// aggregate pass): a single-pass scan with decoupled look-back.  Tile j
+// publishes its aggregate as soon as it has it, then wave 0 looks back 64
+// tiles at a time (lane 0 the nearest) until it meets a published inclusive
+// prefix, combines what it read in order, and publishes its own inclusive
+// prefix.  Status words carry the round's tag (tag << 2 | 1 aggregate, | 2
+// inclusive), so nothing is reset between rounds.  Workgroups are dispatched
+// in index order, so every tile a look-back waits on is running or done; the
+// spins are bounded anyway (release/acquire recipe and timeout flag of
+// grid_barrier, occ_kernels.hip): a timeout raises MT_ERR_SPIN and the host
+// fails the epoch.
+struct __attribute__((aligned(64))) MtLb {
+  uint64_t agg_rmax, agg_wmin, inc_rmax, inc_wmin;
+  uint32_t agg_fu, inc_fu;  // flag | und << 1
+  uint32_t status, pad[5];
+};
+static_assert(sizeof(MtLb) == 64, "one line per tile");
+constexpr uint32_t MT_ERR_SPIN = 8;
+
+// Every field is written and read with device-scope atomics (coherent across
+// the XCDs' L2s without a cache write-back per tile); the payload's stores
+// complete (vmcnt) before the status store.
+template <typename T>
+__device__ inline void st_dev(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ inline T ld_dev(T* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline void mt_publish(MtLb* e, const Ms& v, bool incl, uint32_t tag) {
+  if (incl) {
+    st_dev(&e->inc_rmax, v.rmax);
+    st_dev(&e->inc_wmin, v.wmin);
+    st_dev(&e->inc_fu, v.flag | (v.und << 1));
+  } else {
+    st_dev(&e->agg_rmax, v.rmax);
+    st_dev(&e->agg_wmin, v.wmin);
+    st_dev(&e->agg_fu, v.flag | (v.und << 1));
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  st_dev(&e->status, (tag << 2) | (incl ? 2u : 1u));
+}
+__device__ inline Ms mt_read(MtLb* e, bool incl) {
+  const uint32_t fu = ld_dev(incl ? &e->inc_fu : &e->agg_fu);
+  return Ms{fu & 1u, fu >> 1, ld_dev(incl ? &e->inc_rmax : &e->agg_rmax),
+            ld_dev(incl ? &e->inc_wmin : &e->agg_wmin)};
+}
+// ordered wave reduction, lane 0 rightmost: lane 0 gets v63 (x) ... (x) v0
+__device__ inline Ms wave_rcomb_ms(Ms x) {
+  const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    Ms y;
+    y.flag = __shfl_down(x.flag, d);
+    y.und = __shfl_down(x.und, d);
+    y.rmax = __shfl_down(x.rmax, d);
+    y.wmin = __shfl_down(x.wmin, d);
+    if (lane + d < 64) x = ms_comb(y, x);
+  }
+  return x;
+}
+
+__global__ __launch_bounds__(256) void k_mt_round(MtRoundArgs a, MtLb* lb, uint32_t tag, uint32_t* err) {
+  __shared__ Ms s[4];
+  __shared__ Ms s_pre;
+  __shared__ MtTileLds L;
+  const uint32_t tile = blockIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t base = (uint64_t)tile * MT_TILE;
+  const uint64_t p0 = base + (uint64_t)threadIdx.x * MT_ITEMS;
+  uint8_t f[MT_ITEMS], st[MT_ITEMS];
+  uint32_t tx[MT_ITEMS];
+  uint64_t c[MT_ITEMS];
+  mt_load_tile(a.sfl, a.stx, a.m, base, L, f, tx);
+#pragma unroll
+  for (uint32_t i = 0; i < MT_ITEMS; i++) {
+    st[i] = (f[i] & F_LAST) ? a.state[tx[i]] : ST_ABO;
+    c[i] = 0;
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < MT_ITEMS; i++)
+    if (st[i] == ST_COM) c[i] = a.cts[tx[i]];
+  Ms acc = ms_id();
+#pragma unroll
+  for (uint32_t i = 0; i < MT_ITEMS; i++) acc = ms_comb(acc, ms_elem(f[i], st[i], c[i]));
+  // block exclusive prefix per thread and the tile's total
+  const Ms x = wave_incl_ms(acc);
+  if (lane == 63) s[wv] = x;
+  __syncthreads();
+  Ms pre = ms_id(), tot = ms_id();
+#pragma unroll
+  for (uint32_t w = 0; w < 4; w++) {
+    if (w < wv) pre = ms_comb(pre, s[w]);
+    tot = ms_comb(tot, s[w]);
+  }
+  Ms ex = ms_shfl_up(x, 1);
+  if (lane == 0) ex = ms_id();
+  ex = ms_comb(pre, ex);
+  if (wv == 0) {
+    Ms P = ms_id();
+    if (tile == 0) {
+      if (lane == 0) mt_publish(&lb[0], tot, true, tag);
+    } else {
+      if (lane == 0) mt_publish(&lb[tile], tot, false, tag);
+      bool timed_out = false;
+      for (int64_t hi = (int64_t)tile - 1; hi >= 0; hi -= 64) {
+        const int64_t j = hi - (int64_t)lane;
+        uint32_t stw = 0;
+        if (j >= 0) {
+          uint32_t spins = 0;
+          while (((stw = ld_dev(&lb[j].status)) >> 2) != tag) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > (1u << 24)) {
+              timed_out = true;
+              break;
+            }
+          }
+        }
+        if (ballot64(timed_out)) {
+          if (lane == 0) atomicOr(err, MT_ERR_SPIN);
+          break;
+        }
+        const bool inc = j >= 0 && (stw & 3u) == 2u;
+        const uint64_t im = ballot64(inc);
+        const uint32_t stop = im ? (uint32_t)__builtin_ctzll(im) : 63u;
+        Ms v = ms_id();
+        if (j >= 0 && lane <= stop) v = mt_read(&lb[j], inc);
+        P = ms_comb(wave_rcomb_ms(v), P);  // lane 0's value is the batch's
+        if (im) break;
+      }
+      if (lane == 0) mt_publish(&lb[tile], ms_comb(P, tot), true, tag);
+    }
+    if (lane == 0) s_pre = P;
+  }
+  __syncthreads();
+  Ms run = ms_comb(s_pre, ex);
+#pragma unroll
+  for (uint32_t i = 0; i < MT_ITEMS; i++) {
+    const uint64_t p = p0 + i;
+    if (p >= a.m) break;
+    if (f[i] & F_START) run = Ms{1, 0, 0, U64MAX};  // own group excluded: contributions at its end
+    if ((f[i] & F_LAST) && (f[i] & (F_R | F_W)) && st[i] == ST_UND) {
+      const uint32_t t = tx[i];
+      if ((f[i] & F_W) && run.rmax) atomicMax((unsigned long long*)&a.lacc[t], run.rmax + 1);
+      if (run.wmin != U64MAX) atomicMin((unsigned long long*)&a.uacc[t], run.wmin - 1);
+      if ((run.und & 2u) || ((f[i] & F_W) && (run.und & 1u))) a.pend[t] = 1u;
+    }
+    run = ms_comb(run, ms_elem(f[i] & ~F_START, st[i], c[i]));
+  }
+}
+
 // decide: abort when the known bounds are already empty, commit when no
 // relevant predecessor is undecided; reset the accumulators
 // (over the undecided-txn list ul[0, *ulen) when given, else txns [0, n))
@@ -833,6 +985,18 @@ int dcc_ctx::maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, 
   CR(cv_scratch.ensure(this, rs_scratch_words(mm) * 4 + 64, "radix scratch"));
   const uint64_t tiles = (m + MT_TILE - 1) / MT_TILE;
   CR(mt_agg.ensure(this, std::max<uint64_t>(1, tiles) * sizeof(Ms), "maat scan"));
+  if (mt_fused < 0) {
+    const char* e = getenv("DCC_MT_FUSED");
+    mt_fused = e ? (atoi(e) != 0) : 1;
+  }
+  if (mt_fused) {
+    const void* old = mt_lb.p;
+    CR(mt_lb.ensure(this, std::max<uint64_t>(1, tiles) * sizeof(MtLb), "maat look-back status"));
+    if (mt_lb.p != old || mt_tag + 64 >= (1u << 30)) {  // fresh memory, or the tags wrap
+      CK(hipMemsetAsync(mt_lb.p, 0, mt_lb.cap, stream));
+      mt_tag = 0;
+    }
+  }
   uint64_t* base = (uint64_t*)mt_txn.p;
   uint64_t* cts = base + n;
   uint64_t* lacc = cts + n;
@@ -916,7 +1080,13 @@ int dcc_ctx::maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, 
     }();
     const uint32_t nb = (rounds == 0 || mc > long_scan) ? 1u : batch;
     for (uint32_t q = 0; q < nb; q++, rounds++) {
-      if (mc) {
+      if (mc && mt_fused) {
+        if (mt_tag + 1 >= (1u << 30)) {
+          CK(hipMemsetAsync(mt_lb.p, 0, mt_lb.cap, stream));
+          mt_tag = 0;
+        }
+        k_mt_round<<<(unsigned)tiles_c, 256, 0, stream>>>(ra, (MtLb*)mt_lb.p, ++mt_tag, cnt + 1);
+      } else if (mc) {
         k_mt_up<<<(unsigned)tiles_c, 256, 0, stream>>>(ra);
         k_mt_top<<<1, 256, 0, stream>>>((Ms*)mt_agg.p, (uint32_t)tiles_c);
         k_mt_down<<<(unsigned)tiles_c, 256, 0, stream>>>(ra);
@@ -933,8 +1103,10 @@ int dcc_ctx::maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, 
     CK(hipGetLastError());
     CK(hipMemcpyAsync(hmisc, ring, MT_RING * 4, hipMemcpyDeviceToHost, stream));
     if (mc) CK(hipMemcpyAsync((char*)hmisc + MT_RING * 4, tcnt + tiles_c, 4, hipMemcpyDeviceToHost, stream));
+    CK(hipMemcpyAsync((char*)hmisc + MT_RING * 4 + 4, cnt + 1, 4, hipMemcpyDeviceToHost, stream));
     CK(hipStreamSynchronize(stream));
     const uint32_t* hr = (const uint32_t*)hmisc;
+    if (hr[MT_RING + 1] & MT_ERR_SPIN) return fail(DCC_EIO, "maat: round scan look-back timed out");
     if (mt_debug)  // DCC_MT_DEBUG: undecided txns after each round, scan length
       for (uint32_t q = k0; q < rounds; q++)
         fprintf(stderr, "maat round %u: undecided %u, scan positions %llu\n", q + 1, hr[q % MT_RING],
@@ -985,6 +1157,7 @@ int dcc_ctx::maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, 
   if (hc[1] & MT_ERR_OFF) return fail(DCC_EINVAL, "batch: malformed offsets");
   if (hc[1] & MT_ERR_KEY) return fail(DCC_EINVAL, "batch: key equal to DCC_KEY_RESERVED");
   if (hc[1] & MT_ERR_FULL) return fail(DCC_EIO, "maat: row table full");
+  if (hc[1] & MT_ERR_SPIN) return fail(DCC_EIO, "maat: round scan look-back timed out");
   if (hc[3]) return fail(DCC_EIO, "maat: %u undecided transactions", hc[3]);
   float ms = 0;
   CK(hipEventElapsedTime(&ms, ev0, ev1));

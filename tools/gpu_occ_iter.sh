@@ -6,7 +6,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/${TAG:-occ}
 mkdir -p "$O"
 cd "$R"
-timeout -k 10 400 python -u -m pytest tests/test_gpu_occ.py tests/test_gpu_sweep.py tests/test_gpu_golden.py \
+timeout -k 10 400 python -u -m pytest ${TESTS:-tests/test_gpu_occ.py tests/test_gpu_sweep.py tests/test_gpu_golden.py tests/test_gpu_ro_split.py tests/test_gpu_kat_branches.py} \
    tests/test_gpu_history.py tests/test_gpu_shard.py -x -q --timeout 200 --timeout-method thread > "$O/tests.log" 2>&1 \
  || { tail -30 "$O/tests.log"; exit 1; }
 tail -1 "$O/tests.log"

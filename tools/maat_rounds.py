@@ -1,13 +1,21 @@
 #!/usr/bin/env python3
-"""Per-round undecided counts and scan lengths of a MaaT epoch (DCC_MT_DEBUG=1)."""
+"""MaaT 1M epoch with DCC_MT_DEBUG=1: undecided txns and scan length per round
+(stderr), device ms per epoch.  Run on the GPU box."""
 import os
 import sys
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+import torch  # noqa: E402
 import deneva_amd as d  # noqa: E402
+
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
 b = d.gen_ycsb(n_txn=n, zipf_theta=0.9)
+db = b.to_torch("cuda:0")
+rc = torch.empty(n, dtype=torch.uint8, device="cuda:0")
 with d.Engine(0) as eng:
-    eng.maat_rows_clear()
-    _, _, st = eng.maat_validate_epoch(b, want_cts=False)
-    print(f"{st['device_ms']:.3f} ms, {st['rounds']} rounds, {st['n_commit']} commits", file=sys.stderr)
+    for i in range(2):
+        eng.maat_rows_clear()
+        st = eng.maat_validate_epoch(db, want_cts=False, out_rc=rc)[2]
+        print(f"epoch {i}: device {st['device_ms']:.3f} ms, rounds {st['rounds']}, commits {st['n_commit']}",
+              file=sys.stderr, flush=True)
