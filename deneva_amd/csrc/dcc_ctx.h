@@ -160,6 +160,7 @@ struct dcc_ctx {
   DevBuf mt_misc, mt_slot, mt_sval, mt_slot2, mt_sval2, mt_sfl, mt_stx, mt_txn, mt_agg;
   DevBuf mt_sflB, mt_stxB, mt_k1, mt_tcnt, mt_ul;
   DevBuf mt_lb;          // fused round scan: look-back status per tile (k_mt_round)
+  DevBuf mt_ptab;        // prefix level: per-row commit bounds of the prefix (MtPTab)
   uint32_t mt_tag = 0;   // its round tag (monotone; the buffer is zeroed when it wraps)
   int mt_fused = -1;     // DCC_MT_FUSED: 1 fused round scan (default), 0 up / top / down
   // GPU index (index.hip): key table, newest insert ordinal per key, rows

@@ -241,7 +241,7 @@ std::vector<DevBuf*> dcc_ctx::all_bufs() {
                             &sw_rflag, &sw_ro, &sw_wtab, &sw_cw, &sw_wtab_big,
                             &snap_top, &snap_aoff, &snap_aidx, &snap_cnt, &mt_rk,
                             &mt_misc, &mt_slot, &mt_sval, &mt_slot2, &mt_sval2, &mt_sfl,
-                            &mt_stx, &mt_txn, &mt_agg, &mt_sflB, &mt_stxB, &mt_k1, &mt_tcnt, &mt_ul, &mt_lb, &ix_keys, &ix_ord, &ix_rows, &ix_cnt, &wv_buf, &ix_scr, &wv_hbuf, &wv_obuf,
+                            &mt_stx, &mt_txn, &mt_agg, &mt_sflB, &mt_stxB, &mt_k1, &mt_tcnt, &mt_ul, &mt_lb, &mt_ptab, &ix_keys, &ix_ord, &ix_rows, &ix_cnt, &wv_buf, &ix_scr, &wv_hbuf, &wv_obuf,
                             &h_K[0], &h_K[1], &h_V[0], &h_V[1], &h_scr, &h_bsum,
                             &nar_keys, &nar_at, &nar_tn, &fin_off, &fin_keys, &fin_at, &fin_state, &fin_hasw, &fin_rc, &fin_cnt,
                             &sh_off, &sh_keys, &sh_at, &sh_src, &sh_cnt, &sh_bsum, &sh_rc, &sh_tn, &sh_grp};

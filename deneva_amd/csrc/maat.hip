@@ -61,6 +61,7 @@ constexpr uint32_t MT_TILE = 256 * MT_ITEMS;
 constexpr uint32_t MT_RING = 64;          // per-round undecided counters
 constexpr uint32_t MT_BATCH = 8;          // rounds enqueued per host check (A/B: profiles/r03/maat_batch/)
 constexpr uint64_t MT_LONG = 1u << 22;    // scans longer than this: a check after every round
+constexpr uint64_t MT_PREFIX = 1024;      // txns of the prefix level (DCC_MT_PREFIX; 0: none)
 constexpr uint8_t ST_UND = 0, ST_COM = 1, ST_ABO = 2;
 // sorted-position flags
 constexpr uint8_t F_R = 1, F_W = 2, F_LAST = 4, F_START = 8;
@@ -918,6 +919,129 @@ inline unsigned g1(uint64_t n, uint64_t cap = 8192) {
 
 }  // namespace
 
+// ---------------------------------------------------------------- prefix level
+// The sweep idea: the epoch's first P txns are decided alone
+// by rounds on their own accesses (a txn's constraints come only from earlier
+// txns), then every later txn is checked against their commits -- per row the
+// max commit timestamp of the committed prefix readers and the min of its
+// writers (MtPTab, an open-addressing table on row slots) -- and aborted when
+// its bounds are already empty: L only grows and U only shrinks as more
+// earlier txns commit, so such a txn aborts in the full replay too.  The
+// rounds then run on the survivors' accesses plus the prefix's (its commits
+// constrain the survivors), so the first rounds scan ~2 M positions instead
+// of the epoch's 16.7 M.
+struct MtPTab {
+  uint32_t* key;               // row slot, ~0u empty
+  unsigned long long* rmax;    // max cts of committed prefix readers (0: none)
+  unsigned long long* wmin;    // min cts of committed prefix writers (U64MAX: none)
+  uint32_t mask;
+};
+__device__ inline uint32_t mt_phash(uint32_t s) { return (s * 2654435761u) ^ (s >> 15); }
+
+// committed prefix txns' accesses into the table (a thread per prefix txn)
+__global__ __launch_bounds__(256) void k_mt_ptab(const uint32_t* off, uint32_t P, const uint8_t* at, uint32_t rw_all,
+                                                 const uint32_t* slot, const uint8_t* state, const uint64_t* cts,
+                                                 MtPTab tb) {
+  const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= P || state[t] != ST_COM) return;
+  const uint64_t c = cts[t];
+  for (uint32_t x = off[t]; x < off[t + 1]; x++) {
+    const uint8_t ty = at[x];
+    const bool rd = rw_all || ty == DCC_RD, wr = rw_all || ty == DCC_WR;
+    if (!rd && !wr) continue;
+    const uint32_t sl = slot[x];
+    uint32_t h = mt_phash(sl) & tb.mask;
+    for (uint32_t q = 0; q <= tb.mask; q++, h = (h + 1) & tb.mask) {
+      const uint32_t k = atomicCAS(&tb.key[h], ~0u, sl);
+      if (k == ~0u || k == sl) break;
+    }
+    if (rd) atomicMax(&tb.rmax[h], (unsigned long long)c);
+    if (wr) atomicMin(&tb.wmin[h], (unsigned long long)c);
+  }
+}
+
+// every later access against the table: the round scan's folds (k_mt_round)
+// with the committed prefix as the only earlier committed txns
+__global__ __launch_bounds__(256) void k_mt_filter(const uint32_t* slot, const uint32_t* sval, uint64_t x0,
+                                                   uint64_t nnz, MtPTab tb, uint64_t* lacc, uint64_t* uacc) {
+  for (uint64_t x = x0 + (uint64_t)blockIdx.x * 256 + threadIdx.x; x < nnz; x += (uint64_t)gridDim.x * 256) {
+    const uint32_t v = sval[x];
+    if (!(v & (SV_R | SV_W))) continue;
+    const uint32_t sl = slot[x], t = v >> 2;
+    uint32_t h = mt_phash(sl) & tb.mask;
+    for (uint32_t q = 0; q <= tb.mask; q++, h = (h + 1) & tb.mask) {
+      const uint32_t k = tb.key[h];
+      if (k == ~0u) break;
+      if (k != sl) continue;
+      const uint64_t r = tb.rmax[h], w = tb.wmin[h];
+      if ((v & SV_W) && r) atomicMax((unsigned long long*)&lacc[t], (unsigned long long)(r + 1));
+      if (w != U64MAX) atomicMin((unsigned long long*)&uacc[t], (unsigned long long)(w - 1));
+      break;
+    }
+  }
+}
+
+// the filter's decision for txns [P, n): abort when the bounds are empty
+// (nothing commits here: later txns wait for the rounds); accumulators reset
+__global__ __launch_bounds__(256) void k_mt_fdecide(uint64_t n, uint64_t P, const uint64_t* base, uint8_t* state,
+                                                    uint64_t* lacc, uint64_t* uacc) {
+  for (uint64_t t = P + (uint64_t)blockIdx.x * 256 + threadIdx.x; t < n; t += (uint64_t)gridDim.x * 256) {
+    if (state[t] != ST_UND) continue;
+    if (max(base[t], lacc[t]) >= uacc[t]) state[t] = ST_ABO;
+    lacc[t] = 0;
+    uacc[t] = U64MAX;
+  }
+}
+
+// txns [0, P) as an undecided list
+__global__ __launch_bounds__(256) void k_mt_iota(uint32_t* ul, uint32_t* ulen, uint32_t P) {
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < P; i += gridDim.x * 256) ul[i] = i;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *ulen = P;
+}
+
+// The rounds' input after the filter: the accesses of every txn that is not
+// aborted (the prefix's commits and the survivors), in index order, as the
+// sort's (slot, txn << 2 | R / W) pairs.  Per 256-txn block: its count, then
+// (after the scan of the counts) its pairs at the block's base.
+__device__ inline uint32_t mt_keep_len(const uint32_t* off, uint64_t n, const uint8_t* state, uint64_t t) {
+  return (t < n && state[t] != ST_ABO) ? off[t + 1] - off[t] : 0u;
+}
+__global__ __launch_bounds__(256) void k_mt_gcount(const uint32_t* off, uint64_t n, const uint8_t* state,
+                                                   uint32_t* bsum) {
+  __shared__ uint32_t sh[4];
+  const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  uint32_t c = mt_keep_len(off, n, state, t);
+  for (int d = 32; d > 0; d >>= 1) c += __shfl_xor(c, d);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) bsum[blockIdx.x] = sh[0] + sh[1] + sh[2] + sh[3];
+}
+__global__ __launch_bounds__(256) void k_mt_gscatter(const uint32_t* off, uint64_t n, const uint8_t* state,
+                                                     const uint8_t* at, uint32_t rw_all, const uint32_t* slot,
+                                                     const uint32_t* bsum, uint32_t* okey, uint32_t* oval) {
+  __shared__ uint32_t sh[4];
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const uint32_t len = mt_keep_len(off, n, state, t);
+  uint32_t x = len;
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) sh[wv] = x;
+  __syncthreads();
+  uint32_t b = bsum[blockIdx.x] + x - len;
+  for (uint32_t w = 0; w < wv; w++) b += sh[w];
+  if (!len) return;
+  const uint32_t o0 = off[t];
+  for (uint32_t i = 0; i < len; i++) {
+    const uint8_t ty = at[o0 + i];
+    const bool rd = rw_all || ty == DCC_RD, wr = rw_all || ty == DCC_WR;
+    okey[b + i] = slot[o0 + i];
+    oval[b + i] = ((uint32_t)t << 2) | (rd ? SV_R : 0u) | (wr ? SV_W : 0u);
+  }
+}
+
 // ---------------------------------------------------------------- host
 // Row table capacity for `want` rows at <= 50 % load (rehash on growth).
 int dcc_ctx::maat_rows_reserve(uint64_t want) {
@@ -979,7 +1103,8 @@ int dcc_ctx::maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, 
   CR(mt_sflB.ensure(this, mm, "maat flags b"));
   CR(mt_stxB.ensure(this, mm * 4, "maat sorted txns b"));
   CR(mt_k1.ensure(this, mm * 4, "maat sort keys b"));
-  CR(mt_tcnt.ensure(this, ((mm + MT_TILE - 1) / MT_TILE + 2) * 4, "maat tile counts"));
+  CR(mt_tcnt.ensure(this, (std::max<uint64_t>((mm + MT_TILE - 1) / MT_TILE, (n + 255) / 256) + 2) * 4,
+                     "maat tile / block counts"));
   CR(mt_stx.ensure(this, mm * 4, "maat sorted txns"));
   CR(mt_txn.ensure(this, n * (8 * 4 + 4 + 1) + 64, "maat txn state"));
   CR(cv_scratch.ensure(this, rs_scratch_words(mm) * 4 + 64, "radix scratch"));
@@ -1037,109 +1162,184 @@ int dcc_ctx::maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, 
   uint8_t* sflb[2] = {(uint8_t*)mt_sfl.p, (uint8_t*)mt_sflB.p};
   uint32_t* stxb[2] = {(uint32_t*)mt_stx.p, (uint32_t*)mt_stxB.p};
   uint32_t* ssb[2] = {(uint32_t*)mt_slot2.p, (uint32_t*)mt_k1.p};
-  if (m) {
+  // sort the first mm pairs of (mt_slot2, mt_sval) and flag their groups
+  // into sflb[0] / stxb[0]; ssb / svb point at the sorted pairs afterwards
+  auto sort_groups = [&](uint64_t mm) {
     uint32_t* kk[2] = {(uint32_t*)mt_slot2.p, (uint32_t*)mt_k1.p};
     uint32_t* vb[2] = {(uint32_t*)mt_sval.p, (uint32_t*)mt_sval2.p};
-    const int cur = radix_sort_u32(kk, vb, m, mt_bits, (uint32_t*)cv_scratch.p, stream);
+    const int cur = mm ? radix_sort_u32(kk, vb, mm, mt_bits, (uint32_t*)cv_scratch.p, stream) : 0;
     ssb[0] = kk[cur];
     ssb[1] = kk[cur ^ 1];
-    k_mt_groups<<<g1(m), 256, 0, stream>>>(ssb[0], vb[cur], m, sflb[0], stxb[0]);
-  }
-  CK(hipGetLastError());
+    if (mm) k_mt_groups<<<g1(mm), 256, 0, stream>>>(ssb[0], vb[cur], mm, sflb[0], stxb[0]);
+  };
 
   // ---- rounds: one, then MT_BATCH between host checks; after each check
   // the scan input is compacted to the groups that can still matter
   uint32_t rounds = 0;
-  bool done = false;
   const bool mt_debug = getenv("DCC_MT_DEBUG") != nullptr;
-  // the undecided txns: all of them at first (identity), then a compacted
-  // list whenever the undecided count falls well below it
   CR(mt_ul.ensure(this, 2 * n * 4 + 64, "maat undecided lists"));
   uint32_t* ul_buf[2] = {(uint32_t*)mt_ul.p, (uint32_t*)mt_ul.p + n};
   uint32_t* ulen_w = cnt + 5;  // two count words: cnt[5], cnt[6]
-  const uint32_t* ul_cur = nullptr;
-  const uint32_t* ulen_cur = nullptr;
-  uint64_t ulen_host = n;
-  int ub = 0;
-  uint64_t mc = m;  // current scan length
-  int cb = 0;       // current buffer set
   uint32_t* tcnt = (uint32_t*)mt_tcnt.p;
-  while (!done) {
-    const uint32_t k0 = rounds;
-    const uint64_t tiles_c = (mc + MT_TILE - 1) / MT_TILE;
-    MtRoundArgs ra{mc, n, sflb[cb], stxb[cb], state, cts, lacc, uacc, pend, (Ms*)mt_agg.p};
-    // one round per host check while the scan is long (each check may
-    // compact it), MT_BATCH once it is short
-    static const uint32_t batch = [] {  // DCC_MT_BATCH / DCC_MT_LONG: tuning experiments
-      const char* e = getenv("DCC_MT_BATCH");
-      return e && atoi(e) > 0 ? (uint32_t)atoi(e) : MT_BATCH;
-    }();
-    static const uint64_t long_scan = [] {
-      const char* e = getenv("DCC_MT_LONG");
-      return e && atoll(e) > 0 ? (uint64_t)atoll(e) : MT_LONG;
-    }();
-    const uint32_t nb = (rounds == 0 || mc > long_scan) ? 1u : batch;
-    for (uint32_t q = 0; q < nb; q++, rounds++) {
-      if (mc && mt_fused) {
-        if (mt_tag + 1 >= (1u << 30)) {
-          CK(hipMemsetAsync(mt_lb.p, 0, mt_lb.cap, stream));
-          mt_tag = 0;
+  // Rounds until the txns of the undecided list (null: every txn) are all
+  // decided, over the mc sorted positions in sflb[0] / stxb[0] / ssb[0]; the
+  // list is compacted whenever the undecided count falls well below it
+  // (into ul_buf[ub], alternating).
+  auto solve = [&](uint64_t mc, const uint32_t* ul_cur, const uint32_t* ulen_cur, uint64_t ulen_host,
+                   int ub) -> int {
+    bool done = false;
+    int cb = 0;  // current buffer set
+    while (!done) {
+      const uint32_t k0 = rounds;
+      const uint64_t tiles_c = (mc + MT_TILE - 1) / MT_TILE;
+      MtRoundArgs ra{mc, n, sflb[cb], stxb[cb], state, cts, lacc, uacc, pend, (Ms*)mt_agg.p};
+      // one round per host check while the scan is long (each check may
+      // compact it), MT_BATCH once it is short
+      static const uint32_t batch = [] {  // DCC_MT_BATCH / DCC_MT_LONG: tuning experiments
+        const char* e = getenv("DCC_MT_BATCH");
+        return e && atoi(e) > 0 ? (uint32_t)atoi(e) : MT_BATCH;
+      }();
+      static const uint64_t long_scan = [] {
+        const char* e = getenv("DCC_MT_LONG");
+        return e && atoll(e) > 0 ? (uint64_t)atoll(e) : MT_LONG;
+      }();
+      const uint32_t nb = (rounds == 0 || mc > long_scan) ? 1u : batch;
+      for (uint32_t q = 0; q < nb; q++, rounds++) {
+        if (mc && mt_fused) {
+          if (mt_tag + 1 >= (1u << 30)) {
+            CK(hipMemsetAsync(mt_lb.p, 0, mt_lb.cap, stream));
+            mt_tag = 0;
+          }
+          k_mt_round<<<(unsigned)tiles_c, 256, 0, stream>>>(ra, (MtLb*)mt_lb.p, ++mt_tag, cnt + 1);
+        } else if (mc) {
+          k_mt_up<<<(unsigned)tiles_c, 256, 0, stream>>>(ra);
+          k_mt_top<<<1, 256, 0, stream>>>((Ms*)mt_agg.p, (uint32_t)tiles_c);
+          k_mt_down<<<(unsigned)tiles_c, 256, 0, stream>>>(ra);
         }
-        k_mt_round<<<(unsigned)tiles_c, 256, 0, stream>>>(ra, (MtLb*)mt_lb.p, ++mt_tag, cnt + 1);
-      } else if (mc) {
-        k_mt_up<<<(unsigned)tiles_c, 256, 0, stream>>>(ra);
-        k_mt_top<<<1, 256, 0, stream>>>((Ms*)mt_agg.p, (uint32_t)tiles_c);
-        k_mt_down<<<(unsigned)tiles_c, 256, 0, stream>>>(ra);
+        k_mt_decide<<<g1(ulen_host, 2048), 256, 0, stream>>>(n, ul_cur, ulen_cur, base, state, cts, lacc,
+                                                              uacc, pend, &ring[rounds % MT_RING],
+                                                              &ring[(rounds + 1) % MT_RING]);
       }
-      k_mt_decide<<<g1(ulen_host, 2048), 256, 0, stream>>>(n, ul_cur, ulen_cur, base, state, cts,
-                                                            lacc, uacc, pend,
-                                                   &ring[rounds % MT_RING],
-                                                   &ring[(rounds + 1) % MT_RING]);
-    }
-    if (mc) {
-      k_mt_keep_count<<<(unsigned)tiles_c, 256, 0, stream>>>(mc, sflb[cb], stxb[cb], state, tcnt);
-      rs_scan_one(tcnt, (uint32_t)tiles_c, tcnt + tiles_c, stream);
-    }
-    CK(hipGetLastError());
-    CK(hipMemcpyAsync(hmisc, ring, MT_RING * 4, hipMemcpyDeviceToHost, stream));
-    if (mc) CK(hipMemcpyAsync((char*)hmisc + MT_RING * 4, tcnt + tiles_c, 4, hipMemcpyDeviceToHost, stream));
-    CK(hipMemcpyAsync((char*)hmisc + MT_RING * 4 + 4, cnt + 1, 4, hipMemcpyDeviceToHost, stream));
-    CK(hipStreamSynchronize(stream));
-    const uint32_t* hr = (const uint32_t*)hmisc;
-    if (hr[MT_RING + 1] & MT_ERR_SPIN) return fail(DCC_EIO, "maat: round scan look-back timed out");
-    if (mt_debug)  // DCC_MT_DEBUG: undecided txns after each round, scan length
-      for (uint32_t q = k0; q < rounds; q++)
-        fprintf(stderr, "maat round %u: undecided %u, scan positions %llu\n", q + 1, hr[q % MT_RING],
-                (unsigned long long)mc);
-    for (uint32_t q = k0; q < rounds; q++)
-      if (hr[q % MT_RING] == 0) {
-        rounds = q + 1;
-        done = true;
-        break;
+      if (mc) {
+        k_mt_keep_count<<<(unsigned)tiles_c, 256, 0, stream>>>(mc, sflb[cb], stxb[cb], state, tcnt);
+        rs_scan_one(tcnt, (uint32_t)tiles_c, tcnt + tiles_c, stream);
       }
-    if (!done && rounds > n + 8) return fail(DCC_EIO, "maat: rounds did not converge");
-    if (!done) {
-      const uint32_t und = hr[(rounds - 1) % MT_RING];
-      if ((uint64_t)und * 10 < ulen_host * 3) {  // shrinks to < 30 %: worth a pass
-        CK(hipMemsetAsync(ulen_w + ub, 0, 4, stream));
-        k_mt_ucompact<<<g1(ulen_host, 2048), 256, 0, stream>>>(ul_cur, ulen_cur, n, state, ul_buf[ub],
-                                                              ulen_w + ub);
-        ul_cur = ul_buf[ub];
-        ulen_cur = ulen_w + ub;
-        ulen_host = und;
-        ub ^= 1;
-      }
-    }
-    if (!done && mc && (uint64_t)hr[MT_RING] * 10 <= mc * 9) {  // compact when it drops >= 10 %
-      const uint64_t m2 = hr[MT_RING];
-      k_mt_keep_scatter<<<(unsigned)tiles_c, 256, 0, stream>>>(mc, sflb[cb], stxb[cb], ssb[cb], state,
-                                                             tcnt, sflb[cb ^ 1], stxb[cb ^ 1],
-                                                             ssb[cb ^ 1]);
-      if (m2) k_mt_starts<<<g1(m2), 256, 0, stream>>>(m2, ssb[cb ^ 1], sflb[cb ^ 1]);
+      // the ring, the kept-position total and the error word into pinned
+      // memory with one gather launch (three copies cost ~13 us of device time)
+      GatherArgs ga{};
+      ga.job[ga.n++] = CopyJob{ring, (uint32_t*)hmisc_dev, MT_RING};
+      if (mc) ga.job[ga.n++] = CopyJob{tcnt + tiles_c, (uint32_t*)hmisc_dev + MT_RING, 1};
+      ga.job[ga.n++] = CopyJob{cnt + 1, (uint32_t*)hmisc_dev + MT_RING + 1, 1};
+      launch_gather(ga, stream);
       CK(hipGetLastError());
-      cb ^= 1;
-      mc = m2;
+      CK(hipStreamSynchronize(stream));
+      const uint32_t* hr = (const uint32_t*)hmisc;
+      if (hr[MT_RING + 1] & MT_ERR_SPIN) return fail(DCC_EIO, "maat: round scan look-back timed out");
+      if (mt_debug)  // DCC_MT_DEBUG: undecided txns after each round, scan length
+        for (uint32_t q = k0; q < rounds; q++)
+          fprintf(stderr, "maat round %u: undecided %u, scan positions %llu\n", q + 1, hr[q % MT_RING],
+                  (unsigned long long)mc);
+      for (uint32_t q = k0; q < rounds; q++)
+        if (hr[q % MT_RING] == 0) {
+          rounds = q + 1;
+          done = true;
+          break;
+        }
+      if (!done && rounds > n + 8) return fail(DCC_EIO, "maat: rounds did not converge");
+      if (!done) {
+        const uint32_t und = hr[(rounds - 1) % MT_RING];
+        if ((uint64_t)und * 10 < ulen_host * 3) {  // shrinks to < 30 %: worth a pass
+          CK(hipMemsetAsync(ulen_w + ub, 0, 4, stream));
+          k_mt_ucompact<<<g1(ulen_host, 2048), 256, 0, stream>>>(ul_cur, ulen_cur, n, state, ul_buf[ub],
+                                                                ulen_w + ub);
+          ul_cur = ul_buf[ub];
+          ulen_cur = ulen_w + ub;
+          ulen_host = und;
+          ub ^= 1;
+        }
+      }
+      if (!done && mc && (uint64_t)hr[MT_RING] * 10 <= mc * 9) {  // compact when it drops >= 10 %
+        const uint64_t m2 = hr[MT_RING];
+        k_mt_keep_scatter<<<(unsigned)tiles_c, 256, 0, stream>>>(mc, sflb[cb], stxb[cb], ssb[cb], state,
+                                                               tcnt, sflb[cb ^ 1], stxb[cb ^ 1],
+                                                               ssb[cb ^ 1]);
+        if (m2) k_mt_starts<<<g1(m2), 256, 0, stream>>>(m2, ssb[cb ^ 1], sflb[cb ^ 1]);
+        CK(hipGetLastError());
+        cb ^= 1;
+        mc = m2;
+      }
     }
+    return DCC_OK;
+  };
+
+  // the prefix level (DCC_MT_PREFIX txns, 0: off; epochs of > 4 prefixes)
+  static const uint64_t prefix = [] {
+    const char* e = getenv("DCC_MT_PREFIX");
+    return e ? (uint64_t)atoll(e) : (uint64_t)MT_PREFIX;
+  }();
+  if (m && prefix && n > 4 * prefix) {
+    const uint32_t P = (uint32_t)prefix;
+    uint32_t mp = 0;
+    {
+      GatherArgs ga{};
+      ga.job[ga.n++] = CopyJob{d.off + P, (uint32_t*)hmisc_dev, 1};
+      launch_gather(ga, stream);
+      CK(hipGetLastError());
+      CK(hipStreamSynchronize(stream));
+    }
+    mp = *(const uint32_t*)hmisc;
+    // 1. the prefix alone: its accesses are the first mp pairs of the base
+    //    pass's (slot, value) buffers
+    sort_groups(mp);
+    k_mt_iota<<<g1(P), 256, 0, stream>>>(ul_buf[0], ulen_w, P);
+    CK(hipGetLastError());
+    CR(solve(mp, ul_buf[0], ulen_w, P, 1));
+    // 2. its commits per row, then every later access against them
+    uint64_t cap = 1024;
+    while (cap < 4ull * std::max<uint32_t>(mp, 1)) cap <<= 1;
+    CR(mt_ptab.ensure(this, cap * 20, "maat prefix table"));
+    MtPTab tb{(uint32_t*)mt_ptab.p, (unsigned long long*)((uint32_t*)mt_ptab.p + cap),
+              (unsigned long long*)((uint32_t*)mt_ptab.p + cap) + cap, (uint32_t)(cap - 1)};
+    CK(hipMemsetAsync(tb.key, 0xFF, cap * 4, stream));
+    CK(hipMemsetAsync(tb.rmax, 0, cap * 8, stream));
+    CK(hipMemsetAsync(tb.wmin, 0xFF, cap * 8, stream));
+    k_mt_ptab<<<(P + 255) / 256, 256, 0, stream>>>(d.off, P, d.acctype, rw_all, (const uint32_t*)mt_slot.p, state,
+                                                  cts, tb);
+    k_mt_filter<<<g1(m - mp, 1u << 20), 256, 0, stream>>>((const uint32_t*)mt_slot.p, (const uint32_t*)mt_sval.p, mp, m,
+                                                tb, lacc, uacc);
+    k_mt_fdecide<<<g1(n - P), 256, 0, stream>>>(n, P, base, state, lacc, uacc);
+    // 3. the survivors (undecided list) and the rounds' input: every access of
+    //    a txn not aborted, in index order
+    CK(hipMemsetAsync(ulen_w, 0, 4, stream));
+    k_mt_ucompact<<<g1(n, 2048), 256, 0, stream>>>(nullptr, nullptr, n, state, ul_buf[0], ulen_w);
+    const uint32_t nblk = (uint32_t)((n + 255) / 256);
+    uint32_t* gb = tcnt;  // tile counts are free here (nblk <= tiles + 2)
+    k_mt_gcount<<<nblk, 256, 0, stream>>>(d.off, n, state, gb);
+    rs_scan_one(gb, nblk, gb + nblk, stream);
+    k_mt_gscatter<<<nblk, 256, 0, stream>>>(d.off, n, state, d.acctype, rw_all, (const uint32_t*)mt_slot.p, gb,
+                                            (uint32_t*)mt_slot2.p, (uint32_t*)mt_sval.p);
+    CK(hipGetLastError());
+    {
+      GatherArgs ga{};
+      ga.job[ga.n++] = CopyJob{gb + nblk, (uint32_t*)hmisc_dev, 1};
+      ga.job[ga.n++] = CopyJob{ulen_w, (uint32_t*)hmisc_dev + 1, 1};
+      launch_gather(ga, stream);
+      CK(hipGetLastError());
+      CK(hipStreamSynchronize(stream));
+    }
+    const uint32_t m2 = ((const uint32_t*)hmisc)[0], nsurv = ((const uint32_t*)hmisc)[1];
+    if (mt_debug)
+      fprintf(stderr, "maat prefix %u txns (%u accesses, %u rounds): %u survivors, %u positions\n", P, mp,
+              rounds, nsurv, m2);
+    if (nsurv) {
+      sort_groups(m2);
+      CK(hipGetLastError());
+      CR(solve(m2, ul_buf[0], ulen_w, nsurv, 1));
+    }
+  } else {
+    sort_groups(m);
+    CK(hipGetLastError());
+    CR(solve(m, nullptr, nullptr, n, 0));
   }
   FinArgs fa{n, m, d.off, d.acctype, rw_all, state, cts, (const uint32_t*)mt_slot.p,
              (MtSlot*)mt_rk.p, rc_dev, cts_dev, cnt + 2};

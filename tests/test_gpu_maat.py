@@ -136,3 +136,17 @@ def test_rejected_batch_leaves_rows_unchanged(engine):
     lr1, lw1 = engine.maat_rows_get(rk)
     assert np.array_equal(lr0, lr1) and np.array_equal(lw0, lw1)
     engine.maat_rows_clear()
+
+
+@pytest.mark.parametrize("theta,n", [(0.9, 1 << 20), (0.99, 1 << 18), (0.6, 1 << 18), (0.0, 1 << 16)])
+def test_prefix_level_full_size(engine, theta, n):
+    # epochs of > 4 x 1,024 txns take the prefix level (maat.hip: the first
+    # 1,024 decided alone, later txns filtered against their commits, rounds
+    # on the survivors); with pre-seeded row timestamps the base bounds join in
+    b = d.gen_ycsb(n_txn=n, zipf_theta=theta, seed=0x3A7 + n)
+    run(engine, b)
+    rng = np.random.default_rng(n)
+    rk = np.unique(b.keys[rng.integers(0, b.nnz, size=2000)]).astype(np.uint64)
+    lr = rng.integers(0, 50, size=rk.size).astype(np.uint64)
+    lw = rng.integers(0, 50, size=rk.size).astype(np.uint64)
+    run(engine, b, rows=(rk, lr, lw))
