@@ -935,7 +935,10 @@ struct MtPTab {
   unsigned long long* rmax;    // max cts of committed prefix readers (0: none)
   unsigned long long* wmin;    // min cts of committed prefix writers (U64MAX: none)
   uint32_t mask;
+  uint32_t* bits;              // one-hash presence bitmap of the slots (MT_PBITS bits)
 };
+constexpr uint32_t MT_PBITS_LOG = 18;  // 32 KiB: the filter's LDS copy
+__device__ inline uint32_t mt_pbit(uint32_t s) { return (s * 0x9E3779B1u) >> (32 - MT_PBITS_LOG); }
 __device__ inline uint32_t mt_phash(uint32_t s) { return (s * 2654435761u) ^ (s >> 15); }
 
 // committed prefix txns' accesses into the table (a thread per prefix txn)
@@ -955,28 +958,47 @@ __global__ __launch_bounds__(256) void k_mt_ptab(const uint32_t* off, uint32_t P
       const uint32_t k = atomicCAS(&tb.key[h], ~0u, sl);
       if (k == ~0u || k == sl) break;
     }
+    const uint32_t b = mt_pbit(sl);
+    atomicOr(&tb.bits[b >> 5], 1u << (b & 31u));
     if (rd) atomicMax(&tb.rmax[h], (unsigned long long)c);
     if (wr) atomicMin(&tb.wmin[h], (unsigned long long)c);
   }
 }
 
 // every later access against the table: the round scan's folds (k_mt_round)
-// with the committed prefix as the only earlier committed txns
+// with the committed prefix as the only earlier committed txns.  Persistent
+// workgroups with the presence bitmap in LDS: an access whose bit is clear
+// (almost every access of a row the prefix did not commit) never leaves the CU.
 __global__ __launch_bounds__(256) void k_mt_filter(const uint32_t* slot, const uint32_t* sval, uint64_t x0,
                                                    uint64_t nnz, MtPTab tb, uint64_t* lacc, uint64_t* uacc) {
-  for (uint64_t x = x0 + (uint64_t)blockIdx.x * 256 + threadIdx.x; x < nnz; x += (uint64_t)gridDim.x * 256) {
-    const uint32_t v = sval[x];
-    if (!(v & (SV_R | SV_W))) continue;
-    const uint32_t sl = slot[x], t = v >> 2;
-    uint32_t h = mt_phash(sl) & tb.mask;
-    for (uint32_t q = 0; q <= tb.mask; q++, h = (h + 1) & tb.mask) {
-      const uint32_t k = tb.key[h];
-      if (k == ~0u) break;
-      if (k != sl) continue;
-      const uint64_t r = tb.rmax[h], w = tb.wmin[h];
-      if ((v & SV_W) && r) atomicMax((unsigned long long*)&lacc[t], (unsigned long long)(r + 1));
-      if (w != U64MAX) atomicMin((unsigned long long*)&uacc[t], (unsigned long long)(w - 1));
-      break;
+  __shared__ uint32_t s_bits[(1u << MT_PBITS_LOG) / 32];
+  for (uint32_t q = threadIdx.x; q < (1u << MT_PBITS_LOG) / 32; q += 256) s_bits[q] = tb.bits[q];
+  __syncthreads();
+  constexpr uint32_t U = 4;
+  for (uint64_t xb = x0 + (uint64_t)blockIdx.x * 256 * U; xb < nnz; xb += (uint64_t)gridDim.x * 256 * U) {
+    uint32_t v[U], sl[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++) {
+      const uint64_t x = min(xb + u * 256 + threadIdx.x, nnz - 1);
+      v[u] = sval[x];
+      sl[u] = slot[x];
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++) {
+      if (xb + u * 256 + threadIdx.x >= nnz || !(v[u] & (SV_R | SV_W))) continue;
+      const uint32_t b = mt_pbit(sl[u]);
+      if (!((s_bits[b >> 5] >> (b & 31u)) & 1u)) continue;
+      const uint32_t t = v[u] >> 2;
+      uint32_t h = mt_phash(sl[u]) & tb.mask;
+      for (uint32_t q = 0; q <= tb.mask; q++, h = (h + 1) & tb.mask) {
+        const uint32_t k = tb.key[h];
+        if (k == ~0u) break;
+        if (k != sl[u]) continue;
+        const uint64_t r = tb.rmax[h], w = tb.wmin[h];
+        if ((v[u] & SV_W) && r) atomicMax((unsigned long long*)&lacc[t], (unsigned long long)(r + 1));
+        if (w != U64MAX) atomicMin((unsigned long long*)&uacc[t], (unsigned long long)(w - 1));
+        break;
+      }
     }
   }
 }
@@ -1297,16 +1319,20 @@ int dcc_ctx::maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, 
     // 2. its commits per row, then every later access against them
     uint64_t cap = 1024;
     while (cap < 4ull * std::max<uint32_t>(mp, 1)) cap <<= 1;
-    CR(mt_ptab.ensure(this, cap * 20, "maat prefix table"));
+    const size_t pbytes = (1u << MT_PBITS_LOG) / 8;
+    CR(mt_ptab.ensure(this, cap * 20 + pbytes, "maat prefix table"));
     MtPTab tb{(uint32_t*)mt_ptab.p, (unsigned long long*)((uint32_t*)mt_ptab.p + cap),
-              (unsigned long long*)((uint32_t*)mt_ptab.p + cap) + cap, (uint32_t)(cap - 1)};
+              (unsigned long long*)((uint32_t*)mt_ptab.p + cap) + cap, (uint32_t)(cap - 1),
+              (uint32_t*)((char*)mt_ptab.p + cap * 20)};
     CK(hipMemsetAsync(tb.key, 0xFF, cap * 4, stream));
     CK(hipMemsetAsync(tb.rmax, 0, cap * 8, stream));
     CK(hipMemsetAsync(tb.wmin, 0xFF, cap * 8, stream));
+    CK(hipMemsetAsync(tb.bits, 0, pbytes, stream));
     k_mt_ptab<<<(P + 255) / 256, 256, 0, stream>>>(d.off, P, d.acctype, rw_all, (const uint32_t*)mt_slot.p, state,
                                                   cts, tb);
-    k_mt_filter<<<g1(m - mp, 1u << 20), 256, 0, stream>>>((const uint32_t*)mt_slot.p, (const uint32_t*)mt_sval.p, mp, m,
-                                                tb, lacc, uacc);
+    const unsigned fgrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((m - mp + 1023) / 1024, 4ull * n_cu));
+    k_mt_filter<<<fgrid, 256, 0, stream>>>((const uint32_t*)mt_slot.p, (const uint32_t*)mt_sval.p, mp, m, tb, lacc,
+                                           uacc);
     k_mt_fdecide<<<g1(n - P), 256, 0, stream>>>(n, P, base, state, lacc, uacc);
     // 3. the survivors (undecided list) and the rounds' input: every access of
     //    a txn not aborted, in index order

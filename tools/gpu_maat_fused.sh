@@ -8,7 +8,7 @@ cd "$R"
 timeout -k 10 400 python -u -m pytest tests/test_gpu_maat.py tests/test_gpu_kat_branches.py -x -q --timeout 200 \
   --timeout-method thread > "$O/tests.log" 2>&1 || { tail -30 "$O/tests.log"; exit 1; }
 tail -1 "$O/tests.log"
-DCC_MT_FUSED=1 timeout -k 10 120 python3 tools/maat_rounds.py > "$O/fused.log" 2>&1 || { tail -5 "$O/fused.log"; exit 1; }
+DCC_MT_DEBUG=1 DCC_MT_FUSED=1 timeout -k 10 120 python3 tools/maat_rounds.py > "$O/fused.log" 2>&1 || { tail -5 "$O/fused.log"; exit 1; }
 DCC_MT_FUSED=0 timeout -k 10 120 python3 tools/maat_rounds.py > "$O/split.log" 2>&1 || { tail -5 "$O/split.log"; exit 1; }
 grep epoch "$O/fused.log" "$O/split.log"
 cd /tmp && export TMPDIR=/tmp
