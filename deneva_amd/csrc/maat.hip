@@ -59,7 +59,7 @@ constexpr uint64_t U64MAX = ~0ull;
 constexpr uint32_t MT_ITEMS = 16;
 constexpr uint32_t MT_TILE = 256 * MT_ITEMS;
 constexpr uint32_t MT_RING = 64;          // per-round undecided counters
-constexpr uint32_t MT_BATCH = 8;          // rounds enqueued per host check (A/B: profiles/r03/maat_batch/)
+constexpr uint32_t MT_BATCH = 12;         // rounds enqueued per host check (A/B: tools/ab_maat_batch.sh)
 constexpr uint64_t MT_LONG = 1u << 22;    // scans longer than this: a check after every round
 constexpr uint64_t MT_PREFIX = 1024;      // txns of the prefix level (DCC_MT_PREFIX; 0: none)
 constexpr uint8_t ST_UND = 0, ST_COM = 1, ST_ABO = 2;
@@ -605,10 +605,14 @@ __device__ inline Ms wave_rcomb_ms(Ms x) {
   return x;
 }
 
-__global__ __launch_bounds__(256) void k_mt_round(MtRoundArgs a, MtLb* lb, uint32_t tag, uint32_t* err) {
+__global__ __launch_bounds__(256) void k_mt_round(MtRoundArgs a, MtLb* lb, uint32_t tag, uint32_t* err,
+                                                  const uint32_t* prev_und) {
   __shared__ Ms s[4];
   __shared__ Ms s_pre;
   __shared__ MtTileLds L;
+  // a round enqueued after the list was already decided (a batch runs a
+  // fixed number of rounds between host checks): nothing to do
+  if (prev_und && *prev_und == 0) return;
   const uint32_t tile = blockIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint64_t base = (uint64_t)tile * MT_TILE;
   const uint64_t p0 = base + (uint64_t)threadIdx.x * MT_ITEMS;
@@ -700,8 +704,12 @@ __global__ __launch_bounds__(256) void k_mt_decide(uint64_t n, const uint32_t* u
                                                    const uint64_t* base, uint8_t* state,
                                                    uint64_t* cts, uint64_t* lacc, uint64_t* uacc,
                                                    uint32_t* pend, uint32_t* und_out,
-                                                   uint32_t* und_zero) {
+                                                   uint32_t* und_zero, const uint32_t* prev_und) {
   __shared__ uint32_t sh[4];
+  if (prev_und && *prev_und == 0) {  // already decided: this round's count stays 0
+    if (blockIdx.x == 0 && threadIdx.x == 0) *und_zero = 0;
+    return;
+  }
   uint32_t und = 0;
   const uint64_t cnt = ul ? *ulen : n;
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < cnt; i += (uint64_t)gridDim.x * 256) {
@@ -941,14 +949,14 @@ constexpr uint32_t MT_PBITS_LOG = 18;  // 32 KiB: the filter's LDS copy
 __device__ inline uint32_t mt_pbit(uint32_t s) { return (s * 0x9E3779B1u) >> (32 - MT_PBITS_LOG); }
 __device__ inline uint32_t mt_phash(uint32_t s) { return (s * 2654435761u) ^ (s >> 15); }
 
-// committed prefix txns' accesses into the table (a thread per prefix txn)
+// committed prefix txns' accesses into the table (16 lanes per prefix txn)
 __global__ __launch_bounds__(256) void k_mt_ptab(const uint32_t* off, uint32_t P, const uint8_t* at, uint32_t rw_all,
                                                  const uint32_t* slot, const uint8_t* state, const uint64_t* cts,
                                                  MtPTab tb) {
-  const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+  const uint32_t g = blockIdx.x * 256 + threadIdx.x, t = g >> 4;
   if (t >= P || state[t] != ST_COM) return;
   const uint64_t c = cts[t];
-  for (uint32_t x = off[t]; x < off[t + 1]; x++) {
+  for (uint32_t x = off[t] + (g & 15u); x < off[t + 1]; x += 16) {
     const uint8_t ty = at[x];
     const bool rd = rw_all || ty == DCC_RD, wr = rw_all || ty == DCC_WR;
     if (!rd && !wr) continue;
@@ -1015,6 +1023,101 @@ __global__ __launch_bounds__(256) void k_mt_fdecide(uint64_t n, uint64_t P, cons
   }
 }
 
+// The prefix's rounds in one workgroup: its sorted positions (<= 16,384) and
+// its txns' state (<= 1,024 txns, ids < 1,024) live in LDS, a round is a
+// block scan plus the decisions, with barriers instead of launches and host
+// checks -- the same per-round rule as k_mt_round + k_mt_decide (ms_elem /
+// ms_comb over the state at the round's start, then every undecided txn
+// decided from what the scan folded into it).
+constexpr uint32_t MS_T = 1024, MS_ITEMS = 16, MS_MAXPOS = MS_T * MS_ITEMS, MS_MAXTXN = MS_T;
+__global__ __launch_bounds__(MS_T) void k_mt_small(const uint8_t* sfl, const uint32_t* stx, uint32_t mp, uint32_t P,
+                                                   const uint64_t* base, uint8_t* state, uint64_t* cts,
+                                                   uint32_t* rounds_out) {
+  __shared__ uint8_t s_f[MS_MAXPOS];
+  __shared__ uint16_t s_t[MS_MAXPOS];
+  __shared__ uint8_t s_st[MS_MAXTXN];
+  __shared__ unsigned long long s_cts[MS_MAXTXN], s_l[MS_MAXTXN], s_u[MS_MAXTXN], s_b[MS_MAXTXN];
+  __shared__ uint32_t s_pend[MS_MAXTXN];
+  __shared__ Ms s_w[MS_T / 64];
+  __shared__ uint32_t s_und[MS_T / 64];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  for (uint32_t q = tid; q < MS_MAXPOS; q += MS_T) {
+    s_f[q] = q < mp ? sfl[q] : (uint8_t)0;
+    s_t[q] = q < mp ? (uint16_t)stx[q] : (uint16_t)0;
+  }
+  if (tid < P) {
+    s_st[tid] = state[tid];
+    s_b[tid] = base[tid];
+    s_cts[tid] = 0;
+    s_l[tid] = 0;
+    s_u[tid] = U64MAX;
+    s_pend[tid] = 0;
+  }
+  __syncthreads();
+  uint32_t r = 0;
+  for (;; r++) {
+    // the thread's positions are read from LDS twice (fold, then down pass)
+    // rather than held in registers across the block scan
+    Ms acc = ms_id();
+    for (uint32_t i = 0; i < MS_ITEMS; i++) {
+      const uint8_t f = s_f[tid * MS_ITEMS + i];
+      const uint32_t tx = s_t[tid * MS_ITEMS + i];
+      const uint8_t st = (f & F_LAST) ? s_st[tx] : ST_ABO;
+      acc = ms_comb(acc, ms_elem(f, st, st == ST_COM ? (uint64_t)s_cts[tx] : 0));
+    }
+    const Ms x = wave_incl_ms(acc);
+    if (lane == 63) s_w[wv] = x;
+    __syncthreads();
+    Ms pre = ms_id();
+    for (uint32_t w = 0; w < wv; w++) pre = ms_comb(pre, s_w[w]);
+    Ms ex = ms_shfl_up(x, 1);
+    if (lane == 0) ex = ms_id();
+    Ms run = ms_comb(pre, ex);
+    for (uint32_t i = 0; i < MS_ITEMS; i++) {
+      if (tid * MS_ITEMS + i >= mp) break;
+      const uint8_t f = s_f[tid * MS_ITEMS + i];
+      const uint32_t t = s_t[tid * MS_ITEMS + i];
+      const uint8_t st = (f & F_LAST) ? s_st[t] : ST_ABO;
+      if (f & F_START) run = Ms{1, 0, 0, U64MAX};
+      if ((f & F_LAST) && (f & (F_R | F_W)) && st == ST_UND) {
+        if ((f & F_W) && run.rmax) atomicMax(&s_l[t], (unsigned long long)(run.rmax + 1));
+        if (run.wmin != U64MAX) atomicMin(&s_u[t], (unsigned long long)(run.wmin - 1));
+        if ((run.und & 2u) || ((f & F_W) && (run.und & 1u))) s_pend[t] = 1u;
+      }
+      run = ms_comb(run, ms_elem(f & ~F_START, st, st == ST_COM ? (uint64_t)s_cts[t] : 0));
+    }
+    __syncthreads();
+    uint32_t und = 0;
+    if (tid < P && s_st[tid] == ST_UND) {
+      const uint64_t L = max((uint64_t)s_b[tid], (uint64_t)s_l[tid]);
+      const uint64_t U = s_u[tid];
+      if (L >= U) {
+        s_st[tid] = ST_ABO;
+      } else if (!s_pend[tid]) {
+        s_st[tid] = ST_COM;
+        s_cts[tid] = L;
+      } else {
+        und = 1;
+      }
+      s_l[tid] = 0;
+      s_u[tid] = U64MAX;
+      s_pend[tid] = 0;
+    }
+    for (int d = 32; d > 0; d >>= 1) und += __shfl_xor(und, d);
+    if (lane == 0) s_und[wv] = und;
+    __syncthreads();
+    uint32_t tot = 0;
+    for (uint32_t w = 0; w < MS_T / 64; w++) tot += s_und[w];
+    if (tot == 0 || r > P + 8) break;  // uniform; the smallest undecided txn decides every round
+    __syncthreads();  // s_w / s_und of the next round
+  }
+  if (tid < P) {
+    state[tid] = s_st[tid];
+    if (s_st[tid] == ST_COM) cts[tid] = s_cts[tid];
+  }
+  if (tid == 0) *rounds_out = r + 1;
+}
+
 // txns [0, P) as an undecided list
 __global__ __launch_bounds__(256) void k_mt_iota(uint32_t* ul, uint32_t* ulen, uint32_t P) {
   for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < P; i += gridDim.x * 256) ul[i] = i;
@@ -1045,22 +1148,33 @@ __global__ __launch_bounds__(256) void k_mt_gscatter(const uint32_t* off, uint64
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   const uint32_t len = mt_keep_len(off, n, state, t);
-  uint32_t x = len;
+  const uint32_t o0 = t < n ? off[t] : 0u;
+  uint32_t x = len;  // inclusive prefix of the wave's kept lengths
   for (uint32_t d = 1; d < 64; d <<= 1) {
     const uint32_t y = __shfl_up(x, d);
     if (lane >= d) x += y;
   }
   if (lane == 63) sh[wv] = x;
   __syncthreads();
-  uint32_t b = bsum[blockIdx.x] + x - len;
+  uint32_t b = bsum[blockIdx.x];
   for (uint32_t w = 0; w < wv; w++) b += sh[w];
-  if (!len) return;
-  const uint32_t o0 = off[t];
-  for (uint32_t i = 0; i < len; i++) {
-    const uint8_t ty = at[o0 + i];
-    const bool rd = rw_all || ty == DCC_RD, wr = rw_all || ty == DCC_WR;
-    okey[b + i] = slot[o0 + i];
-    oval[b + i] = ((uint32_t)t << 2) | (rd ? SV_R : 0u) | (wr ? SV_W : 0u);
+  const uint32_t tot = __shfl(x, 63), ex = x - len;
+  // lanes over the wave's kept accesses (coalesced stores): output q belongs
+  // to the first lane whose inclusive prefix exceeds q
+  for (uint32_t q0 = 0; q0 < tot; q0 += 64) {
+    const uint32_t q = q0 + lane;
+    uint32_t lo = 0;
+#pragma unroll
+    for (uint32_t st = 32; st > 0; st >>= 1)
+      if (__shfl(x, lo + st - 1) <= q) lo += st;
+    const uint32_t src = __shfl(o0, lo) + (q - __shfl(ex, lo));
+    const uint32_t tt = (uint32_t)(blockIdx.x * 256 + wv * 64 + lo);
+    if (q < tot) {
+      const uint8_t ty = at[src];
+      const bool rd = rw_all || ty == DCC_RD, wr = rw_all || ty == DCC_WR;
+      okey[b + q] = slot[src];
+      oval[b + q] = (tt << 2) | (rd ? SV_R : 0u) | (wr ? SV_W : 0u);
+    }
   }
 }
 
@@ -1211,6 +1325,7 @@ int dcc_ctx::maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, 
                    int ub) -> int {
     bool done = false;
     int cb = 0;  // current buffer set
+    const uint32_t r0 = rounds;  // this solve's first round (no earlier count of its own)
     while (!done) {
       const uint32_t k0 = rounds;
       const uint64_t tiles_c = (mc + MT_TILE - 1) / MT_TILE;
@@ -1227,12 +1342,13 @@ int dcc_ctx::maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, 
       }();
       const uint32_t nb = (rounds == 0 || mc > long_scan) ? 1u : batch;
       for (uint32_t q = 0; q < nb; q++, rounds++) {
+        const uint32_t* prev = rounds > r0 ? &ring[(rounds - 1) % MT_RING] : nullptr;
         if (mc && mt_fused) {
           if (mt_tag + 1 >= (1u << 30)) {
             CK(hipMemsetAsync(mt_lb.p, 0, mt_lb.cap, stream));
             mt_tag = 0;
           }
-          k_mt_round<<<(unsigned)tiles_c, 256, 0, stream>>>(ra, (MtLb*)mt_lb.p, ++mt_tag, cnt + 1);
+          k_mt_round<<<(unsigned)tiles_c, 256, 0, stream>>>(ra, (MtLb*)mt_lb.p, ++mt_tag, cnt + 1, prev);
         } else if (mc) {
           k_mt_up<<<(unsigned)tiles_c, 256, 0, stream>>>(ra);
           k_mt_top<<<1, 256, 0, stream>>>((Ms*)mt_agg.p, (uint32_t)tiles_c);
@@ -1240,7 +1356,7 @@ int dcc_ctx::maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, 
         }
         k_mt_decide<<<g1(ulen_host, 2048), 256, 0, stream>>>(n, ul_cur, ulen_cur, base, state, cts, lacc,
                                                               uacc, pend, &ring[rounds % MT_RING],
-                                                              &ring[(rounds + 1) % MT_RING]);
+                                                              &ring[(rounds + 1) % MT_RING], prev);
       }
       if (mc) {
         k_mt_keep_count<<<(unsigned)tiles_c, 256, 0, stream>>>(mc, sflb[cb], stxb[cb], state, tcnt);
@@ -1313,9 +1429,15 @@ int dcc_ctx::maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, 
     // 1. the prefix alone: its accesses are the first mp pairs of the base
     //    pass's (slot, value) buffers
     sort_groups(mp);
-    k_mt_iota<<<g1(P), 256, 0, stream>>>(ul_buf[0], ulen_w, P);
-    CK(hipGetLastError());
-    CR(solve(mp, ul_buf[0], ulen_w, P, 1));
+    uint32_t* small_rounds = cnt + 7;  // k_mt_small's round count (0: not used)
+    if (P <= MS_MAXTXN && mp <= MS_MAXPOS) {
+      k_mt_small<<<1, MS_T, 0, stream>>>(sflb[0], stxb[0], mp, P, base, state, cts, small_rounds);
+      CK(hipGetLastError());
+    } else {
+      k_mt_iota<<<g1(P), 256, 0, stream>>>(ul_buf[0], ulen_w, P);
+      CK(hipGetLastError());
+      CR(solve(mp, ul_buf[0], ulen_w, P, 1));
+    }
     // 2. its commits per row, then every later access against them
     uint64_t cap = 1024;
     while (cap < 4ull * std::max<uint32_t>(mp, 1)) cap <<= 1;
@@ -1328,8 +1450,8 @@ int dcc_ctx::maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, 
     CK(hipMemsetAsync(tb.rmax, 0, cap * 8, stream));
     CK(hipMemsetAsync(tb.wmin, 0xFF, cap * 8, stream));
     CK(hipMemsetAsync(tb.bits, 0, pbytes, stream));
-    k_mt_ptab<<<(P + 255) / 256, 256, 0, stream>>>(d.off, P, d.acctype, rw_all, (const uint32_t*)mt_slot.p, state,
-                                                  cts, tb);
+    k_mt_ptab<<<(16 * P + 255) / 256, 256, 0, stream>>>(d.off, P, d.acctype, rw_all, (const uint32_t*)mt_slot.p,
+                                                       state, cts, tb);
     const unsigned fgrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((m - mp + 1023) / 1024, 4ull * n_cu));
     k_mt_filter<<<fgrid, 256, 0, stream>>>((const uint32_t*)mt_slot.p, (const uint32_t*)mt_sval.p, mp, m, tb, lacc,
                                            uacc);
@@ -1349,11 +1471,13 @@ int dcc_ctx::maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, 
       GatherArgs ga{};
       ga.job[ga.n++] = CopyJob{gb + nblk, (uint32_t*)hmisc_dev, 1};
       ga.job[ga.n++] = CopyJob{ulen_w, (uint32_t*)hmisc_dev + 1, 1};
+      ga.job[ga.n++] = CopyJob{small_rounds, (uint32_t*)hmisc_dev + 2, 1};
       launch_gather(ga, stream);
       CK(hipGetLastError());
       CK(hipStreamSynchronize(stream));
     }
     const uint32_t m2 = ((const uint32_t*)hmisc)[0], nsurv = ((const uint32_t*)hmisc)[1];
+    rounds += ((const uint32_t*)hmisc)[2];  // the prefix's rounds when k_mt_small ran them
     if (mt_debug)
       fprintf(stderr, "maat prefix %u txns (%u accesses, %u rounds): %u survivors, %u positions\n", P, mp,
               rounds, nsurv, m2);
