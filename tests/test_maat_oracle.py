@@ -79,3 +79,66 @@ def test_ycsb_agree(theta):
 
 def test_tpcc_agree():
     both(d.gen_tpcc(n_txn=2000, num_wh=4), rw_all=True)
+
+
+def _prefix_level_model(b, P):
+    """maat.hip's prefix level restated on the CPU (empty row timestamps):
+    the first P txns decided by the formula alone, every later txn aborted
+    when its bounds from those commits are already empty, the survivors then
+    decided in index order against every commit before them."""
+    n = b.n_txn
+    off = np.asarray(b.offsets, np.int64)
+    keys = np.asarray(b.keys)
+    at = np.asarray(b.acctype)
+    big = 1 << 62
+
+    def bounds(i, maxr, minw):
+        L, U = 1, big
+        for x in range(off[i], off[i + 1]):
+            k, t = int(keys[x]), int(at[x])
+            rd, wr = t == RD, t == WR
+            if not (rd or wr):
+                continue
+            if wr and k in maxr:
+                L = max(L, maxr[k] + 1)
+            if k in minw:
+                U = min(U, minw[k] - 1)
+        return L, U
+
+    def commit(i, c, maxr, minw):
+        for x in range(off[i], off[i + 1]):
+            k, t = int(keys[x]), int(at[x])
+            if t == WR:
+                minw[k] = min(minw.get(k, big), c)
+            elif t == RD:
+                maxr[k] = max(maxr.get(k, 0), c)
+
+    rc = np.full(n, 2, np.uint8)  # abort unless committed
+    cts = np.zeros(n, np.uint64)
+    maxr, minw = {}, {}
+    for i in range(min(P, n)):
+        L, U = bounds(i, maxr, minw)
+        if L < U:
+            commit(i, L, maxr, minw)
+            rc[i], cts[i] = 0, L
+    pre_r, pre_w = dict(maxr), dict(minw)
+    surv = [i for i in range(P, n) if (lambda lu: lu[0] < lu[1])(bounds(i, pre_r, pre_w))]
+    for i in surv:  # index order: every earlier commit is known
+        L, U = bounds(i, maxr, minw)
+        if L < U:
+            commit(i, L, maxr, minw)
+            rc[i], cts[i] = 0, L
+    return rc, cts, len(surv)
+
+
+@pytest.mark.parametrize("theta,P", [(0.9, 64), (0.99, 128), (0.6, 256)])
+def test_prefix_level_is_exact(theta, P):
+    # the argument behind maat.hip's prefix filter: L only grows and U only
+    # shrinks as earlier txns commit, so a txn whose bounds the prefix's
+    # commits alone empty is aborted by the full replay too
+    b = d.gen_ycsb(n_txn=3000, zipf_theta=theta, seed=0x99 + P)
+    rc, cts, nsurv = _prefix_level_model(b, P)
+    erc, ects, _ = orc.maat(b)
+    assert np.array_equal(rc, erc)
+    assert np.array_equal(cts[erc == 0], np.asarray(ects, np.uint64)[erc == 0])
+    assert nsurv < b.n_txn - P  # the filter aborts something
