@@ -1041,22 +1041,25 @@ __global__ __launch_bounds__(256) void k_sw_cout(SwCoutArgs a) {
   // 1024 accesses per workgroup round (wave w: [256w, 256w + 256)), one
   // fill-counter atomic per round
   for (uint32_t x0 = blockIdx.x * 1024; x0 < range; x0 += gridDim.x * 1024) {
-    uint32_t ent[4];
+    // each access's entry, position and key loaded together (the position
+    // and key of an access that is not a write are read and ignored), then
+    // the commit-mask word: two round trips instead of four
+    uint32_t ent[4], ap[4];
+    uint64_t kx[4];
     bool c[4];
 #pragma unroll
     for (uint32_t u = 0; u < 4; u++) {
       const uint32_t x = x0 + wv * 256 + u * 64 + lane;
-      ent[u] = x < range ? a.aent[x] : 0u;
+      const bool in = x < range;
+      ent[u] = in ? a.aent[x] : 0u;
+      ap[u] = in ? a.apos[x] : 0u;
+      kx[u] = in ? a.in.keys[off0 + x] : 0ull;
     }
+    uint64_t mw[4];
 #pragma unroll
-    for (uint32_t u = 0; u < 4; u++) {
-      const uint32_t x = x0 + wv * 256 + u * 64 + lane;
-      c[u] = false;
-      if (ent[u] & 32u) {
-        const uint32_t p = a.apos[x];
-        c[u] = (a.mg[p >> 6] >> (p & 63u)) & 1ull;
-      }
-    }
+    for (uint32_t u = 0; u < 4; u++) mw[u] = (ent[u] & 32u) ? a.mg[ap[u] >> 6] : 0ull;
+#pragma unroll
+    for (uint32_t u = 0; u < 4; u++) c[u] = (ent[u] & 32u) && ((mw[u] >> (ap[u] & 63u)) & 1ull);
     uint64_t cm[4];
     uint32_t wc = 0;
 #pragma unroll
@@ -1076,8 +1079,7 @@ __global__ __launch_bounds__(256) void k_sw_cout(SwCoutArgs a) {
 #pragma unroll
     for (uint32_t u = 0; u < 4; u++) {
       if (c[u]) {
-        const uint32_t x = x0 + wv * 256 + u * 64 + lane;
-        const uint64_t key = a.in.keys[off0 + x];
+        const uint64_t key = kx[u];
         a.ckeys_out[base + (uint32_t)__popcll(cm[u] & lanemask_lt())] = key;
         const uint32_t id = sw_aid(ent[u]);
         if (id < SW_ID_NONE) atomicOr(&a.cbits_out[id >> 5], 1u << (id & 31u));
@@ -1549,14 +1551,27 @@ __global__ __launch_bounds__(SW_CHUNK) void k_sw_compact(SwFilterArgs a) {
   // totals): packed count|accesses words subtract field by field.
   {
     uint64_t pre = 0, all = 0, rpre = 0, rall = 0;
-    for (uint32_t q = threadIdx.x; q < a.nblocks; q += SW_CHUNK) {
-      const uint64_t v = a.bsum[q];
-      all += v;
-      if (q < blockIdx.x) pre += v;
-      if (a.ro_split) {
-        const uint64_t r = a.rbsum[q];
-        rall += r;
-        if (q < blockIdx.x) rpre += r;
+    // every total of this thread loaded before the first is added (the
+    // filter grid is at most 4 x n_CU: four per thread at 256 CUs), not one
+    // dependent round trip per step
+    constexpr uint32_t TU = 4;
+    for (uint32_t q0 = threadIdx.x; q0 < a.nblocks; q0 += SW_CHUNK * TU) {
+      uint64_t v[TU], r[TU];
+#pragma unroll
+      for (uint32_t u = 0; u < TU; u++) {
+        const uint32_t q = q0 + u * SW_CHUNK;
+        v[u] = q < a.nblocks ? a.bsum[q] : 0ull;
+        r[u] = (a.ro_split && q < a.nblocks) ? a.rbsum[q] : 0ull;
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < TU; u++) {
+        const uint32_t q = q0 + u * SW_CHUNK;
+        all += v[u];
+        rall += r[u];
+        if (q < blockIdx.x) {
+          pre += v[u];
+          rpre += r[u];
+        }
       }
     }
     pre = wave_sum64(pre);
