@@ -93,18 +93,22 @@ def test_c1_calvin_handoff(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("threads,theta,table", [(4, 0.6, 65536), (16, 0.9, 65536)])
-def test_c1_live_capture_replayed_on_gpu(threads, theta, table):
+@pytest.mark.parametrize("threads,theta,table,txns", [(4, 0.6, 65536, 1000), (16, 0.9, 65536, 1000),
+                                                     (16, 0.9, 1 << 24, 65536)])
+def test_c1_live_capture_replayed_on_gpu(threads, theta, table, txns):
     # real worker threads run OptCC live (occ_live.h), capturing every
     # critical section; dcc_occ_validate_snapshot must decide every captured
     # validation exactly as the live run did
-    out = run_driver("--live", "--threads", str(threads), "--txns", "1000", "--theta", str(theta),
-                     "--req", "10", "--table", str(table))
+    # the last case is the headline's scale of capture: 1,048,576 txns (2.3M
+    # live validations with the restarts) by 16 workers over the 16M-key
+    # YCSB table, ~7 s (profiles/r04/live_capture_1m.json)
+    out = run_driver("--live", "--threads", str(threads), "--txns", str(txns), "--theta", str(theta),
+                     "--req", "10", "--table", str(table), timeout=300)
     assert out["failed"] == 0, out
     assert out["live_mismatch"] == 0
     # a txn starved past the retry limit is dropped by the live run (the
     # reference would restart it forever); every validation is still checked
-    assert out["commits"] + out["gave_up"] == threads * 1000
-    assert out["gave_up"] <= threads * 1000 // 100
+    assert out["commits"] + out["gave_up"] == threads * txns
+    assert out["gave_up"] <= threads * txns // 100
     if threads > 4:
         assert out["restarts"] > 0  # the run was really concurrent
