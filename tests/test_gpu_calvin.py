@@ -135,6 +135,27 @@ def test_c4_full_size(engine):
     run(engine, b, waves=False)
 
 
+def test_c4_full_size_waves_and_dispatch(engine):
+    # the C4 epoch with wave levels (row_lock.cpp:317-357 grant chains, one
+    # level per hand-off: ~0.1 s at this size) and the dispatch
+    # lists built from them (txn_table.cpp:151-176), against the oracle
+    b = d.gen_ycsb(n_txn=1 << 20, zipf_theta=0.9, part_cnt=16, chunk_txns=65536, want_home=True)
+    b.order = c4_order(b)
+    g, rc, w, st = engine.calvin_order_epoch(b, want_group=True, want_wave=True)
+    eg, erc, ew = orc.calvin(b)
+    w = np.asarray(w).astype(np.uint32)
+    assert np.array_equal(np.asarray(g).astype(np.uint32), eg)
+    assert np.array_equal(np.asarray(rc), erc)
+    assert np.array_equal(w, ew) and st["rounds"] == int(ew.max()) + 1
+    print(f"C4 waves: {int(ew.max()) + 1} levels, device {st['device_ms']:.2f} ms")
+    off, txn = engine.calvin_dispatch(w, b.order)
+    seq = np.argsort(b.order, kind="stable")
+    want = seq[np.argsort(w[seq], kind="stable")]
+    assert np.array_equal(np.asarray(txn), want.astype(np.uint32))
+    counts = np.bincount(w, minlength=int(w.max()) + 1)
+    assert np.array_equal(np.diff(np.asarray(off, np.int64)), counts)
+
+
 def test_device_pointers(engine):
     import torch
     b = d.gen_ycsb(n_txn=50000, zipf_theta=0.9)
