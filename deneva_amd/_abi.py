@@ -44,6 +44,8 @@ OPT_SWEEP_LEVELS = 6
 OPT_HIST_MERGE = 7
 OPT_FAIL_RANK = 8
 OPT_RO_SPLIT = 10
+OPT_PIPELINE = 11
+OPT_CALVIN_PATH = 12
 
 
 class Batch(C.Structure):
@@ -194,6 +196,8 @@ _SIGS = [
                                    C.POINTER(C.c_uint64)]),
     ("dcc_occ_validate_epoch", C.c_int, [_P, C.POINTER(Batch), _P, _P, C.POINTER(Stats)]),
     ("dcc_occ_finish_epoch", C.c_int, [_P, _P, _P, C.c_uint32]),
+    ("dcc_occ_submit_epoch", C.c_int, [_P, C.POINTER(Batch), _P, _P, C.POINTER(C.c_uint64)]),
+    ("dcc_occ_wait_epoch", C.c_int, [_P, C.c_uint64, C.POINTER(Stats)]),
     ("dcc_occ_validate_snapshot", C.c_int,
      [_P, C.POINTER(Batch), C.POINTER(Snapshot), _P, C.POINTER(Stats)]),
     ("dcc_occ_history_append", C.c_int, [_P, _P, _P, C.c_uint64]),

@@ -110,6 +110,9 @@ extern "C" int dcc_file_write(const char* path, const dcc_file_info* info, const
                               const uint8_t* rc, const uint64_t* commit_tn, const uint32_t* group,
                               const uint32_t* wave) {
   if (!path || !info || !b || (b->flags & DCC_DEVICE_PTRS)) return DCC_EINVAL;
+  // the file holds the full-width form (u64 keys and timestamps, one access
+  // type per byte): a compact batch must be widened by the caller first
+  if (b->flags & DCC_COMPACT_FLAGS) return DCC_EINVAL;
   if (b->n_txn && !b->offsets) return DCC_EINVAL;
   const uint64_t n = b->n_txn, nnz = b->nnz;
   if (n && (b->offsets[0] != 0 || b->offsets[n] != nnz)) return DCC_EINVAL;

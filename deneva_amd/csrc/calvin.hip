@@ -39,6 +39,7 @@
 #include "dcc.h"
 #include "dcc_ctx.h"
 #include "dcc_device.h"
+#include "dcc_env.h"
 #include "occ_kernels.h"
 #include "prep_body.h"
 #include "radix_sort.h"
@@ -1120,12 +1121,11 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint3
   const KeyPack op = have_seq ? make_keypack(oor ^ oand) : KeyPack{};
   static_assert(sizeof(KeyPack) <= sizeof(CvGraphKey::kp), "key image");
   const bool cv_graph_ok = !profiling && !waves && nh == 0 && comm_ranks() == 1 &&
-                           !getenv("DCC_NO_GRAPH");
+                           !DCC_ENV("DCC_NO_GRAPH");
   // the bucket path (calvin_bucket.h) for large epochs of uniform txns;
-  // DCC_CV_BUCKET=0 keeps the global sort + scan, =1 takes the bucket path at
-  // every size it applies to
-  const char* cbe = getenv("DCC_CV_BUCKET");
-  const int cb_mode = cbe ? atoi(cbe) : -1;
+  // DCC_OPT_CALVIN_PATH: 1 keeps the global sort + scan, 2 takes the bucket
+  // path at every size it applies to (0: the bucket path on large epochs)
+  const int cb_mode = cv_path == 1 ? 0 : cv_path == 2 ? 1 : -1;
   CbPlan cbp{};
   const bool use_cb = d.nnz && cb_mode != 0 && !waves && nh == 0 && ulen &&
                       (cb_mode == 1 || d.nnz >= CV_PUT_MIN) && cb_plan(d.n, d.nnz, ulen, kp.bits, &cbp);

@@ -32,6 +32,16 @@
 #include "calvin_gl.h"
 #include "dcc.h"
 #include "dcc_device.h"
+#include "dcc_env.h"
+
+// The DCC_CB_VARIANT timing variants (kernels with one phase removed, wrong
+// results by design) exist only in -DDCC_EXPERIMENTS builds: in the product
+// build every variant test is a compile-time 0.
+#ifdef DCC_EXPERIMENTS
+#define CB_VAR(v, bit) ((v) & (bit))
+#else
+#define CB_VAR(v, bit) 0u
+#endif
 
 namespace dcc {
 namespace {
@@ -273,7 +283,7 @@ __global__ __launch_bounds__(CB_PT) void k_cb_part(CbSrc s, uint32_t bb, const u
     for (uint32_t i = tid; i < W * BM; i += CB_PT) (&s_wc[0][0])[i] = 0;
     uint64_t e[16];
     uint32_t ne;
-    if (s.var & 4u) {
+    if (CB_VAR(s.var, 4u)) {
       ne = nq * s.ulen;
 #pragma unroll
       for (uint32_t it = 0; it < 16; it++)
@@ -289,7 +299,7 @@ __global__ __launch_bounds__(CB_PT) void k_cb_part(CbSrc s, uint32_t bb, const u
     for (uint32_t it = 0; it < 16; it++) {
       const bool act = it * 64 + lane < ne;
       const uint32_t b = (uint32_t)(e[it] >> 32) & bmask;
-      const uint64_t peers = (s.var & 2u) ? (act ? 1ull << lane : 0ull) : bucket_peers<NB>(b, act, bb);
+      const uint64_t peers = (CB_VAR(s.var, 2u)) ? (act ? 1ull << lane : 0ull) : bucket_peers<NB>(b, act, bb);
       const uint32_t lr = (uint32_t)__builtin_popcountll(peers & lt);
       const uint32_t before = my[b];
       loc[it] = (uint16_t)(before + lr);
@@ -327,7 +337,7 @@ __global__ __launch_bounds__(CB_PT) void k_cb_part(CbSrc s, uint32_t bb, const u
     __syncthreads();
     for (uint32_t j = tid; j < n_sub; j += CB_PT) {
       const uint64_t x = s_stg[j];
-      if (!(s.var & 1u)) out[s_gof[(uint32_t)(x >> 32) & bmask] + j] = x;
+      if (!(CB_VAR(s.var, 1u))) out[s_gof[(uint32_t)(x >> 32) & bmask] + j] = x;
     }
     __syncthreads();
   }
@@ -398,7 +408,7 @@ __global__ __launch_bounds__(CB_BT) void k_cb_bucket(CbBucket a) {
   const uint32_t ntab = 1u << a.lbits;
   for (uint32_t i = tid; i < ntab; i += CB_BT) s_tab[i] = TAB_EMPTY;
   for (uint32_t d = tid; d < a.ndig; d += CB_BT) s_dc[d] = 0;
-  const uint32_t npass = (a.var & 8u) ? 0u : (a.lbits + 3) / 4;
+  const uint32_t npass = (CB_VAR(a.var, 8u)) ? 0u : (a.lbits + 3) / 4;
   const uint32_t dpt = (a.ndig + CB_BT - 1) / CB_BT;  // windows per thread (<= 3)
   const uint32_t d0 = min(a.ndig, tid * dpt), d1 = min(a.ndig, d0 + dpt);
   uint32_t t_prev = NOTXN;  // the previous chunk's last txn
@@ -498,7 +508,7 @@ __global__ __launch_bounds__(CB_BT) void k_cb_bucket(CbBucket a) {
     const uint64_t next_e = p0 + CB_IT < nc ? s_stg[stg_ix(p0 + CB_IT)] : ~0ull;
     uint32_t dupm = 0;
     uint32_t grp[CB_IT];
-    if (a.var & 32u) {
+    if (CB_VAR(a.var, 32u)) {
 #pragma unroll
       for (uint32_t i = 0; i < CB_IT; i++) grp[i] = (uint32_t)(e[i] >> 32) >> bsh;
       goto staged;
@@ -587,7 +597,7 @@ __global__ __launch_bounds__(CB_BT) void k_cb_bucket(CbBucket a) {
       }
     }
   staged:
-    if (a.var & 64u) {
+    if (CB_VAR(a.var, 64u)) {
       uint32_t x = 0;
 #pragma unroll
       for (uint32_t i = 0; i < CB_IT; i++) x ^= grp[i];
@@ -625,7 +635,7 @@ __global__ __launch_bounds__(CB_BT) void k_cb_bucket(CbBucket a) {
     for (uint32_t j = tid; j < nc; j += CB_BT) {
       const uint64_t x = s_stg[j];
       const uint32_t d = ((uint32_t)x >> 7) >> a.tsh;
-      if (!(a.var & 16u)) a.out[((uint64_t)r * a.ndig + d) * a.span + (uint32_t)(s_dg[d] + j)] = x;
+      if (!(CB_VAR(a.var, 16u))) a.out[((uint64_t)r * a.ndig + d) * a.span + (uint32_t)(s_dg[d] + j)] = x;
     }
     lds_barrier();
   next_chunk:
@@ -712,7 +722,7 @@ hipError_t cb_run(const CbPlan& p, const CbArgs& a, hipStream_t st, hipEvent_t e
   uint32_t* bbase = tot + B;
   uint32_t* gcnt = bbase + B;
   static const uint32_t var = [] {
-    const char* e = getenv("DCC_CB_VARIANT");
+    const char* e = DCC_ENV("DCC_CB_VARIANT");
     return e ? (uint32_t)atoi(e) : 0u;
   }();
   const CbSrc s{a.keys, a.acctype, a.seq, (uint32_t)a.n, a.ulen, ((1u << 20) + a.ulen - 1) / a.ulen,

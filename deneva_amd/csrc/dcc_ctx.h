@@ -162,7 +162,6 @@ struct dcc_ctx {
   DevBuf mt_lb;          // fused round scan: look-back status per tile (k_mt_round)
   DevBuf mt_ptab;        // prefix level: per-row commit bounds of the prefix (MtPTab)
   uint32_t mt_tag = 0;   // its round tag (monotone; the buffer is zeroed when it wraps)
-  int mt_fused = -1;     // DCC_MT_FUSED: 1 fused round scan (default), 0 up / top / down
   // GPU index (index.hip): key table, newest insert ordinal per key, rows
   DevBuf ix_keys, ix_ord, ix_rows, ix_cnt, wv_buf, ix_scr, wv_hbuf, wv_obuf;
   uint32_t ix_bits = 0;
@@ -201,6 +200,37 @@ struct dcc_ctx {
                   uint64_t* nnz_w_prefix = nullptr);
   int read_partials(size_t bytes);
   int occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dcc_stats* st);
+  // The epoch in two halves (occ_pipe.cpp overlaps epochs of several lane
+  // contexts): begin enqueues; with `async` and a replayable graph it returns
+  // right after the graph launch (run.pending) and end synchronises.
+  struct OccRun {
+    uint64_t n_txn = 0;
+    uint32_t flags = 0;
+    uint8_t* out_rc = nullptr;
+    uint64_t* out_tn = nullptr;
+    DevBatch d;
+    bool sh = false, dev_out = false, defer = false, sweep = false, want_tn = false;
+    bool replay = false, capturing = false, pending = false, active = false;
+    uint32_t glv = 0, maxlen = 0, rounds = 0, handoffs = 0;
+    uint64_t nnz_w = 0;
+    int next_level = 0, serial_tail = -1;
+    uint8_t* rc_dev = nullptr;
+    uint32_t* cf = nullptr;
+    uint64_t* tn_dev = nullptr;
+    PeelInfo info;
+    GraphKey gkey{};
+    dcc_stats S;
+    double t_wall0 = 0;
+    uint64_t n_cw = 0;  // committed writers of the finished epoch (tnc advance)
+  };
+  OccRun run;
+  int occ_begin(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, bool async);
+  int occ_end(dcc_stats* st);
+  int occ_final(bool async);  // finalize launches (or the graph replay) of `run`
+  // pipelined epochs over lane contexts on this device (occ_pipe.cpp)
+  struct OccPipe* pipe = nullptr;
+  uint32_t pipe_lanes = 3;  // DCC_OPT_PIPELINE
+  int cv_path = 0;          // DCC_OPT_CALVIN_PATH: 0 auto, 1 sort, 2 bucket
   // DCC_OCC_DEFER_FINISH: the decided epoch waiting for its global RC
   bool fin_pending = false;
   DevBatch fin_d;
@@ -241,4 +271,7 @@ int dcc_multi_occ_epoch(dcc_ctx* ctx, const dcc_batch* b, uint8_t* out_rc, uint6
 int dcc_multi_calvin_epoch(dcc_ctx* ctx, const dcc_batch* b, const dcc_calvin_held* held,
                            uint32_t* out_group, uint8_t* out_rc, uint32_t* out_wave, dcc_stats* st);
 int dcc_multi_each(dcc_ctx* ctx, int (*fn)(dcc_ctx*, void*), void* user);
+// pipelined epochs (occ_pipe.cpp): complete every epoch in flight / tear down
+void dcc_pipe_drain(dcc_ctx* ctx);
+void dcc_pipe_destroy(dcc_ctx* ctx);
 dcc_ctx* dcc_multi_sub(dcc_ctx* ctx, int rank);

@@ -152,6 +152,7 @@ extern "C" int dcc_init(dcc_ctx** out, int device_id) {
 
 extern "C" void dcc_destroy(dcc_ctx* ctx) {
   if (!ctx) return;
+  dcc_pipe_destroy(ctx);
   dcc_multi_destroy(ctx);
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
@@ -185,6 +186,12 @@ extern "C" int dcc_set_option(dcc_ctx* ctx, int option, int64_t value) {
     if (!ctx->multi) return ctx->fail(DCC_EINVAL, "DCC_OPT_FAIL_RANK: multi-GPU contexts only");
     return dcc_multi_set_fail_rank(ctx, (int)value);
   }
+  if (option == DCC_OPT_PIPELINE) {
+    if (value < 1 || value > 4) return DCC_EINVAL;
+    dcc_pipe_destroy(ctx);  // lanes are re-created at the new count
+    ctx->pipe_lanes = (uint32_t)value;
+    return DCC_OK;
+  }
   if (ctx->multi)
     for (int r = 0; r < dcc_multi_size(ctx); r++) {
       const int e = dcc_set_option(dcc_multi_sub(ctx, r), option, value);
@@ -213,6 +220,10 @@ extern "C" int dcc_set_option(dcc_ctx* ctx, int option, int64_t value) {
     case DCC_OPT_HIST_MERGE:
       if (value < 1) return DCC_EINVAL;
       ctx->hist_merge_min = (uint64_t)value;
+      return DCC_OK;
+    case DCC_OPT_CALVIN_PATH:
+      if (value < 0 || value > 2) return DCC_EINVAL;
+      ctx->cv_path = (int)value;
       return DCC_OK;
     case DCC_OPT_BATCH_MAX:
       if (value < 1 || value > 32) return DCC_EINVAL;
@@ -403,6 +414,7 @@ int dcc_ctx::hist_append_epoch(const DevBatch& d, const uint64_t* tn_dev, uint64
 extern "C" int dcc_occ_history_append(dcc_ctx* ctx, const uint64_t* keys, const uint64_t* tn,
                                       uint64_t n) {
   if (!ctx || (n && (!keys || !tn))) return DCC_EINVAL;
+  dcc_pipe_drain(ctx);
   if (n == 0) return DCC_OK;
   if (ctx->multi) {  // each rank keeps its key shard's history
     const int R = dcc_multi_size(ctx);
@@ -439,6 +451,7 @@ extern "C" int dcc_occ_history_append(dcc_ctx* ctx, const uint64_t* keys, const 
 
 extern "C" int dcc_occ_history_clear(dcc_ctx* ctx) {
   if (!ctx) return DCC_EINVAL;
+  dcc_pipe_drain(ctx);
   if (ctx->multi)
     for (int r = 0; r < dcc_multi_size(ctx); r++) dcc_occ_history_clear(dcc_multi_sub(ctx, r));
   for (HistStore& h : ctx->hs) {
@@ -454,6 +467,7 @@ extern "C" int dcc_occ_history_clear(dcc_ctx* ctx) {
 
 extern "C" int dcc_occ_history_trim(dcc_ctx* ctx, uint64_t tn_floor) {
   if (!ctx) return DCC_EINVAL;
+  dcc_pipe_drain(ctx);
   if (ctx->multi) {
     for (int r = 0; r < dcc_multi_size(ctx); r++) CR(dcc_occ_history_trim(dcc_multi_sub(ctx, r), tn_floor));
     return DCC_OK;
@@ -511,6 +525,7 @@ extern "C" uint64_t dcc_occ_history_size(const dcc_ctx* ctx) {
 extern "C" int dcc_occ_history_export(dcc_ctx* ctx, uint64_t* keys, uint64_t* tn, uint64_t cap,
                                       uint64_t* out_n) {
   if (!ctx || !out_n) return DCC_EINVAL;
+  dcc_pipe_drain(ctx);
   if (ctx->multi) {
     const uint64_t total = dcc_occ_history_size(ctx);
     *out_n = total;
@@ -541,12 +556,14 @@ extern "C" int dcc_occ_history_export(dcc_ctx* ctx, uint64_t* keys, uint64_t* tn
 
 extern "C" int dcc_occ_set_tnc(dcc_ctx* ctx, uint64_t tnc) {
   if (!ctx) return DCC_EINVAL;
+  dcc_pipe_drain(ctx);
   if (ctx->multi)
     for (int r = 0; r < dcc_multi_size(ctx); r++) dcc_multi_sub(ctx, r)->tnc = tnc;
   ctx->tnc = tnc;
   return DCC_OK;
 }
 extern "C" uint64_t dcc_occ_get_tnc(const dcc_ctx* ctx) {
+  dcc_pipe_drain(const_cast<dcc_ctx*>(ctx));  // tnc counts the epochs in flight
   if (ctx && ctx->multi) return dcc_multi_sub((dcc_ctx*)ctx, 0)->tnc;
   return ctx ? ctx->tnc : 0;
 }
@@ -747,6 +764,7 @@ extern "C" int dcc_host_free(dcc_ctx* ctx, void* p) {
 extern "C" int dcc_occ_validate_epoch(dcc_ctx* ctx, const dcc_batch* batch, uint8_t* out_rc,
                                       uint64_t* out_commit_tn, dcc_stats* out_stats) {
   if (!ctx) return DCC_EINVAL;
+  dcc_pipe_drain(ctx);  // submit order
   if (ctx->multi) return dcc_multi_occ_epoch(ctx, batch, out_rc, out_commit_tn, out_stats);
   if (hipSetDevice(ctx->device) != hipSuccess) return DCC_ENODEV;
   return ctx->occ_epoch(batch, out_rc, out_commit_tn, out_stats);
@@ -755,6 +773,7 @@ extern "C" int dcc_occ_validate_epoch(dcc_ctx* ctx, const dcc_batch* batch, uint
 extern "C" int dcc_occ_finish_epoch(dcc_ctx* ctx, const uint8_t* final_rc, uint64_t* out_commit_tn,
                                     uint32_t flags) {
   if (!ctx) return DCC_EINVAL;
+  dcc_pipe_drain(ctx);
   if (ctx->multi) {
     // every shard appends its own keys' writes; tn numbering is alike on all.
     // Every rank is checked first (allocations, the votes): a failure there

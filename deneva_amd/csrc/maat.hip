@@ -37,6 +37,7 @@
 #include "dcc.h"
 #include "dcc_ctx.h"
 #include "dcc_device.h"
+#include "dcc_env.h"
 #include "occ_kernels.h"
 #include "radix_sort.h"
 
@@ -459,90 +460,8 @@ __device__ inline void mt_load_tile(const uint8_t* sfl, const uint32_t* stx, uin
   __syncthreads();  // the caller may reuse L
 }
 
-__global__ __launch_bounds__(256) void k_mt_up(MtRoundArgs a) {
-  __shared__ Ms s[256];
-  __shared__ MtTileLds L;
-  const uint64_t base = (uint64_t)blockIdx.x * MT_TILE;
-  uint8_t f[MT_ITEMS];
-  uint32_t tx[MT_ITEMS];
-  mt_load_tile(a.sfl, a.stx, a.m, base, L, f, tx);
-  uint8_t st[MT_ITEMS];
-  uint64_t c[MT_ITEMS];
-#pragma unroll
-  for (uint32_t i = 0; i < MT_ITEMS; i++) {  // the gathers of a thread's group ends together
-    st[i] = (f[i] & F_LAST) ? a.state[tx[i]] : ST_ABO;
-    c[i] = 0;
-  }
-#pragma unroll
-  for (uint32_t i = 0; i < MT_ITEMS; i++)
-    if (st[i] == ST_COM) c[i] = a.cts[tx[i]];
-  Ms acc = ms_id();
-#pragma unroll
-  for (uint32_t i = 0; i < MT_ITEMS; i++) acc = ms_comb(acc, ms_elem(f[i], st[i], c[i]));
-  const Ms r = block_reduce_ms(acc, s);
-  if (threadIdx.x == 0) a.agg[blockIdx.x] = r;
-}
-
-__global__ __launch_bounds__(256) void k_mt_top(Ms* agg, uint32_t tiles) {
-  __shared__ Ms s[256];
-  __shared__ Ms s_last;
-  Ms carry = ms_id();
-  for (uint32_t c0 = 0; c0 < tiles; c0 += 256) {
-    const uint32_t i = c0 + threadIdx.x;
-    const Ms v = i < tiles ? agg[i] : ms_id();
-    const Ms ex = block_excl_ms(v, s);
-    if (i < tiles) agg[i] = ms_comb(carry, ex);
-    if (threadIdx.x == 255) s_last = ms_comb(ex, v);
-    __syncthreads();
-    carry = ms_comb(carry, s_last);
-    __syncthreads();
-  }
-}
-
-// exclusive prefix per position; every group's last position of an
-// undecided txn folds what the earlier txns of its row imply into the txn:
-// L from committed readers of a row it writes, U from committed writers of a
-// row it touches, pending from undecided ones
-__global__ __launch_bounds__(256) void k_mt_down(MtRoundArgs a) {
-  __shared__ Ms s[256];
-  __shared__ MtTileLds L;
-  const uint64_t base = (uint64_t)blockIdx.x * MT_TILE;
-  const uint64_t p0 = base + (uint64_t)threadIdx.x * MT_ITEMS;
-  uint8_t f[MT_ITEMS], st[MT_ITEMS];
-  uint32_t tx[MT_ITEMS];
-  uint64_t c[MT_ITEMS];
-  mt_load_tile(a.sfl, a.stx, a.m, base, L, f, tx);
-#pragma unroll
-  for (uint32_t i = 0; i < MT_ITEMS; i++) {
-    st[i] = (f[i] & F_LAST) ? a.state[tx[i]] : ST_ABO;
-    c[i] = 0;
-  }
-#pragma unroll
-  for (uint32_t i = 0; i < MT_ITEMS; i++)
-    if (st[i] == ST_COM) c[i] = a.cts[tx[i]];
-  Ms acc = ms_id();
-#pragma unroll
-  for (uint32_t i = 0; i < MT_ITEMS; i++) acc = ms_comb(acc, ms_elem(f[i], st[i], c[i]));
-  Ms run = ms_comb(a.agg[blockIdx.x], block_excl_ms(acc, s));
-#pragma unroll
-  for (uint32_t i = 0; i < MT_ITEMS; i++) {
-    const uint64_t p = p0 + i;
-    if (p >= a.m) break;
-    if (f[i] & F_START) run = Ms{1, 0, 0, U64MAX};  // own group excluded: contributions at its end
-    // a group that only scans / XPs its row is not on the row's soft locks
-    if ((f[i] & F_LAST) && (f[i] & (F_R | F_W)) && st[i] == ST_UND) {
-      const uint32_t t = tx[i];
-      if ((f[i] & F_W) && run.rmax) atomicMax((unsigned long long*)&a.lacc[t], run.rmax + 1);
-      if (run.wmin != U64MAX) atomicMin((unsigned long long*)&a.uacc[t], run.wmin - 1);
-      // a plain store: every writer of the word stores the same 1 (decide resets it)
-      if ((run.und & 2u) || ((f[i] & F_W) && (run.und & 1u))) a.pend[t] = 1u;
-    }
-    run = ms_comb(run, ms_elem(f[i] & ~F_START, st[i], c[i]));
-  }
-}
-
 // ---------------------------------------------------------------- fused round
-// k_mt_up + k_mt_top + k_mt_down in one launch (one read of each tile, no
+// The round scan in one launch (one read of each tile, no
 // aggregate pass): a single-pass scan with decoupled look-back.  Tile j
 // publishes its aggregate as soon as it has it, then wave 0 looks back 64
 // tiles at a time (lane 0 the nearest) until it meets a published inclusive
@@ -562,8 +481,17 @@ static_assert(sizeof(MtLb) == 64, "one line per tile");
 constexpr uint32_t MT_ERR_SPIN = 8;
 
 // Every field is written and read with device-scope atomics (coherent across
-// the XCDs' L2s without a cache write-back per tile); the payload's stores
-// complete (vmcnt) before the status store.
+// the XCDs' L2s without a cache write-back per tile).  The status word is the
+// flag of a message-passing pair, ordered by the hardware rather than by the
+// HIP memory model's release/acquire: the payload's agent-scope stores are
+// write-through (`sc1`) and `s_waitcnt vmcnt(0)` holds the status store until
+// each of them is acknowledged at the coherence point, and a reader issues its
+// payload loads (also `sc1`, read at that point) only after the status load
+// has returned the tag (the spin's branch depends on it).  The model's own
+// recipe -- a release store (`buffer_wbl2 sc1`, a write-back of the whole XCD
+// L2) per publish and an acquire load (`buffer_inv sc1`) per poll -- is what
+// the first version of this scan used, at 517-548 us per 16.7 M-position
+// round against 252 us.
 template <typename T>
 __device__ inline void st_dev(T* p, T v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1246,11 +1174,7 @@ int dcc_ctx::maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, 
   CR(cv_scratch.ensure(this, rs_scratch_words(mm) * 4 + 64, "radix scratch"));
   const uint64_t tiles = (m + MT_TILE - 1) / MT_TILE;
   CR(mt_agg.ensure(this, std::max<uint64_t>(1, tiles) * sizeof(Ms), "maat scan"));
-  if (mt_fused < 0) {
-    const char* e = getenv("DCC_MT_FUSED");
-    mt_fused = e ? (atoi(e) != 0) : 1;
-  }
-  if (mt_fused) {
+  {
     const void* old = mt_lb.p;
     CR(mt_lb.ensure(this, std::max<uint64_t>(1, tiles) * sizeof(MtLb), "maat look-back status"));
     if (mt_lb.p != old || mt_tag + 64 >= (1u << 30)) {  // fresh memory, or the tags wrap
@@ -1312,7 +1236,7 @@ int dcc_ctx::maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, 
   // ---- rounds: one, then MT_BATCH between host checks; after each check
   // the scan input is compacted to the groups that can still matter
   uint32_t rounds = 0;
-  const bool mt_debug = getenv("DCC_MT_DEBUG") != nullptr;
+  const bool mt_debug = DCC_ENV("DCC_MT_DEBUG") != nullptr;
   CR(mt_ul.ensure(this, 2 * n * 4 + 64, "maat undecided lists"));
   uint32_t* ul_buf[2] = {(uint32_t*)mt_ul.p, (uint32_t*)mt_ul.p + n};
   uint32_t* ulen_w = cnt + 5;  // two count words: cnt[5], cnt[6]
@@ -1333,26 +1257,22 @@ int dcc_ctx::maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, 
       // one round per host check while the scan is long (each check may
       // compact it), MT_BATCH once it is short
       static const uint32_t batch = [] {  // DCC_MT_BATCH / DCC_MT_LONG: tuning experiments
-        const char* e = getenv("DCC_MT_BATCH");
+        const char* e = DCC_ENV("DCC_MT_BATCH");
         return e && atoi(e) > 0 ? (uint32_t)atoi(e) : MT_BATCH;
       }();
       static const uint64_t long_scan = [] {
-        const char* e = getenv("DCC_MT_LONG");
+        const char* e = DCC_ENV("DCC_MT_LONG");
         return e && atoll(e) > 0 ? (uint64_t)atoll(e) : MT_LONG;
       }();
       const uint32_t nb = (rounds == 0 || mc > long_scan) ? 1u : batch;
       for (uint32_t q = 0; q < nb; q++, rounds++) {
         const uint32_t* prev = rounds > r0 ? &ring[(rounds - 1) % MT_RING] : nullptr;
-        if (mc && mt_fused) {
+        if (mc) {
           if (mt_tag + 1 >= (1u << 30)) {
             CK(hipMemsetAsync(mt_lb.p, 0, mt_lb.cap, stream));
             mt_tag = 0;
           }
           k_mt_round<<<(unsigned)tiles_c, 256, 0, stream>>>(ra, (MtLb*)mt_lb.p, ++mt_tag, cnt + 1, prev);
-        } else if (mc) {
-          k_mt_up<<<(unsigned)tiles_c, 256, 0, stream>>>(ra);
-          k_mt_top<<<1, 256, 0, stream>>>((Ms*)mt_agg.p, (uint32_t)tiles_c);
-          k_mt_down<<<(unsigned)tiles_c, 256, 0, stream>>>(ra);
         }
         k_mt_decide<<<g1(ulen_host, 2048), 256, 0, stream>>>(n, ul_cur, ulen_cur, base, state, cts, lacc,
                                                               uacc, pend, &ring[rounds % MT_RING],
@@ -1412,7 +1332,7 @@ int dcc_ctx::maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, 
 
   // the prefix level (DCC_MT_PREFIX txns, 0: off; epochs of > 4 prefixes)
   static const uint64_t prefix = [] {
-    const char* e = getenv("DCC_MT_PREFIX");
+    const char* e = DCC_ENV("DCC_MT_PREFIX");
     return e ? (uint64_t)atoll(e) : (uint64_t)MT_PREFIX;
   }();
   if (m && prefix && n > 4 * prefix) {

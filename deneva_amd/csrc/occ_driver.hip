@@ -16,6 +16,7 @@
 #include "dcc.h"
 #include "dcc_ctx.h"
 #include "dcc_device.h"
+#include "dcc_env.h"
 #include "occ_kernels.h"
 
 using namespace dcc;
@@ -279,7 +280,7 @@ static uint32_t sw_pmax(int level, bool split) {
   // DCC_SW_PMAX="p0,p1,...": per-level serial prefixes (tuning experiments)
   static const std::vector<uint32_t> ov = [] {
     std::vector<uint32_t> v;
-    if (const char* e = getenv("DCC_SW_PMAX"))
+    if (const char* e = DCC_ENV("DCC_SW_PMAX"))
       for (const char* c = e; *c;) {
         char* x;
         const unsigned long p = strtoul(c, &x, 10);
@@ -312,7 +313,7 @@ static uint32_t sw_budget(int level, bool split) { return 1u << (sw_budget_bits(
 // lost slot is one more dependent round trip for the whole workgroup
 static uint32_t sw_gbits(int level, bool split) {
   static const int ov = [] {
-    const char* c = getenv("DCC_SW_GBITS");
+    const char* c = DCC_ENV("DCC_SW_GBITS");
     return c ? atoi(c) : 0;
   }();
   uint32_t b = ov > 0 ? (uint32_t)ov : (level == 0 ? 18u : 19u);
@@ -322,7 +323,7 @@ static uint32_t sw_gbits(int level, bool split) {
 
 int dcc_ctx::sweep_reserve(const DevBatch& d) {
   const uint64_t tiles = SW_PMAX_TOP / SW_T;
-  sw_debug = getenv("DCC_SW_DEBUG") != nullptr;
+  sw_debug = DCC_ENV("DCC_SW_DEBUG") != nullptr;
   if (sw_debug) {
     CR(sw_dbg.ensure(this, (4096 + 4 * 256 * 8 + 4 * 64 * 8) * 8, "sweep debug"));
     dcc_ctx* ctx = this;
@@ -601,7 +602,11 @@ int dcc_ctx::fin_save(const DevBatch& d, bool host_batch, uint64_t nnz_w) {
   // buffers of the next call, and a multi-GPU rank's shard (a "device" batch
   // in this context's own sh_* buffers) is rewritten by the next epoch of any
   // kind (e.g. a Calvin epoch before dcc_occ_finish_epoch) -- copy both
-  const bool own = d.off == (const uint32_t*)sh_off.p || d.keys == (const uint64_t*)sh_keys.p;
+  // -- and so is a device batch in compact form, whose widened keys / access
+  // types sit in this context's staging buffers
+  const bool own = d.off == (const uint32_t*)sh_off.p || d.keys == (const uint64_t*)sh_keys.p ||
+                   d.off == (const uint32_t*)off.p || d.keys == (const uint64_t*)keys.p ||
+                   d.acctype == (const uint8_t*)acctype.p;
   if (host_batch || own) {
     CR(fin_off.ensure(this, (d.n + 1) * 4, "deferred finish offsets"));
     CR(fin_keys.ensure(this, std::max<uint64_t>(8, d.nnz * 8), "deferred finish keys"));
@@ -707,42 +712,62 @@ int dcc_ctx::sweep_ro(const DevBatch& d, bool big, bool scan, uint64_t nnz_w) {
 }
 
 int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dcc_stats* st) {
+  CR(occ_begin(b, out_rc, out_tn, false));
+  return occ_end(st);
+}
+
+static double wall_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+// First half of an epoch: checks, staging, and every launch up to the
+// finalize (or the captured graph's replay).  With `async` and a replayable
+// graph the call returns right after the graph launch (run.pending); occ_end
+// synchronises and reads the results back.
+int dcc_ctx::occ_begin(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, bool async) {
   dcc_ctx* ctx = this;
+  if (run.active) return fail(DCC_EINVAL, "an epoch of this context is still in flight");
+  run = OccRun{};
+  OccRun& r = run;
+  r.out_rc = out_rc;
+  r.out_tn = out_tn;
   // key-sharded across ranks: this rank holds only its keys
-  const bool sh = comm_ranks() > 1;
-  const auto t_wall0 = std::chrono::steady_clock::now();
+  r.sh = comm_ranks() > 1;
+  r.t_wall0 = wall_ms();
   // the one-GPU sweep validates a host batch's offsets on the device (its
   // level-0 launch, prep_body; every kernel before clamps its indices), so the
   // O(n) host pass is skipped there
-  CR(check_batch(b, !(use_sweep() && !sh)));
-  const bool dev_out = (b->flags & DCC_DEVICE_PTRS) != 0;
-  const bool defer = (b->flags & DCC_OCC_DEFER_FINISH) != 0;
+  CR(check_batch(b, !(use_sweep() && !r.sh)));
+  r.n_txn = b->n_txn;
+  r.flags = b->flags;
+  r.dev_out = (b->flags & DCC_DEVICE_PTRS) != 0;
+  r.defer = (b->flags & DCC_OCC_DEFER_FINISH) != 0;
   if (fin_pending)
     return fail(DCC_EINVAL, "an epoch validated with DCC_OCC_DEFER_FINISH awaits dcc_occ_finish_epoch");
-  if (defer && (out_tn || (b->flags & DCC_OCC_APPEND_HISTORY)))
+  if (r.defer && (out_tn || (b->flags & DCC_OCC_APPEND_HISTORY)))
     return fail(DCC_EINVAL, "DCC_OCC_DEFER_FINISH: commit tn and history come from dcc_occ_finish_epoch");
-  dcc_stats S;
-  memset(&S, 0, sizeof S);
-  S.n_shards = (uint32_t)comm_ranks();
+  r.S.n_shards = (uint32_t)comm_ranks();
   if (b->n_txn == 0) {
-    if (defer) {
+    if (r.defer) {
       fin_d = DevBatch{};
       fin_nnz_w = 0;
       fin_pending = true;
     }
-    if (st) *st = S;
+    r.active = true;
     return DCC_OK;
   }
-  DevBatch d;
+  DevBatch& d = r.d;
   CR(stage_batch(b, d));
-  const bool sweep = use_sweep();
+  r.sweep = use_sweep();
+  const bool sh = r.sh, sweep = r.sweep;
   ro_on = sweep && ro_split && !sh;
   if (sweep) CR(sweep_reserve(d));
   CR(state.ensure(this, d.n + 16, "state"));
   CR(hasw.ensure(this, d.n + 16, "hasw"));
   CR(rc.ensure(this, d.n + 16, "rc"));
-  const bool want_tn = out_tn != nullptr || (b->flags & DCC_OCC_APPEND_HISTORY);
-  if (want_tn) {
+  r.want_tn = out_tn != nullptr || (b->flags & DCC_OCC_APPEND_HISTORY);
+  if (r.want_tn) {
     CR(cflag.ensure(this, d.n * 4, "cflag"));
     CR(bsum.ensure(this, ((d.n + 1023) / 1024 + 1) * 8, "bsum"));
     CR(tn.ensure(this, d.n * 8, "tn"));
@@ -752,50 +777,45 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   // the ones it was captured with: one graph launch instead of ~30 kernel
   // launches, so the device never waits for the host between kernels.
   const bool hist_on = d.start_tn && hist_size() > 0;
-  const bool graph_ok = sweep && !profiling && !sw_debug && !want_tn && !hist_on && !sh &&
-                        !getenv("DCC_NO_GRAPH");
+  const bool graph_ok = sweep && !profiling && !sw_debug && !r.want_tn && !hist_on && !sh &&
+                        !DCC_ENV("DCC_NO_GRAPH");
   // levels per captured epoch (DCC_OPT_SWEEP_LEVELS; 0 = auto: 3 with the
   // read-only split, 4 without)
-  const uint32_t glv = sw_levels ? sw_levels : (ro_on ? 3u : 4u);
-  const GraphKey gkey{d.off, d.keys, d.acctype, d.n, d.nnz, out_rc, dev_out,
-                      glv | (ro_on ? 0x80u | (wt_bits << 8) : 0u),
-                      buf_gen};
-  bool replay = graph_ok && graph_exec && gkey == graph_key;
-  bool capturing = false;
+  r.glv = sw_levels ? sw_levels : (ro_on ? 3u : 4u);
+  r.gkey = GraphKey{d.off, d.keys, d.acctype, d.n, d.nnz, out_rc, r.dev_out,
+                    r.glv | (ro_on ? 0x80u | (wt_bits << 8) : 0u), buf_gen};
+  r.replay = graph_ok && graph_exec && r.gkey == graph_key;
   // a failure while capturing must still end the capture
   struct CaptureGuard {
     hipStream_t s;
     bool* on;
     ~CaptureGuard() {
       if (*on) {
+        *on = false;
         hipGraph_t g = nullptr;
         (void)hipStreamEndCapture(s, &g);
         if (g) (void)hipGraphDestroy(g);
         (void)hipGetLastError();
       }
     }
-  } capture_guard{stream, &capturing};
-  if (graph_ok && !replay) {
+  } capture_guard{stream, &r.capturing};
+  if (graph_ok && !r.replay) {
     if (graph_exec) {
       (void)hipGraphExecDestroy(graph_exec);
       graph_exec = nullptr;
     }
     CK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
-    capturing = true;
+    r.capturing = true;
   }
   // device clock starts with the batch resident (around the graph launch
   // when one is used: event timing of graph-internal records is unsupported)
-  if (!replay && !capturing) CK(hipEventRecord(ev0, stream));
+  if (!r.replay && !r.capturing) CK(hipEventRecord(ev0, stream));
 
   // ---- prep: validation, max length (tile width), write count (table size).
   // The sweep needs none of it up front (its kernels clamp every index): its
   // partials are read back with the epoch's one synchronisation.
-  uint32_t maxlen = 0;
-  uint64_t nnz_w = 0;
-  // the sweep's prep pass shares the fill launch below (its partials go
-  // straight to pinned memory; only the host reads them)
-  if (!sweep) CR(device_prep(d, maxlen, nnz_w));
-  if (!replay) {
+  if (!sweep) CR(device_prep(d, r.maxlen, r.nnz_w));
+  if (!r.replay) {
     // one launch: error word 0, the constant-one word 1, words 2..15, the
     // async pass count, the state bytes, and for the sweep its control block
     // and level-0 key table
@@ -833,81 +853,116 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   top.state = (uint8_t*)state.p;
   top.hasw = (uint8_t*)hasw.p;
   top.hasw_global = true;
-  top.w_bound = nnz_w;
-  uint32_t rounds = 0;
-  uint32_t handoffs = 0;  // sweep lists handed to the round solver
+  top.w_bound = r.nnz_w;
   bars_used = false;
-  PeelInfo info;
-  int next_level = 0;
-  int serial_tail = -1;  // level enqueued without its filter (sweep_enqueue tail_serial)
   if (sweep) {
     if (profiling) CK(hipEventRecord(pev[0], stream));
-    next_level = (int)std::min<uint32_t>(glv, SW_MAX_LEVEL - 1);
-    if (!sh && next_level >= 2) serial_tail = next_level - 1;
+    r.next_level = (int)std::min<uint32_t>(r.glv, SW_MAX_LEVEL - 1);
+    if (!sh && r.next_level >= 2) r.serial_tail = r.next_level - 1;
     if (sh) {
-      CR(sweep_sharded(d, next_level));
-    } else if (!replay) {
-      CR(sweep_enqueue(d, 0, next_level, nullptr, false, serial_tail >= 0));
+      CR(sweep_sharded(d, r.next_level));
+    } else if (!r.replay) {
+      CR(sweep_enqueue(d, 0, r.next_level, nullptr, false, r.serial_tail >= 0));
       if (ro_on) CR(sweep_ro(d, false, false, 0));
     }
   } else {
-    CR(occ_rounds(top, maxlen, profiling, rounds));
+    CR(occ_rounds(top, r.maxlen, profiling, r.rounds));
   }
   if (profiling) CK(hipEventRecord(pev[3], stream));
 
   // ---- finalize: RC bytes, counts, central_finish tn numbering
-  uint8_t* rc_dev = (dev_out && out_rc) ? out_rc : (uint8_t*)rc.p;
-  uint32_t* cf = want_tn ? (uint32_t*)cflag.p : nullptr;
-  uint64_t* tn_dev = want_tn ? ((dev_out && out_tn) ? out_tn : (uint64_t*)tn.p) : nullptr;
-  auto enqueue_final = [&]() -> int {
-    if (replay) {  // once: a second finalize (after more levels) runs directly
-      replay = false;
-      CK(hipEventRecord(ev0, stream));
-      CK(hipGraphLaunch(graph_exec, stream));
-      CK(hipEventRecord(ev1, stream));
-      CK(hipStreamSynchronize(stream));
-      return DCC_OK;
-    }
-    // everything the host reads back goes to pinned memory from k_final
-    // itself: its partials directly, the error words and the sweep's control
-    // block copied by its last workgroup (prep wrote its partials directly)
-    GatherArgs ga{};
-    auto job = [&](void* hdst_dev, const void* src, size_t bytes) {
-      ga.job[ga.n++] = CopyJob{(const uint32_t*)src, (uint32_t*)hdst_dev, (uint32_t)(bytes / 4)};
-    };
-    job(hmisc_dev, misc.p, 64);
-    job((char*)hmisc_dev + MISC_BARS, (char*)misc.p + MISC_BARS, CTR_RING * 16);
-    if (sweep) job((char*)hmisc_dev + SW_HCTL, sw_ctl.p, sw_ctl_bytes());
-    FinalArgs fa{d.n, (const uint8_t*)state.p, (const uint8_t*)hasw.p, rc_dev, cf,
-                 (FinalPart*)hpart_dev};
-    launch_final(fa, ga, stream);
-    if (want_tn) launch_commit_tn(cf, d.n, (uint64_t*)bsum.p, tnc, tn_dev, stream);
-    CK(hipGetLastError());
-    if (!capturing) CK(hipEventRecord(ev1, stream));
-    if (!dev_out) {
-      if (out_rc) CK(hipMemcpyAsync(out_rc, rc.p, d.n, hipMemcpyDeviceToHost, stream));
-      if (out_tn) CK(hipMemcpyAsync(out_tn, tn.p, d.n * 8, hipMemcpyDeviceToHost, stream));
-    }
-    if (capturing) {
-      capturing = false;
-      hipGraph_t g = nullptr;
-      CK(hipStreamEndCapture(stream, &g));
-      const hipError_t ie = hipGraphInstantiate(&graph_exec, g, nullptr, nullptr, 0);
-      (void)hipGraphDestroy(g);
-      if (ie != hipSuccess) {
-        graph_exec = nullptr;
-        return fail(DCC_EIO, "hipGraphInstantiate: %s", hipGetErrorString(ie));
-      }
-      graph_key = gkey;
-      CK(hipEventRecord(ev0, stream));
-      CK(hipGraphLaunch(graph_exec, stream));
-      CK(hipEventRecord(ev1, stream));
-    }
-    CK(hipStreamSynchronize(stream));
-    return DCC_OK;
-  };
-  CR(enqueue_final());
+  r.rc_dev = (r.dev_out && out_rc) ? out_rc : (uint8_t*)rc.p;
+  r.cf = r.want_tn ? (uint32_t*)cflag.p : nullptr;
+  r.tn_dev = r.want_tn ? ((r.dev_out && out_tn) ? out_tn : (uint64_t*)tn.p) : nullptr;
+  const bool go_async = async && r.replay;
+  CR(occ_final(go_async));
+  r.pending = go_async;
+  r.active = true;
+  return DCC_OK;
+}
 
+// The finalize launches of `run` (k_final, commit tn, read-back copies), the
+// end of a capture, or the replay of the captured graph; synchronises unless
+// `async` (a replay only).
+int dcc_ctx::occ_final(bool async) {
+  dcc_ctx* ctx = this;
+  OccRun& r = run;
+  const DevBatch& d = r.d;
+  if (r.replay) {  // once: a second finalize (after more levels) runs directly
+    r.replay = false;
+    CK(hipEventRecord(ev0, stream));
+    CK(hipGraphLaunch(graph_exec, stream));
+    CK(hipEventRecord(ev1, stream));
+    if (!async) CK(hipStreamSynchronize(stream));
+    return DCC_OK;
+  }
+  // everything the host reads back goes to pinned memory from k_final
+  // itself: its partials directly, the error words and the sweep's control
+  // block copied by its last workgroup (prep wrote its partials directly)
+  GatherArgs ga{};
+  auto job = [&](void* hdst_dev, const void* src, size_t bytes) {
+    ga.job[ga.n++] = CopyJob{(const uint32_t*)src, (uint32_t*)hdst_dev, (uint32_t)(bytes / 4)};
+  };
+  job(hmisc_dev, misc.p, 64);
+  job((char*)hmisc_dev + MISC_BARS, (char*)misc.p + MISC_BARS, CTR_RING * 16);
+  if (r.sweep) job((char*)hmisc_dev + SW_HCTL, sw_ctl.p, sw_ctl_bytes());
+  FinalArgs fa{d.n, (const uint8_t*)state.p, (const uint8_t*)hasw.p, r.rc_dev, r.cf,
+               (FinalPart*)hpart_dev};
+  launch_final(fa, ga, stream);
+  if (r.want_tn) launch_commit_tn(r.cf, d.n, (uint64_t*)bsum.p, tnc, r.tn_dev, stream);
+  CK(hipGetLastError());
+  if (!r.capturing) CK(hipEventRecord(ev1, stream));
+  if (!r.dev_out) {
+    if (r.out_rc) CK(hipMemcpyAsync(r.out_rc, rc.p, d.n, hipMemcpyDeviceToHost, stream));
+    if (r.out_tn) CK(hipMemcpyAsync(r.out_tn, tn.p, d.n * 8, hipMemcpyDeviceToHost, stream));
+  }
+  if (r.capturing) {
+    r.capturing = false;
+    hipGraph_t g = nullptr;
+    CK(hipStreamEndCapture(stream, &g));
+    const hipError_t ie = hipGraphInstantiate(&graph_exec, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (ie != hipSuccess) {
+      graph_exec = nullptr;
+      return fail(DCC_EIO, "hipGraphInstantiate: %s", hipGetErrorString(ie));
+    }
+    graph_key = r.gkey;
+    CK(hipEventRecord(ev0, stream));
+    CK(hipGraphLaunch(graph_exec, stream));
+    CK(hipEventRecord(ev1, stream));
+  }
+  CK(hipStreamSynchronize(stream));
+  return DCC_OK;
+}
+
+// Second half: waits for the epoch (when occ_begin returned early), reads the
+// results back, runs any further levels / hand-offs, and central_finish.
+int dcc_ctx::occ_end(dcc_stats* st) {
+  dcc_ctx* ctx = this;
+  OccRun& r = run;
+  if (!r.active) return fail(DCC_EINVAL, "no epoch of this context is in flight");
+  struct Inactive {
+    bool* a;
+    ~Inactive() { *a = false; }
+  } inactive{&r.active};
+  if (r.pending) {
+    r.pending = false;
+    CK(hipStreamSynchronize(stream));
+  }
+  dcc_stats& S = r.S;
+  if (r.n_txn == 0) {
+    if (st) *st = S;
+    return DCC_OK;
+  }
+  const DevBatch& d = r.d;
+  const bool sh = r.sh, sweep = r.sweep;
+  const uint32_t glv = r.glv;
+  uint32_t& maxlen = r.maxlen;
+  uint64_t& nnz_w = r.nnz_w;
+  uint32_t& rounds = r.rounds;
+  uint32_t& handoffs = r.handoffs;
+  int& next_level = r.next_level;
+  int& serial_tail = r.serial_tail;
   if (sweep) {
     // prep results: the batch is rejected exactly as device_prep would
     const PrepPart* pp = (const PrepPart*)((const char*)hpart + SW_PREP_OFF);
@@ -1011,7 +1066,7 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
     }
     if (again) {
       if (profiling) CK(hipEventRecord(pev[3], stream));
-      CR(enqueue_final());
+      CR(occ_final(false));
     }
     if (ro_fast_rerun) {
       // the rerun's table may have overflowed in turn (more commits than the
@@ -1021,10 +1076,11 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
       if (w[1]) {
         if (wt_bits < 24) wt_bits += 2;
         CR(sweep_ro(d, true, handoffs > 0, nnz_w));
-        CR(enqueue_final());
+        CR(occ_final(false));
       }
     }
     const SwLevel* hc = (const SwLevel*)((const char*)hmisc + SW_HCTL);
+#ifdef DCC_EXPERIMENTS
     if (sw_debug) {
       std::vector<uint64_t> dv(4096 + 4 * 256 * 8 + 4 * 64 * 8);
       CK(hipMemcpy(dv.data(), sw_dbg.p, dv.size() * 8, hipMemcpyDeviceToHost));
@@ -1087,8 +1143,9 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
                   nwc ? 0.01 * fw / nwc : 0, 0.01 * ft / nw);
       }
     }
-    info.prefix = hc[0].pos;
-    info.survivors = hc[1].m;
+#endif
+    r.info.prefix = hc[0].pos;
+    r.info.survivors = hc[1].m;
     for (int l = 0; l < next_level && (l == 0 || hc[l].m); l++) rounds++;
   }
 
@@ -1124,9 +1181,9 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
   S.nnz_w = nnz_w;
   S.alg_bytes = dcc_alg_bytes(d.n, d.nnz, nnz_w);
   S.device_ms = ms;
-  S.peel_prefix = info.prefix;
+  S.peel_prefix = r.info.prefix;
   S.fallback = handoffs;
-  S.n_survivors = info.survivors;
+  S.n_survivors = r.info.survivors;
   if (profiling) {
     float t0 = 0, t1 = 0, t2 = 0;
     if (sweep) {
@@ -1161,14 +1218,14 @@ int dcc_ctx::occ_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, dc
 
   // central_finish (occ.cpp:277-286): committed write sets join the history
   // -- or, deferred, with the global RC (dcc_occ_finish_epoch)
-  if (defer) {
-    CR(fin_save(d, !dev_out, nnz_w));
+  if (r.defer) {
+    CR(fin_save(d, !r.dev_out, nnz_w));
   } else {
-    if (b->flags & DCC_OCC_APPEND_HISTORY) CR(hist_append_epoch(d, tn_dev, nnz_w, n_cw));
+    if (r.flags & DCC_OCC_APPEND_HISTORY) CR(hist_append_epoch(d, r.tn_dev, nnz_w, n_cw));
     tnc += n_cw;
+    r.n_cw = n_cw;
   }
-  const auto t_wall1 = std::chrono::steady_clock::now();
-  S.total_ms = std::chrono::duration<double, std::milli>(t_wall1 - t_wall0).count();
+  S.total_ms = wall_ms() - r.t_wall0;
   if (st) *st = S;
   return DCC_OK;
 }

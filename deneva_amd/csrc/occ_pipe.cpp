@@ -1,0 +1,172 @@
+// Pipelined OCC epochs: dcc_occ_submit_epoch / dcc_occ_wait_epoch
+// (include/dcc.h).
+//
+// One headline epoch is a chain of ~20 dependent launches whose serial passes
+// run on one CU each: most of the chip idles through most of
+// the epoch.  Consecutive epochs of central_validate are independent under
+// TS_CLOCK (no history window; occ.cpp:160-180 never finds
+// an entry) except for the commit counter tnc (occ.cpp:283-284), so they can
+// share the chip: each lane is a full engine context on the same device (its
+// own stream, workspaces and captured graph), epoch k goes to lane k mod L,
+// and the epochs complete -- results read back, tnc advanced -- in submit
+// order.  An epoch that needs anything shared (commit tn, the history,
+// deferred finish) drains the lanes and runs on the parent context itself.
+#include <hip/hip_runtime.h>
+
+#include <deque>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "dcc.h"
+#include "dcc_ctx.h"
+
+struct OccPipe {
+  std::vector<dcc_ctx*> lanes;
+  struct Flight {
+    uint64_t ticket;
+    int lane;
+  };
+  std::deque<Flight> flight;  // submitted and not yet completed, submit order
+  struct Result {
+    int rc;
+    dcc_stats st;
+    std::string err;
+  };
+  std::unordered_map<uint64_t, Result> done;  // completed, not yet waited
+  uint64_t next = 1;
+  uint32_t next_lane = 0;
+  hipEvent_t ready = nullptr;  // the caller's stream, before an epoch's first lane launch
+};
+
+static void pipe_complete_front(dcc_ctx* ctx) {
+  OccPipe* p = ctx->pipe;
+  const OccPipe::Flight f = p->flight.front();
+  p->flight.pop_front();
+  dcc_ctx* lane = p->lanes[f.lane];
+  OccPipe::Result r{};
+  (void)hipSetDevice(lane->device);
+  r.rc = lane->occ_end(&r.st);
+  if (r.rc == DCC_OK) {
+    ctx->tnc += lane->run.n_cw;  // tnc advances in submit order (occ.cpp:283-284)
+  } else {
+    r.err = lane->last_error;
+  }
+  lane->tnc = 0;
+  p->done[f.ticket] = std::move(r);
+}
+
+// Complete every epoch in flight (results stay until waited).
+void dcc_pipe_drain(dcc_ctx* ctx) {
+  if (!ctx || !ctx->pipe) return;
+  while (!ctx->pipe->flight.empty()) pipe_complete_front(ctx);
+}
+
+void dcc_pipe_destroy(dcc_ctx* ctx) {
+  if (!ctx || !ctx->pipe) return;
+  dcc_pipe_drain(ctx);
+  for (dcc_ctx* l : ctx->pipe->lanes) dcc_destroy(l);
+  if (ctx->pipe->ready) (void)hipEventDestroy(ctx->pipe->ready);
+  delete ctx->pipe;
+  ctx->pipe = nullptr;
+}
+
+static int pipe_lanes(dcc_ctx* ctx) {
+  OccPipe* p = ctx->pipe;
+  const size_t want = ctx->pipe_lanes;
+  if (p->lanes.size() == want) return DCC_OK;
+  dcc_pipe_drain(ctx);
+  while (p->lanes.size() > want) {
+    dcc_destroy(p->lanes.back());
+    p->lanes.pop_back();
+  }
+  while (p->lanes.size() < want) {
+    dcc_ctx* l = nullptr;
+    const int e = dcc_init(&l, ctx->device);
+    if (e != DCC_OK) return ctx->fail(e, "pipeline lane on device %d: %s", ctx->device, dcc_strerror(e));
+    p->lanes.push_back(l);
+  }
+  p->next_lane = 0;
+  return DCC_OK;
+}
+
+// The parent's tuning knobs, at every submit (a lane's writer table keeps any
+// growth it needed after an overflow).
+static void lane_options(const dcc_ctx* ctx, dcc_ctx* l) {
+  l->solver = ctx->solver;
+  l->ro_split = ctx->ro_split;
+  l->wt_bits = std::max(l->wt_bits, ctx->wt_bits);
+  l->sw_levels = ctx->sw_levels;
+  l->recheck_max = ctx->recheck_max;
+  l->batch_max = ctx->batch_max;
+}
+
+extern "C" int dcc_occ_submit_epoch(dcc_ctx* ctx, const dcc_batch* b, uint8_t* out_rc,
+                                    uint64_t* out_tn, uint64_t* out_ticket) {
+  if (!ctx || !b || !out_ticket) return DCC_EINVAL;
+  if (hipSetDevice(ctx->device) != hipSuccess) return DCC_ENODEV;
+  if (!ctx->pipe) {
+    ctx->pipe = new OccPipe();
+    if (hipEventCreateWithFlags(&ctx->pipe->ready, hipEventDisableTiming) != hipSuccess) {
+      (void)hipGetLastError();
+      ctx->pipe->ready = nullptr;
+      return ctx->fail(DCC_EIO, "pipeline event");
+    }
+  }
+  OccPipe* p = ctx->pipe;
+  const uint64_t ticket = p->next;
+  const bool shared = out_tn || (b->flags & (DCC_OCC_APPEND_HISTORY | DCC_OCC_DEFER_FINISH)) ||
+                      (b->start_tn && ctx->hist_size() > 0) || ctx->fin_pending;
+  const bool lanes_ok = !ctx->multi && ctx->comm_ranks() <= 1 && !ctx->profiling &&
+                        ctx->use_sweep() && !shared && b->n_txn > 0;
+  if (!lanes_ok) {
+    // in submit order, on the parent context itself
+    dcc_pipe_drain(ctx);
+    OccPipe::Result r{};
+    r.rc = dcc_occ_validate_epoch(ctx, b, out_rc, out_tn, &r.st);
+    if (r.rc != DCC_OK) r.err = ctx->last_error;
+    p->next++;
+    p->done[ticket] = std::move(r);
+    *out_ticket = ticket;
+    return DCC_OK;
+  }
+  if (int e = pipe_lanes(ctx)) return e;
+  const int li = (int)(p->next_lane++ % p->lanes.size());
+  dcc_ctx* lane = p->lanes[li];
+  // the lane's previous epoch completes first (and every epoch before it)
+  while (lane->run.active && !p->flight.empty()) pipe_complete_front(ctx);
+  lane_options(ctx, lane);
+  // device batches may have been written on the caller's stream
+  if (hipEventRecord(p->ready, ctx->stream) != hipSuccess ||
+      hipStreamWaitEvent(lane->stream, p->ready, 0) != hipSuccess)
+    return ctx->hip_fail(hipGetLastError(), "pipeline stream ordering");
+  p->next++;
+  *out_ticket = ticket;
+  const int e = lane->occ_begin(b, out_rc, nullptr, true);
+  if (e != DCC_OK) {
+    OccPipe::Result r{};
+    r.rc = e;
+    r.err = lane->last_error;
+    p->done[ticket] = std::move(r);
+    return DCC_OK;
+  }
+  p->flight.push_back({ticket, li});
+  return DCC_OK;
+}
+
+extern "C" int dcc_occ_wait_epoch(dcc_ctx* ctx, uint64_t ticket, dcc_stats* st) {
+  if (!ctx) return DCC_EINVAL;
+  OccPipe* p = ctx->pipe;
+  if (!p || ticket == 0 || ticket >= p->next) return ctx->fail(DCC_EINVAL, "unknown epoch ticket %llu",
+                                                               (unsigned long long)ticket);
+  while (!p->done.count(ticket) && !p->flight.empty() && p->flight.front().ticket <= ticket)
+    pipe_complete_front(ctx);
+  auto it = p->done.find(ticket);
+  if (it == p->done.end())
+    return ctx->fail(DCC_EINVAL, "epoch ticket %llu was already waited", (unsigned long long)ticket);
+  const int rc = it->second.rc;
+  if (st) *st = it->second.st;
+  if (rc != DCC_OK) ctx->last_error = it->second.err;
+  p->done.erase(it);
+  return rc;
+}

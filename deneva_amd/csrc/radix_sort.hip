@@ -4,6 +4,7 @@
 #include <cstdlib>
 
 #include "dcc_device.h"
+#include "dcc_env.h"
 #include "radix_sort.h"
 
 namespace dcc {
@@ -258,7 +259,7 @@ static int radix_sort_impl(K* k[2], uint32_t* v[2], uint64_t m, uint32_t bits, u
                            hipStream_t st) {
   if (m <= 1 || bits == 0) return 0;
   static const bool small_on = [] {  // DCC_RS_SMALL=0: 8,192-pair tiles at every size (A/B)
-    const char* e = getenv("DCC_RS_SMALL");
+    const char* e = DCC_ENV("DCC_RS_SMALL");
     return !(e && e[0] == '0');
   }();
   if (small_on && m <= RS_SMALL) return radix_sort_run<K, RS_ITEMS_SMALL>(k, v, m, bits, scratch, st);

@@ -23,7 +23,7 @@ extern "C" int dcc_shard_filter(const dcc_batch* in, uint32_t rank, uint32_t nra
                                 uint32_t* out_offsets, uint64_t* out_keys, uint8_t* out_acctype,
                                 uint64_t* out_nnz) {
   if (!in || !out_offsets || !out_nnz || nranks == 0 || rank >= nranks) return DCC_EINVAL;
-  if (in->flags & DCC_DEVICE_PTRS) return DCC_EINVAL;
+  if (in->flags & (DCC_DEVICE_PTRS | DCC_COMPACT_FLAGS)) return DCC_EINVAL;  // full-width host batches
   if (in->nnz && (!in->keys || !in->acctype || !out_keys || !out_acctype)) return DCC_EINVAL;
   uint64_t w = 0;
   out_offsets[0] = 0;

@@ -43,6 +43,12 @@ def pack_acctype(at) -> np.ndarray:
     return (q[:, 0] | (q[:, 1] << 2) | (q[:, 2] << 4) | (q[:, 3] << 6)).astype(np.uint8)
 
 
+def _is_signed(a) -> bool:
+    """A signed numpy array.  Device (torch) tensors are exempt: torch holds
+    u32 row ids as int32 tensors, read bit for bit as DCC_KEYS_U32."""
+    return isinstance(a, np.ndarray) and a.dtype.kind == "i"
+
+
 def _is_device(a) -> bool:
     return a is not None and not isinstance(a, np.ndarray) and bool(getattr(a, "is_cuda", False))
 
@@ -84,11 +90,16 @@ class EpochBatch:
         b.flags = flags | (_abi.DEVICE_PTRS if self.on_device else 0)
         # compact transfer forms (dcc.h): 4-byte keys / timestamps, packed types
         if _itemsize(self.keys) == 4:
+            if _is_signed(self.keys):
+                raise TypeError("4-byte keys must be an unsigned dtype (DCC_KEYS_U32 row ids)")
             b.flags |= _abi.KEYS_U32
         if self.meta.get("acctype_2bit"):
             b.flags |= _abi.ACCTYPE_2BIT
-        if self.start_tn is not None and _itemsize(self.start_tn) == 4:
-            b.flags |= _abi.TN_U32
+        if self.start_tn is not None:
+            if self.finish_tn is None or _itemsize(self.start_tn) != _itemsize(self.finish_tn):
+                raise TypeError("start_tn and finish_tn must both be set, with the same dtype size")
+            if _itemsize(self.start_tn) == 4:
+                b.flags |= _abi.TN_U32
         return b
 
     def to_torch(self, device="cuda"):
@@ -230,6 +241,23 @@ class Engine:
         if defer_finish:
             self._fin_n = n
         return out_rc[:n], (out_tn[:n] if want_tn else None), st.as_dict()
+
+    def occ_submit_epoch(self, batch: EpochBatch, out_rc, out_tn=None) -> int:
+        """Enqueue an epoch on the pipeline (dcc_occ_submit_epoch) and return
+        its ticket; the batch arrays and outputs must stay alive and unchanged
+        until ``occ_wait_epoch(ticket)``.  Results equal dcc_occ_validate_epoch
+        on the epochs in submit order."""
+        b = batch.to_c(0)
+        t = C.c_uint64(0)
+        _check(lib.dcc_occ_submit_epoch(self._h, C.byref(b), _ptr(out_rc), _ptr(out_tn),
+                                        C.byref(t)), self._h)
+        return int(t.value)
+
+    def occ_wait_epoch(self, ticket: int) -> dict:
+        """Complete every epoch up to `ticket` (submit order); that epoch's stats."""
+        st = _abi.Stats()
+        _check(lib.dcc_occ_wait_epoch(self._h, ticket, C.byref(st)), self._h)
+        return st.as_dict()
 
     @property
     def pending_finish(self) -> Optional[int]:
@@ -608,8 +636,12 @@ def write_batch_file(path: str, batch: EpochBatch, kind: int = _abi.FILE_OCC, rc
 
     def c(a, dt):
         return None if a is None else np.ascontiguousarray(a, dt)
+    at = np.asarray(batch.acctype)
+    if batch.meta.get("acctype_2bit"):  # the compact transfer form: unpack to one byte per access
+        nnz = int(np.asarray(batch.keys).shape[0])
+        at = ((np.repeat(at.astype(np.uint8), 4) >> np.tile(np.array([0, 2, 4, 6], np.uint8), at.size)) & 3)[:nnz]
     host = EpochBatch(c(batch.offsets, np.uint32), c(batch.keys, np.uint64),
-                      c(batch.acctype, np.uint8), c(batch.start_tn, np.uint64),
+                      c(at, np.uint8), c(batch.start_tn, np.uint64),
                       c(batch.finish_tn, np.uint64), c(batch.order, np.uint64))
     arrs = [c(rc, np.uint8), c(commit_tn, np.uint64), c(group, np.uint32), c(wave, np.uint32)]
     b = host.to_c()

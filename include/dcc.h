@@ -182,6 +182,14 @@ int dcc_set_profiling(dcc_ctx* ctx, int enable);
 #define DCC_OPT_FAIL_RANK 8   /* fault injection (tests): rank `value` of a multi-GPU context
                                  fails its next epoch before its first exchange; the other
                                  ranks must return DCC_ECOMM instead of waiting for it      */
+#define DCC_OPT_PIPELINE 11   /* lanes of dcc_occ_submit_epoch: epochs in flight at once
+                                 (1..4, default 3).  Each lane is a HIP stream that needs a
+                                 hardware queue of its own: run with GPU_MAX_HW_QUEUES >=
+                                 lanes + the caller's streams (HIP's default of 4 makes
+                                 lanes share queues, which serialises them)                 */
+#define DCC_OPT_CALVIN_PATH 12 /* Calvin grant groups: 0 auto (the bucket path for epochs of
+                                  >= 2M requests it applies to), 1 the global key sort + scan,
+                                  2 the bucket path wherever it applies                       */
 int dcc_set_option(dcc_ctx* ctx, int option, int64_t value);
 /* Pre-size device workspaces so a later call performs no allocation. */
 int dcc_reserve(dcc_ctx* ctx, uint64_t max_txn, uint64_t max_nnz);
@@ -232,6 +240,33 @@ int dcc_shard_filter(const dcc_batch* in, uint32_t rank, uint32_t nranks,
  *                      (tnc++ / wset->tn = tnc, occ.cpp:283-284); may be NULL. */
 int dcc_occ_validate_epoch(dcc_ctx* ctx, const dcc_batch* batch, uint8_t* out_rc,
                            uint64_t* out_commit_tn, dcc_stats* out_stats);
+/* (Any entry point: when a call returns an error, the contents of its output
+ * arrays are unspecified -- e.g. a malformed host batch, whose offsets the
+ * device checks, may already have been decided into out_rc.) */
+/* Pipelined epochs (one GPU).  dcc_occ_submit_epoch enqueues an epoch and
+ * returns without waiting for it.  Consecutive epochs run on separate lanes
+ * (DCC_OPT_PIPELINE of them, each with its own stream, workspaces and
+ * captured graph), so one epoch's latency-bound serial passes overlap the
+ * next epoch's streaming passes.  The results are exactly those of calling
+ * dcc_occ_validate_epoch on the epochs in submit order: under TS_CLOCK (no
+ * history window) epochs of central_validate are
+ * independent except for the commit counter tnc, which advances in submit
+ * order.  An epoch that needs more -- commit tn (out_commit_tn),
+ * DCC_OCC_APPEND_HISTORY, a window against a non-empty history,
+ * DCC_OCC_DEFER_FINISH, profiling, the round solver, or a multi-GPU or
+ * key-sharded context -- first drains the pipeline and then runs
+ * synchronously, still in submit order.  The batch arrays and the outputs
+ * must stay valid and unchanged until the epoch's dcc_occ_wait_epoch
+ * returns.  *out_ticket (1, 2, ...) names the epoch.  Argument errors are
+ * returned by submit; the epoch's own result by wait.
+ * dcc_occ_wait_epoch completes, in submit order, every epoch up to `ticket`
+ * and returns that epoch's status and stats.  Each ticket is waited once;
+ * earlier tickets keep their results until they are waited.  Every other
+ * OCC entry point on the context (validate, finish, history, tnc) first
+ * completes the epochs in flight. */
+int dcc_occ_submit_epoch(dcc_ctx* ctx, const dcc_batch* batch, uint8_t* out_rc,
+                         uint64_t* out_commit_tn, uint64_t* out_ticket);
+int dcc_occ_wait_epoch(dcc_ctx* ctx, uint64_t ticket, dcc_stats* out_stats);
 /* central_finish with the global decision, for an epoch validated with
  * DCC_OCC_DEFER_FINISH (each node votes with its local RC; 2PC's coordinator
  * commits only if every participant voted RCOK, worker_thread.cpp:328-334,

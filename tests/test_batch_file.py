@@ -106,3 +106,43 @@ def test_golden_fixture_file():
     b, meta, dec = d.read_batch_file(p)
     rc, tn, _ = orc.occ(b, literal=True)
     assert np.array_equal(rc, dec["rc"]) and np.array_equal(tn, dec["commit_tn"])
+
+
+def test_compact_forms(tmp_path):
+    """A batch in the compact transfer form (u32 keys, 2-bit access types,
+    u32 timestamps: dcc.h DCC_KEYS_U32 / ACCTYPE_2BIT / TN_U32) is written
+    full width by write_batch_file; the C writer and the host shard filter
+    refuse compact flags instead of misreading the narrow arrays."""
+    import ctypes as C
+    from deneva_amd import _abi
+    b = d.gen_ycsb(n_txn=777, zipf_theta=0.9, seed=11)
+    b.start_tn = np.arange(b.n_txn, dtype=np.uint64)
+    b.finish_tn = b.start_tn + 3
+    cb = d.EpochBatch(np.asarray(b.offsets, np.uint32), np.asarray(b.keys, np.uint32),
+                      d.engine.pack_acctype(b.acctype), b.start_tn.astype(np.uint32),
+                      b.finish_tn.astype(np.uint32), meta={"acctype_2bit": True})
+    p = str(tmp_path / "c.dccb")
+    d.write_batch_file(p, cb)
+    b2, _, _ = d.read_batch_file(p)
+    for f in ("offsets", "keys", "acctype", "start_tn", "finish_tn"):
+        assert np.array_equal(np.asarray(getattr(b, f)), getattr(b2, f)), f
+    raw = cb.to_c()
+    assert raw.flags & _abi.KEYS_U32 and raw.flags & _abi.ACCTYPE_2BIT and raw.flags & _abi.TN_U32
+    info = _abi.FileInfo(kind=FILE_OCC)
+    assert _abi.lib.dcc_file_write(p.encode(), C.byref(info), C.byref(raw), None, None, None,
+                                   None) == _abi.DCC_EINVAL
+    off = np.empty(b.n_txn + 1, np.uint32)
+    keys = np.empty(b.nnz, np.uint64)
+    at = np.empty(b.nnz, np.uint8)
+    w = C.c_uint64()
+    assert _abi.lib.dcc_shard_filter(C.byref(raw), 0, 2, off.ctypes.data, keys.ctypes.data,
+                                     at.ctypes.data, C.byref(w)) == _abi.DCC_EINVAL
+
+
+def test_to_c_rejects_ambiguous_dtypes():
+    b = d.gen_ycsb(n_txn=50, zipf_theta=0.9, seed=12)
+    with pytest.raises(TypeError):  # signed 4-byte keys are not row ids
+        d.EpochBatch(b.offsets, np.asarray(b.keys, np.int32), b.acctype).to_c()
+    with pytest.raises(TypeError):  # mixed timestamp widths
+        d.EpochBatch(b.offsets, b.keys, b.acctype, np.zeros(50, np.uint32),
+                     np.zeros(50, np.uint64)).to_c()

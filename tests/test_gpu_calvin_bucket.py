@@ -3,7 +3,7 @@ partition of the sequence-order requests into key buckets, then per bucket an
 LDS sort + grant-group scan with each row's state carried from chunk to chunk,
 and the windowed group write-out with readiness) against the oracle
 (`orc.calvin`, the Row_lock CALVIN replay restated: row_lock.cpp:78-81,
-152-170, 317-357).  DCC_CV_BUCKET=1 takes the path at every size it applies
+152-170, 317-357).  DCC_OPT_CALVIN_PATH=2 takes the path at every size it applies
 to (uniform txn lengths <= 64, packed keys <= 24 bits); the cases cover one-row
 buckets, a single key, duplicates of a row inside a txn (also where a txn
 straddles a chunk boundary), hot rows spanning many chunks, sequencer orders
@@ -20,8 +20,10 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture
-def bucket(monkeypatch):
-    monkeypatch.setenv("DCC_CV_BUCKET", "1")
+def bucket(engine):
+    engine.set_option(d._abi.OPT_CALVIN_PATH, 2)
+    yield
+    engine.set_option(d._abi.OPT_CALVIN_PATH, 0)
 
 
 def uniform_batch(rng, n, L, n_keys, p_write=0.5, types=None, order=False, zipf=None):
@@ -114,14 +116,20 @@ def test_wide_keys_fall_back(engine, bucket):
     check(engine, uniform_batch(rng, 5000, 16, 1 << 30, order=True))
 
 
-def test_paths_agree_c4(engine, monkeypatch):
+def test_paths_agree_c4(engine):
     # C4 (1,048,576 x 16): the bucket path (the default at this size) and the
     # global sort + scan produce the same groups and readiness
     b = c4_batch()
-    monkeypatch.setenv("DCC_CV_BUCKET", "0")
-    g0, rc0, _, _ = engine.calvin_order_epoch(b, want_group=True)
-    monkeypatch.setenv("DCC_CV_BUCKET", "1")
-    g1, rc1, _, _ = engine.calvin_order_epoch(b, want_group=True)
+    engine.set_option(d._abi.OPT_CALVIN_PATH, 1)
+    try:
+        g0, rc0, _, _ = engine.calvin_order_epoch(b, want_group=True)
+    finally:
+        engine.set_option(d._abi.OPT_CALVIN_PATH, 0)
+    engine.set_option(d._abi.OPT_CALVIN_PATH, 2)
+    try:
+        g1, rc1, _, _ = engine.calvin_order_epoch(b, want_group=True)
+    finally:
+        engine.set_option(d._abi.OPT_CALVIN_PATH, 0)
     assert np.array_equal(np.asarray(g0), np.asarray(g1))
     assert np.array_equal(np.asarray(rc0), np.asarray(rc1))
 

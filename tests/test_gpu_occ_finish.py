@@ -214,3 +214,33 @@ def test_sharded_device_batch_calvin_between(eng):
         rc2, _, _ = m.occ_validate_epoch(b2)
         erc2, _, _ = orc.occ(b2, hist_keys=hk, hist_tn=ht, tnc=etnc)
         assert np.array_equal(np.asarray(rc2), erc2)
+
+
+def test_compact_device_batch_calvin_between(eng):
+    # a DEVICE batch in the compact form (u32 keys, 2-bit types): its widened
+    # keys / types live in the context's staging buffers, which a Calvin
+    # epoch between the deferred validate and the finish rewrites -- the
+    # finish must append the validated epoch's writes (kept aside), not the
+    # Calvin batch's
+    import torch
+    from deneva_amd.engine import pack_acctype
+    rng = np.random.default_rng(31)
+    b = d.gen_ycsb(n_txn=30000, zipf_theta=0.9, table_size=1 << 16, seed=31)
+    keys = torch.from_numpy(np.asarray(b.keys, np.uint32).view(np.int32)).cuda()
+    at = torch.from_numpy(pack_acctype(b.acctype)).cuda()
+    off = torch.from_numpy(np.asarray(b.offsets, np.uint32).view(np.int32)).cuda()
+    db = d.EpochBatch(off, keys, at, meta={"acctype_2bit": True})
+    rc, _, _ = eng.occ_validate_epoch(db, defer_finish=True)
+    torch.cuda.synchronize()
+    rc = rc.cpu().numpy()
+    assert np.array_equal(rc, orc.occ(b)[0])
+    c = d.gen_ycsb(n_txn=40000, zipf_theta=0.9, part_cnt=4, chunk_txns=4096, seed=78)
+    g, _, _, _ = eng.calvin_order_epoch(c, want_group=True)  # host batch: the same staging buffers
+    assert np.array_equal(np.asarray(g).astype(np.uint32), orc.calvin(c)[0])
+    gl = global_rc(rc, rng, 0.2)
+    tn = eng.occ_finish_epoch(gl)
+    etn, hk, ht, etnc = expected_finish(b, gl, 0)
+    assert np.array_equal(np.asarray(tn).astype(np.uint64), etn) and eng.tnc == etnc
+    k, t = eng.history_export()
+    order = np.lexsort((ht, hk))
+    assert np.array_equal(np.asarray(k), hk[order]) and np.array_equal(np.asarray(t), ht[order])

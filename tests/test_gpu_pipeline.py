@@ -1,0 +1,147 @@
+"""GPU parity of pipelined epochs (dcc_occ_submit_epoch / dcc_occ_wait_epoch,
+occ_pipe.cpp): consecutive epochs run on separate lanes of one GPU and must
+decide exactly what dcc_occ_validate_epoch decides on them one after another
+in submit order -- central_validate per epoch (occ.cpp:116-239), with the
+commit counter tnc (occ.cpp:283-284) advancing in submit order.
+
+Cases: 2, 3 and 4 lanes over distinct device batches (graph-replayed after
+each lane's first epoch), host batches, out-of-order waits, an epoch asking
+for commit tn in the middle of the stream (it drains the lanes and numbers
+from the tnc of every epoch before it), a malformed batch (its error comes
+back from its own wait; the others are unaffected), the synchronous entry
+point draining the lanes first, and every epoch of a full-size (1M) stream
+checked against the oracle."""
+import numpy as np
+import pytest
+
+import _oracle as orc
+import deneva_amd as d
+from deneva_amd._abi import OPT_PIPELINE, DccError
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def eng(engine):
+    engine.tnc = 0
+    yield engine
+    engine.set_option(OPT_PIPELINE, 2)
+    engine.tnc = 0
+
+
+def batches(n, count, theta=0.9, seed=0x51DE):
+    return [d.gen_ycsb(n_txn=n, zipf_theta=theta, seed=seed + i) for i in range(count)]
+
+
+def expected(bs, tnc=0):
+    out = []
+    for b in bs:
+        rc, tn, tnc = orc.occ(b, tnc=tnc)
+        out.append((rc, tn, tnc))
+    return out
+
+
+@pytest.mark.parametrize("lanes", [1, 2, 3, 4])
+def test_device_stream_matches_serial(eng, lanes):
+    import torch
+    eng.set_option(OPT_PIPELINE, lanes)
+    bs = batches(65536, 7)
+    exp = expected(bs)
+    dbs = [b.to_torch("cuda:0") for b in bs]
+    outs = [torch.empty(b.n_txn, dtype=torch.uint8, device="cuda:0") for b in bs]
+    # twice over the same buffers: the second pass replays every lane's graph
+    for rep in range(2):
+        eng.tnc = 0
+        ts = [eng.occ_submit_epoch(db, o) for db, o in zip(dbs, outs)]
+        sts = [eng.occ_wait_epoch(t) for t in ts]
+        for i, (o, (erc, _, _)) in enumerate(zip(outs, exp)):
+            assert np.array_equal(o.cpu().numpy(), erc), f"epoch {i}, pass {rep}"
+            assert sts[i]["n_commit"] == int(np.count_nonzero(erc == d.RC_RCOK))
+        assert eng.tnc == exp[-1][2]
+
+
+def test_host_batches_and_out_of_order_waits(eng):
+    eng.set_option(OPT_PIPELINE, 3)
+    bs = batches(20000, 5, seed=0x77)
+    exp = expected(bs)
+    outs = [np.full(b.n_txn, 0xEE, np.uint8) for b in bs]
+    ts = [eng.occ_submit_epoch(b, o) for b, o in zip(bs, outs)]
+    order = [3, 0, 4, 2, 1]
+    for k in order:
+        eng.occ_wait_epoch(ts[k])
+    for i, (o, (erc, _, _)) in enumerate(zip(outs, exp)):
+        assert np.array_equal(o, erc), f"epoch {i}"
+    with pytest.raises(DccError):
+        eng.occ_wait_epoch(ts[0])  # each ticket is waited once
+    assert eng.tnc == exp[-1][2]
+
+
+def test_commit_tn_epoch_drains_and_numbers_in_order(eng):
+    import torch
+    eng.set_option(OPT_PIPELINE, 2)
+    bs = batches(30000, 5, seed=0x99)
+    exp = expected(bs)
+    dbs = [b.to_torch("cuda:0") for b in bs]
+    outs = [torch.empty(b.n_txn, dtype=torch.uint8, device="cuda:0") for b in bs]
+    tn2 = torch.empty(bs[2].n_txn, dtype=torch.int64, device="cuda:0")
+    ts = []
+    for i, (db, o) in enumerate(zip(dbs, outs)):
+        ts.append(eng.occ_submit_epoch(db, o, tn2 if i == 2 else None))
+    for t in ts:
+        eng.occ_wait_epoch(t)
+    for i, (o, (erc, _, _)) in enumerate(zip(outs, exp)):
+        assert np.array_equal(o.cpu().numpy(), erc), f"epoch {i}"
+    assert np.array_equal(tn2.cpu().numpy().astype(np.uint64), exp[2][1])
+    assert eng.tnc == exp[-1][2]
+
+
+def test_malformed_epoch_reports_at_its_wait(eng):
+    eng.set_option(OPT_PIPELINE, 2)
+    bs = batches(10000, 3, seed=0x31)
+    exp = expected([bs[0], bs[2]])
+    bad = d.EpochBatch(bs[1].offsets.copy(), bs[1].keys, bs[1].acctype)
+    bad.offsets[100] = bad.offsets[101] + 1  # offsets decrease
+    outs = [np.zeros(b.n_txn, np.uint8) for b in bs]
+    ts = [eng.occ_submit_epoch(b, o) for b, o in zip([bs[0], bad, bs[2]], outs)]
+    eng.occ_wait_epoch(ts[0])
+    with pytest.raises(DccError):
+        eng.occ_wait_epoch(ts[1])
+    eng.occ_wait_epoch(ts[2])
+    assert np.array_equal(outs[0], exp[0][0])
+    assert np.array_equal(outs[2], exp[1][0])
+
+
+def test_sync_call_drains_first(eng):
+    import torch
+    eng.set_option(OPT_PIPELINE, 2)
+    bs = batches(40000, 3, seed=0x45)
+    exp = expected(bs)
+    dbs = [b.to_torch("cuda:0") for b in bs]
+    outs = [torch.empty(b.n_txn, dtype=torch.uint8, device="cuda:0") for b in bs]
+    t0 = eng.occ_submit_epoch(dbs[0], outs[0])
+    t1 = eng.occ_submit_epoch(dbs[1], outs[1])
+    rc, tn, _ = eng.occ_validate_epoch(dbs[2], want_tn=True, out_rc=outs[2])
+    assert np.array_equal(tn.cpu().numpy().astype(np.uint64), exp[2][1])
+    eng.occ_wait_epoch(t1)
+    eng.occ_wait_epoch(t0)
+    for i, (o, (erc, _, _)) in enumerate(zip(outs, exp)):
+        assert np.array_equal(o.cpu().numpy(), erc), f"epoch {i}"
+
+
+def test_full_size_stream(eng):
+    """The bench's pipelined headline: 1M-txn theta=0.9 epochs on 3 lanes,
+    every epoch in flight checked."""
+    import torch
+    eng.set_option(OPT_PIPELINE, 3)
+    bs = batches(1 << 20, 3, seed=0xD3E7A001)
+    exp = expected(bs)
+    dbs = [b.to_torch("cuda:0") for b in bs]
+    outs = [torch.empty(b.n_txn, dtype=torch.uint8, device="cuda:0") for b in bs]
+    for rep in range(3):
+        eng.tnc = 0
+        ts = [eng.occ_submit_epoch(db, o) for db, o in zip(dbs, outs)]
+        for t in ts:
+            eng.occ_wait_epoch(t)
+        for i, (o, (erc, _, _)) in enumerate(zip(outs, exp)):
+            assert np.array_equal(o.cpu().numpy(), erc), f"epoch {i}, pass {rep}"
+        assert eng.tnc == exp[-1][2]
