@@ -105,9 +105,12 @@ struct dcc_ctx {
     bool dev_out;
     uint32_t levels;
     uint64_t gen;
+    const void *start_tn, *finish_tn, *out_tn;
+    uint32_t fin;  // want tn | append << 1 | window check << 2
     bool operator==(const GraphKey& o) const {
       return off == o.off && keys == o.keys && acc == o.acc && n == o.n && nnz == o.nnz &&
-             out_rc == o.out_rc && dev_out == o.dev_out && levels == o.levels && gen == o.gen;
+             out_rc == o.out_rc && dev_out == o.dev_out && levels == o.levels && gen == o.gen &&
+             start_tn == o.start_tn && finish_tn == o.finish_tn && out_tn == o.out_tn && fin == o.fin;
     }
   };
   hipGraphExec_t graph_exec = nullptr;
@@ -126,6 +129,12 @@ struct dcc_ctx {
   uint64_t buf_gen = 0;
   void* hmisc_dev = nullptr;  // device-visible addresses of the two (k_gather targets)
   void* hpart_dev = nullptr;
+  // per-epoch values of a captured OCC epoch (dcc::OccDyn at offset 0, written
+  // by the host before each launch) and the central_finish totals (offset
+  // HDYN_TOTALS, written by the device); pinned
+  void* hdyn = nullptr;
+  void* hdyn_dev = nullptr;
+  static constexpr size_t HDYN_TOTALS = 128;
 
   // device workspaces (grow-only)
   DevBuf misc;                                   // counters / error words
@@ -135,6 +144,7 @@ struct dcc_ctx {
   DevBuf table;                                  // Slot[cap]
   DevBuf state, hasw, rc, stat;                  // per-txn bytes
   DevBuf cflag, bsum, tn;                        // commit-tn scan
+  DevBuf dyn, fin_part;                          // OccDyn (device copy), central_finish block counts
   DevBuf gst;                                    // sharded per-txn status
   DevBuf hasw_scr;                               // round-solver hand-off
   DevBuf sw_ctl, sw_status, sw_ckeys, sw_dbg;            // sweep solver: level control, look-back, C
@@ -210,6 +220,7 @@ struct dcc_ctx {
     uint64_t* out_tn = nullptr;
     DevBatch d;
     bool sh = false, dev_out = false, defer = false, sweep = false, want_tn = false;
+    bool app = false, hist_on = false;  // history append (central_finish) / window check
     bool replay = false, capturing = false, pending = false, active = false;
     uint32_t glv = 0, maxlen = 0, rounds = 0, handoffs = 0;
     uint64_t nnz_w = 0;

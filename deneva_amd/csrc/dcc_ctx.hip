@@ -136,6 +136,9 @@ extern "C" int dcc_init(dcc_ctx** out, int device_id) {
   CK(hipHostMalloc((void**)&ctx->hpart, 1 << 16, hipHostMallocDefault));
   CK(hipHostGetDevicePointer(&ctx->hmisc_dev, ctx->hmisc, 0));
   CK(hipHostGetDevicePointer(&ctx->hpart_dev, ctx->hpart, 0));
+  CK(hipHostMalloc((void**)&ctx->hdyn, 256, hipHostMallocDefault));
+  CK(hipHostGetDevicePointer(&ctx->hdyn_dev, ctx->hdyn, 0));
+  memset(ctx->hdyn, 0, 256);
   int rc = ctx->misc.ensure(ctx, 16384, "misc");
   if (!rc) rc = ctx->part.ensure(ctx, 1 << 16, "partials");
   // counters and barrier words start zeroed (hipMalloc memory is not)
@@ -162,6 +165,7 @@ extern "C" void dcc_destroy(dcc_ctx* ctx) {
   for (DevBuf* b : ctx->all_bufs()) b->release();
   if (ctx->hmisc) (void)hipHostFree(ctx->hmisc);
   if (ctx->hpart) (void)hipHostFree(ctx->hpart);
+  if (ctx->hdyn) (void)hipHostFree(ctx->hdyn);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   for (auto& e : ctx->pev)
@@ -187,7 +191,7 @@ extern "C" int dcc_set_option(dcc_ctx* ctx, int option, int64_t value) {
     return dcc_multi_set_fail_rank(ctx, (int)value);
   }
   if (option == DCC_OPT_PIPELINE) {
-    if (value < 1 || value > 4) return DCC_EINVAL;
+    if (value < 1 || value > 8) return DCC_EINVAL;
     dcc_pipe_destroy(ctx);  // lanes are re-created at the new count
     ctx->pipe_lanes = (uint32_t)value;
     return DCC_OK;
@@ -242,7 +246,7 @@ extern "C" int dcc_set_stream(dcc_ctx* ctx, void* s) {
 
 std::vector<DevBuf*> dcc_ctx::all_bufs() {
   std::vector<DevBuf*> v = {&misc, &part, &off, &keys, &acctype, &start_tn, &finish_tn, &table, &state,
-                            &hasw, &cflag, &bsum, &tn, &rc, &stat,
+                            &hasw, &cflag, &bsum, &tn, &rc, &stat, &dyn, &fin_part,
                             &order, &perm, &calvin_a, &calvin_b, &calvin_c, &calvin_d,
                             &cv_scratch, &cv_agg, &cv_group, &cv_wave, &cv_pgx, &cv_gsx,
                             &cv_gsize, &cv_done, &cv_maxl, &cv_seq_b, &cv_ok, &cv_len,

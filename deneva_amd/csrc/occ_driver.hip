@@ -767,23 +767,40 @@ int dcc_ctx::occ_begin(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, bo
   CR(hasw.ensure(this, d.n + 16, "hasw"));
   CR(rc.ensure(this, d.n + 16, "rc"));
   r.want_tn = out_tn != nullptr || (b->flags & DCC_OCC_APPEND_HISTORY);
+  r.app = (b->flags & DCC_OCC_APPEND_HISTORY) != 0;
   if (r.want_tn) {
     CR(cflag.ensure(this, d.n * 4, "cflag"));
-    CR(bsum.ensure(this, ((d.n + 1023) / 1024 + 1) * 8, "bsum"));
+    CR(fin_part.ensure(this, ((d.n + 1023) / 1024 + 1) * 24, "finish block counts"));
     CR(tn.ensure(this, d.n * 8, "tn"));
   }
-  // The sweep's whole launch sequence (prep ... gather) is replayed from a
-  // captured HIP graph when the batch, the outputs and every workspace are
-  // the ones it was captured with: one graph launch instead of ~30 kernel
-  // launches, so the device never waits for the host between kernels.
-  const bool hist_on = d.start_tn && hist_size() > 0;
-  const bool graph_ok = sweep && !profiling && !sw_debug && !r.want_tn && !hist_on && !sh &&
-                        !DCC_ENV("DCC_NO_GRAPH");
+  CR(dyn.ensure(this, sizeof(OccDyn), "epoch parameters"));
+  // the history the window check reads (merge / level builds: launched here,
+  // before any capture) and room for this epoch's append
+  r.hist_on = d.start_tn && hist_size() > 0;
+  if (r.hist_on) CR(hist_prepare());
+  if (r.app) CR(hist_grow_flat(hs[1], hs[1].m + d.nnz));
+  {
+    OccDyn& y = *(OccDyn*)hdyn;
+    y.tnc = tnc;
+    y.hist_m = hs[1].m;
+    y.app_k = r.app ? (uint64_t*)hs[1].fk.p : nullptr;
+    y.app_t = r.app ? (uint64_t*)hs[1].ft.p : nullptr;
+    y.view = hist_view();
+  }
+  // The sweep's whole launch sequence (parameters ... central_finish) is
+  // replayed from a captured HIP graph when the batch, the outputs and every
+  // workspace are the ones it was captured with: one graph launch instead of
+  // ~30 kernel launches, so the device never waits for the host between
+  // kernels.  tnc, the history and its append position change every epoch;
+  // the graph reads them from the epoch parameters (OccDyn).
+  const bool graph_ok = sweep && !profiling && !sw_debug && !sh && !DCC_ENV("DCC_NO_GRAPH");
   // levels per captured epoch (DCC_OPT_SWEEP_LEVELS; 0 = auto: 3 with the
   // read-only split, 4 without)
   r.glv = sw_levels ? sw_levels : (ro_on ? 3u : 4u);
   r.gkey = GraphKey{d.off, d.keys, d.acctype, d.n, d.nnz, out_rc, r.dev_out,
-                    r.glv | (ro_on ? 0x80u | (wt_bits << 8) : 0u), buf_gen};
+                    r.glv | (ro_on ? 0x80u | (wt_bits << 8) : 0u), buf_gen,
+                    d.start_tn, d.finish_tn, out_tn,
+                    (r.want_tn ? 1u : 0u) | (r.app ? 2u : 0u) | (r.hist_on ? 4u : 0u)};
   r.replay = graph_ok && graph_exec && r.gkey == graph_key;
   // a failure while capturing must still end the capture
   struct CaptureGuard {
@@ -825,6 +842,7 @@ int dcc_ctx::occ_begin(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, bo
     fa.job[fa.n++] = FillJob{mw + 1, 1, 1u};
     fa.job[fa.n++] = FillJob{mw + 2, 14, 0u};
     fa.job[fa.n++] = FillJob{(uint32_t*)state.p, (d.n + 3) / 4, 0u};  // state holds n + 16
+    fa.job[fa.n++] = FillJob{(uint32_t*)dyn.p, sizeof(OccDyn) / 4, 0u, (const uint32_t*)hdyn_dev};
     if (sweep) {
       fa.job[fa.n++] = FillJob{(uint32_t*)sw_ctl.p, sw_ctl_bytes() / 4, 0u};
       fa.job[fa.n++] = FillJob{(uint32_t*)sw_gtab.p, (1ull << sw_gbits(0, ro_on)) * 2, 0xFFFFFFFFu};
@@ -835,9 +853,8 @@ int dcc_ctx::occ_begin(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, bo
   }
 
   // ---- history window pre-pass (occ.cpp:160-180)
-  if (hist_on) {
-    CR(hist_prepare());
-    HistArgs ha{d.n, d.nnz, d.off, d.keys, d.acctype, d.start_tn, d.finish_tn, hist_view(),
+  if (r.hist_on && !r.replay) {
+    HistArgs ha{d.n, d.nnz, d.off, d.keys, d.acctype, d.start_tn, d.finish_tn, (const OccDyn*)dyn.p,
                 (uint8_t*)state.p, (uint32_t*)misc.p};
     launch_hist(ha, stream);
   }
@@ -909,7 +926,10 @@ int dcc_ctx::occ_final(bool async) {
   FinalArgs fa{d.n, (const uint8_t*)state.p, (const uint8_t*)hasw.p, r.rc_dev, r.cf,
                (FinalPart*)hpart_dev};
   launch_final(fa, ga, stream);
-  if (r.want_tn) launch_commit_tn(r.cf, d.n, (uint64_t*)bsum.p, tnc, r.tn_dev, stream);
+  if (r.want_tn)
+    launch_fin(OccFinArgs{d.n, d.nnz, r.cf, d.off, d.keys, d.acctype, (uint64_t*)fin_part.p,
+                       (const OccDyn*)dyn.p, r.tn_dev, (uint64_t*)((char*)hdyn_dev + HDYN_TOTALS)},
+               stream);
   CK(hipGetLastError());
   if (!r.capturing) CK(hipEventRecord(ev1, stream));
   if (!r.dev_out) {
@@ -1221,7 +1241,21 @@ int dcc_ctx::occ_end(dcc_stats* st) {
   if (r.defer) {
     CR(fin_save(d, !r.dev_out, nnz_w));
   } else {
-    if (r.flags & DCC_OCC_APPEND_HISTORY) CR(hist_append_epoch(d, r.tn_dev, nnz_w, n_cw));
+    if (r.want_tn) {
+      // central_finish ran on the device (k_fin_*): its totals
+      const uint64_t* tot = (const uint64_t*)((const char*)hdyn + HDYN_TOTALS);
+      if (tot[0] != n_cw)
+        return fail(DCC_EIO, "central_finish numbered %llu txns, %llu committed writers",
+                    (unsigned long long)tot[0], (unsigned long long)n_cw);
+      if (r.app && tot[1]) {
+        HistStore& D = hs[1];
+        if (tot[1] > d.nnz) return fail(DCC_EIO, "history append: %llu writes > %llu accesses",
+                                        (unsigned long long)tot[1], (unsigned long long)d.nnz);
+        D.m += tot[1];
+        D.max_key = std::max<uint64_t>(D.max_key, tot[2]);
+        hist_note(D, tnc + 1, tnc + n_cw);
+      }
+    }
     tnc += n_cw;
     r.n_cw = n_cw;
   }

@@ -96,6 +96,171 @@ __global__ __launch_bounds__(HB) void k_hist_emit(uint64_t n, const uint32_t* of
   if (threadIdx.x == 0 && s_mx) atomicMax(kmax, s_mx);  // one per workgroup
 }
 
+// ---------------------------------------------------------------------------
+// central_finish in three launches (OccFinArgs, occ_kernels.h).  Per 1024-txn
+// block: the committed writers (cflag) and, when appending, their writes and
+// largest key; one workgroup scans the block counts from dyn->tnc and
+// dyn->hist_m; then each committed writer takes its tn and emits its write set
+// at its position.  Only committed writers (a few per thousand under
+// contention) read their access lists.
+__device__ inline uint32_t fin_writes(uint64_t t, const OccFinArgs& a, uint64_t& o0, uint64_t& o1,
+                                      uint64_t& kmx) {
+  o0 = min((uint64_t)a.off[t], a.nnz);
+  o1 = min((uint64_t)a.off[t + 1], a.nnz);
+  if (o1 < o0) o1 = o0;
+  o1 = min(o1, o0 + MAX_TXN_LEN);
+  uint32_t c = 0;
+  for (uint64_t x = o0; x < o1; x++)
+    if (a.acctype[x] == DCC_WR) {
+      c++;
+      kmx = max(kmx, a.keys[x]);
+    }
+  return c;
+}
+
+// block-wide exclusive scans of two counters (1024 threads); returns both totals
+__device__ inline void block_excl_scan2(uint32_t v0, uint32_t v1, uint32_t& e0, uint32_t& e1,
+                                        uint32_t& t0, uint32_t& t1) {
+  __shared__ uint32_t s_w[2][HB / 64];
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t x0 = v0, x1 = v1;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y0 = __shfl_up(x0, d), y1 = __shfl_up(x1, d);
+    if (lane >= (uint32_t)d) {
+      x0 += y0;
+      x1 += y1;
+    }
+  }
+  if (lane == 63) {
+    s_w[0][w] = x0;
+    s_w[1][w] = x1;
+  }
+  __syncthreads();
+  uint32_t b0 = 0, b1 = 0;
+  t0 = t1 = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < HB / 64; q++) {
+    if (q < w) {
+      b0 += s_w[0][q];
+      b1 += s_w[1][q];
+    }
+    t0 += s_w[0][q];
+    t1 += s_w[1][q];
+  }
+  e0 = b0 + x0 - v0;
+  e1 = b1 + x1 - v1;
+}
+
+__global__ __launch_bounds__(HB) void k_fin_count(OccFinArgs a) {
+  __shared__ unsigned long long s_mx;
+  const uint64_t t = (uint64_t)blockIdx.x * HB + threadIdx.x;
+  const bool app = a.dyn->app_k != nullptr;
+  const uint32_t c = (t < a.n && a.cflag[t]) ? 1u : 0u;
+  uint64_t o0, o1, kmx = 0;
+  const uint32_t w = (c && app) ? fin_writes(t, a, o0, o1, kmx) : 0u;
+  if (threadIdx.x == 0) s_mx = 0;
+  uint32_t e0, e1, t0, t1;
+  block_excl_scan2(c, w, e0, e1, t0, t1);  // its barrier orders s_mx's reset
+  for (int d = 32; d > 0; d >>= 1) kmx = max(kmx, (uint64_t)__shfl_xor(kmx, d));
+  if ((threadIdx.x & 63) == 0 && kmx) atomicMax(&s_mx, (unsigned long long)kmx);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    a.part[3 * blockIdx.x] = t0;
+    a.part[3 * blockIdx.x + 1] = t1;
+    a.part[3 * blockIdx.x + 2] = s_mx;
+  }
+}
+
+// exclusive scans of the block counts from dyn->tnc / dyn->hist_m (one
+// workgroup, 1024 blocks per step), totals to pinned memory
+__global__ __launch_bounds__(1024) void k_fin_sums(OccFinArgs a, uint64_t nb) {
+  __shared__ uint64_t s_w[2][16];
+  __shared__ uint64_t s_carry[2];
+  __shared__ unsigned long long s_mx;
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (threadIdx.x == 0) {
+    s_carry[0] = a.dyn->tnc;
+    s_carry[1] = a.dyn->hist_m;
+    s_mx = 0;
+  }
+  __syncthreads();
+  const uint64_t c0_base = s_carry[0], c1_base = s_carry[1];
+  uint64_t mx = 0;
+  for (uint64_t c0 = 0; c0 < nb; c0 += 1024) {
+    const uint64_t q = c0 + threadIdx.x;
+    const uint64_t v0 = q < nb ? a.part[3 * q] : 0ull, v1 = q < nb ? a.part[3 * q + 1] : 0ull;
+    if (q < nb) mx = max(mx, a.part[3 * q + 2]);
+    uint64_t x0 = v0, x1 = v1;
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint64_t y0 = __shfl_up(x0, d), y1 = __shfl_up(x1, d);
+      if (lane >= (uint32_t)d) {
+        x0 += y0;
+        x1 += y1;
+      }
+    }
+    if (lane == 63) {
+      s_w[0][wv] = x0;
+      s_w[1][wv] = x1;
+    }
+    __syncthreads();
+    uint64_t b0 = s_carry[0], b1 = s_carry[1];
+    for (uint32_t w = 0; w < wv; w++) {
+      b0 += s_w[0][w];
+      b1 += s_w[1][w];
+    }
+    if (q < nb) {
+      a.part[3 * q] = b0 + x0 - v0;
+      a.part[3 * q + 1] = b1 + x1 - v1;
+    }
+    __syncthreads();
+    if (threadIdx.x == 1023) {
+      s_carry[0] = b0 + x0;
+      s_carry[1] = b1 + x1;
+    }
+    __syncthreads();
+  }
+  for (int d = 32; d > 0; d >>= 1) mx = max(mx, (uint64_t)__shfl_xor(mx, d));
+  if (lane == 0 && mx) atomicMax(&s_mx, (unsigned long long)mx);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    a.totals[0] = s_carry[0] - c0_base;
+    a.totals[1] = s_carry[1] - c1_base;
+    a.totals[2] = s_mx;
+  }
+}
+
+__global__ __launch_bounds__(HB) void k_fin_apply(OccFinArgs a) {
+  const uint64_t t = (uint64_t)blockIdx.x * HB + threadIdx.x;
+  uint64_t* app_k = a.dyn->app_k;
+  const uint32_t c = (t < a.n && a.cflag[t]) ? 1u : 0u;
+  uint64_t o0 = 0, o1 = 0, kmx = 0;
+  const uint32_t w = (c && app_k) ? fin_writes(t, a, o0, o1, kmx) : 0u;
+  uint32_t e0, e1, t0, t1;
+  block_excl_scan2(c, w, e0, e1, t0, t1);
+  if (t >= a.n) return;
+  const uint64_t my_tn = c ? a.part[3 * blockIdx.x] + e0 + 1 : 0;
+  a.tn[t] = my_tn;
+  if (w) {
+    uint64_t* app_t = a.dyn->app_t;
+    uint64_t p = a.part[3 * blockIdx.x + 1] + e1;
+    for (uint64_t x = o0; x < o1; x++)
+      if (a.acctype[x] == DCC_WR) {
+        app_k[p] = a.keys[x];
+        app_t[p] = my_tn;
+        p++;
+      }
+  }
+}
+
+void launch_fin(const OccFinArgs& a, hipStream_t st) {
+  const uint64_t nb = (a.n + HB - 1) / HB;
+  const unsigned g = (unsigned)(nb ? nb : 1);
+  k_fin_count<<<g, HB, 0, st>>>(a);
+  k_fin_sums<<<1, 1024, 0, st>>>(a, nb);
+  k_fin_apply<<<g, HB, 0, st>>>(a);
+}
+
 void launch_hist_count(uint64_t n, const uint32_t* off, const uint8_t* acctype, uint64_t nnz,
                        const uint64_t* tn, uint32_t* bsum, hipStream_t st) {
   const unsigned g = (unsigned)((n + HB - 1) / HB);

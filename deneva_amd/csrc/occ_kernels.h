@@ -45,6 +45,19 @@ struct TileOut {
   uint32_t og, bt, nt, be, ne;
 };
 
+// Per-epoch values a captured epoch graph reads when it runs -- the commit
+// counter, the delta level's append position and arrays, the history levels
+// of the window check -- so one graph serves every epoch of a shape: the
+// host writes them to pinned memory before each launch and the epoch's first
+// kernel (k_fill) copies them to device memory.
+struct OccDyn {
+  uint64_t tnc;     // commit counter before the epoch (occ.cpp:283-284)
+  uint64_t hist_m;  // pairs in the delta level before the epoch's append
+  uint64_t* app_k;  // delta level flat pairs (null: no append this epoch)
+  uint64_t* app_t;
+  HistView view;    // history levels (occ_history.h)
+};
+static_assert(sizeof(OccDyn) % 4 == 0, "copied as words");
 struct HistArgs {
   uint64_t n, nnz;
   const uint32_t* off;
@@ -52,7 +65,7 @@ struct HistArgs {
   const uint8_t* acctype;
   const uint64_t* start_tn;
   const uint64_t* finish_tn;
-  HistView hist;   // device history levels (occ_history.h)
+  const OccDyn* dyn;  // device history levels (dyn->view)
   uint8_t* state;
   uint32_t* err;   // ERR_OFFSETS on a malformed device batch
 };
@@ -427,6 +440,7 @@ struct FillJob {
   uint32_t* p;
   uint64_t words;
   uint32_t value;
+  const uint32_t* src = nullptr;  // copy `words` words from here instead of filling
 };
 struct FillArgs {
   FillJob job[12];
@@ -461,6 +475,24 @@ void launch_final(const FinalArgs& a, const GatherArgs& g, hipStream_t st);
 // clear it for the next round, add the undecided count to *und.
 void launch_decide(uint8_t* state, uint8_t* gst, uint64_t n, uint8_t abort_byte, uint32_t* und,
                    uint32_t* und_next, hipStream_t st);
+// central_finish of a decided epoch in three launches, every per-epoch value
+// read from `dyn` (graph-replayable): commit tn in index order for the txns
+// with cflag set (tn = dyn->tnc + 1, ...) and, when dyn->app_k is set, their
+// write sets appended to the delta level at dyn->hist_m in tn order
+// (occ.cpp:277-286).  totals (pinned): [0] committed writers, [1] pairs
+// appended, [2] largest key appended.
+struct OccFinArgs {
+  uint64_t n, nnz;
+  const uint32_t* cflag;
+  const uint32_t* off;
+  const uint64_t* keys;
+  const uint8_t* acctype;
+  uint64_t* part;      // [3 * blocks] scratch
+  const OccDyn* dyn;
+  uint64_t* tn;        // out: commit tn per txn (0 = none)
+  uint64_t* totals;    // out: pinned host memory
+};
+void launch_fin(const OccFinArgs& a, hipStream_t st);
 void launch_commit_tn(const uint32_t* cflag, uint64_t n, uint64_t* bsum, uint64_t tnc,
                       uint64_t* tn, hipStream_t st);
 // deferred central_finish: cflag[t] = global RCOK && local commit && has a

@@ -60,7 +60,7 @@ __global__ __launch_bounds__(256) void k_hist(HistArgs a) {
   }
   for (uint64_t x = o0; x < o1; x++) {
     if (a.acctype[x] == 1 /* WR */) continue;
-    if (hist_hit(a.hist, a.keys[x], s_tn, f_tn)) {
+    if (hist_hit(a.dyn->view, a.keys[x], s_tn, f_tn)) {
       a.state[t] = ST_ABORT;
       return;
     }
@@ -856,7 +856,10 @@ __global__ __launch_bounds__(256) void k_fill(FillArgs a) {
   const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x, stride = (uint64_t)gridDim.x * 256;
   for (uint32_t q = 0; q < a.n; q++) {
     const FillJob& f = a.job[q];
-    for (uint64_t i = t; i < f.words; i += stride) f.p[i] = f.value;
+    if (f.src)
+      for (uint64_t i = t; i < f.words; i += stride) f.p[i] = f.src[i];
+    else
+      for (uint64_t i = t; i < f.words; i += stride) f.p[i] = f.value;
   }
 }
 void launch_fill(const FillArgs& a, hipStream_t st) {

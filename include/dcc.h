@@ -183,7 +183,7 @@ int dcc_set_profiling(dcc_ctx* ctx, int enable);
                                  fails its next epoch before its first exchange; the other
                                  ranks must return DCC_ECOMM instead of waiting for it      */
 #define DCC_OPT_PIPELINE 11   /* lanes of dcc_occ_submit_epoch: epochs in flight at once
-                                 (1..4, default 3).  Each lane is a HIP stream that needs a
+                                 (1..8, default 3).  Each lane is a HIP stream that needs a
                                  hardware queue of its own: run with GPU_MAX_HW_QUEUES >=
                                  lanes + the caller's streams (HIP's default of 4 makes
                                  lanes share queues, which serialises them)                 */
