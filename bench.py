@@ -287,9 +287,16 @@ def occ_config(eng, dev, timed, orc, tag):
 
 
 def calvin_config(eng, dev, timed, orc, tag="C4"):
-    """C4: Calvin lock ordering, 16 partitions, 1M txns, sequencer order."""
+    """C4: Calvin lock ordering, 16 partitions, 1M txns, sequencer order.
+    C4 is the batch as the sequencers hand it over, origin by origin in FIFO
+    order (the order is non-decreasing in index order; the engine detects that
+    and skips its rank sort); C4_SHUF is the same txns captured with the 16
+    origins interleaved (txn i from origin i % 16), so the engine must rank
+    the order first."""
     import deneva_amd as d
     b = d.gen_ycsb(n_txn=1 << 20, zipf_theta=0.9, part_cnt=16, chunk_txns=65536, want_home=True)
+    if tag == "C4_SHUF":
+        b.meta["home"] = (np.arange(b.n_txn) % 16).astype(np.uint32)
     b.order = c4_order(b)
     db = b.to_torch(dev)
     res = {}
@@ -313,9 +320,12 @@ def calvin_config(eng, dev, timed, orc, tag="C4"):
                      "REF-LITERAL (literal Row_lock CALVIN replay, oracle/calvin_ref.c)",
                      f"first {sub.n_txn} of {b.n_txn} txns (index order; sequenced by `order`)")
     return {"workload": "Calvin lock ordering, YCSB theta=0.9, 16 partitions, "
-                        "1,048,576 txns x 16 keys, sequencer (origin, FIFO) order",
+                        "1,048,576 txns x 16 keys, sequencer (origin, FIFO) order" +
+                        (", origins interleaved in the capture" if tag == "C4_SHUF" else ""),
             "txns_per_s": b.n_txn / dt, "ms_per_epoch": dt * 1e3, "cpu_baseline": cpu,
             "device_ms": st["device_ms"], "ready_at_acquire": int(st["n_commit"]),
+            "bucket_path": bool(st["fallback"]),
+            "order_sorted_on_arrival": bool(np.all(np.diff(b.order.astype(np.int64)) >= 0)),
             "alg_GBps": st["alg_bytes"] / (st["device_ms"] * 1e-3) / 1e9,
             "hbm_frac": st["alg_bytes"] / (st["device_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
             "parity_vs_oracle": par}
@@ -429,11 +439,21 @@ def shim_config(eng, dev, timed, orc, tag="SHIM", n=1 << 20, steps=6):
     windows (start_tn, finish_tn], commit tn wanted and the committed writes
     appended to the device history (DCC_OCC_APPEND_HISTORY, central_finish,
     occ.cpp:277-286).  Each step starts from the same history: the committed
-    writes of the previous epoch of the same shape (tn 1..).  Wall time per
-    call (host-synchronous API) and the call's device time.  The batch sits in
-    pinned memory (dcc_host_alloc) in the compact transfer form the shim builds
-    (u32 keys, 2-bit access types, u32 timestamps: dcc.h DCC_KEYS_U32 ...);
-    `pageable_full` is the same call with plain (pageable) full-width arrays."""
+    writes of the previous epoch of the same shape (tn 1..).  Legs:
+      - compact pinned (the value): the batch in pinned memory in the compact
+        transfer form the shim builds (u32 keys, 2-bit access types, u32
+        timestamps: dcc.h DCC_KEYS_U32 ...), pinned outputs;
+      - wide_pinned: the same call with full-width pinned arrays (u64 keys --
+        the INTEGRATION.md binding that passes row_t* identities --, one byte
+        per access type, u64 timestamps);
+      - pageable_full: full-width pageable arrays;
+      - device_resident: the batch and outputs in HBM -- the device time of
+        the decision plus central_finish (window check, commit tn, history
+        append) replayed from one captured graph.
+    Wall time per call (host-synchronous API) and the call's device time
+    (for host outputs it includes the D2H of rc and tn, which the graph
+    holds)."""
+    import torch
     import deneva_amd as d
     rng = np.random.default_rng(0xD3E7A00C)
     prev = d.gen_ycsb(n_txn=n, zipf_theta=0.9, seed=0xD3E7A00D)
@@ -447,28 +467,46 @@ def shim_config(eng, dev, timed, orc, tag="SHIM", n=1 << 20, steps=6):
     b.finish_tn = (ptnc + rng.integers(0, 64, size=n)).astype(np.uint64)
     erc, etn, _ = orc.occ(b, hist_keys=hk, hist_tn=ht, tnc=ptnc)
     cb = eng.compact_host_batch(b)
-    out_rc, out_tn = eng.host_empty(n, np.uint8), eng.host_empty(n, np.uint64)
-    h2d = sum(int(a.nbytes) for a in (cb.offsets, cb.keys, cb.acctype, cb.start_tn, cb.finish_tn))
 
-    def run(batch, pinned_out, k):
+    def pin(a, dt):
+        out = eng.host_empty(np.asarray(a).size, dt)
+        out[...] = np.asarray(a)
+        return out
+    wb = d.EpochBatch(pin(b.offsets, np.uint32), pin(b.keys, np.uint64), pin(b.acctype, np.uint8),
+                      pin(b.start_tn, np.uint64), pin(b.finish_tn, np.uint64))
+    db = b.to_torch(dev)
+    out_rc, out_tn = eng.host_empty(n, np.uint8), eng.host_empty(n, np.uint64)
+    d_rc = torch.empty(n, dtype=torch.uint8, device=dev)
+    d_tn = torch.empty(n, dtype=torch.int64, device=dev)
+    nbytes = lambda x: sum(int(a.nbytes) for a in (x.offsets, x.keys, x.acctype, x.start_tn,
+                                                     x.finish_tn))
+    h2d, h2d_wide = nbytes(cb), nbytes(wb)
+
+    def run(batch, outs, k):
         walls, devs, res = [], [], None
         for i in range(k + 2):
             eng.history_clear()
             eng.history_append(hk, ht)
             eng.tnc = ptnc
-            kw = {"out_rc": out_rc, "out_tn": out_tn} if pinned_out else {}
+            torch.cuda.synchronize()
             t0 = time.perf_counter()
-            rc, tn, st = eng.occ_validate_epoch(batch, want_tn=True, append_history=True, **kw)
+            rc, tn, st = eng.occ_validate_epoch(batch, want_tn=True, append_history=True, **outs)
+            if batch.on_device:
+                torch.cuda.synchronize()
             w = time.perf_counter() - t0
             if i >= 2:  # warmup
                 walls.append(w)
                 devs.append(st["device_ms"])
-            res = (np.asarray(rc).copy(), np.asarray(tn).copy())
+            res = ((rc.cpu().numpy() if batch.on_device else np.asarray(rc)).copy(),
+                   (tn.cpu().numpy() if batch.on_device else np.asarray(tn)).astype(np.uint64).copy())
         par = bool(np.array_equal(res[0], erc) and np.array_equal(res[1], etn))
         return float(np.median(walls)), float(np.median(devs)), par
 
-    wall, devm, par = run(cb, True, steps)
-    wall_p, _, par_p = run(b, False, 3)
+    pinned_out = {"out_rc": out_rc, "out_tn": out_tn}
+    wall, devm, par = run(cb, pinned_out, steps)
+    wall_w, devm_w, par_w = run(wb, pinned_out, steps)
+    wall_p, _, par_p = run(b, {}, 3)
+    wall_d, devm_d, par_d = run(db, {"out_rc": d_rc, "out_tn": d_tn}, steps)
     eng.history_clear()
     eng.tnc = 0
     return {"workload": f"OCC epoch of {n} YCSB txns x 16 keys (theta=0.9) through the shim's path: "
@@ -477,13 +515,21 @@ def shim_config(eng, dev, timed, orc, tag="SHIM", n=1 << 20, steps=6):
             "txns_per_s": n / wall, "ms_per_epoch": wall * 1e3, "device_ms": devm,
             "h2d_MB": h2d / 1e6, "pcie_h2d_GBps": _pcie_h2d_GBps(h2d),
             "h2d_GBps_in_call": h2d / 1e9 / max(wall - devm * 1e-3, 1e-9),
+            "wide_pinned": {"ms_per_epoch": wall_w * 1e3, "device_ms": devm_w, "h2d_MB": h2d_wide / 1e6,
+                            "parity_vs_oracle": par_w,
+                            "note": "u64 keys (row_t* identities), byte access types, u64 timestamps"},
             "pageable_full": {"ms_per_epoch": wall_p * 1e3, "parity_vs_oracle": par_p},
+            "device_resident": {"device_ms": devm_d, "ms_per_epoch": wall_d * 1e3,
+                                "parity_vs_oracle": par_d,
+                                "note": "batch and outputs in HBM: window check + decision + commit tn + "
+                                        "history append, one graph replay"},
             "note": "wall includes H2D of the compact pinned CSR (h2d_MB), the on-device widening, "
-                    "D2H of rc + tn into pinned outputs",
-            "parity_vs_oracle": par and par_p}
+                    "D2H of rc + tn into pinned outputs (inside the replayed graph, so in device_ms)",
+            "parity_vs_oracle": par and par_w and par_p and par_d}
 
 
 CONFIGS = {"C2": occ_config, "C3": occ_config, "C5": occ_config, "C4": calvin_config,
+           "C4_SHUF": calvin_config,
            "C6": None, "HIST": history_config, "SHIM": shim_config, "MAAT_C2": maat_config,
            "MAAT_1M": maat_config}
 
@@ -502,6 +548,10 @@ def secondary_configs(eng, local, steps=10, warmup=3, only=None):
             continue
         out[tag] = (snapshot_config(eng, dev, timed, orc) if tag == "C6"
                     else fn(eng, dev, timed, orc, tag))
+        if tag == "SHIM":  # the INTEGRATION.md binding (row_t* keys): full-width pinned arrays
+            w = out[tag]["wide_pinned"]
+            out["SHIM_WIDE"] = {"workload": out[tag]["workload"] + ", full-width pinned arrays",
+                                "txns_per_s": (1 << 20) / (w["ms_per_epoch"] * 1e-3), **w}
     return out
 
 

@@ -69,8 +69,9 @@ constexpr uint32_t ERR_WAVE_TIMEOUT = 1u << 8;
 
 struct CvPart {
   uint64_t kor, kand, oor, oand;
-  uint32_t nex, pad[3];
+  uint32_t nex, unsorted, pad[2];  // EX requests; positions t with order[t] > order[t + 1]
 };
+constexpr size_t CV_COUNT_OFF = 65536;  // CvCount partials inside part / hpart (after the prep's)
 
 // ---------------------------------------------------------------- prep
 // Workgroups [0, CV_PREP_BLOCKS): the key / order bit reductions; the rest
@@ -89,7 +90,7 @@ __global__ __launch_bounds__(256) void k_cv_prep(const uint64_t* __restrict__ ke
   __shared__ uint64_t s[4][4];
   __shared__ uint32_t s_ex[4];
   uint64_t kor = 0, kand = ~0ull, oor = 0, oand = ~0ull;
-  uint32_t nex = 0;
+  uint32_t nex = 0, uns = 0;
   const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t stride = (uint64_t)CV_PREP_BLOCKS * blockDim.x;
   // 16-B loads: two keys, sixteen access types per load (when aligned)
@@ -129,6 +130,9 @@ __global__ __launch_bounds__(256) void k_cv_prep(const uint64_t* __restrict__ ke
       const uint64_t o = order[t];
       oor |= o;
       oand &= o;
+      // already in sequence order (a sequencer hands its batch over origin by
+      // origin, FIFO): the stable rank is the identity and needs no sort
+      uns += (t + 1 < n && o > order[t + 1]) ? 1u : 0u;
     }
   for (int d = 32; d > 0; d >>= 1) {
     kor |= __shfl_xor(kor, d);
@@ -136,7 +140,9 @@ __global__ __launch_bounds__(256) void k_cv_prep(const uint64_t* __restrict__ ke
     oor |= __shfl_xor(oor, d);
     oand &= __shfl_xor(oand, d);
     nex += __shfl_xor(nex, d);
+    uns += __shfl_xor(uns, d);
   }
+  __shared__ uint32_t s_un[4];
   const uint32_t wv = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
     s[wv][0] = kor;
@@ -144,16 +150,18 @@ __global__ __launch_bounds__(256) void k_cv_prep(const uint64_t* __restrict__ ke
     s[wv][2] = oor;
     s[wv][3] = oand;
     s_ex[wv] = nex;
+    s_un[wv] = uns;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    CvPart p{0, ~0ull, 0, ~0ull, 0, {0, 0, 0}};
+    CvPart p{0, ~0ull, 0, ~0ull, 0, 0, {0, 0}};
     for (int w = 0; w < 4; w++) {
       p.kor |= s[w][0];
       p.kand &= s[w][1];
       p.oor |= s[w][2];
       p.oand &= s[w][3];
       p.nex += s_ex[w];
+      p.unsorted += s_un[w];
     }
     part[blockIdx.x] = p;
   }
@@ -1039,6 +1047,33 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint3
       hat = (const uint8_t*)cv_hat.p;
     }
   }
+  // ---- outputs / workspaces (they depend on the shape only)
+  CR(rc.ensure(this, d.n + 16, "rc"));
+  uint8_t* rc_dev = (dev_out && out_rc) ? out_rc : (uint8_t*)rc.p;
+  // groups are always produced (readiness is derived from them)
+  uint32_t* grp_dev = nullptr;
+  if (out_group && dev_out) {
+    grp_dev = out_group;
+  } else {
+    CR(cv_group.ensure(this, std::max<uint64_t>(16, d.nnz * 4), "calvin group"));
+    grp_dev = (uint32_t*)cv_group.p;
+  }
+  const bool waves = out_wave != nullptr;
+  uint32_t* err = (uint32_t*)misc.p;
+  const bool cv_graph_ok = !profiling && !waves && nh == 0 && comm_ranks() == 1 &&
+                           !DCC_ENV("DCC_NO_GRAPH");
+  CvGraphKey gk;
+  memset(&gk, 0, sizeof gk);
+  gk.off = d.off;
+  gk.keys = d.keys;
+  gk.acc = d.acctype;
+  gk.order = d.order;
+  gk.grp = grp_dev;
+  gk.rc = rc_dev;
+  gk.n = d.n;
+  gk.nnz = d.nnz;
+  gk.gen = buf_gen;
+
   CK(hipEventRecord(ev0, stream));
   if (profiling) CK(hipEventRecord(pev[0], stream));
 
@@ -1049,8 +1084,42 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint3
   CK(hipGetLastError());
   CK(hipMemcpyAsync(hpart, part.p, 16384 + CV_PREP_BLOCKS * sizeof(CvPart), hipMemcpyDeviceToHost,
                     stream));
-  CK(hipStreamSynchronize(stream));
-  uint32_t maxlen = 0, perr = 0;
+  // The rest of the epoch reads the prep's results (key / order packings, the
+  // plan) as launch constants, so it would wait for a host round trip.  When
+  // this batch shape already has a captured graph, the graph is launched
+  // right behind the prep on the results it was captured with -- a
+  // speculation the host checks once the epoch is done: the epoch is redone
+  // (from the prep results already read) if they changed.  A stable key
+  // universe and sequencer keep them equal from epoch to epoch.
+  auto same_shape = [&](const CvGraphKey& k) {
+    return k.off == gk.off && k.keys == gk.keys && k.acc == gk.acc && k.order == gk.order &&
+           k.grp == gk.grp && k.rc == gk.rc && k.n == gk.n && k.nnz == gk.nnz && k.gen == gk.gen;
+  };
+  // (only a bucket-path graph: it never reads the offsets, which the prep
+  // is still validating, so a malformed batch cannot steer its accesses)
+  const bool spec = cv_graph_ok && cv_graph_exec && cv_graph_key.bucket && same_shape(cv_graph_key);
+  // the tail of every epoch: device clock, outputs to the host, counts
+  auto enqueue_tail = [&](const uint32_t* wave_dev) -> int {
+    CK(hipEventRecord(ev1, stream));
+    if (!dev_out) {
+      if (out_rc) CK(hipMemcpyAsync(out_rc, rc_dev, d.n, hipMemcpyDeviceToHost, stream));
+      if (out_group && d.nnz)
+        CK(hipMemcpyAsync(out_group, grp_dev, d.nnz * 4, hipMemcpyDeviceToHost, stream));
+      if (waves) CK(hipMemcpyAsync(out_wave, wave_dev, d.n * 4, hipMemcpyDeviceToHost, stream));
+    }
+    CK(hipMemcpyAsync(hmisc, misc.p, 64, hipMemcpyDeviceToHost, stream));
+    CK(hipMemcpyAsync((char*)hpart + CV_COUNT_OFF, (char*)part.p + CV_COUNT_OFF,
+                      CV_PREP_BLOCKS * sizeof(CvCount), hipMemcpyDeviceToHost, stream));
+    CK(hipStreamSynchronize(stream));
+    return DCC_OK;
+  };
+  if (spec) {
+    CK(hipGraphLaunch(cv_graph_exec, stream));
+    CR(enqueue_tail(nullptr));
+  } else {
+    CK(hipStreamSynchronize(stream));
+  }
+  uint32_t maxlen = 0, perr = 0, unsorted = 0;
   uint64_t kor = 0, kand = ~0ull, oor = 0, oand = ~0ull, nex = 0;
   {
     const PrepPart* pp = (const PrepPart*)hpart;
@@ -1065,6 +1134,7 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint3
       oor |= cp[q].oor;
       oand &= cp[q].oand;
       nex += cp[q].nex;
+      unsorted += cp[q].unsorted;
     }
   }
   if (perr & ERR_OFFSETS) return fail(DCC_EINVAL, "batch: malformed offsets");
@@ -1072,23 +1142,30 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint3
     return fail(DCC_ERANGE, "batch: a txn has %u accesses (> MAX_ROW_PER_TXN=%u)", maxlen,
                 MAX_TXN_LEN);
   const KeyPack kp = make_keypack(d.nnz + nh ? (kor ^ kand) : 0);
-
-  // ---- outputs / workspaces
-  CR(rc.ensure(this, d.n + 16, "rc"));
-  uint8_t* rc_dev = (dev_out && out_rc) ? out_rc : (uint8_t*)rc.p;
-  // groups are always produced (readiness is derived from them)
-  uint32_t* grp_dev = nullptr;
-  if (out_group && dev_out) {
-    grp_dev = out_group;
-  } else {
-    CR(cv_group.ensure(this, std::max<uint64_t>(16, d.nnz * 4), "calvin group"));
-    grp_dev = (uint32_t*)cv_group.p;
-  }
-  const bool waves = out_wave != nullptr;
-  uint32_t* wave_dev = nullptr;
   // uniform txn length (YCSB's fixed request count): a request's place in
   // request order is t * len + j, no offset lookup per request
   const uint32_t ulen = (maxlen && d.nnz == (uint64_t)d.n * maxlen) ? maxlen : 0u;
+  // a varying order that is already non-decreasing ranks as the identity
+  const bool have_seq = d.order && (oor ^ oand) && unsorted != 0;
+  const KeyPack op = have_seq ? make_keypack(oor ^ oand) : KeyPack{};
+  static_assert(sizeof(KeyPack) <= sizeof(CvGraphKey::kp), "key image");
+  // the bucket path (calvin_bucket.h) for large epochs of uniform txns;
+  // DCC_OPT_CALVIN_PATH: 1 keeps the global sort + scan, 2 takes the bucket
+  // path at every size it applies to (0: the bucket path on large epochs)
+  const int cb_mode = cv_path == 1 ? 0 : cv_path == 2 ? 1 : -1;
+  CbPlan cbp{};
+  const bool use_cb = d.nnz && cb_mode != 0 && !waves && nh == 0 && ulen &&
+                      (cb_mode == 1 || d.nnz >= CV_PUT_MIN) && cb_plan(d.n, d.nnz, ulen, kp.bits, &cbp);
+  gk.ulen = ulen;
+  gk.have_seq = have_seq ? 1u : 0u;
+  gk.bucket = use_cb ? 1u : 0u;
+  memcpy(gk.kp, &kp, sizeof kp);
+  memcpy(gk.op, &op, sizeof op);
+  cv_last_sorted = d.order && !have_seq;
+  cv_last_bucket = use_cb;
+  uint32_t* wave_dev = nullptr;
+  if (!(spec && !memcmp(&gk, &cv_graph_key, sizeof gk))) {
+  cv_spec_miss += spec ? 1 : 0;
   ScanOut so{d.off, ulen, (uint32_t)d.n, grp_dev, rc_dev, nullptr, nullptr, nullptr};
   if (waves) {
     if (dev_out) {
@@ -1110,41 +1187,11 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint3
     so.gsx = (uint32_t*)cv_gsx.p;
     so.gsize = (uint32_t*)cv_gsize.p;
   }
-  uint32_t* err = (uint32_t*)misc.p;
 
   // ---- the rest of the epoch as one captured HIP graph: the launches below
   // depend only on the batch's buffers and shape, the key / order packings
   // and the outputs, so the second epoch of a shape is captured and later
-  // ones replay it (the host enqueued ~30 launches after the prep read-back,
-  // and the first, short ones left the GPU waiting for the host)
-  const bool have_seq = d.order && (oor ^ oand);
-  const KeyPack op = have_seq ? make_keypack(oor ^ oand) : KeyPack{};
-  static_assert(sizeof(KeyPack) <= sizeof(CvGraphKey::kp), "key image");
-  const bool cv_graph_ok = !profiling && !waves && nh == 0 && comm_ranks() == 1 &&
-                           !DCC_ENV("DCC_NO_GRAPH");
-  // the bucket path (calvin_bucket.h) for large epochs of uniform txns;
-  // DCC_OPT_CALVIN_PATH: 1 keeps the global sort + scan, 2 takes the bucket
-  // path at every size it applies to (0: the bucket path on large epochs)
-  const int cb_mode = cv_path == 1 ? 0 : cv_path == 2 ? 1 : -1;
-  CbPlan cbp{};
-  const bool use_cb = d.nnz && cb_mode != 0 && !waves && nh == 0 && ulen &&
-                      (cb_mode == 1 || d.nnz >= CV_PUT_MIN) && cb_plan(d.n, d.nnz, ulen, kp.bits, &cbp);
-  CvGraphKey gk;
-  memset(&gk, 0, sizeof gk);
-  gk.off = d.off;
-  gk.keys = d.keys;
-  gk.acc = d.acctype;
-  gk.order = d.order;
-  gk.grp = grp_dev;
-  gk.rc = rc_dev;
-  gk.n = d.n;
-  gk.nnz = d.nnz;
-  gk.gen = buf_gen;
-  gk.ulen = ulen;
-  gk.have_seq = have_seq ? 1u : 0u;
-  gk.bucket = use_cb ? 1u : 0u;
-  memcpy(gk.kp, &kp, sizeof kp);
-  memcpy(gk.op, &op, sizeof op);
+  // ones replay it (speculatively, above, or here after the prep read-back)
   const bool cv_replay = cv_graph_ok && cv_graph_exec && !memcmp(&gk, &cv_graph_key, sizeof gk);
   const bool cv_cap = cv_graph_ok && !cv_replay && cv_seen && !memcmp(&gk, &cv_seen_key, sizeof gk);
   struct CvCapture {  // a failure while capturing still ends the capture
@@ -1251,7 +1298,7 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint3
     CK(hipGetLastError());
   }
   if (profiling) CK(hipEventRecord(pev[4], stream));
-  CvCount* cc = (CvCount*)part.p;
+  CvCount* cc = (CvCount*)((char*)part.p + CV_COUNT_OFF);
   k_cv_count<<<CV_PREP_BLOCKS, 256, 0, stream>>>(rc_dev, wave_dev, d.n, cc);
   CK(hipGetLastError());
   if (cv_cap) {
@@ -1273,23 +1320,16 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint3
     cv_seen = true;
   }
   }  // not replayed
-  CK(hipEventRecord(ev1, stream));
-  if (!dev_out) {
-    if (out_rc) CK(hipMemcpyAsync(out_rc, rc_dev, d.n, hipMemcpyDeviceToHost, stream));
-    if (out_group && d.nnz)
-      CK(hipMemcpyAsync(out_group, grp_dev, d.nnz * 4, hipMemcpyDeviceToHost, stream));
-    if (waves) CK(hipMemcpyAsync(out_wave, wave_dev, d.n * 4, hipMemcpyDeviceToHost, stream));
-  }
-  CK(hipMemcpyAsync(hmisc, misc.p, 64, hipMemcpyDeviceToHost, stream));
-  CK(hipMemcpyAsync(hpart, part.p, CV_PREP_BLOCKS * sizeof(CvCount), hipMemcpyDeviceToHost, stream));
-  CK(hipStreamSynchronize(stream));
+  CR(enqueue_tail(wave_dev));
+  }  // not a confirmed speculation
   if (*(const uint32_t*)hmisc & ERR_WAVE_TIMEOUT)
     return fail(DCC_EIO, "calvin: wave kernel exceeded its time budget");
   uint64_t ready = 0;
   uint32_t maxwave = 0;
   for (unsigned q = 0; q < CV_PREP_BLOCKS; q++) {
-    ready += ((const CvCount*)hpart)[q].ready;
-    maxwave = std::max(maxwave, ((const CvCount*)hpart)[q].maxwave);
+    const CvCount& c = ((const CvCount*)((const char*)hpart + CV_COUNT_OFF))[q];
+    ready += c.ready;
+    maxwave = std::max(maxwave, c.maxwave);
   }
   float ms = 0;
   CK(hipEventElapsedTime(&ms, ev0, ev1));
@@ -1299,6 +1339,7 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint3
   S.nnz_w = nex;
   S.alg_bytes = dcc_calvin_alg_bytes(d.n, d.nnz, d.order != nullptr, waves);
   S.device_ms = ms;
+  S.fallback = use_cb ? 1u : 0u;  // Calvin: the grant groups came from the bucket path
   if (profiling) {
     float t[4] = {0, 0, 0, 0};
     CK(hipEventElapsedTime(&t[0], pev[0], pev[1]));  // prep + rank + layout

@@ -125,6 +125,8 @@ struct dcc_ctx {
   hipGraphExec_t cv_graph_exec = nullptr;
   CvGraphKey cv_graph_key{}, cv_seen_key{};
   bool cv_seen = false;
+  bool cv_last_sorted = false, cv_last_bucket = false;  // the last Calvin epoch's order / path
+  uint64_t cv_spec_miss = 0;  // speculative Calvin replays whose prep results differed
   GraphKey graph_key{};
   uint64_t buf_gen = 0;
   void* hmisc_dev = nullptr;  // device-visible addresses of the two (k_gather targets)

@@ -133,17 +133,17 @@ extern "C" int dcc_init(dcc_ctx** out, int device_id) {
   CK(hipEventCreate(&ctx->ev1));
   for (auto& e : ctx->pev) CK(hipEventCreate(&e));
   CK(hipHostMalloc((void**)&ctx->hmisc, 16384, hipHostMallocDefault));
-  CK(hipHostMalloc((void**)&ctx->hpart, 1 << 16, hipHostMallocDefault));
+  CK(hipHostMalloc((void**)&ctx->hpart, 1 << 17, hipHostMallocDefault));
   CK(hipHostGetDevicePointer(&ctx->hmisc_dev, ctx->hmisc, 0));
   CK(hipHostGetDevicePointer(&ctx->hpart_dev, ctx->hpart, 0));
   CK(hipHostMalloc((void**)&ctx->hdyn, 256, hipHostMallocDefault));
   CK(hipHostGetDevicePointer(&ctx->hdyn_dev, ctx->hdyn, 0));
   memset(ctx->hdyn, 0, 256);
   int rc = ctx->misc.ensure(ctx, 16384, "misc");
-  if (!rc) rc = ctx->part.ensure(ctx, 1 << 16, "partials");
+  if (!rc) rc = ctx->part.ensure(ctx, 1 << 17, "partials");
   // counters and barrier words start zeroed (hipMalloc memory is not)
   if (!rc && (hipMemset(ctx->misc.p, 0, 16384) != hipSuccess ||
-              hipMemset(ctx->part.p, 0, 1 << 16) != hipSuccess))
+              hipMemset(ctx->part.p, 0, 1 << 17) != hipSuccess))
     rc = DCC_EIO;
   if (rc) {
     dcc_destroy(ctx);

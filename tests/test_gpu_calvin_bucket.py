@@ -152,3 +152,65 @@ def test_graph_replay(engine, bucket):
         eg, erc, _ = orc.calvin(b)
         assert np.array_equal(g.cpu().numpy().astype(np.uint32), eg), f"groups, call {i}"
         assert np.array_equal(rc.cpu().numpy(), erc), f"readiness, call {i}"
+
+
+def test_sorted_order_skips_rank_and_matches(engine):
+    """A sequencer hands its epoch over origin by origin in FIFO order, so the
+    order is non-decreasing in index order (ties included): the engine ranks
+    it as the identity without sorting.  The same txns with the order shuffled
+    take the rank sort; both equal the Row_lock replay."""
+    rng = np.random.default_rng(41)
+    b = uniform_batch(rng, 60000, 16, 1 << 14, zipf=1.3)
+    b.order = np.sort(rng.integers(0, 3000, size=b.n_txn)).astype(np.uint64)  # ties
+    check(engine, b)
+    b.order = rng.permutation(b.order)
+    check(engine, b)
+
+
+def test_speculative_replay_and_miss(engine):
+    """The bucket-path graph of a shape is launched right behind the prep on
+    the packing it was captured with; the host checks it afterwards and redoes
+    the epoch when the key universe changed (here: a key with a new high bit),
+    and a malformed batch is still rejected."""
+    import torch
+    n = 1 << 17
+    dev = "cuda:0"
+    kw = dict(n_txn=n, zipf_theta=0.9, part_cnt=16, chunk_txns=8192, table_size=1 << 18, want_home=True)
+    b0 = d.gen_ycsb(seed=5, **kw)
+    db = b0.to_torch(dev)
+    g_out = torch.empty(b0.nnz, dtype=torch.int32, device=dev)
+    rc_out = torch.empty(n, dtype=torch.uint8, device=dev)
+    engine.set_option(d._abi.OPT_CALVIN_PATH, 2)
+    try:
+        for i, mutate in enumerate([None, None, None, "seed", "highbit", None, "highbit"]):
+            b = d.gen_ycsb(seed=5 if mutate is None else 6, **kw)
+            keys = np.asarray(b.keys, np.uint64).copy()
+            if mutate == "highbit":
+                keys[12345] |= np.uint64(1 << 21)  # a new packed bit (still <= 24)
+            b.keys = keys
+            db.keys.copy_(torch.from_numpy(keys.view(np.int64)).to(dev))
+            g, rc, _, st = engine.calvin_order_epoch(db, want_group=True, out_group=g_out, out_rc=rc_out)
+            torch.cuda.synchronize()
+            eg, erc, _ = orc.calvin(b)
+            assert st["fallback"] == 1, "bucket path"
+            assert np.array_equal(g.cpu().numpy().astype(np.uint32), eg), f"groups, epoch {i}"
+            assert np.array_equal(rc.cpu().numpy(), erc), f"readiness, epoch {i}"
+        bad = d.EpochBatch(db.offsets.clone(), db.keys, db.acctype)
+        bad.offsets[7] = bad.offsets[8] + 1
+        with pytest.raises(d.DccError):
+            engine.calvin_order_epoch(bad, want_group=True, out_group=g_out, out_rc=rc_out)
+    finally:
+        engine.set_option(d._abi.OPT_CALVIN_PATH, 0)
+
+
+def test_c4_interleaved_origins_full_size(engine):
+    # C4 captured with its 16 origins interleaved (txn i from origin i % 16):
+    # the order must be ranked before the bucket path
+    b = c4_batch()
+    home = (np.arange(b.n_txn) % 16).astype(np.uint64)
+    b.order = (home << np.uint64(32)) | (np.arange(b.n_txn, dtype=np.uint64) // np.uint64(16))
+    g, rc, _, st = engine.calvin_order_epoch(b, want_group=True)
+    eg, erc, _ = orc.calvin(b)
+    assert st["fallback"] == 1
+    assert np.array_equal(np.asarray(g).astype(np.uint32), eg)
+    assert np.array_equal(np.asarray(rc), erc)
