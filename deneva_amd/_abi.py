@@ -10,7 +10,9 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdcc.so")
+# DENEVA_AMD_LIB: another build of the library (tools/: the DCC_EXPERIMENTS
+# build with the A/B timing switches); tests, bench and smoke load the default
+LIB_PATH = os.environ.get("DENEVA_AMD_LIB") or os.path.join(_HERE, "libdcc.so")
 
 # ---- constants mirrored from include/dcc.h
 DCC_OK = 0

@@ -46,6 +46,7 @@ struct dcc_multi;       // single-process multi-GPU context (dcc_multi.cpp)
 struct HistStore {
   DevBuf fk, ft;            // flat pairs
   DevBuf skey, stn, hash;   // built level
+  DevBuf bm;                // key bitmap of the built level (occ_history.h HIST_BM_LOG)
   uint64_t m = 0;           // pairs
   uint32_t hbits = 0;
   bool built = true;        // the built level matches the flat pairs
@@ -160,6 +161,7 @@ struct dcc_ctx {
   HistStore hs[2];
   uint64_t hist_merge_min = 65536;  // DCC_OPT_HIST_MERGE
   DevBuf h_K[2], h_V[2], h_scr, h_bsum;          // level-build sort buffers, append scan
+  DevBuf h_bm;                                   // key bitmap of both levels (window check)
   DevBuf perm, calvin_a, calvin_b, calvin_c, calvin_d;  // Calvin workspaces
   DevBuf cv_scratch, cv_agg, cv_group, cv_wave, cv_pgx, cv_gsx, cv_gsize, cv_done, cv_maxl;
   DevBuf cv_seq_b, cv_ok, cv_len, cv_off2, cv_tsum, cv_hkeys, cv_hat;

@@ -257,11 +257,11 @@ std::vector<DevBuf*> dcc_ctx::all_bufs() {
                             &snap_top, &snap_aoff, &snap_aidx, &snap_cnt, &mt_rk,
                             &mt_misc, &mt_slot, &mt_sval, &mt_slot2, &mt_sval2, &mt_sfl,
                             &mt_stx, &mt_txn, &mt_agg, &mt_sflB, &mt_stxB, &mt_k1, &mt_tcnt, &mt_ul, &mt_lb, &mt_ptab, &ix_keys, &ix_ord, &ix_rows, &ix_cnt, &wv_buf, &ix_scr, &wv_hbuf, &wv_obuf,
-                            &h_K[0], &h_K[1], &h_V[0], &h_V[1], &h_scr, &h_bsum,
+                            &h_K[0], &h_K[1], &h_V[0], &h_V[1], &h_scr, &h_bsum, &h_bm,
                             &nar_keys, &nar_at, &nar_tn, &fin_off, &fin_keys, &fin_at, &fin_state, &fin_hasw, &fin_rc, &fin_cnt,
                             &sh_off, &sh_keys, &sh_at, &sh_src, &sh_cnt, &sh_bsum, &sh_rc, &sh_tn, &sh_grp};
   for (auto& h : hs)
-    for (DevBuf* b : {&h.fk, &h.ft, &h.skey, &h.stn, &h.hash}) v.push_back(b);
+    for (DevBuf* b : {&h.fk, &h.ft, &h.skey, &h.stn, &h.hash, &h.bm}) v.push_back(b);
   for (auto& sb : sw_list)
     for (DevBuf* b : {&sb.tid, &sb.off, &sb.keys, &sb.acctype, &sb.state}) v.push_back(b);
   for (int i = 0; i < 2; i++) {
@@ -346,6 +346,9 @@ int dcc_ctx::hist_build(HistStore& h) {
               h.max_key ? 64u - (uint32_t)__builtin_clzll(h.max_key) : 1u,
               64u - (uint32_t)__builtin_clzll(h.max_tn | 1ull)};
   if (hist_build_level(b, stream)) CK(hipGetLastError());
+  CR(h.bm.ensure(this, (1u << HIST_BM_LOG) / 8, "history key bitmap"));
+  launch_hist_bm((const uint64_t*)h.fk.p, h.m, (uint32_t*)h.bm.p, stream);
+  CK(hipGetLastError());
   h.built = true;
   return DCC_OK;
 }
@@ -367,10 +370,17 @@ int dcc_ctx::hist_prepare() {
     B.min_tn = std::min(B.min_tn, D.min_tn);
     B.max_key = std::max(B.max_key, D.max_key);
     B.built = false;
-    D = HistStore{D.fk, D.ft, D.skey, D.stn, D.hash};  // buffers kept, level emptied
+    D = HistStore{D.fk, D.ft, D.skey, D.stn, D.hash, D.bm};  // buffers kept, level emptied
   }
+  const bool rebuilt = !B.built || !D.built;
   CR(hist_build(B));
   CR(hist_build(D));
+  if (rebuilt || !h_bm.p) {
+    CR(h_bm.ensure(this, (1u << HIST_BM_LOG) / 8, "history key bitmap"));
+    launch_hist_bm_or(B.m ? (const uint32_t*)B.bm.p : nullptr, D.m ? (const uint32_t*)D.bm.p : nullptr,
+                      (uint32_t*)h_bm.p, stream);
+    CK(hipGetLastError());
+  }
   return DCC_OK;
 }
 
@@ -381,6 +391,7 @@ HistView dcc_ctx::hist_view() const {
     v.lv[q] = HistLevel{(const uint64_t*)h.hash.p, (const uint64_t*)h.stn.p, h.hbits,
                         h.m && h.built ? 1u : 0u};
   }
+  v.bm = (const uint32_t*)h_bm.p;  // set by hist_prepare
   return v;
 }
 

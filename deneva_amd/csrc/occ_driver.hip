@@ -854,7 +854,7 @@ int dcc_ctx::occ_begin(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, bo
 
   // ---- history window pre-pass (occ.cpp:160-180)
   if (r.hist_on && !r.replay) {
-    HistArgs ha{d.n, d.nnz, d.off, d.keys, d.acctype, d.start_tn, d.finish_tn, (const OccDyn*)dyn.p,
+    HistArgs ha{d.n, d.nnz, d.off, d.keys, d.acctype, d.start_tn, d.finish_tn, (const OccDyn*)dyn.p, 0u,
                 (uint8_t*)state.p, (uint32_t*)misc.p};
     launch_hist(ha, stream);
   }

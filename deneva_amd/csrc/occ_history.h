@@ -30,8 +30,16 @@ struct HistLevel {
   uint32_t hbits;
   uint32_t on;           // 0: the level is empty
 };
+// One-hash bitmap of every key in the history (both levels): the window
+// check loads it into LDS and probes a level's table only for keys whose bit
+// is set (most reads touch keys the history never saw).
+constexpr uint32_t HIST_BM_LOG = 17;  // bits (16 KiB)
+__host__ __device__ inline uint32_t hist_bm_bit(uint64_t key) {
+  return (uint32_t)((key * 0xD6E8FEB86659FD93ull) >> (64 - HIST_BM_LOG));
+}
 struct HistView {
-  HistLevel lv[2];  // base, delta
+  HistLevel lv[2];     // base, delta
+  const uint32_t* bm;  // [2^HIST_BM_LOG / 32] key bitmap of both levels, or null
 };
 
 // does the level hold a pair (key, tn) with lo < tn <= hi?
@@ -86,6 +94,9 @@ struct HistBuild {
   uint32_t kbits, tbits;  // significant bits of the keys / tns (radix passes)
 };
 int hist_build_level(const HistBuild& b, hipStream_t st);
+// the key bitmap of m flat keys (bm zeroed first), and out = a | b
+void launch_hist_bm(const uint64_t* keys, uint64_t m, uint32_t* bm, hipStream_t st);
+void launch_hist_bm_or(const uint32_t* a, const uint32_t* b, uint32_t* out, hipStream_t st);
 // pairs with tn > floor of (ak, at)[na] then (bk, bt)[nb], appended at
 // (ok, ot) + *cnt (atomic position: order not kept)
 void launch_hist_trim(const uint64_t* ak, const uint64_t* at, uint64_t na, const uint64_t* bk,

@@ -363,6 +363,25 @@ int hist_build_level(const HistBuild& b, hipStream_t st) {
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// ---------------------------------------------------------------- key bitmap
+__global__ __launch_bounds__(256) void k_hist_bm(const uint64_t* keys, uint64_t m, uint32_t* bm) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < m; i += (uint64_t)gridDim.x * 256) {
+    const uint32_t b = hist_bm_bit(keys[i]);
+    atomicOr(&bm[b >> 5], 1u << (b & 31u));
+  }
+}
+__global__ __launch_bounds__(256) void k_hist_bm_or(const uint32_t* a, const uint32_t* b, uint32_t* out) {
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < (1u << HIST_BM_LOG) / 32; i += gridDim.x * 256)
+    out[i] = (a ? a[i] : 0u) | (b ? b[i] : 0u);
+}
+void launch_hist_bm(const uint64_t* keys, uint64_t m, uint32_t* bm, hipStream_t st) {
+  (void)hipMemsetAsync(bm, 0, (1u << HIST_BM_LOG) / 8, st);
+  if (m) k_hist_bm<<<hgrid(m), 256, 0, st>>>(keys, m, bm);
+}
+void launch_hist_bm_or(const uint32_t* a, const uint32_t* b, uint32_t* out, hipStream_t st) {
+  k_hist_bm_or<<<16, 256, 0, st>>>(a, b, out);
+}
+
 // ---------------------------------------------------------------- trim
 __global__ __launch_bounds__(256) void k_hist_trim(const uint64_t* ak, const uint64_t* at,
                                                    uint64_t na, const uint64_t* bk,

@@ -66,6 +66,7 @@ struct HistArgs {
   const uint64_t* start_tn;
   const uint64_t* finish_tn;
   const OccDyn* dyn;  // device history levels (dyn->view)
+  uint32_t var;       // DCC_HIST_VAR timing variants (DCC_EXPERIMENTS builds only; 0)
   uint8_t* state;
   uint32_t* err;   // ERR_OFFSETS on a malformed device batch
 };

@@ -29,6 +29,7 @@
 #include <algorithm>
 
 #include "dcc_device.h"
+#include "dcc_env.h"
 #include "occ_kernels.h"
 #include "prep_body.h"
 
@@ -46,23 +47,120 @@ __global__ __launch_bounds__(256) void k_prep(const uint32_t* __restrict__ off, 
 // k_hist: the history window check (occ.cpp:160-180): if finish_tn > start_tn,
 // txn i aborts when a committed history entry with start_tn < tn <= finish_tn
 // wrote a key i READ (history is checked against the read set only).  The
-// history is the device's base + delta levels (occ_history.h).  One thread
-// per txn (this path is off under TS_CLOCK); offsets are clamped to nnz.
-__global__ __launch_bounds__(256) void k_hist(HistArgs a) {
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= a.n) return;
-  const uint64_t s_tn = a.start_tn[t], f_tn = a.finish_tn[t];
-  if (!(f_tn > s_tn)) return;
-  const uint64_t o0 = min((uint64_t)a.off[t], a.nnz), o1 = min((uint64_t)a.off[t + 1], a.nnz);
-  if (o1 < o0 || o1 - o0 > MAX_TXN_LEN) {
-    atomicOr(a.err, ERR_OFFSETS);
-    return;
+// history is the device's base + delta levels (occ_history.h).  A workgroup
+// holds the history's key bitmap in LDS; a wave takes 64 txns and walks their
+// contiguous accesses 64 at a time (coalesced key and type loads, one access
+// per lane), finding each access's txn in the wave's LDS offset prefix; only a
+// read whose key bit is set probes the levels, and a hit marks its txn
+// aborted (every writer stores the same byte).  Offsets are clamped to nnz
+// and made monotone; a malformed batch is reported.
+constexpr uint32_t HIST_WAVES = 16;
+constexpr uint32_t HIST_U = 4;  // accesses per lane in flight
+// first step of a level probe for U keys at once: the key's home slot (16 B:
+// key, first | count << 32); the rest of the walk (a collision, the tn run's
+// binary search) follows per key
+__device__ inline bool hist_level_hit_from(const HistLevel& L, uint64_t key, uint64_t lo, uint64_t hi,
+                                           uint64_t slot, uint64_t k2, uint64_t v) {
+  const uint64_t mask = (1ull << L.hbits) - 1;
+  while (k2 != key) {
+    if (k2 == DCC_KEY_RESERVED) return false;
+    slot = (slot + 1) & mask;
+    k2 = L.hash[2 * slot];
+    v = L.hash[2 * slot + 1];
   }
-  for (uint64_t x = o0; x < o1; x++) {
-    if (a.acctype[x] == 1 /* WR */) continue;
-    if (hist_hit(a.dyn->view, a.keys[x], s_tn, f_tn)) {
-      a.state[t] = ST_ABORT;
-      return;
+  const uint64_t first = (uint32_t)v, end = first + (v >> 32);
+  uint64_t b = first, e = end;
+  while (b < e) {  // first tn > lo
+    const uint64_t m = (b + e) >> 1;
+    if (L.tn[m] <= lo) b = m + 1;
+    else e = m;
+  }
+  return b < end && L.tn[b] <= hi;
+}
+__global__ __launch_bounds__(HIST_WAVES * 64) void k_hist(HistArgs a) {
+  __shared__ uint32_t s_bm[(1u << HIST_BM_LOG) / 32];
+  __shared__ uint32_t s_o[HIST_WAVES][65];
+  __shared__ uint64_t s_lo[HIST_WAVES][64], s_hi[HIST_WAVES][64];
+  const HistView hv = a.dyn->view;  // by value: registers, not a reload per probe
+  for (uint32_t i = threadIdx.x; i < (1u << HIST_BM_LOG) / 32; i += HIST_WAVES * 64)
+    s_bm[i] = hv.bm ? hv.bm[i] : ~0u;
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t t0 = ((uint64_t)blockIdx.x * HIST_WAVES + w) * 64;
+  if (t0 >= a.n) return;
+  const uint32_t nt = (uint32_t)min<uint64_t>(64, a.n - t0);
+  const uint64_t t = t0 + lane;
+  uint64_t lo = 0, hi = 0;
+  if (lane < nt) {
+    lo = a.start_tn[t];
+    hi = a.finish_tn[t];
+    const uint32_t o0 = a.off[t], o1 = a.off[t + 1];
+    if (o1 < o0 || o1 - o0 > MAX_TXN_LEN) atomicOr(a.err, ERR_OFFSETS);
+  }
+  s_lo[w][lane] = lo;
+  s_hi[w][lane] = hi;
+  uint32_t ov = lane <= nt ? (uint32_t)min<uint64_t>(a.off[t0 + lane], a.nnz) : 0u;
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(ov, d);
+    if (lane >= (uint32_t)d && lane <= nt) ov = max(ov, y);
+  }
+  s_o[w][lane] = ov;
+  __builtin_amdgcn_wave_barrier();
+  if (lane == 0) s_o[w][64] = nt == 64 ? max(s_o[w][63], (uint32_t)min<uint64_t>(a.off[t0 + 64], a.nnz)) : 0u;
+  __builtin_amdgcn_wave_barrier();
+  // no txn of the wave has an open window: nothing to check
+  if (!ballot64(lane < nt && hi > lo)) return;
+  const uint32_t a0 = s_o[w][0], a1 = s_o[w][nt];
+  for (uint32_t x0 = a0; x0 < a1; x0 += 64 * HIST_U) {
+    uint64_t key[HIST_U];
+    uint8_t ty[HIST_U];
+#pragma unroll
+    for (uint32_t u = 0; u < HIST_U; u++) {  // every load of the step issued before any use
+      const uint32_t x = min(x0 + 64 * u + lane, a1 - 1);
+      key[u] = a.keys[x];
+      ty[u] = a.acctype[x];
+    }
+    uint32_t txn[HIST_U];
+    bool want[HIST_U];
+#pragma unroll
+    for (uint32_t u = 0; u < HIST_U; u++) {
+      const uint32_t x = x0 + 64 * u + lane;
+      const uint32_t b = hist_bm_bit(key[u]);
+      want[u] = x < a1 && ty[u] != 1 /* WR */ && ((a.var & 2u) || ((s_bm[b >> 5] >> (b & 31u)) & 1u));
+      txn[u] = 0;
+      if (a.var & 1u) want[u] = false;
+      if (want[u] && !(a.var & 4u)) {
+        uint32_t l = 0, h = nt;  // largest k < nt with s_o[k] <= x
+        while (h - l > 1) {
+          const uint32_t mid = (l + h) >> 1;
+          if (s_o[w][mid] <= x) l = mid;
+          else h = mid;
+        }
+        txn[u] = l;
+        want[u] = s_hi[w][l] > s_lo[w][l];
+      }
+    }
+    // level by level: the home slots of every wanted key loaded together
+#pragma unroll
+    for (int q = 1; q >= 0; q--) {
+      const HistLevel& L = hv.lv[q];
+      if (!L.on) continue;
+      uint64_t slot[HIST_U], k2[HIST_U], v[HIST_U];
+#pragma unroll
+      for (uint32_t u = 0; u < HIST_U; u++) {
+        slot[u] = hist_hash_slot(key[u], L.hbits);
+        k2[u] = want[u] ? L.hash[2 * slot[u]] : DCC_KEY_RESERVED;
+        v[u] = want[u] ? L.hash[2 * slot[u] + 1] : 0;
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < HIST_U; u++) {
+        if (!want[u]) continue;
+        const uint32_t l = txn[u];
+        if (hist_level_hit_from(L, key[u], s_lo[w][l], s_hi[w][l], slot[u], k2[u], v[u])) {
+          a.state[t0 + l] = ST_ABORT;
+          want[u] = false;  // decided: the other level need not be probed
+        }
+      }
     }
   }
 }
@@ -814,8 +912,14 @@ void launch_prep(const uint32_t* off, uint64_t n, const uint8_t* at, uint64_t nn
                  PrepPart* part, hipStream_t st) {
   k_prep<<<PREP_BLOCKS, 256, 0, st>>>(off, n, at, nnz, p, part);
 }
-void launch_hist(const HistArgs& a, hipStream_t st) {
-  k_hist<<<grid_for(a.n, 256), 256, 0, st>>>(a);
+void launch_hist(const HistArgs& a0, hipStream_t st) {
+  HistArgs a = a0;
+#ifdef DCC_EXPERIMENTS
+  if (const char* e = DCC_ENV("DCC_HIST_VAR")) a.var = (uint32_t)atoi(e);  // timing variants (wrong results)
+#else
+  a.var = 0;
+#endif
+  k_hist<<<grid_for(a.n, HIST_WAVES * 64), HIST_WAVES * 64, 0, st>>>(a);  // a wave per 64 txns
 }
 static unsigned tile_grid(uint64_t m, uint32_t tw, unsigned max_grid) {
   const uint64_t waves = (m + tw - 1) / tw;

@@ -264,6 +264,7 @@ def test_graph_replay_new_contents(engine, sequenced):
 
     def put(dst, a):  # new contents, same device buffer
         dst.copy_(torch.from_numpy(np.ascontiguousarray(a)).to("cuda:0"))
+        torch.cuda.synchronize()  # the engine reads on its own stream
 
     for i, sd in enumerate(seeds + [14]):
         b = d.gen_ycsb(n_txn=n, zipf_theta=0.9, part_cnt=4, chunk_txns=4096, want_home=True, seed=sd)

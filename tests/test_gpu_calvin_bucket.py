@@ -147,6 +147,7 @@ def test_graph_replay(engine, bucket):
         b = d.gen_ycsb(n_txn=n, zipf_theta=0.9, part_cnt=4, chunk_txns=4096, seed=sd)
         db.keys.copy_(torch.from_numpy(np.ascontiguousarray(b.keys)).to("cuda:0"))
         db.acctype.copy_(torch.from_numpy(np.ascontiguousarray(b.acctype)).to("cuda:0"))
+        torch.cuda.synchronize()  # the engine reads on its own stream
         g, rc, _, _ = engine.calvin_order_epoch(db, want_group=True, out_group=g_out, out_rc=rc_out)
         torch.cuda.synchronize()
         eg, erc, _ = orc.calvin(b)
@@ -189,14 +190,17 @@ def test_speculative_replay_and_miss(engine):
                 keys[12345] |= np.uint64(1 << 21)  # a new packed bit (still <= 24)
             b.keys = keys
             db.keys.copy_(torch.from_numpy(keys.view(np.int64)).to(dev))
+            db.acctype.copy_(torch.from_numpy(np.ascontiguousarray(b.acctype)).to(dev))
+            torch.cuda.synchronize()  # the engine reads on its own stream
             g, rc, _, st = engine.calvin_order_epoch(db, want_group=True, out_group=g_out, out_rc=rc_out)
             torch.cuda.synchronize()
             eg, erc, _ = orc.calvin(b)
             assert st["fallback"] == 1, "bucket path"
             assert np.array_equal(g.cpu().numpy().astype(np.uint32), eg), f"groups, epoch {i}"
             assert np.array_equal(rc.cpu().numpy(), erc), f"readiness, epoch {i}"
-        bad = d.EpochBatch(db.offsets.clone(), db.keys, db.acctype)
-        bad.offsets[7] = bad.offsets[8] + 1
+        off = np.asarray(b0.offsets, np.uint32).copy()
+        off[7] = off[8] + 1  # offsets decrease
+        bad = d.EpochBatch(torch.from_numpy(off).to(dev), db.keys, db.acctype)
         with pytest.raises(d.DccError):
             engine.calvin_order_epoch(bad, want_group=True, out_group=g_out, out_rc=rc_out)
     finally:
