@@ -654,15 +654,16 @@ def main():
                 t = torch.from_numpy(buf)
                 dist.all_reduce(t, op=dist.ReduceOp.MAX)
             eng.comm_init_host(rank, world, allreduce_max)
-        mine = d.shard_filter(batch, rank, world)
-    else:
-        mine = batch
+    # every rank takes the whole epoch and keeps its key shard of the accesses
+    # on its GPU (DCC_SHARD_SELF): the sweep's serial ranges come from the
+    # rank's own copy, so ranks exchange only the filters' kill bits
+    mine = batch
     dbatch = mine.to_torch(f"cuda:{local}")
     out_rc = torch.empty(n_total, dtype=torch.uint8, device=f"cuda:{local}")
     torch.cuda.synchronize()
 
     def step(profile=False):
-        return eng.occ_validate_epoch(dbatch, out_rc=out_rc)[2]
+        return eng.occ_validate_epoch(dbatch, out_rc=out_rc, shard_self=world > 1)[2]
 
     # Pipelined headline (N=1): consecutive epochs over L distinct resident
     # batches of the same workload (seeds seed, seed+1, ...), one per lane,

@@ -34,6 +34,7 @@ OCC_DEFER_FINISH = 0x8
 KEYS_U32 = 0x10
 ACCTYPE_2BIT = 0x20
 TN_U32 = 0x40
+SHARD_SELF = 0x80
 MAAT_READ_AND_PREWRITE = 0x4
 ROW_NONE = 0xFFFFFFFFFFFFFFFF
 UNIQUE_ID_BYTES = 128

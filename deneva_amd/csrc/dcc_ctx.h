@@ -225,6 +225,8 @@ struct dcc_ctx {
     DevBatch d;
     bool sh = false, dev_out = false, defer = false, sweep = false, want_tn = false;
     bool app = false, hist_on = false;  // history append (central_finish) / window check
+    bool whole = false;                 // key-sharded rank holding the whole batch (DCC_SHARD_SELF)
+    DevBatch full;                      // that batch
     bool replay = false, capturing = false, pending = false, active = false;
     uint32_t glv = 0, maxlen = 0, rounds = 0, handoffs = 0;
     uint64_t nnz_w = 0;
@@ -262,7 +264,9 @@ struct dcc_ctx {
   int sweep_enqueue(const DevBatch& d, int l0, int l1, const dcc::SwShard* shard = nullptr,
                     bool resume = false, bool tail_serial = false);
   int sweep_sharded(const DevBatch& d, int& next_level);
-  int sweep_ro(const DevBatch& d, bool big, bool scan, uint64_t nnz_w);  // decide the RO list
+  int sweep_sharded_full(const DevBatch& d, const DevBatch& full, int l0, int l1);  // levels [l0, l1)
+  // decide the RO list (full: a key-sharded rank's whole batch)
+  int sweep_ro(const DevBatch& d, bool big, bool scan, uint64_t nnz_w, const DevBatch* full = nullptr);
   int occ_sweep_finish(const DevBatch& d, int& next_level, bool& done, uint32_t maxlen);
   int occ_snapshot(const dcc_batch* b, const dcc_occ_snapshot* s, uint8_t* out_rc, dcc_stats* st);
   // MaaT (maat.hip): row timestamp table + epoch workspaces
@@ -274,7 +278,7 @@ struct dcc_ctx {
   // device-side key-shard partition (shard_dev.hip): rank `rank` of R of a
   // multi-GPU context; sb is the shard as a device batch
   DevBuf sh_off, sh_keys, sh_at, sh_src, sh_cnt, sh_bsum, sh_rc, sh_tn, sh_grp;
-  int shard_stage(const dcc_batch* b, uint32_t rank, uint32_t R, dcc_batch& sb);
+  int shard_stage(const dcc_batch* b, uint32_t rank, uint32_t R, dcc_batch& sb, DevBatch* full_out = nullptr);
   int shard_groups(const uint32_t* grp, uint64_t m, uint32_t* out_dev);  // groups to batch order
 };
 

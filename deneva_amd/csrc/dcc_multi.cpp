@@ -293,14 +293,16 @@ int dcc_multi_occ_epoch(dcc_ctx* ctx, const dcc_batch* b, uint8_t* out_rc, uint6
   std::vector<uint64_t> tn0;
   std::vector<dcc_stats> S(R);
   const int e = run_ranks(ctx, [&](int r, dcc_ctx* s) -> int {
-    dcc_batch sb;
-    int x = s->shard_stage(b, (uint32_t)r, (uint32_t)R, sb);
-    if (x != DCC_OK) return x;
+    // the whole batch: the rank keeps its key shard (partitioned on its GPU)
+    // and serves its serial passes from the whole batch (DCC_SHARD_SELF)
+    dcc_batch fb = *b;
+    fb.flags |= DCC_SHARD_SELF;
+    int x = DCC_OK;
     if ((x = s->sh_rc.ensure(s, n + 16, "shard rc")) != DCC_OK) return x;
     if (out_tn && (x = s->sh_tn.ensure(s, n * 8 + 16, "shard tn")) != DCC_OK) return x;
     uint8_t* drc = (uint8_t*)s->sh_rc.p;
     uint64_t* dtn = out_tn ? (uint64_t*)s->sh_tn.p : nullptr;
-    if ((x = s->occ_epoch(&sb, drc, dtn, &S[r])) != DCC_OK) return x;
+    if ((x = s->occ_epoch(&fb, drc, dtn, &S[r])) != DCC_OK) return x;
     hipError_t he = hipSuccess;
     if (!dev) {
       rc[r].resize(n + 1);
@@ -326,8 +328,8 @@ int dcc_multi_occ_epoch(dcc_ctx* ctx, const dcc_batch* b, uint8_t* out_rc, uint6
   if (st) {
     *st = S[0];
     for (int r = 1; r < R; r++) st->device_ms = std::max(st->device_ms, S[r].device_ms);
-    st->nnz_w = 0;
-    for (int r = 0; r < R; r++) st->nnz_w += S[r].nnz_w;
+    // every rank counts the whole batch's writes (its has-write pass reads it)
+    st->nnz_w = S[0].nnz_w;
     st->alg_bytes = dcc_alg_bytes(n, b->nnz, st->nnz_w);
   }
   return DCC_OK;
@@ -415,8 +417,8 @@ int dcc_multi_calvin_epoch(dcc_ctx* ctx, const dcc_batch* b, const dcc_calvin_he
   if (st) {
     *st = S[0];
     for (int r = 1; r < R; r++) st->device_ms = std::max(st->device_ms, S[r].device_ms);
-    st->nnz_w = 0;
-    for (int r = 0; r < R; r++) st->nnz_w += S[r].nnz_w;
+    // every rank counts the whole batch's writes (its has-write pass reads it)
+    st->nnz_w = S[0].nnz_w;
     st->alg_bytes = dcc_calvin_alg_bytes(n, b->nnz, b->order != nullptr, 0);
   }
   return DCC_OK;

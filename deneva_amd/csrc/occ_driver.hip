@@ -379,7 +379,7 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1, const SwShard* shl
   unsigned long long* bsum_d = tcount_d + n64 + 32;
   // read-only split (one GPU): level 0 moves its read-only survivors to the
   // RO list (decided after the levels, sweep_ro)
-  const bool ros = ro_on && !shl;
+  const bool ros = ro_on && (!shl || shl->full_off);
   uint32_t* const wctl = abandon;  // [0] abandon [1] writer table full [2] RO count
   for (int l = l0; l < l1; l++) {
     const bool top = l == 0;
@@ -403,8 +403,8 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1, const SwShard* shl
     // key-sharded: the serial part runs on the merged serial range (every
     // shard's accesses of list txns [0, P)), identically on every rank
     const SwList sin = shl ? shl->serial : in;
-    const uint32_t* smdev = shl ? nullptr : mdev;
-    const uint32_t sm_host = shl ? shl->P : n;
+    const uint32_t* smdev = shl ? shl->m_dev : mdev;
+    const uint32_t sm_host = (shl && !shl->m_dev) ? shl->P : n;
     SwPreArgs pa{sin, smdev, sm_host, pmax, top ? (const uint8_t*)state.p : nullptr,
                  (SwRec*)sw_rec.p, (uint32_t*)sw_rk.p,
                  gtab0 + (size_t)(l & 1) * (1ull << SW_GBITS_MAX), sw_gbits(l, ros),
@@ -430,10 +430,12 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1, const SwShard* shl
       }
     }
     if (top) {  // the epoch's validation pass rides along the level-0 serial pass
-      sa.prep_off = d.off;
+      // (a rank holding the whole batch takes its has-write bytes from it)
+      const bool whole = shl && shl->full_off;
+      sa.prep_off = whole ? shl->full_off : d.off;
       sa.prep_n = d.n;
-      sa.prep_at = d.acctype;
-      sa.prep_nnz = d.nnz;
+      sa.prep_at = whole ? shl->full_at : d.acctype;
+      sa.prep_nnz = whole ? shl->full_nnz : d.nnz;
       sa.prep_part = (PrepPart*)((char*)hpart_dev + SW_PREP_OFF);
     }
     if (serial_part) launch_sw_seq(sa, stream);
@@ -481,8 +483,10 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1, const SwShard* shl
     fa.err = err;
     fa.dbg = (sw_debug && l < 4) ? (uint64_t*)sw_dbg.p + 4096 + (size_t)l * 256 * 8 : nullptr;
     fa.cdbg = pa.dbg ? pa.dbg + 32 : nullptr;
-    fa.kill_out = shl ? shl->kill : nullptr;
-    fa.kill_in = shl ? shl->kill : nullptr;
+    fa.kill_out = shl ? shl->kill_out : nullptr;
+    fa.kill_in = shl ? shl->kill_all : nullptr;
+    fa.kill_ranks = shl ? (uint32_t)comm_ranks() : 0u;
+    fa.kill_stride = shl ? shl->kill_words : 0u;
     fa.ro_split = (ros && top) ? 1 : 0;
     fa.rflag = (uint64_t*)sw_rflag.p;
     fa.rtcount = (unsigned long long*)(fa.rflag + n64 + 32);
@@ -494,9 +498,11 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1, const SwShard* shl
     launch_sw_filter(fa, fgrid, stream);
     if (top && profiling) CK(hipEventRecord(pev[2], stream));
     if (shl) {
-      // a kill on any shard wins; then every rank applies the same decision
-      CR(comm_allreduce_max_u8(shl->kill, shl->m));
-      if (top) CR(comm_allreduce_max_u8((uint8_t*)hasw.p, d.n));
+      // a kill on any shard wins (every rank's kill words gathered, OR-ed by
+      // k_sw_apply); then every rank applies the same decision.  The has-write
+      // bytes are global already when the rank holds the whole batch.
+      CR(comm_allgather_u8((const uint8_t*)shl->kill_out, (uint8_t*)shl->kill_all, shl->kill_words * 8));
+      if (top && !shl->full_off) CR(comm_allreduce_max_u8((uint8_t*)hasw.p, d.n));
       launch_sw_apply(fa, fgrid, stream);
     }
     launch_sw_compact(fa, fgrid, stream);
@@ -560,12 +566,12 @@ int dcc_ctx::sweep_sharded(const DevBatch& d, int& next_level) {
     CR(sw_moff.ensure(this, 4ull * (P + 1) + 64, "sweep merged offsets"));
     CR(sw_mkeys.ensure(this, std::max<uint64_t>(64, total * 8), "sweep merged keys"));
     CR(sw_mat.ensure(this, std::max<uint64_t>(64, total), "sweep merged types"));
-    CR(sw_kill.ensure(this, (uint64_t)d.n + 64, "sweep kill bits"));
+    const uint64_t kw = (m - P + 63) / 64 + 1;  // kill words of the list past the serial range
+    CR(sw_kill.ensure(this, kw * 8 * (R + 1) + 64, "sweep kill bits"));
     uint32_t* xrec = (uint32_t*)sw_xrec.p;
     uint32_t* mcnt = (uint32_t*)sw_mcnt.p;
     CK(hipMemsetAsync(sw_xsend.p, 0xFF, chunk, stream));
     CK(hipMemsetAsync(mcnt, 0, 4ull * (P + 1), stream));
-    CK(hipMemsetAsync(sw_kill.p, 0, m, stream));
     launch_sw_merge(in, P, (uint32_t*)sw_xsend.p, 0, 0, nullptr, nullptr, nullptr, nullptr,
                     nullptr, true, stream);
     CR(comm_allgather_u8((const uint8_t*)sw_xsend.p, (uint8_t*)xrec, chunk));
@@ -573,18 +579,75 @@ int dcc_ctx::sweep_sharded(const DevBatch& d, int& next_level) {
     launch_sw_merge(in, P, xrec, 0, (uint32_t)(R * (chunk / 12)), mcnt, mcnt + (P + 1),
                     (uint32_t*)sw_moff.p, (uint64_t*)sw_mkeys.p, (uint8_t*)sw_mat.p, false, stream);
     CK(hipGetLastError());
-    SwShard shl;
+    SwShard shl{};
     shl.serial = SwList{top ? nullptr : in.tid, (const uint32_t*)sw_moff.p,
                         (const uint64_t*)sw_mkeys.p, (const uint8_t*)sw_mat.p, total};
     shl.P = P;
-    shl.m = m;
-    shl.kill = (uint8_t*)sw_kill.p;
+    shl.kill_out = (uint64_t*)sw_kill.p;
+    shl.kill_all = (uint64_t*)sw_kill.p + kw;
+    shl.kill_words = kw;
     CR(sweep_enqueue(d, l, l + 1, &shl));
   }
   next_level = SW_MAX_LEVEL - 1;
   return DCC_OK;
 }
 
+
+// Key-sharded sweep, every rank holding the whole batch (DCC_SHARD_SELF):
+// the serial part of a level needs the whole access lists of the level's first
+// txns, which every rank gathers from its copy of the batch
+// (launch_sw_sgather) instead of exchanging records, so the ranks exchange
+// only the filters' kill bits -- one all-gather of fixed size per level (the
+// list's bound: the epoch at level 0, then the hand-off thresholds), with
+// every list length on the device.  The levels are enqueued with no host
+// synchronisation; the read-only split applies as on one GPU (every rank
+// decides the read-only list from the whole batch).  Levels [0, L) are
+// enqueued; next_level = L.
+int dcc_ctx::sweep_sharded_full(const DevBatch& d, const DevBatch& full, int l0, int L) {
+  dcc_ctx* ctx = this;
+  const int R = comm_ranks();
+  SwLevel* ctl = (SwLevel*)sw_ctl.p;
+  uint32_t* err = (uint32_t*)misc.p;
+  // kill-word capacity per level: list l holds at most cap[l] txns (the
+  // compaction hands a list to the round solver past max(abandon_min, 1/4 of
+  // the epoch) at level 0 and max(abandon_min, 3/4 of the list) later)
+  uint64_t cap = d.n, wmax = 0;
+  std::vector<uint64_t> words(std::max(L, 1));
+  for (int l = 0; l < L; l++) {
+    words[l] = (cap + 63) / 64 + 1;
+    wmax = std::max(wmax, words[l]);
+    cap = std::min<uint64_t>(cap, std::max<uint64_t>(65536, l == 0 ? (cap + 3) / 4 : (cap * 3 + 3) / 4));
+  }
+  CR(sw_kill.ensure(this, wmax * 8 * (R + 1) + 64, "sweep kill bits"));
+  const uint32_t pm = sw_pmax(SW_MAX_LEVEL - 1, ro_on);
+  CR(sw_moff.ensure(this, 4ull * (std::min<uint64_t>(pm, d.n) + 1) + 64, "sweep serial offsets"));
+  CR(sw_mkeys.ensure(this, 8ull * std::min<uint64_t>(pm, d.n) * MAX_TXN_LEN + 64, "sweep serial keys"));
+  CR(sw_mat.ensure(this, std::min<uint64_t>(pm, d.n) * MAX_TXN_LEN + 64, "sweep serial types"));
+  for (int l = l0; l < L; l++) {
+    SwShard shl{};
+    if (l == 0) {
+      shl.serial = SwList{nullptr, full.off, full.keys, full.acctype, full.nnz};
+      shl.P = (uint32_t)d.n;
+    } else {
+      const SubBufs& b = sw_list[(l - 1) & 1];
+      launch_sw_sgather((const uint32_t*)b.tid.p, &ctl[l].m, sw_pmax(l, ro_on), full.off, full.keys,
+                        full.acctype, full.nnz, (uint32_t*)sw_moff.p, (uint64_t*)sw_mkeys.p,
+                        (uint8_t*)sw_mat.p, err, stream);
+      CK(hipGetLastError());
+      shl.serial = SwList{(const uint32_t*)b.tid.p, (const uint32_t*)sw_moff.p, (const uint64_t*)sw_mkeys.p,
+                          (const uint8_t*)sw_mat.p, std::min<uint64_t>(pm, d.n) * MAX_TXN_LEN};
+      shl.m_dev = &ctl[l].m;
+    }
+    shl.kill_out = (uint64_t*)sw_kill.p;
+    shl.kill_all = (uint64_t*)sw_kill.p + wmax;
+    shl.kill_words = words[l];
+    shl.full_off = full.off;
+    shl.full_at = full.acctype;
+    shl.full_nnz = full.nnz;
+    CR(sweep_enqueue(d, l, l + 1, &shl));
+  }
+  return DCC_OK;
+}
 
 // ---------------------------------------------------------------------------
 // Deferred central_finish (DCC_OCC_DEFER_FINISH): the decided epoch is kept --
@@ -690,7 +753,10 @@ int dcc_ctx::occ_finish(const uint8_t* final_rc, uint64_t* out_tn, uint32_t flag
 // committed writer of the epoch), then the list against it (k_sw_ro).  `big`:
 // after an overflow, a table sized for every write of the epoch (<= 50 %
 // load, unbounded probes).
-int dcc_ctx::sweep_ro(const DevBatch& d, bool big, bool scan, uint64_t nnz_w) {
+int dcc_ctx::sweep_ro(const DevBatch& d0, bool big, bool scan, uint64_t nnz_w, const DevBatch* full) {
+  // a key-sharded rank holding the whole batch decides every read-only txn
+  // from it (the writer table then holds every committed write)
+  const DevBatch& d = full ? *full : d0;
   dcc_ctx* ctx = this;
   uint32_t* wctl = (uint32_t*)((SwLevel*)sw_ctl.p + SW_MAX_LEVEL + 1);
   WrTab wt{(WrSlot*)sw_wtab.p, wt_bits, WT_PROBES, wctl + 1};
@@ -705,7 +771,7 @@ int dcc_ctx::sweep_ro(const DevBatch& d, bool big, bool scan, uint64_t nnz_w) {
                 (const uint8_t*)hasw.p, scan ? nullptr : (const uint32_t*)sw_cw.p, wctl + 4, wt};
   launch_sw_wall(wa, (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(scan ? 4096 : 256, (d.n + 255) / 256)),
                  stream);
-  SwRoArgs ra{(const RoEnt*)sw_ro.p, wctl + 2, d.keys, wt, (uint8_t*)state.p};
+  SwRoArgs ra{(const RoEnt*)sw_ro.p, wctl + 2, d.keys, wt, (uint8_t*)state.p, full ? full->off : nullptr};
   launch_sw_ro(ra, (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(4096, (d.n + 63) / 64)), stream);
   CK(hipGetLastError());
   return DCC_OK;
@@ -758,10 +824,19 @@ int dcc_ctx::occ_begin(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, bo
     return DCC_OK;
   }
   DevBatch& d = r.d;
-  CR(stage_batch(b, d));
+  r.whole = r.sh && (b->flags & DCC_SHARD_SELF) && use_sweep();
+  if (r.whole) {
+    // this rank's key shard of the whole batch, partitioned on the device;
+    // the whole batch stays for the serial passes and the read-only list
+    dcc_batch sb;
+    CR(shard_stage(b, (uint32_t)comm_rank(), (uint32_t)comm_ranks(), sb, &r.full));
+    CR(stage_batch(&sb, d));
+  } else {
+    CR(stage_batch(b, d));
+  }
   r.sweep = use_sweep();
   const bool sh = r.sh, sweep = r.sweep;
-  ro_on = sweep && ro_split && !sh;
+  ro_on = sweep && ro_split && (!sh || r.whole);
   if (sweep) CR(sweep_reserve(d));
   CR(state.ensure(this, d.n + 16, "state"));
   CR(hasw.ensure(this, d.n + 16, "hasw"));
@@ -876,7 +951,10 @@ int dcc_ctx::occ_begin(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, bo
     if (profiling) CK(hipEventRecord(pev[0], stream));
     r.next_level = (int)std::min<uint32_t>(r.glv, SW_MAX_LEVEL - 1);
     if (!sh && r.next_level >= 2) r.serial_tail = r.next_level - 1;
-    if (sh) {
+    if (r.whole) {
+      CR(sweep_sharded_full(d, r.full, 0, r.next_level));
+      if (ro_on) CR(sweep_ro(d, false, false, 0, &r.full));
+    } else if (sh) {
       CR(sweep_sharded(d, r.next_level));
     } else if (!r.replay) {
       CR(sweep_enqueue(d, 0, r.next_level, nullptr, false, r.serial_tail >= 0));
@@ -1029,10 +1107,11 @@ int dcc_ctx::occ_end(dcc_stats* st) {
       int L = -1;
       if (ab) L = (int)ab;
       else if (hc[next_level].m == 0) break;  // every list decided
-      else if (sh || next_level + (int)glv >= SW_MAX_LEVEL) L = next_level;
+      else if ((sh && !r.whole) || next_level + (int)glv >= SW_MAX_LEVEL) L = next_level;
       if (L < 0) {
         const int l1 = next_level + (int)glv;
-        CR(sweep_enqueue(d, next_level, l1));
+        if (r.whole) CR(sweep_sharded_full(d, r.full, next_level, l1));
+        else CR(sweep_enqueue(d, next_level, l1));
         next_level = l1;
         GatherArgs ga{};
         ga.job[ga.n++] = CopyJob{(const uint32_t*)sw_ctl.p,
@@ -1079,7 +1158,7 @@ int dcc_ctx::occ_end(dcc_stats* st) {
       const bool full = w[1] != 0, ro_n = w[2] != 0;
       if (full && wt_bits < 24) wt_bits += 2;
       if (ro_n && (full || again)) {
-        CR(sweep_ro(d, full, handoffs > 0, nnz_w));
+        CR(sweep_ro(d, full, handoffs > 0, nnz_w, r.whole ? &r.full : nullptr));
         ro_fast_rerun = !full;
         again = true;
       }
@@ -1095,7 +1174,7 @@ int dcc_ctx::occ_end(dcc_stats* st) {
                                             SW_MAX_LEVEL + 1);
       if (w[1]) {
         if (wt_bits < 24) wt_bits += 2;
-        CR(sweep_ro(d, true, handoffs > 0, nnz_w));
+        CR(sweep_ro(d, true, handoffs > 0, nnz_w, r.whole ? &r.full : nullptr));
         CR(occ_final(false));
       }
     }

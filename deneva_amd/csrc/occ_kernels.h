@@ -260,6 +260,8 @@ struct SwRoArgs {
   const uint64_t* keys;
   WrTab wt;
   uint8_t* state;
+  const uint32_t* full_off;  // key-sharded with the whole batch: a txn's accesses are
+                             // [full_off[t], full_off[t + 1]) of keys, not the entry's range
 };
 // k_sw_wall: the committed writers' writes into wt -- the txns the serial
 // passes listed (cw_list, cw_count), or (cw_list null) every committed txn
@@ -376,8 +378,13 @@ struct SwFilterArgs {
   const uint32_t* abandon;
   uint32_t* abandon_out;  // = level + 1 when the survivors stay too many
   uint32_t abandon_min, abandon_num, abandon_den;
-  uint8_t* kill_out;      // key-sharded: per list position, this shard's kill bit (else null)
-  const uint8_t* kill_in; // key-sharded: the all-reduced kill bits (k_sw_apply)
+  // key-sharded: this shard's kill bits, one 64-bit word per list tile of 64
+  // positions after the serial range (bit = lane), else null; k_sw_apply ORs
+  // the kill_ranks contributions of kill_stride words each in kill_in
+  uint64_t* kill_out;
+  const uint64_t* kill_in;
+  uint32_t kill_ranks;
+  uint64_t kill_stride;
   // read-only split (level 0, one GPU): read-only survivors (hasw[txn] == 0)
   // go to ro_out (txn ids, any order) instead of the next list -- no later
   // level holds them; k_sw_ro decides them once every writer is decided
@@ -397,12 +404,29 @@ struct SwFilterArgs {
 };
 // One key-sharded sweep level (the host side of SURVEY.md §8(e)): the merged
 // serial range, its txn count, the list length and the kill-bit buffer.
+// One key-sharded sweep level: the serial range every rank decides alike
+// (merged records, or gathered from the whole batch each rank holds), and the
+// kill-bit exchange of the level's filter.
 struct SwShard {
   SwList serial;
-  uint32_t P;
-  uint32_t m;
-  uint8_t* kill;
+  const uint32_t* m_dev;  // the serial list's length on the device (null: P)
+  uint32_t P;             // its length on the host (m_dev null)
+  uint64_t* kill_out;     // this rank's kill words (kill_words of them)
+  uint64_t* kill_all;     // every rank's, rank-major
+  uint64_t kill_words;    // words exchanged per rank
+  // the whole batch (DCC_SHARD_SELF): the serial part's has-write bytes come
+  // from it, so no has-write exchange is needed
+  const uint32_t* full_off;
+  const uint8_t* full_at;
+  uint64_t full_nnz;
 };
+// The first min(p_max, *m) list txns' whole access lists (the serial range of
+// a key-sharded level, gathered from the whole batch): offsets soff[0..P],
+// keys / types at soff; two launches, no host synchronisation.
+void launch_sw_sgather(const uint32_t* tid, const uint32_t* m_dev, uint32_t p_max,
+                       const uint32_t* full_off, const uint64_t* full_keys, const uint8_t* full_at,
+                       uint64_t full_nnz, uint32_t* soff, uint64_t* skeys, uint8_t* sat,
+                       uint32_t* err, hipStream_t st);
 void launch_sw_pre(const SwPreArgs& a, unsigned grid, hipStream_t st);
 void launch_sw_seq(const SwSeqArgs& a, hipStream_t st);
 void launch_sw_rows(const SwPreArgs& a, unsigned grid, hipStream_t st);

@@ -1329,8 +1329,9 @@ __global__ __launch_bounds__(SW_CHUNK) void k_sw_filter(SwFilterArgs a) {
     }
     if (dbg && wt == t_lo) dbg[3] = __builtin_amdgcn_s_memrealtime();
     if (dbg) dbg[6]++;
-    if (a.kill_out) {  // key-sharded: this shard's kill bit only (k_sw_apply decides)
-      if (valid) a.kill_out[p] = killed ? 1 : 0;
+    if (a.kill_out) {  // key-sharded: this shard's kill bits only (k_sw_apply decides)
+      const uint64_t km = ballot64(valid && killed);
+      if (lane == 0) a.kill_out[wt] = km;
       continue;
     }
     if (killed) a.state[tid] = ST_ABORT;
@@ -1401,10 +1402,14 @@ __global__ __launch_bounds__(SW_CHUNK) void k_sw_apply(SwFilterArgs a) {
   const uint64_t nnz = a.in.nnz;
   const uint32_t R = sw_tiles_per_wg(n64, gridDim.x);
   const uint32_t t_lo = min(blockIdx.x * R, n64), t_hi = min(t_lo + R, n64);
-  uint64_t wsum = 0;
+  uint64_t wsum = 0, rsum = 0;
   for (uint32_t wt = t_lo + wv; wt < t_hi; wt += SW_CHUNK / 64) {
     const uint32_t p = pos + wt * 64 + lane;
-    bool surv = false;
+    // a kill on any shard wins: the OR of every rank's word of this tile
+    uint64_t kw = 0;
+    for (uint32_t r = 0; r < a.kill_ranks; r++) kw |= a.kill_in[r * a.kill_stride + wt];
+    const bool kill = (kw >> lane) & 1ull;
+    bool surv = false, ro = false;
     uint32_t len = 0;
     if (p < m) {
       const uint32_t tid = a.in.tid ? a.in.tid[p] : p;
@@ -1412,8 +1417,9 @@ __global__ __launch_bounds__(SW_CHUNK) void k_sw_apply(SwFilterArgs a) {
       const uint32_t s = (uint32_t)min((uint64_t)a.in.off[p], nnz);
       const uint32_t e = (uint32_t)min((uint64_t)a.in.off[p + 1], nnz);
       len = e > s ? e - s : 0u;
-      if (cand && a.kill_in[p]) a.state[tid] = ST_ABORT;
-      surv = cand && !a.kill_in[p];
+      if (cand && kill) a.state[tid] = ST_ABORT;
+      surv = cand && !kill;
+      ro = a.ro_split && a.hasw[tid] == 0;  // the has-write bytes are the whole batch's
     }
     const uint64_t sm = ballot64(surv);
     const uint64_t acc = wave_sum64(surv ? len : 0u);
@@ -1423,14 +1429,87 @@ __global__ __launch_bounds__(SW_CHUNK) void k_sw_apply(SwFilterArgs a) {
       a.sflag[wt] = sm;
       a.tcount[wt] = cnt;
     }
+    if (a.ro_split) {  // read-only survivors counted apart (as the filter does)
+      const uint64_t rm = ballot64(surv && ro);
+      const uint64_t racc = wave_sum64(surv && ro ? len : 0u);
+      const uint64_t rc = ((uint64_t)__popcll(rm) << LB_ACC_BITS) | racc;
+      rsum += rc;
+      if (lane == 0) {
+        a.rflag[wt] = rm;
+        a.rtcount[wt] = rc;
+      }
+    }
   }
-  __shared__ unsigned long long s_bs[SW_CHUNK / 64];
-  if (lane == 0) s_bs[wv] = wsum;
+  __shared__ unsigned long long s_bs[SW_CHUNK / 64][2];
+  if (lane == 0) {
+    s_bs[wv][0] = wsum;
+    s_bs[wv][1] = rsum;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
-    uint64_t t = 0;
-    for (uint32_t w = 0; w < SW_CHUNK / 64; w++) t += s_bs[w];
+    uint64_t t = 0, r = 0;
+    for (uint32_t w = 0; w < SW_CHUNK / 64; w++) {
+      t += s_bs[w][0];
+      r += s_bs[w][1];
+    }
     a.bsum[blockIdx.x] = t;
+    if (a.ro_split) a.rbsum[blockIdx.x] = r;
+  }
+}
+
+// k_sw_sg_scan (one workgroup): the offsets of the first P = min(p_max, *m)
+// list txns' whole access lists (soff[0..P]); k_sw_sg_copy: their keys and
+// types, 16 lanes per txn.  The serial range of a level of a key-sharded
+// epoch whose ranks hold the whole batch (DCC_SHARD_SELF).
+constexpr uint32_t SG_T = 1024;
+__global__ __launch_bounds__(SG_T) void k_sw_sg_scan(const uint32_t* tid, const uint32_t* m_dev, uint32_t p_max,
+                                                     const uint32_t* full_off, uint64_t full_nnz, uint32_t* soff,
+                                                     uint32_t* err) {
+  __shared__ uint32_t s_w[SG_T / 64];
+  __shared__ uint32_t s_carry;
+  const uint32_t P = min(p_max, *m_dev), lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (threadIdx.x == 0) s_carry = 0;
+  __syncthreads();
+  for (uint32_t q0 = 0; q0 < P; q0 += SG_T) {
+    const uint32_t q = q0 + threadIdx.x;
+    uint32_t len = 0;
+    if (q < P) {
+      const uint32_t t = tid[q];
+      const uint64_t s = min((uint64_t)full_off[t], full_nnz), e = min((uint64_t)full_off[t + 1], full_nnz);
+      len = e > s ? (uint32_t)(e - s) : 0u;
+      if (len > MAX_TXN_LEN) {
+        atomicOr(err, ERR_OFFSETS);
+        len = 0;
+      }
+    }
+    uint32_t x = len;
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(x, d);
+      if (lane >= (uint32_t)d) x += y;
+    }
+    if (lane == 63) s_w[wv] = x;
+    __syncthreads();
+    uint32_t b = s_carry;
+    for (uint32_t w = 0; w < wv; w++) b += s_w[w];
+    if (q < P) soff[q] = b + x - len;
+    __syncthreads();
+    if (threadIdx.x == SG_T - 1) s_carry = b + x;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) soff[P] = s_carry;
+}
+__global__ __launch_bounds__(256) void k_sw_sg_copy(const uint32_t* tid, const uint32_t* m_dev, uint32_t p_max,
+                                                    const uint32_t* full_off, const uint64_t* full_keys,
+                                                    const uint8_t* full_at, uint64_t full_nnz, const uint32_t* soff,
+                                                    uint64_t* skeys, uint8_t* sat) {
+  const uint32_t P = min(p_max, *m_dev), sl = threadIdx.x & 15u;
+  for (uint32_t q = (blockIdx.x * 256 + threadIdx.x) >> 4; q < P; q += gridDim.x * 16) {
+    const uint32_t t = tid[q], o = soff[q], len = soff[q + 1] - o;
+    const uint64_t s = min((uint64_t)full_off[t], full_nnz);
+    for (uint32_t x = sl; x < len; x += 16) {
+      skeys[o + x] = full_keys[s + x];
+      sat[o + x] = full_at[s + x];
+    }
   }
 }
 
@@ -1732,7 +1811,11 @@ __global__ __launch_bounds__(256) void k_sw_ro(SwRoArgs a) {
   const uint32_t lane = lane_id(), g = lane >> 4, sl = lane & 15u;
   const uint32_t ng = gridDim.x * 16;
   for (uint32_t i = (blockIdx.x * 256 + threadIdx.x) >> 4; i < cnt; i += ng) {
-    const uint4 r = *(const uint4*)&a.ro[i];  // tid, first access, end
+    uint4 r = *(const uint4*)&a.ro[i];  // tid, first access, end
+    if (a.full_off) {  // key-sharded: the txn's accesses in the whole batch
+      r.y = a.full_off[r.x];
+      r.z = a.full_off[r.x + 1];
+    }
     bool kill = false;
     for (uint32_t x = r.y + sl; x < r.z && !kill; x += 16) kill = wt_find(a.wt, a.keys[x]) < r.x;
     const uint64_t b = ballot64(kill);
@@ -1800,6 +1883,14 @@ void launch_sw_share(const uint32_t* m_dev, uint32_t m_host, const uint32_t* aba
                      const uint32_t* off, uint32_t p_max, uint32_t rank, uint32_t* cnt,
                      hipStream_t st) {
   k_sw_share<<<1, 1, 0, st>>>(m_dev, m_host, abandon, off, p_max, rank, cnt);
+}
+void launch_sw_sgather(const uint32_t* tid, const uint32_t* m_dev, uint32_t p_max,
+                       const uint32_t* full_off, const uint64_t* full_keys, const uint8_t* full_at,
+                       uint64_t full_nnz, uint32_t* soff, uint64_t* skeys, uint8_t* sat,
+                       uint32_t* err, hipStream_t st) {
+  k_sw_sg_scan<<<1, SG_T, 0, st>>>(tid, m_dev, p_max, full_off, full_nnz, soff, err);
+  k_sw_sg_copy<<<std::max<uint32_t>(1, std::min<uint32_t>((p_max + 15) / 16, 1024)), 256, 0, st>>>(
+      tid, m_dev, p_max, full_off, full_keys, full_at, full_nnz, soff, skeys, sat);
 }
 void launch_sw_apply(const SwFilterArgs& a, unsigned grid, hipStream_t st) {
   k_sw_apply<<<grid ? grid : 1u, SW_CHUNK, 0, st>>>(a);

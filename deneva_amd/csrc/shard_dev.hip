@@ -118,10 +118,12 @@ inline unsigned blocks(uint64_t n) { return (unsigned)std::max<uint64_t>(1, (n +
 // Rank `rank` of R: this context's shard of batch b as a device batch `sb`
 // (DCC_DEVICE_PTRS; the per-txn windows / order stay those of the staged or
 // caller's batch).  One host synchronisation: the shard's access count.
-int dcc_ctx::shard_stage(const dcc_batch* b, uint32_t rank, uint32_t R, dcc_batch& sb) {
+int dcc_ctx::shard_stage(const dcc_batch* b, uint32_t rank, uint32_t R, dcc_batch& sb,
+                         DevBatch* full_out) {
   dcc_ctx* ctx = this;
   DevBatch full;
   CR(stage_batch(b, full));
+  if (full_out) *full_out = full;
   const uint64_t n = full.n, nnz = full.nnz;
   const unsigned nb = blocks(n);
   CR(sh_off.ensure(this, (n + 1) * 4 + 64, "shard offsets"));

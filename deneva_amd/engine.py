@@ -213,10 +213,12 @@ class Engine:
     # ------------------------------------------------------------ OCC
     def occ_validate_epoch(self, batch: EpochBatch, want_tn: bool = False,
                            append_history: bool = False, out_rc=None, out_tn=None,
-                           defer_finish: bool = False):
+                           defer_finish: bool = False, shard_self: bool = False):
         """Decide every txn of the epoch; returns (rc u8[n], tn u64[n] | None, stats).
         defer_finish: 2PC participant -- rc is the local vote; commit tn and
-        history wait for ``occ_finish_epoch(global_rc)``."""
+        history wait for ``occ_finish_epoch(global_rc)``.  shard_self: a
+        key-sharded rank given the WHOLE epoch keeps its own key shard
+        (DCC_SHARD_SELF)."""
         n = batch.n_txn
         dev = batch.on_device
         if out_rc is None:
@@ -235,6 +237,8 @@ class Engine:
         flags = _abi.OCC_APPEND_HISTORY if append_history else 0
         if defer_finish:
             flags |= _abi.OCC_DEFER_FINISH
+        if shard_self:
+            flags |= _abi.SHARD_SELF
         b = batch.to_c(flags)
         _check(lib.dcc_occ_validate_epoch(self._h, C.byref(b), _ptr(out_rc), _ptr(out_tn),
                                           C.byref(st)), self._h)

@@ -86,6 +86,14 @@ extern "C" {
                                    in bits 2(x%4)..2(x%4)+1 of byte x/4                     */
 #define DCC_TN_U32 0x40u        /* start_tn / finish_tn point to uint32_t timestamps        */
 #define DCC_COMPACT_FLAGS (DCC_KEYS_U32 | DCC_ACCTYPE_2BIT | DCC_TN_U32)
+/* Key-sharded contexts (dcc_comm_init*): the batch is the WHOLE epoch; the
+ * rank keeps its key shard of the accesses itself (partitioned on the device)
+ * and the whole batch for the serial passes, so ranks exchange only kill bits
+ * (one fixed-size all-gather per sweep level, no host synchronisation between
+ * levels).  Without the flag a rank passes only its own accesses
+ * (dcc_shard_filter) and the ranks exchange the serial ranges' records.
+ * A multi-GPU context (dcc_init_multi) always shards this way. */
+#define DCC_SHARD_SELF 0x80u
 
 /* One epoch as a CSR of per-transaction access lists in capture order
  * (Access list of TxnManager, system/txn.h:39-70; txn.cpp:818-847). */

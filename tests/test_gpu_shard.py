@@ -4,8 +4,12 @@ Ranks are separate processes sharing the box's one GPU; each owns the keys
 with dcc_key_shard(key, world) == rank and exchanges the per-round status
 through dcc_comm_init_host (gloo all-reduce MAX on the host).  The engine
 code path is the one RCCL drives on an 8-GPU node — only the all-reduce
-transport differs.  OCC runs the key-sharded sweep (the serial range
-all-gathered and merged on every rank, the filters' kill bits all-reduced).  Decisions, commit tn, history across epochs, and Calvin
+transport differs.  OCC runs the key-sharded sweep in both forms: ranks
+given only their accesses (dcc_shard_filter; the serial range's records
+all-gathered and merged on every rank) and ranks given the whole epoch
+(DCC_SHARD_SELF; each keeps its key shard on the device and gathers the
+serial ranges from its copy of the batch); the filters' kill bits are
+all-gathered.  Decisions, commit tn, history across epochs, and Calvin
 grant groups / readiness must equal the unsharded oracle bit for bit."""
 import os
 import socket
@@ -34,7 +38,14 @@ def _occ_batches():
     yield d.gen_ycsb(n_txn=5000, zipf_theta=0.6, req_per_query=33, table_size=1 << 12)
 
 
-def _worker(rank, world, port, out):
+def _occ(eng, b, rank, world, whole, **kw):
+    """One key-sharded OCC epoch: the rank's accesses only, or the whole batch."""
+    if whole:
+        return eng.occ_validate_epoch(b, shard_self=True, **kw)
+    return eng.occ_validate_epoch(d.shard_filter(b, rank, world), **kw)
+
+
+def _worker(rank, world, port, out, whole=False):
     import torch
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -51,7 +62,7 @@ def _worker(rank, world, port, out):
     res = {"occ": [], "hist": [], "calvin": []}
     for b in _occ_batches():
         eng.tnc = 0  # each batch is checked as a fresh epoch
-        rc, tn, st = eng.occ_validate_epoch(d.shard_filter(b, rank, world), want_tn=True)
+        rc, tn, st = _occ(eng, b, rank, world, whole, want_tn=True)
         res["occ"].append((np.asarray(rc).copy(), np.asarray(tn).copy(), st["rounds"],
                            st["n_shards"], st["peel_prefix"], b.n_txn))
     # three epochs with history (start/finish windows) appended across epochs
@@ -62,8 +73,7 @@ def _worker(rank, world, port, out):
         n = b.n_txn
         b.start_tn = np.full(n, 0, np.uint64)
         b.finish_tn = np.full(n, 1 << 40, np.uint64)
-        rc, tn, st = eng.occ_validate_epoch(d.shard_filter(b, rank, world), want_tn=True,
-                                            append_history=True)
+        rc, tn, st = _occ(eng, b, rank, world, whole, want_tn=True, append_history=True)
         res["hist"].append((np.asarray(rc).copy(), np.asarray(tn).copy(), eng.tnc))
     for theta in (0.0, 0.9):
         b = d.gen_ycsb(n_txn=30000, zipf_theta=theta, req_per_query=16, table_size=1 << 14)
@@ -73,12 +83,13 @@ def _worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("whole", [False, True])
 @pytest.mark.parametrize("world", [2, 3])
-def test_sharded_engine_matches_unsharded(world):
+def test_sharded_engine_matches_unsharded(world, whole):
     import torch.multiprocessing as mp
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), out, whole), nprocs=world, join=True)
     for bi, b in enumerate(_occ_batches()):
         erc, etn, _ = orc.occ(b)
         for r in range(world):
@@ -122,7 +133,7 @@ def test_sharded_engine_matches_unsharded(world):
         assert np.array_equal(got, eg), "calvin grant groups differ"
 
 
-def _c5_worker(rank, world, port, out):
+def _c5_worker(rank, world, port, out, whole=False):
     import torch
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -137,20 +148,21 @@ def _c5_worker(rank, world, port, out):
     eng.comm_init_host(rank, world, allreduce_max)
     b = d.gen_ycsb(n_txn=1 << 20, zipf_theta=0.99, seed=0xD3E7A002)
     eng.tnc = 0
-    rc, tn, st = eng.occ_validate_epoch(d.shard_filter(b, rank, world), want_tn=True)
+    rc, tn, st = _occ(eng, b, rank, world, whole, want_tn=True)
     out[rank] = (np.asarray(rc).copy(), np.asarray(tn).copy(), st["n_shards"], eng.tnc)
     eng.close()
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("whole", [False, True])
 @pytest.mark.parametrize("world", [4, 8])
-def test_sharded_c5_full_size(world):
+def test_sharded_c5_full_size(world, whole):
     """BASELINE config C5 (1,048,576 YCSB txns, theta=0.99) key-sharded over
     4 and 8 ranks (processes sharing the GPU, gloo exchange)."""
     import torch.multiprocessing as mp
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_c5_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    mp.spawn(_c5_worker, args=(world, _free_port(), out, whole), nprocs=world, join=True)
     b = d.gen_ycsb(n_txn=1 << 20, zipf_theta=0.99, seed=0xD3E7A002)
     erc, etn, etnc = orc.occ(b)
     for r in range(world):
