@@ -837,7 +837,7 @@ def main():
                             f"50% WR tuples",
                 "global_batch": n_total,
                 "keys_per_txn": args.keys,
-                "parallelism": (f"key-shard x{world} ({args.exchange} all-reduce)" if world > 1
+                "parallelism": (f"key-shard x{world} ({args.exchange} kill-bit all-gather, whole epoch per rank)" if world > 1
                                 else "single GPU"),
             },
             "pipeline": ({

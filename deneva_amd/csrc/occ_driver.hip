@@ -566,7 +566,9 @@ int dcc_ctx::sweep_sharded(const DevBatch& d, int& next_level) {
     CR(sw_moff.ensure(this, 4ull * (P + 1) + 64, "sweep merged offsets"));
     CR(sw_mkeys.ensure(this, std::max<uint64_t>(64, total * 8), "sweep merged keys"));
     CR(sw_mat.ensure(this, std::max<uint64_t>(64, total), "sweep merged types"));
-    const uint64_t kw = (m - P + 63) / 64 + 1;  // kill words of the list past the serial range
+    // kill words: one per 64 list positions past where the serial pass
+    // stopped (at most P, earlier when its access budget ran out)
+    const uint64_t kw = (m + 63) / 64 + 1;
     CR(sw_kill.ensure(this, kw * 8 * (R + 1) + 64, "sweep kill bits"));
     uint32_t* xrec = (uint32_t*)sw_xrec.p;
     uint32_t* mcnt = (uint32_t*)sw_mcnt.p;
