@@ -67,7 +67,7 @@ def parse():
                     help="PMC summary (tools/gpu_pmc_r04.sh -> tools/pmc_r04.py) the "
                          "roofline.traffic / l2_hit fields and each config's pmc block are read "
                          "from (the workloads it describes at N=1; null otherwise)")
-    ap.add_argument("--pipeline", type=int, default=3,
+    ap.add_argument("--pipeline", type=int, default=4,
                     help="lanes of the pipelined headline (dcc_occ_submit_epoch, DCC_OPT_PIPELINE): "
                          "consecutive epochs over that many distinct resident batches overlap on "
                          "the GPU (N=1; 0 = one epoch at a time)")
