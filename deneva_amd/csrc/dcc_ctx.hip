@@ -326,7 +326,7 @@ int dcc_ctx::hist_build(HistStore& h) {
   while ((1ull << h.hbits) < 2 * h.m) h.hbits++;
   CR(h.skey.ensure(this, h.m * 8, "history keys"));
   CR(h.stn.ensure(this, h.m * 8, "history tns"));
-  CR(h.hash.ensure(this, 16ull << h.hbits, "history table"));
+  CR(h.hash.ensure(this, 32ull << h.hbits, "history table"));
   for (int q = 0; q < 2; q++) {
     CR(h_K[q].ensure(this, h.m * 8, "history sort keys"));
     CR(h_V[q].ensure(this, h.m * 4, "history sort values"));

@@ -1335,7 +1335,7 @@ int dcc_ctx::maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, 
     const char* e = DCC_ENV("DCC_MT_PREFIX");
     return e ? (uint64_t)atoll(e) : (uint64_t)MT_PREFIX;
   }();
-  if (m && prefix && n > 4 * prefix) {
+  if (m != 0 && prefix != 0 && n > 4 * prefix) {
     const uint32_t P = (uint32_t)prefix;
     uint32_t mp = 0;
     {

@@ -8,9 +8,9 @@
 // writes to the delta's flat pair array on the device (count, scan, emit: no
 // D2H of the batch), the delta is rebuilt, and it is merged into the base when
 // it outgrows a quarter of it.  A built level is its pairs sorted by (key, tn)
-// plus an open-addressing table key -> (first pair, pair count) at <= 50 %
-// load, so a window query is one probe per level and a binary search of the
-// key's run of tns.
+// plus an open-addressing table key -> (first pair, pair count, min tn, max
+// tn) at <= 50 % load, so a window query is one probe per level, and a binary
+// search of the key's run of tns only when the window lies inside the run.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -25,11 +25,35 @@ __host__ __device__ inline uint64_t hist_hash_slot(uint64_t key, uint32_t bits) 
 namespace dcc {
 
 struct HistLevel {
-  const uint64_t* hash;  // [2 << hbits]: key, first | count << 32 (DCC_KEY_RESERVED = empty)
+  const uint64_t* hash;  // [4 << hbits]: HistSlot per slot (key DCC_KEY_RESERVED = empty)
   const uint64_t* tn;    // [m] tns, ascending within a key's run
   uint32_t hbits;
   uint32_t on;           // 0: the level is empty
 };
+// A table slot (32 B): the key, its run in the sorted pairs (first | count <<
+// 32) and the run's smallest and largest tn, so a window query resolves from
+// the slot alone unless the window lies strictly inside the run's tn range.
+struct HistSlot {
+  uint64_t key, fc, tmin, tmax;
+};
+__device__ inline HistSlot hist_slot_ld(const uint64_t* hash, uint64_t s) {
+  const ulonglong2* p = reinterpret_cast<const ulonglong2*>(hash + 4 * s);
+  const ulonglong2 a = p[0], b = p[1];
+  return HistSlot{a.x, a.y, b.x, b.y};
+}
+// does the run of a found slot hold a tn with lo < tn <= hi?
+__device__ inline bool hist_slot_hit(const HistLevel& L, const HistSlot& S, uint64_t lo, uint64_t hi) {
+  if (S.tmax <= lo || S.tmin > hi) return false;
+  if (S.tmax <= hi || S.tmin > lo) return true;  // tmax (resp. tmin) is in the window
+  const uint64_t first = (uint32_t)S.fc, end = first + (S.fc >> 32);
+  uint64_t b = first, e = end;
+  while (b < e) {  // first tn > lo
+    const uint64_t m = (b + e) >> 1;
+    if (L.tn[m] <= lo) b = m + 1;
+    else e = m;
+  }
+  return b < end && L.tn[b] <= hi;
+}
 // One-hash bitmap of every key in the history (both levels): the window
 // check loads it into LDS and probes a level's table only for keys whose bit
 // is set (most reads touch keys the history never saw).
@@ -46,24 +70,13 @@ struct HistView {
 __device__ inline bool hist_level_hit(const HistLevel& L, uint64_t key, uint64_t lo, uint64_t hi) {
   if (!L.on) return false;
   const uint64_t mask = (1ull << L.hbits) - 1;
-  uint64_t slot = hist_hash_slot(key, L.hbits), v = 0;
+  uint64_t slot = hist_hash_slot(key, L.hbits);
   for (;;) {  // <= 50 % load: every probe sequence ends at an empty slot
-    const uint64_t k2 = L.hash[2 * slot];
-    if (k2 == key) {
-      v = L.hash[2 * slot + 1];
-      break;
-    }
-    if (k2 == DCC_KEY_RESERVED) return false;
+    const HistSlot S = hist_slot_ld(L.hash, slot);
+    if (S.key == key) return hist_slot_hit(L, S, lo, hi);
+    if (S.key == DCC_KEY_RESERVED) return false;
     slot = (slot + 1) & mask;
   }
-  const uint64_t first = (uint32_t)v, end = first + (v >> 32);
-  uint64_t b = first, e = end;
-  while (b < e) {  // first tn > lo
-    const uint64_t m = (b + e) >> 1;
-    if (L.tn[m] <= lo) b = m + 1;
-    else e = m;
-  }
-  return b < end && L.tn[b] <= hi;
 }
 __device__ inline bool hist_hit(const HistView& h, uint64_t key, uint64_t lo, uint64_t hi) {
   return hist_level_hit(h.lv[1], key, lo, hi) || hist_level_hit(h.lv[0], key, lo, hi);
@@ -89,7 +102,7 @@ struct HistBuild {
   uint32_t* scratch;
   uint64_t* skey;       // out: sorted keys
   uint64_t* stn;        // out: sorted tns
-  uint64_t* hash;       // out: [2 << hbits]
+  uint64_t* hash;       // out: [4 << hbits]
   uint32_t hbits;
   uint32_t kbits, tbits;  // significant bits of the keys / tns (radix passes)
 };

@@ -307,26 +307,29 @@ __global__ __launch_bounds__(256) void k_hist_heads(const uint64_t* skey, uint64
     if (i > 0 && skey[i - 1] == key) continue;
     uint64_t s = hist_hash_slot(key, hbits);
     for (;;) {
-      const unsigned long long prev = atomicCAS((unsigned long long*)&hash[2 * s],
+      const unsigned long long prev = atomicCAS((unsigned long long*)&hash[4 * s],
                                                 (unsigned long long)DCC_KEY_RESERVED,
                                                 (unsigned long long)key);
       if (prev == DCC_KEY_RESERVED) break;
       s = (s + 1) & mask;  // keys are unique here: a taken slot is another key's
     }
-    hash[2 * s + 1] = i;
+    hash[4 * s + 1] = i;
   }
 }
-// the last pair of each run completes its slot: count = last + 1 - first
-__global__ __launch_bounds__(256) void k_hist_tails(const uint64_t* skey, uint64_t m,
+// the last pair of each run completes its slot: count = last + 1 - first,
+// and the run's tn range
+__global__ __launch_bounds__(256) void k_hist_tails(const uint64_t* skey, const uint64_t* stn, uint64_t m,
                                                     uint64_t* hash, uint32_t hbits) {
   const uint64_t mask = (1ull << hbits) - 1;
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < m; i += (uint64_t)gridDim.x * 256) {
     const uint64_t key = skey[i];
     if (i + 1 < m && skey[i + 1] == key) continue;
     uint64_t s = hist_hash_slot(key, hbits);
-    while (hash[2 * s] != key) s = (s + 1) & mask;
-    const uint64_t first = hash[2 * s + 1];
-    hash[2 * s + 1] = first | ((i + 1 - first) << 32);
+    while (hash[4 * s] != key) s = (s + 1) & mask;
+    const uint64_t first = hash[4 * s + 1];
+    hash[4 * s + 1] = first | ((i + 1 - first) << 32);
+    hash[4 * s + 2] = stn[first];
+    hash[4 * s + 3] = stn[i];
   }
 }
 
@@ -357,9 +360,9 @@ int hist_build_level(const HistBuild& b, hipStream_t st) {
     r = 0;
   }
   k_hist_gather<<<hgrid(b.m), 256, 0, st>>>(K[r], V[r], b.ft, b.m, b.skey, b.stn);
-  if (hipMemsetAsync(b.hash, 0xFF, (16ull << b.hbits), st) != hipSuccess) return -1;
+  if (hipMemsetAsync(b.hash, 0xFF, (32ull << b.hbits), st) != hipSuccess) return -1;
   k_hist_heads<<<hgrid(b.m), 256, 0, st>>>(b.skey, b.m, b.hash, b.hbits);
-  k_hist_tails<<<hgrid(b.m), 256, 0, st>>>(b.skey, b.m, b.hash, b.hbits);
+  k_hist_tails<<<hgrid(b.m), 256, 0, st>>>(b.skey, b.stn, b.m, b.hash, b.hbits);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

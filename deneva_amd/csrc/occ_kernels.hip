@@ -56,31 +56,23 @@ __global__ __launch_bounds__(256) void k_prep(const uint32_t* __restrict__ off, 
 // and made monotone; a malformed batch is reported.
 constexpr uint32_t HIST_WAVES = 16;
 constexpr uint32_t HIST_U = 4;  // accesses per lane in flight
-// first step of a level probe for U keys at once: the key's home slot (16 B:
-// key, first | count << 32); the rest of the walk (a collision, the tn run's
-// binary search) follows per key
+// the rest of a level probe whose home slot S is already loaded (a collision
+// walk, then the run's tn range)
 __device__ inline bool hist_level_hit_from(const HistLevel& L, uint64_t key, uint64_t lo, uint64_t hi,
-                                           uint64_t slot, uint64_t k2, uint64_t v) {
+                                           uint64_t slot, HistSlot S) {
   const uint64_t mask = (1ull << L.hbits) - 1;
-  while (k2 != key) {
-    if (k2 == DCC_KEY_RESERVED) return false;
+  while (S.key != key) {
+    if (S.key == DCC_KEY_RESERVED) return false;
     slot = (slot + 1) & mask;
-    k2 = L.hash[2 * slot];
-    v = L.hash[2 * slot + 1];
+    S = hist_slot_ld(L.hash, slot);
   }
-  const uint64_t first = (uint32_t)v, end = first + (v >> 32);
-  uint64_t b = first, e = end;
-  while (b < e) {  // first tn > lo
-    const uint64_t m = (b + e) >> 1;
-    if (L.tn[m] <= lo) b = m + 1;
-    else e = m;
-  }
-  return b < end && L.tn[b] <= hi;
+  return hist_slot_hit(L, S, lo, hi);
 }
 __global__ __launch_bounds__(HIST_WAVES * 64) void k_hist(HistArgs a) {
   __shared__ uint32_t s_bm[(1u << HIST_BM_LOG) / 32];
   __shared__ uint32_t s_o[HIST_WAVES][65];
   __shared__ uint64_t s_lo[HIST_WAVES][64], s_hi[HIST_WAVES][64];
+  __shared__ uint8_t s_dead[HIST_WAVES][64];  // txn already found aborted: its other reads are moot
   const HistView hv = a.dyn->view;  // by value: registers, not a reload per probe
   for (uint32_t i = threadIdx.x; i < (1u << HIST_BM_LOG) / 32; i += HIST_WAVES * 64)
     s_bm[i] = hv.bm ? hv.bm[i] : ~0u;
@@ -99,6 +91,7 @@ __global__ __launch_bounds__(HIST_WAVES * 64) void k_hist(HistArgs a) {
   }
   s_lo[w][lane] = lo;
   s_hi[w][lane] = hi;
+  s_dead[w][lane] = 0;
   uint32_t ov = lane <= nt ? (uint32_t)min<uint64_t>(a.off[t0 + lane], a.nnz) : 0u;
   for (int d = 1; d < 64; d <<= 1) {
     const uint32_t y = __shfl_up(ov, d);
@@ -137,7 +130,7 @@ __global__ __launch_bounds__(HIST_WAVES * 64) void k_hist(HistArgs a) {
           else h = mid;
         }
         txn[u] = l;
-        want[u] = s_hi[w][l] > s_lo[w][l];
+        want[u] = s_hi[w][l] > s_lo[w][l] && !s_dead[w][l];
       }
     }
     // level by level: the home slots of every wanted key loaded together
@@ -145,23 +138,25 @@ __global__ __launch_bounds__(HIST_WAVES * 64) void k_hist(HistArgs a) {
     for (int q = 1; q >= 0; q--) {
       const HistLevel& L = hv.lv[q];
       if (!L.on) continue;
-      uint64_t slot[HIST_U], k2[HIST_U], v[HIST_U];
+      uint64_t slot[HIST_U];
+      HistSlot S[HIST_U];
 #pragma unroll
       for (uint32_t u = 0; u < HIST_U; u++) {
         slot[u] = hist_hash_slot(key[u], L.hbits);
-        k2[u] = want[u] ? L.hash[2 * slot[u]] : DCC_KEY_RESERVED;
-        v[u] = want[u] ? L.hash[2 * slot[u] + 1] : 0;
+        S[u] = want[u] ? hist_slot_ld(L.hash, slot[u]) : HistSlot{DCC_KEY_RESERVED, 0, 0, 0};
       }
 #pragma unroll
       for (uint32_t u = 0; u < HIST_U; u++) {
         if (!want[u]) continue;
         const uint32_t l = txn[u];
-        if (hist_level_hit_from(L, key[u], s_lo[w][l], s_hi[w][l], slot[u], k2[u], v[u])) {
+        if (hist_level_hit_from(L, key[u], s_lo[w][l], s_hi[w][l], slot[u], S[u])) {
           a.state[t0 + l] = ST_ABORT;
+          s_dead[w][l] = 1;
           want[u] = false;  // decided: the other level need not be probed
         }
       }
     }
+    __builtin_amdgcn_wave_barrier();
   }
 }
 

@@ -33,9 +33,9 @@ def main():
     db = b.to_torch("cuda:0")
     rc = torch.empty(n, dtype=torch.uint8, device="cuda:0")
     tn = torch.empty(n, dtype=torch.int64, device="cuda:0")
-    eng = d.Engine(0)
     for var in [int(v) for v in (sys.argv[1:] or ["0", "1", "2", "4"])]:
         os.environ["DCC_HIST_VAR"] = str(var)
+        eng = d.Engine(0)  # a fresh context: the epoch graph is captured with this variant
         ms = []
         for i in range(8):
             eng.history_clear()
@@ -47,6 +47,7 @@ def main():
                 ms.append(st["device_ms"])
         par = bool(np.array_equal(rc.cpu().numpy(), erc))
         print(f"DCC_HIST_VAR={var}: device {np.median(ms):.4f} ms, parity {par}", flush=True)
+        eng.close()
 
 
 if __name__ == "__main__":
