@@ -43,10 +43,13 @@ struct dcc_multi;       // single-process multi-GPU context (dcc_multi.cpp)
 // One level of the device OCC history (occ_history.h): flat (key, tn) pairs in
 // append order and, once built, the pairs sorted by (key, tn) with the key
 // table.
+// The delta level is chained instead (occ_history.h HistInsert): its table
+// takes each pair as it is appended, so an epoch's append needs no rebuild.
 struct HistStore {
   DevBuf fk, ft;            // flat pairs
   DevBuf skey, stn, hash;   // built level
   DevBuf bm;                // key bitmap of the built level (occ_history.h HIST_BM_LOG)
+  DevBuf nx, tcnt;          // chained: next pair of the same key; claims / overflow counters
   uint64_t m = 0;           // pairs
   uint32_t hbits = 0;
   bool built = true;        // the built level matches the flat pairs
@@ -54,6 +57,22 @@ struct HistStore {
   uint64_t max_tn = 0;      // largest tn appended
   uint64_t min_tn = ~0ull;  // smallest tn appended
   uint64_t max_key = 0;     // largest key appended (radix passes of the build)
+  bool chained = false;     // the delta level
+  bool tvalid = false;      // chained: the table holds exactly the first `ins` pairs
+  uint64_t ins = 0;         // chained: pairs inserted
+  uint64_t last_app = 0;    // chained: pairs the last epoch appended (table headroom)
+  bool overflowed = false;  // chained: the table ran out of room (rebuilt twice as big)
+  // empty the level, keeping its buffers
+  void reset() {
+    m = 0;
+    built = true;
+    mono = true;
+    max_tn = 0;
+    min_tn = ~0ull;
+    max_key = 0;
+    tvalid = false;
+    ins = 0;
+  }
 };
 
 // One OCC (sub-)batch: txn i has accesses [off[i], off[i+1]) of keys/acctype
@@ -137,7 +156,7 @@ struct dcc_ctx {
   // HDYN_TOTALS, written by the device); pinned
   void* hdyn = nullptr;
   void* hdyn_dev = nullptr;
-  static constexpr size_t HDYN_TOTALS = 128;
+  static constexpr size_t HDYN_TOTALS = 256, HDYN_BYTES = 512;
 
   // device workspaces (grow-only)
   DevBuf misc;                                   // counters / error words
@@ -162,6 +181,7 @@ struct dcc_ctx {
   uint64_t hist_merge_min = 65536;  // DCC_OPT_HIST_MERGE
   DevBuf h_K[2], h_V[2], h_scr, h_bsum;          // level-build sort buffers, append scan
   DevBuf h_bm;                                   // key bitmap of both levels (window check)
+  bool h_bm_stale = true;                        // h_bm is not B.bm | D.bm
   DevBuf perm, calvin_a, calvin_b, calvin_c, calvin_d;  // Calvin workspaces
   DevBuf cv_scratch, cv_agg, cv_group, cv_wave, cv_pgx, cv_gsx, cv_gsize, cv_done, cv_maxl;
   DevBuf cv_seq_b, cv_ok, cv_len, cv_off2, cv_tsum, cv_hkeys, cv_hat;
@@ -170,6 +190,8 @@ struct dcc_ctx {
   DevBuf mt_rk;                                  // MaaT row table: 32-B {key, last read, last write} slots
   uint32_t mt_bits = 0;                          // log2 row-table slots (0: none yet)
   uint64_t mt_rows = 0;                          // rows in the table
+  uint64_t mt_new_last = 0;                      // rows the last epoch added (table sizing)
+  uint64_t mt_full_redo = 0;                     // epochs run again on a bigger row table
   uint32_t mt_rows32 = 0;                        // upload source of the row counter
   DevBuf mt_misc, mt_slot, mt_sval, mt_slot2, mt_sval2, mt_sfl, mt_stx, mt_txn, mt_agg;
   DevBuf mt_sflB, mt_stxB, mt_k1, mt_tcnt, mt_ul;
@@ -201,6 +223,8 @@ struct dcc_ctx {
   // device history (occ_history.h / dcc_ctx.hip)
   uint64_t hist_size() const { return hs[0].m + hs[1].m; }
   int hist_grow_flat(HistStore& h, uint64_t need);
+  int hist_build_chained(HistStore& h);
+  dcc::HistInsert hist_insert_args(HistStore& h);
   void hist_note(HistStore& h, uint64_t lo_tn, uint64_t hi_tn);
   int hist_build(HistStore& h);
   int hist_prepare();  // merge policy + rebuild: call before a window check
@@ -273,6 +297,8 @@ struct dcc_ctx {
   int maat_rows_reserve(uint64_t want);
   int index_reserve(uint64_t want);
   int maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, dcc_stats* st);
+  int maat_epoch_try(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, dcc_stats* st, bool all_rows,
+                     bool* full);
   int calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint32_t* out_group,
                    uint8_t* out_rc, uint32_t* out_wave, dcc_stats* st);
   // device-side key-shard partition (shard_dev.hip): rank `rank` of R of a

@@ -12,6 +12,7 @@
 
 #include "dcc.h"
 #include "dcc_ctx.h"
+#include "dcc_env.h"
 #include "radix_sort.h"
 #include "dcc_device.h"
 #include "occ_kernels.h"
@@ -136,9 +137,10 @@ extern "C" int dcc_init(dcc_ctx** out, int device_id) {
   CK(hipHostMalloc((void**)&ctx->hpart, 1 << 17, hipHostMallocDefault));
   CK(hipHostGetDevicePointer(&ctx->hmisc_dev, ctx->hmisc, 0));
   CK(hipHostGetDevicePointer(&ctx->hpart_dev, ctx->hpart, 0));
-  CK(hipHostMalloc((void**)&ctx->hdyn, 256, hipHostMallocDefault));
+  ctx->hs[1].chained = true;  // the delta level (dcc_ctx.h HistStore)
+  CK(hipHostMalloc((void**)&ctx->hdyn, dcc_ctx::HDYN_BYTES, hipHostMallocDefault));
   CK(hipHostGetDevicePointer(&ctx->hdyn_dev, ctx->hdyn, 0));
-  memset(ctx->hdyn, 0, 256);
+  memset(ctx->hdyn, 0, dcc_ctx::HDYN_BYTES);
   int rc = ctx->misc.ensure(ctx, 16384, "misc");
   if (!rc) rc = ctx->part.ensure(ctx, 1 << 17, "partials");
   // counters and barrier words start zeroed (hipMalloc memory is not)
@@ -261,7 +263,7 @@ std::vector<DevBuf*> dcc_ctx::all_bufs() {
                             &nar_keys, &nar_at, &nar_tn, &fin_off, &fin_keys, &fin_at, &fin_state, &fin_hasw, &fin_rc, &fin_cnt,
                             &sh_off, &sh_keys, &sh_at, &sh_src, &sh_cnt, &sh_bsum, &sh_rc, &sh_tn, &sh_grp};
   for (auto& h : hs)
-    for (DevBuf* b : {&h.fk, &h.ft, &h.skey, &h.stn, &h.hash, &h.bm}) v.push_back(b);
+    for (DevBuf* b : {&h.fk, &h.ft, &h.skey, &h.stn, &h.hash, &h.bm, &h.nx, &h.tcnt}) v.push_back(b);
   for (auto& sb : sw_list)
     for (DevBuf* b : {&sb.tid, &sb.off, &sb.keys, &sb.acctype, &sb.state}) v.push_back(b);
   for (int i = 0; i < 2; i++) {
@@ -293,12 +295,16 @@ extern "C" int dcc_reserve(dcc_ctx* ctx, uint64_t max_txn, uint64_t max_nnz) {
 // into the delta level's flat pairs, epochs append there on the device.
 int dcc_ctx::hist_grow_flat(HistStore& h, uint64_t need) {
   dcc_ctx* ctx = this;
-  if (need * 8 <= h.fk.cap && need * 8 <= h.ft.cap) return DCC_OK;
+  if (need * 8 <= h.fk.cap && need * 8 <= h.ft.cap && (!h.chained || need * 4 <= h.nx.cap)) return DCC_OK;
+  if (h.chained && need >= HIST_NIL) return fail(DCC_ENOMEM, "history delta level of %llu pairs",
+                                                 (unsigned long long)need);
   const uint64_t want = std::max<uint64_t>(need + need / 2, 4096);
-  for (DevBuf* b : {&h.fk, &h.ft}) {
+  for (DevBuf* b : {&h.fk, &h.ft, &h.nx}) {
+    if (b == &h.nx && !h.chained) continue;
+    const uint64_t w = b == &h.nx ? 4 : 8;
     DevBuf nb;
-    CR(nb.ensure(this, want * 8, "history pairs"));
-    if (h.m) CK(hipMemcpyAsync(nb.p, b->p, h.m * 8, hipMemcpyDeviceToDevice, stream));
+    CR(nb.ensure(this, want * w, "history pairs"));
+    if (h.m) CK(hipMemcpyAsync(nb.p, b->p, h.m * w, hipMemcpyDeviceToDevice, stream));
     CK(hipStreamSynchronize(stream));
     b->release();
     *b = nb;
@@ -322,8 +328,14 @@ int dcc_ctx::hist_build(HistStore& h) {
     h.mono = true;
     return DCC_OK;
   }
+  // table load <= 1 / this: 1/4 keeps the window check's collision walks
+  // short (experiments: DCC_HIST_SLOTS)
+  static const uint64_t slots_per_pair = [] {
+    const char* e = DCC_ENV("DCC_HIST_SLOTS");
+    return e && atoi(e) >= 2 ? (uint64_t)atoi(e) : 4ull;
+  }();
   h.hbits = 4;
-  while ((1ull << h.hbits) < 2 * h.m) h.hbits++;
+  while ((1ull << h.hbits) < slots_per_pair * h.m) h.hbits++;
   CR(h.skey.ensure(this, h.m * 8, "history keys"));
   CR(h.stn.ensure(this, h.m * 8, "history tns"));
   CR(h.hash.ensure(this, 32ull << h.hbits, "history table"));
@@ -353,12 +365,59 @@ int dcc_ctx::hist_build(HistStore& h) {
   return DCC_OK;
 }
 
+// The chained delta: its table sized for a quarter load with the level plus
+// one more epoch like the last (an insert that walks past HIST_WALK flags an
+// overflow, and the table is rebuilt bigger from the flat pairs), then the
+// pairs not yet in it.
+HistInsert dcc_ctx::hist_insert_args(HistStore& h) {
+  return HistInsert{(const uint64_t*)h.fk.p, (const uint64_t*)h.ft.p, (uint64_t*)h.hash.p,
+                    (uint32_t*)h.nx.p, (uint32_t*)h.bm.p, (uint32_t*)h_bm.p, (uint32_t*)h.tcnt.p,
+                    h.hbits, 0u};
+}
+
+int dcc_ctx::hist_build_chained(HistStore& h) {
+  dcc_ctx* ctx = this;
+  uint64_t need = std::max<uint64_t>(65536, 4 * (h.m + h.last_app));
+  if (h.overflowed) need = std::max<uint64_t>(need, 4ull << h.hbits);  // it ran out of room: grow
+  if (!h.tvalid || (2ull << h.hbits) < need) {
+    uint32_t hb = 4;
+    while ((1ull << hb) < need) hb++;
+    CR(h.hash.ensure(this, 32ull << hb, "history delta table"));
+    CR(h.bm.ensure(this, (1u << HIST_BM_LOG) / 8, "history key bitmap"));
+    CR(h.tcnt.ensure(this, 16, "history delta overflow flag"));
+    CK(hipMemsetAsync(h.hash.p, 0xFF, 32ull << hb, stream));
+    CK(hipMemsetAsync(h.bm.p, 0, (1u << HIST_BM_LOG) / 8, stream));
+    CK(hipMemsetAsync(h.tcnt.p, 0, 16, stream));
+    h.hbits = hb;
+    h.ins = 0;
+    h.tvalid = true;
+    h.overflowed = false;
+    h_bm_stale = true;  // the union loses the old table's bits
+  }
+  if (h.ins < h.m) {
+    launch_hist_insert(hist_insert_args(h), h.ins, h.m, stream);
+    CK(hipGetLastError());
+    h.ins = h.m;
+    // a host-side insert's overflow is seen here (the epochs' in their totals)
+    CK(hipMemcpyAsync(hmisc, h.tcnt.p, 4, hipMemcpyDeviceToHost, stream));
+    CK(hipStreamSynchronize(stream));
+    if (*(const uint32_t*)hmisc) {
+      h.tvalid = false;
+      h.overflowed = true;
+      return hist_build_chained(h);
+    }
+  }
+  h.built = true;
+  return DCC_OK;
+}
+
 // Merge the delta into the base once it outgrows a quarter of it (or 64K
 // pairs), then rebuild whatever changed.
 int dcc_ctx::hist_prepare() {
   dcc_ctx* ctx = this;
   HistStore& B = hs[0];
   HistStore& D = hs[1];
+  CR(h_bm.ensure(this, (1u << HIST_BM_LOG) / 8, "history key bitmap"));
   if (D.m > std::max<uint64_t>(hist_merge_min, B.m / 4)) {
     CR(hist_grow_flat(B, B.m + D.m));
     CK(hipMemcpyAsync((uint64_t*)B.fk.p + B.m, D.fk.p, D.m * 8, hipMemcpyDeviceToDevice, stream));
@@ -370,16 +429,16 @@ int dcc_ctx::hist_prepare() {
     B.min_tn = std::min(B.min_tn, D.min_tn);
     B.max_key = std::max(B.max_key, D.max_key);
     B.built = false;
-    D = HistStore{D.fk, D.ft, D.skey, D.stn, D.hash, D.bm};  // buffers kept, level emptied
+    D.reset();  // buffers kept, level emptied
   }
-  const bool rebuilt = !B.built || !D.built;
+  if (!B.built) h_bm_stale = true;
   CR(hist_build(B));
-  CR(hist_build(D));
-  if (rebuilt || !h_bm.p) {
-    CR(h_bm.ensure(this, (1u << HIST_BM_LOG) / 8, "history key bitmap"));
-    launch_hist_bm_or(B.m ? (const uint32_t*)B.bm.p : nullptr, D.m ? (const uint32_t*)D.bm.p : nullptr,
-                      (uint32_t*)h_bm.p, stream);
+  CR(hist_build_chained(D));
+  if (h_bm_stale) {
+    launch_hist_bm_or(B.m ? (const uint32_t*)B.bm.p : nullptr, (const uint32_t*)D.bm.p, (uint32_t*)h_bm.p,
+                      stream);
     CK(hipGetLastError());
+    h_bm_stale = false;
   }
   return DCC_OK;
 }
@@ -388,8 +447,11 @@ HistView dcc_ctx::hist_view() const {
   HistView v{};
   for (int q = 0; q < 2; q++) {
     const HistStore& h = hs[q];
-    v.lv[q] = HistLevel{(const uint64_t*)h.hash.p, (const uint64_t*)h.stn.p, h.hbits,
-                        h.m && h.built ? 1u : 0u};
+    v.lv[q] = h.chained ? HistLevel{(const uint64_t*)h.hash.p, (const uint64_t*)h.ft.p,
+                                    (const uint32_t*)h.nx.p, h.hbits,
+                                    h.m && h.tvalid && h.ins == h.m ? 1u : 0u}
+                        : HistLevel{(const uint64_t*)h.hash.p, (const uint64_t*)h.stn.p, nullptr, h.hbits,
+                                    h.m && h.built ? 1u : 0u};
   }
   v.bm = (const uint32_t*)h_bm.p;  // set by hist_prepare
   return v;
@@ -469,14 +531,7 @@ extern "C" int dcc_occ_history_clear(dcc_ctx* ctx) {
   dcc_pipe_drain(ctx);
   if (ctx->multi)
     for (int r = 0; r < dcc_multi_size(ctx); r++) dcc_occ_history_clear(dcc_multi_sub(ctx, r));
-  for (HistStore& h : ctx->hs) {
-    h.m = 0;
-    h.max_tn = 0;
-    h.min_tn = ~0ull;
-    h.max_key = 0;
-    h.mono = true;
-    h.built = true;
-  }
+  for (HistStore& h : ctx->hs) h.reset();
   return DCC_OK;
 }
 
@@ -518,11 +573,7 @@ extern "C" int dcc_occ_history_trim(dcc_ctx* ctx, uint64_t tn_floor) {
   D.max_key = 0;
   B.mono = false;  // the compaction does not keep the order
   B.built = false;
-  D.m = 0;
-  D.max_tn = 0;
-  D.min_tn = ~0ull;
-  D.mono = true;
-  D.built = true;
+  D.reset();
   ctx->buf_gen++;
   return DCC_OK;
 }

@@ -82,12 +82,15 @@ struct __attribute__((aligned(32))) MtSlot {
 static_assert(sizeof(MtSlot) == 32, "row slot");
 // insert-or-find the row of `key` (ins: this call created it); its lr / lw
 // stay 0 until an epoch commits
+// (a walk past MT_WALK slots reports MT_ERR_FULL: the host grows the table
+// and runs the epoch again)
+constexpr uint64_t MT_WALK = 256;
 __device__ inline uint32_t mt_row(MtSlot* rt, uint32_t bits, uint64_t key, bool& ins,
                                   uint32_t* err) {
   const uint64_t mask = (1ull << bits) - 1;
   uint64_t s = mt_hash(key, bits);
   ins = false;
-  for (uint64_t q = 0; q <= mask; q++) {
+  for (uint64_t q = 0; q <= mask && q < MT_WALK; q++) {
     const uint64_t v = rt[s].key;
     if (v == key) return (uint32_t)s;
     if (v == DCC_KEY_RESERVED) {
@@ -809,10 +812,14 @@ struct FinArgs {
   uint8_t* rc;
   uint64_t* cts_out;
   uint32_t* cnt;  // [0] commits, [1] undecided, [2] write accesses
+  const uint32_t* err;
 };
 __global__ __launch_bounds__(256) void k_mt_finish(FinArgs a) {
   __shared__ uint32_t sh[3][4];
   uint32_t com = 0, und = 0, nw = 0;
+  // a full row table left some accesses without their row: the epoch runs
+  // again on a bigger table, and this one's timestamps must not land anywhere
+  const bool keep = (*(volatile const uint32_t*)a.err & MT_ERR_FULL) == 0;
   for (uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x; t < a.n; t += (uint64_t)gridDim.x * 256) {
     const uint8_t s = a.state[t];
     const bool ok = s == ST_COM;
@@ -825,7 +832,7 @@ __global__ __launch_bounds__(256) void k_mt_finish(FinArgs a) {
     for (uint64_t x = o0; x < o1; x++) {
       const uint8_t ty = a.at[x];
       nw += ty == DCC_WR;
-      if (!ok) continue;
+      if (!ok || !keep) continue;
       const uint32_t sl = a.slot[x];
       if (a.rw_all || ty == DCC_RD) atomicMax((unsigned long long*)&a.rt[sl].lr, c);
       if (a.rw_all || ty == DCC_WR) atomicMax((unsigned long long*)&a.rt[sl].lw, c);
@@ -1119,22 +1126,44 @@ int dcc_ctx::maat_rows_reserve(uint64_t want) {
   DevBuf nt;
   CR(nt.ensure(this, cap * sizeof(MtSlot), "maat row table"));
   k_mt_clear<<<g1(cap, 16384), 256, 0, stream>>>((MtSlot*)nt.p, cap);
-  CK(hipMemsetAsync(cnt, 0, 4, stream));
+  CK(hipMemsetAsync(cnt, 0, 8, stream));
   if (mt_bits) {
     const uint64_t ocap = 1ull << mt_bits;
     k_mt_rehash<<<g1(ocap), 256, 0, stream>>>((const MtSlot*)mt_rk.p, ocap, (MtSlot*)nt.p, bits, cnt,
                                               cnt + 1);
   }
   CK(hipGetLastError());
+  CK(hipMemcpyAsync(hmisc, cnt + 1, 4, hipMemcpyDeviceToHost, stream));
   CK(hipStreamSynchronize(stream));
   mt_rk.release();
   mt_rk = nt;
   mt_bits = bits;
+  if (*(const uint32_t*)hmisc & MT_ERR_FULL) {  // a rehash walk ran past MT_WALK: bigger still
+    CK(hipMemsetAsync(cnt + 1, 0, 4, stream));
+    return maat_rows_reserve(2 * want);
+  }
   return DCC_OK;
 }
 
+// The row table is sized for the rows the epoch is expected to add (the last
+// epoch's count with a quarter of headroom, a quarter of the accesses the
+// first time) instead of one row per access: at the headline 3.3 M distinct
+// rows of 16.7 M accesses that is a 256-MB table instead of 1 GB.  An epoch
+// that finds it full runs again on a table sized for every access.
 int dcc_ctx::maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, dcc_stats* st) {
+  bool full = false;
+  const int e = maat_epoch_try(b, out_rc, out_cts, st, false, &full);
+  if (e != DCC_OK || !full) return e;
+  mt_full_redo++;
+  const int e2 = maat_epoch_try(b, out_rc, out_cts, st, true, &full);
+  if (e2 == DCC_OK && full) return fail(DCC_EIO, "maat: row table full");
+  return e2;
+}
+
+int dcc_ctx::maat_epoch_try(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, dcc_stats* st,
+                            bool all_rows, bool* full) {
   dcc_ctx* ctx = this;
+  *full = false;
   const auto t_wall0 = std::chrono::steady_clock::now();
   CR(check_batch(b));
   if (comm_ranks() > 1) return fail(DCC_ENOTSUP, "maat: single-GPU engine");
@@ -1154,7 +1183,11 @@ int dcc_ctx::maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, 
   uint32_t* cnt = (uint32_t*)mt_misc.p;  // [0] rows, [1] err, [2..4] finish counts, ring at 8
   uint32_t* ring = cnt + 8;
   // the row counter survives between epochs in mt_rows (host copy)
-  CR(maat_rows_reserve(mt_rows + m));
+  {
+    const uint64_t est = mt_new_last ? mt_new_last + mt_new_last / 4 + 4096 : m / 4 + 4096;
+    CR(maat_rows_reserve(mt_rows + (all_rows ? m : std::min<uint64_t>(m, est))));
+  }
+  const uint64_t rows_before = mt_rows;
   mt_rows32 = (uint32_t)mt_rows;
   CK(hipMemcpyAsync(cnt, &mt_rows32, 4, hipMemcpyHostToDevice, stream));
   CK(hipMemsetAsync(cnt + 1, 0, 4 * 7 + MT_RING * 4, stream));
@@ -1293,6 +1326,7 @@ int dcc_ctx::maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, 
       CK(hipStreamSynchronize(stream));
       const uint32_t* hr = (const uint32_t*)hmisc;
       if (hr[MT_RING + 1] & MT_ERR_SPIN) return fail(DCC_EIO, "maat: round scan look-back timed out");
+      if (hr[MT_RING + 1] & MT_ERR_FULL) return DCC_OK;  // the epoch runs again (maat_epoch)
       if (mt_debug)  // DCC_MT_DEBUG: undecided txns after each round, scan length
         for (uint32_t q = k0; q < rounds; q++)
           fprintf(stderr, "maat round %u: undecided %u, scan positions %llu\n", q + 1, hr[q % MT_RING],
@@ -1412,7 +1446,7 @@ int dcc_ctx::maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, 
     CR(solve(m, nullptr, nullptr, n, 0));
   }
   FinArgs fa{n, m, d.off, d.acctype, rw_all, state, cts, (const uint32_t*)mt_slot.p,
-             (MtSlot*)mt_rk.p, rc_dev, cts_dev, cnt + 2};
+             (MtSlot*)mt_rk.p, rc_dev, cts_dev, cnt + 2, cnt + 1};
   k_mt_finish<<<g1(n, 2048), 256, 0, stream>>>(fa);
   CK(hipGetLastError());
   CK(hipEventRecord(ev1, stream));
@@ -1426,9 +1460,13 @@ int dcc_ctx::maat_epoch(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_cts, 
   mt_rows = hc[0];  // rows inserted this epoch stay in the table whatever follows
   if (hc[1] & MT_ERR_OFF) return fail(DCC_EINVAL, "batch: malformed offsets");
   if (hc[1] & MT_ERR_KEY) return fail(DCC_EINVAL, "batch: key equal to DCC_KEY_RESERVED");
-  if (hc[1] & MT_ERR_FULL) return fail(DCC_EIO, "maat: row table full");
+  if (hc[1] & MT_ERR_FULL) {
+    *full = true;
+    return DCC_OK;
+  }
   if (hc[1] & MT_ERR_SPIN) return fail(DCC_EIO, "maat: round scan look-back timed out");
   if (hc[3]) return fail(DCC_EIO, "maat: %u undecided transactions", hc[3]);
+  mt_new_last = mt_rows - rows_before;
   float ms = 0;
   CK(hipEventElapsedTime(&ms, ev0, ev1));
   S.rounds = rounds;

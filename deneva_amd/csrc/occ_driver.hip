@@ -854,14 +854,16 @@ int dcc_ctx::occ_begin(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, bo
   // the history the window check reads (merge / level builds: launched here,
   // before any capture) and room for this epoch's append
   r.hist_on = d.start_tn && hist_size() > 0;
-  if (r.hist_on) CR(hist_prepare());
+  if (r.hist_on || r.app) CR(hist_prepare());  // an append inserts into the delta's table
   if (r.app) CR(hist_grow_flat(hs[1], hs[1].m + d.nnz));
+  static_assert(sizeof(OccDyn) <= HDYN_TOTALS, "epoch parameters overlap the totals");
   {
     OccDyn& y = *(OccDyn*)hdyn;
     y.tnc = tnc;
     y.hist_m = hs[1].m;
     y.app_k = r.app ? (uint64_t*)hs[1].fk.p : nullptr;
     y.app_t = r.app ? (uint64_t*)hs[1].ft.p : nullptr;
+    y.ins = r.app ? hist_insert_args(hs[1]) : HistInsert{};
     y.view = hist_view();
   }
   // The sweep's whole launch sequence (parameters ... central_finish) is
@@ -1334,6 +1336,14 @@ int dcc_ctx::occ_end(dcc_stats* st) {
                                         (unsigned long long)tot[1], (unsigned long long)d.nnz);
         D.m += tot[1];
         D.max_key = std::max<uint64_t>(D.max_key, tot[2]);
+        D.last_app = tot[1];
+        // the pairs went into the delta's table too, unless it ran out of room
+        // (then it is rebuilt bigger from the flat pairs before its next read)
+        if (tot[3]) {
+          D.tvalid = false;
+          D.overflowed = true;
+        }
+        else D.ins = D.m;
         hist_note(D, tnc + 1, tnc + n_cw);
       }
     }

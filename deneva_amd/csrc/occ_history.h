@@ -6,8 +6,9 @@
 // txn numbered tn.  It lives in HBM as two levels, a large `base` and a small
 // `delta` (a two-level log-structured merge): an epoch appends its committed
 // writes to the delta's flat pair array on the device (count, scan, emit: no
-// D2H of the batch), the delta is rebuilt, and it is merged into the base when
-// it outgrows a quarter of it.  A built level is its pairs sorted by (key, tn)
+// D2H of the batch) and inserts them into the delta's table in the same
+// kernel, and the delta is merged into the base when it outgrows a quarter
+// of it.  A built level is its pairs sorted by (key, tn)
 // plus an open-addressing table key -> (first pair, pair count, min tn, max
 // tn) at <= 50 % load, so a window query is one probe per level, and a binary
 // search of the key's run of tns only when the window lies inside the run.
@@ -25,27 +26,46 @@ __host__ __device__ inline uint64_t hist_hash_slot(uint64_t key, uint32_t bits) 
 namespace dcc {
 
 struct HistLevel {
-  const uint64_t* hash;  // [4 << hbits]: HistSlot per slot (key DCC_KEY_RESERVED = empty)
-  const uint64_t* tn;    // [m] tns, ascending within a key's run
+  // [2 << hbits] probe words (HistSlot per slot: key DCC_KEY_RESERVED =
+  // empty), then [2 << hbits] side words (HistSide per slot)
+  const uint64_t* hash;
+  const uint64_t* tn;    // sorted level: [m] tns, ascending within a key's run;
+                         // chained level: the flat pairs' tns
+  const uint32_t* next;  // chained level: [m] next pair of the same key (HIST_NIL ends); null: sorted
   uint32_t hbits;
   uint32_t on;           // 0: the level is empty
 };
-// A table slot (32 B): the key, its run in the sorted pairs (first | count <<
-// 32) and the run's smallest and largest tn, so a window query resolves from
-// the slot alone unless the window lies strictly inside the run's tn range.
+// A probe slot (16 B): the key and the complement of its largest tn (all-ones
+// when empty, so a chained insert lowers it with atomicMin), which answers a
+// window query unless the window ends below that tn.  The slot's side words
+// then give the smallest tn and the key's pairs: a sorted level's run (first
+// | count << 32), a chained level's most recent pair (low word), whose next[]
+// links the rest.  Chained levels keep every key within HIST_WALK slots of
+// its home (an insert that would walk further flags the table instead), so
+// their probes stop there.
 struct HistSlot {
-  uint64_t key, fc, tmin, tmax;
+  uint64_t key, ntmax;
 };
+constexpr uint32_t HIST_NIL = 0xFFFFFFFFu;
+constexpr uint32_t HIST_WALK = 64;
 __device__ inline HistSlot hist_slot_ld(const uint64_t* hash, uint64_t s) {
-  const ulonglong2* p = reinterpret_cast<const ulonglong2*>(hash + 4 * s);
-  const ulonglong2 a = p[0], b = p[1];
-  return HistSlot{a.x, a.y, b.x, b.y};
+  const ulonglong2 a = reinterpret_cast<const ulonglong2*>(hash)[s];
+  return HistSlot{a.x, a.y};
 }
-// does the run of a found slot hold a tn with lo < tn <= hi?
-__device__ inline bool hist_slot_hit(const HistLevel& L, const HistSlot& S, uint64_t lo, uint64_t hi) {
-  if (S.tmax <= lo || S.tmin > hi) return false;
-  if (S.tmax <= hi || S.tmin > lo) return true;  // tmax (resp. tmin) is in the window
-  const uint64_t first = (uint32_t)S.fc, end = first + (S.fc >> 32);
+// does the key of found slot s (largest tn tmax) have a pair with lo < tn <= hi?
+__device__ inline bool hist_found_hit(const HistLevel& L, uint64_t s, uint64_t tmax, uint64_t lo, uint64_t hi) {
+  if (tmax <= lo) return false;
+  if (tmax <= hi) return true;  // tmax is in the window
+  const ulonglong2 side = reinterpret_cast<const ulonglong2*>(L.hash + (2ull << L.hbits))[s];
+  const uint64_t fc = side.x, tmin = side.y;
+  if (tmin > hi) return false;
+  if (tmin > lo) return true;  // tmin is in the window
+  if (L.next) {  // chained: every pair of the key
+    for (uint32_t p = (uint32_t)fc; p != HIST_NIL; p = L.next[p])
+      if (L.tn[p] > lo && L.tn[p] <= hi) return true;
+    return false;
+  }
+  const uint64_t first = (uint32_t)fc, end = first + (fc >> 32);
   uint64_t b = first, e = end;
   while (b < e) {  // first tn > lo
     const uint64_t m = (b + e) >> 1;
@@ -71,12 +91,14 @@ __device__ inline bool hist_level_hit(const HistLevel& L, uint64_t key, uint64_t
   if (!L.on) return false;
   const uint64_t mask = (1ull << L.hbits) - 1;
   uint64_t slot = hist_hash_slot(key, L.hbits);
-  for (;;) {  // <= 50 % load: every probe sequence ends at an empty slot
+  // a sorted level is at most half full: every walk ends at an empty slot
+  for (uint32_t i = 0; !L.next || i < HIST_WALK; i++) {
     const HistSlot S = hist_slot_ld(L.hash, slot);
-    if (S.key == key) return hist_slot_hit(L, S, lo, hi);
+    if (S.key == key) return hist_found_hit(L, slot, ~S.ntmax, lo, hi);
     if (S.key == DCC_KEY_RESERVED) return false;
     slot = (slot + 1) & mask;
   }
+  return false;
 }
 __device__ inline bool hist_hit(const HistView& h, uint64_t key, uint64_t lo, uint64_t hi) {
   return hist_level_hit(h.lv[1], key, lo, hi) || hist_level_hit(h.lv[0], key, lo, hi);
@@ -91,6 +113,47 @@ void launch_hist_count(uint64_t n, const uint32_t* off, const uint8_t* acctype, 
 void launch_hist_emit(uint64_t n, const uint32_t* off, const uint64_t* keys, const uint8_t* acctype,
                       uint64_t nnz, const uint64_t* tn, const uint32_t* bsum, uint64_t* out_k,
                       uint64_t* out_t, unsigned long long* kmax, hipStream_t st);
+// chained (delta) level: insert flat pairs [from, to) into the table (the
+// pair's key slot found or claimed within HIST_WALK of home, else *over set
+// and the pair left out: the host rebuilds the table bigger before it is
+// read again; tmin / ~tmax lowered; the pair pushed on the key's list) and
+// the key bitmaps.  No atomic here returns a value but the claim and the push.
+struct HistInsert {
+  const uint64_t* fk;
+  const uint64_t* ft;
+  uint64_t* hash;
+  uint32_t* next;
+  uint32_t* bm_level;
+  uint32_t* bm_all;
+  uint32_t* over;  // [0] overflow flag, [1] k_fin_insert's finished workgroups
+  uint32_t hbits, pad;
+};
+__device__ inline void hist_insert(const HistInsert& h, uint64_t p, uint64_t key, uint64_t tn) {
+  const uint64_t mask = (1ull << h.hbits) - 1;
+  uint64_t s = hist_hash_slot(key, h.hbits);
+  for (uint32_t i = 0;; i++) {
+    if (i == HIST_WALK) {
+      atomicOr(h.over, 1u);
+      return;
+    }
+    unsigned long long* ks = (unsigned long long*)&h.hash[2 * s];
+    unsigned long long k = *(volatile unsigned long long*)ks;
+    if (k == DCC_KEY_RESERVED) {
+      k = atomicCAS(ks, (unsigned long long)DCC_KEY_RESERVED, (unsigned long long)key);
+      if (k == DCC_KEY_RESERVED) k = key;
+    }
+    if (k == key) break;
+    s = (s + 1) & mask;
+  }
+  unsigned long long* side = (unsigned long long*)&h.hash[(2ull << h.hbits) + 2 * s];
+  atomicMin((unsigned long long*)&h.hash[2 * s + 1], (unsigned long long)~tn);
+  atomicMin(side + 1, (unsigned long long)tn);
+  h.next[p] = atomicExch((uint32_t*)side, (uint32_t)p);
+  const uint32_t b = hist_bm_bit(key);
+  atomicOr(&h.bm_level[b >> 5], 1u << (b & 31u));
+  atomicOr(&h.bm_all[b >> 5], 1u << (b & 31u));
+}
+void launch_hist_insert(const HistInsert& h, uint64_t from, uint64_t to, hipStream_t st);
 // level build from flat pairs (fk, ft)[m]; K/V are radix-sort ping-pong buffers
 struct HistBuild {
   uint64_t m;

@@ -8,6 +8,8 @@
 // stable radix sort, so the host never copies the batch back.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "dcc_device.h"
 #include "occ_history.h"
 #include "occ_kernels.h"
@@ -16,6 +18,7 @@
 namespace dcc {
 
 constexpr uint32_t HB = 1024;  // txns per block of the append kernels
+constexpr uint32_t FIN_INSERT_WG = 512;  // k_fin_insert: the grid walks the appended pairs
 
 // committed writes of txn t (0 when it did not commit or is read-only)
 __device__ inline uint32_t hist_writes_of(uint64_t t, const uint32_t* off, const uint8_t* acctype,
@@ -227,6 +230,7 @@ __global__ __launch_bounds__(1024) void k_fin_sums(OccFinArgs a, uint64_t nb) {
     a.totals[0] = s_carry[0] - c0_base;
     a.totals[1] = s_carry[1] - c1_base;
     a.totals[2] = s_mx;
+    a.part[3 * nb + 1] = s_carry[1] - c1_base;  // the appended count, for k_fin_insert
   }
 }
 
@@ -253,12 +257,48 @@ __global__ __launch_bounds__(HB) void k_fin_apply(OccFinArgs a) {
   }
 }
 
+// the appended pairs into the delta's table (a thread per pair), then its
+// overflow flag to pinned memory by the last workgroup to finish
+__global__ __launch_bounds__(256) void k_fin_insert(OccFinArgs a, uint64_t nb) {
+  const HistInsert ins = a.dyn->ins;
+  if (!ins.hash) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.totals[3] = 0;
+    return;
+  }
+  const uint64_t p0 = a.dyn->hist_m, cnt = a.part[3 * nb + 1];
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < cnt; i += (uint64_t)gridDim.x * 256)
+    hist_insert(ins, p0 + i, ins.fk[p0 + i], ins.ft[p0 + i]);
+  __shared__ bool s_last;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    s_last = atomicAdd(&ins.over[1], 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (s_last && threadIdx.x == 0) {
+    __threadfence();
+    a.totals[3] = atomicAdd(&ins.over[0], 0u);
+    ins.over[1] = 0;  // ready for the next epoch
+  }
+}
+
 void launch_fin(const OccFinArgs& a, hipStream_t st) {
   const uint64_t nb = (a.n + HB - 1) / HB;
   const unsigned g = (unsigned)(nb ? nb : 1);
   k_fin_count<<<g, HB, 0, st>>>(a);
   k_fin_sums<<<1, 1024, 0, st>>>(a, nb);
   k_fin_apply<<<g, HB, 0, st>>>(a);
+  k_fin_insert<<<FIN_INSERT_WG, 256, 0, st>>>(a, nb);
+}
+
+__global__ __launch_bounds__(256) void k_hist_insert(HistInsert h, uint64_t from, uint64_t to) {
+  for (uint64_t p = from + (uint64_t)blockIdx.x * 256 + threadIdx.x; p < to; p += (uint64_t)gridDim.x * 256)
+    hist_insert(h, p, h.fk[p], h.ft[p]);
+}
+void launch_hist_insert(const HistInsert& h, uint64_t from, uint64_t to, hipStream_t st) {
+  if (to <= from) return;
+  const uint64_t g = std::min<uint64_t>((to - from + 255) / 256, 4096);
+  k_hist_insert<<<(unsigned)g, 256, 0, st>>>(h, from, to);
 }
 
 void launch_hist_count(uint64_t n, const uint32_t* off, const uint8_t* acctype, uint64_t nnz,
@@ -302,18 +342,19 @@ __global__ __launch_bounds__(256) void k_hist_gather(const uint64_t* sk, const u
 __global__ __launch_bounds__(256) void k_hist_heads(const uint64_t* skey, uint64_t m,
                                                     uint64_t* hash, uint32_t hbits) {
   const uint64_t mask = (1ull << hbits) - 1;
+  uint64_t* side = hash + (2ull << hbits);
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < m; i += (uint64_t)gridDim.x * 256) {
     const uint64_t key = skey[i];
     if (i > 0 && skey[i - 1] == key) continue;
     uint64_t s = hist_hash_slot(key, hbits);
     for (;;) {
-      const unsigned long long prev = atomicCAS((unsigned long long*)&hash[4 * s],
+      const unsigned long long prev = atomicCAS((unsigned long long*)&hash[2 * s],
                                                 (unsigned long long)DCC_KEY_RESERVED,
                                                 (unsigned long long)key);
       if (prev == DCC_KEY_RESERVED) break;
       s = (s + 1) & mask;  // keys are unique here: a taken slot is another key's
     }
-    hash[4 * s + 1] = i;
+    side[2 * s] = i;
   }
 }
 // the last pair of each run completes its slot: count = last + 1 - first,
@@ -321,15 +362,16 @@ __global__ __launch_bounds__(256) void k_hist_heads(const uint64_t* skey, uint64
 __global__ __launch_bounds__(256) void k_hist_tails(const uint64_t* skey, const uint64_t* stn, uint64_t m,
                                                     uint64_t* hash, uint32_t hbits) {
   const uint64_t mask = (1ull << hbits) - 1;
+  uint64_t* side = hash + (2ull << hbits);
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < m; i += (uint64_t)gridDim.x * 256) {
     const uint64_t key = skey[i];
     if (i + 1 < m && skey[i + 1] == key) continue;
     uint64_t s = hist_hash_slot(key, hbits);
-    while (hash[4 * s] != key) s = (s + 1) & mask;
-    const uint64_t first = hash[4 * s + 1];
-    hash[4 * s + 1] = first | ((i + 1 - first) << 32);
-    hash[4 * s + 2] = stn[first];
-    hash[4 * s + 3] = stn[i];
+    while (hash[2 * s] != key) s = (s + 1) & mask;
+    const uint64_t first = side[2 * s];
+    side[2 * s] = first | ((i + 1 - first) << 32);
+    side[2 * s + 1] = stn[first];
+    hash[2 * s + 1] = ~stn[i];
   }
 }
 

@@ -55,6 +55,7 @@ struct OccDyn {
   uint64_t hist_m;  // pairs in the delta level before the epoch's append
   uint64_t* app_k;  // delta level flat pairs (null: no append this epoch)
   uint64_t* app_t;
+  HistInsert ins;   // the delta's table, updated by the append (hash null: none)
   HistView view;    // history levels (occ_history.h)
 };
 static_assert(sizeof(OccDyn) % 4 == 0, "copied as words");
@@ -515,7 +516,8 @@ struct OccFinArgs {
   uint64_t* part;      // [3 * blocks] scratch
   const OccDyn* dyn;
   uint64_t* tn;        // out: commit tn per txn (0 = none)
-  uint64_t* totals;    // out: pinned host memory
+  uint64_t* totals;    // out: pinned host memory: [0] numbered, [1] appended, [2] largest
+                       // key appended, [3] the delta table's overflow flag
 };
 void launch_fin(const OccFinArgs& a, hipStream_t st);
 void launch_commit_tn(const uint32_t* cflag, uint64_t n, uint64_t* bsum, uint64_t tnc,

@@ -55,31 +55,23 @@ __global__ __launch_bounds__(256) void k_prep(const uint32_t* __restrict__ off, 
 // aborted (every writer stores the same byte).  Offsets are clamped to nnz
 // and made monotone; a malformed batch is reported.
 constexpr uint32_t HIST_WAVES = 16;
-constexpr uint32_t HIST_U = 4;  // accesses per lane in flight
-// the rest of a level probe whose home slot S is already loaded (a collision
-// walk, then the run's tn range)
-__device__ inline bool hist_level_hit_from(const HistLevel& L, uint64_t key, uint64_t lo, uint64_t hi,
-                                           uint64_t slot, HistSlot S) {
-  const uint64_t mask = (1ull << L.hbits) - 1;
-  while (S.key != key) {
-    if (S.key == DCC_KEY_RESERVED) return false;
-    slot = (slot + 1) & mask;
-    S = hist_slot_ld(L.hash, slot);
-  }
-  return hist_slot_hit(L, S, lo, hi);
-}
-__global__ __launch_bounds__(HIST_WAVES * 64) void k_hist(HistArgs a) {
+constexpr uint32_t HIST_U = 2;  // accesses per lane in flight
+constexpr uint32_t HIST_MAP = 2048;  // accesses per wave with an LDS access -> txn map
+__global__ __launch_bounds__(HIST_WAVES * 64, 8) void k_hist(HistArgs a) {
   __shared__ uint32_t s_bm[(1u << HIST_BM_LOG) / 32];
   __shared__ uint32_t s_o[HIST_WAVES][65];
   __shared__ uint64_t s_lo[HIST_WAVES][64], s_hi[HIST_WAVES][64];
-  __shared__ uint8_t s_dead[HIST_WAVES][64];  // txn already found aborted: its other reads are moot
+  __shared__ uint8_t s_live[HIST_WAVES][64];  // window open and not yet found aborted
+  __shared__ uint8_t s_map[HIST_WAVES][HIST_MAP];  // access - a0 -> the wave's txn
   const HistView hv = a.dyn->view;  // by value: registers, not a reload per probe
   for (uint32_t i = threadIdx.x; i < (1u << HIST_BM_LOG) / 32; i += HIST_WAVES * 64)
     s_bm[i] = hv.bm ? hv.bm[i] : ~0u;
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const uint64_t t0 = ((uint64_t)blockIdx.x * HIST_WAVES + w) * 64;
-  if (t0 >= a.n) return;
+  // a resident grid: each wave takes 64-txn tiles in turn (the bitmap loaded
+  // once per workgroup, not once per 1,024 txns)
+  for (uint64_t t0 = ((uint64_t)blockIdx.x * HIST_WAVES + w) * 64; t0 < a.n;
+       t0 += (uint64_t)gridDim.x * HIST_WAVES * 64) {
   const uint32_t nt = (uint32_t)min<uint64_t>(64, a.n - t0);
   const uint64_t t = t0 + lane;
   uint64_t lo = 0, hi = 0;
@@ -91,7 +83,7 @@ __global__ __launch_bounds__(HIST_WAVES * 64) void k_hist(HistArgs a) {
   }
   s_lo[w][lane] = lo;
   s_hi[w][lane] = hi;
-  s_dead[w][lane] = 0;
+  s_live[w][lane] = lane < nt && hi > lo;
   uint32_t ov = lane <= nt ? (uint32_t)min<uint64_t>(a.off[t0 + lane], a.nnz) : 0u;
   for (int d = 1; d < 64; d <<= 1) {
     const uint32_t y = __shfl_up(ov, d);
@@ -102,16 +94,24 @@ __global__ __launch_bounds__(HIST_WAVES * 64) void k_hist(HistArgs a) {
   if (lane == 0) s_o[w][64] = nt == 64 ? max(s_o[w][63], (uint32_t)min<uint64_t>(a.off[t0 + 64], a.nnz)) : 0u;
   __builtin_amdgcn_wave_barrier();
   // no txn of the wave has an open window: nothing to check
-  if (!ballot64(lane < nt && hi > lo)) return;
+  if (!ballot64(lane < nt && hi > lo)) continue;
   const uint32_t a0 = s_o[w][0], a1 = s_o[w][nt];
+  // each access's txn: from the LDS map when the wave's accesses fit, else a
+  // binary search of the offsets
+  const bool mapped = a1 - a0 <= HIST_MAP;
+  if (mapped && lane < nt) {
+    for (uint32_t x = s_o[w][lane]; x < s_o[w][lane + 1]; x++) s_map[w][x - a0] = (uint8_t)lane;
+  }
+  __builtin_amdgcn_wave_barrier();
   for (uint32_t x0 = a0; x0 < a1; x0 += 64 * HIST_U) {
     uint64_t key[HIST_U];
     uint8_t ty[HIST_U];
 #pragma unroll
     for (uint32_t u = 0; u < HIST_U; u++) {  // every load of the step issued before any use
       const uint32_t x = min(x0 + 64 * u + lane, a1 - 1);
-      key[u] = a.keys[x];
-      ty[u] = a.acctype[x];
+      // streamed once: non-temporal, so the batch does not evict the tables from L2
+      key[u] = __builtin_nontemporal_load(a.keys + x);
+      ty[u] = __builtin_nontemporal_load(a.acctype + x);
     }
     uint32_t txn[HIST_U];
     bool want[HIST_U];
@@ -123,40 +123,65 @@ __global__ __launch_bounds__(HIST_WAVES * 64) void k_hist(HistArgs a) {
       txn[u] = 0;
       if (a.var & 1u) want[u] = false;
       if (want[u] && !(a.var & 4u)) {
-        uint32_t l = 0, h = nt;  // largest k < nt with s_o[k] <= x
-        while (h - l > 1) {
-          const uint32_t mid = (l + h) >> 1;
-          if (s_o[w][mid] <= x) l = mid;
-          else h = mid;
+        uint32_t l = 0;
+        if (mapped) {
+          l = s_map[w][x - a0];
+        } else {
+          uint32_t h = nt;  // largest k < nt with s_o[k] <= x
+          while (h - l > 1) {
+            const uint32_t mid = (l + h) >> 1;
+            if (s_o[w][mid] <= x) l = mid;
+            else h = mid;
+          }
         }
         txn[u] = l;
-        want[u] = s_hi[w][l] > s_lo[w][l] && !s_dead[w][l];
+        want[u] = s_live[w][l] != 0;
       }
     }
-    // level by level: the home slots of every wanted key loaded together
+    // level by level, the U probes of a lane in lockstep: every home slot
+    // loaded together, then each round of the collision walks (linear
+    // probing) loaded together, until no lane of the wave has a walk left --
+    // a step costs the longest walk's round trips, not the sum of them
 #pragma unroll
     for (int q = 1; q >= 0; q--) {
       const HistLevel& L = hv.lv[q];
       if (!L.on) continue;
+      const uint64_t mask = (1ull << L.hbits) - 1;
       uint64_t slot[HIST_U];
       HistSlot S[HIST_U];
 #pragma unroll
       for (uint32_t u = 0; u < HIST_U; u++) {
         slot[u] = hist_hash_slot(key[u], L.hbits);
-        S[u] = want[u] ? hist_slot_ld(L.hash, slot[u]) : HistSlot{DCC_KEY_RESERVED, 0, 0, 0};
+        S[u] = want[u] ? hist_slot_ld(L.hash, slot[u]) : HistSlot{DCC_KEY_RESERVED, 0};
+      }
+      // a chained level keeps every key within HIST_WALK of its home
+      for (uint32_t it = 1; !L.next || it < HIST_WALK; it++) {
+        uint32_t walk = 0;
+#pragma unroll
+        for (uint32_t u = 0; u < HIST_U; u++)
+          walk |= (want[u] && S[u].key != key[u] && S[u].key != DCC_KEY_RESERVED) ? 1u << u : 0u;
+        if (!ballot64(walk != 0) || (a.var & 8u)) break;
+#pragma unroll
+        for (uint32_t u = 0; u < HIST_U; u++) {
+          if ((walk >> u) & 1u) {
+            slot[u] = (slot[u] + 1) & mask;
+            S[u] = hist_slot_ld(L.hash, slot[u]);
+          }
+        }
       }
 #pragma unroll
       for (uint32_t u = 0; u < HIST_U; u++) {
-        if (!want[u]) continue;
+        if (!want[u] || S[u].key != key[u]) continue;
         const uint32_t l = txn[u];
-        if (hist_level_hit_from(L, key[u], s_lo[w][l], s_hi[w][l], slot[u], S[u])) {
+        if (hist_found_hit(L, slot[u], ~S[u].ntmax, s_lo[w][l], s_hi[w][l])) {
           a.state[t0 + l] = ST_ABORT;
-          s_dead[w][l] = 1;
+          s_live[w][l] = 0;
           want[u] = false;  // decided: the other level need not be probed
         }
       }
     }
-    __builtin_amdgcn_wave_barrier();
+  }
+  __builtin_amdgcn_wave_barrier();  // the tile's LDS rows are reused by the next
   }
 }
 
@@ -914,7 +939,8 @@ void launch_hist(const HistArgs& a0, hipStream_t st) {
 #else
   a.var = 0;
 #endif
-  k_hist<<<grid_for(a.n, HIST_WAVES * 64), HIST_WAVES * 64, 0, st>>>(a);  // a wave per 64 txns
+  // two workgroups per CU (LDS), each wave looping over 64-txn tiles
+  k_hist<<<(unsigned)std::min<uint64_t>(grid_for(a.n, HIST_WAVES * 64), 512), HIST_WAVES * 64, 0, st>>>(a);
 }
 static unsigned tile_grid(uint64_t m, uint32_t tw, unsigned max_grid) {
   const uint64_t waves = (m + tw - 1) / tw;

@@ -150,3 +150,23 @@ def test_prefix_level_full_size(engine, theta, n):
     lr = rng.integers(0, 50, size=rk.size).astype(np.uint64)
     lw = rng.integers(0, 50, size=rk.size).astype(np.uint64)
     run(engine, b, rows=(rk, lr, lw))
+
+
+def test_row_table_full_runs_again():
+    """A fresh context sizes its row table for a quarter of the epoch's
+    accesses; an epoch of all-distinct rows fills it (a walk past MT_WALK),
+    and the epoch runs again on a table sized for every access: decisions,
+    commit timestamps and row timestamps as the oracle's, and nothing the
+    first attempt did leaks into the row timestamps."""
+    eng = d.Engine(0)
+    try:
+        rng = np.random.default_rng(0xF011)
+        for e in range(2):
+            n, k = 16384, 16
+            keys = rng.choice(1 << 40, size=n * k, replace=False).astype(np.uint64)
+            at = np.where(rng.random(n * k) < 0.5, WR, RD).astype(np.uint8)
+            # one shared row so the epoch has aborts to get right
+            keys[k::k] = keys[0]
+            run(eng, d.EpochBatch(np.arange(0, n * k + 1, k, dtype=np.uint32), keys, at))
+    finally:
+        eng.close()

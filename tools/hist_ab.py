@@ -3,7 +3,7 @@
 (device-resident 1M YCSB batch, TS_CAS windows against the previous epoch's
 ~25K committed writes, commit tn + append).  Needs the DCC_EXPERIMENTS build:
 DENEVA_AMD_LIB=deneva_amd/libdcc_exp.so.  DCC_HIST_VAR bits: 1 no probes,
-2 no key bitmap, 4 no txn search.  Prints device ms per epoch."""
+2 no key bitmap, 4 no txn search, 8 no collision walks.  Prints device ms per epoch."""
 import os
 import sys
 
