@@ -43,35 +43,31 @@ struct dcc_multi;       // single-process multi-GPU context (dcc_multi.cpp)
 // One level of the device OCC history (occ_history.h): flat (key, tn) pairs in
 // append order and, once built, the pairs sorted by (key, tn) with the key
 // table.
-// The delta level is chained instead (occ_history.h HistInsert): its table
-// takes each pair as it is appended, so an epoch's append needs no rebuild.
+// The delta level also takes the epochs' appends as chains in its table
+// (occ_history.h HistInsert), so an epoch's append needs no rebuild.
 struct HistStore {
   DevBuf fk, ft;            // flat pairs
   DevBuf skey, stn, hash;   // built level
   DevBuf bm;                // key bitmap of the built level (occ_history.h HIST_BM_LOG)
-  DevBuf nx, tcnt;          // chained: next pair of the same key; claims / overflow counters
+  DevBuf nx, tcnt;          // delta: chain links per flat pair; the table's overflow flag
   uint64_t m = 0;           // pairs
   uint32_t hbits = 0;
-  bool built = true;        // the built level matches the flat pairs
+  bool built = true;        // the built level (with its chains) holds every flat pair
   bool mono = true;         // append order is tn order within every key
   uint64_t max_tn = 0;      // largest tn appended
   uint64_t min_tn = ~0ull;  // smallest tn appended
   uint64_t max_key = 0;     // largest key appended (radix passes of the build)
   bool chained = false;     // the delta level
-  bool tvalid = false;      // chained: the table holds exactly the first `ins` pairs
-  uint64_t ins = 0;         // chained: pairs inserted
-  uint64_t last_app = 0;    // chained: pairs the last epoch appended (table headroom)
-  bool overflowed = false;  // chained: the table ran out of room (rebuilt twice as big)
-  // empty the level, keeping its buffers
+  bool overflowed = false;  // a key landed past HIST_WALK: the next build doubles the table
+  uint64_t last_app = 0;    // delta: pairs the last epoch appended (table headroom)
+  // empty the level, keeping its buffers (the next build clears its table)
   void reset() {
     m = 0;
-    built = true;
+    built = false;
     mono = true;
     max_tn = 0;
     min_tn = ~0ull;
     max_key = 0;
-    tvalid = false;
-    ins = 0;
   }
 };
 
@@ -182,6 +178,7 @@ struct dcc_ctx {
   DevBuf h_K[2], h_V[2], h_scr, h_bsum;          // level-build sort buffers, append scan
   DevBuf h_bm;                                   // key bitmap of both levels (window check)
   bool h_bm_stale = true;                        // h_bm is not B.bm | D.bm
+  uint32_t fin_tag = 0;                          // k_fin's look-back tag of the last epoch
   DevBuf perm, calvin_a, calvin_b, calvin_c, calvin_d;  // Calvin workspaces
   DevBuf cv_scratch, cv_agg, cv_group, cv_wave, cv_pgx, cv_gsx, cv_gsize, cv_done, cv_maxl;
   DevBuf cv_seq_b, cv_ok, cv_len, cv_off2, cv_tsum, cv_hkeys, cv_hat;
@@ -223,7 +220,6 @@ struct dcc_ctx {
   // device history (occ_history.h / dcc_ctx.hip)
   uint64_t hist_size() const { return hs[0].m + hs[1].m; }
   int hist_grow_flat(HistStore& h, uint64_t need);
-  int hist_build_chained(HistStore& h);
   dcc::HistInsert hist_insert_args(HistStore& h);
   void hist_note(HistStore& h, uint64_t lo_tn, uint64_t hi_tn);
   int hist_build(HistStore& h);
@@ -263,6 +259,7 @@ struct dcc_ctx {
     dcc_stats S;
     double t_wall0 = 0;
     uint64_t n_cw = 0;  // committed writers of the finished epoch (tnc advance)
+    uint32_t fin_runs = 0;  // central_finish launches (a second one after more levels)
   };
   OccRun run;
   int occ_begin(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, bool async);

@@ -320,25 +320,47 @@ void dcc_ctx::hist_note(HistStore& h, uint64_t lo_tn, uint64_t hi_tn) {
   h.built = false;
 }
 
+// A level's sorted build (occ_history.h): the pairs sorted by (key, tn), the
+// table (<= 25 % load; the delta's also has room for the pairs epochs push
+// before its next rebuild: the merge threshold plus one more epoch like the
+// last) and the key bitmap.  A table with a key past HIST_WALK of its home
+// is built again twice as big.
 int dcc_ctx::hist_build(HistStore& h) {
   dcc_ctx* ctx = this;
   if (h.built) return DCC_OK;
-  if (h.m == 0) {
+  h_bm_stale = true;
+  if (h.m == 0 && !h.chained) {
     h.built = true;
     h.mono = true;
     return DCC_OK;
   }
-  // table load <= 1 / this: 1/4 keeps the window check's collision walks
-  // short (experiments: DCC_HIST_SLOTS)
+  // experiments: DCC_HIST_SLOTS (slots per pair)
   static const uint64_t slots_per_pair = [] {
     const char* e = DCC_ENV("DCC_HIST_SLOTS");
     return e && atoi(e) >= 2 ? (uint64_t)atoi(e) : 4ull;
   }();
+  uint64_t need = slots_per_pair * h.m;
+  if (h.chained)
+    need = std::max<uint64_t>({need, 65536,
+                               4 * (std::max<uint64_t>(hist_merge_min, hs[0].m / 4) + h.last_app)});
+  if (h.overflowed) need = std::max<uint64_t>(need, 4ull << h.hbits);
   h.hbits = 4;
-  while ((1ull << h.hbits) < slots_per_pair * h.m) h.hbits++;
-  CR(h.skey.ensure(this, h.m * 8, "history keys"));
-  CR(h.stn.ensure(this, h.m * 8, "history tns"));
+  while ((1ull << h.hbits) < need) h.hbits++;
+  const uint64_t mm = std::max<uint64_t>(h.m, 1);
+  CR(h.skey.ensure(this, mm * 8, "history keys"));
+  CR(h.stn.ensure(this, mm * 8, "history tns"));
   CR(h.hash.ensure(this, 32ull << h.hbits, "history table"));
+  CR(h.tcnt.ensure(this, 16, "history table overflow flag"));
+  CR(h.bm.ensure(this, (1u << HIST_BM_LOG) / 8, "history key bitmap"));
+  CK(hipMemsetAsync(h.tcnt.p, 0, 16, stream));
+  if (h.m == 0) {  // an empty delta: a clear table for the epochs' pushes
+    CK(hipMemsetAsync(h.hash.p, 0xFF, 32ull << h.hbits, stream));
+    CK(hipMemsetAsync(h.bm.p, 0, (1u << HIST_BM_LOG) / 8, stream));
+    h.built = true;
+    h.mono = true;
+    h.overflowed = false;
+    return DCC_OK;
+  }
   for (int q = 0; q < 2; q++) {
     CR(h_K[q].ensure(this, h.m * 8, "history sort keys"));
     CR(h_V[q].ensure(this, h.m * 4, "history sort values"));
@@ -356,59 +378,26 @@ int dcc_ctx::hist_build(HistStore& h) {
               (uint64_t*)h.hash.p,
               h.hbits,
               h.max_key ? 64u - (uint32_t)__builtin_clzll(h.max_key) : 1u,
-              64u - (uint32_t)__builtin_clzll(h.max_tn | 1ull)};
+              64u - (uint32_t)__builtin_clzll(h.max_tn | 1ull),
+              (uint32_t*)h.tcnt.p};
   if (hist_build_level(b, stream)) CK(hipGetLastError());
-  CR(h.bm.ensure(this, (1u << HIST_BM_LOG) / 8, "history key bitmap"));
   launch_hist_bm((const uint64_t*)h.fk.p, h.m, (uint32_t*)h.bm.p, stream);
   CK(hipGetLastError());
+  CK(hipMemcpyAsync(hmisc, h.tcnt.p, 4, hipMemcpyDeviceToHost, stream));
+  CK(hipStreamSynchronize(stream));
+  if (*(const uint32_t*)hmisc) {  // a key past HIST_WALK: twice the slots
+    h.overflowed = true;
+    return hist_build(h);
+  }
+  h.overflowed = false;
   h.built = true;
   return DCC_OK;
 }
 
-// The chained delta: its table sized for a quarter load with the level plus
-// one more epoch like the last (an insert that walks past HIST_WALK flags an
-// overflow, and the table is rebuilt bigger from the flat pairs), then the
-// pairs not yet in it.
 HistInsert dcc_ctx::hist_insert_args(HistStore& h) {
   return HistInsert{(const uint64_t*)h.fk.p, (const uint64_t*)h.ft.p, (uint64_t*)h.hash.p,
                     (uint32_t*)h.nx.p, (uint32_t*)h.bm.p, (uint32_t*)h_bm.p, (uint32_t*)h.tcnt.p,
                     h.hbits, 0u};
-}
-
-int dcc_ctx::hist_build_chained(HistStore& h) {
-  dcc_ctx* ctx = this;
-  uint64_t need = std::max<uint64_t>(65536, 4 * (h.m + h.last_app));
-  if (h.overflowed) need = std::max<uint64_t>(need, 4ull << h.hbits);  // it ran out of room: grow
-  if (!h.tvalid || (2ull << h.hbits) < need) {
-    uint32_t hb = 4;
-    while ((1ull << hb) < need) hb++;
-    CR(h.hash.ensure(this, 32ull << hb, "history delta table"));
-    CR(h.bm.ensure(this, (1u << HIST_BM_LOG) / 8, "history key bitmap"));
-    CR(h.tcnt.ensure(this, 16, "history delta overflow flag"));
-    CK(hipMemsetAsync(h.hash.p, 0xFF, 32ull << hb, stream));
-    CK(hipMemsetAsync(h.bm.p, 0, (1u << HIST_BM_LOG) / 8, stream));
-    CK(hipMemsetAsync(h.tcnt.p, 0, 16, stream));
-    h.hbits = hb;
-    h.ins = 0;
-    h.tvalid = true;
-    h.overflowed = false;
-    h_bm_stale = true;  // the union loses the old table's bits
-  }
-  if (h.ins < h.m) {
-    launch_hist_insert(hist_insert_args(h), h.ins, h.m, stream);
-    CK(hipGetLastError());
-    h.ins = h.m;
-    // a host-side insert's overflow is seen here (the epochs' in their totals)
-    CK(hipMemcpyAsync(hmisc, h.tcnt.p, 4, hipMemcpyDeviceToHost, stream));
-    CK(hipStreamSynchronize(stream));
-    if (*(const uint32_t*)hmisc) {
-      h.tvalid = false;
-      h.overflowed = true;
-      return hist_build_chained(h);
-    }
-  }
-  h.built = true;
-  return DCC_OK;
 }
 
 // Merge the delta into the base once it outgrows a quarter of it (or 64K
@@ -429,14 +418,13 @@ int dcc_ctx::hist_prepare() {
     B.min_tn = std::min(B.min_tn, D.min_tn);
     B.max_key = std::max(B.max_key, D.max_key);
     B.built = false;
-    D.reset();  // buffers kept, level emptied
+    D.reset();  // buffers kept, level emptied (its table cleared by the build)
   }
-  if (!B.built) h_bm_stale = true;
   CR(hist_build(B));
-  CR(hist_build_chained(D));
+  CR(hist_build(D));
   if (h_bm_stale) {
-    launch_hist_bm_or(B.m ? (const uint32_t*)B.bm.p : nullptr, (const uint32_t*)D.bm.p, (uint32_t*)h_bm.p,
-                      stream);
+    launch_hist_bm_or(B.m ? (const uint32_t*)B.bm.p : nullptr, D.m ? (const uint32_t*)D.bm.p : nullptr,
+                      (uint32_t*)h_bm.p, stream);
     CK(hipGetLastError());
     h_bm_stale = false;
   }
@@ -447,11 +435,9 @@ HistView dcc_ctx::hist_view() const {
   HistView v{};
   for (int q = 0; q < 2; q++) {
     const HistStore& h = hs[q];
-    v.lv[q] = h.chained ? HistLevel{(const uint64_t*)h.hash.p, (const uint64_t*)h.ft.p,
-                                    (const uint32_t*)h.nx.p, h.hbits,
-                                    h.m && h.tvalid && h.ins == h.m ? 1u : 0u}
-                        : HistLevel{(const uint64_t*)h.hash.p, (const uint64_t*)h.stn.p, nullptr, h.hbits,
-                                    h.m && h.built ? 1u : 0u};
+    v.lv[q] = HistLevel{(const uint64_t*)h.hash.p, (const uint64_t*)h.stn.p,
+                        h.chained ? (const uint64_t*)h.ft.p : nullptr, h.chained ? (const uint32_t*)h.nx.p : nullptr,
+                        h.hbits, h.m && h.built ? 1u : 0u};
   }
   v.bm = (const uint32_t*)h_bm.p;  // set by hist_prepare
   return v;

@@ -847,7 +847,14 @@ int dcc_ctx::occ_begin(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, bo
   r.app = (b->flags & DCC_OCC_APPEND_HISTORY) != 0;
   if (r.want_tn) {
     CR(cflag.ensure(this, d.n * 4, "cflag"));
-    CR(fin_part.ensure(this, ((d.n + 1023) / 1024 + 1) * 24, "finish block counts"));
+    {
+      const void* old = fin_part.p;
+      CR(fin_part.ensure(this, fin_part_bytes(d.n), "finish look-back words"));
+      if (fin_part.p != old || fin_tag + 4 >= (1u << 30)) {  // fresh memory, or the tags wrap
+        CK(hipMemsetAsync(fin_part.p, 0, fin_part.cap, stream));
+        fin_tag = 0;
+      }
+    }
     CR(tn.ensure(this, d.n * 8, "tn"));
   }
   CR(dyn.ensure(this, sizeof(OccDyn), "epoch parameters"));
@@ -860,6 +867,7 @@ int dcc_ctx::occ_begin(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, bo
   {
     OccDyn& y = *(OccDyn*)hdyn;
     y.tnc = tnc;
+    y.fin_tag = ++fin_tag;
     y.hist_m = hs[1].m;
     y.app_k = r.app ? (uint64_t*)hs[1].fk.p : nullptr;
     y.app_t = r.app ? (uint64_t*)hs[1].ft.p : nullptr;
@@ -989,6 +997,7 @@ int dcc_ctx::occ_final(bool async) {
   const DevBatch& d = r.d;
   if (r.replay) {  // once: a second finalize (after more levels) runs directly
     r.replay = false;
+    if (r.want_tn) r.fin_runs = 1;  // the graph holds the epoch's first central_finish
     CK(hipEventRecord(ev0, stream));
     CK(hipGraphLaunch(graph_exec, stream));
     CK(hipEventRecord(ev1, stream));
@@ -1009,8 +1018,11 @@ int dcc_ctx::occ_final(bool async) {
                (FinalPart*)hpart_dev};
   launch_final(fa, ga, stream);
   if (r.want_tn)
+    // a second central_finish of the epoch (after more levels or a hand-off:
+    // the graph's ran on a partly decided epoch) needs a fresh look-back tag
     launch_fin(OccFinArgs{d.n, d.nnz, r.cf, d.off, d.keys, d.acctype, (uint64_t*)fin_part.p,
-                       (const OccDyn*)dyn.p, r.tn_dev, (uint64_t*)((char*)hdyn_dev + HDYN_TOTALS)},
+                          (const OccDyn*)dyn.p, r.tn_dev, (uint64_t*)((char*)hdyn_dev + HDYN_TOTALS),
+                          r.fin_runs++ ? ++fin_tag : 0u, 0u},
                stream);
   CK(hipGetLastError());
   if (!r.capturing) CK(hipEventRecord(ev1, stream));
@@ -1337,14 +1349,14 @@ int dcc_ctx::occ_end(dcc_stats* st) {
         D.m += tot[1];
         D.max_key = std::max<uint64_t>(D.max_key, tot[2]);
         D.last_app = tot[1];
-        // the pairs went into the delta's table too, unless it ran out of room
-        // (then it is rebuilt bigger from the flat pairs before its next read)
-        if (tot[3]) {
-          D.tvalid = false;
-          D.overflowed = true;
-        }
-        else D.ins = D.m;
         hist_note(D, tnc + 1, tnc + n_cw);
+        // the pairs went onto the delta's chains too, unless its table ran out
+        // of room (then it is rebuilt bigger before its next read) or an
+        // earlier central_finish of this epoch pushed pairs of a partly
+        // decided epoch (then it is rebuilt from the flat pairs, which the
+        // last one rewrote)
+        if (tot[3]) D.overflowed = true;
+        else if (r.fin_runs <= 1) D.built = true;
       }
     }
     tnc += n_cw;

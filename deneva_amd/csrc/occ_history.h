@@ -4,14 +4,15 @@
 //
 // The history is a multiset of (key, tn) pairs: one per write of a committed
 // txn numbered tn.  It lives in HBM as two levels, a large `base` and a small
-// `delta` (a two-level log-structured merge): an epoch appends its committed
-// writes to the delta's flat pair array on the device (count, scan, emit: no
-// D2H of the batch) and inserts them into the delta's table in the same
-// kernel, and the delta is merged into the base when it outgrows a quarter
-// of it.  A built level is its pairs sorted by (key, tn)
-// plus an open-addressing table key -> (first pair, pair count, min tn, max
-// tn) at <= 50 % load, so a window query is one probe per level, and a binary
-// search of the key's run of tns only when the window lies inside the run.
+// `delta` (a two-level log-structured merge), each its pairs sorted by (key,
+// tn) with an open-addressing key table (<= 25 % load).  An epoch appends its
+// committed writes to the delta's flat pairs on the device (count, scan,
+// emit: no D2H of the batch) and pushes each onto its key's chain in the
+// delta's table (no re-sort per epoch); the delta is rebuilt sorted after a
+// host append and merged into the base when it outgrows a quarter of it.
+// A window query is one 16-B probe per level (the key and its largest tn
+// answer it unless the window ends below that tn); only then the key's chain
+// (newest first) and the binary search of its sorted run.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -27,22 +28,20 @@ namespace dcc {
 
 struct HistLevel {
   // [2 << hbits] probe words (HistSlot per slot: key DCC_KEY_RESERVED =
-  // empty), then [2 << hbits] side words (HistSide per slot)
+  // empty), then [2 << hbits] side words per slot: the key's sorted run
+  // (first | count << 32; all-ones: none) and its chain head (low word,
+  // HIST_NIL: none)
   const uint64_t* hash;
-  const uint64_t* tn;    // sorted level: [m] tns, ascending within a key's run;
-                         // chained level: the flat pairs' tns
-  const uint32_t* next;  // chained level: [m] next pair of the same key (HIST_NIL ends); null: sorted
+  const uint64_t* tn;    // [m] the sorted pairs' tns, ascending within a key's run
+  const uint64_t* ctn;   // the flat pairs' tns (chain entries), or null
+  const uint32_t* next;  // the flat pairs' chain links (HIST_NIL ends), or null
   uint32_t hbits;
   uint32_t on;           // 0: the level is empty
 };
-// A probe slot (16 B): the key and the complement of its largest tn (all-ones
-// when empty, so a chained insert lowers it with atomicMin), which answers a
-// window query unless the window ends below that tn.  The slot's side words
-// then give the smallest tn and the key's pairs: a sorted level's run (first
-// | count << 32), a chained level's most recent pair (low word), whose next[]
-// links the rest.  Chained levels keep every key within HIST_WALK slots of
-// its home (an insert that would walk further flags the table instead), so
-// their probes stop there.
+// A probe slot (16 B): the key and the complement of its largest tn
+// (all-ones when empty, so a chain push lowers it with atomicMin).  Every key
+// sits within HIST_WALK slots of its home (a build or push that walks further
+// flags the table, and the host rebuilds it bigger), so probes stop there.
 struct HistSlot {
   uint64_t key, ntmax;
 };
@@ -57,15 +56,17 @@ __device__ inline bool hist_found_hit(const HistLevel& L, uint64_t s, uint64_t t
   if (tmax <= lo) return false;
   if (tmax <= hi) return true;  // tmax is in the window
   const ulonglong2 side = reinterpret_cast<const ulonglong2*>(L.hash + (2ull << L.hbits))[s];
-  const uint64_t fc = side.x, tmin = side.y;
-  if (tmin > hi) return false;
-  if (tmin > lo) return true;  // tmin is in the window
-  if (L.next) {  // chained: every pair of the key
-    for (uint32_t p = (uint32_t)fc; p != HIST_NIL; p = L.next[p])
-      if (L.tn[p] > lo && L.tn[p] <= hi) return true;
-    return false;
-  }
-  const uint64_t first = (uint32_t)fc, end = first + (fc >> 32);
+  // the chain: epochs' appends, pushed in tn order, so newest first
+  if (L.next)
+    for (uint32_t p = (uint32_t)side.y; p != HIST_NIL; p = L.next[p]) {
+      const uint64_t t = L.ctn[p];
+      if (t <= hi) {
+        if (t > lo) return true;
+        break;  // the rest are older still
+      }
+    }
+  if (side.x == ~0ull) return false;
+  const uint64_t first = (uint32_t)side.x, end = first + (side.x >> 32);
   uint64_t b = first, e = end;
   while (b < e) {  // first tn > lo
     const uint64_t m = (b + e) >> 1;
@@ -91,8 +92,7 @@ __device__ inline bool hist_level_hit(const HistLevel& L, uint64_t key, uint64_t
   if (!L.on) return false;
   const uint64_t mask = (1ull << L.hbits) - 1;
   uint64_t slot = hist_hash_slot(key, L.hbits);
-  // a sorted level is at most half full: every walk ends at an empty slot
-  for (uint32_t i = 0; !L.next || i < HIST_WALK; i++) {
+  for (uint32_t i = 0; i < HIST_WALK; i++) {
     const HistSlot S = hist_slot_ld(L.hash, slot);
     if (S.key == key) return hist_found_hit(L, slot, ~S.ntmax, lo, hi);
     if (S.key == DCC_KEY_RESERVED) return false;
@@ -113,11 +113,12 @@ void launch_hist_count(uint64_t n, const uint32_t* off, const uint8_t* acctype, 
 void launch_hist_emit(uint64_t n, const uint32_t* off, const uint64_t* keys, const uint8_t* acctype,
                       uint64_t nnz, const uint64_t* tn, const uint32_t* bsum, uint64_t* out_k,
                       uint64_t* out_t, unsigned long long* kmax, hipStream_t st);
-// chained (delta) level: insert flat pairs [from, to) into the table (the
-// pair's key slot found or claimed within HIST_WALK of home, else *over set
-// and the pair left out: the host rebuilds the table bigger before it is
-// read again; tmin / ~tmax lowered; the pair pushed on the key's list) and
-// the key bitmaps.  No atomic here returns a value but the claim and the push.
+// An epoch's append into the delta's table: each flat pair p (key, tn)
+// finds or claims its key's slot within HIST_WALK of home (else *over is set
+// and the pair left out: the host rebuilds the level before it is read
+// again), lowers the slot's ~tmax and is pushed on the key's chain; the key
+// bitmaps get its bit.  At most one committed txn of an epoch writes a key
+// and tns grow from epoch to epoch, so every chain stays newest first.
 struct HistInsert {
   const uint64_t* fk;
   const uint64_t* ft;
@@ -145,15 +146,13 @@ __device__ inline void hist_insert(const HistInsert& h, uint64_t p, uint64_t key
     if (k == key) break;
     s = (s + 1) & mask;
   }
-  unsigned long long* side = (unsigned long long*)&h.hash[(2ull << h.hbits) + 2 * s];
   atomicMin((unsigned long long*)&h.hash[2 * s + 1], (unsigned long long)~tn);
-  atomicMin(side + 1, (unsigned long long)tn);
-  h.next[p] = atomicExch((uint32_t*)side, (uint32_t)p);
+  uint32_t* head = (uint32_t*)&h.hash[(2ull << h.hbits) + 2 * s + 1];
+  h.next[p] = atomicExch(head, (uint32_t)p);
   const uint32_t b = hist_bm_bit(key);
   atomicOr(&h.bm_level[b >> 5], 1u << (b & 31u));
   atomicOr(&h.bm_all[b >> 5], 1u << (b & 31u));
 }
-void launch_hist_insert(const HistInsert& h, uint64_t from, uint64_t to, hipStream_t st);
 // level build from flat pairs (fk, ft)[m]; K/V are radix-sort ping-pong buffers
 struct HistBuild {
   uint64_t m;
@@ -165,9 +164,10 @@ struct HistBuild {
   uint32_t* scratch;
   uint64_t* skey;       // out: sorted keys
   uint64_t* stn;        // out: sorted tns
-  uint64_t* hash;       // out: [4 << hbits]
+  uint64_t* hash;       // out: [4 << hbits] (HistLevel)
   uint32_t hbits;
   uint32_t kbits, tbits;  // significant bits of the keys / tns (radix passes)
+  uint32_t* over;       // out: set when a key sits past HIST_WALK (rebuild bigger)
 };
 int hist_build_level(const HistBuild& b, hipStream_t st);
 // the key bitmap of m flat keys (bm zeroed first), and out = a | b

@@ -9,8 +9,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "dcc_device.h"
+#include "dcc_env.h"
 #include "occ_history.h"
 #include "occ_kernels.h"
 #include "radix_sort.h"
@@ -18,7 +20,6 @@
 namespace dcc {
 
 constexpr uint32_t HB = 1024;  // txns per block of the append kernels
-constexpr uint32_t FIN_INSERT_WG = 512;  // k_fin_insert: the grid walks the appended pairs
 
 // committed writes of txn t (0 when it did not commit or is read-only)
 __device__ inline uint32_t hist_writes_of(uint64_t t, const uint32_t* off, const uint8_t* acctype,
@@ -100,12 +101,61 @@ __global__ __launch_bounds__(HB) void k_hist_emit(uint64_t n, const uint32_t* of
 }
 
 // ---------------------------------------------------------------------------
-// central_finish in three launches (OccFinArgs, occ_kernels.h).  Per 1024-txn
-// block: the committed writers (cflag) and, when appending, their writes and
-// largest key; one workgroup scans the block counts from dyn->tnc and
-// dyn->hist_m; then each committed writer takes its tn and emits its write set
-// at its position.  Only committed writers (a few per thousand under
+// central_finish in one launch (OccFinArgs, occ_kernels.h): a workgroup per
+// 1,024 txns counts its committed writers (cflag) and, when appending, their
+// writes and largest key; a single-pass scan with decoupled look-back gives
+// its prefix (tnc and the delta's append position from the epoch parameters,
+// dyn->tnc / dyn->hist_m); each committed writer takes its tn and emits its
+// write set there; the workgroup's threads then push its pairs onto the
+// delta's chains (a thread per pair); the last workgroup to finish copies the
+// totals to pinned memory.  Only committed writers (a few per thousand under
 // contention) read their access lists.
+//
+// Look-back words, as MaaT's round scan (maat.hip): payload and status are
+// written with device-scope atomics, the status after `s_waitcnt vmcnt(0)`
+// (the payload is at the coherence point first), and read in the other
+// order; the status carries the epoch's tag (dyn->fin_tag), so nothing is
+// reset between epochs.
+struct __attribute__((aligned(64))) FinLb {
+  uint64_t agg, inc;  // commits | writes << 32: the workgroup's, and through it
+  uint32_t status;    // tag << 2 | 1 aggregate, | 2 inclusive
+  uint32_t pad[11];
+};
+static_assert(sizeof(FinLb) == 64, "one line per workgroup");
+struct FinTail {
+  unsigned long long kmax;  // largest key appended (reset by the last workgroup)
+  uint32_t done;            // finished workgroups (reset by the last one)
+  uint32_t pad[13];
+};
+static_assert(sizeof(FinTail) == 64, "one line");
+template <typename T>
+__device__ inline void fin_st(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ inline T fin_ld(T* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline void fin_publish(FinLb* e, uint64_t v, bool incl, uint32_t tag) {
+  fin_st(incl ? &e->inc : &e->agg, v);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  fin_st(&e->status, (tag << 2) | (incl ? 2u : 1u));
+}
+
+// A committed writer's accesses [o0, o1), FIN_U at a time: every type and
+// key of a step loaded before any is used (one memory round trip per step
+// instead of one per access).
+constexpr uint32_t FIN_U = 8;
+constexpr uint32_t FIN_T = 2;  // k_fin: consecutive txns per thread
+__device__ inline void fin_step(const OccFinArgs& a, uint64_t x, uint64_t o1, uint8_t (&ty)[FIN_U],
+                                uint64_t (&k)[FIN_U]) {
+#pragma unroll
+  for (uint32_t u = 0; u < FIN_U; u++) {
+    const bool in = x + u < o1;
+    ty[u] = in ? a.acctype[x + u] : (uint8_t)0;
+    k[u] = in ? a.keys[x + u] : 0ull;
+  }
+}
 __device__ inline uint32_t fin_writes(uint64_t t, const OccFinArgs& a, uint64_t& o0, uint64_t& o1,
                                       uint64_t& kmx) {
   o0 = min((uint64_t)a.off[t], a.nnz);
@@ -113,11 +163,17 @@ __device__ inline uint32_t fin_writes(uint64_t t, const OccFinArgs& a, uint64_t&
   if (o1 < o0) o1 = o0;
   o1 = min(o1, o0 + MAX_TXN_LEN);
   uint32_t c = 0;
-  for (uint64_t x = o0; x < o1; x++)
-    if (a.acctype[x] == DCC_WR) {
-      c++;
-      kmx = max(kmx, a.keys[x]);
-    }
+  for (uint64_t x = o0; x < o1; x += FIN_U) {
+    uint8_t ty[FIN_U];
+    uint64_t k[FIN_U];
+    fin_step(a, x, o1, ty, k);
+#pragma unroll
+    for (uint32_t u = 0; u < FIN_U; u++)
+      if (ty[u] == DCC_WR) {
+        c++;
+        kmx = max(kmx, k[u]);
+      }
+  }
   return c;
 }
 
@@ -155,151 +211,144 @@ __device__ inline void block_excl_scan2(uint32_t v0, uint32_t v1, uint32_t& e0, 
   e1 = b1 + x1 - v1;
 }
 
-__global__ __launch_bounds__(HB) void k_fin_count(OccFinArgs a) {
+__global__ __launch_bounds__(HB, 8) void k_fin(OccFinArgs a) {  // two workgroups per CU
   __shared__ unsigned long long s_mx;
-  const uint64_t t = (uint64_t)blockIdx.x * HB + threadIdx.x;
-  const bool app = a.dyn->app_k != nullptr;
-  const uint32_t c = (t < a.n && a.cflag[t]) ? 1u : 0u;
-  uint64_t o0, o1, kmx = 0;
-  const uint32_t w = (c && app) ? fin_writes(t, a, o0, o1, kmx) : 0u;
+  __shared__ uint64_t s_pre;
+  __shared__ uint32_t s_last;
+  const OccDyn* dy = a.dyn;
+  const uint32_t tag = a.tag ? a.tag : dy->fin_tag;
+  // the tail first: its place must not depend on the epoch's grid size
+  FinTail* tail = (FinTail*)a.part;
+  FinLb* lb = (FinLb*)(tail + 1);
+  // FIN_T consecutive txns per thread (one generation of workgroups fits the
+  // chip: a workgroup's chain of round trips is paid once, not twice)
+  const uint64_t t_0 = ((uint64_t)blockIdx.x * HB + threadIdx.x) * FIN_T;
+  uint64_t* app_k = dy->app_k;
+  uint64_t* app_t = dy->app_t;
+  uint32_t c[FIN_T], w[FIN_T];
+  uint64_t o0[FIN_T], o1[FIN_T], kmx = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < FIN_T; i++) c[i] = (t_0 + i < a.n && a.cflag[t_0 + i]) ? 1u : 0u;
+#pragma unroll
+  for (uint32_t i = 0; i < FIN_T; i++) {
+    o0[i] = o1[i] = 0;
+    w[i] = (c[i] && app_k) ? fin_writes(t_0 + i, a, o0[i], o1[i], kmx) : 0u;
+  }
+  uint32_t cs = 0, ws = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < FIN_T; i++) {
+    cs += c[i];
+    ws += w[i];
+  }
   if (threadIdx.x == 0) s_mx = 0;
   uint32_t e0, e1, t0, t1;
-  block_excl_scan2(c, w, e0, e1, t0, t1);  // its barrier orders s_mx's reset
+  block_excl_scan2(cs, ws, e0, e1, t0, t1);  // its barrier orders s_mx's reset
   for (int d = 32; d > 0; d >>= 1) kmx = max(kmx, (uint64_t)__shfl_xor(kmx, d));
   if ((threadIdx.x & 63) == 0 && kmx) atomicMax(&s_mx, (unsigned long long)kmx);
   __syncthreads();
-  if (threadIdx.x == 0) {
-    a.part[3 * blockIdx.x] = t0;
-    a.part[3 * blockIdx.x + 1] = t1;
-    a.part[3 * blockIdx.x + 2] = s_mx;
-  }
-}
-
-// exclusive scans of the block counts from dyn->tnc / dyn->hist_m (one
-// workgroup, 1024 blocks per step), totals to pinned memory
-__global__ __launch_bounds__(1024) void k_fin_sums(OccFinArgs a, uint64_t nb) {
-  __shared__ uint64_t s_w[2][16];
-  __shared__ uint64_t s_carry[2];
-  __shared__ unsigned long long s_mx;
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  if (threadIdx.x == 0) {
-    s_carry[0] = a.dyn->tnc;
-    s_carry[1] = a.dyn->hist_m;
-    s_mx = 0;
-  }
-  __syncthreads();
-  const uint64_t c0_base = s_carry[0], c1_base = s_carry[1];
-  uint64_t mx = 0;
-  for (uint64_t c0 = 0; c0 < nb; c0 += 1024) {
-    const uint64_t q = c0 + threadIdx.x;
-    const uint64_t v0 = q < nb ? a.part[3 * q] : 0ull, v1 = q < nb ? a.part[3 * q + 1] : 0ull;
-    if (q < nb) mx = max(mx, a.part[3 * q + 2]);
-    uint64_t x0 = v0, x1 = v1;
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint64_t y0 = __shfl_up(x0, d), y1 = __shfl_up(x1, d);
-      if (lane >= (uint32_t)d) {
-        x0 += y0;
-        x1 += y1;
+  if (wv == 0) {
+    const uint64_t tot = (uint64_t)t0 | ((uint64_t)t1 << 32);
+    uint64_t P = 0;
+    // the block's largest key before its publish (whose waitcnt orders it)
+    if (lane == 0 && s_mx) atomicMax(&tail->kmax, s_mx);
+    if (blockIdx.x == 0) {
+      if (lane == 0) fin_publish(&lb[0], tot, true, tag);
+    } else {
+      if (lane == 0) fin_publish(&lb[blockIdx.x], tot, false, tag);
+      bool timed_out = false;
+      for (int64_t hi = (a.var & 2u) ? -1 : (int64_t)blockIdx.x - 1; hi >= 0; hi -= 64) {
+        const int64_t j = hi - (int64_t)lane;
+        uint32_t stw = 0;
+        if (j >= 0) {
+          uint32_t spins = 0;
+          while (((stw = fin_ld(&lb[j].status)) >> 2) != tag) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > (1u << 24)) {  // dispatch is in index order: never in practice
+              timed_out = true;
+              break;
+            }
+          }
+        }
+        if (ballot64(timed_out)) {
+          P = ~0ull;  // the host sees the numbering fail (totals)
+          break;
+        }
+        const bool inc = j >= 0 && (stw & 3u) == 2u;
+        const uint64_t im = ballot64(inc);
+        const uint32_t stop = im ? (uint32_t)__builtin_ctzll(im) : 63u;
+        uint64_t v = (j >= 0 && lane <= stop) ? fin_ld(inc ? &lb[j].inc : &lb[j].agg) : 0ull;
+        for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d);
+        P += v;
+        if (im) break;
       }
+      if (lane == 0) fin_publish(&lb[blockIdx.x], P == ~0ull ? ~0ull : P + tot, true, tag);
     }
-    if (lane == 63) {
-      s_w[0][wv] = x0;
-      s_w[1][wv] = x1;
-    }
-    __syncthreads();
-    uint64_t b0 = s_carry[0], b1 = s_carry[1];
-    for (uint32_t w = 0; w < wv; w++) {
-      b0 += s_w[0][w];
-      b1 += s_w[1][w];
-    }
-    if (q < nb) {
-      a.part[3 * q] = b0 + x0 - v0;
-      a.part[3 * q + 1] = b1 + x1 - v1;
-    }
-    __syncthreads();
-    if (threadIdx.x == 1023) {
-      s_carry[0] = b0 + x0;
-      s_carry[1] = b1 + x1;
-    }
-    __syncthreads();
+    if (lane == 0) s_pre = P;
   }
-  for (int d = 32; d > 0; d >>= 1) mx = max(mx, (uint64_t)__shfl_xor(mx, d));
-  if (lane == 0 && mx) atomicMax(&s_mx, (unsigned long long)mx);
   __syncthreads();
-  if (threadIdx.x == 0) {
-    a.totals[0] = s_carry[0] - c0_base;
-    a.totals[1] = s_carry[1] - c1_base;
-    a.totals[2] = s_mx;
-    a.part[3 * nb + 1] = s_carry[1] - c1_base;  // the appended count, for k_fin_insert
-  }
-}
-
-__global__ __launch_bounds__(HB) void k_fin_apply(OccFinArgs a) {
-  const uint64_t t = (uint64_t)blockIdx.x * HB + threadIdx.x;
-  uint64_t* app_k = a.dyn->app_k;
-  const uint32_t c = (t < a.n && a.cflag[t]) ? 1u : 0u;
-  uint64_t o0 = 0, o1 = 0, kmx = 0;
-  const uint32_t w = (c && app_k) ? fin_writes(t, a, o0, o1, kmx) : 0u;
-  uint32_t e0, e1, t0, t1;
-  block_excl_scan2(c, w, e0, e1, t0, t1);
-  if (t >= a.n) return;
-  const uint64_t my_tn = c ? a.part[3 * blockIdx.x] + e0 + 1 : 0;
-  a.tn[t] = my_tn;
-  if (w) {
-    uint64_t* app_t = a.dyn->app_t;
-    uint64_t p = a.part[3 * blockIdx.x + 1] + e1;
-    for (uint64_t x = o0; x < o1; x++)
-      if (a.acctype[x] == DCC_WR) {
-        app_k[p] = a.keys[x];
-        app_t[p] = my_tn;
-        p++;
+  const uint64_t P = s_pre;
+  const uint64_t wbase = dy->hist_m + (P >> 32);
+  if (P != ~0ull) {
+    uint32_t ec = e0, ew = e1;
+#pragma unroll
+    for (uint32_t i = 0; i < FIN_T; i++) {
+      const uint64_t t = t_0 + i;
+      if (t >= a.n) break;
+      const uint64_t my_tn = c[i] ? dy->tnc + (uint32_t)P + ec + 1 : 0;
+      if (!(a.var & 8u)) a.tn[t] = my_tn;
+      if (w[i] && !(a.var & 4u)) {
+        uint64_t p = wbase + ew;
+        for (uint64_t x = o0[i]; x < o1[i]; x += FIN_U) {
+          uint8_t ty[FIN_U];
+          uint64_t k[FIN_U];
+          fin_step(a, x, o1[i], ty, k);
+#pragma unroll
+          for (uint32_t u = 0; u < FIN_U; u++)
+            if (ty[u] == DCC_WR) {
+              app_k[p] = k[u];
+              app_t[p] = my_tn;
+              p++;
+            }
+        }
       }
+      ec += c[i];
+      ew += w[i];
+    }
   }
-}
-
-// the appended pairs into the delta's table (a thread per pair), then its
-// overflow flag to pinned memory by the last workgroup to finish
-__global__ __launch_bounds__(256) void k_fin_insert(OccFinArgs a, uint64_t nb) {
-  const HistInsert ins = a.dyn->ins;
-  if (!ins.hash) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) a.totals[3] = 0;
-    return;
+  // the block's pairs onto the delta's chains, a thread per pair
+  const HistInsert ins = dy->ins;
+  if (ins.hash && t1 && P != ~0ull && !(a.var & 1u)) {
+    __syncthreads();  // the pairs written above
+    for (uint32_t i = threadIdx.x; i < t1; i += HB) hist_insert(ins, wbase + i, app_k[wbase + i], app_t[wbase + i]);
   }
-  const uint64_t p0 = a.dyn->hist_m, cnt = a.part[3 * nb + 1];
-  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < cnt; i += (uint64_t)gridDim.x * 256)
-    hist_insert(ins, p0 + i, ins.fk[p0 + i], ins.ft[p0 + i]);
-  __shared__ bool s_last;
+  // the last workgroup to finish: totals to pinned memory (every value it
+  // reads was written with device-scope atomics, acknowledged before the
+  // writer's arrival)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    s_last = atomicAdd(&ins.over[1], 1u) == gridDim.x - 1;
-  }
+  if (threadIdx.x == 0) s_last = atomicAdd(&tail->done, 1u) == gridDim.x - 1;
   __syncthreads();
   if (s_last && threadIdx.x == 0) {
-    __threadfence();
-    a.totals[3] = atomicAdd(&ins.over[0], 0u);
-    ins.over[1] = 0;  // ready for the next epoch
+    const uint64_t g = fin_ld(&lb[gridDim.x - 1].inc);
+    a.totals[0] = g == ~0ull ? ~0ull : (uint32_t)g;
+    a.totals[1] = g >> 32;
+    a.totals[2] = atomicExch(&tail->kmax, 0ull);
+    a.totals[3] = ins.hash ? atomicAdd(ins.over, 0u) : 0u;
+    fin_st(&tail->done, 0u);
   }
 }
 
-void launch_fin(const OccFinArgs& a, hipStream_t st) {
-  const uint64_t nb = (a.n + HB - 1) / HB;
-  const unsigned g = (unsigned)(nb ? nb : 1);
-  k_fin_count<<<g, HB, 0, st>>>(a);
-  k_fin_sums<<<1, 1024, 0, st>>>(a, nb);
-  k_fin_apply<<<g, HB, 0, st>>>(a);
-  k_fin_insert<<<FIN_INSERT_WG, 256, 0, st>>>(a, nb);
+void launch_fin(const OccFinArgs& a0, hipStream_t st) {
+  OccFinArgs a = a0;
+  // timing variants, wrong results by design: 1 no chain pushes, 2 no
+  // look-back wait, 4 no write-set emission, 8 no tn stores
+  if (const char* e = DCC_ENV("DCC_FIN_VAR")) a.var = (uint32_t)atoi(e);
+  const uint64_t nb = (a.n + HB * FIN_T - 1) / (HB * FIN_T);
+  k_fin<<<(unsigned)(nb ? nb : 1), HB, 0, st>>>(a);
 }
 
-__global__ __launch_bounds__(256) void k_hist_insert(HistInsert h, uint64_t from, uint64_t to) {
-  for (uint64_t p = from + (uint64_t)blockIdx.x * 256 + threadIdx.x; p < to; p += (uint64_t)gridDim.x * 256)
-    hist_insert(h, p, h.fk[p], h.ft[p]);
-}
-void launch_hist_insert(const HistInsert& h, uint64_t from, uint64_t to, hipStream_t st) {
-  if (to <= from) return;
-  const uint64_t g = std::min<uint64_t>((to - from + 255) / 256, 4096);
-  k_hist_insert<<<(unsigned)g, 256, 0, st>>>(h, from, to);
-}
+uint64_t fin_part_bytes(uint64_t n) { return (((n + HB * FIN_T - 1) / (HB * FIN_T)) + 2) * sizeof(FinLb); }
 
 void launch_hist_count(uint64_t n, const uint32_t* off, const uint8_t* acctype, uint64_t nnz,
                        const uint64_t* tn, uint32_t* bsum, hipStream_t st) {
@@ -340,14 +389,15 @@ __global__ __launch_bounds__(256) void k_hist_gather(const uint64_t* sk, const u
 }
 // the first pair of each key's run enters the table: (key, first)
 __global__ __launch_bounds__(256) void k_hist_heads(const uint64_t* skey, uint64_t m,
-                                                    uint64_t* hash, uint32_t hbits) {
+                                                    uint64_t* hash, uint32_t hbits, uint32_t* over) {
   const uint64_t mask = (1ull << hbits) - 1;
   uint64_t* side = hash + (2ull << hbits);
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < m; i += (uint64_t)gridDim.x * 256) {
     const uint64_t key = skey[i];
     if (i > 0 && skey[i - 1] == key) continue;
     uint64_t s = hist_hash_slot(key, hbits);
-    for (;;) {
+    for (uint32_t w = 0;; w++) {
+      if (w == HIST_WALK) atomicOr(over, 1u);  // probes stop at HIST_WALK: the host rebuilds
       const unsigned long long prev = atomicCAS((unsigned long long*)&hash[2 * s],
                                                 (unsigned long long)DCC_KEY_RESERVED,
                                                 (unsigned long long)key);
@@ -357,8 +407,8 @@ __global__ __launch_bounds__(256) void k_hist_heads(const uint64_t* skey, uint64
     side[2 * s] = i;
   }
 }
-// the last pair of each run completes its slot: count = last + 1 - first,
-// and the run's tn range
+// the last pair of each run completes its slot: the run (first | count << 32)
+// and ~(its largest tn)
 __global__ __launch_bounds__(256) void k_hist_tails(const uint64_t* skey, const uint64_t* stn, uint64_t m,
                                                     uint64_t* hash, uint32_t hbits) {
   const uint64_t mask = (1ull << hbits) - 1;
@@ -370,7 +420,6 @@ __global__ __launch_bounds__(256) void k_hist_tails(const uint64_t* skey, const 
     while (hash[2 * s] != key) s = (s + 1) & mask;
     const uint64_t first = side[2 * s];
     side[2 * s] = first | ((i + 1 - first) << 32);
-    side[2 * s + 1] = stn[first];
     hash[2 * s + 1] = ~stn[i];
   }
 }
@@ -403,7 +452,7 @@ int hist_build_level(const HistBuild& b, hipStream_t st) {
   }
   k_hist_gather<<<hgrid(b.m), 256, 0, st>>>(K[r], V[r], b.ft, b.m, b.skey, b.stn);
   if (hipMemsetAsync(b.hash, 0xFF, (32ull << b.hbits), st) != hipSuccess) return -1;
-  k_hist_heads<<<hgrid(b.m), 256, 0, st>>>(b.skey, b.m, b.hash, b.hbits);
+  k_hist_heads<<<hgrid(b.m), 256, 0, st>>>(b.skey, b.m, b.hash, b.hbits, b.over);
   k_hist_tails<<<hgrid(b.m), 256, 0, st>>>(b.skey, b.stn, b.m, b.hash, b.hbits);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -52,6 +52,8 @@ struct TileOut {
 // kernel (k_fill) copies them to device memory.
 struct OccDyn {
   uint64_t tnc;     // commit counter before the epoch (occ.cpp:283-284)
+  uint32_t fin_tag; // central_finish's look-back tag (never 0; occ_history.hip k_fin)
+  uint32_t pad;
   uint64_t hist_m;  // pairs in the delta level before the epoch's append
   uint64_t* app_k;  // delta level flat pairs (null: no append this epoch)
   uint64_t* app_t;
@@ -513,13 +515,17 @@ struct OccFinArgs {
   const uint32_t* off;
   const uint64_t* keys;
   const uint8_t* acctype;
-  uint64_t* part;      // [3 * blocks] scratch
+  uint64_t* part;      // fin_part_bytes(n): look-back words (zeroed when allocated)
   const OccDyn* dyn;
   uint64_t* tn;        // out: commit tn per txn (0 = none)
   uint64_t* totals;    // out: pinned host memory: [0] numbered, [1] appended, [2] largest
                        // key appended, [3] the delta table's overflow flag
+  uint32_t tag;        // look-back tag; 0: the epoch's (dyn->fin_tag).  A second launch
+                       // for the same epoch takes a fresh one.
+  uint32_t var;        // DCC_FIN_VAR timing variants (DCC_EXPERIMENTS builds only; 0)
 };
 void launch_fin(const OccFinArgs& a, hipStream_t st);
+uint64_t fin_part_bytes(uint64_t n);
 void launch_commit_tn(const uint32_t* cflag, uint64_t n, uint64_t* bsum, uint64_t tnc,
                       uint64_t* tn, hipStream_t st);
 // deferred central_finish: cflag[t] = global RCOK && local commit && has a

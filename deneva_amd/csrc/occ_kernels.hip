@@ -154,8 +154,8 @@ __global__ __launch_bounds__(HIST_WAVES * 64, 8) void k_hist(HistArgs a) {
         slot[u] = hist_hash_slot(key[u], L.hbits);
         S[u] = want[u] ? hist_slot_ld(L.hash, slot[u]) : HistSlot{DCC_KEY_RESERVED, 0};
       }
-      // a chained level keeps every key within HIST_WALK of its home
-      for (uint32_t it = 1; !L.next || it < HIST_WALK; it++) {
+      // every key sits within HIST_WALK of its home (occ_history.h)
+      for (uint32_t it = 1; it < HIST_WALK; it++) {
         uint32_t walk = 0;
 #pragma unroll
         for (uint32_t u = 0; u < HIST_U; u++)

@@ -77,6 +77,49 @@ def test_many_epochs(engine, device_ptrs, merge_min):
         engine.history_clear()
 
 
+@pytest.mark.parametrize("device_ptrs", [False, True])
+def test_appends_of_handed_off_epochs(engine, device_ptrs):
+    """Low-contention epochs (theta 0) whose lists stop shrinking go to the
+    round solver after the captured graph ran: central_finish runs a second
+    time on the fully decided epoch (a fresh look-back tag), and the delta's
+    chains pushed by the first, partly decided run are dropped (the level is
+    rebuilt from the flat pairs).  Every later window must see exactly the
+    oracle's history; the second and third passes replay the graph."""
+    import torch
+    rng = np.random.default_rng(0x4AD0 + device_ptrs)
+    engine.set_option(OPT_HIST_MERGE, 1 << 22)  # keep everything in the delta
+    bs = [d.gen_ycsb(n_txn=65536, zipf_theta=0.0, table_size=1 << 18, seed=0x4AD0 + e) for e in range(3)]
+    try:
+        for rep in range(3):
+            engine.history_clear()
+            engine.tnc = 0
+            hk = np.zeros(0, np.uint64)
+            ht = np.zeros(0, np.uint64)
+            tnc = 0
+            for e, b in enumerate(bs):
+                b.start_tn, b.finish_tn = windows(np.random.default_rng(e), b.n_txn, tnc, 30000)
+                erc, etn, etnc = orc.occ(b, hist_keys=hk, hist_tn=ht, tnc=tnc)
+                bb = b.to_torch("cuda:0") if device_ptrs else b
+                rc, tn, st = engine.occ_validate_epoch(bb, want_tn=True, append_history=True)
+                if device_ptrs:
+                    torch.cuda.synchronize()
+                    rc = rc.cpu().numpy()
+                    tn = tn.cpu().numpy().view(np.uint64)
+                assert np.array_equal(rc, erc), f"pass {rep} epoch {e}: rc differs"
+                assert np.array_equal(np.asarray(tn, np.uint64), etn), f"pass {rep} epoch {e}: tn differs"
+                nk, nt = committed_writes(b, etn)
+                hk = np.concatenate([hk, nk])
+                ht = np.concatenate([ht, nt])
+                tnc = etnc
+            gk, gt = engine.history_export()
+            wk, wt = sorted_pairs(hk, ht)
+            assert np.array_equal(gk, wk) and np.array_equal(gt, wt)
+    finally:
+        engine.set_option(OPT_HIST_MERGE, 65536)
+        engine.history_clear()
+        engine.tnc = 0
+
+
 def test_out_of_order_appends(engine):
     """Host appends with tns below earlier ones: levels re-sorted by (key, tn)."""
     rng = np.random.default_rng(5)
