@@ -62,9 +62,9 @@ def parse():
                          "N ranks (BASELINE config C5 with --theta 0.99 --seed 0xD3E7A002); "
                          "default is weak scaling (N x --txns txns)")
     ap.add_argument("--pmc", default=next((p for p in (os.path.join(ROOT, "profiles", r, "pmc.json")
-                                                       for r in ("r04", "r03")) if os.path.exists(p)),
-                                          os.path.join(ROOT, "profiles", "r04", "pmc.json")),
-                    help="PMC summary (tools/gpu_pmc_r04.sh -> tools/pmc_r04.py) the "
+                                                       for r in ("r05", "r04")) if os.path.exists(p)),
+                                          os.path.join(ROOT, "profiles", "r05", "pmc.json")),
+                    help="PMC summary (tools/gpu_pmc_r05.sh -> tools/pmc_r05.py) the "
                          "roofline.traffic / l2_hit fields and each config's pmc block are read "
                          "from (the workloads it describes at N=1; null otherwise)")
     ap.add_argument("--pipeline", type=int, default=4,
@@ -127,12 +127,15 @@ def _cpu_model() -> str:
 
 
 def host_threads() -> int:
-    """Host threads this process may run on (its CPU affinity), not
-    OMP_NUM_THREADS: the multi-threaded CPU baseline uses all of them."""
+    """Host threads the multi-threaded CPU baselines use: this process's CPU
+    affinity, capped by its share of the box (OMP_NUM_THREADS, 16 per GPU on
+    the test pool, where affinity and nproc show the whole machine)."""
     try:
-        return len(os.sched_getaffinity(0))
+        n = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
-        return os.cpu_count() or 1
+        n = os.cpu_count() or 1
+    share = os.environ.get("OMP_NUM_THREADS", "")
+    return max(1, min(n, int(share))) if share.isdigit() and int(share) > 0 else n
 
 
 def prefix_batch(b, n):
@@ -148,7 +151,7 @@ def prefix_batch(b, n):
 
 def _kern_l2(pw, name):
     """L2 hit rate of the first kernel of a PMC workload summary whose name
-    holds `name` (profiles/r04/pmc.json), or null."""
+    holds `name` (profiles/r05/pmc.json), or null."""
     for k, v in ((pw or {}).get("kernels") or {}).items():
         if name in k:
             return v.get("l2_hit")
