@@ -1097,7 +1097,9 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint3
   };
   // (only a bucket-path graph: it never reads the offsets, which the prep
   // is still validating, so a malformed batch cannot steer its accesses)
-  const bool spec = cv_graph_ok && cv_graph_exec && cv_graph_key.bucket && same_shape(cv_graph_key);
+  // (uniform txns only: the ragged form reads the offsets)
+  const bool spec = cv_graph_ok && cv_graph_exec && cv_graph_key.bucket && cv_graph_key.ulen &&
+                    same_shape(cv_graph_key);
   // the tail of every epoch: device clock, outputs to the host, counts
   auto enqueue_tail = [&](const uint32_t* wave_dev) -> int {
     CK(hipEventRecord(ev1, stream));
@@ -1149,13 +1151,14 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint3
   const bool have_seq = d.order && (oor ^ oand) && unsorted != 0;
   const KeyPack op = have_seq ? make_keypack(oor ^ oand) : KeyPack{};
   static_assert(sizeof(KeyPack) <= sizeof(CvGraphKey::kp), "key image");
-  // the bucket path (calvin_bucket.h) for large epochs of uniform txns;
+  // the bucket path (calvin_bucket.h) for large epochs, uniform or ragged
+  // txns (TPC-C, a key-sharded rank's share of YCSB);
   // DCC_OPT_CALVIN_PATH: 1 keeps the global sort + scan, 2 takes the bucket
   // path at every size it applies to (0: the bucket path on large epochs)
   const int cb_mode = cv_path == 1 ? 0 : cv_path == 2 ? 1 : -1;
   CbPlan cbp{};
-  const bool use_cb = d.nnz && cb_mode != 0 && !waves && nh == 0 && ulen &&
-                      (cb_mode == 1 || d.nnz >= CV_PUT_MIN) && cb_plan(d.n, d.nnz, ulen, kp.bits, &cbp);
+  const bool use_cb = d.nnz && cb_mode != 0 && !waves && nh == 0 &&
+                      (cb_mode == 1 || d.nnz >= CV_PUT_MIN) && cb_plan(d.n, d.nnz, ulen, maxlen, kp.bits, &cbp);
   gk.ulen = ulen;
   gk.have_seq = have_seq ? 1u : 0u;
   gk.bucket = use_cb ? 1u : 0u;
@@ -1242,7 +1245,7 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint3
     seq = vb[cur];
   }
   // request offsets in sequence order (uniform txns: q * len, no pass)
-  if (have_seq && !ulen) {
+  if (have_seq && !ulen && !use_cb) {  // (the bucket path builds its own per wave)
     const uint64_t lt = (d.n + CV_TILE - 1) / CV_TILE;
     CR(cv_len.ensure(this, d.n * 4 + 16, "calvin len"));
     CR(cv_off2.ensure(this, (d.n + 1) * 4 + 16, "calvin off2"));
@@ -1262,7 +1265,7 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint3
     CR(cb_out.ensure(this, cbp.out_bytes, "calvin bucket pairs"));
     CR(cb_cnt.ensure(this, cbp.cnt_bytes, "calvin bucket counts"));
     CR(cb_small.ensure(this, cbp.small_bytes, "calvin bucket totals"));
-    const CbArgs ca{d.keys, d.acctype, seq, d.n, d.nnz, ulen, kp, (uint64_t*)cb_e.p,
+    const CbArgs ca{d.keys, d.acctype, seq, d.off, d.n, d.nnz, ulen, kp, (uint64_t*)cb_e.p,
                     (uint64_t*)cb_out.p, (uint32_t*)cb_cnt.p, (uint32_t*)cb_small.p, grp_dev, rc_dev};
     CK(cb_run(cbp, ca, stream, profiling ? pev[1] : nullptr, profiling ? pev[2] : nullptr));
   } else if (d.nnz) {

@@ -24,21 +24,24 @@ struct CbPlan {
   uint32_t ndig;   // output windows
   uint32_t ntile;  // partition tiles
   uint32_t R;      // reservation-counter replicas (each with its own pair region)
-  uint64_t span;   // requests per window (2^tsh * ulen)
+  uint32_t wt;     // txns per partition wave (1024 / the longest txn)
+  uint64_t span;   // requests per window at most (2^tsh * the longest txn)
   // workspace sizes in bytes
   uint64_t elem_bytes, out_bytes, cnt_bytes, small_bytes;
 };
 
-// The plan for an epoch of n txns x ulen requests with kbits packed key bits;
-// false when the path does not apply (ragged txns, wide keys, too many windows).
-bool cb_plan(uint64_t n, uint64_t nnz, uint32_t ulen, uint32_t kbits, CbPlan* p);
+// The plan for an epoch of n txns x ulen requests (ulen 0: ragged txns of at
+// most maxlen requests) with kbits packed key bits; false when the path does
+// not apply (wide keys, too many windows).
+bool cb_plan(uint64_t n, uint64_t nnz, uint32_t ulen, uint32_t maxlen, uint32_t kbits, CbPlan* p);
 
 struct CbArgs {
   const uint64_t* keys;
   const uint8_t* acctype;
   const uint32_t* seq;  // sequence position -> txn, or null (index order)
+  const uint32_t* off;  // index-order offsets (read for ragged txns)
   uint64_t n, nnz;
-  uint32_t ulen;
+  uint32_t ulen;        // requests per txn, or 0: ragged
   KeyPack kp;
   // workspaces (CbPlan sizes)
   uint64_t* elems;

@@ -58,6 +58,7 @@ constexpr uint32_t CB_STG = CB_CHUNK + CB_CHUNK / 32;  // one pad slot per 32 (b
 constexpr uint32_t CB_NDIG_MAX = 760;           // output windows (LDS: two bucket workgroups per CU)
 constexpr uint32_t CB_WIN = 32768;              // groups per output window (128 KiB of LDS)
 constexpr uint32_t CB_R = 8;                    // reservation-counter replicas
+constexpr uint32_t CB_TSH_RAGGED = 11;          // ragged txns: at most 2^11 txns per output window
 constexpr uint32_t NOTXN = 0xFFFFFFFFu;
 // carry-table word: bit 0 "the row's last request is the chunk's last txn",
 // bits 1-2 its lock type (CV_NONE: row not seen yet), bits 3.. its group count
@@ -118,10 +119,12 @@ struct CbSrc {
   const uint64_t* keys;
   const uint8_t* at;
   const uint32_t* seq;
+  const uint32_t* off;  // index-order offsets (ragged txns)
   uint32_t n;     // txns
-  uint32_t ulen;  // requests per txn
+  uint32_t ulen;  // requests per txn (0: ragged, at most maxlen each)
   uint32_t um;    // (2^20 + ulen - 1) / ulen: e / ulen == (e * um) >> 20 for e <= 1024
-  uint32_t wt;    // txns per wave and sub-tile (1024 / ulen)
+  uint32_t wt;    // txns per wave and sub-tile (1024 / ulen, or 1024 / maxlen)
+  uint32_t nnz;
   uint32_t var;   // DCC_CB_VARIANT timing variants (wrong results): 1 no partition stores,
                   // 2 no ranking, 4 no element loads
   KeyPack kp;
@@ -133,9 +136,14 @@ struct CbSrc {
 // e % ulen of txn e / ulen: every key (and type) load of the wave is issued
 // before the first is used.  FULL: the element (packed key high, txn:25 |
 // j:6 | EX:1 low), else the packed key alone; past the end ~0 (sorts last).
+//
+// Ragged txns (s.ulen == 0, each at most 1024 / wt requests): the wave also
+// stages each txn's first request (s_b) and a map from its element to (txn
+// slot, request) (s_m, built from a wave scan of the lengths), so element e
+// finds its request with one LDS read instead of a division.
 template <bool FULL>
 __device__ inline uint32_t cb_wave_elems(const CbSrc& s, uint32_t q0, uint32_t nq, uint32_t* s_t,
-                                         uint64_t (&el)[16]) {
+                                         uint32_t* s_b, uint16_t* s_m, uint64_t (&el)[16]) {
   const uint32_t lane = threadIdx.x & 63u;
   if (nq == 0) {
 #pragma unroll
@@ -143,23 +151,65 @@ __device__ inline uint32_t cb_wave_elems(const CbSrc& s, uint32_t q0, uint32_t n
     return 0;
   }
   const uint32_t nk = (nq + 63) / 64;
-  for (uint32_t k = 0; k < nk; k++) {
-    const uint32_t i = k * 64 + lane;
-    if (i < nq) s_t[i] = s.seq ? s.seq[q0 + i] : q0 + i;
+  uint32_t ne = nq * s.ulen;
+  if (s.ulen) {
+    for (uint32_t k = 0; k < nk; k++) {
+      const uint32_t i = k * 64 + lane;
+      if (i < nq) s_t[i] = s.seq ? s.seq[q0 + i] : q0 + i;
+    }
+  } else {
+    uint32_t run = 0;
+    for (uint32_t k = 0; k < nk; k++) {
+      const uint32_t i = k * 64 + lane;
+      uint32_t t = 0, b = 0, len = 0;
+      if (i < nq) {
+        t = s.seq ? s.seq[q0 + i] : q0 + i;
+        b = min(s.off[t], s.nnz);
+        const uint32_t e = min(max(s.off[t + 1], b), s.nnz);
+        len = min(e - b, 64u);  // MAX_ROW_PER_TXN (the prep validated it)
+        s_t[i] = t;
+        s_b[i] = b;  // (the count pass passes s_b == s_t: only b is read there)
+      }
+      uint32_t x = len;  // inclusive wave scan of the lengths
+#pragma unroll
+      for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d);
+        if (lane >= d) x += y;
+      }
+      const uint32_t p = run + x - len;
+      // (the plan keeps wt * maxlen <= 1024; the clamp only guards the LDS)
+      for (uint32_t r = 0; r < len && p + r < 1024u; r++) s_m[p + r] = (uint16_t)((i << 6) | r);
+      run += __shfl(x, 63);
+    }
+    ne = min(run, 1024u);
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const uint32_t ne = nq * s.ulen;
+  if (ne == 0) {
+#pragma unroll
+    for (uint32_t it = 0; it < 16; it++) el[it] = ~0ull;
+    return 0;
+  }
   uint64_t kk[16];
   uint32_t tj[16];
   uint8_t aa[16];
 #pragma unroll
   for (uint32_t it = 0; it < 16; it++) {
     const uint32_t e = min(it * 64 + lane, ne - 1);
-    const uint32_t i = (e * s.um) >> 20, j = e - i * s.ulen;
+    uint32_t i, j;
+    uint64_t x;
+    if (s.ulen) {
+      i = (e * s.um) >> 20;
+      j = e - i * s.ulen;
+      x = (uint64_t)s_t[i] * s.ulen + j;
+    } else {
+      const uint32_t m = s_m[e];
+      i = m >> 6;
+      j = m & 63u;
+      x = (uint64_t)s_b[i] + j;
+    }
     const uint32_t t = s_t[i];
-    const uint64_t x = (uint64_t)t * s.ulen + j;
     kk[it] = s.keys[x];
     if (FULL) aa[it] = s.at[x];
     tj[it] = (t << 7) | (j << 1);
@@ -184,7 +234,8 @@ __device__ inline uint32_t cb_wave_elems(const CbSrc& s, uint32_t q0, uint32_t n
 __global__ __launch_bounds__(CB_PT) void k_cb_count(CbSrc s, uint32_t bmask, uint32_t* __restrict__ cnt) {
   constexpr uint32_t W = CB_PT / 64;
   __shared__ uint32_t s_h[1u << CB_BB_MAX];
-  __shared__ uint32_t s_t[W][1024];
+  __shared__ uint32_t s_t[W][1024];  // txn ids; ragged txns: their first requests (ids are not needed here)
+  __shared__ uint16_t s_m[W][1024];  // ragged txns: element -> (txn slot, request)
   const uint32_t B = bmask + 1, lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   for (uint32_t i = threadIdx.x; i < B; i += CB_PT) s_h[i] = 0;
   __syncthreads();
@@ -194,7 +245,7 @@ __global__ __launch_bounds__(CB_PT) void k_cb_count(CbSrc s, uint32_t bmask, uin
     if (q0 >= s.n) break;  // this wave (no barrier in the loop)
     const uint32_t nq = (uint32_t)min<uint64_t>(s.wt, s.n - q0);
     uint64_t el[16];
-    const uint32_t ne = cb_wave_elems<false>(s, (uint32_t)q0, nq, s_t[wv], el);
+    const uint32_t ne = cb_wave_elems<false>(s, (uint32_t)q0, nq, s_t[wv], s_t[wv], s_m[wv], el);
 #pragma unroll
     for (uint32_t it = 0; it < 16; it++)
       if (it * 64 + lane < ne) atomicAdd(&s_h[(uint32_t)el[it] & bmask], 1u);
@@ -254,7 +305,8 @@ __global__ __launch_bounds__(CB_PT) void k_cb_part(CbSrc s, uint32_t bb, const u
   const uint32_t tpx = (ntile + 7) / 8;
   const uint32_t tile = (blockIdx.x % 8) * tpx + blockIdx.x / 8;
   if (tile >= ntile) return;  // whole workgroup (tile 0 is workgroup 0's)
-  __shared__ uint64_t s_stg[CB_SUB];  // also the waves' txn ids while the elements load
+  __shared__ uint64_t s_stg[CB_SUB];  // also the waves' txn ids (and ragged first requests) while the elements load
+  __shared__ uint16_t s_m[CB_PT / 64][1024];  // ragged txns: element -> (txn slot, request)
   __shared__ uint32_t s_cur[BM];      // global cursor of the bucket
   __shared__ uint32_t s_gof[BM];      // global destination minus staging index
   __shared__ uint16_t s_wc[W][BM];
@@ -284,13 +336,14 @@ __global__ __launch_bounds__(CB_PT) void k_cb_part(CbSrc s, uint32_t bb, const u
     uint64_t e[16];
     uint32_t ne;
     if (CB_VAR(s.var, 4u)) {
-      ne = nq * s.ulen;
+      ne = nq * max(s.ulen, 1u);
 #pragma unroll
       for (uint32_t it = 0; it < 16; it++)
         e[it] = ((uint64_t)((((uint32_t)q0 * 16 + it * 64 + lane) * 2654435761u) >> 8) << 32) |
                 ((uint32_t)min<uint64_t>(q0, s.n - 1) << 7);  // in-range row and txn
     } else {
-      ne = cb_wave_elems<true>(s, (uint32_t)q0, nq, (uint32_t*)s_stg + wv * 1024, e);
+      ne = cb_wave_elems<true>(s, (uint32_t)q0, nq, (uint32_t*)s_stg + wv * 1024,
+                               (uint32_t*)s_stg + CB_SUB + wv * 1024, s_m[wv], e);
     }
     __syncthreads();
     uint16_t loc[16];
@@ -648,16 +701,27 @@ __global__ __launch_bounds__(CB_BT) void k_cb_bucket(CbBucket a) {
 }
 
 // ---------------------------------------------------------------- put
+// Ragged txns (ulen == 0): the window's offsets are staged in LDS (s_off,
+// 2^tsh + 1 words, tsh <= CB_TSH_RAGGED) and a request's place is its txn's
+// offset plus its index.
 __global__ __launch_bounds__(1024) void k_cb_put(const uint64_t* __restrict__ in,
                                                  const uint32_t* __restrict__ gcnt, uint32_t ndig,
                                                  uint64_t span, uint32_t n, uint32_t ulen, uint32_t tsh,
+                                                 const uint32_t* __restrict__ off, uint32_t nnz,
                                                  uint32_t* __restrict__ group, uint8_t* __restrict__ rc) {
   __shared__ uint32_t win[CB_WIN];
   __shared__ uint32_t s_wait[CB_WIN / 32];
+  __shared__ uint32_t s_off[(1u << CB_TSH_RAGGED) + 1];
   const uint32_t d = blockIdx.x, tid = threadIdx.x;
   const uint32_t t_lo = d << tsh, ntx = min(n - t_lo, 1u << tsh);
-  const uint32_t w = ntx * ulen;
-  const uint64_t x_lo = (uint64_t)t_lo * ulen;
+  uint32_t w = ntx * ulen;
+  uint64_t x_lo = (uint64_t)t_lo * ulen;
+  if (!ulen) {
+    for (uint32_t i = tid; i <= ntx; i += 1024) s_off[i] = min(off[t_lo + i], nnz);
+    __syncthreads();
+    x_lo = s_off[0];
+    w = min(s_off[ntx] - s_off[0], (uint32_t)CB_WIN);  // the plan bounds it; the clamp guards the LDS
+  }
   for (uint32_t i = tid; i < (ntx + 31) / 32; i += 1024) s_wait[i] = 0;
   constexpr uint32_t U = 8;
   for (uint32_t r = 0; r < CB_R; r++) {
@@ -671,7 +735,9 @@ __global__ __launch_bounds__(1024) void k_cb_put(const uint64_t* __restrict__ in
       for (uint32_t u = 0; u < U; u++) {
         if (p0 + u * 1024 >= m) continue;
         const uint32_t v = (uint32_t)x[u];
-        win[((v >> 7) - t_lo) * ulen + ((v >> 1) & 63u)] = (uint32_t)(x[u] >> 32);
+        const uint32_t tl = (v >> 7) - t_lo, jj = (v >> 1) & 63u;
+        const uint32_t wi = ulen ? tl * ulen + jj : s_off[tl] - (uint32_t)x_lo + jj;
+        if (wi < w) win[wi] = (uint32_t)(x[u] >> 32);
       }
     }
   }
@@ -680,9 +746,19 @@ __global__ __launch_bounds__(1024) void k_cb_put(const uint64_t* __restrict__ in
   for (uint32_t i = tid; i < w; i += 1024) {
     const uint32_t g = win[i];
     dst[i] = g;
-    if (g != 0 && g != DCC_GROUP_NONE) {
+    if (ulen && g != 0 && g != DCC_GROUP_NONE) {
       const uint32_t tt = i / ulen;
       atomicOr(&s_wait[tt >> 5], 1u << (tt & 31u));
+    }
+  }
+  if (!ulen) {  // a thread per txn over its requests
+    for (uint32_t tt = tid; tt < ntx; tt += 1024) {
+      bool wait = false;
+      for (uint32_t i = s_off[tt] - (uint32_t)x_lo; i < min(s_off[tt + 1] - (uint32_t)x_lo, w); i++) {
+        const uint32_t g = win[i];
+        wait |= g != 0 && g != DCC_GROUP_NONE;
+      }
+      if (wait) atomicOr(&s_wait[tt >> 5], 1u << (tt & 31u));
     }
   }
   __syncthreads();
@@ -692,18 +768,21 @@ __global__ __launch_bounds__(1024) void k_cb_put(const uint64_t* __restrict__ in
 
 }  // namespace
 
-bool cb_plan(uint64_t n, uint64_t nnz, uint32_t ulen, uint32_t kbits, CbPlan* p) {
-  if (!ulen || ulen > 64 || nnz == 0 || nnz != n * ulen || nnz >= 0xFFFFFFFFull) return false;
+bool cb_plan(uint64_t n, uint64_t nnz, uint32_t ulen, uint32_t maxlen, uint32_t kbits, CbPlan* p) {
+  // uniform txns (ulen requests each), or ragged ones of at most maxlen
+  const uint32_t len = ulen ? ulen : maxlen;
+  if (!len || len > 64 || nnz == 0 || (ulen && nnz != n * ulen) || nnz >= 0xFFFFFFFFull) return false;
   if (kbits > CB_BB_MAX + CB_LB_MAX) return false;
   CbPlan q{};
   q.bb = std::min(CB_BB_MAX, kbits);
   q.lbits = kbits - q.bb;
   q.tsh = 0;
-  while ((2ull << q.tsh) * ulen <= CB_WIN) q.tsh++;
-  q.span = (1ull << q.tsh) * ulen;
+  while ((2ull << q.tsh) * len <= CB_WIN && (ulen || q.tsh < CB_TSH_RAGGED)) q.tsh++;
+  q.span = (1ull << q.tsh) * len;
   q.ndig = (uint32_t)((n + (1ull << q.tsh) - 1) >> q.tsh);
   if (q.ndig > CB_NDIG_MAX) return false;
-  const uint64_t tile_txn = (uint64_t)CB_NSUB * (CB_PT / 64) * (1024 / ulen);
+  q.wt = 1024 / len;
+  const uint64_t tile_txn = (uint64_t)CB_NSUB * (CB_PT / 64) * q.wt;
   q.ntile = (uint32_t)((n + tile_txn - 1) / tile_txn);
   q.R = CB_R;
   const uint64_t B = 1ull << q.bb;
@@ -725,8 +804,8 @@ hipError_t cb_run(const CbPlan& p, const CbArgs& a, hipStream_t st, hipEvent_t e
     const char* e = DCC_ENV("DCC_CB_VARIANT");
     return e ? (uint32_t)atoi(e) : 0u;
   }();
-  const CbSrc s{a.keys, a.acctype, a.seq, (uint32_t)a.n, a.ulen, ((1u << 20) + a.ulen - 1) / a.ulen,
-                1024 / a.ulen, var, a.kp};
+  const CbSrc s{a.keys,       a.acctype, a.seq, a.off, (uint32_t)a.n, a.ulen,
+                a.ulen ? ((1u << 20) + a.ulen - 1) / a.ulen : 0u, p.wt, (uint32_t)a.nnz, var, a.kp};
   hipError_t e = hipMemsetAsync(gcnt, 0, (size_t)p.R * p.ndig * 4, st);
   if (e != hipSuccess) return e;
   k_cb_count<<<p.ntile, CB_PT, 0, st>>>(s, B - 1, a.cnt);
@@ -740,8 +819,8 @@ hipError_t cb_run(const CbPlan& p, const CbArgs& a, hipStream_t st, hipEvent_t e
   k_cb_bucket<<<B, CB_BT, 0, st>>>(
       CbBucket{a.elems, tot, bbase, p.bb, p.lbits, p.tsh, p.ndig, p.span, gcnt, a.out, var});
   if (ev_bucket && (e = hipEventRecord(ev_bucket, st)) != hipSuccess) return e;
-  k_cb_put<<<p.ndig, 1024, 0, st>>>(a.out, gcnt, p.ndig, p.span, (uint32_t)a.n, a.ulen, p.tsh, a.group,
-                                    a.rc);
+  k_cb_put<<<p.ndig, 1024, 0, st>>>(a.out, gcnt, p.ndig, p.span, (uint32_t)a.n, a.ulen, p.tsh, a.off,
+                                    (uint32_t)a.nnz, a.group, a.rc);
   return hipGetLastError();
 }
 

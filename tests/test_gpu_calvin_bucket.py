@@ -4,10 +4,12 @@ LDS sort + grant-group scan with each row's state carried from chunk to chunk,
 and the windowed group write-out with readiness) against the oracle
 (`orc.calvin`, the Row_lock CALVIN replay restated: row_lock.cpp:78-81,
 152-170, 317-357).  DCC_OPT_CALVIN_PATH=2 takes the path at every size it applies
-to (uniform txn lengths <= 64, packed keys <= 24 bits); the cases cover one-row
+to (txn lengths <= 64, uniform or ragged, packed keys <= 24 bits); the cases cover one-row
 buckets, a single key, duplicates of a row inside a txn (also where a txn
 straddles a chunk boundary), hot rows spanning many chunks, sequencer orders
-with ties, txn lengths 1..64, and the fallback for wider keys."""
+with ties, txn lengths 1..64, ragged txns (random lengths with empty txns, a
+key-sharded rank's share of C4), and the fallback for wider keys (TPC-C's
+canonical keys pack to 26 bits: the sort path, test_gpu_calvin.py)."""
 import numpy as np
 import pytest
 
@@ -59,6 +61,59 @@ def check(engine, b):
 def test_uniform_random(engine, bucket, n, L, n_keys, order):
     rng = np.random.default_rng(n + L)
     check(engine, uniform_batch(rng, n, L, n_keys, types=(RD, WR, XP, SCAN), order=order))
+
+
+def ragged_batch(rng, n, maxlen, n_keys, order=False, zipf=None, p_empty=0.05):
+    lens = rng.integers(1, maxlen + 1, size=n)
+    lens[rng.random(n) < p_empty] = 0
+    off = np.zeros(n + 1, np.uint32)
+    off[1:] = np.cumsum(lens)
+    m = int(off[-1])
+    keys = ((rng.zipf(zipf, size=m) - 1) % n_keys) if zipf else rng.integers(0, n_keys, size=m)
+    at = rng.choice(np.array([RD, WR, XP, SCAN], np.uint8), size=m, p=[0.5, 0.3, 0.1, 0.1])
+    od = rng.integers(0, max(2, n // 4), size=n).astype(np.uint64) if order else None
+    return d.EpochBatch(off, keys.astype(np.uint64), at, None, None, od)
+
+
+@pytest.mark.parametrize("n,maxlen,n_keys,order", [
+    (7, 3, 5, True), (3000, 64, 50, False), (20000, 17, 4096, True), (50000, 5, 1 << 18, True),
+    (40000, 2, 300, False), (30000, 40, 1 << 22, True), (100000, 9, 1 << 20, False)])
+def test_ragged_random(engine, bucket, n, maxlen, n_keys, order):
+    # ragged txns take the bucket path too (element -> request map per wave,
+    # offsets staged per output window)
+    rng = np.random.default_rng(n * 7 + maxlen)
+    b = ragged_batch(rng, n, maxlen, n_keys, order=order, zipf=1.2 if n_keys > 1000 else None)
+    g, rc, _, st = engine.calvin_order_epoch(b, want_group=True)
+    assert st["fallback"] == 1, "the ragged epoch did not take the bucket path"
+    check(engine, b)
+
+
+def test_ragged_key_shard_of_c4(engine):
+    # one key shard's share of a sequenced YCSB epoch (what a key-sharded rank
+    # of C4 orders: 2 requests per txn on average, empty txns common) at 8
+    # shards, with the default path choice (the bucket path from 2^21 requests)
+    b = d.gen_ycsb(n_txn=1 << 20, zipf_theta=0.9, part_cnt=16, chunk_txns=4096, want_home=True)
+    home = b.meta["home"].astype(np.uint64)
+    seq = np.zeros(b.n_txn, np.uint64)
+    for h in np.unique(home):
+        idx = np.nonzero(home == h)[0]
+        seq[idx] = np.arange(idx.size, dtype=np.uint64)
+    keys = np.asarray(b.keys, np.uint64)
+    keep = np.asarray(d.shard_of_keys(keys, 8)) == 3
+    off = np.asarray(b.offsets, np.int64)
+    own = np.repeat(np.arange(b.n_txn), np.diff(off))
+    cnt = np.bincount(own[keep], minlength=b.n_txn)
+    noff = np.zeros(b.n_txn + 1, np.uint32)
+    noff[1:] = np.cumsum(cnt)
+    sb = d.EpochBatch(noff, keys[keep], np.asarray(b.acctype)[keep], None, None,
+                      (home << np.uint64(32)) | seq)
+    engine.set_option(d._abi.OPT_CALVIN_PATH, 2)
+    try:
+        _, _, _, st = engine.calvin_order_epoch(sb, want_group=True)
+        assert st["fallback"] == 1
+        check(engine, sb)
+    finally:
+        engine.set_option(d._abi.OPT_CALVIN_PATH, 0)
 
 
 def test_chunk_straddling_duplicates(engine, bucket):
