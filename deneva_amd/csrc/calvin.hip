@@ -32,10 +32,12 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
 #include <cstring>
 
 #include "calvin_bucket.h"
 #include "calvin_gl.h"
+#include "calvin_wave.h"
 #include "dcc.h"
 #include "dcc_ctx.h"
 #include "dcc_device.h"
@@ -365,6 +367,10 @@ struct ScanOut {
   uint32_t* pgx;    // [nnz] previous group start per request (waves) or null
   uint32_t* gsx;    // [nnz] own group start per request (waves) or null
   uint32_t* gsize;  // [nnz] group size by start position (waves) or null
+  // the one-CU walk (calvin_wave.h) instead of pgx / gsize: gsx holds the own
+  // group start | has-previous-group << 31, glast [m] the sorted position of
+  // each group's last element (by group start; only groups with a successor)
+  uint32_t* glast;
 };
 
 // Ordered tree reduction of 256 per-thread states (LDS).
@@ -529,14 +535,15 @@ __global__ __launch_bounds__(256) void k_cv_down(const K* __restrict__ sk,
     const uint32_t x = xo[i] + j;
     if (dup) {
       o.group[x] = DCC_GROUP_NONE;
-      if (o.pgx) {
-        o.pgx[x] = NOPOS;
-        o.gsx[x] = NOPOS;
-      }
+      if (o.gsx) o.gsx[x] = NOPOS;
+      if (o.pgx) o.pgx[x] = NOPOS;
       continue;
     }
     o.group[x] = run.cnt;
-    if (o.pgx) {
+    if (o.glast) {
+      o.gsx[x] = run.gs | (run.cnt ? 0x80000000u : 0u);
+      if (run.cnt && run.gs == (uint32_t)p) o.glast[run.pgs] = (uint32_t)p - 1u;
+    } else if (o.pgx) {
       o.pgx[x] = run.cnt ? run.pgs : NOPOS;
       o.gsx[x] = run.gs;
       if (last_gs != NOPOS && last_gs != run.gs) atomicMax(&o.gsize[last_gs], last_gnd);
@@ -941,7 +948,7 @@ template <typename K>
 static int calvin_sort_and_scan(dcc_ctx* ctx, const DevBatch& d, const uint32_t* seq,
                                 const uint32_t* off2, const KeyPack& kp, const ScanOut& so,
                                 const uint64_t* hkeys, const uint8_t* hat, uint64_t nh,
-                                bool prof) {
+                                bool prof, const uint32_t** sv_out) {
   const uint64_t m = nh + d.nnz;
   hipStream_t st = ctx->stream;
   CR(ctx->calvin_a.ensure(ctx, std::max<uint64_t>(16, m * sizeof(K)), "calvin keys a"));
@@ -968,7 +975,8 @@ static int calvin_sort_and_scan(dcc_ctx* ctx, const DevBatch& d, const uint32_t*
   else
     cur = radix_sort_u64((uint64_t**)kb, vb, m, kp.bits, (uint32_t*)ctx->cv_scratch.p, st);
   if (prof) CK(hipEventRecord(ctx->pev[2], st));
-  if (so.pgx) {  // wave levels: the full scan state
+  *sv_out = vb[cur];
+  if (so.gsx) {  // wave levels: the full scan state
     Gs* agg = (Gs*)ctx->cv_agg.p;
     k_cv_up<K><<<(unsigned)tiles, 256, 0, st>>>(kb[cur], vb[cur], m, agg);
     k_cv_top<<<1, 256, 0, st>>>(agg, (uint32_t)tiles);
@@ -1169,7 +1177,12 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint3
   uint32_t* wave_dev = nullptr;
   if (!(spec && !memcmp(&gk, &cv_graph_key, sizeof gk))) {
   cv_spec_miss += spec ? 1 : 0;
-  ScanOut so{d.off, ulen, (uint32_t)d.n, grp_dev, rc_dev, nullptr, nullptr, nullptr};
+  ScanOut so{d.off, ulen, (uint32_t)d.n, grp_dev, rc_dev, nullptr, nullptr, nullptr, nullptr};
+  const uint32_t* sv = nullptr;  // the sorted request values (waves)
+  // wave levels: the one-CU walk for txns of at most CW_LMAX requests, the
+  // dataflow grid (k_cv_wave) for longer ones
+  CwPlan cwp{};
+  const bool cw = waves && !DCC_ENV("DCC_CV_WAVE_GRID") && cw_plan(d.n, maxlen, &cwp);
   if (waves) {
     if (dev_out) {
       wave_dev = out_wave;
@@ -1178,17 +1191,33 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint3
       wave_dev = (uint32_t*)cv_wave.p;
     }
     const uint64_t m = std::max<uint64_t>(16, d.nnz * 4);
-    CR(cv_pgx.ensure(this, m, "calvin pgx"));
     CR(cv_gsx.ensure(this, m, "calvin gsx"));
-    CR(cv_gsize.ensure(this, m, "calvin gsize"));
-    CR(cv_done.ensure(this, m, "calvin done"));
-    CR(cv_maxl.ensure(this, m, "calvin maxl"));
-    CK(hipMemsetAsync(cv_gsize.p, 0, m, stream));
-    CK(hipMemsetAsync(cv_done.p, 0, m, stream));
-    CK(hipMemsetAsync(cv_maxl.p, 0, m, stream));
-    so.pgx = (uint32_t*)cv_pgx.p;
     so.gsx = (uint32_t*)cv_gsx.p;
-    so.gsize = (uint32_t*)cv_gsize.p;
+    if (cw) {
+      CR(cv_pgx.ensure(this, m, "calvin group last"));
+      CK(hipMemsetAsync(cv_pgx.p, 0xFF, m, stream));
+      so.glast = (uint32_t*)cv_pgx.p;
+      const uint64_t sb = std::max<uint64_t>(16, cwp.slots * 4);
+      CR(cv_gsize.ensure(this, sb, "calvin wave records"));
+      CR(cv_done.ensure(this, sb, "calvin wave previous"));
+      CR(cv_maxl.ensure(this, sb, "calvin wave own"));
+      CR(cv_cwmax.ensure(this, sb, "calvin wave maxima"));
+      CR(cv_cwpos.ensure(this, d.n * 4 + 16, "calvin seqpos"));
+      CR(cv_cwmark.ensure(this, cwp.slots + 16, "calvin wave marks"));
+      CR(cv_cwhot.ensure(this, (uint64_t)cwp.nch * cwp.C * 32 + 16, "calvin wave compact records"));
+      CR(cv_cwpa.ensure(this, sb, "calvin wave read addresses"));
+      CR(cv_cwoa.ensure(this, sb, "calvin wave publish addresses"));
+    } else {
+      CR(cv_pgx.ensure(this, m, "calvin pgx"));
+      CR(cv_gsize.ensure(this, m, "calvin gsize"));
+      CR(cv_done.ensure(this, m, "calvin done"));
+      CR(cv_maxl.ensure(this, m, "calvin maxl"));
+      CK(hipMemsetAsync(cv_gsize.p, 0, m, stream));
+      CK(hipMemsetAsync(cv_done.p, 0, m, stream));
+      CK(hipMemsetAsync(cv_maxl.p, 0, m, stream));
+      so.pgx = (uint32_t*)cv_pgx.p;
+      so.gsize = (uint32_t*)cv_gsize.p;
+    }
   }
 
   // ---- the rest of the epoch as one captured HIP graph: the launches below
@@ -1270,9 +1299,9 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint3
     CK(cb_run(cbp, ca, stream, profiling ? pev[1] : nullptr, profiling ? pev[2] : nullptr));
   } else if (d.nnz) {
     if (kp.bits <= 32)
-      CR(calvin_sort_and_scan<uint32_t>(this, d, seq, off2, kp, so, hkeys, hat, nh, profiling));
+      CR(calvin_sort_and_scan<uint32_t>(this, d, seq, off2, kp, so, hkeys, hat, nh, profiling, &sv));
     else
-      CR(calvin_sort_and_scan<uint64_t>(this, d, seq, off2, kp, so, hkeys, hat, nh, profiling));
+      CR(calvin_sort_and_scan<uint64_t>(this, d, seq, off2, kp, so, hkeys, hat, nh, profiling, &sv));
   } else if (profiling) {
     CK(hipEventRecord(pev[1], stream));
     CK(hipEventRecord(pev[2], stream));
@@ -1292,7 +1321,33 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint3
   if (comm_ranks() > 1) CR(comm_allreduce_max_u8(rc_dev, d.n));
 
   // ---- wave levels
-  if (waves) {
+  if (cw) {
+    const CwArgs ca{d.n, seq, d.off, ulen, so.gsx, so.glast, sv, (uint32_t*)cv_cwpos.p,
+                    (uint32_t*)cv_gsize.p, (uint32_t*)cv_done.p, (uint32_t*)cv_maxl.p,
+                    (uint32_t*)cv_cwmax.p, (uint8_t*)cv_cwmark.p, (uint32_t*)cv_cwpa.p,
+                    (uint32_t*)cv_cwoa.p, (uint32_t*)cv_cwhot.p,
+                    wave_dev, err, nullptr};
+    if (DCC_ENV("DCC_CW_DBG")) {  // experiments builds: the walker's timing counters
+      static uint64_t* dbg = nullptr;
+      if (!dbg) CK(hipMalloc(&dbg, 128));
+      CK(hipMemsetAsync(dbg, 0, 128, stream));
+      CwArgs cd = ca;
+      cd.dbg = dbg;
+      CK(cw_run(cwp, cd, stream));
+      uint64_t h[15];
+      CK(hipMemcpyAsync(h, dbg, 120, hipMemcpyDeviceToHost, stream));
+      CK(hipStreamSynchronize(stream));
+      fprintf(stderr, "cw: chunks %u C %u H %u walk %.3f ms rounds-loop %.3f ms barriers %.3f ms rounds %llu"
+              " | staging: maxima+fence %.3f sync %.3f bounds %.3f rest %.3f ms | clock %.0f MHz"
+              " | sub-chunks with intra %llu overflow %llu plain rounds %llu\n",
+              cwp.nch, cwp.C, cwp.H, h[0] * 1e-5, h[1] * 1e-5, h[2] * 1e-5, (unsigned long long)h[3],
+              h[4] * 1e-5, h[5] * 1e-5, h[6] * 1e-5, h[7] * 1e-5,
+              h[9] ? (double)h[8] / (h[9] * 1e-2) : 0.0, (unsigned long long)h[10],
+              (unsigned long long)h[11], (unsigned long long)h[12]);
+    } else {
+      CK(cw_run(cwp, ca, stream));
+    }
+  } else if (waves) {
     WaveArgs wa{d.n, seq, d.off, so.pgx, so.gsx, so.gsize, (uint32_t*)cv_done.p,
                 (uint32_t*)cv_maxl.p, wave_dev, err, 100000000ull * 20};
     // co-resident persistent grid: 4 workgroups of 4 waves per CU
@@ -1325,7 +1380,7 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint3
   }  // not replayed
   CR(enqueue_tail(wave_dev));
   }  // not a confirmed speculation
-  if (*(const uint32_t*)hmisc & ERR_WAVE_TIMEOUT)
+  if (*(const uint32_t*)hmisc & (ERR_WAVE_TIMEOUT | CW_ERR_SPIN))
     return fail(DCC_EIO, "calvin: wave kernel exceeded its time budget");
   uint64_t ready = 0;
   uint32_t maxwave = 0;
