@@ -26,8 +26,9 @@
 //   key sort       stable radix sort by packed key -> per-row FIFO runs
 //   k_cv_up/top/down  one segmented scan (monoid below) -> group, dedup,
 //                  readiness, and the group links the wave kernel needs
-//   k_cv_wave      (optional) wave levels, dependency-driven, one txn per
-//                  wave64 in sequence order
+//   waves          (optional) wave levels: the one-CU sequence-order walk
+//                  (calvin_wave.h) for txns of at most 32 requests, else
+//                  k_cv_wave, dependency-driven, one txn per wave64
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
