@@ -339,7 +339,24 @@ int dcc_multi_calvin_epoch(dcc_ctx* ctx, const dcc_batch* b, const dcc_calvin_he
                            uint32_t* out_group, uint8_t* out_rc, uint32_t* out_wave,
                            dcc_stats* st) {
   if (!b) return ctx->fail(DCC_EINVAL, "null batch");
-  if (out_wave) return ctx->fail(DCC_ENOTSUP, "calvin: wave levels need the whole epoch on one GPU");
+  if (out_wave) {
+    // wave levels chain through every row of the epoch (one walk in
+    // sequence order, calvin_wave.h): the whole epoch runs on rank 0's GPU,
+    // as one context (no exchange), reading a device batch over xGMI
+    if (held && held->n)
+      return ctx->fail(DCC_ENOTSUP, "calvin: wave levels need an empty lock table (no held prefix)");
+    dcc_ctx* s = ctx->multi->sub[0];
+    int prev = 0;
+    if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(s->device) != hipSuccess)
+      return ctx->fail(DCC_ENODEV, "multi-GPU: cannot select rank 0's device");
+    dcc_comm_state* const cm = s->comm;
+    s->comm = nullptr;
+    const int e = s->calvin_epoch(b, nullptr, out_group, out_rc, out_wave, st);
+    s->comm = cm;
+    (void)hipSetDevice(prev);
+    if (e != DCC_OK) return ctx->fail(e, "%s", s->last_error.c_str());
+    return DCC_OK;
+  }
   if (int e = ctx->check_batch(b)) return e;
   if (int e = multi_check_device_batch(ctx, b)) return e;
   if (held && held->n && (!held->keys || !held->acctype))

@@ -130,6 +130,26 @@ def test_multi_calvin_c4_full_8_shards(c4):
         assert st["n_shards"] == 8 and st["n_commit"] == int((erc == 0).sum())
 
 
+def test_multi_calvin_waves_on_rank0():
+    """Wave levels on a multi-GPU context: the whole epoch runs on rank 0's
+    GPU (the levels chain through every row); groups, readiness and waves
+    equal the oracle's, host and device batches."""
+    import torch
+    from helpers import c4_batch
+    b = c4_batch(40000)
+    eg, erc, ew = orc.calvin(b)
+    with d.Engine(devices=[0, 0, 0]) as eng:
+        g, rc, w, st = eng.calvin_order_epoch(b, want_group=True, want_wave=True)
+        assert np.array_equal(np.asarray(g).astype(np.uint32), eg)
+        assert np.array_equal(np.asarray(rc), erc)
+        assert np.array_equal(np.asarray(w).astype(np.uint32), ew)
+        assert st["rounds"] == int(ew.max()) + 1
+        g2, rc2, w2, _ = eng.calvin_order_epoch(b.to_torch("cuda:0"), want_group=True, want_wave=True)
+        torch.cuda.synchronize()
+        assert np.array_equal(w2.cpu().numpy().view(np.uint32)[:b.n_txn], ew)
+        assert np.array_equal(rc2.cpu().numpy()[:b.n_txn], erc)
+
+
 @pytest.mark.parametrize("bad_rank", [0, 2])
 def test_multi_rank_failure_does_not_hang(bad_rank):
     """One rank fails before its first exchange (fault injection): every
