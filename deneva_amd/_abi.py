@@ -49,6 +49,7 @@ OPT_FAIL_RANK = 8
 OPT_RO_SPLIT = 10
 OPT_PIPELINE = 11
 OPT_CALVIN_PATH = 12
+OPT_COMM_SOLO = 13
 
 
 class Batch(C.Structure):
@@ -192,6 +193,7 @@ _SIGS = [
     ("dcc_comm_init_host", C.c_int, [_P, C.c_int, C.c_int, C.c_void_p, _P]),
     ("dcc_comm_rank", C.c_int, [_P]),
     ("dcc_comm_size", C.c_int, [_P]),
+    ("dcc_comm_calls", C.c_uint64, [_P]),
     ("dcc_comm_destroy", C.c_int, [_P]),
     ("dcc_key_shard", C.c_uint32, [C.c_uint64, C.c_uint32]),
     ("dcc_key_shard_n", C.c_int, [_P, C.c_uint64, C.c_uint32, _P]),

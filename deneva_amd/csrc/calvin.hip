@@ -1069,7 +1069,7 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint3
   }
   const bool waves = out_wave != nullptr;
   uint32_t* err = (uint32_t*)misc.p;
-  const bool cv_graph_ok = !profiling && !waves && nh == 0 && comm_ranks() == 1 &&
+  const bool cv_graph_ok = !profiling && !waves && nh == 0 && !sharded() &&
                            !DCC_ENV("DCC_NO_GRAPH");
   CvGraphKey gk;
   memset(&gk, 0, sizeof gk);
@@ -1319,7 +1319,7 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint3
 
   // ---- sharded: grant groups are per row, hence shard-local; a txn is
   // ready only if it is ready on every shard (WAIT = 3 > RCOK = 0)
-  if (comm_ranks() > 1) CR(comm_allreduce_max_u8(rc_dev, d.n));
+  if (sharded()) CR(comm_allreduce_max_u8(rc_dev, d.n));
 
   // ---- wave levels
   if (cw) {

@@ -29,15 +29,19 @@ struct dcc_comm_state {
   uint8_t* hbuf = nullptr;  // pinned staging for the host backend
   uint64_t hcap = 0;
   bool aborted = false;     // ncclCommAbort ran (a peer rank failed)
+  bool solo = false;        // a one-rank RCCL clique running the sharded paths (DCC_OPT_COMM_SOLO)
+  uint64_t calls = 0;       // collectives run (dcc_comm_calls)
 };
 
 int dcc_ctx::comm_ranks() const { return comm ? comm->nranks : 1; }
+bool dcc_ctx::sharded() const { return comm && (comm->nranks > 1 || comm->solo); }
 int dcc_ctx::comm_rank() const { return comm ? comm->rank : 0; }
 
 int dcc_ctx::comm_allreduce_max_u8(uint8_t* dev, uint64_t n) {
   dcc_ctx* ctx = this;
-  if (!comm || comm->nranks <= 1 || n == 0) return DCC_OK;
+  if (!sharded() || n == 0) return DCC_OK;
   if (comm->aborted) return fail(DCC_ECOMM, "communicator aborted (a peer rank failed)");
+  comm->calls++;
   if (comm->nccl) {
     const ncclResult_t r = ncclAllReduce(dev, dev, n, ncclUint8, ncclMax, comm->nccl, stream);
     if (r != ncclSuccess) return fail(DCC_ECOMM, "ncclAllReduce: %s", ncclGetErrorString(r));
@@ -63,12 +67,13 @@ int dcc_ctx::comm_allreduce_max_u8(uint8_t* dev, uint64_t n) {
 
 int dcc_ctx::comm_allgather_u8(const uint8_t* send, uint8_t* recv, uint64_t bytes) {
   const int R = comm_ranks(), me = comm_rank();
-  if (R <= 1) {
+  if (!sharded()) {
     const hipError_t e = hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, stream);
     return e == hipSuccess ? DCC_OK : hip_fail(e, "allgather copy");
   }
   if (comm->aborted) return fail(DCC_ECOMM, "communicator aborted (a peer rank failed)");
   if (comm->nccl) {
+    comm->calls++;
     const ncclResult_t r = ncclAllGather(send, recv, bytes, ncclUint8, comm->nccl, stream);
     if (r != ncclSuccess) return fail(DCC_ECOMM, "ncclAllGather: %s", ncclGetErrorString(r));
     return DCC_OK;
@@ -104,7 +109,8 @@ extern "C" int dcc_comm_init(dcc_ctx* ctx, int rank, int nranks, const void* uni
   auto* c = new dcc_comm_state;
   c->rank = rank;
   c->nranks = nranks;
-  if (nranks > 1) {
+  c->solo = nranks == 1 && ctx->comm_solo;
+  if (nranks > 1 || c->solo) {
     ncclUniqueId id;
     memcpy(&id, unique_id, sizeof id);
     const ncclResult_t e = ncclCommInitRank(&c->nccl, nranks, id, rank);
@@ -159,6 +165,16 @@ extern "C" int dcc_comm_destroy(dcc_ctx* ctx) {
   delete ctx->comm;
   ctx->comm = nullptr;
   return DCC_OK;
+}
+
+extern "C" uint64_t dcc_comm_calls(const dcc_ctx* ctx) {
+  if (!ctx) return 0;
+  if (ctx->multi) {
+    uint64_t s = 0;
+    for (int r = 0; r < dcc_multi_size(ctx); r++) s += dcc_comm_calls(dcc_multi_sub((dcc_ctx*)ctx, r));
+    return s;
+  }
+  return ctx->comm ? ctx->comm->calls : 0;
 }
 
 extern "C" int dcc_comm_rank(const dcc_ctx* ctx) { return ctx && ctx->comm ? ctx->comm->rank : 0; }

@@ -206,6 +206,8 @@ struct dcc_ctx {
   dcc_comm_state* comm = nullptr;
   dcc_multi* multi = nullptr;  // non-null: this context drives per-GPU sub-contexts
   int comm_ranks() const;
+  bool sharded() const;    // the key-sharded paths run (ranks > 1, or a one-rank RCCL clique)
+  bool comm_solo = false;  // DCC_OPT_COMM_SOLO
   int comm_allreduce_max_u8(uint8_t* dev, uint64_t n);  // in place, on `stream`
   // every rank's `bytes` from send into recv[rank * bytes ...], on `stream`
   int comm_allgather_u8(const uint8_t* send, uint8_t* recv, uint64_t bytes);

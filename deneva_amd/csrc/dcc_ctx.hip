@@ -194,7 +194,9 @@ extern "C" int dcc_set_option(dcc_ctx* ctx, int option, int64_t value) {
   }
   if (option == DCC_OPT_PIPELINE) {
     if (value < 1 || value > 8) return DCC_EINVAL;
-    dcc_pipe_destroy(ctx);  // lanes are re-created at the new count
+    // the epochs in flight complete on their lanes (their results and
+    // tickets stay until waited); the next submit resizes the lanes
+    dcc_pipe_drain(ctx);
     ctx->pipe_lanes = (uint32_t)value;
     return DCC_OK;
   }
@@ -230,6 +232,11 @@ extern "C" int dcc_set_option(dcc_ctx* ctx, int option, int64_t value) {
     case DCC_OPT_CALVIN_PATH:
       if (value < 0 || value > 2) return DCC_EINVAL;
       ctx->cv_path = (int)value;
+      return DCC_OK;
+    case DCC_OPT_COMM_SOLO:
+      if (value != 0 && value != 1) return DCC_EINVAL;
+      if (ctx->comm) return ctx->fail(DCC_EINVAL, "DCC_OPT_COMM_SOLO: set before dcc_comm_init");
+      ctx->comm_solo = value != 0;
       return DCC_OK;
     case DCC_OPT_BATCH_MAX:
       if (value < 1 || value > 32) return DCC_EINVAL;
@@ -437,7 +444,8 @@ HistView dcc_ctx::hist_view() const {
     const HistStore& h = hs[q];
     v.lv[q] = HistLevel{(const uint64_t*)h.hash.p, (const uint64_t*)h.stn.p,
                         h.chained ? (const uint64_t*)h.ft.p : nullptr, h.chained ? (const uint32_t*)h.nx.p : nullptr,
-                        h.hbits, h.m && h.built ? 1u : 0u};
+                        h.hbits, h.m && h.built ? 1u : 0u,
+                        (uint32_t)std::min<uint64_t>(h.m, HIST_NIL), 0u};
   }
   v.bm = (const uint32_t*)h_bm.p;  // set by hist_prepare
   return v;

@@ -1208,9 +1208,11 @@ int dcc_ctx::maat_epoch_try(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_c
   const uint64_t tiles = (m + MT_TILE - 1) / MT_TILE;
   CR(mt_agg.ensure(this, std::max<uint64_t>(1, tiles) * sizeof(Ms), "maat scan"));
   {
-    const void* old = mt_lb.p;
+    // any reallocation is cleared, even at the old address (its grown tail
+    // holds the previous owner's words; see occ_begin's fin_part)
+    const size_t old_cap = mt_lb.cap;
     CR(mt_lb.ensure(this, std::max<uint64_t>(1, tiles) * sizeof(MtLb), "maat look-back status"));
-    if (mt_lb.p != old || mt_tag + 64 >= (1u << 30)) {  // fresh memory, or the tags wrap
+    if (mt_lb.cap != old_cap || mt_tag + 64 >= (1u << 30)) {  // reallocated, or the tags wrap
       CK(hipMemsetAsync(mt_lb.p, 0, mt_lb.cap, stream));
       mt_tag = 0;
     }

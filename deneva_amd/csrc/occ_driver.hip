@@ -111,7 +111,7 @@ static constexpr size_t MISC_KFLAG = 64, MISC_RING = 512,
 // per batch.
 int dcc_ctx::occ_rounds(const SubProb& sp, uint32_t maxlen, bool prof, uint32_t& rounds_out) {
   dcc_ctx* ctx = this;
-  const bool sh = comm_ranks() > 1;
+  const bool sh = sharded();
   rounds_out = 0;
   if (sp.n == 0) return DCC_OK;
   // txns per wave: build tiles stage TILE_CAP accesses, round tiles ROUND_CAP
@@ -801,7 +801,7 @@ int dcc_ctx::occ_begin(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, bo
   r.out_rc = out_rc;
   r.out_tn = out_tn;
   // key-sharded across ranks: this rank holds only its keys
-  r.sh = comm_ranks() > 1;
+  r.sh = sharded();
   r.t_wall0 = wall_ms();
   // the one-GPU sweep validates a host batch's offsets on the device (its
   // level-0 launch, prep_body; every kernel before clamps its indices), so the
@@ -826,12 +826,14 @@ int dcc_ctx::occ_begin(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, bo
     return DCC_OK;
   }
   DevBatch& d = r.d;
-  r.whole = r.sh && (b->flags & DCC_SHARD_SELF) && use_sweep();
-  if (r.whole) {
+  const bool self_shard = r.sh && (b->flags & DCC_SHARD_SELF);
+  r.whole = self_shard && use_sweep();
+  if (self_shard) {
     // this rank's key shard of the whole batch, partitioned on the device;
-    // the whole batch stays for the serial passes and the read-only list
+    // the sweep keeps the whole batch for its serial passes and the
+    // read-only list (the round solver needs only the shard)
     dcc_batch sb;
-    CR(shard_stage(b, (uint32_t)comm_rank(), (uint32_t)comm_ranks(), sb, &r.full));
+    CR(shard_stage(b, (uint32_t)comm_rank(), (uint32_t)comm_ranks(), sb, r.whole ? &r.full : nullptr));
     CR(stage_batch(&sb, d));
   } else {
     CR(stage_batch(b, d));
@@ -848,9 +850,15 @@ int dcc_ctx::occ_begin(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, bo
   if (r.want_tn) {
     CR(cflag.ensure(this, d.n * 4, "cflag"));
     {
-      const void* old = fin_part.p;
+      // Any reallocation is cleared, even one that returns the old address:
+      // the grown tail then holds whatever the allocator's previous owner left
+      // there -- for a context sharing the GPU with another one (the shards of
+      // a multi-GPU context on one device), look-back words carrying the same
+      // tag sequence, which k_fin would take as its own predecessors'
+      // prefixes (the round-5 "numbered 339 txns, 480 committed writers").
+      const size_t old_cap = fin_part.cap;
       CR(fin_part.ensure(this, fin_part_bytes(d.n), "finish look-back words"));
-      if (fin_part.p != old || fin_tag + 4 >= (1u << 30)) {  // fresh memory, or the tags wrap
+      if (fin_part.cap != old_cap || fin_tag + 4 >= (1u << 30)) {  // reallocated, or the tags wrap
         CK(hipMemsetAsync(fin_part.p, 0, fin_part.cap, stream));
         fin_tag = 0;
       }
@@ -874,6 +882,12 @@ int dcc_ctx::occ_begin(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, bo
     y.ins = r.app ? hist_insert_args(hs[1]) : HistInsert{};
     y.view = hist_view();
   }
+  // central_finish pushes this epoch's pairs onto the delta's chains before
+  // the host learns whether the epoch succeeded: until occ_end accepts the
+  // append, the delta counts as unbuilt, so an epoch that fails (and a retry
+  // that pushes the same flat positions again) leaves a table the next
+  // window check rebuilds from the flat pairs instead of walking
+  if (r.app) hs[1].built = false;
   // The sweep's whole launch sequence (parameters ... central_finish) is
   // replayed from a captured HIP graph when the batch, the outputs and every
   // workspace are the ones it was captured with: one graph launch instead of
@@ -1339,24 +1353,33 @@ int dcc_ctx::occ_end(dcc_stats* st) {
     if (r.want_tn) {
       // central_finish ran on the device (k_fin_*): its totals
       const uint64_t* tot = (const uint64_t*)((const char*)hdyn + HDYN_TOTALS);
-      if (tot[0] != n_cw)
-        return fail(DCC_EIO, "central_finish numbered %llu txns, %llu committed writers",
-                    (unsigned long long)tot[0], (unsigned long long)n_cw);
-      if (r.app && tot[1]) {
+      if (tot[0] != n_cw) {
+        // the look-back words of the last launch explain the mismatch
+        std::string why = "look-back words unreadable";
+        std::vector<uint8_t> w(fin_part_bytes(d.n));
+        if (hipMemcpy(w.data(), fin_part.p, w.size(), hipMemcpyDeviceToHost) == hipSuccess)
+          why = fin_diag(w.data(), d.n, fin_tag);
+        (void)hipGetLastError();
+        return fail(DCC_EIO, "central_finish numbered %llu txns, %llu committed writers (%s)",
+                    (unsigned long long)tot[0], (unsigned long long)n_cw, why.c_str());
+      }
+      if (r.app) {
         HistStore& D = hs[1];
         if (tot[1] > d.nnz) return fail(DCC_EIO, "history append: %llu writes > %llu accesses",
                                         (unsigned long long)tot[1], (unsigned long long)d.nnz);
-        D.m += tot[1];
-        D.max_key = std::max<uint64_t>(D.max_key, tot[2]);
-        D.last_app = tot[1];
-        hist_note(D, tnc + 1, tnc + n_cw);
-        // the pairs went onto the delta's chains too, unless its table ran out
-        // of room (then it is rebuilt bigger before its next read) or an
-        // earlier central_finish of this epoch pushed pairs of a partly
-        // decided epoch (then it is rebuilt from the flat pairs, which the
-        // last one rewrote)
+        if (tot[1]) {
+          D.m += tot[1];
+          D.max_key = std::max<uint64_t>(D.max_key, tot[2]);
+          D.last_app = tot[1];
+          hist_note(D, tnc + 1, tnc + n_cw);
+        }
+        // the pairs went onto the delta's chains too (the table holds every
+        // flat pair again), unless its table ran out of room (then it is
+        // rebuilt bigger before its next read) or an earlier central_finish
+        // of this epoch pushed pairs of a partly decided epoch (then it is
+        // rebuilt from the flat pairs, which the last one rewrote)
         if (tot[3]) D.overflowed = true;
-        else if (r.fin_runs <= 1) D.built = true;
+        D.built = !tot[3] && r.fin_runs <= 1;
       }
     }
     tnc += n_cw;

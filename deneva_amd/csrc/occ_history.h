@@ -37,6 +37,8 @@ struct HistLevel {
   const uint32_t* next;  // the flat pairs' chain links (HIST_NIL ends), or null
   uint32_t hbits;
   uint32_t on;           // 0: the level is empty
+  uint32_t walk;         // flat pairs of the level: no chain is longer, no link points past it
+  uint32_t pad;
 };
 // A probe slot (16 B): the key and the complement of its largest tn
 // (all-ones when empty, so a chain push lowers it with atomicMin).  Every key
@@ -56,9 +58,11 @@ __device__ inline bool hist_found_hit(const HistLevel& L, uint64_t s, uint64_t t
   if (tmax <= lo) return false;
   if (tmax <= hi) return true;  // tmax is in the window
   const ulonglong2 side = reinterpret_cast<const ulonglong2*>(L.hash + (2ull << L.hbits))[s];
-  // the chain: epochs' appends, pushed in tn order, so newest first
+  // the chain: epochs' appends, pushed in tn order, so newest first (a walk
+  // is bounded by the level's pairs even if a chain were ever corrupt: a
+  // step past them ends it instead of looping)
   if (L.next)
-    for (uint32_t p = (uint32_t)side.y; p != HIST_NIL; p = L.next[p]) {
+    for (uint32_t p = (uint32_t)side.y, st = 0; p < L.walk && st < L.walk; p = L.next[p], st++) {
       const uint64_t t = L.ctn[p];
       if (t <= hi) {
         if (t > lo) return true;

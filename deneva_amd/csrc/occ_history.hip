@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 
 #include "dcc_device.h"
@@ -349,6 +350,49 @@ void launch_fin(const OccFinArgs& a0, hipStream_t st) {
 }
 
 uint64_t fin_part_bytes(uint64_t n) { return (((n + HB * FIN_T - 1) / (HB * FIN_T)) + 2) * sizeof(FinLb); }
+
+// A host copy of k_fin's look-back words (fin_part_bytes(n) bytes) after a
+// launch with `tag`, summarised for the error message of a totals mismatch:
+// workgroups whose status carries another tag or no inclusive value, and the
+// first one whose inclusive prefix is not its predecessor's plus its own
+// aggregate (a foreign or stale prefix taken by the look-back).
+std::string fin_diag(const void* words, uint64_t n, uint32_t tag) {
+  const FinLb* lb = (const FinLb*)((const FinTail*)words + 1);
+  const uint64_t nb = std::max<uint64_t>(1, (n + HB * FIN_T - 1) / (HB * FIN_T));
+  uint64_t stale = 0, first_stale = ~0ull, bad = ~0ull;
+  uint32_t stale_tag = 0;
+  uint64_t prev = 0;
+  for (uint64_t b = 0; b < nb; b++) {
+    const FinLb& e = lb[b];
+    if ((e.status >> 2) != tag || (e.status & 3u) != 2u) {
+      if (!stale++) {
+        first_stale = b;
+        stale_tag = e.status;
+      }
+      continue;
+    }
+    const uint64_t own = b == 0 ? e.inc : e.agg;
+    if (bad == ~0ull && b > 0 && e.inc != prev + own) bad = b;
+    prev = e.inc;
+  }
+  char buf[512];
+  int k = snprintf(buf, sizeof buf, "look-back of %llu workgroups, tag %u: %llu not inclusive under the tag",
+                   (unsigned long long)nb, tag, (unsigned long long)stale);
+  if (stale)
+    k += snprintf(buf + k, sizeof buf - k, " (first: workgroup %llu, status tag %u flag %u)",
+                  (unsigned long long)first_stale, stale_tag >> 2, stale_tag & 3u);
+  if (bad != ~0ull) {
+    const FinLb& e = lb[bad];
+    snprintf(buf + k, sizeof buf - k,
+             "; workgroup %llu's prefix is not its predecessor's plus its own: inclusive %llu commits, "
+             "aggregate %llu, predecessor inclusive %llu",
+             (unsigned long long)bad, (unsigned long long)(uint32_t)e.inc, (unsigned long long)(uint32_t)e.agg,
+             (unsigned long long)(uint32_t)lb[bad - 1].inc);
+  } else {
+    snprintf(buf + k, sizeof buf - k, "; inclusive prefixes consistent");
+  }
+  return buf;
+}
 
 void launch_hist_count(uint64_t n, const uint32_t* off, const uint8_t* acctype, uint64_t nnz,
                        const uint64_t* tn, uint32_t* bsum, hipStream_t st) {

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string>
 #include "occ_history.h"
 
 namespace dcc {
@@ -526,6 +527,9 @@ struct OccFinArgs {
 };
 void launch_fin(const OccFinArgs& a, hipStream_t st);
 uint64_t fin_part_bytes(uint64_t n);
+// summary of a host copy of the look-back words after a launch with `tag`
+// (the totals-mismatch error message)
+std::string fin_diag(const void* words, uint64_t n, uint32_t tag);
 void launch_commit_tn(const uint32_t* cflag, uint64_t n, uint64_t* bsum, uint64_t tnc,
                       uint64_t* tn, hipStream_t st);
 // deferred central_finish: cflag[t] = global RCOK && local commit && has a

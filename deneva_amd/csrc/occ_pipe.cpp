@@ -117,7 +117,7 @@ extern "C" int dcc_occ_submit_epoch(dcc_ctx* ctx, const dcc_batch* b, uint8_t* o
   const uint64_t ticket = p->next;
   const bool shared = out_tn || (b->flags & (DCC_OCC_APPEND_HISTORY | DCC_OCC_DEFER_FINISH)) ||
                       (b->start_tn && ctx->hist_size() > 0) || ctx->fin_pending;
-  const bool lanes_ok = !ctx->multi && ctx->comm_ranks() <= 1 && !ctx->profiling &&
+  const bool lanes_ok = !ctx->multi && !ctx->sharded() && !ctx->profiling &&
                         ctx->use_sweep() && !shared && b->n_txn > 0;
   if (!lanes_ok) {
     // in submit order, on the parent context itself

@@ -533,6 +533,11 @@ class Engine:
     def comm_size(self) -> int:
         return int(lib.dcc_comm_size(self._h))
 
+    @property
+    def comm_calls(self) -> int:
+        """Collectives run by this engine's communicator (dcc_comm_calls)."""
+        return int(lib.dcc_comm_calls(self._h))
+
     def comm_destroy(self) -> None:
         _check(lib.dcc_comm_destroy(self._h), self._h)
 

@@ -199,6 +199,11 @@ int dcc_set_profiling(dcc_ctx* ctx, int enable);
 #define DCC_OPT_CALVIN_PATH 12 /* Calvin grant groups: 0 auto (the bucket path for epochs of
                                   >= 2M requests it applies to), 1 the global key sort + scan,
                                   2 the bucket path wherever it applies                       */
+#define DCC_OPT_COMM_SOLO 13  /* tests: with 1, a later dcc_comm_init(ctx, 0, 1, id) forms a
+                                 one-rank RCCL clique and the context runs the key-sharded
+                                 paths with their collectives (ncclAllReduce / ncclAllGather
+                                 over the one rank) instead of the one-GPU paths: the RCCL
+                                 call path executes on a one-GPU box                         */
 int dcc_set_option(dcc_ctx* ctx, int option, int64_t value);
 /* Pre-size device workspaces so a later call performs no allocation. */
 int dcc_reserve(dcc_ctx* ctx, uint64_t max_txn, uint64_t max_nnz);
@@ -231,6 +236,9 @@ int dcc_comm_init_host(dcc_ctx* ctx, int rank, int nranks, dcc_exchange_fn fn, v
 int dcc_comm_destroy(dcc_ctx* ctx);
 int dcc_comm_rank(const dcc_ctx* ctx);
 int dcc_comm_size(const dcc_ctx* ctx);
+/* Collectives this context's communicator has run since dcc_comm_init (RCCL
+ * calls enqueued, or host exchanges); 0 without a communicator. */
+uint64_t dcc_comm_calls(const dcc_ctx* ctx);
 uint32_t dcc_key_shard(uint64_t key, uint32_t nranks);
 /* dcc_key_shard of n keys (host arrays): out[i] = shard of keys[i] */
 int dcc_key_shard_n(const uint64_t* keys, uint64_t n, uint32_t nranks, uint32_t* out);

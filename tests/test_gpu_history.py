@@ -199,3 +199,53 @@ def test_snapshot_sees_epoch_history(engine):
     want = orc.occ_snapshot(b2, aoff, np.zeros(0, np.uint32), top, hk, ht)
     assert np.array_equal(np.asarray(rc), want)
     engine.history_clear()
+
+
+@pytest.mark.parametrize("device_ptrs", [False, True])
+def test_failed_append_retry_then_window(engine, device_ptrs):
+    """central_finish pushes an epoch's pairs onto the delta's chains before
+    the host checks the epoch.  An epoch that fails afterwards (one txn holds
+    the reserved key: rejected with DCC_EINVAL once the epoch ran) must leave
+    no trace: tnc and the history stay as they were, the retry without that
+    txn pushes the same flat positions again, and the windows of the epoch
+    after it -- reaching below the retried epoch's tns, so they walk the
+    chains -- decide exactly as the oracle (a pair pushed twice
+    linked to itself and the walk never ended)."""
+    import torch
+    rng = np.random.default_rng(0xFA11 + device_ptrs)
+    engine.history_clear()
+    engine.tnc = 0
+    engine.set_option(OPT_HIST_MERGE, 1 << 22)  # every append stays in the chained delta
+    try:
+        hk, ht = np.zeros(0, np.uint64), np.zeros(0, np.uint64)
+        tnc = 0
+        as_dev = (lambda b: b.to_torch("cuda:0")) if device_ptrs else (lambda b: b)
+        for e in range(4):
+            b = d.gen_ycsb(n_txn=20000, zipf_theta=0.8, table_size=1 << 12, seed=0xFA00 + e)
+            b.start_tn, b.finish_tn = windows(rng, b.n_txn, tnc, 3000)
+            if e == 2:
+                bad = d.EpochBatch(b.offsets, np.asarray(b.keys, np.uint64).copy(), b.acctype,
+                                   b.start_tn, b.finish_tn)
+                bad.keys[-1] = d.KEY_RESERVED
+                with pytest.raises(d.DccError):
+                    engine.occ_validate_epoch(as_dev(bad), want_tn=True, append_history=True)
+                if device_ptrs:
+                    torch.cuda.synchronize()
+                assert engine.tnc == tnc and engine.history_size == hk.size
+            erc, etn, etnc = orc.occ(b, hist_keys=hk, hist_tn=ht, tnc=tnc)
+            rc, tn, _ = engine.occ_validate_epoch(as_dev(b), want_tn=True, append_history=True)
+            if device_ptrs:
+                torch.cuda.synchronize()
+                rc, tn = rc.cpu().numpy(), tn.cpu().numpy().view(np.uint64)
+            assert np.array_equal(np.asarray(rc), erc), f"epoch {e}: rc differs"
+            assert np.array_equal(np.asarray(tn, np.uint64), etn), f"epoch {e}: tn differs"
+            nk, nt = committed_writes(b, etn)
+            hk, ht = np.concatenate([hk, nk]), np.concatenate([ht, nt])
+            tnc = etnc
+        gk, gt = engine.history_export()
+        wk, wt = sorted_pairs(hk, ht)
+        assert np.array_equal(gk, wk) and np.array_equal(gt, wt)
+    finally:
+        engine.set_option(OPT_HIST_MERGE, 65536)
+        engine.history_clear()
+        engine.tnc = 0

@@ -203,3 +203,57 @@ def test_multi_rejects_malformed_device_batch(fault):
         rc, _, _ = eng.occ_validate_epoch(b.to_torch("cuda:0"))
         torch.cuda.synchronize()
         assert np.array_equal(rc.cpu().numpy(), erc)
+
+
+def test_multi_occ_growing_epochs_share_one_gpu():
+    """Two shards of one context on one GPU, commit tn wanted, epochs growing
+    from one to the next (every epoch reallocates the central_finish
+    look-back words; the allocator may hand a shard memory the other shard
+    just freed, holding words with the same tag sequence).  Round 5's
+    intermittent 'central_finish numbered 339 txns, 480 committed writers'
+    was a grown buffer whose tail was never cleared (occ_begin); every
+    epoch's commit tns must equal the oracle's (occ.cpp:277-286)."""
+    with d.Engine(devices=[0, 0]) as eng, d.Engine(0) as other:
+        eng.tnc = 0
+        tnc = 0
+        for e, n in enumerate([700, 3000, 9000, 40000, 150000, 600000]):
+            b = d.gen_ycsb(n_txn=n, zipf_theta=0.99, table_size=1 << 18, seed=0x61A0 + e)
+            erc, etn, etnc = orc.occ(b, tnc=tnc)
+            rc, tn, _ = eng.occ_validate_epoch(b, want_tn=True)
+            assert np.array_equal(np.asarray(rc), erc), f"epoch {e}"
+            assert np.array_equal(np.asarray(tn, np.uint64), etn), f"epoch {e}"
+            assert eng.tnc == etnc
+            tnc = etnc
+            # a third context on the same GPU churns the allocator in between
+            other.tnc = 0
+            other.occ_validate_epoch(b, want_tn=True)
+
+
+@pytest.mark.parametrize("solver", [1, 3])
+def test_multi_shard_self_history_per_solver(solver):
+    """Every solver shards the batch by key: with the round solver too, a
+    rank appends only its own keys' committed writes, so the context's
+    history holds each pair once (the round solver used to stage
+    the whole batch as its shard)."""
+    from deneva_amd._abi import OPT_SOLVER
+    rng = np.random.default_rng(19)
+    with d.Engine(devices=[0, 0, 0]) as eng:
+        eng.set_option(OPT_SOLVER, solver)
+        eng.tnc = 0
+        eng.history_clear()
+        hk, ht = np.zeros(0, np.uint64), np.zeros(0, np.uint64)
+        tnc = 0
+        for e in range(3):
+            b = d.gen_ycsb(n_txn=12000, zipf_theta=0.8, table_size=1 << 14, seed=70 + e)
+            b.start_tn = rng.integers(0, tnc + 1, size=b.n_txn).astype(np.uint64)
+            b.finish_tn = (b.start_tn + rng.integers(0, 300, size=b.n_txn)).astype(np.uint64)
+            erc, etn, etnc = orc.occ(b, hist_keys=hk, hist_tn=ht, tnc=tnc)
+            rc, tn, _ = eng.occ_validate_epoch(b, want_tn=True, append_history=True)
+            assert np.array_equal(np.asarray(rc), erc) and np.array_equal(np.asarray(tn), etn)
+            off = np.asarray(b.offsets, np.int64)
+            owner = np.repeat(np.arange(b.n_txn), np.diff(off))
+            sel = (np.asarray(b.acctype) == WR) & (etn[owner] != 0)
+            hk = np.concatenate([hk, np.asarray(b.keys)[sel]])
+            ht = np.concatenate([ht, etn[owner[sel]]])
+            tnc = etnc
+            assert eng.history_size == hk.size

@@ -129,11 +129,12 @@ def test_sync_call_drains_first(eng):
 
 
 def test_full_size_stream(eng):
-    """The bench's pipelined headline: 1M-txn theta=0.9 epochs on 3 lanes,
-    every epoch in flight checked."""
+    """The bench's pipelined headline: 1M-txn theta=0.9 epochs on the bench's
+    4 lanes (five epochs, so one lane takes two), every epoch in flight
+    checked."""
     import torch
-    eng.set_option(OPT_PIPELINE, 3)
-    bs = batches(1 << 20, 3, seed=0xD3E7A001)
+    eng.set_option(OPT_PIPELINE, 4)
+    bs = batches(1 << 20, 5, seed=0xD3E7A001)
     exp = expected(bs)
     dbs = [b.to_torch("cuda:0") for b in bs]
     outs = [torch.empty(b.n_txn, dtype=torch.uint8, device="cuda:0") for b in bs]
@@ -145,3 +146,24 @@ def test_full_size_stream(eng):
         for i, (o, (erc, _, _)) in enumerate(zip(outs, exp)):
             assert np.array_equal(o.cpu().numpy(), erc), f"epoch {i}, pass {rep}"
         assert eng.tnc == exp[-1][2]
+
+
+def test_option_change_keeps_outstanding_tickets(eng):
+    """DCC_OPT_PIPELINE while epochs are in flight: they complete on their
+    lanes and keep their results until waited (dcc.h); tickets keep counting
+    up, so an old ticket never aliases a new epoch."""
+    import torch
+    eng.set_option(OPT_PIPELINE, 3)
+    bs = batches(30000, 6, seed=0x5E7)
+    exp = expected(bs)
+    dbs = [b.to_torch("cuda:0") for b in bs]
+    outs = [torch.empty(b.n_txn, dtype=torch.uint8, device="cuda:0") for b in bs]
+    ts = [eng.occ_submit_epoch(dbs[i], outs[i]) for i in range(3)]
+    eng.set_option(OPT_PIPELINE, 2)
+    ts += [eng.occ_submit_epoch(dbs[i], outs[i]) for i in range(3, 6)]
+    assert len(set(ts)) == 6 and ts == sorted(ts)
+    sts = [eng.occ_wait_epoch(t) for t in ts]
+    for i, (o, (erc, _, _)) in enumerate(zip(outs, exp)):
+        assert np.array_equal(o.cpu().numpy(), erc), f"epoch {i}"
+        assert sts[i]["n_commit"] == int(np.count_nonzero(erc == d.RC_RCOK))
+    assert eng.tnc == exp[-1][2]
