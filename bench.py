@@ -71,6 +71,9 @@ def parse():
                     help="lanes of the pipelined headline (dcc_occ_submit_epoch, DCC_OPT_PIPELINE): "
                          "consecutive epochs over that many distinct resident batches overlap on "
                          "the GPU (N=1; 0 = one epoch at a time)")
+    ap.add_argument("--partition", type=int, default=0, choices=[0, 1],
+                    help="pipeline lanes on their own XCDs (DCC_OPT_PIPE_PARTITION): lane i of L "
+                         "on the XCDs x with x %% L == i, CU-masked streams")
     ap.add_argument("--exchange", choices=["rccl", "host"], default="rccl",
                     help="N>1 status all-reduce: RCCL over xGMI (one GPU per rank), or "
                          "host/gloo (rehearsal: ranks may share one GPU)")
@@ -676,6 +679,7 @@ def main():
     pipe_batches, pipe_outs = [], []
     if lanes:
         eng.set_option(d._abi.OPT_PIPELINE, lanes)
+        eng.set_option(d._abi.OPT_PIPE_PARTITION, args.partition)
         pipe_batches = [batch] + [d.gen_ycsb(n_txn=n_total, zipf_theta=args.theta,
                                              req_per_query=args.keys, seed=args.seed + i)
                                   for i in range(1, lanes)]
@@ -845,6 +849,8 @@ def main():
             },
             "pipeline": ({
                 "lanes": lanes,
+                "partition": ("lane i on the XCDs x with x % lanes == i (CU-masked streams)"
+                              if args.partition else "every lane on the whole chip"),
                 "ms_per_epoch_steady": dt / args.steps * 1e3,
                 "txns_per_s": value,
                 "batches": f"{lanes} distinct resident batches (seeds {args.seed:#x}+0..{lanes - 1}), "

@@ -50,6 +50,7 @@ OPT_RO_SPLIT = 10
 OPT_PIPELINE = 11
 OPT_CALVIN_PATH = 12
 OPT_COMM_SOLO = 13
+OPT_PIPE_PARTITION = 14
 
 
 class Batch(C.Structure):

@@ -270,6 +270,7 @@ struct dcc_ctx {
   // pipelined epochs over lane contexts on this device (occ_pipe.cpp)
   struct OccPipe* pipe = nullptr;
   uint32_t pipe_lanes = 3;  // DCC_OPT_PIPELINE
+  uint32_t pipe_part = 0;   // DCC_OPT_PIPE_PARTITION
   int cv_path = 0;          // DCC_OPT_CALVIN_PATH: 0 auto, 1 sort, 2 bucket
   // DCC_OCC_DEFER_FINISH: the decided epoch waiting for its global RC
   bool fin_pending = false;

@@ -200,6 +200,12 @@ extern "C" int dcc_set_option(dcc_ctx* ctx, int option, int64_t value) {
     ctx->pipe_lanes = (uint32_t)value;
     return DCC_OK;
   }
+  if (option == DCC_OPT_PIPE_PARTITION) {
+    if (value != 0 && value != 1) return DCC_EINVAL;
+    dcc_pipe_drain(ctx);  // as DCC_OPT_PIPELINE; the lanes are re-created at the next submit
+    ctx->pipe_part = (uint32_t)value;
+    return DCC_OK;
+  }
   if (ctx->multi)
     for (int r = 0; r < dcc_multi_size(ctx); r++) {
       const int e = dcc_set_option(dcc_multi_sub(ctx, r), option, value);

@@ -11,6 +11,7 @@
 // and the epochs complete -- results read back, tnc advanced -- in submit
 // order.  An epoch that needs anything shared (commit tn, the history,
 // deferred finish) drains the lanes and runs on the parent context itself.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <deque>
@@ -37,6 +38,7 @@ struct OccPipe {
   uint64_t next = 1;
   uint32_t next_lane = 0;
   hipEvent_t ready = nullptr;  // the caller's stream, before an epoch's first lane launch
+  uint32_t part = 0;           // DCC_OPT_PIPE_PARTITION the lanes were made with
 };
 
 static void pipe_complete_front(dcc_ctx* ctx) {
@@ -71,20 +73,60 @@ void dcc_pipe_destroy(dcc_ctx* ctx) {
   ctx->pipe = nullptr;
 }
 
+// Lanes on their own CUs (DCC_OPT_PIPE_PARTITION): lane i of L runs on the
+// XCDs x with x % L == i (L <= 8; 8 / L whole XCDs each), so a lane's
+// one-workgroup serial passes never wait for a CU that another lane's
+// chip-wide kernels hold, and a lane's working set (key tables, bitmaps,
+// level lists) stays in its own XCDs' L2s.  A stream's CU mask names CUs by
+// bit; the driver deals mask bits to the XCDs round-robin (bit b -> XCD
+// b % 8, tools/cumask_probe.hip), so XCD x is every bit b with b % 8 == x.
+static int lane_partition(dcc_ctx* ctx, dcc_ctx* l, uint32_t i, uint32_t L) {
+  const uint32_t n = (uint32_t)ctx->n_cu;
+  if (L < 2 || n % 8) return DCC_OK;  // one lane, or a chip without 8 equal XCDs: unmasked
+  std::vector<uint32_t> mask((n + 31) / 32, 0u);
+  uint32_t cus = 0;
+  for (uint32_t b = 0; b < n; b++)
+    if ((b % 8) % L == i % L) {
+      mask[b / 32] |= 1u << (b % 32);
+      cus++;
+    }
+  hipStream_t s = nullptr;
+  const hipError_t e = hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data());
+  if (e != hipSuccess) return ctx->hip_fail(e, "pipeline lane: hipExtStreamCreateWithCUMask");
+  if (l->own_stream) (void)hipStreamDestroy(l->own_stream);
+  l->own_stream = l->stream = s;
+  l->n_cu = (int)cus;  // grids are sized to the lane's CUs
+  return DCC_OK;
+}
+
 static int pipe_lanes(dcc_ctx* ctx) {
   OccPipe* p = ctx->pipe;
   const size_t want = ctx->pipe_lanes;
-  if (p->lanes.size() == want) return DCC_OK;
+  if (p->lanes.size() == want && p->part == ctx->pipe_part) return DCC_OK;
   dcc_pipe_drain(ctx);
+  if (p->part != ctx->pipe_part) {  // every lane is re-created on its new CUs
+    for (dcc_ctx* l : p->lanes) dcc_destroy(l);
+    p->lanes.clear();
+    p->part = ctx->pipe_part;
+  }
   while (p->lanes.size() > want) {
     dcc_destroy(p->lanes.back());
     p->lanes.pop_back();
   }
+  if (p->part)  // the partition depends on the lane count
+    while (!p->lanes.empty() && p->lanes.size() != want) {
+      dcc_destroy(p->lanes.back());
+      p->lanes.pop_back();
+    }
   while (p->lanes.size() < want) {
     dcc_ctx* l = nullptr;
     const int e = dcc_init(&l, ctx->device);
     if (e != DCC_OK) return ctx->fail(e, "pipeline lane on device %d: %s", ctx->device, dcc_strerror(e));
     p->lanes.push_back(l);
+    if (p->part) {
+      const int x = lane_partition(ctx, l, (uint32_t)p->lanes.size() - 1, (uint32_t)want);
+      if (x != DCC_OK) return x;
+    }
   }
   p->next_lane = 0;
   return DCC_OK;

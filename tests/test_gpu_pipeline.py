@@ -16,7 +16,7 @@ import pytest
 
 import _oracle as orc
 import deneva_amd as d
-from deneva_amd._abi import OPT_PIPELINE, DccError
+from deneva_amd._abi import OPT_PIPE_PARTITION, OPT_PIPELINE, DccError
 
 pytestmark = pytest.mark.gpu
 
@@ -26,6 +26,7 @@ def eng(engine):
     engine.tnc = 0
     yield engine
     engine.set_option(OPT_PIPELINE, 2)
+    engine.set_option(OPT_PIPE_PARTITION, 0)
     engine.tnc = 0
 
 
@@ -41,10 +42,13 @@ def expected(bs, tnc=0):
     return out
 
 
-@pytest.mark.parametrize("lanes", [1, 2, 3, 4])
-def test_device_stream_matches_serial(eng, lanes):
+@pytest.mark.parametrize("lanes,part", [(1, 0), (2, 0), (3, 0), (4, 0), (2, 1), (3, 1), (4, 1), (8, 1)])
+def test_device_stream_matches_serial(eng, lanes, part):
+    """part 1: each lane on its own XCDs (CU-masked streams, grids sized to
+    the lane's CUs)."""
     import torch
     eng.set_option(OPT_PIPELINE, lanes)
+    eng.set_option(OPT_PIPE_PARTITION, part)
     bs = batches(65536, 7)
     exp = expected(bs)
     dbs = [b.to_torch("cuda:0") for b in bs]
@@ -128,13 +132,15 @@ def test_sync_call_drains_first(eng):
         assert np.array_equal(o.cpu().numpy(), erc), f"epoch {i}"
 
 
-def test_full_size_stream(eng):
+@pytest.mark.parametrize("lanes,part", [(4, 0), (4, 1), (8, 1)])
+def test_full_size_stream(eng, lanes, part):
     """The bench's pipelined headline: 1M-txn theta=0.9 epochs on the bench's
-    4 lanes (five epochs, so one lane takes two), every epoch in flight
-    checked."""
+    lanes (one more epoch than lanes, so one lane takes two), unmasked or
+    each lane on its own XCDs; every epoch in flight checked."""
     import torch
-    eng.set_option(OPT_PIPELINE, 4)
-    bs = batches(1 << 20, 5, seed=0xD3E7A001)
+    eng.set_option(OPT_PIPELINE, lanes)
+    eng.set_option(OPT_PIPE_PARTITION, part)
+    bs = batches(1 << 20, lanes + 1, seed=0xD3E7A001)
     exp = expected(bs)
     dbs = [b.to_torch("cuda:0") for b in bs]
     outs = [torch.empty(b.n_txn, dtype=torch.uint8, device="cuda:0") for b in bs]
