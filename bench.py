@@ -72,8 +72,8 @@ def parse():
                          "consecutive epochs over that many distinct resident batches overlap on "
                          "the GPU (N=1; 0 = one epoch at a time)")
     ap.add_argument("--partition", type=int, default=0, choices=[0, 1],
-                    help="pipeline lanes on their own XCDs (DCC_OPT_PIPE_PARTITION): lane i of L "
-                         "on the XCDs x with x %% L == i, CU-masked streams")
+                    help="pipeline lanes on their own CUs (DCC_OPT_PIPE_PARTITION): lane i of L "
+                         "on 1/L of every XCD's CUs, CU-masked streams")
     ap.add_argument("--exchange", choices=["rccl", "host"], default="rccl",
                     help="N>1 status all-reduce: RCCL over xGMI (one GPU per rank), or "
                          "host/gloo (rehearsal: ranks may share one GPU)")
@@ -849,7 +849,7 @@ def main():
             },
             "pipeline": ({
                 "lanes": lanes,
-                "partition": ("lane i on the XCDs x with x % lanes == i (CU-masked streams)"
+                "partition": ("lane i on 1/lanes of every XCD's CUs (CU-masked streams)"
                               if args.partition else "every lane on the whole chip"),
                 "ms_per_epoch_steady": dt / args.steps * 1e3,
                 "txns_per_s": value,

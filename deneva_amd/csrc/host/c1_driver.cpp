@@ -41,6 +41,7 @@ struct Cfg {
   bool calvin = false;
   bool live = false;           // live OptCC run on the workers, capture replayed on the GPU
   bool overlap = true;         // OccEpoch fills epoch N+1 while N is on the GPU
+  int depth = 4;               // OccEpoch: closed epochs on the GPU at once
   std::string capture;
 };
 
@@ -48,7 +49,7 @@ static void usage() {
   fprintf(stderr,
           "c1_driver [--threads N] [--txns N] [--theta T] [--req N] [--table N]\n"
           "          [--epoch-max N] [--timer-ms T] [--seed S] [--device D] [--gpus N]\n"
-          "          [--capture DIR] [--calvin | --live] [--no-overlap]\n");
+          "          [--capture DIR] [--calvin | --live] [--no-overlap] [--depth N]\n");
 }
 
 static int parse(int argc, char** argv, Cfg& c) {
@@ -72,9 +73,10 @@ static int parse(int argc, char** argv, Cfg& c) {
     else if (a == "--device") c.device = atoi(v);
     else if (a == "--gpus") c.gpus = atoi(v);
     else if (a == "--capture") c.capture = v;
+    else if (a == "--depth") c.depth = atoi(v);
     else return 2;
   }
-  return (c.threads > 0 && c.txns > 0 && c.req > 0) ? 0 : 2;
+  return (c.threads > 0 && c.txns > 0 && c.req > 0 && c.depth >= 1) ? 0 : 2;
 }
 
 // one worker's txns from the restated generator (its own stream)
@@ -186,6 +188,7 @@ int main(int argc, char** argv) {
     o.timer_ms = c.timer_ms;
     o.capture_dir = c.capture;
     o.overlap = c.overlap;
+    o.depth = c.depth;
     OccEpoch occ(ctx, o);
     std::vector<std::thread> ws;
     for (int w = 0; w < c.threads; w++)
@@ -253,12 +256,12 @@ int main(int argc, char** argv) {
   printf("{\"driver\": \"c1\", \"cc\": \"%s\", \"threads\": %d, \"txns\": %llu, "
          "\"epochs\": %llu, \"commits\": %llu, \"restarts\": %llu, \"ready\": %llu, "
          "\"waits\": %llu, \"device_ms\": %.3f, \"wall_s\": %.3f, \"txns_per_s\": %.1f, "
-         "\"live_mismatch\": %lld, \"gave_up\": %llu, \"overlap\": %d, \"failed\": %d}\n",
+         "\"live_mismatch\": %lld, \"gave_up\": %llu, \"overlap\": %d, \"depth\": %d, \"failed\": %d}\n",
          c.calvin ? "CALVIN" : (c.live ? "OCC-live" : "OCC"), c.threads, (unsigned long long)total,
          (unsigned long long)epochs, (unsigned long long)commits.load(),
          (unsigned long long)restarts.load(), (unsigned long long)ready.load(),
          (unsigned long long)waits.load(), device_ms, wall, total / wall, live_mismatch,
-         (unsigned long long)gave_up.load(), c.overlap ? 1 : 0, failed.load());
+         (unsigned long long)gave_up.load(), c.overlap ? 1 : 0, c.depth, failed.load());
   dcc_destroy(ctx);
   return failed ? 1 : 0;
 }

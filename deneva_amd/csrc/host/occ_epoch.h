@@ -15,13 +15,21 @@
 // has waited timer_ms.  Decided epochs can be captured as .dccb files
 // (dcc_file_write) with their decisions, for offline parity checks.
 //
-// Capture and validation overlap: the closing thread swaps the open epoch's
-// CSR into the in-flight buffer and releases the mutex for the engine call,
-// so workers fill epoch N+1 while epoch N is on the GPU.  Engine calls stay
-// serialized (one in flight; the context is thread-compatible), and an epoch
-// closes only when the previous one is decided, which keeps tnc and the
-// history in epoch order.  Options::overlap = false holds the mutex across
-// the call (the pre-overlap behaviour, kept for A/B measurement).
+// Epochs in flight (Options::depth, default 4): a closed epoch is submitted
+// to the engine's pipeline (dcc_occ_submit_epoch: its own lane, stream and
+// captured graph) and the workers fill the next one at once; up to `depth`
+// closed epochs are on the GPU together.  They complete in close order
+// (dcc_occ_wait_epoch), driven by one of the threads waiting on the oldest,
+// so decisions, tnc and the history are those of validating the epochs one
+// after another (occ.cpp:116-294).  Engine calls are serialised by their own
+// mutex (the context is thread-compatible), never under the shim's state
+// mutex.  Counting "every worker is waiting" takes the workers blocked on
+// closed epochs into account: an epoch closes when every worker is either in
+// it or waiting on an epoch already closed.  depth = 1 is one epoch in flight
+// (the round-4 shim); Options::overlap = false additionally holds the state
+// mutex across the engine calls (the pre-overlap behaviour, for A/B).
+// An epoch that needs shared state in order (the TS_CAS history below) runs
+// synchronously inside dcc_occ_submit_epoch: the pipeline drains first.
 //
 // Timestamps: with the reference's default TS_CLOCK (config.h:124) the history
 // window of central_validate never fires, so by
@@ -41,7 +49,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
+#include <deque>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <new>
 #include <string>
@@ -138,6 +149,7 @@ class OccEpoch {
     std::string capture_dir;     // "" = no capture
     bool ts_window = false;      // pass start/finish tn and keep the history
     bool overlap = true;         // fill epoch N+1 while epoch N is decided
+    int depth = 4;               // closed epochs on the GPU at once (engine pipeline lanes)
   };
   struct Stats {
     uint64_t epochs = 0, txns = 0, commits = 0, aborts = 0;
@@ -145,8 +157,12 @@ class OccEpoch {
     double device_ms = 0, wall_ms = 0;
   };
 
-  OccEpoch(dcc_ctx* ctx, const Options& o) : ctx_(ctx), opt_(o), open_(ctx), fly_(ctx) {
-    open_.off.push_back(0);
+  OccEpoch(dcc_ctx* ctx, const Options& o)
+      : ctx_(ctx), opt_(o), depth_((size_t)std::max(1, o.overlap ? o.depth : 1)), open_(new Csr(ctx)) {
+    open_->clear();  // offsets start at 0
+    tnc_done_ = dcc_occ_get_tnc(ctx);
+    // one engine lane per epoch in flight (DCC_OPT_PIPELINE, 1..8)
+    if (depth_ > 1) (void)dcc_set_option(ctx, DCC_OPT_PIPELINE, (int64_t)std::min<size_t>(depth_, 8));
   }
 
   // TxnManager::validate for CC_ALG == OCC: DCC_RC_RCOK or DCC_RC_ABORT in *rc.
@@ -156,33 +172,38 @@ class OccEpoch {
                uint64_t finish_tn = 0) {
     std::unique_lock<std::mutex> lk(mu_);
     const uint64_t ep = epoch_;
-    const uint64_t slot = open_.off.size() - 1;
-    for (size_t i = 0; i < n; i++) open_.add(acc[i].key, acc[i].type);
-    open_.off.push_back((uint32_t)open_.nnz);
-    if (opt_.ts_window) open_.add_tn(start_tn, finish_tn);
+    const uint64_t slot = open_->off.size() - 1;
+    for (size_t i = 0; i < n; i++) open_->add(acc[i].key, acc[i].type);
+    open_->off.push_back((uint32_t)open_->nnz);
+    if (opt_.ts_window) open_->add_tn(start_tn, finish_tn);
     if (slot == 0) opened_ = std::chrono::steady_clock::now();
-    // waiting for the OPEN epoch: a worker blocked on the in-flight one will
-    // add its next txn to the open epoch once that one is decided, so it does
-    // not count towards "every worker is in" (the open epoch would otherwise
-    // close early, right after the in-flight call returns and before its
-    // waiters have woken)
+    // waiting for the OPEN epoch; once it closes, its waiters count as
+    // waiting on a closed epoch (closed_waiting_) until it is decided
     open_waiting_++;
     int err = 0;
     while (decided_.find(ep) == decided_.end()) {
-      const bool full = open_.off.size() - 1 >= opt_.max_txns;
-      const bool all_in = open_waiting_ >= opt_.n_workers;
+      const size_t open_n = open_->off.size() - 1;
+      const bool full = open_n >= opt_.max_txns;
+      const bool all_in = open_waiting_ + closed_waiting_ >= opt_.n_workers;
       const auto age = std::chrono::duration<double, std::milli>(
                            std::chrono::steady_clock::now() - opened_).count();
-      if (ep == epoch_ && !busy_ && (full || all_in || age >= opt_.timer_ms)) {
-        err = close(lk);
-        continue;  // decided (or failed) now
+      if (ep == epoch_ && open_n > 0 && !submitting_ && fly_.size() < depth_ &&
+          (full || all_in || age >= opt_.timer_ms)) {
+        err = submit(lk);
+        continue;
+      }
+      // complete the oldest closed epoch: this thread's own, an earlier one,
+      // or one that holds the slot the open epoch needs
+      if (!driving_ && !fly_.empty() && fly_.front().submitted &&
+          (ep < epoch_ || fly_.size() >= depth_)) {
+        err = drive(lk);
+        continue;
       }
       // a system_clock deadline (pthread_cond_timedwait: the wait ThreadSanitizer
       // intercepts; a 200 us poll does not care about clock steps)
       cv_.wait_until(lk, std::chrono::system_clock::now() + std::chrono::microseconds(200));
     }
     auto it = decided_.find(ep);
-    if (it == decided_.end()) return err ? err : DCC_EIO;
     if (it->second.err) err = it->second.err;
     *rc = err ? (uint8_t)DCC_RC_ABORT : it->second.rc[slot];
     if (--it->second.readers == 0) decided_.erase(it);
@@ -301,75 +322,159 @@ class OccEpoch {
     }
   };
 
-  // decide the open epoch: it moves to the in-flight buffer, the mutex is
-  // released for the engine call (Options::overlap), then everyone wakes.
-  // Called with lk held and no call in flight; returns with lk held.
-  int close(std::unique_lock<std::mutex>& lk) {
-    std::swap(open_, fly_);
-    open_.clear();
-    const uint64_t id = epoch_++;
-    open_waiting_ = 0;  // they wait for the closed epoch now
-    busy_ = true;
-    if (opt_.overlap) lk.unlock();
-    const uint64_t n = fly_.off.size() - 1;
-    Decided d;
-    d.rc.assign(n, DCC_RC_ABORT);
-    d.readers = n;
+  // A closed epoch on its way through the engine: its CSR and decision
+  // buffers (pinned; they stay untouched until it completes) and ticket.
+  struct Flight {
+    uint64_t id = 0, ticket = 0, n = 0;
+    std::unique_ptr<Csr> csr;
+    std::unique_ptr<PinnedVec<uint8_t>> rc;
     dcc_batch b{};
-    if (opt_.ts_window) b.flags = DCC_OCC_APPEND_HISTORY;  // central_finish: commit tn + history
-    fly_.to_batch(b);
+    bool submitted = false;
+    int err = 0;
+    std::chrono::steady_clock::time_point t0{};
+  };
+
+  std::unique_ptr<Csr> take_csr() {
+    std::unique_ptr<Csr> c;
+    if (free_csr_.empty()) {
+      c.reset(new Csr(ctx_));
+    } else {
+      c = std::move(free_csr_.back());
+      free_csr_.pop_back();
+    }
+    c->clear();  // offsets start at 0
+    return c;
+  }
+
+  // Close the open epoch and submit it.  Called with lk held, the open epoch
+  // non-empty and a slot free; returns with lk held.
+  int submit(std::unique_lock<std::mutex>& lk) {
+    fly_.emplace_back();
+    Flight& f = fly_.back();  // deque: stays put while others append
+    f.csr = std::move(open_);
+    open_ = take_csr();
+    f.id = epoch_++;
+    f.n = f.csr->off.size() - 1;
+    closed_waiting_ += open_waiting_;  // they wait for the closed epoch now (one per txn)
+    open_waiting_ = 0;
+    if (!free_rc_.empty()) {
+      f.rc = std::move(free_rc_.back());
+      free_rc_.pop_back();
+    } else {
+      f.rc.reset(new PinnedVec<uint8_t>(ctx_));
+    }
+    f.rc->resize(f.n);
+    if (opt_.ts_window) f.b.flags = DCC_OCC_APPEND_HISTORY;  // central_finish: commit tn + history
+    f.csr->to_batch(f.b);
+    submitting_ = true;
+    if (opt_.overlap) lk.unlock();
+    uint64_t ticket = 0;
+    int e;
+    {
+      std::lock_guard<std::mutex> eg(eng_mu_);
+      f.t0 = std::chrono::steady_clock::now();
+      e = dcc_occ_submit_epoch(ctx_, &f.b, f.rc->data(), nullptr, &ticket);
+    }
+    if (opt_.overlap) lk.lock();
+    f.ticket = ticket;
+    f.err = e;
+    f.submitted = true;
+    submitting_ = false;
+    cv_.notify_all();
+    return 0;
+  }
+
+  // Complete the oldest closed epoch (dcc_occ_wait_epoch), capture it, and
+  // hand its decisions to its waiters.  Called with lk held; returns with it.
+  int drive(std::unique_lock<std::mutex>& lk) {
+    driving_ = true;
+    Flight& f = fly_.front();  // only the driver removes entries
+    if (opt_.overlap) lk.unlock();
     dcc_stats st{};
-    const uint64_t tnc0 = dcc_occ_get_tnc(ctx_);
-    const auto t0 = std::chrono::steady_clock::now();
-    d.err = n ? dcc_occ_validate_epoch(ctx_, &b, d.rc.data(), nullptr, &st) : 0;
+    int err = f.err;
+    if (!err) {
+      std::lock_guard<std::mutex> eg(eng_mu_);
+      err = dcc_occ_wait_epoch(ctx_, f.ticket, &st);
+    }
     const auto t1 = std::chrono::steady_clock::now();
+    // tnc before this epoch: the epochs complete in close order, each
+    // advancing tnc by its committed writers (occ.cpp:283-284)
+    const uint64_t tnc0 = tnc_done_;
+    uint64_t n_cw = 0;
+    if (!err) {
+      const Csr& c = *f.csr;
+      for (uint64_t t = 0; t < f.n; t++) {
+        if ((*f.rc)[t] != DCC_RC_RCOK) continue;
+        for (uint64_t x = c.off[t]; x < c.off[t + 1]; x++)
+          if (((c.at2[x >> 2] >> (2 * (x & 3))) & 3u) == DCC_WR) {
+            n_cw++;
+            break;
+          }
+      }
+      tnc_done_ += n_cw;
+    }
     bool cap_err = false;
-    if (!d.err && !opt_.capture_dir.empty()) {
+    if (!err && !opt_.capture_dir.empty()) {
       dcc_file_info fi{};
       fi.kind = DCC_FILE_OCC;
-      fi.epoch = id;
+      fi.epoch = f.id;
       fi.tnc_before = tnc0;
       char path[4096];
       snprintf(path, sizeof path, "%s/epoch_%06llu.dccb", opt_.capture_dir.c_str(),
-               (unsigned long long)id);
+               (unsigned long long)f.id);
       // the epoch is decided (tnc and history advanced): a failed capture is
       // counted, never turned into aborts
       std::vector<uint64_t> fk, fs, ff;
       std::vector<uint8_t> fa;
-      fly_.full(fk, fa, fs, ff);
-      dcc_batch fb = b;
+      f.csr->full(fk, fa, fs, ff);
+      dcc_batch fb = f.b;
       fb.flags &= ~DCC_COMPACT_FLAGS;
       fb.keys = fk.data();
       fb.acctype = fa.data();
-      if (fly_.ntn) {
+      if (f.csr->ntn) {
         fb.start_tn = fs.data();
         fb.finish_tn = ff.data();
       }
-      cap_err = dcc_file_write(path, &fi, &fb, d.rc.data(), nullptr, nullptr, nullptr) != DCC_OK;
+      cap_err = dcc_file_write(path, &fi, &fb, f.rc->data(), nullptr, nullptr, nullptr) != DCC_OK;
     }
     if (opt_.overlap) lk.lock();
-    busy_ = false;
+    Decided d;
+    d.rc.assign(f.rc->data(), f.rc->data() + f.n);
+    if (err) std::fill(d.rc.begin(), d.rc.end(), (uint8_t)DCC_RC_ABORT);
+    d.readers = f.n;
+    d.err = err;
+    closed_waiting_ -= (int)f.n;
     stats_.capture_errors += cap_err ? 1 : 0;
     stats_.epochs++;
-    stats_.txns += n;
+    stats_.txns += f.n;
     for (uint8_t r : d.rc) (r == DCC_RC_RCOK ? stats_.commits : stats_.aborts)++;
     stats_.device_ms += st.device_ms;
-    stats_.wall_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
-    const int err = d.err;
-    decided_.emplace(id, std::move(d));
+    stats_.wall_ms += std::chrono::duration<double, std::milli>(t1 - f.t0).count();
+    decided_.emplace(f.id, std::move(d));
+    free_csr_.push_back(std::move(f.csr));
+    free_rc_.push_back(std::move(f.rc));
+    fly_.pop_front();
+    driving_ = false;
     cv_.notify_all();
     return err;
   }
 
   dcc_ctx* ctx_;
   Options opt_;
-  std::mutex mu_;
+  size_t depth_ = 1;
+  std::mutex mu_;      // the shim's state
+  std::mutex eng_mu_;  // engine calls (the context is thread-compatible)
   std::condition_variable cv_;
-  Csr open_, fly_;     // the epoch workers fill; the one on the GPU
-  bool busy_ = false;  // an engine call is in flight
+  std::unique_ptr<Csr> open_;  // the epoch the workers fill
+  std::deque<Flight> fly_;     // closed epochs in close order
+  std::vector<std::unique_ptr<Csr>> free_csr_;
+  std::vector<std::unique_ptr<PinnedVec<uint8_t>>> free_rc_;
+  bool submitting_ = false, driving_ = false;
   std::chrono::steady_clock::time_point opened_{};
   uint64_t epoch_ = 0;
-  int open_waiting_ = 0;  // workers in validate() for the open epoch
+  int open_waiting_ = 0;    // workers in validate() for the open epoch
+  int closed_waiting_ = 0;  // workers in validate() for closed, undecided epochs
+  uint64_t tnc_done_ = 0;   // commit counter after the last completed epoch
   std::map<uint64_t, Decided> decided_;
   Stats stats_;
 };

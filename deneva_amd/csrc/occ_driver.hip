@@ -898,9 +898,10 @@ int dcc_ctx::occ_begin(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, bo
   // levels per captured epoch (DCC_OPT_SWEEP_LEVELS; 0 = auto: 3 with the
   // read-only split, 4 without)
   r.glv = sw_levels ? sw_levels : (ro_on ? 3u : 4u);
-  r.gkey = GraphKey{d.off, d.keys, d.acctype, d.n, d.nnz, out_rc, r.dev_out,
+  // (host outputs are copied outside the graph: their addresses are not part of it)
+  r.gkey = GraphKey{d.off, d.keys, d.acctype, d.n, d.nnz, r.dev_out ? out_rc : nullptr, r.dev_out,
                     r.glv | (ro_on ? 0x80u | (wt_bits << 8) : 0u), buf_gen,
-                    d.start_tn, d.finish_tn, out_tn,
+                    d.start_tn, d.finish_tn, r.dev_out ? out_tn : (const void*)(uintptr_t)(out_tn != nullptr),
                     (r.want_tn ? 1u : 0u) | (r.app ? 2u : 0u) | (r.hist_on ? 4u : 0u)};
   r.replay = graph_ok && graph_exec && r.gkey == graph_key;
   // a failure while capturing must still end the capture
@@ -1009,11 +1010,21 @@ int dcc_ctx::occ_final(bool async) {
   dcc_ctx* ctx = this;
   OccRun& r = run;
   const DevBatch& d = r.d;
+  // host outputs are copied after the epoch's launches, outside any graph:
+  // one captured graph then serves every host output buffer (the pipeline's
+  // callers rotate theirs), and the device time includes the copies
+  auto copy_out = [&]() -> int {
+    if (r.dev_out) return DCC_OK;
+    if (r.out_rc) CK(hipMemcpyAsync(r.out_rc, rc.p, d.n, hipMemcpyDeviceToHost, stream));
+    if (r.out_tn) CK(hipMemcpyAsync(r.out_tn, tn.p, d.n * 8, hipMemcpyDeviceToHost, stream));
+    return DCC_OK;
+  };
   if (r.replay) {  // once: a second finalize (after more levels) runs directly
     r.replay = false;
     if (r.want_tn) r.fin_runs = 1;  // the graph holds the epoch's first central_finish
     CK(hipEventRecord(ev0, stream));
     CK(hipGraphLaunch(graph_exec, stream));
+    CR(copy_out());
     CK(hipEventRecord(ev1, stream));
     if (!async) CK(hipStreamSynchronize(stream));
     return DCC_OK;
@@ -1039,11 +1050,6 @@ int dcc_ctx::occ_final(bool async) {
                           r.fin_runs++ ? ++fin_tag : 0u, 0u},
                stream);
   CK(hipGetLastError());
-  if (!r.capturing) CK(hipEventRecord(ev1, stream));
-  if (!r.dev_out) {
-    if (r.out_rc) CK(hipMemcpyAsync(r.out_rc, rc.p, d.n, hipMemcpyDeviceToHost, stream));
-    if (r.out_tn) CK(hipMemcpyAsync(r.out_tn, tn.p, d.n * 8, hipMemcpyDeviceToHost, stream));
-  }
   if (r.capturing) {
     r.capturing = false;
     hipGraph_t g = nullptr;
@@ -1057,8 +1063,9 @@ int dcc_ctx::occ_final(bool async) {
     graph_key = r.gkey;
     CK(hipEventRecord(ev0, stream));
     CK(hipGraphLaunch(graph_exec, stream));
-    CK(hipEventRecord(ev1, stream));
   }
+  CR(copy_out());
+  CK(hipEventRecord(ev1, stream));
   CK(hipStreamSynchronize(stream));
   return DCC_OK;
 }
@@ -1075,7 +1082,21 @@ int dcc_ctx::occ_end(dcc_stats* st) {
   } inactive{&r.active};
   if (r.pending) {
     r.pending = false;
-    CK(hipStreamSynchronize(stream));
+    // the replayed graph's last record (ev1) marks the epoch done
+    static const int wait_mode = [] {
+      const char* e = DCC_ENV("DCC_WAIT_MODE");  // experiments: 0 stream sync, 1 event sync, 2 event poll
+      return e ? atoi(e) : 0;
+    }();
+    if (wait_mode == 1) {
+      CK(hipEventSynchronize(ev1));
+    } else if (wait_mode == 2) {
+      hipError_t q;
+      while ((q = hipEventQuery(ev1)) == hipErrorNotReady) {
+      }
+      CK(q);
+    } else {
+      CK(hipStreamSynchronize(stream));
+    }
   }
   dcc_stats& S = r.S;
   if (r.n_txn == 0) {

@@ -73,29 +73,28 @@ void dcc_pipe_destroy(dcc_ctx* ctx) {
   ctx->pipe = nullptr;
 }
 
-// Lanes on their own CUs (DCC_OPT_PIPE_PARTITION): lane i of L runs on the
-// XCDs x with x % L == i (L <= 8; 8 / L whole XCDs each), so a lane's
-// one-workgroup serial passes never wait for a CU that another lane's
-// chip-wide kernels hold, and a lane's working set (key tables, bitmaps,
-// level lists) stays in its own XCDs' L2s.  A stream's CU mask names CUs by
-// bit; the driver deals mask bits to the XCDs round-robin (bit b -> XCD
-// b % 8, tools/cumask_probe.hip), so XCD x is every bit b with b % 8 == x.
+// Lanes on their own CUs (DCC_OPT_PIPE_PARTITION): lane i of L runs on CU
+// mask bits [i n / L, (i + 1) n / L), so a lane's one-workgroup serial passes
+// never wait for a CU that another lane's chip-wide kernels hold.  A queue's
+// workgroups are dealt round-robin to all 8 XCDs whatever its mask, so every
+// XCD must keep CUs in every lane's mask (a mask that empties an XCD is
+// ignored: the stream then runs on the whole chip); the driver spreads a
+// range of consecutive mask bits evenly over the XCDs and their shader
+// engines (bits 0-31: four CUs on each XCD, one per SE;
+// tools/cumask_probe.hip, profiles/r06/cumask_probe.txt), so each lane gets
+// n / (8 L) CUs of every XCD.
 static int lane_partition(dcc_ctx* ctx, dcc_ctx* l, uint32_t i, uint32_t L) {
   const uint32_t n = (uint32_t)ctx->n_cu;
-  if (L < 2 || n % 8) return DCC_OK;  // one lane, or a chip without 8 equal XCDs: unmasked
+  if (L < 2 || n % (8 * L)) return DCC_OK;  // one lane, or CUs that do not split evenly: unmasked
   std::vector<uint32_t> mask((n + 31) / 32, 0u);
-  uint32_t cus = 0;
-  for (uint32_t b = 0; b < n; b++)
-    if ((b % 8) % L == i % L) {
-      mask[b / 32] |= 1u << (b % 32);
-      cus++;
-    }
+  const uint32_t b0 = i * n / L, b1 = (i + 1) * n / L;
+  for (uint32_t b = b0; b < b1; b++) mask[b / 32] |= 1u << (b % 32);
   hipStream_t s = nullptr;
   const hipError_t e = hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data());
   if (e != hipSuccess) return ctx->hip_fail(e, "pipeline lane: hipExtStreamCreateWithCUMask");
   if (l->own_stream) (void)hipStreamDestroy(l->own_stream);
   l->own_stream = l->stream = s;
-  l->n_cu = (int)cus;  // grids are sized to the lane's CUs
+  l->n_cu = (int)(b1 - b0);  // grids are sized to the lane's CUs
   return DCC_OK;
 }
 

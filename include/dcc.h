@@ -205,10 +205,10 @@ int dcc_set_profiling(dcc_ctx* ctx, int enable);
                                  over the one rank) instead of the one-GPU paths: the RCCL
                                  call path executes on a one-GPU box                         */
 #define DCC_OPT_PIPE_PARTITION 14 /* pipeline lanes on their own CUs: 0 every lane on the whole
-                                  chip; 1 lane i of L on the XCDs x with x % L == i (8 / L
-                                  whole XCDs each, its streams CU-masked), so a lane's serial
-                                  passes never queue behind another lane's chip-wide kernels
-                                  and its working set stays in its own XCDs' L2s           */
+                                  chip; 1 lane i of L on 1/L of the CUs of every XCD (its
+                                  stream CU-masked), so a lane's serial passes never queue
+                                  behind another lane's chip-wide kernels (L must divide
+                                  n_CU / 8; otherwise the lanes stay unmasked)             */
 int dcc_set_option(dcc_ctx* ctx, int option, int64_t value);
 /* Pre-size device workspaces so a later call performs no allocation. */
 int dcc_reserve(dcc_ctx* ctx, uint64_t max_txn, uint64_t max_nnz);

@@ -33,17 +33,18 @@ static int fails = 0;
     }                                                                   \
   } while (0)
 
-static void shim_threads(const char* dir, bool overlap) {
+static void shim_threads(const char* dir, bool overlap, int depth = 4, int workers = 4) {
   dcc_host::OccEpoch::Options o;
   o.overlap = overlap;
+  o.depth = depth;
   o.max_txns = 64;
-  o.n_workers = 4;
+  o.n_workers = workers;
   o.timer_ms = 1.0;
   o.capture_dir = dir;
   dcc_host::OccEpoch ep(stub_ctx(), o);
   std::atomic<uint64_t> commits{0}, aborts{0}, errs{0};
   std::vector<std::thread> th;
-  for (int w = 0; w < 4; w++)
+  for (int w = 0; w < workers; w++)
     th.emplace_back([&, w] {
       std::mt19937_64 rng(100 + w);
       for (int i = 0; i < 400; i++) {
@@ -61,8 +62,8 @@ static void shim_threads(const char* dir, bool overlap) {
   for (auto& t : th) t.join();
   const auto s = ep.stats();
   CHECK(errs == 0);
-  CHECK(commits + aborts == 1600);
-  CHECK(s.txns == 1600);
+  CHECK(commits + aborts == 400ull * workers);
+  CHECK(s.txns == 400ull * workers);
   CHECK(s.capture_errors == 0);
 }
 
@@ -188,7 +189,9 @@ static void oracles() {
 
 int main(int argc, char** argv) {
   const char* dir = argc > 1 ? argv[1] : ".";
-  shim_threads(dir, true);
+  shim_threads(dir, true);         // 4 epochs in flight
+  shim_threads(dir, true, 1);      // one in flight
+  shim_threads(dir, true, 4, 12);  // 12 workers: epochs close while others are in flight
   shim_threads(dir, false);
   batch_files(dir);
   oracles();

@@ -83,3 +83,47 @@ int dcc_host_free(dcc_ctx* ctx, void* p) {
   free(p);
   return DCC_OK;
 }
+
+/* The pipeline entry points (dcc_occ_submit_epoch / dcc_occ_wait_epoch):
+ * submit only records the epoch -- the shim must leave its arrays and the
+ * decision buffer alone until the wait -- and a wait decides every recorded
+ * epoch up to its ticket, in submit order (tnc advances in that order). */
+#define STUB_RING 64
+static struct {
+  dcc_batch b;
+  uint8_t* rc;
+  int done, err;
+} g_pend[STUB_RING];
+static uint64_t g_next = 1, g_decided = 0;
+
+int dcc_set_option(dcc_ctx* ctx, int option, int64_t value) {
+  (void)option;
+  (void)value;
+  return ctx ? DCC_OK : DCC_EINVAL;
+}
+
+int dcc_occ_submit_epoch(dcc_ctx* ctx, const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn,
+                         uint64_t* out_ticket) {
+  if (!ctx || !b || !out_ticket || out_tn) return DCC_EINVAL;
+  if (g_next - g_decided > STUB_RING) return DCC_ERANGE;
+  const uint64_t t = g_next++;
+  g_pend[t % STUB_RING].b = *b;
+  g_pend[t % STUB_RING].rc = out_rc;
+  g_pend[t % STUB_RING].done = 0;
+  *out_ticket = t;
+  return DCC_OK;
+}
+
+int dcc_occ_wait_epoch(dcc_ctx* ctx, uint64_t ticket, dcc_stats* st) {
+  if (!ctx || ticket == 0 || ticket >= g_next) return DCC_EINVAL;
+  while (g_decided < ticket) {
+    const uint64_t t = ++g_decided;
+    g_pend[t % STUB_RING].err = dcc_occ_validate_epoch(ctx, &g_pend[t % STUB_RING].b, g_pend[t % STUB_RING].rc,
+                                                       NULL, NULL);
+    g_pend[t % STUB_RING].done = 1;
+  }
+  if (!g_pend[ticket % STUB_RING].done) return DCC_EINVAL;
+  g_pend[ticket % STUB_RING].done = 0;
+  if (st) memset(st, 0, sizeof *st);
+  return g_pend[ticket % STUB_RING].err;
+}
