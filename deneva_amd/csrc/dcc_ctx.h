@@ -262,9 +262,14 @@ struct dcc_ctx {
     double t_wall0 = 0;
     uint64_t n_cw = 0;  // committed writers of the finished epoch (tnc advance)
     uint32_t fin_runs = 0;  // central_finish launches (a second one after more levels)
+    bool fin_later = false; // pipeline lane: central_finish runs at completion (pipe_finish)
   };
   OccRun run;
-  int occ_begin(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, bool async);
+  int occ_begin(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, bool async, bool fin_later = false);
+  // the central_finish of lane `l`'s completed epoch (decided with fin_later):
+  // commit tn from this context's tnc, the history append into this
+  // context's delta level -- run by the parent in submit order (occ_pipe.cpp)
+  int pipe_finish(dcc_ctx* l);
   int occ_end(dcc_stats* st);
   int occ_final(bool async);  // finalize launches (or the graph replay) of `run`
   // pipelined epochs over lane contexts on this device (occ_pipe.cpp)

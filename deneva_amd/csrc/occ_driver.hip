@@ -749,6 +749,74 @@ int dcc_ctx::occ_finish(const uint8_t* final_rc, uint64_t* out_tn, uint32_t flag
   return occ_finish_commit(n_cw, out_tn, flags);
 }
 
+// central_finish of a pipeline lane's epoch (occ.cpp:248-294), run by the
+// parent context when the epoch completes in submit order: every epoch before
+// it has finished, so this context's tnc and delta level are exactly what a
+// synchronous call would see.  The lane decided the epoch (its committed-
+// writer flags are in its cflag buffer, its batch still in place); k_fin
+// numbers the committed writers from this context's tnc and appends their
+// write sets to this context's delta level, on the lane's stream.  The lanes
+// never read the history (an epoch with a window check drains the pipeline
+// and runs here), so the history changes only in this host-ordered step.
+int dcc_ctx::pipe_finish(dcc_ctx* l) {
+  dcc_ctx* ctx = this;
+  OccRun& r = l->run;
+  const DevBatch& d = r.d;
+  if (r.n_txn == 0 || !r.fin_later) return DCC_OK;
+  HistStore& D = hs[1];
+  if (r.app) {
+    CR(hist_prepare());  // merge / rebuild as a synchronous append would
+    CR(hist_grow_flat(D, D.m + d.nnz));
+    CK(hipStreamSynchronize(stream));  // this context's launches before the lane's k_fin
+  }
+  if (l->fin_tag + 4 >= (1u << 30)) {
+    CK(hipMemsetAsync(l->fin_part.p, 0, l->fin_part.cap, l->stream));
+    l->fin_tag = 0;
+  }
+  OccDyn& y = *(OccDyn*)l->hdyn;
+  y.tnc = tnc;
+  y.fin_tag = ++l->fin_tag;
+  y.hist_m = D.m;
+  y.app_k = r.app ? (uint64_t*)D.fk.p : nullptr;
+  y.app_t = r.app ? (uint64_t*)D.ft.p : nullptr;
+  y.ins = r.app ? hist_insert_args(D) : HistInsert{};
+  y.view = HistView{};
+  if (r.app) D.built = false;  // until the append is accepted (see occ_begin)
+  FillArgs fa{};
+  fa.job[fa.n++] = FillJob{(uint32_t*)l->dyn.p, sizeof(OccDyn) / 4, 0u, (const uint32_t*)l->hdyn_dev};
+  launch_fill(fa, l->stream);
+  launch_fin(OccFinArgs{d.n, d.nnz, r.cf, d.off, d.keys, d.acctype, (uint64_t*)l->fin_part.p,
+                        (const OccDyn*)l->dyn.p, r.tn_dev, (uint64_t*)((char*)l->hdyn_dev + HDYN_TOTALS), 0u, 0u},
+             l->stream);
+  CK(hipGetLastError());
+  if (!r.dev_out && r.out_tn) CK(hipMemcpyAsync(r.out_tn, l->tn.p, d.n * 8, hipMemcpyDeviceToHost, l->stream));
+  CK(hipStreamSynchronize(l->stream));
+  const uint64_t* tot = (const uint64_t*)((const char*)l->hdyn + HDYN_TOTALS);
+  if (tot[0] != r.n_cw) {
+    std::string why = "look-back words unreadable";
+    std::vector<uint8_t> w(fin_part_bytes(d.n));
+    if (hipMemcpy(w.data(), l->fin_part.p, w.size(), hipMemcpyDeviceToHost) == hipSuccess)
+      why = fin_diag(w.data(), d.n, l->fin_tag);
+    (void)hipGetLastError();
+    return fail(DCC_EIO, "central_finish numbered %llu txns, %llu committed writers (%s)",
+                (unsigned long long)tot[0], (unsigned long long)r.n_cw, why.c_str());
+  }
+  if (r.app) {
+    if (tot[1] > d.nnz) return fail(DCC_EIO, "history append: %llu writes > %llu accesses",
+                                    (unsigned long long)tot[1], (unsigned long long)d.nnz);
+    if (tot[1]) {
+      D.m += tot[1];
+      D.max_key = std::max<uint64_t>(D.max_key, tot[2]);
+      D.last_app = tot[1];
+      hist_note(D, tnc + 1, tnc + r.n_cw);
+    }
+    if (tot[3]) D.overflowed = true;
+    D.built = !tot[3];
+  }
+  tnc += r.n_cw;
+  return DCC_OK;
+}
+
 // The read-only list of a split epoch, once every writer is decided: the
 // writer table of the committed writes (k_sw_wall: the committed writers the
 // serial passes listed, or after a hand-off to the round solver every
@@ -793,7 +861,7 @@ static double wall_ms() {
 // finalize (or the captured graph's replay).  With `async` and a replayable
 // graph the call returns right after the graph launch (run.pending); occ_end
 // synchronises and reads the results back.
-int dcc_ctx::occ_begin(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, bool async) {
+int dcc_ctx::occ_begin(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, bool async, bool fin_later) {
   dcc_ctx* ctx = this;
   if (run.active) return fail(DCC_EINVAL, "an epoch of this context is still in flight");
   run = OccRun{};
@@ -847,6 +915,11 @@ int dcc_ctx::occ_begin(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, bo
   CR(rc.ensure(this, d.n + 16, "rc"));
   r.want_tn = out_tn != nullptr || (b->flags & DCC_OCC_APPEND_HISTORY);
   r.app = (b->flags & DCC_OCC_APPEND_HISTORY) != 0;
+  // a pipeline lane's epoch: central_finish (commit tn, history append) is
+  // left to the parent context when the epoch completes in submit order
+  // (dcc_ctx::pipe_finish); the lane decides only
+  r.fin_later = fin_later && r.want_tn;
+  const bool app_here = r.app && !r.fin_later;
   if (r.want_tn) {
     CR(cflag.ensure(this, d.n * 4, "cflag"));
     {
@@ -869,17 +942,17 @@ int dcc_ctx::occ_begin(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, bo
   // the history the window check reads (merge / level builds: launched here,
   // before any capture) and room for this epoch's append
   r.hist_on = d.start_tn && hist_size() > 0;
-  if (r.hist_on || r.app) CR(hist_prepare());  // an append inserts into the delta's table
-  if (r.app) CR(hist_grow_flat(hs[1], hs[1].m + d.nnz));
+  if (r.hist_on || app_here) CR(hist_prepare());  // an append inserts into the delta's table
+  if (app_here) CR(hist_grow_flat(hs[1], hs[1].m + d.nnz));
   static_assert(sizeof(OccDyn) <= HDYN_TOTALS, "epoch parameters overlap the totals");
   {
     OccDyn& y = *(OccDyn*)hdyn;
     y.tnc = tnc;
     y.fin_tag = ++fin_tag;
     y.hist_m = hs[1].m;
-    y.app_k = r.app ? (uint64_t*)hs[1].fk.p : nullptr;
-    y.app_t = r.app ? (uint64_t*)hs[1].ft.p : nullptr;
-    y.ins = r.app ? hist_insert_args(hs[1]) : HistInsert{};
+    y.app_k = app_here ? (uint64_t*)hs[1].fk.p : nullptr;
+    y.app_t = app_here ? (uint64_t*)hs[1].ft.p : nullptr;
+    y.ins = app_here ? hist_insert_args(hs[1]) : HistInsert{};
     y.view = hist_view();
   }
   // central_finish pushes this epoch's pairs onto the delta's chains before
@@ -887,7 +960,7 @@ int dcc_ctx::occ_begin(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, bo
   // append, the delta counts as unbuilt, so an epoch that fails (and a retry
   // that pushes the same flat positions again) leaves a table the next
   // window check rebuilds from the flat pairs instead of walking
-  if (r.app) hs[1].built = false;
+  if (app_here) hs[1].built = false;
   // The sweep's whole launch sequence (parameters ... central_finish) is
   // replayed from a captured HIP graph when the batch, the outputs and every
   // workspace are the ones it was captured with: one graph launch instead of
@@ -902,7 +975,8 @@ int dcc_ctx::occ_begin(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, bo
   r.gkey = GraphKey{d.off, d.keys, d.acctype, d.n, d.nnz, r.dev_out ? out_rc : nullptr, r.dev_out,
                     r.glv | (ro_on ? 0x80u | (wt_bits << 8) : 0u), buf_gen,
                     d.start_tn, d.finish_tn, r.dev_out ? out_tn : (const void*)(uintptr_t)(out_tn != nullptr),
-                    (r.want_tn ? 1u : 0u) | (r.app ? 2u : 0u) | (r.hist_on ? 4u : 0u)};
+                    (r.want_tn ? 1u : 0u) | (r.app ? 2u : 0u) | (r.hist_on ? 4u : 0u) |
+                        (r.fin_later ? 8u : 0u)};
   r.replay = graph_ok && graph_exec && r.gkey == graph_key;
   // a failure while capturing must still end the capture
   struct CaptureGuard {
@@ -1016,7 +1090,7 @@ int dcc_ctx::occ_final(bool async) {
   auto copy_out = [&]() -> int {
     if (r.dev_out) return DCC_OK;
     if (r.out_rc) CK(hipMemcpyAsync(r.out_rc, rc.p, d.n, hipMemcpyDeviceToHost, stream));
-    if (r.out_tn) CK(hipMemcpyAsync(r.out_tn, tn.p, d.n * 8, hipMemcpyDeviceToHost, stream));
+    if (r.out_tn && !r.fin_later) CK(hipMemcpyAsync(r.out_tn, tn.p, d.n * 8, hipMemcpyDeviceToHost, stream));
     return DCC_OK;
   };
   if (r.replay) {  // once: a second finalize (after more levels) runs directly
@@ -1042,7 +1116,7 @@ int dcc_ctx::occ_final(bool async) {
   FinalArgs fa{d.n, (const uint8_t*)state.p, (const uint8_t*)hasw.p, r.rc_dev, r.cf,
                (FinalPart*)hpart_dev};
   launch_final(fa, ga, stream);
-  if (r.want_tn)
+  if (r.want_tn && !r.fin_later)
     // a second central_finish of the epoch (after more levels or a hand-off:
     // the graph's ran on a partly decided epoch) needs a fresh look-back tag
     launch_fin(OccFinArgs{d.n, d.nnz, r.cf, d.off, d.keys, d.acctype, (uint64_t*)fin_part.p,
@@ -1371,7 +1445,7 @@ int dcc_ctx::occ_end(dcc_stats* st) {
   if (r.defer) {
     CR(fin_save(d, !r.dev_out, nnz_w));
   } else {
-    if (r.want_tn) {
+    if (r.want_tn && !r.fin_later) {
       // central_finish ran on the device (k_fin_*): its totals
       const uint64_t* tot = (const uint64_t*)((const char*)hdyn + HDYN_TOTALS);
       if (tot[0] != n_cw) {

@@ -9,8 +9,12 @@
 // share the chip: each lane is a full engine context on the same device (its
 // own stream, workspaces and captured graph), epoch k goes to lane k mod L,
 // and the epochs complete -- results read back, tnc advanced -- in submit
-// order.  An epoch that needs anything shared (commit tn, the history,
-// deferred finish) drains the lanes and runs on the parent context itself.
+// order.  Commit tn and the history append (central_finish, occ.cpp:277-286)
+// are the parent's: a lane only decides, and the parent numbers and appends
+// each epoch when it completes (dcc_ctx::pipe_finish), so the history changes
+// only in submit order.  An epoch that reads the history (a window over a
+// non-empty history, or over appends still in flight) or defers its finish
+// drains the lanes and runs on the parent context itself.
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
@@ -39,6 +43,7 @@ struct OccPipe {
   uint32_t next_lane = 0;
   hipEvent_t ready = nullptr;  // the caller's stream, before an epoch's first lane launch
   uint32_t part = 0;           // DCC_OPT_PIPE_PARTITION the lanes were made with
+  uint32_t app_in_flight = 0;  // epochs in flight whose history append is still to come
 };
 
 static void pipe_complete_front(dcc_ctx* ctx) {
@@ -49,11 +54,17 @@ static void pipe_complete_front(dcc_ctx* ctx) {
   OccPipe::Result r{};
   (void)hipSetDevice(lane->device);
   r.rc = lane->occ_end(&r.st);
-  if (r.rc == DCC_OK) {
-    ctx->tnc += lane->run.n_cw;  // tnc advances in submit order (occ.cpp:283-284)
-  } else {
+  if (r.rc != DCC_OK) {
     r.err = lane->last_error;
+  } else if (lane->run.fin_later) {
+    // commit tn and the history append from the parent's state, in submit
+    // order (central_finish, occ.cpp:248-294)
+    r.rc = ctx->pipe_finish(lane);
+    if (r.rc != DCC_OK) r.err = ctx->last_error;
+  } else {
+    ctx->tnc += lane->run.n_cw;  // tnc advances in submit order (occ.cpp:283-284)
   }
+  if (lane->run.fin_later && lane->run.app) p->app_in_flight--;
   lane->tnc = 0;
   p->done[f.ticket] = std::move(r);
 }
@@ -156,8 +167,13 @@ extern "C" int dcc_occ_submit_epoch(dcc_ctx* ctx, const dcc_batch* b, uint8_t* o
   }
   OccPipe* p = ctx->pipe;
   const uint64_t ticket = p->next;
-  const bool shared = out_tn || (b->flags & (DCC_OCC_APPEND_HISTORY | DCC_OCC_DEFER_FINISH)) ||
-                      (b->start_tn && ctx->hist_size() > 0) || ctx->fin_pending;
+  // Commit tn and the history append go to lanes too (the parent runs each
+  // epoch's central_finish when it completes, pipe_finish).  What needs the
+  // epochs before it finished runs on the parent after a drain: a history
+  // window over a non-empty history -- or over appends still in flight --
+  // and the deferred 2PC finish.
+  const bool shared = (b->flags & DCC_OCC_DEFER_FINISH) || ctx->fin_pending ||
+                      (b->start_tn && (ctx->hist_size() > 0 || p->app_in_flight > 0));
   const bool lanes_ok = !ctx->multi && !ctx->sharded() && !ctx->profiling &&
                         ctx->use_sweep() && !shared && b->n_txn > 0;
   if (!lanes_ok) {
@@ -183,7 +199,8 @@ extern "C" int dcc_occ_submit_epoch(dcc_ctx* ctx, const dcc_batch* b, uint8_t* o
     return ctx->hip_fail(hipGetLastError(), "pipeline stream ordering");
   p->next++;
   *out_ticket = ticket;
-  const int e = lane->occ_begin(b, out_rc, nullptr, true);
+  const int e = lane->occ_begin(b, out_rc, out_tn, true, true);
+  if (e == DCC_OK && lane->run.fin_later && lane->run.app) p->app_in_flight++;
   if (e != DCC_OK) {
     OccPipe::Result r{};
     r.rc = e;

@@ -246,12 +246,14 @@ class Engine:
             self._fin_n = n
         return out_rc[:n], (out_tn[:n] if want_tn else None), st.as_dict()
 
-    def occ_submit_epoch(self, batch: EpochBatch, out_rc, out_tn=None) -> int:
+    def occ_submit_epoch(self, batch: EpochBatch, out_rc, out_tn=None,
+                         append_history: bool = False) -> int:
         """Enqueue an epoch on the pipeline (dcc_occ_submit_epoch) and return
         its ticket; the batch arrays and outputs must stay alive and unchanged
         until ``occ_wait_epoch(ticket)``.  Results equal dcc_occ_validate_epoch
-        on the epochs in submit order."""
-        b = batch.to_c(0)
+        on the epochs in submit order (commit tn and the history append
+        included: the context runs each epoch's central_finish as it completes)."""
+        b = batch.to_c(_abi.OCC_APPEND_HISTORY if append_history else 0)
         t = C.c_uint64(0)
         _check(lib.dcc_occ_submit_epoch(self._h, C.byref(b), _ptr(out_rc), _ptr(out_tn),
                                         C.byref(t)), self._h)

@@ -272,11 +272,14 @@ int dcc_occ_validate_epoch(dcc_ctx* ctx, const dcc_batch* batch, uint8_t* out_rc
  * next epoch's streaming passes.  The results are exactly those of calling
  * dcc_occ_validate_epoch on the epochs in submit order: under TS_CLOCK (no
  * history window) epochs of central_validate are
- * independent except for the commit counter tnc, which advances in submit
- * order.  An epoch that needs more -- commit tn (out_commit_tn),
- * DCC_OCC_APPEND_HISTORY, a window against a non-empty history,
- * DCC_OCC_DEFER_FINISH, profiling, the round solver, or a multi-GPU or
- * key-sharded context -- first drains the pipeline and then runs
+ * independent except for central_finish's commit counter and history
+ * (occ.cpp:277-286), so each lane decides its epoch and the context runs the
+ * epoch's central_finish -- commit tn (out_commit_tn) and the
+ * DCC_OCC_APPEND_HISTORY append -- when the epoch completes, in submit
+ * order.  An epoch that needs the epochs before it finished -- a window
+ * against a non-empty history or against appends still in flight,
+ * DCC_OCC_DEFER_FINISH -- or profiling, the round solver, or a multi-GPU or
+ * key-sharded context first drains the pipeline and then runs
  * synchronously, still in submit order.  The batch arrays and the outputs
  * must stay valid and unchanged until the epoch's dcc_occ_wait_epoch
  * returns.  *out_ticket (1, 2, ...) names the epoch.  Argument errors are

@@ -6,11 +6,14 @@ commit counter tnc (occ.cpp:283-284) advancing in submit order.
 
 Cases: 2, 3 and 4 lanes over distinct device batches (graph-replayed after
 each lane's first epoch), host batches, out-of-order waits, an epoch asking
-for commit tn in the middle of the stream (it drains the lanes and numbers
-from the tnc of every epoch before it), a malformed batch (its error comes
-back from its own wait; the others are unaffected), the synchronous entry
-point draining the lanes first, and every epoch of a full-size (1M) stream
-checked against the oracle."""
+for commit tn in the middle of the stream (numbered from the tnc of every
+epoch before it), streams of epochs with commit tn and the history append
+(central_finish, occ.cpp:277-286, run by the context as each epoch
+completes) checked tn by tn and pair by pair, a history window behind
+appends still in flight (it drains the lanes), a malformed batch (its error
+comes back from its own wait; the others are unaffected), the synchronous
+entry point draining the lanes first, and every epoch of a full-size (1M)
+stream checked against the oracle."""
 import numpy as np
 import pytest
 
@@ -80,7 +83,10 @@ def test_host_batches_and_out_of_order_waits(eng):
     assert eng.tnc == exp[-1][2]
 
 
-def test_commit_tn_epoch_drains_and_numbers_in_order(eng):
+def test_commit_tn_epoch_in_stream_numbers_in_order(eng):
+    """An epoch asking for commit tn in the middle of the stream stays on its
+    lane; the context numbers it when it completes, from the tnc of every
+    epoch before it (occ.cpp:283-284)."""
     import torch
     eng.set_option(OPT_PIPELINE, 2)
     bs = batches(30000, 5, seed=0x99)
@@ -173,3 +179,116 @@ def test_option_change_keeps_outstanding_tickets(eng):
         assert np.array_equal(o.cpu().numpy(), erc), f"epoch {i}"
         assert sts[i]["n_commit"] == int(np.count_nonzero(erc == d.RC_RCOK))
     assert eng.tnc == exp[-1][2]
+
+
+def committed_pairs(b, tn):
+    off = np.asarray(b.offsets, np.int64)
+    owner = np.repeat(np.arange(b.n_txn), np.diff(off))
+    sel = (np.asarray(b.acctype) == d.WR) & (np.asarray(tn)[owner] != 0)
+    return np.asarray(b.keys, np.uint64)[sel], np.asarray(tn, np.uint64)[owner[sel]]
+
+
+def sorted_pairs(k, t):
+    k, t = np.asarray(k, np.uint64), np.asarray(t, np.uint64)
+    o = np.lexsort((t, k))
+    return k[o], t[o]
+
+
+@pytest.mark.parametrize("lanes,device", [(2, True), (4, True), (3, False)])
+def test_tn_and_history_stream(eng, lanes, device):
+    """Every epoch of the stream wants commit tn and appends its committed
+    writes (the reference's central_finish under TS_CLOCK); the lanes only
+    decide, the context numbers and appends in submit order.  Each epoch's
+    tns, tnc and the final history equal the oracle's serial chain; then an
+    epoch with TS_CAS windows behind two appends still in flight drains the
+    lanes and sees all of them."""
+    import torch
+    eng.set_option(OPT_PIPELINE, lanes)
+    eng.history_clear()
+    try:
+        bs = batches(40000, 7, seed=0x7A1)
+        tnc, exp, hk, ht = 0, [], np.zeros(0, np.uint64), np.zeros(0, np.uint64)
+        for b in bs:
+            rc, tn, tnc = orc.occ(b, tnc=tnc)
+            exp.append((rc, tn, tnc))
+            k, t = committed_pairs(b, tn)
+            hk, ht = np.concatenate([hk, k]), np.concatenate([ht, t])
+        if device:
+            ins = [b.to_torch("cuda:0") for b in bs]
+            rcs = [torch.empty(b.n_txn, dtype=torch.uint8, device="cuda:0") for b in bs]
+            tns = [torch.empty(b.n_txn, dtype=torch.int64, device="cuda:0") for b in bs]
+        else:
+            ins = bs
+            rcs = [np.zeros(b.n_txn, np.uint8) for b in bs]
+            tns = [np.zeros(b.n_txn, np.uint64) for b in bs]
+        for rep in range(2):  # the second pass replays every lane's graph
+            eng.history_clear()
+            eng.tnc = 0
+            ts = [eng.occ_submit_epoch(x, r, t, append_history=True) for x, r, t in zip(ins, rcs, tns)]
+            for t in ts:
+                eng.occ_wait_epoch(t)
+            for i, (r, t, (erc, etn, _)) in enumerate(zip(rcs, tns, exp)):
+                r = r.cpu().numpy() if device else r
+                t = t.cpu().numpy().view(np.uint64) if device else t
+                assert np.array_equal(r, erc), f"pass {rep} epoch {i}: rc"
+                assert np.array_equal(t, etn), f"pass {rep} epoch {i}: tn"
+            assert eng.tnc == exp[-1][2]
+            assert eng.history_size == hk.size
+            gk, gt = eng.history_export()
+            wk, wt = sorted_pairs(hk, ht)
+            assert np.array_equal(gk, wk) and np.array_equal(gt, wt)
+        # a window epoch behind appends still in flight
+        eng.history_clear()
+        eng.tnc = 0
+        w = d.gen_ycsb(n_txn=30000, zipf_theta=0.9, seed=0x7A9)
+        rng = np.random.default_rng(5)
+        t2 = exp[1][2]
+        w.start_tn = rng.integers(0, t2 + 1, size=w.n_txn).astype(np.uint64)
+        w.finish_tn = (w.start_tn + rng.integers(0, t2 + 1, size=w.n_txn)).astype(np.uint64)
+        k01 = [committed_pairs(bs[i], exp[i][1]) for i in range(2)]
+        wrc, wtn, wtnc = orc.occ(w, hist_keys=np.concatenate([k01[0][0], k01[1][0]]),
+                                 hist_tn=np.concatenate([k01[0][1], k01[1][1]]), tnc=t2)
+        ow = np.zeros(w.n_txn, np.uint8)
+        otw = np.zeros(w.n_txn, np.uint64)
+        keep = [(np.zeros(bs[i].n_txn, np.uint8), np.zeros(bs[i].n_txn, np.uint64)) for i in range(2)]
+        ts = [eng.occ_submit_epoch(bs[i], keep[i][0], keep[i][1], append_history=True) for i in range(2)]
+        tw = eng.occ_submit_epoch(w, ow, otw, append_history=True)
+        for t in ts + [tw]:
+            eng.occ_wait_epoch(t)
+        assert np.array_equal(ow, wrc) and np.array_equal(otw, wtn) and eng.tnc == wtnc
+    finally:
+        eng.history_clear()
+
+
+def test_full_size_tn_history_stream(eng):
+    """Five 1M-txn theta=0.9 epochs on 4 lanes, each with commit tn and the
+    history append: every epoch's tns and the history against the oracle."""
+    import torch
+    eng.set_option(OPT_PIPELINE, 4)
+    eng.history_clear()
+    try:
+        bs = batches(1 << 20, 5, seed=0xD3E7A001)
+        tnc, exp = 0, []
+        hk, ht = [], []
+        for b in bs:
+            rc, tn, tnc = orc.occ(b, tnc=tnc)
+            exp.append((rc, tn, tnc))
+            k, t = committed_pairs(b, tn)
+            hk.append(k)
+            ht.append(t)
+        dbs = [b.to_torch("cuda:0") for b in bs]
+        rcs = [torch.empty(b.n_txn, dtype=torch.uint8, device="cuda:0") for b in bs]
+        tns = [torch.empty(b.n_txn, dtype=torch.int64, device="cuda:0") for b in bs]
+        eng.tnc = 0
+        ts = [eng.occ_submit_epoch(x, r, t, append_history=True) for x, r, t in zip(dbs, rcs, tns)]
+        for t in ts:
+            eng.occ_wait_epoch(t)
+        for i, (r, t, (erc, etn, _)) in enumerate(zip(rcs, tns, exp)):
+            assert np.array_equal(r.cpu().numpy(), erc), f"epoch {i}: rc"
+            assert np.array_equal(t.cpu().numpy().view(np.uint64), etn), f"epoch {i}: tn"
+        assert eng.tnc == exp[-1][2]
+        gk, gt = eng.history_export()
+        wk, wt = sorted_pairs(np.concatenate(hk), np.concatenate(ht))
+        assert np.array_equal(gk, wk) and np.array_equal(gt, wt)
+    finally:
+        eng.history_clear()
