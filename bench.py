@@ -423,6 +423,69 @@ def history_config(eng, dev, timed, orc, tag="HIST", n=1 << 18, epochs=8):
             "parity_vs_oracle": bool(par)}
 
 
+def pipe_fin_config(eng, dev, timed, orc, tag="PIPE_FIN", n=1 << 20, lanes=4, k=40):
+    """The headline stream with the reference's whole central_finish
+    (occ.cpp:248-294) under its default TS_CLOCK: every epoch wants commit tn
+    and appends its committed writes to the device history
+    (DCC_OCC_APPEND_HISTORY), submitted through the pipeline
+    (dcc_occ_submit_epoch): the lanes decide, the context numbers and appends
+    each epoch as it completes, in submit order (dcc_ctx::pipe_finish).  k
+    epochs over `lanes` distinct resident batches from an empty history
+    (merges of the delta into the base included); each lane's last epoch's
+    decisions and tns are checked against the oracle (tn = the batch's own
+    numbering from tnc 0 shifted by the tnc before the epoch)."""
+    import torch
+    import deneva_amd as d
+    from collections import deque
+    bs = [d.gen_ycsb(n_txn=n, zipf_theta=0.9, seed=0xD3E7A001 + i) for i in range(lanes)]
+    dbs = [b.to_torch(dev) for b in bs]
+    rcs = [torch.empty(n, dtype=torch.uint8, device=dev) for _ in range(lanes)]
+    tns = [torch.empty(n, dtype=torch.int64, device=dev) for _ in range(lanes)]
+    exp = [orc.occ(b) for b in bs]  # (rc, tn from tnc 0, committed writers)
+    eng.set_option(d._abi.OPT_PIPELINE, lanes)
+
+    def stream(kk):
+        eng.history_clear()
+        eng.tnc = 0
+        tnc_before = [0] * kk
+        fl, t = deque(), 0
+        for i in range(kk):
+            tnc_before[i] = t
+            t += exp[i % lanes][2]
+            fl.append(eng.occ_submit_epoch(dbs[i % lanes], rcs[i % lanes], tns[i % lanes],
+                                           append_history=True))
+            if len(fl) >= lanes:
+                eng.occ_wait_epoch(fl.popleft())
+        while fl:
+            eng.occ_wait_epoch(fl.popleft())
+        return tnc_before
+
+    stream(2 * lanes)  # warm-up: every lane's graph captured
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    tnc_before = stream(k)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / k
+    par = eng.tnc == sum(exp[i % lanes][2] for i in range(k))
+    for i in range(k - lanes, k):
+        erc, etn, _ = exp[i % lanes]
+        want = np.where(etn != 0, etn + np.uint64(tnc_before[i]), np.uint64(0))
+        par = par and np.array_equal(rcs[i % lanes].cpu().numpy(), erc)
+        par = par and np.array_equal(tns[i % lanes].cpu().numpy().view(np.uint64), want)
+    hist = eng.history_size
+    eng.history_clear()
+    eng.tnc = 0
+    return {"workload": f"{k} consecutive OCC epochs of {n} YCSB txns x 16 keys (theta=0.9) through "
+                        f"the pipeline ({lanes} lanes), each with commit tn and its committed writes "
+                        f"appended to the device history (central_finish under TS_CLOCK)",
+            "txns_per_s": n / dt, "ms_per_epoch": dt * 1e3,
+            "history_pairs_at_end": int(hist),
+            "parity_vs_oracle": bool(par),
+            "parity_scope": "rc and tn of each lane's last epoch, tnc after the stream",
+            "note": "a stream whose epochs carry TS_CAS windows reading the previous epochs' history "
+                    "cannot overlap (each window needs the epoch before it finished): see HIST / SHIM"}
+
+
 def _pcie_h2d_GBps(nbytes):
     """The link: a pinned host -> device copy of nbytes (torch, median of 5)."""
     import torch
@@ -536,7 +599,8 @@ def shim_config(eng, dev, timed, orc, tag="SHIM", n=1 << 20, steps=6):
 
 CONFIGS = {"C2": occ_config, "C3": occ_config, "C5": occ_config, "C4": calvin_config,
            "C4_SHUF": calvin_config,
-           "C6": None, "HIST": history_config, "SHIM": shim_config, "MAAT_C2": maat_config,
+           "C6": None, "HIST": history_config, "SHIM": shim_config, "PIPE_FIN": pipe_fin_config,
+           "MAAT_C2": maat_config,
            "MAAT_1M": maat_config}
 
 

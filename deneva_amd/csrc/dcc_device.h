@@ -21,6 +21,15 @@
 namespace dcc {
 
 constexpr uint64_t KEY_EMPTY = 0xFFFFFFFFFFFFFFFFull;
+
+// Bounded spins of cross-workgroup waits (look-back predecessors, grid
+// barriers) are bounded in time, generously: processes sharing one GPU are
+// time-sliced, and a workgroup dispatched before the waiter can stay
+// switched out for hundreds of milliseconds (round 6: an iteration bound of
+// ~0.4 s expired under four rank processes on one GPU, and k_fin numbered a
+// partly published prefix).  The bound only turns a hang into an error.
+constexpr uint64_t SPIN_TICKS = 2000000000ull;  // 20 s of the 100 MHz realtime clock
+__device__ inline uint64_t spin_clock() { return __builtin_amdgcn_s_memrealtime(); }
 constexpr uint32_t OWN_EMPTY = 0xFFFFFFFFu;
 constexpr uint32_t IDX_BITS = 26;
 constexpr uint32_t IDX_MASK = (1u << IDX_BITS) - 1;

@@ -586,10 +586,10 @@ __global__ __launch_bounds__(256) void k_mt_round(MtRoundArgs a, MtLb* lb, uint3
         const int64_t j = hi - (int64_t)lane;
         uint32_t stw = 0;
         if (j >= 0) {
-          uint32_t spins = 0;
+          const uint64_t t0 = spin_clock();
           while (((stw = ld_dev(&lb[j].status)) >> 2) != tag) {
             __builtin_amdgcn_s_sleep(1);
-            if (++spins > (1u << 24)) {
+            if (spin_clock() - t0 > SPIN_TICKS) {
               timed_out = true;
               break;
             }

@@ -424,19 +424,6 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1, const SwShard* shl
     if (ros) {
       sa.cw_list = (uint32_t*)sw_cw.p;
       sa.cw_count = wctl + 4;
-      if (top) {
-        sa.wclear = (uint4*)sw_wtab.p;
-        sa.wclear_n16 = (sizeof(WrSlot) << wt_bits) / 16;
-      }
-    }
-    if (top) {  // the epoch's validation pass rides along the level-0 serial pass
-      // (a rank holding the whole batch takes its has-write bytes from it)
-      const bool whole = shl && shl->full_off;
-      sa.prep_off = whole ? shl->full_off : d.off;
-      sa.prep_n = d.n;
-      sa.prep_at = whole ? shl->full_at : d.acctype;
-      sa.prep_nnz = whole ? shl->full_nnz : d.nnz;
-      sa.prep_part = (PrepPart*)((char*)hpart_dev + SW_PREP_OFF);
     }
     if (serial_part) launch_sw_seq(sa, stream);
     // the last level of a graph-captured epoch usually decides its whole list
@@ -445,6 +432,20 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1, const SwShard* shl
     if (tail_serial && l == l1 - 1) break;
     SwCoutArgs ca{sin,     aent,    apos,    (const uint64_t*)sw_mg.p, lv, cbits_d, ckeys_d,
                   bloom_d, abandon, smdev, sm_host, shl ? 0 : 1};
+    if (top && serial_part) {  // the epoch's validation pass rides along the level-0 listing
+      // (a rank holding the whole batch takes its has-write bytes from it)
+      const bool whole = shl && shl->full_off;
+      ca.prep_off = whole ? shl->full_off : d.off;
+      ca.prep_n = d.n;
+      ca.prep_at = whole ? shl->full_at : d.acctype;
+      ca.prep_nnz = whole ? shl->full_nnz : d.nnz;
+      ca.prep_part = (PrepPart*)((char*)hpart_dev + SW_PREP_OFF);
+      ca.hasw = (uint8_t*)hasw.p;
+      if (ros) {
+        ca.wclear = (uint4*)sw_wtab.p;
+        ca.wclear_n16 = (sizeof(WrSlot) << wt_bits) / 16;
+      }
+    }
     launch_sw_cout(ca, (unsigned)std::min<uint64_t>((pa.budget + 1023) / 1024, 4ull * n_cu), stream);
     SwFilterArgs fa;
     fa.in = in;
@@ -767,7 +768,10 @@ int dcc_ctx::pipe_finish(dcc_ctx* l) {
   if (r.app) {
     CR(hist_prepare());  // merge / rebuild as a synchronous append would
     CR(hist_grow_flat(D, D.m + d.nnz));
-    CK(hipStreamSynchronize(stream));  // this context's launches before the lane's k_fin
+    // this context's launches (merge, rebuild) before the lane's k_fin: a
+    // device-side wait, the host does not block
+    CK(hipEventRecord(ev1, stream));
+    CK(hipStreamWaitEvent(l->stream, ev1, 0));
   }
   if (l->fin_tag + 4 >= (1u << 30)) {
     CK(hipMemsetAsync(l->fin_part.p, 0, l->fin_part.cap, l->stream));
@@ -1189,9 +1193,9 @@ int dcc_ctx::occ_end(dcc_stats* st) {
   if (sweep) {
     // prep results: the batch is rejected exactly as device_prep would
     const PrepPart* pp = (const PrepPart*)((const char*)hpart + SW_PREP_OFF);
-    static_assert(SW_PREP_OFF + SW_SEQ_PREP_BLOCKS * sizeof(PrepPart) <= (1u << 16), "hpart holds them");
+    static_assert(SW_PREP_OFF + SW_PREP_BLOCKS * sizeof(PrepPart) <= (1u << 16), "hpart holds them");
     uint32_t perr = 0;
-    for (unsigned q = 0; q < SW_SEQ_PREP_BLOCKS; q++) {
+    for (unsigned q = 0; q < SW_PREP_BLOCKS; q++) {
       perr |= pp[q].err;
       maxlen = std::max(maxlen, pp[q].maxlen);
       nnz_w += pp[q].nw;

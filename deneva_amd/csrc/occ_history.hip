@@ -126,7 +126,8 @@ static_assert(sizeof(FinLb) == 64, "one line per workgroup");
 struct FinTail {
   unsigned long long kmax;  // largest key appended (reset by the last workgroup)
   uint32_t done;            // finished workgroups (reset by the last one)
-  uint32_t pad[13];
+  uint32_t ticket;          // workgroups started (reset by the last one)
+  uint32_t pad[12];
 };
 static_assert(sizeof(FinTail) == 64, "one line");
 template <typename T>
@@ -215,15 +216,25 @@ __device__ inline void block_excl_scan2(uint32_t v0, uint32_t v1, uint32_t& e0, 
 __global__ __launch_bounds__(HB, 8) void k_fin(OccFinArgs a) {  // two workgroups per CU
   __shared__ unsigned long long s_mx;
   __shared__ uint64_t s_pre;
-  __shared__ uint32_t s_last;
+  __shared__ uint32_t s_last, s_id;
   const OccDyn* dy = a.dyn;
   const uint32_t tag = a.tag ? a.tag : dy->fin_tag;
   // the tail first: its place must not depend on the epoch's grid size
   FinTail* tail = (FinTail*)a.part;
   FinLb* lb = (FinLb*)(tail + 1);
+  // The workgroup's place in the scan is a ticket, not blockIdx: workgroups
+  // are dealt to the XCDs round-robin and each XCD dispatches its share as
+  // its own CUs free up, so workgroup b can run while b - 4 still waits for
+  // a slot -- held, when other kernels share the GPU, by workgroups that
+  // spin themselves (two key shards of one context on one GPU, or rank
+  // processes sharing it: the round-5/6 "numbered 339 txns" failures).  A
+  // ticket holder's predecessors all hold tickets, so all of them run.
+  if (threadIdx.x == 0) s_id = atomicAdd(&tail->ticket, 1u);
+  __syncthreads();
+  const uint32_t bid = s_id;
   // FIN_T consecutive txns per thread (one generation of workgroups fits the
   // chip: a workgroup's chain of round trips is paid once, not twice)
-  const uint64_t t_0 = ((uint64_t)blockIdx.x * HB + threadIdx.x) * FIN_T;
+  const uint64_t t_0 = ((uint64_t)bid * HB + threadIdx.x) * FIN_T;
   uint64_t* app_k = dy->app_k;
   uint64_t* app_t = dy->app_t;
   uint32_t c[FIN_T], w[FIN_T];
@@ -253,19 +264,19 @@ __global__ __launch_bounds__(HB, 8) void k_fin(OccFinArgs a) {  // two workgroup
     uint64_t P = 0;
     // the block's largest key before its publish (whose waitcnt orders it)
     if (lane == 0 && s_mx) atomicMax(&tail->kmax, s_mx);
-    if (blockIdx.x == 0) {
+    if (bid == 0) {
       if (lane == 0) fin_publish(&lb[0], tot, true, tag);
     } else {
-      if (lane == 0) fin_publish(&lb[blockIdx.x], tot, false, tag);
+      if (lane == 0) fin_publish(&lb[bid], tot, false, tag);
       bool timed_out = false;
-      for (int64_t hi = (a.var & 2u) ? -1 : (int64_t)blockIdx.x - 1; hi >= 0; hi -= 64) {
+      for (int64_t hi = (a.var & 2u) ? -1 : (int64_t)bid - 1; hi >= 0; hi -= 64) {
         const int64_t j = hi - (int64_t)lane;
         uint32_t stw = 0;
         if (j >= 0) {
-          uint32_t spins = 0;
+          const uint64_t t0 = spin_clock();
           while (((stw = fin_ld(&lb[j].status)) >> 2) != tag) {
             __builtin_amdgcn_s_sleep(1);
-            if (++spins > (1u << 24)) {  // dispatch is in index order: never in practice
+            if (spin_clock() - t0 > SPIN_TICKS) {  // dispatch is in index order: a hang, not a wait
               timed_out = true;
               break;
             }
@@ -283,7 +294,7 @@ __global__ __launch_bounds__(HB, 8) void k_fin(OccFinArgs a) {  // two workgroup
         P += v;
         if (im) break;
       }
-      if (lane == 0) fin_publish(&lb[blockIdx.x], P == ~0ull ? ~0ull : P + tot, true, tag);
+      if (lane == 0) fin_publish(&lb[bid], P == ~0ull ? ~0ull : P + tot, true, tag);
     }
     if (lane == 0) s_pre = P;
   }
@@ -336,6 +347,7 @@ __global__ __launch_bounds__(HB, 8) void k_fin(OccFinArgs a) {  // two workgroup
     a.totals[1] = g >> 32;
     a.totals[2] = atomicExch(&tail->kmax, 0ull);
     a.totals[3] = ins.hash ? atomicAdd(ins.over, 0u) : 0u;
+    fin_st(&tail->ticket, 0u);  // every workgroup took its ticket before it arrived
     fin_st(&tail->done, 0u);
   }
 }

@@ -325,22 +325,13 @@ struct SwSeqArgs {
   const uint32_t* abandon;
   uint32_t* err;
   uint64_t* dbg;          // per-tile clock stamps (DCC_SW_DEBUG) or null
-  // the epoch's batch validation (prep_body.h), run by workgroups 1.. of the
-  // level-0 launch beside the one-CU serial pass (prep_part null: none); it
-  // also writes every txn's has-write byte into `hasw`
-  const uint32_t* prep_off;
-  uint64_t prep_n;
-  const uint8_t* prep_at;
-  uint64_t prep_nnz;
-  PrepPart* prep_part;    // [SW_SEQ_PREP_BLOCKS] (pinned host memory)
   // read-only split: committed txns with a write are appended here (their
   // writes enter the writer table after the levels, k_sw_wall); null: none
   uint32_t* cw_list;
   uint32_t* cw_count;
-  uint4* wclear;          // level 0: the writer table, cleared by the prep workgroups
-  uint64_t wclear_n16;    // its size in 16-B words (0: none)
 };
-constexpr unsigned SW_SEQ_PREP_BLOCKS = 240;  // prep workgroups beside the level-0 serial pass
+// prep workgroups beside the level-0 committed-set listing (k_sw_cout)
+constexpr unsigned SW_PREP_BLOCKS = 1024;
 struct SwCoutArgs {
   SwList in;
   const uint32_t* aent;
@@ -354,6 +345,20 @@ struct SwCoutArgs {
   const uint32_t* m_dev;  // list length: with skip_done, a level whose serial
   uint32_t m_host;        // pass decided the whole list lists nothing (no
   int skip_done;          // filter follows)
+  uint32_t cout_grid;     // workgroups of the listing; the launch's others (level 0):
+  // the epoch's batch validation (prep_body.h) -- offsets, lengths, write
+  // count, and every txn's has-write byte into `hasw` (read first by the
+  // level-0 filter) -- on 0-LDS workgroups beside the listing rather than
+  // beside the serial pass, whose 160 KB of LDS made each of them hold a
+  // whole CU (prep_part null: none)
+  const uint32_t* prep_off;
+  uint64_t prep_n;
+  const uint8_t* prep_at;
+  uint64_t prep_nnz;
+  PrepPart* prep_part;    // [SW_PREP_BLOCKS] (pinned host memory)
+  uint8_t* hasw;
+  uint4* wclear;          // the writer table, cleared by the prep workgroups
+  uint64_t wclear_n16;    // its size in 16-B words (0: none)
 };
 // k_sw_filter / k_sw_scan / k_sw_compact (one argument block for the three)
 struct SwFilterArgs {

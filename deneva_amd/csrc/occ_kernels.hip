@@ -300,10 +300,10 @@ __device__ inline void grid_barrier(GridBar* b) {
     if (a == gridDim.x - 1) {
       __hip_atomic_store(&b->gen, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
-      unsigned spins = 0;
+      const uint64_t t0 = spin_clock();
       while (__hip_atomic_load(&b->gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
         __builtin_amdgcn_s_sleep(2);
-        if (++spins > (1u << 23)) {
+        if (spin_clock() - t0 > SPIN_TICKS / 10) {  // 2 s: a resident grid meets in microseconds
           __hip_atomic_store(&b->timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
         }

@@ -752,19 +752,6 @@ __global__ __launch_bounds__(SEQ_B) void k_sw_seq(SwSeqArgs a) {
     SwRec ring[SEQ_RING];
   };
   __shared__ __attribute__((aligned(16))) Lds L;
-  // workgroups 1.. (level 0 only): the batch validation pass on the CUs the
-  // serial pass leaves idle -- the host reads its partials after the epoch
-  if (blockIdx.x) {
-    prep_body_hasw(a.prep_off, a.prep_n, a.prep_at, a.prep_nnz, a.hasw, a.prep_part,
-                   blockIdx.x - 1, gridDim.x - 1);
-    // the epoch's committed-writer table, KEY_EMPTY-filled here (used only
-    // after the last level)
-    const uint4 e = make_uint4(~0u, ~0u, ~0u, ~0u);
-    for (uint64_t q = (uint64_t)(blockIdx.x - 1) * SEQ_B + threadIdx.x; q < a.wclear_n16;
-         q += (uint64_t)(gridDim.x - 1) * SEQ_B)
-      a.wclear[q] = e;
-    return;
-  }
   uint32_t* const cbits = L.cbits;
   uint32_t* const s_ready = L.s_ready;
   uint32_t &s_done = L.s_done, &s_stop = L.s_stop, &s_k = L.s_k;
@@ -1028,6 +1015,17 @@ __global__ __launch_bounds__(SEQ_B) void k_sw_seq(SwSeqArgs a) {
 __global__ __launch_bounds__(256) void k_sw_cout(SwCoutArgs a) {
   __shared__ uint32_t s_cnt[4];
   __shared__ uint32_t s_base;
+  // workgroups past the listing's (level 0 only): the batch validation pass
+  // -- the host reads its partials after the epoch -- and the clear of the
+  // epoch's committed-writer table (used only after the last level)
+  if (blockIdx.x >= a.cout_grid) {
+    const uint32_t b = blockIdx.x - a.cout_grid, nb = gridDim.x - a.cout_grid;
+    prep_body_hasw(a.prep_off, a.prep_n, a.prep_at, a.prep_nnz, a.hasw, a.prep_part, b, nb);
+    const uint4 e = make_uint4(~0u, ~0u, ~0u, ~0u);
+    for (uint64_t q = (uint64_t)b * 256 + threadIdx.x; q < a.wclear_n16; q += (uint64_t)nb * 256)
+      a.wclear[q] = e;
+    return;
+  }
   const uint32_t ab = *a.abandon;
   const uint32_t pos = a.lv->pos;
   const uint32_t m = list_len(a.m_dev, a.m_host);
@@ -1868,13 +1866,15 @@ void launch_sw_pre(const SwPreArgs& a, unsigned grid, hipStream_t st) {
   k_sw_pre<<<grid ? grid : 1u, PRE_B, 0, st>>>(a);
 }
 void launch_sw_seq(const SwSeqArgs& a, hipStream_t st) {
-  k_sw_seq<<<a.prep_part ? 1 + SW_SEQ_PREP_BLOCKS : 1, SEQ_B, 0, st>>>(a);
+  k_sw_seq<<<1, SEQ_B, 0, st>>>(a);
 }
 void launch_sw_rows(const SwPreArgs& a, unsigned grid, hipStream_t st) {
   k_sw_rows<<<grid ? grid : 1u, 256, 0, st>>>(a);  // one workgroup per tile
 }
-void launch_sw_cout(const SwCoutArgs& a, unsigned grid, hipStream_t st) {
-  k_sw_cout<<<grid ? grid : 1u, 256, 0, st>>>(a);
+void launch_sw_cout(const SwCoutArgs& a0, unsigned grid, hipStream_t st) {
+  SwCoutArgs a = a0;
+  a.cout_grid = grid ? grid : 1u;
+  k_sw_cout<<<a.cout_grid + (a.prep_part ? SW_PREP_BLOCKS : 0u), 256, 0, st>>>(a);
 }
 void launch_sw_filter(const SwFilterArgs& a, unsigned grid, hipStream_t st) {
   k_sw_filter<<<grid ? grid : 1u, SW_CHUNK, 0, st>>>(a);

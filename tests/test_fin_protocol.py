@@ -48,3 +48,24 @@ def test_fixed_policy_is_exact():
     for seed in range(200):
         tot, want, ok = fin_model.scenario("realloc", seed)
         assert tot == want and ok, seed
+
+
+def test_blockidx_lookback_can_deadlock_when_launches_share_the_gpu():
+    """The cause of the round-5/6 totals mismatches (the round-6 diagnostic:
+    a workgroup's look-back timed out with every word published by the end):
+    two look-back launches sharing the GPU, each workgroup's scan position
+    its blockIdx.  Workgroups are dealt round-robin to the XCDs; a workgroup
+    whose predecessor is still waiting for a slot on another XCD -- held by
+    the other launch's spinning workgroups -- waits forever (the bounded
+    spin then fails the epoch)."""
+    outcomes = {fin_model.dispatch_model("blockidx", s) for s in range(300)}
+    assert "deadlock" in outcomes
+
+
+def test_ticket_lookback_never_deadlocks():
+    """The fix: a workgroup's scan position is a ticket taken when it starts,
+    so all its predecessors have started (and published) -- every schedule
+    completes, also with more launches than the slots can hold at once."""
+    for s in range(300):
+        assert fin_model.dispatch_model("ticket", s) == "done", s
+        assert fin_model.dispatch_model("ticket", s, launches=3, grid=20) == "done", s

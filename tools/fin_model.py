@@ -106,3 +106,61 @@ def scenario(policy, seed, small=6, big=40):
     counts = [rng.randrange(0, 5) for _ in range(big)]
     tot, pre = run_launch(B, counts, 2, seed + 2)
     return tot, sum(counts), pre == [sum(counts[:b]) for b in range(big)]
+
+
+def dispatch_model(order, seed, xcds=4, slots=2, grid=12, launches=2):
+    """Several k_fin launches sharing one GPU (key shards of one context, or
+    rank processes): workgroup b of each launch is dealt to XCD b % xcds,
+    each XCD dispatches its share in b order as its `slots` free up, in any
+    interleaving between the launches.  A running workgroup has published
+    its aggregate; it finishes (publishes inclusive, frees its slot) once its
+    look-back sees every predecessor's status down to the nearest inclusive
+    one.  `order`: "blockidx" (the scan position is blockIdx, round 5) or
+    "ticket" (the position is the order in which workgroups started: the
+    fix).  Returns "done" or "deadlock" (no workgroup can start or finish)."""
+    rng = random.Random(seed)
+    pend = [[[b for b in range(grid) if b % xcds == x] for x in range(xcds)] for _ in range(launches)]
+    free = [slots] * xcds
+    status = [[0] * grid for _ in range(launches)]  # 0 none, 1 aggregate, 2 inclusive
+    running = []  # (launch, position, xcd)
+    tickets = [0] * launches
+    done = 0
+    while done < launches * grid:
+        acts = []
+        for L in range(launches):
+            for x in range(xcds):
+                if pend[L][x] and free[x] > 0:
+                    acts.append(("start", L, x))
+        for k, (L, p, x) in enumerate(running):
+            j = p - 1
+            ok = True
+            while j >= 0:
+                if status[L][j] == 0:
+                    ok = False
+                    break
+                if status[L][j] == 2:
+                    break
+                j -= 1
+            if ok:
+                acts.append(("finish", k))
+        if not acts:
+            return "deadlock"
+        a = rng.choice(acts)
+        if a[0] == "start":
+            _, L, x = a
+            b = pend[L][x].pop(0)
+            free[x] -= 1
+            p = b if order == "blockidx" else tickets[L]
+            tickets[L] += 1
+            status[L][p] = 2 if p == 0 else 1
+            if p == 0:  # workgroup 0 publishes its inclusive value and is done
+                free[x] += 1
+                done += 1
+            else:
+                running.append((L, p, x))
+        else:
+            L, p, x = running.pop(a[1])
+            status[L][p] = 2
+            free[x] += 1
+            done += 1
+    return "done"
