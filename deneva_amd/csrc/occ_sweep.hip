@@ -1800,24 +1800,60 @@ __global__ __launch_bounds__(SW_CHUNK) void k_sw_compact(SwFilterArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// k_sw_ro: the read-only txns level 0 split off, 16 lanes per txn (a lane per
-// access, then every 16th): a key whose committed writer precedes the txn
-// kills it.  Read-only txns never kill or block anyone, so each is decided
-// alone once every writer is.
+// k_sw_ro: the read-only txns level 0 split off, 4 lanes per txn, each lane
+// four accesses per step (accesses sl, sl + 4, sl + 8, sl + 12 of the step)
+// with their key loads and first probes in flight together: a key whose
+// committed writer precedes the txn kills it.  Read-only txns never kill or
+// block anyone, so each is decided alone once every writer is.  (Round 5 ran
+// 16 lanes per txn, one access each: twice the waves for the same probes,
+// ~12 us of the whole chip per headline epoch.)
 __global__ __launch_bounds__(256) void k_sw_ro(SwRoArgs a) {
   const uint32_t cnt = *a.ro_count;
-  const uint32_t lane = lane_id(), g = lane >> 4, sl = lane & 15u;
-  const uint32_t ng = gridDim.x * 16;
-  for (uint32_t i = (blockIdx.x * 256 + threadIdx.x) >> 4; i < cnt; i += ng) {
+  const uint32_t lane = lane_id(), g = lane >> 2, sl = lane & 3u;
+  const uint32_t ng = gridDim.x * 64;
+  const uint32_t mask = (1u << a.wt.bits) - 1u;
+  for (uint32_t i = (blockIdx.x * 256 + threadIdx.x) >> 2; i < cnt; i += ng) {
     uint4 r = *(const uint4*)&a.ro[i];  // tid, first access, end
     if (a.full_off) {  // key-sharded: the txn's accesses in the whole batch
       r.y = a.full_off[r.x];
       r.z = a.full_off[r.x + 1];
     }
     bool kill = false;
-    for (uint32_t x = r.y + sl; x < r.z && !kill; x += 16) kill = wt_find(a.wt, a.keys[x]) < r.x;
+    for (uint32_t x0 = r.y + sl; x0 < r.z && !kill; x0 += 16) {
+      uint64_t k[4];
+      bool in[4];
+#pragma unroll
+      for (uint32_t u = 0; u < 4; u++) {
+        in[u] = x0 + 4 * u < r.z;
+        k[u] = in[u] ? a.keys[x0 + 4 * u] : KEY_EMPTY;
+      }
+      uint32_t sv[4];
+      uint4 v[4];
+#pragma unroll
+      for (uint32_t u = 0; u < 4; u++) {
+        sv[u] = sw_hash(k[u], a.wt.bits);
+        v[u] = in[u] ? *(const uint4*)&a.wt.slot[sv[u]] : make_uint4(~0u, ~0u, ~0u, ~0u);
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < 4; u++) {
+        if (!in[u]) continue;
+        // the first slot was loaded above; the rest of the probe sequence
+        // (rare at the table's ~10 % load) as wt_find walks it
+        uint32_t q = 0, s0 = sv[u];
+        for (;;) {
+          const uint64_t kk = ((uint64_t)v[u].y << 32) | v[u].x;
+          if (kk == k[u]) {
+            kill |= v[u].z < r.x;
+            break;
+          }
+          if (kk == KEY_EMPTY || ++q >= a.wt.probes) break;
+          s0 = (s0 + 1) & mask;
+          v[u] = *(const uint4*)&a.wt.slot[s0];
+        }
+      }
+    }
     const uint64_t b = ballot64(kill);
-    if (sl == 0) a.state[r.x] = ((b >> (16 * g)) & 0xFFFFull) ? ST_ABORT : ST_COMMIT;
+    if (sl == 0) a.state[r.x] = ((b >> (4 * g)) & 0xFull) ? ST_ABORT : ST_COMMIT;
   }
 }
 
