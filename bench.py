@@ -62,7 +62,7 @@ def parse():
                          "N ranks (BASELINE config C5 with --theta 0.99 --seed 0xD3E7A002); "
                          "default is weak scaling (N x --txns txns)")
     ap.add_argument("--pmc", default=next((p for p in (os.path.join(ROOT, "profiles", r, "pmc.json")
-                                                       for r in ("r05", "r04")) if os.path.exists(p)),
+                                                       for r in ("r06", "r05", "r04")) if os.path.exists(p)),
                                           os.path.join(ROOT, "profiles", "r05", "pmc.json")),
                     help="PMC summary (tools/gpu_pmc_r05.sh -> tools/pmc_r05.py) the "
                          "roofline.traffic / l2_hit fields and each config's pmc block are read "
