@@ -321,6 +321,9 @@ int dcc_multi_occ_epoch(dcc_ctx* ctx, const dcc_batch* b, uint8_t* out_rc, uint6
 int dcc_multi_calvin_epoch(dcc_ctx* ctx, const dcc_batch* b, const dcc_calvin_held* held,
                            uint32_t* out_group, uint8_t* out_rc, uint32_t* out_wave, dcc_stats* st);
 int dcc_multi_each(dcc_ctx* ctx, int (*fn)(dcc_ctx*, void*), void* user);
+int dcc_multi_occ_snapshot(dcc_ctx* ctx, const dcc_batch* b, const dcc_occ_snapshot* snap,
+                           uint8_t* out_rc, dcc_stats* st);
+dcc_ctx* dcc_multi_rank0(dcc_ctx* ctx);  // rank 0's sub-context, its device selected
 // pipelined epochs (occ_pipe.cpp): complete every epoch in flight / tear down
 void dcc_pipe_drain(dcc_ctx* ctx);
 void dcc_pipe_destroy(dcc_ctx* ctx);

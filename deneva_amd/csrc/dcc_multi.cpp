@@ -362,18 +362,33 @@ int dcc_multi_calvin_epoch(dcc_ctx* ctx, const dcc_batch* b, const dcc_calvin_he
   if (held && held->n && (!held->keys || !held->acctype))
     return ctx->fail(DCC_EINVAL, "calvin: null held arrays");
   const bool dev = (b->flags & DCC_DEVICE_PTRS) != 0;
-  if (dev && held && held->n)
-    return ctx->fail(DCC_ENOTSUP, "multi-GPU calvin: held rows with host arrays only");
   const uint64_t n = b->n_txn;
   const int R = (int)ctx->multi->sub.size();
-  // the held prefix is sharded by row as well (host)
+  // the held prefix is sharded by row as well, on the host: with a device
+  // batch its arrays are device arrays too (dcc.h), read back first (a few
+  // requests per still-locked row, against the epoch's millions)
+  std::vector<uint64_t> hkeys_h;
+  std::vector<uint8_t> hat_h;
+  const uint64_t* hkeys = held ? held->keys : nullptr;
+  const uint8_t* hat = held ? held->acctype : nullptr;
+  if (dev && held && held->n) {
+    hkeys_h.resize(held->n);
+    hat_h.resize(held->n);
+    if (hipMemcpy(hkeys_h.data(), held->keys, held->n * 8, hipMemcpyDefault) != hipSuccess ||
+        hipMemcpy(hat_h.data(), held->acctype, held->n, hipMemcpyDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      return ctx->fail(DCC_EINVAL, "multi-GPU calvin: held arrays unreadable as device arrays");
+    }
+    hkeys = hkeys_h.data();
+    hat = hat_h.data();
+  }
   std::vector<std::vector<uint64_t>> hk(R);
   std::vector<std::vector<uint8_t>> ha(R);
   if (held)
     for (uint64_t i = 0; i < held->n; i++) {
-      const int r = (int)dcc_key_shard(held->keys[i], (uint32_t)R);
-      hk[r].push_back(held->keys[i]);
-      ha[r].push_back(held->acctype[i]);
+      const int r = (int)dcc_key_shard(hkeys[i], (uint32_t)R);
+      hk[r].push_back(hkeys[i]);
+      ha[r].push_back(hat[i]);
     }
   std::vector<std::vector<uint8_t>> rc(R);
   std::vector<std::vector<uint32_t>> grp(R), src(R);
@@ -439,6 +454,123 @@ int dcc_multi_calvin_epoch(dcc_ctx* ctx, const dcc_batch* b, const dcc_calvin_he
     st->alg_bytes = dcc_calvin_alg_bytes(n, b->nnz, b->order != nullptr, 0);
   }
   return DCC_OK;
+}
+
+// Captured-snapshot validation (occ_snapshot.hip) key-sharded: a txn's
+// decision is an OR over its accesses -- a history pair of a key it read, a
+// captured active write set meeting one of its keys (occ.cpp:167-199) -- and
+// every such meeting is between accesses of one key, so each rank decides its
+// key shard against its own history shard and the captured lists (txn
+// indices of the whole batch), and a txn commits iff it commits on every
+// rank.  The snapshot arrays go to every rank's GPU beside its shard.
+int dcc_multi_occ_snapshot(dcc_ctx* ctx, const dcc_batch* b, const dcc_occ_snapshot* snap,
+                           uint8_t* out_rc, dcc_stats* st) {
+  if (!b) return ctx->fail(DCC_EINVAL, "null batch");
+  if (!snap || !snap->active_off) return ctx->fail(DCC_EINVAL, "snapshot: null snapshot or active_off");
+  if (int e = ctx->check_batch(b)) return e;
+  if (int e = multi_check_device_batch(ctx, b)) return e;
+  const bool dev = (b->flags & DCC_DEVICE_PTRS) != 0;
+  if (dev && !snap->active_idx)
+    return ctx->fail(DCC_EINVAL, "snapshot: device capture needs active_idx (a 1-element buffer "
+                                 "when every list is empty)");
+  const uint64_t n = b->n_txn;
+  dcc_stats S0{};
+  S0.n_shards = (uint32_t)dcc_multi_size(ctx);
+  if (n == 0) {
+    if (st) *st = S0;
+    return DCC_OK;
+  }
+  if (!out_rc) return ctx->fail(DCC_EINVAL, "snapshot: null out_rc");
+  // a host capture: the structural checks of the one-GPU path, then its
+  // arrays to every GPU (the shards are device batches)
+  uint64_t n_active = 0;
+  if (!dev) {
+    const uint32_t* ao = snap->active_off;
+    if (ao[0] != 0) return ctx->fail(DCC_EINVAL, "snapshot: active_off[0] must be 0");
+    for (uint64_t t = 0; t < n; t++)
+      if (ao[t + 1] < ao[t])
+        return ctx->fail(DCC_EINVAL, "snapshot: active_off decreases at txn %llu", (unsigned long long)t);
+    n_active = ao[n];
+    if (n_active && !snap->active_idx) return ctx->fail(DCC_EINVAL, "snapshot: null active_idx");
+    for (uint64_t q = 0; q < n_active; q++)
+      if (snap->active_idx[q] >= n)
+        return ctx->fail(DCC_EINVAL, "snapshot: active_idx[%llu] = %u >= n_txn", (unsigned long long)q,
+                         snap->active_idx[q]);
+  }
+  const int R = (int)ctx->multi->sub.size();
+  std::vector<std::vector<uint8_t>> rc(R);
+  std::vector<dcc_stats> S(R);
+  const int e = run_ranks(ctx, [&](int r, dcc_ctx* s) -> int {
+    dcc_batch sb;
+    int x = s->shard_stage(b, (uint32_t)r, (uint32_t)R, sb);
+    if (x != DCC_OK) return x;
+    dcc_occ_snapshot ds = *snap;
+    if (!dev) {
+      if ((x = s->snap_aoff.ensure(s, (n + 1) * 4, "snapshot active_off")) != DCC_OK ||
+          (x = s->snap_aidx.ensure(s, std::max<uint64_t>(16, n_active * 4), "snapshot active_idx")) != DCC_OK)
+        return x;
+      hipError_t he = hipMemcpy(s->snap_aoff.p, snap->active_off, (n + 1) * 4, hipMemcpyHostToDevice);
+      if (he == hipSuccess && n_active)
+        he = hipMemcpy(s->snap_aidx.p, snap->active_idx, n_active * 4, hipMemcpyHostToDevice);
+      if (he == hipSuccess && snap->hist_top) {
+        if ((x = s->snap_top.ensure(s, n * 8, "snapshot hist_top")) != DCC_OK) return x;
+        he = hipMemcpy(s->snap_top.p, snap->hist_top, n * 8, hipMemcpyHostToDevice);
+      }
+      if (he != hipSuccess) return s->hip_fail(he, "multi-GPU snapshot: capture in");
+      ds.active_off = (const uint32_t*)s->snap_aoff.p;
+      ds.active_idx = (const uint32_t*)s->snap_aidx.p;
+      ds.hist_top = snap->hist_top ? (const uint64_t*)s->snap_top.p : nullptr;
+    }
+    if ((x = s->sh_rc.ensure(s, n + 16, "shard rc")) != DCC_OK) return x;
+    // the shard's decisions alone (no collective: the ranks are combined below)
+    dcc_comm_state* const cm = s->comm;
+    s->comm = nullptr;
+    x = s->occ_snapshot(&sb, &ds, (uint8_t*)s->sh_rc.p, &S[r]);
+    s->comm = cm;
+    if (x != DCC_OK) return x;
+    rc[r].resize(n);
+    const hipError_t he = hipMemcpy(rc[r].data(), s->sh_rc.p, n, hipMemcpyDeviceToHost);
+    return he == hipSuccess ? DCC_OK : s->hip_fail(he, "multi-GPU snapshot: decisions out");
+  });
+  if (e != DCC_OK) return e;
+  // a txn aborts if any rank aborts it (DCC_RC_ABORT > DCC_RC_RCOK)
+  std::vector<uint8_t> fin(rc[0]);
+  for (int r = 1; r < R; r++)
+    for (uint64_t t = 0; t < n; t++) fin[t] = std::max(fin[t], rc[r][t]);
+  if (dev) {
+    if (hipMemcpy(out_rc, fin.data(), n, hipMemcpyHostToDevice) != hipSuccess)
+      return ctx->hip_fail(hipGetLastError(), "multi-GPU snapshot: decisions to the caller");
+  } else {
+    memcpy(out_rc, fin.data(), n);
+  }
+  if (st) {
+    dcc_stats T = S0;
+    for (int r = 0; r < R; r++) {
+      T.device_ms = std::max(T.device_ms, S[r].device_ms);
+      T.nnz_w += S[r].nnz_w;
+      T.alg_bytes += S[r].alg_bytes;
+    }
+    for (uint64_t t = 0; t < n; t++) (fin[t] == DCC_RC_RCOK ? T.n_commit : T.n_abort)++;
+    if (!dev) {  // read-only txns of the whole batch (a rank sees only its shard)
+      for (uint64_t t = 0; t < n; t++) {
+        bool w = false;
+        for (uint32_t x = b->offsets[t]; x < b->offsets[t + 1] && !w; x++) w = b->acctype[x] == DCC_WR;
+        T.n_readonly += w ? 0 : 1;
+      }
+    }
+    *st = T;
+  }
+  return DCC_OK;
+}
+
+// MaaT on a multi-GPU context: the whole epoch on rank 0's GPU, whose row
+// table holds every row's timestamps (the bounds of a txn combine every row
+// it touches; a key-sharded MaaT would all-reduce a txn's lower and upper
+// bound per round -- a u64 max and min -- not built).
+dcc_ctx* dcc_multi_rank0(dcc_ctx* ctx) {
+  dcc_ctx* s = ctx->multi->sub[0];
+  (void)hipSetDevice(s->device);
+  return s;
 }
 
 // per-rank state kept identical on every rank (options, tnc, history)

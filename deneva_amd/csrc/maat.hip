@@ -1492,14 +1492,22 @@ extern "C" uint64_t dcc_maat_alg_bytes(uint64_t n_txn, uint64_t nnz) {
 extern "C" int dcc_maat_validate_epoch(dcc_ctx* ctx, const dcc_batch* batch, uint8_t* out_rc,
                                        uint64_t* out_commit_ts, dcc_stats* out_stats) {
   if (!ctx) return DCC_EINVAL;
-  if (ctx->multi) return ctx->fail(DCC_ENOTSUP, "maat: single-GPU engine");
+  if (ctx->multi) {  // the whole epoch on rank 0 (dcc_multi.cpp)
+    dcc_ctx* s = dcc_multi_rank0(ctx);
+    dcc_comm_state* const cm = s->comm;  // one GPU's engine: no collective
+    s->comm = nullptr;
+    const int e = s->maat_epoch(batch, out_rc, out_commit_ts, out_stats);
+    s->comm = cm;
+    if (e != DCC_OK) ctx->last_error = s->last_error;
+    return e;
+  }
   if (hipSetDevice(ctx->device) != hipSuccess) return DCC_ENODEV;
   return ctx->maat_epoch(batch, out_rc, out_commit_ts, out_stats);
 }
 
 extern "C" int dcc_maat_rows_clear(dcc_ctx* ctx) {
   if (!ctx) return DCC_EINVAL;
-  if (ctx->multi) return ctx->fail(DCC_ENOTSUP, "maat: single-GPU engine");
+  if (ctx->multi) return dcc_maat_rows_clear(dcc_multi_rank0(ctx));
   if (hipSetDevice(ctx->device) != hipSuccess) return DCC_ENODEV;
   if (ctx->mt_bits) {
     const uint64_t cap = 1ull << ctx->mt_bits;
@@ -1514,7 +1522,7 @@ extern "C" int dcc_maat_rows_clear(dcc_ctx* ctx) {
 extern "C" int dcc_maat_rows_set(dcc_ctx* ctx, const uint64_t* keys, const uint64_t* last_read,
                                  const uint64_t* last_write, uint64_t n) {
   if (!ctx || (n && (!keys || !last_read || !last_write))) return DCC_EINVAL;
-  if (ctx->multi) return ctx->fail(DCC_ENOTSUP, "maat: single-GPU engine");
+  if (ctx->multi) return dcc_maat_rows_set(dcc_multi_rank0(ctx), keys, last_read, last_write, n);
   if (n == 0) return DCC_OK;
   if (hipSetDevice(ctx->device) != hipSuccess) return DCC_ENODEV;
   CR(ctx->mt_misc.ensure(ctx, 64 + MT_RING * 4, "maat counters"));
@@ -1545,7 +1553,7 @@ extern "C" int dcc_maat_rows_set(dcc_ctx* ctx, const uint64_t* keys, const uint6
 extern "C" int dcc_maat_rows_get(dcc_ctx* ctx, const uint64_t* keys, uint64_t* last_read,
                                  uint64_t* last_write, uint64_t n) {
   if (!ctx || (n && (!keys || !last_read || !last_write))) return DCC_EINVAL;
-  if (ctx->multi) return ctx->fail(DCC_ENOTSUP, "maat: single-GPU engine");
+  if (ctx->multi) return dcc_maat_rows_get(dcc_multi_rank0(ctx), keys, last_read, last_write, n);
   if (n == 0) return DCC_OK;
   if (hipSetDevice(ctx->device) != hipSuccess) return DCC_ENODEV;
   if (!ctx->mt_bits) {
@@ -1567,4 +1575,7 @@ extern "C" int dcc_maat_rows_get(dcc_ctx* ctx, const uint64_t* keys, uint64_t* l
   return DCC_OK;
 }
 
-extern "C" uint64_t dcc_maat_rows_size(const dcc_ctx* ctx) { return ctx ? ctx->mt_rows : 0; }
+extern "C" uint64_t dcc_maat_rows_size(const dcc_ctx* ctx) {
+  if (ctx && ctx->multi) return dcc_multi_sub((dcc_ctx*)ctx, 0)->mt_rows;
+  return ctx ? ctx->mt_rows : 0;
+}

@@ -428,7 +428,7 @@ extern "C" int dcc_occ_validate_snapshot(dcc_ctx* ctx, const dcc_batch* batch,
                                          const dcc_occ_snapshot* snap, uint8_t* out_rc,
                                          dcc_stats* out_stats) {
   if (!ctx) return DCC_EINVAL;
-  if (ctx->multi) return ctx->fail(DCC_ENOTSUP, "snapshot validation is single-GPU");
+  if (ctx->multi) return dcc_multi_occ_snapshot(ctx, batch, snap, out_rc, out_stats);
   if (hipSetDevice(ctx->device) != hipSuccess) return DCC_ENODEV;
   return ctx->occ_snapshot(batch, snap, out_rc, out_stats);
 }

@@ -157,10 +157,12 @@ int dcc_init(dcc_ctx** out, int device_id);
  * is copied to every GPU; a device batch, DCC_DEVICE_PTRS, is read where it
  * lies -- peer access between distinct GPUs is enabled here).  OCC and Calvin
  * epochs return the same decisions as one GPU (device outputs are written by
- * rank 0); options, tnc and history apply to every shard.  Calvin wave
- * levels run the whole epoch on rank 0's GPU (they chain through every row).
- * Snapshot validation, MaaT, held rows with a device batch and
- * dcc_set_stream are DCC_ENOTSUP on it. */
+ * rank 0); options, tnc and history apply to every shard.  Captured-snapshot
+ * validation is key-sharded too (each rank against its history shard; a txn
+ * commits iff every rank commits it).  Calvin wave levels and MaaT run the
+ * whole epoch on rank 0's GPU (the levels chain through every row; MaaT's
+ * bounds combine every row of a txn; its row table lives on rank 0).
+ * dcc_set_stream is DCC_ENOTSUP on it. */
 int dcc_init_multi(dcc_ctx** out, int n_gpus, const int* device_ids);
 void dcc_destroy(dcc_ctx* ctx);
 const char* dcc_strerror(int code);

@@ -68,11 +68,77 @@ def test_multi_history_and_calvin():
         assert np.array_equal(np.asarray(crc), erc2)
 
 
-def test_multi_rejects_maat():
-    b = d.gen_ycsb(n_txn=1000, zipf_theta=0.9)
-    with d.Engine(devices=[0, 0]) as eng:
-        with pytest.raises(d.DccError):
-            eng.maat_validate_epoch(b)
+@pytest.mark.parametrize("dev", [False, True])
+def test_multi_maat_on_rank0(dev):
+    """MaaT on a multi-GPU context runs the whole epoch on rank 0 (its row
+    table holds every row's timestamps): rc, commit timestamps and the row
+    timestamps equal the oracle's, across two epochs."""
+    with d.Engine(devices=[0, 0, 0]) as eng:
+        eng.maat_rows_clear()
+        rk = lr = lw = None
+        for e in range(2):
+            b = d.gen_ycsb(n_txn=20000, zipf_theta=0.9, table_size=1 << 15, seed=0x3A0 + e)
+            bb = b.to_torch("cuda:0") if dev else b
+            rc, cts, _ = eng.maat_validate_epoch(bb)
+            if dev:
+                rc, cts = rc.cpu().numpy(), cts.cpu().numpy().view(np.uint64)
+            erc, ects, (rk, lr, lw) = orc.maat(b, rk, lr, lw)
+            assert np.array_equal(np.asarray(rc), erc), f"epoch {e}"
+            assert np.array_equal(np.asarray(cts, np.uint64), ects), f"epoch {e}"
+            glr, glw = eng.maat_rows_get(rk)
+            assert np.array_equal(glr, lr) and np.array_equal(glw, lw)
+        assert eng.maat_rows_size == rk.size
+
+
+@pytest.mark.parametrize("dev", [False, True])
+def test_multi_snapshot_key_sharded(dev):
+    """Captured-snapshot validation on a multi-GPU context: each rank decides
+    its key shard against its history shard (the history is sharded by key,
+    dcc_occ_history_append) and the captured active lists; a txn commits iff
+    every rank commits it -- equal to the literal snapshot oracle."""
+    import torch
+    from test_snapshot_oracle import live_case
+    hist0 = [(tn, [int(k) for k in np.random.default_rng(3).integers(0, 200, 3)]) for tn in range(1, 41)]
+    b, cap = live_case(2, n=2000, threads=16, hist0=hist0, tnc0=40)
+    want = orc.occ_snapshot(b, cap["active_off"], cap["active_idx"], cap["hist_top"], cap["hist_keys"],
+                            cap["hist_tn"])
+    assert np.array_equal(want, cap["rc"])
+    with d.Engine(devices=[0, 0, 0]) as eng:
+        eng.history_clear()
+        eng.history_append(cap["hist_keys"], cap["hist_tn"])
+        if dev:
+            cv = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(
+                np.int64 if a.dtype == np.uint64 else np.int32)).cuda()
+            aidx = cap["active_idx"]
+            rc, st = eng.occ_validate_snapshot(b.to_torch(), cv(cap["active_off"]),
+                                               cv(aidx) if len(aidx) else torch.zeros(1, dtype=torch.int32,
+                                                                                      device="cuda"),
+                                               cv(cap["hist_top"]))
+            rc = rc.cpu().numpy()
+        else:
+            rc, st = eng.occ_validate_snapshot(b, cap["active_off"], cap["active_idx"], cap["hist_top"])
+            rc = np.asarray(rc)
+        assert np.array_equal(rc, want)
+        assert st["n_commit"] == int((want == 0).sum()) and st["n_shards"] == 3
+        eng.history_clear()
+
+
+def test_multi_calvin_held_device_batch():
+    """Held rows with a device batch on a multi-GPU context (the held arrays
+    are device arrays too): sharded by row like the host form, equal to the
+    literal Row_lock replay of the held prefix then the epoch."""
+    import torch
+    c = d.gen_ycsb(n_txn=50000, zipf_theta=0.9, part_cnt=4, chunk_txns=4096, seed=0x4E1D)
+    c.order = np.random.default_rng(9).integers(0, 1 << 20, size=c.n_txn).astype(np.uint64)
+    hk = np.asarray(c.keys[:3000], np.uint64)
+    ha = np.where(np.arange(3000) % 3 == 0, WR, RD).astype(np.uint8)
+    eg, erc = orc.calvin_held(c, hk, ha)
+    dh = (torch.from_numpy(hk.view(np.int64)).cuda(), torch.from_numpy(ha).cuda())
+    with d.Engine(devices=[0, 0, 0]) as eng:
+        g, rc, _, _ = eng.calvin_order_epoch(c.to_torch("cuda:0"), want_group=True, held=dh)
+        torch.cuda.synchronize()
+        assert np.array_equal(g.cpu().numpy().view(np.uint32), eg)
+        assert np.array_equal(rc.cpu().numpy(), erc)
 
 
 @pytest.mark.parametrize("shards", [2, 4])
