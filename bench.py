@@ -486,6 +486,59 @@ def pipe_fin_config(eng, dev, timed, orc, tag="PIPE_FIN", n=1 << 20, lanes=4, k=
                     "cannot overlap (each window needs the epoch before it finished): see HIST / SHIM"}
 
 
+def shim_pipe_config(eng, dev, timed, orc, tag="SHIM_PIPE", n=1 << 20, lanes=4, k=24):
+    """The shim's transfer form through the pipeline: what OccEpoch
+    (deneva_amd/csrc/host/occ_epoch.h, Options::depth = 4) hands the engine
+    under the reference's default TS_CLOCK -- HOST arrays in the compact
+    pinned form (u32 keys, 2-bit access types), commit tn and the history
+    append (central_finish) -- submitted with dcc_occ_submit_epoch, `lanes`
+    epochs in flight: each lane's H2D copy overlaps the other lanes' kernels.
+    Wall time per epoch over k epochs; each lane's last epoch's rc and tn
+    checked against the oracle (tn shifted by the tnc before the epoch)."""
+    import torch
+    import deneva_amd as d
+    from collections import deque
+    b = d.gen_ycsb(n_txn=n, zipf_theta=0.9, seed=0xD3E7A00E)
+    cb = eng.compact_host_batch(b)
+    erc, etn, ecw = orc.occ(b)
+    rcs = [eng.host_empty(n, np.uint8) for _ in range(lanes)]
+    tns = [eng.host_empty(n, np.uint64) for _ in range(lanes)]
+    eng.set_option(d._abi.OPT_PIPELINE, lanes)
+
+    def stream(kk):
+        eng.history_clear()
+        eng.tnc = 0
+        fl = deque()
+        for i in range(kk):
+            fl.append(eng.occ_submit_epoch(cb, rcs[i % lanes], tns[i % lanes], append_history=True))
+            if len(fl) >= lanes:
+                eng.occ_wait_epoch(fl.popleft())
+        while fl:
+            eng.occ_wait_epoch(fl.popleft())
+
+    stream(2 * lanes)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    stream(k)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / k
+    par = eng.tnc == k * ecw
+    for i in range(k - lanes, k):
+        want = np.where(etn != 0, etn + np.uint64(i * ecw), np.uint64(0))
+        par = par and np.array_equal(np.asarray(rcs[i % lanes]), erc)
+        par = par and np.array_equal(np.asarray(tns[i % lanes]), want)
+    h2d = sum(int(np.asarray(a).nbytes) for a in (cb.offsets, cb.keys, cb.acctype))
+    eng.history_clear()
+    eng.tnc = 0
+    return {"workload": f"{k} consecutive OCC epochs of {n} YCSB txns x 16 keys (theta=0.9) from pinned "
+                        f"host arrays in the shim's compact form, {lanes} epochs in flight, commit tn + "
+                        f"history append (central_finish under TS_CLOCK)",
+            "txns_per_s": n / dt, "ms_per_epoch": dt * 1e3, "h2d_MB": h2d / 1e6,
+            "h2d_GBps_effective": h2d / dt / 1e9,
+            "parity_vs_oracle": bool(par),
+            "parity_scope": "rc and tn of each lane's last epoch, tnc after the stream"}
+
+
 def _pcie_h2d_GBps(nbytes):
     """The link: a pinned host -> device copy of nbytes (torch, median of 5)."""
     import torch
@@ -599,7 +652,8 @@ def shim_config(eng, dev, timed, orc, tag="SHIM", n=1 << 20, steps=6):
 
 CONFIGS = {"C2": occ_config, "C3": occ_config, "C5": occ_config, "C4": calvin_config,
            "C4_SHUF": calvin_config,
-           "C6": None, "HIST": history_config, "SHIM": shim_config, "PIPE_FIN": pipe_fin_config,
+           "C6": None, "HIST": history_config, "SHIM": shim_config, "SHIM_PIPE": shim_pipe_config,
+           "PIPE_FIN": pipe_fin_config,
            "MAAT_C2": maat_config,
            "MAAT_1M": maat_config}
 

@@ -107,6 +107,8 @@ struct dcc_ctx {
   uint32_t wt_bits = 18;          // committed-writer table slots (WT_BITS_DEFAULT; grows after an overflow)
   uint32_t wf_bits = 0;           // fallback table (k_sw_wall) slots
   uint32_t sw_levels = 0;          // DCC_OPT_SWEEP_LEVELS (0: auto)
+  uint32_t sw_mode = 1;            // this epoch's level schedule (occ_driver.hip sw_pmax)
+  uint32_t sw_l1_last = ~0u;       // level-1 list length of the last one-GPU split epoch
   bool sw_debug = false;        // DCC_SW_DEBUG: per-tile clock stamps of the serial pass       // sweep levels enqueued between host synchronisations
   hipEvent_t pev[8] = {};  // phase boundary events (profiling only)
   std::string last_error;

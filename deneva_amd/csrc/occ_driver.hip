@@ -275,8 +275,11 @@ static constexpr uint32_t SW_PMAX_TOP = 65536;
 // the serial prefixes per level: 1,024 txns at level 0; with the read-only
 // split (lists of write txns only after level 0) 3,072 and 8,192 next, so the
 // headline epoch ends in three levels (tools/sweep_model.py, measured A/B in
-// DESIGN.md §3); without it 1,024 << level
-static uint32_t sw_pmax(int level, bool split) {
+// DESIGN.md §3); without it 1,024 << level.  mode: 0 no split, 1 split (three
+// levels per graph), 2 split with two levels per graph -- level 1 a serial
+// tail of 8,192, for epochs whose level-1 list fits it (C2, C3: the last
+// epoch's list decides, dcc_ctx::sw_l1_last)
+static uint32_t sw_pmax(int level, int mode) {
   // DCC_SW_PMAX="p0,p1,...": per-level serial prefixes (tuning experiments)
   static const std::vector<uint32_t> ov = [] {
     std::vector<uint32_t> v;
@@ -291,7 +294,11 @@ static uint32_t sw_pmax(int level, bool split) {
     return v;
   }();
   if (level < (int)ov.size()) return ov[level];
-  if (split) {
+  if (mode == 2) {
+    if (level == 0) return 1024u;
+    return level >= 4 ? SW_PMAX_TOP : (8192u << (level - 1));
+  }
+  if (mode) {
     if (level == 0) return 1024u;
     if (level == 1) return 3072u;
     return level >= 5 ? SW_PMAX_TOP : (8192u << (level - 2));
@@ -301,23 +308,23 @@ static uint32_t sw_pmax(int level, bool split) {
 static size_t sw_ctl_bytes() { return (SW_MAX_LEVEL + 2) * sizeof(SwLevel) + 64; }
 // the access budget of a level's serial range: a quarter of the smallest
 // table with four slots per access of p_max 16-access txns
-static uint32_t sw_budget_bits(int level, bool split) {
+static uint32_t sw_budget_bits(int level, int mode) {
   uint32_t b = 12;
-  while (b < SW_GBITS_MAX && (1ull << b) < 4ull * sw_pmax(level, split) * 16) b++;
+  while (b < SW_GBITS_MAX && (1ull << b) < 4ull * sw_pmax(level, mode) * 16) b++;
   return b;
 }
-static uint32_t sw_budget(int level, bool split) { return 1u << (sw_budget_bits(level, split) - 2); }
+static uint32_t sw_budget(int level, int mode) { return 1u << (sw_budget_bits(level, mode) - 2); }
 // key-table slots of a level: sparse (2^18 at level 0, 2^19 after; the
 // DCC_SW_GBITS override for experiments), so a pre-pass workgroup's ~500
 // first inserts almost never meet another key at their first slot -- each
 // lost slot is one more dependent round trip for the whole workgroup
-static uint32_t sw_gbits(int level, bool split) {
+static uint32_t sw_gbits(int level, int mode) {
   static const int ov = [] {
     const char* c = DCC_ENV("DCC_SW_GBITS");
     return c ? atoi(c) : 0;
   }();
   uint32_t b = ov > 0 ? (uint32_t)ov : (level == 0 ? 18u : 19u);
-  b = std::max(b, sw_budget_bits(level, split));
+  b = std::max(b, sw_budget_bits(level, mode));
   return std::min<uint32_t>(b, SW_GBITS_MAX);
 }
 
@@ -380,6 +387,7 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1, const SwShard* shl
   // read-only split (one GPU): level 0 moves its read-only survivors to the
   // RO list (decided after the levels, sweep_ro)
   const bool ros = ro_on && (!shl || shl->full_off);
+  const int rmode = ros ? (int)sw_mode : 0;  // the schedule (sw_pmax)
   uint32_t* const wctl = abandon;  // [0] abandon [1] writer table full [2] RO count
   for (int l = l0; l < l1; l++) {
     const bool top = l == 0;
@@ -394,7 +402,7 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1, const SwShard* shl
     SubBufs& out = sw_list[l & 1];
     SwLevel* lv = ctl + l;
     const uint32_t* mdev = top ? nullptr : &lv->m;
-    const uint32_t pmax = sw_pmax(l, ros);
+    const uint32_t pmax = sw_pmax(l, rmode);
     const uint64_t tiles = (std::min<uint64_t>(pmax, d.n) + SW_T - 1) / SW_T;
     uint32_t* fw = (uint32_t*)sw_fw.p;
     uint32_t* la = fw + (1u << SW_GBITS_MAX);
@@ -407,8 +415,8 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1, const SwShard* shl
     const uint32_t sm_host = (shl && !shl->m_dev) ? shl->P : n;
     SwPreArgs pa{sin, smdev, sm_host, pmax, top ? (const uint8_t*)state.p : nullptr,
                  (SwRec*)sw_rec.p, (uint32_t*)sw_rk.p,
-                 gtab0 + (size_t)(l & 1) * (1ull << SW_GBITS_MAX), sw_gbits(l, ros),
-                 sw_budget(l, ros), fw, la, aent, apos, abandon, err, nullptr};
+                 gtab0 + (size_t)(l & 1) * (1ull << SW_GBITS_MAX), sw_gbits(l, rmode),
+                 sw_budget(l, rmode), fw, la, aent, apos, abandon, err, nullptr};
     if (sw_debug && l < 4) pa.dbg = (uint64_t*)sw_dbg.p + 4096 + 4 * 256 * 8 + (size_t)l * 64 * 8;
     const bool serial_part = !(resume && l == l0);
     if (serial_part) {
@@ -416,7 +424,7 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1, const SwShard* shl
       launch_sw_rows(pa, (unsigned)tiles, stream);
     }
     SwSeqArgs sa{smdev, sm_host, pmax, top ? 1 : 0, (const SwRec*)sw_rec.p, (const uint32_t*)sw_rk.p,
-                 gtab0 + (size_t)(l & 1) * (1ull << SW_GBITS_MAX), sw_gbits(l, ros),
+                 gtab0 + (size_t)(l & 1) * (1ull << SW_GBITS_MAX), sw_gbits(l, rmode),
                  (uint8_t*)state.p, (uint8_t*)hasw.p,
                  cbits_d, ckeys_d, bloom_d, lv, lv + 1, (uint32_t*)out.off.p, (uint64_t*)sw_mg.p,
                  abandon, err, nullptr};
@@ -454,7 +462,7 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1, const SwShard* shl
     fa.cand_state = top ? 1 : 0;
     fa.level = (uint32_t)l;
     fa.gtab = gtab0 + (size_t)(l & 1) * (1ull << SW_GBITS_MAX);
-    fa.gbits = sw_gbits(l, ros);
+    fa.gbits = sw_gbits(l, rmode);
     fa.cbits = cbits_d;
     fa.bloom = bloom_d;
     fa.ckeys = ckeys_d;
@@ -478,7 +486,7 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1, const SwShard* shl
     fa.abandon_num = top ? 1 : 3;
     fa.abandon_den = 4;
     fa.gclear = gtab0 + (size_t)((l + 1) & 1) * (1ull << SW_GBITS_MAX);
-    fa.gclear_n = 1ull << sw_gbits(l + 1, ros);
+    fa.gclear_n = 1ull << sw_gbits(l + 1, rmode);
     fa.fw_clear = fw;
     fa.la_clear = la;
     fa.err = err;
@@ -541,7 +549,7 @@ int dcc_ctx::sweep_sharded(const DevBatch& d, int& next_level) {
     uint32_t* cnt = (uint32_t*)sw_xcnt.p;
     CK(hipMemsetAsync(cnt, 0, 4ull * (R + 2), stream));
     launch_sw_share(top ? nullptr : &ctl[l].m, (uint32_t)d.n, abandon, top ? d.off : in.off,
-                    sw_pmax(l, false), (uint32_t)me, cnt, stream);
+                    sw_pmax(l, 0), (uint32_t)me, cnt, stream);
     CR(comm_allreduce_max_u8((uint8_t*)cnt, 4ull * (R + 2)));
     std::vector<uint32_t> hc(R + 2);
     CK(hipMemcpyAsync(hc.data(), cnt, 4ull * (R + 2), hipMemcpyDeviceToHost, stream));
@@ -549,7 +557,7 @@ int dcc_ctx::sweep_sharded(const DevBatch& d, int& next_level) {
     const uint32_t m = hc[0];
     if (hc[1]) return DCC_OK;  // an earlier level handed off
     if (m == 0) return DCC_OK;
-    const uint32_t P = std::min<uint32_t>(sw_pmax(l, false), m);
+    const uint32_t P = std::min<uint32_t>(sw_pmax(l, 0), m);
     const uint32_t* share = hc.data() + 2;
     uint64_t total = 0, before = 0;
     for (int r = 0; r < R; r++) {
@@ -622,7 +630,7 @@ int dcc_ctx::sweep_sharded_full(const DevBatch& d, const DevBatch& full, int l0,
     cap = std::min<uint64_t>(cap, std::max<uint64_t>(65536, l == 0 ? (cap + 3) / 4 : (cap * 3 + 3) / 4));
   }
   CR(sw_kill.ensure(this, wmax * 8 * (R + 1) + 64, "sweep kill bits"));
-  const uint32_t pm = sw_pmax(SW_MAX_LEVEL - 1, ro_on);
+  const uint32_t pm = sw_pmax(SW_MAX_LEVEL - 1, ro_on ? (int)sw_mode : 0);
   CR(sw_moff.ensure(this, 4ull * (std::min<uint64_t>(pm, d.n) + 1) + 64, "sweep serial offsets"));
   CR(sw_mkeys.ensure(this, 8ull * std::min<uint64_t>(pm, d.n) * MAX_TXN_LEN + 64, "sweep serial keys"));
   CR(sw_mat.ensure(this, std::min<uint64_t>(pm, d.n) * MAX_TXN_LEN + 64, "sweep serial types"));
@@ -633,7 +641,7 @@ int dcc_ctx::sweep_sharded_full(const DevBatch& d, const DevBatch& full, int l0,
       shl.P = (uint32_t)d.n;
     } else {
       const SubBufs& b = sw_list[(l - 1) & 1];
-      launch_sw_sgather((const uint32_t*)b.tid.p, &ctl[l].m, sw_pmax(l, ro_on), full.off, full.keys,
+      launch_sw_sgather((const uint32_t*)b.tid.p, &ctl[l].m, sw_pmax(l, ro_on ? (int)sw_mode : 0), full.off, full.keys,
                         full.acctype, full.nnz, (uint32_t*)sw_moff.p, (uint64_t*)sw_mkeys.p,
                         (uint8_t*)sw_mat.p, err, stream);
       CK(hipGetLastError());
@@ -973,8 +981,17 @@ int dcc_ctx::occ_begin(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, bo
   // the graph reads them from the epoch parameters (OccDyn).
   const bool graph_ok = sweep && !profiling && !sw_debug && !sh && !DCC_ENV("DCC_NO_GRAPH");
   // levels per captured epoch (DCC_OPT_SWEEP_LEVELS; 0 = auto: 3 with the
-  // read-only split, 4 without)
-  r.glv = sw_levels ? sw_levels : (ro_on ? 3u : 4u);
+  // read-only split, 4 without) and the schedule.  Auto with the split: two
+  // levels (level 1 a serial tail of 8,192) while the last epoch's level-1
+  // list fitted comfortably, three otherwise -- a longer list in a two-level
+  // epoch is still decided exactly, by more levels after a host round trip.
+  if (ro_on && !sw_levels && !sh) {
+    if (sw_l1_last <= 6144) sw_mode = 2;
+    else if (sw_l1_last > 8192) sw_mode = 1;
+  } else {
+    sw_mode = 1;
+  }
+  r.glv = sw_levels ? sw_levels : (ro_on ? (sw_mode == 2 ? 2u : 3u) : 4u);
   // (host outputs are copied outside the graph: their addresses are not part of it)
   r.gkey = GraphKey{d.off, d.keys, d.acctype, d.n, d.nnz, r.dev_out ? out_rc : nullptr, r.dev_out,
                     r.glv | (ro_on ? 0x80u | (wt_bits << 8) : 0u), buf_gen,
@@ -1025,9 +1042,10 @@ int dcc_ctx::occ_begin(const dcc_batch* b, uint8_t* out_rc, uint64_t* out_tn, bo
     fa.job[fa.n++] = FillJob{(uint32_t*)dyn.p, sizeof(OccDyn) / 4, 0u, (const uint32_t*)hdyn_dev};
     if (sweep) {
       fa.job[fa.n++] = FillJob{(uint32_t*)sw_ctl.p, sw_ctl_bytes() / 4, 0u};
-      fa.job[fa.n++] = FillJob{(uint32_t*)sw_gtab.p, (1ull << sw_gbits(0, ro_on)) * 2, 0xFFFFFFFFu};
-      fa.job[fa.n++] = FillJob{(uint32_t*)sw_fw.p, 1ull << sw_gbits(0, ro_on), 0xFFFFFFFFu};
-      fa.job[fa.n++] = FillJob{(uint32_t*)sw_fw.p + (1u << SW_GBITS_MAX), 1ull << sw_gbits(0, ro_on), 0u};
+      const int m0 = ro_on ? (int)sw_mode : 0;
+      fa.job[fa.n++] = FillJob{(uint32_t*)sw_gtab.p, (1ull << sw_gbits(0, m0)) * 2, 0xFFFFFFFFu};
+      fa.job[fa.n++] = FillJob{(uint32_t*)sw_fw.p, 1ull << sw_gbits(0, m0), 0xFFFFFFFFu};
+      fa.job[fa.n++] = FillJob{(uint32_t*)sw_fw.p + (1u << SW_GBITS_MAX), 1ull << sw_gbits(0, m0), 0u};
     }
     launch_fill(fa, stream);  // the sweep's prep runs inside its level-0 serial pass
   }
@@ -1374,6 +1392,7 @@ int dcc_ctx::occ_end(dcc_stats* st) {
 #endif
     r.info.prefix = hc[0].pos;
     r.info.survivors = hc[1].m;
+    if (ro_on && !sh) sw_l1_last = hc[1].m;  // the next epoch's schedule (occ_begin)
     for (int l = 0; l < next_level && (l == 0 || hc[l].m); l++) rounds++;
   }
 

@@ -141,3 +141,27 @@ def test_device_batch_and_repeat(sw, levels):
         rc, _, _ = sw.occ_validate_epoch(db)
         torch.cuda.synchronize()
         assert np.array_equal(rc.cpu().numpy(), erc)
+
+
+@pytest.mark.parametrize("device", [False, True])
+def test_adaptive_two_level_schedule(device):
+    """Auto schedule (DCC_OPT_SWEEP_LEVELS 0, read-only split): an epoch whose
+    last predecessor's level-1 list was short runs two levels per graph
+    (level 1 a serial tail of 8,192); one whose list then overflows the tail
+    continues exactly through more levels after a host round trip, and the
+    next epoch goes back to three.  Every epoch bit-exact against the oracle,
+    graph replays included (C2, then the headline size, then C2 again)."""
+    import torch
+    small = d.gen_ycsb(n_txn=65536, zipf_theta=0.9, seed=0x2C2)
+    big = d.gen_ycsb(n_txn=1 << 20, zipf_theta=0.9, seed=0x2C3)
+    exp = {id(small): orc.occ(small)[0], id(big): orc.occ(big)[0]}
+    with d.Engine(0) as eng:
+        rounds = []
+        for b in [small, small, small, big, big, small, small]:
+            bb = b.to_torch("cuda:0") if device else b
+            rc, _, st = eng.occ_validate_epoch(bb)
+            rc = rc.cpu().numpy() if device else np.asarray(rc)
+            assert np.array_equal(rc, exp[id(b)])
+            rounds.append(st["rounds"])
+        # C2's level-1 list fits the tail: two levels from the second epoch on
+        assert rounds[1] == 2 and rounds[2] == 2
