@@ -19,10 +19,15 @@ def main():
     if lv:
         eng.set_option(d._abi.OPT_SWEEP_LEVELS, lv)
     out = []
-    for tag, b in (("C2", d.gen_ycsb(n_txn=65536, zipf_theta=0.9)),
-                   ("C2s", d.gen_ycsb(n_txn=65536, zipf_theta=0.9, seed=77)),
-                   ("C3", d.gen_tpcc(n_txn=262144, num_wh=128)),
-                   ("H", d.gen_ycsb(n_txn=1 << 20, zipf_theta=0.9))):
+    cases = (("C2", lambda: d.gen_ycsb(n_txn=65536, zipf_theta=0.9)),
+             ("C2s", lambda: d.gen_ycsb(n_txn=65536, zipf_theta=0.9, seed=77)),
+             ("C3", lambda: d.gen_tpcc(n_txn=262144, num_wh=128)),
+             ("H", lambda: d.gen_ycsb(n_txn=1 << 20, zipf_theta=0.9)))
+    only = os.environ.get("C2_ONLY")
+    for tag, gen in cases:
+        if only and tag != only:
+            continue
+        b = gen()
         db = b.to_torch("cuda:0")
         rc = torch.empty(b.n_txn, dtype=torch.uint8, device="cuda:0")
         ms = []
