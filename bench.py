@@ -428,8 +428,10 @@ def pipe_fin_config(eng, dev, timed, orc, tag="PIPE_FIN", n=1 << 20, lanes=4, k=
     (occ.cpp:248-294) under its default TS_CLOCK: every epoch wants commit tn
     and appends its committed writes to the device history
     (DCC_OCC_APPEND_HISTORY), submitted through the pipeline
-    (dcc_occ_submit_epoch): the lanes decide, the context numbers and appends
-    each epoch as it completes, in submit order (dcc_ctx::pipe_finish).  k
+    (dcc_occ_submit_epoch): each lane decides its epoch and numbers / appends
+    it on the device right behind the decision, from the device tnc and append
+    position the epochs advance in submit order (DCC_OPT_PIPE_CHAIN; the
+    context finishes an epoch itself when that could not: dcc_ctx::pipe_finish).  k
     epochs over `lanes` distinct resident batches from an empty history
     (merges of the delta into the base included); each lane's last epoch's
     decisions and tns are checked against the oracle (tn = the batch's own
@@ -444,9 +446,12 @@ def pipe_fin_config(eng, dev, timed, orc, tag="PIPE_FIN", n=1 << 20, lanes=4, k=
     exp = [orc.occ(b) for b in bs]  # (rc, tn from tnc 0, committed writers)
     eng.set_option(d._abi.OPT_PIPELINE, lanes)
 
+    where = []
+
     def stream(kk):
         eng.history_clear()
         eng.tnc = 0
+        where.clear()
         tnc_before = [0] * kk
         fl, t = deque(), 0
         for i in range(kk):
@@ -455,9 +460,9 @@ def pipe_fin_config(eng, dev, timed, orc, tag="PIPE_FIN", n=1 << 20, lanes=4, k=
             fl.append(eng.occ_submit_epoch(dbs[i % lanes], rcs[i % lanes], tns[i % lanes],
                                            append_history=True))
             if len(fl) >= lanes:
-                eng.occ_wait_epoch(fl.popleft())
+                where.append(eng.occ_wait_epoch(fl.popleft())["fin_where"])
         while fl:
-            eng.occ_wait_epoch(fl.popleft())
+            where.append(eng.occ_wait_epoch(fl.popleft())["fin_where"])
         return tnc_before
 
     stream(2 * lanes)  # warm-up: every lane's graph captured
@@ -480,6 +485,7 @@ def pipe_fin_config(eng, dev, timed, orc, tag="PIPE_FIN", n=1 << 20, lanes=4, k=
                         f"appended to the device history (central_finish under TS_CLOCK)",
             "txns_per_s": n / dt, "ms_per_epoch": dt * 1e3,
             "history_pairs_at_end": int(hist),
+            "finished_on_device": where.count(1), "finished_by_host": where.count(2),
             "parity_vs_oracle": bool(par),
             "parity_scope": "rc and tn of each lane's last epoch, tnc after the stream",
             "note": "a stream whose epochs carry TS_CAS windows reading the previous epochs' history "

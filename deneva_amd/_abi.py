@@ -51,6 +51,7 @@ OPT_PIPELINE = 11
 OPT_CALVIN_PATH = 12
 OPT_COMM_SOLO = 13
 OPT_PIPE_PARTITION = 14
+OPT_PIPE_CHAIN = 15
 
 
 class Batch(C.Structure):
@@ -97,7 +98,7 @@ class Stats(C.Structure):
         ("peel_prefix", C.c_uint64),
         ("n_survivors", C.c_uint64),
         ("fallback", C.c_uint32),
-        ("reserved2", C.c_uint32),
+        ("fin_where", C.c_uint32),
     ]
 
     def as_dict(self) -> dict:

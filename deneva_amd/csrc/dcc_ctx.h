@@ -271,7 +271,27 @@ struct dcc_ctx {
   // the central_finish of lane `l`'s completed epoch (decided with fin_later):
   // commit tn from this context's tnc, the history append into this
   // context's delta level -- run by the parent in submit order (occ_pipe.cpp)
-  int pipe_finish(dcc_ctx* l);
+  // chained: other chained epochs may be in flight behind it (their finishes
+  // write into the delta level): no merge, rebuild or growth here
+  int pipe_finish(dcc_ctx* l, bool chained = false);
+  // Chained central_finish (occ_pipe.cpp, DCC_OPT_PIPE_CHAIN): lane l's epoch
+  // `seq` numbered and appended on the device right after its decision, from
+  // this context's device tnc / append position (fin_ctl), which the finish
+  // advances; `after`: the previous epoch's last work (its finish) is waited
+  // for on the device; reset: fin_ctl starts at this context's values
+  int chain_enqueue(dcc_ctx* l, uint64_t seq, hipEvent_t after, bool reset);
+  // fin_ctl = {tnc, delta size, seq} after lane l's work: the host finished
+  // the epoch before `seq` itself
+  int chain_set(dcc_ctx* l, uint64_t seq);
+  // the chained finish of lane l's epoch numbered it: tnc and the delta level follow
+  int chain_accept(dcc_ctx* l);
+  uint64_t hist_room() const;  // flat pairs the delta level holds without moving
+  DevBuf fin_ctl;                  // parent: dcc::FinCtl
+  DevBuf fdyn;                     // lane: the chained finish's OccDyn
+  void* hfin = nullptr;            // lane: its staging and totals (pinned, HDYN_BYTES)
+  void* hfin_dev = nullptr;
+  hipEvent_t ev_done = nullptr;    // lane: after the work of its last submitted epoch
+  uint32_t pipe_chain = 1;         // DCC_OPT_PIPE_CHAIN
   int occ_end(dcc_stats* st);
   int occ_final(bool async);  // finalize launches (or the graph replay) of `run`
   // pipelined epochs over lane contexts on this device (occ_pipe.cpp)

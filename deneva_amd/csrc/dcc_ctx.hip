@@ -168,6 +168,8 @@ extern "C" void dcc_destroy(dcc_ctx* ctx) {
   if (ctx->hmisc) (void)hipHostFree(ctx->hmisc);
   if (ctx->hpart) (void)hipHostFree(ctx->hpart);
   if (ctx->hdyn) (void)hipHostFree(ctx->hdyn);
+  if (ctx->hfin) (void)hipHostFree(ctx->hfin);
+  if (ctx->ev_done) (void)hipEventDestroy(ctx->ev_done);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   for (auto& e : ctx->pev)
@@ -204,6 +206,12 @@ extern "C" int dcc_set_option(dcc_ctx* ctx, int option, int64_t value) {
     if (value != 0 && value != 1) return DCC_EINVAL;
     dcc_pipe_drain(ctx);  // as DCC_OPT_PIPELINE; the lanes are re-created at the next submit
     ctx->pipe_part = (uint32_t)value;
+    return DCC_OK;
+  }
+  if (option == DCC_OPT_PIPE_CHAIN) {
+    if (value != 0 && value != 1) return DCC_EINVAL;
+    dcc_pipe_drain(ctx);
+    ctx->pipe_chain = (uint32_t)value;
     return DCC_OK;
   }
   if (ctx->multi)
@@ -273,7 +281,7 @@ std::vector<DevBuf*> dcc_ctx::all_bufs() {
                             &mt_misc, &mt_slot, &mt_sval, &mt_slot2, &mt_sval2, &mt_sfl,
                             &mt_stx, &mt_txn, &mt_agg, &mt_sflB, &mt_stxB, &mt_k1, &mt_tcnt, &mt_ul, &mt_lb, &mt_ptab, &ix_keys, &ix_ord, &ix_rows, &ix_cnt, &wv_buf, &ix_scr, &wv_hbuf, &wv_obuf,
                             &h_K[0], &h_K[1], &h_V[0], &h_V[1], &h_scr, &h_bsum, &h_bm,
-                            &nar_keys, &nar_at, &nar_tn, &fin_off, &fin_keys, &fin_at, &fin_state, &fin_hasw, &fin_rc, &fin_cnt,
+                            &nar_keys, &nar_at, &nar_tn, &fin_ctl, &fdyn, &fin_off, &fin_keys, &fin_at, &fin_state, &fin_hasw, &fin_rc, &fin_cnt,
                             &sh_off, &sh_keys, &sh_at, &sh_src, &sh_cnt, &sh_bsum, &sh_rc, &sh_tn, &sh_grp};
   for (auto& h : hs)
     for (DevBuf* b : {&h.fk, &h.ft, &h.skey, &h.stn, &h.hash, &h.bm, &h.nx, &h.tcnt}) v.push_back(b);

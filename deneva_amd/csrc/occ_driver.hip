@@ -454,6 +454,7 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1, const SwShard* shl
       ca.prep_nnz = whole ? shl->full_nnz : d.nnz;
       ca.prep_part = (PrepPart*)((char*)hpart_dev + SW_PREP_OFF);
       ca.hasw = (uint8_t*)hasw.p;
+      ca.prep_err = err;
       if (ros) {
         ca.wclear = (uint4*)sw_wtab.p;
         ca.wclear_n16 = (sizeof(WrSlot) << wt_bits) / 16;
@@ -772,14 +773,25 @@ int dcc_ctx::occ_finish(const uint8_t* final_rc, uint64_t* out_tn, uint32_t flag
 // write sets to this context's delta level, on the lane's stream.  The lanes
 // never read the history (an epoch with a window check drains the pipeline
 // and runs here), so the history changes only in this host-ordered step.
-int dcc_ctx::pipe_finish(dcc_ctx* l) {
+// chained: the epoch's own chained finish did not number it (an epoch before
+// it was not finished yet, or this one was not final), and chained epochs
+// behind it may still be finishing on the device: the delta level is not
+// merged, rebuilt or moved here -- only grown, once the device is idle.
+int dcc_ctx::pipe_finish(dcc_ctx* l, bool chained) {
   dcc_ctx* ctx = this;
   OccRun& r = l->run;
   const DevBatch& d = r.d;
   if (r.n_txn == 0 || !r.fin_later) return DCC_OK;
   HistStore& D = hs[1];
   if (r.app) {
-    CR(hist_prepare());  // merge / rebuild as a synchronous append would
+    if (!chained) {
+      CR(hist_prepare());  // merge / rebuild as a synchronous append would
+    } else if (D.m + d.nnz > hist_room()) {
+      // the later chained finishes were all skipped (this epoch did not
+      // advance the device control): once they have run, nothing writes the
+      // level while it moves
+      CK(hipDeviceSynchronize());
+    }
     CR(hist_grow_flat(D, D.m + d.nnz));
     // this context's launches (merge, rebuild) before the lane's k_fin: a
     // device-side wait, the host does not block
@@ -828,9 +840,118 @@ int dcc_ctx::pipe_finish(dcc_ctx* l) {
       hist_note(D, tnc + 1, tnc + r.n_cw);
     }
     if (tot[3]) D.overflowed = true;
-    D.built = !tot[3];
+    // chained: the table may hold pushes of a finish that ran on this epoch
+    // before it was final, or of a skipped one's successors: rebuilt from the
+    // flat pairs before its next read
+    D.built = !tot[3] && !chained;
   }
   tnc += r.n_cw;
+  return DCC_OK;
+}
+
+// flat pairs the delta level can hold without moving
+uint64_t dcc_ctx::hist_room() const {
+  const HistStore& D = hs[1];
+  return std::min<uint64_t>({D.fk.cap / 8, D.ft.cap / 8, D.nx.cap / 4});
+}
+
+// A chained central_finish (OccFinArgs::ctl; occ_pipe.cpp): enqueued on lane
+// l's stream right behind its decision, so the lane needs no host round trip
+// between deciding an epoch and numbering it.  The finish waits on the device
+// for the previous epoch's last work (`after`), snapshots fin_ctl and numbers
+// and appends only when fin_ctl is at `seq`; the delta level's pointers are
+// this context's at submit (the level does not move while chained epochs are
+// in flight: occ_pipe.cpp reserves room up front).
+int dcc_ctx::chain_enqueue(dcc_ctx* l, uint64_t seq, hipEvent_t after, bool reset) {
+  dcc_ctx* ctx = this;
+  OccRun& r = l->run;
+  const DevBatch& d = r.d;
+  HistStore& D = hs[1];
+  CR(fin_ctl.ensure(this, sizeof(FinCtl), "chained finish control"));
+  CR(l->fdyn.ensure(l, sizeof(OccDyn), "chained finish parameters"));
+  if (!l->hfin) {
+    CK(hipHostMalloc(&l->hfin, HDYN_BYTES, hipHostMallocDefault));
+    CK(hipHostGetDevicePointer(&l->hfin_dev, l->hfin, 0));
+    memset(l->hfin, 0, HDYN_BYTES);
+  }
+  if (l->fin_tag + 4 >= (1u << 30)) {
+    CK(hipMemsetAsync(l->fin_part.p, 0, l->fin_part.cap, l->stream));
+    l->fin_tag = 0;
+  }
+  OccDyn& y = *(OccDyn*)l->hfin;
+  y.tnc = 0;
+  y.hist_m = 0;
+  y.fin_tag = ++l->fin_tag;
+  y.pad = 0;
+  y.app_k = r.app ? (uint64_t*)D.fk.p : nullptr;
+  y.app_t = r.app ? (uint64_t*)D.ft.p : nullptr;
+  y.ins = r.app ? hist_insert_args(D) : HistInsert{};
+  y.view = HistView{};
+  if (after) CK(hipStreamWaitEvent(l->stream, after, 0));
+  if (reset) {
+    // this context's merges / builds first, then the device control starts
+    // from this context's values (no epoch is in flight)
+    CK(hipEventRecord(ev1, stream));
+    CK(hipStreamWaitEvent(l->stream, ev1, 0));
+    launch_fin_ctl_set((FinCtl*)fin_ctl.p, tnc, D.m, seq, l->stream);
+  }
+  launch_fin_prep((const uint32_t*)l->hfin_dev, (OccDyn*)l->fdyn.p, (const FinCtl*)fin_ctl.p, seq, l->stream);
+  OccFinArgs fa{d.n, d.nnz, r.cf, d.off, d.keys, d.acctype, (uint64_t*)l->fin_part.p,
+                (const OccDyn*)l->fdyn.p, r.tn_dev, (uint64_t*)((char*)l->hfin_dev + HDYN_TOTALS),
+                y.fin_tag, 0u};
+  fa.ctl = (FinCtl*)fin_ctl.p;
+  fa.seq = seq;
+  fa.state = (const uint8_t*)l->state.p;
+  fa.err = (const uint32_t*)l->misc.p;
+  fa.wfull = (const uint32_t*)((const SwLevel*)l->sw_ctl.p + SW_MAX_LEVEL + 1) + 1;
+  fa.cap = r.app ? hist_room() : ~0ull;
+  launch_fin(fa, l->stream);
+  CK(hipGetLastError());
+  if (!r.dev_out && r.out_tn) CK(hipMemcpyAsync(r.out_tn, l->tn.p, d.n * 8, hipMemcpyDeviceToHost, l->stream));
+  return DCC_OK;
+}
+
+// The chained finish numbered and appended lane l's epoch (its totals, read
+// after the lane's stream passed it): the host's tnc and delta level follow.
+int dcc_ctx::chain_accept(dcc_ctx* l) {
+  OccRun& r = l->run;
+  const DevBatch& d = r.d;
+  const uint64_t* tot = (const uint64_t*)((const char*)l->hfin + HDYN_TOTALS);
+  if (tot[0] != r.n_cw) {
+    std::string why = "look-back words unreadable";
+    std::vector<uint8_t> w(fin_part_bytes(d.n));
+    if (hipMemcpy(w.data(), l->fin_part.p, w.size(), hipMemcpyDeviceToHost) == hipSuccess)
+      why = fin_diag(w.data(), d.n, l->fin_tag);
+    (void)hipGetLastError();
+    return fail(DCC_EIO, "chained central_finish numbered %llu txns, %llu committed writers (%s)",
+                (unsigned long long)tot[0], (unsigned long long)r.n_cw, why.c_str());
+  }
+  if (r.app) {
+    HistStore& D = hs[1];
+    if (tot[1] > d.nnz) return fail(DCC_EIO, "history append: %llu writes > %llu accesses",
+                                    (unsigned long long)tot[1], (unsigned long long)d.nnz);
+    if (tot[1]) {
+      D.m += tot[1];
+      D.max_key = std::max<uint64_t>(D.max_key, tot[2]);
+      D.last_app = tot[1];
+      const bool b = D.built;
+      hist_note(D, tnc + 1, tnc + r.n_cw);
+      D.built = b;  // the pushes went onto the chains
+    }
+    if (tot[3]) {
+      D.overflowed = true;
+      D.built = false;
+    }
+  }
+  tnc += r.n_cw;
+  return DCC_OK;
+}
+
+int dcc_ctx::chain_set(dcc_ctx* l, uint64_t seq) {
+  dcc_ctx* ctx = this;
+  CR(fin_ctl.ensure(this, sizeof(FinCtl), "chained finish control"));
+  launch_fin_ctl_set((FinCtl*)fin_ctl.p, tnc, hs[1].m, seq, l->stream);
+  CK(hipGetLastError());
   return DCC_OK;
 }
 

@@ -127,7 +127,9 @@ struct FinTail {
   unsigned long long kmax;  // largest key appended (reset by the last workgroup)
   uint32_t done;            // finished workgroups (reset by the last one)
   uint32_t ticket;          // workgroups started (reset by the last one)
-  uint32_t pad[12];
+  uint32_t und;             // chained: undecided txns seen (reset by the last one)
+  uint32_t capx;            // chained: a workgroup's pairs did not fit (reset by the last one)
+  uint32_t pad[10];
 };
 static_assert(sizeof(FinTail) == 64, "one line");
 template <typename T>
@@ -219,6 +221,14 @@ __global__ __launch_bounds__(HB, 8) void k_fin(OccFinArgs a) {  // two workgroup
   __shared__ uint32_t s_last, s_id;
   const OccDyn* dy = a.dyn;
   const uint32_t tag = a.tag ? a.tag : dy->fin_tag;
+  const bool chained = a.ctl != nullptr;
+  if (chained && dy->pad != 1u) {
+    // an epoch before this one is not finished yet (its host finish is still
+    // to come): the host finishes this one too, nothing is written
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+      for (int q = 0; q < 5; q++) a.totals[q] = 0;
+    return;
+  }
   // the tail first: its place must not depend on the epoch's grid size
   FinTail* tail = (FinTail*)a.part;
   FinLb* lb = (FinLb*)(tail + 1);
@@ -246,11 +256,16 @@ __global__ __launch_bounds__(HB, 8) void k_fin(OccFinArgs a) {  // two workgroup
     o0[i] = o1[i] = 0;
     w[i] = (c[i] && app_k) ? fin_writes(t_0 + i, a, o0[i], o1[i], kmx) : 0u;
   }
-  uint32_t cs = 0, ws = 0;
+  uint32_t cs = 0, ws = 0, und = 0;
 #pragma unroll
   for (uint32_t i = 0; i < FIN_T; i++) {
     cs += c[i];
     ws += w[i];
+    if (chained && t_0 + i < a.n) und += a.state[t_0 + i] == ST_UNDECIDED;
+  }
+  if (chained) {  // the epoch's undecided txns, one atomic per wave (none usually)
+    for (int d = 32; d > 0; d >>= 1) und += __shfl_xor(und, d);
+    if ((threadIdx.x & 63) == 0 && und) atomicAdd(&tail->und, und);
   }
   if (threadIdx.x == 0) s_mx = 0;
   uint32_t e0, e1, t0, t1;
@@ -301,6 +316,10 @@ __global__ __launch_bounds__(HB, 8) void k_fin(OccFinArgs a) {  // two workgroup
   __syncthreads();
   const uint64_t P = s_pre;
   const uint64_t wbase = dy->hist_m + (P >> 32);
+  // chained: the host reserved room for the epochs in flight from a bound;
+  // pairs past it are not written and the host finishes the epoch itself
+  const bool room = !chained || wbase + t1 <= a.cap;
+  if (!room && threadIdx.x == 0) atomicOr(&tail->capx, 1u);
   if (P != ~0ull) {
     uint32_t ec = e0, ew = e1;
 #pragma unroll
@@ -309,7 +328,7 @@ __global__ __launch_bounds__(HB, 8) void k_fin(OccFinArgs a) {  // two workgroup
       if (t >= a.n) break;
       const uint64_t my_tn = c[i] ? dy->tnc + (uint32_t)P + ec + 1 : 0;
       if (!(a.var & 8u)) a.tn[t] = my_tn;
-      if (w[i] && !(a.var & 4u)) {
+      if (w[i] && room && !(a.var & 4u)) {
         uint64_t p = wbase + ew;
         for (uint64_t x = o0[i]; x < o1[i]; x += FIN_U) {
           uint8_t ty[FIN_U];
@@ -330,7 +349,7 @@ __global__ __launch_bounds__(HB, 8) void k_fin(OccFinArgs a) {  // two workgroup
   }
   // the block's pairs onto the delta's chains, a thread per pair
   const HistInsert ins = dy->ins;
-  if (ins.hash && t1 && P != ~0ull && !(a.var & 1u)) {
+  if (ins.hash && t1 && P != ~0ull && room && !(a.var & 1u)) {
     __syncthreads();  // the pairs written above
     for (uint32_t i = threadIdx.x; i < t1; i += HB) hist_insert(ins, wbase + i, app_k[wbase + i], app_t[wbase + i]);
   }
@@ -347,9 +366,47 @@ __global__ __launch_bounds__(HB, 8) void k_fin(OccFinArgs a) {  // two workgroup
     a.totals[1] = g >> 32;
     a.totals[2] = atomicExch(&tail->kmax, 0ull);
     a.totals[3] = ins.hash ? atomicAdd(ins.over, 0u) : 0u;
+    if (chained) {
+      // the epoch is final and numbered from the snapshot: the next one in
+      // submit order may go on from here
+      const bool ok = g != ~0ull && fin_ld(&tail->und) == 0 && fin_ld(&tail->capx) == 0 &&
+                      (fin_ld(a.err) & ERR_NOT_FINAL) == 0 && (!a.wfull || fin_ld(a.wfull) == 0);
+      if (ok) {
+        fin_st(&a.ctl->tnc, dy->tnc + (uint32_t)g);
+        fin_st(&a.ctl->hist_m, dy->hist_m + (g >> 32));
+        __hip_atomic_store(&a.ctl->seq, a.seq + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      a.totals[4] = ok ? 1u : 0u;
+      fin_st(&tail->und, 0u);
+      fin_st(&tail->capx, 0u);
+    }
     fin_st(&tail->ticket, 0u);  // every workgroup took its ticket before it arrived
     fin_st(&tail->done, 0u);
   }
+}
+
+// A chained finish's parameters (OccFinArgs::ctl): the epoch's OccDyn words
+// from pinned host memory, then -- once every thread's copy is in -- the
+// snapshot of the device tnc / append position when *ctl is at `seq`.
+__global__ __launch_bounds__(256) void k_fin_prep(const uint32_t* src, OccDyn* dyn, const FinCtl* ctl,
+                                                   uint64_t seq) {
+  uint32_t* d = (uint32_t*)dyn;
+  for (uint32_t i = threadIdx.x; i < sizeof(OccDyn) / 4; i += 256) d[i] = src[i];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint64_t s = __hip_atomic_load(&ctl->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    const bool at = s == seq;
+    if (at) {
+      dyn->tnc = fin_ld(&ctl->tnc);
+      dyn->hist_m = fin_ld(&ctl->hist_m);
+    }
+    dyn->pad = at ? 1u : 0u;
+  }
+}
+__global__ void k_fin_ctl_set(FinCtl* ctl, uint64_t tnc, uint64_t hist_m, uint64_t seq) {
+  fin_st(&ctl->tnc, tnc);
+  fin_st(&ctl->hist_m, hist_m);
+  __hip_atomic_store(&ctl->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 void launch_fin(const OccFinArgs& a0, hipStream_t st) {
@@ -359,6 +416,13 @@ void launch_fin(const OccFinArgs& a0, hipStream_t st) {
   if (const char* e = DCC_ENV("DCC_FIN_VAR")) a.var = (uint32_t)atoi(e);
   const uint64_t nb = (a.n + HB * FIN_T - 1) / (HB * FIN_T);
   k_fin<<<(unsigned)(nb ? nb : 1), HB, 0, st>>>(a);
+}
+
+void launch_fin_prep(const uint32_t* src, OccDyn* dyn, const FinCtl* ctl, uint64_t seq, hipStream_t st) {
+  k_fin_prep<<<1, 256, 0, st>>>(src, dyn, ctl, seq);
+}
+void launch_fin_ctl_set(FinCtl* ctl, uint64_t tnc, uint64_t hist_m, uint64_t seq, hipStream_t st) {
+  k_fin_ctl_set<<<1, 1, 0, st>>>(ctl, tnc, hist_m, seq);
 }
 
 uint64_t fin_part_bytes(uint64_t n) { return (((n + HB * FIN_T - 1) / (HB * FIN_T)) + 2) * sizeof(FinLb); }

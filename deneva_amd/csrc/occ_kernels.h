@@ -30,6 +30,12 @@ constexpr uint32_t ERR_KEY = 4;
 constexpr uint32_t ERR_FULL = 8;
 constexpr uint32_t ERR_UNDECIDED = 16;
 constexpr uint32_t ERR_SPIN = 128;  // sweep filter: look-back spin limit reached
+// the level-0 validation pass found malformed offsets or an over-long txn (the
+// host reports it from the pass's partials; the bit tells a chained
+// central_finish not to number the epoch, occ_history.hip k_fin)
+constexpr uint32_t ERR_PREP = 256;
+// error bits after which an epoch's decisions are not final
+constexpr uint32_t ERR_NOT_FINAL = ERR_OFFSETS | ERR_TILE | ERR_KEY | ERR_FULL | ERR_SPIN | ERR_PREP;
 
 constexpr unsigned PREP_BLOCKS = 512;
 constexpr unsigned FINAL_BLOCKS = 512;
@@ -359,6 +365,7 @@ struct SwCoutArgs {
   uint8_t* hasw;
   uint4* wclear;          // the writer table, cleared by the prep workgroups
   uint64_t wclear_n16;    // its size in 16-B words (0: none)
+  uint32_t* prep_err;     // ERR_PREP joins the epoch's error word (null: none)
 };
 // k_sw_filter / k_sw_scan / k_sw_compact (one argument block for the three)
 struct SwFilterArgs {
@@ -515,6 +522,12 @@ void launch_decide(uint8_t* state, uint8_t* gst, uint64_t n, uint8_t abort_byte,
 // write sets appended to the delta level at dyn->hist_m in tn order
 // (occ.cpp:277-286).  totals (pinned): [0] committed writers, [1] pairs
 // appended, [2] largest key appended.
+// The device copy of the commit counter and the delta level's append position
+// that chained central_finish launches advance in submit order (seq: the next
+// epoch entitled to them).
+struct FinCtl {
+  uint64_t tnc, hist_m, seq, pad;
+};
 struct OccFinArgs {
   uint64_t n, nnz;
   const uint32_t* cflag;
@@ -529,8 +542,27 @@ struct OccFinArgs {
   uint32_t tag;        // look-back tag; 0: the epoch's (dyn->fin_tag).  A second launch
                        // for the same epoch takes a fresh one.
   uint32_t var;        // DCC_FIN_VAR timing variants (DCC_EXPERIMENTS builds only; 0)
+  // Chained (a pipeline lane's epoch, finished on the device in submit order;
+  // ctl null: not chained).  dyn->tnc / hist_m are then the snapshot of *ctl
+  // taken by k_fin_prep, dyn->pad 1 when *ctl was at `seq` (every epoch before
+  // this one finished): only then does k_fin number the epoch, and it advances
+  // *ctl past it when the epoch was final -- no undecided txn (state), no
+  // ERR_NOT_FINAL bit in *err, no overflow of the committed-writer table
+  // (*wfull), every pair within `cap` -- reporting totals[4] = 1.  Otherwise
+  // totals[4] = 0 and the host finishes the epoch itself.
+  FinCtl* ctl;
+  uint64_t seq;
+  const uint8_t* state;
+  const uint32_t* err;
+  const uint32_t* wfull;
+  uint64_t cap;
 };
 void launch_fin(const OccFinArgs& a, hipStream_t st);
+// a chained finish's parameters: the OccDyn words from pinned `src` into
+// `dyn`, then the snapshot of *ctl (occ_history.hip)
+void launch_fin_prep(const uint32_t* src, OccDyn* dyn, const FinCtl* ctl, uint64_t seq, hipStream_t st);
+// *ctl = {tnc, hist_m, seq} (seq stored last, release)
+void launch_fin_ctl_set(FinCtl* ctl, uint64_t tnc, uint64_t hist_m, uint64_t seq, hipStream_t st);
 uint64_t fin_part_bytes(uint64_t n);
 // summary of a host copy of the look-back words after a launch with `tag`
 // (the totals-mismatch error message)

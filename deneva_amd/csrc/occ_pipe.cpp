@@ -18,6 +18,7 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <deque>
 #include <string>
 #include <unordered_map>
@@ -31,6 +32,10 @@ struct OccPipe {
   struct Flight {
     uint64_t ticket;
     int lane;
+    uint64_t seq;       // submit sequence of lane epochs (the chained finishes' order)
+    bool chain;         // its central_finish is chained on the device (chain_enqueue)
+    bool app;           // ... and appends to the history
+    uint64_t res;       // delta-level pairs reserved for that append
   };
   std::deque<Flight> flight;  // submitted and not yet completed, submit order
   struct Result {
@@ -44,8 +49,26 @@ struct OccPipe {
   hipEvent_t ready = nullptr;  // the caller's stream, before an epoch's first lane launch
   uint32_t part = 0;           // DCC_OPT_PIPE_PARTITION the lanes were made with
   uint32_t app_in_flight = 0;  // epochs in flight whose history append is still to come
+  uint64_t seq = 0;            // the last lane epoch's sequence number
+  uint64_t app_res = 0;        // delta-level pairs reserved by chained appends in flight
+  uint64_t app_max = 0;        // largest append seen (the reservation estimate)
+  bool broken = false;         // an epoch failed after its chained finish numbered it
 };
 
+// Another chained epoch in flight (its finish may wait for fin_ctl to move).
+static bool chain_behind(const OccPipe* p) {
+  for (const OccPipe::Flight& f : p->flight)
+    if (f.chain) return true;
+  return false;
+}
+
+// Completion, in submit order.  A chained epoch's finish ran behind its
+// decision on the lane: when it numbered the epoch (totals[4] == 1) the
+// context's tnc and delta level follow its totals; when it did not (an epoch
+// before it was not finished when it ran, or this one was not final and took
+// more levels), the context finishes the epoch itself (pipe_finish) and moves
+// fin_ctl past it, as it does after every other epoch it finishes on the host
+// while chained epochs are in flight behind it.
 static void pipe_complete_front(dcc_ctx* ctx) {
   OccPipe* p = ctx->pipe;
   const OccPipe::Flight f = p->flight.front();
@@ -54,17 +77,63 @@ static void pipe_complete_front(dcc_ctx* ctx) {
   OccPipe::Result r{};
   (void)hipSetDevice(lane->device);
   r.rc = lane->occ_end(&r.st);
-  if (r.rc != DCC_OK) {
-    r.err = lane->last_error;
-  } else if (lane->run.fin_later) {
+  if (r.rc != DCC_OK) r.err = lane->last_error;
+  bool host_done = true;  // fin_ctl does not know this epoch's outcome
+  if (f.chain) {
+    uint64_t st = 0;
+    const hipError_t e = hipEventSynchronize(lane->ev_done);  // the finish (and tn copy) passed
+    if (e == hipSuccess) {
+      st = ((const uint64_t*)((const char*)lane->hfin + dcc_ctx::HDYN_TOTALS))[4];
+    } else if (r.rc == DCC_OK) {
+      r.rc = ctx->hip_fail(e, "chained central_finish");
+      r.err = ctx->last_error;
+    }
+    if (st == 2 && lane->run.app) ctx->hs[1].built = false;  // pushed before the epoch was final
+    if (p->broken) {
+      // numbered behind an epoch that failed after its finish ran
+      r.rc = DCC_EIO;
+      r.err = "an epoch before this one in the pipeline failed after its central_finish ran on the device";
+      host_done = false;
+    } else if (r.rc != DCC_OK) {
+      if (st == 1) {  // the later finishes followed its numbering
+        p->broken = true;
+        ctx->hs[1].built = false;
+        host_done = false;
+      }
+    } else if (st == 1) {
+      r.rc = ctx->chain_accept(lane);
+      r.st.fin_where = 1;
+      host_done = false;
+      if (r.rc != DCC_OK) {
+        r.err = ctx->last_error;
+        p->broken = true;
+        ctx->hs[1].built = false;
+      }
+    } else {
+      r.rc = ctx->pipe_finish(lane, true);
+      r.st.fin_where = 2;
+      if (r.rc != DCC_OK) r.err = ctx->last_error;
+    }
+  } else if (r.rc == DCC_OK && lane->run.fin_later) {
     // commit tn and the history append from the parent's state, in submit
     // order (central_finish, occ.cpp:248-294)
-    r.rc = ctx->pipe_finish(lane);
+    // (chained epochs behind it: the delta level stays where their finishes
+    // will write)
+    r.rc = ctx->pipe_finish(lane, chain_behind(p));
+    r.st.fin_where = 2;
     if (r.rc != DCC_OK) r.err = ctx->last_error;
-  } else {
+  } else if (r.rc == DCC_OK) {
     ctx->tnc += lane->run.n_cw;  // tnc advances in submit order (occ.cpp:283-284)
   }
+  if (host_done && !p->broken && chain_behind(p) && ctx->chain_set(lane, f.seq + 1) != DCC_OK) {
+    p->broken = true;  // the chained epochs behind it cannot be trusted to follow
+    ctx->hs[1].built = false;
+  }
   if (lane->run.fin_later && lane->run.app) p->app_in_flight--;
+  if (f.chain && f.app) {
+    p->app_res -= f.res;
+    p->app_max = std::max<uint64_t>(p->app_max, ctx->hs[1].last_app);
+  }
   lane->tnc = 0;
   p->done[f.ticket] = std::move(r);
 }
@@ -73,6 +142,7 @@ static void pipe_complete_front(dcc_ctx* ctx) {
 void dcc_pipe_drain(dcc_ctx* ctx) {
   if (!ctx || !ctx->pipe) return;
   while (!ctx->pipe->flight.empty()) pipe_complete_front(ctx);
+  ctx->pipe->broken = false;  // the next chained epoch starts fin_ctl afresh
 }
 
 void dcc_pipe_destroy(dcc_ctx* ctx) {
@@ -188,10 +258,32 @@ extern "C" int dcc_occ_submit_epoch(dcc_ctx* ctx, const dcc_batch* b, uint8_t* o
     return DCC_OK;
   }
   if (int e = pipe_lanes(ctx)) return e;
+  // Chained central_finish (DCC_OPT_PIPE_CHAIN): the epoch's commit tn and
+  // history append are enqueued behind its decision on its lane.  Its append
+  // needs room in the delta level reserved now (the level never moves while
+  // chained epochs are in flight): an estimate from the largest append seen,
+  // a sixteenth of the accesses before any; a finish that does not fit leaves
+  // the epoch to the host (pipe_finish).
+  const bool fin = out_tn || (b->flags & DCC_OCC_APPEND_HISTORY);
+  const bool chain = fin && ctx->pipe_chain;
+  const bool app = chain && (b->flags & DCC_OCC_APPEND_HISTORY);
+  const uint64_t res = app ? (p->app_max ? 2 * p->app_max : b->nnz / 16) + 4096 : 0;
+  if (p->broken) dcc_pipe_drain(ctx);
+  if (app && ctx->hs[1].m + p->app_res + res > ctx->hist_room()) dcc_pipe_drain(ctx);
   const int li = (int)(p->next_lane++ % p->lanes.size());
   dcc_ctx* lane = p->lanes[li];
   // the lane's previous epoch completes first (and every epoch before it)
   while (lane->run.active && !p->flight.empty()) pipe_complete_front(ctx);
+  // with nothing in flight the host's tnc and history are exact: fin_ctl
+  // starts from them (after any merge / rebuild the history is due, and room
+  // for the appends of a full pipeline)
+  const bool reset = chain && p->flight.empty();
+  if (reset && app) {
+    if (int e = ctx->hist_prepare()) return e;
+    const uint64_t want = ctx->hs[1].m + 4 * (p->lanes.size() + 1) * res;
+    if (want > ctx->hist_room())
+      if (int e = ctx->hist_grow_flat(ctx->hs[1], want)) return e;
+  }
   lane_options(ctx, lane);
   // device batches may have been written on the caller's stream
   if (hipEventRecord(p->ready, ctx->stream) != hipSuccess ||
@@ -208,7 +300,23 @@ extern "C" int dcc_occ_submit_epoch(dcc_ctx* ctx, const dcc_batch* b, uint8_t* o
     p->done[ticket] = std::move(r);
     return DCC_OK;
   }
-  p->flight.push_back({ticket, li});
+  OccPipe::Flight f{ticket, li, ++p->seq, false, false, 0};
+  if (ctx->pipe_chain) {
+    if (!lane->ev_done && hipEventCreateWithFlags(&lane->ev_done, hipEventDisableTiming) != hipSuccess)
+      return ctx->hip_fail(hipGetLastError(), "pipeline lane event");
+    if (chain && lane->run.fin_later) {
+      // behind the previous epoch's last work (its own finish, or its decision)
+      hipEvent_t after = p->flight.empty() ? nullptr : p->lanes[p->flight.back().lane]->ev_done;
+      f.chain = ctx->chain_enqueue(lane, f.seq, after, reset) == DCC_OK;
+      if (!f.chain) (void)hipGetLastError();  // the host finishes it at completion instead
+      f.app = f.chain && app;
+      f.res = f.app ? res : 0;
+      p->app_res += f.res;
+    }
+    if (hipEventRecord(lane->ev_done, lane->stream) != hipSuccess)
+      return ctx->hip_fail(hipGetLastError(), "pipeline lane event");
+  }
+  p->flight.push_back(f);
   return DCC_OK;
 }
 

@@ -1020,7 +1020,7 @@ __global__ __launch_bounds__(256) void k_sw_cout(SwCoutArgs a) {
   // epoch's committed-writer table (used only after the last level)
   if (blockIdx.x >= a.cout_grid) {
     const uint32_t b = blockIdx.x - a.cout_grid, nb = gridDim.x - a.cout_grid;
-    prep_body_hasw(a.prep_off, a.prep_n, a.prep_at, a.prep_nnz, a.hasw, a.prep_part, b, nb);
+    prep_body_hasw(a.prep_off, a.prep_n, a.prep_at, a.prep_nnz, a.hasw, a.prep_part, b, nb, a.prep_err);
     const uint4 e = make_uint4(~0u, ~0u, ~0u, ~0u);
     for (uint64_t q = (uint64_t)b * 256 + threadIdx.x; q < a.wclear_n16; q += (uint64_t)nb * 256)
       a.wclear[q] = e;

@@ -84,7 +84,7 @@ __device__ inline void prep_body(const uint32_t* __restrict__ off, uint64_t n, c
 __device__ inline void prep_body_hasw(const uint32_t* __restrict__ off, uint64_t n,
                                       const uint8_t* __restrict__ at, uint64_t nnz,
                                       uint8_t* __restrict__ hasw, PrepPart* __restrict__ part,
-                                      uint32_t blk, uint32_t nblk) {
+                                      uint32_t blk, uint32_t nblk, uint32_t* errw = nullptr) {
   __shared__ uint32_t sh[16];
   uint32_t len = 0, bad = 0, nw = 0;
   const uint64_t tid = (uint64_t)blk * blockDim.x + threadIdx.x;
@@ -117,6 +117,9 @@ __device__ inline void prep_body_hasw(const uint32_t* __restrict__ off, uint64_t
   const uint32_t tl = block_max_u32(len, sh);
   const uint32_t tb = block_max_u32(bad, sh);
   const uint32_t tw = block_sum_u32(nw, sh);
-  if (threadIdx.x == 0) part[blk] = PrepPart{tb, tl, tw, 0u};
+  if (threadIdx.x == 0) {
+    part[blk] = PrepPart{tb, tl, tw, 0u};
+    if (errw && ((tb & ERR_OFFSETS) || tl > MAX_TXN_LEN)) atomicOr(errw, ERR_PREP);
+  }
 }
 }  // namespace dcc

@@ -252,7 +252,9 @@ class Engine:
         its ticket; the batch arrays and outputs must stay alive and unchanged
         until ``occ_wait_epoch(ticket)``.  Results equal dcc_occ_validate_epoch
         on the epochs in submit order (commit tn and the history append
-        included: the context runs each epoch's central_finish as it completes)."""
+        included: each epoch's central_finish runs on its lane right behind its
+        decision once the epoch before it finished, DCC_OPT_PIPE_CHAIN, or the
+        context runs it as the epoch completes)."""
         b = batch.to_c(_abi.OCC_APPEND_HISTORY if append_history else 0)
         t = C.c_uint64(0)
         _check(lib.dcc_occ_submit_epoch(self._h, C.byref(b), _ptr(out_rc), _ptr(out_tn),

@@ -139,7 +139,9 @@ typedef struct dcc_stats {
   uint64_t n_survivors;
   uint32_t fallback;     /* sweep lists handed to the round solver (they stopped
                             shrinking); the decisions are the same                    */
-  uint32_t reserved2;
+  uint32_t fin_where;    /* pipelined epochs with commit tn / append (dcc_occ_wait_epoch):
+                            1 numbered on the device behind the decision (chained),
+                            2 by the context at completion; 0 otherwise              */
 } dcc_stats;
 
 /* ------------------------------------------------------------- context  */
@@ -211,6 +213,11 @@ int dcc_set_profiling(dcc_ctx* ctx, int enable);
                                   stream CU-masked), so a lane's serial passes never queue
                                   behind another lane's chip-wide kernels (L must divide
                                   n_CU / 8; otherwise the lanes stay unmasked)             */
+#define DCC_OPT_PIPE_CHAIN 15 /* pipelined epochs with commit tn / history append: 1 (default)
+                                 each lane numbers and appends its epoch on the device right
+                                 after deciding it, from a device copy of tnc and the append
+                                 position that the epochs advance in submit order; 0 the
+                                 context finishes each epoch on its lane's completion     */
 int dcc_set_option(dcc_ctx* ctx, int option, int64_t value);
 /* Pre-size device workspaces so a later call performs no allocation. */
 int dcc_reserve(dcc_ctx* ctx, uint64_t max_txn, uint64_t max_nnz);
@@ -275,10 +282,12 @@ int dcc_occ_validate_epoch(dcc_ctx* ctx, const dcc_batch* batch, uint8_t* out_rc
  * dcc_occ_validate_epoch on the epochs in submit order: under TS_CLOCK (no
  * history window) epochs of central_validate are
  * independent except for central_finish's commit counter and history
- * (occ.cpp:277-286), so each lane decides its epoch and the context runs the
- * epoch's central_finish -- commit tn (out_commit_tn) and the
- * DCC_OCC_APPEND_HISTORY append -- when the epoch completes, in submit
- * order.  An epoch that needs the epochs before it finished -- a window
+ * (occ.cpp:277-286), so each lane decides its epoch and its central_finish --
+ * commit tn (out_commit_tn) and the DCC_OCC_APPEND_HISTORY append -- runs in
+ * submit order: on the device right after the decision, once the epoch before
+ * it has finished (DCC_OPT_PIPE_CHAIN), or by the context when the epoch
+ * completes.  An epoch that fails after its finish ran on the device fails
+ * the epochs in flight behind it too (their numbering followed it).  An epoch that needs the epochs before it finished -- a window
  * against a non-empty history or against appends still in flight,
  * DCC_OCC_DEFER_FINISH -- or profiling, the round solver, or a multi-GPU or
  * key-sharded context first drains the pipeline and then runs

@@ -9,7 +9,10 @@ each lane's first epoch), host batches, out-of-order waits, an epoch asking
 for commit tn in the middle of the stream (numbered from the tnc of every
 epoch before it), streams of epochs with commit tn and the history append
 (central_finish, occ.cpp:277-286, run by the context as each epoch
-completes) checked tn by tn and pair by pair, a history window behind
+completes, or chained on the device behind each decision: DCC_OPT_PIPE_CHAIN)
+checked tn by tn and pair by pair -- also when chained finishes fall back to
+the host (epochs not final inside their graph, a malformed epoch in the
+stream, epochs without tn between them) -- a history window behind
 appends still in flight (it drains the lanes), a malformed batch (its error
 comes back from its own wait; the others are unaffected), the synchronous
 entry point draining the lanes first, and every epoch of a full-size (1M)
@@ -19,7 +22,7 @@ import pytest
 
 import _oracle as orc
 import deneva_amd as d
-from deneva_amd._abi import OPT_PIPE_PARTITION, OPT_PIPELINE, DccError
+from deneva_amd._abi import OPT_PIPE_CHAIN, OPT_PIPE_PARTITION, OPT_PIPELINE, OPT_SWEEP_LEVELS, DccError
 
 pytestmark = pytest.mark.gpu
 
@@ -30,6 +33,8 @@ def eng(engine):
     yield engine
     engine.set_option(OPT_PIPELINE, 2)
     engine.set_option(OPT_PIPE_PARTITION, 0)
+    engine.set_option(OPT_PIPE_CHAIN, 1)
+    engine.set_option(OPT_SWEEP_LEVELS, 0)
     engine.tnc = 0
 
 
@@ -194,8 +199,9 @@ def sorted_pairs(k, t):
     return k[o], t[o]
 
 
-@pytest.mark.parametrize("lanes,device", [(2, True), (4, True), (3, False)])
-def test_tn_and_history_stream(eng, lanes, device):
+@pytest.mark.parametrize("lanes,device,chain", [(2, True, 1), (4, True, 1), (3, False, 1), (4, True, 0),
+                                               (3, False, 0)])
+def test_tn_and_history_stream(eng, lanes, device, chain):
     """Every epoch of the stream wants commit tn and appends its committed
     writes (the reference's central_finish under TS_CLOCK); the lanes only
     decide, the context numbers and appends in submit order.  Each epoch's
@@ -204,6 +210,7 @@ def test_tn_and_history_stream(eng, lanes, device):
     lanes and sees all of them."""
     import torch
     eng.set_option(OPT_PIPELINE, lanes)
+    eng.set_option(OPT_PIPE_CHAIN, chain)
     eng.history_clear()
     try:
         bs = batches(40000, 7, seed=0x7A1)
@@ -225,8 +232,8 @@ def test_tn_and_history_stream(eng, lanes, device):
             eng.history_clear()
             eng.tnc = 0
             ts = [eng.occ_submit_epoch(x, r, t, append_history=True) for x, r, t in zip(ins, rcs, tns)]
-            for t in ts:
-                eng.occ_wait_epoch(t)
+            where = [eng.occ_wait_epoch(t)["fin_where"] for t in ts]
+            assert all(w == 2 for w in where) if not chain else where.count(1) >= 4, where
             for i, (r, t, (erc, etn, _)) in enumerate(zip(rcs, tns, exp)):
                 r = r.cpu().numpy() if device else r
                 t = t.cpu().numpy().view(np.uint64) if device else t
@@ -290,5 +297,130 @@ def test_full_size_tn_history_stream(eng):
         gk, gt = eng.history_export()
         wk, wt = sorted_pairs(np.concatenate(hk), np.concatenate(ht))
         assert np.array_equal(gk, wk) and np.array_equal(gt, wt)
+    finally:
+        eng.history_clear()
+
+
+def run_mixed(eng, bs, want, app, device):
+    """Submit every batch (want[i]: commit tn, app[i]: history append), wait
+    for all; returns (rcs, tns or None, errors)."""
+    import torch
+    if device:
+        ins = [b.to_torch("cuda:0") for b in bs]
+        rcs = [torch.empty(b.n_txn, dtype=torch.uint8, device="cuda:0") for b in bs]
+        tns = [torch.empty(b.n_txn, dtype=torch.int64, device="cuda:0") if w else None
+               for b, w in zip(bs, want)]
+    else:
+        ins = bs
+        rcs = [np.zeros(b.n_txn, np.uint8) for b in bs]
+        tns = [np.zeros(b.n_txn, np.uint64) if w else None for b, w in zip(bs, want)]
+    ts = [eng.occ_submit_epoch(x, r, t, append_history=a) for x, r, t, a in zip(ins, rcs, tns, app)]
+    errs, where = [], []
+    for t in ts:
+        try:
+            where.append(eng.occ_wait_epoch(t)["fin_where"])
+            errs.append(None)
+        except DccError as e:
+            where.append(None)
+            errs.append(e)
+    rcs = [r.cpu().numpy() if device else r for r in rcs]
+    tns = [None if t is None else (t.cpu().numpy().view(np.uint64) if device else t) for t in tns]
+    return rcs, tns, errs, where
+
+
+def check_mixed(eng, bs, want, app, rcs, tns, errs, where, skip=()):
+    """Against the oracle's serial chain (a skipped epoch leaves no trace)."""
+    tnc, hk, ht = 0, [np.zeros(0, np.uint64)], [np.zeros(0, np.uint64)]
+    for i, b in enumerate(bs):
+        if i in skip:
+            assert errs[i] is not None, f"epoch {i} should fail"
+            continue
+        assert errs[i] is None, f"epoch {i}: {errs[i]}"
+        rc, tn, tnc = orc.occ(b, tnc=tnc)
+        assert np.array_equal(rcs[i], rc), f"epoch {i}: rc"
+        if want[i]:
+            assert np.array_equal(tns[i], tn), f"epoch {i}: tn"
+        if app[i]:
+            k, t = committed_pairs(b, tn)
+            hk.append(k)
+            ht.append(t)
+    assert eng.tnc == tnc
+    gk, gt = eng.history_export()
+    wk, wt = sorted_pairs(np.concatenate(hk), np.concatenate(ht))
+    assert np.array_equal(gk, wk) and np.array_equal(gt, wt)
+
+
+@pytest.mark.parametrize("levels", [1, 2])
+def test_chained_finish_falls_back_when_not_final(eng, levels):
+    """One or two sweep levels per lane graph: the 1M-txn theta=0.9 epochs are
+    not decided inside their graphs (more levels follow a host round trip), so
+    every chained finish finds its epoch not final, or an epoch before it not
+    finished, and the context finishes them in submit order; then a second
+    pass at the default schedule numbers them on the device."""
+    eng.set_option(OPT_PIPELINE, 3)
+    eng.history_clear()
+    try:
+        bs = batches(1 << 20, 4, seed=0x3C1)
+        want, app = [True] * 4, [True] * 4
+        eng.set_option(OPT_SWEEP_LEVELS, levels)
+        eng.tnc = 0
+        out = run_mixed(eng, bs, want, app, True)
+        check_mixed(eng, bs, want, app, *out)
+        assert all(w == 2 for w in out[3]), out[3]  # every one finished by the host
+        eng.set_option(OPT_SWEEP_LEVELS, 0)
+        eng.history_clear()
+        eng.tnc = 0
+        out = run_mixed(eng, bs, want, app, True)
+        check_mixed(eng, bs, want, app, *out)
+        assert out[3].count(1) >= 3, out[3]  # numbered on the device (a lane's first may not be)
+    finally:
+        eng.set_option(OPT_SWEEP_LEVELS, 0)
+        eng.history_clear()
+
+
+@pytest.mark.parametrize("lanes", [2, 4])
+def test_chained_finish_mixed_stream(eng, lanes):
+    """Epochs with commit tn and the append, commit tn only, and neither, in
+    one stream: the ones the host completes (no tn) move the device tnc past
+    them for the chained finishes behind them."""
+    eng.set_option(OPT_PIPELINE, lanes)
+    eng.history_clear()
+    try:
+        bs = batches(50000, 9, seed=0x4D1)
+        want = [True, False, True, True, False, False, True, True, True]
+        app = [True, False, False, True, False, False, True, False, True]
+        for rep in range(2):
+            eng.history_clear()
+            eng.tnc = 0
+            out = run_mixed(eng, bs, want, app, rep == 0)
+            check_mixed(eng, bs, want, app, *out)
+            assert all((w == 0) == (not t) for w, t in zip(out[3], want)), out[3]
+            assert 1 in out[3], out[3]
+    finally:
+        eng.history_clear()
+
+
+def test_chained_finish_malformed_epoch_in_stream(eng):
+    """A malformed epoch among chained ones: its error at its own wait, no
+    trace in tnc or the history; the epochs behind it numbered as if it had
+    not been submitted."""
+    eng.set_option(OPT_PIPELINE, 3)
+    eng.history_clear()
+    try:
+        bs = batches(20000, 6, seed=0x5E1)
+        bad = d.EpochBatch(bs[2].offsets.copy(), bs[2].keys, bs[2].acctype)
+        bad.offsets[100] = bad.offsets[101] + 1  # offsets decrease
+        bs[2] = bad
+        want, app = [True] * 6, [True] * 6
+        eng.tnc = 0
+        out = run_mixed(eng, bs, want, app, False)
+        check_mixed(eng, bs, want, app, *out, skip=(2,))
+        # and the stream goes on chained behind it
+        eng.history_clear()
+        eng.tnc = 0
+        good = batches(20000, 6, seed=0x5E1)
+        out = run_mixed(eng, good, want, app, False)
+        check_mixed(eng, good, want, app, *out)
+        assert 1 in out[3], out[3]
     finally:
         eng.history_clear()
