@@ -380,7 +380,11 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1, const SwShard* shl
   // small epoch's grid (C2: 256 workgroups) would otherwise be spread over a
   // quarter of the CUs; the workgroups past the tiles clear and leave
   // (measured neutral on C2, 0.132 ms either way: the clears overlap)
-  const unsigned fgrid = (unsigned)std::max<uint64_t>(1, 4ull * n_cu);
+  static const unsigned fgrid_ov = [] {  // DCC_SW_FGRID: experiments
+    const char* e = DCC_ENV("DCC_SW_FGRID");
+    return e ? (unsigned)atoi(e) : 0u;
+  }();
+  const unsigned fgrid = fgrid_ov ? fgrid_ov : (unsigned)std::max<uint64_t>(1, 4ull * n_cu);
   uint64_t* gtab0 = (uint64_t*)sw_gtab.p;
   uint32_t* cbits_d = (uint32_t*)sw_ckeys.p;
   uint32_t* bloom_d = cbits_d + (1u << SW_GBITS_MAX) / 32;
