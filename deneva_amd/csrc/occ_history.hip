@@ -150,7 +150,10 @@ __device__ inline void fin_publish(FinLb* e, uint64_t v, bool incl, uint32_t tag
 // key of a step loaded before any is used (one memory round trip per step
 // instead of one per access).
 constexpr uint32_t FIN_U = 8;
-constexpr uint32_t FIN_T = 2;  // k_fin: consecutive txns per thread
+#ifndef DCC_FIN_T
+#define DCC_FIN_T 2
+#endif
+constexpr uint32_t FIN_T = DCC_FIN_T;  // k_fin: consecutive txns per thread
 __device__ inline void fin_step(const OccFinArgs& a, uint64_t x, uint64_t o1, uint8_t (&ty)[FIN_U],
                                 uint64_t (&k)[FIN_U]) {
 #pragma unroll

@@ -1,6 +1,6 @@
-"""Level-0 filter timing of the headline epoch (measurement aid; experiments
+"""Sweep stamps of one YCSB theta=0.9 epoch (measurement aid; experiments
 build with DCC_SW_DEBUG=1 prints the per-level stamps to stderr):
-  DENEVA_AMD_LIB=deneva_amd/libdcc_exp.so DCC_SW_DEBUG=1 python tools/filter_probe.py"""
+  DENEVA_AMD_LIB=deneva_amd/libdcc_exp.so DCC_SW_DEBUG=1 python tools/filter_probe.py [n_txn]"""
 import os
 import sys
 
@@ -12,7 +12,8 @@ import deneva_amd as d  # noqa: E402
 
 def main():
     eng = d.Engine(0)
-    b = d.gen_ycsb(n_txn=1 << 20, zipf_theta=0.9)
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
+    b = d.gen_ycsb(n_txn=n, zipf_theta=0.9)
     db = b.to_torch("cuda:0")
     rc = torch.empty(b.n_txn, dtype=torch.uint8, device="cuda:0")
     for i in range(4):
