@@ -984,7 +984,11 @@ int dcc_ctx::sweep_ro(const DevBatch& d0, bool big, bool scan, uint64_t nnz_w, c
   launch_sw_wall(wa, (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(scan ? 4096 : 256, (d.n + 255) / 256)),
                  stream);
   SwRoArgs ra{(const RoEnt*)sw_ro.p, wctl + 2, d.keys, wt, (uint8_t*)state.p, full ? full->off : nullptr};
-  launch_sw_ro(ra, (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(1024, (d.n + 255) / 256)), stream);
+  static const uint64_t ro_grid = [] {  // DCC_SW_ROGRID: experiments
+    const char* e = DCC_ENV("DCC_SW_ROGRID");
+    return e && atoi(e) > 0 ? (uint64_t)atoi(e) : 1024ull;
+  }();
+  launch_sw_ro(ra, (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(ro_grid, (d.n + 255) / 256)), stream);
   CK(hipGetLastError());
   return DCC_OK;
 }

@@ -337,7 +337,10 @@ struct SwSeqArgs {
   uint32_t* cw_count;
 };
 // prep workgroups beside the level-0 committed-set listing (k_sw_cout)
-constexpr unsigned SW_PREP_BLOCKS = 1024;
+#ifndef DCC_SW_PREP_BLOCKS
+#define DCC_SW_PREP_BLOCKS 1024
+#endif
+constexpr unsigned SW_PREP_BLOCKS = DCC_SW_PREP_BLOCKS;
 struct SwCoutArgs {
   SwList in;
   const uint32_t* aent;
