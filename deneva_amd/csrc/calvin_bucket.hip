@@ -292,7 +292,9 @@ __global__ __launch_bounds__(256) void k_cb_scan(uint32_t* __restrict__ cnt, uin
 // LDS row; the waves' counts become per-(bucket, wave) bases of a
 // bucket-ordered LDS staging, written out as one run per bucket at the
 // bucket's cursor.  Workgroup 0 also stores the buckets' bases for the
-// bucket pass.
+// bucket pass.  Its barriers are LDS-only: the workgroup shares nothing
+// through global memory, so a sub-tile's stores and the next sub-tile's
+// loads stay in flight across them.
 template <uint32_t NB>  // bucket bits at compile time (0: bb at run time)
 __global__ __launch_bounds__(CB_PT) void k_cb_part(CbSrc s, uint32_t bb, const uint32_t* __restrict__ cnt,
                                                    const uint32_t* __restrict__ tot,
@@ -345,7 +347,7 @@ __global__ __launch_bounds__(CB_PT) void k_cb_part(CbSrc s, uint32_t bb, const u
       ne = cb_wave_elems<true>(s, (uint32_t)q0, nq, (uint32_t*)s_stg + wv * 1024,
                                (uint32_t*)s_stg + CB_SUB + wv * 1024, s_m[wv], e);
     }
-    __syncthreads();
+    lds_barrier();
     uint16_t loc[16];
     uint16_t* my = s_wc[wv];
 #pragma unroll
@@ -359,7 +361,7 @@ __global__ __launch_bounds__(CB_PT) void k_cb_part(CbSrc s, uint32_t bb, const u
       // the bucket's first lane advances the count (same wave: in order)
       if (act && lr == 0) my[b] = (uint16_t)(before + (uint32_t)__builtin_popcountll(peers));
     }
-    __syncthreads();
+    lds_barrier();
     uint32_t n_sub;
     {
       uint32_t ls = 0;
@@ -379,7 +381,7 @@ __global__ __launch_bounds__(CB_PT) void k_cb_part(CbSrc s, uint32_t bb, const u
         s_cur[b] += run - lb;
       }
     }
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (uint32_t it = 0; it < 16; it++) {
       if (it * 64 + lane < ne) {
@@ -387,12 +389,12 @@ __global__ __launch_bounds__(CB_PT) void k_cb_part(CbSrc s, uint32_t bb, const u
         s_stg[my[b] + loc[it]] = e[it];
       }
     }
-    __syncthreads();
+    lds_barrier();
     for (uint32_t j = tid; j < n_sub; j += CB_PT) {
       const uint64_t x = s_stg[j];
       if (!(CB_VAR(s.var, 1u))) out[s_gof[(uint32_t)(x >> 32) & bmask] + j] = x;
     }
-    __syncthreads();
+    lds_barrier();
   }
 }
 
