@@ -424,3 +424,26 @@ def test_chained_finish_malformed_epoch_in_stream(eng):
         assert 1 in out[3], out[3]
     finally:
         eng.history_clear()
+
+
+def test_chained_finish_out_of_order_waits_and_lane_change(eng):
+    """Chained epochs waited newest first, then the lane count changed with
+    chained epochs in flight (they complete on their lanes first), then more
+    chained epochs on the new lanes, CU-partitioned: one serial chain."""
+    eng.set_option(OPT_PIPELINE, 3)
+    eng.history_clear()
+    try:
+        bs = batches(30000, 8, seed=0x6A1)
+        want, app = [True] * 8, [True, True, False, True, True, True, False, True]
+        eng.tnc = 0
+        rcs = [np.zeros(b.n_txn, np.uint8) for b in bs]
+        tns = [np.zeros(b.n_txn, np.uint64) for b in bs]
+        ts = [eng.occ_submit_epoch(bs[i], rcs[i], tns[i], append_history=app[i]) for i in range(4)]
+        eng.set_option(OPT_PIPELINE, 4)
+        eng.set_option(OPT_PIPE_PARTITION, 1)
+        ts += [eng.occ_submit_epoch(bs[i], rcs[i], tns[i], append_history=app[i]) for i in range(4, 8)]
+        where = {t: eng.occ_wait_epoch(t)["fin_where"] for t in reversed(ts)}
+        check_mixed(eng, bs, want, app, rcs, tns, [None] * 8, [where[t] for t in ts])
+        assert 1 in where.values(), where
+    finally:
+        eng.history_clear()
