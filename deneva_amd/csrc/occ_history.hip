@@ -151,9 +151,13 @@ __device__ inline void fin_publish(FinLb* e, uint64_t v, bool incl, uint32_t tag
 // instead of one per access).
 constexpr uint32_t FIN_U = 8;
 #ifndef DCC_FIN_T
-#define DCC_FIN_T 2
+#define DCC_FIN_T 4
 #endif
 constexpr uint32_t FIN_T = DCC_FIN_T;  // k_fin: consecutive txns per thread
+#ifndef DCC_FIN_B
+#define DCC_FIN_B 512
+#endif
+constexpr uint32_t FB = DCC_FIN_B;  // k_fin: threads per workgroup
 __device__ inline void fin_step(const OccFinArgs& a, uint64_t x, uint64_t o1, uint8_t (&ty)[FIN_U],
                                 uint64_t (&k)[FIN_U]) {
 #pragma unroll
@@ -184,10 +188,10 @@ __device__ inline uint32_t fin_writes(uint64_t t, const OccFinArgs& a, uint64_t&
   return c;
 }
 
-// block-wide exclusive scans of two counters (1024 threads); returns both totals
+// block-wide exclusive scans of two counters (FB threads); returns both totals
 __device__ inline void block_excl_scan2(uint32_t v0, uint32_t v1, uint32_t& e0, uint32_t& e1,
                                         uint32_t& t0, uint32_t& t1) {
-  __shared__ uint32_t s_w[2][HB / 64];
+  __shared__ uint32_t s_w[2][FB / 64];
   const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   uint32_t x0 = v0, x1 = v1;
 #pragma unroll
@@ -206,7 +210,7 @@ __device__ inline void block_excl_scan2(uint32_t v0, uint32_t v1, uint32_t& e0, 
   uint32_t b0 = 0, b1 = 0;
   t0 = t1 = 0;
 #pragma unroll
-  for (uint32_t q = 0; q < HB / 64; q++) {
+  for (uint32_t q = 0; q < FB / 64; q++) {
     if (q < w) {
       b0 += s_w[0][q];
       b1 += s_w[1][q];
@@ -218,7 +222,7 @@ __device__ inline void block_excl_scan2(uint32_t v0, uint32_t v1, uint32_t& e0, 
   e1 = b1 + x1 - v1;
 }
 
-__global__ __launch_bounds__(HB, 8) void k_fin(OccFinArgs a) {  // two workgroups per CU
+__global__ __launch_bounds__(FB, 8) void k_fin(OccFinArgs a) {
   __shared__ unsigned long long s_mx;
   __shared__ uint64_t s_pre;
   __shared__ uint32_t s_last, s_id;
@@ -247,7 +251,7 @@ __global__ __launch_bounds__(HB, 8) void k_fin(OccFinArgs a) {  // two workgroup
   const uint32_t bid = s_id;
   // FIN_T consecutive txns per thread (one generation of workgroups fits the
   // chip: a workgroup's chain of round trips is paid once, not twice)
-  const uint64_t t_0 = ((uint64_t)bid * HB + threadIdx.x) * FIN_T;
+  const uint64_t t_0 = ((uint64_t)bid * FB + threadIdx.x) * FIN_T;
   uint64_t* app_k = dy->app_k;
   uint64_t* app_t = dy->app_t;
   uint32_t c[FIN_T], w[FIN_T];
@@ -354,7 +358,7 @@ __global__ __launch_bounds__(HB, 8) void k_fin(OccFinArgs a) {  // two workgroup
   const HistInsert ins = dy->ins;
   if (ins.hash && t1 && P != ~0ull && room && !(a.var & 1u)) {
     __syncthreads();  // the pairs written above
-    for (uint32_t i = threadIdx.x; i < t1; i += HB) hist_insert(ins, wbase + i, app_k[wbase + i], app_t[wbase + i]);
+    for (uint32_t i = threadIdx.x; i < t1; i += FB) hist_insert(ins, wbase + i, app_k[wbase + i], app_t[wbase + i]);
   }
   // the last workgroup to finish: totals to pinned memory (every value it
   // reads was written with device-scope atomics, acknowledged before the
@@ -417,8 +421,8 @@ void launch_fin(const OccFinArgs& a0, hipStream_t st) {
   // timing variants, wrong results by design: 1 no chain pushes, 2 no
   // look-back wait, 4 no write-set emission, 8 no tn stores
   if (const char* e = DCC_ENV("DCC_FIN_VAR")) a.var = (uint32_t)atoi(e);
-  const uint64_t nb = (a.n + HB * FIN_T - 1) / (HB * FIN_T);
-  k_fin<<<(unsigned)(nb ? nb : 1), HB, 0, st>>>(a);
+  const uint64_t nb = (a.n + FB * FIN_T - 1) / (FB * FIN_T);
+  k_fin<<<(unsigned)(nb ? nb : 1), FB, 0, st>>>(a);
 }
 
 void launch_fin_prep(const uint32_t* src, OccDyn* dyn, const FinCtl* ctl, uint64_t seq, hipStream_t st) {
@@ -428,7 +432,7 @@ void launch_fin_ctl_set(FinCtl* ctl, uint64_t tnc, uint64_t hist_m, uint64_t seq
   k_fin_ctl_set<<<1, 1, 0, st>>>(ctl, tnc, hist_m, seq);
 }
 
-uint64_t fin_part_bytes(uint64_t n) { return (((n + HB * FIN_T - 1) / (HB * FIN_T)) + 2) * sizeof(FinLb); }
+uint64_t fin_part_bytes(uint64_t n) { return (((n + FB * FIN_T - 1) / (FB * FIN_T)) + 2) * sizeof(FinLb); }
 
 // A host copy of k_fin's look-back words (fin_part_bytes(n) bytes) after a
 // launch with `tag`, summarised for the error message of a totals mismatch:
@@ -437,7 +441,7 @@ uint64_t fin_part_bytes(uint64_t n) { return (((n + HB * FIN_T - 1) / (HB * FIN_
 // aggregate (a foreign or stale prefix taken by the look-back).
 std::string fin_diag(const void* words, uint64_t n, uint32_t tag) {
   const FinLb* lb = (const FinLb*)((const FinTail*)words + 1);
-  const uint64_t nb = std::max<uint64_t>(1, (n + HB * FIN_T - 1) / (HB * FIN_T));
+  const uint64_t nb = std::max<uint64_t>(1, (n + FB * FIN_T - 1) / (FB * FIN_T));
   uint64_t stale = 0, first_stale = ~0ull, bad = ~0ull;
   uint32_t stale_tag = 0;
   uint64_t prev = 0;

@@ -4,7 +4,7 @@
 set -o pipefail
 O=gpurun_out/fint
 mkdir -p $O
-for v in fin4 fin8 dcc; do
+for v in ${VARS:-fin4 fin8 dcc}; do
   lib=$PWD/deneva_amd/libdcc_${v}.so
   [ $v = dcc ] && lib=$PWD/deneva_amd/libdcc.so
   DENEVA_AMD_LIB=$lib timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_pipeline.py tests/test_gpu_occ_finish.py tests/test_gpu_history.py > $O/t_$v.txt 2>&1 || exit 1
