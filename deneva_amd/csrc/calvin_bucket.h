@@ -26,6 +26,7 @@ struct CbPlan {
   uint32_t R;      // reservation-counter replicas (each with its own pair region)
   uint32_t wt;     // txns per partition wave (1024 / the longest txn)
   uint64_t span;   // requests per window at most (2^tsh * the longest txn)
+  uint32_t hashed; // lbits > 13: the carry table is hashed on the row bits (tagged words)
   // workspace sizes in bytes
   uint64_t elem_bytes, out_bytes, cnt_bytes, small_bytes;
 };
@@ -51,7 +52,9 @@ struct CbArgs {
   // outputs
   uint32_t* group;
   uint8_t* rc;
+  uint32_t* err;  // CB_ERR_TAB: a hashed carry table ran out of room (redo on the sort path)
 };
+constexpr uint32_t CB_ERR_TAB = 1u << 12;
 
 // Enqueues the path on st.  ev[0..1] (optional) are recorded after the
 // partition and after the bucket pass.

@@ -14,7 +14,8 @@
 //                LDS radix sort of the chunk by the row bits above the bucket
 //                bits (stable, so a row's requests stay in sequence order),
 //                the grant-group scan with each row's state carried across
-//                chunks in an LDS table indexed by those bits, and the
+//                chunks in an LDS table indexed by those bits (hashed on them
+//                past 13 bits, up to 17: TPC-C), and the
 //                (request, group) pairs staged by output window and appended
 //                to the window's region (one returning atomic per window and
 //                chunk, on one of R replicated counters)
@@ -50,7 +51,11 @@ constexpr uint32_t CB_PT = 512;                 // count / partition threads (8 
 constexpr uint32_t CB_SUB = CB_PT * 16;         // requests per partition sub-tile (LDS staging)
 constexpr uint32_t CB_NSUB = 8;                 // sub-tiles per tile
 constexpr uint32_t CB_BB_MAX = 11;              // bucket bits
-constexpr uint32_t CB_LB_MAX = 13;              // row bits inside a bucket
+constexpr uint32_t CB_LB_MAX = 13;              // row bits inside a bucket (direct carry table)
+constexpr uint32_t CB_LB_HASH_MAX = 17;         // ... with the hashed carry table
+constexpr uint32_t CB_HSLOTS = 1u << CB_LB_MAX; // hashed table slots (the same 32 KiB of LDS)
+constexpr uint32_t CB_HWALK = 64;               // longest probe of a hashed slot
+constexpr uint32_t CB_HCNT_MAX = (1u << 12) - 1;  // group counts a tagged word holds (below)
 constexpr uint32_t CB_BT = 256;                 // bucket workgroup
 constexpr uint32_t CB_IT = 16;                  // requests per thread per chunk
 constexpr uint32_t CB_CHUNK = CB_BT * CB_IT;
@@ -63,6 +68,47 @@ constexpr uint32_t NOTXN = 0xFFFFFFFFu;
 // carry-table word: bit 0 "the row's last request is the chunk's last txn",
 // bits 1-2 its lock type (CV_NONE: row not seen yet), bits 3.. its group count
 constexpr uint32_t TAB_EMPTY = CV_NONE << 1;
+// Hashed carry table (row bits 14-17: TPC-C's packed keys are 28 bits at 128
+// warehouses): the word is tagged -- row bits 31..15, group count 14..3 -- in
+// open addressing over the same 8,192 LDS words; a bucket's rows never leave
+// it, so linear probing needs no deletion.  A row whose probe runs past
+// CB_HWALK slots or whose group count outgrows 12 bits raises CB_ERR_TAB and
+// the host redoes the epoch on the sort path.
+constexpr uint32_t TAB_HEMPTY = 0xFFFFFFFFu;
+__device__ inline uint32_t cb_hslot(uint32_t r) { return (r * 0x9E3779B1u) >> (32 - CB_LB_MAX); }
+// the carry word of row r (TAB_EMPTY: not seen in this bucket yet), from its
+// first probe w at slot h
+__device__ inline uint32_t cb_hget(const uint32_t* t, uint32_t r, uint32_t h, uint32_t w) {
+  for (uint32_t q = 1; w != TAB_HEMPTY && (w >> 15) != r && q < CB_HWALK; q++) {
+    h = (h + 1) & (CB_HSLOTS - 1);
+    w = *(volatile const uint32_t*)&t[h];
+  }
+  return (w == TAB_HEMPTY || (w >> 15) != r) ? TAB_EMPTY : (w & 0x7FFFu);
+}
+// store row r's carry word v (untagged); returns its slot (CB_HSLOTS: no room)
+__device__ inline uint32_t cb_hput(uint32_t* t, uint32_t r, uint32_t v, uint32_t* err) {
+  if ((v >> 3) >= CB_HCNT_MAX) {
+    atomicOr(err, CB_ERR_TAB);
+    return CB_HSLOTS;
+  }
+  const uint32_t wn = (r << 15) | v;
+  uint32_t h = cb_hslot(r);
+  for (uint32_t q = 0; q < CB_HWALK;) {
+    const uint32_t w = *(volatile uint32_t*)&t[h];
+    if (w == TAB_HEMPTY) {
+      if (atomicCAS(&t[h], TAB_HEMPTY, wn) == TAB_HEMPTY) return h;
+      continue;  // another row took the slot: look at it again
+    }
+    if ((w >> 15) == r) {  // this row's slot (one writer per row and chunk)
+      t[h] = wn;
+      return h;
+    }
+    h = (h + 1) & (CB_HSLOTS - 1);
+    q++;
+  }
+  atomicOr(err, CB_ERR_TAB);
+  return CB_HSLOTS;
+}
 
 __device__ inline uint32_t stg_ix(uint32_t p) { return p + (p >> 5); }
 
@@ -407,6 +453,7 @@ struct CbBucket {
   uint64_t span;
   uint32_t* gcnt;  // [R][ndig]
   uint64_t* out;   // [R][ndig][span]
+  uint32_t* err;   // CB_ERR_TAB
   uint32_t var;    // DCC_CB_VARIANT (wrong results): 8 no radix passes, 16 no pair stores,
                    // 32 no grant-group scan, 64 no staging/output
 };
@@ -446,6 +493,7 @@ __device__ inline uint32_t gl_block_excl_lds(uint32_t v, uint32_t* s_w, uint32_t
   return gl_combine(wp, lane ? ex_in : GL_ID);
 }
 
+template <bool H>  // the hashed carry table (row bits > CB_LB_MAX)
 __global__ __launch_bounds__(CB_BT) void k_cb_bucket(CbBucket a) {
   __shared__ uint32_t s_tab[1u << CB_LB_MAX];
   __shared__ uint64_t s_stg[CB_STG];
@@ -460,8 +508,8 @@ __global__ __launch_bounds__(CB_BT) void k_cb_bucket(CbBucket a) {
   if (size == 0) return;  // whole workgroup
   const uint64_t base = a.bbase[blockIdx.x];
   const uint32_t r = blockIdx.x % CB_R;
-  const uint32_t ntab = 1u << a.lbits;
-  for (uint32_t i = tid; i < ntab; i += CB_BT) s_tab[i] = TAB_EMPTY;
+  const uint32_t ntab = H ? CB_HSLOTS : 1u << a.lbits;
+  for (uint32_t i = tid; i < ntab; i += CB_BT) s_tab[i] = H ? TAB_HEMPTY : TAB_EMPTY;
   for (uint32_t d = tid; d < a.ndig; d += CB_BT) s_dc[d] = 0;
   const uint32_t npass = (CB_VAR(a.var, 8u)) ? 0u : (a.lbits + 3) / 4;
   const uint32_t dpt = (a.ndig + CB_BT - 1) / CB_BT;  // windows per thread (<= 3)
@@ -572,8 +620,20 @@ __global__ __launch_bounds__(CB_BT) void k_cb_bucket(CbBucket a) {
       // every item's carry word read up front (one LDS round trip, not one per
       // row start inside the branches below)
       uint32_t cw[CB_IT];
+      if (H) {  // first probes in one round trip, then the rare longer walks
+        uint32_t hs[CB_IT];
 #pragma unroll
-      for (uint32_t i = 0; i < CB_IT; i++) cw[i] = s_tab[min((uint32_t)(e[i] >> 32) >> bsh, ntab - 1)];
+        for (uint32_t i = 0; i < CB_IT; i++) {
+          hs[i] = cb_hslot((uint32_t)(e[i] >> 32) >> bsh);
+          cw[i] = s_tab[hs[i]];
+        }
+#pragma unroll
+        for (uint32_t i = 0; i < CB_IT; i++)
+          cw[i] = p0 + i < nc ? cb_hget(s_tab, (uint32_t)(e[i] >> 32) >> bsh, hs[i], cw[i]) : TAB_EMPTY;
+      } else {
+#pragma unroll
+        for (uint32_t i = 0; i < CB_IT; i++) cw[i] = s_tab[min((uint32_t)(e[i] >> 32) >> bsh, ntab - 1)];
+      }
       // The thread's 16 requests folded left to right into the gl state
       // (flag, ft, lt, cnt) in separate registers; per request the inclusive
       // local count lc[i], and bit masks: a row start at or before i (startm),
@@ -645,8 +705,12 @@ __global__ __launch_bounds__(CB_BT) void k_cb_bucket(CbBucket a) {
           if (p0 + i + 1 == nc || (uint32_t)(ne >> 32) >> bsh != lk) {
             const uint32_t tx = (uint32_t)e[i] >> 7;
             const uint32_t lt_i = (ltp >> (2 * i)) & 3u;
-            s_tab[lk] = (cnt << 3) | ((lt_i != CV_NONE ? lt_i : plt) << 1) | (tx == t_last ? 1u : 0u);
-            if (tx == t_last) s_fl[pc][atomicAdd(&s_fln[pc], 1u)] = lk;  // <= 64: one txn's requests
+            const uint32_t v = (cnt << 3) | ((lt_i != CV_NONE ? lt_i : plt) << 1) | (tx == t_last ? 1u : 0u);
+            uint32_t slot = lk;
+            if (H) slot = cb_hput(s_tab, lk, v, a.err);
+            else s_tab[lk] = v;
+            // <= 64 flagged: one txn's requests
+            if (tx == t_last && slot < ntab) s_fl[pc][atomicAdd(&s_fln[pc], 1u)] = slot;
           }
         }
       }
@@ -774,10 +838,11 @@ bool cb_plan(uint64_t n, uint64_t nnz, uint32_t ulen, uint32_t maxlen, uint32_t 
   // uniform txns (ulen requests each), or ragged ones of at most maxlen
   const uint32_t len = ulen ? ulen : maxlen;
   if (!len || len > 64 || nnz == 0 || (ulen && nnz != n * ulen) || nnz >= 0xFFFFFFFFull) return false;
-  if (kbits > CB_BB_MAX + CB_LB_MAX) return false;
+  if (kbits > CB_BB_MAX + CB_LB_HASH_MAX) return false;
   CbPlan q{};
   q.bb = std::min(CB_BB_MAX, kbits);
   q.lbits = kbits - q.bb;
+  q.hashed = q.lbits > CB_LB_MAX ? 1u : 0u;
   q.tsh = 0;
   while ((2ull << q.tsh) * len <= CB_WIN && (ulen || q.tsh < CB_TSH_RAGGED)) q.tsh++;
   q.span = (1ull << q.tsh) * len;
@@ -818,8 +883,11 @@ hipError_t cb_run(const CbPlan& p, const CbArgs& a, hipStream_t st, hipEvent_t e
   else
     k_cb_part<0><<<8 * ((p.ntile + 7) / 8), CB_PT, 0, st>>>(s, p.bb, a.cnt, tot, bbase, a.elems, p.ntile);
   if (ev_part && (e = hipEventRecord(ev_part, st)) != hipSuccess) return e;
-  k_cb_bucket<<<B, CB_BT, 0, st>>>(
-      CbBucket{a.elems, tot, bbase, p.bb, p.lbits, p.tsh, p.ndig, p.span, gcnt, a.out, var});
+  const CbBucket ba{a.elems, tot, bbase, p.bb, p.lbits, p.tsh, p.ndig, p.span, gcnt, a.out, a.err, var};
+  if (p.hashed)
+    k_cb_bucket<true><<<B, CB_BT, 0, st>>>(ba);
+  else
+    k_cb_bucket<false><<<B, CB_BT, 0, st>>>(ba);
   if (ev_bucket && (e = hipEventRecord(ev_bucket, st)) != hipSuccess) return e;
   k_cb_put<<<p.ndig, 1024, 0, st>>>(a.out, gcnt, p.ndig, p.span, (uint32_t)a.n, a.ulen, p.tsh, a.off,
                                     (uint32_t)a.nnz, a.group, a.rc);

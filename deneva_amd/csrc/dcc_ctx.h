@@ -299,6 +299,7 @@ struct dcc_ctx {
   uint32_t pipe_lanes = 3;  // DCC_OPT_PIPELINE
   uint32_t pipe_part = 0;   // DCC_OPT_PIPE_PARTITION
   int cv_path = 0;          // DCC_OPT_CALVIN_PATH: 0 auto, 1 sort, 2 bucket
+  bool cb_hash_off = false; // a hashed bucket carry table overflowed: sort path for such epochs
   // DCC_OCC_DEFER_FINISH: the decided epoch waiting for its global RC
   bool fin_pending = false;
   DevBatch fin_d;

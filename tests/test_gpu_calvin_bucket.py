@@ -4,12 +4,15 @@ LDS sort + grant-group scan with each row's state carried from chunk to chunk,
 and the windowed group write-out with readiness) against the oracle
 (`orc.calvin`, the Row_lock CALVIN replay restated: row_lock.cpp:78-81,
 152-170, 317-357).  DCC_OPT_CALVIN_PATH=2 takes the path at every size it applies
-to (txn lengths <= 64, uniform or ragged, packed keys <= 24 bits); the cases cover one-row
+to (txn lengths <= 64, uniform or ragged, packed keys <= 28 bits -- past 24
+the carry table is hashed on the row bits, TPC-C's canonical keys among
+them); the cases cover one-row
 buckets, a single key, duplicates of a row inside a txn (also where a txn
 straddles a chunk boundary), hot rows spanning many chunks, sequencer orders
 with ties, txn lengths 1..64, ragged txns (random lengths with empty txns, a
-key-sharded rank's share of C4), and the fallback for wider keys (TPC-C's
-canonical keys pack to 26 bits: the sort path, test_gpu_calvin.py)."""
+key-sharded rank's share of C4), 25- to 28-bit keys and TPC-C on the hashed
+carry table, a bucket with more rows than that table holds (the epoch is
+redone on the sort path), and the fallback for wider keys."""
 import numpy as np
 import pytest
 
@@ -273,3 +276,48 @@ def test_c4_interleaved_origins_full_size(engine):
     assert st["fallback"] == 1
     assert np.array_equal(np.asarray(g).astype(np.uint32), eg)
     assert np.array_equal(np.asarray(rc), erc)
+
+
+@pytest.mark.parametrize("n,L,kbits,order", [(20000, 16, 25, True), (30000, 8, 26, False),
+                                             (50000, 16, 28, True), (4000, 64, 27, True)])
+def test_hashed_carry_table(engine, bucket, n, L, kbits, order):
+    """Packed keys of 25-28 bits: row bits 14-17 above the 11 bucket bits,
+    the carry table hashed on them."""
+    rng = np.random.default_rng(kbits * 7 + L)
+    b = uniform_batch(rng, n, L, 1 << kbits, order=order)
+    b.keys[0] = (1 << kbits) - 1  # every bit varies: the packing keeps kbits
+    b.keys[1] = 0
+    check(engine, b)
+    _, _, _, st = engine.calvin_order_epoch(b, want_group=True)
+    assert st["fallback"] == 1, "not on the bucket path"
+
+
+@pytest.mark.parametrize("num_wh,n", [(4, 50000), (128, 262144)])
+def test_tpcc_on_bucket_path(engine, bucket, num_wh, n):
+    """Canonical TPC-C keys (28 bits packed at 128 warehouses, ragged
+    NewOrder / Payment txns) on the bucket path with the hashed carry table."""
+    b = d.gen_tpcc(n_txn=n, num_wh=num_wh)
+    check(engine, b)
+    _, _, _, st = engine.calvin_order_epoch(b, want_group=True)
+    assert st["fallback"] == 1, "not on the bucket path"
+
+
+def test_hashed_table_overflow_redoes_on_sort_path():
+    """20,000 rows in one bucket (more than the 8,192-slot hashed table): the
+    epoch is redone on the sort path, exactly, and the context keeps the sort
+    path for such epochs (a fresh context: the switch is per context)."""
+    eng = d.Engine(0)
+    eng.set_option(d._abi.OPT_CALVIN_PATH, 2)
+    rng = np.random.default_rng(33)
+    n, L = 20000, 4
+    rows = rng.permutation(1 << 15)[: n * L // 2].astype(np.uint64)
+    keys = np.concatenate([(rows << np.uint64(11)) | np.uint64(5),
+                           rng.integers(0, 1 << 26, size=n * L - rows.size).astype(np.uint64)])
+    keys[-1] = (1 << 26) - 1  # 26 varying bits: hashed
+    keys[-2] = 0
+    at = np.where(rng.random(n * L) < 0.5, WR, RD).astype(np.uint8)
+    off = (np.arange(n + 1) * L).astype(np.uint32)
+    b = d.EpochBatch(off, keys, at)
+    check(eng, b)
+    _, _, _, st = eng.calvin_order_epoch(b, want_group=True)
+    assert st["fallback"] == 0, "the overflowing epoch should end on the sort path"
