@@ -150,14 +150,12 @@ __device__ inline void fin_publish(FinLb* e, uint64_t v, bool incl, uint32_t tag
 // key of a step loaded before any is used (one memory round trip per step
 // instead of one per access).
 constexpr uint32_t FIN_U = 8;
-#ifndef DCC_FIN_T
-#define DCC_FIN_T 4
-#endif
-constexpr uint32_t FIN_T = DCC_FIN_T;  // k_fin: consecutive txns per thread
-#ifndef DCC_FIN_B
-#define DCC_FIN_B 512
-#endif
-constexpr uint32_t FB = DCC_FIN_B;  // k_fin: threads per workgroup
+// k_fin: 2,048 txns per workgroup, as 1,024 threads x 2 consecutive txns for
+// an epoch finished on its own (its pushes and write-set emission spread over
+// more threads: the SHIM / HIST epochs) and as 512 x 4 for a chained finish
+// beside other lanes' kernels (half the wave slots while its look-back waits;
+// profiles/r06/fin_t/)
+constexpr uint32_t FIN_TXN_WG = 2048;
 __device__ inline void fin_step(const OccFinArgs& a, uint64_t x, uint64_t o1, uint8_t (&ty)[FIN_U],
                                 uint64_t (&k)[FIN_U]) {
 #pragma unroll
@@ -189,6 +187,7 @@ __device__ inline uint32_t fin_writes(uint64_t t, const OccFinArgs& a, uint64_t&
 }
 
 // block-wide exclusive scans of two counters (FB threads); returns both totals
+template <uint32_t FB>
 __device__ inline void block_excl_scan2(uint32_t v0, uint32_t v1, uint32_t& e0, uint32_t& e1,
                                         uint32_t& t0, uint32_t& t1) {
   __shared__ uint32_t s_w[2][FB / 64];
@@ -222,6 +221,7 @@ __device__ inline void block_excl_scan2(uint32_t v0, uint32_t v1, uint32_t& e0, 
   e1 = b1 + x1 - v1;
 }
 
+template <uint32_t FB, uint32_t FIN_T>
 __global__ __launch_bounds__(FB, 8) void k_fin(OccFinArgs a) {
   __shared__ unsigned long long s_mx;
   __shared__ uint64_t s_pre;
@@ -276,7 +276,7 @@ __global__ __launch_bounds__(FB, 8) void k_fin(OccFinArgs a) {
   }
   if (threadIdx.x == 0) s_mx = 0;
   uint32_t e0, e1, t0, t1;
-  block_excl_scan2(cs, ws, e0, e1, t0, t1);  // its barrier orders s_mx's reset
+  block_excl_scan2<FB>(cs, ws, e0, e1, t0, t1);  // its barrier orders s_mx's reset
   for (int d = 32; d > 0; d >>= 1) kmx = max(kmx, (uint64_t)__shfl_xor(kmx, d));
   if ((threadIdx.x & 63) == 0 && kmx) atomicMax(&s_mx, (unsigned long long)kmx);
   __syncthreads();
@@ -421,8 +421,11 @@ void launch_fin(const OccFinArgs& a0, hipStream_t st) {
   // timing variants, wrong results by design: 1 no chain pushes, 2 no
   // look-back wait, 4 no write-set emission, 8 no tn stores
   if (const char* e = DCC_ENV("DCC_FIN_VAR")) a.var = (uint32_t)atoi(e);
-  const uint64_t nb = (a.n + FB * FIN_T - 1) / (FB * FIN_T);
-  k_fin<<<(unsigned)(nb ? nb : 1), FB, 0, st>>>(a);
+  const uint64_t nb = (a.n + FIN_TXN_WG - 1) / FIN_TXN_WG;
+  if (a.ctl)
+    k_fin<512, 4><<<(unsigned)(nb ? nb : 1), 512, 0, st>>>(a);
+  else
+    k_fin<1024, 2><<<(unsigned)(nb ? nb : 1), 1024, 0, st>>>(a);
 }
 
 void launch_fin_prep(const uint32_t* src, OccDyn* dyn, const FinCtl* ctl, uint64_t seq, hipStream_t st) {
@@ -432,7 +435,7 @@ void launch_fin_ctl_set(FinCtl* ctl, uint64_t tnc, uint64_t hist_m, uint64_t seq
   k_fin_ctl_set<<<1, 1, 0, st>>>(ctl, tnc, hist_m, seq);
 }
 
-uint64_t fin_part_bytes(uint64_t n) { return (((n + FB * FIN_T - 1) / (FB * FIN_T)) + 2) * sizeof(FinLb); }
+uint64_t fin_part_bytes(uint64_t n) { return (((n + FIN_TXN_WG - 1) / FIN_TXN_WG) + 2) * sizeof(FinLb); }
 
 // A host copy of k_fin's look-back words (fin_part_bytes(n) bytes) after a
 // launch with `tag`, summarised for the error message of a totals mismatch:
@@ -441,7 +444,7 @@ uint64_t fin_part_bytes(uint64_t n) { return (((n + FB * FIN_T - 1) / (FB * FIN_
 // aggregate (a foreign or stale prefix taken by the look-back).
 std::string fin_diag(const void* words, uint64_t n, uint32_t tag) {
   const FinLb* lb = (const FinLb*)((const FinTail*)words + 1);
-  const uint64_t nb = std::max<uint64_t>(1, (n + FB * FIN_T - 1) / (FB * FIN_T));
+  const uint64_t nb = std::max<uint64_t>(1, (n + FIN_TXN_WG - 1) / FIN_TXN_WG);
   uint64_t stale = 0, first_stale = ~0ull, bad = ~0ull;
   uint32_t stale_tag = 0;
   uint64_t prev = 0;
