@@ -308,7 +308,13 @@ extern "C" int dcc_occ_submit_epoch(dcc_ctx* ctx, const dcc_batch* b, uint8_t* o
       // behind the previous epoch's last work (its own finish, or its decision)
       hipEvent_t after = p->flight.empty() ? nullptr : p->lanes[p->flight.back().lane]->ev_done;
       f.chain = ctx->chain_enqueue(lane, f.seq, after, reset) == DCC_OK;
-      if (!f.chain) (void)hipGetLastError();  // the host finishes it at completion instead
+      if (!f.chain) {
+        // the host finishes it at completion instead; a finish the failed
+        // enqueue may still have launched can have pushed its pairs onto the
+        // delta's chains: rebuilt from the flat pairs before the next read
+        (void)hipGetLastError();
+        ctx->hs[1].built = false;
+      }
       f.app = f.chain && app;
       f.res = f.app ? res : 0;
       p->app_res += f.res;
