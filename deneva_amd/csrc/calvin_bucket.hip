@@ -554,6 +554,30 @@ __global__ __launch_bounds__(CB_BT) void k_cb_bucket(CbBucket a) {
     // (3) stable LDS radix sort of the chunk by the row bits, 4 per pass
     for (uint32_t ps = 0; ps < npass; ps++) {
       const uint32_t sh = a.bb + 4 * ps;  // in the high word
+      if (a.lbits - 4 * ps == 1) {
+        // a last pass of one bit (13 row bits: C4): a stable split, zeros
+        // first -- one block scan of the zero counts instead of the 16-digit
+        // count table (real requests have no row bit above; padding sorts last)
+        uint32_t z = 0, rk[CB_IT];
+#pragma unroll
+        for (uint32_t i = 0; i < CB_IT; i++) {
+          const uint32_t bit = ((uint32_t)(e[i] >> 32) >> sh) & 1u;
+          rk[i] = bit ? i - z : z;
+          z += bit ^ 1u;
+        }
+        uint32_t Z;
+        const uint32_t zp = blk_excl_add(z, s_w, Z);
+#pragma unroll
+        for (uint32_t i = 0; i < CB_IT; i++) {
+          const uint32_t bit = ((uint32_t)(e[i] >> 32) >> sh) & 1u;
+          s_stg[stg_ix(bit ? Z + (p0 - zp) + rk[i] : zp + rk[i])] = e[i];
+        }
+        lds_barrier();
+#pragma unroll
+        for (uint32_t i = 0; i < CB_IT; i++) e[i] = s_stg[stg_ix(p0 + i)];
+        lds_barrier();
+        continue;
+      }
       uint64_t clo = 0, chi = 0;  // 8-bit running counts of digits 0-7 / 8-15
       uint32_t rk[CB_IT];
 #pragma unroll

@@ -103,7 +103,7 @@ __global__ __launch_bounds__(HB) void k_hist_emit(uint64_t n, const uint32_t* of
 
 // ---------------------------------------------------------------------------
 // central_finish in one launch (OccFinArgs, occ_kernels.h): a workgroup per
-// 1,024 txns counts its committed writers (cflag) and, when appending, their
+// 2,048 txns counts its committed writers (cflag) and, when appending, their
 // writes and largest key; a single-pass scan with decoupled look-back gives
 // its prefix (tnc and the delta's append position from the epoch parameters,
 // dyn->tnc / dyn->hist_m); each committed writer takes its tn and emits its
