@@ -385,6 +385,10 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1, const SwShard* shl
     return e ? (unsigned)atoi(e) : 0u;
   }();
   const unsigned fgrid = fgrid_ov ? fgrid_ov : (unsigned)std::max<uint64_t>(1, 4ull * n_cu);
+  static const unsigned fgrid1_ov = [] {  // DCC_SW_FGRID1: experiments, the levels after 0
+    const char* e = DCC_ENV("DCC_SW_FGRID1");
+    return e ? (unsigned)atoi(e) : 0u;
+  }();
   uint64_t* gtab0 = (uint64_t*)sw_gtab.p;
   uint32_t* cbits_d = (uint32_t*)sw_ckeys.p;
   uint32_t* bloom_d = cbits_d + (1u << SW_GBITS_MAX) / 32;
@@ -479,7 +483,8 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1, const SwShard* shl
     fa.sflag = sflag_d;
     fa.tcount = tcount_d;
     fa.bsum = bsum_d;
-    fa.nblocks = fgrid;
+    const unsigned lgrid = (!top && fgrid1_ov) ? std::min(fgrid1_ov, fgrid) : fgrid;
+    fa.nblocks = lgrid;
     fa.lv = lv;
     fa.lv_next = lv + 1;
     fa.state = (uint8_t*)state.p;
@@ -514,7 +519,7 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1, const SwShard* shl
     fa.ro_count = wctl + 2;
     // phase 1 of the profile is exactly the level-0 streaming filter
     if (top && profiling) CK(hipEventRecord(pev[1], stream));
-    launch_sw_filter(fa, fgrid, stream);
+    launch_sw_filter(fa, lgrid, stream);
     if (top && profiling) CK(hipEventRecord(pev[2], stream));
     if (shl) {
       // a kill on any shard wins (every rank's kill words gathered, OR-ed by
@@ -522,9 +527,9 @@ int dcc_ctx::sweep_enqueue(const DevBatch& d, int l0, int l1, const SwShard* shl
       // bytes are global already when the rank holds the whole batch.
       CR(comm_allgather_u8((const uint8_t*)shl->kill_out, (uint8_t*)shl->kill_all, shl->kill_words * 8));
       if (top && !shl->full_off) CR(comm_allreduce_max_u8((uint8_t*)hasw.p, d.n));
-      launch_sw_apply(fa, fgrid, stream);
+      launch_sw_apply(fa, lgrid, stream);
     }
-    launch_sw_compact(fa, fgrid, stream);
+    launch_sw_compact(fa, lgrid, stream);
   }
   CK(hipGetLastError());
   return DCC_OK;
