@@ -1125,8 +1125,14 @@ __device__ inline bool c_exact(const SwFilterArgs& a, uint64_t key) {
   return false;
 }
 constexpr uint32_t F_STASH = 256;  // Bloom-positive keys kept in LDS per wave
-constexpr uint32_t F_XS = 2048;    // small-C filter instance: LDS exact-set slots
-constexpr uint32_t F_XCAP = 1024;  // ... for C of up to this many keys (<= 50% load)
+#ifndef DCC_F_XS
+#define DCC_F_XS 2048
+#endif
+#ifndef DCC_F_WPE
+#define DCC_F_WPE 1
+#endif
+constexpr uint32_t F_XS = DCC_F_XS;    // small-C filter instance: LDS exact-set slots
+constexpr uint32_t F_XCAP = F_XS / 2;  // ... for C of up to this many keys (<= 50% load)
 constexpr uint32_t F_XBITS_LOG = 16;  // ... its one-hash bitmap of C (8 KiB)
 
 // ---------------------------------------------------------------------------
@@ -1137,7 +1143,7 @@ constexpr uint32_t F_XBITS_LOG = 16;  // ... its one-hash bitmap of C (8 KiB)
 // -- C as an LDS hash set behind a one-hash LDS bitmap, nothing global --
 // and the level's Bloom filter with exact checks in the global key table
 // otherwise.  Their LDS overlaps (36 KB in all: four workgroups fit a CU).
-__global__ __launch_bounds__(SW_CHUNK) void k_sw_filter(SwFilterArgs a) {
+__global__ __launch_bounds__(SW_CHUNK, DCC_F_WPE) void k_sw_filter(SwFilterArgs a) {
   constexpr uint32_t B = SW_CHUNK, FW = B / 64;
   constexpr uint32_t CS = F_XS;  // exact-set slots (X)
   struct XSet {
