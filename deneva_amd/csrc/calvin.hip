@@ -34,6 +34,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "calvin_bucket.h"
@@ -61,6 +62,15 @@ using namespace dcc;
   } while (0)
 
 namespace {
+// helper workgroups of the wave walk (calvin_wave.hip), each on a CU of its
+// own (experiments builds: DCC_CW_HELPERS, 0 = the walker's workgroup alone;
+// C4: 0 34.7 ms, 16 18.1, 32 18.1 -- profiles/r06/cwhelp/)
+constexpr uint32_t CW_NH = 16;
+uint32_t cw_helpers(int n_cu) {
+  uint32_t nh = CW_NH;
+  if (const char* e = DCC_ENV("DCC_CW_HELPERS")) nh = (uint32_t)atoi(e);
+  return std::min<uint32_t>(nh, n_cu > 1 ? (uint32_t)n_cu - 1u : 0u);
+}
 
 constexpr uint32_t NOPOS = 0xFFFFFFFFu;
 constexpr uint32_t CV_MAX_TXN = 1u << 25;  // value = txn:25 | j:6 | EX:1
@@ -1189,6 +1199,7 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint3
   // dataflow grid (k_cv_wave) for longer ones
   CwPlan cwp{};
   const bool cw = waves && !DCC_ENV("DCC_CV_WAVE_GRID") && cw_plan(d.n, maxlen, &cwp);
+  const uint32_t cw_nh = cw && cwp.nch > 2 ? cw_helpers(n_cu) : 0u;
   if (waves) {
     if (dev_out) {
       wave_dev = out_wave;
@@ -1213,6 +1224,10 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint3
       CR(cv_cwhot.ensure(this, (uint64_t)cwp.nch * cwp.C * 32 + 16, "calvin wave compact records"));
       CR(cv_cwpa.ensure(this, sb, "calvin wave read addresses"));
       CR(cv_cwoa.ensure(this, sb, "calvin wave publish addresses"));
+      if (cw_nh) {
+        CR(cv_cwhelp.ensure(this, cw_help_words(cwp) * 4, "calvin wave helper hand-offs"));
+        CR(cv_cwrec2.ensure(this, sb, "calvin wave two-chunk records"));
+      }
     } else {
       CR(cv_pgx.ensure(this, m, "calvin pgx"));
       CR(cv_gsize.ensure(this, m, "calvin gsize"));
@@ -1332,7 +1347,7 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint3
                     (uint32_t*)cv_gsize.p, (uint32_t*)cv_done.p, (uint32_t*)cv_maxl.p,
                     (uint32_t*)cv_cwmax.p, (uint8_t*)cv_cwmark.p, (uint32_t*)cv_cwpa.p,
                     (uint32_t*)cv_cwoa.p, (uint32_t*)cv_cwhot.p,
-                    wave_dev, err, nullptr};
+                    wave_dev, err, nullptr, (uint32_t*)cv_cwhelp.p, cw_nh ? (uint32_t*)cv_cwrec2.p : nullptr, cw_nh};
     if (DCC_ENV("DCC_CW_DBG")) {  // experiments builds: the walker's timing counters
       static uint64_t* dbg = nullptr;
       if (!dbg) CK(hipMalloc(&dbg, 128));
@@ -1340,16 +1355,18 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint3
       CwArgs cd = ca;
       cd.dbg = dbg;
       CK(cw_run(cwp, cd, stream));
-      uint64_t h[15];
-      CK(hipMemcpyAsync(h, dbg, 120, hipMemcpyDeviceToHost, stream));
+      uint64_t h[16];
+      CK(hipMemcpyAsync(h, dbg, 128, hipMemcpyDeviceToHost, stream));
       CK(hipStreamSynchronize(stream));
       fprintf(stderr, "cw: chunks %u C %u H %u walk %.3f ms rounds-loop %.3f ms barriers %.3f ms rounds %llu"
               " | staging: maxima+fence %.3f sync %.3f bounds %.3f rest %.3f ms | clock %.0f MHz"
-              " | sub-chunks with intra %llu overflow %llu plain rounds %llu\n",
+              " | sub-chunks with intra %llu overflow %llu plain rounds %llu"
+              " | helpers: staging poll %.3f, helper 0 wait %.3f busy %.3f ms\n",
               cwp.nch, cwp.C, cwp.H, h[0] * 1e-5, h[1] * 1e-5, h[2] * 1e-5, (unsigned long long)h[3],
               h[4] * 1e-5, h[5] * 1e-5, h[6] * 1e-5, h[7] * 1e-5,
               h[9] ? (double)h[8] / (h[9] * 1e-2) : 0.0, (unsigned long long)h[10],
-              (unsigned long long)h[11], (unsigned long long)h[12]);
+              (unsigned long long)h[11], (unsigned long long)h[12], h[13] * 1e-5, h[14] * 1e-5,
+              h[15] * 1e-5);
     } else {
       CK(cw_run(cwp, ca, stream));
     }

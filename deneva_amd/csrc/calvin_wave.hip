@@ -6,7 +6,8 @@
 //                LDS byte addresses (walker)
 //   k_cw_mark / k_cw_cr  the slots read inside their own sub-chunk, and per
 //                txn its (at most two) such reads and publications
-//   k_cw_walk    one workgroup: wave 0 walks, the other waves stage
+//   k_cw_walk    one workgroup: wave 0 walks, the other waves stage (with
+//                helper workgroups on other CUs taking the scattered part)
 //
 // LDS and global group maxima hold (max wave + 1): 0 is "no member yet", and
 // a request's bound is the value it reads.
@@ -48,8 +49,43 @@ __device__ inline uint32_t cw_ld(__amdgpu_buffer_rsrc_t r, uint32_t idx) {
 __device__ inline uint32_t cw_ld_l2(__amdgpu_buffer_rsrc_t r, uint32_t idx) {
   return __builtin_amdgcn_raw_buffer_load_b32(r, idx * 4u, 0, 16);
 }
+// (helpers) a write-through store: sc1, like an agent-scope relaxed store
+__device__ inline void cw_st_l2(__amdgpu_buffer_rsrc_t r, uint32_t idx, uint32_t v) {
+  __builtin_amdgcn_raw_buffer_store_b32(v, r, idx * 4u, 0, 16);
+}
 
 __device__ inline void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Hand-offs between the walker's workgroup and the helper workgroups (other
+// CUs, any XCD): every handed-off word is stored and loaded with agent-scope
+// relaxed atomics (global_store / global_load sc1: past the L1, write-through)
+// or changed by agent-scope atomics; a storing wave waits for its stores
+// (vmcnt 0) before the flag that covers them is raised (MI355X_MICROARCH.md,
+// inter-workgroup visibility, the sc1 hand-off row).
+__device__ inline uint32_t ag_ld(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline void ag_st(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// help block: [0] chunks published by the walker's workgroup, [16] helper
+// iterations done (summed over helpers), [32] abort (a poll gave up), then the
+// bounds of every chunk's txns and the waves of every chunk, in sequence order
+constexpr uint32_t CW_HP = 0, CW_HR = 16, CW_HAB = 32, CW_HDATA = 64;
+constexpr uint32_t CW_POLL_MAX = 1u << 22;  // ~0.2 s of s_sleep(2) per poll
+// wait until *ctr >= target; false when this or another poll gave up
+__device__ inline bool cw_poll(uint32_t* help, uint32_t at, uint32_t target) {
+  for (uint32_t k = 0; ag_ld(help + at) < target; k++) {
+    if (ag_ld(help + CW_HAB)) return false;
+    if (k >= CW_POLL_MAX) {
+      __hip_atomic_fetch_or(help + CW_HAB, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  return true;
+}
 
 __global__ __launch_bounds__(256) void k_cw_seqpos(const uint32_t* __restrict__ seq, uint64_t n,
                                                    uint32_t* __restrict__ seqpos) {
@@ -109,6 +145,23 @@ __global__ __launch_bounds__(256) void k_cw_link(LinkArgs A) {
   a.rec16[s] = f_prev | (f_own << 16);
   a.recp[s] = prevc;
   a.reco[s] = ownc;
+  if (a.rec2) {
+    // (helpers) the staging record: low half, the LDS slot of a previous
+    // group that ended exactly two chunks back; high half, the LDS slot an
+    // own group ending in the next chunk (F_FLAG clear) or two chunks ahead
+    // (F_FLAG set) is added to at a boundary; F_NONE: none
+    uint32_t p2 = F_NONE, o2 = F_NONE;
+    if (prevc != NONE) {
+      const uint32_t pc = prevc / p.H;
+      if (pc + 2 == c) p2 = (pc & 1u) * p.H + (prevc - pc * p.H);
+    }
+    if (ownc != NONE) {
+      const uint32_t oc = ownc / p.H;
+      if (oc == c + 1 || oc == c + 2)
+        o2 = ((oc & 1u) * p.H + (ownc - oc * p.H)) | (oc == c + 2 ? F_FLAG : 0u);
+    }
+    a.rec2[s] = p2 | (o2 << 16);
+  }
   // the walker's addresses: a far / absent previous group reads the zero
   // slot; an own group not in this chunk publishes to the lane's sink
   a.pa[s] = 4u * (f_prev < F_FAR ? (f_prev & 0x7FFFu) : CW_ZERO);
@@ -199,6 +252,17 @@ __device__ inline void cw_load(uint32_t (&r)[N], const uint32_t* base, uint32_t 
   }
 }
 
+// experiments builds: a staging wave's time per step (h_m: the last stamp)
+#ifdef DCC_EXPERIMENTS
+#define CW_H(v)                                           \
+  do {                                                    \
+    const uint64_t m_ = __builtin_amdgcn_s_memrealtime(); \
+    v += m_ - h_m;                                        \
+    h_m = m_;                                             \
+  } while (0)
+#else
+#define CW_H(v) ((void)0)
+#endif
 // The walk (see calvin_wave.h).  Iteration c: wave 0 walks chunk c while the
 // staging waves (1) add chunk c-1's maxima of groups ending two or more chunks
 // ahead to the global maxima, (2) read chunk c+1's records: own fields, and
@@ -209,19 +273,91 @@ __device__ inline void cw_load(uint32_t (&r)[N], const uint32_t* base, uint32_t 
 // members of groups ending in chunk c+1 add themselves.  The two roles run
 // their own loops (same barrier count per iteration), so neither's registers
 // are live in the other's.
-template <int LR>
+//
+// HELP (a.nh helper workgroups, blockIdx 1..nh): the scattered part moves to
+// helpers on other CUs, a whole chunk ahead of where it is needed.  Groups
+// ending exactly two chunks away go through LDS (rec2): a request whose
+// previous group ended two chunks back reads chunk c-1's region while chunk
+// c+1 is staged, and a member of a group ending two chunks ahead adds itself
+// to that chunk's region at the boundary after its refill.  What is three or
+// more chunks away goes through the global maxima: at iteration c the
+// staging waves publish chunk c-1 (its region -- final once walk c-1 is done
+// -- and its waves) and raise P = c; helper iteration c then adds chunk
+// c-1's members to groups ending three or more chunks ahead and gathers the
+// bounds of chunk c+2's requests from groups that ended three or more chunks
+// back, and counts itself in R; staging iteration c+1 waits for R, loads
+// chunk c+2's bounds and its maxima share, and the boundary refills the
+// region without a flush.
+template <int LR, bool HELP>
 __global__ __launch_bounds__(CW_T) void k_cw_walk(CwPlan p, CwArgs a) {
   __shared__ uint32_t sgm[CW_ZERO + 1];
   __shared__ uint32_t sE[2][CW_CMAX];
   __shared__ uint32_t swt[2][CW_CMAX];
-  __shared__ uint32_t s_ctr;
+  __shared__ uint32_t s_ctr, s_pub;
   const uint32_t tid = threadIdx.x, lane = lane_id(), wid = tid >> 6;
   const uint32_t H = p.H, C = p.C, lg = p.lg, nch = p.nch;
   const uint32_t n = (uint32_t)a.n;
+  if (HELP && blockIdx.x > 0) {
+    // ---------------------------------------------------------------- helper
+    const uint32_t nh = gridDim.x - 1, hid = blockIdx.x - 1, L = 1u << lg;
+    uint32_t* const sEg = a.help + CW_HDATA;
+    uint32_t* const wsq = sEg + (uint64_t)nch * C;
+    bool spun = false;
+#ifdef DCC_EXPERIMENTS
+    uint64_t hw_wait = 0, hw_busy = 0, hw_m = __builtin_amdgcn_s_memrealtime();
+#endif
+    for (uint32_t c = 0; c + 2 < nch; c++) {
+      const uint32_t c2 = c + 2, cp = c ? c - 1 : 0u;
+      // (H and the stride are multiples of 64: the loop is wave-uniform, and a
+      // txn's L slots sit in one wave)
+      for (uint32_t l = hid * CW_T + tid, it = 0; l < H; l += nh * CW_T, it++) {
+        const uint64_t s1 = (uint64_t)cp * H + l, s2 = (uint64_t)c2 * H + l;
+        // the records (inputs) before the wait for the hand-off
+        const uint32_t w1 = c ? a.rec16[s1] : F_NONE << 16, x1 = a.rec2[s1], o1 = a.reco[s1];
+        const uint32_t w2 = a.rec16[s2], x2 = a.rec2[s2], p2 = a.recp[s2];
+        if (it == 0) {  // chunks < c published
+#ifdef DCC_EXPERIMENTS
+          const uint64_t m0 = __builtin_amdgcn_s_memrealtime();
+          hw_busy += m0 - hw_m;
+#endif
+          if (wid == 0 && !cw_poll(a.help, CW_HP, c)) spun = true;
+          __syncthreads();
+#ifdef DCC_EXPERIMENTS
+          hw_m = __builtin_amdgcn_s_memrealtime();
+          hw_wait += hw_m - m0;
+#endif
+        }
+        // chunk c-1's member of a group ending three or more chunks ahead
+        if ((w1 >> 16) == F_FAR && (x1 >> 16) == F_NONE)
+          __hip_atomic_fetch_max(a.mg + o1, ag_ld(wsq + (uint64_t)cp * C + (l >> lg)) + 1u,
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // chunk c+2's request after a group that ended three or more chunks back
+        uint32_t v = ((w2 & F_NONE) == F_FAR && (x2 & F_NONE) == F_NONE) ? ag_ld(a.mg + p2) : 0u;
+        for (uint32_t d = 1; d < L; d <<= 1) v = max(v, (uint32_t)__shfl_xor(v, d));
+        if ((l & (L - 1u)) == 0) ag_st(sEg + (uint64_t)c2 * C + (l >> lg), v);
+      }
+      if (hid * CW_T >= H) {  // no slots this iteration: only the wait
+        if (wid == 0 && !cw_poll(a.help, CW_HP, c)) spun = true;
+        __syncthreads();
+      }
+      vm_drain();
+      __syncthreads();
+      if (tid == 0) __hip_atomic_fetch_add(a.help + CW_HR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#ifdef DCC_EXPERIMENTS
+    if (a.dbg && hid == 0 && tid == 0) {
+      a.dbg[14] = hw_wait;
+      a.dbg[15] = hw_busy + (__builtin_amdgcn_s_memrealtime() - hw_m);
+    }
+#endif
+    if (spun && lane == 0) atomicOr(a.err, CW_ERR_SPIN);
+    return;
+  }
   for (uint32_t i = tid; i < H; i += CW_T) sgm[i] = 0;
   for (uint32_t i = tid; i < C; i += CW_T) sE[0][i] = 0;
   if (tid == 0) {
     s_ctr = 0;
+    s_pub = 0;
     sgm[CW_ZERO] = 0;
   }
   __syncthreads();
@@ -383,6 +519,172 @@ __global__ __launch_bounds__(CW_T) void k_cw_walk(CwPlan p, CwArgs a) {
       a.dbg[12] = n_plain;
     }
 #endif
+  } else if (HELP) {
+    // ------------------------------------------------- staging (with helpers)
+    const uint32_t h0 = tid - 64, nh = gridDim.x - 1;
+    constexpr uint32_t LG = LR == 16 ? 4u : 5u;  // == lg (cw_plan; cw_run picks LR by it)
+    // buffer loads / stores, sc1 (32-bit offsets: one VGPR per access in flight)
+    const __amdgpu_buffer_rsrc_t rs_mg = cw_rsrc(a.mg, (uint64_t)p.slots * 4),
+                                 rs_hp = cw_rsrc(a.help, cw_help_words(p) * 4);
+    const uint32_t o_sE = CW_HDATA, o_wsq = CW_HDATA + nch * C;
+    // staging records' high halves (16-bit, two per word): boundary-add
+    // targets of chunk c+1 (ownp), c (own) and c-1 (ownq)
+    uint32_t own[CW_K / 2], ownp[CW_K / 2], ownq[CW_K / 2], ini[CW_K];
+    const __amdgpu_buffer_rsrc_t rs_r2 = cw_rsrc(a.rec2, (uint64_t)p.slots * 4);
+    bool spun = false;
+    uint32_t target = 0;
+#ifdef DCC_EXPERIMENTS
+    uint64_t h_t1 = 0, h_sync = 0, h_t2 = 0, h_rest = 0, h_m = 0, h_poll = 0;
+#endif
+    auto put16 = [](uint32_t (&w)[CW_K / 2], uint32_t k, uint32_t f) {
+      if (k & 1) w[k >> 1] |= f << 16;
+      else w[k >> 1] = f;
+    };
+    auto get16 = [](const uint32_t (&w)[CW_K / 2], uint32_t k) { return (w[k >> 1] >> (16 * (k & 1))) & F_NONE; };
+#pragma unroll
+    for (uint32_t k = 0; k < CW_K; k++) {  // chunk 0's
+      const uint32_t l = h0 + k * CW_HELP;
+      put16(own, k, l < H ? a.rec2[l] >> 16 : F_NONE);
+      put16(ownq, k, F_NONE);
+    }
+    for (uint32_t c = 0; c <= nch; c++) {
+      // a fresh copy of the thread's slot base each iteration: the per-slot
+      // offsets are recomputed, not hoisted out of the loop (and spilled)
+      uint32_t h = h0;
+      asm volatile("" : "+v"(h));
+#ifdef DCC_EXPERIMENTS
+      h_m = __builtin_amdgcn_s_memrealtime();
+#endif
+      // (A) chunk c-1 to the helpers: its region and its waves, then P = c
+      if (c >= 1) {
+        const uint32_t cp = c - 1, rp = cp & 1u, nqp = min(C, n - cp * C);
+#pragma unroll
+        for (uint32_t k = 0; k < CW_K; k++) {
+          const uint32_t l = h + k * CW_HELP;
+          if (l < H) cw_st_l2(rs_mg, cp * H + l, sgm[rp * H + l]);
+        }
+        for (uint32_t ql = h; ql < nqp; ql += CW_HELP) cw_st_l2(rs_hp, o_wsq + cp * C + ql, swt[rp][ql]);
+        vm_drain();
+        // the staging wave whose count completes this iteration's raises P
+        // (a counter of its own: a wave may reach the sync in (B) before
+        // another has counted here)
+        if (lane == 0 && atomicAdd(&s_pub, 1u) == CW_HWAVES * c - 1u) ag_st(a.help + CW_HP, c);
+        // the outputs (not handed off)
+        for (uint32_t ql = h; ql < nqp; ql += CW_HELP) {
+          const uint32_t q = cp * C + ql;
+          a.wave[a.seq ? a.seq[q] : q] = swt[rp][ql];
+        }
+      }
+      CW_H(h_t1);
+      // (B) chunk c+1: its staging records; its requests' bounds from groups
+      // that ended in chunk c-1 (LDS: that region is refilled only at this
+      // iteration's boundary) and, once helper iteration c-1 is done, from
+      // older ones (sEg) and its maxima share
+      if (c + 1 < nch) {
+        const uint32_t c1 = c + 1, r1 = c1 & 1u, base = c1 * H;
+        uint32_t p2[CW_K / 2];  // the two-back LDS slots of chunk c+1's requests
+        {
+          uint32_t x[CW_K];
+#pragma unroll
+          for (uint32_t k = 0; k < CW_K; k++) {
+            const uint32_t l = h + k * CW_HELP;
+            x[k] = cw_ld(rs_r2, base + (l < H ? l : 0u));
+          }
+#pragma unroll
+          for (uint32_t k = 0; k < CW_K; k++) {
+            const bool in = h + k * CW_HELP < H;
+            put16(ownp, k, in ? x[k] >> 16 : F_NONE);
+            put16(p2, k, in ? x[k] & F_NONE : F_NONE);
+          }
+        }
+#ifdef DCC_EXPERIMENTS
+        const uint64_t pw0 = __builtin_amdgcn_s_memrealtime();
+#endif
+        if (c1 >= 2 && !cw_poll(a.help, CW_HR, nh * c)) spun = true;
+        asm volatile("" ::: "memory");  // the loads below stay behind the poll
+#ifdef DCC_EXPERIMENTS
+        h_poll += __builtin_amdgcn_s_memrealtime() - pw0;
+#endif
+        CW_H(h_sync);
+#pragma unroll
+        for (uint32_t k = 0; k < CW_K; k++) {
+          const uint32_t l = h + k * CW_HELP;
+          ini[k] = cw_ld_l2(rs_mg, base + (l < H ? l : 0u));
+        }
+        for (uint32_t ql = h; ql < C; ql += CW_HELP)
+          sE[r1][ql] = c1 >= 2 ? cw_ld_l2(rs_hp, o_sE + c1 * C + ql) : 0u;
+        // every staging wave's sE stores before the LDS maxima below
+        target += CW_HWAVES;
+        cw_sync(&s_ctr, target, spun);
+        // (LDS reads in batches ahead of their maxima: one wait per batch)
+#pragma unroll
+        for (uint32_t k0 = 0; k0 < CW_K; k0 += 12) {
+          uint32_t v[12];
+#pragma unroll
+          for (uint32_t k = 0; k < 12; k++) {
+            const uint32_t x = get16(p2, k0 + k);
+            v[k] = sgm[x == F_NONE ? CW_ZERO : x];
+          }
+#pragma unroll
+          for (uint32_t k = 0; k < 12; k++)
+            if (v[k]) atomicMax(&sE[r1][(h + (k0 + k) * CW_HELP) >> LG], v[k]);
+        }
+      } else {
+#pragma unroll
+        for (uint32_t k = 0; k < CW_K; k++) put16(ownp, k, F_NONE);
+      }
+      CW_H(h_t2);
+      lds_barrier();  // walk done / staging done
+      if (c + 1 < nch) {  // chunk c-1's region (published in (A)) <- chunk c+1's
+        const uint32_t rn = (c + 1) & 1u;
+#pragma unroll
+        for (uint32_t k = 0; k < CW_K; k++) {
+          const uint32_t l = h + k * CW_HELP;
+          if (l < H) sgm[rn * H + l] = ini[k];
+        }
+      }
+      lds_barrier();
+      if (c < nch) {
+        // chunk c's members of groups ending in chunk c+1, and chunk c-1's of
+        // groups ending in chunk c+1 (its waves are still in swt until walk
+        // c+1)
+        const uint32_t r = c & 1u, rq = (c + 1) & 1u;
+        // (LDS reads in batches ahead of their maxima: one wait per batch)
+#pragma unroll
+        for (uint32_t k0 = 0; k0 < CW_K; k0 += 12) {
+          uint32_t wf[12], wg[12];
+#pragma unroll
+          for (uint32_t k = 0; k < 12; k++) {
+            const uint32_t t = (h + (k0 + k) * CW_HELP) >> LG;  // (< CW_CMAX: l < CW_HPLAN)
+            wf[k] = swt[r][t];
+            wg[k] = swt[rq][t];
+          }
+#pragma unroll
+          for (uint32_t k = 0; k < 12; k++) {
+            const uint32_t f = get16(own, k0 + k), g = get16(ownq, k0 + k);
+            if (f != F_NONE && !(f & F_FLAG)) atomicMax(&sgm[f], wf[k] + 1u);
+            if (g != F_NONE && (g & F_FLAG)) atomicMax(&sgm[g & 0x7FFFu], wg[k] + 1u);
+          }
+        }
+      }
+      lds_barrier();
+      CW_H(h_rest);
+#pragma unroll
+      for (uint32_t k = 0; k < CW_K / 2; k++) {
+        ownq[k] = own[k];
+        own[k] = ownp[k];
+      }
+    }
+    if (spun && lane == 0) atomicOr(a.err, CW_ERR_SPIN);
+#ifdef DCC_EXPERIMENTS
+    if (a.dbg && h0 == 0) {
+      a.dbg[4] = h_t1;
+      a.dbg[5] = h_sync;
+      a.dbg[6] = h_t2;
+      a.dbg[7] = h_rest;
+      a.dbg[13] = h_poll;
+    }
+#endif
   } else {
     // --------------------------------------------------------------- staging
     const uint32_t h = tid - 64;
@@ -397,14 +699,6 @@ __global__ __launch_bounds__(CW_T) void k_cw_walk(CwPlan p, CwArgs a) {
     bool spun = false;
 #ifdef DCC_EXPERIMENTS
     uint64_t h_t1 = 0, h_sync = 0, h_t2 = 0, h_rest = 0, h_m = 0;  // staging wave 1's steps
-#define CW_H(v)                                             \
-  do {                                                      \
-    const uint64_t m_ = __builtin_amdgcn_s_memrealtime();   \
-    v += m_ - h_m;                                          \
-    h_m = m_;                                               \
-  } while (0)
-#else
-#define CW_H(v) ((void)0)
 #endif
 #pragma unroll
     for (uint32_t k = 0; k < CW_K; k++) {  // chunk 0's own fields
@@ -589,10 +883,20 @@ hipError_t cw_run(const CwPlan& p, const CwArgs& a, hipStream_t st) {
   const uint64_t nq = (uint64_t)p.nch * p.C;
   if (p.lg == 4)
     k_cw_cr<<<(unsigned)((nq + 255) / 256), 256, 0, st>>>(a.rec16, a.reco, a.mark, nq, p.lg, a.cr);
-  if (p.lg <= 4)
-    k_cw_walk<16><<<1, CW_T, 0, st>>>(p, a);
-  else
-    k_cw_walk<32><<<1, CW_T, 0, st>>>(p, a);
+  if (a.nh && a.rec2 && p.nch > 2) {
+    // the walker's workgroup and a.nh helpers (each a CU of its own: the
+    // kernel's LDS); the helpers' counters start at 0
+    e = hipMemsetAsync(a.help, 0, CW_HDATA * 4, st);
+    if (e != hipSuccess) return e;
+    if (p.lg <= 4)
+      k_cw_walk<16, true><<<1 + a.nh, CW_T, 0, st>>>(p, a);
+    else
+      k_cw_walk<32, true><<<1 + a.nh, CW_T, 0, st>>>(p, a);
+  } else if (p.lg <= 4) {
+    k_cw_walk<16, false><<<1, CW_T, 0, st>>>(p, a);
+  } else {
+    k_cw_walk<32, false><<<1, CW_T, 0, st>>>(p, a);
+  }
   return hipGetLastError();
 }
 

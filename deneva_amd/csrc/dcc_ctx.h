@@ -182,7 +182,7 @@ struct dcc_ctx {
   bool h_bm_stale = true;                        // h_bm is not B.bm | D.bm
   uint32_t fin_tag = 0;                          // k_fin's look-back tag of the last epoch
   DevBuf perm, calvin_a, calvin_b, calvin_c, calvin_d;  // Calvin workspaces
-  DevBuf cv_scratch, cv_agg, cv_group, cv_wave, cv_pgx, cv_gsx, cv_gsize, cv_done, cv_maxl, cv_cwmax, cv_cwpos, cv_cwmark, cv_cwhot, cv_cwpa, cv_cwoa;
+  DevBuf cv_scratch, cv_agg, cv_group, cv_wave, cv_pgx, cv_gsx, cv_gsize, cv_done, cv_maxl, cv_cwmax, cv_cwpos, cv_cwmark, cv_cwhot, cv_cwpa, cv_cwoa, cv_cwhelp, cv_cwrec2;
   DevBuf cv_seq_b, cv_ok, cv_len, cv_off2, cv_tsum, cv_hkeys, cv_hat;
   DevBuf cb_e, cb_out, cb_cnt, cb_small;           // Calvin bucket path (calvin_bucket.h)
   DevBuf snap_top, snap_aoff, snap_aidx, snap_cnt;  // captured-snapshot validation

@@ -272,7 +272,7 @@ std::vector<DevBuf*> dcc_ctx::all_bufs() {
                             &hasw, &cflag, &bsum, &tn, &rc, &stat, &dyn, &fin_part,
                             &order, &perm, &calvin_a, &calvin_b, &calvin_c, &calvin_d,
                             &cv_scratch, &cv_agg, &cv_group, &cv_wave, &cv_pgx, &cv_gsx,
-                            &cv_gsize, &cv_done, &cv_maxl, &cv_cwmax, &cv_cwpos, &cv_cwmark, &cv_cwhot, &cv_cwpa, &cv_cwoa, &cv_seq_b, &cv_ok, &cv_len,
+                            &cv_gsize, &cv_done, &cv_maxl, &cv_cwmax, &cv_cwpos, &cv_cwmark, &cv_cwhot, &cv_cwpa, &cv_cwoa, &cv_cwhelp, &cv_cwrec2, &cv_seq_b, &cv_ok, &cv_len,
                             &cv_off2, &cv_tsum, &cv_hkeys, &cv_hat, &cb_e, &cb_out, &cb_cnt, &cb_small, &gst, &hasw_scr, &sw_ctl, &sw_status, &sw_dbg,
                             &sw_ckeys, &sw_gtab, &sw_rec, &sw_rk, &sw_fw, &sw_aent, &sw_mg, &sw_xcnt, &sw_xsend,
                             &sw_xrec, &sw_mcnt, &sw_moff, &sw_mkeys, &sw_mat, &sw_kill,

@@ -137,7 +137,8 @@ def test_c4_full_size(engine):
 
 def test_c4_full_size_waves_and_dispatch(engine):
     # the C4 epoch with wave levels (row_lock.cpp:317-357 grant chains,
-    # 49,489 levels: the one-CU walk, ~35 ms at this size) and the dispatch
+    # 49,489 levels: the one-CU walk with its helper workgroups, ~18 ms at this size,
+    # DESIGN.md §8) and the dispatch
     # lists built from them (txn_table.cpp:151-176), against the oracle
     b = d.gen_ycsb(n_txn=1 << 20, zipf_theta=0.9, part_cnt=16, chunk_txns=65536, want_home=True)
     b.order = c4_order(b)
