@@ -1350,23 +1350,24 @@ int dcc_ctx::calvin_epoch(const dcc_batch* b, const dcc_calvin_held* held, uint3
                     wave_dev, err, nullptr, (uint32_t*)cv_cwhelp.p, cw_nh ? (uint32_t*)cv_cwrec2.p : nullptr, cw_nh};
     if (DCC_ENV("DCC_CW_DBG")) {  // experiments builds: the walker's timing counters
       static uint64_t* dbg = nullptr;
-      if (!dbg) CK(hipMalloc(&dbg, 128));
-      CK(hipMemsetAsync(dbg, 0, 128, stream));
+      if (!dbg) CK(hipMalloc(&dbg, 256));
+      CK(hipMemsetAsync(dbg, 0, 256, stream));
       CwArgs cd = ca;
       cd.dbg = dbg;
       CK(cw_run(cwp, cd, stream));
-      uint64_t h[16];
-      CK(hipMemcpyAsync(h, dbg, 128, hipMemcpyDeviceToHost, stream));
+      uint64_t h[18];
+      CK(hipMemcpyAsync(h, dbg, 144, hipMemcpyDeviceToHost, stream));
       CK(hipStreamSynchronize(stream));
       fprintf(stderr, "cw: chunks %u C %u H %u walk %.3f ms rounds-loop %.3f ms barriers %.3f ms rounds %llu"
               " | staging: maxima+fence %.3f sync %.3f bounds %.3f rest %.3f ms | clock %.0f MHz"
               " | sub-chunks with intra %llu overflow %llu plain rounds %llu"
-              " | helpers: staging poll %.3f, helper 0 wait %.3f busy %.3f ms\n",
+              " | helpers: staging poll %.3f, helper 0 wait %.3f busy %.3f ms"
+              " | boundary: walk wait %.3f refill %.3f adds %.3f ms\n",
               cwp.nch, cwp.C, cwp.H, h[0] * 1e-5, h[1] * 1e-5, h[2] * 1e-5, (unsigned long long)h[3],
               h[4] * 1e-5, h[5] * 1e-5, h[6] * 1e-5, h[7] * 1e-5,
               h[9] ? (double)h[8] / (h[9] * 1e-2) : 0.0, (unsigned long long)h[10],
               (unsigned long long)h[11], (unsigned long long)h[12], h[13] * 1e-5, h[14] * 1e-5,
-              h[15] * 1e-5);
+              h[15] * 1e-5, h[16] * 1e-5, h[17] * 1e-5, h[7] * 1e-5);
     } else {
       CK(cw_run(cwp, ca, stream));
     }

@@ -500,7 +500,7 @@ __global__ __launch_bounds__(CW_T) void k_cw_walk(CwPlan p, CwArgs a) {
       t_walk += tb0 - tw0;
 #endif
       lds_barrier();  // walk done / staging done
-      lds_barrier();  // region refilled
+      if constexpr (!HELP) lds_barrier();  // region refilled (HELP: among the staging waves)
       lds_barrier();  // next-chunk members added
 #ifdef DCC_EXPERIMENTS
       t_bar += __builtin_amdgcn_s_memrealtime() - tb0;
@@ -534,7 +534,7 @@ __global__ __launch_bounds__(CW_T) void k_cw_walk(CwPlan p, CwArgs a) {
     bool spun = false;
     uint32_t target = 0;
 #ifdef DCC_EXPERIMENTS
-    uint64_t h_t1 = 0, h_sync = 0, h_t2 = 0, h_rest = 0, h_m = 0, h_poll = 0;
+    uint64_t h_t1 = 0, h_sync = 0, h_t2 = 0, h_rest = 0, h_m = 0, h_poll = 0, h_b1 = 0, h_b2 = 0;
 #endif
     auto put16 = [](uint32_t (&w)[CW_K / 2], uint32_t k, uint32_t f) {
       if (k & 1) w[k >> 1] |= f << 16;
@@ -615,6 +615,7 @@ __global__ __launch_bounds__(CW_T) void k_cw_walk(CwPlan p, CwArgs a) {
           sE[r1][ql] = c1 >= 2 ? cw_ld_l2(rs_hp, o_sE + c1 * C + ql) : 0u;
         // every staging wave's sE stores before the LDS maxima below
         target += CW_HWAVES;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         cw_sync(&s_ctr, target, spun);
         // (LDS reads in batches ahead of their maxima: one wait per batch)
 #pragma unroll
@@ -635,6 +636,7 @@ __global__ __launch_bounds__(CW_T) void k_cw_walk(CwPlan p, CwArgs a) {
       }
       CW_H(h_t2);
       lds_barrier();  // walk done / staging done
+      CW_H(h_b1);
       if (c + 1 < nch) {  // chunk c-1's region (published in (A)) <- chunk c+1's
         const uint32_t rn = (c + 1) & 1u;
 #pragma unroll
@@ -643,7 +645,12 @@ __global__ __launch_bounds__(CW_T) void k_cw_walk(CwPlan p, CwArgs a) {
           if (l < H) sgm[rn * H + l] = ini[k];
         }
       }
-      lds_barrier();
+      // the refill before the adds: a sync of the staging waves only (the
+      // walker waits for the adds)
+      target += CW_HWAVES;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      cw_sync(&s_ctr, target, spun);
+      CW_H(h_b2);
       if (c < nch) {
         // chunk c's members of groups ending in chunk c+1, and chunk c-1's of
         // groups ending in chunk c+1 (its waves are still in swt until walk
@@ -683,6 +690,8 @@ __global__ __launch_bounds__(CW_T) void k_cw_walk(CwPlan p, CwArgs a) {
       a.dbg[6] = h_t2;
       a.dbg[7] = h_rest;
       a.dbg[13] = h_poll;
+      a.dbg[16] = h_b1;
+      a.dbg[17] = h_b2;
     }
 #endif
   } else {
