@@ -836,9 +836,18 @@ __global__ __launch_bounds__(1024) void k_cb_put(const uint64_t* __restrict__ in
   for (uint32_t i = tid; i < w; i += 1024) {
     const uint32_t g = win[i];
     dst[i] = g;
-    if (ulen && g != 0 && g != DCC_GROUP_NONE) {
-      const uint32_t tt = i / ulen;
-      atomicOr(&s_wait[tt >> 5], 1u << (tt & 31u));
+    if (ulen) {
+      // one atomic per txn and wave, from the txn's first lane in the wave:
+      // a wave's 64 requests belong to a few txns, whose wait bits share a
+      // word (64 same-word atomics serialise: SQ_LDS_BANK_CONFLICT)
+      const uint64_t fm = ballot64(g != 0 && g != DCC_GROUP_NONE);
+      const uint32_t tt = i / ulen, base = i - (tid & 63u);
+      const uint32_t lo = max(tt * ulen, base);
+      if (i == lo) {
+        const uint32_t hi = min((tt + 1) * ulen, base + 64u);
+        const uint64_t rm = (hi - lo >= 64u ? ~0ull : ((1ull << (hi - lo)) - 1ull)) << (lo - base);
+        if (fm & rm) atomicOr(&s_wait[tt >> 5], 1u << (tt & 31u));
+      }
     }
   }
   if (!ulen) {  // a thread per txn over its requests
@@ -848,7 +857,11 @@ __global__ __launch_bounds__(1024) void k_cb_put(const uint64_t* __restrict__ in
         const uint32_t g = win[i];
         wait |= g != 0 && g != DCC_GROUP_NONE;
       }
-      if (wait) atomicOr(&s_wait[tt >> 5], 1u << (tt & 31u));
+      // a wave's 64 txns are two whole words (tt of lane 0 is a multiple of
+      // 64): one store per word, no same-word atomics
+      const uint64_t wm = ballot64(wait);
+      const uint32_t ln = tid & 63u;
+      if ((ln & 31u) == 0) s_wait[tt >> 5] = (uint32_t)(wm >> ln);
     }
   }
   __syncthreads();
