@@ -20,7 +20,17 @@ NONE = 0xFFFFFFFF
 F_NONE, F_FLAG = 0xFFFF, 0x8000
 
 
-def model(b, C=128, sub=64):
+def model(b, C=128, sub=64, helpers=False, broken=None):
+    """helpers: the helper-workgroup protocol (k_cw_walk<LR, true>): groups
+    two chunks away through LDS, three or more through the global maxima on
+    the helpers, a chunk ahead.  Each helper iteration reads its inputs at the
+    earliest point the kernel allows (right after the staging waves raise P)
+    and its writes land at the latest (right before the staging iteration that
+    waits for them), so a read of a value not yet final, or a write landing
+    after its reader, shows as a mismatch against the oracle.  broken (a check
+    of the check): "no_wait" stages chunk c+1 without waiting for helper
+    iteration c-1's writes; "three_is_two" lets the helpers take groups that
+    ended two chunks back (not yet published when they read)."""
     import _oracle as orc
     g, rc, wv = orc.calvin(b)
     n = b.n_txn
@@ -88,15 +98,75 @@ def model(b, C=128, sub=64):
     wave = np.zeros(n, np.int64)
     rounds = 0
     ini = None
+    sEg = np.zeros((nch + 1, C), np.int64)  # helpers: bounds per chunk (+1 applied)
+    wsq = np.zeros((nch + 1, C), np.int64)  # helpers: published waves per chunk
+    pending = []  # helper writes not landed yet: ("mg", slot, v) / ("sE", chunk, ql, v)
     for c in range(nch + 1):
+        if helpers:
+            # ---- (A) chunk c-1 published: its region (final) and its waves
+            if c >= 1:
+                cp = c - 1
+                for l in range(H):
+                    mg[cp * H + l] = sgm[(cp & 1) * H + l]
+                wsq[cp] = swt[cp & 1]
+            # ---- (B) chunk c+1 staged, after helper iteration c-1's writes
+            late = pending if broken == "no_wait" else []
+            for w_ in ([] if broken == "no_wait" else pending):
+                if w_[0] == "mg":
+                    mg[w_[1]] = max(mg[w_[1]], w_[2])
+                else:
+                    sEg[w_[1]][w_[2]] = max(sEg[w_[1]][w_[2]], w_[3])
+            pending = []
+            if c + 1 < nch:
+                c1 = c + 1
+                ini = [mg[c1 * H + l] for l in range(H)]
+                for ql in range(C):
+                    e = sEg[c1][ql] if c1 >= 2 else 0
+                    for j in range(L):
+                        pc = prevc[c1 * H + (ql << lg) + j]
+                        if pc != NONE and pc // H == c - 1 and broken != "three_is_two":  # two back: LDS
+                            e = max(e, sgm[((c - 1) & 1) * H + pc - (pc // H) * H] + 1)
+                    sE[c1 & 1][ql] = e
+            else:
+                ini = [0] * H
+            for w_ in late:  # (broken: the writes land after their reader)
+                if w_[0] == "mg":
+                    mg[w_[1]] = max(mg[w_[1]], w_[2])
+                else:
+                    sEg[w_[1]][w_[2]] = max(sEg[w_[1]][w_[2]], w_[3])
+            own = [ownc[c * H + l] if c < nch else NONE for l in range(H)]
+            ownq = [ownc[(c - 1) * H + l] if 1 <= c <= nch else NONE for l in range(H)]
+            # ---- helper iteration c reads now (P = c), its writes land later
+            if c + 2 < nch:
+                if c >= 1:
+                    cp = c - 1
+                    for l in range(H):
+                        oc = ownc[cp * H + l]
+                        if oc != NONE and oc // H >= c + 2:  # three or more ahead
+                            pending.append(("mg", int(oc), int(wsq[cp][l >> lg])))
+                c2 = c + 2
+                for ql in range(C):
+                    e = 0
+                    for j in range(L):
+                        pc = prevc[c2 * H + (ql << lg) + j]
+                        lim = c if broken == "three_is_two" else c - 1
+                        if pc != NONE and pc // H <= lim:  # three or more back
+                            e = max(e, mg[pc] + 1)
+                    pending.append(("sE", c2, ql, int(e)))
+            if c >= 1:
+                cp = c - 1
+                for ql in range(min(C, n - cp * C)):
+                    wave[seq[cp * C + ql]] = swt[cp & 1][ql]
         # ---- helpers (disjoint from the walker's data)
-        if c >= 1:
+        if helpers:
+            pass
+        elif c >= 1:
             cp = c - 1
             for l in range(H):
                 oc = ownc[cp * H + l]
                 if oc != NONE and oc // H >= c + 1:
                     mg[oc] = max(mg[oc], swt[cp & 1][l >> lg])
-        if c + 1 < nch:
+        if c + 1 < nch and not helpers:
             c1 = c + 1
             for ql in range(min(C, n - c1 * C)):
                 e = 0
@@ -110,9 +180,10 @@ def model(b, C=128, sub=64):
                     v = sgm[((c - 1) & 1) * H + pc - ch * H] if ch + 1 == c else mg[pc]
                     e = max(e, v + 1)
                 sE[c1 & 1][ql] = e
-        ini = [mg[(c + 1) * H + l] if c + 1 < nch else 0 for l in range(H)]
-        own = [(rec16[c * H + l] >> 16) if c < nch else F_NONE for l in range(H)]
-        if c >= 1:
+        if not helpers:
+            ini = [mg[(c + 1) * H + l] if c + 1 < nch else 0 for l in range(H)]
+            own = [(rec16[c * H + l] >> 16) if c < nch else F_NONE for l in range(H)]
+        if c >= 1 and not helpers:
             cp = c - 1
             for ql in range(min(C, n - cp * C)):
                 wave[seq[cp * C + ql]] = swt[cp & 1][ql]
@@ -167,6 +238,24 @@ def model(b, C=128, sub=64):
                     swt[r][ql] = w[ql]
         # ---- boundary
         rn = (c + 1) & 1
+        if helpers:
+            # refill (no flush: chunk c-1 was published in (A)), then chunk c's
+            # members of groups ending in chunk c+1 and chunk c-1's of groups
+            # ending in chunk c+1 (exactly two ahead; its waves still in swt)
+            if c + 1 < nch:
+                for l in range(H):
+                    sgm[rn * H + l] = ini[l]
+            if c < nch:
+                for l in range(H):
+                    o = own[l]
+                    if o != NONE and o // H == c + 1:
+                        sgm[rn * H + o - (c + 1) * H] = max(sgm[rn * H + o - (c + 1) * H],
+                                                             swt[c & 1][l >> lg])
+                    o = ownq[l]
+                    if o != NONE and o // H == c + 1:
+                        sgm[rn * H + o - (c + 1) * H] = max(sgm[rn * H + o - (c + 1) * H],
+                                                             swt[(c - 1) & 1][l >> lg])
+            continue
         for l in range(H):
             if c >= 1:
                 mg[(c - 1) * H + l] = sgm[rn * H + l]
@@ -178,8 +267,8 @@ def model(b, C=128, sub=64):
                 if f != F_NONE and (f & F_FLAG):
                     sgm[f & 0x7FFF] = max(sgm[f & 0x7FFF], swt[c & 1][l >> lg])
     ok = np.array_equal(wave.astype(np.uint32), wv)
-    print(f"n={n} L={L} C={C} chunks={nch} max_wave={int(wv.max())} rounds={rounds} "
-          f"matches_oracle={ok}")
+    print(f"n={n} L={L} C={C} chunks={nch} helpers={helpers} max_wave={int(wv.max())} "
+          f"rounds={rounds} matches_oracle={ok}")
     if not ok:
         bad = np.nonzero(wave.astype(np.uint32) != wv)[0]
         print("first mismatches", [(int(t), int(wave[t]), int(wv[t])) for t in bad[:8]])
@@ -190,9 +279,10 @@ if __name__ == "__main__":
     from helpers import c4_batch, random_batch
     rng = np.random.default_rng(5)
     ok = True
-    for nt, C, sub in ((2048, 128, 64), (3000, 64, 16), (1024, 64, 64)):
-        ok &= model(c4_batch(nt), C, sub)
-    for seed in range(3):
-        b = random_batch(np.random.default_rng(seed), 900, 12, 40, p_write=0.4)
-        ok &= model(b, 64, 16)
+    for hp in (False, True):
+        for nt, C, sub in ((2048, 128, 64), (3000, 64, 16), (1024, 64, 64)):
+            ok &= model(c4_batch(nt), C, sub, helpers=hp)
+        for seed in range(3):
+            b = random_batch(np.random.default_rng(seed), 900, 12, 40, p_write=0.4)
+            ok &= model(b, 64, 16, helpers=hp)
     sys.exit(0 if ok else 1)
